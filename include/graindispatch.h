@@ -1,0 +1,229 @@
+/*
+ * graindispatch.h -- C ABI of libgraindispatch.so, the MI355X (gfx950) batched
+ * message-routing engine for the Orleans virtual-actor dispatch path.
+ *
+ * The Orleans host (C#) keeps its Dispatcher / MessageCenter / IGrainFactory
+ * surface.  A batching stage hands message headers to this library through
+ * P/Invoke (see INTEGRATION.md for the [DllImport] stubs).  Plain pointers and
+ * sizes only; no exceptions cross this boundary; every entry point returns
+ * GD_OK (0) or a negative GD_E* code, with a message in gd_last_error().
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * rikbosch/orleans root):
+ *   ring       LocalGrainDirectory.CalculateTargetSilo      src/Orleans.Runtime/GrainDirectory/LocalGrainDirectory.cs:477-545
+ *              IConsistentRingProvider.GetPrimaryTargetSilo src/Orleans.Runtime/ConsistentRing/IConsistentRingProvider.cs:34
+ *              (ConsistentRingProvider.cs:322-372, VirtualBucketsRingProvider.cs:244-293)
+ *              ring rebuild: LocalGrainDirectory.AddServer  LocalGrainDirectory.cs:284-309,
+ *              VirtualBucketsRingProvider.AddServer         VirtualBucketsRingProvider.cs:122-149
+ *   directory  GrainDirectoryPartition.AddSingleActivation  src/Orleans.Runtime/GrainDirectory/GrainDirectoryPartition.cs:304-326
+ *              GrainDirectoryPartition.RemoveActivation     GrainDirectoryPartition.cs:335-363
+ *              GrainDirectoryPartition.LookUpActivations    GrainDirectoryPartition.cs:385-441
+ *              ILocalGrainDirectory.LocalLookup             src/Orleans.Runtime/GrainDirectory/ILocalGrainDirectory.cs:22
+ *   address    Dispatcher.AddressMessage                    src/Orleans.Runtime/Core/Dispatcher.cs:715-767
+ *   enqueue    IncomingMessageAgent.ReceiveMessage          src/Orleans.Runtime/Messaging/IncomingMessageAgent.cs:92-190
+ *              + ActivationData.EnqueueMessage (FIFO)       src/Orleans.Runtime/Catalog/ActivationData.cs:566-606
+ *   identity   JenkinsHash.ComputeHash                      src/Orleans.Core.Abstractions/IDs/JenkinsHash.cs:25-105
+ *              UniqueKey.GetUniformHashCode                 src/Orleans.Core.Abstractions/IDs/UniqueKey.cs:272-293
+ *              SiloAddress.GetConsistentHashCode / GetUniformHashCodes  SiloAddress.cs:164-248
+ *              Utils.CalculateIdHash                        src/Orleans.Core/Utils/Utils.cs:184-203
+ *
+ * Threading: one handle = one HIP stream.  Calls on a handle are serialised
+ * by the caller (the reference serialises the same state under
+ * lock(membershipCache) / lock(lockable), LocalGrainDirectory.cs:512,
+ * GrainDirectoryPartition.cs:282,393).  gd_ring_set installs a new immutable
+ * ring snapshot that the next route call uses (the mirror of the lock-free
+ * snapshot swap at VirtualBucketsRingProvider.cs:143-144).
+ *
+ * Ownership: host arrays are caller-owned and never retained past return.
+ * *_device entry points take device pointers (hipMalloc'd / torch tensors)
+ * and only enqueue on the handle's stream; call gd_synchronize() before
+ * reading results.  The library owns the table, ring snapshot and scratch.
+ */
+#ifndef GRAINDISPATCH_H
+#define GRAINDISPATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GD_ABI_VERSION 1
+
+/* ---- return codes ------------------------------------------------------ */
+#define GD_OK        0
+#define GD_EINVAL   -1   /* bad argument / unsorted ring / n too large       */
+#define GD_ENOMEM   -2   /* device or host allocation failed                 */
+#define GD_EHIP     -3   /* HIP runtime error                                */
+#define GD_ERCCL    -4   /* collective error (multi-GPU path)                */
+#define GD_EFULL    -5   /* directory table cannot take more entries         */
+#define GD_ESTATE   -6   /* no ring installed / handle not ready             */
+#define GD_ETIMEOUT -7   /* a bounded device spin gave up (never expected)   */
+
+/* ---- ring modes ----------------------------------------- */
+#define GD_RING_DIRECTORY        0 /* D: LocalGrainDirectory, signed predecessor, wrap to last */
+#define GD_RING_CONSISTENT       1 /* R: ConsistentRingProvider, (long)int >= (long)uint, wrap to first */
+#define GD_RING_VIRTUAL_BUCKETS  2 /* V: VirtualBucketsRingProvider, uint successor, wrap to first */
+
+/* ---- per-message routing status (out_status) ------------------------------ */
+#define GD_ROUTE_OK             0 /* directory hit: (silo, act) = the single activation     */
+#define GD_ROUTE_MISS           1 /* not registered: C# slow path (Dispatcher.cs:742);
+                                     out_silo = directory owner silo                         */
+#define GD_ROUTE_SYSTEM_TARGET  2 /* UniqueKey category SystemTarget: out_silo = my silo
+                                     (LocalGrainDirectory.cs:480-485)                         */
+#define GD_ROUTE_MEMBERSHIP     3 /* Constants.SystemMembershipTableId: out_silo = seed silo
+                                     (LocalGrainDirectory.cs:487-503)                         */
+#define GD_ROUTE_KEYEXT         4 /* KeyExtGrain / GeoClient: the uniform hash needs the
+                                     KeyExt string (UniqueKey.cs:279-281); C# handles it     */
+
+#define GD_NO_ACTIVATION 0xFFFFFFFFu
+#define GD_NO_SILO       0xFFFFFFFFu
+
+/* UniqueKey fields (UniqueKey.cs:28-31) of a GrainId.  24 bytes, AoS. */
+typedef struct gd_key {
+    uint64_t n0;
+    uint64_t n1;
+    uint64_t type_code_data;
+} gd_key;
+
+/* Directory value: the compact form of ActivationAddress (ActivationAddress.cs:6-34).
+ * act  = host-side activation index (the C# side maps it to its ActivationData),
+ * silo = index into the host's silo table. */
+typedef struct gd_val {
+    uint32_t act;
+    uint32_t silo;
+} gd_val;
+
+/* SiloAddress (SiloAddress.cs:33-35): IPv4 in ip[12..15] with is_v4 = 1
+ * (BinaryTokenStreamWriter.cs:485-500 layout), or 16-byte IPv6. */
+typedef struct gd_silo_addr {
+    uint8_t ip[16];
+    int32_t port;
+    int32_t generation;
+    int32_t is_v4;
+} gd_silo_addr;
+
+typedef struct gd_config {
+    uint32_t struct_size;     /* sizeof(gd_config)                                   */
+    int32_t  device;          /* HIP device ordinal                                  */
+    uint64_t table_capacity;  /* directory slots (rounded up to a power of two);
+                                 0 = 1<<20.  Keep load <= 0.5 for short probes.      */
+    uint32_t my_silo;         /* silo index this handle acts for (system targets)    */
+    uint32_t seed_silo;       /* owner of the membership-table grain; GD_NO_SILO = none */
+    uint32_t max_batch;       /* messages per call the scratch is sized for (0 = 1<<24);
+                                 larger calls grow the scratch (outside graph capture) */
+    uint32_t flags;           /* GD_CFG_* bits                                       */
+} gd_config;
+
+#define GD_CFG_KERNEL_TIMING 1u  /* record per-kernel HIP events (gd_kernel_times) */
+
+typedef struct gd_stats {
+    uint64_t routed;          /* messages through gd_route*                          */
+    uint64_t table_live;      /* live directory entries                              */
+    uint64_t table_tombstones;
+    uint64_t table_capacity;
+    uint64_t ring_points;
+    uint64_t ring_mode;
+} gd_stats;
+
+typedef struct gd_handle gd_handle;
+
+/* ---- lifecycle -------------------------------------------------------------- */
+int         gd_create(const gd_config* cfg, gd_handle** out);
+void        gd_destroy(gd_handle* h);
+const char* gd_last_error(const gd_handle* h);   /* never NULL; h may be NULL     */
+int         gd_abi_version(void);
+int         gd_set_stream(gd_handle* h, void* hip_stream); /* NULL = library stream */
+void*       gd_get_stream(gd_handle* h);
+int         gd_synchronize(gd_handle* h);
+int         gd_stats_get(gd_handle* h, gd_stats* out);
+
+/* ---- identity (host; L0) ------------------------------------------------------ */
+uint32_t gd_jenkins_hash_bytes(const uint8_t* data, size_t len);                 /* JenkinsHash.cs:25-74  */
+uint32_t gd_jenkins_hash_u64x3(uint64_t u1, uint64_t u2, uint64_t u3);          /* JenkinsHash.cs:85-105 */
+uint32_t gd_uniform_hash(const gd_key* key);                                     /* UniqueKey.cs:272-293 (no KeyExt) */
+int32_t  gd_calculate_id_hash(const char* utf8_text);                            /* Utils.cs:184-203      */
+int32_t  gd_silo_consistent_hash(const gd_silo_addr* silo);                      /* SiloAddress.cs:164-173 */
+int      gd_silo_uniform_hashes(const gd_silo_addr* silo, uint32_t n, uint32_t* out); /* SiloAddress.cs:197-248 */
+int      gd_silo_compare(const gd_silo_addr* a, const gd_silo_addr* b);          /* SiloAddress.cs:280-329 */
+
+/* ---- ring ------------------------------------------------------------------- */
+/* Build a ring from silos added in the given order (membership-change order):
+ * mode D/R -> AddServer sorted insert by signed consistent hash (ties: newcomer
+ * before equals); mode V -> buckets_per_silo uniform points per silo, uint
+ * sorted, collision -> lesser SiloAddress.  out_points / out_owner must hold
+ * n_silos (D/R) or n_silos*buckets_per_silo (V) entries; *out_n = ring size. */
+int gd_ring_build(int mode, const gd_silo_addr* silos, uint32_t n_silos, uint32_t buckets_per_silo,
+                  uint32_t* out_points, uint32_t* out_owner, uint32_t* out_n);
+/* Install a ring snapshot: points are 32-bit patterns in ring order (int32 sorted
+ * ascending for D/R, uint32 ascending for V); owner[i] = silo index of point i. */
+int gd_ring_set(gd_handle* h, int mode, const uint32_t* points, const uint32_t* owner, uint32_t n);
+
+/* CalculateTargetSilo(GrainId) for a batch: directory-owner silo per key
+ * (special categories follow the same rules as gd_route).  Host pointers. */
+int gd_ring_owner(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* out_silo);
+/* GetPrimaryTargetSilo(uint key) for a batch of raw ring keys.  Host pointers. */
+int gd_ring_lookup_hashes(gd_handle* h, const uint32_t* hashes, uint32_t n, uint32_t* out_silo);
+
+/* ---- directory (one table per handle = the silo partitions this GPU owns) ---- */
+/* AddSingleActivation for a batch, applied in batch order: the first registration
+ * of a grain wins; out_vals receives the winning (act, silo) for every item and
+ * out_inserted 1 for the item that created the entry.  Host pointers. */
+int gd_dir_register(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t n,
+                    gd_val* out_vals, uint8_t* out_inserted);
+/* RemoveActivation(grain, act) for a batch; out_removed may be NULL. */
+int gd_dir_unregister(gd_handle* h, const gd_key* keys, const uint32_t* acts, uint32_t n,
+                      uint8_t* out_removed);
+/* LookUpActivations for a batch; out_found[i] = 0 -> out_vals[i] = {GD_NO_ACTIVATION, GD_NO_SILO}. */
+int gd_dir_lookup(gd_handle* h, const gd_key* keys, uint32_t n, gd_val* out_vals, uint8_t* out_found);
+int gd_dir_clear(gd_handle* h);
+/* Rebuild into a table of new_capacity slots (drops tombstones). */
+int gd_dir_rehash(gd_handle* h, uint64_t new_capacity);
+
+/* ---- the hot path -------------------------------------------------------------- */
+/* Address a batch: ring lookup + directory probe.  Host pointers. */
+int gd_route(gd_handle* h, const gd_key* keys, uint32_t n,
+             uint32_t* out_silo, uint32_t* out_act, uint8_t* out_status);
+/* Per-activation bucketing: stable partition of message indices by activation.
+ * acts >= n_act (e.g. GD_NO_ACTIVATION) go to the trailing bucket n_act.
+ * out_perm[n]; out_offsets[n_act + 2] (bucket a = [off[a], off[a+1])).  Host pointers. */
+int gd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act,
+              uint32_t* out_perm, uint32_t* out_offsets);
+/* Fused route + bucket.  Host pointers. */
+int gd_route_bucket(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act,
+                    uint32_t* out_silo, uint32_t* out_act, uint8_t* out_status,
+                    uint32_t* out_perm, uint32_t* out_offsets);
+
+/* Device-pointer forms (enqueue only).  Same semantics as above. */
+int gd_route_device(gd_handle* h, const gd_key* d_keys, uint32_t n,
+                    uint32_t* d_silo, uint32_t* d_act, uint8_t* d_status);
+int gd_bucket_device(gd_handle* h, const uint32_t* d_acts, uint32_t n, uint32_t n_act,
+                     uint32_t* d_perm, uint32_t* d_offsets);
+int gd_route_bucket_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act,
+                           uint32_t* d_silo, uint32_t* d_act, uint8_t* d_status,
+                           uint32_t* d_perm, uint32_t* d_offsets);
+int gd_ring_owner_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t* d_silo);
+
+/* ---- multi-GPU helpers (directory sharded by ring owner, SURVEY 8 e) ------------ */
+/* Stable partition of a batch by destination shard = owner_silo % n_shards
+ * (owner from the installed ring).  Writes the keys in shard order to
+ * d_send_keys, the original message index to d_send_idx, and per-shard
+ * message counts to d_counts[n_shards].  Device pointers; n_shards <= 256. */
+int gd_pack_by_shard_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_shards,
+                            gd_key* d_send_keys, uint32_t* d_send_idx, uint32_t* d_counts);
+
+/* ---- per-kernel timing (cfg.flags & GD_CFG_KERNEL_TIMING) ----------------------- */
+/* Up to max entries of {name, launches, total_ms} accumulated since the last reset. */
+typedef struct gd_kernel_time {
+    char     name[48];
+    uint64_t launches;
+    double   total_ms;
+} gd_kernel_time;
+int gd_kernel_times(gd_handle* h, gd_kernel_time* out, uint32_t max, uint32_t* out_n);
+int gd_kernel_times_reset(gd_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GRAINDISPATCH_H */

@@ -1,0 +1,76 @@
+// gd_common.h -- definitions shared by the host identity code and the gfx950
+// kernels of libgraindispatch.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+#include "graindispatch.h"
+
+#if defined(__HIPCC__)
+#define GD_HD __host__ __device__ __forceinline__
+#else
+#define GD_HD inline
+#endif
+
+namespace gd {
+
+// ---- L0 identity (host), gd_identity.cpp --------------------------------------------
+uint32_t jenkins_bytes(const uint8_t* data, size_t len);
+uint32_t jenkins_u64x3(uint64_t u1, uint64_t u2, uint64_t u3);
+void sha256(const uint8_t* data, size_t len, uint8_t out[32]);
+int32_t calculate_id_hash(const char* utf8);
+std::string endpoint_string(const gd_silo_addr& s);
+int32_t silo_consistent_hash(const gd_silo_addr& s);
+void silo_uniform_hashes(const gd_silo_addr& s, uint32_t n, uint32_t* out);
+int silo_compare(const gd_silo_addr& a, const gd_silo_addr& b);
+
+// ---- UniqueKey categories (UniqueKey.cs:17-26) ---------------------------------------
+constexpr uint32_t CAT_SYSTEM_TARGET = 1;
+constexpr uint32_t CAT_SYSTEM_GRAIN = 2;
+constexpr uint32_t CAT_GRAIN = 3;
+constexpr uint32_t CAT_KEYEXT_GRAIN = 6;
+constexpr uint32_t CAT_GEO_CLIENT = 7;
+
+// Constants.SystemMembershipTableId (src/Orleans.Core/Runtime/Constants.cs:52):
+// SystemGrain key of Guid 01145FEC-C21E-11E0-9105-D0FB4724019B in Guid.ToByteArray
+// order (bytes EC 5F 14 01 1E C2 E0 11 | 91 05 D0 FB 47 24 01 9B, little-endian
+// u64 words).  Cross-checked against the oracle in the GPU parity tests.
+constexpr uint64_t MEMBERSHIP_N0 = 0x11E0C21E01145FECull;
+constexpr uint64_t MEMBERSHIP_N1 = 0x9B012447FBD00591ull;
+constexpr uint64_t MEMBERSHIP_TCD = (uint64_t)CAT_SYSTEM_GRAIN << 56;
+
+// ---- directory slot layout in HBM ---------------------------------------------------
+// 32 B slot, 4 per 128-B line: the 24-B GrainId key, the activation index and a
+// meta word {silo:16 | state:16}.  The state lives in the word the CAS claims.
+enum SlotState : uint32_t {
+    SLOT_EMPTY = 0,
+    SLOT_LIVE = 1,
+    SLOT_TOMB = 2,
+    SLOT_CLAIMED = 3,   // transient inside the register kernel
+    SLOT_PENDING = 4,   // created by the current register batch, winner not yet chosen
+};
+
+struct alignas(32) Slot {
+    uint64_t n0;
+    uint64_t n1;
+    uint64_t tcd;
+    uint32_t act;
+    uint32_t meta;  // (state << 16) | silo
+};
+static_assert(sizeof(Slot) == 32, "slot must be 32 bytes");
+
+GD_HD uint32_t slot_state(uint32_t meta) { return meta >> 16; }
+GD_HD uint32_t slot_silo(uint32_t meta) { return meta & 0xFFFFu; }
+GD_HD uint32_t make_meta(uint32_t state, uint32_t silo) { return (state << 16) | (silo & 0xFFFFu); }
+
+// Home slot: murmur3 fmix32 of the uniform hash, so that a shard holding one
+// contiguous ring range still spreads over the whole table.
+GD_HD uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85ebca6bu;
+    h ^= h >> 13; h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+
+}  // namespace gd

@@ -1,0 +1,739 @@
+// gd_engine.hip -- handle, scratch management and the C ABI of libgraindispatch
+// (declared in include/graindispatch.h).  Kernels live in gd_kernels.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gd_common.h"
+#include "gd_kernels.h"
+#include "graindispatch.h"
+
+using namespace gd;
+
+namespace {
+
+thread_local std::string g_tls_error = "";
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct TimedLaunch {
+    int name;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct gd_handle {
+    gd_config cfg{};
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // ring snapshot
+    int ring_mode = -1;
+    uint32_t ring_n = 0, ring_top = 0;
+    DevBuf ring_pts, ring_own;
+
+    // directory table
+    Slot* slots = nullptr;
+    unsigned long long capacity = 0;
+    DevCounters* ctr = nullptr;       // device
+    DevCounters ctr_host{};           // last copy
+
+    // scratch
+    DevBuf keys_in, u32_a, u32_b, u32_c, u32_d, u8_a, out_a, out_b, out_c, hist, partials, offs;
+    uint64_t routed = 0;
+
+    // per-kernel timing
+    bool timing = false;
+    std::vector<std::string> tnames;
+    std::vector<double> tms;
+    std::vector<uint64_t> tcount;
+    std::vector<TimedLaunch> pending;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace {
+
+int set_err(gd_handle* h, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (h) h->err = buf;
+    g_tls_error = buf;
+    return code;
+}
+
+#define HIP_TRY(h, expr)                                                                    \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return set_err((h), GD_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+    } while (0)
+
+#define GD_TRY(expr)              \
+    do {                          \
+        int r_ = (expr);          \
+        if (r_ != GD_OK) return r_; \
+    } while (0)
+
+int ensure(gd_handle* h, DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return GD_OK;
+    if (b.p) {
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+        HIP_TRY(h, hipFree(b.p));
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    size_t want = std::max<size_t>(bytes, 256);
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) return set_err(h, GD_ENOMEM, "hipMalloc(%zu): %s", want, hipGetErrorString(e));
+    b.bytes = want;
+    return GD_OK;
+}
+
+void free_buf(DevBuf& b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+int name_id(gd_handle* h, const char* name) {
+    for (size_t i = 0; i < h->tnames.size(); ++i)
+        if (h->tnames[i] == name) return (int)i;
+    h->tnames.emplace_back(name);
+    h->tms.push_back(0.0);
+    h->tcount.push_back(0);
+    return (int)h->tnames.size() - 1;
+}
+
+hipEvent_t take_event(gd_handle* h) {
+    if (!h->event_pool.empty()) {
+        hipEvent_t e = h->event_pool.back();
+        h->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+// Launch a kernel on the handle's stream; with GD_CFG_KERNEL_TIMING bracket it by events.
+template <typename K, typename... Args>
+int launch(gd_handle* h, const char* name, dim3 grid, dim3 block, size_t lds, K kernel, Args... args) {
+    if (grid.x == 0) return GD_OK;
+    hipEvent_t a = nullptr, b = nullptr;
+    if (h->timing) {
+        a = take_event(h);
+        b = take_event(h);
+        HIP_TRY(h, hipEventRecord(a, h->stream));
+    }
+    hipLaunchKernelGGL(kernel, grid, block, lds, h->stream, args...);
+    HIP_TRY(h, hipGetLastError());
+    if (h->timing) {
+        HIP_TRY(h, hipEventRecord(b, h->stream));
+        h->pending.push_back(TimedLaunch{name_id(h, name), a, b});
+    }
+    return GD_OK;
+}
+
+int resolve_timing(gd_handle* h) {
+    if (h->pending.empty()) return GD_OK;
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    for (auto& t : h->pending) {
+        float ms = 0.f;
+        HIP_TRY(h, hipEventElapsedTime(&ms, t.a, t.b));
+        h->tms[t.name] += ms;
+        h->tcount[t.name] += 1;
+        h->event_pool.push_back(t.a);
+        h->event_pool.push_back(t.b);
+    }
+    h->pending.clear();
+    return GD_OK;
+}
+
+inline uint32_t blocks_for(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
+
+int check_ring(gd_handle* h) {
+    if (h->ring_mode < 0 || h->ring_n == 0) return set_err(h, GD_ESTATE, "no ring installed (gd_ring_set)");
+    return GD_OK;
+}
+
+RingArgs ring_args(gd_handle* h) {
+    return RingArgs{(const uint32_t*)h->ring_pts.p, (const uint32_t*)h->ring_own.p, h->ring_n, h->ring_top,
+                    h->cfg.my_silo, h->cfg.seed_silo};
+}
+
+TableArgs table_args(gd_handle* h) { return TableArgs{h->slots, h->capacity - 1, h->ctr}; }
+
+size_t ring_lds(gd_handle* h) { return (size_t)h->ring_n * 2 * sizeof(uint32_t); }
+
+int pull_counters(gd_handle* h) {
+    HIP_TRY(h, hipMemcpyAsync(&h->ctr_host, h->ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    return GD_OK;
+}
+
+int alloc_table(gd_handle* h, unsigned long long cap, Slot** out) {
+    Slot* s = nullptr;
+    hipError_t e = hipMalloc(&s, cap * sizeof(Slot));
+    if (e != hipSuccess) return set_err(h, GD_ENOMEM, "table hipMalloc(%llu slots): %s", cap, hipGetErrorString(e));
+    e = hipMemsetAsync(s, 0, cap * sizeof(Slot), h->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(s);
+        return set_err(h, GD_EHIP, "table memset: %s", hipGetErrorString(e));
+    }
+    *out = s;
+    return GD_OK;
+}
+
+unsigned long long pow2_at_least(unsigned long long x) {
+    unsigned long long c = 1024;
+    while (c < x) c <<= 1;
+    return c;
+}
+
+// ---- route -------------------------------------------------------------------
+int route_device(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
+    GD_TRY(check_ring(h));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    const RingArgs r = ring_args(h);
+    const TableArgs t = table_args(h);
+    const size_t lds = ring_lds(h);
+    h->routed += n;
+    switch (h->ring_mode) {
+        case GD_RING_DIRECTORY:
+            return launch(h, "k_route", g, b, lds, k_route<GD_RING_DIRECTORY, true>, keys, n, r, t, silo, act, status);
+        case GD_RING_CONSISTENT:
+            return launch(h, "k_route", g, b, lds, k_route<GD_RING_CONSISTENT, true>, keys, n, r, t, silo, act, status);
+        default:
+            return launch(h, "k_route", g, b, lds, k_route<GD_RING_VIRTUAL_BUCKETS, true>, keys, n, r, t, silo, act, status);
+    }
+}
+
+int ring_owner_device(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo) {
+    GD_TRY(check_ring(h));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    const RingArgs r = ring_args(h);
+    const TableArgs t = table_args(h);
+    const size_t lds = ring_lds(h);
+    switch (h->ring_mode) {
+        case GD_RING_DIRECTORY:
+            return launch(h, "k_ring_owner", g, b, lds, k_route<GD_RING_DIRECTORY, false>, keys, n, r, t, silo,
+                          (uint32_t*)nullptr, (uint8_t*)nullptr);
+        case GD_RING_CONSISTENT:
+            return launch(h, "k_ring_owner", g, b, lds, k_route<GD_RING_CONSISTENT, false>, keys, n, r, t, silo,
+                          (uint32_t*)nullptr, (uint8_t*)nullptr);
+        default:
+            return launch(h, "k_ring_owner", g, b, lds, k_route<GD_RING_VIRTUAL_BUCKETS, false>, keys, n, r, t, silo,
+                          (uint32_t*)nullptr, (uint8_t*)nullptr);
+    }
+}
+
+// ---- scans -------------------------------------------------------------------
+template <class Op>
+int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inclusive, const char* tag) {
+    if (n == 0) return GD_OK;
+    const uint32_t nb = blocks_for(n, SCAN_TILE);
+    GD_TRY(ensure(h, h->partials, (size_t)nb * sizeof(uint32_t)));
+    uint32_t* part = (uint32_t*)h->partials.p;
+    (void)tag;
+    GD_TRY(launch(h, "k_scan_reduce", dim3(nb), dim3(BLOCK), 0, k_scan_reduce<Op>, (const uint32_t*)data, n, reverse, part));
+    GD_TRY(launch(h, "k_scan_partials", dim3(1), dim3(BLOCK), 0, k_scan_partials<Op>, part, nb));
+    return launch(h, "k_scan_down", dim3(nb), dim3(BLOCK), 0, k_scan_down<Op>, (const uint32_t*)data, data, n, reverse,
+                  inclusive, (const uint32_t*)part);
+}
+
+// ---- K3 bucketing -------------------------------------------------------------
+template <int BITS>
+int radix_pass(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
+               uint32_t* kout, uint32_t* vout, bool first) {
+    const uint32_t tiles = blocks_for(n, RADIX_TILE);
+    const uint32_t R = 1u << BITS;
+    GD_TRY(ensure(h, h->hist, (size_t)R * tiles * sizeof(uint32_t)));
+    uint32_t* hist = (uint32_t*)h->hist.p;
+    GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(BLOCK), 0, k_radix_hist<BITS>, kin, n, clamp, shift, tiles, hist));
+    GD_TRY(scan_device<OpAdd>(h, hist, R * tiles, false, false, "hist"));
+    if (first)
+        return launch(h, "k_radix_scatter", dim3(tiles), dim3(BLOCK), 0, k_radix_scatter<BITS, true>, kin, vin, n, clamp,
+                      shift, tiles, (const uint32_t*)hist, kout, vout);
+    return launch(h, "k_radix_scatter", dim3(tiles), dim3(BLOCK), 0, k_radix_scatter<BITS, false>, kin, vin, n, clamp,
+                  shift, tiles, (const uint32_t*)hist, kout, vout);
+}
+
+int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp,
+                   uint32_t shift, uint32_t* kout, uint32_t* vout, bool first) {
+    switch (bits) {
+        case 4: return radix_pass<4>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        case 5: return radix_pass<5>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        case 6: return radix_pass<6>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        case 7: return radix_pass<7>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        default: return radix_pass<8>(h, kin, vin, n, clamp, shift, kout, vout, first);
+    }
+}
+
+// Stable partition of indices 0..n-1 by min(acts[i], n_act):
+// LSD passes of <= 8 bits, then bucket offsets from the sorted keys.
+int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets) {
+    if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    const uint32_t n_off = n_act + 2;
+    GD_TRY(launch(h, "k_fill", dim3(blocks_for(n_off, BLOCK)), dim3(BLOCK), 0, k_fill_u32, offsets, n_off, n));
+    if (n == 0) return GD_OK;
+    uint32_t key_bits = 1;
+    while (key_bits < 32 && (n_act >> key_bits) != 0) ++key_bits;
+    const uint32_t passes = (key_bits + 7) / 8;
+    const uint32_t bits = std::max<uint32_t>(4, (key_bits + passes - 1) / passes);
+    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
+    GD_TRY(ensure(h, h->u32_b, (size_t)n * 4));
+    GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
+    GD_TRY(ensure(h, h->u32_d, (size_t)n * 4));
+    uint32_t* kb[2] = {(uint32_t*)h->u32_a.p, (uint32_t*)h->u32_b.p};
+    uint32_t* vb[2] = {(uint32_t*)h->u32_c.p, (uint32_t*)h->u32_d.p};
+    const uint32_t* kin = acts;
+    const uint32_t* vin = nullptr;
+    for (uint32_t p = 0; p < passes; ++p) {
+        uint32_t* kout = kb[p & 1];
+        uint32_t* vout = (p + 1 == passes) ? perm : vb[p & 1];
+        GD_TRY(radix_dispatch(h, (int)bits, kin, vin, n, n_act, p * bits, kout, vout, p == 0));
+        kin = kout;
+        vin = vout;
+    }
+    GD_TRY(launch(h, "k_bucket_starts", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_bucket_starts, kin, n, offsets));
+    return scan_device<OpMin>(h, offsets, n_act + 1, true, true, "offsets");
+}
+
+template <typename T>
+int h2d(gd_handle* h, DevBuf& b, const T* src, size_t count) {
+    GD_TRY(ensure(h, b, count * sizeof(T)));
+    if (count) HIP_TRY(h, hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, h->stream));
+    return GD_OK;
+}
+
+template <typename T>
+int d2h(gd_handle* h, T* dst, const DevBuf& b, size_t count) {
+    if (count && dst) HIP_TRY(h, hipMemcpyAsync(dst, b.p, count * sizeof(T), hipMemcpyDeviceToHost, h->stream));
+    return GD_OK;
+}
+
+int sync(gd_handle* h) {
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    return GD_OK;
+}
+
+int maybe_grow_table(gd_handle* h, uint64_t incoming) {
+    GD_TRY(pull_counters(h));
+    const unsigned long long used = h->ctr_host.live + h->ctr_host.tomb + incoming;
+    if (used * 4 <= h->capacity * 3) return GD_OK;  // keep load <= 0.75
+    unsigned long long cap = h->capacity;
+    while ((h->ctr_host.live + incoming) * 2 > cap) cap <<= 1;
+    return gd_dir_rehash(h, cap);
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" {
+
+const char* gd_last_error(const gd_handle* h) {
+    if (h) return h->err.c_str();
+    return g_tls_error.c_str();
+}
+
+int gd_create(const gd_config* cfg, gd_handle** out) {
+    if (!cfg || !out) return set_err(nullptr, GD_EINVAL, "gd_create: null argument");
+    if (cfg->struct_size != sizeof(gd_config)) return set_err(nullptr, GD_EINVAL, "gd_create: struct_size mismatch");
+    *out = nullptr;
+    gd_handle* h = new (std::nothrow) gd_handle();
+    if (!h) return set_err(nullptr, GD_ENOMEM, "gd_create: out of host memory");
+    h->cfg = *cfg;
+    h->device = cfg->device;
+    h->timing = (cfg->flags & GD_CFG_KERNEL_TIMING) != 0;
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) {
+        int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));
+        delete h;
+        return r;
+    }
+    e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        int r = set_err(nullptr, GD_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+        delete h;
+        return r;
+    }
+    h->stream = h->own_stream;
+    h->capacity = pow2_at_least(cfg->table_capacity ? cfg->table_capacity : (1ull << 20));
+    int r = alloc_table(h, h->capacity, &h->slots);
+    if (r == GD_OK) {
+        e = hipMalloc(&h->ctr, sizeof(DevCounters));
+        if (e != hipSuccess) r = set_err(nullptr, GD_ENOMEM, "counters: %s", hipGetErrorString(e));
+        else if ((e = hipMemsetAsync(h->ctr, 0, sizeof(DevCounters), h->stream)) != hipSuccess)
+            r = set_err(nullptr, GD_EHIP, "counters memset: %s", hipGetErrorString(e));
+    }
+    if (r == GD_OK) {
+        const uint32_t mb = cfg->max_batch ? cfg->max_batch : (1u << 24);
+        (void)mb;  // scratch grows on demand; nothing pre-sized beyond the table
+        r = sync(h);
+    }
+    if (r != GD_OK) {
+        gd_destroy(h);
+        return r;
+    }
+    *out = h;
+    return GD_OK;
+}
+
+void gd_destroy(gd_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (DevBuf* b : {&h->ring_pts, &h->ring_own, &h->keys_in, &h->u32_a, &h->u32_b, &h->u32_c, &h->u32_d, &h->u8_a,
+                      &h->out_a, &h->out_b, &h->out_c, &h->hist, &h->partials, &h->offs})
+        free_buf(*b);
+    if (h->slots) (void)hipFree(h->slots);
+    if (h->ctr) (void)hipFree(h->ctr);
+    for (auto& t : h->pending) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    for (auto e : h->event_pool) (void)hipEventDestroy(e);
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    delete h;
+}
+
+int gd_set_stream(gd_handle* h, void* s) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    GD_TRY(resolve_timing(h));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    h->stream = s ? (hipStream_t)s : h->own_stream;
+    return GD_OK;
+}
+
+void* gd_get_stream(gd_handle* h) { return h ? (void*)h->stream : nullptr; }
+
+int gd_synchronize(gd_handle* h) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    HIP_TRY(h, hipSetDevice(h->device));
+    return sync(h);
+}
+
+int gd_stats_get(gd_handle* h, gd_stats* out) {
+    if (!h || !out) return set_err(h, GD_EINVAL, "null argument");
+    GD_TRY(pull_counters(h));
+    out->routed = h->routed;
+    out->table_live = h->ctr_host.live;
+    out->table_tombstones = h->ctr_host.tomb;
+    out->table_capacity = h->capacity;
+    out->ring_points = h->ring_n;
+    out->ring_mode = (uint64_t)(int64_t)h->ring_mode;
+    return GD_OK;
+}
+
+int gd_ring_set(gd_handle* h, int mode, const uint32_t* points, const uint32_t* owner, uint32_t n) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (mode < GD_RING_DIRECTORY || mode > GD_RING_VIRTUAL_BUCKETS) return set_err(h, GD_EINVAL, "bad ring mode %d", mode);
+    if (n == 0 || n > 4096 || !points || !owner) return set_err(h, GD_EINVAL, "ring size %u not in [1, 4096]", n);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (owner[i] > 0xFFFEu) return set_err(h, GD_EINVAL, "ring owner %u out of range", owner[i]);
+        if (i == 0) continue;
+        const bool ok = (mode == GD_RING_VIRTUAL_BUCKETS) ? (points[i - 1] < points[i])
+                                                          : ((int32_t)points[i - 1] <= (int32_t)points[i]);
+        if (!ok) return set_err(h, GD_EINVAL, "ring points not in ring order at %u", i);
+    }
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(ensure(h, h->ring_pts, (size_t)n * 4));
+    GD_TRY(ensure(h, h->ring_own, (size_t)n * 4));
+    HIP_TRY(h, hipMemcpyAsync(h->ring_pts.p, points, (size_t)n * 4, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(h->ring_own.p, owner, (size_t)n * 4, hipMemcpyHostToDevice, h->stream));
+    GD_TRY(sync(h));
+    uint32_t top = 1;
+    while (top * 2 <= n) top *= 2;
+    h->ring_mode = mode;
+    h->ring_n = n;
+    h->ring_top = top;
+    return GD_OK;
+}
+
+int gd_ring_owner(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* out_silo) {
+    if (!h || (n && (!keys || !out_silo))) return set_err(h, GD_EINVAL, "null argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * 4));
+    if (n) GD_TRY(ring_owner_device(h, (const gd_key*)h->keys_in.p, n, (uint32_t*)h->out_a.p));
+    GD_TRY(d2h(h, out_silo, h->out_a, n));
+    return sync(h);
+}
+
+int gd_ring_owner_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t* d_silo) {
+    if (!h || (n && (!d_keys || !d_silo))) return set_err(h, GD_EINVAL, "null argument");
+    return n ? ring_owner_device(h, d_keys, n, d_silo) : GD_OK;
+}
+
+int gd_ring_lookup_hashes(gd_handle* h, const uint32_t* hashes, uint32_t n, uint32_t* out_silo) {
+    if (!h || (n && (!hashes || !out_silo))) return set_err(h, GD_EINVAL, "null argument");
+    GD_TRY(check_ring(h));
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->u32_a, hashes, n));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * 4));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    const RingArgs r = ring_args(h);
+    const uint32_t* in = (const uint32_t*)h->u32_a.p;
+    uint32_t* o = (uint32_t*)h->out_a.p;
+    if (n) {
+        if (h->ring_mode == GD_RING_DIRECTORY)
+            GD_TRY(launch(h, "k_ring_hashes", g, b, ring_lds(h), k_ring_hashes<GD_RING_DIRECTORY>, in, n, r, o));
+        else if (h->ring_mode == GD_RING_CONSISTENT)
+            GD_TRY(launch(h, "k_ring_hashes", g, b, ring_lds(h), k_ring_hashes<GD_RING_CONSISTENT>, in, n, r, o));
+        else
+            GD_TRY(launch(h, "k_ring_hashes", g, b, ring_lds(h), k_ring_hashes<GD_RING_VIRTUAL_BUCKETS>, in, n, r, o));
+    }
+    GD_TRY(d2h(h, out_silo, h->out_a, n));
+    return sync(h);
+}
+
+int gd_dir_register(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t n, gd_val* out_vals,
+                    uint8_t* out_inserted) {
+    if (!h || (n && (!keys || !vals || !out_vals || !out_inserted))) return set_err(h, GD_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n; ++i)
+        if (vals[i].silo > 0xFFFEu) return set_err(h, GD_EINVAL, "silo index %u out of range at %u", vals[i].silo, i);
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(maybe_grow_table(h, n));
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(h2d(h, h->out_c, vals, n));     // gd_val staging
+    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));   // slot_of
+    GD_TRY(ensure(h, h->u32_b, (size_t)n * 4));   // win
+    GD_TRY(ensure(h, h->u8_a, (size_t)n));        // is_new
+    GD_TRY(ensure(h, h->out_a, (size_t)n * sizeof(gd_val)));
+    GD_TRY(ensure(h, h->out_b, (size_t)n));
+    HIP_TRY(h, hipMemsetAsync(h->u8_a.p, 0, n, h->stream));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    uint32_t* slot_of = (uint32_t*)h->u32_a.p;
+    uint32_t* win = (uint32_t*)h->u32_b.p;
+    uint8_t* is_new = (uint8_t*)h->u8_a.p;
+    const gd_key* dk = (const gd_key*)h->keys_in.p;
+    const unsigned long long mask = h->capacity - 1;
+    // claim pass, then relaunches for the items that met an unpublished claim
+    for (uint32_t pass = 0;; ++pass) {
+        HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
+        GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
+                      (uint32_t)(pass > 0)));
+        GD_TRY(pull_counters(h));
+        if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
+        if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_register: claims did not settle");
+    }
+    GD_TRY(launch(h, "k_reg_minwin", g, b, 0, k_reg_minwin, (const uint32_t*)slot_of, (const uint8_t*)is_new, n, h->slots));
+    GD_TRY(launch(h, "k_reg_resolve", g, b, 0, k_reg_resolve, (const uint32_t*)slot_of, (const uint8_t*)is_new, n,
+                  (const Slot*)h->slots, win));
+    GD_TRY(launch(h, "k_reg_commit", g, b, 0, k_reg_commit, (const uint32_t*)slot_of, (const uint32_t*)win,
+                  (const gd_val*)h->out_c.p, n, h->slots, h->ctr));
+    GD_TRY(launch(h, "k_reg_report", g, b, 0, k_reg_report, (const uint32_t*)slot_of, (const uint32_t*)win, n,
+                  (const Slot*)h->slots, (gd_val*)h->out_a.p, (uint8_t*)h->out_b.p));
+    GD_TRY(d2h(h, out_vals, h->out_a, n));
+    GD_TRY(d2h(h, out_inserted, h->out_b, n));
+    GD_TRY(pull_counters(h));
+    if (h->ctr_host.err) {
+        const uint32_t e = h->ctr_host.err;
+        HIP_TRY(h, hipMemsetAsync(&h->ctr->err, 0, sizeof(uint32_t), h->stream));
+        return set_err(h, (e & 2) ? GD_EFULL : GD_ETIMEOUT, "gd_dir_register: device error bits 0x%x", e);
+    }
+    return GD_OK;
+}
+
+int gd_dir_unregister(gd_handle* h, const gd_key* keys, const uint32_t* acts, uint32_t n, uint8_t* out_removed) {
+    if (!h || (n && (!keys || !acts))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(h2d(h, h->u32_b, acts, n));
+    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
+    GD_TRY(ensure(h, h->out_b, (size_t)n));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    uint32_t* slot_of = (uint32_t*)h->u32_a.p;
+    const unsigned long long mask = h->capacity - 1;
+    GD_TRY(launch(h, "k_unreg_find", g, b, 0, k_unreg_find, (const gd_key*)h->keys_in.p, (const uint32_t*)h->u32_b.p, n,
+                  (const Slot*)h->slots, mask, (const DevCounters*)h->ctr, slot_of));
+    GD_TRY(launch(h, "k_unreg_poison", g, b, 0, k_unreg_poison, (const uint32_t*)slot_of, n, h->slots));
+    GD_TRY(launch(h, "k_unreg_min", g, b, 0, k_unreg_min, (const uint32_t*)slot_of, n, h->slots));
+    GD_TRY(launch(h, "k_unreg_commit", g, b, 0, k_unreg_commit, (const uint32_t*)slot_of, n, h->slots, h->ctr,
+                  (uint8_t*)h->out_b.p));
+    GD_TRY(d2h(h, out_removed, h->out_b, n));
+    return sync(h);
+}
+
+int gd_dir_lookup(gd_handle* h, const gd_key* keys, uint32_t n, gd_val* out_vals, uint8_t* out_found) {
+    if (!h || (n && (!keys || !out_vals || !out_found))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * sizeof(gd_val)));
+    GD_TRY(ensure(h, h->out_b, (size_t)n));
+    GD_TRY(launch(h, "k_dir_lookup", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_dir_lookup,
+                  (const gd_key*)h->keys_in.p, n, table_args(h), (gd_val*)h->out_a.p, (uint8_t*)h->out_b.p));
+    GD_TRY(d2h(h, out_vals, h->out_a, n));
+    GD_TRY(d2h(h, out_found, h->out_b, n));
+    return sync(h);
+}
+
+int gd_dir_clear(gd_handle* h) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    HIP_TRY(h, hipSetDevice(h->device));
+    HIP_TRY(h, hipMemsetAsync(h->slots, 0, h->capacity * sizeof(Slot), h->stream));
+    HIP_TRY(h, hipMemsetAsync(h->ctr, 0, sizeof(DevCounters), h->stream));
+    return sync(h);
+}
+
+int gd_dir_rehash(gd_handle* h, uint64_t new_capacity) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(pull_counters(h));
+    const unsigned long long cap = pow2_at_least(new_capacity);
+    if (cap < h->ctr_host.live) return set_err(h, GD_EINVAL, "capacity %llu below live entries", cap);
+    Slot* ns = nullptr;
+    GD_TRY(alloc_table(h, cap, &ns));
+    DevCounters fresh{};
+    HIP_TRY(h, hipMemcpyAsync(h->ctr, &fresh, sizeof fresh, hipMemcpyHostToDevice, h->stream));
+    const unsigned long long old_cap = h->capacity;
+    const uint32_t g = (uint32_t)((old_cap + BLOCK - 1) / BLOCK);
+    GD_TRY(launch(h, "k_rehash", dim3(g), dim3(BLOCK), 0, k_rehash, (const Slot*)h->slots, old_cap, ns, cap - 1, h->ctr));
+    GD_TRY(sync(h));
+    HIP_TRY(h, hipFree(h->slots));
+    h->slots = ns;
+    h->capacity = cap;
+    GD_TRY(pull_counters(h));
+    if (h->ctr_host.err) return set_err(h, GD_EFULL, "rehash failed (0x%x)", h->ctr_host.err);
+    return GD_OK;
+}
+
+int gd_route_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t* d_silo, uint32_t* d_act, uint8_t* d_status) {
+    if (!h || (n && (!d_keys || !d_silo || !d_act || !d_status))) return set_err(h, GD_EINVAL, "null argument");
+    return n ? route_device(h, d_keys, n, d_silo, d_act, d_status) : GD_OK;
+}
+
+int gd_bucket_device(gd_handle* h, const uint32_t* d_acts, uint32_t n, uint32_t n_act, uint32_t* d_perm,
+                     uint32_t* d_offsets) {
+    if (!h || !d_offsets || (n && (!d_acts || !d_perm))) return set_err(h, GD_EINVAL, "null argument");
+    return bucket_device(h, d_acts, n, n_act, d_perm, d_offsets);
+}
+
+int gd_route_bucket_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, uint32_t* d_silo,
+                           uint32_t* d_act, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets) {
+    if (!h || !d_offsets || (n && (!d_keys || !d_silo || !d_act || !d_status || !d_perm)))
+        return set_err(h, GD_EINVAL, "null argument");
+    if (n) GD_TRY(route_device(h, d_keys, n, d_silo, d_act, d_status));
+    return bucket_device(h, d_act, n, n_act, d_perm, d_offsets);
+}
+
+int gd_route(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* out_silo, uint32_t* out_act, uint8_t* out_status) {
+    if (!h || (n && (!keys || !out_silo || !out_act || !out_status))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * 4));
+    GD_TRY(ensure(h, h->out_b, (size_t)n * 4));
+    GD_TRY(ensure(h, h->out_c, (size_t)n));
+    GD_TRY(route_device(h, (const gd_key*)h->keys_in.p, n, (uint32_t*)h->out_a.p, (uint32_t*)h->out_b.p,
+                        (uint8_t*)h->out_c.p));
+    GD_TRY(d2h(h, out_silo, h->out_a, n));
+    GD_TRY(d2h(h, out_act, h->out_b, n));
+    GD_TRY(d2h(h, out_status, h->out_c, n));
+    return sync(h);
+}
+
+int gd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* out_perm, uint32_t* out_offsets) {
+    if (!h || !out_offsets || (n && (!acts || !out_perm))) return set_err(h, GD_EINVAL, "null argument");
+    if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->out_b, acts, n));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * 4 + 4));
+    GD_TRY(ensure(h, h->offs, ((size_t)n_act + 2) * 4));
+    GD_TRY(bucket_device(h, (const uint32_t*)h->out_b.p, n, n_act, (uint32_t*)h->out_a.p, (uint32_t*)h->offs.p));
+    GD_TRY(d2h(h, out_perm, h->out_a, n));
+    GD_TRY(d2h(h, out_offsets, h->offs, (size_t)n_act + 2));
+    return sync(h);
+}
+
+int gd_route_bucket(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, uint32_t* out_silo, uint32_t* out_act,
+                    uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets) {
+    if (!h || !out_offsets || (n && (!keys || !out_silo || !out_act || !out_status || !out_perm)))
+        return set_err(h, GD_EINVAL, "null argument");
+    if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * 4 + 4));
+    GD_TRY(ensure(h, h->out_b, (size_t)n * 4 + 4));
+    GD_TRY(ensure(h, h->out_c, (size_t)n + 4));
+    GD_TRY(ensure(h, h->u8_a, (size_t)n * 4 + 4));   // perm
+    GD_TRY(ensure(h, h->offs, ((size_t)n_act + 2) * 4));
+    if (n)
+        GD_TRY(route_device(h, (const gd_key*)h->keys_in.p, n, (uint32_t*)h->out_a.p, (uint32_t*)h->out_b.p,
+                            (uint8_t*)h->out_c.p));
+    GD_TRY(bucket_device(h, (const uint32_t*)h->out_b.p, n, n_act, (uint32_t*)h->u8_a.p, (uint32_t*)h->offs.p));
+    GD_TRY(d2h(h, out_silo, h->out_a, n));
+    GD_TRY(d2h(h, out_act, h->out_b, n));
+    GD_TRY(d2h(h, out_status, h->out_c, n));
+    GD_TRY(d2h(h, out_perm, h->u8_a, n));
+    GD_TRY(d2h(h, out_offsets, h->offs, (size_t)n_act + 2));
+    return sync(h);
+}
+
+int gd_pack_by_shard_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_shards, gd_key* d_send_keys,
+                            uint32_t* d_send_idx, uint32_t* d_counts) {
+    if (!h || !d_counts || (n && (!d_keys || !d_send_keys || !d_send_idx))) return set_err(h, GD_EINVAL, "null argument");
+    if (n_shards == 0 || n_shards > 256) return set_err(h, GD_EINVAL, "n_shards %u not in [1, 256]", n_shards);
+    GD_TRY(check_ring(h));
+    GD_TRY(ensure(h, h->out_b, (size_t)n * 4 + 4));                 // dest
+    GD_TRY(ensure(h, h->offs, ((size_t)n_shards + 2) * 4));
+    uint32_t* dest = (uint32_t*)h->out_b.p;
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    const RingArgs r = ring_args(h);
+    if (n) {
+        if (h->ring_mode == GD_RING_DIRECTORY)
+            GD_TRY(launch(h, "k_shard_dest", g, b, ring_lds(h), k_shard_dest<GD_RING_DIRECTORY>, d_keys, n, r, n_shards, dest));
+        else if (h->ring_mode == GD_RING_CONSISTENT)
+            GD_TRY(launch(h, "k_shard_dest", g, b, ring_lds(h), k_shard_dest<GD_RING_CONSISTENT>, d_keys, n, r, n_shards, dest));
+        else
+            GD_TRY(launch(h, "k_shard_dest", g, b, ring_lds(h), k_shard_dest<GD_RING_VIRTUAL_BUCKETS>, d_keys, n, r,
+                          n_shards, dest));
+    }
+    GD_TRY(bucket_device(h, dest, n, n_shards, d_send_idx, (uint32_t*)h->offs.p));
+    if (n)
+        GD_TRY(launch(h, "k_gather_keys", g, b, 0, k_gather_keys, d_keys, (const uint32_t*)d_send_idx, n, d_send_keys));
+    return launch(h, "k_counts", dim3(1), dim3(BLOCK), 0, k_counts_from_offsets, (const uint32_t*)h->offs.p, n_shards,
+                  d_counts);
+}
+
+int gd_kernel_times(gd_handle* h, gd_kernel_time* out, uint32_t max, uint32_t* out_n) {
+    if (!h || !out_n) return set_err(h, GD_EINVAL, "null argument");
+    GD_TRY(resolve_timing(h));
+    const uint32_t m = (uint32_t)std::min<size_t>(max, h->tnames.size());
+    for (uint32_t i = 0; i < m; ++i) {
+        std::memset(out[i].name, 0, sizeof out[i].name);
+        std::strncpy(out[i].name, h->tnames[i].c_str(), sizeof out[i].name - 1);
+        out[i].launches = h->tcount[i];
+        out[i].total_ms = h->tms[i];
+    }
+    *out_n = (uint32_t)h->tnames.size();
+    return GD_OK;
+}
+
+int gd_kernel_times_reset(gd_handle* h) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    GD_TRY(resolve_timing(h));
+    std::fill(h->tms.begin(), h->tms.end(), 0.0);
+    std::fill(h->tcount.begin(), h->tcount.end(), 0);
+    return GD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,733 @@
+// gd_kernels.h -- gfx950 device code of libgraindispatch.
+//
+// Hot path (per message, all integer, HBM-bound, no MFMA):
+//   K0+K1+K2  k_route        Jenkins hash of the 24-B GrainId (JenkinsHash.cs:85-105),
+//                            ring search over an LDS-staged snapshot
+//                            (LocalGrainDirectory.cs:477-545 / ConsistentRingProvider.cs:322-372 /
+//                            VirtualBucketsRingProvider.cs:257-293), linear-probe of the
+//                            open-addressing directory (GrainDirectoryPartition.cs:385-441).
+//   K3        k_radix_*      stable LSD partition of message indices by activation
+//                            (ActivationData.cs:566-606 per-activation FIFO), reduce-then-scan.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gd_common.h"
+
+namespace gd {
+
+constexpr int WAVE = 64;
+constexpr int BLOCK = 256;               // 4 waves
+constexpr int RADIX_ITEMS = 16;          // items per thread in a radix tile
+constexpr int RADIX_TILE = BLOCK * RADIX_ITEMS;   // 4096 messages per tile
+constexpr int SCAN_ITEMS = 16;
+constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+
+struct DevCounters {
+    uint32_t max_probe;     // largest probe distance of any entry placed so far
+    uint32_t err;           // bit 1: table full
+    uint32_t retry;         // items k_reg_claim deferred to a relaunch
+    uint32_t pad;
+    unsigned long long live;
+    unsigned long long tomb;
+};
+
+// ------------------------------------------------------------------ identity
+__device__ __forceinline__ void jmix(uint32_t& a, uint32_t& b, uint32_t& c) {
+    a -= b; a -= c; a ^= (c >> 13);
+    b -= c; b -= a; b ^= (a << 8);
+    c -= a; c -= b; c ^= (b >> 13);
+    a -= b; a -= c; a ^= (c >> 12);
+    b -= c; b -= a; b ^= (a << 16);
+    c -= a; c -= b; c ^= (b >> 5);
+    a -= b; a -= c; a ^= (c >> 3);
+    b -= c; b -= a; b ^= (a << 10);
+    c -= a; c -= b; c ^= (b >> 15);
+}
+
+// UniqueKey.GetUniformHashCode = JenkinsHash.ComputeHash(TypeCodeData, N0, N1)
+// (UniqueKey.cs:285; JenkinsHash.cs:85-105).
+__device__ __forceinline__ uint32_t uniform_hash(uint64_t n0, uint64_t n1, uint64_t tcd) {
+    uint32_t a = 0x9e3779b9u, b = a, c = 0;
+    a += (uint32_t)tcd;
+    b += (uint32_t)(tcd >> 32);
+    c += (uint32_t)n0;
+    jmix(a, b, c);
+    a += (uint32_t)(n0 >> 32);
+    b += (uint32_t)n1;
+    c += (uint32_t)(n1 >> 32);
+    jmix(a, b, c);
+    c += 24;
+    jmix(a, b, c);
+    return c;
+}
+
+// ------------------------------------------------------------------ ring
+// Count of the prefix of the ring satisfying the mode's monotone predicate,
+// by a branch-free power-of-two search over the LDS copy.
+template <int MODE>
+__device__ __forceinline__ bool ring_pred(uint32_t p, uint32_t h) {
+    if constexpr (MODE == GD_RING_DIRECTORY) {
+        // IsSiloNextInTheRing: siloHash <= (int)grainHash (LocalGrainDirectory.cs:1141-1144)
+        return (int32_t)p <= (int32_t)h;
+    } else if constexpr (MODE == GD_RING_CONSISTENT) {
+        // complement of (long)siloHash >= (long)key (ConsistentRingProvider.cs:369-372)
+        return (int32_t)p < 0 || p < h;
+    } else {
+        // complement of point >= key, uint (VirtualBucketsRingProvider.cs:276)
+        return p < h;
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ uint32_t ring_position(const uint32_t* pts, uint32_t n, uint32_t top, uint32_t h) {
+    uint32_t cnt = 0;
+    for (uint32_t step = top; step > 0; step >>= 1) {
+        const uint32_t c = cnt + step;
+        if (c <= n && ring_pred<MODE>(pts[c - 1], h)) cnt = c;
+    }
+    if constexpr (MODE == GD_RING_DIRECTORY) {
+        // scan from the end for the first match; none -> last silo (:521-538)
+        return cnt == 0 ? n - 1 : cnt - 1;
+    } else {
+        // scan from the start for the first match; none -> first (:341-352 / :279-289)
+        return cnt == n ? 0 : cnt;
+    }
+}
+
+struct RingArgs {
+    const uint32_t* pts;
+    const uint32_t* own;
+    uint32_t n;
+    uint32_t top;       // highest power of two <= n
+    uint32_t my_silo;
+    uint32_t seed_silo;
+};
+
+struct TableArgs {
+    const Slot* slots;
+    unsigned long long mask;
+    const DevCounters* ctr;
+};
+
+__device__ __forceinline__ void stage_ring(const RingArgs& r, uint32_t* s_pts, uint32_t* s_own) {
+    for (uint32_t i = threadIdx.x; i < r.n; i += blockDim.x) {
+        s_pts[i] = r.pts[i];
+        s_own[i] = r.own[i];
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ bool is_membership(uint64_t n0, uint64_t n1, uint64_t tcd) {
+    return n0 == MEMBERSHIP_N0 && n1 == MEMBERSHIP_N1 && tcd == MEMBERSHIP_TCD;
+}
+
+// Linear probe of the open-addressing directory for a live entry with this key.
+__device__ __forceinline__ bool probe(const Slot* slots, unsigned long long mask, uint32_t max_probe,
+                                      uint32_t h, uint64_t n0, uint64_t n1, uint64_t tcd,
+                                      uint32_t& act, uint32_t& meta) {
+    unsigned long long s = fmix32(h) & mask;
+    for (uint32_t p = 0; p <= max_probe; ++p) {
+        const uint4* q = reinterpret_cast<const uint4*>(slots + s);
+        const uint4 a = q[0];
+        const uint4 b = q[1];
+        const uint32_t st = slot_state(b.w);
+        if (st == SLOT_EMPTY) return false;
+        const uint64_t k0 = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        const uint64_t k1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
+        const uint64_t k2 = (uint64_t)b.x | ((uint64_t)b.y << 32);
+        if (st == SLOT_LIVE && k0 == n0 && k1 == n1 && k2 == tcd) {
+            act = b.z;
+            meta = b.w;
+            return true;
+        }
+        s = (s + 1) & mask;
+    }
+    return false;
+}
+
+// ------------------------------------------------------------------ K0+K1+K2: route
+// One message per thread.  PROBE=false gives CalculateTargetSilo only.
+template <int MODE, bool PROBE>
+__global__ void __launch_bounds__(BLOCK) k_route(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+                                                 TableArgs tab, uint32_t* __restrict__ out_silo,
+                                                 uint32_t* __restrict__ out_act,
+                                                 uint8_t* __restrict__ out_status) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    stage_ring(ring, s_pts, s_own);
+    const uint32_t max_probe = PROBE ? tab.ctr->max_probe : 0;
+
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
+    const uint64_t n0 = kp[0], n1 = kp[1], tcd = kp[2];
+    const uint32_t cat = (uint32_t)(tcd >> 56);
+    uint32_t silo, act = NONE32;
+    uint8_t status;
+    if (cat == CAT_SYSTEM_TARGET) {                        // LocalGrainDirectory.cs:480-485
+        silo = ring.my_silo;
+        status = GD_ROUTE_SYSTEM_TARGET;
+    } else if (is_membership(n0, n1, tcd)) {               // :487-503
+        silo = ring.seed_silo;
+        status = GD_ROUTE_MEMBERSHIP;
+    } else if (cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) {  // UniqueKey.cs:279-281
+        silo = NONE32;
+        status = GD_ROUTE_KEYEXT;
+    } else {
+        const uint32_t h = uniform_hash(n0, n1, tcd);
+        silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h)];
+        status = GD_ROUTE_OK;
+        if constexpr (PROBE) {
+            uint32_t a, meta;
+            if (probe(tab.slots, tab.mask, max_probe, h, n0, n1, tcd, a, meta)) {
+                act = a;
+                silo = slot_silo(meta);                    // ActivationAddress.Silo (Message.cs:629-639)
+            } else {
+                status = GD_ROUTE_MISS;                    // Dispatcher.cs:742 slow path
+            }
+        }
+    }
+    out_silo[i] = silo;
+    if constexpr (PROBE) {
+        out_act[i] = act;
+        out_status[i] = status;
+    }
+}
+
+// GetPrimaryTargetSilo(uint key) over raw ring keys.
+template <int MODE>
+__global__ void __launch_bounds__(BLOCK) k_ring_hashes(const uint32_t* __restrict__ hashes, uint32_t n,
+                                                       RingArgs ring, uint32_t* __restrict__ out_silo) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    stage_ring(ring, s_pts, s_own);
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    out_silo[i] = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, hashes[i])];
+}
+
+// Destination shard of each message (owner silo % n_shards) for the exchange.
+template <int MODE>
+__global__ void __launch_bounds__(BLOCK) k_shard_dest(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+                                                      uint32_t n_shards, uint32_t* __restrict__ dest) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    stage_ring(ring, s_pts, s_own);
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
+    const uint64_t n0 = kp[0], n1 = kp[1], tcd = kp[2];
+    const uint32_t cat = (uint32_t)(tcd >> 56);
+    uint32_t silo;
+    if (cat == CAT_SYSTEM_TARGET || cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) silo = ring.my_silo;
+    else if (is_membership(n0, n1, tcd)) silo = ring.seed_silo;
+    else silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(n0, n1, tcd))];
+    dest[i] = (silo == NONE32 ? ring.my_silo : silo) % n_shards;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_gather_keys(const gd_key* __restrict__ keys,
+                                                       const uint32_t* __restrict__ perm, uint32_t n,
+                                                       gd_key* __restrict__ out) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    out[i] = keys[perm[i]];
+}
+
+__global__ void k_counts_from_offsets(const uint32_t* __restrict__ off, uint32_t m, uint32_t* __restrict__ counts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) counts[i] = off[i + 1] - off[i];
+}
+
+// ------------------------------------------------------------------ directory maintenance
+// AddSingleActivation (GrainDirectoryPartition.cs:304-326, GrainInfo :110-124) for a batch.
+// Phase 1: find the key's slot or claim an empty one.  A lane that meets a slot
+// another lane has claimed but not yet published does NOT wait (a divergent
+// wait can starve the claimer of the same wave once the compiler sinks its
+// publish to the loop exit): it is marked RETRY and the host relaunches the
+// kernel for the retried items, after the kernel boundary has published every
+// claim.
+constexpr uint32_t SLOT_RETRY = 0xFFFFFFFEu;
+
+__global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __restrict__ keys, uint32_t n, Slot* slots,
+                                                     unsigned long long mask, DevCounters* ctr,
+                                                     uint32_t* __restrict__ slot_of,
+                                                     uint8_t* __restrict__ is_new, uint32_t retry_only) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    if (retry_only && slot_of[i] != SLOT_RETRY) return;
+    const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
+    unsigned long long s = fmix32(uniform_hash(n0, n1, tcd)) & mask;
+    unsigned long long dist = 0;
+    uint32_t res = NONE32;
+    uint8_t fresh = 0;
+    for (;;) {
+        uint32_t* meta_p = &slots[s].meta;
+        const uint32_t meta = __hip_atomic_load(meta_p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t st = slot_state(meta);
+        if (st == SLOT_EMPTY) {
+            uint32_t expected = meta;
+            if (__hip_atomic_compare_exchange_strong(meta_p, &expected, make_meta(SLOT_CLAIMED, 0),
+                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)) {
+                __hip_atomic_store(&slots[s].n0, n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&slots[s].n1, n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&slots[s].tcd, tcd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&slots[s].act, NONE32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(meta_p, make_meta(SLOT_PENDING, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicMax(&ctr->max_probe, (uint32_t)dist);
+                res = (uint32_t)s;
+                fresh = 1;
+                break;
+            }
+            continue;   // lost the CAS: re-read the same slot
+        }
+        if (st == SLOT_CLAIMED) {        // claimed in this launch, key not yet visible
+            res = SLOT_RETRY;
+            atomicAdd(&ctr->retry, 1u);
+            break;
+        }
+        if (st == SLOT_LIVE || st == SLOT_PENDING) {
+            const uint64_t k0 = __hip_atomic_load(&slots[s].n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t k1 = __hip_atomic_load(&slots[s].n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t k2 = __hip_atomic_load(&slots[s].tcd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k0 == n0 && k1 == n1 && k2 == tcd) {
+                res = (uint32_t)s;
+                fresh = (st == SLOT_PENDING) ? 1 : 0;
+                break;
+            }
+        }
+        s = (s + 1) & mask;
+        if (++dist > mask) {
+            atomicOr(&ctr->err, 2u);
+            break;
+        }
+    }
+    slot_of[i] = res;
+    is_new[i] = fresh;
+}
+
+// Phase 2: the lowest batch index among the items of a new entry wins (sequential
+// "first registration wins" order).
+__global__ void __launch_bounds__(BLOCK) k_reg_minwin(const uint32_t* __restrict__ slot_of,
+                                                      const uint8_t* __restrict__ is_new, uint32_t n, Slot* slots) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n || !is_new[i]) return;
+    atomicMin(&slots[slot_of[i]].act, i);   // is_new implies a real slot index
+}
+
+__global__ void __launch_bounds__(BLOCK) k_reg_resolve(const uint32_t* __restrict__ slot_of,
+                                                       const uint8_t* __restrict__ is_new, uint32_t n,
+                                                       const Slot* slots, uint32_t* __restrict__ win) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    win[i] = is_new[i] ? slots[slot_of[i]].act : NONE32;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_reg_commit(const uint32_t* __restrict__ slot_of,
+                                                      const uint32_t* __restrict__ win,
+                                                      const gd_val* __restrict__ vals, uint32_t n, Slot* slots,
+                                                      DevCounters* ctr) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n || win[i] != i) return;
+    Slot& sl = slots[slot_of[i]];
+    sl.act = vals[i].act;
+    sl.meta = make_meta(SLOT_LIVE, vals[i].silo);
+    atomicAdd(&ctr->live, 1ull);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_reg_report(const uint32_t* __restrict__ slot_of,
+                                                      const uint32_t* __restrict__ win, uint32_t n,
+                                                      const Slot* slots, gd_val* __restrict__ out_vals,
+                                                      uint8_t* __restrict__ out_inserted) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slot_of[i];
+    if (s >= SLOT_RETRY) {
+        out_vals[i] = gd_val{NONE32, NONE32};
+        out_inserted[i] = 0;
+        return;
+    }
+    const Slot sl = slots[s];
+    out_vals[i] = gd_val{sl.act, slot_silo(sl.meta)};
+    out_inserted[i] = (win[i] == i) ? 1 : 0;
+}
+
+// RemoveActivation (GrainDirectoryPartition.cs:335-363, Force): find the live entry
+// whose single activation matches; the first matching item of the batch removes it.
+__global__ void __launch_bounds__(BLOCK) k_unreg_find(const gd_key* __restrict__ keys,
+                                                      const uint32_t* __restrict__ acts, uint32_t n,
+                                                      const Slot* slots, unsigned long long mask,
+                                                      const DevCounters* ctr, uint32_t* __restrict__ slot_of) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
+    const uint32_t h = uniform_hash(n0, n1, tcd);
+    unsigned long long s = fmix32(h) & mask;
+    uint32_t res = NONE32;
+    for (uint32_t p = 0; p <= ctr->max_probe; ++p) {
+        const Slot sl = slots[s];
+        const uint32_t st = slot_state(sl.meta);
+        if (st == SLOT_EMPTY) break;
+        if (st == SLOT_LIVE && sl.n0 == n0 && sl.n1 == n1 && sl.tcd == tcd) {
+            if (sl.act == acts[i]) res = (uint32_t)s;
+            break;
+        }
+        s = (s + 1) & mask;
+    }
+    slot_of[i] = res;
+}
+
+// The matched entry is being removed, so its n0 word can carry the election.
+__global__ void __launch_bounds__(BLOCK) k_unreg_poison(const uint32_t* __restrict__ slot_of, uint32_t n, Slot* slots) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n || slot_of[i] == NONE32) return;
+    slots[slot_of[i]].n0 = ~0ull;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_unreg_min(const uint32_t* __restrict__ slot_of, uint32_t n, Slot* slots) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n || slot_of[i] == NONE32) return;
+    atomicMin(reinterpret_cast<unsigned long long*>(&slots[slot_of[i]].n0), (unsigned long long)i);
+}
+
+__global__ void __launch_bounds__(BLOCK) k_unreg_commit(const uint32_t* __restrict__ slot_of, uint32_t n,
+                                                        Slot* slots, DevCounters* ctr,
+                                                        uint8_t* __restrict__ out_removed) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slot_of[i];
+    uint8_t removed = 0;
+    if (s != NONE32 && slots[s].n0 == (uint64_t)i) {
+        slots[s].meta = make_meta(SLOT_TOMB, 0);
+        atomicAdd(&ctr->live, ~0ull);   // -1
+        atomicAdd(&ctr->tomb, 1ull);
+        removed = 1;
+    }
+    if (out_removed) out_removed[i] = removed;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_dir_lookup(const gd_key* __restrict__ keys, uint32_t n, TableArgs tab,
+                                                      gd_val* __restrict__ out_vals, uint8_t* __restrict__ found) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
+    uint32_t act, meta;
+    const bool hit = probe(tab.slots, tab.mask, tab.ctr->max_probe, uniform_hash(n0, n1, tcd), n0, n1, tcd, act, meta);
+    out_vals[i] = hit ? gd_val{act, slot_silo(meta)} : gd_val{NONE32, NONE32};
+    found[i] = hit ? 1 : 0;
+}
+
+// Rebuild: every live entry of the old table into the new one (keys are distinct,
+// so a claimer never needs to compare keys).
+__global__ void __launch_bounds__(BLOCK) k_rehash(const Slot* __restrict__ old_slots, unsigned long long old_cap,
+                                                  Slot* slots, unsigned long long mask, DevCounters* ctr) {
+    const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= old_cap) return;
+    const Slot sl = old_slots[j];
+    if (slot_state(sl.meta) != SLOT_LIVE) return;
+    unsigned long long s = fmix32(uniform_hash(sl.n0, sl.n1, sl.tcd)) & mask;
+    for (uint32_t dist = 0; dist <= mask; ++dist) {
+        uint32_t expected = make_meta(SLOT_EMPTY, 0);
+        if (__hip_atomic_compare_exchange_strong(&slots[s].meta, &expected, make_meta(SLOT_CLAIMED, 0),
+                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            slots[s].n0 = sl.n0;
+            slots[s].n1 = sl.n1;
+            slots[s].tcd = sl.tcd;
+            slots[s].act = sl.act;
+            __hip_atomic_store(&slots[s].meta, sl.meta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            atomicMax(&ctr->max_probe, dist);
+            atomicAdd(&ctr->live, 1ull);
+            return;
+        }
+        s = (s + 1) & mask;
+    }
+    atomicOr(&ctr->err, 2u);
+}
+
+// ------------------------------------------------------------------ wave helpers
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Lanes of the wave holding the same BITS-bit digit (match_any by ballots).
+template <int BITS>
+__device__ __forceinline__ unsigned long long match_digit(uint32_t d, bool valid) {
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const unsigned long long bal = __ballot(bit);
+        peers &= bit ? bal : ~bal;
+    }
+    return peers;
+}
+
+// Block-wide exclusive add-scan of one value per thread (BLOCK threads).
+__device__ __forceinline__ uint32_t block_excl_scan_add(uint32_t v, uint32_t* s_wsum, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, WAVE);
+        if (lane >= (uint32_t)off) x += y;
+    }
+    if (lane == WAVE - 1) s_wsum[w] = x;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < BLOCK / WAVE; ++k) {
+        const uint32_t t = s_wsum[k];
+        if ((uint32_t)k < w) wbase += t;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return wbase + x - v;
+}
+
+// ------------------------------------------------------------------ K3: stable radix partition
+// Tile = RADIX_TILE consecutive messages.  Upsweep: per-tile digit counts,
+// stored digit-major (hist[d * tiles + t]) so that one exclusive scan gives
+// every (digit, tile) its global base.
+template <int BITS>
+__global__ void __launch_bounds__(BLOCK) k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n,
+                                                      uint32_t clamp, uint32_t shift, uint32_t tiles,
+                                                      uint32_t* __restrict__ hist) {
+    constexpr uint32_t R = 1u << BITS;
+    __shared__ uint32_t s_cnt[R];
+    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) s_cnt[d] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * RADIX_TILE;
+    const uint32_t lane = lane_id();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll 4
+    for (int j = 0; j < RADIX_ITEMS; ++j) {
+        const uint32_t idx = base + j * BLOCK + threadIdx.x;
+        const bool valid = idx < n;
+        const uint32_t k = valid ? min(keys[idx], clamp) : 0u;
+        const uint32_t d = (k >> shift) & (R - 1);
+        const unsigned long long peers = match_digit<BITS>(d, valid);
+        if (valid && (peers & lt) == 0) atomicAdd(&s_cnt[d], (uint32_t)__popcll(peers));
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) hist[d * tiles + blockIdx.x] = s_cnt[d];
+}
+
+// Downsweep: stable rank inside the tile (wave-striped order = index order),
+// stage the tile in LDS in digit order, write each digit run contiguously.
+// FIRST: values are the message indices themselves.  The keys are clamped to
+// `clamp` (unrouted messages -> trailing bucket).
+template <int BITS, bool FIRST>
+__global__ void __launch_bounds__(BLOCK) k_radix_scatter(const uint32_t* __restrict__ keys_in,
+                                                         const uint32_t* __restrict__ vals_in, uint32_t n,
+                                                         uint32_t clamp, uint32_t shift, uint32_t tiles,
+                                                         const uint32_t* __restrict__ gscan,
+                                                         uint32_t* __restrict__ keys_out,
+                                                         uint32_t* __restrict__ vals_out) {
+    constexpr uint32_t R = 1u << BITS;
+    constexpr int NW = BLOCK / WAVE;
+    __shared__ uint32_t s_wcnt[NW][R];
+    __shared__ uint32_t s_lstart[R];
+    __shared__ uint32_t s_gbase[R];
+    __shared__ uint32_t s_key[RADIX_TILE];
+    __shared__ uint32_t s_val[RADIX_TILE];
+    __shared__ uint32_t s_wsum[NW];
+
+    const uint32_t tile = blockIdx.x;
+    const uint32_t base = tile * RADIX_TILE;
+    const uint32_t cnt_tile = min((uint32_t)RADIX_TILE, n - base);
+    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) s_wcnt[w][d] = 0;
+        s_gbase[d] = gscan[d * tiles + tile];
+    }
+    __syncthreads();
+
+    const uint32_t lane = lane_id();
+    const uint32_t w = threadIdx.x / WAVE;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    uint32_t rk[RADIX_ITEMS], kk[RADIX_ITEMS], vv[RADIX_ITEMS];
+#pragma unroll
+    for (int r = 0; r < RADIX_ITEMS; ++r) {
+        const uint32_t idx = base + (w * RADIX_ITEMS + r) * WAVE + lane;
+        const bool valid = idx < n;
+        const uint32_t k = valid ? min(keys_in[idx], clamp) : 0u;
+        const uint32_t v = FIRST ? idx : (valid ? vals_in[idx] : 0u);
+        const uint32_t d = (k >> shift) & (R - 1);
+        const unsigned long long peers = match_digit<BITS>(d, valid);
+        uint32_t c = 0;
+        if (valid) c = s_wcnt[w][d];
+        rk[r] = c + (uint32_t)__popcll(peers & lt);
+        if (valid && (peers & lt) == 0) s_wcnt[w][d] = c + (uint32_t)__popcll(peers);
+        kk[r] = k;
+        vv[r] = v;
+    }
+    __syncthreads();
+    // cross-wave exclusive prefix per digit, then tile-local digit starts
+    uint32_t my_total = 0;
+    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) {
+            const uint32_t t = s_wcnt[ww][d];
+            s_wcnt[ww][d] = run;
+            run += t;
+        }
+        my_total = run;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_add(threadIdx.x < R ? my_total : 0u, s_wsum, tot);
+    if (threadIdx.x < R) s_lstart[threadIdx.x] = ex;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RADIX_ITEMS; ++r) {
+        const uint32_t idx = base + (w * RADIX_ITEMS + r) * WAVE + lane;
+        if (idx < n) {
+            const uint32_t d = (kk[r] >> shift) & (R - 1);
+            const uint32_t lpos = s_lstart[d] + s_wcnt[w][d] + rk[r];
+            s_key[lpos] = kk[r];
+            s_val[lpos] = vv[r];
+        }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < RADIX_ITEMS; ++j) {
+        const uint32_t p = j * BLOCK + threadIdx.x;
+        if (p < cnt_tile) {
+            const uint32_t k = s_key[p];
+            const uint32_t d = (k >> shift) & (R - 1);
+            const uint32_t g = s_gbase[d] + (p - s_lstart[d]);
+            if (g < n) {            // always true when the scan is right; never write out of bounds
+                keys_out[g] = k;
+                vals_out[g] = s_val[p];
+            }
+        }
+    }
+}
+
+// offsets[k] = first position of key k in the sorted keys (others stay at the fill
+// value and are fixed by a reverse min-scan).
+__global__ void __launch_bounds__(BLOCK) k_bucket_starts(const uint32_t* __restrict__ skeys, uint32_t n,
+                                                         uint32_t* __restrict__ offsets) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = skeys[i];
+    if (i == 0 || skeys[i - 1] != k) offsets[k] = i;
+}
+
+__global__ void k_fill_u32(uint32_t* __restrict__ p, uint32_t n, uint32_t v) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+// ------------------------------------------------------------------ device-wide scan
+struct OpAdd {
+    static constexpr uint32_t identity = 0u;
+    __device__ static uint32_t apply(uint32_t a, uint32_t b) { return a + b; }
+};
+struct OpMin {
+    static constexpr uint32_t identity = 0xFFFFFFFFu;
+    __device__ static uint32_t apply(uint32_t a, uint32_t b) { return min(a, b); }
+};
+
+template <class Op>
+__device__ __forceinline__ uint32_t block_reduce(uint32_t v, uint32_t* s_wsum) {
+#pragma unroll
+    for (int off = WAVE / 2; off > 0; off >>= 1) v = Op::apply(v, __shfl_xor(v, off, WAVE));
+    if ((threadIdx.x & (WAVE - 1)) == 0) s_wsum[threadIdx.x / WAVE] = v;
+    __syncthreads();
+    uint32_t r = Op::identity;
+#pragma unroll
+    for (int k = 0; k < BLOCK / WAVE; ++k) r = Op::apply(r, s_wsum[k]);
+    __syncthreads();
+    return r;
+}
+
+template <class Op>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wsum) {
+    const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, WAVE);
+        if (lane >= (uint32_t)off) x = Op::apply(y, x);
+    }
+    uint32_t ex = __shfl_up(x, 1, WAVE);
+    if (lane == 0) ex = Op::identity;
+    if (lane == WAVE - 1) s_wsum[w] = x;
+    __syncthreads();
+    uint32_t wbase = Op::identity;
+#pragma unroll
+    for (int k = 0; k < BLOCK / WAVE; ++k)
+        if ((uint32_t)k < w) wbase = Op::apply(wbase, s_wsum[k]);
+    __syncthreads();
+    return Op::apply(wbase, ex);
+}
+
+// logical index j -> physical (reverse scans run from the end)
+__device__ __forceinline__ uint32_t phys(uint32_t j, uint32_t n, bool rev) { return rev ? n - 1 - j : j; }
+
+template <class Op>
+__global__ void __launch_bounds__(BLOCK) k_scan_reduce(const uint32_t* __restrict__ in, uint32_t n, bool rev,
+                                                       uint32_t* __restrict__ partials) {
+    __shared__ uint32_t s_wsum[BLOCK / WAVE];
+    const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+    uint32_t acc = Op::identity;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint32_t j = base + k;
+        if (j < n) acc = Op::apply(acc, in[phys(j, n, rev)]);
+    }
+    acc = block_reduce<Op>(acc, s_wsum);
+    if (threadIdx.x == 0) partials[blockIdx.x] = acc;
+}
+
+// Exclusive scan of `m` partials in one block (sequential over chunks).
+template <class Op>
+__global__ void __launch_bounds__(BLOCK) k_scan_partials(uint32_t* partials, uint32_t m) {
+    __shared__ uint32_t s_wsum[BLOCK / WAVE];
+    __shared__ uint32_t s_carry;
+    if (threadIdx.x == 0) s_carry = Op::identity;
+    __syncthreads();
+    for (uint32_t c = 0; c < m; c += BLOCK) {
+        const uint32_t j = c + threadIdx.x;
+        const uint32_t v = j < m ? partials[j] : Op::identity;
+        const uint32_t ex = block_excl_scan<Op>(v, s_wsum);
+        const uint32_t carry = s_carry;
+        __syncthreads();
+        if (j < m) partials[j] = Op::apply(carry, ex);
+        if (threadIdx.x == BLOCK - 1) s_carry = Op::apply(carry, Op::apply(ex, v));
+        __syncthreads();
+    }
+}
+
+template <class Op>
+__global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_t* out, uint32_t n, bool rev,
+                                                     bool inclusive, const uint32_t* __restrict__ partials) {
+    __shared__ uint32_t s_wsum[BLOCK / WAVE];
+    const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    uint32_t acc = Op::identity;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint32_t j = base + k;
+        v[k] = j < n ? in[phys(j, n, rev)] : Op::identity;
+        acc = Op::apply(acc, v[k]);
+    }
+    uint32_t run = Op::apply(partials[blockIdx.x], block_excl_scan<Op>(acc, s_wsum));
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        const uint32_t j = base + k;
+        const uint32_t next = Op::apply(run, v[k]);
+        if (j < n) out[phys(j, n, rev)] = inclusive ? next : run;
+        run = next;
+    }
+}
+
+}  // namespace gd

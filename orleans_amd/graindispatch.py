@@ -1,0 +1,353 @@
+"""ctypes binding of libgraindispatch.so (include/graindispatch.h).
+
+This is the Python face of the C ABI that the Orleans C# host binds with
+[DllImport("graindispatch")].  It holds no routing logic:
+every call goes straight through the C ABI to the gfx950 kernels.  There is
+no CPU fallback -- if the shared library is missing, import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GRAINDISPATCH_LIB", os.path.join(_HERE, "libgraindispatch.so"))
+
+# ---- constants mirrored from include/graindispatch.h --------------------------
+GD_OK, GD_EINVAL, GD_ENOMEM, GD_EHIP, GD_ERCCL, GD_EFULL, GD_ESTATE, GD_ETIMEOUT = 0, -1, -2, -3, -4, -5, -6, -7
+RING_DIRECTORY, RING_CONSISTENT, RING_VIRTUAL_BUCKETS = 0, 1, 2
+ROUTE_OK, ROUTE_MISS, ROUTE_SYSTEM_TARGET, ROUTE_MEMBERSHIP, ROUTE_KEYEXT = 0, 1, 2, 3, 4
+NO_ACTIVATION = 0xFFFFFFFF
+NO_SILO = 0xFFFFFFFF
+CFG_KERNEL_TIMING = 1
+
+RING_MODES = {"D": RING_DIRECTORY, "R": RING_CONSISTENT, "V": RING_VIRTUAL_BUCKETS}
+
+# C-ABI symbols the header declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = [
+    "gd_create", "gd_destroy", "gd_last_error", "gd_abi_version", "gd_set_stream", "gd_get_stream",
+    "gd_synchronize", "gd_stats_get", "gd_jenkins_hash_bytes", "gd_jenkins_hash_u64x3", "gd_uniform_hash",
+    "gd_calculate_id_hash", "gd_silo_consistent_hash", "gd_silo_uniform_hashes", "gd_silo_compare",
+    "gd_ring_build", "gd_ring_set", "gd_ring_owner", "gd_ring_lookup_hashes", "gd_dir_register",
+    "gd_dir_unregister", "gd_dir_lookup", "gd_dir_clear", "gd_dir_rehash", "gd_route", "gd_bucket",
+    "gd_route_bucket", "gd_route_device", "gd_bucket_device", "gd_route_bucket_device",
+    "gd_ring_owner_device", "gd_pack_by_shard_device", "gd_kernel_times", "gd_kernel_times_reset",
+]
+
+
+class gd_key(C.Structure):
+    _fields_ = [("n0", C.c_uint64), ("n1", C.c_uint64), ("type_code_data", C.c_uint64)]
+
+
+class gd_val(C.Structure):
+    _fields_ = [("act", C.c_uint32), ("silo", C.c_uint32)]
+
+
+class gd_silo_addr(C.Structure):
+    _fields_ = [("ip", C.c_uint8 * 16), ("port", C.c_int32), ("generation", C.c_int32), ("is_v4", C.c_int32)]
+
+
+class gd_config(C.Structure):
+    _fields_ = [("struct_size", C.c_uint32), ("device", C.c_int32), ("table_capacity", C.c_uint64),
+                ("my_silo", C.c_uint32), ("seed_silo", C.c_uint32), ("max_batch", C.c_uint32),
+                ("flags", C.c_uint32)]
+
+
+class gd_stats(C.Structure):
+    _fields_ = [("routed", C.c_uint64), ("table_live", C.c_uint64), ("table_tombstones", C.c_uint64),
+                ("table_capacity", C.c_uint64), ("ring_points", C.c_uint64), ("ring_mode", C.c_uint64)]
+
+
+class gd_kernel_time(C.Structure):
+    _fields_ = [("name", C.c_char * 48), ("launches", C.c_uint64), ("total_ms", C.c_double)]
+
+
+class GrainDispatchError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"graindispatch error {code}: {msg}")
+        self.code = code
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libgraindispatch.so not built at {LIB_PATH}; run __graft_entry__.build()")
+    lib = C.CDLL(LIB_PATH)
+    P, U32, U64, I32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
+    sig = {
+        "gd_create": (C.c_int, [C.POINTER(gd_config), C.POINTER(P)]),
+        "gd_destroy": (None, [P]),
+        "gd_last_error": (C.c_char_p, [P]),
+        "gd_abi_version": (C.c_int, []),
+        "gd_set_stream": (C.c_int, [P, P]),
+        "gd_get_stream": (P, [P]),
+        "gd_synchronize": (C.c_int, [P]),
+        "gd_stats_get": (C.c_int, [P, C.POINTER(gd_stats)]),
+        "gd_jenkins_hash_bytes": (U32, [P, C.c_size_t]),
+        "gd_jenkins_hash_u64x3": (U32, [U64, U64, U64]),
+        "gd_uniform_hash": (U32, [C.POINTER(gd_key)]),
+        "gd_calculate_id_hash": (I32, [C.c_char_p]),
+        "gd_silo_consistent_hash": (I32, [C.POINTER(gd_silo_addr)]),
+        "gd_silo_uniform_hashes": (C.c_int, [C.POINTER(gd_silo_addr), U32, P]),
+        "gd_silo_compare": (C.c_int, [C.POINTER(gd_silo_addr), C.POINTER(gd_silo_addr)]),
+        "gd_ring_build": (C.c_int, [C.c_int, P, U32, U32, P, P, C.POINTER(U32)]),
+        "gd_ring_set": (C.c_int, [P, C.c_int, P, P, U32]),
+        "gd_ring_owner": (C.c_int, [P, P, U32, P]),
+        "gd_ring_lookup_hashes": (C.c_int, [P, P, U32, P]),
+        "gd_dir_register": (C.c_int, [P, P, P, U32, P, P]),
+        "gd_dir_unregister": (C.c_int, [P, P, P, U32, P]),
+        "gd_dir_lookup": (C.c_int, [P, P, U32, P, P]),
+        "gd_dir_clear": (C.c_int, [P]),
+        "gd_dir_rehash": (C.c_int, [P, U64]),
+        "gd_route": (C.c_int, [P, P, U32, P, P, P]),
+        "gd_bucket": (C.c_int, [P, P, U32, U32, P, P]),
+        "gd_route_bucket": (C.c_int, [P, P, U32, U32, P, P, P, P, P]),
+        "gd_route_device": (C.c_int, [P, P, U32, P, P, P]),
+        "gd_bucket_device": (C.c_int, [P, P, U32, U32, P, P]),
+        "gd_route_bucket_device": (C.c_int, [P, P, U32, U32, P, P, P, P, P]),
+        "gd_ring_owner_device": (C.c_int, [P, P, U32, P]),
+        "gd_pack_by_shard_device": (C.c_int, [P, P, U32, U32, P, P, P]),
+        "gd_kernel_times": (C.c_int, [P, C.POINTER(gd_kernel_time), U32, C.POINTER(U32)]),
+        "gd_kernel_times_reset": (C.c_int, [P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def keys_array(keys) -> np.ndarray:
+    """(N,3) uint64 [n0, n1, type_code_data] in C order (the gd_key AoS layout)."""
+    k = np.ascontiguousarray(np.asarray(keys, dtype=np.uint64).reshape(-1, 3))
+    return k
+
+
+# ---- identity helpers ------------------------------------------------------------
+
+def silo_addr(ip: str, port: int, gen: int) -> gd_silo_addr:
+    import ipaddress
+    a = ipaddress.ip_address(ip)
+    s = gd_silo_addr()
+    raw = (b"\x00" * 12 + a.packed) if a.version == 4 else a.packed
+    for i, b in enumerate(raw):
+        s.ip[i] = b
+    s.port, s.generation, s.is_v4 = port, gen, 1 if a.version == 4 else 0
+    return s
+
+
+def jenkins_bytes(data: bytes) -> int:
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    return lib.gd_jenkins_hash_bytes(buf, len(data))
+
+
+def jenkins_u64x3(u1: int, u2: int, u3: int) -> int:
+    return lib.gd_jenkins_hash_u64x3(u1, u2, u3)
+
+
+def calculate_id_hash(text: str) -> int:
+    return lib.gd_calculate_id_hash(text.encode("utf-8"))
+
+
+def silo_consistent_hash(ip: str, port: int, gen: int) -> int:
+    return lib.gd_silo_consistent_hash(C.byref(silo_addr(ip, port, gen)))
+
+
+def silo_uniform_hashes(ip: str, port: int, gen: int, n: int) -> List[int]:
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    _check(None, lib.gd_silo_uniform_hashes(C.byref(silo_addr(ip, port, gen)), n, _ptr(out)))
+    return [int(x) for x in out[:n]]
+
+
+def ring_build(mode: str, silos: Sequence[Tuple[str, int, int]], buckets: int = 30) -> Tuple[np.ndarray, np.ndarray]:
+    """LocalGrainDirectory / ConsistentRingProvider / VirtualBucketsRingProvider
+    AddServer over `silos` (added in order).  Returns (points u32, owner u32)."""
+    m = RING_MODES[mode] if isinstance(mode, str) else mode
+    arr = (gd_silo_addr * len(silos))(*[silo_addr(*s) for s in silos])
+    cap = len(silos) * (buckets if m == RING_VIRTUAL_BUCKETS else 1)
+    pts = np.zeros(cap, dtype=np.uint32)
+    own = np.zeros(cap, dtype=np.uint32)
+    n = C.c_uint32(0)
+    _check(None, lib.gd_ring_build(m, arr, len(silos), buckets, _ptr(pts), _ptr(own), C.byref(n)))
+    return pts[: n.value].copy(), own[: n.value].copy()
+
+
+def _check(h, rc: int):
+    if rc != GD_OK:
+        msg = lib.gd_last_error(h)
+        raise GrainDispatchError(rc, msg.decode() if msg else "")
+
+
+# ---- the handle --------------------------------------------------------------------
+
+class GrainDispatch:
+    """One libgraindispatch handle: a ring snapshot + the directory partitions this
+    GPU owns + scratch, on one HIP stream."""
+
+    def __init__(self, device: int = 0, table_capacity: int = 1 << 20, my_silo: int = 0,
+                 seed_silo: int = NO_SILO, kernel_timing: bool = False):
+        cfg = gd_config(C.sizeof(gd_config), device, table_capacity, my_silo, seed_silo, 0,
+                        CFG_KERNEL_TIMING if kernel_timing else 0)
+        h = C.c_void_p()
+        _check(None, lib.gd_create(C.byref(cfg), C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.gd_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _c(self, rc):
+        _check(self.h, rc)
+
+    # -- stream ---------------------------------------------------------------
+    def set_stream(self, hip_stream: Optional[int]):
+        self._c(lib.gd_set_stream(self.h, C.c_void_p(hip_stream or 0)))
+
+    def synchronize(self):
+        self._c(lib.gd_synchronize(self.h))
+
+    def stats(self) -> dict:
+        s = gd_stats()
+        self._c(lib.gd_stats_get(self.h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in gd_stats._fields_}
+
+    # -- ring -----------------------------------------------------------------
+    def ring_set(self, mode, points, owner):
+        m = RING_MODES[mode] if isinstance(mode, str) else mode
+        p = np.ascontiguousarray(np.asarray(points, dtype=np.int64).astype(np.uint32) if np.asarray(points).dtype.kind == "i"
+                                 else np.asarray(points, dtype=np.uint32))
+        o = np.ascontiguousarray(np.asarray(owner, dtype=np.uint32))
+        self._c(lib.gd_ring_set(self.h, m, _ptr(p), _ptr(o), len(p)))
+
+    def ring_set_silos(self, mode: str, silos, buckets: int = 30):
+        pts, own = ring_build(mode, silos, buckets)
+        self.ring_set(mode, pts, own)
+        return pts, own
+
+    def ring_owner(self, keys) -> np.ndarray:
+        k = keys_array(keys)
+        out = np.zeros(len(k), dtype=np.uint32)
+        self._c(lib.gd_ring_owner(self.h, _ptr(k), len(k), _ptr(out)))
+        return out
+
+    def ring_lookup_hashes(self, hashes) -> np.ndarray:
+        hs = np.ascontiguousarray(np.asarray(hashes, dtype=np.uint32))
+        out = np.zeros(len(hs), dtype=np.uint32)
+        self._c(lib.gd_ring_lookup_hashes(self.h, _ptr(hs), len(hs), _ptr(out)))
+        return out
+
+    # -- directory ------------------------------------------------------------
+    def register(self, keys, acts, silos):
+        k = keys_array(keys)
+        n = len(k)
+        vals = np.zeros((n, 2), dtype=np.uint32)
+        vals[:, 0] = acts
+        vals[:, 1] = silos
+        out = np.zeros((n, 2), dtype=np.uint32)
+        ins = np.zeros(n, dtype=np.uint8)
+        self._c(lib.gd_dir_register(self.h, _ptr(k), _ptr(vals), n, _ptr(out), _ptr(ins)))
+        return out[:, 0].copy(), out[:, 1].copy(), ins
+
+    def unregister(self, keys, acts) -> np.ndarray:
+        k = keys_array(keys)
+        a = np.ascontiguousarray(np.asarray(acts, dtype=np.uint32))
+        out = np.zeros(len(k), dtype=np.uint8)
+        self._c(lib.gd_dir_unregister(self.h, _ptr(k), _ptr(a), len(k), _ptr(out)))
+        return out
+
+    def lookup(self, keys):
+        k = keys_array(keys)
+        n = len(k)
+        out = np.zeros((n, 2), dtype=np.uint32)
+        found = np.zeros(n, dtype=np.uint8)
+        self._c(lib.gd_dir_lookup(self.h, _ptr(k), n, _ptr(out), _ptr(found)))
+        return out[:, 0].copy(), out[:, 1].copy(), found
+
+    def clear(self):
+        self._c(lib.gd_dir_clear(self.h))
+
+    def rehash(self, capacity: int):
+        self._c(lib.gd_dir_rehash(self.h, capacity))
+
+    # -- hot path (host arrays) --------------------------------------------------
+    def route(self, keys):
+        k = keys_array(keys)
+        n = len(k)
+        silo = np.zeros(n, dtype=np.uint32)
+        act = np.zeros(n, dtype=np.uint32)
+        st = np.zeros(n, dtype=np.uint8)
+        self._c(lib.gd_route(self.h, _ptr(k), n, _ptr(silo), _ptr(act), _ptr(st)))
+        return st, silo, act
+
+    def bucket(self, acts, n_act: int):
+        a = np.ascontiguousarray(np.asarray(acts, dtype=np.uint32))
+        perm = np.zeros(len(a), dtype=np.uint32)
+        off = np.zeros(n_act + 2, dtype=np.uint32)
+        self._c(lib.gd_bucket(self.h, _ptr(a), len(a), n_act, _ptr(perm), _ptr(off)))
+        return perm, off
+
+    def route_bucket(self, keys, n_act: int):
+        k = keys_array(keys)
+        n = len(k)
+        silo = np.zeros(n, dtype=np.uint32)
+        act = np.zeros(n, dtype=np.uint32)
+        st = np.zeros(n, dtype=np.uint8)
+        perm = np.zeros(n, dtype=np.uint32)
+        off = np.zeros(n_act + 2, dtype=np.uint32)
+        self._c(lib.gd_route_bucket(self.h, _ptr(k), n, n_act, _ptr(silo), _ptr(act), _ptr(st), _ptr(perm), _ptr(off)))
+        return st, silo, act, perm, off
+
+    # -- hot path (device pointers; enqueue only) -----------------------------------
+    def route_device(self, d_keys: int, n: int, d_silo: int, d_act: int, d_status: int):
+        self._c(lib.gd_route_device(self.h, C.c_void_p(d_keys), n, C.c_void_p(d_silo), C.c_void_p(d_act),
+                                    C.c_void_p(d_status)))
+
+    def bucket_device(self, d_acts: int, n: int, n_act: int, d_perm: int, d_offsets: int):
+        self._c(lib.gd_bucket_device(self.h, C.c_void_p(d_acts), n, n_act, C.c_void_p(d_perm), C.c_void_p(d_offsets)))
+
+    def route_bucket_device(self, d_keys: int, n: int, n_act: int, d_silo: int, d_act: int, d_status: int,
+                            d_perm: int, d_offsets: int):
+        self._c(lib.gd_route_bucket_device(self.h, C.c_void_p(d_keys), n, n_act, C.c_void_p(d_silo),
+                                           C.c_void_p(d_act), C.c_void_p(d_status), C.c_void_p(d_perm),
+                                           C.c_void_p(d_offsets)))
+
+    def ring_owner_device(self, d_keys: int, n: int, d_silo: int):
+        self._c(lib.gd_ring_owner_device(self.h, C.c_void_p(d_keys), n, C.c_void_p(d_silo)))
+
+    def pack_by_shard_device(self, d_keys: int, n: int, n_shards: int, d_send_keys: int, d_send_idx: int,
+                             d_counts: int):
+        self._c(lib.gd_pack_by_shard_device(self.h, C.c_void_p(d_keys), n, n_shards, C.c_void_p(d_send_keys),
+                                            C.c_void_p(d_send_idx), C.c_void_p(d_counts)))
+
+    # -- per-kernel timing ----------------------------------------------------------
+    def kernel_times(self) -> dict:
+        arr = (gd_kernel_time * 64)()
+        n = C.c_uint32(0)
+        self._c(lib.gd_kernel_times(self.h, arr, 64, C.byref(n)))
+        return {arr[i].name.decode(): (int(arr[i].launches), float(arr[i].total_ms)) for i in range(min(n.value, 64))}
+
+    def kernel_times_reset(self):
+        self._c(lib.gd_kernel_times_reset(self.h))
