@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""Routed messages/sec for the Orleans grain-dispatch hot path on MI355X.
+
+One step = one batch of message headers through ring lookup + directory probe
++ per-activation bucketing (libgraindispatch, gfx950), inputs resident in HBM.
+
+  N = 1  BASELINE.json config 2: 16,777,216 messages, uniform over 1,048,576
+         grains (GrainId = Ping grain type code + long key), 8 silos
+         10.0.0.{1..8}:11111@1, directory ring mode D (LocalGrainDirectory),
+         table load 0.5, every grain registered with one activation on its owner.
+  N > 1  weak scaling: the same 16M messages per GPU over 2^20 x N grains;
+         silo s lives on GPU s % N; each GPU owns its silos' directory
+         partition; a stable partition by owner + all-to-all-v (RCCL over xGMI)
+         moves headers to their owner, which probes and buckets them.
+
+Prints ONE JSON line on rank 0 (see DESIGN.md for the byte model behind the
+roofline object).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from orleans_amd import graindispatch as g          # noqa: E402
+from orleans_amd.sharded import DeviceEngine, ShardedRouter  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SILOS = [(f"10.0.0.{i + 1}", 11111, 1) for i in range(8)]
+PING_GRAIN_CLASS = "BenchmarkGrains.Ping.PingGrain"
+
+
+def grain_keys(type_code_data: int, ks: np.ndarray) -> np.ndarray:
+    out = np.zeros((ks.shape[0], 3), dtype=np.uint64)
+    out[:, 1] = ks.astype(np.int64).view(np.uint64)
+    out[:, 2] = np.uint64(type_code_data)
+    return out
+
+
+def kernel_bytes(name: str, n: int, n_act: int, passes: int, world: int) -> float:
+    """Algorithmic HBM bytes of one step for a kernel (all launches of it), per
+    DESIGN.md 'Byte model'."""
+    if name == "k_route":
+        return n * (24 + 32 + 4 + 4 + 1)          # key, one slot, silo+act+status
+    if name == "k_radix_scatter":
+        return n * (12 + 16 * (passes - 1))       # pass 1 reads act only; later passes move (key, idx)
+    if name == "k_radix_hist":
+        return n * 4 * passes
+    if name == "k_bucket_starts":
+        return n * 4 + (n_act + 2) * 4
+    return 0.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--msgs", type=int, default=1 << 24, help="messages per GPU per step")
+    ap.add_argument("--grains", type=int, default=1 << 20, help="grains per GPU")
+    ap.add_argument("--mode", default="D", choices=["D", "R", "V"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=5, help="extra steps with per-kernel events")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == args.gpus or "WORLD_SIZE" not in os.environ, "--gpus must match WORLD_SIZE"
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29571")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+
+    N, Gr = args.msgs, args.grains
+    G_total = Gr * world
+    tc = g.calculate_id_hash(PING_GRAIN_CLASS)
+    tcd = (3 << 56) + ((tc & 0xFFFFFFFFFFFFFFFF) & 0x00FFFFFFFFFFFFFF)
+
+    # ---- directory: this rank owns the grains whose owner silo lives here -----
+    all_keys = grain_keys(tcd, np.arange(G_total, dtype=np.int64))
+    e = g.GrainDispatch(device=local, table_capacity=2 * Gr, my_silo=rank % 8, kernel_timing=False)
+    pts, own = e.ring_set_silos(args.mode, SILOS)
+    owner = e.ring_owner(all_keys)
+    mine = np.nonzero(owner % world == rank)[0]
+    n_act = len(mine)
+    e.register(all_keys[mine], np.arange(n_act, dtype=np.uint32), owner[mine])
+    del all_keys
+
+    # ---- synthetic message batch, resident in HBM ----------------------------------
+    rng = np.random.default_rng(0x5EED0001 + rank)
+    ks = rng.integers(0, G_total, size=N, dtype=np.int64)
+    keys = torch.from_numpy(grain_keys(tcd, ks).view(np.int64)).to(dev)
+    del ks
+    torch.cuda.synchronize()
+
+    engine = DeviceEngine(e, dev)
+    router = ShardedRouter(engine)
+    stream = engine.stream
+
+    def step():
+        return router.route_bucket(keys, n_act)
+
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        routed_local = 0
+        for _ in range(args.steps):
+            res = step()
+            routed_local += N
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+    gpu_ms = ev0.elapsed_time(ev1)
+    total_msgs = routed_local * world
+    value = total_msgs / wall_max
+
+    # received (owner-side) message count, for the byte model
+    m_recv = int(res.recv_keys.shape[0])
+    st_ok = int((res.status == 0).sum().item())
+
+    # ---- per-kernel durations (separate steps, HIP events around every launch) -----
+    kt = {}
+    if args.profile_steps > 0:
+        e.set_kernel_timing(True)
+        e.kernel_times_reset()
+        with torch.cuda.stream(stream):
+            for _ in range(args.profile_steps):
+                router.route_bucket(keys, n_act)
+        torch.cuda.synchronize()
+        kt = e.kernel_times()
+        e.set_kernel_timing(False)
+
+    key_bits = max(1, int(n_act).bit_length())
+    passes = (key_bits + 7) // 8
+    kernels = {}
+    for name, (launches, ms) in kt.items():
+        if launches == 0:
+            continue
+        per_step_ms = ms / args.profile_steps
+        b = kernel_bytes(name, m_recv, n_act, passes, world)
+        gbs = b / (per_step_ms * 1e-3) / 1e9 if b and per_step_ms > 0 else None
+        kernels[name] = {"launches_per_step": launches // args.profile_steps, "ms_per_step": round(per_step_ms, 4),
+                         "alg_GBps": round(gbs, 1) if gbs else None,
+                         "frac_hbm": round(gbs / PEAK_HBM_GBS, 4) if gbs else None}
+    roofline = None
+    if kernels:
+        dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
+        d = kernels[dom]
+        launches = max(1, d["launches_per_step"])
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{dom}.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        roofline = {"bound": "hbm", "kernel": dom,
+                    "achieved": d["alg_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": d["frac_hbm"], "traffic": traffic,
+                    "alg_bytes_per_launch": kernel_bytes(dom, m_recv, n_act, passes, world) / launches,
+                    "avg_launch_ms": round(d["ms_per_step"] / launches, 5)}
+
+    # ---- CPU baseline: the C restatement (oracle/cpu_ref.c), bounded sample ---------
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, tcd, G_total, pts, own, owner)
+
+    if rank == 0:
+        line = {
+            "metric": "routed messages/sec (lookup+bucket, whole node)",
+            "value": round(value, 1),
+            "unit": "messages/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32/u64 integer",
+            "data": "synthetic GrainIds (no dataset); uniform keys, seed 0x5EED0001+rank",
+            "config": {"workload": "cfg2: 16M msgs uniform over 1M grains, 8 silos, ring D" if world == 1 else
+                       f"cfg2 per GPU (16M msgs/GPU over {G_total} grains), directory sharded by ring owner, "
+                       f"RCCL all-to-all-v",
+                       "msgs_per_gpu": N, "grains_total": G_total, "ring_mode": args.mode, "silos": 8,
+                       "table_load": round(n_act / (2 * Gr), 3), "parallelism": f"shard{world}"},
+            "routed_ok_last_step_rank0": st_ok,
+            "roofline": roofline,
+            "kernels": kernels,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    e.close()
+    dist.destroy_process_group()
+
+
+def cpu_baseline(args, tcd, G_total, pts, own, owner):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_ref  # test-infrastructure checker, timed here as the CPU baseline only
+
+    nthreads = min(16, os.cpu_count() or 1)
+    sample = 1 << 22
+    rng = np.random.default_rng(0x5EED0001)
+    keys = grain_keys(tcd, rng.integers(0, G_total, size=sample, dtype=np.int64))
+    all_keys = grain_keys(tcd, np.arange(G_total, dtype=np.int64))
+    res = {}
+    for label, faithful, thr in (("faithful", True, 1), ("fast", False, nthreads)):
+        d = cpu_ref.CpuDirectory(faithful, G_total)
+        d.register(all_keys, np.arange(G_total, dtype=np.uint32), owner)
+        done, t0 = 0, time.perf_counter()
+        budget = args.cpu_seconds / 2
+        while True:
+            st, silo, act = d.route(args.mode, pts, own, keys, nthreads=thr)
+            perm, off = cpu_ref.bucket(act, G_total, faithful=faithful, nthreads=thr)
+            done += sample
+            if time.perf_counter() - t0 >= budget:
+                break
+        res[label] = (done / (time.perf_counter() - t0), thr, done)
+        del d
+    v, thr, done = res["faithful"]
+    return {"value": round(v, 1), "unit": "messages/s", "cores": thr, "kind": "port",
+            "sample": f"{done} messages (cfg2 distribution, {sample}-message batches repeated) through the C "
+                      f"restatement in faithful mode (linear ring scan under a mutex, chained Dictionary-style "
+                      f"map, per-activation FIFO append), 1 thread",
+            "fast_value": round(res["fast"][0], 1), "fast_cores": res["fast"][1],
+            "host_cpus": os.cpu_count()}
+
+
+if __name__ == "__main__":
+    main()

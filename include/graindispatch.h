@@ -222,6 +222,7 @@ typedef struct gd_kernel_time {
 } gd_kernel_time;
 int gd_kernel_times(gd_handle* h, gd_kernel_time* out, uint32_t max, uint32_t* out_n);
 int gd_kernel_times_reset(gd_handle* h);
+int gd_set_kernel_timing(gd_handle* h, int enable);
 
 #ifdef __cplusplus
 }

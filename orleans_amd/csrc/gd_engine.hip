@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -53,6 +54,11 @@ struct gd_handle {
     // scratch
     DevBuf keys_in, u32_a, u32_b, u32_c, u32_d, u8_a, out_a, out_b, out_c, hist, partials, offs;
     uint64_t routed = 0;
+
+    // kernel tuning (defaults measured on MI355X; GD_ROUTE_M / GD_ROUTE_NT override for A/B runs)
+    int route_m = 1;
+    bool route_nt = false;
+    int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
 
     // per-kernel timing
     bool timing = false;
@@ -206,20 +212,32 @@ unsigned long long pow2_at_least(unsigned long long x) {
 }
 
 // ---- route -------------------------------------------------------------------
+template <int MODE, int M, bool NT>
+int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
+    return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h), k_route_m<MODE, M, NT>, keys,
+                  n, ring_args(h), table_args(h), silo, act, status);
+}
+
+template <int MODE>
+int route_mode(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
+    const bool nt = h->route_nt;
+    switch (h->route_m) {
+        case 1: return nt ? route_launch<MODE, 1, true>(h, keys, n, silo, act, status)
+                          : route_launch<MODE, 1, false>(h, keys, n, silo, act, status);
+        case 4: return nt ? route_launch<MODE, 4, true>(h, keys, n, silo, act, status)
+                          : route_launch<MODE, 4, false>(h, keys, n, silo, act, status);
+        default: return nt ? route_launch<MODE, 2, true>(h, keys, n, silo, act, status)
+                           : route_launch<MODE, 2, false>(h, keys, n, silo, act, status);
+    }
+}
+
 int route_device(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
     GD_TRY(check_ring(h));
-    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
-    const RingArgs r = ring_args(h);
-    const TableArgs t = table_args(h);
-    const size_t lds = ring_lds(h);
     h->routed += n;
     switch (h->ring_mode) {
-        case GD_RING_DIRECTORY:
-            return launch(h, "k_route", g, b, lds, k_route<GD_RING_DIRECTORY, true>, keys, n, r, t, silo, act, status);
-        case GD_RING_CONSISTENT:
-            return launch(h, "k_route", g, b, lds, k_route<GD_RING_CONSISTENT, true>, keys, n, r, t, silo, act, status);
-        default:
-            return launch(h, "k_route", g, b, lds, k_route<GD_RING_VIRTUAL_BUCKETS, true>, keys, n, r, t, silo, act, status);
+        case GD_RING_DIRECTORY: return route_mode<GD_RING_DIRECTORY>(h, keys, n, silo, act, status);
+        case GD_RING_CONSISTENT: return route_mode<GD_RING_CONSISTENT>(h, keys, n, silo, act, status);
+        default: return route_mode<GD_RING_VIRTUAL_BUCKETS>(h, keys, n, silo, act, status);
     }
 }
 
@@ -251,26 +269,42 @@ int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inc
     uint32_t* part = (uint32_t*)h->partials.p;
     (void)tag;
     GD_TRY(launch(h, "k_scan_reduce", dim3(nb), dim3(BLOCK), 0, k_scan_reduce<Op>, (const uint32_t*)data, n, reverse, part));
-    GD_TRY(launch(h, "k_scan_partials", dim3(1), dim3(BLOCK), 0, k_scan_partials<Op>, part, nb));
+    // few blocks: every block folds its predecessors' aggregates itself (2 launches);
+    // many: a single-block scan of the aggregates in between (3 launches)
+    const bool fold = nb <= 1024;
+    if (!fold) GD_TRY(launch(h, "k_scan_partials", dim3(1), dim3(BLOCK), 0, k_scan_partials<Op>, part, nb));
     return launch(h, "k_scan_down", dim3(nb), dim3(BLOCK), 0, k_scan_down<Op>, (const uint32_t*)data, data, n, reverse,
-                  inclusive, (const uint32_t*)part);
+                  inclusive, (const uint32_t*)part, fold ? nb : 0u);
 }
 
 // ---- K3 bucketing -------------------------------------------------------------
-template <int BITS>
-int radix_pass(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
-               uint32_t* kout, uint32_t* vout, bool first) {
-    const uint32_t tiles = blocks_for(n, RADIX_TILE);
+template <int BITS, int NT, int IT>
+int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
+                 uint32_t* kout, uint32_t* vout, bool first) {
+    constexpr uint32_t TILE = NT * IT;
+    const uint32_t tiles = blocks_for(n, TILE);
     const uint32_t R = 1u << BITS;
     GD_TRY(ensure(h, h->hist, (size_t)R * tiles * sizeof(uint32_t)));
     uint32_t* hist = (uint32_t*)h->hist.p;
-    GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(BLOCK), 0, k_radix_hist<BITS>, kin, n, clamp, shift, tiles, hist));
+    GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_radix_hist<BITS, NT, IT>, kin, n, clamp, shift, tiles,
+                  hist));
     GD_TRY(scan_device<OpAdd>(h, hist, R * tiles, false, false, "hist"));
     if (first)
-        return launch(h, "k_radix_scatter", dim3(tiles), dim3(BLOCK), 0, k_radix_scatter<BITS, true>, kin, vin, n, clamp,
-                      shift, tiles, (const uint32_t*)hist, kout, vout);
-    return launch(h, "k_radix_scatter", dim3(tiles), dim3(BLOCK), 0, k_radix_scatter<BITS, false>, kin, vin, n, clamp,
-                  shift, tiles, (const uint32_t*)hist, kout, vout);
+        return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, true, NT, IT>, kin, vin, n,
+                      clamp, shift, tiles, (const uint32_t*)hist, kout, vout);
+    return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, false, NT, IT>, kin, vin, n,
+                  clamp, shift, tiles, (const uint32_t*)hist, kout, vout);
+}
+
+template <int BITS>
+int radix_pass(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
+               uint32_t* kout, uint32_t* vout, bool first) {
+    switch (h->radix_cfg) {
+        case 1: return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        case 2: return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        case 3: return radix_pass_t<BITS, 512, 16>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        default: return radix_pass_t<BITS, 256, 16>(h, kin, vin, n, clamp, shift, kout, vout, first);
+    }
 }
 
 int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp,
@@ -332,6 +366,18 @@ int sync(gd_handle* h) {
     return GD_OK;
 }
 
+// Surface device-side error bits after a synchronising call.
+int sync_checked(gd_handle* h) {
+    GD_TRY(pull_counters(h));
+    if (h->ctr_host.err) {
+        const uint32_t e = h->ctr_host.err;
+        HIP_TRY(h, hipMemsetAsync(&h->ctr->err, 0, sizeof(uint32_t), h->stream));
+        GD_TRY(sync(h));
+        return set_err(h, GD_EFULL, "device error bits 0x%x", e);
+    }
+    return GD_OK;
+}
+
 int maybe_grow_table(gd_handle* h, uint64_t incoming) {
     GD_TRY(pull_counters(h));
     const unsigned long long used = h->ctr_host.live + h->ctr_host.tomb + incoming;
@@ -360,6 +406,9 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     h->cfg = *cfg;
     h->device = cfg->device;
     h->timing = (cfg->flags & GD_CFG_KERNEL_TIMING) != 0;
+    if (const char* v = std::getenv("GD_ROUTE_M")) h->route_m = std::atoi(v);
+    if (const char* v = std::getenv("GD_ROUTE_NT")) h->route_nt = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));
@@ -425,7 +474,7 @@ void* gd_get_stream(gd_handle* h) { return h ? (void*)h->stream : nullptr; }
 int gd_synchronize(gd_handle* h) {
     if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
     HIP_TRY(h, hipSetDevice(h->device));
-    return sync(h);
+    return sync_checked(h);
 }
 
 int gd_stats_get(gd_handle* h, gd_stats* out) {
@@ -661,7 +710,7 @@ int gd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, ui
     GD_TRY(bucket_device(h, (const uint32_t*)h->out_b.p, n, n_act, (uint32_t*)h->out_a.p, (uint32_t*)h->offs.p));
     GD_TRY(d2h(h, out_perm, h->out_a, n));
     GD_TRY(d2h(h, out_offsets, h->offs, (size_t)n_act + 2));
-    return sync(h);
+    return sync_checked(h);
 }
 
 int gd_route_bucket(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, uint32_t* out_silo, uint32_t* out_act,
@@ -685,7 +734,7 @@ int gd_route_bucket(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act
     GD_TRY(d2h(h, out_status, h->out_c, n));
     GD_TRY(d2h(h, out_perm, h->u8_a, n));
     GD_TRY(d2h(h, out_offsets, h->offs, (size_t)n_act + 2));
-    return sync(h);
+    return sync_checked(h);
 }
 
 int gd_pack_by_shard_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_shards, gd_key* d_send_keys,
@@ -725,6 +774,13 @@ int gd_kernel_times(gd_handle* h, gd_kernel_time* out, uint32_t max, uint32_t* o
         out[i].total_ms = h->tms[i];
     }
     *out_n = (uint32_t)h->tnames.size();
+    return GD_OK;
+}
+
+int gd_set_kernel_timing(gd_handle* h, int enable) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    GD_TRY(resolve_timing(h));
+    h->timing = enable != 0;
     return GD_OK;
 }
 

@@ -198,6 +198,117 @@ __global__ void __launch_bounds__(BLOCK) k_route(const gd_key* __restrict__ keys
     }
 }
 
+template <bool NT, typename T>
+__device__ __forceinline__ T ld(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st(T* p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// The route kernel proper: M messages per thread (coalesced: message
+// base + j*BLOCK + tid), all M first probes issued before any is inspected so
+// that each lane keeps M random 32-B slot reads in flight.  NT streams the key
+// reads and result writes non-temporally so they do not push the table out of
+// the caches it shares with them.
+template <int MODE, int M, bool NT>
+__global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+                                                   TableArgs tab, uint32_t* __restrict__ out_silo,
+                                                   uint32_t* __restrict__ out_act,
+                                                   uint8_t* __restrict__ out_status) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    stage_ring(ring, s_pts, s_own);
+    const uint32_t max_probe = tab.ctr->max_probe;
+    const uint32_t base = blockIdx.x * (BLOCK * M) + threadIdx.x;
+
+    uint64_t n0[M], n1[M], tcd[M];
+    uint32_t h[M], silo[M], act[M];
+    uint8_t status[M];
+    bool need[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        const uint32_t i = base + j * BLOCK;
+        n0[j] = n1[j] = tcd[j] = 0;
+        if (i < n) {
+            const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
+            n0[j] = ld<NT>(kp);
+            n1[j] = ld<NT>(kp + 1);
+            tcd[j] = ld<NT>(kp + 2);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        const uint32_t cat = (uint32_t)(tcd[j] >> 56);
+        act[j] = NONE32;
+        need[j] = false;
+        h[j] = 0;
+        if (cat == CAT_SYSTEM_TARGET) {                        // LocalGrainDirectory.cs:480-485
+            silo[j] = ring.my_silo;
+            status[j] = GD_ROUTE_SYSTEM_TARGET;
+        } else if (is_membership(n0[j], n1[j], tcd[j])) {     // :487-503
+            silo[j] = ring.seed_silo;
+            status[j] = GD_ROUTE_MEMBERSHIP;
+        } else if (cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) {  // UniqueKey.cs:279-281
+            silo[j] = NONE32;
+            status[j] = GD_ROUTE_KEYEXT;
+        } else {
+            h[j] = uniform_hash(n0[j], n1[j], tcd[j]);
+            silo[j] = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[j])];
+            status[j] = GD_ROUTE_MISS;
+            need[j] = true;
+        }
+    }
+    // first probe of every message, all in flight together
+    unsigned long long s[M];
+    uint4 qa[M], qb[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        s[j] = fmix32(h[j]) & tab.mask;
+        if (need[j]) {
+            const uint4* q = reinterpret_cast<const uint4*>(tab.slots + s[j]);
+            qa[j] = q[0];
+            qb[j] = q[1];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        if (!need[j]) continue;
+        uint4 a = qa[j], b = qb[j];
+        for (uint32_t p = 0;;) {
+            const uint32_t stt = slot_state(b.w);
+            if (stt == SLOT_EMPTY) break;
+            const uint64_t k0 = (uint64_t)a.x | ((uint64_t)a.y << 32);
+            const uint64_t k1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
+            const uint64_t k2 = (uint64_t)b.x | ((uint64_t)b.y << 32);
+            if (stt == SLOT_LIVE && k0 == n0[j] && k1 == n1[j] && k2 == tcd[j]) {
+                act[j] = b.z;
+                silo[j] = slot_silo(b.w);                     // ActivationAddress.Silo (Message.cs:629-639)
+                status[j] = GD_ROUTE_OK;
+                break;
+            }
+            if (++p > max_probe) break;                        // miss: Dispatcher.cs:742 slow path
+            s[j] = (s[j] + 1) & tab.mask;
+            const uint4* q = reinterpret_cast<const uint4*>(tab.slots + s[j]);
+            a = q[0];
+            b = q[1];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        const uint32_t i = base + j * BLOCK;
+        if (i < n) {
+            st<NT>(out_silo + i, silo[j]);
+            st<NT>(out_act + i, act[j]);
+            st<NT>(out_status + i, status[j]);
+        }
+    }
+}
+
 // GetPrimaryTargetSilo(uint key) over raw ring keys.
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK) k_ring_hashes(const uint32_t* __restrict__ hashes, uint32_t n,
@@ -468,8 +579,20 @@ __device__ __forceinline__ unsigned long long match_digit(uint32_t d, bool valid
     return peers;
 }
 
-// Block-wide exclusive add-scan of one value per thread (BLOCK threads).
-__device__ __forceinline__ uint32_t block_excl_scan_add(uint32_t v, uint32_t* s_wsum, uint32_t& total) {
+// ------------------------------------------------------------------ K3: stable radix partition
+// LSD passes, reduce-then-scan (no in-kernel waiting between workgroups: on
+// gfx950 every cross-CU hand-off round-trips through the memory side, which a
+// chained look-back pays per step; a kernel boundary costs ~1.5 us once).
+// Tile = NT*IT consecutive positions.  Per pass:
+//   k_radix_hist    per-tile digit counts, stored digit-major hist[d * tiles + t]
+//   scan            one exclusive scan gives every (digit, tile) its global base
+//   k_radix_scatter stable rank in the tile (wave-striped order = index order),
+//                   stage the tile in LDS in digit order, write each digit run
+//                   contiguously.
+
+// Block-wide exclusive add-scan of one value per thread (NTH threads).
+template <int NTH>
+__device__ __forceinline__ uint32_t block_excl_scan_add_n(uint32_t v, uint32_t* s_wsum) {
     const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     uint32_t x = v;
 #pragma unroll
@@ -479,99 +602,122 @@ __device__ __forceinline__ uint32_t block_excl_scan_add(uint32_t v, uint32_t* s_
     }
     if (lane == WAVE - 1) s_wsum[w] = x;
     __syncthreads();
-    uint32_t wbase = 0, tot = 0;
+    uint32_t wbase = 0;
 #pragma unroll
-    for (int k = 0; k < BLOCK / WAVE; ++k) {
-        const uint32_t t = s_wsum[k];
-        if ((uint32_t)k < w) wbase += t;
-        tot += t;
-    }
+    for (int k = 0; k < NTH / WAVE; ++k)
+        if ((uint32_t)k < w) wbase += s_wsum[k];
     __syncthreads();
-    total = tot;
     return wbase + x - v;
 }
 
-// ------------------------------------------------------------------ K3: stable radix partition
-// Tile = RADIX_TILE consecutive messages.  Upsweep: per-tile digit counts,
-// stored digit-major (hist[d * tiles + t]) so that one exclusive scan gives
-// every (digit, tile) its global base.
-template <int BITS>
-__global__ void __launch_bounds__(BLOCK) k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n,
-                                                      uint32_t clamp, uint32_t shift, uint32_t tiles,
-                                                      uint32_t* __restrict__ hist) {
+// Histogram.  Keys are read 16 B per lane (order is irrelevant here).  Equal
+// digits within a wave instruction: the lanes sharing the first active lane's
+// digit (the hot key under Zipf skew) are folded into one LDS atomic.
+template <int BITS, int NT, int IT>
+__global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t clamp,
+                                                   uint32_t shift, uint32_t tiles, uint32_t* __restrict__ hist) {
     constexpr uint32_t R = 1u << BITS;
-    __shared__ uint32_t s_cnt[R];
-    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) s_cnt[d] = 0;
+    constexpr int NW = NT / WAVE;
+    constexpr uint32_t TILE = NT * IT;
+    static_assert(IT % 4 == 0, "16-B loads");
+    __shared__ uint32_t s_cnt[NW * R];
+    for (uint32_t d = threadIdx.x; d < NW * R; d += NT) s_cnt[d] = 0;
     __syncthreads();
-    const uint32_t base = blockIdx.x * RADIX_TILE;
+    uint32_t* my_cnt = s_cnt + (threadIdx.x / WAVE) * R;
+    const uint32_t base = blockIdx.x * TILE;
     const uint32_t lane = lane_id();
-    const unsigned long long lt = (1ull << lane) - 1ull;
-#pragma unroll 4
-    for (int j = 0; j < RADIX_ITEMS; ++j) {
-        const uint32_t idx = base + j * BLOCK + threadIdx.x;
-        const bool valid = idx < n;
-        const uint32_t k = valid ? min(keys[idx], clamp) : 0u;
-        const uint32_t d = (k >> shift) & (R - 1);
-        const unsigned long long peers = match_digit<BITS>(d, valid);
-        if (valid && (peers & lt) == 0) atomicAdd(&s_cnt[d], (uint32_t)__popcll(peers));
+    const bool vec = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0 && base + TILE <= n;
+    uint32_t k[IT];
+#pragma unroll
+    for (int j = 0; j < IT / 4; ++j) {
+        const uint32_t i0 = base + 4 * (j * NT + threadIdx.x);
+        if (vec) {
+            const uint4 v = *reinterpret_cast<const uint4*>(keys + i0);
+            k[4 * j] = v.x; k[4 * j + 1] = v.y; k[4 * j + 2] = v.z; k[4 * j + 3] = v.w;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) k[4 * j + q] = (i0 + q < n) ? keys[i0 + q] : NONE32;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+        const uint32_t i = base + 4 * ((j / 4) * NT + threadIdx.x) + (j % 4);
+        const bool valid = i < n;
+        const uint32_t d = (min(k[j], clamp) >> shift) & (R - 1);
+        const unsigned long long act = __ballot(valid);
+        if (act == 0) continue;
+        const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
+        const uint32_t d0 = __shfl(d, lead, WAVE);
+        const unsigned long long hot = __ballot(valid && d == d0);
+        if (valid) {
+            if (d != d0) atomicAdd(&my_cnt[d], 1u);
+            else if (lane == lead) atomicAdd(&my_cnt[d], (uint32_t)__popcll(hot));
+        }
     }
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) hist[d * tiles + blockIdx.x] = s_cnt[d];
+    for (uint32_t d = threadIdx.x; d < R; d += NT) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) c += s_cnt[w * R + d];
+        hist[d * tiles + blockIdx.x] = c;
+    }
 }
 
-// Downsweep: stable rank inside the tile (wave-striped order = index order),
-// stage the tile in LDS in digit order, write each digit run contiguously.
-// FIRST: values are the message indices themselves.  The keys are clamped to
-// `clamp` (unrouted messages -> trailing bucket).
-template <int BITS, bool FIRST>
-__global__ void __launch_bounds__(BLOCK) k_radix_scatter(const uint32_t* __restrict__ keys_in,
-                                                         const uint32_t* __restrict__ vals_in, uint32_t n,
-                                                         uint32_t clamp, uint32_t shift, uint32_t tiles,
-                                                         const uint32_t* __restrict__ gscan,
-                                                         uint32_t* __restrict__ keys_out,
-                                                         uint32_t* __restrict__ vals_out) {
+// Downsweep.  FIRST: values are the message indices themselves.  The keys are
+// clamped to `clamp` (unrouted messages -> trailing bucket).
+template <int BITS, bool FIRST, int NT, int IT>
+__global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict__ keys_in,
+                                                      const uint32_t* __restrict__ vals_in, uint32_t n,
+                                                      uint32_t clamp, uint32_t shift, uint32_t tiles,
+                                                      const uint32_t* __restrict__ gscan,
+                                                      uint32_t* __restrict__ keys_out,
+                                                      uint32_t* __restrict__ vals_out) {
     constexpr uint32_t R = 1u << BITS;
-    constexpr int NW = BLOCK / WAVE;
+    constexpr int NW = NT / WAVE;
+    constexpr uint32_t TILE = NT * IT;
+    static_assert(R <= NT, "one thread per digit");
     __shared__ uint32_t s_wcnt[NW][R];
     __shared__ uint32_t s_lstart[R];
     __shared__ uint32_t s_gbase[R];
-    __shared__ uint32_t s_key[RADIX_TILE];
-    __shared__ uint32_t s_val[RADIX_TILE];
+    __shared__ uint2 s_kv[TILE];
     __shared__ uint32_t s_wsum[NW];
 
     const uint32_t tile = blockIdx.x;
-    const uint32_t base = tile * RADIX_TILE;
-    const uint32_t cnt_tile = min((uint32_t)RADIX_TILE, n - base);
-    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) {
+    const uint32_t base = tile * TILE;
+    const uint32_t cnt_tile = min(TILE, n - base);
+    for (uint32_t d = threadIdx.x; d < R; d += NT) {
 #pragma unroll
         for (int w = 0; w < NW; ++w) s_wcnt[w][d] = 0;
         s_gbase[d] = gscan[d * tiles + tile];
     }
-    __syncthreads();
-
     const uint32_t lane = lane_id();
     const uint32_t w = threadIdx.x / WAVE;
     const unsigned long long lt = (1ull << lane) - 1ull;
-    uint32_t rk[RADIX_ITEMS], kk[RADIX_ITEMS], vv[RADIX_ITEMS];
+    uint32_t rk[IT], kk[IT], vv[IT];
 #pragma unroll
-    for (int r = 0; r < RADIX_ITEMS; ++r) {
-        const uint32_t idx = base + (w * RADIX_ITEMS + r) * WAVE + lane;
+    for (int r = 0; r < IT; ++r) {
+        const uint32_t idx = base + (w * IT + r) * WAVE + lane;
         const bool valid = idx < n;
-        const uint32_t k = valid ? min(keys_in[idx], clamp) : 0u;
-        const uint32_t v = FIRST ? idx : (valid ? vals_in[idx] : 0u);
-        const uint32_t d = (k >> shift) & (R - 1);
+        kk[r] = valid ? min(keys_in[idx], clamp) : 0u;
+        vv[r] = FIRST ? idx : (valid ? vals_in[idx] : 0u);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < IT; ++r) {
+        const uint32_t idx = base + (w * IT + r) * WAVE + lane;
+        const bool valid = idx < n;
+        const uint32_t d = (kk[r] >> shift) & (R - 1);
         const unsigned long long peers = match_digit<BITS>(d, valid);
         uint32_t c = 0;
         if (valid) c = s_wcnt[w][d];
         rk[r] = c + (uint32_t)__popcll(peers & lt);
         if (valid && (peers & lt) == 0) s_wcnt[w][d] = c + (uint32_t)__popcll(peers);
-        kk[r] = k;
-        vv[r] = v;
     }
     __syncthreads();
     // cross-wave exclusive prefix per digit, then tile-local digit starts
     uint32_t my_total = 0;
-    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) {
+    if (threadIdx.x < R) {
+        const uint32_t d = threadIdx.x;
         uint32_t run = 0;
 #pragma unroll
         for (int ww = 0; ww < NW; ++ww) {
@@ -581,31 +727,28 @@ __global__ void __launch_bounds__(BLOCK) k_radix_scatter(const uint32_t* __restr
         }
         my_total = run;
     }
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan_add(threadIdx.x < R ? my_total : 0u, s_wsum, tot);
+    const uint32_t ex = block_excl_scan_add_n<NT>(my_total, s_wsum);
     if (threadIdx.x < R) s_lstart[threadIdx.x] = ex;
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < RADIX_ITEMS; ++r) {
-        const uint32_t idx = base + (w * RADIX_ITEMS + r) * WAVE + lane;
+    for (int r = 0; r < IT; ++r) {
+        const uint32_t idx = base + (w * IT + r) * WAVE + lane;
         if (idx < n) {
             const uint32_t d = (kk[r] >> shift) & (R - 1);
-            const uint32_t lpos = s_lstart[d] + s_wcnt[w][d] + rk[r];
-            s_key[lpos] = kk[r];
-            s_val[lpos] = vv[r];
+            s_kv[s_lstart[d] + s_wcnt[w][d] + rk[r]] = make_uint2(kk[r], vv[r]);
         }
     }
     __syncthreads();
 #pragma unroll 4
-    for (int j = 0; j < RADIX_ITEMS; ++j) {
-        const uint32_t p = j * BLOCK + threadIdx.x;
+    for (int j = 0; j < IT; ++j) {
+        const uint32_t p = j * NT + threadIdx.x;
         if (p < cnt_tile) {
-            const uint32_t k = s_key[p];
-            const uint32_t d = (k >> shift) & (R - 1);
+            const uint2 kv = s_kv[p];
+            const uint32_t d = (kv.x >> shift) & (R - 1);
             const uint32_t g = s_gbase[d] + (p - s_lstart[d]);
             if (g < n) {            // always true when the scan is right; never write out of bounds
-                keys_out[g] = k;
-                vals_out[g] = s_val[p];
+                keys_out[g] = kv.x;
+                vals_out[g] = kv.y;
             }
         }
     }
@@ -709,8 +852,22 @@ __global__ void __launch_bounds__(BLOCK) k_scan_partials(uint32_t* partials, uin
 
 template <class Op>
 __global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_t* out, uint32_t n, bool rev,
-                                                     bool inclusive, const uint32_t* __restrict__ partials) {
+                                                     bool inclusive, const uint32_t* __restrict__ partials,
+                                                     uint32_t n_partials_raw) {
     __shared__ uint32_t s_wsum[BLOCK / WAVE];
+    __shared__ uint32_t s_prefix;
+    // n_partials_raw > 0: `partials` holds raw block aggregates; fold those of the
+    // preceding blocks here instead of a separate single-block scan launch.
+    if (n_partials_raw) {
+        uint32_t acc = Op::identity;
+        for (uint32_t j = threadIdx.x; j < blockIdx.x; j += BLOCK) acc = Op::apply(acc, partials[j]);
+        acc = block_reduce<Op>(acc, s_wsum);
+        if (threadIdx.x == 0) s_prefix = acc;
+    } else if (threadIdx.x == 0) {
+        s_prefix = partials[blockIdx.x];
+    }
+    __syncthreads();
+    const uint32_t prefix = s_prefix;
     const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
     uint32_t v[SCAN_ITEMS];
     uint32_t acc = Op::identity;
@@ -720,7 +877,7 @@ __global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_
         v[k] = j < n ? in[phys(j, n, rev)] : Op::identity;
         acc = Op::apply(acc, v[k]);
     }
-    uint32_t run = Op::apply(partials[blockIdx.x], block_excl_scan<Op>(acc, s_wsum));
+    uint32_t run = Op::apply(prefix, block_excl_scan<Op>(acc, s_wsum));
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) {
         const uint32_t j = base + k;

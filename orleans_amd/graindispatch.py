@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = [
     "gd_dir_unregister", "gd_dir_lookup", "gd_dir_clear", "gd_dir_rehash", "gd_route", "gd_bucket",
     "gd_route_bucket", "gd_route_device", "gd_bucket_device", "gd_route_bucket_device",
     "gd_ring_owner_device", "gd_pack_by_shard_device", "gd_kernel_times", "gd_kernel_times_reset",
+    "gd_set_kernel_timing",
 ]
 
 
@@ -111,6 +112,7 @@ def _load() -> C.CDLL:
         "gd_pack_by_shard_device": (C.c_int, [P, P, U32, U32, P, P, P]),
         "gd_kernel_times": (C.c_int, [P, C.POINTER(gd_kernel_time), U32, C.POINTER(U32)]),
         "gd_kernel_times_reset": (C.c_int, [P]),
+        "gd_set_kernel_timing": (C.c_int, [P, C.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -348,6 +350,9 @@ class GrainDispatch:
         n = C.c_uint32(0)
         self._c(lib.gd_kernel_times(self.h, arr, 64, C.byref(n)))
         return {arr[i].name.decode(): (int(arr[i].launches), float(arr[i].total_ms)) for i in range(min(n.value, 64))}
+
+    def set_kernel_timing(self, enable: bool):
+        self._c(lib.gd_set_kernel_timing(self.h, 1 if enable else 0))
 
     def kernel_times_reset(self):
         self._c(lib.gd_kernel_times_reset(self.h))

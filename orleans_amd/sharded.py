@@ -1,0 +1,109 @@
+"""Directory sharded by ring owner across GPUs (one process per GPU).
+
+The mirror of Orleans' per-silo directory partitions (GrainDirectoryPartition,
+LocalGrainDirectory.cs:477-545) and of its per-target-silo outbound queues
+(OutboundMessageQueue.cs:54-131): every rank owns the directory entries of the
+silos it hosts (silo s lives on rank s % world); a batch of message headers is
+partitioned by owner rank (stable), exchanged with one all-to-all-v, then
+routed (directory probe) and bucketed per activation on the owner.
+
+Exchange = torch.distributed all_to_all_single: RCCL over xGMI on MI355X
+(backend "nccl"), gloo in the CPU tests.  The local steps run through an
+engine object; `DeviceEngine` is the product engine (libgraindispatch device
+entry points on torch-allocated HBM buffers).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from . import graindispatch as g
+
+
+@dataclass
+class ShardedResult:
+    recv_keys: torch.Tensor     # (M,3) int64 -- message headers this rank owns, arrival order
+    recv_idx: Optional[torch.Tensor]   # (M,) int32 -- index in the sender's batch (None: world 1, identity)
+    recv_src: Optional[torch.Tensor]   # (M,) int32 -- sender rank (None: world 1, all rank 0)
+    status: torch.Tensor        # (M,) uint8
+    silo: torch.Tensor          # (M,) int32 (uint32 bit pattern)
+    act: torch.Tensor           # (M,) int32 (uint32 bit pattern)
+    perm: torch.Tensor          # (M,) int32: stable per-activation order of recv positions
+    offsets: torch.Tensor       # (n_act+2,) int32
+
+
+class DeviceEngine:
+    """libgraindispatch on this rank's GPU, driven through the *_device C-ABI
+    entry points on the current torch stream."""
+
+    def __init__(self, dispatch: g.GrainDispatch, device: torch.device, stream: Optional[torch.cuda.Stream] = None):
+        self.gd = dispatch
+        self.device = device
+        # A dedicated (non-null) stream: torch's legacy default stream has handle 0,
+        # which the C ABI reads as "use the library's own stream".  Callers run
+        # their torch work under `with torch.cuda.stream(engine.stream)`.
+        self.stream = stream or torch.cuda.Stream(device)
+        self.gd.set_stream(self.stream.cuda_stream)
+
+    def pack_by_shard(self, keys: torch.Tensor, n_shards: int):
+        n = keys.shape[0]
+        send_keys = torch.empty_like(keys)
+        send_idx = torch.empty(n, dtype=torch.int32, device=self.device)
+        counts = torch.empty(n_shards, dtype=torch.int32, device=self.device)
+        self.gd.pack_by_shard_device(keys.data_ptr(), n, n_shards, send_keys.data_ptr(), send_idx.data_ptr(),
+                                     counts.data_ptr())
+        return send_keys, send_idx, counts
+
+    def route_bucket(self, keys: torch.Tensor, n_act: int):
+        n = keys.shape[0]
+        dev = self.device
+        st = torch.empty(n, dtype=torch.uint8, device=dev)
+        silo = torch.empty(n, dtype=torch.int32, device=dev)
+        act = torch.empty(n, dtype=torch.int32, device=dev)
+        perm = torch.empty(n, dtype=torch.int32, device=dev)
+        off = torch.empty(n_act + 2, dtype=torch.int32, device=dev)
+        self.gd.route_bucket_device(keys.data_ptr(), n, n_act, silo.data_ptr(), act.data_ptr(), st.data_ptr(),
+                                    perm.data_ptr(), off.data_ptr())
+        return st, silo, act, perm, off
+
+
+class ShardedRouter:
+    def __init__(self, engine, group: Optional[dist.ProcessGroup] = None):
+        self.engine = engine
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def exchange(self, keys: torch.Tensor):
+        """Stable partition by owner rank + all-to-all-v of the headers."""
+        send_keys, send_idx, counts = self.engine.pack_by_shard(keys, self.world)
+        counts64 = counts.to(torch.int64)
+        recv_counts = torch.empty_like(counts64)
+        dist.all_to_all_single(recv_counts, counts64, group=self.group)
+        in_splits = counts64.tolist()
+        out_splits = recv_counts.tolist()
+        m = int(sum(out_splits))
+        recv_keys = torch.empty((m, 3), dtype=keys.dtype, device=keys.device)
+        dist.all_to_all_single(recv_keys, send_keys, out_splits, in_splits, group=self.group)
+        recv_idx = torch.empty(m, dtype=torch.int32, device=keys.device)
+        dist.all_to_all_single(recv_idx, send_idx, out_splits, in_splits, group=self.group)
+        recv_src = torch.repeat_interleave(torch.arange(self.world, dtype=torch.int32, device=keys.device),
+                                           recv_counts.to(keys.device))
+        return recv_keys, recv_idx, recv_src
+
+    def route_bucket(self, keys: torch.Tensor, n_act: int) -> ShardedResult:
+        if self.world == 1:
+            # no exchange: arrival order is the batch order, all from this rank
+            recv_keys, recv_idx, recv_src = keys, None, None
+        else:
+            recv_keys, recv_idx, recv_src = self.exchange(keys)
+        st, silo, act, perm, off = self.engine.route_bucket(recv_keys, n_act)
+        return ShardedResult(recv_keys, recv_idx, recv_src, st, silo, act, perm, off)
+
+
+def silo_rank(silo: int, world: int) -> int:
+    """Which rank hosts (owns the directory partition of) a silo."""
+    return silo % world
