@@ -1,0 +1,108 @@
+"""Worker for tests/test_sharded_gloo.py: run under
+`torch.distributed.run --nproc-per-node N` with the gloo backend on CPU.
+
+It drives orleans_amd.sharded.ShardedRouter -- the exact exchange code bench.py
+runs over RCCL -- with a CPU engine built from the oracle (test infrastructure
+standing in for the GPU engine), and checks the sharded results against a
+single-node oracle run."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle as o                                   # noqa: E402
+from orleans_amd.sharded import ShardedRouter        # noqa: E402
+
+TC = o.grain_type_code(o.PING_GRAIN_CLASS)
+SPEC = o.ring_spec(o.bench_silos(8), "D")
+G_TOTAL = 3000
+N_PER_RANK = 20000
+
+
+def batch_of(rank):
+    rng = np.random.default_rng(1000 + rank)
+    keys = o.grain_keys(TC, rng.integers(0, G_TOTAL + 200, size=N_PER_RANK))   # ~6% unregistered
+    keys[::997] = np.array(o.UniqueKey(0, 7, o.type_code_data(o.CAT_SYSTEM_TARGET, 1)).as_tuple(), dtype=np.uint64)
+    return keys
+
+
+class OracleEngine:
+    """CPU stand-in for orleans_amd.sharded.DeviceEngine (same method contract)."""
+
+    def __init__(self, rank, world, my_silo):
+        self.rank, self.world, self.my_silo = rank, world, my_silo
+        reg = o.grain_keys(TC, np.arange(G_TOTAL))
+        own = o.ring_owner_np(SPEC, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1]))
+        mine = np.nonzero(own % world == rank)[0]
+        self.n_act = len(mine)
+        self.dir = o.DirectoryArrays(reg[mine], np.arange(self.n_act), own[mine])
+        self.local_act_of_grain = {int(g): i for i, g in enumerate(mine)}
+
+    def pack_by_shard(self, keys, n_shards):
+        k = keys.numpy().view(np.uint64)
+        st, silo, act, owner, h = o.route_batch_np(k, SPEC, o.DirectoryArrays(np.zeros((0, 3), np.uint64), [], []),
+                                                   my_silo=self.my_silo, seed_silo=0)
+        owner = np.where(owner == o.M32, self.my_silo, owner)
+        dest = (owner % n_shards).astype(np.uint32)
+        perm, off = o.bucket_stable(dest, n_shards)
+        counts = np.diff(off[: n_shards + 1]).astype(np.int32)
+        return (torch.from_numpy(k[perm].view(np.int64).copy()), torch.from_numpy(perm.astype(np.int32)),
+                torch.from_numpy(counts))
+
+    def route_bucket(self, keys, n_act):
+        k = keys.numpy().view(np.uint64)
+        st, silo, act, owner, h = o.route_batch_np(k, SPEC, self.dir, my_silo=self.my_silo, seed_silo=0)
+        perm, off = o.bucket_stable(act, n_act)
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt))
+        return (t(st, np.uint8), t(silo, np.int32), t(act, np.int32), t(perm, np.int32), t(off, np.int32))
+
+
+def main():
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    eng = OracleEngine(rank, world, my_silo=rank)
+    router = ShardedRouter(eng)
+    keys = torch.from_numpy(batch_of(rank).view(np.int64).copy())
+    res = router.route_bucket(keys, eng.n_act)
+    m = res.recv_keys.shape[0]
+    rk = res.recv_keys.numpy().view(np.uint64)
+    src = res.recv_src.numpy()
+    idx = res.recv_idx.numpy()
+    # 1) every received header is the sender's message at (src, idx)
+    batches = {r: batch_of(r) for r in range(world)}
+    for j in range(m):
+        assert (batches[src[j]][idx[j]] == rk[j]).all()
+    # 2) arrival order: grouped by sender rank, each group in the sender's batch order
+    order = src.astype(np.int64) * (1 << 32) + idx
+    assert (np.diff(order) > 0).all()
+    # 3) this rank owns what it received (system targets stay with their sender's silo)
+    st, silo, act, owner, h = o.route_batch_np(rk, SPEC, eng.dir, my_silo=rank, seed_silo=0)
+    owner = np.where(owner == o.M32, src, owner)
+    is_sys = st == o.ST_SYSTEM_TARGET
+    assert ((owner[~is_sys] % world) == rank).all()
+    # 4) routed results = the oracle on the received headers; per-activation FIFO
+    assert np.array_equal(res.status.numpy(), st)
+    assert np.array_equal(res.act.numpy().view(np.uint32), act)
+    wp, wo = o.bucket_stable(act, eng.n_act)
+    assert np.array_equal(res.perm.numpy().view(np.uint32), wp)
+    assert np.array_equal(res.offsets.numpy().view(np.uint32), wo)
+    # 5) nothing lost: messages received over all ranks == messages sent
+    tot = torch.tensor([m], dtype=torch.int64)
+    dist.all_reduce(tot)
+    assert tot.item() == world * N_PER_RANK
+    # 6) every OK message found its grain: act is the owner's local index of that grain
+    ok = st == o.ST_OK
+    assert (rk[ok, 1] < G_TOTAL).all()
+    for j in np.nonzero(ok)[0][:500]:
+        assert act[j] == eng.local_act_of_grain[int(rk[j, 1])]
+    print(f"OK rank {rank}/{world}: received {m}, ok {int(ok.sum())}", flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,129 @@
+"""CPU tests of the C ABI boundary: libgraindispatch.so loads, exports every
+symbol include/graindispatch.h declares, and its host-side identity / ring
+builders agree with the oracle and the golden vectors.  No kernel is launched."""
+import ctypes as C
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle as o
+from orleans_amd import graindispatch as g
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+
+
+def _declared_symbols():
+    hdr = open(os.path.join(ROOT, "include", "graindispatch.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"\b(gd_[a-z0-9_]+)\s*\(", hdr)))
+
+
+def test_every_declared_symbol_is_exported():
+    syms = _declared_symbols()
+    assert len(syms) >= 30
+    lib = C.CDLL(g.LIB_PATH)
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(g.EXPORTED_SYMBOLS) == syms
+
+
+def test_abi_version_and_struct_sizes():
+    assert g.lib.gd_abi_version() == 1
+    assert C.sizeof(g.gd_key) == 24
+    assert C.sizeof(g.gd_val) == 8
+    assert C.sizeof(g.gd_silo_addr) == 28
+    assert C.sizeof(g.gd_config) == 32
+
+
+def test_jenkins_matches_oracle_and_golden():
+    r = np.random.default_rng(1)
+    for n in list(range(0, 40)) + [100, 257]:
+        b = bytes(r.integers(0, 256, size=n, dtype=np.uint8))
+        assert g.jenkins_bytes(b) == o.jenkins_bytes(b)
+    for hexb, h in GOLDEN["jenkins_bytes"]:
+        assert g.jenkins_bytes(bytes.fromhex(hexb)) == h
+    for a, b, c, h in GOLDEN["jenkins_u64x3"]:
+        assert g.jenkins_u64x3(int(a), int(b), int(c)) == h
+    k = g.gd_key(5, 6, o.type_code_data(o.CAT_GRAIN, 9))
+    assert g.lib.gd_uniform_hash(C.byref(k)) == o.UniqueKey(5, 6, k.type_code_data).uniform_hash()
+
+
+def test_calculate_id_hash_sha256_utf16():
+    for t, h in GOLDEN["calculate_id_hash"]:
+        assert g.calculate_id_hash(t) == h, t
+    # lengths around the SHA-256 block boundaries (55/56/64 bytes of UTF-16)
+    for n in range(20, 70):
+        t = "q" * n
+        assert g.calculate_id_hash(t) == o.calculate_id_hash(t)
+
+
+def test_silo_hashes_match_golden():
+    for s in GOLDEN["silos"]:
+        assert g.silo_consistent_hash(s["ip"], s["port"], s["gen"]) == s["consistent_hash"], s
+        assert g.silo_uniform_hashes(s["ip"], s["port"], s["gen"], 30) == s["uniform_hashes_30"], s
+
+
+def test_silo_compare_matches_reference_order():
+    a = g.silo_addr("10.0.0.1", 11111, 1)
+    b = g.silo_addr("10.0.0.2", 11111, 1)
+    c = g.silo_addr("10.0.0.1", 11112, 1)
+    d = g.silo_addr("10.0.0.9", 1, 2)
+    cmp = lambda x, y: g.lib.gd_silo_compare(C.byref(x), C.byref(y))
+    assert cmp(a, b) < 0 and cmp(b, a) > 0 and cmp(a, a) == 0
+    assert cmp(b, c) < 0          # port before IP (SiloAddress.cs:287-291)
+    assert cmp(c, d) < 0          # generation first
+    assert o.Silo("10.0.0.2", 11111, 1).compare_to(o.Silo("10.0.0.1", 11112, 1)) < 0
+
+
+@pytest.mark.parametrize("mode", ["D", "R", "V"])
+def test_ring_build_matches_oracle(mode):
+    sets = {"bench8": o.bench_silos(8),
+            "mixed10": [o.Silo(s["ip"], s["port"], s["gen"]) for s in GOLDEN["silos"]],
+            "loopback5": [o.Silo("127.0.0.1", 0, k) for k in range(1, 6)]}
+    for name, silos in sets.items():
+        pts, own = g.ring_build(mode, [(s.ip, s.port, s.gen) for s in silos])
+        want = GOLDEN["rings"][f"{name}/{mode}"]
+        got_pts = [int(x) - (1 << 32) if (mode != "V" and x >= 1 << 31) else int(x) for x in pts]
+        assert got_pts == want["points"] and own.tolist() == want["owners"], name
+    many = [o.Silo(f"10.{i // 200}.{i % 200}.7", 11111 + i % 7, 1 + i % 3) for i in range(64)]
+    pts, own = g.ring_build(mode, [(s.ip, s.port, s.gen) for s in many])
+    sp = o.ring_spec(many, mode)
+    assert own.tolist() == sp.owners
+
+
+def test_ring_build_collision_rule():
+    """VirtualBucketsRingProvider.AddServer (:129-134) skips a colliding newcomer only when
+    it compares GREATER; an equal silo (same address, port, generation) overwrites."""
+    s = [("10.0.0.1", 11111, 1), ("10.0.0.1", 11111, 1)]
+    pts, own = g.ring_build("V", s, 4)
+    assert len(pts) == 4 and set(own.tolist()) == {1}
+    sp = o.ring_spec([o.Silo(*x) for x in s], "V", 4)
+    assert sp.owners == own.tolist()
+
+
+def test_ring_build_rejects_bad_args():
+    pts = np.zeros(4, np.uint32)
+    n = C.c_uint32(0)
+    assert g.lib.gd_ring_build(9, None, 0, 0, pts.ctypes.data, pts.ctypes.data, C.byref(n)) == g.GD_EINVAL
+    arr = (g.gd_silo_addr * 1)(g.silo_addr("10.0.0.1", 1, 1))
+    assert g.lib.gd_ring_build(2, arr, 1, 0, pts.ctypes.data, pts.ctypes.data, C.byref(n)) == g.GD_EINVAL
+
+
+def test_create_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the GPU tests")
+    with pytest.raises(g.GrainDispatchError) as ei:
+        g.GrainDispatch(device=0)
+    assert ei.value.code in (g.GD_EHIP, g.GD_ENOMEM)
+    assert g.lib.gd_last_error(None)
+
+
+def test_null_handle_errors():
+    assert g.lib.gd_synchronize(None) == g.GD_EINVAL
+    assert g.lib.gd_ring_set(None, 0, None, None, 0) == g.GD_EINVAL
+    assert b"null" in g.lib.gd_last_error(None)
