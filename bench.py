@@ -69,15 +69,21 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=5, help="extra steps with per-kernel events")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="rehearsal only: every rank on cuda:0, gloo, host-staged all-to-all")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == args.gpus or "WORLD_SIZE" not in os.environ, "--gpus must match WORLD_SIZE"
+    if args.rehearse_one_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 and args.rehearse_one_gpu:
+        dist.init_process_group("gloo")
+    elif world > 1:
         dist.init_process_group("nccl", device_id=dev)
     else:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -107,7 +113,7 @@ def main():
     torch.cuda.synchronize()
 
     engine = DeviceEngine(e, dev)
-    router = ShardedRouter(engine)
+    router = ShardedRouter(engine, stage_via_cpu=args.rehearse_one_gpu)
     stream = engine.stream
 
     def step():
@@ -209,6 +215,7 @@ def main():
                        "msgs_per_gpu": N, "grains_total": G_total, "ring_mode": args.mode, "silos": 8,
                        "table_load": round(n_act / (2 * Gr), 3), "parallelism": f"shard{world}"},
             "routed_ok_last_step_rank0": st_ok,
+            "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
             "roofline": roofline,
             "kernels": kernels,
             "cpu_baseline": cpu,

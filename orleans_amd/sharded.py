@@ -71,25 +71,37 @@ class DeviceEngine:
 
 
 class ShardedRouter:
-    def __init__(self, engine, group: Optional[dist.ProcessGroup] = None):
+    """`stage_via_cpu` is a rehearsal mode only (several ranks sharing one GPU with
+    the gloo backend): the all-to-all then runs on host copies of the buffers."""
+
+    def __init__(self, engine, group: Optional[dist.ProcessGroup] = None, stage_via_cpu: bool = False):
         self.engine = engine
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.stage_via_cpu = stage_via_cpu
+
+    def _a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None):
+        if self.stage_via_cpu and out.device.type != "cpu":
+            o_cpu = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(o_cpu, inp.cpu(), out_splits, in_splits, group=self.group)
+            out.copy_(o_cpu)
+        else:
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
     def exchange(self, keys: torch.Tensor):
         """Stable partition by owner rank + all-to-all-v of the headers."""
         send_keys, send_idx, counts = self.engine.pack_by_shard(keys, self.world)
         counts64 = counts.to(torch.int64)
         recv_counts = torch.empty_like(counts64)
-        dist.all_to_all_single(recv_counts, counts64, group=self.group)
+        self._a2a(recv_counts, counts64)
         in_splits = counts64.tolist()
         out_splits = recv_counts.tolist()
         m = int(sum(out_splits))
         recv_keys = torch.empty((m, 3), dtype=keys.dtype, device=keys.device)
-        dist.all_to_all_single(recv_keys, send_keys, out_splits, in_splits, group=self.group)
+        self._a2a(recv_keys, send_keys, out_splits, in_splits)
         recv_idx = torch.empty(m, dtype=torch.int32, device=keys.device)
-        dist.all_to_all_single(recv_idx, send_idx, out_splits, in_splits, group=self.group)
+        self._a2a(recv_idx, send_idx, out_splits, in_splits)
         recv_src = torch.repeat_interleave(torch.arange(self.world, dtype=torch.int32, device=keys.device),
                                            recv_counts.to(keys.device))
         return recv_keys, recv_idx, recv_src
