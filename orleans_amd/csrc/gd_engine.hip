@@ -58,6 +58,7 @@ struct gd_handle {
     // kernel tuning (defaults measured on MI355X; GD_ROUTE_M / GD_ROUTE_NT override for A/B runs)
     int route_m = 1;
     bool route_nt = false;
+    int radix_max_bits = 8;   // digit width cap (GD_RADIX_MAXBITS, 4..11)
     int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
 
     // per-kernel timing
@@ -301,7 +302,9 @@ int radix_pass(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t 
                uint32_t* kout, uint32_t* vout, bool first) {
     switch (h->radix_cfg) {
         case 1: return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first);
-        case 2: return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        case 2:
+            if constexpr (BITS <= 8) return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first);
+            else return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first);
         case 3: return radix_pass_t<BITS, 512, 16>(h, kin, vin, n, clamp, shift, kout, vout, first);
         default: return radix_pass_t<BITS, 256, 16>(h, kin, vin, n, clamp, shift, kout, vout, first);
     }
@@ -314,7 +317,10 @@ int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* 
         case 5: return radix_pass<5>(h, kin, vin, n, clamp, shift, kout, vout, first);
         case 6: return radix_pass<6>(h, kin, vin, n, clamp, shift, kout, vout, first);
         case 7: return radix_pass<7>(h, kin, vin, n, clamp, shift, kout, vout, first);
-        default: return radix_pass<8>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        case 8: return radix_pass<8>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        case 9: return radix_pass<9>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        case 10: return radix_pass<10>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        default: return radix_pass<11>(h, kin, vin, n, clamp, shift, kout, vout, first);
     }
 }
 
@@ -327,7 +333,7 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
     if (n == 0) return GD_OK;
     uint32_t key_bits = 1;
     while (key_bits < 32 && (n_act >> key_bits) != 0) ++key_bits;
-    const uint32_t passes = (key_bits + 7) / 8;
+    const uint32_t passes = (key_bits + h->radix_max_bits - 1) / h->radix_max_bits;
     const uint32_t bits = std::max<uint32_t>(4, (key_bits + passes - 1) / passes);
     GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
     GD_TRY(ensure(h, h->u32_b, (size_t)n * 4));
@@ -409,6 +415,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_ROUTE_M")) h->route_m = std::atoi(v);
     if (const char* v = std::getenv("GD_ROUTE_NT")) h->route_nt = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
+    if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));

@@ -21,7 +21,7 @@ constexpr int WAVE = 64;
 constexpr int BLOCK = 256;               // 4 waves
 constexpr int RADIX_ITEMS = 16;          // items per thread in a radix tile
 constexpr int RADIX_TILE = BLOCK * RADIX_ITEMS;   // 4096 messages per tile
-constexpr int SCAN_ITEMS = 16;
+constexpr int SCAN_ITEMS = 4;     // 1024-entry scan tiles: enough blocks to fill the chip
 constexpr int SCAN_TILE = BLOCK * SCAN_ITEMS;
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 
@@ -675,7 +675,6 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = NT / WAVE;
     constexpr uint32_t TILE = NT * IT;
-    static_assert(R <= NT, "one thread per digit");
     __shared__ uint32_t s_wcnt[NW][R];
     __shared__ uint32_t s_lstart[R];
     __shared__ uint32_t s_gbase[R];
@@ -694,12 +693,20 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
     const uint32_t w = threadIdx.x / WAVE;
     const unsigned long long lt = (1ull << lane) - 1ull;
     uint32_t rk[IT], kk[IT], vv[IT];
+    // Branch-free loads (clamped index, masked after): a per-item `if (valid)` around
+    // each load makes hipcc wait vmcnt(0) after every one of them.
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
         const uint32_t idx = base + (w * IT + r) * WAVE + lane;
-        const bool valid = idx < n;
-        kk[r] = valid ? min(keys_in[idx], clamp) : 0u;
-        vv[r] = FIRST ? idx : (valid ? vals_in[idx] : 0u);
+        const uint32_t li = min(idx, n - 1);
+        kk[r] = keys_in[li];
+        if constexpr (!FIRST) vv[r] = vals_in[li];
+    }
+#pragma unroll
+    for (int r = 0; r < IT; ++r) {
+        const uint32_t idx = base + (w * IT + r) * WAVE + lane;
+        kk[r] = idx < n ? min(kk[r], clamp) : 0u;
+        if constexpr (FIRST) vv[r] = idx;
     }
     __syncthreads();
 #pragma unroll
@@ -715,20 +722,37 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
     }
     __syncthreads();
     // cross-wave exclusive prefix per digit, then tile-local digit starts
+    // (thread t owns digits [t*DPT, (t+1)*DPT))
+    constexpr uint32_t DPT = (R + NT - 1) / NT;
     uint32_t my_total = 0;
-    if (threadIdx.x < R) {
-        const uint32_t d = threadIdx.x;
-        uint32_t run = 0;
 #pragma unroll
-        for (int ww = 0; ww < NW; ++ww) {
-            const uint32_t t = s_wcnt[ww][d];
-            s_wcnt[ww][d] = run;
-            run += t;
+    for (uint32_t q = 0; q < DPT; ++q) {
+        const uint32_t d = threadIdx.x * DPT + q;
+        if (d < R) {
+            uint32_t run = 0;
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) {
+                const uint32_t t = s_wcnt[ww][d];
+                s_wcnt[ww][d] = run;
+                run += t;
+            }
+            s_lstart[d] = run;          // digit total for now
+            my_total += run;
         }
-        my_total = run;
     }
     const uint32_t ex = block_excl_scan_add_n<NT>(my_total, s_wsum);
-    if (threadIdx.x < R) s_lstart[threadIdx.x] = ex;
+    {
+        uint32_t run = ex;
+#pragma unroll
+        for (uint32_t q = 0; q < DPT; ++q) {
+            const uint32_t d = threadIdx.x * DPT + q;
+            if (d < R) {
+                const uint32_t t = s_lstart[d];
+                s_lstart[d] = run;
+                run += t;
+            }
+        }
+    }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
@@ -823,9 +847,10 @@ __global__ void __launch_bounds__(BLOCK) k_scan_reduce(const uint32_t* __restric
     const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
     uint32_t acc = Op::identity;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
+    for (int k = 0; k < SCAN_ITEMS; ++k) {          // clamped loads: no per-item branch
         const uint32_t j = base + k;
-        if (j < n) acc = Op::apply(acc, in[phys(j, n, rev)]);
+        const uint32_t x = in[phys(min(j, n - 1), n, rev)];
+        acc = Op::apply(acc, j < n ? x : Op::identity);
     }
     acc = block_reduce<Op>(acc, s_wsum);
     if (threadIdx.x == 0) partials[blockIdx.x] = acc;
@@ -874,7 +899,8 @@ __global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; ++k) {
         const uint32_t j = base + k;
-        v[k] = j < n ? in[phys(j, n, rev)] : Op::identity;
+        const uint32_t x = in[phys(min(j, n - 1), n, rev)];
+        v[k] = j < n ? x : Op::identity;
         acc = Op::apply(acc, v[k]);
     }
     uint32_t run = Op::apply(prefix, block_excl_scan<Op>(acc, s_wsum));
