@@ -33,7 +33,15 @@ from orleans_amd import graindispatch as g          # noqa: E402
 from orleans_amd.sharded import DeviceEngine, ShardedRouter  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-SILOS = [(f"10.0.0.{i + 1}", 11111, 1) for i in range(8)]
+# 8 silos 10.0.0.{1..8}:11111.  "literal" = generation 1; its ring gives
+# one silo 35.7% of the directory.  "balanced" (default) = generations found by
+# tools/balanced_silos.py so that every silo owns 1/8 of the hash space -- Orleans
+# generations are arbitrary timestamps (SiloAddress.cs:72-76); routing is unchanged.
+SILO_SETS = {
+    "literal": [(f"10.0.0.{i + 1}", 11111, 1) for i in range(8)],
+    "balanced": [(f"10.0.0.{i + 1}", 11111, g) for i, g in
+                 enumerate([138558, 165678, 215136, 61804, 17808, 48728, 207265, 76820])],
+}
 PING_GRAIN_CLASS = "BenchmarkGrains.Ping.PingGrain"
 
 
@@ -66,6 +74,7 @@ def main():
     ap.add_argument("--msgs", type=int, default=1 << 24, help="messages per GPU per step")
     ap.add_argument("--grains", type=int, default=1 << 20, help="grains per GPU")
     ap.add_argument("--mode", default="D", choices=["D", "R", "V"])
+    ap.add_argument("--silos", default="balanced", choices=sorted(SILO_SETS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=5, help="extra steps with per-kernel events")
@@ -98,7 +107,8 @@ def main():
     # ---- directory: this rank owns the grains whose owner silo lives here -----
     all_keys = grain_keys(tcd, np.arange(G_total, dtype=np.int64))
     e = g.GrainDispatch(device=local, table_capacity=2 * Gr, my_silo=rank % 8, kernel_timing=False)
-    pts, own = e.ring_set_silos(args.mode, SILOS)
+    silos = SILO_SETS[args.silos]
+    pts, own = e.ring_set_silos(args.mode, silos)
     owner = e.ring_owner(all_keys)
     mine = np.nonzero(owner % world == rank)[0]
     n_act = len(mine)
@@ -212,7 +222,9 @@ def main():
             "config": {"workload": "cfg2: 16M msgs uniform over 1M grains, 8 silos, ring D" if world == 1 else
                        f"cfg2 per GPU (16M msgs/GPU over {G_total} grains), directory sharded by ring owner, "
                        f"RCCL all-to-all-v",
-                       "msgs_per_gpu": N, "grains_total": G_total, "ring_mode": args.mode, "silos": 8,
+                       "msgs_per_gpu": N, "grains_total": G_total, "ring_mode": args.mode,
+                       "silos": f"8 x 10.0.0.{{1..8}}:11111, {args.silos} generations",
+                       "owner_share_max": round(float(np.bincount(owner % world, minlength=world).max()) / G_total, 4),
                        "table_load": round(n_act / (2 * Gr), 3), "parallelism": f"shard{world}"},
             "routed_ok_last_step_rank0": st_ok,
             "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
