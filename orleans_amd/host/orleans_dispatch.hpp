@@ -1,0 +1,524 @@
+// orleans_dispatch.hpp -- C++ host layer above the libgraindispatch C ABI that
+// mirrors the reference's interfaces on the dispatch path (same names, argument
+// meaning and error behaviour), so host code and parity tests read like the
+// reference's own.  The reference is C# (rikbosch/orleans); .NET is absent from
+// this image, so this C++ layer stands where the C# batching stage would
+// (INTEGRATION.md shows the C# P/Invoke form of the same calls).
+//
+//   UniqueKey / GrainId / SiloAddress   src/Orleans.Core.Abstractions/IDs/{UniqueKey,GrainId,SiloAddress}.cs
+//   ActivationAddress                   src/Orleans.Core.Abstractions/IDs/ActivationAddress.cs:6-34
+//   AddressAndTag / AddressesAndTag     src/Orleans.Core/GrainDirectory/IGrainDirectory.cs:75-87
+//   GrainDirectoryPartition             src/Orleans.Runtime/GrainDirectory/GrainDirectoryPartition.cs:207-441
+//   LocalGrainDirectory                 src/Orleans.Runtime/GrainDirectory/LocalGrainDirectory.cs:284-850
+//   ConsistentRingProvider              src/Orleans.Runtime/ConsistentRing/ConsistentRingProvider.cs:54-372
+//   VirtualBucketsRingProvider          src/Orleans.Runtime/ConsistentRing/VirtualBucketsRingProvider.cs:122-293
+//   Dispatcher.AddressMessage           src/Orleans.Runtime/Core/Dispatcher.cs:715-767
+//   IncomingMessageAgent.ReceiveMessage src/Orleans.Runtime/Messaging/IncomingMessageAgent.cs:92-190
+//
+// Every per-message decision runs on the GPU through the C ABI; single-grain
+// calls are batches of one.  Errors from the ABI throw OrleansException (the C#
+// side's exception type on this path).
+#pragma once
+
+#include <algorithm>
+#include <array>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "graindispatch.h"
+
+namespace orleans {
+
+class OrleansException : public std::runtime_error {
+public:
+    OrleansException(int code, const std::string& msg) : std::runtime_error(msg), code(code) {}
+    int code;
+};
+
+inline void Check(gd_handle* h, int rc) {
+    if (rc != GD_OK) throw OrleansException(rc, gd_last_error(h));
+}
+
+// ------------------------------------------------------------------ identity
+struct UniqueKey {
+    enum class Category : uint8_t { None = 0, SystemTarget = 1, SystemGrain = 2, Grain = 3, Client = 4,
+                                    KeyExtGrain = 6, GeoClient = 7 };   // UniqueKey.cs:17-26
+    uint64_t N0 = 0, N1 = 0, TypeCodeData = 0;
+    std::optional<std::string> KeyExt;
+
+    Category IdCategory() const { return static_cast<Category>((TypeCodeData >> 56) & 0xFF); }
+    bool HasKeyExt() const { return IdCategory() == Category::KeyExtGrain || IdCategory() == Category::GeoClient; }
+    bool IsLongKey() const { return N0 == 0; }
+
+    // UniqueKey.NewKey(long, category, typeData) (UniqueKey.cs:112-128): typeData is a long,
+    // sign-extended from the int grain type code before the 56-bit mask.
+    static UniqueKey NewKey(int64_t longKey, Category category, int64_t typeData) {
+        UniqueKey k;
+        k.N1 = static_cast<uint64_t>(longKey);
+        k.TypeCodeData = (static_cast<uint64_t>(category) << 56) + (static_cast<uint64_t>(typeData) & 0x00FFFFFFFFFFFFFFull);
+        return k;
+    }
+
+    // UniqueKey.ToByteArray (UniqueKey.cs:295-336)
+    std::vector<uint8_t> ToByteArray() const {
+        std::vector<uint8_t> b(24);
+        std::memcpy(b.data(), &N0, 8);
+        std::memcpy(b.data() + 8, &N1, 8);
+        std::memcpy(b.data() + 16, &TypeCodeData, 8);
+        const int32_t len = KeyExt ? static_cast<int32_t>(KeyExt->size()) : -1;
+        const uint8_t* lp = reinterpret_cast<const uint8_t*>(&len);
+        b.insert(b.end(), lp, lp + 4);
+        if (KeyExt) b.insert(b.end(), KeyExt->begin(), KeyExt->end());
+        return b;
+    }
+
+    // UniqueKey.GetUniformHashCode (UniqueKey.cs:272-293)
+    uint32_t GetUniformHashCode() const {
+        if (HasKeyExt() && KeyExt) {
+            const auto b = ToByteArray();
+            return gd_jenkins_hash_bytes(b.data(), b.size());
+        }
+        const gd_key k{N0, N1, TypeCodeData};
+        return gd_uniform_hash(&k);
+    }
+
+    bool operator==(const UniqueKey& o) const {   // UniqueKey.Equals (:245-251)
+        return N0 == o.N0 && N1 == o.N1 && TypeCodeData == o.TypeCodeData && (!HasKeyExt() || KeyExt == o.KeyExt);
+    }
+    bool operator<(const UniqueKey& o) const {    // UniqueKey.CompareTo order (:255-265)
+        if (TypeCodeData != o.TypeCodeData) return TypeCodeData < o.TypeCodeData;
+        if (N0 != o.N0) return N0 < o.N0;
+        if (N1 != o.N1) return N1 < o.N1;
+        return HasKeyExt() && KeyExt < o.KeyExt;
+    }
+    gd_key ToNative() const { return gd_key{N0, N1, TypeCodeData}; }
+};
+
+struct GrainId {
+    UniqueKey Key;
+    // GrainId.GetGrainId(long typeCode, long primaryKey) (GrainId.cs:72-77)
+    static GrainId GetGrainId(int64_t typeCode, int64_t primaryKey) {
+        return GrainId{UniqueKey::NewKey(primaryKey, UniqueKey::Category::Grain, typeCode)};
+    }
+    bool IsSystemTarget() const { return Key.IdCategory() == UniqueKey::Category::SystemTarget; }
+    uint32_t GetUniformHashCode() const { return Key.GetUniformHashCode(); }
+    bool operator==(const GrainId& o) const { return Key == o.Key; }
+    bool operator<(const GrainId& o) const { return Key < o.Key; }
+};
+
+using ActivationId = UniqueKey;   // ActivationId.cs: a UniqueKey of Category None
+
+struct SiloAddress {
+    std::array<uint8_t, 16> Ip{};   // IPv4 in [12..15]
+    bool IsV4 = true;
+    int32_t Port = 0;
+    int32_t Generation = 0;
+
+    static SiloAddress New(uint8_t a, uint8_t b, uint8_t c, uint8_t d, int32_t port, int32_t gen) {
+        SiloAddress s;
+        s.Ip[12] = a; s.Ip[13] = b; s.Ip[14] = c; s.Ip[15] = d;
+        s.Port = port;
+        s.Generation = gen;
+        return s;
+    }
+    gd_silo_addr ToNative() const {
+        gd_silo_addr n{};
+        std::memcpy(n.ip, Ip.data(), 16);
+        n.port = Port;
+        n.generation = Generation;
+        n.is_v4 = IsV4 ? 1 : 0;
+        return n;
+    }
+    int32_t GetConsistentHashCode() const { const auto n = ToNative(); return gd_silo_consistent_hash(&n); }
+    std::vector<uint32_t> GetUniformHashCodes(int numHashes) const {
+        std::vector<uint32_t> out(numHashes);
+        const auto n = ToNative();
+        if (gd_silo_uniform_hashes(&n, numHashes, out.data()) != GD_OK) throw OrleansException(GD_EINVAL, "hashes");
+        return out;
+    }
+    int CompareTo(const SiloAddress& o) const { const auto a = ToNative(), b = o.ToNative(); return gd_silo_compare(&a, &b); }
+    bool operator==(const SiloAddress& o) const {
+        return Ip == o.Ip && IsV4 == o.IsV4 && Port == o.Port && Generation == o.Generation;
+    }
+    std::string ToString() const {
+        return std::to_string(Ip[12]) + "." + std::to_string(Ip[13]) + "." + std::to_string(Ip[14]) + "." +
+               std::to_string(Ip[15]) + ":" + std::to_string(Port) + "@" + std::to_string(Generation);
+    }
+};
+
+struct ActivationAddress {   // ActivationAddress.cs:6-34
+    SiloAddress Silo;
+    GrainId Grain;
+    ActivationId Activation;
+};
+
+struct AddressAndTag { std::optional<ActivationAddress> Address; int VersionTag = 0; };
+struct AddressesAndTag { std::optional<std::vector<ActivationAddress>> Addresses; int VersionTag = 0; };
+
+// ------------------------------------------------------------------ native handle
+class DispatchHandle {
+public:
+    explicit DispatchHandle(int device = 0, uint64_t tableCapacity = 1u << 20, uint32_t mySilo = 0,
+                            uint32_t seedSilo = GD_NO_SILO) {
+        gd_config cfg{};
+        cfg.struct_size = sizeof(gd_config);
+        cfg.device = device;
+        cfg.table_capacity = tableCapacity;
+        cfg.my_silo = mySilo;
+        cfg.seed_silo = seedSilo;
+        Check(nullptr, gd_create(&cfg, &h_));
+    }
+    ~DispatchHandle() { gd_destroy(h_); }
+    DispatchHandle(const DispatchHandle&) = delete;
+    DispatchHandle& operator=(const DispatchHandle&) = delete;
+    gd_handle* get() const { return h_; }
+
+private:
+    gd_handle* h_ = nullptr;
+};
+
+// Index tables shared by the host-side objects: the GPU stores compact indices.
+class SiloTable {
+public:
+    uint32_t IndexOf(const SiloAddress& s) {
+        for (uint32_t i = 0; i < silos_.size(); ++i)
+            if (silos_[i] == s) return i;
+        silos_.push_back(s);
+        return static_cast<uint32_t>(silos_.size() - 1);
+    }
+    const SiloAddress& At(uint32_t i) const { return silos_.at(i); }
+    size_t Size() const { return silos_.size(); }
+
+private:
+    std::vector<SiloAddress> silos_;
+};
+
+// ------------------------------------------------------------------ rings
+// A ring snapshot built by the reference's AddServer rules and installed on the GPU.
+class RingSnapshot {
+public:
+    RingSnapshot(gd_handle* h, int mode, uint32_t bucketsPerSilo) : h_(h), mode_(mode), buckets_(bucketsPerSilo) {}
+
+    void Rebuild(const std::vector<SiloAddress>& membershipInAddOrder) {
+        members_ = membershipInAddOrder;
+        if (members_.empty()) { n_ = 0; return; }
+        std::vector<gd_silo_addr> nat;
+        for (const auto& s : members_) nat.push_back(s.ToNative());
+        const size_t cap = members_.size() * (mode_ == GD_RING_VIRTUAL_BUCKETS ? buckets_ : 1);
+        points_.assign(cap, 0);
+        owner_.assign(cap, 0);
+        uint32_t n = 0;
+        Check(h_, gd_ring_build(mode_, nat.data(), (uint32_t)nat.size(), buckets_, points_.data(), owner_.data(), &n));
+        points_.resize(n);
+        owner_.resize(n);
+        n_ = n;
+        Check(h_, gd_ring_set(h_, mode_, points_.data(), owner_.data(), n));
+    }
+    const std::vector<SiloAddress>& Members() const { return members_; }
+    const std::vector<uint32_t>& Points() const { return points_; }
+    const std::vector<uint32_t>& Owners() const { return owner_; }
+    uint32_t Size() const { return n_; }
+
+    // batch GetPrimaryTargetSilo(uint key)
+    std::vector<uint32_t> LookupHashes(const std::vector<uint32_t>& keys) const {
+        std::vector<uint32_t> out(keys.size());
+        if (!keys.empty()) Check(h_, gd_ring_lookup_hashes(h_, keys.data(), (uint32_t)keys.size(), out.data()));
+        return out;
+    }
+
+private:
+    gd_handle* h_;
+    int mode_;
+    uint32_t buckets_;
+    std::vector<SiloAddress> members_;
+    std::vector<uint32_t> points_, owner_;
+    uint32_t n_ = 0;
+};
+
+// IConsistentRingProvider, ConsistentRingProvider flavour (mode R, clockwise, one point per silo)
+class ConsistentRingProvider {
+public:
+    ConsistentRingProvider(gd_handle* h, SiloAddress me) : ring_(h, GD_RING_CONSISTENT, 1), me_(std::move(me)) {
+        AddServer(me_);
+    }
+    void AddServer(const SiloAddress& s) {
+        auto m = ring_.Members();
+        if (std::find(m.begin(), m.end(), s) != m.end()) return;
+        m.push_back(s);
+        ring_.Rebuild(m);
+    }
+    void RemoveServer(const SiloAddress& s) {
+        auto m = ring_.Members();
+        m.erase(std::remove(m.begin(), m.end(), s), m.end());
+        ring_.Rebuild(m);
+    }
+    SiloAddress GetPrimaryTargetSilo(uint32_t key) const { return ring_.Members().at(ring_.LookupHashes({key})[0]); }
+    std::vector<uint32_t> GetPrimaryTargetSilos(const std::vector<uint32_t>& keys) const { return ring_.LookupHashes(keys); }
+    // MyRange (ConsistentRingProvider.cs:112-124): (predecessor hash, my hash] as uint; full ring if alone
+    std::pair<uint32_t, uint32_t> GetMyRange() const {
+        const auto& pts = ring_.Points();
+        const auto& own = ring_.Owners();
+        const auto& mem = ring_.Members();
+        if (pts.size() <= 1) return {0u, 0u};
+        for (size_t i = 0; i < pts.size(); ++i)
+            if (mem[own[i]] == me_) return {pts[(i + pts.size() - 1) % pts.size()], pts[i]};
+        throw OrleansException(GD_ESTATE, "not in the ring");
+    }
+    const RingSnapshot& Ring() const { return ring_; }
+
+private:
+    RingSnapshot ring_;
+    SiloAddress me_;
+};
+
+// IConsistentRingProvider default: VirtualBucketsRingProvider (mode V, 30 buckets per silo)
+class VirtualBucketsRingProvider {
+public:
+    VirtualBucketsRingProvider(gd_handle* h, SiloAddress me, uint32_t numBucketsPerSilo = 30)
+        : ring_(h, GD_RING_VIRTUAL_BUCKETS, numBucketsPerSilo), me_(std::move(me)) {
+        AddServer(me_);
+    }
+    void AddServer(const SiloAddress& s) {
+        auto m = ring_.Members();
+        if (std::find(m.begin(), m.end(), s) != m.end()) return;
+        m.push_back(s);
+        ring_.Rebuild(m);
+    }
+    void RemoveServer(const SiloAddress& s) {
+        auto m = ring_.Members();
+        m.erase(std::remove(m.begin(), m.end(), s), m.end());
+        ring_.Rebuild(m);
+    }
+    SiloAddress GetPrimaryTargetSilo(uint32_t key) const { return ring_.Members().at(ring_.LookupHashes({key})[0]); }
+    // CalculateRange (VirtualBucketsRingProvider.cs:176-200): (prev point, point] for each of my buckets
+    std::vector<std::pair<uint32_t, uint32_t>> GetMyRanges() const {
+        std::vector<std::pair<uint32_t, uint32_t>> r;
+        const auto& pts = ring_.Points();
+        const auto& own = ring_.Owners();
+        const auto& mem = ring_.Members();
+        for (size_t i = 0; i < pts.size(); ++i)
+            if (mem[own[i]] == me_) r.emplace_back(pts[(i + pts.size() - 1) % pts.size()], pts[i]);
+        return r;
+    }
+    const RingSnapshot& Ring() const { return ring_; }
+
+private:
+    RingSnapshot ring_;
+    SiloAddress me_;
+};
+
+// ------------------------------------------------------------------ directory
+// GrainDirectoryPartition: single-activation entries in the GPU table.
+class GrainDirectoryPartition {
+public:
+    GrainDirectoryPartition(gd_handle* h, SiloTable& silos) : h_(h), silos_(silos) {}
+
+    // AddSingleActivation (GrainDirectoryPartition.cs:304-326): first registration wins.
+    // VersionTag is a random number in the reference (GrainInfo :121); here 0.
+    AddressAndTag AddSingleActivation(const GrainId& grain, const ActivationId& act, const SiloAddress& silo) {
+        return AddSingleActivations({grain}, {act}, {silo}).at(0);
+    }
+    std::vector<AddressAndTag> AddSingleActivations(const std::vector<GrainId>& grains,
+                                                    const std::vector<ActivationId>& acts,
+                                                    const std::vector<SiloAddress>& silos) {
+        const size_t n = grains.size();
+        std::vector<gd_key> keys(n);
+        std::vector<gd_val> vals(n), out(n);
+        std::vector<uint8_t> ins(n);
+        for (size_t i = 0; i < n; ++i) {
+            keys[i] = grains[i].Key.ToNative();
+            vals[i] = gd_val{ActIndex(acts[i]), silos_.IndexOf(silos[i])};
+        }
+        if (n) Check(h_, gd_dir_register(h_, keys.data(), vals.data(), (uint32_t)n, out.data(), ins.data()));
+        std::vector<AddressAndTag> r(n);
+        for (size_t i = 0; i < n; ++i)
+            r[i].Address = ActivationAddress{silos_.At(out[i].silo), grains[i], acts_.at(out[i].act)};
+        return r;
+    }
+
+    // RemoveActivation (GrainDirectoryPartition.cs:335-363, UnregistrationCause.Force)
+    bool RemoveActivation(const GrainId& grain, const ActivationId& act) {
+        const auto it = act_index_.find(act);
+        if (it == act_index_.end()) return false;
+        const gd_key k = grain.Key.ToNative();
+        const uint32_t a = it->second;
+        uint8_t removed = 0;
+        Check(h_, gd_dir_unregister(h_, &k, &a, 1, &removed));
+        return removed != 0;
+    }
+
+    // LookUpActivations (GrainDirectoryPartition.cs:385-441): null Addresses when absent.
+    AddressesAndTag LookUpActivations(const GrainId& grain) const {
+        const gd_key k = grain.Key.ToNative();
+        gd_val v{};
+        uint8_t found = 0;
+        Check(h_, gd_dir_lookup(h_, &k, 1, &v, &found));
+        AddressesAndTag r;
+        if (found) r.Addresses = std::vector<ActivationAddress>{{silos_.At(v.silo), grain, acts_.at(v.act)}};
+        return r;
+    }
+
+    int Count() const { gd_stats s{}; Check(h_, gd_stats_get(h_, &s)); return (int)s.table_live; }
+    const ActivationId& ActivationAt(uint32_t idx) const { return acts_.at(idx); }
+    uint32_t ActIndex(const ActivationId& a) {
+        const auto it = act_index_.find(a);
+        if (it != act_index_.end()) return it->second;
+        acts_.push_back(a);
+        act_index_.emplace(a, (uint32_t)acts_.size() - 1);
+        return (uint32_t)acts_.size() - 1;
+    }
+    size_t ActivationCount() const { return acts_.size(); }
+
+private:
+    gd_handle* h_;
+    SiloTable& silos_;
+    std::vector<ActivationId> acts_;
+    std::map<ActivationId, uint32_t> act_index_;
+};
+
+// LocalGrainDirectory: directory ring (mode D) + this GPU's partition, whole-node model.
+class LocalGrainDirectory {
+public:
+    // One ring snapshot per handle: give every ring provider its own DispatchHandle.
+    LocalGrainDirectory(gd_handle* h, SiloAddress me)
+        : MyAddress(std::move(me)), h_(h), ring_(h, GD_RING_DIRECTORY, 1), partition_(h, silos_) {
+        silos_.IndexOf(MyAddress);
+        AddServer(MyAddress);
+    }
+
+    // AddServer / RemoveServer (LocalGrainDirectory.cs:284-345): membership in add order.
+    void AddServer(const SiloAddress& s) {
+        auto m = ring_.Members();
+        if (std::find(m.begin(), m.end(), s) != m.end()) return;
+        silos_.IndexOf(s);
+        m.push_back(s);
+        Install(m);
+    }
+    void RemoveServer(const SiloAddress& s) {
+        auto m = ring_.Members();
+        m.erase(std::remove(m.begin(), m.end(), s), m.end());
+        Install(m);
+    }
+
+    // CalculateTargetSilo (LocalGrainDirectory.cs:477-545) for a batch; excludeThisSiloIfStopping is
+    // false (what LocalLookup passes, :801) -- a running silo.
+    std::vector<SiloAddress> CalculateTargetSilos(const std::vector<GrainId>& grains) const {
+        std::vector<gd_key> keys;
+        for (const auto& g : grains) keys.push_back(g.Key.ToNative());
+        std::vector<uint32_t> idx(keys.size());
+        if (!keys.empty()) Check(h_, gd_ring_owner(h_, keys.data(), (uint32_t)keys.size(), idx.data()));
+        std::vector<SiloAddress> r;
+        for (uint32_t i : idx) r.push_back(RingSilo(i));
+        return r;
+    }
+    SiloAddress CalculateTargetSilo(const GrainId& grain) const { return CalculateTargetSilos({grain})[0]; }
+    SiloAddress GetPrimaryForGrain(const GrainId& grain) const { return CalculateTargetSilo(grain); }
+
+    // LocalLookup (LocalGrainDirectory.cs:797-837), whole-node model: the owning partition is
+    // always consulted, so a miss is a false return.
+    bool LocalLookup(const GrainId& grain, AddressesAndTag& result) const {
+        result = partition_.LookUpActivations(grain);
+        return result.Addresses.has_value();
+    }
+    AddressesAndTag GetLocalDirectoryData(const GrainId& grain) const { return partition_.LookUpActivations(grain); }
+
+    GrainDirectoryPartition& DirectoryPartition() { return partition_; }
+    SiloTable& Silos() { return silos_; }
+    gd_handle* Handle() const { return h_; }
+    const RingSnapshot& Ring() const { return ring_; }
+
+    const SiloAddress MyAddress;
+
+private:
+    // the ring stores member positions; translate to the shared silo table
+    void Install(const std::vector<SiloAddress>& m) {
+        ring_.Rebuild(m);
+        // re-install with owners expressed as silo-table indices
+        std::vector<uint32_t> own;
+        for (uint32_t o : ring_.Owners()) own.push_back(silos_.IndexOf(m[o]));
+        std::vector<uint32_t> pts = ring_.Points();
+        Check(h_, gd_ring_set(h_, GD_RING_DIRECTORY, pts.data(), own.data(), (uint32_t)pts.size()));
+    }
+    SiloAddress RingSilo(uint32_t siloIndex) const {
+        if (siloIndex == GD_NO_SILO) throw OrleansException(GD_ESTATE, "no owner");
+        return silos_.At(siloIndex);
+    }
+
+    gd_handle* h_;
+    SiloTable silos_;
+    RingSnapshot ring_;
+    GrainDirectoryPartition partition_;
+};
+
+// ------------------------------------------------------------------ dispatch stages
+struct Message {                       // the header fields the path reads/writes (Message.cs:105-330)
+    GrainId TargetGrain;
+    std::optional<SiloAddress> TargetSilo;
+    std::optional<ActivationId> TargetActivation;
+    uint8_t RouteStatus = 0xFF;        // GD_ROUTE_* after AddressMessages
+};
+
+// Batched Dispatcher.AddressMessage (Dispatcher.cs:715-767): messages whose TargetAddress is
+// complete are skipped (:718); the rest get SetTargetPlacement (Message.cs:629-639) on a hit.
+// Returns the indices that stay on the C# slow path (MISS, system target, membership, KeyExt).
+class Dispatcher {
+public:
+    explicit Dispatcher(LocalGrainDirectory& dir) : dir_(dir) {}
+    std::vector<size_t> AddressMessages(std::vector<Message>& msgs) {
+        std::vector<size_t> todo;
+        std::vector<gd_key> keys;
+        for (size_t i = 0; i < msgs.size(); ++i)
+            if (!(msgs[i].TargetSilo && msgs[i].TargetActivation)) {
+                todo.push_back(i);
+                keys.push_back(msgs[i].TargetGrain.Key.ToNative());
+            }
+        std::vector<uint32_t> silo(keys.size()), act(keys.size());
+        std::vector<uint8_t> st(keys.size());
+        if (!keys.empty())
+            Check(dir_.Handle(), gd_route(dir_.Handle(), keys.data(), (uint32_t)keys.size(), silo.data(), act.data(),
+                                          st.data()));
+        std::vector<size_t> slow;
+        for (size_t j = 0; j < todo.size(); ++j) {
+            Message& m = msgs[todo[j]];
+            m.RouteStatus = st[j];
+            if (st[j] == GD_ROUTE_OK) {
+                m.TargetSilo = dir_.Silos().At(silo[j]);
+                m.TargetActivation = dir_.DirectoryPartition().ActivationAt(act[j]);
+            } else {
+                slow.push_back(todo[j]);
+            }
+        }
+        return slow;
+    }
+
+private:
+    LocalGrainDirectory& dir_;
+};
+
+// Batched IncomingMessageAgent.ReceiveMessage (IncomingMessageAgent.cs:92-190) up to the
+// per-activation FIFO (ActivationData.EnqueueMessage, ActivationData.cs:566-606): returns, for each
+// activation index, the batch positions of its messages in arrival order.
+class IncomingMessageAgent {
+public:
+    explicit IncomingMessageAgent(gd_handle* h) : h_(h) {}
+    std::vector<std::vector<uint32_t>> ReceiveMessages(const std::vector<uint32_t>& targetActivation,
+                                                       uint32_t numActivations) {
+        const uint32_t n = (uint32_t)targetActivation.size();
+        std::vector<uint32_t> perm(n), off(numActivations + 2);
+        Check(h_, gd_bucket(h_, targetActivation.data(), n, numActivations, perm.data(), off.data()));
+        std::vector<std::vector<uint32_t>> q(numActivations + 1);
+        for (uint32_t a = 0; a <= numActivations; ++a) q[a].assign(perm.begin() + off[a], perm.begin() + off[a + 1]);
+        return q;
+    }
+
+private:
+    gd_handle* h_;
+};
+
+}  // namespace orleans

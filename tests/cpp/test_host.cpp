@@ -1,0 +1,341 @@
+// test_host.cpp -- the reference's own tests on this path, restated in C++ against
+// the host layer (orleans_amd/host/orleans_dispatch.hpp) over the C ABI.
+//
+//   ./test_host cpu            identity tests only (no GPU needed)
+//   ./test_host all DUMPFILE   + GPU tests; writes a routing dump that
+//                              tests/test_host_cpp.py compares with the oracle
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <memory>
+#include <algorithm>
+#include <random>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "orleans_dispatch.hpp"
+
+using namespace orleans;
+
+static int g_failures = 0;
+#define EXPECT(cond)                                                               \
+    do {                                                                           \
+        if (!(cond)) {                                                             \
+            std::fprintf(stderr, "  FAILED %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+            ++g_failures;                                                          \
+        }                                                                          \
+    } while (0)
+
+static void Run(const char* name, const std::function<void()>& f) {
+    const int before = g_failures;
+    try {
+        f();
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "  EXCEPTION in %s: %s\n", name, e.what());
+        ++g_failures;
+    }
+    std::printf("%s %s\n", g_failures == before ? "PASS" : "FAIL", name);
+}
+
+static SiloAddress Loopback(int gen) { return SiloAddress::New(127, 0, 0, 1, 0, gen); }  // SiloAddressUtils.NewLocalSiloAddress
+
+// ---------------------------------------------------------------- Identifiertests.cs
+static void ID_HashCorrectness() {        // Identifiertests.cs:278-293
+    std::mt19937_64 r(278);
+    for (int i = 0; i < 1000; ++i) {
+        uint8_t b[24];
+        for (auto& x : b) x = (uint8_t)r();
+        uint64_t u1, u2, u3;
+        std::memcpy(&u1, b, 8);
+        std::memcpy(&u2, b + 8, 8);
+        std::memcpy(&u3, b + 16, 8);
+        EXPECT(gd_jenkins_hash_bytes(b, 24) == gd_jenkins_hash_u64x3(u1, u2, u3));
+    }
+}
+
+static void SiloAddressGetUniformHashCodes() {   // Identifiertests.cs:51-68
+    const SiloAddress s = SiloAddress::New(127, 0, 0, 1, 8080, 26);
+    const auto result = s.GetUniformHashCodes(3);
+    for (int i = 0; i < 3; ++i) {
+        // BinaryTokenStreamWriter: Write(SiloAddress) then Write(int)
+        uint8_t w[28] = {0};
+        w[12] = 127; w[15] = 1;
+        const int32_t port = 8080, gen = 26, extra = i;
+        std::memcpy(w + 16, &port, 4);
+        std::memcpy(w + 20, &gen, 4);
+        std::memcpy(w + 24, &extra, 4);
+        EXPECT(result[i] == gd_jenkins_hash_bytes(w, 28));
+    }
+}
+
+static void UniqueKeyToByteArray() {              // Identifiertests.cs:32-48
+    UniqueKey k;
+    k.N0 = 0x1122334455667788ull;
+    k.N1 = 0x99AABBCCDDEEFF00ull;
+    k.TypeCodeData = (uint64_t)UniqueKey::Category::KeyExtGrain << 56;
+    k.KeyExt = "hello world";
+    const auto b = k.ToByteArray();
+    EXPECT(b.size() == 24 + 4 + 11);
+    int32_t len;
+    std::memcpy(&len, b.data() + 24, 4);
+    EXPECT(len == 11);
+    EXPECT(std::string(b.begin() + 28, b.end()) == "hello world");
+    EXPECT(k.GetUniformHashCode() == gd_jenkins_hash_bytes(b.data(), b.size()));
+    UniqueKey plain = UniqueKey::NewKey(42, UniqueKey::Category::Grain, -7);
+    EXPECT(plain.TypeCodeData == ((3ull << 56) | (0x00FFFFFFFFFFFFFFull & (uint64_t)(int64_t)-7)));
+    EXPECT(plain.GetUniformHashCode() == gd_jenkins_hash_u64x3(plain.TypeCodeData, plain.N0, plain.N1));
+}
+
+static void CalculateIdHashKnownSilos() {
+    // 127.0.0.1:0 generations 1..5 (RingTests_Standalone silos)
+    const int32_t want[5] = {-2064684674, -1337777665, -605710880, -2359351, -1047635457};
+    for (int g = 1; g <= 5; ++g) EXPECT(Loopback(g).GetConsistentHashCode() == want[g - 1]);
+    EXPECT(gd_calculate_id_hash("BenchmarkGrains.Ping.PingGrain") == 1596181187);
+}
+
+// ---------------------------------------------------------------- RingTests_Standalone.cs
+// RangeBreakable (RingTests_Standalone.cs:212-261): every point of the ring is owned exactly once.
+static bool InRange(uint32_t b, uint32_t e, uint32_t n) {   // RingRange.cs:72-81
+    if (b == e) return true;   // full range
+    if (b < e) return n > b && n <= e;
+    return n > b || n <= e;
+}
+static void VerifyRing(const std::vector<std::vector<std::pair<uint32_t, uint32_t>>>& ranges) {
+    std::set<uint32_t> pts = {0u, 1u, 0xFFFFFFFFu, 0x7FFFFFFFu, 0x80000000u};
+    for (const auto& rs : ranges)
+        for (const auto& r : rs)
+            for (int d = -1; d <= 1; ++d) {
+                pts.insert(r.first + d);
+                pts.insert(r.second + d);
+            }
+    std::mt19937 rng(5);
+    for (int i = 0; i < 4000; ++i) pts.insert(rng());
+    for (uint32_t p : pts) {
+        int owners = 0;
+        for (const auto& rs : ranges)
+            for (const auto& r : rs) owners += InRange(r.first, r.second, p);
+        EXPECT(owners == 1);
+        if (owners != 1) return;
+    }
+}
+
+static void RingStandalone(const std::vector<int>& failIdx, const std::vector<int>& joinIdx) {
+    // CreateServers(5) -> Combine -> fail -> join -> VerifyRing (RingTests_Standalone.cs:73-97)
+    std::vector<SiloAddress> all;
+    for (int g = 1; g <= 5; ++g) all.push_back(Loopback(g));
+    std::vector<SiloAddress> byHash = all;
+    std::sort(byHash.begin(), byHash.end(),
+              [](const SiloAddress& a, const SiloAddress& b) { return a.GetConsistentHashCode() < b.GetConsistentHashCode(); });
+    std::vector<SiloAddress> live, joiners;
+    for (int i = 0; i < 5; ++i) {
+        if (std::find(failIdx.begin(), failIdx.end(), i) != failIdx.end()) continue;
+        if (std::find(joinIdx.begin(), joinIdx.end(), i) != joinIdx.end()) joiners.push_back(byHash[i]);
+        else live.push_back(byHash[i]);
+    }
+    std::vector<std::unique_ptr<DispatchHandle>> handles;
+    std::vector<std::unique_ptr<ConsistentRingProvider>> rings;
+    for (const auto& s : live) {
+        handles.emplace_back(new DispatchHandle(0, 1024));
+        rings.emplace_back(new ConsistentRingProvider(handles.back()->get(), s));
+    }
+    for (auto& r : rings)
+        for (const auto& s : all) r->AddServer(s);               // Combine(rings, rings) incl. to-be-failed
+    for (auto& r : rings)
+        for (int i : failIdx) r->RemoveServer(byHash[i]);
+    for (const auto& s : joiners) {
+        handles.emplace_back(new DispatchHandle(0, 1024));
+        rings.emplace_back(new ConsistentRingProvider(handles.back()->get(), s));
+    }
+    for (auto& r : rings)
+        for (const auto& s : live) r->AddServer(s);
+    for (auto& r : rings)
+        for (const auto& s : joiners) r->AddServer(s);
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> ranges;
+    for (auto& r : rings) ranges.push_back({r->GetMyRange()});
+    VerifyRing(ranges);
+    // ConsistentRingProviderTests_Silo.VerifyKey (:254-275): every silo agrees on the owner
+    std::mt19937 rng(254);
+    std::vector<uint32_t> keys;
+    for (int i = 0; i < 2000; ++i) keys.push_back(rng());
+    const auto first = rings[0]->GetPrimaryTargetSilos(keys);
+    for (auto& r : rings) {
+        const auto got = r->GetPrimaryTargetSilos(keys);
+        for (size_t i = 0; i < keys.size(); ++i)
+            EXPECT(r->Ring().Members()[got[i]] == rings[0]->Ring().Members()[first[i]]);
+    }
+}
+
+static void VirtualBucketsRanges() {
+    std::vector<SiloAddress> silos;
+    for (int i = 1; i <= 6; ++i) silos.push_back(SiloAddress::New(10, 0, 0, (uint8_t)i, 11111, 1));
+    std::vector<std::unique_ptr<DispatchHandle>> handles;
+    std::vector<std::unique_ptr<VirtualBucketsRingProvider>> rings;
+    for (const auto& s : silos) {
+        handles.emplace_back(new DispatchHandle(0, 1024));
+        rings.emplace_back(new VirtualBucketsRingProvider(handles.back()->get(), s, 30));
+    }
+    for (auto& r : rings)
+        for (const auto& s : silos) r->AddServer(s);
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> ranges;
+    for (auto& r : rings) ranges.push_back(r->GetMyRanges());
+    VerifyRing(ranges);
+    // the lookup lands in the owner's ranges
+    std::mt19937 rng(9);
+    for (int i = 0; i < 500; ++i) {
+        const uint32_t k = rng();
+        const SiloAddress o = rings[0]->GetPrimaryTargetSilo(k);
+        size_t oi = std::find(silos.begin(), silos.end(), o) - silos.begin();
+        bool in = false;
+        for (const auto& r : ranges[oi]) in |= InRange(r.first, r.second, k);
+        EXPECT(in);
+    }
+}
+
+// ---------------------------------------------------------------- directory partition
+static ActivationId NewActivationId(uint64_t seed) {  // ActivationId.NewId: Category None guid key
+    ActivationId a;
+    a.N0 = seed * 0x9E3779B97F4A7C15ull + 1;
+    a.N1 = ~seed;
+    a.TypeCodeData = 0;
+    return a;
+}
+
+static void DirectorySemantics() {
+    DispatchHandle h(0, 4096, 0);
+    const SiloAddress me = SiloAddress::New(10, 0, 0, 1, 11111, 1);
+    LocalGrainDirectory dir(h.get(), me);
+    for (int i = 2; i <= 8; ++i) dir.AddServer(SiloAddress::New(10, 0, 0, (uint8_t)i, 11111, 1));
+    auto& part = dir.DirectoryPartition();
+    const int tc = gd_calculate_id_hash("BenchmarkGrains.Ping.PingGrain");
+    const GrainId g1 = GrainId::GetGrainId(tc, 1), g2 = GrainId::GetGrainId(tc, 2);
+    const ActivationId a1 = NewActivationId(1), a2 = NewActivationId(2);
+    const SiloAddress s3 = SiloAddress::New(10, 0, 0, 3, 11111, 1);
+    // AddSingleActivation: first registration wins, the second gets the first's address back
+    auto r1 = part.AddSingleActivation(g1, a1, s3);
+    EXPECT(r1.Address && r1.Address->Activation == a1 && r1.Address->Silo == s3);
+    auto r2 = part.AddSingleActivation(g1, a2, me);
+    EXPECT(r2.Address && r2.Address->Activation == a1 && r2.Address->Silo == s3);
+    // LookUpActivations / LocalLookup
+    AddressesAndTag res;
+    EXPECT(dir.LocalLookup(g1, res) && res.Addresses->size() == 1 && (*res.Addresses)[0].Activation == a1);
+    EXPECT(!dir.LocalLookup(g2, res) && !res.Addresses);
+    // RemoveActivation: wrong activation is a no-op, right one removes the grain
+    EXPECT(!part.RemoveActivation(g1, a2));
+    EXPECT(part.RemoveActivation(g1, a1));
+    EXPECT(!dir.GetLocalDirectoryData(g1).Addresses);
+    auto r3 = part.AddSingleActivation(g1, a2, me);
+    EXPECT(r3.Address && r3.Address->Activation == a2);
+    EXPECT(part.Count() == 1);
+    // CalculateTargetSilo equals the silo the ring's owner table gives
+    EXPECT(dir.GetPrimaryForGrain(g1) == dir.CalculateTargetSilo(g1));
+}
+
+static void DispatcherAndAgent() {
+    DispatchHandle h(0, 1 << 14, 0, /*seed*/ 0);
+    const SiloAddress me = SiloAddress::New(10, 0, 0, 1, 11111, 1);
+    LocalGrainDirectory dir(h.get(), me);
+    for (int i = 2; i <= 8; ++i) dir.AddServer(SiloAddress::New(10, 0, 0, (uint8_t)i, 11111, 1));
+    auto& part = dir.DirectoryPartition();
+    const int tc = gd_calculate_id_hash("BenchmarkGrains.Ping.PingGrain");
+    std::vector<GrainId> grains;
+    std::vector<ActivationId> acts;
+    std::vector<SiloAddress> where;
+    for (int k = 0; k < 1000; ++k) {
+        grains.push_back(GrainId::GetGrainId(tc, k));
+        acts.push_back(NewActivationId(1000 + k));
+    }
+    const auto owners = dir.CalculateTargetSilos(grains);
+    part.AddSingleActivations(grains, acts, owners);          // co-located with the directory owner
+    std::vector<Message> msgs;
+    std::mt19937 rng(7);
+    for (int i = 0; i < 5000; ++i) msgs.push_back(Message{GrainId::GetGrainId(tc, rng() % 1100), {}, {}, 0xFF});
+    Message st;                                                 // a system target: stays in C#
+    st.TargetGrain.Key = UniqueKey::NewKey(3, UniqueKey::Category::Grain, 0);
+    st.TargetGrain.Key.TypeCodeData = 1ull << 56;
+    msgs.push_back(st);
+    Message done = msgs[0];                                     // complete address: skipped (Dispatcher.cs:718)
+    done.TargetSilo = me;
+    done.TargetActivation = acts[0];
+    msgs.push_back(done);
+    Dispatcher disp(dir);
+    const auto slow = disp.AddressMessages(msgs);
+    size_t expect_slow = 0;
+    for (size_t i = 0; i + 2 < msgs.size(); ++i) {
+        const int64_t k = (int64_t)msgs[i].TargetGrain.Key.N1;
+        if (k < 1000) {
+            EXPECT(msgs[i].RouteStatus == GD_ROUTE_OK);
+            EXPECT(msgs[i].TargetActivation && *msgs[i].TargetActivation == acts[k]);
+            EXPECT(msgs[i].TargetSilo && *msgs[i].TargetSilo == owners[k]);
+        } else {
+            EXPECT(msgs[i].RouteStatus == GD_ROUTE_MISS && !msgs[i].TargetActivation);
+            ++expect_slow;
+        }
+    }
+    EXPECT(msgs[msgs.size() - 2].RouteStatus == GD_ROUTE_SYSTEM_TARGET);
+    EXPECT(msgs.back().RouteStatus == 0xFF);
+    EXPECT(slow.size() == expect_slow + 1);
+    // IncomingMessageAgent: per-activation FIFO of the routed messages
+    std::vector<uint32_t> target;
+    for (size_t i = 0; i + 2 < msgs.size(); ++i)
+        target.push_back(msgs[i].RouteStatus == GD_ROUTE_OK ? part.ActIndex(*msgs[i].TargetActivation) : GD_NO_ACTIVATION);
+    IncomingMessageAgent agent(h.get());
+    const uint32_t nAct = (uint32_t)part.ActivationCount();
+    const auto q = agent.ReceiveMessages(target, nAct);
+    size_t total = 0;
+    for (uint32_t a = 0; a <= nAct; ++a) {
+        total += q[a].size();
+        for (size_t j = 0; j < q[a].size(); ++j) {
+            EXPECT((a < nAct ? target[q[a][j]] == a : target[q[a][j]] >= nAct));
+            if (j) EXPECT(q[a][j - 1] < q[a][j]);                      // arrival order kept
+        }
+    }
+    EXPECT(total == target.size());
+}
+
+static void RoutingDump(const char* path) {
+    // bench silos, ring D, 20000 grains of the Ping type: owner silo index per grain (oracle-checked)
+    DispatchHandle h(0, 1 << 15, 0);
+    LocalGrainDirectory dir(h.get(), SiloAddress::New(10, 0, 0, 1, 11111, 1));
+    for (int i = 2; i <= 8; ++i) dir.AddServer(SiloAddress::New(10, 0, 0, (uint8_t)i, 11111, 1));
+    const int tc = gd_calculate_id_hash("BenchmarkGrains.Ping.PingGrain");
+    std::vector<GrainId> grains;
+    for (int k = -10000; k < 10000; ++k) grains.push_back(GrainId::GetGrainId(tc, k));
+    const auto owners = dir.CalculateTargetSilos(grains);
+    std::ofstream f(path);
+    for (size_t i = 0; i < grains.size(); ++i)
+        f << (int64_t)grains[i].Key.N1 << " " << (int)owners[i].Ip[15] << "\n";
+}
+
+int main(int argc, char** argv) {
+    const std::string mode = argc > 1 ? argv[1] : "all";
+    Run("ID_HashCorrectness", ID_HashCorrectness);
+    Run("SiloAddressGetUniformHashCodes", SiloAddressGetUniformHashCodes);
+    Run("UniqueKeyToByteArray", UniqueKeyToByteArray);
+    Run("CalculateIdHashKnownSilos", CalculateIdHashKnownSilos);
+    if (mode == "all") {
+        Run("RingStandalone_Basic", [] { RingStandalone({}, {}); });
+        Run("RingStandalone_Failures", [] {
+            for (auto f : std::vector<std::vector<int>>{{0}, {0, 1}, {4}, {4, 3}, {2}, {2, 3}, {1, 3}, {0, 4}})
+                RingStandalone(f, {});
+        });
+        Run("RingStandalone_Joins", [] {
+            for (auto j : std::vector<std::vector<int>>{{0}, {0, 1}, {4}, {4, 3}, {2}, {2, 3}, {1, 3}, {0, 4}})
+                RingStandalone({}, j);
+        });
+        Run("RingStandalone_Mixed", [] {
+            RingStandalone({0}, {1});
+            RingStandalone({1}, {0});
+            RingStandalone({3}, {4});
+            RingStandalone({4}, {3});
+        });
+        Run("VirtualBucketsRanges", VirtualBucketsRanges);
+        Run("DirectorySemantics", DirectorySemantics);
+        Run("DispatcherAndAgent", DispatcherAndAgent);
+        if (argc > 2) Run("RoutingDump", [&] { RoutingDump(argv[2]); });
+    }
+    std::printf("%s (%d failure%s)\n", g_failures ? "FAILED" : "OK", g_failures, g_failures == 1 ? "" : "s");
+    return g_failures ? 1 : 0;
+}
