@@ -213,6 +213,79 @@ int gd_ring_owner_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_
 int gd_pack_by_shard_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_shards,
                             gd_key* d_send_keys, uint32_t* d_send_idx, uint32_t* d_counts);
 
+/* ---- micro-batch latency path (BASELINE config 5) ----------------------
+ * Small batches (e.g. 4k messages: Presence / GPSTracker traffic,
+ * Samples/GPSTracker/GPSTracker.GrainImplementation/DeviceGrain.cs:18-37) pay launch
+ * and copy overheads, not bandwidth.  A micro-batch owns pinned host buffers and
+ * device buffers; the whole step (H2D keys -> route -> bucket -> D2H results) is
+ * captured once per batch size as a hipGraph and replayed.  The caller writes
+ * gd_microbatch_keys(), calls gd_microbatch_run(), and reads the output buffers. */
+typedef struct gd_microbatch gd_microbatch;
+int      gd_microbatch_create(gd_handle* h, uint32_t capacity, uint32_t n_act, gd_microbatch** out);
+void     gd_microbatch_destroy(gd_microbatch* mb);
+gd_key*  gd_microbatch_keys(gd_microbatch* mb);                     /* pinned, capacity entries */
+int      gd_microbatch_outputs(gd_microbatch* mb, uint32_t** silo, uint32_t** act, uint8_t** status,
+                               uint32_t** perm, uint32_t** offsets); /* pinned host results */
+/* Route + bucket the first n keys; synchronous.  use_graph = 0 runs the same
+ * launches eagerly (for comparison); the graph for a given n is captured on first use. */
+int      gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph);
+
+/* ---- batched header decode -------------------------------------------
+ * Replaces, for the fields the dispatch path reads, the per-message
+ * HeadersContainer.Deserializer (src/Orleans.Core/Messaging/Message.cs:1247-1356) run by
+ * IncomingMessageBuffer (src/Orleans.Core/Messaging/IncomingMessageBuffer.cs) over each frame
+ * [int32 headerLength][int32 bodyLength][header][body] (Message.cs:481-516).  The caller hands
+ * over the receive buffer as is plus the byte offset of every frame (the receive loop already
+ * knows them from the two length prefixes). */
+#define GD_FRAME_HAS_TARGET     0x01u /* TargetGrain decoded                                       */
+#define GD_FRAME_COMPLETE       0x02u /* TargetGrain + TargetActivation + TargetSilo bits set:
+                                         TargetAddress.IsComplete -> AddressMessage skips it        */
+#define GD_FRAME_FALLBACK       0x04u /* an object-serialized field precedes a field read here:
+                                         CacheInvalidationHeader / RequestContext -> nothing decoded;
+                                         TargetObserver -> all but TargetSilo decoded. C# decodes it */
+#define GD_FRAME_MALFORMED      0x08u /* lengths run past the header or the buffer: nothing decoded  */
+#define GD_FRAME_TARGET_KEYEXT  0x10u /* TargetGrain carries a KeyExt string (not returned)          */
+
+#define GD_ROUTE_ADDRESSED      5 /* frame address already complete: not looked up (Dispatcher.cs:718) */
+#define GD_ROUTE_UNDECODED      6 /* no TargetGrain decoded (absent / fallback / malformed): C# path    */
+
+/* Output arrays, n entries each.  flags and target_grain are required; any other pointer may
+ * be NULL (field not extracted).  Absent fields read 0 (direction: 0xFF = null).  Silo
+ * addresses are the 24-byte wire form (16-byte IP, int32 port, int32 generation,
+ * BinaryTokenStreamWriter.cs:485-513), 4-byte aligned. */
+typedef struct gd_frame_fields {
+    uint32_t* flags;               /* GD_FRAME_* */
+    gd_key*   target_grain;
+    uint32_t* mask;                /* HeadersContainer.Headers bits (Message.cs:728-765) */
+    gd_key*   target_activation;
+    gd_key*   sending_activation;
+    gd_key*   sending_grain;
+    uint8_t*  target_silo;         /* 24 B per frame */
+    uint8_t*  sending_silo;        /* 24 B per frame */
+    int64_t*  correlation_id;
+    uint8_t*  category;            /* Message.Categories */
+    uint8_t*  direction;           /* Message.Directions, 0xFF = null */
+} gd_frame_fields;
+
+/* Device pointers; enqueue only.  frame_off[i] = byte offset of frame i in buf. */
+int gd_decode_frames_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
+                            uint32_t n, const gd_frame_fields* d_out);
+/* Host pointers (buffer, offsets and outputs); synchronous. */
+int gd_decode_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
+                     const gd_frame_fields* out);
+/* Decode -> route -> (optional) bucket, device pointers, enqueue only.  d_out receives the
+ * decoded fields (flags + target_grain required).  Statuses are gd_route's plus
+ * GD_ROUTE_ADDRESSED / GD_ROUTE_UNDECODED (silo = act = GD_NO_*, trailing bucket).
+ * d_perm / d_offsets NULL = no bucketing. */
+int gd_route_frames_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
+                           uint32_t n, uint32_t n_act, const gd_frame_fields* d_out, uint32_t* d_silo,
+                           uint32_t* d_act, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets);
+/* Host-pointer form of gd_route_frames_device (flags + target keys are returned through out
+ * when it is non-NULL; perm/offsets NULL = no bucketing); synchronous. */
+int gd_route_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
+                    uint32_t n_act, const gd_frame_fields* out, uint32_t* out_silo, uint32_t* out_act,
+                    uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets);
+
 /* ---- per-kernel timing (cfg.flags & GD_CFG_KERNEL_TIMING) ----------------------- */
 /* Up to max entries of {name, launches, total_ms} accumulated since the last reset. */
 typedef struct gd_kernel_time {

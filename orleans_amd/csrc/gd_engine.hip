@@ -12,7 +12,7 @@
 #include <vector>
 
 #include "gd_common.h"
-#include "gd_kernels.h"
+#include "gd_frames.h"
 #include "graindispatch.h"
 
 using namespace gd;
@@ -53,6 +53,7 @@ struct gd_handle {
 
     // scratch
     DevBuf keys_in, u32_a, u32_b, u32_c, u32_d, u8_a, out_a, out_b, out_c, hist, partials, offs;
+    DevBuf fr[16];                    // header-decode scratch (host-pointer entry points)
     uint64_t routed = 0;
 
     // kernel tuning (defaults measured on MI355X; GD_ROUTE_M / GD_ROUTE_NT override for A/B runs)
@@ -457,6 +458,7 @@ void gd_destroy(gd_handle* h) {
     for (DevBuf* b : {&h->ring_pts, &h->ring_own, &h->keys_in, &h->u32_a, &h->u32_b, &h->u32_c, &h->u32_d, &h->u8_a,
                       &h->out_a, &h->out_b, &h->out_c, &h->hist, &h->partials, &h->offs})
         free_buf(*b);
+    for (DevBuf& b : h->fr) free_buf(b);
     if (h->slots) (void)hipFree(h->slots);
     if (h->ctr) (void)hipFree(h->ctr);
     for (auto& t : h->pending) {
@@ -797,6 +799,283 @@ int gd_kernel_times_reset(gd_handle* h) {
     std::fill(h->tms.begin(), h->tms.end(), 0.0);
     std::fill(h->tcount.begin(), h->tcount.end(), 0);
     return GD_OK;
+}
+
+}  // extern "C"
+
+// ================================================================== micro-batch latency path
+struct gd_microbatch {
+    gd_handle* h = nullptr;
+    uint32_t capacity = 0, n_act = 0;
+    // pinned host
+    gd_key* h_keys = nullptr;
+    uint32_t *h_silo = nullptr, *h_act = nullptr, *h_perm = nullptr, *h_off = nullptr;
+    uint8_t* h_status = nullptr;
+    // device
+    gd_key* d_keys = nullptr;
+    uint32_t *d_silo = nullptr, *d_act = nullptr, *d_perm = nullptr, *d_off = nullptr;
+    uint8_t* d_status = nullptr;
+    std::vector<std::pair<uint32_t, hipGraphExec_t>> graphs;
+};
+
+namespace {
+
+int mb_enqueue(gd_microbatch* mb, uint32_t n) {
+    gd_handle* h = mb->h;
+    HIP_TRY(h, hipMemcpyAsync(mb->d_keys, mb->h_keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice, h->stream));
+    if (n) GD_TRY(route_device(h, mb->d_keys, n, mb->d_silo, mb->d_act, mb->d_status));
+    GD_TRY(bucket_device(h, mb->d_act, n, mb->n_act, mb->d_perm, mb->d_off));
+    HIP_TRY(h, hipMemcpyAsync(mb->h_silo, mb->d_silo, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(mb->h_act, mb->d_act, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(mb->h_status, mb->d_status, (size_t)n, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(mb->h_perm, mb->d_perm, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(mb->h_off, mb->d_off, ((size_t)mb->n_act + 2) * 4, hipMemcpyDeviceToHost, h->stream));
+    return GD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void gd_microbatch_destroy(gd_microbatch* mb) {
+    if (!mb) return;
+    if (mb->h) (void)hipStreamSynchronize(mb->h->stream);
+    for (auto& g : mb->graphs) (void)hipGraphExecDestroy(g.second);
+    for (void* p : {(void*)mb->h_keys, (void*)mb->h_silo, (void*)mb->h_act, (void*)mb->h_perm, (void*)mb->h_off,
+                    (void*)mb->h_status})
+        if (p) (void)hipHostFree(p);
+    for (void* p : {(void*)mb->d_keys, (void*)mb->d_silo, (void*)mb->d_act, (void*)mb->d_perm, (void*)mb->d_off,
+                    (void*)mb->d_status})
+        if (p) (void)hipFree(p);
+    delete mb;
+}
+
+int gd_microbatch_create(gd_handle* h, uint32_t capacity, uint32_t n_act, gd_microbatch** out) {
+    if (!h || !out || capacity == 0 || n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "gd_microbatch_create: bad argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    gd_microbatch* mb = new (std::nothrow) gd_microbatch();
+    if (!mb) return set_err(h, GD_ENOMEM, "out of host memory");
+    mb->h = h;
+    mb->capacity = capacity;
+    mb->n_act = n_act;
+    const size_t n = capacity, no = (size_t)n_act + 2;
+    bool ok = hipHostMalloc((void**)&mb->h_keys, n * sizeof(gd_key)) == hipSuccess &&
+              hipHostMalloc((void**)&mb->h_silo, n * 4) == hipSuccess &&
+              hipHostMalloc((void**)&mb->h_act, n * 4) == hipSuccess &&
+              hipHostMalloc((void**)&mb->h_perm, n * 4) == hipSuccess &&
+              hipHostMalloc((void**)&mb->h_off, no * 4) == hipSuccess &&
+              hipHostMalloc((void**)&mb->h_status, n) == hipSuccess &&
+              hipMalloc((void**)&mb->d_keys, n * sizeof(gd_key)) == hipSuccess &&
+              hipMalloc((void**)&mb->d_silo, n * 4) == hipSuccess &&
+              hipMalloc((void**)&mb->d_act, n * 4) == hipSuccess &&
+              hipMalloc((void**)&mb->d_perm, n * 4) == hipSuccess &&
+              hipMalloc((void**)&mb->d_off, no * 4) == hipSuccess &&
+              hipMalloc((void**)&mb->d_status, n) == hipSuccess;
+    if (!ok) {
+        gd_microbatch_destroy(mb);
+        return set_err(h, GD_ENOMEM, "gd_microbatch_create: allocation failed");
+    }
+    std::memset(mb->h_keys, 0, n * sizeof(gd_key));
+    *out = mb;
+    return GD_OK;
+}
+
+gd_key* gd_microbatch_keys(gd_microbatch* mb) { return mb ? mb->h_keys : nullptr; }
+
+int gd_microbatch_outputs(gd_microbatch* mb, uint32_t** silo, uint32_t** act, uint8_t** status, uint32_t** perm,
+                          uint32_t** offsets) {
+    if (!mb) return set_err(nullptr, GD_EINVAL, "null micro-batch");
+    if (silo) *silo = mb->h_silo;
+    if (act) *act = mb->h_act;
+    if (status) *status = mb->h_status;
+    if (perm) *perm = mb->h_perm;
+    if (offsets) *offsets = mb->h_off;
+    return GD_OK;
+}
+
+int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
+    if (!mb) return set_err(nullptr, GD_EINVAL, "null micro-batch");
+    gd_handle* h = mb->h;
+    if (n > mb->capacity) return set_err(h, GD_EINVAL, "n %u above micro-batch capacity %u", n, mb->capacity);
+    GD_TRY(check_ring(h));
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!use_graph) {
+        GD_TRY(mb_enqueue(mb, n));
+        return sync(h);
+    }
+    hipGraphExec_t exec = nullptr;
+    for (auto& g : mb->graphs)
+        if (g.first == n) exec = g.second;
+    if (!exec) {
+        // size every scratch buffer with one eager run, then capture (no allocation inside capture)
+        GD_TRY(mb_enqueue(mb, n));
+        GD_TRY(sync(h));
+        const bool timing = h->timing;
+        h->timing = false;
+        hipGraph_t graph = nullptr;
+        HIP_TRY(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+        const int rc = mb_enqueue(mb, n);
+        const hipError_t ec = hipStreamEndCapture(h->stream, &graph);
+        h->timing = timing;
+        if (rc != GD_OK) return rc;
+        if (ec != hipSuccess) return set_err(h, GD_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
+        const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (ei != hipSuccess) return set_err(h, GD_EHIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
+        mb->graphs.emplace_back(n, exec);
+    }
+    HIP_TRY(h, hipGraphLaunch(exec, h->stream));
+    return sync(h);
+}
+
+}  // extern "C"
+
+// ================================================================== header decode
+namespace {
+
+FrameFields frame_fields(const gd_frame_fields* f) {
+    return FrameFields{f->flags,
+                       (uint64_t*)f->target_grain,
+                       f->mask,
+                       (uint64_t*)f->target_activation,
+                       (uint64_t*)f->sending_activation,
+                       (uint64_t*)f->sending_grain,
+                       (uint32_t*)f->target_silo,
+                       (uint32_t*)f->sending_silo,
+                       f->correlation_id,
+                       f->category,
+                       f->direction};
+}
+
+int check_frames_args(gd_handle* h, const void* buf, const void* off, uint32_t n, const gd_frame_fields* out) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (n == 0) return GD_OK;
+    if (!buf || !off || !out || !out->flags || !out->target_grain) return set_err(h, GD_EINVAL, "null argument");
+    if (((uintptr_t)out->target_silo | (uintptr_t)out->sending_silo) & 3)
+        return set_err(h, GD_EINVAL, "silo outputs must be 4-byte aligned");
+    return GD_OK;
+}
+
+int decode_frames_device(gd_handle* h, const uint8_t* buf, uint64_t len, const uint64_t* off, uint32_t n,
+                         const gd_frame_fields* out) {
+    return launch(h, "k_decode_frames", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_decode_frames, buf, len, off, n,
+                  frame_fields(out));
+}
+
+int route_frames_device(gd_handle* h, const uint8_t* buf, uint64_t len, const uint64_t* off, uint32_t n,
+                        uint32_t n_act, const gd_frame_fields* out, uint32_t* silo, uint32_t* act, uint8_t* status,
+                        uint32_t* perm, uint32_t* offsets) {
+    if (n) {
+        GD_TRY(check_ring(h));
+        GD_TRY(decode_frames_device(h, buf, len, off, n, out));
+        GD_TRY(route_device(h, out->target_grain, n, silo, act, status));
+        GD_TRY(launch(h, "k_frame_status", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_frame_status,
+                      (const uint32_t*)out->flags, n, silo, act, status));
+    }
+    if (perm && offsets) GD_TRY(bucket_device(h, act, n, n_act, perm, offsets));
+    return GD_OK;
+}
+
+// Host-pointer outputs -> device scratch fr[2..12] (fr[0] buffer, fr[1] offsets).
+int frame_scratch(gd_handle* h, uint32_t n, const gd_frame_fields* want, gd_frame_fields* dev) {
+    const size_t sz[11] = {4, 24, 4, 24, 24, 24, 24, 24, 8, 1, 1};
+    void* const* w = (void* const*)want;
+    void** d = (void**)dev;
+    for (int k = 0; k < 11; ++k) {
+        d[k] = nullptr;
+        if (k < 2 || (w && w[k])) {
+            GD_TRY(ensure(h, h->fr[2 + k], sz[k] * n + 8));
+            d[k] = h->fr[2 + k].p;
+        }
+    }
+    return GD_OK;
+}
+
+int frame_results(gd_handle* h, uint32_t n, const gd_frame_fields* want, const gd_frame_fields* dev) {
+    if (!want) return GD_OK;
+    const size_t sz[11] = {4, 24, 4, 24, 24, 24, 24, 24, 8, 1, 1};
+    void* const* w = (void* const*)want;
+    void* const* d = (void* const*)dev;
+    for (int k = 0; k < 11; ++k)
+        if (w[k] && d[k]) HIP_TRY(h, hipMemcpyAsync(w[k], d[k], sz[k] * n, hipMemcpyDeviceToHost, h->stream));
+    return GD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gd_decode_frames_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
+                            uint32_t n, const gd_frame_fields* d_out) {
+    GD_TRY(check_frames_args(h, d_buf, d_frame_off, n, d_out));
+    return n ? decode_frames_device(h, d_buf, buf_len, d_frame_off, n, d_out) : GD_OK;
+}
+
+int gd_decode_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
+                     const gd_frame_fields* out) {
+    GD_TRY(check_frames_args(h, buf, frame_off, n, out));
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->fr[0], buf, (size_t)buf_len));
+    GD_TRY(h2d(h, h->fr[1], frame_off, n));
+    gd_frame_fields dev{};
+    GD_TRY(frame_scratch(h, n, out, &dev));
+    GD_TRY(decode_frames_device(h, (const uint8_t*)h->fr[0].p, buf_len, (const uint64_t*)h->fr[1].p, n, &dev));
+    GD_TRY(frame_results(h, n, out, &dev));
+    return sync(h);
+}
+
+int gd_route_frames_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
+                           uint32_t n, uint32_t n_act, const gd_frame_fields* d_out, uint32_t* d_silo,
+                           uint32_t* d_act, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets) {
+    GD_TRY(check_frames_args(h, d_buf, d_frame_off, n, d_out));
+    if (n && (!d_silo || !d_act || !d_status)) return set_err(h, GD_EINVAL, "null argument");
+    if ((d_perm != nullptr) != (d_offsets != nullptr)) return set_err(h, GD_EINVAL, "perm and offsets go together");
+    if (d_perm && n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    return route_frames_device(h, d_buf, buf_len, d_frame_off, n, n_act, d_out, d_silo, d_act, d_status, d_perm,
+                               d_offsets);
+}
+
+int gd_route_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
+                    uint32_t n_act, const gd_frame_fields* out, uint32_t* out_silo, uint32_t* out_act,
+                    uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (n && (!buf || !frame_off || !out_silo || !out_act || !out_status)) return set_err(h, GD_EINVAL, "null argument");
+    if ((out_perm != nullptr) != (out_offsets != nullptr)) return set_err(h, GD_EINVAL, "perm and offsets go together");
+    if (out_perm && n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    if (out && (((uintptr_t)out->target_silo | (uintptr_t)out->sending_silo) & 3))
+        return set_err(h, GD_EINVAL, "silo outputs must be 4-byte aligned");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (n) {
+        GD_TRY(h2d(h, h->fr[0], buf, (size_t)buf_len));
+        GD_TRY(h2d(h, h->fr[1], frame_off, n));
+    }
+    gd_frame_fields dev{};
+    GD_TRY(frame_scratch(h, n, out, &dev));
+    GD_TRY(ensure(h, h->fr[13], (size_t)n * 4 + 4));     // silo
+    GD_TRY(ensure(h, h->fr[14], (size_t)n * 4 + 4));     // act
+    GD_TRY(ensure(h, h->fr[15], (size_t)n + 8));         // status
+    uint32_t* perm = nullptr;
+    uint32_t* offs = nullptr;
+    if (out_perm) {
+        GD_TRY(ensure(h, h->u8_a, (size_t)n * 4 + 4));
+        GD_TRY(ensure(h, h->offs, ((size_t)n_act + 2) * 4));
+        perm = (uint32_t*)h->u8_a.p;
+        offs = (uint32_t*)h->offs.p;
+    }
+    GD_TRY(route_frames_device(h, (const uint8_t*)h->fr[0].p, buf_len, (const uint64_t*)h->fr[1].p, n, n_act, &dev,
+                               (uint32_t*)h->fr[13].p, (uint32_t*)h->fr[14].p, (uint8_t*)h->fr[15].p, perm, offs));
+    GD_TRY(frame_results(h, n, out, &dev));
+    if (n) {
+        HIP_TRY(h, hipMemcpyAsync(out_silo, h->fr[13].p, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipMemcpyAsync(out_act, h->fr[14].p, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipMemcpyAsync(out_status, h->fr[15].p, (size_t)n, hipMemcpyDeviceToHost, h->stream));
+    }
+    if (out_perm) {
+        if (n) HIP_TRY(h, hipMemcpyAsync(out_perm, perm, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipMemcpyAsync(out_offsets, offs, ((size_t)n_act + 2) * 4, hipMemcpyDeviceToHost, h->stream));
+    }
+    return sync_checked(h);
 }
 
 }  // extern "C"

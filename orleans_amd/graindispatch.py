@@ -20,6 +20,8 @@ LIB_PATH = os.environ.get("GRAINDISPATCH_LIB", os.path.join(_HERE, "libgraindisp
 GD_OK, GD_EINVAL, GD_ENOMEM, GD_EHIP, GD_ERCCL, GD_EFULL, GD_ESTATE, GD_ETIMEOUT = 0, -1, -2, -3, -4, -5, -6, -7
 RING_DIRECTORY, RING_CONSISTENT, RING_VIRTUAL_BUCKETS = 0, 1, 2
 ROUTE_OK, ROUTE_MISS, ROUTE_SYSTEM_TARGET, ROUTE_MEMBERSHIP, ROUTE_KEYEXT = 0, 1, 2, 3, 4
+ROUTE_ADDRESSED, ROUTE_UNDECODED = 5, 6
+FRAME_HAS_TARGET, FRAME_COMPLETE, FRAME_FALLBACK, FRAME_MALFORMED, FRAME_TARGET_KEYEXT = 1, 2, 4, 8, 16
 NO_ACTIVATION = 0xFFFFFFFF
 NO_SILO = 0xFFFFFFFF
 CFG_KERNEL_TIMING = 1
@@ -35,7 +37,9 @@ EXPORTED_SYMBOLS = [
     "gd_dir_unregister", "gd_dir_lookup", "gd_dir_clear", "gd_dir_rehash", "gd_route", "gd_bucket",
     "gd_route_bucket", "gd_route_device", "gd_bucket_device", "gd_route_bucket_device",
     "gd_ring_owner_device", "gd_pack_by_shard_device", "gd_kernel_times", "gd_kernel_times_reset",
-    "gd_set_kernel_timing",
+    "gd_set_kernel_timing", "gd_microbatch_create", "gd_microbatch_destroy", "gd_microbatch_keys",
+    "gd_microbatch_outputs", "gd_microbatch_run", "gd_decode_frames_device", "gd_decode_frames",
+    "gd_route_frames_device", "gd_route_frames",
 ]
 
 
@@ -64,6 +68,20 @@ class gd_stats(C.Structure):
 
 class gd_kernel_time(C.Structure):
     _fields_ = [("name", C.c_char * 48), ("launches", C.c_uint64), ("total_ms", C.c_double)]
+
+
+class gd_frame_fields(C.Structure):
+    _fields_ = [(name, C.c_void_p) for name in
+                ("flags", "target_grain", "mask", "target_activation", "sending_activation", "sending_grain",
+                 "target_silo", "sending_silo", "correlation_id", "category", "direction")]
+
+
+# gd_frame_fields member -> (numpy dtype, trailing shape) of the host arrays
+FRAME_FIELDS = {"flags": (np.uint32, ()), "target_grain": (np.uint64, (3,)), "mask": (np.uint32, ()),
+                "target_activation": (np.uint64, (3,)), "sending_activation": (np.uint64, (3,)),
+                "sending_grain": (np.uint64, (3,)), "target_silo": (np.uint8, (24,)),
+                "sending_silo": (np.uint8, (24,)), "correlation_id": (np.int64, ()),
+                "category": (np.uint8, ()), "direction": (np.uint8, ())}
 
 
 class GrainDispatchError(RuntimeError):
@@ -113,6 +131,15 @@ def _load() -> C.CDLL:
         "gd_kernel_times": (C.c_int, [P, C.POINTER(gd_kernel_time), U32, C.POINTER(U32)]),
         "gd_kernel_times_reset": (C.c_int, [P]),
         "gd_set_kernel_timing": (C.c_int, [P, C.c_int]),
+        "gd_microbatch_create": (C.c_int, [P, U32, U32, C.POINTER(P)]),
+        "gd_microbatch_destroy": (None, [P]),
+        "gd_microbatch_keys": (P, [P]),
+        "gd_microbatch_outputs": (C.c_int, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
+        "gd_microbatch_run": (C.c_int, [P, U32, C.c_int]),
+        "gd_decode_frames_device": (C.c_int, [P, P, U64, P, U32, C.POINTER(gd_frame_fields)]),
+        "gd_decode_frames": (C.c_int, [P, P, U64, P, U32, C.POINTER(gd_frame_fields)]),
+        "gd_route_frames_device": (C.c_int, [P, P, U64, P, U32, U32, C.POINTER(gd_frame_fields), P, P, P, P, P]),
+        "gd_route_frames": (C.c_int, [P, P, U64, P, U32, U32, C.POINTER(gd_frame_fields), P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -344,6 +371,53 @@ class GrainDispatch:
         self._c(lib.gd_pack_by_shard_device(self.h, C.c_void_p(d_keys), n, n_shards, C.c_void_p(d_send_keys),
                                             C.c_void_p(d_send_idx), C.c_void_p(d_counts)))
 
+    # -- header decode -------------------------------------------------
+    @staticmethod
+    def _frame_host(n: int, fields) -> Tuple[dict, gd_frame_fields]:
+        want = set(FRAME_FIELDS) if fields is None else {"flags", "target_grain", *fields}
+        arrs = {k: np.zeros((n,) + FRAME_FIELDS[k][1], dtype=FRAME_FIELDS[k][0]) for k in want}
+        ff = gd_frame_fields(**{k: (_ptr(a) if n else None) for k, a in arrs.items()})
+        return arrs, ff
+
+    def decode_frames(self, buf: bytes, offsets, fields: Optional[Iterable[str]] = None) -> dict:
+        """Decode the frames starting at `offsets` in `buf` (host bytes).  Returns a dict of
+        numpy arrays named like gd_frame_fields (all fields unless `fields` narrows it)."""
+        b = np.frombuffer(buf, dtype=np.uint8) if len(buf) else np.zeros(1, dtype=np.uint8)
+        off = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
+        n = len(off)
+        arrs, ff = self._frame_host(n, fields)
+        self._c(lib.gd_decode_frames(self.h, _ptr(b), len(buf), _ptr(off), n, C.byref(ff)))
+        return arrs
+
+    def route_frames(self, buf: bytes, offsets, n_act: Optional[int] = None, fields: Optional[Iterable[str]] = ()):
+        """Decode -> route (-> bucket when n_act is given).  Returns (decoded fields, status,
+        silo, act[, perm, offsets])."""
+        b = np.frombuffer(buf, dtype=np.uint8) if len(buf) else np.zeros(1, dtype=np.uint8)
+        off = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
+        n = len(off)
+        arrs, ff = self._frame_host(n, fields)
+        silo = np.zeros(n, dtype=np.uint32)
+        act = np.zeros(n, dtype=np.uint32)
+        st = np.zeros(n, dtype=np.uint8)
+        perm = np.zeros(n, dtype=np.uint32) if n_act is not None else None
+        offs = np.zeros(n_act + 2, dtype=np.uint32) if n_act is not None else None
+        self._c(lib.gd_route_frames(self.h, _ptr(b), len(buf), _ptr(off), n, n_act or 0, C.byref(ff), _ptr(silo),
+                                    _ptr(act), _ptr(st), None if perm is None else _ptr(perm),
+                                    None if offs is None else _ptr(offs)))
+        return (arrs, st, silo, act) if n_act is None else (arrs, st, silo, act, perm, offs)
+
+    def decode_frames_device(self, d_buf: int, buf_len: int, d_offsets: int, n: int, d_fields: dict):
+        ff = gd_frame_fields(**{k: C.c_void_p(v) for k, v in d_fields.items()})
+        self._c(lib.gd_decode_frames_device(self.h, C.c_void_p(d_buf), buf_len, C.c_void_p(d_offsets), n,
+                                            C.byref(ff)))
+
+    def route_frames_device(self, d_buf: int, buf_len: int, d_offsets: int, n: int, n_act: int, d_fields: dict,
+                            d_silo: int, d_act: int, d_status: int, d_perm: Optional[int], d_offs: Optional[int]):
+        ff = gd_frame_fields(**{k: C.c_void_p(v) for k, v in d_fields.items()})
+        self._c(lib.gd_route_frames_device(self.h, C.c_void_p(d_buf), buf_len, C.c_void_p(d_offsets), n, n_act,
+                                           C.byref(ff), C.c_void_p(d_silo), C.c_void_p(d_act), C.c_void_p(d_status),
+                                           C.c_void_p(d_perm or 0), C.c_void_p(d_offs or 0)))
+
     # -- per-kernel timing ----------------------------------------------------------
     def kernel_times(self) -> dict:
         arr = (gd_kernel_time * 64)()
@@ -356,3 +430,40 @@ class GrainDispatch:
 
     def kernel_times_reset(self):
         self._c(lib.gd_kernel_times_reset(self.h))
+
+
+class MicroBatch:
+    """gd_microbatch: pinned host buffers + a hipGraph per batch size.
+    `keys`, `silo`, `act`, `status`, `perm`, `offsets` are numpy views of the pinned
+    buffers (no copies)."""
+
+    def __init__(self, dispatch: GrainDispatch, capacity: int, n_act: int):
+        self.gd = dispatch
+        self.capacity, self.n_act = capacity, n_act
+        mb = C.c_void_p()
+        _check(dispatch.h, lib.gd_microbatch_create(dispatch.h, capacity, n_act, C.byref(mb)))
+        self.mb = mb
+        kp = lib.gd_microbatch_keys(mb)
+        self.keys = np.ctypeslib.as_array(C.cast(kp, C.POINTER(C.c_uint64)), shape=(capacity, 3))
+        ptrs = [C.c_void_p() for _ in range(5)]
+        _check(dispatch.h, lib.gd_microbatch_outputs(mb, *[C.byref(x) for x in ptrs]))
+        u32 = lambda p, n: np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint32)), shape=(n,))
+        self.silo = u32(ptrs[0], capacity)
+        self.act = u32(ptrs[1], capacity)
+        self.status = np.ctypeslib.as_array(C.cast(ptrs[2], C.POINTER(C.c_uint8)), shape=(capacity,))
+        self.perm = u32(ptrs[3], capacity)
+        self.offsets = u32(ptrs[4], n_act + 2)
+
+    def run(self, n: int, use_graph: bool = True):
+        _check(self.gd.h, lib.gd_microbatch_run(self.mb, n, 1 if use_graph else 0))
+
+    def close(self):
+        if getattr(self, "mb", None):
+            lib.gd_microbatch_destroy(self.mb)
+            self.mb = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
