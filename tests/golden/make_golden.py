@@ -16,6 +16,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
 import oracle as o  # noqa: E402
+import headers as H  # noqa: E402
 
 SILOS = [o.Silo("10.0.0.1", 11111, 1), o.Silo("10.0.0.2", 11111, 1), o.Silo("127.0.0.1", 0, 1),
          o.Silo("127.0.0.1", 0, 5), o.Silo("127.0.0.1", 8080, 26), o.Silo("192.168.1.200", 30000, 123456789),
@@ -66,6 +67,21 @@ def main():
     acts[::17] = o.M32
     perm, off = o.bucket_stable(acts, 37)
     g["bucket"] = {"acts": acts.tolist(), "n_act": 37, "perm": perm.tolist(), "offsets": off.tolist()}
+    # frames (oracle/headers.py encoder) and their decode, incl. fallback/malformed cases
+    frng = np.random.default_rng(20261016)
+    fkeys = o.grain_keys(tc, frng.integers(0, 48, size=40))
+    fkeys[5] = o.UniqueKey(0, 5, o.type_code_data(o.CAT_KEYEXT_GRAIN, tc)).as_tuple()
+    buf, offs = H.random_frames(40, fkeys, frng, p_fallback=0.1, p_complete=0.15, p_malformed=0.08)
+    dec = H.decode_frames(buf, offs)
+    fst, fsilo, fact = H.route_frames_np(buf, offs, spec, d)[1:]
+    g["frames"] = {"buffer_hex": buf.hex(), "offsets": [int(x) for x in offs],
+                   "flags": dec["flags"].tolist(), "mask": dec["mask"].tolist(),
+                   "target_grain": [[str(int(x)) for x in k] for k in dec["target_grain"]],
+                   "sending_grain": [[str(int(x)) for x in k] for k in dec["sending_grain"]],
+                   "target_silo_hex": [bytes(x).hex() for x in dec["target_silo"]],
+                   "correlation_id": [str(int(x)) for x in dec["correlation_id"]],
+                   "category": dec["category"].tolist(), "direction": dec["direction"].tolist(),
+                   "route_status": fst.tolist(), "route_silo": fsilo.tolist(), "route_act": fact.tolist()}
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(g, f, indent=0)
     print("wrote", os.path.join(HERE, "golden.json"))

@@ -342,3 +342,212 @@ def test_full_size_cfg2_properties(gd):
     np.testing.assert_array_equal(np.diff(off_h), counts)
     assert off_h[0] == 0 and off_h[-1] == N
     e.close()
+
+
+# ----------------------------------------------------------------------------- micro-batch graphs (f3)
+def test_microbatch_graph_matches_eager_and_oracle(gd):
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    G = 50000
+    e = _engine(gd, silos, "D", cap=1 << 17)
+    reg = o.grain_keys(TC, np.arange(G))
+    owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1]))
+    e.register(reg, np.arange(G), owner)
+    d = o.DirectoryArrays(reg, np.arange(G), owner)
+    mb = gd.MicroBatch(e, 4096, G)
+    rng = np.random.default_rng(55)
+    for n in (4096, 4096, 1000, 4096, 1, 0, 1000):
+        keys = o.grain_keys(TC, rng.integers(0, G + 300, size=n))
+        mb.keys[:n] = keys
+        for use_graph in (True, False):
+            mb.run(n, use_graph)
+            want = o.route_batch_np(keys, spec, d)
+            assert np.array_equal(mb.status[:n], want[0]) and np.array_equal(mb.silo[:n], want[1])
+            assert np.array_equal(mb.act[:n], want[2])
+            wp, wo = o.bucket_stable(want[2], G)
+            assert np.array_equal(mb.perm[:n], wp) and np.array_equal(mb.offsets, wo)
+    mb.close()
+    e.close()
+
+
+# ----------------------------------------------------------------------------- header decode (f1)
+import json  # noqa: E402
+import os  # noqa: E402
+import struct  # noqa: E402
+import sys  # noqa: E402
+
+import headers as H  # noqa: E402
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tools"))
+import frames_synth as FS  # noqa: E402
+
+
+def _assert_decoded(got, want, rows=None):
+    for k in want:
+        if k in got:
+            g = got[k] if rows is None else got[k][rows]
+            np.testing.assert_array_equal(g, want[k], err_msg=k)
+
+
+def test_decode_frames_golden(gd):
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden.json")))["frames"]
+    buf = bytes.fromhex(g["buffer_hex"])
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 10)
+    got = e.decode_frames(buf, g["offsets"])
+    assert got["flags"].tolist() == g["flags"] and got["mask"].tolist() == g["mask"]
+    assert [[str(int(x)) for x in k] for k in got["target_grain"]] == g["target_grain"]
+    assert [bytes(x).hex() for x in got["target_silo"]] == g["target_silo_hex"]
+    assert [str(int(x)) for x in got["correlation_id"]] == g["correlation_id"]
+    _assert_decoded(got, H.decode_frames(buf, g["offsets"]))
+    e.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_decode_frames_random_vs_oracle(gd, seed):
+    rng = np.random.default_rng(seed)
+    n = 20000 + seed * 37                                          # not a multiple of 64
+    keys = o.grain_keys(TC, rng.integers(0, 1 << 20, size=n))
+    buf, off = H.random_frames(n, keys, rng, p_fallback=0.03, p_complete=0.08, p_malformed=0.02)
+    if seed == 2:                                                  # shuffled, unaligned frame order
+        off = off[rng.permutation(n)]
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 10)
+    got = e.decode_frames(buf, off)
+    _assert_decoded(got, H.decode_frames(buf, off))
+    e.close()
+
+
+def test_decode_frames_edges(gd):
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 10)
+    k = (7, 8, o.type_code_data(o.CAT_GRAIN, TC))
+    frames = [
+        H.encode_frame({"target_grain": (k, None), "debug_context": "d" * 600}),          # past the LDS window
+        H.encode_frame({"target_grain": (k, "ext" * 70), "category": 1}),                 # long KeyExt
+        H.encode_frame({"sending_grain": ((1, 2, 3), "s" * 300), "target_grain": (k, None),
+                        "target_activation": ((5, 6, 0), None), "target_silo": (bytes(16), 9, 9)}),
+        H.encode_frame({"target_grain": (k, None)}, b"body"),
+        H.encode_frame({"category": 0}),                                                  # no target grain
+        H.encode_frame({"target_observer": b"\x01" * 9, "target_grain": (k, None), "target_silo": (bytes(16), 1, 1)}),
+    ]
+    # every alignment of every frame, back to back
+    for pad in range(4):
+        buf = b"\xee" * pad
+        offs = []
+        for f in frames:
+            offs.append(len(buf))
+            buf += f
+        got = e.decode_frames(buf, offs)
+        _assert_decoded(got, H.decode_frames(buf, offs))
+    # the last frame cut at every length (tail bytes not a whole dword; past-the-end offsets)
+    last = H.encode_frame({"target_grain": (k, "tail"), "correlation_id": 5, "direction": 2}, b"xyz")
+    head = frames[3] + b"\x00"
+    for cut in range(len(last) + 1):
+        buf = head + last[:cut]
+        offs = [0, len(head), len(buf), len(buf) + 1, 1 << 62]
+        got = e.decode_frames(buf, offs)
+        want = H.decode_frames(buf, offs)
+        _assert_decoded(got, want)
+        assert (got["flags"][1] == H.F_HAS_TARGET | H.F_TARGET_KEYEXT) == (cut == len(last))
+    # corrupted lengths
+    bad = bytearray(frames[3])
+    struct.pack_into("<i", bad, 0, -5)
+    bad2 = bytearray(frames[0])
+    struct.pack_into("<i", bad2, 12, -2)                                   # DebugContext length -2
+    buf = bytes(bad) + bytes(bad2)
+    got = e.decode_frames(buf, [0, len(bad)])
+    assert got["flags"].tolist() == [H.F_MALFORMED, H.F_MALFORMED]
+    # empty batch
+    got = e.decode_frames(b"", [])
+    assert got["flags"].shape == (0,)
+    e.close()
+
+
+def _frames_engine(gd, G=5000):
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    e = _engine(gd, silos, "D", cap=1 << 14, my_silo=3, seed_silo=5)
+    reg = o.grain_keys(TC, np.arange(G))
+    owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1]))
+    e.register(reg, np.arange(G), owner)
+    return e, spec, o.DirectoryArrays(reg, np.arange(G), owner)
+
+
+def test_route_frames_vs_oracle(gd):
+    G = 5000
+    e, spec, d = _frames_engine(gd, G)
+    rng = np.random.default_rng(11)
+    n = 12000
+    keys = np.concatenate([o.grain_keys(TC, rng.integers(0, G + 500, size=n - 8)), _special_keys()])
+    buf, off = H.random_frames(n, keys, rng, p_fallback=0.03, p_complete=0.1, p_malformed=0.02)
+    dec, st, silo, act, perm, offs = e.route_frames(buf, off, n_act=G, fields=["mask"])
+    f, wst, wsilo, wact = H.route_frames_np(buf, off, spec, d)
+    wst2, wsilo2, wact2 = o.route_batch_np(f["target_grain"], spec, d, my_silo=3, seed_silo=5)[:3]
+    routed = wst < H.ROUTE_ADDRESSED
+    wst[routed], wsilo[routed], wact[routed] = wst2[routed], wsilo2[routed], wact2[routed]
+    np.testing.assert_array_equal(st, wst)
+    np.testing.assert_array_equal(silo, wsilo)
+    np.testing.assert_array_equal(act, wact)
+    np.testing.assert_array_equal(dec["flags"], f["flags"])
+    np.testing.assert_array_equal(dec["target_grain"], f["target_grain"])
+    np.testing.assert_array_equal(dec["mask"], f["mask"])
+    wp, wo = o.bucket_stable(wact, G)
+    np.testing.assert_array_equal(perm, wp)
+    np.testing.assert_array_equal(offs, wo)
+    assert {int(x) for x in np.unique(st)} >= {0, 1, 2, 3, 4, 5, 6}
+    # without bucketing
+    _, st2, silo2, act2 = e.route_frames(buf, off)
+    np.testing.assert_array_equal(st2, st)
+    np.testing.assert_array_equal(act2, act)
+    e.close()
+
+
+def test_route_frames_device_full_size(gd):
+    """2^22 frames of the cfg2 distribution straight from a device receive buffer: decode ->
+    route -> bucket equals route_bucket on the keys; a sample against the oracle."""
+    import torch
+    G, N = 1 << 20, 1 << 22
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    e = _engine(gd, silos, "D", cap=1 << 22)
+    reg = o.grain_keys(TC, np.arange(G))
+    owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1]))
+    e.register(reg, np.arange(G), owner)
+    rng = np.random.default_rng(0xF1)
+    keys = reg[rng.integers(0, G, size=N)]
+    buf, off, fl = FS.build_frames(keys, rng)
+    dev = torch.device("cuda:0")
+    d_buf = torch.from_numpy(buf).to(dev)
+    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    flags = torch.empty(N, dtype=torch.int32, device=dev)
+    tg = torch.empty((N, 3), dtype=torch.int64, device=dev)
+    corr = torch.empty(N, dtype=torch.int64, device=dev)
+    silo = torch.empty(N, dtype=torch.int32, device=dev)
+    act = torch.empty(N, dtype=torch.int32, device=dev)
+    st = torch.empty(N, dtype=torch.uint8, device=dev)
+    perm = torch.empty(N, dtype=torch.int32, device=dev)
+    offs = torch.empty(G + 2, dtype=torch.int32, device=dev)
+    s = torch.cuda.Stream(device=dev)
+    e.set_stream(s.cuda_stream)
+    e.route_frames_device(d_buf.data_ptr(), len(buf), d_off.data_ptr(), N, G,
+                          {"flags": flags.data_ptr(), "target_grain": tg.data_ptr(),
+                           "correlation_id": corr.data_ptr()},
+                          silo.data_ptr(), act.data_ptr(), st.data_ptr(), perm.data_ptr(), offs.data_ptr())
+    e.synchronize()
+    assert (flags.cpu().numpy() == H.F_HAS_TARGET).all()
+    np.testing.assert_array_equal(tg.cpu().numpy().view(np.uint64), keys)
+    np.testing.assert_array_equal(corr.cpu().numpy(), np.arange(1, N + 1))
+    e.set_stream(None)
+    wst, wsilo, wact, wperm, woff = e.route_bucket(keys, G)
+    np.testing.assert_array_equal(st.cpu().numpy(), wst)
+    np.testing.assert_array_equal(silo.cpu().numpy().view(np.uint32), wsilo)
+    np.testing.assert_array_equal(act.cpu().numpy().view(np.uint32), wact)
+    np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), wperm)
+    np.testing.assert_array_equal(offs.cpu().numpy().view(np.uint32), woff)
+    rows = rng.integers(0, N, size=3000)
+    d = o.DirectoryArrays(reg, np.arange(G), owner)
+    want = o.route_batch_np(keys[rows], spec, d)
+    np.testing.assert_array_equal(wst[rows], want[0])
+    np.testing.assert_array_equal(wact[rows], want[2])
+    sample = H.decode_frames(buf[int(off[rows[0]]):int(off[rows[0]]) + 100 * fl].tobytes(),
+                             np.arange(100, dtype=np.uint64) * np.uint64(fl))
+    np.testing.assert_array_equal(sample["target_grain"], keys[rows[0]:rows[0] + 100])
+    e.close()
