@@ -217,17 +217,23 @@ int gd_pack_by_shard_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint
  * Small batches (e.g. 4k messages: Presence / GPSTracker traffic,
  * Samples/GPSTracker/GPSTracker.GrainImplementation/DeviceGrain.cs:18-37) pay launch
  * and copy overheads, not bandwidth.  A micro-batch owns pinned host buffers and
- * device buffers; the whole step (H2D keys -> route -> bucket -> D2H results) is
- * captured once per batch size as a hipGraph and replayed.  The caller writes
- * gd_microbatch_keys(), calls gd_microbatch_run(), and reads the output buffers. */
+ * device buffers; the whole step (H2D keys -> route -> one-workgroup stable sort by
+ * activation -> one D2H of every result) is captured once per batch size as a hipGraph
+ * and replayed.  Instead of gd_bucket's n_act+2 offsets it returns the runs of the
+ * activations present: run r = activation run_act[r] (n_act for acts >= n_act), its
+ * messages perm[run_start[r] .. run_start[r+1]) in arrival order; run_start[n_runs] = n.
+ * The caller writes gd_microbatch_keys(), calls gd_microbatch_run(), reads the outputs. */
+#define GD_MICROBATCH_MAX 8192u
 typedef struct gd_microbatch gd_microbatch;
 int      gd_microbatch_create(gd_handle* h, uint32_t capacity, uint32_t n_act, gd_microbatch** out);
 void     gd_microbatch_destroy(gd_microbatch* mb);
 gd_key*  gd_microbatch_keys(gd_microbatch* mb);                     /* pinned, capacity entries */
+/* Pinned host results, valid after gd_microbatch_run: silo/act/status/perm[capacity],
+ * n_runs[1], run_start[capacity + 1], run_act[capacity]. */
 int      gd_microbatch_outputs(gd_microbatch* mb, uint32_t** silo, uint32_t** act, uint8_t** status,
-                               uint32_t** perm, uint32_t** offsets); /* pinned host results */
-/* Route + bucket the first n keys; synchronous.  use_graph = 0 runs the same
- * launches eagerly (for comparison); the graph for a given n is captured on first use. */
+                               uint32_t** perm, uint32_t** n_runs, uint32_t** run_start, uint32_t** run_act);
+/* Route + bucket the first n keys (n <= capacity <= GD_MICROBATCH_MAX); synchronous.
+ * use_graph = 0 runs the same launches eagerly; the graph for a given n is captured on first use. */
 int      gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph);
 
 /* ---- batched header decode -------------------------------------------

@@ -43,6 +43,8 @@ struct gd_handle {
     // ring snapshot
     int ring_mode = -1;
     uint32_t ring_n = 0, ring_top = 0;
+    uint64_t layout_gen = 0;          // bumped whenever ring / table pointers or sizes change
+                                      // (captured micro-batch graphs bake them in)
     DevBuf ring_pts, ring_own;
 
     // directory table
@@ -520,6 +522,7 @@ int gd_ring_set(gd_handle* h, int mode, const uint32_t* points, const uint32_t* 
     h->ring_mode = mode;
     h->ring_n = n;
     h->ring_top = top;
+    h->layout_gen++;
     return GD_OK;
 }
 
@@ -669,6 +672,7 @@ int gd_dir_rehash(gd_handle* h, uint64_t new_capacity) {
     HIP_TRY(h, hipFree(h->slots));
     h->slots = ns;
     h->capacity = cap;
+    h->layout_gen++;
     GD_TRY(pull_counters(h));
     if (h->ctr_host.err) return set_err(h, GD_EFULL, "rehash failed (0x%x)", h->ctr_host.err);
     return GD_OK;
@@ -807,29 +811,49 @@ int gd_kernel_times_reset(gd_handle* h) {
 struct gd_microbatch {
     gd_handle* h = nullptr;
     uint32_t capacity = 0, n_act = 0;
-    // pinned host
+    // One output block, same layout on both sides (capacity-sized, so host views never move):
+    //   silo[cap] | act[cap] | perm[cap] | n_runs[1] | run_start[cap + 1] | run_act[cap] | status[cap] (u8)
+    size_t out_bytes = 0;
     gd_key* h_keys = nullptr;
-    uint32_t *h_silo = nullptr, *h_act = nullptr, *h_perm = nullptr, *h_off = nullptr;
-    uint8_t* h_status = nullptr;
-    // device
+    uint8_t* h_out = nullptr;      // pinned
     gd_key* d_keys = nullptr;
-    uint32_t *d_silo = nullptr, *d_act = nullptr, *d_perm = nullptr, *d_off = nullptr;
-    uint8_t* d_status = nullptr;
+    uint8_t* d_out = nullptr;
     std::vector<std::pair<uint32_t, hipGraphExec_t>> graphs;
+    uint64_t graphs_gen = 0;       // handle layout the cached graphs were captured against
+
+    uint32_t* out_u32(uint8_t* base, int k) const {
+        const size_t c = capacity;
+        const size_t at[6] = {0, c, 2 * c, 3 * c, 3 * c + 1, 4 * c + 2};   // silo act perm n_runs run_start run_act
+        return (uint32_t*)base + at[k];
+    }
+    uint8_t* out_status(uint8_t* base) const { return base + (5 * (size_t)capacity + 2) * 4; }
 };
 
 namespace {
 
+// H2D keys -> route -> one-workgroup radix sort + runs -> one D2H of the whole output block.
 int mb_enqueue(gd_microbatch* mb, uint32_t n) {
     gd_handle* h = mb->h;
-    HIP_TRY(h, hipMemcpyAsync(mb->d_keys, mb->h_keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice, h->stream));
-    if (n) GD_TRY(route_device(h, mb->d_keys, n, mb->d_silo, mb->d_act, mb->d_status));
-    GD_TRY(bucket_device(h, mb->d_act, n, mb->n_act, mb->d_perm, mb->d_off));
-    HIP_TRY(h, hipMemcpyAsync(mb->h_silo, mb->d_silo, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(h, hipMemcpyAsync(mb->h_act, mb->d_act, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(h, hipMemcpyAsync(mb->h_status, mb->d_status, (size_t)n, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(h, hipMemcpyAsync(mb->h_perm, mb->d_perm, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(h, hipMemcpyAsync(mb->h_off, mb->d_off, ((size_t)mb->n_act + 2) * 4, hipMemcpyDeviceToHost, h->stream));
+    uint8_t* d = mb->d_out;
+    if (n) {
+        HIP_TRY(h, hipMemcpyAsync(mb->d_keys, mb->h_keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice, h->stream));
+        GD_TRY(route_device(h, mb->d_keys, n, mb->out_u32(d, 0), mb->out_u32(d, 1), mb->out_status(d)));
+    }
+    uint32_t key_bits = 1;
+    while (key_bits < 32 && (mb->n_act >> key_bits) != 0) ++key_bits;
+    const uint32_t passes = (key_bits + 7) / 8;
+    const uint32_t bits = std::max<uint32_t>(4, (key_bits + passes - 1) / passes);
+    const uint32_t* a = mb->out_u32(d, 1);
+    uint32_t *pm = mb->out_u32(d, 2), *ra = mb->out_u32(d, 5), *rs = mb->out_u32(d, 4), *nr = mb->out_u32(d, 3);
+    const dim3 g1(1), b1(MB_THREADS);
+    switch (bits) {
+        case 4: GD_TRY(launch(h, "k_mb_sort_runs", g1, b1, 0, k_mb_sort_runs<4>, a, n, passes, mb->n_act, pm, ra, rs, nr)); break;
+        case 5: GD_TRY(launch(h, "k_mb_sort_runs", g1, b1, 0, k_mb_sort_runs<5>, a, n, passes, mb->n_act, pm, ra, rs, nr)); break;
+        case 6: GD_TRY(launch(h, "k_mb_sort_runs", g1, b1, 0, k_mb_sort_runs<6>, a, n, passes, mb->n_act, pm, ra, rs, nr)); break;
+        case 7: GD_TRY(launch(h, "k_mb_sort_runs", g1, b1, 0, k_mb_sort_runs<7>, a, n, passes, mb->n_act, pm, ra, rs, nr)); break;
+        default: GD_TRY(launch(h, "k_mb_sort_runs", g1, b1, 0, k_mb_sort_runs<8>, a, n, passes, mb->n_act, pm, ra, rs, nr)); break;
+    }
+    HIP_TRY(h, hipMemcpyAsync(mb->h_out, d, mb->out_bytes, hipMemcpyDeviceToHost, h->stream));
     return GD_OK;
 }
 
@@ -841,41 +865,34 @@ void gd_microbatch_destroy(gd_microbatch* mb) {
     if (!mb) return;
     if (mb->h) (void)hipStreamSynchronize(mb->h->stream);
     for (auto& g : mb->graphs) (void)hipGraphExecDestroy(g.second);
-    for (void* p : {(void*)mb->h_keys, (void*)mb->h_silo, (void*)mb->h_act, (void*)mb->h_perm, (void*)mb->h_off,
-                    (void*)mb->h_status})
-        if (p) (void)hipHostFree(p);
-    for (void* p : {(void*)mb->d_keys, (void*)mb->d_silo, (void*)mb->d_act, (void*)mb->d_perm, (void*)mb->d_off,
-                    (void*)mb->d_status})
-        if (p) (void)hipFree(p);
+    if (mb->h_keys) (void)hipHostFree(mb->h_keys);
+    if (mb->h_out) (void)hipHostFree(mb->h_out);
+    if (mb->d_keys) (void)hipFree(mb->d_keys);
+    if (mb->d_out) (void)hipFree(mb->d_out);
     delete mb;
 }
 
 int gd_microbatch_create(gd_handle* h, uint32_t capacity, uint32_t n_act, gd_microbatch** out) {
-    if (!h || !out || capacity == 0 || n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "gd_microbatch_create: bad argument");
+    if (!h || !out || capacity == 0 || n_act == 0xFFFFFFFFu)
+        return set_err(h, GD_EINVAL, "gd_microbatch_create: bad argument");
+    if (capacity > MB_MAX) return set_err(h, GD_EINVAL, "micro-batch capacity %u above %u", capacity, MB_MAX);
     HIP_TRY(h, hipSetDevice(h->device));
     gd_microbatch* mb = new (std::nothrow) gd_microbatch();
     if (!mb) return set_err(h, GD_ENOMEM, "out of host memory");
     mb->h = h;
     mb->capacity = capacity;
     mb->n_act = n_act;
-    const size_t n = capacity, no = (size_t)n_act + 2;
-    bool ok = hipHostMalloc((void**)&mb->h_keys, n * sizeof(gd_key)) == hipSuccess &&
-              hipHostMalloc((void**)&mb->h_silo, n * 4) == hipSuccess &&
-              hipHostMalloc((void**)&mb->h_act, n * 4) == hipSuccess &&
-              hipHostMalloc((void**)&mb->h_perm, n * 4) == hipSuccess &&
-              hipHostMalloc((void**)&mb->h_off, no * 4) == hipSuccess &&
-              hipHostMalloc((void**)&mb->h_status, n) == hipSuccess &&
-              hipMalloc((void**)&mb->d_keys, n * sizeof(gd_key)) == hipSuccess &&
-              hipMalloc((void**)&mb->d_silo, n * 4) == hipSuccess &&
-              hipMalloc((void**)&mb->d_act, n * 4) == hipSuccess &&
-              hipMalloc((void**)&mb->d_perm, n * 4) == hipSuccess &&
-              hipMalloc((void**)&mb->d_off, no * 4) == hipSuccess &&
-              hipMalloc((void**)&mb->d_status, n) == hipSuccess;
+    mb->out_bytes = (5 * (size_t)capacity + 2) * 4 + capacity;
+    const size_t kb = (size_t)capacity * sizeof(gd_key);
+    bool ok = hipHostMalloc((void**)&mb->h_keys, kb) == hipSuccess &&
+              hipHostMalloc((void**)&mb->h_out, mb->out_bytes) == hipSuccess &&
+              hipMalloc((void**)&mb->d_keys, kb) == hipSuccess && hipMalloc((void**)&mb->d_out, mb->out_bytes) == hipSuccess;
     if (!ok) {
         gd_microbatch_destroy(mb);
         return set_err(h, GD_ENOMEM, "gd_microbatch_create: allocation failed");
     }
-    std::memset(mb->h_keys, 0, n * sizeof(gd_key));
+    std::memset(mb->h_keys, 0, kb);
+    std::memset(mb->h_out, 0, mb->out_bytes);
     *out = mb;
     return GD_OK;
 }
@@ -883,13 +900,15 @@ int gd_microbatch_create(gd_handle* h, uint32_t capacity, uint32_t n_act, gd_mic
 gd_key* gd_microbatch_keys(gd_microbatch* mb) { return mb ? mb->h_keys : nullptr; }
 
 int gd_microbatch_outputs(gd_microbatch* mb, uint32_t** silo, uint32_t** act, uint8_t** status, uint32_t** perm,
-                          uint32_t** offsets) {
+                          uint32_t** n_runs, uint32_t** run_start, uint32_t** run_act) {
     if (!mb) return set_err(nullptr, GD_EINVAL, "null micro-batch");
-    if (silo) *silo = mb->h_silo;
-    if (act) *act = mb->h_act;
-    if (status) *status = mb->h_status;
-    if (perm) *perm = mb->h_perm;
-    if (offsets) *offsets = mb->h_off;
+    if (silo) *silo = mb->out_u32(mb->h_out, 0);
+    if (act) *act = mb->out_u32(mb->h_out, 1);
+    if (perm) *perm = mb->out_u32(mb->h_out, 2);
+    if (n_runs) *n_runs = mb->out_u32(mb->h_out, 3);
+    if (run_start) *run_start = mb->out_u32(mb->h_out, 4);
+    if (run_act) *run_act = mb->out_u32(mb->h_out, 5);
+    if (status) *status = mb->out_status(mb->h_out);
     return GD_OK;
 }
 
@@ -903,13 +922,16 @@ int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
         GD_TRY(mb_enqueue(mb, n));
         return sync(h);
     }
+    if (mb->graphs_gen != h->layout_gen) {     // ring or table moved: drop stale graphs
+        for (auto& g : mb->graphs) (void)hipGraphExecDestroy(g.second);
+        mb->graphs.clear();
+        mb->graphs_gen = h->layout_gen;
+    }
     hipGraphExec_t exec = nullptr;
     for (auto& g : mb->graphs)
         if (g.first == n) exec = g.second;
     if (!exec) {
-        // size every scratch buffer with one eager run, then capture (no allocation inside capture)
-        GD_TRY(mb_enqueue(mb, n));
-        GD_TRY(sync(h));
+        // no allocation happens inside mb_enqueue (route needs no scratch), so capture directly
         const bool timing = h->timing;
         h->timing = false;
         hipGraph_t graph = nullptr;
@@ -917,7 +939,10 @@ int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
         const int rc = mb_enqueue(mb, n);
         const hipError_t ec = hipStreamEndCapture(h->stream, &graph);
         h->timing = timing;
-        if (rc != GD_OK) return rc;
+        if (rc != GD_OK) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return rc;
+        }
         if (ec != hipSuccess) return set_err(h, GD_EHIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
         const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
         (void)hipGraphDestroy(graph);

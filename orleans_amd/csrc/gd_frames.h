@@ -8,7 +8,7 @@
 //          :485-513 (SiloAddress).  Oracle: oracle/headers.py decode_frame.
 //
 // One lane per frame.  Each wave first stages a FRAME_WIN-byte window of each of its 64 frames
-// into LDS with coalesced dword loads (one 192-B row per frame, all loads independent), then
+// into LDS (12 independent 16-B loads per lane cover the wave's 64 windows), then
 // every lane walks its own frame's mask-driven layout out of LDS.  Reads past the window (long
 // strings) fall back to byte loads from global memory for that lane only.  HBM-bound byte
 // work: no MFMA.
@@ -152,13 +152,30 @@ __global__ __launch_bounds__(BLOCK) void k_decode_frames(const uint8_t* __restri
 
     // ---- stage: frame f's window = dwords [start_f & ~3, +FRAME_WIN) clamped into the buffer
     const uint64_t dw_end = buf_len & ~3ull;                  // [0, dw_end) readable as dwords
-    if (lane < FRAME_WIN_DW && dw_end >= 4) {
-        const uint32_t lo = (uint32_t)start, hi = (uint32_t)(start >> 32);
-#pragma unroll 8
-        for (int f = 0; f < WAVE; ++f) {
-            const uint64_t s = ((uint64_t)__shfl(hi, f) << 32) | (uint32_t)__shfl(lo, f);
-            const uint64_t a = min((s & ~3ull) + 4ull * lane, dw_end - 4);
-            s_win[w][f][lane] = *(const uint32_t*)(buf + a);
+    // The wave's 64 windows are 64 x 12 chunks of 16 B: chunk q = it * 64 + lane belongs to frame
+    // q / 12.  Every lane issues its 12 loads back to back (one memory round trip per wave);
+    // a chunk that would cross dw_end is clamped to the last whole 16 B below it (its bytes are
+    // then wrong, but lim keeps the walk from using bytes at or past dw_end).
+    constexpr int CHUNKS = FRAME_WIN / 16;
+    __shared__ unsigned long long s_start[BLOCK / WAVE][WAVE];
+    s_start[w][lane] = start;
+    __syncthreads();
+    if (dw_end >= 16) {
+        uint4 v[CHUNKS];
+#pragma unroll
+        for (int it = 0; it < CHUNKS; ++it) {
+            const uint32_t q = it * WAVE + lane, f = q / CHUNKS, c = q % CHUNKS;
+            const uint64_t a = (s_start[w][f] & ~3ull) + 16ull * c;
+            v[it] = *(const uint4*)(buf + (a <= dw_end - 16 ? a : ((dw_end - 16) & ~3ull)));
+        }
+#pragma unroll
+        for (int it = 0; it < CHUNKS; ++it) {
+            const uint32_t q = it * WAVE + lane, f = q / CHUNKS, c = q % CHUNKS;
+            uint32_t* r = &s_win[w][f][4 * c];
+            r[0] = v[it].x;
+            r[1] = v[it].y;
+            r[2] = v[it].z;
+            r[3] = v[it].w;
         }
     }
     __syncthreads();
@@ -171,7 +188,12 @@ __global__ __launch_bounds__(BLOCK) void k_decode_frames(const uint8_t* __restri
     uint32_t ts[6] = {0, 0, 0, 0, 0, 0}, ss[6] = {0, 0, 0, 0, 0, 0};
 
     const uint64_t a0 = start & ~3ull;
-    const uint64_t win_end = min(a0 + FRAME_WIN, dw_end);
+    // staged bytes = the whole 16-B chunks of the window that lie below dw_end
+    uint64_t win_end = a0;
+    if (dw_end >= 16 && dw_end > a0) {
+        const uint64_t full = (dw_end - a0) / 16;
+        win_end = a0 + 16 * (full < (uint64_t)CHUNKS ? full : (uint64_t)CHUNKS);
+    }
     HeaderWalk hw;
     hw.c.row = s_win[w][lane];
     hw.c.g = buf + start;

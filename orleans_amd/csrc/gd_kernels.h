@@ -913,4 +913,134 @@ __global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_
     }
 }
 
+// ------------------------------------------------------------------ micro-batch bucketing (f3)
+// One workgroup sorts the whole micro-batch: LSD radix passes of BITS-bit digits of
+// min(act, n_act), each pass ranking stably inside the block (the same wave-ballot ranking as
+// k_radix_scatter, item (w, r, lane) <-> position (w * IT + r) * 64 + lane) and exchanging the
+// (key, index) pairs through LDS.  Then the runs of equal keys are compacted with ballots.
+// For micro-batches this replaces the multi-launch radix pipeline and the O(n_act) offsets:
+// the host gets perm[n] and, per activation present, run_act[r] / run_start[r]
+// (run_start[n_runs] = n), each run in arrival order (ActivationData.cs:566-606).
+constexpr int MB_THREADS = 1024;
+constexpr int MB_IT = 8;
+constexpr uint32_t MB_MAX = MB_THREADS * MB_IT;   // 8192 messages
+
+template <int BITS>
+__global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32_t* __restrict__ act, uint32_t n,
+                                                              uint32_t passes, uint32_t n_act,
+                                                              uint32_t* __restrict__ perm,
+                                                              uint32_t* __restrict__ run_act,
+                                                              uint32_t* __restrict__ run_start,
+                                                              uint32_t* __restrict__ n_runs) {
+    constexpr uint32_t R = 1u << BITS;
+    constexpr int NW = MB_THREADS / WAVE;
+    __shared__ uint32_t s_wcnt[NW][R];
+    __shared__ uint32_t s_lstart[R];
+    __shared__ uint2 s_kv[MB_MAX];
+    __shared__ uint32_t s_wsum[NW];
+    const uint32_t lane = lane_id(), w = threadIdx.x / WAVE;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    uint32_t kk[MB_IT], vv[MB_IT];
+#pragma unroll
+    for (int r = 0; r < MB_IT; ++r) {
+        const uint32_t idx = (w * MB_IT + r) * WAVE + lane;
+        const uint32_t a = act[idx < n ? idx : (n ? n - 1 : 0)];
+        kk[r] = a < n_act ? a : n_act;
+        vv[r] = idx;
+    }
+    for (uint32_t pass = 0; pass < passes; ++pass) {
+        const uint32_t shift = pass * BITS;
+        for (uint32_t d = threadIdx.x; d < R; d += MB_THREADS)
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) s_wcnt[ww][d] = 0;
+        __syncthreads();
+        uint32_t rk[MB_IT];
+#pragma unroll
+        for (int r = 0; r < MB_IT; ++r) {
+            const bool valid = (w * MB_IT + r) * WAVE + lane < n;
+            const uint32_t d = (kk[r] >> shift) & (R - 1);
+            const unsigned long long peers = match_digit<BITS>(d, valid);
+            uint32_t c = 0;
+            if (valid) c = s_wcnt[w][d];
+            rk[r] = c + (uint32_t)__popcll(peers & lt);
+            if (valid && (peers & lt) == 0) s_wcnt[w][d] = c + (uint32_t)__popcll(peers);
+        }
+        __syncthreads();
+        uint32_t total = 0;
+        if (threadIdx.x < R) {
+            uint32_t run = 0;
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) {
+                const uint32_t t = s_wcnt[ww][threadIdx.x];
+                s_wcnt[ww][threadIdx.x] = run;
+                run += t;
+            }
+            total = run;
+        }
+        const uint32_t ex = block_excl_scan_add_n<MB_THREADS>(total, s_wsum);
+        if (threadIdx.x < R) s_lstart[threadIdx.x] = ex;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < MB_IT; ++r) {
+            if ((w * MB_IT + r) * WAVE + lane < n) {
+                const uint32_t d = (kk[r] >> shift) & (R - 1);
+                s_kv[s_lstart[d] + s_wcnt[w][d] + rk[r]] = make_uint2(kk[r], vv[r]);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < MB_IT; ++r) {
+            const uint32_t p = (w * MB_IT + r) * WAVE + lane;
+            if (p < n) {
+                const uint2 kv = s_kv[p];
+                kk[r] = kv.x;
+                vv[r] = kv.y;
+            }
+        }
+        __syncthreads();
+    }
+    // runs: a head where the key changes; wave w owns positions [w * IT * 64, (w + 1) * IT * 64)
+    // in (r, lane) order, so heads are counted per wave, scanned across waves, ranked in-wave.
+    uint32_t prev[MB_IT];
+#pragma unroll
+    for (int r = 0; r < MB_IT; ++r) {
+        const uint32_t p = (w * MB_IT + r) * WAVE + lane;
+        // key of position p - 1: lane - 1 of the same row, lane 63 of the previous row, or the
+        // previous wave's last item (read through LDS, which still holds the sorted pairs)
+        const uint32_t up = __shfl_up(kk[r], 1, WAVE);
+        uint32_t pk = up;
+        if (lane == 0) pk = p > 0 ? s_kv[p - 1].x : ~0u;
+        prev[r] = pk;
+    }
+    uint32_t heads_w = 0;
+    unsigned long long hb[MB_IT];
+#pragma unroll
+    for (int r = 0; r < MB_IT; ++r) {
+        const uint32_t p = (w * MB_IT + r) * WAVE + lane;
+        hb[r] = __ballot(p < n && (p == 0 || prev[r] != kk[r]));
+        heads_w += (uint32_t)__popcll(hb[r]);
+    }
+    const uint32_t wbase = block_excl_scan_add_n<MB_THREADS>(lane == 0 ? heads_w : 0u, s_wsum);
+    const uint32_t base = __shfl(wbase, 0, WAVE);
+    uint32_t before = base;
+#pragma unroll
+    for (int r = 0; r < MB_IT; ++r) {
+        const uint32_t p = (w * MB_IT + r) * WAVE + lane;
+        if (p < n) {
+            perm[p] = vv[r];
+            if ((hb[r] >> lane) & 1ull) {
+                const uint32_t q = before + (uint32_t)__popcll(hb[r] & lt);
+                run_act[q] = kk[r];
+                run_start[q] = p;
+            }
+        }
+        before += (uint32_t)__popcll(hb[r]);
+    }
+    if (threadIdx.x == MB_THREADS - 1) {
+        const uint32_t tot = base + heads_w;   // last wave's base + its heads = all runs
+        n_runs[0] = tot;
+        run_start[tot] = n;
+    }
+}
+
 }  // namespace gd

@@ -93,6 +93,15 @@ class GrainDispatchError(RuntimeError):
 def _load() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libgraindispatch.so not built at {LIB_PATH}; run __graft_entry__.build()")
+    # One HIP runtime per process.  torch ships its own libamdhip64 / libhsa-runtime64 with the
+    # same sonames as /opt/rocm's but is linked against the unversioned names: if this library
+    # loaded /opt/rocm's copies first, a later `import torch` would load its copies beside them
+    # and whichever HSA runtime initialises second finds no device.  With torch imported first,
+    # our NEEDED libamdhip64.so.7 resolves to the copy torch already holds.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     P, U32, U64, I32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
     sig = {
@@ -134,7 +143,7 @@ def _load() -> C.CDLL:
         "gd_microbatch_create": (C.c_int, [P, U32, U32, C.POINTER(P)]),
         "gd_microbatch_destroy": (None, [P]),
         "gd_microbatch_keys": (P, [P]),
-        "gd_microbatch_outputs": (C.c_int, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
+        "gd_microbatch_outputs": (C.c_int, [P] + [C.POINTER(P)] * 7),
         "gd_microbatch_run": (C.c_int, [P, U32, C.c_int]),
         "gd_decode_frames_device": (C.c_int, [P, P, U64, P, U32, C.POINTER(gd_frame_fields)]),
         "gd_decode_frames": (C.c_int, [P, P, U64, P, U32, C.POINTER(gd_frame_fields)]),
@@ -434,8 +443,8 @@ class GrainDispatch:
 
 class MicroBatch:
     """gd_microbatch: pinned host buffers + a hipGraph per batch size.
-    `keys`, `silo`, `act`, `status`, `perm`, `offsets` are numpy views of the pinned
-    buffers (no copies)."""
+    `keys`, `silo`, `act`, `status`, `perm`, `run_start`, `run_act` are numpy views of the
+    pinned buffers (no copies); `n_runs` reads the run count of the last run()."""
 
     def __init__(self, dispatch: GrainDispatch, capacity: int, n_act: int):
         self.gd = dispatch
@@ -445,14 +454,31 @@ class MicroBatch:
         self.mb = mb
         kp = lib.gd_microbatch_keys(mb)
         self.keys = np.ctypeslib.as_array(C.cast(kp, C.POINTER(C.c_uint64)), shape=(capacity, 3))
-        ptrs = [C.c_void_p() for _ in range(5)]
+        ptrs = [C.c_void_p() for _ in range(7)]
         _check(dispatch.h, lib.gd_microbatch_outputs(mb, *[C.byref(x) for x in ptrs]))
         u32 = lambda p, n: np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint32)), shape=(n,))
         self.silo = u32(ptrs[0], capacity)
         self.act = u32(ptrs[1], capacity)
         self.status = np.ctypeslib.as_array(C.cast(ptrs[2], C.POINTER(C.c_uint8)), shape=(capacity,))
         self.perm = u32(ptrs[3], capacity)
-        self.offsets = u32(ptrs[4], n_act + 2)
+        self._n_runs = u32(ptrs[4], 1)
+        self.run_start = u32(ptrs[5], capacity + 1)
+        self.run_act = u32(ptrs[6], capacity)
+
+    @property
+    def n_runs(self) -> int:
+        return int(self._n_runs[0])
+
+    def offsets(self) -> np.ndarray:
+        """The runs expanded to gd_bucket's offsets[n_act + 2] (for comparison with it)."""
+        r = self.n_runs
+        out = np.empty(self.n_act + 2, dtype=np.uint32)
+        # offsets[a] = start of the first run with activation >= a; empty buckets share it
+        starts = np.append(self.run_start[:r], self.run_start[r])
+        acts = np.append(self.run_act[:r].astype(np.int64), self.n_act + 1)
+        idx = np.searchsorted(acts, np.arange(self.n_act + 2), side="left")
+        out[:] = starts[idx]
+        return out
 
     def run(self, n: int, use_graph: bool = True):
         _check(self.gd.h, lib.gd_microbatch_run(self.mb, n, 1 if use_graph else 0))

@@ -345,6 +345,19 @@ def test_full_size_cfg2_properties(gd):
 
 
 # ----------------------------------------------------------------------------- micro-batch graphs (f3)
+def _check_runs(mb, n, want_act, n_act):
+    wp, wo = o.bucket_stable(want_act, n_act)
+    assert np.array_equal(mb.perm[:n], wp)
+    assert np.array_equal(mb.offsets(), wo)
+    r = mb.n_runs
+    clamped = np.minimum(want_act.astype(np.int64), n_act)
+    ua, first = np.unique(clamped, return_index=True) if n else (np.zeros(0, np.int64), np.zeros(0, np.int64))
+    assert r == len(ua)
+    assert np.array_equal(mb.run_act[:r], ua)
+    assert mb.run_start[r] == n
+    assert np.array_equal(np.diff(mb.run_start[:r + 1]), np.bincount(clamped, minlength=n_act + 1)[ua])
+
+
 def test_microbatch_graph_matches_eager_and_oracle(gd):
     silos = o.bench_silos(8)
     spec = o.ring_spec(silos, "D")
@@ -356,16 +369,65 @@ def test_microbatch_graph_matches_eager_and_oracle(gd):
     d = o.DirectoryArrays(reg, np.arange(G), owner)
     mb = gd.MicroBatch(e, 4096, G)
     rng = np.random.default_rng(55)
-    for n in (4096, 4096, 1000, 4096, 1, 0, 1000):
-        keys = o.grain_keys(TC, rng.integers(0, G + 300, size=n))
+    for n in (4096, 4096, 1000, 4096, 1, 0, 1000, 2):
+        hot = rng.integers(0, 64, size=n)                           # skewed: many messages per activation
+        keys = o.grain_keys(TC, np.where(rng.random(n) < 0.5, hot, rng.integers(0, G + 300, size=n)))
         mb.keys[:n] = keys
         for use_graph in (True, False):
             mb.run(n, use_graph)
             want = o.route_batch_np(keys, spec, d)
             assert np.array_equal(mb.status[:n], want[0]) and np.array_equal(mb.silo[:n], want[1])
             assert np.array_equal(mb.act[:n], want[2])
-            wp, wo = o.bucket_stable(want[2], G)
-            assert np.array_equal(mb.perm[:n], wp) and np.array_equal(mb.offsets, wo)
+            _check_runs(mb, n, want[2], G)
+    mb.close()
+    e.close()
+
+
+def test_microbatch_graph_recaptured_after_ring_and_table_change(gd):
+    """Cached graphs bake in the ring snapshot and table pointers; a ring swap or a rehash
+    must not replay a stale graph."""
+    silos = o.bench_silos(8)
+    G = 3000
+    e = _engine(gd, silos, "D", cap=1 << 12)
+    reg = o.grain_keys(TC, np.arange(G))
+    spec = o.ring_spec(silos, "D")
+    owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1]))
+    e.register(reg, np.arange(G), owner)
+    mb = gd.MicroBatch(e, 2048, 4 * G)
+    rng = np.random.default_rng(9)
+    keys = o.grain_keys(TC, rng.integers(0, 4 * G, size=2048))
+    mb.keys[:] = keys
+    mb.run(2048, True)
+    # ring change: 3 silos only
+    spec3 = o.ring_spec(silos[:3], "D")
+    e.ring_set_silos("D", _silo_tuples(silos[:3]))
+    # table growth: register 9000 more grains (forces a rehash of the 4096-slot table)
+    reg2 = o.grain_keys(TC, np.arange(G, 4 * G))
+    own2 = o.ring_owner_np(spec3, o.jenkins_u64x3_np(reg2[:, 2], reg2[:, 0], reg2[:, 1]))
+    e.register(reg2, np.arange(G, 4 * G), own2)
+    assert e.stats()["table_capacity"] > (1 << 12)
+    mb.run(2048, True)
+    d = o.DirectoryArrays(np.concatenate([reg, reg2]), np.arange(4 * G), np.concatenate([owner, own2]))
+    want = o.route_batch_np(keys, spec3, d)
+    assert np.array_equal(mb.status[:2048], want[0]) and np.array_equal(mb.silo[:2048], want[1])
+    assert np.array_equal(mb.act[:2048], want[2])
+    _check_runs(mb, 2048, want[2], 4 * G)
+    mb.close()
+    e.close()
+
+
+def test_microbatch_limits(gd):
+    e = _engine(gd, o.bench_silos(2), "D")
+    with pytest.raises(gd.GrainDispatchError):
+        gd.MicroBatch(e, 8193, 10)
+    mb = gd.MicroBatch(e, 8192, 10)
+    keys = o.grain_keys(TC, np.arange(8192))
+    mb.keys[:] = keys
+    mb.run(8192, True)
+    assert mb.n_runs == 1 and mb.run_act[0] == 10 and mb.run_start[1] == 8192    # all misses: trailing bucket
+    assert np.array_equal(mb.perm, np.arange(8192))
+    with pytest.raises(gd.GrainDispatchError):
+        mb.run(8193, True)
     mb.close()
     e.close()
 
