@@ -671,7 +671,7 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
                                                       uint32_t clamp, uint32_t shift, uint32_t tiles,
                                                       const uint32_t* __restrict__ gscan,
                                                       uint32_t* __restrict__ keys_out,
-                                                      uint32_t* __restrict__ vals_out) {
+                                                      uint32_t* __restrict__ vals_out, uint32_t rank_atomic) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = NT / WAVE;
     constexpr uint32_t TILE = NT * IT;
@@ -709,16 +709,50 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
         if constexpr (FIRST) vv[r] = idx;
     }
     __syncthreads();
+    if (rank_atomic) {
+        // One ds_add_rtn per item: lanes of one wave instruction that hit the same counter are
+        // served in ascending lane order (checked on gfx950 by tools/ubench_lds_order.hip), and a
+        // wave's LDS instructions complete in program order, so the returned count is the stable
+        // rank in (row, lane) = index order.
+        // The lanes sharing the first valid lane's digit (the hot key under skew) take one
+        // counter update by that lane and rank among themselves by ballot; the others use
+        // their own ds_add_rtn.  Different digits are different counters, so the two groups
+        // do not interact.
+        // Issue every row's counter update first (one ds_add_rtn per row: the lead adds the
+        // hot group's size, the other non-hot lanes add 1, hot non-lead lanes stay idle), then
+        // resolve the hot lanes' ranks: no per-row wait for an LDS result.
+        unsigned long long hot[IT];
+        uint32_t lead[IT], hd[IT];
 #pragma unroll
-    for (int r = 0; r < IT; ++r) {
-        const uint32_t idx = base + (w * IT + r) * WAVE + lane;
-        const bool valid = idx < n;
-        const uint32_t d = (kk[r] >> shift) & (R - 1);
-        const unsigned long long peers = match_digit<BITS>(d, valid);
-        uint32_t c = 0;
-        if (valid) c = s_wcnt[w][d];
-        rk[r] = c + (uint32_t)__popcll(peers & lt);
-        if (valid && (peers & lt) == 0) s_wcnt[w][d] = c + (uint32_t)__popcll(peers);
+        for (int r = 0; r < IT; ++r) {
+            const uint32_t idx = base + (w * IT + r) * WAVE + lane;
+            const bool valid = idx < n;
+            const uint32_t d = (kk[r] >> shift) & (R - 1);
+            const unsigned long long live = __ballot(valid);
+            lead[r] = live ? (uint32_t)__ffsll((long long)live) - 1 : 0u;
+            hd[r] = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead[r]);
+            hot[r] = __ballot(valid && d == hd[r]);
+            rk[r] = 0;
+            if (valid && (d != hd[r] || lane == lead[r]))
+                rk[r] = atomicAdd(&s_wcnt[w][d], lane == lead[r] ? (uint32_t)__popcll(hot[r]) : 1u);
+        }
+#pragma unroll
+        for (int r = 0; r < IT; ++r) {
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)rk[r], (int)lead[r]);
+            if ((hot[r] >> lane) & 1ull) rk[r] = b0 + (uint32_t)__popcll(hot[r] & lt);
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < IT; ++r) {
+            const uint32_t idx = base + (w * IT + r) * WAVE + lane;
+            const bool valid = idx < n;
+            const uint32_t d = (kk[r] >> shift) & (R - 1);
+            const unsigned long long peers = match_digit<BITS>(d, valid);
+            uint32_t c = 0;
+            if (valid) c = s_wcnt[w][d];
+            rk[r] = c + (uint32_t)__popcll(peers & lt);
+            if (valid && (peers & lt) == 0) s_wcnt[w][d] = c + (uint32_t)__popcll(peers);
+        }
     }
     __syncthreads();
     // cross-wave exclusive prefix per digit, then tile-local digit starts
