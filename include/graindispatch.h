@@ -292,6 +292,24 @@ int gd_route_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const ui
                     uint32_t n_act, const gd_frame_fields* out, uint32_t* out_silo, uint32_t* out_act,
                     uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets);
 
+/* ---- membership change ------------------------------------------------
+ * GrainDirectoryPartition.Split(predicate, modifyOrigin) (GrainDirectoryPartition.cs:532-570)
+ * with the handoff predicate "CalculateTargetSilo(grain) is not me"
+ * (GrainDirectoryHandoffManager.cs:212-218), evaluated on the GPU under the installed ring
+ * (install the new ring with gd_ring_set first).  "me" = the silos whose partitions this
+ * handle holds: keep_silo[s] != 0 (silo indices >= n_keep count as not kept).  Selected live
+ * entries are written in slot order; move != 0 also removes them (the RemoveGrain after
+ * RegisterMany, :228-232).  KeyExt grains are never selected (their owner needs the C# hash).
+ * out_keys == NULL: size query only (*out_n = entries selected, nothing moved).  The merge on
+ * the receiving handle is gd_dir_register (GrainDirectoryPartition.Merge, :497-520: entries
+ * already present keep their activation and are reported; the host applies the reference's
+ * smallest-ActivationId rule to those). */
+int gd_dir_split(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int move, gd_key* out_keys,
+                 gd_val* out_vals, uint64_t out_capacity, uint64_t* out_n);
+/* Same, device output arrays (keep_silo stays a host array); synchronous. */
+int gd_dir_split_device(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int move, gd_key* d_out_keys,
+                        gd_val* d_out_vals, uint64_t out_capacity, uint64_t* out_n);
+
 /* ---- per-kernel timing (cfg.flags & GD_CFG_KERNEL_TIMING) ----------------------- */
 /* Up to max entries of {name, launches, total_ms} accumulated since the last reset. */
 typedef struct gd_kernel_time {

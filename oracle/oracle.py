@@ -595,6 +595,45 @@ class DirectoryArrays:
         return found, act, silo
 
 
+def directory_keys(d: DirectoryArrays) -> np.ndarray:
+    """The (n,3) u64 keys of a DirectoryArrays snapshot (inverse of _key_void)."""
+    if len(d.sorted_keys) == 0:
+        return np.zeros((0, 3), dtype=np.uint64)
+    return np.frombuffer(d.sorted_keys.tobytes(), dtype=">u8").reshape(-1, 3).astype(np.uint64)
+
+
+def split_directory(d: DirectoryArrays, spec: RingSpec, keep, my_silo: int = 0, seed_silo: int = M32):
+    """GrainDirectoryPartition.Split(grain => CalculateTargetSilo(grain) is not kept, true)
+    (GrainDirectoryPartition.cs:532-570; predicate GrainDirectoryHandoffManager.cs:212-218).
+    `keep` = silo indices held here.  KeyExt grains (owner needs the KeyExt string) stay.
+    Returns (moved keys, acts, silos) sorted by key, and the remaining snapshot."""
+    keys = directory_keys(d)
+    st, silo, act, owner, h = route_batch_np(keys, spec, DirectoryArrays(np.zeros((0, 3), np.uint64), [], []),
+                                             my_silo=my_silo, seed_silo=seed_silo)
+    keep_set = np.zeros(max([int(x) for x in keep] + [int(owner[owner != M32].max()) if (owner != M32).any() else 0])
+                        + 1, dtype=bool)
+    keep_set[[int(x) for x in keep]] = True
+    known = owner != M32
+    sel = known & ~keep_set[np.where(known, owner, 0)]
+    rest = DirectoryArrays(keys[~sel], d.acts[~sel], d.silos[~sel])
+    return keys[sel], d.acts[sel], d.silos[sel], rest
+
+
+def merge_directory(d: DirectoryArrays, keys, acts, silos):
+    """GrainDirectoryPartition.Merge as a batched AddSingleActivation (first registration
+    wins, existing entries first).  Returns (merged snapshot, inserted flags per incoming)."""
+    keys = np.asarray(keys, dtype=np.uint64).reshape(-1, 3)
+    found, _, _ = d.lookup(keys) if len(keys) else (np.zeros(0, bool), None, None)
+    kv = _key_void(keys)
+    _, first = np.unique(kv, return_index=True)
+    first_mask = np.zeros(len(keys), dtype=bool)
+    first_mask[first] = True
+    inserted = ~found & first_mask
+    merged = DirectoryArrays(np.concatenate([directory_keys(d), keys]), np.concatenate([d.acts, acts]),
+                             np.concatenate([d.silos, silos]))
+    return merged, inserted
+
+
 def route_batch_np(keys: np.ndarray, spec: RingSpec, directory: DirectoryArrays,
                    my_silo: int = 0, seed_silo: int = M32):
     """Vectorised route_batch (Dispatcher.cs:715-743 -> LocalGrainDirectory.cs:

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "gd_common.h"
+#include "gd_churn.h"
 #include "gd_frames.h"
 #include "graindispatch.h"
 
@@ -56,6 +57,7 @@ struct gd_handle {
     // scratch
     DevBuf keys_in, u32_a, u32_b, u32_c, u32_d, u8_a, out_a, out_b, out_c, hist, partials, offs;
     DevBuf fr[16];                    // header-decode scratch (host-pointer entry points)
+    DevBuf churn[5];                  // split scratch: keep mask, flags, positions, out keys/vals
     uint64_t routed = 0;
 
     // kernel tuning (defaults measured on MI355X; GD_ROUTE_M / GD_ROUTE_NT override for A/B runs)
@@ -463,6 +465,7 @@ void gd_destroy(gd_handle* h) {
                       &h->out_a, &h->out_b, &h->out_c, &h->hist, &h->partials, &h->offs})
         free_buf(*b);
     for (DevBuf& b : h->fr) free_buf(b);
+    for (DevBuf& b : h->churn) free_buf(b);
     if (h->slots) (void)hipFree(h->slots);
     if (h->ctr) (void)hipFree(h->ctr);
     for (auto& t : h->pending) {
@@ -1102,6 +1105,93 @@ int gd_route_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const ui
         if (n) HIP_TRY(h, hipMemcpyAsync(out_perm, perm, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(h, hipMemcpyAsync(out_offsets, offs, ((size_t)n_act + 2) * 4, hipMemcpyDeviceToHost, h->stream));
     }
+    return sync_checked(h);
+}
+
+}  // extern "C"
+
+// ================================================================== membership change
+namespace {
+
+// Mark + scan; returns the number of entries the split selects in *total.
+int split_count(gd_handle* h, const uint8_t* keep, uint32_t n_keep, uint64_t* total) {
+    GD_TRY(check_ring(h));
+    const unsigned long long cap = h->capacity;
+    if (cap > 0x7FFFFFFFull) return set_err(h, GD_EINVAL, "split: table of %llu slots too large", cap);
+    GD_TRY(h2d(h, h->churn[0], keep, n_keep ? n_keep : 1));
+    GD_TRY(ensure(h, h->churn[1], (size_t)cap * 4));
+    GD_TRY(ensure(h, h->churn[2], (size_t)cap * 4));
+    uint32_t* flag = (uint32_t*)h->churn[1].p;
+    uint32_t* pos = (uint32_t*)h->churn[2].p;
+    const dim3 g(blocks_for(cap, BLOCK)), b(BLOCK);
+    const RingArgs r = ring_args(h);
+    const uint8_t* dk = (const uint8_t*)h->churn[0].p;
+    switch (h->ring_mode) {
+        case GD_RING_DIRECTORY:
+            GD_TRY(launch(h, "k_split_mark", g, b, ring_lds(h), k_split_mark<GD_RING_DIRECTORY>, (const Slot*)h->slots,
+                          cap, r, dk, n_keep, flag));
+            break;
+        case GD_RING_CONSISTENT:
+            GD_TRY(launch(h, "k_split_mark", g, b, ring_lds(h), k_split_mark<GD_RING_CONSISTENT>, (const Slot*)h->slots,
+                          cap, r, dk, n_keep, flag));
+            break;
+        default:
+            GD_TRY(launch(h, "k_split_mark", g, b, ring_lds(h), k_split_mark<GD_RING_VIRTUAL_BUCKETS>,
+                          (const Slot*)h->slots, cap, r, dk, n_keep, flag));
+    }
+    HIP_TRY(h, hipMemcpyAsync(pos, flag, (size_t)cap * 4, hipMemcpyDeviceToDevice, h->stream));
+    GD_TRY(scan_device<OpAdd>(h, pos, (uint32_t)cap, false, false, "split"));
+    uint32_t last[2] = {0, 0};
+    HIP_TRY(h, hipMemcpyAsync(&last[0], pos + cap - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(&last[1], flag + cap - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(sync(h));
+    *total = (uint64_t)last[0] + last[1];
+    return GD_OK;
+}
+
+int split_emit(gd_handle* h, int move, gd_key* d_keys, gd_val* d_vals) {
+    const unsigned long long cap = h->capacity;
+    return launch(h, "k_split_emit", dim3(blocks_for(cap, BLOCK)), dim3(BLOCK), 0, k_split_emit, h->slots, cap,
+                  (const uint32_t*)h->churn[1].p, (const uint32_t*)h->churn[2].p, move, d_keys, d_vals, h->ctr);
+}
+
+}  // namespace
+
+extern "C" {
+
+int gd_dir_split_device(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int move, gd_key* d_out_keys,
+                        gd_val* d_out_vals, uint64_t out_capacity, uint64_t* out_n) {
+    if (!h || !out_n || (n_keep && !keep_silo)) return set_err(h, GD_EINVAL, "null argument");
+    if ((d_out_keys == nullptr) != (d_out_vals == nullptr)) return set_err(h, GD_EINVAL, "keys and vals go together");
+    HIP_TRY(h, hipSetDevice(h->device));
+    uint64_t total = 0;
+    GD_TRY(split_count(h, keep_silo, n_keep, &total));
+    *out_n = total;
+    if (!d_out_keys || total == 0) return GD_OK;                  // size query
+    if (total > out_capacity)
+        return set_err(h, GD_EINVAL, "split selects %llu entries, output holds %llu", (unsigned long long)total,
+                       (unsigned long long)out_capacity);
+    GD_TRY(split_emit(h, move, d_out_keys, d_out_vals));
+    return sync_checked(h);
+}
+
+int gd_dir_split(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int move, gd_key* out_keys,
+                 gd_val* out_vals, uint64_t out_capacity, uint64_t* out_n) {
+    if (!h || !out_n || (n_keep && !keep_silo)) return set_err(h, GD_EINVAL, "null argument");
+    if ((out_keys == nullptr) != (out_vals == nullptr)) return set_err(h, GD_EINVAL, "keys and vals go together");
+    HIP_TRY(h, hipSetDevice(h->device));
+    uint64_t total = 0;
+    GD_TRY(split_count(h, keep_silo, n_keep, &total));
+    *out_n = total;
+    if (!out_keys || total == 0) return GD_OK;
+    if (total > out_capacity)
+        return set_err(h, GD_EINVAL, "split selects %llu entries, output holds %llu", (unsigned long long)total,
+                       (unsigned long long)out_capacity);
+    GD_TRY(ensure(h, h->churn[3], (size_t)total * sizeof(gd_key)));
+    GD_TRY(ensure(h, h->churn[4], (size_t)total * sizeof(gd_val)));
+    GD_TRY(split_emit(h, move, (gd_key*)h->churn[3].p, (gd_val*)h->churn[4].p));
+    HIP_TRY(h, hipMemcpyAsync(out_keys, h->churn[3].p, (size_t)total * sizeof(gd_key), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(out_vals, h->churn[4].p, (size_t)total * sizeof(gd_val), hipMemcpyDeviceToHost, h->stream));
     return sync_checked(h);
 }
 

@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = [
     "gd_ring_owner_device", "gd_pack_by_shard_device", "gd_kernel_times", "gd_kernel_times_reset",
     "gd_set_kernel_timing", "gd_microbatch_create", "gd_microbatch_destroy", "gd_microbatch_keys",
     "gd_microbatch_outputs", "gd_microbatch_run", "gd_decode_frames_device", "gd_decode_frames",
-    "gd_route_frames_device", "gd_route_frames",
+    "gd_route_frames_device", "gd_route_frames", "gd_dir_split", "gd_dir_split_device",
 ]
 
 
@@ -149,6 +149,8 @@ def _load() -> C.CDLL:
         "gd_decode_frames": (C.c_int, [P, P, U64, P, U32, C.POINTER(gd_frame_fields)]),
         "gd_route_frames_device": (C.c_int, [P, P, U64, P, U32, U32, C.POINTER(gd_frame_fields), P, P, P, P, P]),
         "gd_route_frames": (C.c_int, [P, P, U64, P, U32, U32, C.POINTER(gd_frame_fields), P, P, P, P, P]),
+        "gd_dir_split": (C.c_int, [P, P, U32, C.c_int, P, P, U64, C.POINTER(U64)]),
+        "gd_dir_split_device": (C.c_int, [P, P, U32, C.c_int, P, P, U64, C.POINTER(U64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -326,6 +328,40 @@ class GrainDispatch:
 
     def clear(self):
         self._c(lib.gd_dir_clear(self.h))
+
+    def split(self, keep_silos, move: bool = True):
+        """GrainDirectoryPartition.Split by "owner under the installed ring is not kept here"
+        (SURVEY 8 f4).  keep_silos: iterable of silo indices this handle keeps.  Returns
+        (keys (n,3) u64, acts u32, silos u32) in slot order; move=True removes them here."""
+        ks = [int(x) for x in keep_silos]
+        keep = np.zeros(max(ks) + 1 if ks else 1, dtype=np.uint8)
+        keep[ks] = 1
+        n = C.c_uint64(0)
+        self._c(lib.gd_dir_split(self.h, _ptr(keep), len(keep), 1 if move else 0, None, None, 0, C.byref(n)))
+        keys = np.zeros((n.value, 3), dtype=np.uint64)
+        vals = np.zeros((n.value, 2), dtype=np.uint32)
+        if n.value:
+            got = C.c_uint64(0)
+            self._c(lib.gd_dir_split(self.h, _ptr(keep), len(keep), 1 if move else 0, _ptr(keys), _ptr(vals),
+                                     n.value, C.byref(got)))
+            assert got.value == n.value
+        return keys, vals[:, 0].copy(), vals[:, 1].copy()
+
+    @staticmethod
+    def keep_mask(keep_silos, n_silos: int) -> np.ndarray:
+        keep = np.zeros(max(n_silos, 1), dtype=np.uint8)
+        keep[[int(x) for x in keep_silos]] = 1
+        return keep
+
+    def split_device(self, keep: np.ndarray, move: bool, d_keys: Optional[int], d_vals: Optional[int],
+                     capacity: int) -> int:
+        """gd_dir_split_device; d_keys None = size query.  Returns the entries selected."""
+        keep = np.ascontiguousarray(keep, dtype=np.uint8)
+        n = C.c_uint64(0)
+        self._c(lib.gd_dir_split_device(self.h, _ptr(keep), len(keep), 1 if move else 0,
+                                        C.c_void_p(d_keys) if d_keys else None,
+                                        C.c_void_p(d_vals) if d_vals else None, capacity, C.byref(n)))
+        return n.value
 
     def rehash(self, capacity: int):
         self._c(lib.gd_dir_rehash(self.h, capacity))

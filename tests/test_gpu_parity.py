@@ -613,3 +613,93 @@ def test_route_frames_device_full_size(gd):
                              np.arange(100, dtype=np.uint64) * np.uint64(fl))
     np.testing.assert_array_equal(sample["target_grain"], keys[rows[0]:rows[0] + 100])
     e.close()
+
+
+# ----------------------------------------------------------------------------- membership change (f4)
+def _sorted_rows(keys, *cols):
+    keys = np.asarray(keys, dtype=np.uint64).reshape(-1, 3)
+    order = np.lexsort((keys[:, 2], keys[:, 1], keys[:, 0]))
+    return (keys[order],) + tuple(np.asarray(c)[order] for c in cols)
+
+
+@pytest.mark.parametrize("mode", ["D", "R", "V"])
+def test_dir_split_vs_oracle(gd, mode):
+    silos8, silos9 = o.bench_silos(8), o.bench_silos(9)
+    spec8, spec9 = o.ring_spec(silos8, mode), o.ring_spec(silos9, mode)
+    e = _engine(gd, silos8, mode, cap=1 << 16, my_silo=2, seed_silo=6)
+    G = 20000
+    reg = o.grain_keys(TC, np.arange(G))
+    owner = o.ring_owner_np(spec8, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1]))
+    special = _special_keys()[:3]          # system target, membership grain, KeyExt grain
+    keys = np.concatenate([reg, special])
+    acts = np.arange(G + 3, dtype=np.uint32)
+    silos = np.concatenate([owner, [2, 6, 1]]).astype(np.uint32)
+    e.register(keys, acts, silos)
+    d = o.DirectoryArrays(keys, acts, silos)
+    e.ring_set_silos(mode, _silo_tuples(silos9))                      # silo 8 joins
+    keep = [0, 1, 2, 3, 8]
+    wk, wa, ws, rest = o.split_directory(d, spec9, keep, my_silo=2, seed_silo=6)
+    # copy (modifyOrigin false): same entries, table untouched
+    ck, ca, cs = e.split(keep, move=False)
+    gk, ga, gs = _sorted_rows(ck, ca, cs)
+    np.testing.assert_array_equal(gk, wk)
+    np.testing.assert_array_equal(ga, wa)
+    np.testing.assert_array_equal(gs, ws)
+    assert e.stats()["table_live"] == G + 3
+    # move: the same entries leave; everything else stays findable
+    mk, ma, ms = e.split(keep, move=True)
+    np.testing.assert_array_equal(_sorted_rows(mk)[0], wk)
+    st = e.stats()
+    assert st["table_live"] == G + 3 - len(wk) and st["table_tombstones"] == len(wk)
+    _, _, found = e.lookup(keys)
+    kv = {tuple(int(x) for x in k) for k in wk}
+    assert all(bool(f) != (tuple(int(x) for x in k) in kv) for k, f in zip(keys, found))
+    # specials: system target owned by my silo (2, kept), membership by the seed (6, not kept),
+    # KeyExt never selected
+    assert tuple(int(x) for x in special[0]) not in kv
+    assert tuple(int(x) for x in special[1]) in kv
+    assert tuple(int(x) for x in special[2]) not in kv
+    # nothing left to move
+    assert len(e.split(keep, move=True)[0]) == 0
+    # merge into the partition that now owns them: inserted, then a second merge conflicts
+    e2 = _engine(gd, silos9, mode, cap=1 << 16, my_silo=2, seed_silo=6)
+    a2, s2, ins = e2.register(mk, ma, ms)
+    assert ins.all()
+    a3, s3, ins2 = e2.register(mk, ma + 100000, ms)                    # same grains, other activations
+    assert not ins2.any()
+    np.testing.assert_array_equal(a3, ma)                              # existing entries kept
+    e.close()
+    e2.close()
+
+
+def test_dir_split_device_and_full_size(gd):
+    import torch
+    silos8, silos9 = o.bench_silos(8), o.bench_silos(9)
+    spec9 = o.ring_spec(silos9, "D")
+    G = 1 << 20
+    e = _engine(gd, silos8, "D", cap=1 << 21)
+    reg = o.grain_keys(TC, np.arange(G))
+    spec8 = o.ring_spec(silos8, "D")
+    owner = o.ring_owner_np(spec8, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1]))
+    e.register(reg, np.arange(G), owner)
+    e.ring_set_silos("D", _silo_tuples(silos9))
+    keep = [s for s in range(9) if s % 2 == 0]
+    mask = gd.GrainDispatch.keep_mask(keep, 9)
+    n = e.split_device(mask, False, None, None, 0)
+    d = o.DirectoryArrays(reg, np.arange(G), owner)
+    wk, wa, ws, _ = o.split_directory(d, spec9, keep)
+    assert n == len(wk)
+    dev = torch.device("cuda:0")
+    k = torch.empty((n, 3), dtype=torch.int64, device=dev)
+    v = torch.empty((n, 2), dtype=torch.int32, device=dev)
+    with pytest.raises(gd.GrainDispatchError):
+        e.split_device(mask, True, k.data_ptr(), v.data_ptr(), n - 1)     # too small: nothing moved
+    assert e.stats()["table_live"] == G
+    assert e.split_device(mask, True, k.data_ptr(), v.data_ptr(), n) == n
+    torch.cuda.synchronize()
+    gk, gv = _sorted_rows(k.cpu().numpy().view(np.uint64), v.cpu().numpy().view(np.uint32))
+    np.testing.assert_array_equal(gk, wk)
+    np.testing.assert_array_equal(gv[:, 0], wa)
+    np.testing.assert_array_equal(gv[:, 1], ws)
+    assert e.stats()["table_live"] == G - n
+    e.close()
