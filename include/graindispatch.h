@@ -310,6 +310,52 @@ int gd_dir_split(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int mo
 int gd_dir_split_device(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int move, gd_key* d_out_keys,
                         gd_val* d_out_vals, uint64_t out_capacity, uint64_t* out_n);
 
+/* ---- follower fan-out (BASELINE cfg 4) -----------------------------------
+ * ChirperAccount.PublishMessage (Samples/Chirper/ChirperGrains/ChirperAccount.cs:106-147): each
+ * publisher sends IChirperSubscriber.NewChirp to every follower, in State.Followers enumeration
+ * order (:131-134).  The follower graph is CSR over node ids, where node u is the grain
+ * GrainId(type_code, (long)u) (GrainId.cs:72-77): row_off[n_nodes + 1] (u32, row_off[n_nodes] =
+ * edges < 2^32), dst[edges] = the followers of u in row_off[u]..row_off[u+1], in enumeration
+ * order.  One hop over a frontier of publishers emits, in this order,
+ *     for i in 0..n_frontier:  for each follower f of frontier[i]:  (target f, sender frontier[i])
+ * Publishers >= n_nodes have no followers.  *out_n = messages emitted (the hop's size; computed
+ * on the device and read back, so these calls synchronise).  capacity = room in the outputs;
+ * more messages than that is GD_EINVAL with *out_n set (a size query).  All ids are u32. */
+/* Expansion only (the multi-GPU path ships (target, sender) to the owner).  d_target == NULL:
+ * size query. */
+int gd_fanout_expand_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_nodes,
+                            const uint32_t* d_frontier, uint32_t n_frontier, uint32_t* d_target, uint32_t* d_sender,
+                            uint64_t capacity, uint64_t* out_n);
+/* Fused expansion + route (GrainId formed in registers, K0+K1+K2 as gd_route) + optional
+ * bucketing by activation (d_perm / d_offsets NULL = none; as gd_bucket over d_act).
+ * d_target may be NULL. */
+int gd_fanout_route_bucket_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_nodes,
+                                  const uint32_t* d_frontier, uint32_t n_frontier, int32_t type_code, uint32_t n_act,
+                                  uint32_t* d_target, uint32_t* d_sender, uint32_t* d_silo, uint32_t* d_act,
+                                  uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets, uint64_t capacity,
+                                  uint64_t* out_n);
+/* Host-pointer form (graph, frontier and outputs in host memory; any output may be NULL
+ * except that perm and offsets go together). */
+int gd_fanout_route_bucket(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint32_t n_nodes,
+                           const uint32_t* frontier, uint32_t n_frontier, int32_t type_code, uint32_t n_act,
+                           uint32_t* out_target, uint32_t* out_sender, uint32_t* out_silo, uint32_t* out_act,
+                           uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets, uint64_t capacity,
+                           uint64_t* out_n);
+/* gd_route_device for GrainId(type_code, (long)node) given node ids (4 B per message instead of
+ * a 24-B key): the owner side of the sharded fan-out. */
+int gd_route_nodes_device(gd_handle* h, const uint32_t* d_nodes, uint32_t n, int32_t type_code, uint32_t* d_silo,
+                          uint32_t* d_act, uint8_t* d_status);
+/* gd_pack_by_shard_device for (node, payload) pairs: stable partition by owner silo % n_shards
+ * under the installed ring (OutboundMessageQueue.cs:54-131 per target silo). */
+int gd_pack_nodes_by_shard_device(gd_handle* h, const uint32_t* d_nodes, const uint32_t* d_payload, uint32_t n,
+                                  int32_t type_code, uint32_t n_shards, uint32_t* d_send_nodes,
+                                  uint32_t* d_send_payload, uint32_t* d_counts);
+/* Next cascade frontier from a hop's bucketing: activations a < n_act with
+ * d_offsets[a+1] > d_offsets[a] and d_visited[a] == 0, ascending; marks them visited.
+ * d_out holds n_act entries; *out_n = frontier size (synchronises). */
+int gd_frontier_next_device(gd_handle* h, const uint32_t* d_offsets, uint32_t n_act, uint8_t* d_visited,
+                            uint32_t* d_out, uint32_t* out_n);
+
 /* ---- per-kernel timing (cfg.flags & GD_CFG_KERNEL_TIMING) ----------------------- */
 /* Up to max entries of {name, launches, total_ms} accumulated since the last reset. */
 typedef struct gd_kernel_time {

@@ -13,6 +13,7 @@
 
 #include "gd_common.h"
 #include "gd_churn.h"
+#include "gd_fanout.h"
 #include "gd_frames.h"
 #include "graindispatch.h"
 
@@ -58,6 +59,7 @@ struct gd_handle {
     DevBuf keys_in, u32_a, u32_b, u32_c, u32_d, u8_a, out_a, out_b, out_c, hist, partials, offs;
     DevBuf fr[16];                    // header-decode scratch (host-pointer entry points)
     DevBuf churn[5];                  // split scratch: keep mask, flags, positions, out keys/vals
+    DevBuf fan[8];                    // fan-out scratch: ends, total, flags, positions, host-form buffers
     uint64_t routed = 0;
 
     // kernel tuning (defaults measured on MI355X; GD_ROUTE_M / GD_ROUTE_NT override for A/B runs)
@@ -268,9 +270,12 @@ int ring_owner_device(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* si
 }
 
 // ---- scans -------------------------------------------------------------------
+// Scan of data[0..n) into out (default: in place).
 template <class Op>
-int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inclusive, const char* tag) {
+int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inclusive, const char* tag,
+                uint32_t* out = nullptr) {
     if (n == 0) return GD_OK;
+    if (!out) out = data;
     const uint32_t nb = blocks_for(n, SCAN_TILE);
     GD_TRY(ensure(h, h->partials, (size_t)nb * sizeof(uint32_t)));
     uint32_t* part = (uint32_t*)h->partials.p;
@@ -280,7 +285,7 @@ int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inc
     // many: a single-block scan of the aggregates in between (3 launches)
     const bool fold = nb <= 1024;
     if (!fold) GD_TRY(launch(h, "k_scan_partials", dim3(1), dim3(BLOCK), 0, k_scan_partials<Op>, part, nb));
-    return launch(h, "k_scan_down", dim3(nb), dim3(BLOCK), 0, k_scan_down<Op>, (const uint32_t*)data, data, n, reverse,
+    return launch(h, "k_scan_down", dim3(nb), dim3(BLOCK), 0, k_scan_down<Op>, (const uint32_t*)data, out, n, reverse,
                   inclusive, (const uint32_t*)part, fold ? nb : 0u);
 }
 
@@ -466,6 +471,7 @@ void gd_destroy(gd_handle* h) {
         free_buf(*b);
     for (DevBuf& b : h->fr) free_buf(b);
     for (DevBuf& b : h->churn) free_buf(b);
+    for (DevBuf& b : h->fan) free_buf(b);
     if (h->slots) (void)hipFree(h->slots);
     if (h->ctr) (void)hipFree(h->ctr);
     for (auto& t : h->pending) {
@@ -1193,6 +1199,268 @@ int gd_dir_split(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int mo
     HIP_TRY(h, hipMemcpyAsync(out_keys, h->churn[3].p, (size_t)total * sizeof(gd_key), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(h, hipMemcpyAsync(out_vals, h->churn[4].p, (size_t)total * sizeof(gd_val), hipMemcpyDeviceToHost, h->stream));
     return sync_checked(h);
+}
+
+}  // extern "C"
+
+// ================================================================== follower fan-out
+namespace {
+
+uint64_t grain_tcd(int32_t type_code) {
+    // UniqueKey.NewKey(long, Category.Grain, typeData) (UniqueKey.cs:112-128): the int type code is
+    // sign-extended, then masked to 56 bits.
+    return ((uint64_t)CAT_GRAIN << 56) + ((uint64_t)(int64_t)type_code & 0x00FFFFFFFFFFFFFFull);
+}
+
+// Degrees + inclusive scan into fan[0] (ends); the total message count comes back to the host.
+int fan_count(gd_handle* h, const uint32_t* row_off, uint32_t n_nodes, const uint32_t* frontier, uint32_t nf,
+              uint64_t* total) {
+    *total = 0;
+    if (nf == 0) return GD_OK;
+    GD_TRY(ensure(h, h->fan[0], (size_t)nf * 4));
+    GD_TRY(ensure(h, h->fan[1], 8));
+    unsigned long long* dtot = (unsigned long long*)h->fan[1].p;
+    HIP_TRY(h, hipMemsetAsync(dtot, 0, 8, h->stream));
+    uint32_t* ends = (uint32_t*)h->fan[0].p;
+    GD_TRY(launch(h, "k_fan_degree", dim3(blocks_for(nf, BLOCK)), dim3(BLOCK), 0, k_fan_degree, row_off, n_nodes,
+                  frontier, nf, ends, dtot));
+    GD_TRY(scan_device<OpAdd>(h, ends, nf, false, true, "fan"));
+    unsigned long long t = 0;
+    HIP_TRY(h, hipMemcpyAsync(&t, dtot, 8, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(sync(h));
+    if (t > 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "fan-out of %llu messages exceeds 2^32 - 1", t);
+    *total = t;
+    return GD_OK;
+}
+
+int fan_args_ok(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint32_t nf, const uint32_t* frontier,
+                uint64_t* out_n) {
+    if (!h || !out_n) return set_err(h, GD_EINVAL, "null argument");
+    if (nf && (!row_off || !dst || !frontier)) return set_err(h, GD_EINVAL, "null graph / frontier");
+    return GD_OK;
+}
+
+template <int MODE>
+int fan_route_launch(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier, uint32_t nf,
+                     uint32_t total, uint64_t tcd, uint32_t* target, uint32_t* sender, uint32_t* silo, uint32_t* act,
+                     uint8_t* status) {
+    return launch(h, "k_fan_route", dim3(blocks_for(total, FAN_TILE)), dim3(BLOCK), ring_lds(h), k_fan_route<MODE>,
+                  row_off, dst, frontier, nf, (const uint32_t*)h->fan[0].p, total, tcd, ring_args(h), table_args(h),
+                  target, sender, silo, act, status);
+}
+
+int fan_route(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier, uint32_t nf,
+              uint32_t total, uint64_t tcd, uint32_t* target, uint32_t* sender, uint32_t* silo, uint32_t* act,
+              uint8_t* status) {
+    h->routed += total;
+    switch (h->ring_mode) {
+        case GD_RING_DIRECTORY:
+            return fan_route_launch<GD_RING_DIRECTORY>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo,
+                                                       act, status);
+        case GD_RING_CONSISTENT:
+            return fan_route_launch<GD_RING_CONSISTENT>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo,
+                                                        act, status);
+        default:
+            return fan_route_launch<GD_RING_VIRTUAL_BUCKETS>(h, row_off, dst, frontier, nf, total, tcd, target, sender,
+                                                             silo, act, status);
+    }
+}
+
+int route_nodes(gd_handle* h, const uint32_t* nodes, uint32_t n, uint64_t tcd, uint32_t* silo, uint32_t* act,
+                uint8_t* status) {
+    GD_TRY(check_ring(h));
+    h->routed += n;
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    const RingArgs r = ring_args(h);
+    const TableArgs t = table_args(h);
+    switch (h->ring_mode) {
+        case GD_RING_DIRECTORY:
+            return launch(h, "k_route_nodes", g, b, ring_lds(h), k_route_nodes<GD_RING_DIRECTORY>, nodes, n, tcd, r, t,
+                          silo, act, status);
+        case GD_RING_CONSISTENT:
+            return launch(h, "k_route_nodes", g, b, ring_lds(h), k_route_nodes<GD_RING_CONSISTENT>, nodes, n, tcd, r, t,
+                          silo, act, status);
+        default:
+            return launch(h, "k_route_nodes", g, b, ring_lds(h), k_route_nodes<GD_RING_VIRTUAL_BUCKETS>, nodes, n, tcd,
+                          r, t, silo, act, status);
+    }
+}
+
+// flag / scan / emit over n_act; returns the new frontier size.
+int frontier_next(gd_handle* h, const uint32_t* offsets, uint32_t n_act, uint8_t* visited, uint32_t* out,
+                  uint32_t* out_n) {
+    *out_n = 0;
+    if (n_act == 0) return GD_OK;
+    GD_TRY(ensure(h, h->fan[2], (size_t)n_act * 4));
+    GD_TRY(ensure(h, h->fan[3], (size_t)n_act * 4));
+    uint32_t* flag = (uint32_t*)h->fan[2].p;
+    uint32_t* pos = (uint32_t*)h->fan[3].p;
+    const dim3 g(blocks_for(n_act, BLOCK)), b(BLOCK);
+    GD_TRY(launch(h, "k_frontier_flag", g, b, 0, k_frontier_flag, offsets, n_act, visited, flag));
+    GD_TRY(scan_device<OpAdd>(h, flag, n_act, false, true, "frontier", pos));
+    uint32_t cnt = 0;
+    HIP_TRY(h, hipMemcpyAsync(&cnt, pos + n_act - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(launch(h, "k_frontier_emit", g, b, 0, k_frontier_emit, (const uint32_t*)flag, (const uint32_t*)pos, n_act,
+                  out));
+    GD_TRY(sync(h));
+    *out_n = cnt;
+    return GD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gd_fanout_expand_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_nodes,
+                            const uint32_t* d_frontier, uint32_t n_frontier, uint32_t* d_target, uint32_t* d_sender,
+                            uint64_t capacity, uint64_t* out_n) {
+    GD_TRY(fan_args_ok(h, d_row_off, d_dst, n_frontier, d_frontier, out_n));
+    if ((d_target == nullptr) != (d_sender == nullptr)) return set_err(h, GD_EINVAL, "target and sender go together");
+    HIP_TRY(h, hipSetDevice(h->device));
+    uint64_t total = 0;
+    GD_TRY(fan_count(h, d_row_off, n_nodes, d_frontier, n_frontier, &total));
+    *out_n = total;
+    if (!d_target || total == 0) return GD_OK;                    // size query
+    if (total > capacity)
+        return set_err(h, GD_EINVAL, "fan-out emits %llu messages, output holds %llu", (unsigned long long)total,
+                       (unsigned long long)capacity);
+    return launch(h, "k_fan_expand", dim3(blocks_for(total, FAN_TILE)), dim3(BLOCK), 0, k_fan_expand, d_row_off, d_dst,
+                  d_frontier, n_frontier, (const uint32_t*)h->fan[0].p, (uint32_t)total, d_target, d_sender);
+}
+
+int gd_fanout_route_bucket_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_nodes,
+                                  const uint32_t* d_frontier, uint32_t n_frontier, int32_t type_code, uint32_t n_act,
+                                  uint32_t* d_target, uint32_t* d_sender, uint32_t* d_silo, uint32_t* d_act,
+                                  uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets, uint64_t capacity,
+                                  uint64_t* out_n) {
+    GD_TRY(fan_args_ok(h, d_row_off, d_dst, n_frontier, d_frontier, out_n));
+    if (!d_sender || !d_silo || !d_act || !d_status) return set_err(h, GD_EINVAL, "null output");
+    if ((d_perm == nullptr) != (d_offsets == nullptr)) return set_err(h, GD_EINVAL, "perm and offsets go together");
+    if (d_perm && n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    GD_TRY(check_ring(h));
+    HIP_TRY(h, hipSetDevice(h->device));
+    uint64_t total = 0;
+    GD_TRY(fan_count(h, d_row_off, n_nodes, d_frontier, n_frontier, &total));
+    *out_n = total;
+    if (total > capacity)
+        return set_err(h, GD_EINVAL, "fan-out emits %llu messages, output holds %llu", (unsigned long long)total,
+                       (unsigned long long)capacity);
+    if (total)
+        GD_TRY(fan_route(h, d_row_off, d_dst, d_frontier, n_frontier, (uint32_t)total, grain_tcd(type_code), d_target,
+                         d_sender, d_silo, d_act, d_status));
+    if (d_perm) GD_TRY(bucket_device(h, d_act, (uint32_t)total, n_act, d_perm, d_offsets));
+    return GD_OK;
+}
+
+int gd_fanout_route_bucket(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint32_t n_nodes,
+                           const uint32_t* frontier, uint32_t n_frontier, int32_t type_code, uint32_t n_act,
+                           uint32_t* out_target, uint32_t* out_sender, uint32_t* out_silo, uint32_t* out_act,
+                           uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets, uint64_t capacity,
+                           uint64_t* out_n) {
+    GD_TRY(fan_args_ok(h, row_off, dst, n_frontier, frontier, out_n));
+    if ((out_perm == nullptr) != (out_offsets == nullptr)) return set_err(h, GD_EINVAL, "perm and offsets go together");
+    if (out_perm && n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    GD_TRY(check_ring(h));
+    HIP_TRY(h, hipSetDevice(h->device));
+    *out_n = 0;
+    if (n_frontier == 0 || n_nodes == 0) {
+        if (out_perm) {
+            GD_TRY(ensure(h, h->offs, ((size_t)n_act + 2) * 4));
+            GD_TRY(bucket_device(h, nullptr, 0, n_act, nullptr, (uint32_t*)h->offs.p));
+            GD_TRY(d2h(h, out_offsets, h->offs, (size_t)n_act + 2));
+        }
+        return sync_checked(h);
+    }
+    // graph + frontier in; the graph buffers are re-sent per call (the device form keeps them resident)
+    uint64_t edges = 0;
+    edges = row_off[n_nodes];
+    GD_TRY(h2d(h, h->fan[4], row_off, (size_t)n_nodes + 1));
+    GD_TRY(h2d(h, h->fan[5], dst, edges ? edges : 1));
+    GD_TRY(h2d(h, h->fan[6], frontier, n_frontier));
+    const uint32_t* d_row_off = (const uint32_t*)h->fan[4].p;
+    const uint32_t* d_dst = (const uint32_t*)h->fan[5].p;
+    const uint32_t* d_front = (const uint32_t*)h->fan[6].p;
+    uint64_t total = 0;
+    GD_TRY(fan_count(h, d_row_off, n_nodes, d_front, n_frontier, &total));
+    *out_n = total;
+    if (total > capacity)
+        return set_err(h, GD_EINVAL, "fan-out emits %llu messages, output holds %llu", (unsigned long long)total,
+                       (unsigned long long)capacity);
+    const size_t n = (size_t)total;
+    // message outputs: target, sender, silo, act (4 x u32), status (u8), perm (u32)
+    GD_TRY(ensure(h, h->fan[7], n * 21 + 64));
+    uint32_t* d_target = (uint32_t*)h->fan[7].p;
+    uint32_t* d_sender = d_target + n;
+    uint32_t* d_silo = d_sender + n;
+    uint32_t* d_act = d_silo + n;
+    uint32_t* d_perm = d_act + n;
+    uint8_t* d_status = (uint8_t*)(d_perm + n);
+    if (out_perm) GD_TRY(ensure(h, h->offs, ((size_t)n_act + 2) * 4));
+    if (n)
+        GD_TRY(fan_route(h, d_row_off, d_dst, d_front, n_frontier, (uint32_t)n, grain_tcd(type_code), d_target,
+                         d_sender, d_silo, d_act, d_status));
+    if (out_perm) GD_TRY(bucket_device(h, d_act, (uint32_t)n, n_act, d_perm, (uint32_t*)h->offs.p));
+    auto get = [&](void* dstp, const void* src, size_t bytes) -> int {
+        if (dstp && bytes) HIP_TRY(h, hipMemcpyAsync(dstp, src, bytes, hipMemcpyDeviceToHost, h->stream));
+        return GD_OK;
+    };
+    GD_TRY(get(out_target, d_target, n * 4));
+    GD_TRY(get(out_sender, d_sender, n * 4));
+    GD_TRY(get(out_silo, d_silo, n * 4));
+    GD_TRY(get(out_act, d_act, n * 4));
+    GD_TRY(get(out_status, d_status, n));
+    if (out_perm) {
+        GD_TRY(get(out_perm, d_perm, n * 4));
+        GD_TRY(d2h(h, out_offsets, h->offs, (size_t)n_act + 2));
+    }
+    return sync_checked(h);
+}
+
+int gd_route_nodes_device(gd_handle* h, const uint32_t* d_nodes, uint32_t n, int32_t type_code, uint32_t* d_silo,
+                          uint32_t* d_act, uint8_t* d_status) {
+    if (!h || (n && (!d_nodes || !d_silo || !d_act || !d_status))) return set_err(h, GD_EINVAL, "null argument");
+    return n ? route_nodes(h, d_nodes, n, grain_tcd(type_code), d_silo, d_act, d_status) : GD_OK;
+}
+
+int gd_pack_nodes_by_shard_device(gd_handle* h, const uint32_t* d_nodes, const uint32_t* d_payload, uint32_t n,
+                                  int32_t type_code, uint32_t n_shards, uint32_t* d_send_nodes,
+                                  uint32_t* d_send_payload, uint32_t* d_counts) {
+    if (!h || !d_counts || (n && (!d_nodes || !d_payload || !d_send_nodes || !d_send_payload)))
+        return set_err(h, GD_EINVAL, "null argument");
+    if (n_shards == 0 || n_shards > 256) return set_err(h, GD_EINVAL, "n_shards %u not in [1, 256]", n_shards);
+    GD_TRY(check_ring(h));
+    GD_TRY(ensure(h, h->out_b, (size_t)n * 4 + 4));                 // dest
+    GD_TRY(ensure(h, h->out_a, (size_t)n * 4 + 4));                 // perm
+    GD_TRY(ensure(h, h->offs, ((size_t)n_shards + 2) * 4));
+    uint32_t* dest = (uint32_t*)h->out_b.p;
+    uint32_t* perm = (uint32_t*)h->out_a.p;
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    const RingArgs r = ring_args(h);
+    const uint64_t tcd = grain_tcd(type_code);
+    if (n) {
+        if (h->ring_mode == GD_RING_DIRECTORY)
+            GD_TRY(launch(h, "k_node_shard_dest", g, b, ring_lds(h), k_node_shard_dest<GD_RING_DIRECTORY>, d_nodes, n,
+                          tcd, r, n_shards, dest));
+        else if (h->ring_mode == GD_RING_CONSISTENT)
+            GD_TRY(launch(h, "k_node_shard_dest", g, b, ring_lds(h), k_node_shard_dest<GD_RING_CONSISTENT>, d_nodes, n,
+                          tcd, r, n_shards, dest));
+        else
+            GD_TRY(launch(h, "k_node_shard_dest", g, b, ring_lds(h), k_node_shard_dest<GD_RING_VIRTUAL_BUCKETS>,
+                          d_nodes, n, tcd, r, n_shards, dest));
+    }
+    GD_TRY(bucket_device(h, dest, n, n_shards, perm, (uint32_t*)h->offs.p));
+    if (n)
+        GD_TRY(launch(h, "k_gather_pairs", g, b, 0, k_gather_pairs, d_nodes, d_payload, (const uint32_t*)perm, n,
+                      d_send_nodes, d_send_payload));
+    return launch(h, "k_counts", dim3(1), dim3(BLOCK), 0, k_counts_from_offsets, (const uint32_t*)h->offs.p, n_shards,
+                  d_counts);
+}
+
+int gd_frontier_next_device(gd_handle* h, const uint32_t* d_offsets, uint32_t n_act, uint8_t* d_visited,
+                            uint32_t* d_out, uint32_t* out_n) {
+    if (!h || !out_n || (n_act && (!d_offsets || !d_visited || !d_out))) return set_err(h, GD_EINVAL, "null argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    return frontier_next(h, d_offsets, n_act, d_visited, d_out, out_n);
 }
 
 }  // extern "C"

@@ -1,0 +1,262 @@
+// gd_fanout.h -- gfx950 device code for SURVEY 8 f2: follower fan-out (Chirper, cfg 4).
+//
+// ChirperAccount.PublishMessage (Samples/Chirper/ChirperGrains/ChirperAccount.cs:106-147) sends
+// one NewChirp per follower, in State.Followers enumeration order (:131-134).  For a frontier of
+// publishers F (node ids = long grain keys of one grain type) over a CSR follower graph
+// (row_off[u]..row_off[u+1] = u's followers in enumeration order), one hop emits the messages
+//     for i in 0..|F|:  for j in row(F[i]):  (target = dst[j], sender = F[i])
+// in that order.  The emission is a load-balanced expansion: an inclusive scan of the degrees
+// gives ends[i]; output p belongs to item upper_bound(ends, p).  Each block owns FAN_TILE
+// consecutive outputs, finds its item range with two global searches, stages the items'
+// (end, dst base, sender) in LDS and searches there, so a celebrity row is spread over many
+// blocks and a run of zero-follower publishers costs nothing.  Writes are coalesced
+// (output p = block base + j * BLOCK + lane).
+//
+// k_fan_route fuses the expansion with K0+K1+K2: the target's GrainId(typeCode, node) is
+// formed in registers (GrainId.cs:72-77, UniqueKey.cs:122-128), hashed, looked up on the
+// LDS ring and probed, so the 24-B key never goes to HBM.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gd_common.h"
+#include "gd_kernels.h"
+
+namespace gd {
+
+constexpr int FAN_IT = 8;
+constexpr uint32_t FAN_TILE = BLOCK * FAN_IT;      // 2048 messages per block
+constexpr uint32_t FAN_LDS_ITEMS = FAN_TILE;       // publishers staged per block (24 KB: 6 blocks / CU)
+
+// ends[i] = out-degree of frontier[i] (0 for ids outside the graph: a grain nobody follows);
+// the u64 total goes to *total (block reduce + one atomic per block).
+__global__ void __launch_bounds__(BLOCK) k_fan_degree(const uint32_t* __restrict__ row_off, uint32_t n_nodes,
+                                                      const uint32_t* __restrict__ frontier, uint32_t n_front,
+                                                      uint32_t* __restrict__ ends,
+                                                      unsigned long long* __restrict__ total) {
+    __shared__ unsigned long long s_sum[BLOCK / WAVE];
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    uint32_t d = 0;
+    if (i < n_front) {
+        const uint32_t u = frontier[i];
+        if (u < n_nodes) d = row_off[u + 1] - row_off[u];
+        ends[i] = d;
+    }
+    unsigned long long v = d;
+#pragma unroll
+    for (int off = WAVE / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, WAVE);
+    if ((threadIdx.x & (WAVE - 1)) == 0) s_sum[threadIdx.x / WAVE] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long s = 0;
+#pragma unroll
+        for (int k = 0; k < BLOCK / WAVE; ++k) s += s_sum[k];
+        if (s) atomicAdd(total, s);
+    }
+}
+
+// first i in [lo, hi) with a[i] > p  (hi if none)
+__device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t p) {
+    while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if (a[mid] <= p) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Per-block staging of the publishers covering outputs [p0, p1): items [lo, lo + cnt).  When
+// cnt exceeds FAN_LDS_ITEMS (a long run of zero-follower publishers inside the range) nothing
+// is staged and fan_item searches global memory instead.
+struct FanStage {
+    uint32_t end[FAN_LDS_ITEMS];
+    uint32_t base[FAN_LDS_ITEMS];   // row_off[u] - (first output of item): dst index = base + p
+    uint32_t src[FAN_LDS_ITEMS];    // publisher node id (the NewChirp sender)
+    uint32_t lo, cnt;
+};
+
+__device__ __forceinline__ void fan_stage(FanStage& s, const uint32_t* __restrict__ row_off,
+                                          const uint32_t* __restrict__ frontier, uint32_t n_front,
+                                          const uint32_t* __restrict__ ends, uint32_t p0, uint32_t p1) {
+    if (threadIdx.x == 0) {
+        const uint32_t lo = upper_bound_u32(ends, 0, n_front, p0);
+        const uint32_t hi = upper_bound_u32(ends, lo, n_front, p1 - 1);
+        s.lo = lo;
+        s.cnt = hi - lo + 1;
+    }
+    __syncthreads();
+    const uint32_t lo = s.lo, cnt = s.cnt;
+    if (cnt <= FAN_LDS_ITEMS) {
+        for (uint32_t k = threadIdx.x; k < cnt; k += BLOCK) {
+            const uint32_t i = lo + k;
+            const uint32_t e = ends[i];
+            const uint32_t b = i ? ends[i - 1] : 0u;
+            const uint32_t u = frontier[i];
+            s.end[k] = e;
+            s.base[k] = (e != b ? row_off[u] : 0u) - b;   // zero-degree items are never selected
+            s.src[k] = u;
+        }
+    }
+    __syncthreads();
+}
+
+// Item of output p: (dst index, sender).
+__device__ __forceinline__ void fan_item(const FanStage& s, const uint32_t* __restrict__ row_off,
+                                         const uint32_t* __restrict__ frontier, uint32_t n_front,
+                                         const uint32_t* __restrict__ ends, uint32_t p, uint32_t& j,
+                                         uint32_t& sender) {
+    if (s.cnt <= FAN_LDS_ITEMS) {
+        const uint32_t k = upper_bound_u32(s.end, 0, s.cnt, p);
+        j = s.base[k] + p;
+        sender = s.src[k];
+    } else {
+        const uint32_t i = upper_bound_u32(ends, s.lo, min(s.lo + s.cnt, n_front), p);
+        const uint32_t b = i ? ends[i - 1] : 0u;
+        sender = frontier[i];
+        j = row_off[sender] + (p - b);
+    }
+}
+
+// Expansion only: (target, sender) per message -- the multi-GPU path ships these 8 B to the
+// owner instead of a 28-B header.
+__global__ void __launch_bounds__(BLOCK) k_fan_expand(const uint32_t* __restrict__ row_off,
+                                                      const uint32_t* __restrict__ dst,
+                                                      const uint32_t* __restrict__ frontier, uint32_t n_front,
+                                                      const uint32_t* __restrict__ ends, uint32_t total,
+                                                      uint32_t* __restrict__ out_target,
+                                                      uint32_t* __restrict__ out_sender) {
+    __shared__ FanStage s;
+    const uint32_t p0 = blockIdx.x * FAN_TILE;
+    const uint32_t p1 = min(p0 + FAN_TILE, total);
+    fan_stage(s, row_off, frontier, n_front, ends, p0, p1);
+    for (int it = 0; it < FAN_IT; ++it) {
+        const uint32_t p = p0 + it * BLOCK + threadIdx.x;
+        if (p >= p1) break;
+        uint32_t j, sender;
+        fan_item(s, row_off, frontier, n_front, ends, p, j, sender);
+        out_target[p] = dst[j];
+        out_sender[p] = sender;
+    }
+}
+
+// Route of GrainId(typeCode, node) (category Grain, N0 = 0, N1 = node): ring owner + probe.
+// Returns the status; silo / act as k_route_m writes them.
+template <int MODE>
+__device__ __forceinline__ uint8_t route_node(uint32_t node, uint64_t tcd, const uint32_t* s_pts,
+                                              const uint32_t* s_own, const RingArgs& ring, const TableArgs& tab,
+                                              uint32_t max_probe, uint32_t& silo, uint32_t& act) {
+    const uint64_t n0 = 0, n1 = node;
+    const uint32_t h = uniform_hash(n0, n1, tcd);
+    silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h)];
+    act = NONE32;
+    uint32_t a, meta;
+    if (probe(tab.slots, tab.mask, max_probe, h, n0, n1, tcd, a, meta)) {
+        act = a;
+        silo = slot_silo(meta);                    // ActivationAddress.Silo (Message.cs:629-639)
+        return GD_ROUTE_OK;
+    }
+    return GD_ROUTE_MISS;                          // Dispatcher.cs:742 slow path
+}
+
+// Route a batch of node ids (GrainId(typeCode, node), the owner side of the sharded fan-out).
+template <int MODE>
+__global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restrict__ nodes, uint32_t n, uint64_t tcd,
+                                                       RingArgs ring, TableArgs tab, uint32_t* __restrict__ out_silo,
+                                                       uint32_t* __restrict__ out_act,
+                                                       uint8_t* __restrict__ out_status) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    stage_ring(ring, s_pts, s_own);
+    const uint32_t max_probe = tab.ctr->max_probe;
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t silo, act;
+    const uint8_t st = route_node<MODE>(nodes[i], tcd, s_pts, s_own, ring, tab, max_probe, silo, act);
+    out_silo[i] = silo;
+    out_act[i] = act;
+    out_status[i] = st;
+}
+
+// Fused expansion + route.  out_target may be null.
+template <int MODE>
+__global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict__ row_off,
+                                                     const uint32_t* __restrict__ dst,
+                                                     const uint32_t* __restrict__ frontier, uint32_t n_front,
+                                                     const uint32_t* __restrict__ ends, uint32_t total, uint64_t tcd,
+                                                     RingArgs ring, TableArgs tab,
+                                                     uint32_t* __restrict__ out_target,
+                                                     uint32_t* __restrict__ out_sender,
+                                                     uint32_t* __restrict__ out_silo, uint32_t* __restrict__ out_act,
+                                                     uint8_t* __restrict__ out_status) {
+    __shared__ FanStage s;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    stage_ring(ring, s_pts, s_own);
+    const uint32_t max_probe = tab.ctr->max_probe;
+    const uint32_t p0 = blockIdx.x * FAN_TILE;
+    const uint32_t p1 = min(p0 + FAN_TILE, total);
+    fan_stage(s, row_off, frontier, n_front, ends, p0, p1);
+    for (int it = 0; it < FAN_IT; ++it) {
+        const uint32_t p = p0 + it * BLOCK + threadIdx.x;
+        if (p >= p1) break;
+        uint32_t j, sender, silo, act;
+        fan_item(s, row_off, frontier, n_front, ends, p, j, sender);
+        const uint32_t target = dst[j];
+        const uint8_t st = route_node<MODE>(target, tcd, s_pts, s_own, ring, tab, max_probe, silo, act);
+        if (out_target) out_target[p] = target;
+        out_sender[p] = sender;
+        out_silo[p] = silo;
+        out_act[p] = act;
+        out_status[p] = st;
+    }
+}
+
+// Next frontier (BFS over the cascade): activation a received >= 1 message this hop
+// (offsets[a+1] > offsets[a]) and has not published yet.  flag[a] in {0,1}; visited updated.
+__global__ void __launch_bounds__(BLOCK) k_frontier_flag(const uint32_t* __restrict__ offsets, uint32_t n_act,
+                                                         uint8_t* __restrict__ visited, uint32_t* __restrict__ flag) {
+    const uint32_t a = blockIdx.x * BLOCK + threadIdx.x;
+    if (a >= n_act) return;
+    const bool got = offsets[a + 1] > offsets[a];
+    const bool fresh = got && visited[a] == 0;
+    if (fresh) visited[a] = 1;
+    flag[a] = fresh ? 1u : 0u;
+}
+
+// Compaction: pos = inclusive scan of flag, so a flagged activation goes to pos[a] - 1.
+__global__ void __launch_bounds__(BLOCK) k_frontier_emit(const uint32_t* __restrict__ flag,
+                                                         const uint32_t* __restrict__ pos, uint32_t n_act,
+                                                         uint32_t* __restrict__ out) {
+    const uint32_t a = blockIdx.x * BLOCK + threadIdx.x;
+    if (a < n_act && flag[a]) out[pos[a] - 1] = a;
+}
+
+// Destination shard of GrainId(typeCode, node) (owner silo % n_shards), for the exchange.
+template <int MODE>
+__global__ void __launch_bounds__(BLOCK) k_node_shard_dest(const uint32_t* __restrict__ nodes, uint32_t n,
+                                                           uint64_t tcd, RingArgs ring, uint32_t n_shards,
+                                                           uint32_t* __restrict__ dest) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    stage_ring(ring, s_pts, s_own);
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(0, nodes[i], tcd))];
+    dest[i] = silo % n_shards;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_gather_pairs(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                                                        const uint32_t* __restrict__ perm, uint32_t n,
+                                                        uint32_t* __restrict__ out_a, uint32_t* __restrict__ out_b) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t j = perm[i];
+    out_a[i] = a[j];
+    out_b[i] = b[j];
+}
+
+}  // namespace gd

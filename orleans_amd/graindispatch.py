@@ -40,6 +40,8 @@ EXPORTED_SYMBOLS = [
     "gd_set_kernel_timing", "gd_microbatch_create", "gd_microbatch_destroy", "gd_microbatch_keys",
     "gd_microbatch_outputs", "gd_microbatch_run", "gd_decode_frames_device", "gd_decode_frames",
     "gd_route_frames_device", "gd_route_frames", "gd_dir_split", "gd_dir_split_device",
+    "gd_fanout_expand_device", "gd_fanout_route_bucket_device", "gd_fanout_route_bucket", "gd_route_nodes_device",
+    "gd_pack_nodes_by_shard_device", "gd_frontier_next_device",
 ]
 
 
@@ -151,6 +153,12 @@ def _load() -> C.CDLL:
         "gd_route_frames": (C.c_int, [P, P, U64, P, U32, U32, C.POINTER(gd_frame_fields), P, P, P, P, P]),
         "gd_dir_split": (C.c_int, [P, P, U32, C.c_int, P, P, U64, C.POINTER(U64)]),
         "gd_dir_split_device": (C.c_int, [P, P, U32, C.c_int, P, P, U64, C.POINTER(U64)]),
+        "gd_fanout_expand_device": (C.c_int, [P, P, P, U32, P, U32, P, P, U64, C.POINTER(U64)]),
+        "gd_fanout_route_bucket_device": (C.c_int, [P, P, P, U32, P, U32, I32, U32] + [P] * 7 + [U64, C.POINTER(U64)]),
+        "gd_fanout_route_bucket": (C.c_int, [P, P, P, U32, P, U32, I32, U32] + [P] * 7 + [U64, C.POINTER(U64)]),
+        "gd_route_nodes_device": (C.c_int, [P, P, U32, I32, P, P, P]),
+        "gd_pack_nodes_by_shard_device": (C.c_int, [P, P, P, U32, I32, U32, P, P, P]),
+        "gd_frontier_next_device": (C.c_int, [P, P, U32, P, P, C.POINTER(U32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -393,6 +401,66 @@ class GrainDispatch:
         off = np.zeros(n_act + 2, dtype=np.uint32)
         self._c(lib.gd_route_bucket(self.h, _ptr(k), n, n_act, _ptr(silo), _ptr(act), _ptr(st), _ptr(perm), _ptr(off)))
         return st, silo, act, perm, off
+
+    # -- follower fan-out ----------------------------------------------
+    def fanout_route_bucket(self, row_off, dst, frontier, type_code: int, n_act: Optional[int]):
+        """One publish hop (gd_fanout_route_bucket): returns dict of target, sender, status,
+        silo, act (+ perm, offsets when n_act is not None)."""
+        ro = np.ascontiguousarray(np.asarray(row_off, dtype=np.uint32))
+        d = np.ascontiguousarray(np.asarray(dst, dtype=np.uint32))
+        if d.size == 0:
+            d = np.zeros(1, dtype=np.uint32)
+        fr = np.ascontiguousarray(np.asarray(frontier, dtype=np.uint32))
+        n_nodes = len(ro) - 1
+        n = C.c_uint64(0)
+        na = 0 if n_act is None else n_act
+        # size query through the fused call with capacity 0 would do the work twice: count on the host
+        valid = fr[fr < n_nodes]
+        m = int((ro[valid.astype(np.int64) + 1].astype(np.int64) - ro[valid].astype(np.int64)).sum())
+        out = {k: np.zeros(m, dtype=np.uint32) for k in ("target", "sender", "silo", "act")}
+        out["status"] = np.zeros(m, dtype=np.uint8)
+        perm = off = None
+        if n_act is not None:
+            perm = np.zeros(m, dtype=np.uint32)
+            off = np.zeros(na + 2, dtype=np.uint32)
+        P = lambda a: None if a is None else _ptr(a)  # noqa: E731
+        self._c(lib.gd_fanout_route_bucket(self.h, _ptr(ro), _ptr(d), n_nodes, _ptr(fr) if len(fr) else None, len(fr),
+                                           type_code, na, P(out["target"]), P(out["sender"]), P(out["silo"]),
+                                           P(out["act"]), P(out["status"]), P(perm), P(off), m, C.byref(n)))
+        assert n.value == m
+        if n_act is not None:
+            out["perm"], out["offsets"] = perm, off
+        return out
+
+    def fanout_expand_device(self, d_row_off: int, d_dst: int, n_nodes: int, d_frontier: int, n_frontier: int,
+                             d_target: Optional[int], d_sender: Optional[int], capacity: int) -> int:
+        n = C.c_uint64(0)
+        self._c(lib.gd_fanout_expand_device(self.h, d_row_off, d_dst, n_nodes, d_frontier, n_frontier,
+                                            d_target or None, d_sender or None, capacity, C.byref(n)))
+        return n.value
+
+    def fanout_route_bucket_device(self, d_row_off: int, d_dst: int, n_nodes: int, d_frontier: int, n_frontier: int,
+                                   type_code: int, n_act: int, d_target: Optional[int], d_sender: int, d_silo: int,
+                                   d_act: int, d_status: int, d_perm: Optional[int], d_offsets: Optional[int],
+                                   capacity: int) -> int:
+        n = C.c_uint64(0)
+        self._c(lib.gd_fanout_route_bucket_device(self.h, d_row_off, d_dst, n_nodes, d_frontier, n_frontier, type_code,
+                                                  n_act, d_target or None, d_sender, d_silo, d_act, d_status,
+                                                  d_perm or None, d_offsets or None, capacity, C.byref(n)))
+        return n.value
+
+    def route_nodes_device(self, d_nodes: int, n: int, type_code: int, d_silo: int, d_act: int, d_status: int):
+        self._c(lib.gd_route_nodes_device(self.h, d_nodes, n, type_code, d_silo, d_act, d_status))
+
+    def pack_nodes_by_shard_device(self, d_nodes: int, d_payload: int, n: int, type_code: int, n_shards: int,
+                                   d_send_nodes: int, d_send_payload: int, d_counts: int):
+        self._c(lib.gd_pack_nodes_by_shard_device(self.h, d_nodes, d_payload, n, type_code, n_shards, d_send_nodes,
+                                                  d_send_payload, d_counts))
+
+    def frontier_next_device(self, d_offsets: int, n_act: int, d_visited: int, d_out: int) -> int:
+        n = C.c_uint32(0)
+        self._c(lib.gd_frontier_next_device(self.h, d_offsets, n_act, d_visited, d_out, C.byref(n)))
+        return n.value
 
     # -- hot path (device pointers; enqueue only) -----------------------------------
     def route_device(self, d_keys: int, n: int, d_silo: int, d_act: int, d_status: int):

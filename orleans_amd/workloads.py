@@ -1,0 +1,33 @@
+"""Synthetic workloads for the benches and tests (no datasets: there is no network).
+
+Data generation only -- no routing logic lives here.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def power_law_graph(n_nodes: int, mean_deg: float, seed: int, max_deg: int = 1 << 16, alpha: float = 2.5):
+    """Synthetic follower graph for cfg 4: power-law follower counts (Pareto tail,
+    exponent ``alpha``, capped at ``max_deg``), followers distinct within a row and never
+    the publisher itself -- the shape ``AddFollower`` keeps (one dictionary key per
+    follower).  Row u's followers are (u + 1 + S[(r_u + k) % L]) mod n for k < deg(u),
+    with S a fixed sample of L distinct offsets in [0, n-1): distinct by construction.
+    Returns (row_off u32[n+1], dst u32[E])."""
+    rng = np.random.default_rng(seed)
+    raw = (rng.pareto(alpha - 1.0, size=n_nodes) + 1.0)
+    # P(deg >= x) ~ x^(1 - alpha); scale so that E[deg] = mean_deg before the cap (rounded)
+    deg = np.minimum(np.floor(raw * (mean_deg * (alpha - 2.0) / (alpha - 1.0)) + 0.5).astype(np.int64), max_deg)
+    deg = np.minimum(deg, n_nodes - 1)
+    row_off = np.zeros(n_nodes + 1, dtype=np.int64)
+    np.cumsum(deg, out=row_off[1:])
+    if row_off[-1] >= 1 << 32:
+        raise ValueError("graph too large for u32 edge offsets")
+    L = int(min(n_nodes - 1, max(max_deg, 1)))
+    S = rng.choice(n_nodes - 1, size=L, replace=False).astype(np.int64)
+    r = rng.integers(0, L, size=n_nodes)
+    E = int(row_off[-1])
+    item = np.repeat(np.arange(n_nodes, dtype=np.int64), deg)
+    k = np.arange(E, dtype=np.int64) - row_off[item]
+    dst = ((item + 1 + S[(r[item] + k) % L]) % n_nodes).astype(np.uint32)
+    return row_off.astype(np.uint32), dst
