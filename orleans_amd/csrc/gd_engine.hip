@@ -56,7 +56,7 @@ struct gd_handle {
     DevCounters ctr_host{};           // last copy
 
     // scratch
-    DevBuf keys_in, u32_a, u32_b, u32_c, u32_d, u8_a, out_a, out_b, out_c, hist, partials, offs;
+    DevBuf keys_in, u32_a, u32_b, u32_c, u32_d, u8_a, out_a, out_b, out_c, hist, partials, partials2, offs;
     DevBuf fr[16];                    // header-decode scratch (host-pointer entry points)
     DevBuf churn[5];                  // split scratch: keep mask, flags, positions, out keys/vals
     DevBuf fan[8];                    // fan-out scratch: ends, total, flags, positions, host-form buffers
@@ -282,9 +282,23 @@ int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inc
     (void)tag;
     GD_TRY(launch(h, "k_scan_reduce", dim3(nb), dim3(BLOCK), 0, k_scan_reduce<Op>, (const uint32_t*)data, n, reverse, part));
     // few blocks: every block folds its predecessors' aggregates itself (2 launches);
-    // many: a single-block scan of the aggregates in between (3 launches)
+    // many: the aggregates are scanned in between -- by the same two-launch fold scan one level
+    // up while that has <= 1024 blocks (4 launches), else by one block (3 launches)
     const bool fold = nb <= 1024;
-    if (!fold) GD_TRY(launch(h, "k_scan_partials", dim3(1), dim3(BLOCK), 0, k_scan_partials<Op>, part, nb));
+    if (!fold) {
+        const uint32_t nb2 = blocks_for(nb, SCAN_TILE);
+        if (nb2 <= 1024) {
+            GD_TRY(ensure(h, h->partials2, (size_t)nb2 * sizeof(uint32_t)));
+            uint32_t* part2 = (uint32_t*)h->partials2.p;
+            // partials are in logical order already: scan them forward, exclusive, in place
+            GD_TRY(launch(h, "k_scan_reduce", dim3(nb2), dim3(BLOCK), 0, k_scan_reduce<Op>, (const uint32_t*)part, nb,
+                          false, part2));
+            GD_TRY(launch(h, "k_scan_down", dim3(nb2), dim3(BLOCK), 0, k_scan_down<Op>, (const uint32_t*)part, part, nb,
+                          false, false, (const uint32_t*)part2, nb2));
+        } else {
+            GD_TRY(launch(h, "k_scan_partials", dim3(1), dim3(BLOCK), 0, k_scan_partials<Op>, part, nb));
+        }
+    }
     return launch(h, "k_scan_down", dim3(nb), dim3(BLOCK), 0, k_scan_down<Op>, (const uint32_t*)data, out, n, reverse,
                   inclusive, (const uint32_t*)part, fold ? nb : 0u);
 }
@@ -467,7 +481,7 @@ void gd_destroy(gd_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (DevBuf* b : {&h->ring_pts, &h->ring_own, &h->keys_in, &h->u32_a, &h->u32_b, &h->u32_c, &h->u32_d, &h->u8_a,
-                      &h->out_a, &h->out_b, &h->out_c, &h->hist, &h->partials, &h->offs})
+                      &h->out_a, &h->out_b, &h->out_c, &h->hist, &h->partials, &h->partials2, &h->offs})
         free_buf(*b);
     for (DevBuf& b : h->fr) free_buf(b);
     for (DevBuf& b : h->churn) free_buf(b);
@@ -1222,7 +1236,7 @@ int fan_count(gd_handle* h, const uint32_t* row_off, uint32_t n_nodes, const uin
     unsigned long long* dtot = (unsigned long long*)h->fan[1].p;
     HIP_TRY(h, hipMemsetAsync(dtot, 0, 8, h->stream));
     uint32_t* ends = (uint32_t*)h->fan[0].p;
-    GD_TRY(launch(h, "k_fan_degree", dim3(blocks_for(nf, BLOCK)), dim3(BLOCK), 0, k_fan_degree, row_off, n_nodes,
+    GD_TRY(launch(h, "k_fan_degree", dim3(std::min<uint32_t>(blocks_for(nf, BLOCK), 1024)), dim3(BLOCK), 0, k_fan_degree, row_off, n_nodes,
                   frontier, nf, ends, dtot));
     GD_TRY(scan_device<OpAdd>(h, ends, nf, false, true, "fan"));
     unsigned long long t = 0;

@@ -36,14 +36,13 @@ __global__ void __launch_bounds__(BLOCK) k_fan_degree(const uint32_t* __restrict
                                                       uint32_t* __restrict__ ends,
                                                       unsigned long long* __restrict__ total) {
     __shared__ unsigned long long s_sum[BLOCK / WAVE];
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    uint32_t d = 0;
-    if (i < n_front) {
-        const uint32_t u = frontier[i];
-        if (u < n_nodes) d = row_off[u + 1] - row_off[u];
+    unsigned long long v = 0;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_front; i += gridDim.x * BLOCK) {  // grid-stride:
+        const uint32_t u = frontier[i];                                                           // few atomics
+        const uint32_t d = u < n_nodes ? row_off[u + 1] - row_off[u] : 0u;
         ends[i] = d;
+        v += d;
     }
-    unsigned long long v = d;
 #pragma unroll
     for (int off = WAVE / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, WAVE);
     if ((threadIdx.x & (WAVE - 1)) == 0) s_sum[threadIdx.x / WAVE] = v;
