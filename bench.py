@@ -66,13 +66,32 @@ def kernel_bytes(name: str, n: int, n_act: int, passes: int, world: int) -> floa
     return 0.0
 
 
+def zipf_keys(tcd: int, n_grains: int, n: int, seed: int, dev) -> torch.Tensor:
+    """(n, 3) int64 keys on `dev`: grain k ~ Zipf(s=1.1) over ranks 0..n_grains-1 by inverse CDF
+    (SURVEY 8 d cfg 3), sampled on the GPU; grain k is GrainId(Ping type, k)."""
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    cdf = torch.arange(1, n_grains + 1, dtype=torch.float64, device=dev).pow_(-1.1).cumsum_(0)
+    cdf /= cdf[-1].clone()
+    u = torch.rand(n, dtype=torch.float64, device=dev, generator=gen)
+    k = torch.searchsorted(cdf, u).clamp_(max=n_grains - 1)
+    del cdf, u
+    keys = torch.zeros((n, 3), dtype=torch.int64, device=dev)
+    keys[:, 1] = k
+    keys[:, 2] = np.uint64(tcd).astype(np.int64).item()
+    return keys
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--msgs", type=int, default=1 << 24, help="messages per GPU per step")
-    ap.add_argument("--grains", type=int, default=1 << 20, help="grains per GPU")
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3"],
+                    help="cfg2: 16M uniform msgs/GPU over 2^20 grains/GPU (weak scaling); cfg3: 64M Zipf(1.1) "
+                         "msgs over 100M grains for the whole node (strong scaling)")
+    ap.add_argument("--msgs", type=int, default=None, help="messages per GPU per step (cfg2 default 2^24)")
+    ap.add_argument("--grains", type=int, default=None, help="grains per GPU (cfg2 default 2^20)")
     ap.add_argument("--mode", default="D", choices=["D", "R", "V"])
     ap.add_argument("--silos", default="balanced", choices=sorted(SILO_SETS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline budget")
@@ -99,14 +118,22 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29571")
         dist.init_process_group("gloo", rank=0, world_size=1)
 
-    N, Gr = args.msgs, args.grains
-    G_total = Gr * world
+    if args.workload == "cfg3":
+        # BASELINE cfg 3 (SURVEY 8 d): 67,108,864 messages for the whole node, k ~ Zipf(1.1) over
+        # 100,000,000 grains, directory sharded by mode-D owner
+        G_total = args.grains * world if args.grains else 100_000_000
+        N = args.msgs or (1 << 26) // world
+        Gr = -(-G_total // world)
+    else:
+        N, Gr = args.msgs or 1 << 24, args.grains or 1 << 20
+        G_total = Gr * world
     tc = g.calculate_id_hash(PING_GRAIN_CLASS)
     tcd = (3 << 56) + ((tc & 0xFFFFFFFFFFFFFFFF) & 0x00FFFFFFFFFFFFFF)
 
     # ---- directory: this rank owns the grains whose owner silo lives here -----
     all_keys = grain_keys(tcd, np.arange(G_total, dtype=np.int64))
-    e = g.GrainDispatch(device=local, table_capacity=2 * Gr, my_silo=rank % 8, kernel_timing=False)
+    cap = 2 * Gr if args.workload == "cfg2" else 1 << int(np.ceil(np.log2(2 * Gr)))
+    e = g.GrainDispatch(device=local, table_capacity=cap, my_silo=rank % 8, kernel_timing=False)
     silos = SILO_SETS[args.silos]
     pts, own = e.ring_set_silos(args.mode, silos)
     owner = e.ring_owner(all_keys)
@@ -116,10 +143,13 @@ def main():
     del all_keys
 
     # ---- synthetic message batch, resident in HBM ----------------------------------
-    rng = np.random.default_rng(0x5EED0001 + rank)
-    ks = rng.integers(0, G_total, size=N, dtype=np.int64)
-    keys = torch.from_numpy(grain_keys(tcd, ks).view(np.int64)).to(dev)
-    del ks
+    if args.workload == "cfg3":
+        keys = zipf_keys(tcd, G_total, N, 0x5EED0003 + rank, dev)
+    else:
+        rng = np.random.default_rng(0x5EED0001 + rank)
+        ks = rng.integers(0, G_total, size=N, dtype=np.int64)
+        keys = torch.from_numpy(grain_keys(tcd, ks).view(np.int64)).to(dev)
+        del ks
     torch.cuda.synchronize()
 
     engine = DeviceEngine(e, dev)
@@ -189,8 +219,8 @@ def main():
         d = kernels[dom]
         launches = max(1, d["launches_per_step"])
         traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{dom}.json")
-        if os.path.exists(pmc_path):
+        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{dom}.json")   # collected on cfg2 at N = 1
+        if os.path.exists(pmc_path) and args.workload == "cfg2" and world == 1:
             with open(pmc_path) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         roofline = {"bound": "hbm", "kernel": dom,
@@ -201,7 +231,7 @@ def main():
 
     # ---- CPU baseline: the C restatement (oracle/cpu_ref.c), bounded sample ---------
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "cfg2":
         cpu = cpu_baseline(args, tcd, G_total, pts, own, owner)
 
     if rank == 0:
@@ -215,17 +245,17 @@ def main():
             "ms_per_step": round(wall_max / args.steps * 1e3, 4),
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.workload == "cfg2" else "strong",
             "vs_baseline": None,
             "dtype": "u32/u64 integer",
-            "data": "synthetic GrainIds (no dataset); uniform keys, seed 0x5EED0001+rank",
-            "config": {"workload": "cfg2: 16M msgs uniform over 1M grains, 8 silos, ring D" if world == 1 else
-                       f"cfg2 per GPU (16M msgs/GPU over {G_total} grains), directory sharded by ring owner, "
-                       f"RCCL all-to-all-v",
+            "data": "synthetic GrainIds (no dataset); " + (
+                "uniform keys, seed 0x5EED0001+rank" if args.workload == "cfg2" else
+                "Zipf(1.1) keys by inverse CDF on the GPU, seed 0x5EED0003+rank"),
+            "config": {"workload": workload_name(args.workload, world, N, G_total),
                        "msgs_per_gpu": N, "grains_total": G_total, "ring_mode": args.mode,
                        "silos": f"8 x 10.0.0.{{1..8}}:11111, {args.silos} generations",
                        "owner_share_max": round(float(np.bincount(owner % world, minlength=world).max()) / G_total, 4),
-                       "table_load": round(n_act / (2 * Gr), 3), "parallelism": f"shard{world}"},
+                       "table_load": round(n_act / cap, 3), "parallelism": f"shard{world}"},
             "routed_ok_last_step_rank0": st_ok,
             "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
             "roofline": roofline,
@@ -235,6 +265,15 @@ def main():
         print(json.dumps(line), flush=True)
     e.close()
     dist.destroy_process_group()
+
+
+def workload_name(w: str, world: int, n: int, g_total: int) -> str:
+    if w == "cfg3":
+        return (f"cfg3: {n * world} msgs Zipf(1.1) over {g_total} grains, directory sharded by ring owner over "
+                f"{world} GPU(s)" + (", RCCL all-to-all-v" if world > 1 else ""))
+    if world == 1:
+        return "cfg2: 16M msgs uniform over 1M grains, 8 silos, ring D"
+    return f"cfg2 per GPU (16M msgs/GPU over {g_total} grains), directory sharded by ring owner, RCCL all-to-all-v"
 
 
 def cpu_baseline(args, tcd, G_total, pts, own, owner):

@@ -38,7 +38,7 @@ SILOS = [(f"10.0.0.{i + 1}", 11111, gen) for i, gen in
 
 
 def kernel_bytes(name, msgs, n_front, n_act, passes, keep_target, n_hops):
-    """Algorithmic HBM bytes over all launches of a kernel (DESIGN.md 5.4)."""
+    """Algorithmic HBM bytes over all launches of a kernel (DESIGN.md 5.3)."""
     if name == "k_fan_route":
         # dst read 4 + one slot 32 + sender/silo/act 12 + status 1 (+ target 4); per publisher 16
         return msgs * (49 + (4 if keep_target else 0)) + n_front * 16
