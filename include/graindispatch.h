@@ -356,6 +356,43 @@ int gd_pack_nodes_by_shard_device(gd_handle* h, const uint32_t* d_nodes, const u
 int gd_frontier_next_device(gd_handle* h, const uint32_t* d_offsets, uint32_t n_act, uint8_t* d_visited,
                             uint32_t* d_out, uint32_t* out_n);
 
+/* ---- non-owner directory cache -------------------------------------------
+ * AdaptiveGrainDirectoryCache over LRU<GrainId, entry> (src/Orleans.Runtime/GrainDirectory/
+ * AdaptiveGrainDirectoryCache.cs:7-140, src/Orleans.Core/Utils/LRU.cs) on the LocalLookup path
+ * (LocalGrainDirectory.cs:797-850).  Configured (max_size > 0), gd_route / gd_route_device /
+ * gd_route_bucket[_device] run LocalLookup per message: a grain whose ring owner is a local
+ * silo (local_silo[owner] != 0) is probed in this handle's directory partition; any other grain
+ * in the cache.  A cache hit whose silo is not valid (valid_silo[silo] == 0, IsValidSilo) is
+ * GD_ROUTE_MISS, as is a cache miss (silo = ring owner, act = GD_NO_ACTIVATION).  The LRU is the
+ * reference's exactly: every hit and every add takes the next generation (hits in batch order),
+ * AdjustSize evicts the lowest generation while count >= max_size.  max_size 0 = no cache
+ * (whole-node mode: every grain is probed in this handle's table).  The specialised paths
+ * (frames, micro-batch, fan-out) do not consult the cache. */
+typedef struct gd_cache_stats {
+    uint64_t count;             /* live entries (LRU.Count)                       */
+    uint64_t accesses;          /* NumAccesses                                     */
+    uint64_t hits;              /* NumHits                                         */
+    uint64_t next_generation;   /* LRU.nextGeneration                              */
+    uint64_t max_size;
+    uint64_t capacity;          /* table slots                                     */
+} gd_cache_stats;
+int gd_cache_configure(gd_handle* h, uint32_t max_size, const uint8_t* local_silo, const uint8_t* valid_silo,
+                       uint32_t n_silos);
+/* Membership change: new local / valid silo masks; entries stay (the maintainer refreshes them). */
+int gd_cache_set_silos(gd_handle* h, const uint8_t* local_silo, const uint8_t* valid_silo, uint32_t n_silos);
+/* AddOrUpdate(key, value, version) for each entry in order (after a remote lookup, :920). */
+int gd_cache_add(gd_handle* h, const gd_key* keys, const gd_val* vals, const int32_t* versions, uint32_t n);
+/* Remove (:79-83); out_removed may be NULL. */
+int gd_cache_remove(gd_handle* h, const gd_key* keys, uint32_t n, uint8_t* out_removed);
+/* LookUp (:90-109) in order: value + version (ETag) of hits. */
+int gd_cache_lookup(gd_handle* h, const gd_key* keys, uint32_t n, gd_val* out_vals, int32_t* out_versions,
+                    uint8_t* out_found);
+int gd_cache_clear(gd_handle* h);
+int gd_cache_stats_get(gd_handle* h, gd_cache_stats* out);
+/* KeyValues (:111-127) with each entry's generation, in slot order; keys NULL = size query. */
+int gd_cache_entries(gd_handle* h, gd_key* keys, gd_val* vals, int32_t* versions, uint64_t* generations,
+                     uint64_t capacity, uint64_t* out_n);
+
 /* ---- per-kernel timing (cfg.flags & GD_CFG_KERNEL_TIMING) ----------------------- */
 /* Up to max entries of {name, launches, total_ms} accumulated since the last reset. */
 typedef struct gd_kernel_time {

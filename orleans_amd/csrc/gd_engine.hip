@@ -8,12 +8,15 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <queue>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
 #include "gd_common.h"
 #include "gd_churn.h"
 #include "gd_fanout.h"
+#include "gd_cache.h"
 #include "gd_frames.h"
 #include "graindispatch.h"
 
@@ -60,6 +63,15 @@ struct gd_handle {
     DevBuf fr[16];                    // header-decode scratch (host-pointer entry points)
     DevBuf churn[5];                  // split scratch: keep mask, flags, positions, out keys/vals
     DevBuf fan[8];                    // fan-out scratch: ends, total, flags, positions, host-form buffers
+
+    // non-owner directory cache (LocalLookup mode when cache_max > 0)
+    CacheSlot* cslots = nullptr;
+    unsigned long long ccap = 0;
+    CacheCounters* cctr = nullptr;   // device
+    uint32_t cache_max = 0;
+    uint32_t cache_nsilos = 0;
+    DevBuf cache_local, cache_valid;
+    DevBuf cbuf[8];                   // cache scratch
     uint64_t routed = 0;
 
     // kernel tuning (defaults measured on MI355X; GD_ROUTE_M / GD_ROUTE_NT override for A/B runs)
@@ -240,9 +252,12 @@ int route_mode(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uin
     }
 }
 
+int route_cached(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status);
+
 int route_device(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
     GD_TRY(check_ring(h));
     h->routed += n;
+    if (h->cache_max) return route_cached(h, keys, n, silo, act, status);
     switch (h->ring_mode) {
         case GD_RING_DIRECTORY: return route_mode<GD_RING_DIRECTORY>(h, keys, n, silo, act, status);
         case GD_RING_CONSISTENT: return route_mode<GD_RING_CONSISTENT>(h, keys, n, silo, act, status);
@@ -486,6 +501,11 @@ void gd_destroy(gd_handle* h) {
     for (DevBuf& b : h->fr) free_buf(b);
     for (DevBuf& b : h->churn) free_buf(b);
     for (DevBuf& b : h->fan) free_buf(b);
+    for (DevBuf& b : h->cbuf) free_buf(b);
+    free_buf(h->cache_local);
+    free_buf(h->cache_valid);
+    if (h->cslots) (void)hipFree(h->cslots);
+    if (h->cctr) (void)hipFree(h->cctr);
     if (h->slots) (void)hipFree(h->slots);
     if (h->ctr) (void)hipFree(h->ctr);
     for (auto& t : h->pending) {
@@ -1475,6 +1495,431 @@ int gd_frontier_next_device(gd_handle* h, const uint32_t* d_offsets, uint32_t n_
     if (!h || !out_n || (n_act && (!d_offsets || !d_visited || !d_out))) return set_err(h, GD_EINVAL, "null argument");
     HIP_TRY(h, hipSetDevice(h->device));
     return frontier_next(h, d_offsets, n_act, d_visited, d_out, out_n);
+}
+
+}  // extern "C"
+
+// ================================================================== non-owner directory cache
+namespace {
+
+CacheArgs cache_args(gd_handle* h) {
+    return CacheArgs{h->cslots, h->ccap - 1, h->cctr, (const uint8_t*)h->cache_local.p,
+                     (const uint8_t*)h->cache_valid.p, h->cache_nsilos};
+}
+
+// Generations for the hits of a batch, in batch order (hit flags in `hit`, slots in `cslot`).
+int cache_touch(gd_handle* h, uint32_t* hit, const uint32_t* cslot, uint32_t n) {
+    GD_TRY(ensure(h, h->cbuf[2], (size_t)n * 4));
+    uint32_t* pos = (uint32_t*)h->cbuf[2].p;
+    GD_TRY(scan_device<OpAdd>(h, hit, n, false, true, "cache", pos));
+    GD_TRY(launch(h, "k_cache_touch", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_cache_touch, cslot,
+                  (const uint32_t*)pos, n, h->cslots, (const CacheCounters*)h->cctr));
+    return launch(h, "k_cache_advance", dim3(1), dim3(64), 0, k_cache_advance, (const uint32_t*)pos, n, h->cctr);
+}
+
+template <int MODE>
+int route_cached_t(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status,
+                   uint32_t* hit, uint32_t* cslot) {
+    return launch(h, "k_route_cached", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), ring_lds(h), k_route_cached<MODE>, keys,
+                  n, ring_args(h), table_args(h), cache_args(h), silo, act, status, hit, cslot, h->cctr);
+}
+
+int route_cached(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
+    if (n == 0) return GD_OK;
+    GD_TRY(ensure(h, h->cbuf[0], (size_t)n * 4));
+    GD_TRY(ensure(h, h->cbuf[1], (size_t)n * 4));
+    uint32_t* hit = (uint32_t*)h->cbuf[0].p;
+    uint32_t* cslot = (uint32_t*)h->cbuf[1].p;
+    switch (h->ring_mode) {
+        case GD_RING_DIRECTORY: GD_TRY(route_cached_t<GD_RING_DIRECTORY>(h, keys, n, silo, act, status, hit, cslot)); break;
+        case GD_RING_CONSISTENT: GD_TRY(route_cached_t<GD_RING_CONSISTENT>(h, keys, n, silo, act, status, hit, cslot)); break;
+        default: GD_TRY(route_cached_t<GD_RING_VIRTUAL_BUCKETS>(h, keys, n, silo, act, status, hit, cslot));
+    }
+    return cache_touch(h, hit, cslot, n);
+}
+
+int cache_pull(gd_handle* h, CacheCounters* c) {
+    HIP_TRY(h, hipMemcpyAsync(c, h->cctr, sizeof(CacheCounters), hipMemcpyDeviceToHost, h->stream));
+    return sync(h);
+}
+
+int cache_check(gd_handle* h) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (!h->cache_max) return set_err(h, GD_ESTATE, "no directory cache configured (gd_cache_configure)");
+    return GD_OK;
+}
+
+// (Re)build the table with `cap` slots, moving the live entries (tombstone compaction).
+int cache_rehash(gd_handle* h, unsigned long long cap) {
+    CacheSlot* ns = nullptr;
+    hipError_t e = hipMalloc(&ns, cap * sizeof(CacheSlot));
+    if (e != hipSuccess) return set_err(h, GD_ENOMEM, "cache hipMalloc(%llu slots): %s", cap, hipGetErrorString(e));
+    HIP_TRY(h, hipMemsetAsync(ns, 0, cap * sizeof(CacheSlot), h->stream));
+    CacheCounters c{};
+    GD_TRY(cache_pull(h, &c));
+    CacheCounters fresh = c;
+    fresh.live = fresh.tomb = 0;
+    fresh.max_probe = 0;
+    fresh.err = 0;
+    HIP_TRY(h, hipMemcpyAsync(h->cctr, &fresh, sizeof fresh, hipMemcpyHostToDevice, h->stream));
+    if (h->cslots) {
+        GD_TRY(launch(h, "k_cache_rehash", dim3(blocks_for(h->ccap, BLOCK)), dim3(BLOCK), 0, k_cache_rehash,
+                      (const CacheSlot*)h->cslots, h->ccap, ns, cap - 1, h->cctr));
+        GD_TRY(sync(h));
+        HIP_TRY(h, hipFree(h->cslots));
+    }
+    h->cslots = ns;
+    h->ccap = cap;
+    return sync(h);
+}
+
+int cache_masks(gd_handle* h, const uint8_t* local, const uint8_t* valid, uint32_t n_silos) {
+    std::vector<uint8_t> l(n_silos ? n_silos : 1, 0), v(n_silos ? n_silos : 1, 0);
+    for (uint32_t i = 0; i < n_silos; ++i) {
+        l[i] = local ? (local[i] != 0) : 0;
+        v[i] = valid ? (valid[i] != 0) : 1;
+    }
+    GD_TRY(h2d(h, h->cache_local, l.data(), l.size()));
+    GD_TRY(h2d(h, h->cache_valid, v.data(), v.size()));
+    h->cache_nsilos = n_silos;
+    return sync(h);
+}
+
+struct KeyHash {
+    size_t operator()(const gd_key& k) const {
+        return std::hash<uint64_t>()(k.n0 * 0x9E3779B97F4A7C15ull ^ k.n1 * 0xC2B2AE3D27D4EB4Full ^ k.type_code_data);
+    }
+};
+struct KeyEq {
+    bool operator()(const gd_key& a, const gd_key& b) const {
+        return a.n0 == b.n0 && a.n1 == b.n1 && a.type_code_data == b.type_code_data;
+    }
+};
+
+// The `v` lowest live generations as (gen, slot), ascending.
+int cache_lowest(gd_handle* h, uint64_t v, uint64_t next_gen, std::vector<std::pair<uint64_t, uint32_t>>* out) {
+    out->clear();
+    if (v == 0) return GD_OK;
+    GD_TRY(ensure(h, h->cbuf[6], 16));
+    unsigned long long* dcount = (unsigned long long*)h->cbuf[6].p;
+    const uint32_t grid = std::min<uint32_t>(blocks_for(h->ccap, BLOCK), 2048);
+    // smallest t with |{live: gen <= t}| >= v (generations are distinct, so the count is exactly v)
+    uint64_t lo = 1, hi = next_gen;
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        HIP_TRY(h, hipMemsetAsync(dcount, 0, 8, h->stream));
+        GD_TRY(launch(h, "k_cache_count_le", dim3(grid), dim3(BLOCK), 0, k_cache_count_le, (const CacheSlot*)h->cslots,
+                      h->ccap, (unsigned long long)mid, dcount));
+        unsigned long long c = 0;
+        HIP_TRY(h, hipMemcpyAsync(&c, dcount, 8, hipMemcpyDeviceToHost, h->stream));
+        GD_TRY(sync(h));
+        if (c >= v) hi = mid;
+        else lo = mid + 1;
+    }
+    GD_TRY(ensure(h, h->cbuf[7], (size_t)v * 12 + 16));
+    unsigned long long* dgen = (unsigned long long*)h->cbuf[7].p;
+    uint32_t* dslot = (uint32_t*)(dgen + v);
+    uint32_t* cursor = (uint32_t*)h->cbuf[6].p;
+    HIP_TRY(h, hipMemsetAsync(cursor, 0, 4, h->stream));
+    GD_TRY(launch(h, "k_cache_collect_le", dim3(blocks_for(h->ccap, BLOCK)), dim3(BLOCK), 0, k_cache_collect_le,
+                  (const CacheSlot*)h->cslots, h->ccap, (unsigned long long)lo, cursor, dgen, dslot, (uint32_t)v));
+    uint32_t got = 0;
+    std::vector<unsigned long long> g(v);
+    std::vector<uint32_t> sl(v);
+    HIP_TRY(h, hipMemcpyAsync(&got, cursor, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(g.data(), dgen, v * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(sl.data(), dslot, v * 4, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(sync(h));
+    if (got != v) return set_err(h, GD_ESTATE, "cache: %u entries at or below generation %llu, expected %llu", got,
+                                 (unsigned long long)lo, (unsigned long long)v);
+    out->resize(v);
+    for (uint64_t i = 0; i < v; ++i) (*out)[i] = {g[i], sl[i]};
+    std::sort(out->begin(), out->end());
+    return GD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gd_cache_configure(gd_handle* h, uint32_t max_size, const uint8_t* local_silo, const uint8_t* valid_silo,
+                       uint32_t n_silos) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (n_silos && !local_silo) return set_err(h, GD_EINVAL, "null local_silo");
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(sync(h));
+    h->layout_gen++;
+    if (max_size == 0) {                       // back to whole-node mode
+        h->cache_max = 0;
+        return GD_OK;
+    }
+    if (!h->cctr) {
+        hipError_t e = hipMalloc(&h->cctr, sizeof(CacheCounters));
+        if (e != hipSuccess) return set_err(h, GD_ENOMEM, "cache counters: %s", hipGetErrorString(e));
+    }
+    CacheCounters z{};
+    HIP_TRY(h, hipMemcpyAsync(h->cctr, &z, sizeof z, hipMemcpyHostToDevice, h->stream));
+    if (h->cslots) {
+        HIP_TRY(h, hipFree(h->cslots));
+        h->cslots = nullptr;
+    }
+    const unsigned long long cap = pow2_at_least(2ull * max_size);
+    h->cache_max = max_size;
+    GD_TRY(cache_rehash(h, cap));
+    return cache_masks(h, local_silo, valid_silo, n_silos);
+}
+
+int gd_cache_set_silos(gd_handle* h, const uint8_t* local_silo, const uint8_t* valid_silo, uint32_t n_silos) {
+    GD_TRY(cache_check(h));
+    if (n_silos && !local_silo) return set_err(h, GD_EINVAL, "null local_silo");
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(sync(h));
+    return cache_masks(h, local_silo, valid_silo, n_silos);
+}
+
+int gd_cache_add(gd_handle* h, const gd_key* keys, const gd_val* vals, const int32_t* versions, uint32_t n) {
+    GD_TRY(cache_check(h));
+    if (n && (!keys || !vals || !versions)) return set_err(h, GD_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n; ++i)
+        if (vals[i].silo > 0xFFFEu) return set_err(h, GD_EINVAL, "silo index %u out of range at %u", vals[i].silo, i);
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    CacheCounters c{};
+    GD_TRY(cache_pull(h, &c));
+    if ((c.live + c.tomb + n) * 4 > h->ccap * 3) {      // compact tombstones (and grow if a batch needs it)
+        unsigned long long cap = pow2_at_least(2ull * h->cache_max);
+        while ((c.live + n) * 2 > cap) cap <<= 1;
+        GD_TRY(cache_rehash(h, cap));
+        GD_TRY(cache_pull(h, &c));
+    }
+    // 1. where each key lives now
+    GD_TRY(h2d(h, h->cbuf[3], keys, n));
+    GD_TRY(ensure(h, h->cbuf[4], (size_t)n * 4));
+    GD_TRY(ensure(h, h->cbuf[5], (size_t)n * 8));
+    GD_TRY(launch(h, "k_cache_find", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_cache_find,
+                  (const gd_key*)h->cbuf[3].p, n, cache_args(h), (uint32_t*)h->cbuf[4].p,
+                  (unsigned long long*)h->cbuf[5].p));
+    std::vector<uint32_t> slot_of(n);
+    HIP_TRY(h, hipMemcpyAsync(slot_of.data(), h->cbuf[4].p, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(sync(h));
+    // 2. eviction candidates: each add evicts at most one entry and renews at most one, so the
+    //    2n lowest generations cover every pre-existing entry this batch can evict
+    const uint64_t M = h->cache_max;
+    std::vector<std::pair<uint64_t, uint32_t>> victims;
+    if (c.live + n >= M) GD_TRY(cache_lowest(h, std::min<uint64_t>(c.live, 2ull * n), c.next_gen, &victims));
+    // 3. AdjustSize + Add (LRU.cs:71-76,165-182) in batch order
+    struct Ent {
+        gd_key key;
+        uint32_t act, silo;
+        int32_t ver;
+        uint64_t gen;
+        uint32_t from_slot;   // pre-existing slot this entry renews, or NONE32
+        bool alive;
+    };
+    std::vector<Ent> ents;
+    ents.reserve(n);
+    std::unordered_map<gd_key, uint32_t, KeyHash, KeyEq> ent_of;
+    std::unordered_map<uint32_t, uint8_t> pre;          // pre-existing slot -> 1 evicted, 2 renewed
+    typedef std::pair<uint64_t, uint32_t> GI;
+    std::priority_queue<GI, std::vector<GI>, std::greater<GI>> heap;   // (gen, ent) of batch entries
+    size_t vp = 0;
+    uint64_t count = c.live, ng = c.next_gen;
+    for (uint32_t i = 0; i < n; ++i) {
+        while (count >= M) {
+            while (vp < victims.size() && pre.count(victims[vp].second)) ++vp;
+            if (vp < victims.size()) {
+                pre[victims[vp].second] = 1;
+                ++vp;
+                --count;
+                continue;
+            }
+            bool evicted = false;
+            while (!heap.empty()) {
+                const GI top = heap.top();
+                heap.pop();
+                Ent& e = ents[top.second];
+                if (!e.alive || e.gen != top.first) continue;
+                e.alive = false;
+                --count;
+                evicted = true;
+                break;
+            }
+            if (!evicted) return set_err(h, GD_ESTATE, "cache: nothing to evict at add %u (count %llu)", i,
+                                         (unsigned long long)count);
+        }
+        auto it = ent_of.find(keys[i]);
+        if (it != ent_of.end() && ents[it->second].alive) {
+            Ent& e = ents[it->second];
+            e.act = vals[i].act;
+            e.silo = vals[i].silo;
+            e.ver = versions[i];
+            e.gen = ++ng;
+            heap.push({e.gen, it->second});
+        } else if (it == ent_of.end() && slot_of[i] != NONE32 && !pre.count(slot_of[i])) {
+            pre[slot_of[i]] = 2;
+            ents.push_back(Ent{keys[i], vals[i].act, vals[i].silo, versions[i], ++ng, slot_of[i], true});
+            ent_of[keys[i]] = (uint32_t)ents.size() - 1;
+            heap.push({ng, (uint32_t)ents.size() - 1});
+        } else {
+            ents.push_back(Ent{keys[i], vals[i].act, vals[i].silo, versions[i], ++ng, NONE32, true});
+            ent_of[keys[i]] = (uint32_t)ents.size() - 1;
+            heap.push({ng, (uint32_t)ents.size() - 1});
+            ++count;
+        }
+    }
+    // 4. apply: tombstones and in-place updates, then the new entries
+    std::vector<CacheOp> ops;
+    std::vector<gd_key> ins_keys;
+    std::vector<CacheOp> ins;
+    for (const auto& p : pre)
+        if (p.second == 1) ops.push_back(CacheOp{p.first, 0, 0, 0, 0, 0, 0});
+    for (const Ent& e : ents) {
+        if (e.from_slot != NONE32)
+            ops.push_back(e.alive ? CacheOp{e.from_slot, 1, e.act, e.silo, e.gen, e.ver, 0}
+                                  : CacheOp{e.from_slot, 0, 0, 0, 0, 0, 0});
+        else if (e.alive) {
+            ins_keys.push_back(e.key);
+            ins.push_back(CacheOp{NONE32, 1, e.act, e.silo, e.gen, e.ver, 0});
+        }
+    }
+    if (!ops.empty()) {
+        GD_TRY(h2d(h, h->cbuf[4], ops.data(), ops.size()));
+        GD_TRY(launch(h, "k_cache_apply", dim3(blocks_for(ops.size(), BLOCK)), dim3(BLOCK), 0, k_cache_apply,
+                      (const CacheOp*)h->cbuf[4].p, (uint32_t)ops.size(), h->cslots, h->cctr));
+    }
+    if (!ins.empty()) {
+        GD_TRY(h2d(h, h->cbuf[3], ins_keys.data(), ins_keys.size()));
+        GD_TRY(h2d(h, h->cbuf[5], ins.data(), ins.size()));
+        GD_TRY(launch(h, "k_cache_insert", dim3(blocks_for(ins.size(), BLOCK)), dim3(BLOCK), 0, k_cache_insert,
+                      (const gd_key*)h->cbuf[3].p, (const CacheOp*)h->cbuf[5].p, (uint32_t)ins.size(), h->cslots,
+                      h->ccap - 1, h->cctr));
+    }
+    GD_TRY(sync(h));
+    CacheCounters after{};
+    GD_TRY(cache_pull(h, &after));
+    after.next_gen = ng;
+    HIP_TRY(h, hipMemcpyAsync(&h->cctr->next_gen, &after.next_gen, 8, hipMemcpyHostToDevice, h->stream));
+    GD_TRY(sync(h));
+    if (after.err) return set_err(h, GD_EFULL, "cache: device error bits 0x%x", after.err);
+    if (after.live != count)
+        return set_err(h, GD_ESTATE, "cache: %llu live entries after the batch, expected %llu",
+                       (unsigned long long)after.live, (unsigned long long)count);
+    return GD_OK;
+}
+
+int gd_cache_remove(gd_handle* h, const gd_key* keys, uint32_t n, uint8_t* out_removed) {
+    GD_TRY(cache_check(h));
+    if (n && !keys) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->cbuf[3], keys, n));
+    GD_TRY(ensure(h, h->cbuf[4], (size_t)n * 4));
+    GD_TRY(ensure(h, h->cbuf[5], (size_t)n * 8));
+    GD_TRY(launch(h, "k_cache_find", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_cache_find,
+                  (const gd_key*)h->cbuf[3].p, n, cache_args(h), (uint32_t*)h->cbuf[4].p,
+                  (unsigned long long*)h->cbuf[5].p));
+    std::vector<uint32_t> slot_of(n);
+    HIP_TRY(h, hipMemcpyAsync(slot_of.data(), h->cbuf[4].p, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(sync(h));
+    std::vector<CacheOp> ops;
+    std::unordered_map<uint32_t, bool> seen;
+    for (uint32_t i = 0; i < n; ++i) {
+        const bool first = slot_of[i] != NONE32 && seen.emplace(slot_of[i], true).second;
+        if (first) ops.push_back(CacheOp{slot_of[i], 0, 0, 0, 0, 0, 0});
+        if (out_removed) out_removed[i] = first ? 1 : 0;
+    }
+    if (!ops.empty()) {
+        GD_TRY(h2d(h, h->cbuf[6], ops.data(), ops.size()));
+        GD_TRY(launch(h, "k_cache_apply", dim3(blocks_for(ops.size(), BLOCK)), dim3(BLOCK), 0, k_cache_apply,
+                      (const CacheOp*)h->cbuf[6].p, (uint32_t)ops.size(), h->cslots, h->cctr));
+    }
+    return sync(h);
+}
+
+int gd_cache_lookup(gd_handle* h, const gd_key* keys, uint32_t n, gd_val* out_vals, int32_t* out_versions,
+                    uint8_t* out_found) {
+    GD_TRY(cache_check(h));
+    if (n && (!keys || !out_vals || !out_versions || !out_found)) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->cbuf[3], keys, n));
+    GD_TRY(ensure(h, h->cbuf[0], (size_t)n * 4));
+    GD_TRY(ensure(h, h->cbuf[1], (size_t)n * 4));
+    GD_TRY(ensure(h, h->cbuf[4], (size_t)n * sizeof(gd_val)));
+    GD_TRY(ensure(h, h->cbuf[5], (size_t)n * 4));
+    uint32_t* hit = (uint32_t*)h->cbuf[0].p;
+    GD_TRY(launch(h, "k_cache_lookup", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_cache_lookup,
+                  (const gd_key*)h->cbuf[3].p, n, cache_args(h), (gd_val*)h->cbuf[4].p, (int32_t*)h->cbuf[5].p, hit,
+                  (uint32_t*)h->cbuf[1].p));
+    std::vector<uint32_t> found(n);
+    HIP_TRY(h, hipMemcpyAsync(found.data(), hit, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(out_vals, h->cbuf[4].p, (size_t)n * sizeof(gd_val), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(out_versions, h->cbuf[5].p, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(launch(h, "k_cache_count_access", dim3(1), dim3(64), 0, k_cache_count_access, n, h->cctr));
+    GD_TRY(cache_touch(h, hit, (const uint32_t*)h->cbuf[1].p, n));
+    GD_TRY(sync(h));
+    for (uint32_t i = 0; i < n; ++i) out_found[i] = found[i] ? 1 : 0;
+    return GD_OK;
+}
+
+int gd_cache_clear(gd_handle* h) {
+    GD_TRY(cache_check(h));
+    HIP_TRY(h, hipSetDevice(h->device));
+    // LRU.Clear (:94-106) empties the dictionary; nextGeneration and the statistics stay
+    HIP_TRY(h, hipMemsetAsync(h->cslots, 0, h->ccap * sizeof(CacheSlot), h->stream));
+    CacheCounters c{};
+    GD_TRY(cache_pull(h, &c));
+    c.live = c.tomb = 0;
+    c.max_probe = 0;
+    HIP_TRY(h, hipMemcpyAsync(h->cctr, &c, sizeof c, hipMemcpyHostToDevice, h->stream));
+    return sync(h);
+}
+
+int gd_cache_stats_get(gd_handle* h, gd_cache_stats* out) {
+    GD_TRY(cache_check(h));
+    if (!out) return set_err(h, GD_EINVAL, "null argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    CacheCounters c{};
+    GD_TRY(cache_pull(h, &c));
+    *out = gd_cache_stats{c.live, c.accesses, c.hits, c.next_gen, h->cache_max, h->ccap};
+    return GD_OK;
+}
+
+int gd_cache_entries(gd_handle* h, gd_key* keys, gd_val* vals, int32_t* versions, uint64_t* generations,
+                     uint64_t capacity, uint64_t* out_n) {
+    GD_TRY(cache_check(h));
+    if (!out_n) return set_err(h, GD_EINVAL, "null argument");
+    if (keys && (!vals || !versions || !generations)) return set_err(h, GD_EINVAL, "null output");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (h->ccap > 0x7FFFFFFFull) return set_err(h, GD_EINVAL, "cache table too large to dump");
+    const uint32_t cap = (uint32_t)h->ccap;
+    GD_TRY(ensure(h, h->cbuf[0], (size_t)cap * 4));
+    GD_TRY(ensure(h, h->cbuf[2], (size_t)cap * 4));
+    uint32_t* flag = (uint32_t*)h->cbuf[0].p;
+    uint32_t* pos = (uint32_t*)h->cbuf[2].p;
+    GD_TRY(launch(h, "k_cache_live_flag", dim3(blocks_for(cap, BLOCK)), dim3(BLOCK), 0, k_cache_live_flag,
+                  (const CacheSlot*)h->cslots, cap, flag));
+    GD_TRY(scan_device<OpAdd>(h, flag, cap, false, true, "cache", pos));
+    uint32_t total = 0;
+    HIP_TRY(h, hipMemcpyAsync(&total, pos + cap - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(sync(h));
+    *out_n = total;
+    if (!keys || total == 0) return GD_OK;
+    if (total > capacity)
+        return set_err(h, GD_EINVAL, "cache holds %u entries, output holds %llu", total, (unsigned long long)capacity);
+    GD_TRY(ensure(h, h->cbuf[7], (size_t)total * (sizeof(gd_key) + sizeof(gd_val) + 4 + 8) + 64));
+    uint8_t* base = (uint8_t*)h->cbuf[7].p;
+    gd_key* dk = (gd_key*)base;
+    unsigned long long* dg = (unsigned long long*)(base + (size_t)total * sizeof(gd_key));
+    gd_val* dv = (gd_val*)(dg + total);
+    int32_t* dver = (int32_t*)(dv + total);
+    GD_TRY(launch(h, "k_cache_dump", dim3(blocks_for(cap, BLOCK)), dim3(BLOCK), 0, k_cache_dump,
+                  (const CacheSlot*)h->cslots, cap, (const uint32_t*)flag, (const uint32_t*)pos, dk, dv, dver, dg));
+    HIP_TRY(h, hipMemcpyAsync(keys, dk, (size_t)total * sizeof(gd_key), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(vals, dv, (size_t)total * sizeof(gd_val), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(versions, dver, (size_t)total * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(generations, dg, (size_t)total * 8, hipMemcpyDeviceToHost, h->stream));
+    return sync(h);
 }
 
 }  // extern "C"

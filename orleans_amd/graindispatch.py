@@ -42,6 +42,8 @@ EXPORTED_SYMBOLS = [
     "gd_route_frames_device", "gd_route_frames", "gd_dir_split", "gd_dir_split_device",
     "gd_fanout_expand_device", "gd_fanout_route_bucket_device", "gd_fanout_route_bucket", "gd_route_nodes_device",
     "gd_pack_nodes_by_shard_device", "gd_frontier_next_device",
+    "gd_cache_configure", "gd_cache_set_silos", "gd_cache_add", "gd_cache_remove", "gd_cache_lookup",
+    "gd_cache_clear", "gd_cache_stats_get", "gd_cache_entries",
 ]
 
 
@@ -66,6 +68,11 @@ class gd_config(C.Structure):
 class gd_stats(C.Structure):
     _fields_ = [("routed", C.c_uint64), ("table_live", C.c_uint64), ("table_tombstones", C.c_uint64),
                 ("table_capacity", C.c_uint64), ("ring_points", C.c_uint64), ("ring_mode", C.c_uint64)]
+
+
+class gd_cache_stats(C.Structure):
+    _fields_ = [("count", C.c_uint64), ("accesses", C.c_uint64), ("hits", C.c_uint64),
+                ("next_generation", C.c_uint64), ("max_size", C.c_uint64), ("capacity", C.c_uint64)]
 
 
 class gd_kernel_time(C.Structure):
@@ -159,6 +166,14 @@ def _load() -> C.CDLL:
         "gd_route_nodes_device": (C.c_int, [P, P, U32, I32, P, P, P]),
         "gd_pack_nodes_by_shard_device": (C.c_int, [P, P, P, U32, I32, U32, P, P, P]),
         "gd_frontier_next_device": (C.c_int, [P, P, U32, P, P, C.POINTER(U32)]),
+        "gd_cache_configure": (C.c_int, [P, U32, P, P, U32]),
+        "gd_cache_set_silos": (C.c_int, [P, P, P, U32]),
+        "gd_cache_add": (C.c_int, [P, P, P, P, U32]),
+        "gd_cache_remove": (C.c_int, [P, P, U32, P]),
+        "gd_cache_lookup": (C.c_int, [P, P, U32, P, P, P]),
+        "gd_cache_clear": (C.c_int, [P]),
+        "gd_cache_stats_get": (C.c_int, [P, C.POINTER(gd_cache_stats)]),
+        "gd_cache_entries": (C.c_int, [P, P, P, P, P, U64, C.POINTER(U64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -401,6 +416,74 @@ class GrainDispatch:
         off = np.zeros(n_act + 2, dtype=np.uint32)
         self._c(lib.gd_route_bucket(self.h, _ptr(k), n, n_act, _ptr(silo), _ptr(act), _ptr(st), _ptr(perm), _ptr(off)))
         return st, silo, act, perm, off
+
+    # -- non-owner directory cache -------------------------------------
+    @staticmethod
+    def _silo_mask(silos, n_silos: int, default: int) -> np.ndarray:
+        m = np.full(max(n_silos, 1), default, dtype=np.uint8)
+        if silos is not None:
+            m[:] = 0
+            m[[int(x) for x in silos]] = 1
+        return m
+
+    def cache_configure(self, max_size: int, local_silos, n_silos: int, valid_silos=None):
+        """LocalLookup mode: grains owned by `local_silos` are probed here, the rest in an
+        LRU cache of `max_size` entries (valid_silos None = every silo valid)."""
+        loc = self._silo_mask(local_silos, n_silos, 0)
+        val = self._silo_mask(valid_silos, n_silos, 1)
+        self._c(lib.gd_cache_configure(self.h, max_size, _ptr(loc), _ptr(val), n_silos))
+
+    def cache_set_silos(self, local_silos, n_silos: int, valid_silos=None):
+        loc = self._silo_mask(local_silos, n_silos, 0)
+        val = self._silo_mask(valid_silos, n_silos, 1)
+        self._c(lib.gd_cache_set_silos(self.h, _ptr(loc), _ptr(val), n_silos))
+
+    def cache_add(self, keys, acts, silos, versions):
+        k = keys_array(keys)
+        n = len(k)
+        vals = np.zeros((n, 2), dtype=np.uint32)
+        vals[:, 0] = acts
+        vals[:, 1] = silos
+        ver = np.ascontiguousarray(np.asarray(versions, dtype=np.int32))
+        self._c(lib.gd_cache_add(self.h, _ptr(k), _ptr(vals), _ptr(ver), n))
+
+    def cache_remove(self, keys) -> np.ndarray:
+        k = keys_array(keys)
+        out = np.zeros(len(k), dtype=np.uint8)
+        self._c(lib.gd_cache_remove(self.h, _ptr(k), len(k), _ptr(out)))
+        return out
+
+    def cache_lookup(self, keys):
+        """Returns (found u8, act u32, silo u32, version i32)."""
+        k = keys_array(keys)
+        n = len(k)
+        vals = np.zeros((n, 2), dtype=np.uint32)
+        ver = np.zeros(n, dtype=np.int32)
+        found = np.zeros(n, dtype=np.uint8)
+        self._c(lib.gd_cache_lookup(self.h, _ptr(k), n, _ptr(vals), _ptr(ver), _ptr(found)))
+        return found, vals[:, 0].copy(), vals[:, 1].copy(), ver
+
+    def cache_clear(self):
+        self._c(lib.gd_cache_clear(self.h))
+
+    def cache_stats(self) -> dict:
+        s = gd_cache_stats()
+        self._c(lib.gd_cache_stats_get(self.h, C.byref(s)))
+        return {name: int(getattr(s, name)) for name, _ in gd_cache_stats._fields_}
+
+    def cache_entries(self) -> dict:
+        """key tuple -> (act, silo, version, generation)."""
+        n = C.c_uint64(0)
+        self._c(lib.gd_cache_entries(self.h, None, None, None, None, 0, C.byref(n)))
+        m = n.value
+        k = np.zeros((max(m, 1), 3), dtype=np.uint64)
+        v = np.zeros((max(m, 1), 2), dtype=np.uint32)
+        ver = np.zeros(max(m, 1), dtype=np.int32)
+        gen = np.zeros(max(m, 1), dtype=np.uint64)
+        if m:
+            self._c(lib.gd_cache_entries(self.h, _ptr(k), _ptr(v), _ptr(ver), _ptr(gen), m, C.byref(n)))
+        return {tuple(int(x) for x in k[i]): (int(v[i, 0]), int(v[i, 1]), int(ver[i]), int(gen[i]))
+                for i in range(m)}
 
     # -- follower fan-out (SURVEY 8 f2) ----------------------------------------------
     def fanout_route_bucket(self, row_off, dst, frontier, type_code: int, n_act: Optional[int]):
