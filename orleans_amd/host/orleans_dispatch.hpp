@@ -14,6 +14,8 @@
 //   VirtualBucketsRingProvider          src/Orleans.Runtime/ConsistentRing/VirtualBucketsRingProvider.cs:122-293
 //   Dispatcher.AddressMessage           src/Orleans.Runtime/Core/Dispatcher.cs:715-767
 //   IncomingMessageAgent.ReceiveMessage src/Orleans.Runtime/Messaging/IncomingMessageAgent.cs:92-190
+//   AdaptiveGrainDirectoryCache         src/Orleans.Runtime/GrainDirectory/AdaptiveGrainDirectoryCache.cs:7-140
+//                                       (over LRU, src/Orleans.Core/Utils/LRU.cs)
 //
 // Every per-message decision runs on the GPU through the C ABI; single-grain
 // calls are batches of one.  Errors from the ABI throw OrleansException (the C#
@@ -28,6 +30,7 @@
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -382,12 +385,92 @@ private:
     std::map<ActivationId, uint32_t> act_index_;
 };
 
-// LocalGrainDirectory: directory ring (mode D) + this GPU's partition, whole-node model.
+// AdaptiveGrainDirectoryCache<IReadOnlyList<Tuple<SiloAddress, ActivationId>>> for
+// single-activation grains (AdaptiveGrainDirectoryCache.cs:7-140 over LRU.cs): the handle's GPU
+// cache, exact LRU generations.  Owned by a LocalGrainDirectory in per-silo mode.
+class AdaptiveGrainDirectoryCache {
+public:
+    using Value = std::pair<SiloAddress, ActivationId>;
+    AdaptiveGrainDirectoryCache(gd_handle* h, SiloTable& silos, GrainDirectoryPartition& acts)
+        : h_(h), silos_(silos), acts_(acts) {}
+
+    // AddOrUpdate (:71-77); a batch is applied in order.
+    void AddOrUpdate(const GrainId& key, const Value& value, int version) {
+        AddOrUpdate(std::vector<GrainId>{key}, std::vector<Value>{value}, std::vector<int>{version});
+    }
+    void AddOrUpdate(const std::vector<GrainId>& keys, const std::vector<Value>& values,
+                     const std::vector<int>& versions) {
+        const size_t n = keys.size();
+        std::vector<gd_key> k(n);
+        std::vector<gd_val> v(n);
+        std::vector<int32_t> ver(versions.begin(), versions.end());
+        for (size_t i = 0; i < n; ++i) {
+            k[i] = keys[i].Key.ToNative();
+            v[i] = gd_val{acts_.ActIndex(values[i].second), silos_.IndexOf(values[i].first)};
+        }
+        if (n) Check(h_, gd_cache_add(h_, k.data(), v.data(), ver.data(), (uint32_t)n));
+    }
+    bool Remove(const GrainId& key) {                   // :79-83
+        const gd_key k = key.Key.ToNative();
+        uint8_t removed = 0;
+        Check(h_, gd_cache_remove(h_, &k, 1, &removed));
+        return removed != 0;
+    }
+    void Clear() { Check(h_, gd_cache_clear(h_)); }     // :85-88
+    bool LookUp(const GrainId& key, Value& result, int& version) {   // :90-109
+        const gd_key k = key.Key.ToNative();
+        gd_val v{};
+        int32_t ver = 0;
+        uint8_t found = 0;
+        Check(h_, gd_cache_lookup(h_, &k, 1, &v, &ver, &found));
+        if (!found) return false;
+        result = Value{silos_.At(v.silo), acts_.ActivationAt(v.act)};
+        version = ver;
+        return true;
+    }
+    // KeyValues (:111-127)
+    std::vector<std::tuple<GrainId, Value, int>> KeyValues() const {
+        uint64_t n = 0;
+        Check(h_, gd_cache_entries(h_, nullptr, nullptr, nullptr, nullptr, 0, &n));
+        std::vector<gd_key> k(n);
+        std::vector<gd_val> v(n);
+        std::vector<int32_t> ver(n);
+        std::vector<uint64_t> gen(n);
+        if (n) Check(h_, gd_cache_entries(h_, k.data(), v.data(), ver.data(), gen.data(), n, &n));
+        std::vector<std::tuple<GrainId, Value, int>> r;
+        for (uint64_t i = 0; i < n; ++i) {
+            GrainId g;
+            g.Key.N0 = k[i].n0;
+            g.Key.N1 = k[i].n1;
+            g.Key.TypeCodeData = k[i].type_code_data;
+            r.emplace_back(g, Value{silos_.At(v[i].silo), acts_.ActivationAt(v[i].act)}, ver[i]);
+        }
+        return r;
+    }
+    int Count() const { return (int)Stats().count; }
+    long NumAccesses() const { return (long)Stats().accesses; }
+    long NumHits() const { return (long)Stats().hits; }
+
+private:
+    gd_cache_stats Stats() const {
+        gd_cache_stats s{};
+        Check(h_, gd_cache_stats_get(h_, &s));
+        return s;
+    }
+    gd_handle* h_;
+    SiloTable& silos_;
+    GrainDirectoryPartition& acts_;
+};
+
+// LocalGrainDirectory: directory ring (mode D) + this GPU's partition.  Whole-node model by
+// default (the owner partition is always consulted); EnableCache switches to the reference's
+// per-silo model: only MyAddress's partition is local, other grains go through the cache.
 class LocalGrainDirectory {
 public:
     // One ring snapshot per handle: give every ring provider its own DispatchHandle.
     LocalGrainDirectory(gd_handle* h, SiloAddress me)
-        : MyAddress(std::move(me)), h_(h), ring_(h, GD_RING_DIRECTORY, 1), partition_(h, silos_) {
+        : MyAddress(std::move(me)), h_(h), ring_(h, GD_RING_DIRECTORY, 1), partition_(h, silos_),
+          cache_(h, silos_, partition_) {
         silos_.IndexOf(MyAddress);
         AddServer(MyAddress);
     }
@@ -420,11 +503,32 @@ public:
     SiloAddress CalculateTargetSilo(const GrainId& grain) const { return CalculateTargetSilos({grain})[0]; }
     SiloAddress GetPrimaryForGrain(const GrainId& grain) const { return CalculateTargetSilo(grain); }
 
-    // LocalLookup (LocalGrainDirectory.cs:797-837), whole-node model: the owning partition is
-    // always consulted, so a miss is a false return.
+    // Per-silo model with a DirectoryCache of maxCacheSize entries (GrainDirectoryOptions'
+    // CacheSize, default 1,000,000).  The valid silos are the ring's members (IsValidSilo).
+    void EnableCache(uint32_t maxCacheSize) {
+        cacheOn_ = true;
+        const auto m = Masks();
+        Check(h_, gd_cache_configure(h_, maxCacheSize, m.first.data(), m.second.data(), (uint32_t)m.first.size()));
+    }
+    AdaptiveGrainDirectoryCache& DirectoryCache() { return cache_; }
+
+    // LocalLookup (LocalGrainDirectory.cs:797-837).  Whole-node model: the owning partition is
+    // always consulted.  Per-silo model: the partition when this silo owns the
+    // grain, else the cache (a hit on an invalid silo, an empty list in the reference, is a
+    // false return here: either way the dispatcher takes the full lookup).
     bool LocalLookup(const GrainId& grain, AddressesAndTag& result) const {
-        result = partition_.LookUpActivations(grain);
-        return result.Addresses.has_value();
+        if (!cacheOn_) {
+            result = partition_.LookUpActivations(grain);
+            return result.Addresses.has_value();
+        }
+        const gd_key k = grain.Key.ToNative();
+        uint32_t silo = 0, act = 0;
+        uint8_t st = 0;
+        Check(h_, gd_route(h_, &k, 1, &silo, &act, &st));
+        result = AddressesAndTag{};
+        if (st != GD_ROUTE_OK) return false;
+        result.Addresses = std::vector<ActivationAddress>{{silos_.At(silo), grain, partition_.ActivationAt(act)}};
+        return true;
     }
     AddressesAndTag GetLocalDirectoryData(const GrainId& grain) const { return partition_.LookUpActivations(grain); }
 
@@ -444,6 +548,19 @@ private:
         for (uint32_t o : ring_.Owners()) own.push_back(silos_.IndexOf(m[o]));
         std::vector<uint32_t> pts = ring_.Points();
         Check(h_, gd_ring_set(h_, GD_RING_DIRECTORY, pts.data(), own.data(), (uint32_t)pts.size()));
+        if (cacheOn_) {                    // membership changed: new IsValidSilo set
+            const auto mk = Masks();
+            Check(h_, gd_cache_set_silos(h_, mk.first.data(), mk.second.data(), (uint32_t)mk.first.size()));
+        }
+    }
+    std::pair<std::vector<uint8_t>, std::vector<uint8_t>> Masks() {
+        const uint32_t me = silos_.IndexOf(MyAddress);
+        std::vector<uint8_t> local(silos_.Size(), 0), valid(silos_.Size(), 0);
+        local[me] = 1;
+        for (const auto& s : ring_.Members()) valid[silos_.IndexOf(s)] = 1;
+        local.resize(silos_.Size(), 0);
+        valid.resize(silos_.Size(), 0);
+        return {local, valid};
     }
     SiloAddress RingSilo(uint32_t siloIndex) const {
         if (siloIndex == GD_NO_SILO) throw OrleansException(GD_ESTATE, "no owner");
@@ -454,6 +571,8 @@ private:
     SiloTable silos_;
     RingSnapshot ring_;
     GrainDirectoryPartition partition_;
+    AdaptiveGrainDirectoryCache cache_;
+    bool cacheOn_ = false;
 };
 
 // ------------------------------------------------------------------ dispatch stages

@@ -31,6 +31,7 @@ static int g_failures = 0;
 
 static void Run(const char* name, const std::function<void()>& f) {
     const int before = g_failures;
+    std::fprintf(stderr, "RUN %s\n", name);
     try {
         f();
     } catch (const std::exception& e) {
@@ -38,6 +39,7 @@ static void Run(const char* name, const std::function<void()>& f) {
         ++g_failures;
     }
     std::printf("%s %s\n", g_failures == before ? "PASS" : "FAIL", name);
+    std::fflush(stdout);
 }
 
 static SiloAddress Loopback(int gen) { return SiloAddress::New(127, 0, 0, 1, 0, gen); }  // SiloAddressUtils.NewLocalSiloAddress
@@ -295,6 +297,88 @@ static void DispatcherAndAgent() {
     EXPECT(total == target.size());
 }
 
+// ---------------------------------------------------------------- LruTest.cs (test/NonSilo.Tests/General)
+// The reference's LRU tests, restated against the GPU directory cache (AdaptiveGrainDirectoryCache
+// over LRU); keys "1".."n" become grains 1..n of one type.
+struct CacheFixture {
+    DispatchHandle h{0, 4096, 0};
+    LocalGrainDirectory dir{h.get(), SiloAddress::New(10, 0, 0, 1, 11111, 1)};
+    int tc = gd_calculate_id_hash("UnitTests.LruTestGrain");
+    explicit CacheFixture(uint32_t maxSize) {
+        for (int i = 2; i <= 4; ++i) dir.AddServer(SiloAddress::New(10, 0, 0, (uint8_t)i, 11111, 1));
+        dir.EnableCache(maxSize);
+    }
+    GrainId Key(int i) const { return GrainId::GetGrainId(tc, i); }
+    AdaptiveGrainDirectoryCache::Value Val(int i) const {
+        return {SiloAddress::New(10, 0, 0, 2, 11111, 1), NewActivationId(500 + i)};
+    }
+    bool Contains(int i) const {
+        for (const auto& kv : const_cast<CacheFixture*>(this)->dir.DirectoryCache().KeyValues())
+            if (std::get<0>(kv) == Key(i)) return true;
+        return false;
+    }
+};
+
+static void LruCountTest() {                 // LruTest.cs:14-29
+    CacheFixture f(10);
+    auto& c = f.dir.DirectoryCache();
+    EXPECT(c.Count() == 0);
+    c.AddOrUpdate(f.Key(1), f.Val(1), 0);
+    EXPECT(c.Count() == 1);
+    c.AddOrUpdate(f.Key(2), f.Val(2), 0);
+    EXPECT(c.Count() == 2);
+}
+
+static void LruMaximumSizeTest() {           // LruTest.cs:31-52
+    const int maxSize = 10;
+    CacheFixture f(maxSize);
+    auto& c = f.dir.DirectoryCache();
+    for (int i = 1; i <= maxSize + 5; ++i) c.AddOrUpdate(f.Key(i), f.Val(i), i);
+    EXPECT(c.Count() == maxSize);
+    for (int i = 1; i <= 5; ++i) EXPECT(!f.Contains(i));      // 'Older' entries are gone
+}
+
+static void LruUsageTest() {                 // LruTest.cs:54-88
+    const int maxSize = 10;
+    CacheFixture f(maxSize);
+    auto& c = f.dir.DirectoryCache();
+    for (int i = 1; i <= maxSize; ++i) c.AddOrUpdate(f.Key(i), f.Val(i), i);
+    AdaptiveGrainDirectoryCache::Value v;
+    int ver = 0;
+    for (int i = maxSize; i >= 1; --i) EXPECT(c.LookUp(f.Key(i), v, ver) && ver == i && v == f.Val(i));
+    c.AddOrUpdate(f.Key(maxSize + 1), f.Val(maxSize + 1), 0);
+    EXPECT(c.Count() == maxSize);
+    EXPECT(!f.Contains(maxSize));                              // the least recently used went
+    for (int i = 1; i < maxSize; ++i) EXPECT(f.Contains(i));
+    EXPECT(c.NumAccesses() == maxSize && c.NumHits() == maxSize);
+}
+
+static void PerSiloLocalLookup() {           // LocalGrainDirectory.LocalLookup, :797-837
+    CacheFixture f(100);
+    auto& part = f.dir.DirectoryPartition();
+    auto& c = f.dir.DirectoryCache();
+    int mine = -1, theirs = -1;
+    for (int k = 0; k < 200 && (mine < 0 || theirs < 0); ++k) {
+        const bool own = f.dir.CalculateTargetSilo(f.Key(k)) == f.dir.MyAddress;
+        if (own && mine < 0) mine = k;
+        if (!own && theirs < 0) theirs = k;
+    }
+    EXPECT(mine >= 0 && theirs >= 0);
+    part.AddSingleActivation(f.Key(mine), NewActivationId(1), f.dir.MyAddress);
+    AddressesAndTag r;
+    EXPECT(f.dir.LocalLookup(f.Key(mine), r) && (*r.Addresses)[0].Activation == NewActivationId(1));
+    EXPECT(!f.dir.LocalLookup(f.Key(theirs), r));              // not owned, not cached
+    EXPECT(c.NumAccesses() == 1 && c.NumHits() == 0);
+    const SiloAddress s3 = SiloAddress::New(10, 0, 0, 3, 11111, 1);
+    c.AddOrUpdate(f.Key(theirs), {s3, NewActivationId(2)}, 7);  // after a remote lookup (:920)
+    EXPECT(f.dir.LocalLookup(f.Key(theirs), r) && (*r.Addresses)[0].Silo == s3);
+    // the cached silo leaves the membership: IsValidSilo filters the hit out (:848)
+    f.dir.RemoveServer(s3);
+    EXPECT(!f.dir.LocalLookup(f.Key(theirs), r));
+    EXPECT(c.NumAccesses() == 3 && c.NumHits() == 2);
+    EXPECT(c.Remove(f.Key(theirs)) && !c.Remove(f.Key(theirs)) && c.Count() == 0);
+}
+
 static void RoutingDump(const char* path) {
     // bench silos, ring D, 20000 grains of the Ping type: owner silo index per grain (oracle-checked)
     DispatchHandle h(0, 1 << 15, 0);
@@ -334,6 +418,10 @@ int main(int argc, char** argv) {
         Run("VirtualBucketsRanges", VirtualBucketsRanges);
         Run("DirectorySemantics", DirectorySemantics);
         Run("DispatcherAndAgent", DispatcherAndAgent);
+        Run("LruCountTest", LruCountTest);
+        Run("LruMaximumSizeTest", LruMaximumSizeTest);
+        Run("LruUsageTest", LruUsageTest);
+        Run("PerSiloLocalLookup", PerSiloLocalLookup);
         if (argc > 2) Run("RoutingDump", [&] { RoutingDump(argv[2]); });
     }
     std::printf("%s (%d failure%s)\n", g_failures ? "FAILED" : "OK", g_failures, g_failures == 1 ? "" : "s");

@@ -44,3 +44,32 @@ def test_local_lookup_route():
                    (None, None, None)]
     assert (c.num_accesses, c.num_hits) == (3, 2)
     assert c.key_values()["r2"][3] == 4                  # the invalid-silo hit still renews the entry
+
+
+# LruTest.cs (test/NonSilo.Tests/General/LruTest.cs) restated on the oracle
+def test_LruCountTest():
+    c = co.DirectoryCacheOracle(10)
+    assert len(c.entries) == 0
+    c.add_or_update("1", 1, 0, 0)
+    assert len(c.entries) == 1
+    c.add_or_update("2", 2, 0, 0)
+    assert len(c.entries) == 2
+
+
+def test_LruMaximumSizeTest():
+    c = co.DirectoryCacheOracle(10)
+    for i in range(1, 16):
+        c.add_or_update(str(i), i, 0, 0)
+    assert len(c.entries) == 10
+    assert all(str(i) not in c.entries for i in range(1, 6))
+
+
+def test_LruUsageTest():
+    c = co.DirectoryCacheOracle(10)
+    for i in range(1, 11):
+        c.add_or_update(str(i), i, 0, 0)
+    for i in range(10, 0, -1):
+        c.lookup(str(i))
+    c.add_or_update("11", 11, 0, 0)
+    assert len(c.entries) == 10 and "10" not in c.entries
+    assert all(str(i) in c.entries for i in range(1, 10))

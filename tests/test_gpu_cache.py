@@ -168,3 +168,32 @@ def test_local_lookup_route_vs_oracle(gd, mode):
         assert st[i] == (o.ST_OK if ws == "OK" else o.ST_MISS) and silo[i] == wsi
     _check(e, oc)
     e.close()
+
+
+def test_lru_reference_tests(gd):
+    """LruCountTest / LruMaximumSizeTest / LruUsageTest (test/NonSilo.Tests/General/LruTest.cs) on
+    the GPU cache; keys "1".."n" are grains 1..n."""
+    e = gd.GrainDispatch(device=0, table_capacity=1024)
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in o.bench_silos(4)])
+    e.cache_configure(10, [0], 4)
+    k = lambda i: _keys([i])  # noqa: E731
+    assert e.cache_stats()["count"] == 0
+    e.cache_add(k(1), [1], [1], [0])
+    assert e.cache_stats()["count"] == 1
+    e.cache_add(k(2), [2], [1], [0])
+    assert e.cache_stats()["count"] == 2
+    e.cache_clear()
+    for i in range(1, 16):                                  # LruMaximumSizeTest
+        e.cache_add(k(i), [i], [1], [0])
+    ent = e.cache_entries()
+    assert len(ent) == 10 and all(tuple(int(x) for x in k(i)[0]) not in ent for i in range(1, 6))
+    e.cache_clear()
+    for i in range(1, 11):                                  # LruUsageTest
+        e.cache_add(k(i), [i], [1], [0])
+    for i in range(10, 0, -1):
+        assert e.cache_lookup(k(i))[0][0] == 1
+    e.cache_add(k(11), [11], [1], [0])
+    ent = e.cache_entries()
+    assert len(ent) == 10 and tuple(int(x) for x in k(10)[0]) not in ent
+    assert all(tuple(int(x) for x in k(i)[0]) in ent for i in range(1, 10))
+    e.close()

@@ -30,10 +30,11 @@ def test_host_cpp_identity_cpu():
 def test_host_cpp_gpu(tmp_path):
     _build()
     dump = tmp_path / "route_dump.txt"
-    p = subprocess.run([BIN, "all", str(dump)], capture_output=True, text=True, timeout=600)
+    p = subprocess.run([BIN, "all", str(dump)], capture_output=True, text=True, timeout=150)
     assert p.returncode == 0, p.stdout + p.stderr
     for name in ("RingStandalone_Basic", "RingStandalone_Failures", "RingStandalone_Joins", "RingStandalone_Mixed",
-                 "VirtualBucketsRanges", "DirectorySemantics", "DispatcherAndAgent", "RoutingDump"):
+                 "VirtualBucketsRanges", "DirectorySemantics", "DispatcherAndAgent", "LruCountTest",
+                 "LruMaximumSizeTest", "LruUsageTest", "PerSiloLocalLookup", "RoutingDump"):
         assert f"PASS {name}" in p.stdout, p.stdout + p.stderr
     rows = np.loadtxt(dump, dtype=np.int64)
     tc = o.grain_type_code(o.PING_GRAIN_CLASS)
