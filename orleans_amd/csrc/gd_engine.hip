@@ -17,6 +17,7 @@
 #include "gd_churn.h"
 #include "gd_fanout.h"
 #include "gd_cache.h"
+#include "gd_shard.h"
 #include "gd_frames.h"
 #include "graindispatch.h"
 
@@ -72,6 +73,7 @@ struct gd_handle {
     uint32_t cache_nsilos = 0;
     DevBuf cache_local, cache_valid;
     DevBuf cbuf[8];                   // cache scratch
+    DevBuf shard_dest, shard_hist;    // exchange partition scratch
     uint64_t routed = 0;
 
     // kernel tuning (defaults measured on MI355X; GD_ROUTE_M / GD_ROUTE_NT override for A/B runs)
@@ -433,6 +435,63 @@ int maybe_grow_table(gd_handle* h, uint64_t incoming) {
     return gd_dir_rehash(h, cap);
 }
 
+// ---- exchange partition (gd_shard.h) -------------------------------------------------
+template <int MODE, bool NODES>
+int shard_hist_t(gd_handle* h, const void* recs, uint32_t n, uint64_t tcd, uint32_t n_shards, uint32_t tiles,
+                 uint8_t* dest, uint32_t* hist) {
+    return launch(h, "k_shard_hist", dim3(tiles), dim3(SH_NT), ring_lds(h), k_shard_hist<MODE, NODES>, recs, n, tcd,
+                  ring_args(h), n_shards, tiles, dest, hist);
+}
+
+template <int BITS, bool NODES>
+int shard_scatter_t(gd_handle* h, const void* recs, const uint32_t* payload, const uint8_t* dest, uint32_t n,
+                    uint32_t n_shards, uint32_t tiles, const uint32_t* gscan, void* out, uint32_t* out_pay) {
+    return launch(h, "k_shard_scatter", dim3(tiles), dim3(SH_NT), 0, k_shard_scatter<BITS, NODES>, recs, payload, dest,
+                  n, n_shards, tiles, gscan, out, out_pay);
+}
+
+// Stable partition of n records (gd_key or u32 node ids) by destination rank, payload alongside
+// (payload == nullptr: the batch index); counts[d] per destination.
+template <bool NODES>
+int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t n, uint64_t tcd, uint32_t n_shards,
+               void* out_recs, uint32_t* out_pay, uint32_t* counts) {
+    GD_TRY(check_ring(h));
+    if (n == 0)
+        return launch(h, "k_fill", dim3(1), dim3(BLOCK), 0, k_fill_u32, counts, n_shards, 0u);
+    const uint32_t tiles = blocks_for(n, SH_TILE);
+    if ((uint64_t)tiles * n_shards > 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "batch too large to partition");
+    GD_TRY(ensure(h, h->shard_dest, (size_t)n));
+    GD_TRY(ensure(h, h->shard_hist, (size_t)tiles * n_shards * 4));
+    uint8_t* dest = (uint8_t*)h->shard_dest.p;
+    uint32_t* hist = (uint32_t*)h->shard_hist.p;
+    switch (h->ring_mode) {
+        case GD_RING_DIRECTORY:
+            GD_TRY((shard_hist_t<GD_RING_DIRECTORY, NODES>(h, recs, n, tcd, n_shards, tiles, dest, hist)));
+            break;
+        case GD_RING_CONSISTENT:
+            GD_TRY((shard_hist_t<GD_RING_CONSISTENT, NODES>(h, recs, n, tcd, n_shards, tiles, dest, hist)));
+            break;
+        default:
+            GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, tiles, dest, hist)));
+    }
+    GD_TRY(scan_device<OpAdd>(h, hist, tiles * n_shards, false, false, "shard"));
+    GD_TRY(launch(h, "k_shard_counts", dim3(1), dim3(256), 0, k_shard_counts, (const uint32_t*)hist, tiles, n_shards, n,
+                  counts));
+    uint32_t bits = 1;
+    while ((1u << bits) < n_shards) ++bits;
+    const uint32_t* gs = hist;
+    switch (bits) {
+        case 1: return shard_scatter_t<1, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
+        case 2: return shard_scatter_t<2, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
+        case 3: return shard_scatter_t<3, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
+        case 4: return shard_scatter_t<4, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
+        case 5: return shard_scatter_t<5, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
+        case 6: return shard_scatter_t<6, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
+        case 7: return shard_scatter_t<7, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
+        default: return shard_scatter_t<8, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
+    }
+}
+
 }  // namespace
 
 // ================================================================== C ABI
@@ -503,6 +562,8 @@ void gd_destroy(gd_handle* h) {
     for (DevBuf& b : h->fan) free_buf(b);
     for (DevBuf& b : h->cbuf) free_buf(b);
     free_buf(h->cache_local);
+    free_buf(h->shard_dest);
+    free_buf(h->shard_hist);
     free_buf(h->cache_valid);
     if (h->cslots) (void)hipFree(h->cslots);
     if (h->cctr) (void)hipFree(h->cctr);
@@ -799,26 +860,7 @@ int gd_pack_by_shard_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint
                             uint32_t* d_send_idx, uint32_t* d_counts) {
     if (!h || !d_counts || (n && (!d_keys || !d_send_keys || !d_send_idx))) return set_err(h, GD_EINVAL, "null argument");
     if (n_shards == 0 || n_shards > 256) return set_err(h, GD_EINVAL, "n_shards %u not in [1, 256]", n_shards);
-    GD_TRY(check_ring(h));
-    GD_TRY(ensure(h, h->out_b, (size_t)n * 4 + 4));                 // dest
-    GD_TRY(ensure(h, h->offs, ((size_t)n_shards + 2) * 4));
-    uint32_t* dest = (uint32_t*)h->out_b.p;
-    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
-    const RingArgs r = ring_args(h);
-    if (n) {
-        if (h->ring_mode == GD_RING_DIRECTORY)
-            GD_TRY(launch(h, "k_shard_dest", g, b, ring_lds(h), k_shard_dest<GD_RING_DIRECTORY>, d_keys, n, r, n_shards, dest));
-        else if (h->ring_mode == GD_RING_CONSISTENT)
-            GD_TRY(launch(h, "k_shard_dest", g, b, ring_lds(h), k_shard_dest<GD_RING_CONSISTENT>, d_keys, n, r, n_shards, dest));
-        else
-            GD_TRY(launch(h, "k_shard_dest", g, b, ring_lds(h), k_shard_dest<GD_RING_VIRTUAL_BUCKETS>, d_keys, n, r,
-                          n_shards, dest));
-    }
-    GD_TRY(bucket_device(h, dest, n, n_shards, d_send_idx, (uint32_t*)h->offs.p));
-    if (n)
-        GD_TRY(launch(h, "k_gather_keys", g, b, 0, k_gather_keys, d_keys, (const uint32_t*)d_send_idx, n, d_send_keys));
-    return launch(h, "k_counts", dim3(1), dim3(BLOCK), 0, k_counts_from_offsets, (const uint32_t*)h->offs.p, n_shards,
-                  d_counts);
+    return shard_pack<false>(h, d_keys, nullptr, n, 0, n_shards, d_send_keys, d_send_idx, d_counts);
 }
 
 int gd_kernel_times(gd_handle* h, gd_kernel_time* out, uint32_t max, uint32_t* out_n) {
@@ -1462,32 +1504,8 @@ int gd_pack_nodes_by_shard_device(gd_handle* h, const uint32_t* d_nodes, const u
     if (!h || !d_counts || (n && (!d_nodes || !d_payload || !d_send_nodes || !d_send_payload)))
         return set_err(h, GD_EINVAL, "null argument");
     if (n_shards == 0 || n_shards > 256) return set_err(h, GD_EINVAL, "n_shards %u not in [1, 256]", n_shards);
-    GD_TRY(check_ring(h));
-    GD_TRY(ensure(h, h->out_b, (size_t)n * 4 + 4));                 // dest
-    GD_TRY(ensure(h, h->out_a, (size_t)n * 4 + 4));                 // perm
-    GD_TRY(ensure(h, h->offs, ((size_t)n_shards + 2) * 4));
-    uint32_t* dest = (uint32_t*)h->out_b.p;
-    uint32_t* perm = (uint32_t*)h->out_a.p;
-    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
-    const RingArgs r = ring_args(h);
-    const uint64_t tcd = grain_tcd(type_code);
-    if (n) {
-        if (h->ring_mode == GD_RING_DIRECTORY)
-            GD_TRY(launch(h, "k_node_shard_dest", g, b, ring_lds(h), k_node_shard_dest<GD_RING_DIRECTORY>, d_nodes, n,
-                          tcd, r, n_shards, dest));
-        else if (h->ring_mode == GD_RING_CONSISTENT)
-            GD_TRY(launch(h, "k_node_shard_dest", g, b, ring_lds(h), k_node_shard_dest<GD_RING_CONSISTENT>, d_nodes, n,
-                          tcd, r, n_shards, dest));
-        else
-            GD_TRY(launch(h, "k_node_shard_dest", g, b, ring_lds(h), k_node_shard_dest<GD_RING_VIRTUAL_BUCKETS>,
-                          d_nodes, n, tcd, r, n_shards, dest));
-    }
-    GD_TRY(bucket_device(h, dest, n, n_shards, perm, (uint32_t*)h->offs.p));
-    if (n)
-        GD_TRY(launch(h, "k_gather_pairs", g, b, 0, k_gather_pairs, d_nodes, d_payload, (const uint32_t*)perm, n,
-                      d_send_nodes, d_send_payload));
-    return launch(h, "k_counts", dim3(1), dim3(BLOCK), 0, k_counts_from_offsets, (const uint32_t*)h->offs.p, n_shards,
-                  d_counts);
+    return shard_pack<true>(h, d_nodes, d_payload, n, grain_tcd(type_code), n_shards, d_send_nodes, d_send_payload,
+                            d_counts);
 }
 
 int gd_frontier_next_device(gd_handle* h, const uint32_t* d_offsets, uint32_t n_act, uint8_t* d_visited,

@@ -233,29 +233,4 @@ __global__ void __launch_bounds__(BLOCK) k_frontier_emit(const uint32_t* __restr
     if (a < n_act && flag[a]) out[pos[a] - 1] = a;
 }
 
-// Destination shard of GrainId(typeCode, node) (owner silo % n_shards), for the exchange.
-template <int MODE>
-__global__ void __launch_bounds__(BLOCK) k_node_shard_dest(const uint32_t* __restrict__ nodes, uint32_t n,
-                                                           uint64_t tcd, RingArgs ring, uint32_t n_shards,
-                                                           uint32_t* __restrict__ dest) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
-    uint32_t* s_pts = s_ring;
-    uint32_t* s_own = s_ring + ring.n;
-    stage_ring(ring, s_pts, s_own);
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(0, nodes[i], tcd))];
-    dest[i] = silo % n_shards;
-}
-
-__global__ void __launch_bounds__(BLOCK) k_gather_pairs(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
-                                                        const uint32_t* __restrict__ perm, uint32_t n,
-                                                        uint32_t* __restrict__ out_a, uint32_t* __restrict__ out_b) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t j = perm[i];
-    out_a[i] = a[j];
-    out_b[i] = b[j];
-}
-
 }  // namespace gd

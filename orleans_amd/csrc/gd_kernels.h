@@ -322,39 +322,6 @@ __global__ void __launch_bounds__(BLOCK) k_ring_hashes(const uint32_t* __restric
     out_silo[i] = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, hashes[i])];
 }
 
-// Destination shard of each message (owner silo % n_shards) for the exchange.
-template <int MODE>
-__global__ void __launch_bounds__(BLOCK) k_shard_dest(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
-                                                      uint32_t n_shards, uint32_t* __restrict__ dest) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
-    uint32_t* s_pts = s_ring;
-    uint32_t* s_own = s_ring + ring.n;
-    stage_ring(ring, s_pts, s_own);
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
-    const uint64_t n0 = kp[0], n1 = kp[1], tcd = kp[2];
-    const uint32_t cat = (uint32_t)(tcd >> 56);
-    uint32_t silo;
-    if (cat == CAT_SYSTEM_TARGET || cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) silo = ring.my_silo;
-    else if (is_membership(n0, n1, tcd)) silo = ring.seed_silo;
-    else silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(n0, n1, tcd))];
-    dest[i] = (silo == NONE32 ? ring.my_silo : silo) % n_shards;
-}
-
-__global__ void __launch_bounds__(BLOCK) k_gather_keys(const gd_key* __restrict__ keys,
-                                                       const uint32_t* __restrict__ perm, uint32_t n,
-                                                       gd_key* __restrict__ out) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    out[i] = keys[perm[i]];
-}
-
-__global__ void k_counts_from_offsets(const uint32_t* __restrict__ off, uint32_t m, uint32_t* __restrict__ counts) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < m) counts[i] = off[i + 1] - off[i];
-}
-
 // ------------------------------------------------------------------ directory maintenance
 // AddSingleActivation (GrainDirectoryPartition.cs:304-326, GrainInfo :110-124) for a batch.
 // Phase 1: find the key's slot or claim an empty one.  A lane that meets a slot

@@ -1,0 +1,215 @@
+// gd_shard.h -- gfx950 device code for the exchange partition (SURVEY 8 a14 / e): a stable
+// partition of message records by destination rank (owner silo % n_shards), the per-target-silo
+// outbound queues of OutboundMessageQueue.SendMessage (OutboundMessageQueue.cs:54-131) laid out
+// as the contiguous per-destination chunks an all-to-all-v sends.
+//
+// Two kernels per batch (plus one scan):
+//   k_shard_hist    ring owner of every record -> dest byte, per-tile destination counts
+//   scan            digit-major exclusive scan: (dest, tile) -> global base
+//   k_shard_scatter stable rank in the tile by ballot matching, the records (24-B keys or 4-B
+//                   node ids) and a 4-B payload staged in LDS in destination order, then written
+//                   run by run (coalesced)
+// The records move once (read 24 B, write 24 B + 4 B); the earlier form (radix pass over a dest
+// array, then a gather of the keys through the permutation) read each key twice, the second
+// time at 1/n_shards density.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gd_common.h"
+#include "gd_kernels.h"
+
+namespace gd {
+
+constexpr int SH_NT = 256;
+constexpr int SH_IT = 8;
+constexpr uint32_t SH_TILE = SH_NT * SH_IT;   // 2048 records per tile
+
+template <int MODE>
+__device__ __forceinline__ uint32_t key_dest(uint64_t n0, uint64_t n1, uint64_t tcd, const uint32_t* s_pts,
+                                             const uint32_t* s_own, const RingArgs& ring, uint32_t n_shards) {
+    const uint32_t cat = (uint32_t)(tcd >> 56);
+    uint32_t silo;
+    if (cat == CAT_SYSTEM_TARGET || cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) silo = ring.my_silo;
+    else if (is_membership(n0, n1, tcd)) silo = ring.seed_silo;
+    else silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(n0, n1, tcd))];
+    return (silo == NONE32 ? ring.my_silo : silo) % n_shards;
+}
+
+// Item (w, r, lane) of a tile <-> record base + (w * SH_IT + r) * 64 + lane, as in k_radix_scatter.
+template <int MODE, bool NODES>
+__global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ recs, uint32_t n, uint64_t tcd,
+                                                      RingArgs ring, uint32_t n_shards, uint32_t tiles,
+                                                      uint8_t* __restrict__ dest, uint32_t* __restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    __shared__ uint32_t s_cnt[256];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    for (uint32_t d = threadIdx.x; d < 256; d += SH_NT) s_cnt[d] = 0;
+    stage_ring(ring, s_pts, s_own);
+    const uint32_t base = blockIdx.x * SH_TILE;
+    const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+#pragma unroll
+    for (int r = 0; r < SH_IT; ++r) {
+        const uint32_t i = base + (w * SH_IT + r) * WAVE + lane;
+        if (i >= n) continue;
+        uint32_t d;
+        if constexpr (NODES) {
+            const uint32_t node = reinterpret_cast<const uint32_t*>(recs)[i];
+            d = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(0, node, tcd))] % n_shards;
+        } else {
+            const uint64_t* kp = reinterpret_cast<const uint64_t*>(recs) + 3ull * i;
+            d = key_dest<MODE>(kp[0], kp[1], kp[2], s_pts, s_own, ring, n_shards);
+        }
+        dest[i] = (uint8_t)d;
+        atomicAdd(&s_cnt[d], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < n_shards; d += SH_NT) hist[d * tiles + blockIdx.x] = s_cnt[d];
+}
+
+// payload_in == nullptr: the payload is the record's batch index (the origin index).
+template <int BITS, bool NODES>
+__global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict__ recs,
+                                                         const uint32_t* __restrict__ payload_in,
+                                                         const uint8_t* __restrict__ dest, uint32_t n,
+                                                         uint32_t n_shards, uint32_t tiles,
+                                                         const uint32_t* __restrict__ gscan,
+                                                         void* __restrict__ out_recs,
+                                                         uint32_t* __restrict__ out_payload) {
+    constexpr uint32_t R = 1u << BITS;
+    constexpr int NW = SH_NT / WAVE;
+    constexpr int RW = NODES ? 1 : 3;           // 8-B words per record (keys) / one u32 (nodes)
+    __shared__ uint32_t s_wcnt[NW][R];
+    __shared__ uint32_t s_lstart[R];
+    __shared__ uint32_t s_gbase[R];
+    __shared__ uint32_t s_wsum[NW];
+    __shared__ uint64_t s_key[NODES ? 1 : 3][NODES ? 1 : SH_TILE];
+    __shared__ uint32_t s_node[NODES ? SH_TILE : 1];
+    __shared__ uint32_t s_pay[SH_TILE];
+    __shared__ uint8_t s_dig[SH_TILE];
+
+    const uint32_t tile = blockIdx.x;
+    const uint32_t base = tile * SH_TILE;
+    const uint32_t cnt_tile = min(SH_TILE, n - base);
+    for (uint32_t d = threadIdx.x; d < R; d += SH_NT) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) s_wcnt[w][d] = 0;
+        s_gbase[d] = d < n_shards ? gscan[d * tiles + tile] : 0u;   // no record has a digit >= n_shards
+    }
+    const uint32_t lane = lane_id();
+    const uint32_t w = threadIdx.x / WAVE;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    uint32_t dd[SH_IT], rk[SH_IT], pay[SH_IT];
+    uint64_t kv[SH_IT][RW];
+#pragma unroll
+    for (int r = 0; r < SH_IT; ++r) {
+        const uint32_t idx = base + (w * SH_IT + r) * WAVE + lane;
+        const uint32_t li = min(idx, n - 1);
+        dd[r] = dest[li];
+        if constexpr (NODES) {
+            kv[r][0] = reinterpret_cast<const uint32_t*>(recs)[li];
+        } else {
+            const uint64_t* kp = reinterpret_cast<const uint64_t*>(recs) + 3ull * li;
+            kv[r][0] = kp[0];
+            kv[r][1] = kp[1];
+            kv[r][2] = kp[2];
+        }
+        pay[r] = payload_in ? payload_in[li] : idx;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SH_IT; ++r) {
+        const uint32_t idx = base + (w * SH_IT + r) * WAVE + lane;
+        const bool valid = idx < n;
+        const uint32_t d = dd[r] & (R - 1);
+        const unsigned long long peers = match_digit<BITS>(d, valid);
+        uint32_t c = 0;
+        if (valid) c = s_wcnt[w][d];
+        rk[r] = c + (uint32_t)__popcll(peers & lt);
+        if (valid && (peers & lt) == 0) s_wcnt[w][d] = c + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    // cross-wave exclusive prefix per digit, then tile-local digit starts
+    constexpr uint32_t DPT = (R + SH_NT - 1) / SH_NT;
+    uint32_t my_total = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < DPT; ++q) {
+        const uint32_t d = threadIdx.x * DPT + q;
+        if (d < R) {
+            uint32_t run = 0;
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) {
+                const uint32_t t = s_wcnt[ww][d];
+                s_wcnt[ww][d] = run;
+                run += t;
+            }
+            s_lstart[d] = run;
+            my_total += run;
+        }
+    }
+    const uint32_t ex = block_excl_scan_add_n<SH_NT>(my_total, s_wsum);
+    {
+        uint32_t run = ex;
+#pragma unroll
+        for (uint32_t q = 0; q < DPT; ++q) {
+            const uint32_t d = threadIdx.x * DPT + q;
+            if (d < R) {
+                const uint32_t t = s_lstart[d];
+                s_lstart[d] = run;
+                run += t;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SH_IT; ++r) {
+        const uint32_t idx = base + (w * SH_IT + r) * WAVE + lane;
+        if (idx < n) {
+            const uint32_t d = dd[r] & (R - 1);
+            const uint32_t p = s_lstart[d] + s_wcnt[w][d] + rk[r];
+            if constexpr (NODES) {
+                s_node[p] = (uint32_t)kv[r][0];
+            } else {
+                s_key[0][p] = kv[r][0];
+                s_key[1][p] = kv[r][1];
+                s_key[2][p] = kv[r][2];
+            }
+            s_pay[p] = pay[r];
+            s_dig[p] = (uint8_t)d;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SH_IT; ++j) {
+        const uint32_t p = j * SH_NT + threadIdx.x;
+        if (p < cnt_tile) {
+            const uint32_t d = s_dig[p];
+            const uint32_t g = s_gbase[d] + (p - s_lstart[d]);
+            if (g < n) {            // always true when the scan is right; never write out of bounds
+                if constexpr (NODES) {
+                    reinterpret_cast<uint32_t*>(out_recs)[g] = s_node[p];
+                } else {
+                    uint64_t* o = reinterpret_cast<uint64_t*>(out_recs) + 3ull * g;
+                    o[0] = s_key[0][p];
+                    o[1] = s_key[1][p];
+                    o[2] = s_key[2][p];
+                }
+                out_payload[g] = s_pay[p];
+            }
+        }
+    }
+}
+
+// counts[d] = records for destination d, from the scanned (dest, tile) bases.
+__global__ void k_shard_counts(const uint32_t* __restrict__ gscan, uint32_t tiles, uint32_t n_shards, uint32_t n,
+                               uint32_t* __restrict__ counts) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= n_shards) return;
+    const uint32_t start = gscan[d * tiles];
+    const uint32_t end = d + 1 < n_shards ? gscan[(d + 1) * tiles] : n;
+    counts[d] = end - start;
+}
+
+}  // namespace gd

@@ -703,3 +703,37 @@ def test_dir_split_device_and_full_size(gd):
     np.testing.assert_array_equal(gv[:, 1], ws)
     assert e.stats()["table_live"] == G - n
     e.close()
+
+
+@pytest.mark.parametrize("n", [0, 1, 2047, 2048, 2049, 100003])
+def test_pack_by_shard_vs_oracle(gd, n):
+    """gd_pack_by_shard_device (the exchange partition, OutboundMessageQueue.cs:54-131 per target
+    silo): stable partition of the 24-B headers by owner silo % n_shards, origin indices alongside;
+    system targets / KeyExt go to my silo's rank, the membership grain to the seed's."""
+    import torch
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    rng = np.random.default_rng(n + 5)
+    keys = o.grain_keys(TC, rng.integers(-5000, 5000, size=n))
+    if n > 10:
+        keys[::7] = np.array(o.UniqueKey(0, 7, o.type_code_data(o.CAT_SYSTEM_TARGET, 1)).as_tuple(), dtype=np.uint64)
+        keys[3::11] = np.array(o.MEMBERSHIP_TABLE_ID.as_tuple(), dtype=np.uint64)
+        keys[5::13, 2] = np.uint64(o.type_code_data(o.CAT_KEYEXT_GRAIN, 77))
+    e = _engine(gd, silos, "D", my_silo=3, seed_silo=6)
+    dev = torch.device("cuda", 0)
+    tk = torch.from_numpy(keys.view(np.int64).copy()).to(dev)
+    st, silo, act, owner, h = o.route_batch_np(keys, spec, o.DirectoryArrays(np.zeros((0, 3), np.uint64), [], []),
+                                               my_silo=3, seed_silo=6)
+    owner = np.where(st == o.ST_KEYEXT, 3, owner).astype(np.int64)
+    for shards in (1, 2, 3, 8, 13, 256):
+        sk = torch.empty_like(tk)
+        si = torch.empty(n, dtype=torch.int32, device=dev)
+        cnt = torch.empty(shards, dtype=torch.int32, device=dev)
+        e.pack_by_shard_device(tk.data_ptr(), n, shards, sk.data_ptr(), si.data_ptr(), cnt.data_ptr())
+        torch.cuda.synchronize()
+        dest = (owner % shards).astype(np.uint32)
+        perm, off = o.bucket_stable(dest, shards)
+        np.testing.assert_array_equal(si.cpu().numpy().view(np.uint32), perm)
+        np.testing.assert_array_equal(sk.cpu().numpy().view(np.uint64).reshape(-1, 3), keys[perm])
+        np.testing.assert_array_equal(cnt.cpu().numpy(), np.diff(off[:shards + 1]))
+    e.close()
