@@ -30,7 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from orleans_amd import graindispatch as g          # noqa: E402
-from orleans_amd.sharded import DeviceEngine, ShardedRouter  # noqa: E402
+from orleans_amd.sharded import DeviceEngine, LibraryRouter, ShardedRouter, same_result  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # 8 silos 10.0.0.{1..8}:11111.  "literal" = generation 1; its ring gives
@@ -97,6 +97,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=5, help="extra steps with per-kernel events")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "library", "torch"],
+                    help="N>1: RCCL exchange inside libgraindispatch (gd_route_multi_device) or torch.distributed "
+                         "all_to_all_single; auto = library once it matches torch bit for bit on the first batch")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo, host-staged all-to-all")
     args = ap.parse_args()
@@ -155,6 +158,26 @@ def main():
     engine = DeviceEngine(e, dev)
     router = ShardedRouter(engine, stage_via_cpu=args.rehearse_one_gpu)
     stream = engine.stream
+    exchange = "none" if world == 1 else "torch.distributed all_to_all_single (RCCL)"
+    if not args.rehearse_one_gpu and ((world > 1 and args.exchange != "torch") or args.exchange == "library"):
+        # the in-library exchange, checked bit for bit against the torch exchange on the first batch
+        try:
+            lib_router = LibraryRouter(engine)
+            with torch.cuda.stream(stream):
+                ok = same_result(lib_router.route_bucket(keys, n_act), router.route_bucket(keys, n_act))
+                torch.cuda.synchronize()
+            agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(agree, op=dist.ReduceOp.MIN)
+            if int(agree.item()) == 1:
+                router = lib_router
+                exchange = "libgraindispatch gd_route_multi_device (grouped RCCL send/recv)"
+            else:
+                exchange = "torch.distributed all_to_all_single (RCCL); library exchange disagreed on batch 1"
+                assert args.exchange != "library", "library exchange disagrees with the torch exchange"
+        except Exception as ex:   # noqa: BLE001 -- reported in the JSON line, torch exchange used instead
+            if args.exchange == "library":
+                raise
+            exchange = f"torch.distributed all_to_all_single (RCCL); library exchange failed: {ex!r}"[:300]
 
     def step():
         return router.route_bucket(keys, n_act)
@@ -215,7 +238,7 @@ def main():
                          "frac_hbm": round(gbs / PEAK_HBM_GBS, 4) if gbs else None}
     roofline = None
     if kernels:
-        dom = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
+        dom = max((k for k in kernels if not k.startswith("rccl_")), key=lambda k: kernels[k]["ms_per_step"])
         d = kernels[dom]
         launches = max(1, d["launches_per_step"])
         traffic = None
@@ -258,6 +281,7 @@ def main():
                        "table_load": round(n_act / cap, 3), "parallelism": f"shard{world}"},
             "routed_ok_last_step_rank0": st_ok,
             "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
+            "exchange": exchange,
             "roofline": roofline,
             "kernels": kernels,
             "cpu_baseline": cpu,

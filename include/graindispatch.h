@@ -213,6 +213,53 @@ int gd_ring_owner_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_
 int gd_pack_by_shard_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_shards,
                             gd_key* d_send_keys, uint32_t* d_send_idx, uint32_t* d_counts);
 
+/* ---- in-library exchange over RCCL (SURVEY 8 b gd_route_multi, 8 e) ------------------
+ * One process (one handle) per GPU.  Rank r hosts the directory partitions of silos
+ * s with s % n_ranks == r (GrainDirectoryPartition per silo, LocalGrainDirectory.cs:477-545).
+ * gd_route_multi sends each message of a rank's batch to the rank owning its grain
+ * (the per-target-silo outbound queues of OutboundMessageQueue.SendMessage,
+ * OutboundMessageQueue.cs:54-131, as one grouped RCCL send/recv over xGMI), probes the
+ * directory and buckets per activation there (IncomingMessageAgent.cs:92-190), and with
+ * return_routes sends (silo, act, status) back so the sender holds each of its messages'
+ * target address in batch order (Dispatcher.AddressMessage, Dispatcher.cs:715-767).
+ * RCCL is loaded at run time (librccl.so.1); without it these return GD_ERCCL.
+ * The unique id (128 B) is created by one rank and handed to the others by the host
+ * (any out-of-band channel); gd_comm_init is collective over all ranks. */
+#define GD_COMM_ID_BYTES 128
+int gd_comm_unique_id(uint8_t out_id[GD_COMM_ID_BYTES]);
+int gd_comm_init(gd_handle* h, const uint8_t id[GD_COMM_ID_BYTES], int n_ranks, int rank);
+int gd_comm_destroy(gd_handle* h);
+
+/* Results of the last gd_route_multi* call on a handle: device pointers into library-owned
+ * buffers, valid until the next gd_route_multi* / gd_comm_destroy / gd_destroy.  The received
+ * messages are in arrival order = (sender rank, sender batch order); perm / offsets are the
+ * stable per-activation bucketing of that order (offsets: n_act + 2 entries). */
+typedef struct gd_multi_result {
+    uint32_t        n_recv;       /* messages this rank owns in this batch            */
+    uint32_t        n_act;
+    const gd_key*   recv_keys;    /* [n_recv]                                         */
+    const uint32_t* recv_idx;     /* [n_recv] index in the sender's batch             */
+    const uint32_t* recv_src;     /* [n_recv] sender rank                             */
+    const uint32_t* silo;         /* [n_recv] route results on the owner              */
+    const uint32_t* act;
+    const uint8_t*  status;
+    const uint32_t* perm;         /* [n_recv]                                         */
+    const uint32_t* offsets;      /* [n_act + 2]                                      */
+    const uint32_t* ret_silo;     /* [n] in this rank's batch order (return_routes)   */
+    const uint32_t* ret_act;
+    const uint8_t*  ret_status;
+} gd_multi_result;
+
+int gd_route_multi_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int return_routes,
+                          gd_multi_result* out);
+/* Host keys in (C# pinned array); results stay on the device -> gd_multi_fetch. */
+int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, int return_routes,
+                   gd_multi_result* out);
+/* Copy the last result to host arrays sized from gd_multi_result (any pointer may be NULL). */
+int gd_multi_fetch(gd_handle* h, gd_key* recv_keys, uint32_t* recv_idx, uint32_t* recv_src, uint32_t* silo,
+                   uint32_t* act, uint8_t* status, uint32_t* perm, uint32_t* offsets, uint32_t* ret_silo,
+                   uint32_t* ret_act, uint8_t* ret_status);
+
 /* ---- micro-batch latency path (BASELINE config 5) ----------------------
  * Small batches (e.g. 4k messages: Presence / GPSTracker traffic,
  * Samples/GPSTracker/GPSTracker.GrainImplementation/DeviceGrain.cs:18-37) pay launch

@@ -18,6 +18,7 @@
 #include "gd_fanout.h"
 #include "gd_cache.h"
 #include "gd_shard.h"
+#include "gd_comm.h"
 #include "gd_frames.h"
 #include "graindispatch.h"
 
@@ -74,6 +75,14 @@ struct gd_handle {
     DevBuf cache_local, cache_valid;
     DevBuf cbuf[8];                   // cache scratch
     DevBuf shard_dest, shard_hist;    // exchange partition scratch
+
+    // in-library exchange over RCCL (gd_comm.h): one communicator per handle
+    ncclComm_t comm = nullptr;
+    int n_ranks = 0, rank = -1;
+    DevBuf mx[20];                    // send/recv/result buffers of gd_route_multi*
+    uint32_t* h_xcnt = nullptr;       // pinned: send counts, recv counts, recv offsets
+    gd_multi_result mres{};
+    uint32_t mres_n = 0;              // sender-side batch size of the last result
     uint64_t routed = 0;
 
     // kernel tuning (defaults measured on MI355X; GD_ROUTE_M / GD_ROUTE_NT override for A/B runs)
@@ -564,6 +573,9 @@ void gd_destroy(gd_handle* h) {
     free_buf(h->cache_local);
     free_buf(h->shard_dest);
     free_buf(h->shard_hist);
+    if (h->comm) (void)rccl().CommDestroy(h->comm);
+    for (DevBuf& b : h->mx) free_buf(b);
+    if (h->h_xcnt) (void)hipHostFree(h->h_xcnt);
     free_buf(h->cache_valid);
     if (h->cslots) (void)hipFree(h->cslots);
     if (h->cctr) (void)hipFree(h->cctr);
@@ -1937,6 +1949,264 @@ int gd_cache_entries(gd_handle* h, gd_key* keys, gd_val* vals, int32_t* versions
     HIP_TRY(h, hipMemcpyAsync(vals, dv, (size_t)total * sizeof(gd_val), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(h, hipMemcpyAsync(versions, dver, (size_t)total * 4, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(h, hipMemcpyAsync(generations, dg, (size_t)total * 8, hipMemcpyDeviceToHost, h->stream));
+    return sync(h);
+}
+
+// ================================================================== in-library exchange (RCCL)
+namespace {
+
+#define NCCL_TRY(h, expr)                                                                          \
+    do {                                                                                           \
+        ncclResult_t r_ = (expr);                                                                  \
+        if (r_ != ncclSuccess)                                                                     \
+            return set_err((h), GD_ERCCL, "%s: %s", #expr, rccl().GetErrorString(r_));             \
+    } while (0)
+
+int need_comm(gd_handle* h) {
+    if (!h->comm) return set_err(h, GD_ESTATE, "no communicator (gd_comm_init)");
+    return GD_OK;
+}
+
+// One grouped send/recv round: for every peer r, send sc[r] elements at soff[r] of each send
+// array and receive rc[r] elements at roff[r] of each recv array (both sides skip empty chunks,
+// which they agree on: my count to r is r's count from me).  With per-kernel timing the round is
+// bracketed by events under `name`.
+struct Lane {
+    const void* send;
+    void* recv;
+    size_t elem;            // bytes per element
+    ncclDataType_t type;
+    size_t per;             // elements of `type` per element
+};
+
+int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uint64_t* soff, const uint32_t* rc,
+                   const uint64_t* roff, const Lane* lanes, int n_lanes) {
+    const Rccl& R = rccl();
+    hipEvent_t a = nullptr, b = nullptr;
+    if (h->timing) {
+        a = take_event(h);
+        b = take_event(h);
+        HIP_TRY(h, hipEventRecord(a, h->stream));
+    }
+    NCCL_TRY(h, R.GroupStart());
+    for (int r = 0; r < h->n_ranks; ++r) {
+        for (int l = 0; l < n_lanes; ++l) {
+            const Lane& L = lanes[l];
+            if (sc[r])
+                NCCL_TRY(h, R.Send((const uint8_t*)L.send + soff[r] * L.elem, (size_t)sc[r] * L.per, L.type, r,
+                                   h->comm, h->stream));
+            if (rc[r])
+                NCCL_TRY(h, R.Recv((uint8_t*)L.recv + roff[r] * L.elem, (size_t)rc[r] * L.per, L.type, r, h->comm,
+                                   h->stream));
+        }
+    }
+    NCCL_TRY(h, R.GroupEnd());
+    if (h->timing) {
+        HIP_TRY(h, hipEventRecord(b, h->stream));
+        h->pending.push_back(TimedLaunch{name_id(h, name), a, b});
+    }
+    return GD_OK;
+}
+
+// Sender batch d_keys[n] -> owner ranks (exchange) -> route + bucket there (-> routes back).
+int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, bool ret, gd_multi_result* out) {
+    GD_TRY(need_comm(h));
+    GD_TRY(check_ring(h));
+    if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    const int W = h->n_ranks;
+    const Rccl& R = rccl();
+    // 1. stable partition by owner rank (gd_shard.h)
+    GD_TRY(ensure(h, h->mx[0], (size_t)n * sizeof(gd_key) + 8));
+    GD_TRY(ensure(h, h->mx[1], (size_t)n * 4 + 4));
+    GD_TRY(ensure(h, h->mx[2], (size_t)W * 8));
+    gd_key* send_keys = (gd_key*)h->mx[0].p;
+    uint32_t* send_idx = (uint32_t*)h->mx[1].p;
+    uint32_t* dcnt = (uint32_t*)h->mx[2].p;           // [0, W): send counts, [W, 2W): recv counts
+    GD_TRY(shard_pack<false>(h, d_keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt));
+    // 2. counts: one u32 to every peer, then to the host (the only host sync: it sizes the receive)
+    NCCL_TRY(h, R.GroupStart());
+    for (int r = 0; r < W; ++r) {
+        NCCL_TRY(h, R.Send(dcnt + r, 1, ncclUint32, r, h->comm, h->stream));
+        NCCL_TRY(h, R.Recv(dcnt + W + r, 1, ncclUint32, r, h->comm, h->stream));
+    }
+    NCCL_TRY(h, R.GroupEnd());
+    HIP_TRY(h, hipMemcpyAsync(h->h_xcnt, dcnt, (size_t)W * 8, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(sync(h));
+    ncclResult_t async_err = ncclSuccess;
+    NCCL_TRY(h, R.CommGetAsyncError(h->comm, &async_err));
+    if (async_err != ncclSuccess) return set_err(h, GD_ERCCL, "RCCL async error: %s", R.GetErrorString(async_err));
+    const uint32_t* sc = h->h_xcnt;
+    const uint32_t* rc = h->h_xcnt + W;
+    std::vector<uint64_t> soff(W + 1, 0), roff(W + 1, 0);
+    for (int r = 0; r < W; ++r) {
+        soff[r + 1] = soff[r] + sc[r];
+        roff[r + 1] = roff[r] + rc[r];
+    }
+    if (soff[W] != n) return set_err(h, GD_ERCCL, "partition counts sum to %llu, batch is %u",
+                                     (unsigned long long)soff[W], n);
+    if (roff[W] >= 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "%llu messages received: more than a batch can hold",
+                                                 (unsigned long long)roff[W]);
+    const uint32_t m = (uint32_t)roff[W];
+    // 3. the headers and their origin indices, one grouped round
+    GD_TRY(ensure(h, h->mx[3], (size_t)m * sizeof(gd_key) + 8));
+    GD_TRY(ensure(h, h->mx[4], (size_t)m * 4 + 4));
+    GD_TRY(ensure(h, h->mx[5], (size_t)m * 4 + 4));
+    GD_TRY(ensure(h, h->mx[6], (size_t)m * 4 + 4));
+    GD_TRY(ensure(h, h->mx[7], (size_t)m * 4 + 4));
+    GD_TRY(ensure(h, h->mx[8], (size_t)m + 4));
+    GD_TRY(ensure(h, h->mx[9], (size_t)m * 4 + 4));
+    GD_TRY(ensure(h, h->mx[10], ((size_t)n_act + 2) * 4));
+    GD_TRY(ensure(h, h->mx[11], ((size_t)W + 1) * 4));
+    gd_key* recv_keys = (gd_key*)h->mx[3].p;
+    uint32_t* recv_idx = (uint32_t*)h->mx[4].p;
+    uint32_t* recv_src = (uint32_t*)h->mx[5].p;
+    uint32_t* silo = (uint32_t*)h->mx[6].p;
+    uint32_t* act = (uint32_t*)h->mx[7].p;
+    uint8_t* st = (uint8_t*)h->mx[8].p;
+    uint32_t* perm = (uint32_t*)h->mx[9].p;
+    uint32_t* offs = (uint32_t*)h->mx[10].p;
+    {
+        const Lane lanes[2] = {{send_keys, recv_keys, sizeof(gd_key), ncclUint64, 3},
+                               {send_idx, recv_idx, 4, ncclUint32, 1}};
+        GD_TRY(exchange_round(h, "rccl_headers", sc, soff.data(), rc, roff.data(), lanes, 2));
+    }
+    uint32_t* h_roff = h->h_xcnt + 2 * W;
+    for (int r = 0; r <= W; ++r) h_roff[r] = (uint32_t)roff[r];
+    HIP_TRY(h, hipMemcpyAsync(h->mx[11].p, h_roff, ((size_t)W + 1) * 4, hipMemcpyHostToDevice, h->stream));
+    GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
+                  (const uint32_t*)h->mx[11].p, (uint32_t)W, m, recv_src));
+    // 4. probe + bucket on the owner
+    if (m) GD_TRY(route_device(h, recv_keys, m, silo, act, st));
+    GD_TRY(bucket_device(h, act, m, n_act, perm, offs));
+    // 5. routes back to the senders, into their batch order
+    gd_multi_result r{};
+    if (ret) {
+        GD_TRY(ensure(h, h->mx[12], (size_t)n * 4 + 4));
+        GD_TRY(ensure(h, h->mx[13], (size_t)n * 4 + 4));
+        GD_TRY(ensure(h, h->mx[14], (size_t)n + 4));
+        GD_TRY(ensure(h, h->mx[15], (size_t)n * 4 + 4));
+        GD_TRY(ensure(h, h->mx[16], (size_t)n * 4 + 4));
+        GD_TRY(ensure(h, h->mx[17], (size_t)n + 4));
+        const Lane lanes[3] = {{silo, h->mx[12].p, 4, ncclUint32, 1},
+                               {act, h->mx[13].p, 4, ncclUint32, 1},
+                               {st, h->mx[14].p, 1, ncclUint8, 1}};
+        GD_TRY(exchange_round(h, "rccl_routes", rc, roff.data(), sc, soff.data(), lanes, 3));
+        GD_TRY(launch(h, "k_unpartition", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_unpartition,
+                      (const uint32_t*)send_idx, n, (const uint32_t*)h->mx[12].p, (const uint32_t*)h->mx[13].p,
+                      (const uint8_t*)h->mx[14].p, (uint32_t*)h->mx[15].p, (uint32_t*)h->mx[16].p,
+                      (uint8_t*)h->mx[17].p));
+        r.ret_silo = (const uint32_t*)h->mx[15].p;
+        r.ret_act = (const uint32_t*)h->mx[16].p;
+        r.ret_status = (const uint8_t*)h->mx[17].p;
+    }
+    r.n_recv = m;
+    r.n_act = n_act;
+    r.recv_keys = recv_keys;
+    r.recv_idx = recv_idx;
+    r.recv_src = recv_src;
+    r.silo = silo;
+    r.act = act;
+    r.status = st;
+    r.perm = perm;
+    r.offsets = offs;
+    h->mres = r;
+    h->mres_n = n;
+    h->routed += m;
+    if (out) *out = r;
+    return GD_OK;
+}
+
+}  // namespace
+
+int gd_comm_unique_id(uint8_t out_id[GD_COMM_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == GD_COMM_ID_BYTES, "ncclUniqueId size");
+    if (!out_id) return set_err(nullptr, GD_EINVAL, "null argument");
+    const Rccl& R = rccl();
+    if (!R.ok) return set_err(nullptr, GD_ERCCL, "%s", R.why);
+    ncclUniqueId id;
+    const ncclResult_t e = R.GetUniqueId(&id);
+    if (e != ncclSuccess) return set_err(nullptr, GD_ERCCL, "ncclGetUniqueId: %s", R.GetErrorString(e));
+    std::memcpy(out_id, &id, GD_COMM_ID_BYTES);
+    return GD_OK;
+}
+
+int gd_comm_init(gd_handle* h, const uint8_t id[GD_COMM_ID_BYTES], int n_ranks, int rank) {
+    if (!h || !id) return set_err(h, GD_EINVAL, "null argument");
+    if (n_ranks < 1 || n_ranks > 256 || rank < 0 || rank >= n_ranks)
+        return set_err(h, GD_EINVAL, "rank %d of %d: need 0 <= rank < n_ranks <= 256", rank, n_ranks);
+    const Rccl& R = rccl();
+    if (!R.ok) return set_err(h, GD_ERCCL, "%s", R.why);
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (h->comm) {
+        GD_TRY(sync(h));
+        (void)R.CommDestroy(h->comm);
+        h->comm = nullptr;
+    }
+    if (!h->h_xcnt) HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 4 * 257 * sizeof(uint32_t)));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, GD_COMM_ID_BYTES);
+    NCCL_TRY(h, R.CommInitRank(&h->comm, n_ranks, uid, rank));
+    h->n_ranks = n_ranks;
+    h->rank = rank;
+    h->mres = gd_multi_result{};
+    return GD_OK;
+}
+
+int gd_comm_destroy(gd_handle* h) {
+    if (!h) return set_err(h, GD_EINVAL, "null argument");
+    if (!h->comm) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(sync(h));
+    NCCL_TRY(h, rccl().CommDestroy(h->comm));
+    h->comm = nullptr;
+    h->n_ranks = 0;
+    h->rank = -1;
+    h->mres = gd_multi_result{};
+    return GD_OK;
+}
+
+int gd_route_multi_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int return_routes,
+                          gd_multi_result* out) {
+    if (!h || (n && !d_keys)) return set_err(h, GD_EINVAL, "null argument");
+    return route_multi(h, d_keys, n, n_act, return_routes != 0, out);
+}
+
+int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, int return_routes,
+                   gd_multi_result* out) {
+    if (!h || (n && !keys)) return set_err(h, GD_EINVAL, "null argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(route_multi(h, (const gd_key*)h->keys_in.p, n, n_act, return_routes != 0, out));
+    return sync_checked(h);
+}
+
+int gd_multi_fetch(gd_handle* h, gd_key* recv_keys, uint32_t* recv_idx, uint32_t* recv_src, uint32_t* silo,
+                   uint32_t* act, uint8_t* status, uint32_t* perm, uint32_t* offsets, uint32_t* ret_silo,
+                   uint32_t* ret_act, uint8_t* ret_status) {
+    if (!h) return set_err(h, GD_EINVAL, "null argument");
+    const gd_multi_result& r = h->mres;
+    if (!r.offsets) return set_err(h, GD_ESTATE, "no gd_route_multi result on this handle");
+    if (!r.ret_silo && (ret_silo || ret_act || ret_status))
+        return set_err(h, GD_EINVAL, "the last gd_route_multi ran without return_routes");
+    HIP_TRY(h, hipSetDevice(h->device));
+    const size_t m = r.n_recv, n = h->mres_n;
+    auto cp = [&](void* dst, const void* src, size_t bytes) -> int {
+        if (dst && bytes) HIP_TRY(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
+        return GD_OK;
+    };
+    GD_TRY(cp(recv_keys, r.recv_keys, m * sizeof(gd_key)));
+    GD_TRY(cp(recv_idx, r.recv_idx, m * 4));
+    GD_TRY(cp(recv_src, r.recv_src, m * 4));
+    GD_TRY(cp(silo, r.silo, m * 4));
+    GD_TRY(cp(act, r.act, m * 4));
+    GD_TRY(cp(status, r.status, m));
+    GD_TRY(cp(perm, r.perm, m * 4));
+    GD_TRY(cp(offsets, r.offsets, ((size_t)r.n_act + 2) * 4));
+    if (r.ret_silo) {
+        GD_TRY(cp(ret_silo, r.ret_silo, n * 4));
+        GD_TRY(cp(ret_act, r.ret_act, n * 4));
+        GD_TRY(cp(ret_status, r.ret_status, n));
+    }
     return sync(h);
 }
 

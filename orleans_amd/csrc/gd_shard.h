@@ -212,4 +212,38 @@ __global__ void k_shard_counts(const uint32_t* __restrict__ gscan, uint32_t tile
     counts[d] = end - start;
 }
 
+// recv_src[i] = the rank chunk i of the receive buffer came from: roff[r] <= i < roff[r + 1]
+// (roff = exclusive scan of the receive counts, world + 1 entries, staged in LDS).
+__global__ void __launch_bounds__(BLOCK) k_recv_src(const uint32_t* __restrict__ roff, uint32_t world, uint32_t m,
+                                                    uint32_t* __restrict__ src) {
+    __shared__ uint32_t s_off[257];
+    for (uint32_t r = threadIdx.x; r <= world; r += BLOCK) s_off[r] = roff[r];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= m) return;
+    uint32_t lo = 0, hi = world;          // largest r with s_off[r] <= i
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_off[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    src[i] = lo;
+}
+
+// Routes returned to the sender in shard order -> the sender's batch order (send_idx is the
+// partition's origin index): Dispatcher.AddressMessage's TargetSilo / TargetActivation per message.
+__global__ void __launch_bounds__(BLOCK) k_unpartition(const uint32_t* __restrict__ send_idx, uint32_t n,
+                                                       const uint32_t* __restrict__ silo_in,
+                                                       const uint32_t* __restrict__ act_in,
+                                                       const uint8_t* __restrict__ st_in, uint32_t* __restrict__ silo,
+                                                       uint32_t* __restrict__ act, uint8_t* __restrict__ st) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t i = send_idx[j];
+    if (i >= n) return;
+    silo[i] = silo_in[j];
+    act[i] = act_in[j];
+    st[i] = st_in[j];
+}
+
 }  // namespace gd

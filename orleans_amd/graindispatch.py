@@ -44,6 +44,8 @@ EXPORTED_SYMBOLS = [
     "gd_pack_nodes_by_shard_device", "gd_frontier_next_device",
     "gd_cache_configure", "gd_cache_set_silos", "gd_cache_add", "gd_cache_remove", "gd_cache_lookup",
     "gd_cache_clear", "gd_cache_stats_get", "gd_cache_entries",
+    "gd_comm_unique_id", "gd_comm_init", "gd_comm_destroy", "gd_route_multi_device", "gd_route_multi",
+    "gd_multi_fetch",
 ]
 
 
@@ -91,6 +93,15 @@ FRAME_FIELDS = {"flags": (np.uint32, ()), "target_grain": (np.uint64, (3,)), "ma
                 "sending_grain": (np.uint64, (3,)), "target_silo": (np.uint8, (24,)),
                 "sending_silo": (np.uint8, (24,)), "correlation_id": (np.int64, ()),
                 "category": (np.uint8, ()), "direction": (np.uint8, ())}
+
+
+class gd_multi_result(C.Structure):
+    _fields_ = [("n_recv", C.c_uint32), ("n_act", C.c_uint32)] + [
+        (f, C.c_void_p) for f in ("recv_keys", "recv_idx", "recv_src", "silo", "act", "status", "perm", "offsets",
+                                  "ret_silo", "ret_act", "ret_status")]
+
+
+GD_COMM_ID_BYTES = 128
 
 
 class GrainDispatchError(RuntimeError):
@@ -174,6 +185,12 @@ def _load() -> C.CDLL:
         "gd_cache_clear": (C.c_int, [P]),
         "gd_cache_stats_get": (C.c_int, [P, C.POINTER(gd_cache_stats)]),
         "gd_cache_entries": (C.c_int, [P, P, P, P, P, U64, C.POINTER(U64)]),
+        "gd_comm_unique_id": (C.c_int, [P]),
+        "gd_comm_init": (C.c_int, [P, P, C.c_int, C.c_int]),
+        "gd_comm_destroy": (C.c_int, [P]),
+        "gd_route_multi_device": (C.c_int, [P, P, U32, U32, C.c_int, C.POINTER(gd_multi_result)]),
+        "gd_route_multi": (C.c_int, [P, P, U32, U32, C.c_int, C.POINTER(gd_multi_result)]),
+        "gd_multi_fetch": (C.c_int, [P] + [P] * 11),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -566,6 +583,49 @@ class GrainDispatch:
                              d_counts: int):
         self._c(lib.gd_pack_by_shard_device(self.h, C.c_void_p(d_keys), n, n_shards, C.c_void_p(d_send_keys),
                                             C.c_void_p(d_send_idx), C.c_void_p(d_counts)))
+
+    # -- in-library exchange over RCCL (SURVEY 8 b gd_route_multi, 8 e) ----------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (C.c_uint8 * GD_COMM_ID_BYTES)()
+        _check(None, lib.gd_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, unique_id: bytes, n_ranks: int, rank: int):
+        assert len(unique_id) == GD_COMM_ID_BYTES
+        buf = (C.c_uint8 * GD_COMM_ID_BYTES).from_buffer_copy(unique_id)
+        self._c(lib.gd_comm_init(self.h, buf, n_ranks, rank))
+
+    def comm_destroy(self):
+        self._c(lib.gd_comm_destroy(self.h))
+
+    def route_multi_device(self, d_keys: int, n: int, n_act: int, return_routes: bool = False) -> gd_multi_result:
+        """Enqueue-only after the counts round: the result holds device pointers (library-owned)."""
+        r = gd_multi_result()
+        self._c(lib.gd_route_multi_device(self.h, C.c_void_p(d_keys), n, n_act, int(return_routes), C.byref(r)))
+        return r
+
+    def route_multi(self, keys, n_act: int, return_routes: bool = False) -> dict:
+        """Host batch in, host results out (gd_route_multi + gd_multi_fetch)."""
+        k = keys_array(keys)
+        n = k.shape[0]
+        r = gd_multi_result()
+        self._c(lib.gd_route_multi(self.h, _ptr(k), n, n_act, int(return_routes), C.byref(r)))
+        return self.multi_fetch(r, n)
+
+    def multi_fetch(self, r: gd_multi_result, n: int) -> dict:
+        """Host copies of the last gd_route_multi* result (n = this rank's batch size)."""
+        m = r.n_recv
+        out = {"recv_keys": np.empty((m, 3), np.uint64), "recv_idx": np.empty(m, np.uint32),
+               "recv_src": np.empty(m, np.uint32), "silo": np.empty(m, np.uint32), "act": np.empty(m, np.uint32),
+               "status": np.empty(m, np.uint8), "perm": np.empty(m, np.uint32),
+               "offsets": np.empty(r.n_act + 2, np.uint32)}
+        if r.ret_silo:
+            out.update(ret_silo=np.empty(n, np.uint32), ret_act=np.empty(n, np.uint32), ret_status=np.empty(n, np.uint8))
+        names = ("recv_keys", "recv_idx", "recv_src", "silo", "act", "status", "perm", "offsets", "ret_silo",
+                 "ret_act", "ret_status")
+        self._c(lib.gd_multi_fetch(self.h, *[C.c_void_p(_ptr(out[f])) if f in out else None for f in names]))
+        return out
 
     # -- header decode (SURVEY 8 f1) -------------------------------------------------
     @staticmethod

@@ -168,6 +168,65 @@ class ShardedRouter:
         return ShardedResult(recv_keys, recv_idx, recv_src, st, silo, act, perm, off)
 
 
+class _DevView:
+    """A torch view of library-owned HBM (__cuda_array_interface__, no copy)."""
+
+    def __init__(self, ptr: int, shape, typestr: str):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (int(ptr), False),
+                                         "version": 3, "strides": None}
+
+
+def _view(ptr: int, shape, typestr: str, device) -> torch.Tensor:
+    if not ptr or 0 in tuple(shape):
+        dt = {"<i4": torch.int32, "<i8": torch.int64, "|u1": torch.uint8}[typestr]
+        return torch.empty(shape, dtype=dt, device=device)
+    return torch.as_tensor(_DevView(ptr, shape, typestr), device=device)
+
+
+class LibraryRouter:
+    """The exchange inside libgraindispatch (gd_comm_init + gd_route_multi_device): the
+    partition, the grouped RCCL send/recv of headers and origin indices, the probe and the
+    bucketing all run in the library on the engine's stream -- the path a C# host drives
+    through P/Invoke.  torch.distributed only hands the RCCL unique id to the other ranks."""
+
+    def __init__(self, engine: DeviceEngine, group: Optional[dist.ProcessGroup] = None):
+        self.engine = engine
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        dev = engine.device
+        uid = torch.zeros(g.GD_COMM_ID_BYTES, dtype=torch.uint8)
+        if self.rank == 0:
+            uid = torch.frombuffer(bytearray(g.GrainDispatch.comm_unique_id()), dtype=torch.uint8)
+        # the backend may need the id on the device (nccl) or the host (gloo)
+        on_dev = dist.get_backend(group) == "nccl"
+        t = uid.to(dev) if on_dev else uid
+        dist.broadcast(t, src=0, group=group)
+        engine.gd.comm_init(bytes(t.cpu().numpy().tobytes()), self.world, self.rank)
+
+    def route_bucket(self, keys: torch.Tensor, n_act: int, return_routes: bool = False) -> ShardedResult:
+        n = keys.shape[0]
+        r = self.engine.gd.route_multi_device(keys.data_ptr(), n, n_act, return_routes)
+        m, dev = r.n_recv, self.engine.device
+        return ShardedResult(_view(r.recv_keys, (m, 3), "<i8", dev), _view(r.recv_idx, (m,), "<i4", dev),
+                             _view(r.recv_src, (m,), "<i4", dev), _view(r.status, (m,), "|u1", dev),
+                             _view(r.silo, (m,), "<i4", dev), _view(r.act, (m,), "<i4", dev),
+                             _view(r.perm, (m,), "<i4", dev), _view(r.offsets, (n_act + 2,), "<i4", dev))
+
+    def close(self):
+        self.engine.gd.comm_destroy()
+
+
+def same_result(a: ShardedResult, b: ShardedResult) -> bool:
+    """Bit-identical owner-side results (both routers on the same batch)."""
+    if a.recv_keys.shape != b.recv_keys.shape:
+        return False
+    pairs = [(a.recv_keys, b.recv_keys), (a.status, b.status), (a.silo, b.silo), (a.act, b.act), (a.perm, b.perm),
+             (a.offsets, b.offsets)]
+    if a.recv_idx is not None and b.recv_idx is not None:
+        pairs += [(a.recv_idx, b.recv_idx), (a.recv_src, b.recv_src)]
+    return all(torch.equal(x, y) for x, y in pairs)
+
+
 def silo_rank(silo: int, world: int) -> int:
     """Which rank hosts (owns the directory partition of) a silo."""
     return silo % world

@@ -127,3 +127,14 @@ def test_null_handle_errors():
     assert g.lib.gd_synchronize(None) == g.GD_EINVAL
     assert g.lib.gd_ring_set(None, 0, None, None, 0) == g.GD_EINVAL
     assert b"null" in g.lib.gd_last_error(None)
+
+
+def test_rccl_loads_at_run_time_and_issues_unique_ids():
+    """The in-library exchange resolves RCCL with dlopen (orleans_amd/csrc/gd_comm.h): the
+    library itself has no NEEDED librccl, and gd_comm_unique_id works without a GPU."""
+    import subprocess
+    from orleans_amd import graindispatch as g
+    needed = subprocess.run(["readelf", "-d", g.LIB_PATH], capture_output=True, text=True).stdout
+    assert "librccl" not in needed
+    a, b = g.GrainDispatch.comm_unique_id(), g.GrainDispatch.comm_unique_id()
+    assert len(a) == g.GD_COMM_ID_BYTES == 128 and a != b

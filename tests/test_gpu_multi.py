@@ -1,0 +1,164 @@
+"""In-library exchange over RCCL (gd_comm_* + gd_route_multi*, SURVEY 8 b / 8 e) against the
+oracle: the sender's batch is partitioned by owner rank (OutboundMessageQueue.cs:54-131 per
+target silo), exchanged, probed and bucketed on the owner (GrainDirectoryPartition.cs:385-441,
+ActivationData.cs:566-606), and the routes come back in the sender's batch order
+(Dispatcher.AddressMessage, Dispatcher.cs:715-767).  World 1 runs the whole path (the exchange
+is a send/recv to self); the 2-rank case runs two processes on cuda:0 if RCCL allows it."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle as o
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TC = o.grain_type_code(o.PING_GRAIN_CLASS)
+
+
+@pytest.fixture(scope="module")
+def gd():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from orleans_amd import graindispatch as g
+    return g
+
+
+def _directory(G, world, rank, spec):
+    reg = o.grain_keys(TC, np.arange(G))
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    mine = np.nonzero(own % world == rank)[0]
+    return reg, own, mine
+
+
+@pytest.mark.parametrize("n", [0, 1, 4999, 100003])
+def test_route_multi_world1(gd, n):
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    G = 4096
+    reg, own, mine = _directory(G, 1, 0, spec)
+    rng = np.random.default_rng(n + 11)
+    keys = o.grain_keys(TC, rng.integers(0, G + 300, size=n))
+    if n > 100:
+        keys[::13] = np.array(o.UniqueKey(0, 7, o.type_code_data(o.CAT_SYSTEM_TARGET, 1)).as_tuple(), dtype=np.uint64)
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 14, my_silo=2)
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+    e.register(reg, np.arange(G), own)
+    e.comm_init(gd.GrainDispatch.comm_unique_id(), 1, 0)
+    for ret in (False, True):
+        r = e.route_multi(keys, G, return_routes=ret)
+        st, silo, act, _, _ = o.route_batch_np(keys, spec, o.DirectoryArrays(reg, np.arange(G), own), my_silo=2)
+        np.testing.assert_array_equal(r["recv_keys"], keys)
+        np.testing.assert_array_equal(r["recv_idx"], np.arange(n, dtype=np.uint32))
+        np.testing.assert_array_equal(r["recv_src"], np.zeros(n, np.uint32))
+        np.testing.assert_array_equal(r["status"], st)
+        np.testing.assert_array_equal(r["silo"], silo)
+        np.testing.assert_array_equal(r["act"], act)
+        wp, wo = o.bucket_stable(act, G)
+        np.testing.assert_array_equal(r["perm"], wp)
+        np.testing.assert_array_equal(r["offsets"], wo)
+        if ret:
+            np.testing.assert_array_equal(r["ret_status"], st)
+            np.testing.assert_array_equal(r["ret_silo"], silo)
+            np.testing.assert_array_equal(r["ret_act"], act)
+    e.comm_destroy()
+    with pytest.raises(gd.GrainDispatchError):
+        e.route_multi(keys, G)              # no communicator any more: GD_ESTATE
+    e.close()
+
+
+def test_route_multi_device_pointers(gd):
+    """gd_route_multi_device on torch-allocated HBM keys; results read through the returned
+    device pointers (library-owned buffers)."""
+    import torch
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "V")
+    G, n = 2048, 30000
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 13)
+    e.ring_set_silos("V", [(s.ip, s.port, s.gen) for s in silos])
+    reg, own, _ = _directory(G, 1, 0, spec)
+    e.register(reg, np.arange(G), own)
+    e.comm_init(gd.GrainDispatch.comm_unique_id(), 1, 0)
+    keys = o.grain_keys(TC, np.random.default_rng(3).integers(0, G, size=n))
+    tk = torch.from_numpy(keys.view(np.int64).copy()).cuda()
+    stream = torch.cuda.Stream()
+    e.set_stream(stream.cuda_stream)
+    with torch.cuda.stream(stream):
+        r = e.route_multi_device(tk.data_ptr(), n, G, return_routes=True)
+    torch.cuda.synchronize()
+    assert r.n_recv == n and r.ret_act and r.perm
+    got = e.multi_fetch(r, n)
+    st, silo, act, _, _ = o.route_batch_np(keys, spec, o.DirectoryArrays(reg, np.arange(G), own))
+    np.testing.assert_array_equal(got["act"], act)
+    np.testing.assert_array_equal(got["ret_act"], act)
+    np.testing.assert_array_equal(got["ret_silo"], silo)
+    wp, wo = o.bucket_stable(act, G)
+    np.testing.assert_array_equal(got["perm"], wp)
+    np.testing.assert_array_equal(got["offsets"], wo)
+    e.comm_destroy()
+    e.close()
+
+
+def test_route_multi_two_ranks_one_gpu(tmp_path):
+    """Two processes, one communicator, both on cuda:0.  Skips if RCCL refuses two ranks on one
+    device; the 8-GPU form runs in bench.py --exchange library."""
+    world, n = 2, 20011
+    env = dict(os.environ)
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_rccl_worker.py"), str(tmp_path),
+                               str(world), str(r), str(n)], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("RCCL worker timed out")
+        outs.append(out)
+    codes = [p.returncode for p in procs]
+    if 77 in codes:
+        pytest.skip("RCCL refuses two ranks on one GPU: " + " | ".join(x.strip()[-300:] for x in outs))
+    assert codes == [0] * world, outs
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _rccl_worker as w
+    spec = o.ring_spec(o.bench_silos(8), "D")
+    reg, own, _ = _directory(w.G_TOTAL, 1, 0, spec)
+    res = [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
+    batches = [w.batch_of(r, n) for r in range(world)]
+    for r in range(world):
+        mine = np.nonzero(own % world == r)[0]
+        local = np.full(w.G_TOTAL, o.M32, np.int64)
+        local[mine] = np.arange(len(mine))
+        d = o.DirectoryArrays(reg[mine], np.arange(len(mine)), own[mine])
+        exp_keys, exp_idx, exp_src = [], [], []
+        for s in range(world):
+            k = batches[s]
+            _, _, _, owner, _ = o.route_batch_np(k, spec, o.DirectoryArrays(np.zeros((0, 3), np.uint64), [], []))
+            sel = np.nonzero(owner % world == r)[0]
+            exp_keys.append(k[sel]), exp_idx.append(sel), exp_src.append(np.full(len(sel), s))
+        ek = np.concatenate(exp_keys)
+        np.testing.assert_array_equal(res[r]["recv_keys"], ek)
+        np.testing.assert_array_equal(res[r]["recv_idx"], np.concatenate(exp_idx))
+        np.testing.assert_array_equal(res[r]["recv_src"], np.concatenate(exp_src))
+        st, silo, act, _, _ = o.route_batch_np(ek, spec, d, my_silo=r)
+        np.testing.assert_array_equal(res[r]["status"], st)
+        np.testing.assert_array_equal(res[r]["act"], act)
+        wp, wo = o.bucket_stable(act, len(mine))
+        np.testing.assert_array_equal(res[r]["perm"], wp)
+        np.testing.assert_array_equal(res[r]["offsets"], wo)
+    # routes back at each sender, in batch order, equal the owner's answer
+    for s in range(world):
+        k = batches[s]
+        _, _, _, owner, _ = o.route_batch_np(k, spec, o.DirectoryArrays(np.zeros((0, 3), np.uint64), [], []))
+        for r in range(world):
+            mine = np.nonzero(own % world == r)[0]
+            d = o.DirectoryArrays(reg[mine], np.arange(len(mine)), own[mine])
+            sel = np.nonzero(owner % world == r)[0]
+            st, silo, act, _, _ = o.route_batch_np(k[sel], spec, d, my_silo=r)
+            np.testing.assert_array_equal(res[s]["ret_status"][sel], st)
+            np.testing.assert_array_equal(res[s]["ret_act"][sel], act)
+            np.testing.assert_array_equal(res[s]["ret_silo"][sel], silo)
