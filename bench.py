@@ -169,7 +169,9 @@ def main():
             agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
             dist.all_reduce(agree, op=dist.ReduceOp.MIN)
             if int(agree.item()) == 1:
+                # keys are resident and complete: batch i+1's exchange overlaps batch i's probe + bucket
                 router = lib_router
+                lib_router.keys_ready = True
                 exchange = "libgraindispatch gd_route_multi_device (grouped RCCL send/recv)"
             else:
                 exchange = "torch.distributed all_to_all_single (RCCL); library exchange disagreed on batch 1"

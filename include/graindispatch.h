@@ -250,10 +250,22 @@ typedef struct gd_multi_result {
     const uint8_t*  ret_status;
 } gd_multi_result;
 
-int gd_route_multi_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int return_routes,
+/* flags: GD_MULTI_RETURN_ROUTES -- also send (silo, act, status) back to the senders (ret_*).
+ *        GD_MULTI_KEYS_READY    -- d_keys are complete already (their producer was synchronised);
+ *        without it the exchange waits for all work enqueued on the handle's stream, which includes
+ *        the previous batch's probe + bucketing.  With it, batch i+1's partition and RCCL rounds
+ *        (on the library's exchange stream) run while batch i is probed and bucketed (on the
+ *        handle's stream).  Results are complete when the handle's stream reaches them
+ *        (gd_synchronize, or stream order for later work); they stay valid through the next
+ *        call and are overwritten by the one after (two batches in flight).
+ * Blocks the host once per call, on the per-rank counts round (it sizes the receive). */
+#define GD_MULTI_RETURN_ROUTES 1
+#define GD_MULTI_KEYS_READY    2
+int gd_route_multi_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int flags,
                           gd_multi_result* out);
-/* Host keys in (C# pinned array); results stay on the device -> gd_multi_fetch. */
-int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, int return_routes,
+/* Host keys in (C# pinned array), copied on the exchange stream; returns with the batch done
+ * (results stay on the device -> gd_multi_fetch). */
+int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, int flags,
                    gd_multi_result* out);
 /* Copy the last result to host arrays sized from gd_multi_result (any pointer may be NULL). */
 int gd_multi_fetch(gd_handle* h, gd_key* recv_keys, uint32_t* recv_idx, uint32_t* recv_src, uint32_t* silo,

@@ -76,13 +76,22 @@ struct gd_handle {
     DevBuf cbuf[8];                   // cache scratch
     DevBuf shard_dest, shard_hist;    // exchange partition scratch
 
-    // in-library exchange over RCCL (gd_comm.h): one communicator per handle
+    // in-library exchange over RCCL (gd_comm.h): one communicator per handle.  The partition and
+    // the RCCL rounds run on xstream; probe + bucketing on `stream`; batch i's exchange overlaps
+    // batch i-1's probe + bucketing (receive/result buffers double-buffered by batch parity).
     ncclComm_t comm = nullptr;
     int n_ranks = 0, rank = -1;
-    DevBuf mx[20];                    // send/recv/result buffers of gd_route_multi*
-    uint32_t* h_xcnt = nullptr;       // pinned: send counts, recv counts, recv offsets
-    gd_multi_result mres{};
-    uint32_t mres_n = 0;              // sender-side batch size of the last result
+    hipStream_t xstream = nullptr;
+    hipEvent_t x_in = nullptr, x_hdr[2] = {}, x_route[2] = {}, x_ret[2] = {}, x_done[2] = {};
+    bool x_done_rec[2] = {false, false};
+    DevBuf mx_send[3];                // send keys, send idx, counts (send [W], recv [W])
+    DevBuf mx[2][16];                 // per batch parity: receive / result buffers
+    DevBuf mx_keys;                   // host-keys entry point: the batch, on xstream
+    DevBuf x_scratch[4];              // xstream's own scan partials + partition scratch
+    uint32_t* h_xcnt = nullptr;       // pinned: send counts, recv counts
+    gd_multi_result mres[2] = {};
+    uint32_t mres_n[2] = {0, 0};
+    uint64_t mcalls = 0;
     uint64_t routed = 0;
 
     // kernel tuning (defaults measured on MI355X; GD_ROUTE_M / GD_ROUTE_NT override for A/B runs)
@@ -190,6 +199,7 @@ int launch(gd_handle* h, const char* name, dim3 grid, dim3 block, size_t lds, K 
 int resolve_timing(gd_handle* h) {
     if (h->pending.empty()) return GD_OK;
     HIP_TRY(h, hipStreamSynchronize(h->stream));
+    if (h->xstream) HIP_TRY(h, hipStreamSynchronize(h->xstream));
     for (auto& t : h->pending) {
         float ms = 0.f;
         HIP_TRY(h, hipEventElapsedTime(&ms, t.a, t.b));
@@ -446,10 +456,10 @@ int maybe_grow_table(gd_handle* h, uint64_t incoming) {
 
 // ---- exchange partition (gd_shard.h) -------------------------------------------------
 template <int MODE, bool NODES>
-int shard_hist_t(gd_handle* h, const void* recs, uint32_t n, uint64_t tcd, uint32_t n_shards, uint32_t tiles,
-                 uint8_t* dest, uint32_t* hist) {
+int shard_hist_t(gd_handle* h, const void* recs, uint32_t n, uint64_t tcd, uint32_t n_shards, uint32_t bits,
+                 uint32_t tiles, uint8_t* dest, uint32_t* hist) {
     return launch(h, "k_shard_hist", dim3(tiles), dim3(SH_NT), ring_lds(h), k_shard_hist<MODE, NODES>, recs, n, tcd,
-                  ring_args(h), n_shards, tiles, dest, hist);
+                  ring_args(h), n_shards, bits, tiles, dest, hist);
 }
 
 template <int BITS, bool NODES>
@@ -473,21 +483,21 @@ int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t
     GD_TRY(ensure(h, h->shard_hist, (size_t)tiles * n_shards * 4));
     uint8_t* dest = (uint8_t*)h->shard_dest.p;
     uint32_t* hist = (uint32_t*)h->shard_hist.p;
+    uint32_t bits = 1;
+    while ((1u << bits) < n_shards) ++bits;
     switch (h->ring_mode) {
         case GD_RING_DIRECTORY:
-            GD_TRY((shard_hist_t<GD_RING_DIRECTORY, NODES>(h, recs, n, tcd, n_shards, tiles, dest, hist)));
+            GD_TRY((shard_hist_t<GD_RING_DIRECTORY, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist)));
             break;
         case GD_RING_CONSISTENT:
-            GD_TRY((shard_hist_t<GD_RING_CONSISTENT, NODES>(h, recs, n, tcd, n_shards, tiles, dest, hist)));
+            GD_TRY((shard_hist_t<GD_RING_CONSISTENT, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist)));
             break;
         default:
-            GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, tiles, dest, hist)));
+            GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist)));
     }
     GD_TRY(scan_device<OpAdd>(h, hist, tiles * n_shards, false, false, "shard"));
     GD_TRY(launch(h, "k_shard_counts", dim3(1), dim3(256), 0, k_shard_counts, (const uint32_t*)hist, tiles, n_shards, n,
                   counts));
-    uint32_t bits = 1;
-    while ((1u << bits) < n_shards) ++bits;
     const uint32_t* gs = hist;
     switch (bits) {
         case 1: return shard_scatter_t<1, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
@@ -559,6 +569,10 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     return GD_OK;
 }
 
+namespace {
+void comm_release(gd_handle* h);
+}
+
 void gd_destroy(gd_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
@@ -573,9 +587,7 @@ void gd_destroy(gd_handle* h) {
     free_buf(h->cache_local);
     free_buf(h->shard_dest);
     free_buf(h->shard_hist);
-    if (h->comm) (void)rccl().CommDestroy(h->comm);
-    for (DevBuf& b : h->mx) free_buf(b);
-    if (h->h_xcnt) (void)hipHostFree(h->h_xcnt);
+    comm_release(h);
     free_buf(h->cache_valid);
     if (h->cslots) (void)hipFree(h->cslots);
     if (h->cctr) (void)hipFree(h->cctr);
@@ -603,6 +615,7 @@ void* gd_get_stream(gd_handle* h) { return h ? (void*)h->stream : nullptr; }
 int gd_synchronize(gd_handle* h) {
     if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
     HIP_TRY(h, hipSetDevice(h->device));
+    if (h->xstream) HIP_TRY(h, hipStreamSynchronize(h->xstream));
     return sync_checked(h);
 }
 
@@ -1962,15 +1975,71 @@ namespace {
             return set_err((h), GD_ERCCL, "%s: %s", #expr, rccl().GetErrorString(r_));             \
     } while (0)
 
+// Launches inside the scope go to the exchange stream (launch() uses h->stream), with the
+// exchange stream's own scratch for the helpers both streams run (scan partials, partition):
+// the probe + bucketing of the previous batch may be using the handle's at the same time.
+struct OnXStream {
+    gd_handle* h;
+    hipStream_t saved;
+    explicit OnXStream(gd_handle* hh) : h(hh), saved(hh->stream) {
+        h->stream = h->xstream;
+        swap_scratch();
+    }
+    ~OnXStream() {
+        swap_scratch();
+        h->stream = saved;
+    }
+    void swap_scratch() {
+        std::swap(h->partials, h->x_scratch[0]);
+        std::swap(h->partials2, h->x_scratch[1]);
+        std::swap(h->shard_dest, h->x_scratch[2]);
+        std::swap(h->shard_hist, h->x_scratch[3]);
+    }
+};
+
+void comm_release(gd_handle* h) {
+    if (h->xstream) (void)hipStreamSynchronize(h->xstream);
+    if (h->comm) (void)rccl().CommDestroy(h->comm);
+    h->comm = nullptr;
+    for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
+                          &h->x_ret[1], &h->x_done[0], &h->x_done[1]})
+        if (*e) {
+            (void)hipEventDestroy(*e);
+            *e = nullptr;
+        }
+    if (h->xstream) (void)hipStreamDestroy(h->xstream);
+    h->xstream = nullptr;
+    for (DevBuf& b : h->mx_send) free_buf(b);
+    for (auto& slot : h->mx)
+        for (DevBuf& b : slot) free_buf(b);
+    free_buf(h->mx_keys);
+    for (DevBuf& b : h->x_scratch) free_buf(b);
+    if (h->h_xcnt) (void)hipHostFree(h->h_xcnt);
+    h->h_xcnt = nullptr;
+    h->x_done_rec[0] = h->x_done_rec[1] = false;
+    h->mres[0] = h->mres[1] = gd_multi_result{};
+    h->mcalls = 0;
+    h->n_ranks = 0;
+    h->rank = -1;
+}
+
 int need_comm(gd_handle* h) {
     if (!h->comm) return set_err(h, GD_ESTATE, "no communicator (gd_comm_init)");
     return GD_OK;
 }
 
-// One grouped send/recv round: for every peer r, send sc[r] elements at soff[r] of each send
-// array and receive rc[r] elements at roff[r] of each recv array (both sides skip empty chunks,
-// which they agree on: my count to r is r's count from me).  With per-kernel timing the round is
-// bracketed by events under `name`.
+// Grow a buffer either stream may touch: drain both first.
+int grow(gd_handle* h, DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return GD_OK;
+    HIP_TRY(h, hipStreamSynchronize(h->xstream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    return ensure(h, b, bytes);
+}
+
+// One grouped send/recv round on h->stream: for every peer r, send sc[r] elements at soff[r] of
+// each lane's send array and receive rc[r] elements at roff[r] of its recv array (both sides skip
+// empty chunks, which they agree on: my count to r is r's count from me).  With per-kernel timing
+// the round is bracketed by events under `name`.
 struct Lane {
     const void* send;
     void* recv;
@@ -2008,97 +2077,110 @@ int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uin
     return GD_OK;
 }
 
-// Sender batch d_keys[n] -> owner ranks (exchange) -> route + bucket there (-> routes back).
-int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, bool ret, gd_multi_result* out) {
+// Sender batch d_keys[n] -> owner ranks (exchange) -> probe + bucket there (-> routes back).
+//   xstream: [wait caller] partition, counts round, (host: sizes) header round, recv_src
+//   stream:  [wait headers] probe, bucket
+//   xstream: [wait probe] routes round, unpartition            (GD_MULTI_RETURN_ROUTES)
+// Only the counts round blocks the host, and only on xstream, so batch i+1's partition and
+// exchange run while batch i is probed and bucketed.
+int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int flags, gd_multi_result* out) {
     GD_TRY(need_comm(h));
     GD_TRY(check_ring(h));
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
     const int W = h->n_ranks;
     const Rccl& R = rccl();
-    // 1. stable partition by owner rank (gd_shard.h)
-    GD_TRY(ensure(h, h->mx[0], (size_t)n * sizeof(gd_key) + 8));
-    GD_TRY(ensure(h, h->mx[1], (size_t)n * 4 + 4));
-    GD_TRY(ensure(h, h->mx[2], (size_t)W * 8));
-    gd_key* send_keys = (gd_key*)h->mx[0].p;
-    uint32_t* send_idx = (uint32_t*)h->mx[1].p;
-    uint32_t* dcnt = (uint32_t*)h->mx[2].p;           // [0, W): send counts, [W, 2W): recv counts
-    GD_TRY(shard_pack<false>(h, d_keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt));
-    // 2. counts: one u32 to every peer, then to the host (the only host sync: it sizes the receive)
-    NCCL_TRY(h, R.GroupStart());
-    for (int r = 0; r < W; ++r) {
-        NCCL_TRY(h, R.Send(dcnt + r, 1, ncclUint32, r, h->comm, h->stream));
-        NCCL_TRY(h, R.Recv(dcnt + W + r, 1, ncclUint32, r, h->comm, h->stream));
+    const int s = (int)(h->mcalls & 1);
+    DevBuf* B = h->mx[s];
+    const bool ret = (flags & GD_MULTI_RETURN_ROUTES) != 0;
+    if (!(flags & GD_MULTI_KEYS_READY)) {
+        HIP_TRY(h, hipEventRecord(h->x_in, h->stream));
+        HIP_TRY(h, hipStreamWaitEvent(h->xstream, h->x_in, 0));
     }
-    NCCL_TRY(h, R.GroupEnd());
-    HIP_TRY(h, hipMemcpyAsync(h->h_xcnt, dcnt, (size_t)W * 8, hipMemcpyDeviceToHost, h->stream));
-    GD_TRY(sync(h));
+    // 1. stable partition by owner rank (gd_shard.h) + counts, on the exchange stream
+    GD_TRY(grow(h, h->mx_send[0], (size_t)n * sizeof(gd_key) + 8));
+    GD_TRY(grow(h, h->mx_send[1], (size_t)n * 4 + 4));
+    GD_TRY(grow(h, h->mx_send[2], (size_t)W * 8));
+    gd_key* send_keys = (gd_key*)h->mx_send[0].p;
+    uint32_t* send_idx = (uint32_t*)h->mx_send[1].p;
+    uint32_t* dcnt = (uint32_t*)h->mx_send[2].p;           // [0, W): send counts, [W, 2W): recv counts
+    {
+        OnXStream on(h);
+        GD_TRY(shard_pack<false>(h, d_keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt));
+        NCCL_TRY(h, R.GroupStart());
+        for (int r = 0; r < W; ++r) {
+            NCCL_TRY(h, R.Send(dcnt + r, 1, ncclUint32, r, h->comm, h->stream));
+            NCCL_TRY(h, R.Recv(dcnt + W + r, 1, ncclUint32, r, h->comm, h->stream));
+        }
+        NCCL_TRY(h, R.GroupEnd());
+        HIP_TRY(h, hipMemcpyAsync(h->h_xcnt, dcnt, (size_t)W * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+    }
     ncclResult_t async_err = ncclSuccess;
     NCCL_TRY(h, R.CommGetAsyncError(h->comm, &async_err));
     if (async_err != ncclSuccess) return set_err(h, GD_ERCCL, "RCCL async error: %s", R.GetErrorString(async_err));
-    const uint32_t* sc = h->h_xcnt;
-    const uint32_t* rc = h->h_xcnt + W;
+    std::vector<uint32_t> sc(h->h_xcnt, h->h_xcnt + W), rc(h->h_xcnt + W, h->h_xcnt + 2 * W);
     std::vector<uint64_t> soff(W + 1, 0), roff(W + 1, 0);
     for (int r = 0; r < W; ++r) {
         soff[r + 1] = soff[r] + sc[r];
         roff[r + 1] = roff[r] + rc[r];
     }
-    if (soff[W] != n) return set_err(h, GD_ERCCL, "partition counts sum to %llu, batch is %u",
-                                     (unsigned long long)soff[W], n);
-    if (roff[W] >= 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "%llu messages received: more than a batch can hold",
-                                                 (unsigned long long)roff[W]);
+    if (soff[W] != n)
+        return set_err(h, GD_ERCCL, "partition counts sum to %llu, batch is %u", (unsigned long long)soff[W], n);
+    if (roff[W] >= 0xFFFFFFFFull)
+        return set_err(h, GD_EINVAL, "%llu messages received: more than a batch can hold",
+                       (unsigned long long)roff[W]);
     const uint32_t m = (uint32_t)roff[W];
-    // 3. the headers and their origin indices, one grouped round
-    GD_TRY(ensure(h, h->mx[3], (size_t)m * sizeof(gd_key) + 8));
-    GD_TRY(ensure(h, h->mx[4], (size_t)m * 4 + 4));
-    GD_TRY(ensure(h, h->mx[5], (size_t)m * 4 + 4));
-    GD_TRY(ensure(h, h->mx[6], (size_t)m * 4 + 4));
-    GD_TRY(ensure(h, h->mx[7], (size_t)m * 4 + 4));
-    GD_TRY(ensure(h, h->mx[8], (size_t)m + 4));
-    GD_TRY(ensure(h, h->mx[9], (size_t)m * 4 + 4));
-    GD_TRY(ensure(h, h->mx[10], ((size_t)n_act + 2) * 4));
-    GD_TRY(ensure(h, h->mx[11], ((size_t)W + 1) * 4));
-    gd_key* recv_keys = (gd_key*)h->mx[3].p;
-    uint32_t* recv_idx = (uint32_t*)h->mx[4].p;
-    uint32_t* recv_src = (uint32_t*)h->mx[5].p;
-    uint32_t* silo = (uint32_t*)h->mx[6].p;
-    uint32_t* act = (uint32_t*)h->mx[7].p;
-    uint8_t* st = (uint8_t*)h->mx[8].p;
-    uint32_t* perm = (uint32_t*)h->mx[9].p;
-    uint32_t* offs = (uint32_t*)h->mx[10].p;
+    // 2. this parity's buffers: batch i-2 must be done with them (probe/bucket and routes round)
+    const size_t m4 = (size_t)m * 4 + 4, n4 = (size_t)n * 4 + 4;
+    const size_t want[16] = {(size_t)m * sizeof(gd_key) + 8, m4, m4, m4, m4, (size_t)m + 4, m4,
+                             ((size_t)n_act + 2) * 4, n4, n4, (size_t)n + 4, n4, n4, (size_t)n + 4, 0, 0};
+    for (int b = 0; b < 16; ++b)
+        if (want[b] && (b < 8 || ret)) GD_TRY(grow(h, B[b], want[b]));
+    gd_key* recv_keys = (gd_key*)B[0].p;
+    uint32_t* recv_idx = (uint32_t*)B[1].p;
+    uint32_t* recv_src = (uint32_t*)B[2].p;
+    uint32_t* silo = (uint32_t*)B[3].p;
+    uint32_t* act = (uint32_t*)B[4].p;
+    uint8_t* st = (uint8_t*)B[5].p;
+    uint32_t* perm = (uint32_t*)B[6].p;
+    uint32_t* offs = (uint32_t*)B[7].p;
+    if (h->x_done_rec[s]) HIP_TRY(h, hipStreamWaitEvent(h->xstream, h->x_done[s], 0));
     {
+        OnXStream on(h);
         const Lane lanes[2] = {{send_keys, recv_keys, sizeof(gd_key), ncclUint64, 3},
                                {send_idx, recv_idx, 4, ncclUint32, 1}};
-        GD_TRY(exchange_round(h, "rccl_headers", sc, soff.data(), rc, roff.data(), lanes, 2));
+        GD_TRY(exchange_round(h, "rccl_headers", sc.data(), soff.data(), rc.data(), roff.data(), lanes, 2));
+        GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
+                      (const uint32_t*)(dcnt + W), (uint32_t)W, m, recv_src));
+        HIP_TRY(h, hipEventRecord(h->x_hdr[s], h->xstream));
     }
-    uint32_t* h_roff = h->h_xcnt + 2 * W;
-    for (int r = 0; r <= W; ++r) h_roff[r] = (uint32_t)roff[r];
-    HIP_TRY(h, hipMemcpyAsync(h->mx[11].p, h_roff, ((size_t)W + 1) * 4, hipMemcpyHostToDevice, h->stream));
-    GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
-                  (const uint32_t*)h->mx[11].p, (uint32_t)W, m, recv_src));
-    // 4. probe + bucket on the owner
+    // 3. probe + bucket on the owner (the handle's stream)
+    HIP_TRY(h, hipStreamWaitEvent(h->stream, h->x_hdr[s], 0));
     if (m) GD_TRY(route_device(h, recv_keys, m, silo, act, st));
+    HIP_TRY(h, hipEventRecord(h->x_route[s], h->stream));
     GD_TRY(bucket_device(h, act, m, n_act, perm, offs));
-    // 5. routes back to the senders, into their batch order
+    // 4. routes back to the senders, into their batch order (Dispatcher.AddressMessage)
     gd_multi_result r{};
     if (ret) {
-        GD_TRY(ensure(h, h->mx[12], (size_t)n * 4 + 4));
-        GD_TRY(ensure(h, h->mx[13], (size_t)n * 4 + 4));
-        GD_TRY(ensure(h, h->mx[14], (size_t)n + 4));
-        GD_TRY(ensure(h, h->mx[15], (size_t)n * 4 + 4));
-        GD_TRY(ensure(h, h->mx[16], (size_t)n * 4 + 4));
-        GD_TRY(ensure(h, h->mx[17], (size_t)n + 4));
-        const Lane lanes[3] = {{silo, h->mx[12].p, 4, ncclUint32, 1},
-                               {act, h->mx[13].p, 4, ncclUint32, 1},
-                               {st, h->mx[14].p, 1, ncclUint8, 1}};
-        GD_TRY(exchange_round(h, "rccl_routes", rc, roff.data(), sc, soff.data(), lanes, 3));
-        GD_TRY(launch(h, "k_unpartition", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_unpartition,
-                      (const uint32_t*)send_idx, n, (const uint32_t*)h->mx[12].p, (const uint32_t*)h->mx[13].p,
-                      (const uint8_t*)h->mx[14].p, (uint32_t*)h->mx[15].p, (uint32_t*)h->mx[16].p,
-                      (uint8_t*)h->mx[17].p));
-        r.ret_silo = (const uint32_t*)h->mx[15].p;
-        r.ret_act = (const uint32_t*)h->mx[16].p;
-        r.ret_status = (const uint8_t*)h->mx[17].p;
+        HIP_TRY(h, hipStreamWaitEvent(h->xstream, h->x_route[s], 0));
+        {
+            OnXStream on(h);
+            const Lane lanes[3] = {{silo, B[8].p, 4, ncclUint32, 1},
+                                   {act, B[9].p, 4, ncclUint32, 1},
+                                   {st, B[10].p, 1, ncclUint8, 1}};
+            GD_TRY(exchange_round(h, "rccl_routes", rc.data(), roff.data(), sc.data(), soff.data(), lanes, 3));
+            GD_TRY(launch(h, "k_unpartition", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_unpartition,
+                          (const uint32_t*)send_idx, n, (const uint32_t*)B[8].p, (const uint32_t*)B[9].p,
+                          (const uint8_t*)B[10].p, (uint32_t*)B[11].p, (uint32_t*)B[12].p, (uint8_t*)B[13].p));
+            HIP_TRY(h, hipEventRecord(h->x_ret[s], h->xstream));
+        }
+        HIP_TRY(h, hipStreamWaitEvent(h->stream, h->x_ret[s], 0));   // the caller syncs one stream
+        r.ret_silo = (const uint32_t*)B[11].p;
+        r.ret_act = (const uint32_t*)B[12].p;
+        r.ret_status = (const uint8_t*)B[13].p;
     }
+    HIP_TRY(h, hipEventRecord(h->x_done[s], h->stream));
+    h->x_done_rec[s] = true;
     r.n_recv = m;
     r.n_act = n_act;
     r.recv_keys = recv_keys;
@@ -2109,8 +2191,9 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     r.status = st;
     r.perm = perm;
     r.offsets = offs;
-    h->mres = r;
-    h->mres_n = n;
+    h->mres[s] = r;
+    h->mres_n[s] = n;
+    h->mcalls += 1;
     h->routed += m;
     if (out) *out = r;
     return GD_OK;
@@ -2137,46 +2220,52 @@ int gd_comm_init(gd_handle* h, const uint8_t id[GD_COMM_ID_BYTES], int n_ranks, 
     const Rccl& R = rccl();
     if (!R.ok) return set_err(h, GD_ERCCL, "%s", R.why);
     HIP_TRY(h, hipSetDevice(h->device));
-    if (h->comm) {
-        GD_TRY(sync(h));
-        (void)R.CommDestroy(h->comm);
-        h->comm = nullptr;
-    }
-    if (!h->h_xcnt) HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 4 * 257 * sizeof(uint32_t)));
+    GD_TRY(sync(h));
+    comm_release(h);
+    HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 2 * 256 * sizeof(uint32_t)));
+    HIP_TRY(h, hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
+                          &h->x_ret[1], &h->x_done[0], &h->x_done[1]})
+        HIP_TRY(h, hipEventCreateWithFlags(e, hipEventDisableTiming));
     ncclUniqueId uid;
     std::memcpy(&uid, id, GD_COMM_ID_BYTES);
-    NCCL_TRY(h, R.CommInitRank(&h->comm, n_ranks, uid, rank));
+    const ncclResult_t e = R.CommInitRank(&h->comm, n_ranks, uid, rank);
+    if (e != ncclSuccess) {
+        h->comm = nullptr;
+        comm_release(h);
+        return set_err(h, GD_ERCCL, "ncclCommInitRank(%d of %d): %s", rank, n_ranks, R.GetErrorString(e));
+    }
     h->n_ranks = n_ranks;
     h->rank = rank;
-    h->mres = gd_multi_result{};
     return GD_OK;
 }
 
 int gd_comm_destroy(gd_handle* h) {
     if (!h) return set_err(h, GD_EINVAL, "null argument");
-    if (!h->comm) return GD_OK;
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(sync(h));
-    NCCL_TRY(h, rccl().CommDestroy(h->comm));
-    h->comm = nullptr;
-    h->n_ranks = 0;
-    h->rank = -1;
-    h->mres = gd_multi_result{};
+    comm_release(h);
     return GD_OK;
 }
 
-int gd_route_multi_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int return_routes,
+int gd_route_multi_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int flags,
                           gd_multi_result* out) {
     if (!h || (n && !d_keys)) return set_err(h, GD_EINVAL, "null argument");
-    return route_multi(h, d_keys, n, n_act, return_routes != 0, out);
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
+    HIP_TRY(h, hipSetDevice(h->device));
+    return route_multi(h, d_keys, n, n_act, flags, out);
 }
 
-int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, int return_routes,
-                   gd_multi_result* out) {
+int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, int flags, gd_multi_result* out) {
     if (!h || (n && !keys)) return set_err(h, GD_EINVAL, "null argument");
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
     HIP_TRY(h, hipSetDevice(h->device));
-    GD_TRY(h2d(h, h->keys_in, keys, n));
-    GD_TRY(route_multi(h, (const gd_key*)h->keys_in.p, n, n_act, return_routes != 0, out));
+    GD_TRY(need_comm(h));
+    // the batch goes to the device on the exchange stream, so the partition needs no other wait
+    GD_TRY(grow(h, h->mx_keys, (size_t)n * sizeof(gd_key) + 8));
+    if (n) HIP_TRY(h, hipMemcpyAsync(h->mx_keys.p, keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice, h->xstream));
+    GD_TRY(route_multi(h, (const gd_key*)h->mx_keys.p, n, n_act, flags | GD_MULTI_KEYS_READY, out));
+    HIP_TRY(h, hipStreamSynchronize(h->xstream));
     return sync_checked(h);
 }
 
@@ -2184,12 +2273,13 @@ int gd_multi_fetch(gd_handle* h, gd_key* recv_keys, uint32_t* recv_idx, uint32_t
                    uint32_t* act, uint8_t* status, uint32_t* perm, uint32_t* offsets, uint32_t* ret_silo,
                    uint32_t* ret_act, uint8_t* ret_status) {
     if (!h) return set_err(h, GD_EINVAL, "null argument");
-    const gd_multi_result& r = h->mres;
-    if (!r.offsets) return set_err(h, GD_ESTATE, "no gd_route_multi result on this handle");
+    if (h->mcalls == 0) return set_err(h, GD_ESTATE, "no gd_route_multi result on this handle");
+    const int s = (int)((h->mcalls - 1) & 1);
+    const gd_multi_result& r = h->mres[s];
     if (!r.ret_silo && (ret_silo || ret_act || ret_status))
-        return set_err(h, GD_EINVAL, "the last gd_route_multi ran without return_routes");
+        return set_err(h, GD_EINVAL, "the last gd_route_multi ran without GD_MULTI_RETURN_ROUTES");
     HIP_TRY(h, hipSetDevice(h->device));
-    const size_t m = r.n_recv, n = h->mres_n;
+    const size_t m = r.n_recv, n = h->mres_n[s];
     auto cp = [&](void* dst, const void* src, size_t bytes) -> int {
         if (dst && bytes) HIP_TRY(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
         return GD_OK;

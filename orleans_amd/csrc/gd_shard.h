@@ -38,35 +38,56 @@ __device__ __forceinline__ uint32_t key_dest(uint64_t n0, uint64_t n1, uint64_t 
 }
 
 // Item (w, r, lane) of a tile <-> record base + (w * SH_IT + r) * 64 + lane, as in k_radix_scatter.
+// Counts per wave by ballot matching (the lowest lane of each destination group adds the group's
+// size), not per-lane LDS atomics: with few destinations every lane of a wave would hit one
+// counter.  `bits` = destination bits (n_shards <= 1 << bits).
 template <int MODE, bool NODES>
 __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ recs, uint32_t n, uint64_t tcd,
-                                                      RingArgs ring, uint32_t n_shards, uint32_t tiles,
-                                                      uint8_t* __restrict__ dest, uint32_t* __restrict__ hist) {
+                                                      RingArgs ring, uint32_t n_shards, uint32_t bits,
+                                                      uint32_t tiles, uint8_t* __restrict__ dest,
+                                                      uint32_t* __restrict__ hist) {
+    constexpr int NW = SH_NT / WAVE;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
-    __shared__ uint32_t s_cnt[256];
+    __shared__ uint32_t s_wc[NW][256];
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
-    for (uint32_t d = threadIdx.x; d < 256; d += SH_NT) s_cnt[d] = 0;
+    for (uint32_t d = threadIdx.x; d < 256; d += SH_NT)
+#pragma unroll
+        for (int w = 0; w < NW; ++w) s_wc[w][d] = 0;
     stage_ring(ring, s_pts, s_own);
     const uint32_t base = blockIdx.x * SH_TILE;
     const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < SH_IT; ++r) {
         const uint32_t i = base + (w * SH_IT + r) * WAVE + lane;
-        if (i >= n) continue;
-        uint32_t d;
-        if constexpr (NODES) {
-            const uint32_t node = reinterpret_cast<const uint32_t*>(recs)[i];
-            d = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(0, node, tcd))] % n_shards;
-        } else {
-            const uint64_t* kp = reinterpret_cast<const uint64_t*>(recs) + 3ull * i;
-            d = key_dest<MODE>(kp[0], kp[1], kp[2], s_pts, s_own, ring, n_shards);
+        const bool valid = i < n;
+        uint32_t d = 0;
+        if (valid) {
+            if constexpr (NODES) {
+                const uint32_t node = reinterpret_cast<const uint32_t*>(recs)[i];
+                d = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(0, node, tcd))] % n_shards;
+            } else {
+                const uint64_t* kp = reinterpret_cast<const uint64_t*>(recs) + 3ull * i;
+                d = key_dest<MODE>(kp[0], kp[1], kp[2], s_pts, s_own, ring, n_shards);
+            }
+            dest[i] = (uint8_t)d;
         }
-        dest[i] = (uint8_t)d;
-        atomicAdd(&s_cnt[d], 1u);
+        unsigned long long peers = __ballot(valid);
+        for (uint32_t b = 0; b < bits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const unsigned long long bal = __ballot(bit);
+            peers &= bit ? bal : ~bal;
+        }
+        if (valid && (peers & lt) == 0) s_wc[w][d] += (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < n_shards; d += SH_NT) hist[d * tiles + blockIdx.x] = s_cnt[d];
+    for (uint32_t d = threadIdx.x; d < n_shards; d += SH_NT) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) t += s_wc[ww][d];
+        hist[d * tiles + blockIdx.x] = t;
+    }
 }
 
 // payload_in == nullptr: the payload is the record's batch index (the origin index).
@@ -212,12 +233,19 @@ __global__ void k_shard_counts(const uint32_t* __restrict__ gscan, uint32_t tile
     counts[d] = end - start;
 }
 
-// recv_src[i] = the rank chunk i of the receive buffer came from: roff[r] <= i < roff[r + 1]
-// (roff = exclusive scan of the receive counts, world + 1 entries, staged in LDS).
-__global__ void __launch_bounds__(BLOCK) k_recv_src(const uint32_t* __restrict__ roff, uint32_t world, uint32_t m,
+// recv_src[i] = the rank chunk i of the receive buffer came from: off[r] <= i < off[r + 1], off =
+// exclusive scan of the per-rank receive counts (world <= 256, scanned in LDS by every block).
+__global__ void __launch_bounds__(BLOCK) k_recv_src(const uint32_t* __restrict__ rcount, uint32_t world, uint32_t m,
                                                     uint32_t* __restrict__ src) {
     __shared__ uint32_t s_off[257];
-    for (uint32_t r = threadIdx.x; r <= world; r += BLOCK) s_off[r] = roff[r];
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t r = 0; r < world; ++r) {
+            s_off[r] = run;
+            run += rcount[r];
+        }
+        s_off[world] = run;
+    }
     __syncthreads();
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= m) return;

@@ -102,6 +102,8 @@ class gd_multi_result(C.Structure):
 
 
 GD_COMM_ID_BYTES = 128
+GD_MULTI_RETURN_ROUTES = 1
+GD_MULTI_KEYS_READY = 2
 
 
 class GrainDispatchError(RuntimeError):
@@ -599,10 +601,13 @@ class GrainDispatch:
     def comm_destroy(self):
         self._c(lib.gd_comm_destroy(self.h))
 
-    def route_multi_device(self, d_keys: int, n: int, n_act: int, return_routes: bool = False) -> gd_multi_result:
-        """Enqueue-only after the counts round: the result holds device pointers (library-owned)."""
+    def route_multi_device(self, d_keys: int, n: int, n_act: int, return_routes: bool = False,
+                           keys_ready: bool = False) -> gd_multi_result:
+        """Returns after the counts round; the rest is enqueued.  The result holds device pointers
+        into library-owned buffers, valid through the next call (two batches in flight)."""
         r = gd_multi_result()
-        self._c(lib.gd_route_multi_device(self.h, C.c_void_p(d_keys), n, n_act, int(return_routes), C.byref(r)))
+        flags = (GD_MULTI_RETURN_ROUTES if return_routes else 0) | (GD_MULTI_KEYS_READY if keys_ready else 0)
+        self._c(lib.gd_route_multi_device(self.h, C.c_void_p(d_keys), n, n_act, flags, C.byref(r)))
         return r
 
     def route_multi(self, keys, n_act: int, return_routes: bool = False) -> dict:
@@ -610,7 +615,8 @@ class GrainDispatch:
         k = keys_array(keys)
         n = k.shape[0]
         r = gd_multi_result()
-        self._c(lib.gd_route_multi(self.h, _ptr(k), n, n_act, int(return_routes), C.byref(r)))
+        flags = GD_MULTI_RETURN_ROUTES if return_routes else 0
+        self._c(lib.gd_route_multi(self.h, _ptr(k), n, n_act, flags, C.byref(r)))
         return self.multi_fetch(r, n)
 
     def multi_fetch(self, r: gd_multi_result, n: int) -> dict:

@@ -202,10 +202,16 @@ class LibraryRouter:
         t = uid.to(dev) if on_dev else uid
         dist.broadcast(t, src=0, group=group)
         engine.gd.comm_init(bytes(t.cpu().numpy().tobytes()), self.world, self.rank)
+        self.keys_ready = False
 
-    def route_bucket(self, keys: torch.Tensor, n_act: int, return_routes: bool = False) -> ShardedResult:
+    def route_bucket(self, keys: torch.Tensor, n_act: int, return_routes: bool = False,
+                     keys_ready: Optional[bool] = None) -> ShardedResult:
+        """keys_ready: `keys` are complete already (their producer was synchronised), so this
+        batch's partition + exchange may overlap the previous batch's probe + bucketing.  The
+        returned views stay valid through the next call.  None: the router's `keys_ready`."""
         n = keys.shape[0]
-        r = self.engine.gd.route_multi_device(keys.data_ptr(), n, n_act, return_routes)
+        keys_ready = self.keys_ready if keys_ready is None else keys_ready
+        r = self.engine.gd.route_multi_device(keys.data_ptr(), n, n_act, return_routes, keys_ready)
         m, dev = r.n_recv, self.engine.device
         return ShardedResult(_view(r.recv_keys, (m, 3), "<i8", dev), _view(r.recv_idx, (m,), "<i4", dev),
                              _view(r.recv_src, (m,), "<i4", dev), _view(r.status, (m,), "|u1", dev),

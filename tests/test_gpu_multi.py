@@ -162,3 +162,57 @@ def test_route_multi_two_ranks_one_gpu(tmp_path):
             np.testing.assert_array_equal(res[s]["ret_status"][sel], st)
             np.testing.assert_array_equal(res[s]["ret_act"][sel], act)
             np.testing.assert_array_equal(res[s]["ret_silo"][sel], silo)
+
+
+def test_route_multi_pipelined_batches(gd):
+    """GD_MULTI_KEYS_READY: batch i+1's partition + exchange (library exchange stream) overlap
+    batch i's probe + bucketing (handle stream); results of a batch stay valid through the next
+    call.  Five different batches, each checked after the call that follows it."""
+    import torch
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    G = 50000
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 17, my_silo=1)
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+    reg, own, _ = _directory(G, 1, 0, spec)
+    e.register(reg, np.arange(G), own)
+    e.comm_init(gd.GrainDispatch.comm_unique_id(), 1, 0)
+    stream = torch.cuda.Stream()
+    e.set_stream(stream.cuda_stream)
+    d = o.DirectoryArrays(reg, np.arange(G), own)
+    batches = [o.grain_keys(TC, np.random.default_rng(40 + i).integers(0, G + 500, size=200000 + 7919 * i))
+               for i in range(5)]
+    dev_keys = [torch.from_numpy(b.view(np.int64).copy()).cuda() for b in batches]
+    torch.cuda.synchronize()
+    prev = None
+    for i in range(len(batches) + 1):
+        if i < len(batches):
+            with torch.cuda.stream(stream):
+                r = e.route_multi_device(dev_keys[i].data_ptr(), len(batches[i]), G, return_routes=(i % 2 == 1),
+                                         keys_ready=True)
+            cur = (i, r)
+        if prev is not None:
+            j, rp = prev
+            e.synchronize()
+            m = rp.n_recv
+            assert m == len(batches[j])
+            act = torch.as_tensor(_Cai(rp.act, m), device="cuda").cpu().numpy().view(np.uint32)
+            perm = torch.as_tensor(_Cai(rp.perm, m), device="cuda").cpu().numpy().view(np.uint32)
+            offs = torch.as_tensor(_Cai(rp.offsets, G + 2), device="cuda").cpu().numpy().view(np.uint32)
+            st, silo, want_act, _, _ = o.route_batch_np(batches[j], spec, d, my_silo=1)
+            np.testing.assert_array_equal(act, want_act)
+            wp, wo = o.bucket_stable(want_act, G)
+            np.testing.assert_array_equal(perm, wp)
+            np.testing.assert_array_equal(offs, wo)
+            if j % 2 == 1:
+                ra = torch.as_tensor(_Cai(rp.ret_act, m), device="cuda").cpu().numpy().view(np.uint32)
+                np.testing.assert_array_equal(ra, want_act)
+        prev = cur if i < len(batches) else None
+    e.comm_destroy()
+    e.close()
+
+
+class _Cai:
+    def __init__(self, ptr, n):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i4", "data": (int(ptr), False), "version": 3,
+                                         "strides": None}
