@@ -58,7 +58,9 @@ def kernel_bytes(name: str, n: int, n_act: int, passes: int, world: int) -> floa
     if name == "k_route":
         return n * (24 + 32 + 4 + 4 + 1)          # key, one slot, silo+act+status
     if name == "k_radix_scatter":
-        return n * (12 + 16 * (passes - 1))       # pass 1 reads act only; later passes move (key, idx)
+        # pass 1 reads act, writes (key, idx); middle passes move (key, idx); the last pass reads
+        # (key, idx) and writes idx only (it emits the bucket starts instead of the sorted keys)
+        return n * 8 if passes == 1 else n * (12 + 16 * (passes - 2) + 12)
     if name == "k_radix_hist":
         return n * 4 * passes
     if name == "k_bucket_starts":

@@ -99,6 +99,7 @@ struct gd_handle {
     bool route_nt = false;
     int radix_max_bits = 8;   // digit width cap (GD_RADIX_MAXBITS, 4..11)
     int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
+    bool fused_starts = true;   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
 
     // per-kernel timing
@@ -342,7 +343,8 @@ int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inc
 // ---- K3 bucketing -------------------------------------------------------------
 template <int BITS, int NT, int IT>
 int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
-                 uint32_t* kout, uint32_t* vout, bool first) {
+                 uint32_t* kout, uint32_t* vout, bool first,
+                 uint32_t* offsets) {
     constexpr uint32_t TILE = NT * IT;
     const uint32_t tiles = blocks_for(n, TILE);
     const uint32_t R = 1u << BITS;
@@ -353,35 +355,37 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
     GD_TRY(scan_device<OpAdd>(h, hist, R * tiles, false, false, "hist"));
     if (first)
         return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, true, NT, IT>, kin, vin, n,
-                      clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic);
+                      clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets);
     return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, false, NT, IT>, kin, vin, n,
-                  clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic);
+                  clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets);
 }
 
 template <int BITS>
 int radix_pass(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
-               uint32_t* kout, uint32_t* vout, bool first) {
+               uint32_t* kout, uint32_t* vout, bool first,
+                 uint32_t* offsets) {
     switch (h->radix_cfg) {
-        case 1: return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        case 1: return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
         case 2:
-            if constexpr (BITS <= 8) return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first);
-            else return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first);
-        case 3: return radix_pass_t<BITS, 512, 16>(h, kin, vin, n, clamp, shift, kout, vout, first);
-        default: return radix_pass_t<BITS, 256, 16>(h, kin, vin, n, clamp, shift, kout, vout, first);
+            if constexpr (BITS <= 8) return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+            else return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+        case 3: return radix_pass_t<BITS, 512, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+        default: return radix_pass_t<BITS, 256, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
     }
 }
 
 int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp,
-                   uint32_t shift, uint32_t* kout, uint32_t* vout, bool first) {
+                   uint32_t shift, uint32_t* kout, uint32_t* vout, bool first,
+                 uint32_t* offsets) {
     switch (bits) {
-        case 4: return radix_pass<4>(h, kin, vin, n, clamp, shift, kout, vout, first);
-        case 5: return radix_pass<5>(h, kin, vin, n, clamp, shift, kout, vout, first);
-        case 6: return radix_pass<6>(h, kin, vin, n, clamp, shift, kout, vout, first);
-        case 7: return radix_pass<7>(h, kin, vin, n, clamp, shift, kout, vout, first);
-        case 8: return radix_pass<8>(h, kin, vin, n, clamp, shift, kout, vout, first);
-        case 9: return radix_pass<9>(h, kin, vin, n, clamp, shift, kout, vout, first);
-        case 10: return radix_pass<10>(h, kin, vin, n, clamp, shift, kout, vout, first);
-        default: return radix_pass<11>(h, kin, vin, n, clamp, shift, kout, vout, first);
+        case 4: return radix_pass<4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+        case 5: return radix_pass<5>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+        case 6: return radix_pass<6>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+        case 7: return radix_pass<7>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+        case 8: return radix_pass<8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+        case 9: return radix_pass<9>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+        case 10: return radix_pass<10>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+        default: return radix_pass<11>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
     }
 }
 
@@ -407,11 +411,16 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
     for (uint32_t p = 0; p < passes; ++p) {
         uint32_t* kout = kb[p & 1];
         uint32_t* vout = (p + 1 == passes) ? perm : vb[p & 1];
-        GD_TRY(radix_dispatch(h, (int)bits, kin, vin, n, n_act, p * bits, kout, vout, p == 0));
+        // the last pass writes the bucket starts itself (no sorted keys, no k_bucket_starts)
+        const bool last = p + 1 == passes && h->fused_starts;
+        GD_TRY(radix_dispatch(h, (int)bits, kin, vin, n, n_act, p * bits, kout, vout, p == 0,
+                              last ? offsets : nullptr));
         kin = kout;
         vin = vout;
     }
-    GD_TRY(launch(h, "k_bucket_starts", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_bucket_starts, kin, n, offsets));
+    if (!h->fused_starts)
+        GD_TRY(launch(h, "k_bucket_starts", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_bucket_starts, kin, n,
+                      offsets));
     return scan_device<OpMin>(h, offsets, n_act + 1, true, true, "offsets");
 }
 
@@ -535,6 +544,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
     if (const char* v = std::getenv("GD_RADIX_RANK")) h->radix_rank_atomic = std::atoi(v) ? 1u : 0u;
+    if (const char* v = std::getenv("GD_FUSED_STARTS")) h->fused_starts = std::atoi(v) != 0;
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));

@@ -632,13 +632,18 @@ __global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ 
 
 // Downsweep.  FIRST: values are the message indices themselves.  The keys are
 // clamped to `clamp` (unrouted messages -> trailing bucket).
+// starts != nullptr (the last pass): the output is fully sorted, so instead of the keys the
+// pass writes bucket starts -- the first item of each key in a tile's digit run (the run is
+// sorted by the whole key: the lower passes ordered it) lowers starts[key] to its output
+// position with atomicMin; the earliest tile holding the key wins (starts pre-filled with n).
 template <int BITS, bool FIRST, int NT, int IT>
 __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                       const uint32_t* __restrict__ vals_in, uint32_t n,
                                                       uint32_t clamp, uint32_t shift, uint32_t tiles,
                                                       const uint32_t* __restrict__ gscan,
                                                       uint32_t* __restrict__ keys_out,
-                                                      uint32_t* __restrict__ vals_out, uint32_t rank_atomic) {
+                                                      uint32_t* __restrict__ vals_out, uint32_t rank_atomic,
+                                                      uint32_t* __restrict__ starts) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = NT / WAVE;
     constexpr uint32_t TILE = NT * IT;
@@ -772,7 +777,11 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
             const uint32_t d = (kv.x >> shift) & (R - 1);
             const uint32_t g = s_gbase[d] + (p - s_lstart[d]);
             if (g < n) {            // always true when the scan is right; never write out of bounds
-                keys_out[g] = kv.x;
+                if (starts) {
+                    if (p == s_lstart[d] || s_kv[p - 1].x != kv.x) atomicMin(&starts[kv.x], g);
+                } else {
+                    keys_out[g] = kv.x;
+                }
                 vals_out[g] = kv.y;
             }
         }
