@@ -99,6 +99,7 @@ struct gd_handle {
     bool route_nt = false;
     int radix_max_bits = 8;   // digit width cap (GD_RADIX_MAXBITS, 4..11)
     int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
+    uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
     bool fused_starts = true;   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
 
@@ -355,9 +356,9 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
     GD_TRY(scan_device<OpAdd>(h, hist, R * tiles, false, false, "hist"));
     if (first)
         return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, true, NT, IT>, kin, vin, n,
-                      clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets);
+                      clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets, h->xcd_tiles);
     return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, false, NT, IT>, kin, vin, n,
-                  clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets);
+                  clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets, h->xcd_tiles);
 }
 
 template <int BITS>
@@ -545,6 +546,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
     if (const char* v = std::getenv("GD_RADIX_RANK")) h->radix_rank_atomic = std::atoi(v) ? 1u : 0u;
     if (const char* v = std::getenv("GD_FUSED_STARTS")) h->fused_starts = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_XCD_TILES")) h->xcd_tiles = std::atoi(v) ? 1u : 0u;
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));

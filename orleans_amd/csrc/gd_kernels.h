@@ -630,6 +630,16 @@ __global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ 
     }
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each with its own
+// L2.  With xcd != 0 block b processes tile start(b % 8) + b / 8, so every XCD owns a contiguous
+// tile range: the digit-run fragments that consecutive tiles write next to each other in the
+// output meet in one L2 instead of being written back as partial lines by two.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb, uint32_t xcd) {
+    if (!xcd) return b;
+    const uint32_t x = b & 7u, k = b >> 3, q = nb >> 3, rem = nb & 7u;
+    return x * q + min(x, rem) + k;
+}
+
 // Downsweep.  FIRST: values are the message indices themselves.  The keys are
 // clamped to `clamp` (unrouted messages -> trailing bucket).
 // starts != nullptr (the last pass): the output is fully sorted, so instead of the keys the
@@ -643,7 +653,7 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ gscan,
                                                       uint32_t* __restrict__ keys_out,
                                                       uint32_t* __restrict__ vals_out, uint32_t rank_atomic,
-                                                      uint32_t* __restrict__ starts) {
+                                                      uint32_t* __restrict__ starts, uint32_t xcd) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = NT / WAVE;
     constexpr uint32_t TILE = NT * IT;
@@ -653,7 +663,7 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
     __shared__ uint2 s_kv[TILE];
     __shared__ uint32_t s_wsum[NW];
 
-    const uint32_t tile = blockIdx.x;
+    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, xcd);
     const uint32_t base = tile * TILE;
     const uint32_t cnt_tile = min(TILE, n - base);
     for (uint32_t d = threadIdx.x; d < R; d += NT) {
