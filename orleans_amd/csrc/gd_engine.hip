@@ -319,10 +319,11 @@ int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inc
     uint32_t* part = (uint32_t*)h->partials.p;
     (void)tag;
     GD_TRY(launch(h, "k_scan_reduce", dim3(nb), dim3(BLOCK), 0, k_scan_reduce<Op>, (const uint32_t*)data, n, reverse, part));
-    // few blocks: every block folds its predecessors' aggregates itself (2 launches);
+    // few blocks (<= 2048: each block then reads <= 8 aggregates per thread): every block folds its
+    // predecessors' aggregates itself (2 launches);
     // many: the aggregates are scanned in between -- by the same two-launch fold scan one level
     // up while that has <= 1024 blocks (4 launches), else by one block (3 launches)
-    const bool fold = nb <= 1024;
+    const bool fold = nb <= 2048;
     if (!fold) {
         const uint32_t nb2 = blocks_for(nb, SCAN_TILE);
         if (nb2 <= 1024) {
