@@ -181,6 +181,57 @@ int gd_dir_clear(gd_handle* h);
 /* Rebuild into a table of new_capacity slots (drops tombstones). */
 int gd_dir_rehash(gd_handle* h, uint64_t new_capacity);
 
+/* ---- KeyExt grains (string keys, compound keys, geo clients) ---------
+ * UniqueKey.HasKeyExt categories (KeyExtGrain 6, GeoClient 7; UniqueKey.cs:60-66) hash
+ * JenkinsHash.ComputeHash(ToByteArray()) = N0|N1|TCD|int32 len|UTF-8 when KeyExt != null
+ * (UniqueKey.cs:272-336) and compare the KeyExt string (UniqueKey.cs:245-251).  They live in a
+ * second table (64-B slots + a KeyExt byte heap).  A batch's KeyExt strings travel beside the
+ * 24-B keys: message i's UTF-8 bytes are bytes[offset[i] .. offset[i] + length[i]).  Messages
+ * of other categories ignore their entry.  Equality is on UTF-8 bytes, which is C#'s ordinal
+ * equality except for strings with unpaired surrogates (Encoding.UTF8 maps them to U+FFFD):
+ * send those as GD_KEYEXT_HOST and they keep status GD_ROUTE_KEYEXT. */
+#define GD_KEYEXT_NULL (-1)   /* KeyExt == null: three-word hash; equal only to a null KeyExt */
+#define GD_KEYEXT_HOST (-2)   /* leave the message to the C# path (status GD_ROUTE_KEYEXT)    */
+typedef struct gd_key_ext {
+    const uint8_t*  bytes;      /* UTF-8 KeyExt strings of the batch, concatenated      */
+    const uint64_t* offset;     /* [n] start of message i's string in bytes              */
+    const int32_t*  length;     /* [n] UTF-8 byte length, GD_KEYEXT_NULL or GD_KEYEXT_HOST */
+    uint64_t        bytes_len;  /* size of bytes (offset + length beyond it -> KEYEXT)  */
+} gd_key_ext;
+
+/* AddSingleActivation / RemoveActivation / LookUpActivations for KeyExt grains, batch order,
+ * first registration wins (as gd_dir_register).  Keys must have a KeyExt category (GD_EINVAL
+ * otherwise).  Registrations are applied to a host-side index of the table and the changed
+ * slots uploaded (registration is off the per-message path); lookups run on the GPU.
+ * Host pointers (ext included). */
+int gd_dir_register_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, const gd_val* vals, uint32_t n,
+                        gd_val* out_vals, uint8_t* out_inserted);
+int gd_dir_unregister_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, const uint32_t* acts,
+                          uint32_t n, uint8_t* out_removed);
+int gd_dir_lookup_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, gd_val* out_vals,
+                      uint8_t* out_found);
+/* UniqueKey.GetUniformHashCode of KeyExt keys computed on the device (the hash k_route_keyext
+ * uses; 0 for GD_KEYEXT_HOST items).  Host pointers. */
+int gd_uniform_hashes_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t* out);
+/* KeyExt entries, capacity, heap bytes in use. */
+int gd_dir_ext_stats(gd_handle* h, uint64_t* live, uint64_t* capacity, uint64_t* heap_bytes);
+
+/* gd_route / gd_route_bucket with KeyExt grains routed on the GPU too (their status is then
+ * OK or MISS like any grain; GD_KEYEXT_HOST items stay GD_ROUTE_KEYEXT).  ext == NULL behaves
+ * as gd_route.  Host pointers. */
+int gd_route_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n,
+                 uint32_t* out_silo, uint32_t* out_act, uint8_t* out_status);
+int gd_route_bucket_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t n_act,
+                        uint32_t* out_silo, uint32_t* out_act, uint8_t* out_status,
+                        uint32_t* out_perm, uint32_t* out_offsets);
+/* Device forms: d_keys and the arrays inside *d_ext are device pointers (d_ext itself is a host
+ * struct).  Enqueue only. */
+int gd_route_ext_device(gd_handle* h, const gd_key* d_keys, const gd_key_ext* d_ext, uint32_t n,
+                        uint32_t* d_silo, uint32_t* d_act, uint8_t* d_status);
+int gd_route_bucket_ext_device(gd_handle* h, const gd_key* d_keys, const gd_key_ext* d_ext, uint32_t n,
+                               uint32_t n_act, uint32_t* d_silo, uint32_t* d_act, uint8_t* d_status,
+                               uint32_t* d_perm, uint32_t* d_offsets);
+
 /* ---- the hot path -------------------------------------------------------------- */
 /* Address a batch: ring lookup + directory probe.  Host pointers. */
 int gd_route(gd_handle* h, const gd_key* keys, uint32_t n,

@@ -60,6 +60,21 @@ struct alignas(32) Slot {
 };
 static_assert(sizeof(Slot) == 32, "slot must be 32 bytes");
 
+// KeyExt grain slot (gd_keyext.h): one 64-B DRAM atom -- the three words, the KeyExt string's
+// place in the KeyExt heap, its uniform hash (compared before the bytes) and the value.
+struct alignas(64) KxSlot {
+    uint64_t n0;
+    uint64_t n1;
+    uint64_t tcd;
+    uint64_t off;       // heap offset of the UTF-8 KeyExt
+    int32_t len;        // UTF-8 length, GD_KEYEXT_NULL = null KeyExt
+    uint32_t uhash;     // UniqueKey.GetUniformHashCode
+    uint32_t act;
+    uint32_t meta;      // (state << 16) | silo
+    uint64_t pad[2];
+};
+static_assert(sizeof(KxSlot) == 64, "KeyExt slot must be 64 bytes");
+
 GD_HD uint32_t slot_state(uint32_t meta) { return meta >> 16; }
 GD_HD uint32_t slot_silo(uint32_t meta) { return meta & 0xFFFFu; }
 GD_HD uint32_t make_meta(uint32_t state, uint32_t silo) { return (state << 16) | (silo & 0xFFFFu); }

@@ -19,6 +19,7 @@
 #include "gd_cache.h"
 #include "gd_shard.h"
 #include "gd_comm.h"
+#include "gd_keyext.h"
 #include "gd_frames.h"
 #include "graindispatch.h"
 
@@ -75,6 +76,17 @@ struct gd_handle {
     DevBuf cache_local, cache_valid;
     DevBuf cbuf[8];                   // cache scratch
     DevBuf shard_dest, shard_hist;    // exchange partition scratch
+
+    // KeyExt grains (gd_keyext.h): device table + heap, and the host index both are kept from
+    KxSlot* kx_slots = nullptr;
+    uint64_t kx_cap = 0;
+    DevBuf kx_heap;
+    uint64_t kx_heap_dev = 0;          // host heap bytes already on the device
+    std::vector<KxSlot> kx_m;          // host index (same layout as the device table)
+    std::vector<uint8_t> kx_hheap;
+    uint64_t kx_live = 0, kx_tomb = 0;
+    uint32_t kx_maxp = 0;
+    DevBuf kx_buf[5];                  // apply / ext staging scratch
 
     // in-library exchange over RCCL (gd_comm.h): one communicator per handle.  The partition and
     // the RCCL rounds run on xstream; probe + bucketing on `stream`; batch i's exchange overlaps
@@ -601,6 +613,9 @@ void gd_destroy(gd_handle* h) {
     free_buf(h->shard_dest);
     free_buf(h->shard_hist);
     comm_release(h);
+    if (h->kx_slots) (void)hipFree(h->kx_slots);
+    free_buf(h->kx_heap);
+    for (DevBuf& b : h->kx_buf) free_buf(b);
     free_buf(h->cache_valid);
     if (h->cslots) (void)hipFree(h->cslots);
     if (h->cctr) (void)hipFree(h->cctr);
@@ -796,6 +811,14 @@ int gd_dir_clear(gd_handle* h) {
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, hipMemsetAsync(h->slots, 0, h->capacity * sizeof(Slot), h->stream));
     HIP_TRY(h, hipMemsetAsync(h->ctr, 0, sizeof(DevCounters), h->stream));
+    if (h->kx_cap) {                   // KeyExt entries go too
+        h->kx_m.assign(h->kx_cap, KxSlot{});
+        h->kx_hheap.clear();
+        h->kx_live = h->kx_tomb = 0;
+        h->kx_maxp = 0;
+        h->kx_heap_dev = 0;
+        HIP_TRY(h, hipMemsetAsync(h->kx_slots, 0, h->kx_cap * sizeof(KxSlot), h->stream));
+    }
     return sync(h);
 }
 
@@ -2310,6 +2333,384 @@ int gd_multi_fetch(gd_handle* h, gd_key* recv_keys, uint32_t* recv_idx, uint32_t
         GD_TRY(cp(ret_act, r.ret_act, n * 4));
         GD_TRY(cp(ret_status, r.ret_status, n));
     }
+    return sync(h);
+}
+
+// ================================================================== KeyExt grains (gd_keyext.h)
+namespace {
+
+bool is_keyext_cat(uint64_t tcd) {
+    const uint32_t c = (uint32_t)(tcd >> 56);
+    return c == CAT_KEYEXT_GRAIN || c == CAT_GEO_CLIENT;
+}
+
+// UniqueKey.GetUniformHashCode of a KeyExt-category key (UniqueKey.cs:272-336).
+uint32_t kx_hash_host(const gd_key& k, const uint8_t* s, int32_t len) {
+    if (len < 0) return jenkins_u64x3(k.type_code_data, k.n0, k.n1);
+    std::vector<uint8_t> b(28 + (size_t)len);
+    std::memcpy(b.data(), &k.n0, 8);
+    std::memcpy(b.data() + 8, &k.n1, 8);
+    std::memcpy(b.data() + 16, &k.type_code_data, 8);
+    std::memcpy(b.data() + 24, &len, 4);
+    if (len) std::memcpy(b.data() + 28, s, (size_t)len);
+    return jenkins_bytes(b.data(), b.size());
+}
+
+// Host view of message i's KeyExt (validated: GD_EINVAL for GD_KEYEXT_HOST or a bad range).
+int host_ext(gd_handle* h, const gd_key_ext* ext, uint32_t i, const uint8_t*& s, int32_t& len) {
+    len = ext->length[i];
+    s = nullptr;
+    if (len == GD_KEYEXT_NULL) return GD_OK;
+    if (len < 0) return set_err(h, GD_EINVAL, "item %u: KeyExt length %d (GD_KEYEXT_HOST is for routing only)", i, len);
+    const uint64_t off = ext->offset[i];
+    if (off > ext->bytes_len || (uint64_t)len > ext->bytes_len - off)
+        return set_err(h, GD_EINVAL, "item %u: KeyExt [%llu, +%d) outside the %llu-byte buffer", i,
+                       (unsigned long long)off, len, (unsigned long long)ext->bytes_len);
+    s = ext->bytes + off;
+    return GD_OK;
+}
+
+// Probe the host index: the live equal entry, else the first reusable slot on the way.
+bool kx_find_host(gd_handle* h, const gd_key& k, const uint8_t* s, int32_t len, uint32_t uh, uint64_t* at,
+                  uint64_t* free_at, uint32_t* dist) {
+    const uint64_t mask = h->kx_cap - 1;
+    uint64_t i = fmix32(uh) & mask;
+    *free_at = UINT64_MAX;
+    for (uint64_t p = 0; p < h->kx_cap; ++p, i = (i + 1) & mask) {
+        const KxSlot& q = h->kx_m[i];
+        const uint32_t st = slot_state(q.meta);
+        if (st == SLOT_EMPTY) {
+            if (*free_at == UINT64_MAX) {
+                *free_at = i;
+                *dist = (uint32_t)p;
+            }
+            return false;
+        }
+        if (st == SLOT_TOMB) {
+            if (*free_at == UINT64_MAX) {
+                *free_at = i;
+                *dist = (uint32_t)p;
+            }
+            continue;
+        }
+        if (q.uhash == uh && q.len == len && q.n0 == k.n0 && q.n1 == k.n1 && q.tcd == k.type_code_data &&
+            (len <= 0 || std::memcmp(h->kx_hheap.data() + q.off, s, (size_t)len) == 0)) {
+            *at = i;
+            return true;
+        }
+    }
+    return false;
+}
+
+int kx_upload_all(gd_handle* h) {
+    if (h->kx_slots) {
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+        HIP_TRY(h, hipFree(h->kx_slots));
+        h->kx_slots = nullptr;
+    }
+    hipError_t e = hipMalloc((void**)&h->kx_slots, h->kx_cap * sizeof(KxSlot));
+    if (e != hipSuccess) return set_err(h, GD_ENOMEM, "KeyExt table (%llu slots): %s",
+                                        (unsigned long long)h->kx_cap, hipGetErrorString(e));
+    HIP_TRY(h, hipMemcpyAsync(h->kx_slots, h->kx_m.data(), h->kx_cap * sizeof(KxSlot), hipMemcpyHostToDevice,
+                              h->stream));
+    GD_TRY(ensure(h, h->kx_heap, std::max<size_t>(2 * h->kx_hheap.size(), 1 << 16)));   // room to append
+    if (!h->kx_hheap.empty())
+        HIP_TRY(h, hipMemcpyAsync(h->kx_heap.p, h->kx_hheap.data(), h->kx_hheap.size(), hipMemcpyHostToDevice,
+                                  h->stream));
+    h->kx_heap_dev = h->kx_hheap.size();
+    h->layout_gen++;
+    return sync(h);
+}
+
+// Rebuild the host index at cap slots (tombstones dropped, heap compacted), then upload it whole.
+int kx_rehash(gd_handle* h, uint64_t cap) {
+    std::vector<KxSlot> old;
+    old.swap(h->kx_m);
+    std::vector<uint8_t> old_heap;
+    old_heap.swap(h->kx_hheap);
+    h->kx_cap = cap;
+    h->kx_m.assign(cap, KxSlot{});
+    h->kx_live = h->kx_tomb = 0;
+    h->kx_maxp = 0;
+    const uint64_t mask = cap - 1;
+    for (const KxSlot& q : old) {
+        if (slot_state(q.meta) != SLOT_LIVE) continue;
+        KxSlot v = q;
+        if (q.len > 0) {
+            v.off = h->kx_hheap.size();
+            h->kx_hheap.insert(h->kx_hheap.end(), old_heap.begin() + q.off, old_heap.begin() + q.off + q.len);
+        }
+        uint64_t i = fmix32(q.uhash) & mask;
+        uint32_t p = 0;
+        while (slot_state(h->kx_m[i].meta) != SLOT_EMPTY) {
+            i = (i + 1) & mask;
+            ++p;
+        }
+        h->kx_m[i] = v;
+        h->kx_maxp = std::max(h->kx_maxp, p);
+        h->kx_live++;
+    }
+    return kx_upload_all(h);
+}
+
+// Push the host index changes: new heap bytes, then the changed slots.
+int kx_commit(gd_handle* h, std::vector<uint64_t>& dirty) {
+    if (h->kx_hheap.size() > h->kx_heap.bytes) {
+        std::sort(dirty.begin(), dirty.end());
+        return kx_upload_all(h);   // the device heap grows: upload table + heap whole
+    }
+    if (h->kx_hheap.size() > h->kx_heap_dev) {
+        HIP_TRY(h, hipMemcpyAsync((uint8_t*)h->kx_heap.p + h->kx_heap_dev, h->kx_hheap.data() + h->kx_heap_dev,
+                                  h->kx_hheap.size() - h->kx_heap_dev, hipMemcpyHostToDevice, h->stream));
+        h->kx_heap_dev = h->kx_hheap.size();
+    }
+    std::sort(dirty.begin(), dirty.end());
+    dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+    const uint32_t m = (uint32_t)dirty.size();
+    if (m == 0) return sync(h);
+    if ((uint64_t)m * 4 > h->kx_cap) {
+        HIP_TRY(h, hipMemcpyAsync(h->kx_slots, h->kx_m.data(), h->kx_cap * sizeof(KxSlot), hipMemcpyHostToDevice,
+                                  h->stream));
+        return sync(h);
+    }
+    std::vector<KxSlot> vals(m);
+    for (uint32_t j = 0; j < m; ++j) vals[j] = h->kx_m[dirty[j]];
+    GD_TRY(h2d(h, h->kx_buf[0], dirty.data(), m));
+    GD_TRY(h2d(h, h->kx_buf[1], vals.data(), m));
+    GD_TRY(launch(h, "k_kx_apply", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_kx_apply,
+                  (const uint64_t*)h->kx_buf[0].p, (const KxSlot*)h->kx_buf[1].p, m, h->kx_slots));
+    return sync(h);
+}
+
+KxArgs kx_args(gd_handle* h) {
+    return KxArgs{h->kx_slots, h->kx_cap ? h->kx_cap - 1 : 0ull, h->kx_maxp, (const uint8_t*)h->kx_heap.p};
+}
+
+extern "C++" {
+template <int MODE>
+int route_keyext_t(gd_handle* h, const gd_key* keys, const ExtArgs& x, uint32_t n, uint32_t* silo, uint32_t* act,
+                   uint8_t* st) {
+    return launch(h, "k_route_keyext", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), ring_lds(h), k_route_keyext<MODE>,
+                  keys, n, x, ring_args(h), kx_args(h), silo, act, st);
+}
+}
+
+// Route (24-B keys) then the KeyExt pass over what it left at GD_ROUTE_KEYEXT.
+int route_ext_device(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t* silo,
+                     uint32_t* act, uint8_t* st) {
+    GD_TRY(route_device(h, keys, n, silo, act, st));
+    if (!ext || n == 0 || h->cache_max) return GD_OK;   // LocalLookup mode: KeyExt grains stay in C#
+    const ExtArgs x{ext->bytes, ext->offset, ext->length, ext->bytes_len};
+    switch (h->ring_mode) {
+        case GD_RING_DIRECTORY: return route_keyext_t<GD_RING_DIRECTORY>(h, keys, x, n, silo, act, st);
+        case GD_RING_CONSISTENT: return route_keyext_t<GD_RING_CONSISTENT>(h, keys, x, n, silo, act, st);
+        default: return route_keyext_t<GD_RING_VIRTUAL_BUCKETS>(h, keys, x, n, silo, act, st);
+    }
+}
+
+// Host ext -> device copies in kx_buf[2..4]; *dx gets the device form.
+int stage_ext(gd_handle* h, const gd_key_ext* ext, uint32_t n, gd_key_ext* dx) {
+    GD_TRY(h2d(h, h->kx_buf[2], ext->bytes, (size_t)ext->bytes_len));
+    GD_TRY(h2d(h, h->kx_buf[3], ext->offset, n));
+    GD_TRY(h2d(h, h->kx_buf[4], ext->length, n));
+    *dx = gd_key_ext{(const uint8_t*)h->kx_buf[2].p, (const uint64_t*)h->kx_buf[3].p,
+                     (const int32_t*)h->kx_buf[4].p, ext->bytes_len};
+    return GD_OK;
+}
+
+bool ext_ok(const gd_key_ext* ext, uint32_t n) {
+    return !ext || n == 0 || (ext->offset && ext->length && (ext->bytes || ext->bytes_len == 0));
+}
+
+}  // namespace
+
+int gd_dir_register_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, const gd_val* vals, uint32_t n,
+                        gd_val* out_vals, uint8_t* out_inserted) {
+    if (!h || (n && (!keys || !ext || !vals || !ext_ok(ext, n)))) return set_err(h, GD_EINVAL, "null argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    std::vector<uint32_t> uh(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!is_keyext_cat(keys[i].type_code_data))
+            return set_err(h, GD_EINVAL, "item %u: category %u has no KeyExt (use gd_dir_register)", i,
+                           (unsigned)(keys[i].type_code_data >> 56));
+        const uint8_t* s;
+        int32_t len;
+        GD_TRY(host_ext(h, ext, i, s, len));
+        uh[i] = kx_hash_host(keys[i], s, len);
+    }
+    if (h->kx_cap == 0 || (h->kx_live + h->kx_tomb + n) * 2 > h->kx_cap) {
+        uint64_t cap = std::max<uint64_t>(h->kx_cap, 1024);
+        while ((h->kx_live + n) * 2 > cap) cap *= 2;
+        GD_TRY(kx_rehash(h, cap));
+    }
+    std::vector<uint64_t> dirty;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* s;
+        int32_t len;
+        GD_TRY(host_ext(h, ext, i, s, len));
+        uint64_t at = 0, free_at = 0;
+        uint32_t dist = 0;
+        if (kx_find_host(h, keys[i], s, len, uh[i], &at, &free_at, &dist)) {     // first registration wins
+            if (out_vals) out_vals[i] = gd_val{h->kx_m[at].act, slot_silo(h->kx_m[at].meta)};
+            if (out_inserted) out_inserted[i] = 0;
+            continue;
+        }
+        if (free_at == UINT64_MAX) return set_err(h, GD_EFULL, "KeyExt table full");
+        KxSlot& q = h->kx_m[free_at];
+        if (slot_state(q.meta) == SLOT_TOMB) h->kx_tomb--;
+        q = KxSlot{};
+        q.n0 = keys[i].n0;
+        q.n1 = keys[i].n1;
+        q.tcd = keys[i].type_code_data;
+        q.len = len;
+        q.uhash = uh[i];
+        q.act = vals[i].act;
+        q.meta = make_meta(SLOT_LIVE, vals[i].silo);
+        if (len > 0) {
+            q.off = h->kx_hheap.size();
+            h->kx_hheap.insert(h->kx_hheap.end(), s, s + len);
+        }
+        h->kx_live++;
+        h->kx_maxp = std::max(h->kx_maxp, dist);
+        dirty.push_back(free_at);
+        if (out_vals) out_vals[i] = vals[i];
+        if (out_inserted) out_inserted[i] = 1;
+    }
+    return kx_commit(h, dirty);
+}
+
+int gd_dir_unregister_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, const uint32_t* acts, uint32_t n,
+                          uint8_t* out_removed) {
+    if (!h || (n && (!keys || !ext || !acts || !ext_ok(ext, n)))) return set_err(h, GD_EINVAL, "null argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    std::vector<uint64_t> dirty;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* s;
+        int32_t len;
+        GD_TRY(host_ext(h, ext, i, s, len));
+        uint64_t at = 0, free_at = 0;
+        uint32_t dist = 0;
+        bool removed = false;
+        if (h->kx_cap && kx_find_host(h, keys[i], s, len, kx_hash_host(keys[i], s, len), &at, &free_at, &dist) &&
+            h->kx_m[at].act == acts[i]) {          // RemoveActivation: only the matching activation
+            h->kx_m[at].meta = make_meta(SLOT_TOMB, slot_silo(h->kx_m[at].meta));
+            h->kx_live--;
+            h->kx_tomb++;
+            dirty.push_back(at);
+            removed = true;
+        }
+        if (out_removed) out_removed[i] = removed ? 1 : 0;
+    }
+    return kx_commit(h, dirty);
+}
+
+int gd_dir_lookup_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, gd_val* out_vals,
+                      uint8_t* out_found) {
+    if (!h || (n && (!keys || !ext || !out_vals || !out_found || !ext_ok(ext, n))))
+        return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t* s;
+        int32_t len;
+        GD_TRY(host_ext(h, ext, i, s, len));
+    }
+    gd_key_ext dx;
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(stage_ext(h, ext, n, &dx));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * sizeof(gd_val)));
+    GD_TRY(ensure(h, h->out_c, (size_t)n));
+    const ExtArgs x{dx.bytes, dx.offset, dx.length, dx.bytes_len};
+    GD_TRY(launch(h, "k_kx_lookup", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_kx_lookup,
+                  (const gd_key*)h->keys_in.p, n, x, kx_args(h), (gd_val*)h->out_a.p, (uint8_t*)h->out_c.p));
+    GD_TRY(d2h(h, out_vals, h->out_a, n));
+    GD_TRY(d2h(h, out_found, h->out_c, n));
+    return sync(h);
+}
+
+int gd_dir_ext_stats(gd_handle* h, uint64_t* live, uint64_t* capacity, uint64_t* heap_bytes) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (live) *live = h->kx_live;
+    if (capacity) *capacity = h->kx_cap;
+    if (heap_bytes) *heap_bytes = h->kx_hheap.size();
+    return GD_OK;
+}
+
+int gd_route_ext_device(gd_handle* h, const gd_key* d_keys, const gd_key_ext* d_ext, uint32_t n, uint32_t* d_silo,
+                        uint32_t* d_act, uint8_t* d_status) {
+    if (!h || (n && (!d_keys || !d_silo || !d_act || !d_status || !ext_ok(d_ext, n))))
+        return set_err(h, GD_EINVAL, "null argument");
+    return n ? route_ext_device(h, d_keys, d_ext, n, d_silo, d_act, d_status) : GD_OK;
+}
+
+int gd_route_bucket_ext_device(gd_handle* h, const gd_key* d_keys, const gd_key_ext* d_ext, uint32_t n,
+                               uint32_t n_act, uint32_t* d_silo, uint32_t* d_act, uint8_t* d_status,
+                               uint32_t* d_perm, uint32_t* d_offsets) {
+    if (!h || !d_offsets || (n && (!d_keys || !d_silo || !d_act || !d_status || !d_perm || !ext_ok(d_ext, n))))
+        return set_err(h, GD_EINVAL, "null argument");
+    if (n) GD_TRY(route_ext_device(h, d_keys, d_ext, n, d_silo, d_act, d_status));
+    return bucket_device(h, d_act, n, n_act, d_perm, d_offsets);
+}
+
+int gd_route_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t* out_silo,
+                 uint32_t* out_act, uint8_t* out_status) {
+    if (!h || (n && (!keys || !out_silo || !out_act || !out_status || !ext_ok(ext, n))))
+        return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    gd_key_ext dx{};
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    if (ext) GD_TRY(stage_ext(h, ext, n, &dx));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * 4));
+    GD_TRY(ensure(h, h->out_b, (size_t)n * 4));
+    GD_TRY(ensure(h, h->out_c, (size_t)n));
+    GD_TRY(route_ext_device(h, (const gd_key*)h->keys_in.p, ext ? &dx : nullptr, n, (uint32_t*)h->out_a.p,
+                            (uint32_t*)h->out_b.p, (uint8_t*)h->out_c.p));
+    GD_TRY(d2h(h, out_silo, h->out_a, n));
+    GD_TRY(d2h(h, out_act, h->out_b, n));
+    GD_TRY(d2h(h, out_status, h->out_c, n));
+    return sync(h);
+}
+
+int gd_route_bucket_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t n_act,
+                        uint32_t* out_silo, uint32_t* out_act, uint8_t* out_status, uint32_t* out_perm,
+                        uint32_t* out_offsets) {
+    if (!h || !out_offsets || (n && (!keys || !out_silo || !out_act || !out_status || !out_perm || !ext_ok(ext, n))))
+        return set_err(h, GD_EINVAL, "null argument");
+    if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    HIP_TRY(h, hipSetDevice(h->device));
+    gd_key_ext dx{};
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    if (ext && n) GD_TRY(stage_ext(h, ext, n, &dx));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * 4 + 4));
+    GD_TRY(ensure(h, h->out_b, (size_t)n * 4 + 4));
+    GD_TRY(ensure(h, h->out_c, (size_t)n + 4));
+    GD_TRY(ensure(h, h->u8_a, (size_t)n * 4 + 4));   // perm
+    GD_TRY(ensure(h, h->offs, ((size_t)n_act + 2) * 4));
+    if (n)
+        GD_TRY(route_ext_device(h, (const gd_key*)h->keys_in.p, ext ? &dx : nullptr, n, (uint32_t*)h->out_a.p,
+                                (uint32_t*)h->out_b.p, (uint8_t*)h->out_c.p));
+    GD_TRY(bucket_device(h, (const uint32_t*)h->out_b.p, n, n_act, (uint32_t*)h->u8_a.p, (uint32_t*)h->offs.p));
+    GD_TRY(d2h(h, out_silo, h->out_a, n));
+    GD_TRY(d2h(h, out_act, h->out_b, n));
+    GD_TRY(d2h(h, out_status, h->out_c, n));
+    GD_TRY(d2h(h, out_perm, h->u8_a, n));
+    GD_TRY(d2h(h, out_offsets, h->offs, (size_t)n_act + 2));
+    return sync_checked(h);
+}
+
+int gd_uniform_hashes_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t* out) {
+    if (!h || (n && (!keys || !ext || !out || !ext_ok(ext, n)))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    gd_key_ext dx;
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(stage_ext(h, ext, n, &dx));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * 4));
+    const ExtArgs x{dx.bytes, dx.offset, dx.length, dx.bytes_len};
+    GD_TRY(launch(h, "k_kx_hash", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_kx_hash, (const gd_key*)h->keys_in.p,
+                  n, x, (uint32_t*)h->out_a.p));
+    GD_TRY(d2h(h, out, h->out_a, n));
     return sync(h);
 }
 

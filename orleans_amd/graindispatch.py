@@ -44,6 +44,8 @@ EXPORTED_SYMBOLS = [
     "gd_pack_nodes_by_shard_device", "gd_frontier_next_device",
     "gd_cache_configure", "gd_cache_set_silos", "gd_cache_add", "gd_cache_remove", "gd_cache_lookup",
     "gd_cache_clear", "gd_cache_stats_get", "gd_cache_entries",
+    "gd_dir_register_ext", "gd_dir_unregister_ext", "gd_dir_lookup_ext", "gd_uniform_hashes_ext",
+    "gd_dir_ext_stats", "gd_route_ext", "gd_route_bucket_ext", "gd_route_ext_device", "gd_route_bucket_ext_device",
     "gd_comm_unique_id", "gd_comm_init", "gd_comm_destroy", "gd_route_multi_device", "gd_route_multi",
     "gd_multi_fetch",
 ]
@@ -102,6 +104,37 @@ class gd_multi_result(C.Structure):
 
 
 GD_COMM_ID_BYTES = 128
+GD_KEYEXT_NULL = -1
+GD_KEYEXT_HOST = -2
+
+
+class gd_key_ext(C.Structure):
+    _fields_ = [("bytes", C.c_void_p), ("offset", C.c_void_p), ("length", C.c_void_p), ("bytes_len", C.c_uint64)]
+
+
+class KeyExtBatch:
+    """A batch's KeyExt strings in the gd_key_ext layout.  Items: bytes (UTF-8), str (encoded
+    UTF-8), None (KeyExt null) or GD_KEYEXT_HOST (leave to the C# path).  Holds the arrays the
+    struct points at."""
+
+    def __init__(self, exts):
+        n = len(exts)
+        self.offset = np.zeros(n, np.uint64)
+        self.length = np.zeros(n, np.int32)
+        parts, pos = [], 0
+        for i, e in enumerate(exts):
+            if e is None:
+                self.length[i] = GD_KEYEXT_NULL
+            elif isinstance(e, (int, np.integer)):
+                self.length[i] = int(e)
+            else:
+                b = e.encode("utf-8") if isinstance(e, str) else bytes(e)
+                self.offset[i] = pos
+                self.length[i] = len(b)
+                parts.append(b)
+                pos += len(b)
+        self.blob = np.frombuffer(b"".join(parts) + b"\0", dtype=np.uint8).copy()
+        self.struct = gd_key_ext(self.blob.ctypes.data, self.offset.ctypes.data, self.length.ctypes.data, pos)
 GD_MULTI_RETURN_ROUTES = 1
 GD_MULTI_KEYS_READY = 2
 
@@ -187,6 +220,15 @@ def _load() -> C.CDLL:
         "gd_cache_clear": (C.c_int, [P]),
         "gd_cache_stats_get": (C.c_int, [P, C.POINTER(gd_cache_stats)]),
         "gd_cache_entries": (C.c_int, [P, P, P, P, P, U64, C.POINTER(U64)]),
+        "gd_dir_register_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), P, U32, P, P]),
+        "gd_dir_unregister_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), P, U32, P]),
+        "gd_dir_lookup_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, P, P]),
+        "gd_uniform_hashes_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, P]),
+        "gd_dir_ext_stats": (C.c_int, [P, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]),
+        "gd_route_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, P, P, P]),
+        "gd_route_bucket_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, U32, P, P, P, P, P]),
+        "gd_route_ext_device": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, P, P, P]),
+        "gd_route_bucket_ext_device": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, U32, P, P, P, P, P]),
         "gd_comm_unique_id": (C.c_int, [P]),
         "gd_comm_init": (C.c_int, [P, P, C.c_int, C.c_int]),
         "gd_comm_destroy": (C.c_int, [P]),
@@ -435,6 +477,86 @@ class GrainDispatch:
         off = np.zeros(n_act + 2, dtype=np.uint32)
         self._c(lib.gd_route_bucket(self.h, _ptr(k), n, n_act, _ptr(silo), _ptr(act), _ptr(st), _ptr(perm), _ptr(off)))
         return st, silo, act, perm, off
+
+    # -- KeyExt grains (string keys, compound keys, geo clients) ------------------------
+    @staticmethod
+    def _ext(exts, n: int) -> KeyExtBatch:
+        x = exts if isinstance(exts, KeyExtBatch) else KeyExtBatch(list(exts))
+        assert len(x.length) == n, "one KeyExt entry per key"
+        return x
+
+    def register_ext(self, keys, exts, acts, silos):
+        k = keys_array(keys)
+        n = len(k)
+        x = self._ext(exts, n)
+        vals = np.zeros((n, 2), dtype=np.uint32)
+        vals[:, 0] = acts
+        vals[:, 1] = silos
+        out = np.zeros((n, 2), dtype=np.uint32)
+        ins = np.zeros(n, dtype=np.uint8)
+        self._c(lib.gd_dir_register_ext(self.h, _ptr(k), C.byref(x.struct), _ptr(vals), n, _ptr(out), _ptr(ins)))
+        return out[:, 0].copy(), out[:, 1].copy(), ins
+
+    def unregister_ext(self, keys, exts, acts) -> np.ndarray:
+        k = keys_array(keys)
+        n = len(k)
+        x = self._ext(exts, n)
+        a = np.ascontiguousarray(acts, dtype=np.uint32)
+        out = np.zeros(n, dtype=np.uint8)
+        self._c(lib.gd_dir_unregister_ext(self.h, _ptr(k), C.byref(x.struct), _ptr(a), n, _ptr(out)))
+        return out
+
+    def lookup_ext(self, keys, exts):
+        k = keys_array(keys)
+        n = len(k)
+        x = self._ext(exts, n)
+        vals = np.zeros((n, 2), dtype=np.uint32)
+        found = np.zeros(n, dtype=np.uint8)
+        self._c(lib.gd_dir_lookup_ext(self.h, _ptr(k), C.byref(x.struct), n, _ptr(vals), _ptr(found)))
+        return found, vals[:, 0].copy(), vals[:, 1].copy()
+
+    def uniform_hashes_ext(self, keys, exts) -> np.ndarray:
+        k = keys_array(keys)
+        n = len(k)
+        x = self._ext(exts, n)
+        out = np.zeros(n, dtype=np.uint32)
+        self._c(lib.gd_uniform_hashes_ext(self.h, _ptr(k), C.byref(x.struct), n, _ptr(out)))
+        return out
+
+    def ext_stats(self) -> dict:
+        live, cap, heap = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._c(lib.gd_dir_ext_stats(self.h, C.byref(live), C.byref(cap), C.byref(heap)))
+        return {"live": live.value, "capacity": cap.value, "heap_bytes": heap.value}
+
+    def route_ext(self, keys, exts):
+        k = keys_array(keys)
+        n = len(k)
+        x = self._ext(exts, n)
+        silo = np.zeros(n, dtype=np.uint32)
+        act = np.zeros(n, dtype=np.uint32)
+        st = np.zeros(n, dtype=np.uint8)
+        self._c(lib.gd_route_ext(self.h, _ptr(k), C.byref(x.struct), n, _ptr(silo), _ptr(act), _ptr(st)))
+        return st, silo, act
+
+    def route_bucket_ext(self, keys, exts, n_act: int):
+        k = keys_array(keys)
+        n = len(k)
+        x = self._ext(exts, n)
+        silo = np.zeros(n, dtype=np.uint32)
+        act = np.zeros(n, dtype=np.uint32)
+        st = np.zeros(n, dtype=np.uint8)
+        perm = np.zeros(n, dtype=np.uint32)
+        off = np.zeros(n_act + 2, dtype=np.uint32)
+        self._c(lib.gd_route_bucket_ext(self.h, _ptr(k), C.byref(x.struct), n, n_act, _ptr(silo), _ptr(act), _ptr(st),
+                                        _ptr(perm), _ptr(off)))
+        return st, silo, act, perm, off
+
+    def route_bucket_ext_device(self, d_keys: int, d_bytes: int, d_offset: int, d_length: int, bytes_len: int, n: int,
+                                n_act: int, d_silo: int, d_act: int, d_status: int, d_perm: int, d_offsets: int):
+        dx = gd_key_ext(d_bytes, d_offset, d_length, bytes_len)
+        self._c(lib.gd_route_bucket_ext_device(self.h, C.c_void_p(d_keys), C.byref(dx), n, n_act, C.c_void_p(d_silo),
+                                               C.c_void_p(d_act), C.c_void_p(d_status), C.c_void_p(d_perm),
+                                               C.c_void_p(d_offsets)))
 
     # -- non-owner directory cache -------------------------------------
     @staticmethod
