@@ -60,19 +60,35 @@ struct alignas(32) Slot {
 };
 static_assert(sizeof(Slot) == 32, "slot must be 32 bytes");
 
-// KeyExt grain slot (gd_keyext.h): one 64-B DRAM atom -- the three words, the KeyExt string's
-// place in the KeyExt heap, its uniform hash (compared before the bytes) and the value.
+// KeyExt grain slot (gd_keyext.h): one 64-B DRAM atom -- the three words, the KeyExt string
+// (inline when it has at most KX_INLINE bytes: bytes 0..7 in `off`, 8..23 in `tail`; else its
+// place in the KeyExt heap), its uniform hash (compared before the bytes) and the value.
+constexpr int32_t KX_INLINE = 24;
 struct alignas(64) KxSlot {
     uint64_t n0;
     uint64_t n1;
     uint64_t tcd;
-    uint64_t off;       // heap offset of the UTF-8 KeyExt
+    uint64_t off;       // heap offset of the UTF-8 KeyExt, or its first 8 bytes (inline)
     int32_t len;        // UTF-8 length, GD_KEYEXT_NULL = null KeyExt
     uint32_t uhash;     // UniqueKey.GetUniformHashCode
     uint32_t act;
     uint32_t meta;      // (state << 16) | silo
-    uint64_t pad[2];
+    uint64_t tail[2];   // inline string bytes 8..23
 };
+inline void kx_inline_put(KxSlot& q, const uint8_t* s, int32_t len) {
+    uint8_t b[KX_INLINE] = {0};
+    for (int32_t i = 0; i < len; ++i) b[i] = s[i];
+    __builtin_memcpy(&q.off, b, 8);
+    __builtin_memcpy(q.tail, b + 8, 16);
+}
+inline bool kx_inline_eq(const KxSlot& q, const uint8_t* s, int32_t len) {
+    uint8_t b[KX_INLINE];
+    __builtin_memcpy(b, &q.off, 8);
+    __builtin_memcpy(b + 8, q.tail, 16);
+    for (int32_t i = 0; i < len; ++i)
+        if (b[i] != s[i]) return false;
+    return true;
+}
 static_assert(sizeof(KxSlot) == 64, "KeyExt slot must be 64 bytes");
 
 GD_HD uint32_t slot_state(uint32_t meta) { return meta >> 16; }

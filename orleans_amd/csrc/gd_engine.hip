@@ -2394,7 +2394,8 @@ bool kx_find_host(gd_handle* h, const gd_key& k, const uint8_t* s, int32_t len, 
             continue;
         }
         if (q.uhash == uh && q.len == len && q.n0 == k.n0 && q.n1 == k.n1 && q.tcd == k.type_code_data &&
-            (len <= 0 || std::memcmp(h->kx_hheap.data() + q.off, s, (size_t)len) == 0)) {
+            (len <= 0 || (len <= KX_INLINE ? kx_inline_eq(q, s, len)
+                                           : std::memcmp(h->kx_hheap.data() + q.off, s, (size_t)len) == 0))) {
             *at = i;
             return true;
         }
@@ -2436,7 +2437,8 @@ int kx_rehash(gd_handle* h, uint64_t cap) {
     for (const KxSlot& q : old) {
         if (slot_state(q.meta) != SLOT_LIVE) continue;
         KxSlot v = q;
-        if (q.len > 0) {
+        if (q.len > KX_INLINE) {
+            h->kx_hheap.resize((h->kx_hheap.size() + 15) & ~(size_t)15, 0);
             v.off = h->kx_hheap.size();
             h->kx_hheap.insert(h->kx_hheap.end(), old_heap.begin() + q.off, old_heap.begin() + q.off + q.len);
         }
@@ -2566,7 +2568,10 @@ int gd_dir_register_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext,
         q.uhash = uh[i];
         q.act = vals[i].act;
         q.meta = make_meta(SLOT_LIVE, vals[i].silo);
-        if (len > 0) {
+        if (len > 0 && len <= KX_INLINE) {
+            kx_inline_put(q, s, len);
+        } else if (len > 0) {          // 16-B aligned entries: the device compares them word by word
+            h->kx_hheap.resize((h->kx_hheap.size() + 15) & ~(size_t)15, 0);
             q.off = h->kx_hheap.size();
             h->kx_hheap.insert(h->kx_hheap.end(), s, s + len);
         }

@@ -89,24 +89,152 @@ __device__ __forceinline__ bool bytes_equal(const uint8_t* x, const uint8_t* y, 
     return true;
 }
 
+// ---- register fast path: KeyExt strings up to KX_FAST_BYTES ---------------------------------
+// The string is fetched as the aligned dwords covering it (clamped indices: every load is issued,
+// none past the string's last dword) and shifted into place with v_alignbyte; bytes past `len` are
+// zero.  The Jenkins blocks then run fully unrolled over registers (at most 92 stream bytes = 8
+// blocks incl. the tail), and the heap copy (16-B aligned by the host) is compared word by word.
+constexpr int KX_FAST_WORDS = 16;
+constexpr int KX_FAST_BYTES = 4 * KX_FAST_WORDS;
+
+__device__ __forceinline__ void load_str_fast(const uint8_t* s, int32_t len, uint32_t (&w)[KX_FAST_WORDS]) {
+    if (len <= 0) {                                      // nothing to read (s may be one past the end)
+#pragma unroll
+        for (int q = 0; q < KX_FAST_WORDS; ++q) w[q] = 0;
+        return;
+    }
+    const uintptr_t a = reinterpret_cast<uintptr_t>(s);
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const int32_t nd = (int32_t)((sh + (uint32_t)len + 3) >> 2);   // dwords holding the string
+    uint32_t d[KX_FAST_WORDS + 1];
+#pragma unroll
+    for (int j = 0; j <= KX_FAST_WORDS; ++j) d[j] = base[min(j, nd - 1)];
+#pragma unroll
+    for (int q = 0; q < KX_FAST_WORDS; ++q) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(d[q + 1], d[q], sh);
+        const int32_t left = len - 4 * q;                 // valid bytes in word q
+        w[q] = left >= 4 ? v : (left <= 0 ? 0u : (v & ((1u << (8 * left)) - 1u)));
+    }
+}
+
+__device__ __forceinline__ uint32_t jenkins_keyext_fast(uint64_t n0, uint64_t n1, uint64_t tcd, int32_t len,
+                                                        const uint32_t (&w)[KX_FAST_WORDS]) {
+    uint32_t W[24];
+    W[0] = (uint32_t)n0;
+    W[1] = (uint32_t)(n0 >> 32);
+    W[2] = (uint32_t)n1;
+    W[3] = (uint32_t)(n1 >> 32);
+    W[4] = (uint32_t)tcd;
+    W[5] = (uint32_t)(tcd >> 32);
+    W[6] = (uint32_t)len;
+#pragma unroll
+    for (int q = 0; q < KX_FAST_WORDS; ++q) W[7 + q] = w[q];
+    W[23] = 0;
+    const uint32_t L = 28u + (uint32_t)len;
+    const uint32_t nb = L / 12u;
+    uint32_t a = 0x9e3779b9u, b = a, c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        if (j < nb) {
+            a += W[3 * j];
+            b += W[3 * j + 1];
+            c += W[3 * j + 2];
+            jmix(a, b, c);
+        } else if (j == nb) {                               // the byte variant's tail (JenkinsHash.cs:51-73)
+            c += L;
+            a += W[3 * j];
+            b += W[3 * j + 1];
+            c += W[3 * j + 2] << 8;
+            jmix(a, b, c);
+        }
+    }
+    return c;
+}
+
+__device__ __forceinline__ bool heap_equal_fast(const uint8_t* heap, uint64_t off, int32_t len,
+                                                const uint32_t (&w)[KX_FAST_WORDS]) {
+    const uint32_t* hp = reinterpret_cast<const uint32_t*>(heap + off);   // 16-B aligned by the host
+    const int32_t nw = (len + 3) >> 2;
+    bool eq = true;
+#pragma unroll
+    for (int q = 0; q < KX_FAST_WORDS; ++q) {
+        if (q < nw) {
+            const int32_t left = len - 4 * q;
+            const uint32_t m = left >= 4 ? 0xFFFFFFFFu : ((1u << (8 * left)) - 1u);
+            eq = eq && ((hp[q] & m) == w[q]);
+        }
+    }
+    return eq;
+}
+
 // Live KeyExt entry equal to (n0, n1, tcd, s[0..len)) -- len = GD_KEYEXT_NULL for a null KeyExt.
+// FAST: the string is in w[] (len <= KX_FAST_BYTES).  The slot is read as four 16-B loads (one
+// 64-B atom); strings of at most KX_INLINE bytes are compared in the slot, longer ones in the heap.
+template <bool FAST>
 __device__ __forceinline__ bool kx_find(const KxArgs& t, uint64_t n0, uint64_t n1, uint64_t tcd, const uint8_t* s,
-                                        int32_t len, uint32_t uh, uint32_t& act, uint32_t& meta) {
+                                        int32_t len, uint32_t uh, const uint32_t (&w)[KX_FAST_WORDS], uint32_t& act,
+                                        uint32_t& meta) {
     unsigned long long i = fmix32(uh) & t.mask;
     for (uint32_t p = 0; p <= t.max_probe; ++p) {
-        const KxSlot& q = t.slots[i];
-        const uint32_t m = q.meta;
+        const uint4* qp = reinterpret_cast<const uint4*>(t.slots + i);
+        const uint4 q0 = qp[0], q1 = qp[1], q2 = qp[2], q3 = qp[3];
+        const uint32_t m = q2.w;
         const uint32_t st = slot_state(m);
         if (st == SLOT_EMPTY) return false;
-        if (st == SLOT_LIVE && q.uhash == uh && q.len == len && q.n0 == n0 && q.n1 == n1 && q.tcd == tcd &&
-            (len <= 0 || bytes_equal(t.heap + q.off, s, len))) {
-            act = q.act;
-            meta = m;
-            return true;
+        const uint64_t k0 = (uint64_t)q0.x | ((uint64_t)q0.y << 32);
+        const uint64_t k1 = (uint64_t)q0.z | ((uint64_t)q0.w << 32);
+        const uint64_t k2 = (uint64_t)q1.x | ((uint64_t)q1.y << 32);
+        const uint64_t off = (uint64_t)q1.z | ((uint64_t)q1.w << 32);
+        if (st == SLOT_LIVE && q2.y == uh && (int32_t)q2.x == len && k0 == n0 && k1 == n1 && k2 == tcd) {
+            bool eq = true;
+            if (len > 0 && len <= KX_INLINE) {              // inline: compare against the slot itself
+                if constexpr (FAST) {
+                    const uint32_t iw[6] = {q1.z, q1.w, q3.x, q3.y, q3.z, q3.w};
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) eq = eq && (iw[k] == w[k]);   // zero past len on both sides
+                } else {
+                    const uint32_t iw[6] = {q1.z, q1.w, q3.x, q3.y, q3.z, q3.w};
+                    for (int32_t k = 0; k < len; ++k)
+                        eq = eq && (((iw[k >> 2] >> (8 * (k & 3))) & 0xFFu) == s[k]);
+                }
+            } else if (len > 0) {
+                if constexpr (FAST) eq = heap_equal_fast(t.heap, off, len, w);
+                else eq = bytes_equal(t.heap + off, s, len);
+            }
+            if (eq) {
+                act = q2.z;
+                meta = m;
+                return true;
+            }
         }
         i = (i + 1) & t.mask;
     }
     return false;
+}
+
+// Uniform hash + lookup of one KeyExt message; FAST path for strings that fit the registers.
+__device__ __forceinline__ uint32_t kx_hash_and_find(const KxArgs& t, uint64_t n0, uint64_t n1, uint64_t tcd,
+                                                     const uint8_t* s, int32_t len, bool& found, uint32_t& act,
+                                                     uint32_t& meta) {
+    uint32_t w[KX_FAST_WORDS];
+    uint32_t uh;
+    found = false;
+    if (len <= KX_FAST_BYTES) {
+        if (len >= 0) {
+            load_str_fast(s, len, w);
+            uh = jenkins_keyext_fast(n0, n1, tcd, len, w);
+        } else {
+#pragma unroll
+            for (int q = 0; q < KX_FAST_WORDS; ++q) w[q] = 0;
+            uh = uniform_hash(n0, n1, tcd);
+        }
+        if (t.slots) found = kx_find<true>(t, n0, n1, tcd, s, len, uh, w, act, meta);
+    } else {
+        uh = jenkins_keyext(n0, n1, tcd, s, len);
+        if (t.slots) found = kx_find<false>(t, n0, n1, tcd, s, len, uh, w, act, meta);
+    }
+    return uh;
 }
 
 // Message i's KeyExt: false when the host keeps it (GD_KEYEXT_HOST, or a range outside bytes).
@@ -141,10 +269,11 @@ __global__ void __launch_bounds__(BLOCK) k_route_keyext(const gd_key* __restrict
     if (!ext_of(ext, i, s, len)) return;
     const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
     const uint64_t n0 = kp[0], n1 = kp[1], tcd = kp[2];
-    const uint32_t uh = len >= 0 ? jenkins_keyext(n0, n1, tcd, s, len) : uniform_hash(n0, n1, tcd);
-    const uint32_t owner = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uh)];
     uint32_t act = NONE32, meta = 0;
-    if (tab.slots && kx_find(tab, n0, n1, tcd, s, len, uh, act, meta)) {
+    bool found;
+    const uint32_t uh = kx_hash_and_find(tab, n0, n1, tcd, s, len, found, act, meta);
+    const uint32_t owner = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uh)];
+    if (found) {
         out_silo[i] = slot_silo(meta);                 // ActivationAddress.Silo (Message.cs:629-639)
         out_act[i] = act;
         out_status[i] = GD_ROUTE_OK;
@@ -169,10 +298,11 @@ __global__ void __launch_bounds__(BLOCK) k_kx_lookup(const gd_key* __restrict__ 
     if (ext_of(ext, i, s, len)) {
         const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
         const uint64_t n0 = kp[0], n1 = kp[1], tcd = kp[2];
-        const uint32_t uh = len >= 0 ? jenkins_keyext(n0, n1, tcd, s, len) : uniform_hash(n0, n1, tcd);
         uint32_t act = NONE32, meta = 0;
+        bool found;
+        (void)kx_hash_and_find(tab, n0, n1, tcd, s, len, found, act, meta);
         f = 0;
-        if (tab.slots && kx_find(tab, n0, n1, tcd, s, len, uh, act, meta)) {
+        if (found) {
             v.act = act;
             v.silo = slot_silo(meta);
             f = 1;
@@ -195,7 +325,15 @@ __global__ void __launch_bounds__(BLOCK) k_kx_hash(const gd_key* __restrict__ ke
         out[i] = 0;
         return;
     }
-    out[i] = len >= 0 ? jenkins_keyext(kp[0], kp[1], kp[2], s, len) : uniform_hash(kp[0], kp[1], kp[2]);
+    if (len < 0) {
+        out[i] = uniform_hash(kp[0], kp[1], kp[2]);
+    } else if (len <= KX_FAST_BYTES) {               // the path k_route_keyext takes
+        uint32_t w[KX_FAST_WORDS];
+        load_str_fast(s, len, w);
+        out[i] = jenkins_keyext_fast(kp[0], kp[1], kp[2], len, w);
+    } else {
+        out[i] = jenkins_keyext(kp[0], kp[1], kp[2], s, len);
+    }
 }
 
 // Apply host-index changes: slots[idx[j]] = val[j].
