@@ -401,6 +401,14 @@ int gd_route_frames_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len,
 int gd_route_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
                     uint32_t n_act, const gd_frame_fields* out, uint32_t* out_silo, uint32_t* out_act,
                     uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets);
+/* The same with KeyExt targets (string-keyed grains) routed on the GPU as gd_route_ext does:
+ * each TargetGrain's KeyExt string is read from the frame buffer where the decoder found it. */
+int gd_route_frames_ext_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
+                               uint32_t n, uint32_t n_act, const gd_frame_fields* d_out, uint32_t* d_silo,
+                               uint32_t* d_act, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets);
+int gd_route_frames_ext(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
+                        uint32_t n_act, const gd_frame_fields* out, uint32_t* out_silo, uint32_t* out_act,
+                        uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets);
 
 /* ---- membership change ------------------------------------------------
  * GrainDirectoryPartition.Split(predicate, modifyOrigin) (GrainDirectoryPartition.cs:532-570)

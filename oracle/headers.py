@@ -153,7 +153,8 @@ def encode_frame(h: Dict, body: bytes = b"") -> bytes:
 F_TARGET_KEYEXT = 16
 FIELDS_DEFAULT = {"target_grain": (0, 0, 0), "target_activation": (0, 0, 0), "sending_activation": (0, 0, 0),
                   "sending_grain": (0, 0, 0), "target_silo": b"\0" * 24, "sending_silo": b"\0" * 24,
-                  "correlation_id": 0, "category": 0, "direction": 0xFF, "mask": 0}
+                  "correlation_id": 0, "category": 0, "direction": 0xFF, "mask": 0,
+                  "target_ext": None}   # TargetGrain's KeyExt bytes (None: null or not decoded)
 
 
 def decode_frame(buf: bytes, off: int):
@@ -210,6 +211,14 @@ def decode_frame(buf: bytes, off: int):
         k = struct.unpack("<QQQ", take(24))
         return k, skip_string()
 
+    def key_with_ext():
+        """ReadUniqueKey keeping the KeyExt bytes (BinaryTokenStreamReader.cs:36-43)."""
+        k = struct.unpack("<QQQ", take(24))
+        ln = struct.unpack("<i", take(4))[0]
+        if ln < -1:
+            raise Bad()
+        return k, ln, (take(ln) if ln > 0 else (b"" if ln == 0 else None))
+
     try:
         if m & CATEGORY:
             out["category"] = take(1)[0]
@@ -246,8 +255,9 @@ def decode_frame(buf: bytes, off: int):
         if m & TARGET_ACTIVATION:
             out["target_activation"] = key()[0]
         if m & TARGET_GRAIN:
-            k, ext = key()
+            k, ext, ext_bytes = key_with_ext()
             out["target_grain"] = k
+            out["target_ext"] = ext_bytes
             flags |= F_HAS_TARGET | (F_TARGET_KEYEXT if ext >= 0 else 0)
         if m & TARGET_SILO:
             if m & TARGET_OBSERVER:
@@ -300,16 +310,36 @@ def route_frames_np(buf: bytes, offsets, spec, d):
     return f, st, silo, act
 
 
+def route_frames_ext_np(buf: bytes, offsets, spec, d, kxdir):
+    """route_frames_np with KeyExt targets routed too (gd_route_frames_ext): the TargetGrain's
+    KeyExt string comes from the frame itself (oracle/keyext.py route_batch_ext)."""
+    import keyext as kx
+    rows = [decode_frame(buf, int(o)) for o in offsets]
+    f = decode_frames(buf, offsets)
+    exts = [r.get("target_ext") for r in rows]
+    st, silo, act = kx.route_batch_ext(f["target_grain"], exts, spec, d, kxdir)[:3]
+    st, silo, act = st.copy(), silo.copy(), act.copy()
+    undecoded = ((f["flags"] & F_HAS_TARGET) == 0) | ((f["flags"] & (F_FALLBACK | F_MALFORMED)) != 0)
+    addressed = ~undecoded & ((f["flags"] & F_COMPLETE) != 0)
+    st[addressed] = ROUTE_ADDRESSED
+    st[undecoded] = ROUTE_UNDECODED
+    silo[addressed | undecoded] = 0xFFFFFFFF
+    act[addressed | undecoded] = 0xFFFFFFFF
+    return f, st, silo, act
+
+
 def random_frames(n: int, target_keys: np.ndarray, rng: np.random.Generator, p_fallback=0.03,
-                  p_complete=0.05, p_malformed=0.01):
+                  p_complete=0.05, p_malformed=0.01, target_exts=None):
     """Synthetic request frames around the given target GrainIds, with every optional
-    field drawn at random.  Returns (buffer bytes, frame offsets u64)."""
+    field drawn at random.  target_exts[i] (str or None), when given, is frame i's TargetGrain
+    KeyExt.  Returns (buffer bytes, frame offsets u64)."""
     parts, offs, pos = [], [], 0
     silo = (b"\x00" * 12 + bytes([10, 0, 0, 1]), 11111, 7)
     for i in range(n):
         h = {"category": 2, "direction": int(rng.integers(0, 3)), "correlation_id": int(rng.integers(1, 1 << 62))}
         k = tuple(int(x) for x in target_keys[i])
-        h["target_grain"] = (k, "ext" if rng.random() < 0.02 else None)
+        ext_draw = "ext" if rng.random() < 0.02 else None
+        h["target_grain"] = (k, target_exts[i] if target_exts is not None else ext_draw)
         if rng.random() < 0.5:
             h["sending_grain"] = ((0, int(rng.integers(0, 1 << 40)), int(target_keys[i][2])), None)
             h["sending_activation"] = ((int(rng.integers(1, 1 << 60)), int(rng.integers(0, 1 << 60)), 0), None)

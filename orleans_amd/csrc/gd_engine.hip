@@ -64,6 +64,7 @@ struct gd_handle {
     // scratch
     DevBuf keys_in, u32_a, u32_b, u32_c, u32_d, u8_a, out_a, out_b, out_c, hist, partials, partials2, offs;
     DevBuf fr[16];                    // header-decode scratch (host-pointer entry points)
+    DevBuf fr_ext[2];                 // TargetGrain KeyExt offsets / lengths (gd_route_frames_ext*)
     DevBuf churn[5];                  // split scratch: keep mask, flags, positions, out keys/vals
     DevBuf fan[8];                    // fan-out scratch: ends, total, flags, positions, host-form buffers
 
@@ -297,6 +298,29 @@ int route_device(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, u
         case GD_RING_DIRECTORY: return route_mode<GD_RING_DIRECTORY>(h, keys, n, silo, act, status);
         case GD_RING_CONSISTENT: return route_mode<GD_RING_CONSISTENT>(h, keys, n, silo, act, status);
         default: return route_mode<GD_RING_VIRTUAL_BUCKETS>(h, keys, n, silo, act, status);
+    }
+}
+
+KxArgs kx_args(gd_handle* h) {
+    return KxArgs{h->kx_slots, h->kx_cap ? h->kx_cap - 1 : 0ull, h->kx_maxp, (const uint8_t*)h->kx_heap.p};
+}
+
+template <int MODE>
+int route_keyext_t(gd_handle* h, const gd_key* keys, const ExtArgs& x, uint32_t n, uint32_t* silo, uint32_t* act,
+                   uint8_t* st) {
+    return launch(h, "k_route_keyext", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), ring_lds(h), k_route_keyext<MODE>,
+                  keys, n, x, ring_args(h), kx_args(h), silo, act, st);
+}
+
+// The KeyExt pass (gd_keyext.h) over the messages route_device left at GD_ROUTE_KEYEXT.  Not in
+// LocalLookup (cache) mode: there KeyExt grains stay with the C# path.
+int keyext_pass(gd_handle* h, const gd_key* keys, const ExtArgs& x, uint32_t n, uint32_t* silo, uint32_t* act,
+                uint8_t* st) {
+    if (n == 0 || h->cache_max) return GD_OK;
+    switch (h->ring_mode) {
+        case GD_RING_DIRECTORY: return route_keyext_t<GD_RING_DIRECTORY>(h, keys, x, n, silo, act, st);
+        case GD_RING_CONSISTENT: return route_keyext_t<GD_RING_CONSISTENT>(h, keys, x, n, silo, act, st);
+        default: return route_keyext_t<GD_RING_VIRTUAL_BUCKETS>(h, keys, x, n, silo, act, st);
     }
 }
 
@@ -606,6 +630,7 @@ void gd_destroy(gd_handle* h) {
                       &h->out_a, &h->out_b, &h->out_c, &h->hist, &h->partials, &h->partials2, &h->offs})
         free_buf(*b);
     for (DevBuf& b : h->fr) free_buf(b);
+    for (DevBuf& b : h->fr_ext) free_buf(b);
     for (DevBuf& b : h->churn) free_buf(b);
     for (DevBuf& b : h->fan) free_buf(b);
     for (DevBuf& b : h->cbuf) free_buf(b);
@@ -1117,7 +1142,9 @@ FrameFields frame_fields(const gd_frame_fields* f) {
                        (uint32_t*)f->sending_silo,
                        f->correlation_id,
                        f->category,
-                       f->direction};
+                       f->direction,
+                       nullptr,
+                       nullptr};
 }
 
 int check_frames_args(gd_handle* h, const void* buf, const void* off, uint32_t n, const gd_frame_fields* out) {
@@ -1130,18 +1157,30 @@ int check_frames_args(gd_handle* h, const void* buf, const void* off, uint32_t n
 }
 
 int decode_frames_device(gd_handle* h, const uint8_t* buf, uint64_t len, const uint64_t* off, uint32_t n,
-                         const gd_frame_fields* out) {
+                         const gd_frame_fields* out, bool ext = false) {
+    FrameFields ff = frame_fields(out);
+    if (ext) {                          // where each TargetGrain's KeyExt string lies in buf
+        GD_TRY(ensure(h, h->fr_ext[0], (size_t)n * 8 + 8));
+        GD_TRY(ensure(h, h->fr_ext[1], (size_t)n * 4 + 4));
+        ff.tg_ext_off = (uint64_t*)h->fr_ext[0].p;
+        ff.tg_ext_len = (int32_t*)h->fr_ext[1].p;
+    }
     return launch(h, "k_decode_frames", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_decode_frames, buf, len, off, n,
-                  frame_fields(out));
+                  ff);
 }
 
+// ext: KeyExt targets (string-keyed grains) are routed too, their strings read from buf itself.
 int route_frames_device(gd_handle* h, const uint8_t* buf, uint64_t len, const uint64_t* off, uint32_t n,
                         uint32_t n_act, const gd_frame_fields* out, uint32_t* silo, uint32_t* act, uint8_t* status,
-                        uint32_t* perm, uint32_t* offsets) {
+                        uint32_t* perm, uint32_t* offsets, bool ext = false) {
     if (n) {
         GD_TRY(check_ring(h));
-        GD_TRY(decode_frames_device(h, buf, len, off, n, out));
+        GD_TRY(decode_frames_device(h, buf, len, off, n, out, ext));
         GD_TRY(route_device(h, out->target_grain, n, silo, act, status));
+        if (ext)
+            GD_TRY(keyext_pass(h, out->target_grain,
+                               ExtArgs{buf, (const uint64_t*)h->fr_ext[0].p, (const int32_t*)h->fr_ext[1].p, len}, n,
+                               silo, act, status));
         GD_TRY(launch(h, "k_frame_status", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_frame_status,
                       (const uint32_t*)out->flags, n, silo, act, status));
     }
@@ -1198,20 +1237,35 @@ int gd_decode_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const u
     return sync(h);
 }
 
-int gd_route_frames_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
-                           uint32_t n, uint32_t n_act, const gd_frame_fields* d_out, uint32_t* d_silo,
-                           uint32_t* d_act, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets) {
+static int route_frames_device_abi(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
+                                   uint32_t n, uint32_t n_act, const gd_frame_fields* d_out, uint32_t* d_silo,
+                                   uint32_t* d_act, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets,
+                                   bool ext) {
     GD_TRY(check_frames_args(h, d_buf, d_frame_off, n, d_out));
     if (n && (!d_silo || !d_act || !d_status)) return set_err(h, GD_EINVAL, "null argument");
     if ((d_perm != nullptr) != (d_offsets != nullptr)) return set_err(h, GD_EINVAL, "perm and offsets go together");
     if (d_perm && n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
     return route_frames_device(h, d_buf, buf_len, d_frame_off, n, n_act, d_out, d_silo, d_act, d_status, d_perm,
-                               d_offsets);
+                               d_offsets, ext);
 }
 
-int gd_route_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
-                    uint32_t n_act, const gd_frame_fields* out, uint32_t* out_silo, uint32_t* out_act,
-                    uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets) {
+int gd_route_frames_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
+                           uint32_t n, uint32_t n_act, const gd_frame_fields* d_out, uint32_t* d_silo,
+                           uint32_t* d_act, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets) {
+    return route_frames_device_abi(h, d_buf, buf_len, d_frame_off, n, n_act, d_out, d_silo, d_act, d_status, d_perm,
+                                   d_offsets, false);
+}
+
+int gd_route_frames_ext_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
+                               uint32_t n, uint32_t n_act, const gd_frame_fields* d_out, uint32_t* d_silo,
+                               uint32_t* d_act, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets) {
+    return route_frames_device_abi(h, d_buf, buf_len, d_frame_off, n, n_act, d_out, d_silo, d_act, d_status, d_perm,
+                                   d_offsets, true);
+}
+
+static int route_frames_host(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
+                             uint32_t n_act, const gd_frame_fields* out, uint32_t* out_silo, uint32_t* out_act,
+                             uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets, bool ext) {
     if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
     if (n && (!buf || !frame_off || !out_silo || !out_act || !out_status)) return set_err(h, GD_EINVAL, "null argument");
     if ((out_perm != nullptr) != (out_offsets != nullptr)) return set_err(h, GD_EINVAL, "perm and offsets go together");
@@ -1237,7 +1291,8 @@ int gd_route_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const ui
         offs = (uint32_t*)h->offs.p;
     }
     GD_TRY(route_frames_device(h, (const uint8_t*)h->fr[0].p, buf_len, (const uint64_t*)h->fr[1].p, n, n_act, &dev,
-                               (uint32_t*)h->fr[13].p, (uint32_t*)h->fr[14].p, (uint8_t*)h->fr[15].p, perm, offs));
+                               (uint32_t*)h->fr[13].p, (uint32_t*)h->fr[14].p, (uint8_t*)h->fr[15].p, perm, offs,
+                               ext));
     GD_TRY(frame_results(h, n, out, &dev));
     if (n) {
         HIP_TRY(h, hipMemcpyAsync(out_silo, h->fr[13].p, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
@@ -1249,6 +1304,20 @@ int gd_route_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const ui
         HIP_TRY(h, hipMemcpyAsync(out_offsets, offs, ((size_t)n_act + 2) * 4, hipMemcpyDeviceToHost, h->stream));
     }
     return sync_checked(h);
+}
+
+int gd_route_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
+                    uint32_t n_act, const gd_frame_fields* out, uint32_t* out_silo, uint32_t* out_act,
+                    uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets) {
+    return route_frames_host(h, buf, buf_len, frame_off, n, n_act, out, out_silo, out_act, out_status, out_perm,
+                             out_offsets, false);
+}
+
+int gd_route_frames_ext(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
+                        uint32_t n_act, const gd_frame_fields* out, uint32_t* out_silo, uint32_t* out_act,
+                        uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets) {
+    return route_frames_host(h, buf, buf_len, frame_off, n, n_act, out, out_silo, out_act, out_status, out_perm,
+                             out_offsets, true);
 }
 
 }  // extern "C"
@@ -2484,30 +2553,12 @@ int kx_commit(gd_handle* h, std::vector<uint64_t>& dirty) {
     return sync(h);
 }
 
-KxArgs kx_args(gd_handle* h) {
-    return KxArgs{h->kx_slots, h->kx_cap ? h->kx_cap - 1 : 0ull, h->kx_maxp, (const uint8_t*)h->kx_heap.p};
-}
-
-extern "C++" {
-template <int MODE>
-int route_keyext_t(gd_handle* h, const gd_key* keys, const ExtArgs& x, uint32_t n, uint32_t* silo, uint32_t* act,
-                   uint8_t* st) {
-    return launch(h, "k_route_keyext", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), ring_lds(h), k_route_keyext<MODE>,
-                  keys, n, x, ring_args(h), kx_args(h), silo, act, st);
-}
-}
-
 // Route (24-B keys) then the KeyExt pass over what it left at GD_ROUTE_KEYEXT.
 int route_ext_device(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t* silo,
                      uint32_t* act, uint8_t* st) {
     GD_TRY(route_device(h, keys, n, silo, act, st));
-    if (!ext || n == 0 || h->cache_max) return GD_OK;   // LocalLookup mode: KeyExt grains stay in C#
-    const ExtArgs x{ext->bytes, ext->offset, ext->length, ext->bytes_len};
-    switch (h->ring_mode) {
-        case GD_RING_DIRECTORY: return route_keyext_t<GD_RING_DIRECTORY>(h, keys, x, n, silo, act, st);
-        case GD_RING_CONSISTENT: return route_keyext_t<GD_RING_CONSISTENT>(h, keys, x, n, silo, act, st);
-        default: return route_keyext_t<GD_RING_VIRTUAL_BUCKETS>(h, keys, x, n, silo, act, st);
-    }
+    if (!ext || n == 0) return GD_OK;
+    return keyext_pass(h, keys, ExtArgs{ext->bytes, ext->offset, ext->length, ext->bytes_len}, n, silo, act, st);
 }
 
 // Host ext -> device copies in kx_buf[2..4]; *dx gets the device form.

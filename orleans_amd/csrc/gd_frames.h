@@ -55,6 +55,8 @@ struct FrameFields {   // device pointers; nullptr = field not wanted (flags and
     int64_t* correlation_id;
     uint8_t* category;
     uint8_t* direction;
+    uint64_t* tg_ext_off;          // TargetGrain's KeyExt: absolute offset in buf (KeyExt routing)
+    int32_t* tg_ext_len;           //   and UTF-8 length (-1 null, GD_KEYEXT_HOST: no target decoded)
 };
 
 // Byte cursor over one frame: LDS window first, global memory past it.
@@ -185,6 +187,8 @@ __global__ __launch_bounds__(BLOCK) void k_decode_frames(const uint8_t* __restri
     uint32_t flags = 0, mask = 0, cat = 0, dir = 0xFFu;
     int64_t corr = 0;
     Key3 tg{0, 0, 0}, ta{0, 0, 0}, sa{0, 0, 0}, sg{0, 0, 0};
+    int32_t tg_ext = GD_KEYEXT_HOST;
+    uint64_t tg_ext_off = 0;
     uint32_t ts[6] = {0, 0, 0, 0, 0, 0}, ss[6] = {0, 0, 0, 0, 0, 0};
 
     const uint64_t a0 = start & ~3ull;
@@ -244,6 +248,8 @@ __global__ __launch_bounds__(BLOCK) void k_decode_frames(const uint8_t* __restri
                 int32_t ext = -1;
                 tg = hw.key(&ext);
                 flags |= FR_HAS_TARGET | (ext >= 0 ? FR_TARGET_KEYEXT : 0u);
+                tg_ext = ext;                              // the string is the last ext bytes read
+                tg_ext_off = start + hw.p - (uint32_t)(ext > 0 ? ext : 0);
             }
             if (m & H_TARGET_SILO) {
                 if (m & H_TARGET_OBSERVER) {
@@ -263,6 +269,7 @@ __global__ __launch_bounds__(BLOCK) void k_decode_frames(const uint8_t* __restri
         dir = 0xFFu;
         corr = 0;
         tg = ta = sa = sg = Key3{0, 0, 0};
+        tg_ext = GD_KEYEXT_HOST;
 #pragma unroll
         for (int j = 0; j < 6; ++j) ts[j] = ss[j] = 0;
     }
@@ -277,6 +284,10 @@ __global__ __launch_bounds__(BLOCK) void k_decode_frames(const uint8_t* __restri
     if (o.correlation_id) o.correlation_id[i] = corr;
     if (o.category) o.category[i] = (uint8_t)cat;
     if (o.direction) o.direction[i] = (uint8_t)dir;
+    if (o.tg_ext_len) {
+        o.tg_ext_len[i] = (flags & FR_FALLBACK) ? GD_KEYEXT_HOST : tg_ext;
+        o.tg_ext_off[i] = tg_ext_off;
+    }
 }
 
 // Dispatcher.AddressMessage skips complete addresses (Dispatcher.cs:718); frames without a decoded

@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = [
     "gd_pack_nodes_by_shard_device", "gd_frontier_next_device",
     "gd_cache_configure", "gd_cache_set_silos", "gd_cache_add", "gd_cache_remove", "gd_cache_lookup",
     "gd_cache_clear", "gd_cache_stats_get", "gd_cache_entries",
+    "gd_route_frames_ext_device", "gd_route_frames_ext",
     "gd_dir_register_ext", "gd_dir_unregister_ext", "gd_dir_lookup_ext", "gd_uniform_hashes_ext",
     "gd_dir_ext_stats", "gd_route_ext", "gd_route_bucket_ext", "gd_route_ext_device", "gd_route_bucket_ext_device",
     "gd_comm_unique_id", "gd_comm_init", "gd_comm_destroy", "gd_route_multi_device", "gd_route_multi",
@@ -204,6 +205,8 @@ def _load() -> C.CDLL:
         "gd_decode_frames": (C.c_int, [P, P, U64, P, U32, C.POINTER(gd_frame_fields)]),
         "gd_route_frames_device": (C.c_int, [P, P, U64, P, U32, U32, C.POINTER(gd_frame_fields), P, P, P, P, P]),
         "gd_route_frames": (C.c_int, [P, P, U64, P, U32, U32, C.POINTER(gd_frame_fields), P, P, P, P, P]),
+        "gd_route_frames_ext_device": (C.c_int, [P, P, U64, P, U32, U32, C.POINTER(gd_frame_fields), P, P, P, P, P]),
+        "gd_route_frames_ext": (C.c_int, [P, P, U64, P, U32, U32, C.POINTER(gd_frame_fields), P, P, P, P, P]),
         "gd_dir_split": (C.c_int, [P, P, U32, C.c_int, P, P, U64, C.POINTER(U64)]),
         "gd_dir_split_device": (C.c_int, [P, P, U32, C.c_int, P, P, U64, C.POINTER(U64)]),
         "gd_fanout_expand_device": (C.c_int, [P, P, P, U32, P, U32, P, P, U64, C.POINTER(U64)]),
@@ -773,9 +776,10 @@ class GrainDispatch:
         self._c(lib.gd_decode_frames(self.h, _ptr(b), len(buf), _ptr(off), n, C.byref(ff)))
         return arrs
 
-    def route_frames(self, buf: bytes, offsets, n_act: Optional[int] = None, fields: Optional[Iterable[str]] = ()):
+    def route_frames(self, buf: bytes, offsets, n_act: Optional[int] = None, fields: Optional[Iterable[str]] = (),
+                     keyext: bool = False):
         """Decode -> route (-> bucket when n_act is given).  Returns (decoded fields, status,
-        silo, act[, perm, offsets])."""
+        silo, act[, perm, offsets]).  keyext: gd_route_frames_ext (KeyExt targets routed too)."""
         b = np.frombuffer(buf, dtype=np.uint8) if len(buf) else np.zeros(1, dtype=np.uint8)
         off = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
         n = len(off)
@@ -785,9 +789,9 @@ class GrainDispatch:
         st = np.zeros(n, dtype=np.uint8)
         perm = np.zeros(n, dtype=np.uint32) if n_act is not None else None
         offs = np.zeros(n_act + 2, dtype=np.uint32) if n_act is not None else None
-        self._c(lib.gd_route_frames(self.h, _ptr(b), len(buf), _ptr(off), n, n_act or 0, C.byref(ff), _ptr(silo),
-                                    _ptr(act), _ptr(st), None if perm is None else _ptr(perm),
-                                    None if offs is None else _ptr(offs)))
+        fn = lib.gd_route_frames_ext if keyext else lib.gd_route_frames
+        self._c(fn(self.h, _ptr(b), len(buf), _ptr(off), n, n_act or 0, C.byref(ff), _ptr(silo),
+                   _ptr(act), _ptr(st), None if perm is None else _ptr(perm), None if offs is None else _ptr(offs)))
         return (arrs, st, silo, act) if n_act is None else (arrs, st, silo, act, perm, offs)
 
     def decode_frames_device(self, d_buf: int, buf_len: int, d_offsets: int, n: int, d_fields: dict):

@@ -261,3 +261,45 @@ def test_device_entry_point(gd):
     np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), wp)
     np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), wo)
     e.close()
+
+
+@pytest.mark.parametrize("mode", ["D", "V"])
+def test_route_frames_ext(gd, mode):
+    """gd_route_frames_ext: frames whose TargetGrain is a string-keyed grain are routed with the
+    KeyExt string read from the frame buffer (oracle/headers.py route_frames_ext_np), next to
+    ordinary, complete, fallback and malformed frames; bucketing over the result."""
+    import headers as H
+    e, spec = _engine(gd, mode, cap=1 << 13)
+    rng = np.random.default_rng(23)
+    G = 1000
+    reg = o.grain_keys(TC, np.arange(G))
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    e.register(reg, np.arange(G), own)
+    d = kx.KeyExtDirectory()
+    names = [f"device/{i}" + ("ü" * (i % 3)) + "q" * (i % 41) for i in range(600)]    # inline and heap strings
+    tcd = o.type_code_data(o.CAT_KEYEXT_GRAIN, STC)
+    e.register_ext(np.tile(np.array([[0, 0, tcd]], np.uint64), (300, 1)), names[:300], np.arange(300) + G,
+                   np.arange(300) % 8)
+    for i in range(300):
+        d.add_single_activation((0, 0, tcd), names[i].encode(), G + i, i % 8)
+    n = 5000
+    keys = o.grain_keys(TC, rng.integers(0, G + 50, size=n))
+    exts = [None] * n
+    for i in np.nonzero(rng.random(n) < 0.5)[0]:
+        keys[i] = (0, 0, tcd)
+        exts[i] = names[int(rng.integers(0, 600))]
+    buf, offs = H.random_frames(n, keys, rng, p_fallback=0.05, p_complete=0.05, p_malformed=0.03, target_exts=exts)
+    f, wst, wsilo, wact = H.route_frames_ext_np(buf, offs, spec, o.DirectoryArrays(reg, np.arange(G), own), d)
+    n_act = G + 300
+    _, st, silo, act, perm, off = e.route_frames(buf, offs, n_act, keyext=True)
+    np.testing.assert_array_equal(st, wst)
+    np.testing.assert_array_equal(silo, wsilo)
+    np.testing.assert_array_equal(act, wact)
+    wp, wo = o.bucket_stable(wact, n_act)
+    np.testing.assert_array_equal(perm, wp)
+    np.testing.assert_array_equal(off, wo)
+    assert ((wst == o.ST_OK) & (keys[:, 2] == np.uint64(tcd))).sum() > 500
+    _, st0, _, _ = e.route_frames(buf, offs)           # gd_route_frames: KeyExt targets stay KEYEXT
+    assert ((st0 == o.ST_KEYEXT) == ((wst != H.ROUTE_ADDRESSED) & (wst != H.ROUTE_UNDECODED) &
+                                    (f["target_grain"][:, 2] == np.uint64(tcd)))).all()
+    e.close()
