@@ -255,6 +255,15 @@ def main():
                     "frac": d["frac_hbm"], "traffic": traffic,
                     "alg_bytes_per_launch": kernel_bytes(dom, m_recv, n_act, passes, world) / launches,
                     "avg_launch_ms": round(d["ms_per_step"] / launches, 5)}
+        if dom == "k_route" and args.workload == "cfg2":
+            # k_route is one random 32-B slot read per message beside the 24-B key stream: its
+            # real ceiling is the random-probe rate, measured on MI355X by tools/ubench_random.hip
+            # for this shape (16M probes, 64-MiB table, key stream on): 0.3453 ms per launch
+            # (profiles/r01_ubench_random_ceiling.txt).
+            ceil_ms = 0.3453 * (m_recv / (1 << 24))
+            roofline["random_probe_ceiling"] = {
+                "ms_per_launch": round(ceil_ms, 4), "source": "profiles/r01_ubench_random_ceiling.txt",
+                "frac_of_ceiling": round(ceil_ms / (d["ms_per_step"] / launches), 3)}
 
     # ---- CPU baseline: the C restatement (oracle/cpu_ref.c), bounded sample ---------
     cpu = None
