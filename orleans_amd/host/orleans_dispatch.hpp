@@ -70,14 +70,13 @@ struct UniqueKey {
 
     // UniqueKey.ToByteArray (UniqueKey.cs:295-336)
     std::vector<uint8_t> ToByteArray() const {
-        std::vector<uint8_t> b(24);
+        const int32_t len = KeyExt ? static_cast<int32_t>(KeyExt->size()) : -1;
+        std::vector<uint8_t> b(28 + (KeyExt ? KeyExt->size() : 0));
         std::memcpy(b.data(), &N0, 8);
         std::memcpy(b.data() + 8, &N1, 8);
         std::memcpy(b.data() + 16, &TypeCodeData, 8);
-        const int32_t len = KeyExt ? static_cast<int32_t>(KeyExt->size()) : -1;
-        const uint8_t* lp = reinterpret_cast<const uint8_t*>(&len);
-        b.insert(b.end(), lp, lp + 4);
-        if (KeyExt) b.insert(b.end(), KeyExt->begin(), KeyExt->end());
+        std::memcpy(b.data() + 24, &len, 4);
+        if (KeyExt && !KeyExt->empty()) std::memcpy(b.data() + 28, KeyExt->data(), KeyExt->size());
         return b;
     }
 
@@ -105,9 +104,21 @@ struct UniqueKey {
 
 struct GrainId {
     UniqueKey Key;
-    // GrainId.GetGrainId(long typeCode, long primaryKey) (GrainId.cs:72-77)
-    static GrainId GetGrainId(int64_t typeCode, int64_t primaryKey) {
-        return GrainId{UniqueKey::NewKey(primaryKey, UniqueKey::Category::Grain, typeCode)};
+    // GrainId.GetGrainId(long typeCode, long primaryKey, string keyExt = null) (GrainId.cs:72-77):
+    // a key extension makes it a KeyExtGrain (compound key).
+    static GrainId GetGrainId(int64_t typeCode, int64_t primaryKey,
+                              const std::optional<std::string>& keyExt = std::nullopt) {
+        GrainId g{UniqueKey::NewKey(primaryKey, keyExt ? UniqueKey::Category::KeyExtGrain : UniqueKey::Category::Grain,
+                                    typeCode)};
+        g.Key.KeyExt = keyExt;
+        return g;
+    }
+    // GrainId.GetGrainId(long typeCode, string primaryKey) (GrainId.cs:86-91): string-keyed grains
+    // (IGrainWithStringKey), N0 = N1 = 0, the string is the KeyExt (UTF-8 here).
+    static GrainId GetGrainId(int64_t typeCode, const std::string& primaryKey) {
+        GrainId g{UniqueKey::NewKey(0, UniqueKey::Category::KeyExtGrain, typeCode)};
+        g.Key.KeyExt = primaryKey;
+        return g;
     }
     bool IsSystemTarget() const { return Key.IdCategory() == UniqueKey::Category::SystemTarget; }
     uint32_t GetUniformHashCode() const { return Key.GetUniformHashCode(); }
@@ -163,6 +174,38 @@ struct ActivationAddress {   // ActivationAddress.cs:6-34
 
 struct AddressAndTag { std::optional<ActivationAddress> Address; int VersionTag = 0; };
 struct AddressesAndTag { std::optional<std::vector<ActivationAddress>> Addresses; int VersionTag = 0; };
+
+// The KeyExt strings of a batch of keys in the gd_key_ext layout (one UTF-8 blob, offset + length
+// per key; GD_KEYEXT_NULL for a null KeyExt or a category without one).
+class KeyExtBatch {
+public:
+    explicit KeyExtBatch(const std::vector<const UniqueKey*>& keys) {
+        off_.resize(keys.size());
+        len_.resize(keys.size());
+        for (size_t i = 0; i < keys.size(); ++i) {
+            const UniqueKey& k = *keys[i];
+            if (k.HasKeyExt() && k.KeyExt) {
+                off_[i] = bytes_.size();
+                len_[i] = (int32_t)k.KeyExt->size();
+                bytes_.insert(bytes_.end(), k.KeyExt->begin(), k.KeyExt->end());
+            } else {
+                off_[i] = 0;
+                len_[i] = GD_KEYEXT_NULL;
+            }
+        }
+        bytes_.push_back(0);   // a valid pointer even when empty
+    }
+    const gd_key_ext* get() {
+        ext_ = gd_key_ext{bytes_.data(), off_.data(), len_.data(), (uint64_t)(bytes_.size() - 1)};
+        return &ext_;
+    }
+
+private:
+    std::vector<uint8_t> bytes_;
+    std::vector<uint64_t> off_;
+    std::vector<int32_t> len_;
+    gd_key_ext ext_{};
+};
 
 // ------------------------------------------------------------------ native handle
 class DispatchHandle {
@@ -331,14 +374,32 @@ public:
                                                     const std::vector<ActivationId>& acts,
                                                     const std::vector<SiloAddress>& silos) {
         const size_t n = grains.size();
-        std::vector<gd_key> keys(n);
-        std::vector<gd_val> vals(n), out(n);
-        std::vector<uint8_t> ins(n);
-        for (size_t i = 0; i < n; ++i) {
-            keys[i] = grains[i].Key.ToNative();
-            vals[i] = gd_val{ActIndex(acts[i]), silos_.IndexOf(silos[i])};
+        std::vector<gd_val> out(n);
+        // KeyExt grains (string / compound keys) go to the KeyExt table, the rest to the main one;
+        // each keeps its batch order (first registration wins within each).
+        for (int ext = 0; ext < 2; ++ext) {
+            std::vector<size_t> idx;
+            for (size_t i = 0; i < n; ++i)
+                if (grains[i].Key.HasKeyExt() == (ext == 1)) idx.push_back(i);
+            if (idx.empty()) continue;
+            std::vector<gd_key> keys;
+            std::vector<gd_val> vals, o(idx.size());
+            std::vector<const UniqueKey*> uk;
+            std::vector<uint8_t> ins(idx.size());
+            for (size_t i : idx) {
+                keys.push_back(grains[i].Key.ToNative());
+                vals.push_back(gd_val{ActIndex(acts[i]), silos_.IndexOf(silos[i])});
+                uk.push_back(&grains[i].Key);
+            }
+            if (ext) {
+                KeyExtBatch kx(uk);
+                Check(h_, gd_dir_register_ext(h_, keys.data(), kx.get(), vals.data(), (uint32_t)idx.size(), o.data(),
+                                              ins.data()));
+            } else {
+                Check(h_, gd_dir_register(h_, keys.data(), vals.data(), (uint32_t)idx.size(), o.data(), ins.data()));
+            }
+            for (size_t j = 0; j < idx.size(); ++j) out[idx[j]] = o[j];
         }
-        if (n) Check(h_, gd_dir_register(h_, keys.data(), vals.data(), (uint32_t)n, out.data(), ins.data()));
         std::vector<AddressAndTag> r(n);
         for (size_t i = 0; i < n; ++i)
             r[i].Address = ActivationAddress{silos_.At(out[i].silo), grains[i], acts_.at(out[i].act)};
@@ -352,7 +413,12 @@ public:
         const gd_key k = grain.Key.ToNative();
         const uint32_t a = it->second;
         uint8_t removed = 0;
-        Check(h_, gd_dir_unregister(h_, &k, &a, 1, &removed));
+        if (grain.Key.HasKeyExt()) {
+            KeyExtBatch kx({&grain.Key});
+            Check(h_, gd_dir_unregister_ext(h_, &k, kx.get(), &a, 1, &removed));
+        } else {
+            Check(h_, gd_dir_unregister(h_, &k, &a, 1, &removed));
+        }
         return removed != 0;
     }
 
@@ -361,13 +427,24 @@ public:
         const gd_key k = grain.Key.ToNative();
         gd_val v{};
         uint8_t found = 0;
-        Check(h_, gd_dir_lookup(h_, &k, 1, &v, &found));
+        if (grain.Key.HasKeyExt()) {
+            KeyExtBatch kx({&grain.Key});
+            Check(h_, gd_dir_lookup_ext(h_, &k, kx.get(), 1, &v, &found));
+        } else {
+            Check(h_, gd_dir_lookup(h_, &k, 1, &v, &found));
+        }
         AddressesAndTag r;
         if (found) r.Addresses = std::vector<ActivationAddress>{{silos_.At(v.silo), grain, acts_.at(v.act)}};
         return r;
     }
 
-    int Count() const { gd_stats s{}; Check(h_, gd_stats_get(h_, &s)); return (int)s.table_live; }
+    int Count() const {
+        gd_stats s{};
+        Check(h_, gd_stats_get(h_, &s));
+        uint64_t ext = 0;
+        Check(h_, gd_dir_ext_stats(h_, &ext, nullptr, nullptr));
+        return (int)(s.table_live + ext);
+    }
     const ActivationId& ActivationAt(uint32_t idx) const { return acts_.at(idx); }
     uint32_t ActIndex(const ActivationId& a) {
         const auto it = act_index_.find(a);
@@ -496,6 +573,18 @@ public:
         for (const auto& g : grains) keys.push_back(g.Key.ToNative());
         std::vector<uint32_t> idx(keys.size());
         if (!keys.empty()) Check(h_, gd_ring_owner(h_, keys.data(), (uint32_t)keys.size(), idx.data()));
+        // KeyExt grains: the owner of their uniform hash over ToByteArray (UniqueKey.cs:272-293)
+        std::vector<uint32_t> at, hashes;
+        for (size_t i = 0; i < grains.size(); ++i)
+            if (grains[i].Key.HasKeyExt()) {
+                at.push_back((uint32_t)i);
+                hashes.push_back(grains[i].GetUniformHashCode());
+            }
+        if (!at.empty()) {
+            std::vector<uint32_t> own(at.size());
+            Check(h_, gd_ring_lookup_hashes(h_, hashes.data(), (uint32_t)at.size(), own.data()));
+            for (size_t j = 0; j < at.size(); ++j) idx[at[j]] = own[j];
+        }
         std::vector<SiloAddress> r;
         for (uint32_t i : idx) r.push_back(RingSilo(i));
         return r;
@@ -585,23 +674,27 @@ struct Message {                       // the header fields the path reads/write
 
 // Batched Dispatcher.AddressMessage (Dispatcher.cs:715-767): messages whose TargetAddress is
 // complete are skipped (:718); the rest get SetTargetPlacement (Message.cs:629-639) on a hit.
-// Returns the indices that stay on the C# slow path (MISS, system target, membership, KeyExt).
+// Returns the indices that stay on the C# slow path (MISS, system target, membership grain).
 class Dispatcher {
 public:
     explicit Dispatcher(LocalGrainDirectory& dir) : dir_(dir) {}
     std::vector<size_t> AddressMessages(std::vector<Message>& msgs) {
         std::vector<size_t> todo;
         std::vector<gd_key> keys;
+        std::vector<const UniqueKey*> uk;
         for (size_t i = 0; i < msgs.size(); ++i)
             if (!(msgs[i].TargetSilo && msgs[i].TargetActivation)) {
                 todo.push_back(i);
                 keys.push_back(msgs[i].TargetGrain.Key.ToNative());
+                uk.push_back(&msgs[i].TargetGrain.Key);
             }
         std::vector<uint32_t> silo(keys.size()), act(keys.size());
         std::vector<uint8_t> st(keys.size());
-        if (!keys.empty())
-            Check(dir_.Handle(), gd_route(dir_.Handle(), keys.data(), (uint32_t)keys.size(), silo.data(), act.data(),
-                                          st.data()));
+        if (!keys.empty()) {        // string-keyed targets are routed on the GPU too (gd_route_ext)
+            KeyExtBatch kx(uk);
+            Check(dir_.Handle(), gd_route_ext(dir_.Handle(), keys.data(), kx.get(), (uint32_t)keys.size(), silo.data(),
+                                              act.data(), st.data()));
+        }
         std::vector<size_t> slow;
         for (size_t j = 0; j < todo.size(); ++j) {
             Message& m = msgs[todo[j]];

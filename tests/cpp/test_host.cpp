@@ -297,6 +297,84 @@ static void DispatcherAndAgent() {
     EXPECT(total == target.size());
 }
 
+// String-keyed grains (GrainId.GetGrainId(long, string), GrainId.cs:86-91) and compound keys
+// (:72-77) through the same partition / directory / dispatcher objects.
+static SiloAddress RingOwnerD(const LocalGrainDirectory& dir, uint32_t hash) {   // LocalGrainDirectory.cs:506-541
+    const auto& pts = dir.Ring().Points();
+    const auto& own = dir.Ring().Owners();
+    size_t pick = pts.size() - 1;
+    for (size_t i = pts.size(); i-- > 0;)
+        if ((int32_t)pts[i] <= (int32_t)hash) { pick = i; break; }
+    return dir.Ring().Members()[own[pick]];
+}
+
+static void StringKeyGrains() {
+    DispatchHandle h(0, 4096, 0);
+    const SiloAddress me = SiloAddress::New(10, 0, 0, 1, 11111, 1);
+    LocalGrainDirectory dir(h.get(), me);
+    for (int i = 2; i <= 8; ++i) dir.AddServer(SiloAddress::New(10, 0, 0, (uint8_t)i, 11111, 1));
+    auto& part = dir.DirectoryPartition();
+    const int tc = gd_calculate_id_hash("UnitTests.GrainInterfaces.IStringKeyGrain");
+    std::vector<GrainId> grains;
+    std::vector<ActivationId> acts;
+    for (int k = 0; k < 600; ++k) {
+        std::string name = "user/" + std::to_string(k) + (k % 3 ? "" : "\xC3\xA9") + std::string(k % 40, 'x');
+        grains.push_back(k % 5 ? GrainId::GetGrainId(tc, name) : GrainId::GetGrainId(tc, (int64_t)k, name));
+        acts.push_back(NewActivationId(9000 + k));
+    }
+    const auto owners = dir.CalculateTargetSilos(grains);
+    for (size_t i = 0; i < grains.size(); ++i) EXPECT(owners[i] == RingOwnerD(dir, grains[i].GetUniformHashCode()));
+    std::vector<GrainId> reg(grains.begin(), grains.begin() + 400);
+    std::vector<ActivationId> regActs(acts.begin(), acts.begin() + 400);
+    std::vector<SiloAddress> regSilos(owners.begin(), owners.begin() + 400);
+    const GrainId plain = GrainId::GetGrainId(tc, (int64_t)77);          // same type, no KeyExt
+    reg.push_back(plain);
+    regActs.push_back(NewActivationId(1));
+    regSilos.push_back(me);
+    reg.push_back(grains[0]);                                             // duplicate: first wins
+    regActs.push_back(NewActivationId(2));
+    regSilos.push_back(me);
+    const auto r = part.AddSingleActivations(reg, regActs, regSilos);
+    EXPECT(r.back().Address && r.back().Address->Activation == acts[0]);
+    EXPECT(part.Count() == 401);
+    AddressesAndTag res;
+    EXPECT(dir.LocalLookup(grains[7], res) && (*res.Addresses)[0].Activation == acts[7]);
+    EXPECT(!dir.LocalLookup(grains[500], res));
+    EXPECT(dir.LocalLookup(plain, res) && (*res.Addresses)[0].Activation == regActs[400]);
+    // a string grain and a long grain with the same words but another (or no) KeyExt differ
+    GrainId other = grains[5];
+    other.Key.KeyExt = *other.Key.KeyExt + "!";
+    EXPECT(!dir.LocalLookup(other, res));
+    // Dispatcher: string targets are addressed on the GPU
+    std::vector<Message> msgs;
+    std::mt19937 rng(11);
+    std::vector<int> pick;
+    for (int i = 0; i < 3000; ++i) {
+        const int k = (int)(rng() % 600);
+        pick.push_back(k);
+        msgs.push_back(Message{grains[k], {}, {}, 0xFF});
+    }
+    Dispatcher disp(dir);
+    const auto slow = disp.AddressMessages(msgs);
+    size_t misses = 0;
+    for (size_t i = 0; i < msgs.size(); ++i) {
+        const int k = pick[i];
+        if (k < 400) {
+            EXPECT(msgs[i].RouteStatus == GD_ROUTE_OK && *msgs[i].TargetActivation == acts[k] &&
+                   *msgs[i].TargetSilo == owners[k]);
+        } else {
+            EXPECT(msgs[i].RouteStatus == GD_ROUTE_MISS);
+            ++misses;
+        }
+    }
+    EXPECT(slow.size() == misses);
+    // RemoveActivation on a string grain
+    EXPECT(!part.RemoveActivation(grains[3], acts[4]));
+    EXPECT(part.RemoveActivation(grains[3], acts[3]));
+    EXPECT(!dir.LocalLookup(grains[3], res));
+    EXPECT(part.Count() == 400);
+}
+
 // ---------------------------------------------------------------- LruTest.cs (test/NonSilo.Tests/General)
 // The reference's LRU tests, restated against the GPU directory cache (AdaptiveGrainDirectoryCache
 // over LRU); keys "1".."n" become grains 1..n of one type.
@@ -418,6 +496,7 @@ int main(int argc, char** argv) {
         Run("VirtualBucketsRanges", VirtualBucketsRanges);
         Run("DirectorySemantics", DirectorySemantics);
         Run("DispatcherAndAgent", DispatcherAndAgent);
+        Run("StringKeyGrains", StringKeyGrains);
         Run("LruCountTest", LruCountTest);
         Run("LruMaximumSizeTest", LruMaximumSizeTest);
         Run("LruUsageTest", LruUsageTest);
