@@ -318,6 +318,18 @@ int gd_route_multi_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32
  * (results stay on the device -> gd_multi_fetch). */
 int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, int flags,
                    gd_multi_result* out);
+/* CalculateTargetSilo (LocalGrainDirectory.cs:477-545) with KeyExt strings: the owner silo the
+ * exchange partition uses (system targets / KeyExt without a string -> my silo, the membership
+ * grain -> the seed).  Host pointers. */
+int gd_ring_owner_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t* out_silo);
+/* With the batch's KeyExt strings (gd_key_ext, as gd_route_ext): KeyExt grains go to the rank
+ * owning their KeyExt hash, their strings travel in a byte round after the header round, and they
+ * are routed there like any grain (without ext they stay on the sender, status GD_ROUTE_KEYEXT).
+ * The _device form takes device arrays inside *d_ext. */
+int gd_route_multi_ext_device(gd_handle* h, const gd_key* d_keys, const gd_key_ext* d_ext, uint32_t n,
+                              uint32_t n_act, int flags, gd_multi_result* out);
+int gd_route_multi_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t n_act,
+                       int flags, gd_multi_result* out);
 /* Copy the last result to host arrays sized from gd_multi_result (any pointer may be NULL). */
 int gd_multi_fetch(gd_handle* h, gd_key* recv_keys, uint32_t* recv_idx, uint32_t* recv_src, uint32_t* silo,
                    uint32_t* act, uint8_t* status, uint32_t* perm, uint32_t* offsets, uint32_t* ret_silo,

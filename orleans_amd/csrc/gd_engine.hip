@@ -97,11 +97,13 @@ struct gd_handle {
     hipStream_t xstream = nullptr;
     hipEvent_t x_in = nullptr, x_hdr[2] = {}, x_route[2] = {}, x_ret[2] = {}, x_done[2] = {};
     bool x_done_rec[2] = {false, false};
-    DevBuf mx_send[3];                // send keys, send idx, counts (send [W], recv [W])
-    DevBuf mx[2][16];                 // per batch parity: receive / result buffers
+    DevBuf mx_send[6];                // send keys, send idx, counts (send/recv messages, send/recv KeyExt
+                                      // bytes: 4 x [W]), KeyExt lengths, KeyExt byte offsets, KeyExt blob
+    DevBuf mx[2][20];                 // per batch parity: receive / result buffers
     DevBuf mx_keys;                   // host-keys entry point: the batch, on xstream
+    DevBuf mx_ext[3];                 // host-keys entry point: its KeyExt blob, offsets, lengths
     DevBuf x_scratch[4];              // xstream's own scan partials + partition scratch
-    uint32_t* h_xcnt = nullptr;       // pinned: send counts, recv counts
+    uint32_t* h_xcnt = nullptr;       // pinned: send/recv message counts, send/recv KeyExt byte counts
     gd_multi_result mres[2] = {};
     uint32_t mres_n[2] = {0, 0};
     uint64_t mcalls = 0;
@@ -504,9 +506,9 @@ int maybe_grow_table(gd_handle* h, uint64_t incoming) {
 // ---- exchange partition (gd_shard.h) -------------------------------------------------
 template <int MODE, bool NODES>
 int shard_hist_t(gd_handle* h, const void* recs, uint32_t n, uint64_t tcd, uint32_t n_shards, uint32_t bits,
-                 uint32_t tiles, uint8_t* dest, uint32_t* hist) {
+                 uint32_t tiles, uint8_t* dest, uint32_t* hist, const ExtArgs& ext) {
     return launch(h, "k_shard_hist", dim3(tiles), dim3(SH_NT), ring_lds(h), k_shard_hist<MODE, NODES>, recs, n, tcd,
-                  ring_args(h), n_shards, bits, tiles, dest, hist);
+                  ring_args(h), n_shards, bits, tiles, dest, hist, ext);
 }
 
 template <int BITS, bool NODES>
@@ -520,7 +522,7 @@ int shard_scatter_t(gd_handle* h, const void* recs, const uint32_t* payload, con
 // (payload == nullptr: the batch index); counts[d] per destination.
 template <bool NODES>
 int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t n, uint64_t tcd, uint32_t n_shards,
-               void* out_recs, uint32_t* out_pay, uint32_t* counts) {
+               void* out_recs, uint32_t* out_pay, uint32_t* counts, const ExtArgs& ext = ExtArgs{}) {
     GD_TRY(check_ring(h));
     if (n == 0)
         return launch(h, "k_fill", dim3(1), dim3(BLOCK), 0, k_fill_u32, counts, n_shards, 0u);
@@ -534,13 +536,13 @@ int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t
     while ((1u << bits) < n_shards) ++bits;
     switch (h->ring_mode) {
         case GD_RING_DIRECTORY:
-            GD_TRY((shard_hist_t<GD_RING_DIRECTORY, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist)));
+            GD_TRY((shard_hist_t<GD_RING_DIRECTORY, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext)));
             break;
         case GD_RING_CONSISTENT:
-            GD_TRY((shard_hist_t<GD_RING_CONSISTENT, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist)));
+            GD_TRY((shard_hist_t<GD_RING_CONSISTENT, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext)));
             break;
         default:
-            GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist)));
+            GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext)));
     }
     GD_TRY(scan_device<OpAdd>(h, hist, tiles * n_shards, false, false, "shard"));
     GD_TRY(launch(h, "k_shard_counts", dim3(1), dim3(256), 0, k_shard_counts, (const uint32_t*)hist, tiles, n_shards, n,
@@ -2118,6 +2120,7 @@ void comm_release(gd_handle* h) {
     for (auto& slot : h->mx)
         for (DevBuf& b : slot) free_buf(b);
     free_buf(h->mx_keys);
+    for (DevBuf& b : h->mx_ext) free_buf(b);
     for (DevBuf& b : h->x_scratch) free_buf(b);
     if (h->h_xcnt) (void)hipHostFree(h->h_xcnt);
     h->h_xcnt = nullptr;
@@ -2188,7 +2191,8 @@ int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uin
 //   xstream: [wait probe] routes round, unpartition            (GD_MULTI_RETURN_ROUTES)
 // Only the counts round blocks the host, and only on xstream, so batch i+1's partition and
 // exchange run while batch i is probed and bucketed.
-int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int flags, gd_multi_result* out) {
+int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int flags, gd_multi_result* out,
+                const gd_key_ext* ext = nullptr) {
     GD_TRY(need_comm(h));
     GD_TRY(check_ring(h));
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
@@ -2197,6 +2201,8 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     const int s = (int)(h->mcalls & 1);
     DevBuf* B = h->mx[s];
     const bool ret = (flags & GD_MULTI_RETURN_ROUTES) != 0;
+    const bool has_ext = ext && n && !h->cache_max;      // KeyExt strings travel with their messages
+    const ExtArgs x = has_ext ? ExtArgs{ext->bytes, ext->offset, ext->length, ext->bytes_len} : ExtArgs{};
     if (!(flags & GD_MULTI_KEYS_READY)) {
         HIP_TRY(h, hipEventRecord(h->x_in, h->stream));
         HIP_TRY(h, hipStreamWaitEvent(h->xstream, h->x_in, 0));
@@ -2204,43 +2210,70 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     // 1. stable partition by owner rank (gd_shard.h) + counts, on the exchange stream
     GD_TRY(grow(h, h->mx_send[0], (size_t)n * sizeof(gd_key) + 8));
     GD_TRY(grow(h, h->mx_send[1], (size_t)n * 4 + 4));
-    GD_TRY(grow(h, h->mx_send[2], (size_t)W * 8));
+    GD_TRY(grow(h, h->mx_send[2], (size_t)W * 16));
+    if (has_ext) {
+        GD_TRY(grow(h, h->mx_send[3], (size_t)n * 4 + 4));
+        GD_TRY(grow(h, h->mx_send[4], (size_t)n * 4 + 4));
+    }
     gd_key* send_keys = (gd_key*)h->mx_send[0].p;
     uint32_t* send_idx = (uint32_t*)h->mx_send[1].p;
-    uint32_t* dcnt = (uint32_t*)h->mx_send[2].p;           // [0, W): send counts, [W, 2W): recv counts
+    uint32_t* dcnt = (uint32_t*)h->mx_send[2].p;   // send msgs [0,W), recv msgs [W,2W), send bytes, recv bytes
+    int32_t* send_len = (int32_t*)h->mx_send[3].p;
+    uint32_t* send_boff = (uint32_t*)h->mx_send[4].p;
     {
         OnXStream on(h);
-        GD_TRY(shard_pack<false>(h, d_keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt));
+        GD_TRY(shard_pack<false>(h, d_keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt, x));
+        if (has_ext) {                 // KeyExt bytes per destination; lengths and byte offsets in send order
+            HIP_TRY(h, hipMemsetAsync(dcnt + 2 * W, 0, (size_t)W * 4, h->stream));
+            GD_TRY(launch(h, "k_dest_bytes", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_dest_bytes,
+                          (const uint8_t*)h->shard_dest.p, n, x, (uint32_t)W, dcnt + 2 * W));
+            GD_TRY(launch(h, "k_send_lengths", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_send_lengths,
+                          (const uint32_t*)send_idx, n, x, send_len, send_boff));
+            GD_TRY(scan_device<OpAdd>(h, send_boff, n, false, false, "ext_offsets"));
+        }
         NCCL_TRY(h, R.GroupStart());
         for (int r = 0; r < W; ++r) {
             NCCL_TRY(h, R.Send(dcnt + r, 1, ncclUint32, r, h->comm, h->stream));
             NCCL_TRY(h, R.Recv(dcnt + W + r, 1, ncclUint32, r, h->comm, h->stream));
+            if (has_ext) {
+                NCCL_TRY(h, R.Send(dcnt + 2 * W + r, 1, ncclUint32, r, h->comm, h->stream));
+                NCCL_TRY(h, R.Recv(dcnt + 3 * W + r, 1, ncclUint32, r, h->comm, h->stream));
+            }
         }
         NCCL_TRY(h, R.GroupEnd());
-        HIP_TRY(h, hipMemcpyAsync(h->h_xcnt, dcnt, (size_t)W * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipMemcpyAsync(h->h_xcnt, dcnt, (size_t)W * (has_ext ? 16 : 8), hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(h, hipStreamSynchronize(h->stream));
     }
     ncclResult_t async_err = ncclSuccess;
     NCCL_TRY(h, R.CommGetAsyncError(h->comm, &async_err));
     if (async_err != ncclSuccess) return set_err(h, GD_ERCCL, "RCCL async error: %s", R.GetErrorString(async_err));
     std::vector<uint32_t> sc(h->h_xcnt, h->h_xcnt + W), rc(h->h_xcnt + W, h->h_xcnt + 2 * W);
-    std::vector<uint64_t> soff(W + 1, 0), roff(W + 1, 0);
+    std::vector<uint32_t> sbc(W, 0), rbc(W, 0);
+    if (has_ext) {
+        sbc.assign(h->h_xcnt + 2 * W, h->h_xcnt + 3 * W);
+        rbc.assign(h->h_xcnt + 3 * W, h->h_xcnt + 4 * W);
+    }
+    std::vector<uint64_t> soff(W + 1, 0), roff(W + 1, 0), sboff(W + 1, 0), rboff(W + 1, 0);
     for (int r = 0; r < W; ++r) {
         soff[r + 1] = soff[r] + sc[r];
         roff[r + 1] = roff[r] + rc[r];
+        sboff[r + 1] = sboff[r] + sbc[r];
+        rboff[r + 1] = rboff[r] + rbc[r];
     }
     if (soff[W] != n)
         return set_err(h, GD_ERCCL, "partition counts sum to %llu, batch is %u", (unsigned long long)soff[W], n);
-    if (roff[W] >= 0xFFFFFFFFull)
-        return set_err(h, GD_EINVAL, "%llu messages received: more than a batch can hold",
-                       (unsigned long long)roff[W]);
+    if (roff[W] >= 0xFFFFFFFFull || rboff[W] >= 0xFFFFFFFFull || sboff[W] >= 0xFFFFFFFFull)
+        return set_err(h, GD_EINVAL, "%llu messages / %llu KeyExt bytes received: more than a batch can hold",
+                       (unsigned long long)roff[W], (unsigned long long)rboff[W]);
     const uint32_t m = (uint32_t)roff[W];
     // 2. this parity's buffers: batch i-2 must be done with them (probe/bucket and routes round)
     const size_t m4 = (size_t)m * 4 + 4, n4 = (size_t)n * 4 + 4;
-    const size_t want[16] = {(size_t)m * sizeof(gd_key) + 8, m4, m4, m4, m4, (size_t)m + 4, m4,
-                             ((size_t)n_act + 2) * 4, n4, n4, (size_t)n + 4, n4, n4, (size_t)n + 4, 0, 0};
-    for (int b = 0; b < 16; ++b)
-        if (want[b] && (b < 8 || ret)) GD_TRY(grow(h, B[b], want[b]));
+    const size_t want[20] = {(size_t)m * sizeof(gd_key) + 8, m4, m4, m4, m4, (size_t)m + 4, m4,
+                             ((size_t)n_act + 2) * 4, n4, n4, (size_t)n + 4, n4, n4, (size_t)n + 4,
+                             m4, (size_t)rboff[W] + 16, m4, (size_t)m * 8 + 8, 0, 0};
+    for (int b = 0; b < 20; ++b)
+        if (want[b] && (b < 8 || (ret && b < 14) || (has_ext && b >= 14))) GD_TRY(grow(h, B[b], want[b]));
+    if (has_ext) GD_TRY(grow(h, h->mx_send[5], (size_t)sboff[W] + 16));
     gd_key* recv_keys = (gd_key*)B[0].p;
     uint32_t* recv_idx = (uint32_t*)B[1].p;
     uint32_t* recv_src = (uint32_t*)B[2].p;
@@ -2252,9 +2285,23 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     if (h->x_done_rec[s]) HIP_TRY(h, hipStreamWaitEvent(h->xstream, h->x_done[s], 0));
     {
         OnXStream on(h);
-        const Lane lanes[2] = {{send_keys, recv_keys, sizeof(gd_key), ncclUint64, 3},
-                               {send_idx, recv_idx, 4, ncclUint32, 1}};
-        GD_TRY(exchange_round(h, "rccl_headers", sc.data(), soff.data(), rc.data(), roff.data(), lanes, 2));
+        if (has_ext)
+            GD_TRY(launch(h, "k_gather_ext", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_gather_ext,
+                          (const uint32_t*)send_idx, n, x, (const uint32_t*)send_boff, (uint8_t*)h->mx_send[5].p));
+        const Lane lanes[3] = {{send_keys, recv_keys, sizeof(gd_key), ncclUint64, 3},
+                               {send_idx, recv_idx, 4, ncclUint32, 1},
+                               {send_len, B[14].p, 4, ncclInt32, 1}};
+        GD_TRY(exchange_round(h, "rccl_headers", sc.data(), soff.data(), rc.data(), roff.data(), lanes,
+                              has_ext ? 3 : 2));
+        if (has_ext) {                 // the KeyExt strings, then their offsets in the receive blob
+            const Lane bl[1] = {{h->mx_send[5].p, B[15].p, 1, ncclUint8, 1}};
+            GD_TRY(exchange_round(h, "rccl_keyext", sbc.data(), sboff.data(), rbc.data(), rboff.data(), bl, 1));
+            GD_TRY(launch(h, "k_len_bytes", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_len_bytes,
+                          (const int32_t*)B[14].p, m, (uint32_t*)B[16].p));
+            GD_TRY(scan_device<OpAdd>(h, (uint32_t*)B[16].p, m, false, false, "ext_offsets"));
+            GD_TRY(launch(h, "k_u32_to_u64", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_u32_to_u64,
+                          (const uint32_t*)B[16].p, m, (uint64_t*)B[17].p));
+        }
         GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
                       (const uint32_t*)(dcnt + W), (uint32_t)W, m, recv_src));
         HIP_TRY(h, hipEventRecord(h->x_hdr[s], h->xstream));
@@ -2262,6 +2309,11 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     // 3. probe + bucket on the owner (the handle's stream)
     HIP_TRY(h, hipStreamWaitEvent(h->stream, h->x_hdr[s], 0));
     if (m) GD_TRY(route_device(h, recv_keys, m, silo, act, st));
+    if (m && has_ext)                  // the received strings: KeyExt grains are routed on their owner
+        GD_TRY(keyext_pass(h, recv_keys,
+                           ExtArgs{(const uint8_t*)B[15].p, (const uint64_t*)B[17].p, (const int32_t*)B[14].p,
+                                   rboff[W]},
+                           m, silo, act, st));
     HIP_TRY(h, hipEventRecord(h->x_route[s], h->stream));
     GD_TRY(bucket_device(h, act, m, n_act, perm, offs));
     // 4. routes back to the senders, into their batch order (Dispatcher.AddressMessage)
@@ -2327,7 +2379,7 @@ int gd_comm_init(gd_handle* h, const uint8_t id[GD_COMM_ID_BYTES], int n_ranks, 
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(sync(h));
     comm_release(h);
-    HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 2 * 256 * sizeof(uint32_t)));
+    HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 4 * 256 * sizeof(uint32_t)));
     HIP_TRY(h, hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
     for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
                           &h->x_ret[1], &h->x_done[0], &h->x_done[1]})
@@ -2370,6 +2422,39 @@ int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act,
     GD_TRY(grow(h, h->mx_keys, (size_t)n * sizeof(gd_key) + 8));
     if (n) HIP_TRY(h, hipMemcpyAsync(h->mx_keys.p, keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice, h->xstream));
     GD_TRY(route_multi(h, (const gd_key*)h->mx_keys.p, n, n_act, flags | GD_MULTI_KEYS_READY, out));
+    HIP_TRY(h, hipStreamSynchronize(h->xstream));
+    return sync_checked(h);
+}
+
+int gd_route_multi_ext_device(gd_handle* h, const gd_key* d_keys, const gd_key_ext* d_ext, uint32_t n, uint32_t n_act,
+                              int flags, gd_multi_result* out) {
+    if (!h || (n && (!d_keys || !d_ext || !d_ext->offset || !d_ext->length))) return set_err(h, GD_EINVAL, "null argument");
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
+    HIP_TRY(h, hipSetDevice(h->device));
+    return route_multi(h, d_keys, n, n_act, flags, out, d_ext);
+}
+
+int gd_route_multi_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t n_act, int flags,
+                       gd_multi_result* out) {
+    if (!h || (n && (!keys || !ext || !ext->offset || !ext->length))) return set_err(h, GD_EINVAL, "null argument");
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(need_comm(h));
+    // the batch and its strings go to the device on the exchange stream
+    GD_TRY(grow(h, h->mx_keys, (size_t)n * sizeof(gd_key) + 8));
+    GD_TRY(grow(h, h->mx_ext[0], (size_t)ext->bytes_len + 16));
+    GD_TRY(grow(h, h->mx_ext[1], (size_t)n * 8 + 8));
+    GD_TRY(grow(h, h->mx_ext[2], (size_t)n * 4 + 4));
+    if (n) {
+        HIP_TRY(h, hipMemcpyAsync(h->mx_keys.p, keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice, h->xstream));
+        if (ext->bytes_len)
+            HIP_TRY(h, hipMemcpyAsync(h->mx_ext[0].p, ext->bytes, ext->bytes_len, hipMemcpyHostToDevice, h->xstream));
+        HIP_TRY(h, hipMemcpyAsync(h->mx_ext[1].p, ext->offset, (size_t)n * 8, hipMemcpyHostToDevice, h->xstream));
+        HIP_TRY(h, hipMemcpyAsync(h->mx_ext[2].p, ext->length, (size_t)n * 4, hipMemcpyHostToDevice, h->xstream));
+    }
+    const gd_key_ext dx{(const uint8_t*)h->mx_ext[0].p, (const uint64_t*)h->mx_ext[1].p,
+                        (const int32_t*)h->mx_ext[2].p, ext->bytes_len};
+    GD_TRY(route_multi(h, (const gd_key*)h->mx_keys.p, n, n_act, flags | GD_MULTI_KEYS_READY, out, &dx));
     HIP_TRY(h, hipStreamSynchronize(h->xstream));
     return sync_checked(h);
 }
@@ -2767,6 +2852,31 @@ int gd_uniform_hashes_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ex
     GD_TRY(launch(h, "k_kx_hash", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_kx_hash, (const gd_key*)h->keys_in.p,
                   n, x, (uint32_t*)h->out_a.p));
     GD_TRY(d2h(h, out, h->out_a, n));
+    return sync(h);
+}
+
+int gd_ring_owner_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t* out_silo) {
+    if (!h || (n && (!keys || !ext || !out_silo || !ext->offset || !ext->length)))
+        return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(check_ring(h));
+    gd_key_ext dx;
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(stage_ext(h, ext, n, &dx));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * 4));
+    const ExtArgs x{dx.bytes, dx.offset, dx.length, dx.bytes_len};
+    const gd_key* k = (const gd_key*)h->keys_in.p;
+    uint32_t* o = (uint32_t*)h->out_a.p;
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    if (h->ring_mode == GD_RING_DIRECTORY)
+        GD_TRY(launch(h, "k_owner_ext", g, b, ring_lds(h), k_owner_ext<GD_RING_DIRECTORY>, k, n, ring_args(h), x, o));
+    else if (h->ring_mode == GD_RING_CONSISTENT)
+        GD_TRY(launch(h, "k_owner_ext", g, b, ring_lds(h), k_owner_ext<GD_RING_CONSISTENT>, k, n, ring_args(h), x, o));
+    else
+        GD_TRY(launch(h, "k_owner_ext", g, b, ring_lds(h), k_owner_ext<GD_RING_VIRTUAL_BUCKETS>, k, n, ring_args(h), x,
+                      o));
+    GD_TRY(d2h(h, out_silo, h->out_a, n));
     return sync(h);
 }
 

@@ -19,6 +19,7 @@
 
 #include "gd_common.h"
 #include "gd_kernels.h"
+#include "gd_keyext.h"
 
 namespace gd {
 
@@ -26,12 +27,29 @@ constexpr int SH_NT = 256;
 constexpr int SH_IT = 8;
 constexpr uint32_t SH_TILE = SH_NT * SH_IT;   // 2048 records per tile
 
+// Owner rank of message i.  KeyExt grains go to the owner of their KeyExt hash when the batch's
+// strings are given (ext.len != nullptr, gd_route_multi_ext), else they stay here (KEYEXT).
 template <int MODE>
 __device__ __forceinline__ uint32_t key_dest(uint64_t n0, uint64_t n1, uint64_t tcd, const uint32_t* s_pts,
-                                             const uint32_t* s_own, const RingArgs& ring, uint32_t n_shards) {
+                                             const uint32_t* s_own, const RingArgs& ring, uint32_t n_shards,
+                                             const ExtArgs& ext, uint32_t i) {
     const uint32_t cat = (uint32_t)(tcd >> 56);
     uint32_t silo;
-    if (cat == CAT_SYSTEM_TARGET || cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) silo = ring.my_silo;
+    const uint8_t* s;
+    int32_t len;
+    if ((cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) && ext.len && ext_of(ext, i, s, len)) {
+        uint32_t uh;
+        if (len < 0) {
+            uh = uniform_hash(n0, n1, tcd);
+        } else if (len <= KX_FAST_BYTES) {
+            uint32_t w[KX_FAST_WORDS];
+            load_str_fast(s, len, w);
+            uh = jenkins_keyext_fast(n0, n1, tcd, len, w);
+        } else {
+            uh = jenkins_keyext(n0, n1, tcd, s, len);
+        }
+        silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uh)];
+    } else if (cat == CAT_SYSTEM_TARGET || cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) silo = ring.my_silo;
     else if (is_membership(n0, n1, tcd)) silo = ring.seed_silo;
     else silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(n0, n1, tcd))];
     return (silo == NONE32 ? ring.my_silo : silo) % n_shards;
@@ -45,7 +63,7 @@ template <int MODE, bool NODES>
 __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ recs, uint32_t n, uint64_t tcd,
                                                       RingArgs ring, uint32_t n_shards, uint32_t bits,
                                                       uint32_t tiles, uint8_t* __restrict__ dest,
-                                                      uint32_t* __restrict__ hist) {
+                                                      uint32_t* __restrict__ hist, ExtArgs ext) {
     constexpr int NW = SH_NT / WAVE;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     __shared__ uint32_t s_wc[NW][256];
@@ -69,7 +87,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
                 d = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(0, node, tcd))] % n_shards;
             } else {
                 const uint64_t* kp = reinterpret_cast<const uint64_t*>(recs) + 3ull * i;
-                d = key_dest<MODE>(kp[0], kp[1], kp[2], s_pts, s_own, ring, n_shards);
+                d = key_dest<MODE>(kp[0], kp[1], kp[2], s_pts, s_own, ring, n_shards, ext, i);
             }
             dest[i] = (uint8_t)d;
         }
@@ -272,6 +290,81 @@ __global__ void __launch_bounds__(BLOCK) k_unpartition(const uint32_t* __restric
     silo[i] = silo_in[j];
     act[i] = act_in[j];
     st[i] = st_in[j];
+}
+
+// CalculateTargetSilo for a batch with KeyExt strings: the owner silo key_dest uses (no modulo).
+template <int MODE>
+__global__ void __launch_bounds__(BLOCK) k_owner_ext(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+                                                     ExtArgs ext, uint32_t* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    stage_ring(ring, s_pts, s_own);
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
+    out[i] = key_dest<MODE>(kp[0], kp[1], kp[2], s_pts, s_own, ring, 0xFFFFFFFFu, ext, i);
+}
+
+// ---- KeyExt strings through the exchange (gd_route_multi_ext) -----------------------------------
+// Payload bytes of message i's KeyExt (0 for null / host-kept / other categories).
+__device__ __forceinline__ uint32_t ext_bytes(const ExtArgs& e, uint32_t i) {
+    const int32_t l = e.len[i];
+    return l > 0 ? (uint32_t)l : 0u;
+}
+
+// Per destination: bytes of KeyExt payload (LDS per block, one atomic per destination per block).
+__global__ void __launch_bounds__(BLOCK) k_dest_bytes(const uint8_t* __restrict__ dest, uint32_t n, ExtArgs ext,
+                                                      uint32_t n_shards, uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_b[256];
+    for (uint32_t d = threadIdx.x; d < 256; d += BLOCK) s_b[d] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n) {
+        const uint32_t b = ext_bytes(ext, i);
+        if (b) atomicAdd(&s_b[dest[i]], b);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < n_shards; d += BLOCK)
+        if (s_b[d]) atomicAdd(&out[d], s_b[d]);
+}
+
+// Lengths in send order (the partition's origin index picks them); payload sizes for the scan.
+__global__ void __launch_bounds__(BLOCK) k_send_lengths(const uint32_t* __restrict__ send_idx, uint32_t n,
+                                                        ExtArgs ext, int32_t* __restrict__ send_len,
+                                                        uint32_t* __restrict__ send_bytes) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t i = send_idx[j];
+    send_len[j] = ext.len[i];
+    send_bytes[j] = ext_bytes(ext, i);
+}
+
+// Copy each message's KeyExt bytes to its place in the send blob (boff = exclusive scan).
+__global__ void __launch_bounds__(BLOCK) k_gather_ext(const uint32_t* __restrict__ send_idx, uint32_t n, ExtArgs ext,
+                                                      const uint32_t* __restrict__ boff, uint8_t* __restrict__ blob) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t i = send_idx[j];
+    const uint32_t b = ext_bytes(ext, i);
+    if (!b) return;
+    const uint64_t off = ext.off[i];
+    if (off > ext.bytes_len || b > ext.bytes_len - off) return;   // k_route_keyext keeps such items KEYEXT
+    const uint8_t* src = ext.bytes + off;
+    uint8_t* dst = blob + boff[j];
+    for (uint32_t k = 0; k < b; ++k) dst[k] = src[k];
+}
+
+// Receiver: payload sizes of the received lengths (for the scan), then 64-bit offsets.
+__global__ void __launch_bounds__(BLOCK) k_len_bytes(const int32_t* __restrict__ len, uint32_t m,
+                                                     uint32_t* __restrict__ bytes) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j < m) bytes[j] = len[j] > 0 ? (uint32_t)len[j] : 0u;
+}
+__global__ void __launch_bounds__(BLOCK) k_u32_to_u64(const uint32_t* __restrict__ a, uint32_t m,
+                                                      uint64_t* __restrict__ b) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j < m) b[j] = a[j];
 }
 
 }  // namespace gd

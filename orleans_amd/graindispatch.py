@@ -48,7 +48,7 @@ EXPORTED_SYMBOLS = [
     "gd_dir_register_ext", "gd_dir_unregister_ext", "gd_dir_lookup_ext", "gd_uniform_hashes_ext",
     "gd_dir_ext_stats", "gd_route_ext", "gd_route_bucket_ext", "gd_route_ext_device", "gd_route_bucket_ext_device",
     "gd_comm_unique_id", "gd_comm_init", "gd_comm_destroy", "gd_route_multi_device", "gd_route_multi",
-    "gd_multi_fetch",
+    "gd_multi_fetch", "gd_route_multi_ext_device", "gd_route_multi_ext", "gd_ring_owner_ext",
 ]
 
 
@@ -238,6 +238,10 @@ def _load() -> C.CDLL:
         "gd_route_multi_device": (C.c_int, [P, P, U32, U32, C.c_int, C.POINTER(gd_multi_result)]),
         "gd_route_multi": (C.c_int, [P, P, U32, U32, C.c_int, C.POINTER(gd_multi_result)]),
         "gd_multi_fetch": (C.c_int, [P] + [P] * 11),
+        "gd_route_multi_ext_device": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, U32, C.c_int,
+                                                C.POINTER(gd_multi_result)]),
+        "gd_ring_owner_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, P]),
+        "gd_route_multi_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, U32, C.c_int, C.POINTER(gd_multi_result)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -742,6 +746,24 @@ class GrainDispatch:
         r = gd_multi_result()
         flags = GD_MULTI_RETURN_ROUTES if return_routes else 0
         self._c(lib.gd_route_multi(self.h, _ptr(k), n, n_act, flags, C.byref(r)))
+        return self.multi_fetch(r, n)
+
+    def ring_owner_ext(self, keys, exts) -> np.ndarray:
+        k = keys_array(keys)
+        n = len(k)
+        x = self._ext(exts, n)
+        out = np.zeros(n, dtype=np.uint32)
+        self._c(lib.gd_ring_owner_ext(self.h, _ptr(k), C.byref(x.struct), n, _ptr(out)))
+        return out
+
+    def route_multi_ext(self, keys, exts, n_act: int, return_routes: bool = False) -> dict:
+        """route_multi with KeyExt grains routed on their owner (strings travel with the batch)."""
+        k = keys_array(keys)
+        n = k.shape[0]
+        x = self._ext(exts, n)
+        r = gd_multi_result()
+        flags = GD_MULTI_RETURN_ROUTES if return_routes else 0
+        self._c(lib.gd_route_multi_ext(self.h, _ptr(k), C.byref(x.struct), n, n_act, flags, C.byref(r)))
         return self.multi_fetch(r, n)
 
     def multi_fetch(self, r: gd_multi_result, n: int) -> dict:

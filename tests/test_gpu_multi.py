@@ -216,3 +216,89 @@ class _Cai:
     def __init__(self, ptr, n):
         self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i4", "data": (int(ptr), False), "version": 3,
                                          "strides": None}
+
+
+@pytest.mark.parametrize("n", [0, 7, 30011])
+def test_route_multi_ext_world1(gd, n):
+    """gd_route_multi_ext: KeyExt grains partitioned by their KeyExt hash, strings carried in the
+    byte round, routed on the owner; results and returned routes against oracle/keyext.py."""
+    import keyext as kx
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    G = 2048
+    reg, own, _ = _directory(G, 1, 0, spec)
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 13, my_silo=4)
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+    e.register(reg, np.arange(G), own)
+    stc = o.grain_type_code("UnitTests.GrainInterfaces.IStringKeyGrain")
+    names = [f"acct:{i}" + "ß" * (i % 4) + "z" * (i % 50) for i in range(400)]
+    tcd = o.type_code_data(o.CAT_KEYEXT_GRAIN, stc)
+    d = kx.KeyExtDirectory()
+    e.register_ext(np.tile(np.array([[0, 0, tcd]], np.uint64), (200, 1)), names[:200], np.arange(200) + G,
+                   np.arange(200) % 8)
+    for i in range(200):
+        d.add_single_activation((0, 0, tcd), names[i].encode(), G + i, i % 8)
+    rng = np.random.default_rng(n + 3)
+    keys = o.grain_keys(TC, rng.integers(0, G + 100, size=n))
+    exts = [None] * n
+    for i in np.nonzero(rng.random(n) < 0.4)[0]:
+        keys[i] = (0, 0, tcd)
+        exts[i] = names[int(rng.integers(0, 400))].encode()
+    for i in range(0, n, 97):
+        if exts[i] is not None:
+            exts[i] = kx.EXT_HOST
+    e.comm_init(gd.GrainDispatch.comm_unique_id(), 1, 0)
+    bexts = [gd.GD_KEYEXT_HOST if (isinstance(x, str) and x == kx.EXT_HOST) else x for x in exts]
+    r = e.route_multi_ext(keys, bexts, G + 200, return_routes=True)
+    st, silo, act, _, _ = kx.route_batch_ext(keys, exts, spec, o.DirectoryArrays(reg, np.arange(G), own), d, my_silo=4)
+    np.testing.assert_array_equal(r["recv_keys"], keys)
+    np.testing.assert_array_equal(r["status"], st)
+    np.testing.assert_array_equal(r["silo"], silo)
+    np.testing.assert_array_equal(r["act"], act)
+    wp, wo = o.bucket_stable(act, G + 200)
+    np.testing.assert_array_equal(r["perm"], wp)
+    np.testing.assert_array_equal(r["offsets"], wo)
+    np.testing.assert_array_equal(r["ret_act"], act)
+    np.testing.assert_array_equal(r["ret_status"], st)
+    if n > 1000:
+        assert ((st == o.ST_OK) & (keys[:, 2] == np.uint64(tcd))).sum() > n // 10
+    e.comm_destroy()
+    e.close()
+
+
+@pytest.mark.parametrize("mode", ["D", "R", "V"])
+def test_ring_owner_ext_is_the_partition_owner(gd, mode):
+    """gd_ring_owner_ext runs the exchange partition's owner function (key_dest, gd_shard.h):
+    KeyExt grains by their KeyExt hash, null KeyExt by the three words, GD_KEYEXT_HOST and system
+    targets to my silo, the membership grain to the seed (LocalGrainDirectory.cs:477-545)."""
+    import keyext as kx
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, mode)
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 10, my_silo=5, seed_silo=2)
+    e.ring_set_silos(mode, [(s.ip, s.port, s.gen) for s in silos])
+    rng = np.random.default_rng(9)
+    n = 4000
+    keys = o.grain_keys(TC, rng.integers(0, 10 ** 6, size=n))
+    exts = [None] * n
+    geo = o.type_code_data(o.CAT_GEO_CLIENT, 0)
+    for i in range(n):
+        c = i % 6
+        if c == 1:
+            keys[i] = (0, 0, o.type_code_data(o.CAT_KEYEXT_GRAIN, 77))
+            exts[i] = ("k%d" % i + "é" * (i % 9) + "x" * (i % 70)).encode()
+        elif c == 2:
+            keys[i] = (i, 1, geo)                      # geo client with a null KeyExt
+        elif c == 3:
+            keys[i] = (0, 0, o.type_code_data(o.CAT_KEYEXT_GRAIN, 77))
+            exts[i] = kx.EXT_HOST
+    keys[5::97] = np.array(o.UniqueKey(0, 3, o.type_code_data(o.CAT_SYSTEM_TARGET, 1)).as_tuple(), dtype=np.uint64)
+    keys[7::89] = np.array(o.MEMBERSHIP_TABLE_ID.as_tuple(), dtype=np.uint64)
+    for i in list(range(5, n, 97)) + list(range(7, n, 89)):
+        exts[i] = None
+    bexts = [gd.GD_KEYEXT_HOST if (isinstance(x, str) and x == kx.EXT_HOST) else x for x in exts]
+    got = e.ring_owner_ext(keys, bexts)
+    _, _, _, owner, _ = kx.route_batch_ext(keys, exts, spec, o.DirectoryArrays(np.zeros((0, 3), np.uint64), [], []),
+                                           kx.KeyExtDirectory(), my_silo=5, seed_silo=2)
+    want = np.where(owner == o.M32, 5, owner)          # KEYEXT kept here -> my silo
+    np.testing.assert_array_equal(got, want)
+    e.close()
