@@ -28,7 +28,7 @@ def main():
     knobs = [a.split("=") for a in sys.argv[2:]]
     names = [k for k, _ in knobs]
     combos = list(itertools.product(*[v.split(",") for _, v in knobs]))
-    N, A = 1 << 24, 1 << 20
+    N, A = int(os.environ.get("AB_N", 1 << 24)), int(os.environ.get("AB_A", 1 << 20))
     rng = np.random.default_rng(1)
     dev = torch.device("cuda:0")
     workloads = {"uniform": rng.integers(0, A, size=N).astype(np.uint32),
