@@ -1001,16 +1001,31 @@ __global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32_t* __r
 #pragma unroll
             for (int ww = 0; ww < NW; ++ww) s_wcnt[ww][d] = 0;
         __syncthreads();
-        uint32_t rk[MB_IT];
+        // Stable in-wave rank by ds_add_rtn (lanes served in ascending order, wave LDS ops in program
+        // order: the k_radix_scatter ranking); the first live lane's digit group takes one update.
+        // Rows past n are skipped wave-uniformly (a 4096-message batch fills half the rows).
+        uint32_t rk[MB_IT], lead[MB_IT];
+        unsigned long long hot[MB_IT];
 #pragma unroll
         for (int r = 0; r < MB_IT; ++r) {
+            rk[r] = 0;
+            hot[r] = 0;
+            lead[r] = 0;
+            if ((uint32_t)(w * MB_IT + r) * WAVE >= n) continue;
             const bool valid = (w * MB_IT + r) * WAVE + lane < n;
             const uint32_t d = (kk[r] >> shift) & (R - 1);
-            const unsigned long long peers = match_digit<BITS>(d, valid);
-            uint32_t c = 0;
-            if (valid) c = s_wcnt[w][d];
-            rk[r] = c + (uint32_t)__popcll(peers & lt);
-            if (valid && (peers & lt) == 0) s_wcnt[w][d] = c + (uint32_t)__popcll(peers);
+            const unsigned long long live = __ballot(valid);
+            lead[r] = (uint32_t)__ffsll((long long)live) - 1;
+            const uint32_t hd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead[r]);
+            hot[r] = __ballot(valid && d == hd);
+            if (valid && (d != hd || lane == lead[r]))
+                rk[r] = atomicAdd(&s_wcnt[w][d], lane == lead[r] ? (uint32_t)__popcll(hot[r]) : 1u);
+        }
+#pragma unroll
+        for (int r = 0; r < MB_IT; ++r) {
+            if ((uint32_t)(w * MB_IT + r) * WAVE >= n) continue;
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)rk[r], (int)lead[r]);
+            if ((hot[r] >> lane) & 1ull) rk[r] = b0 + (uint32_t)__popcll(hot[r] & lt);
         }
         __syncthreads();
         uint32_t total = 0;
