@@ -436,6 +436,14 @@ int gd_route_frames_ext(gd_handle* h, const uint8_t* buf, uint64_t buf_len, cons
  * smallest-ActivationId rule to those). */
 int gd_dir_split(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int move, gd_key* out_keys,
                  gd_val* out_vals, uint64_t out_capacity, uint64_t* out_n);
+/* The same split over the KeyExt table (string-keyed grains): the owner of each entry's stored
+ * uniform hash under the installed ring.  Entries in slot order with their KeyExt strings:
+ * out_length[i] (GD_KEYEXT_NULL for a null KeyExt), out_offset[i] into out_bytes.  out_keys == NULL:
+ * size query (*out_n entries, *out_nbytes string bytes).  Host pointers; the merge on the receiving
+ * handle is gd_dir_register_ext. */
+int gd_dir_split_ext(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int move, gd_key* out_keys,
+                     gd_val* out_vals, uint64_t* out_offset, int32_t* out_length, uint8_t* out_bytes,
+                     uint64_t capacity, uint64_t bytes_capacity, uint64_t* out_n, uint64_t* out_nbytes);
 /* Same, device output arrays (keep_silo stays a host array); synchronous. */
 int gd_dir_split_device(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int move, gd_key* d_out_keys,
                         gd_val* d_out_vals, uint64_t out_capacity, uint64_t* out_n);

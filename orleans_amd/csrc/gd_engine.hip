@@ -2880,4 +2880,66 @@ int gd_ring_owner_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, u
     return sync(h);
 }
 
+
+int gd_dir_split_ext(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int move, gd_key* out_keys,
+                     gd_val* out_vals, uint64_t* out_offset, int32_t* out_length, uint8_t* out_bytes,
+                     uint64_t capacity, uint64_t bytes_capacity, uint64_t* out_n, uint64_t* out_nbytes) {
+    if (!h || !out_n || !out_nbytes || (n_keep && !keep_silo)) return set_err(h, GD_EINVAL, "null argument");
+    if (out_keys && (!out_vals || !out_offset || !out_length || !out_bytes))
+        return set_err(h, GD_EINVAL, "keys, vals, offsets, lengths and bytes go together");
+    *out_n = *out_nbytes = 0;
+    if (h->kx_live == 0) return GD_OK;
+    // owners of the live entries' stored uniform hashes under the installed ring (slot order)
+    std::vector<uint64_t> live;
+    std::vector<uint32_t> hashes;
+    for (uint64_t i = 0; i < h->kx_cap; ++i)
+        if (slot_state(h->kx_m[i].meta) == SLOT_LIVE) {
+            live.push_back(i);
+            hashes.push_back(h->kx_m[i].uhash);
+        }
+    std::vector<uint32_t> owner(live.size());
+    GD_TRY(gd_ring_lookup_hashes(h, hashes.data(), (uint32_t)live.size(), owner.data()));
+    std::vector<uint64_t> sel;
+    uint64_t nbytes = 0;
+    for (size_t j = 0; j < live.size(); ++j) {
+        const bool kept = owner[j] < n_keep && keep_silo[owner[j]];
+        if (kept) continue;
+        sel.push_back(live[j]);
+        nbytes += (uint64_t)std::max(0, h->kx_m[live[j]].len);
+    }
+    *out_n = sel.size();
+    *out_nbytes = nbytes;
+    if (!out_keys || sel.empty()) return GD_OK;
+    if (sel.size() > capacity || nbytes > bytes_capacity)
+        return set_err(h, GD_EINVAL, "split selects %llu entries / %llu bytes, output holds %llu / %llu",
+                       (unsigned long long)sel.size(), (unsigned long long)nbytes, (unsigned long long)capacity,
+                       (unsigned long long)bytes_capacity);
+    uint64_t pos = 0;
+    std::vector<uint64_t> dirty;
+    for (size_t j = 0; j < sel.size(); ++j) {
+        KxSlot& q = h->kx_m[sel[j]];
+        out_keys[j] = gd_key{q.n0, q.n1, q.tcd};
+        out_vals[j] = gd_val{q.act, slot_silo(q.meta)};
+        out_length[j] = q.len;
+        out_offset[j] = pos;
+        if (q.len > 0) {
+            if (q.len <= KX_INLINE) {
+                uint8_t b[KX_INLINE];
+                std::memcpy(b, &q.off, 8);
+                std::memcpy(b + 8, q.tail, 16);
+                std::memcpy(out_bytes + pos, b, (size_t)q.len);
+            } else {
+                std::memcpy(out_bytes + pos, h->kx_hheap.data() + q.off, (size_t)q.len);
+            }
+            pos += (uint64_t)q.len;
+        }
+        if (move) {                    // the RemoveGrain after RegisterMany (GrainDirectoryHandoffManager.cs:228-232)
+            q.meta = make_meta(SLOT_TOMB, slot_silo(q.meta));
+            h->kx_live--;
+            h->kx_tomb++;
+            dirty.push_back(sel[j]);
+        }
+    }
+    return move ? kx_commit(h, dirty) : GD_OK;
+}
 }  // extern "C"

@@ -49,6 +49,7 @@ EXPORTED_SYMBOLS = [
     "gd_dir_ext_stats", "gd_route_ext", "gd_route_bucket_ext", "gd_route_ext_device", "gd_route_bucket_ext_device",
     "gd_comm_unique_id", "gd_comm_init", "gd_comm_destroy", "gd_route_multi_device", "gd_route_multi",
     "gd_multi_fetch", "gd_route_multi_ext_device", "gd_route_multi_ext", "gd_ring_owner_ext",
+    "gd_dir_split_ext",
 ]
 
 
@@ -241,6 +242,7 @@ def _load() -> C.CDLL:
         "gd_route_multi_ext_device": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, U32, C.c_int,
                                                 C.POINTER(gd_multi_result)]),
         "gd_ring_owner_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, P]),
+        "gd_dir_split_ext": (C.c_int, [P, P, U32, C.c_int, P, P, P, P, P, U64, U64, C.POINTER(U64), C.POINTER(U64)]),
         "gd_route_multi_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, U32, C.c_int, C.POINTER(gd_multi_result)]),
     }
     for name, (res, args) in sig.items():
@@ -747,6 +749,24 @@ class GrainDispatch:
         flags = GD_MULTI_RETURN_ROUTES if return_routes else 0
         self._c(lib.gd_route_multi(self.h, _ptr(k), n, n_act, flags, C.byref(r)))
         return self.multi_fetch(r, n)
+
+    def split_ext(self, keep_silos, n_silos: int, move: bool = True):
+        """gd_dir_split_ext: (keys (m,3) u64, acts, silos, KeyExt list (bytes / None)) in slot order."""
+        keep = self.keep_mask(keep_silos, n_silos)
+        n, nb = C.c_uint64(), C.c_uint64()
+        self._c(lib.gd_dir_split_ext(self.h, _ptr(keep), len(keep), int(move), None, None, None, None, None, 0, 0,
+                                     C.byref(n), C.byref(nb)))
+        m = n.value
+        keys = np.zeros((m, 3), np.uint64)
+        vals = np.zeros((m, 2), np.uint32)
+        off = np.zeros(m, np.uint64)
+        ln = np.zeros(m, np.int32)
+        blob = np.zeros(max(1, nb.value), np.uint8)
+        if m:
+            self._c(lib.gd_dir_split_ext(self.h, _ptr(keep), len(keep), int(move), _ptr(keys), _ptr(vals), _ptr(off),
+                                         _ptr(ln), _ptr(blob), m, nb.value, C.byref(n), C.byref(nb)))
+        exts = [None if ln[i] < 0 else bytes(blob[int(off[i]):int(off[i]) + int(ln[i])]) for i in range(m)]
+        return keys, vals[:, 0].copy(), vals[:, 1].copy(), exts
 
     def ring_owner_ext(self, keys, exts) -> np.ndarray:
         k = keys_array(keys)

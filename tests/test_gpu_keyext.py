@@ -303,3 +303,47 @@ def test_route_frames_ext(gd, mode):
     assert ((st0 == o.ST_KEYEXT) == ((wst != H.ROUTE_ADDRESSED) & (wst != H.ROUTE_UNDECODED) &
                                     (f["target_grain"][:, 2] == np.uint64(tcd)))).all()
     e.close()
+
+
+@pytest.mark.parametrize("mode", ["D", "V"])
+def test_split_ext_membership_change(gd, mode):
+    """gd_dir_split_ext: after a ring change, the KeyExt entries whose new owner (the stored
+    uniform hash under the new ring) is not kept leave the partition with their strings
+    (GrainDirectoryPartition.Split, GrainDirectoryPartition.cs:532-570; handoff predicate
+    GrainDirectoryHandoffManager.cs:212-218); merged elsewhere with gd_dir_register_ext."""
+    silos = o.bench_silos(8)
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 12)
+    e.ring_set_silos(mode, [(s.ip, s.port, s.gen) for s in silos])
+    tcd = o.type_code_data(o.CAT_KEYEXT_GRAIN, STC)
+    names = [f"player/{i}" + "ö" * (i % 5) + "y" * (i % 33) for i in range(3000)]
+    keys = np.tile(np.array([[0, 0, tcd]], np.uint64), (3000, 1))
+    keys[::7, 1] = np.arange(0, 3000, 7, dtype=np.uint64)                 # compound keys too
+    exts = [n.encode() for n in names]
+    exts[5] = None
+    keys[5] = (1, 2, o.type_code_data(o.CAT_GEO_CLIENT, 0))               # a geo client, null KeyExt
+    acts = np.arange(3000, dtype=np.uint32)
+    e.register_ext(keys, exts, acts, acts % 8)
+    new = silos[:6] + [o.Silo("10.0.0.99", 11111, 3)]                       # silos 6, 7 leave, one joins
+    e.ring_set_silos(mode, [(s.ip, s.port, s.gen) for s in new])
+    spec = o.ring_spec(new, mode)
+    keep = [0, 1, 2]
+    owner = o.ring_owner_np(spec, np.array([kx.ext_uniform_hash(int(a), int(b), int(c), x)
+                                            for (a, b, c), x in zip(keys, exts)], dtype=np.uint32))
+    want = {(tuple(int(v) for v in keys[i]), exts[i], int(acts[i]), int(acts[i] % 8))
+            for i in range(3000) if int(owner[i]) not in keep}
+    k, a, s, x = e.split_ext(keep, len(new), move=True)
+    got = {(tuple(int(v) for v in k[i]), x[i], int(a[i]), int(s[i])) for i in range(len(a))}
+    assert got == want and len(a) == len(want) > 1000
+    assert e.ext_stats()["live"] == 3000 - len(want)
+    f, _, _ = e.lookup_ext(keys, exts)
+    assert (f.astype(bool) == np.array([int(o_) in keep for o_ in owner])).all()
+    k2, a2, _, _ = e.split_ext(keep, len(new), move=True)                   # nothing left to move
+    assert len(a2) == 0
+    other = gd.GrainDispatch(device=0, table_capacity=1 << 12)              # the merge on the receiver
+    other.ring_set_silos(mode, [(s_.ip, s_.port, s_.gen) for s_ in new])
+    _, _, ins = other.register_ext(k, x, a, s)
+    assert ins.all()
+    f2, a3, _ = other.lookup_ext(k, x)
+    assert f2.all() and (a3 == a).all()
+    other.close()
+    e.close()
