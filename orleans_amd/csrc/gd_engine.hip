@@ -95,14 +95,18 @@ struct gd_handle {
     ncclComm_t comm = nullptr;
     int n_ranks = 0, rank = -1;
     hipStream_t xstream = nullptr;
+    hipStream_t pstream = nullptr;    // the partition (pack) of the next batch, beside this one's rounds
     hipEvent_t x_in = nullptr, x_hdr[2] = {}, x_route[2] = {}, x_ret[2] = {}, x_done[2] = {};
-    bool x_done_rec[2] = {false, false};
-    DevBuf mx_send[6];                // send keys, send idx, counts (send/recv messages, send/recv KeyExt
-                                      // bytes: 4 x [W]), KeyExt lengths, KeyExt byte offsets, KeyExt blob
+    hipEvent_t p_packed = nullptr, x_sent[2] = {};
+    bool x_done_rec[2] = {false, false}, x_sent_rec[2] = {false, false};
+    DevBuf mx_send[2][6];             // per batch parity: send keys, send idx, counts (send/recv messages,
+                                      // send/recv KeyExt bytes: 4 x [W]), KeyExt lengths, KeyExt byte
+                                      // offsets, KeyExt blob
     DevBuf mx[2][20];                 // per batch parity: receive / result buffers
     DevBuf mx_keys;                   // host-keys entry point: the batch, on xstream
     DevBuf mx_ext[3];                 // host-keys entry point: its KeyExt blob, offsets, lengths
     DevBuf x_scratch[4];              // xstream's own scan partials + partition scratch
+    DevBuf p_scratch[4];              // pstream's
     uint32_t* h_xcnt = nullptr;       // pinned: send/recv message counts, send/recv KeyExt byte counts
     gd_multi_result mres[2] = {};
     uint32_t mres_n[2] = {0, 0};
@@ -217,6 +221,7 @@ int resolve_timing(gd_handle* h) {
     if (h->pending.empty()) return GD_OK;
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     if (h->xstream) HIP_TRY(h, hipStreamSynchronize(h->xstream));
+    if (h->pstream) HIP_TRY(h, hipStreamSynchronize(h->pstream));
     for (auto& t : h->pending) {
         float ms = 0.f;
         HIP_TRY(h, hipEventElapsedTime(&ms, t.a, t.b));
@@ -670,6 +675,7 @@ void* gd_get_stream(gd_handle* h) { return h ? (void*)h->stream : nullptr; }
 int gd_synchronize(gd_handle* h) {
     if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
     HIP_TRY(h, hipSetDevice(h->device));
+    if (h->pstream) HIP_TRY(h, hipStreamSynchronize(h->pstream));
     if (h->xstream) HIP_TRY(h, hipStreamSynchronize(h->xstream));
     return sync_checked(h);
 }
@@ -2085,38 +2091,50 @@ namespace {
 // Launches inside the scope go to the exchange stream (launch() uses h->stream), with the
 // exchange stream's own scratch for the helpers both streams run (scan partials, partition):
 // the probe + bucketing of the previous batch may be using the handle's at the same time.
-struct OnXStream {
+struct OnStream {
     gd_handle* h;
     hipStream_t saved;
-    explicit OnXStream(gd_handle* hh) : h(hh), saved(hh->stream) {
-        h->stream = h->xstream;
+    DevBuf* scratch;
+    OnStream(gd_handle* hh, hipStream_t st, DevBuf* sc) : h(hh), saved(hh->stream), scratch(sc) {
+        h->stream = st;
         swap_scratch();
     }
-    ~OnXStream() {
+    ~OnStream() {
         swap_scratch();
         h->stream = saved;
     }
     void swap_scratch() {
-        std::swap(h->partials, h->x_scratch[0]);
-        std::swap(h->partials2, h->x_scratch[1]);
-        std::swap(h->shard_dest, h->x_scratch[2]);
-        std::swap(h->shard_hist, h->x_scratch[3]);
+        std::swap(h->partials, scratch[0]);
+        std::swap(h->partials2, scratch[1]);
+        std::swap(h->shard_dest, scratch[2]);
+        std::swap(h->shard_hist, scratch[3]);
     }
+};
+struct OnXStream : OnStream {
+    explicit OnXStream(gd_handle* hh) : OnStream(hh, hh->xstream, hh->x_scratch) {}
+};
+struct OnPStream : OnStream {
+    explicit OnPStream(gd_handle* hh) : OnStream(hh, hh->pstream, hh->p_scratch) {}
 };
 
 void comm_release(gd_handle* h) {
+    if (h->pstream) (void)hipStreamSynchronize(h->pstream);
     if (h->xstream) (void)hipStreamSynchronize(h->xstream);
     if (h->comm) (void)rccl().CommDestroy(h->comm);
     h->comm = nullptr;
     for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
-                          &h->x_ret[1], &h->x_done[0], &h->x_done[1]})
+                          &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1]})
         if (*e) {
             (void)hipEventDestroy(*e);
             *e = nullptr;
         }
     if (h->xstream) (void)hipStreamDestroy(h->xstream);
     h->xstream = nullptr;
-    for (DevBuf& b : h->mx_send) free_buf(b);
+    if (h->pstream) (void)hipStreamDestroy(h->pstream);
+    h->pstream = nullptr;
+    for (auto& par : h->mx_send)
+        for (DevBuf& b : par) free_buf(b);
+    for (DevBuf& b : h->p_scratch) free_buf(b);
     for (auto& slot : h->mx)
         for (DevBuf& b : slot) free_buf(b);
     free_buf(h->mx_keys);
@@ -2125,6 +2143,7 @@ void comm_release(gd_handle* h) {
     if (h->h_xcnt) (void)hipHostFree(h->h_xcnt);
     h->h_xcnt = nullptr;
     h->x_done_rec[0] = h->x_done_rec[1] = false;
+    h->x_sent_rec[0] = h->x_sent_rec[1] = false;
     h->mres[0] = h->mres[1] = gd_multi_result{};
     h->mcalls = 0;
     h->n_ranks = 0;
@@ -2136,9 +2155,10 @@ int need_comm(gd_handle* h) {
     return GD_OK;
 }
 
-// Grow a buffer either stream may touch: drain both first.
+// Grow a buffer any of the streams may touch: drain them first.
 int grow(gd_handle* h, DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return GD_OK;
+    HIP_TRY(h, hipStreamSynchronize(h->pstream));
     HIP_TRY(h, hipStreamSynchronize(h->xstream));
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     return ensure(h, b, bytes);
@@ -2203,25 +2223,28 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     const bool ret = (flags & GD_MULTI_RETURN_ROUTES) != 0;
     const bool has_ext = ext && n && !h->cache_max;      // KeyExt strings travel with their messages
     const ExtArgs x = has_ext ? ExtArgs{ext->bytes, ext->offset, ext->length, ext->bytes_len} : ExtArgs{};
+    DevBuf* SB = h->mx_send[s];
+    // 1. stable partition by owner rank (gd_shard.h) on the partition stream, into this parity's send
+    //    buffers once batch i-2's rounds have read them; it runs beside batch i-1's header round
+    GD_TRY(grow(h, SB[0], (size_t)n * sizeof(gd_key) + 8));
+    GD_TRY(grow(h, SB[1], (size_t)n * 4 + 4));
+    GD_TRY(grow(h, SB[2], (size_t)W * 16));
+    if (has_ext) {
+        GD_TRY(grow(h, SB[3], (size_t)n * 4 + 4));
+        GD_TRY(grow(h, SB[4], (size_t)n * 4 + 4));
+    }
     if (!(flags & GD_MULTI_KEYS_READY)) {
         HIP_TRY(h, hipEventRecord(h->x_in, h->stream));
-        HIP_TRY(h, hipStreamWaitEvent(h->xstream, h->x_in, 0));
+        HIP_TRY(h, hipStreamWaitEvent(h->pstream, h->x_in, 0));
     }
-    // 1. stable partition by owner rank (gd_shard.h) + counts, on the exchange stream
-    GD_TRY(grow(h, h->mx_send[0], (size_t)n * sizeof(gd_key) + 8));
-    GD_TRY(grow(h, h->mx_send[1], (size_t)n * 4 + 4));
-    GD_TRY(grow(h, h->mx_send[2], (size_t)W * 16));
-    if (has_ext) {
-        GD_TRY(grow(h, h->mx_send[3], (size_t)n * 4 + 4));
-        GD_TRY(grow(h, h->mx_send[4], (size_t)n * 4 + 4));
-    }
-    gd_key* send_keys = (gd_key*)h->mx_send[0].p;
-    uint32_t* send_idx = (uint32_t*)h->mx_send[1].p;
-    uint32_t* dcnt = (uint32_t*)h->mx_send[2].p;   // send msgs [0,W), recv msgs [W,2W), send bytes, recv bytes
-    int32_t* send_len = (int32_t*)h->mx_send[3].p;
-    uint32_t* send_boff = (uint32_t*)h->mx_send[4].p;
+    if (h->x_sent_rec[s]) HIP_TRY(h, hipStreamWaitEvent(h->pstream, h->x_sent[s], 0));
+    gd_key* send_keys = (gd_key*)SB[0].p;
+    uint32_t* send_idx = (uint32_t*)SB[1].p;
+    uint32_t* dcnt = (uint32_t*)SB[2].p;           // send msgs [0,W), recv msgs [W,2W), send bytes, recv bytes
+    int32_t* send_len = (int32_t*)SB[3].p;
+    uint32_t* send_boff = (uint32_t*)SB[4].p;
     {
-        OnXStream on(h);
+        OnPStream on(h);
         GD_TRY(shard_pack<false>(h, d_keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt, x));
         if (has_ext) {                 // KeyExt bytes per destination; lengths and byte offsets in send order
             HIP_TRY(h, hipMemsetAsync(dcnt + 2 * W, 0, (size_t)W * 4, h->stream));
@@ -2231,6 +2254,12 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
                           (const uint32_t*)send_idx, n, x, send_len, send_boff));
             GD_TRY(scan_device<OpAdd>(h, send_boff, n, false, false, "ext_offsets"));
         }
+        HIP_TRY(h, hipEventRecord(h->p_packed, h->pstream));
+    }
+    // 2. counts round on the exchange stream (after batch i-1's rounds), then the host sizes
+    HIP_TRY(h, hipStreamWaitEvent(h->xstream, h->p_packed, 0));
+    {
+        OnXStream on(h);
         NCCL_TRY(h, R.GroupStart());
         for (int r = 0; r < W; ++r) {
             NCCL_TRY(h, R.Send(dcnt + r, 1, ncclUint32, r, h->comm, h->stream));
@@ -2273,7 +2302,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
                              m4, (size_t)rboff[W] + 16, m4, (size_t)m * 8 + 8, 0, 0};
     for (int b = 0; b < 20; ++b)
         if (want[b] && (b < 8 || (ret && b < 14) || (has_ext && b >= 14))) GD_TRY(grow(h, B[b], want[b]));
-    if (has_ext) GD_TRY(grow(h, h->mx_send[5], (size_t)sboff[W] + 16));
+    if (has_ext) GD_TRY(grow(h, SB[5], (size_t)sboff[W] + 16));
     gd_key* recv_keys = (gd_key*)B[0].p;
     uint32_t* recv_idx = (uint32_t*)B[1].p;
     uint32_t* recv_src = (uint32_t*)B[2].p;
@@ -2287,14 +2316,14 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         OnXStream on(h);
         if (has_ext)
             GD_TRY(launch(h, "k_gather_ext", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_gather_ext,
-                          (const uint32_t*)send_idx, n, x, (const uint32_t*)send_boff, (uint8_t*)h->mx_send[5].p));
+                          (const uint32_t*)send_idx, n, x, (const uint32_t*)send_boff, (uint8_t*)SB[5].p));
         const Lane lanes[3] = {{send_keys, recv_keys, sizeof(gd_key), ncclUint64, 3},
                                {send_idx, recv_idx, 4, ncclUint32, 1},
                                {send_len, B[14].p, 4, ncclInt32, 1}};
         GD_TRY(exchange_round(h, "rccl_headers", sc.data(), soff.data(), rc.data(), roff.data(), lanes,
                               has_ext ? 3 : 2));
         if (has_ext) {                 // the KeyExt strings, then their offsets in the receive blob
-            const Lane bl[1] = {{h->mx_send[5].p, B[15].p, 1, ncclUint8, 1}};
+            const Lane bl[1] = {{SB[5].p, B[15].p, 1, ncclUint8, 1}};
             GD_TRY(exchange_round(h, "rccl_keyext", sbc.data(), sboff.data(), rbc.data(), rboff.data(), bl, 1));
             GD_TRY(launch(h, "k_len_bytes", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_len_bytes,
                           (const int32_t*)B[14].p, m, (uint32_t*)B[16].p));
@@ -2305,6 +2334,10 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
                       (const uint32_t*)(dcnt + W), (uint32_t)W, m, recv_src));
         HIP_TRY(h, hipEventRecord(h->x_hdr[s], h->xstream));
+        if (!ret) {                    // this parity's send buffers are free for batch i+2's partition
+            HIP_TRY(h, hipEventRecord(h->x_sent[s], h->xstream));
+            h->x_sent_rec[s] = true;
+        }
     }
     // 3. probe + bucket on the owner (the handle's stream)
     HIP_TRY(h, hipStreamWaitEvent(h->stream, h->x_hdr[s], 0));
@@ -2330,6 +2363,8 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
                           (const uint32_t*)send_idx, n, (const uint32_t*)B[8].p, (const uint32_t*)B[9].p,
                           (const uint8_t*)B[10].p, (uint32_t*)B[11].p, (uint32_t*)B[12].p, (uint8_t*)B[13].p));
             HIP_TRY(h, hipEventRecord(h->x_ret[s], h->xstream));
+            HIP_TRY(h, hipEventRecord(h->x_sent[s], h->xstream));   // send_idx read: buffers free
+            h->x_sent_rec[s] = true;
         }
         HIP_TRY(h, hipStreamWaitEvent(h->stream, h->x_ret[s], 0));   // the caller syncs one stream
         r.ret_silo = (const uint32_t*)B[11].p;
@@ -2381,8 +2416,9 @@ int gd_comm_init(gd_handle* h, const uint8_t id[GD_COMM_ID_BYTES], int n_ranks, 
     comm_release(h);
     HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 4 * 256 * sizeof(uint32_t)));
     HIP_TRY(h, hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
+    HIP_TRY(h, hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking));
     for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
-                          &h->x_ret[1], &h->x_done[0], &h->x_done[1]})
+                          &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1]})
         HIP_TRY(h, hipEventCreateWithFlags(e, hipEventDisableTiming));
     ncclUniqueId uid;
     std::memcpy(&uid, id, GD_COMM_ID_BYTES);
@@ -2420,7 +2456,7 @@ int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act,
     GD_TRY(need_comm(h));
     // the batch goes to the device on the exchange stream, so the partition needs no other wait
     GD_TRY(grow(h, h->mx_keys, (size_t)n * sizeof(gd_key) + 8));
-    if (n) HIP_TRY(h, hipMemcpyAsync(h->mx_keys.p, keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice, h->xstream));
+    if (n) HIP_TRY(h, hipMemcpyAsync(h->mx_keys.p, keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice, h->pstream));
     GD_TRY(route_multi(h, (const gd_key*)h->mx_keys.p, n, n_act, flags | GD_MULTI_KEYS_READY, out));
     HIP_TRY(h, hipStreamSynchronize(h->xstream));
     return sync_checked(h);
@@ -2446,11 +2482,11 @@ int gd_route_multi_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, 
     GD_TRY(grow(h, h->mx_ext[1], (size_t)n * 8 + 8));
     GD_TRY(grow(h, h->mx_ext[2], (size_t)n * 4 + 4));
     if (n) {
-        HIP_TRY(h, hipMemcpyAsync(h->mx_keys.p, keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice, h->xstream));
+        HIP_TRY(h, hipMemcpyAsync(h->mx_keys.p, keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice, h->pstream));
         if (ext->bytes_len)
-            HIP_TRY(h, hipMemcpyAsync(h->mx_ext[0].p, ext->bytes, ext->bytes_len, hipMemcpyHostToDevice, h->xstream));
-        HIP_TRY(h, hipMemcpyAsync(h->mx_ext[1].p, ext->offset, (size_t)n * 8, hipMemcpyHostToDevice, h->xstream));
-        HIP_TRY(h, hipMemcpyAsync(h->mx_ext[2].p, ext->length, (size_t)n * 4, hipMemcpyHostToDevice, h->xstream));
+            HIP_TRY(h, hipMemcpyAsync(h->mx_ext[0].p, ext->bytes, ext->bytes_len, hipMemcpyHostToDevice, h->pstream));
+        HIP_TRY(h, hipMemcpyAsync(h->mx_ext[1].p, ext->offset, (size_t)n * 8, hipMemcpyHostToDevice, h->pstream));
+        HIP_TRY(h, hipMemcpyAsync(h->mx_ext[2].p, ext->length, (size_t)n * 4, hipMemcpyHostToDevice, h->pstream));
     }
     const gd_key_ext dx{(const uint8_t*)h->mx_ext[0].p, (const uint64_t*)h->mx_ext[1].p,
                         (const int32_t*)h->mx_ext[2].p, ext->bytes_len};
