@@ -77,7 +77,12 @@ extern "C" {
 #define GD_ROUTE_KEYEXT         4 /* KeyExtGrain / GeoClient: the uniform hash needs the
                                      KeyExt string (UniqueKey.cs:279-281); C# handles it     */
 
+#define GD_ROUTE_MULTI_ACT      7 /* the grain has several activations (GrainInfo.Instances.Count >= 2,
+                                     e.g. StatelessWorker): RandomPlacementDirector picks one in C#
+                                     (RandomPlacementDirector.cs:33-53); out_silo = directory owner */
+
 #define GD_NO_ACTIVATION 0xFFFFFFFFu
+#define GD_ACT_MULTI     0xFFFFFFFEu   /* gd_val.act of a multi-activation grain (gd_dir_upsert)   */
 #define GD_NO_SILO       0xFFFFFFFFu
 
 /* UniqueKey fields (UniqueKey.cs:28-31) of a GrainId.  24 bytes, AoS. */
@@ -172,6 +177,12 @@ int gd_ring_lookup_hashes(gd_handle* h, const uint32_t* hashes, uint32_t n, uint
  * out_inserted 1 for the item that created the entry.  Host pointers. */
 int gd_dir_register(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t n,
                     gd_val* out_vals, uint8_t* out_inserted);
+/* Overwrite for a batch, applied in batch order (the last item of a grain wins): how the host
+ * mirrors GrainDirectoryPartition.AddActivation (GrainDirectoryPartition.cs:274-302; GrainInfo
+ * .AddActivation :89-108) for multi-instance grains: one instance -> {act, silo}, two or more ->
+ * {GD_ACT_MULTI, any silo} (routes then return GD_ROUTE_MULTI_ACT).  out_inserted[i] = 1 for the
+ * item that created a grain's entry (may be NULL).  Host pointers. */
+int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t n, uint8_t* out_inserted);
 /* RemoveActivation(grain, act) for a batch; out_removed may be NULL. */
 int gd_dir_unregister(gd_handle* h, const gd_key* keys, const uint32_t* acts, uint32_t n,
                       uint8_t* out_removed);

@@ -43,6 +43,8 @@ CAT_KEYEXT_GRAIN, CAT_GEO_CLIENT = 6, 7
 
 # Per-message routing status (the boundary's out_status codes, include/graindispatch.h)
 ST_OK, ST_MISS, ST_SYSTEM_TARGET, ST_MEMBERSHIP, ST_KEYEXT = 0, 1, 2, 3, 4
+ST_MULTI_ACT = 7               # several activations: the C# random selection (RandomPlacementDirector.cs:33-53)
+ACT_MULTI = 0xFFFFFFFE         # directory value of a multi-activation grain (gd_dir_upsert)
 
 # ---------------------------------------------------------------------------
 # L0: Jenkins hash   src/Orleans.Core.Abstractions/IDs/JenkinsHash.cs
@@ -488,6 +490,8 @@ def route_batch(keys: np.ndarray, spec: RingSpec, directory: Dict[Tuple[int, int
         v = directory.get(k)
         if v is None:
             status[i] = ST_MISS                               # Dispatcher.cs:742 slow path
+        elif v[0] == ACT_MULTI:
+            status[i] = ST_MULTI_ACT                          # RandomPlacementDirector.cs:33-53, in C#
         else:
             act[i], silo[i] = v
     return status, silo, act, owner, h
@@ -647,6 +651,12 @@ def route_batch_np(keys: np.ndarray, spec: RingSpec, directory: DirectoryArrays,
     found, act, dsilo = directory.lookup(keys)
     status = np.where(found, ST_OK, ST_MISS).astype(np.uint8)
     silo = np.where(found, dsilo, owner).astype(np.uint32)
+    # a grain with several activations (GrainInfo.Instances.Count >= 2): RandomPlacementDirector's
+    # random choice (RandomPlacementDirector.cs:33-53) is left to C#; the silo is the owner's
+    multi = found & (act == ACT_MULTI)
+    status[multi] = ST_MULTI_ACT
+    silo[multi] = owner[multi]
+    act = np.where(multi, M32, act).astype(np.uint32)
     mt = MEMBERSHIP_TABLE_ID
     is_mt = (n0 == np.uint64(mt.n0)) & (n1 == np.uint64(mt.n1)) & (tcd == np.uint64(mt.tcd))
     is_st = cat == CAT_SYSTEM_TARGET

@@ -123,9 +123,13 @@ __global__ void __launch_bounds__(BLOCK) k_route_cached(const gd_key* __restrict
             uint32_t a, meta;
             if (silo_flag(cache.local, cache.n_silos, owner)) {     // we own the grain (:806-821)
                 if (probe(tab.slots, tab.mask, max_probe, h, n0, n1, tcd, a, meta)) {
-                    act = a;
-                    silo = slot_silo(meta);
-                    status = GD_ROUTE_OK;
+                    if (a == GD_ACT_MULTI) {
+                        status = GD_ROUTE_MULTI_ACT;          // RandomPlacementDirector.cs:33-53, in C#
+                    } else {
+                        act = a;
+                        silo = slot_silo(meta);
+                        status = GD_ROUTE_OK;
+                    }
                 }
             } else {                                              // cache (:823-836)
                 access = true;

@@ -77,6 +77,7 @@ struct gd_handle {
     DevBuf cache_local, cache_valid;
     DevBuf cbuf[8];                   // cache scratch
     DevBuf shard_dest, shard_hist;    // exchange partition scratch
+    DevBuf up_last;                   // gd_dir_upsert: last batch item per table slot (zero between calls)
 
     // KeyExt grains (gd_keyext.h): device table + heap, and the host index both are kept from
     KxSlot* kx_slots = nullptr;
@@ -644,6 +645,7 @@ void gd_destroy(gd_handle* h) {
     free_buf(h->cache_local);
     free_buf(h->shard_dest);
     free_buf(h->shard_hist);
+    free_buf(h->up_last);
     comm_release(h);
     if (h->kx_slots) (void)hipFree(h->kx_slots);
     free_buf(h->kx_heap);
@@ -800,6 +802,51 @@ int gd_dir_register(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32
         const uint32_t e = h->ctr_host.err;
         HIP_TRY(h, hipMemsetAsync(&h->ctr->err, 0, sizeof(uint32_t), h->stream));
         return set_err(h, (e & 2) ? GD_EFULL : GD_ETIMEOUT, "gd_dir_register: device error bits 0x%x", e);
+    }
+    return GD_OK;
+}
+
+int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t n, uint8_t* out_inserted) {
+    if (!h || (n && (!keys || !vals))) return set_err(h, GD_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n; ++i)
+        if (vals[i].silo > 0xFFFEu) return set_err(h, GD_EINVAL, "silo index %u out of range at %u", vals[i].silo, i);
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(maybe_grow_table(h, n));
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(h2d(h, h->out_c, vals, n));            // gd_val staging
+    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));   // slot_of
+    GD_TRY(ensure(h, h->u8_a, (size_t)n));        // is_new
+    GD_TRY(ensure(h, h->out_b, (size_t)n));
+    if (h->up_last.bytes < h->capacity * 4) {     // one u32 per slot, kept zero between calls
+        GD_TRY(ensure(h, h->up_last, h->capacity * 4));
+        HIP_TRY(h, hipMemsetAsync(h->up_last.p, 0, h->up_last.bytes, h->stream));
+    }
+    HIP_TRY(h, hipMemsetAsync(h->u8_a.p, 0, n, h->stream));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    uint32_t* slot_of = (uint32_t*)h->u32_a.p;
+    uint8_t* is_new = (uint8_t*)h->u8_a.p;
+    uint32_t* last = (uint32_t*)h->up_last.p;
+    const gd_key* dk = (const gd_key*)h->keys_in.p;
+    const unsigned long long mask = h->capacity - 1;
+    for (uint32_t pass = 0;; ++pass) {            // the registration's claim protocol (k_reg_claim)
+        HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
+        GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
+                      (uint32_t)(pass > 0)));
+        GD_TRY(pull_counters(h));
+        if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
+        if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_upsert: claims did not settle");
+    }
+    GD_TRY(launch(h, "k_up_last", g, b, 0, k_up_last, (const uint32_t*)slot_of, n, last));
+    GD_TRY(launch(h, "k_up_apply", g, b, 0, k_up_apply, (const uint32_t*)slot_of, (const uint8_t*)is_new,
+                  (const gd_val*)h->out_c.p, n, (const uint32_t*)last, h->slots, h->ctr, (uint8_t*)h->out_b.p));
+    GD_TRY(launch(h, "k_up_clear", g, b, 0, k_up_clear, (const uint32_t*)slot_of, n, last));
+    if (out_inserted) GD_TRY(d2h(h, out_inserted, h->out_b, n));
+    GD_TRY(pull_counters(h));
+    if (h->ctr_host.err) {
+        const uint32_t e = h->ctr_host.err;
+        HIP_TRY(h, hipMemsetAsync(&h->ctr->err, 0, sizeof(uint32_t), h->stream));
+        return set_err(h, (e & 2) ? GD_EFULL : GD_ETIMEOUT, "gd_dir_upsert: device error bits 0x%x", e);
     }
     return GD_OK;
 }

@@ -184,8 +184,12 @@ __global__ void __launch_bounds__(BLOCK) k_route(const gd_key* __restrict__ keys
         if constexpr (PROBE) {
             uint32_t a, meta;
             if (probe(tab.slots, tab.mask, max_probe, h, n0, n1, tcd, a, meta)) {
-                act = a;
-                silo = slot_silo(meta);                    // ActivationAddress.Silo (Message.cs:629-639)
+                if (a == GD_ACT_MULTI) {
+                    status = GD_ROUTE_MULTI_ACT;           // RandomPlacementDirector.cs:33-53, in C#
+                } else {
+                    act = a;
+                    silo = slot_silo(meta);                // ActivationAddress.Silo (Message.cs:629-639)
+                }
             } else {
                 status = GD_ROUTE_MISS;                    // Dispatcher.cs:742 slow path
             }
@@ -286,9 +290,13 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
             const uint64_t k1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
             const uint64_t k2 = (uint64_t)b.x | ((uint64_t)b.y << 32);
             if (stt == SLOT_LIVE && k0 == n0[j] && k1 == n1[j] && k2 == tcd[j]) {
-                act[j] = b.z;
-                silo[j] = slot_silo(b.w);                     // ActivationAddress.Silo (Message.cs:629-639)
-                status[j] = GD_ROUTE_OK;
+                if (b.z == GD_ACT_MULTI) {                    // several activations: the C# random
+                    status[j] = GD_ROUTE_MULTI_ACT;           // choice (RandomPlacementDirector.cs:33-53)
+                } else {
+                    act[j] = b.z;
+                    silo[j] = slot_silo(b.w);                 // ActivationAddress.Silo (Message.cs:629-639)
+                    status[j] = GD_ROUTE_OK;
+                }
                 break;
             }
             if (++p > max_probe) break;                        // miss: Dispatcher.cs:742 slow path
@@ -419,6 +427,39 @@ __global__ void __launch_bounds__(BLOCK) k_reg_commit(const uint32_t* __restrict
     sl.act = vals[i].act;
     sl.meta = make_meta(SLOT_LIVE, vals[i].silo);
     atomicAdd(&ctr->live, 1ull);
+}
+
+// gd_dir_upsert: the last batch item of each slot wins (batch order), then writes its value.
+// `last` (one u32 per table slot, zero between calls) holds 1 + the winning index.
+__global__ void __launch_bounds__(BLOCK) k_up_last(const uint32_t* __restrict__ slot_of, uint32_t n,
+                                                   uint32_t* __restrict__ last) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n || slot_of[i] >= SLOT_RETRY) return;
+    atomicMax(&last[slot_of[i]], i + 1);
+}
+__global__ void __launch_bounds__(BLOCK) k_up_apply(const uint32_t* __restrict__ slot_of,
+                                                    const uint8_t* __restrict__ is_new, const gd_val* __restrict__ vals,
+                                                    uint32_t n, const uint32_t* __restrict__ last, Slot* slots,
+                                                    DevCounters* ctr, uint8_t* __restrict__ out_inserted) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slot_of[i];
+    uint8_t ins = 0;
+    if (s < SLOT_RETRY && last[s] == i + 1) {
+        Slot& sl = slots[s];
+        sl.act = vals[i].act;
+        sl.meta = make_meta(SLOT_LIVE, vals[i].silo);
+        if (is_new[i]) {
+            atomicAdd(&ctr->live, 1ull);
+            ins = 1;
+        }
+    }
+    out_inserted[i] = ins;
+}
+__global__ void __launch_bounds__(BLOCK) k_up_clear(const uint32_t* __restrict__ slot_of, uint32_t n,
+                                                    uint32_t* __restrict__ last) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n && slot_of[i] < SLOT_RETRY) last[slot_of[i]] = 0;
 }
 
 __global__ void __launch_bounds__(BLOCK) k_reg_report(const uint32_t* __restrict__ slot_of,

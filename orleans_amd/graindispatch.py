@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = [
     "gd_dir_ext_stats", "gd_route_ext", "gd_route_bucket_ext", "gd_route_ext_device", "gd_route_bucket_ext_device",
     "gd_comm_unique_id", "gd_comm_init", "gd_comm_destroy", "gd_route_multi_device", "gd_route_multi",
     "gd_multi_fetch", "gd_route_multi_ext_device", "gd_route_multi_ext", "gd_ring_owner_ext",
-    "gd_dir_split_ext",
+    "gd_dir_split_ext", "gd_dir_upsert",
 ]
 
 
@@ -106,6 +106,8 @@ class gd_multi_result(C.Structure):
 
 
 GD_COMM_ID_BYTES = 128
+GD_ACT_MULTI = 0xFFFFFFFE
+GD_ROUTE_MULTI_ACT = 7
 GD_KEYEXT_NULL = -1
 GD_KEYEXT_HOST = -2
 
@@ -183,6 +185,7 @@ def _load() -> C.CDLL:
         "gd_ring_lookup_hashes": (C.c_int, [P, P, U32, P]),
         "gd_dir_register": (C.c_int, [P, P, P, U32, P, P]),
         "gd_dir_unregister": (C.c_int, [P, P, P, U32, P]),
+        "gd_dir_upsert": (C.c_int, [P, P, P, U32, P]),
         "gd_dir_lookup": (C.c_int, [P, P, U32, P, P]),
         "gd_dir_clear": (C.c_int, [P]),
         "gd_dir_rehash": (C.c_int, [P, U64]),
@@ -403,6 +406,17 @@ class GrainDispatch:
         ins = np.zeros(n, dtype=np.uint8)
         self._c(lib.gd_dir_register(self.h, _ptr(k), _ptr(vals), n, _ptr(out), _ptr(ins)))
         return out[:, 0].copy(), out[:, 1].copy(), ins
+
+    def upsert(self, keys, acts, silos) -> np.ndarray:
+        """gd_dir_upsert: overwrite, the last item of a grain wins; acts may hold GD_ACT_MULTI."""
+        k = keys_array(keys)
+        n = len(k)
+        vals = np.zeros((n, 2), dtype=np.uint32)
+        vals[:, 0] = acts
+        vals[:, 1] = silos
+        ins = np.zeros(n, dtype=np.uint8)
+        self._c(lib.gd_dir_upsert(self.h, _ptr(k), _ptr(vals), n, _ptr(ins)))
+        return ins
 
     def unregister(self, keys, acts) -> np.ndarray:
         k = keys_array(keys)

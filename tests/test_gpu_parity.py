@@ -737,3 +737,51 @@ def test_pack_by_shard_vs_oracle(gd, n):
         np.testing.assert_array_equal(sk.cpu().numpy().view(np.uint64).reshape(-1, 3), keys[perm])
         np.testing.assert_array_equal(cnt.cpu().numpy(), np.diff(off[:shards + 1]))
     e.close()
+
+
+@pytest.mark.parametrize("mode", ["D", "V"])
+def test_upsert_and_multi_activation_grains(gd, mode):
+    """gd_dir_upsert (the host's mirror of GrainDirectoryPartition.AddActivation for multi-instance
+    grains, GrainDirectoryPartition.cs:274-302): overwrite in batch order (the last item of a grain
+    wins); a grain marked GD_ACT_MULTI routes as GD_ROUTE_MULTI_ACT with the owner silo, no
+    activation, trailing bucket (RandomPlacementDirector.cs:33-53 stays in C#)."""
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, mode)
+    e = _engine(gd, silos, mode, cap=1 << 13, my_silo=2)
+    G = 2000
+    reg = o.grain_keys(TC, np.arange(G))
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    e.register(reg[:1000], np.arange(1000), own[:1000])               # first-wins registrations
+    final = {tuple(int(x) for x in reg[i]): (i, int(own[i])) for i in range(1000)}
+    rng = np.random.default_rng(4)
+    idx = rng.integers(0, G, size=6000)                                 # many duplicates, old and new grains
+    acts = rng.integers(0, 50000, size=6000).astype(np.uint32)
+    acts[rng.random(6000) < 0.2] = gd.GD_ACT_MULTI
+    ss = rng.integers(0, 8, size=6000).astype(np.uint32)
+    before = e.stats()["table_live"]
+    ins = e.upsert(reg[idx], acts, ss)
+    new_keys = set()
+    for j, i in enumerate(idx):
+        k = tuple(int(x) for x in reg[i])
+        if k not in final:
+            new_keys.add(k)
+        final[k] = (int(acts[j]), int(ss[j]))
+    assert e.stats()["table_live"] == before + len(new_keys)
+    assert int(ins.sum()) == len(new_keys)
+    fk = np.array(list(final.keys()), dtype=np.uint64)
+    d = o.DirectoryArrays(fk, [v[0] for v in final.values()], [v[1] for v in final.values()])
+    msgs = o.grain_keys(TC, rng.integers(0, G + 100, size=50000))
+    st, silo, act, perm, off = e.route_bucket(msgs, 50000)
+    wst, wsilo, wact, _, _ = o.route_batch_np(msgs, spec, d, my_silo=2)
+    np.testing.assert_array_equal(st, wst)
+    np.testing.assert_array_equal(silo, wsilo)
+    np.testing.assert_array_equal(act, wact)
+    assert (wst == o.ST_MULTI_ACT).sum() > 1000
+    wp, wo = o.bucket_stable(wact, 50000)
+    np.testing.assert_array_equal(perm, wp)
+    np.testing.assert_array_equal(off, wo)
+    # the scalar restatement agrees on the multi-activation rule
+    st2, silo2, act2, _, _ = o.route_batch(msgs[:3000], spec, final, 2, o.M32)
+    np.testing.assert_array_equal(st2, wst[:3000])
+    np.testing.assert_array_equal(act2, wact[:3000])
+    e.close()
