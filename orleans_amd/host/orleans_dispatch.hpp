@@ -406,8 +406,41 @@ public:
         return r;
     }
 
+    // AddActivation (GrainDirectoryPartition.cs:274-302; GrainInfo.AddActivation :89-108): multi-
+    // instance grains (StatelessWorker).  The instances live here; the GPU table holds the lookup
+    // result -- the single instance, or GD_ACT_MULTI once there are two or more (routes then answer
+    // GD_ROUTE_MULTI_ACT and the random choice of RandomPlacementDirector.cs:33-53 stays on the host).
+    // Returns false when the activation was already registered on that silo (a refresh).
+    bool AddActivation(const GrainId& grain, const ActivationId& act, const SiloAddress& silo) {
+        auto& inst = multi_[grain];
+        const auto it = inst.find(act);
+        if (it != inst.end() && it->second == silo) return false;
+        inst[act] = silo;
+        ActIndex(act);
+        Publish(grain, inst);
+        return true;
+    }
+
     // RemoveActivation (GrainDirectoryPartition.cs:335-363, UnregistrationCause.Force)
     bool RemoveActivation(const GrainId& grain, const ActivationId& act) {
+        const auto mit = multi_.find(grain);
+        if (mit != multi_.end()) {                     // a multi-instance grain: update its GPU entry
+            if (!mit->second.erase(act)) return false;
+            if (mit->second.empty()) {
+                const gd_key k = grain.Key.ToNative();
+                const uint32_t a = GD_ACT_MULTI;
+                uint8_t removed = 0;
+                Check(h_, gd_dir_unregister(h_, &k, &a, 1, &removed));
+                if (!removed) {                        // the entry held the last single instance
+                    const uint32_t a1 = ActIndex(act);
+                    Check(h_, gd_dir_unregister(h_, &k, &a1, 1, &removed));
+                }
+                multi_.erase(mit);
+            } else {
+                Publish(grain, mit->second);
+            }
+            return true;
+        }
         const auto it = act_index_.find(act);
         if (it == act_index_.end()) return false;
         const gd_key k = grain.Key.ToNative();
@@ -434,7 +467,13 @@ public:
             Check(h_, gd_dir_lookup(h_, &k, 1, &v, &found));
         }
         AddressesAndTag r;
-        if (found) r.Addresses = std::vector<ActivationAddress>{{silos_.At(v.silo), grain, acts_.at(v.act)}};
+        if (found && v.act == GD_ACT_MULTI) {          // every instance, from the host's list
+            std::vector<ActivationAddress> all;
+            for (const auto& kv : multi_.at(grain)) all.push_back(ActivationAddress{kv.second, grain, kv.first});
+            r.Addresses = std::move(all);
+        } else if (found) {
+            r.Addresses = std::vector<ActivationAddress>{{silos_.At(v.silo), grain, acts_.at(v.act)}};
+        }
         return r;
     }
 
@@ -456,10 +495,18 @@ public:
     size_t ActivationCount() const { return acts_.size(); }
 
 private:
+    void Publish(const GrainId& grain, const std::map<ActivationId, SiloAddress>& inst) {
+        const gd_key k = grain.Key.ToNative();
+        const auto& first = *inst.begin();
+        const gd_val v{inst.size() == 1 ? ActIndex(first.first) : GD_ACT_MULTI, silos_.IndexOf(first.second)};
+        Check(h_, gd_dir_upsert(h_, &k, &v, 1, nullptr));
+    }
+
     gd_handle* h_;
     SiloTable& silos_;
     std::vector<ActivationId> acts_;
     std::map<ActivationId, uint32_t> act_index_;
+    std::map<GrainId, std::map<ActivationId, SiloAddress>> multi_;   // AddActivation grains
 };
 
 // AdaptiveGrainDirectoryCache<IReadOnlyList<Tuple<SiloAddress, ActivationId>>> for
@@ -674,7 +721,8 @@ struct Message {                       // the header fields the path reads/write
 
 // Batched Dispatcher.AddressMessage (Dispatcher.cs:715-767): messages whose TargetAddress is
 // complete are skipped (:718); the rest get SetTargetPlacement (Message.cs:629-639) on a hit.
-// Returns the indices that stay on the C# slow path (MISS, system target, membership grain).
+// Returns the indices that stay on the C# slow path (MISS, system target, membership grain, and
+// multi-activation grains, whose random choice is RandomPlacementDirector's).
 class Dispatcher {
 public:
     explicit Dispatcher(LocalGrainDirectory& dir) : dir_(dir) {}

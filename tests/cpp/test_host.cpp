@@ -375,6 +375,36 @@ static void StringKeyGrains() {
     EXPECT(part.Count() == 400);
 }
 
+// Multi-instance grains (GrainDirectoryPartition.AddActivation, GrainInfo.AddActivation :89-108).
+static void MultiActivationGrains() {
+    DispatchHandle h(0, 4096, 0);
+    const SiloAddress me = SiloAddress::New(10, 0, 0, 1, 11111, 1);
+    LocalGrainDirectory dir(h.get(), me);
+    for (int i = 2; i <= 4; ++i) dir.AddServer(SiloAddress::New(10, 0, 0, (uint8_t)i, 11111, 1));
+    auto& part = dir.DirectoryPartition();
+    const int tc = gd_calculate_id_hash("UnitTests.Grains.StatelessWorkerGrain");
+    const GrainId g = GrainId::GetGrainId(tc, 5);
+    const SiloAddress s2 = SiloAddress::New(10, 0, 0, 2, 11111, 1), s3 = SiloAddress::New(10, 0, 0, 3, 11111, 1);
+    const ActivationId a1 = NewActivationId(71), a2 = NewActivationId(72);
+    EXPECT(part.AddActivation(g, a1, s2));
+    EXPECT(!part.AddActivation(g, a1, s2));                         // refresh: same silo
+    std::vector<Message> m{Message{g, {}, {}, 0xFF}};
+    Dispatcher disp(dir);
+    EXPECT(disp.AddressMessages(m).empty() && m[0].RouteStatus == GD_ROUTE_OK && *m[0].TargetActivation == a1);
+    EXPECT(part.AddActivation(g, a2, s3));                          // a second instance
+    m = {Message{g, {}, {}, 0xFF}};
+    const auto slow = disp.AddressMessages(m);
+    EXPECT(slow.size() == 1 && m[0].RouteStatus == GD_ROUTE_MULTI_ACT && !m[0].TargetActivation);
+    EXPECT(!m[0].TargetSilo);                                       // the host picks the instance
+    AddressesAndTag res;
+    EXPECT(dir.LocalLookup(g, res) && res.Addresses->size() == 2);
+    EXPECT(part.RemoveActivation(g, a1));                          // back to one instance
+    m = {Message{g, {}, {}, 0xFF}};
+    EXPECT(disp.AddressMessages(m).empty() && *m[0].TargetActivation == a2 && *m[0].TargetSilo == s3);
+    EXPECT(part.RemoveActivation(g, a2));
+    EXPECT(!dir.LocalLookup(g, res));
+}
+
 // ---------------------------------------------------------------- LruTest.cs (test/NonSilo.Tests/General)
 // The reference's LRU tests, restated against the GPU directory cache (AdaptiveGrainDirectoryCache
 // over LRU); keys "1".."n" become grains 1..n of one type.
@@ -497,6 +527,7 @@ int main(int argc, char** argv) {
         Run("DirectorySemantics", DirectorySemantics);
         Run("DispatcherAndAgent", DispatcherAndAgent);
         Run("StringKeyGrains", StringKeyGrains);
+        Run("MultiActivationGrains", MultiActivationGrains);
         Run("LruCountTest", LruCountTest);
         Run("LruMaximumSizeTest", LruMaximumSizeTest);
         Run("LruUsageTest", LruUsageTest);

@@ -33,7 +33,7 @@ def test_host_cpp_gpu(tmp_path):
     p = subprocess.run([BIN, "all", str(dump)], capture_output=True, text=True, timeout=150)
     assert p.returncode == 0, p.stdout + p.stderr
     for name in ("RingStandalone_Basic", "RingStandalone_Failures", "RingStandalone_Joins", "RingStandalone_Mixed",
-                 "VirtualBucketsRanges", "DirectorySemantics", "DispatcherAndAgent", "StringKeyGrains", "LruCountTest",
+                 "VirtualBucketsRanges", "DirectorySemantics", "DispatcherAndAgent", "StringKeyGrains", "MultiActivationGrains", "LruCountTest",
                  "LruMaximumSizeTest", "LruUsageTest", "PerSiloLocalLookup", "RoutingDump"):
         assert f"PASS {name}" in p.stdout, p.stdout + p.stderr
     rows = np.loadtxt(dump, dtype=np.int64)
