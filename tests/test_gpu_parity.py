@@ -785,3 +785,55 @@ def test_upsert_and_multi_activation_grains(gd, mode):
     np.testing.assert_array_equal(st2, wst[:3000])
     np.testing.assert_array_equal(act2, wact[:3000])
     e.close()
+
+
+def test_randomized_configurations(gd):
+    """Random shapes through route + bucket against the oracle: ring modes and sizes (1..70 silos,
+    V-ring bucket counts), table capacities far below the grain count (growth/rehash), n_act
+    around powers of two (radix digit widths and pass counts change there), unregistered and
+    special-category keys, empty, tiny and tile-straddling batches."""
+    rng = np.random.default_rng(20261016)
+    special = _special_keys()
+    for trial in range(24):
+        mode = "DRV"[trial % 3]
+        n_silos = int(rng.choice([1, 2, 3, 8, 13, 70]))
+        silos = [o.Silo(f"10.{trial}.{i // 200}.{i % 200 + 1}", 11111 + i % 7, 1 + int(rng.integers(0, 9)))
+                 for i in range(n_silos)]
+        buckets = int(rng.choice([1, 3, 30]))
+        spec = o.ring_spec(silos, mode, buckets)
+        G = int(rng.choice([1, 17, 255, 256, 257, 4095, 4097, 65535, 65537]))
+        n_act = G + int(rng.integers(0, 3))
+        my_silo, seed_silo = int(rng.integers(0, n_silos)), int(rng.integers(0, n_silos))
+        e = gd.GrainDispatch(device=0, table_capacity=int(rng.choice([16, 1024, 1 << 17])),
+                             my_silo=my_silo, seed_silo=seed_silo)
+        e.ring_set_silos(mode, _silo_tuples(silos), buckets)
+        reg = o.grain_keys(TC, rng.permutation(G * 3)[:G])
+        own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+        acts = rng.permutation(n_act)[:G].astype(np.uint32)
+        e.register(reg, acts, own)
+        n = int(rng.choice([0, 1, 63, 64, 4095, 4096, 4097, 100000]))
+        pick = rng.integers(0, G + max(1, G // 4), size=n)
+        keys = np.where((pick < G)[:, None], reg[np.minimum(pick, G - 1)], o.grain_keys(TC, G * 3 + pick))
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        if n > 64:
+            keys[5::31] = special[rng.integers(0, len(special), size=len(keys[5::31]))]
+        st, silo, act, perm, off = e.route_bucket(keys, n_act)
+        d = o.DirectoryArrays(reg, acts, own)
+        wst, wsilo, wact, _, _ = o.route_batch_np(keys, spec, d, my_silo=my_silo, seed_silo=seed_silo)
+        msg = f"trial {trial}: mode {mode} silos {n_silos} G {G} n_act {n_act} n {n}"
+        np.testing.assert_array_equal(st, wst, err_msg=msg)
+        np.testing.assert_array_equal(silo, wsilo, err_msg=msg)
+        np.testing.assert_array_equal(act, wact, err_msg=msg)
+        wp, wo = o.bucket_stable(wact, n_act)
+        np.testing.assert_array_equal(perm, wp, err_msg=msg)
+        np.testing.assert_array_equal(off, wo, err_msg=msg)
+        if 0 < n <= 4096:                                   # the hipGraph micro-batch path too
+            mb = gd.MicroBatch(e, 4096, n_act)
+            mb.keys[:n] = keys
+            mb.run(n, use_graph=bool(trial & 1))
+            np.testing.assert_array_equal(mb.status[:n], wst, err_msg=msg)
+            np.testing.assert_array_equal(mb.act[:n], wact, err_msg=msg)
+            np.testing.assert_array_equal(mb.perm[:n], wp, err_msg=msg)
+            np.testing.assert_array_equal(mb.offsets(), wo, err_msg=msg)
+            mb.close()
+        e.close()
