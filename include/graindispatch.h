@@ -274,6 +274,15 @@ int gd_ring_owner_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_
  * message counts to d_counts[n_shards].  Device pointers; n_shards <= 256. */
 int gd_pack_by_shard_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_shards,
                             gd_key* d_send_keys, uint32_t* d_send_idx, uint32_t* d_counts);
+/* The second hop when the directory owner is not the activation's silo (ActivationAddress.Silo,
+ * the send after a remote lookup, LocalGrainDirectory.cs:920 -> OutboundMessageQueue.cs:125):
+ * stable partition of routed messages by the rank hosting their activation -- status
+ * GD_ROUTE_OK: d_silo[i] % n_shards; any other status: my_rank (the message stays on the owner).
+ * Writes the keys in rank order to d_send_keys, each message's input position to d_send_pos and
+ * per-rank counts to d_counts[n_shards].  Device pointers; n_shards <= 256. */
+int gd_pack_routes_by_rank_device(gd_handle* h, const gd_key* d_keys, const uint8_t* d_status,
+                                  const uint32_t* d_silo, uint32_t n, uint32_t n_shards, uint32_t my_rank,
+                                  gd_key* d_send_keys, uint32_t* d_send_pos, uint32_t* d_counts);
 
 /* ---- in-library exchange over RCCL (SURVEY 8 b gd_route_multi, 8 e) ------------------
  * One process (one handle) per GPU.  Rank r hosts the directory partitions of silos
@@ -323,6 +332,16 @@ typedef struct gd_multi_result {
  * Blocks the host once per call, on the per-rank counts round (it sizes the receive). */
 #define GD_MULTI_RETURN_ROUTES 1
 #define GD_MULTI_KEYS_READY    2
+/* GD_MULTI_FORWARD -- the directory owner is not the activation's silo in general (Orleans
+ *        co-locates neither; ActivationAddress.Silo): after the probe on the owner, directory hits
+ *        travel on to the rank hosting their activation (silo % n_ranks, a second grouped round,
+ *        gd_pack_routes_by_rank_device) and are bucketed there; every other status stays on the
+ *        owner.  The result then describes the messages delivered to this rank: recv_idx / recv_src
+ *        still name the original sender, silo / act / status are the owner's routes, and each
+ *        activation's messages keep (sender rank, sender batch order).  A second host sync (the
+ *        forward counts) per call.  Combines with GD_MULTI_RETURN_ROUTES (routes go back from the
+ *        owner). */
+#define GD_MULTI_FORWARD       4
 int gd_route_multi_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int flags,
                           gd_multi_result* out);
 /* Host keys in (C# pinned array), copied on the exchange stream; returns with the batch done

@@ -98,17 +98,21 @@ struct gd_handle {
     hipStream_t xstream = nullptr;
     hipStream_t pstream = nullptr;    // the partition (pack) of the next batch, beside this one's rounds
     hipEvent_t x_in = nullptr, x_hdr[2] = {}, x_route[2] = {}, x_ret[2] = {}, x_done[2] = {};
-    hipEvent_t p_packed = nullptr, x_sent[2] = {};
+    hipEvent_t p_packed = nullptr, x_sent[2] = {}, x_fwd[2] = {};
     bool x_done_rec[2] = {false, false}, x_sent_rec[2] = {false, false};
     DevBuf mx_send[2][6];             // per batch parity: send keys, send idx, counts (send/recv messages,
                                       // send/recv KeyExt bytes: 4 x [W]), KeyExt lengths, KeyExt byte
                                       // offsets, KeyExt blob
     DevBuf mx[2][20];                 // per batch parity: receive / result buffers
+    DevBuf mf[2][16];                 // per batch parity, GD_MULTI_FORWARD: forward send (keys, pos, idx,
+                                      // src, silo, act, status, counts), forward receive (keys, idx, src,
+                                      // silo, act, status), perm, offsets
     DevBuf mx_keys;                   // host-keys entry point: the batch, on xstream
     DevBuf mx_ext[3];                 // host-keys entry point: its KeyExt blob, offsets, lengths
     DevBuf x_scratch[4];              // xstream's own scan partials + partition scratch
     DevBuf p_scratch[4];              // pstream's
-    uint32_t* h_xcnt = nullptr;       // pinned: send/recv message counts, send/recv KeyExt byte counts
+    uint32_t* h_xcnt = nullptr;       // pinned: send/recv message counts, send/recv KeyExt byte counts,
+                                      // send/recv forward counts (6 x 256)
     gd_multi_result mres[2] = {};
     uint32_t mres_n[2] = {0, 0};
     uint64_t mcalls = 0;
@@ -524,6 +528,11 @@ int shard_scatter_t(gd_handle* h, const void* recs, const uint32_t* payload, con
                   n, n_shards, tiles, gscan, out, out_pay);
 }
 
+template <bool NODES>
+int shard_finish(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t n, uint32_t n_shards, uint32_t bits,
+                 uint32_t tiles, const uint8_t* dest, uint32_t* hist, void* out_recs, uint32_t* out_pay,
+                 uint32_t* counts);
+
 // Stable partition of n records (gd_key or u32 node ids) by destination rank, payload alongside
 // (payload == nullptr: the batch index); counts[d] per destination.
 template <bool NODES>
@@ -550,6 +559,32 @@ int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t
         default:
             GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext)));
     }
+    return shard_finish<NODES>(h, recs, payload, n, n_shards, bits, tiles, dest, hist, out_recs, out_pay, counts);
+}
+
+// Forward partition of routed messages by the rank hosting their activation (k_fwd_hist): keys
+// move, out_pos[j] = the message's position in the input.
+int fwd_pack(gd_handle* h, const gd_key* keys, const uint8_t* st, const uint32_t* silo, uint32_t n, uint32_t n_shards,
+             uint32_t my_rank, gd_key* out_keys, uint32_t* out_pos, uint32_t* counts) {
+    if (n == 0)
+        return launch(h, "k_fill", dim3(1), dim3(BLOCK), 0, k_fill_u32, counts, n_shards, 0u);
+    const uint32_t tiles = blocks_for(n, SH_TILE);
+    if ((uint64_t)tiles * n_shards > 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "batch too large to partition");
+    GD_TRY(ensure(h, h->shard_dest, (size_t)n));
+    GD_TRY(ensure(h, h->shard_hist, (size_t)tiles * n_shards * 4));
+    uint8_t* dest = (uint8_t*)h->shard_dest.p;
+    uint32_t* hist = (uint32_t*)h->shard_hist.p;
+    uint32_t bits = 1;
+    while ((1u << bits) < n_shards) ++bits;
+    GD_TRY(launch(h, "k_fwd_hist", dim3(tiles), dim3(SH_NT), 0, k_fwd_hist, st, silo, n, n_shards, my_rank, bits, tiles,
+                  dest, hist));
+    return shard_finish<false>(h, keys, nullptr, n, n_shards, bits, tiles, dest, hist, out_keys, out_pos, counts);
+}
+
+template <bool NODES>
+int shard_finish(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t n, uint32_t n_shards, uint32_t bits,
+                 uint32_t tiles, const uint8_t* dest, uint32_t* hist, void* out_recs, uint32_t* out_pay,
+                 uint32_t* counts) {
     GD_TRY(scan_device<OpAdd>(h, hist, tiles * n_shards, false, false, "shard"));
     GD_TRY(launch(h, "k_shard_counts", dim3(1), dim3(256), 0, k_shard_counts, (const uint32_t*)hist, tiles, n_shards, n,
                   counts));
@@ -1002,6 +1037,16 @@ int gd_pack_by_shard_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint
     if (!h || !d_counts || (n && (!d_keys || !d_send_keys || !d_send_idx))) return set_err(h, GD_EINVAL, "null argument");
     if (n_shards == 0 || n_shards > 256) return set_err(h, GD_EINVAL, "n_shards %u not in [1, 256]", n_shards);
     return shard_pack<false>(h, d_keys, nullptr, n, 0, n_shards, d_send_keys, d_send_idx, d_counts);
+}
+
+int gd_pack_routes_by_rank_device(gd_handle* h, const gd_key* d_keys, const uint8_t* d_status, const uint32_t* d_silo,
+                                  uint32_t n, uint32_t n_shards, uint32_t my_rank, gd_key* d_send_keys,
+                                  uint32_t* d_send_pos, uint32_t* d_counts) {
+    if (!h || !d_counts || (n && (!d_keys || !d_status || !d_silo || !d_send_keys || !d_send_pos)))
+        return set_err(h, GD_EINVAL, "null argument");
+    if (n_shards == 0 || n_shards > 256 || my_rank >= n_shards)
+        return set_err(h, GD_EINVAL, "n_shards %u not in [1, 256] or my_rank %u >= n_shards", n_shards, my_rank);
+    return fwd_pack(h, d_keys, d_status, d_silo, n, n_shards, my_rank, d_send_keys, d_send_pos, d_counts);
 }
 
 int gd_kernel_times(gd_handle* h, gd_kernel_time* out, uint32_t max, uint32_t* out_n) {
@@ -2170,7 +2215,7 @@ void comm_release(gd_handle* h) {
     if (h->comm) (void)rccl().CommDestroy(h->comm);
     h->comm = nullptr;
     for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
-                          &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1]})
+                          &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1], &h->x_fwd[0], &h->x_fwd[1]})
         if (*e) {
             (void)hipEventDestroy(*e);
             *e = nullptr;
@@ -2183,6 +2228,8 @@ void comm_release(gd_handle* h) {
         for (DevBuf& b : par) free_buf(b);
     for (DevBuf& b : h->p_scratch) free_buf(b);
     for (auto& slot : h->mx)
+        for (DevBuf& b : slot) free_buf(b);
+    for (auto& slot : h->mf)
         for (DevBuf& b : slot) free_buf(b);
     free_buf(h->mx_keys);
     for (DevBuf& b : h->mx_ext) free_buf(b);
@@ -2252,6 +2299,81 @@ int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uin
     return GD_OK;
 }
 
+// GD_MULTI_FORWARD: the second hop, owner -> the rank hosting the activation (SURVEY 8 e caveat;
+// the send to ActivationAddress.Silo after a remote lookup, LocalGrainDirectory.cs:920,
+// OutboundMessageQueue.cs:125).  Directory hits go to silo % W with their route, origin index and
+// origin rank; every other status stays here.  All messages of one grain pass through its one
+// owner, so each activation's arrival order stays (sender rank, sender batch order).  r holds the
+// owner's routes on entry (probe enqueued, x_route[s] recorded) and the forwarded result on exit.
+int forward_multi(gd_handle* h, int s, uint32_t n_act, gd_multi_result& r) {
+    const int W = h->n_ranks;
+    const Rccl& R = rccl();
+    const uint32_t m = r.n_recv;
+    DevBuf* F = h->mf[s];
+    const size_t m4 = (size_t)m * 4 + 4;
+    const size_t want_s[8] = {(size_t)m * sizeof(gd_key) + 8, m4, m4, m4, m4, m4, (size_t)m + 4, (size_t)W * 8};
+    for (int b = 0; b < 8; ++b) GD_TRY(grow(h, F[b], want_s[b]));
+    uint32_t* fcnt = (uint32_t*)F[7].p;           // send [0,W), recv [W,2W)
+    uint32_t* hc = h->h_xcnt + 4 * 256;
+    HIP_TRY(h, hipStreamWaitEvent(h->xstream, h->x_route[s], 0));
+    {
+        OnXStream on(h);
+        GD_TRY(fwd_pack(h, r.recv_keys, r.status, r.silo, m, (uint32_t)W, (uint32_t)h->rank, (gd_key*)F[0].p,
+                        (uint32_t*)F[1].p, fcnt));
+        if (m)
+            GD_TRY(launch(h, "k_fwd_gather", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_fwd_gather,
+                          (const uint32_t*)F[1].p, m, r.recv_idx, r.recv_src, r.silo, r.act, r.status,
+                          (uint32_t*)F[2].p, (uint32_t*)F[3].p, (uint32_t*)F[4].p, (uint32_t*)F[5].p,
+                          (uint8_t*)F[6].p));
+        NCCL_TRY(h, R.GroupStart());
+        for (int q = 0; q < W; ++q) {
+            NCCL_TRY(h, R.Send(fcnt + q, 1, ncclUint32, q, h->comm, h->stream));
+            NCCL_TRY(h, R.Recv(fcnt + W + q, 1, ncclUint32, q, h->comm, h->stream));
+        }
+        NCCL_TRY(h, R.GroupEnd());
+        HIP_TRY(h, hipMemcpyAsync(hc, fcnt, (size_t)W * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+    }
+    std::vector<uint32_t> sc(hc, hc + W), rc(hc + W, hc + 2 * W);
+    std::vector<uint64_t> soff(W + 1, 0), roff(W + 1, 0);
+    for (int q = 0; q < W; ++q) {
+        soff[q + 1] = soff[q] + sc[q];
+        roff[q + 1] = roff[q] + rc[q];
+    }
+    if (soff[W] != m)
+        return set_err(h, GD_ERCCL, "forward counts sum to %llu, %u messages here", (unsigned long long)soff[W], m);
+    if (roff[W] >= 0xFFFFFFFFull)
+        return set_err(h, GD_EINVAL, "%llu forwarded messages: more than a batch can hold", (unsigned long long)roff[W]);
+    const uint32_t m2 = (uint32_t)roff[W];
+    const size_t q4 = (size_t)m2 * 4 + 4;
+    const size_t want_r[8] = {(size_t)m2 * sizeof(gd_key) + 8, q4, q4, q4, q4, (size_t)m2 + 4, q4,
+                              ((size_t)n_act + 2) * 4};
+    for (int b = 0; b < 8; ++b) GD_TRY(grow(h, F[8 + b], want_r[b]));
+    {
+        OnXStream on(h);
+        const Lane lanes[6] = {{F[0].p, F[8].p, sizeof(gd_key), ncclUint64, 3},
+                               {F[2].p, F[9].p, 4, ncclUint32, 1},
+                               {F[3].p, F[10].p, 4, ncclUint32, 1},
+                               {F[4].p, F[11].p, 4, ncclUint32, 1},
+                               {F[5].p, F[12].p, 4, ncclUint32, 1},
+                               {F[6].p, F[13].p, 1, ncclUint8, 1}};
+        GD_TRY(exchange_round(h, "rccl_forward", sc.data(), soff.data(), rc.data(), roff.data(), lanes, 6));
+        HIP_TRY(h, hipEventRecord(h->x_fwd[s], h->xstream));
+    }
+    HIP_TRY(h, hipStreamWaitEvent(h->stream, h->x_fwd[s], 0));
+    GD_TRY(bucket_device(h, (const uint32_t*)F[12].p, m2, n_act, (uint32_t*)F[14].p, (uint32_t*)F[15].p));
+    r.n_recv = m2;
+    r.recv_keys = (const gd_key*)F[8].p;
+    r.recv_idx = (const uint32_t*)F[9].p;
+    r.recv_src = (const uint32_t*)F[10].p;
+    r.silo = (const uint32_t*)F[11].p;
+    r.act = (const uint32_t*)F[12].p;
+    r.status = (const uint8_t*)F[13].p;
+    r.perm = (const uint32_t*)F[14].p;
+    r.offsets = (const uint32_t*)F[15].p;
+    return GD_OK;
+}
+
 // Sender batch d_keys[n] -> owner ranks (exchange) -> probe + bucket there (-> routes back).
 //   xstream: [wait caller] partition, counts round, (host: sizes) header round, recv_src
 //   stream:  [wait headers] probe, bucket
@@ -2268,6 +2390,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     const int s = (int)(h->mcalls & 1);
     DevBuf* B = h->mx[s];
     const bool ret = (flags & GD_MULTI_RETURN_ROUTES) != 0;
+    const bool fwd = (flags & GD_MULTI_FORWARD) != 0;
     const bool has_ext = ext && n && !h->cache_max;      // KeyExt strings travel with their messages
     const ExtArgs x = has_ext ? ExtArgs{ext->bytes, ext->offset, ext->length, ext->bytes_len} : ExtArgs{};
     DevBuf* SB = h->mx_send[s];
@@ -2395,7 +2518,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
                                    rboff[W]},
                            m, silo, act, st));
     HIP_TRY(h, hipEventRecord(h->x_route[s], h->stream));
-    GD_TRY(bucket_device(h, act, m, n_act, perm, offs));
+    if (!fwd) GD_TRY(bucket_device(h, act, m, n_act, perm, offs));
     // 4. routes back to the senders, into their batch order (Dispatcher.AddressMessage)
     gd_multi_result r{};
     if (ret) {
@@ -2418,8 +2541,6 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         r.ret_act = (const uint32_t*)B[12].p;
         r.ret_status = (const uint8_t*)B[13].p;
     }
-    HIP_TRY(h, hipEventRecord(h->x_done[s], h->stream));
-    h->x_done_rec[s] = true;
     r.n_recv = m;
     r.n_act = n_act;
     r.recv_keys = recv_keys;
@@ -2430,6 +2551,9 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     r.status = st;
     r.perm = perm;
     r.offsets = offs;
+    if (fwd) GD_TRY(forward_multi(h, s, n_act, r));
+    HIP_TRY(h, hipEventRecord(h->x_done[s], h->stream));
+    h->x_done_rec[s] = true;
     h->mres[s] = r;
     h->mres_n[s] = n;
     h->mcalls += 1;
@@ -2461,11 +2585,11 @@ int gd_comm_init(gd_handle* h, const uint8_t id[GD_COMM_ID_BYTES], int n_ranks, 
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(sync(h));
     comm_release(h);
-    HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 4 * 256 * sizeof(uint32_t)));
+    HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 6 * 256 * sizeof(uint32_t)));
     HIP_TRY(h, hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
     HIP_TRY(h, hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking));
     for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
-                          &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1]})
+                          &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1], &h->x_fwd[0], &h->x_fwd[1]})
         HIP_TRY(h, hipEventCreateWithFlags(e, hipEventDisableTiming));
     ncclUniqueId uid;
     std::memcpy(&uid, id, GD_COMM_ID_BYTES);
@@ -2491,14 +2615,14 @@ int gd_comm_destroy(gd_handle* h) {
 int gd_route_multi_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int flags,
                           gd_multi_result* out) {
     if (!h || (n && !d_keys)) return set_err(h, GD_EINVAL, "null argument");
-    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
     HIP_TRY(h, hipSetDevice(h->device));
     return route_multi(h, d_keys, n, n_act, flags, out);
 }
 
 int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, int flags, gd_multi_result* out) {
     if (!h || (n && !keys)) return set_err(h, GD_EINVAL, "null argument");
-    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(need_comm(h));
     // the batch goes to the device on the exchange stream, so the partition needs no other wait
@@ -2512,7 +2636,7 @@ int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act,
 int gd_route_multi_ext_device(gd_handle* h, const gd_key* d_keys, const gd_key_ext* d_ext, uint32_t n, uint32_t n_act,
                               int flags, gd_multi_result* out) {
     if (!h || (n && (!d_keys || !d_ext || !d_ext->offset || !d_ext->length))) return set_err(h, GD_EINVAL, "null argument");
-    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
     HIP_TRY(h, hipSetDevice(h->device));
     return route_multi(h, d_keys, n, n_act, flags, out, d_ext);
 }
@@ -2520,7 +2644,7 @@ int gd_route_multi_ext_device(gd_handle* h, const gd_key* d_keys, const gd_key_e
 int gd_route_multi_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t n_act, int flags,
                        gd_multi_result* out) {
     if (!h || (n && (!keys || !ext || !ext->offset || !ext->length))) return set_err(h, GD_EINVAL, "null argument");
-    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(need_comm(h));
     // the batch and its strings go to the device on the exchange stream

@@ -108,6 +108,70 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
     }
 }
 
+// Forward partition (SURVEY 8 e, the owner != activation silo case): after the probe on the owner,
+// a message whose route is a directory hit goes on to the rank hosting its activation (silo %
+// n_shards: the send to ActivationAddress.Silo after the remote lookup, LocalGrainDirectory.cs:920,
+// OutboundMessageQueue.cs:125); every other status stays on this rank.  Same counting as
+// k_shard_hist; k_shard_scatter then moves the keys with payload = position in the input.
+__global__ void __launch_bounds__(SH_NT) k_fwd_hist(const uint8_t* __restrict__ st, const uint32_t* __restrict__ silo,
+                                                    uint32_t n, uint32_t n_shards, uint32_t my_rank, uint32_t bits,
+                                                    uint32_t tiles, uint8_t* __restrict__ dest,
+                                                    uint32_t* __restrict__ hist) {
+    constexpr int NW = SH_NT / WAVE;
+    __shared__ uint32_t s_wc[NW][256];
+    for (uint32_t d = threadIdx.x; d < 256; d += SH_NT)
+#pragma unroll
+        for (int w = 0; w < NW; ++w) s_wc[w][d] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * SH_TILE;
+    const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < SH_IT; ++r) {
+        const uint32_t i = base + (w * SH_IT + r) * WAVE + lane;
+        const bool valid = i < n;
+        uint32_t d = 0;
+        if (valid) {
+            d = st[i] == GD_ROUTE_OK ? silo[i] % n_shards : my_rank;
+            dest[i] = (uint8_t)d;
+        }
+        unsigned long long peers = __ballot(valid);
+        for (uint32_t b = 0; b < bits; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const unsigned long long bal = __ballot(bit);
+            peers &= bit ? bal : ~bal;
+        }
+        if (valid && (peers & lt) == 0) s_wc[w][d] += (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < n_shards; d += SH_NT) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) t += s_wc[ww][d];
+        hist[d * tiles + blockIdx.x] = t;
+    }
+}
+
+// The forwarded messages' other fields in send order (pos = k_shard_scatter's payload).
+__global__ void __launch_bounds__(BLOCK) k_fwd_gather(const uint32_t* __restrict__ pos, uint32_t n,
+                                                      const uint32_t* __restrict__ idx_in,
+                                                      const uint32_t* __restrict__ src_in,
+                                                      const uint32_t* __restrict__ silo_in,
+                                                      const uint32_t* __restrict__ act_in,
+                                                      const uint8_t* __restrict__ st_in, uint32_t* __restrict__ idx,
+                                                      uint32_t* __restrict__ src, uint32_t* __restrict__ silo,
+                                                      uint32_t* __restrict__ act, uint8_t* __restrict__ st) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t i = pos[j];
+    if (i >= n) return;
+    idx[j] = idx_in[i];
+    src[j] = src_in[i];
+    silo[j] = silo_in[i];
+    act[j] = act_in[i];
+    st[j] = st_in[i];
+}
+
 // payload_in == nullptr: the payload is the record's batch index (the origin index).
 template <int BITS, bool NODES>
 __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict__ recs,

@@ -36,7 +36,8 @@ EXPORTED_SYMBOLS = [
     "gd_ring_build", "gd_ring_set", "gd_ring_owner", "gd_ring_lookup_hashes", "gd_dir_register",
     "gd_dir_unregister", "gd_dir_lookup", "gd_dir_clear", "gd_dir_rehash", "gd_route", "gd_bucket",
     "gd_route_bucket", "gd_route_device", "gd_bucket_device", "gd_route_bucket_device",
-    "gd_ring_owner_device", "gd_pack_by_shard_device", "gd_kernel_times", "gd_kernel_times_reset",
+    "gd_ring_owner_device", "gd_pack_by_shard_device", "gd_pack_routes_by_rank_device", "gd_kernel_times",
+    "gd_kernel_times_reset",
     "gd_set_kernel_timing", "gd_microbatch_create", "gd_microbatch_destroy", "gd_microbatch_keys",
     "gd_microbatch_outputs", "gd_microbatch_run", "gd_decode_frames_device", "gd_decode_frames",
     "gd_route_frames_device", "gd_route_frames", "gd_dir_split", "gd_dir_split_device",
@@ -139,8 +140,11 @@ class KeyExtBatch:
                 pos += len(b)
         self.blob = np.frombuffer(b"".join(parts) + b"\0", dtype=np.uint8).copy()
         self.struct = gd_key_ext(self.blob.ctypes.data, self.offset.ctypes.data, self.length.ctypes.data, pos)
+
+
 GD_MULTI_RETURN_ROUTES = 1
 GD_MULTI_KEYS_READY = 2
+GD_MULTI_FORWARD = 4
 
 
 class GrainDispatchError(RuntimeError):
@@ -197,6 +201,7 @@ def _load() -> C.CDLL:
         "gd_route_bucket_device": (C.c_int, [P, P, U32, U32, P, P, P, P, P]),
         "gd_ring_owner_device": (C.c_int, [P, P, U32, P]),
         "gd_pack_by_shard_device": (C.c_int, [P, P, U32, U32, P, P, P]),
+        "gd_pack_routes_by_rank_device": (C.c_int, [P, P, P, P, U32, U32, U32, P, P, P]),
         "gd_kernel_times": (C.c_int, [P, C.POINTER(gd_kernel_time), U32, C.POINTER(U32)]),
         "gd_kernel_times_reset": (C.c_int, [P]),
         "gd_set_kernel_timing": (C.c_int, [P, C.c_int]),
@@ -731,6 +736,12 @@ class GrainDispatch:
         self._c(lib.gd_pack_by_shard_device(self.h, C.c_void_p(d_keys), n, n_shards, C.c_void_p(d_send_keys),
                                             C.c_void_p(d_send_idx), C.c_void_p(d_counts)))
 
+    def pack_routes_by_rank_device(self, d_keys: int, d_status: int, d_silo: int, n: int, n_shards: int, my_rank: int,
+                                   d_send_keys: int, d_send_pos: int, d_counts: int):
+        self._c(lib.gd_pack_routes_by_rank_device(self.h, C.c_void_p(d_keys), C.c_void_p(d_status), C.c_void_p(d_silo),
+                                                  n, n_shards, my_rank, C.c_void_p(d_send_keys),
+                                                  C.c_void_p(d_send_pos), C.c_void_p(d_counts)))
+
     # -- in-library exchange over RCCL (SURVEY 8 b gd_route_multi, 8 e) ----------------
     @staticmethod
     def comm_unique_id() -> bytes:
@@ -747,20 +758,21 @@ class GrainDispatch:
         self._c(lib.gd_comm_destroy(self.h))
 
     def route_multi_device(self, d_keys: int, n: int, n_act: int, return_routes: bool = False,
-                           keys_ready: bool = False) -> gd_multi_result:
+                           keys_ready: bool = False, forward: bool = False) -> gd_multi_result:
         """Returns after the counts round; the rest is enqueued.  The result holds device pointers
         into library-owned buffers, valid through the next call (two batches in flight)."""
         r = gd_multi_result()
-        flags = (GD_MULTI_RETURN_ROUTES if return_routes else 0) | (GD_MULTI_KEYS_READY if keys_ready else 0)
+        flags = ((GD_MULTI_RETURN_ROUTES if return_routes else 0) | (GD_MULTI_KEYS_READY if keys_ready else 0)
+                 | (GD_MULTI_FORWARD if forward else 0))
         self._c(lib.gd_route_multi_device(self.h, C.c_void_p(d_keys), n, n_act, flags, C.byref(r)))
         return r
 
-    def route_multi(self, keys, n_act: int, return_routes: bool = False) -> dict:
+    def route_multi(self, keys, n_act: int, return_routes: bool = False, forward: bool = False) -> dict:
         """Host batch in, host results out (gd_route_multi + gd_multi_fetch)."""
         k = keys_array(keys)
         n = k.shape[0]
         r = gd_multi_result()
-        flags = GD_MULTI_RETURN_ROUTES if return_routes else 0
+        flags = (GD_MULTI_RETURN_ROUTES if return_routes else 0) | (GD_MULTI_FORWARD if forward else 0)
         self._c(lib.gd_route_multi(self.h, _ptr(k), n, n_act, flags, C.byref(r)))
         return self.multi_fetch(r, n)
 
@@ -790,13 +802,13 @@ class GrainDispatch:
         self._c(lib.gd_ring_owner_ext(self.h, _ptr(k), C.byref(x.struct), n, _ptr(out)))
         return out
 
-    def route_multi_ext(self, keys, exts, n_act: int, return_routes: bool = False) -> dict:
+    def route_multi_ext(self, keys, exts, n_act: int, return_routes: bool = False, forward: bool = False) -> dict:
         """route_multi with KeyExt grains routed on their owner (strings travel with the batch)."""
         k = keys_array(keys)
         n = k.shape[0]
         x = self._ext(exts, n)
         r = gd_multi_result()
-        flags = GD_MULTI_RETURN_ROUTES if return_routes else 0
+        flags = (GD_MULTI_RETURN_ROUTES if return_routes else 0) | (GD_MULTI_FORWARD if forward else 0)
         self._c(lib.gd_route_multi_ext(self.h, _ptr(k), C.byref(x.struct), n, n_act, flags, C.byref(r)))
         return self.multi_fetch(r, n)
 

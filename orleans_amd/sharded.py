@@ -57,6 +57,32 @@ class DeviceEngine:
                                      counts.data_ptr())
         return send_keys, send_idx, counts
 
+    def route(self, keys: torch.Tensor):
+        n = keys.shape[0]
+        dev = self.device
+        st = torch.empty(n, dtype=torch.uint8, device=dev)
+        silo = torch.empty(n, dtype=torch.int32, device=dev)
+        act = torch.empty(n, dtype=torch.int32, device=dev)
+        self.gd.route_device(keys.data_ptr(), n, silo.data_ptr(), act.data_ptr(), st.data_ptr())
+        return st, silo, act
+
+    def bucket(self, act: torch.Tensor, n_act: int):
+        n = act.shape[0]
+        perm = torch.empty(n, dtype=torch.int32, device=self.device)
+        off = torch.empty(n_act + 2, dtype=torch.int32, device=self.device)
+        self.gd.bucket_device(act.data_ptr(), n, n_act, perm.data_ptr(), off.data_ptr())
+        return perm, off
+
+    def pack_routes_by_rank(self, keys: torch.Tensor, st: torch.Tensor, silo: torch.Tensor, n_shards: int,
+                            my_rank: int):
+        n = keys.shape[0]
+        send_keys = torch.empty_like(keys)
+        send_pos = torch.empty(n, dtype=torch.int32, device=self.device)
+        counts = torch.empty(n_shards, dtype=torch.int32, device=self.device)
+        self.gd.pack_routes_by_rank_device(keys.data_ptr(), st.data_ptr(), silo.data_ptr(), n, n_shards, my_rank,
+                                           send_keys.data_ptr(), send_pos.data_ptr(), counts.data_ptr())
+        return send_keys, send_pos, counts
+
     def route_bucket(self, keys: torch.Tensor, n_act: int):
         n = keys.shape[0]
         dev = self.device
@@ -158,14 +184,40 @@ class ShardedRouter:
         _, _, inserted = self.engine.register(recv_keys, recv_vals)
         return HandoffResult(moved, m, int((inserted == 0).sum()))
 
-    def route_bucket(self, keys: torch.Tensor, n_act: int) -> ShardedResult:
+    def _a2a_v(self, tensors, in_splits, out_splits):
+        outs = []
+        for t in tensors:
+            o = torch.empty((int(sum(out_splits)),) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+            self._a2a(o, t, out_splits, in_splits)
+            outs.append(o)
+        return outs
+
+    def route_bucket(self, keys: torch.Tensor, n_act: int, forward: bool = False) -> ShardedResult:
+        """forward=False: the benchmark's co-location (activation silo = directory owner): probe and
+        bucket on the owner.  forward=True: the general case -- probe on the owner, then directory
+        hits travel on to the rank hosting their activation (silo % world; the send to
+        ActivationAddress.Silo after a remote lookup, LocalGrainDirectory.cs:920,
+        OutboundMessageQueue.cs:125) and are bucketed there; other statuses stay on the owner.
+        One grain has one owner, so each activation still sees (sender rank, sender order)."""
         if self.world == 1:
             # no exchange: arrival order is the batch order, all from this rank
             recv_keys, recv_idx, recv_src = keys, None, None
         else:
             recv_keys, recv_idx, recv_src = self.exchange(keys)
-        st, silo, act, perm, off = self.engine.route_bucket(recv_keys, n_act)
-        return ShardedResult(recv_keys, recv_idx, recv_src, st, silo, act, perm, off)
+        if not forward or self.world == 1:
+            st, silo, act, perm, off = self.engine.route_bucket(recv_keys, n_act)
+            return ShardedResult(recv_keys, recv_idx, recv_src, st, silo, act, perm, off)
+        st, silo, act = self.engine.route(recv_keys)
+        send_keys, send_pos, counts = self.engine.pack_routes_by_rank(recv_keys, st, silo, self.world, self.rank)
+        pos = send_pos.long()
+        counts64 = counts.to(torch.int64)
+        recv_counts = torch.empty_like(counts64)
+        self._a2a(recv_counts, counts64)
+        in_splits, out_splits = counts64.tolist(), recv_counts.tolist()
+        keys2, idx2, src2, silo2, act2, st2 = self._a2a_v(
+            [send_keys, recv_idx[pos], recv_src[pos], silo[pos], act[pos], st[pos]], in_splits, out_splits)
+        perm, off = self.engine.bucket(act2, n_act)
+        return ShardedResult(keys2, idx2, src2, st2, silo2, act2, perm, off)
 
 
 class _DevView:

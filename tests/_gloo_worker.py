@@ -64,6 +64,24 @@ class OracleEngine:
         return (t(st, np.uint8), t(silo, np.int32), t(act, np.int32), t(perm, np.int32), t(off, np.int32))
 
 
+    def route(self, keys):
+        k = keys.numpy().view(np.uint64)
+        st, silo, act, _, _ = o.route_batch_np(k, self.spec, self.dir, my_silo=self.my_silo, seed_silo=0)
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt))
+        return t(st, np.uint8), t(silo, np.int32), t(act, np.int32)
+
+    def bucket(self, act, n_act):
+        perm, off = o.bucket_stable(act.numpy().view(np.uint32), n_act)
+        return torch.from_numpy(perm.view(np.int32)), torch.from_numpy(off.view(np.int32))
+
+    def pack_routes_by_rank(self, keys, st, silo, n_shards, my_rank):
+        s, sl = st.numpy(), silo.numpy().view(np.uint32)
+        dest = np.where(s == o.ST_OK, sl % n_shards, my_rank).astype(np.uint32)
+        perm, off = o.bucket_stable(dest, n_shards)
+        counts = np.diff(off[: n_shards + 1]).astype(np.int32)
+        k = keys.numpy()
+        return torch.from_numpy(k[perm].copy()), torch.from_numpy(perm.astype(np.int32)), torch.from_numpy(counts)
+
     def split(self, keep, n_silos):
         keys, acts, silos, self.dir = o.split_directory(self.dir, self.spec, keep, my_silo=self.my_silo, seed_silo=0)
         vals = np.stack([acts, silos], axis=1).astype(np.uint32)
@@ -74,6 +92,70 @@ class OracleEngine:
         v = vals.numpy().view(np.uint32).reshape(-1, 2)
         self.dir, inserted = o.merge_directory(self.dir, k, v[:, 0], v[:, 1])
         return None, None, inserted.astype(np.uint8)
+
+
+class ForwardEngine(OracleEngine):
+    """Activations not co-located with their directory owner: grain g lives on silo (5g + 1) % 8,
+    activation id = its index among the grains hosted on that silo's rank."""
+
+    def __init__(self, rank, world, my_silo):
+        super().__init__(rank, world, my_silo)
+        reg = o.grain_keys(TC, np.arange(G_TOTAL))
+        own = o.ring_owner_np(SPEC, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1]))
+        act_silo = ((5 * np.arange(G_TOTAL) + 1) % 8).astype(np.uint32)
+        host = act_silo % world
+        act_id = np.zeros(G_TOTAL, np.uint32)
+        for r in range(world):
+            act_id[host == r] = np.arange(int((host == r).sum()))
+        self.n_act = int((host == rank).sum())
+        mine = own % world == rank
+        self.dir = o.DirectoryArrays(reg[mine], act_id[mine], act_silo[mine])
+        self.full = o.DirectoryArrays(reg, act_id, act_silo)
+
+
+def check_forward(rank, world):
+    """ShardedRouter.route_bucket(forward=True): every message ends on the rank hosting its
+    activation (directory hits) or on its owner (anything else), with the owner's route, and each
+    activation's messages in (sender rank, sender batch order)."""
+    eng = ForwardEngine(rank, world, my_silo=rank)
+    router = ShardedRouter(eng)
+    keys = torch.from_numpy(batch_of(rank).view(np.int64).copy())
+    res = router.route_bucket(keys, eng.n_act, forward=True)
+    rk = res.recv_keys.numpy().view(np.uint64)
+    src, idx = res.recv_src.numpy(), res.recv_idx.numpy()
+    batches = {r: batch_of(r) for r in range(world)}
+    expect = []
+    for r in range(world):
+        st, silo, act, owner, _ = o.route_batch_np(batches[r], SPEC, eng.full, my_silo=r, seed_silo=0)
+        orank = np.where(owner == o.M32, r, owner % world)
+        final = np.where(st == o.ST_OK, silo % world, orank)
+        for i in np.nonzero(final == rank)[0]:
+            expect.append((int(orank[i]), r, int(i)))
+    # arrival order = (owner rank, sender rank, sender order)
+    expect.sort()
+    assert [(s_, i_) for _, s_, i_ in expect] == list(zip(src.tolist(), idx.tolist()))
+    for j in range(len(rk)):
+        assert (batches[src[j]][idx[j]] == rk[j]).all()
+    # the owner's routes (a system target's owner is its sender's silo, which is this rank)
+    w_st, w_silo, w_act, _, _ = o.route_batch_np(rk, SPEC, eng.full, my_silo=rank, seed_silo=0)
+    assert np.array_equal(res.status.numpy(), w_st)
+    assert np.array_equal(res.silo.numpy().view(np.uint32), w_silo)
+    assert np.array_equal(res.act.numpy().view(np.uint32), w_act)
+    ok = w_st == o.ST_OK
+    assert (w_silo[ok] % world == rank).all()
+    wp, wo = o.bucket_stable(res.act.numpy().view(np.uint32), eng.n_act)
+    assert np.array_equal(res.perm.numpy().view(np.uint32), wp)
+    assert np.array_equal(res.offsets.numpy().view(np.uint32), wo)
+    # per activation: (sender rank, sender order) increasing
+    order = src.astype(np.int64) * (1 << 32) + idx
+    perm = wp
+    for a in range(eng.n_act):
+        seg = order[perm[wo[a]:wo[a + 1]]]
+        assert (np.diff(seg) > 0).all()
+    tot = torch.tensor([len(rk), int(ok.sum())], dtype=torch.int64)
+    dist.all_reduce(tot)
+    assert tot[0].item() == world * N_PER_RANK
+    return int(ok.sum())
 
 
 def entries(eng):
@@ -145,7 +227,9 @@ def main():
     assert (rk[ok, 1] < G_TOTAL).all()
     for j in np.nonzero(ok)[0][:500]:
         assert act[j] == eng.local_act_of_grain[int(rk[j, 1])]
-    # 7) membership change: silo 8 joins, then silo 5 leaves
+    # 7) activations away from their directory owner: the forward hop (SURVEY 8 e caveat)
+    n_fwd_ok = check_forward(rank, world)
+    # 8) membership change: silo 8 joins, then silo 5 leaves
     silos9 = o.bench_silos(9)
     spec9 = o.ring_spec(silos9, "D")
     _, moved_add = check_handoff(router, eng, spec9, 9, rank, world)
@@ -154,7 +238,8 @@ def main():
     spec_rm = o.RingSpec("D", sp.points, [alive[x] for x in sp.owners])
     _, moved_rm = check_handoff(router, eng, spec_rm, 9, rank, world)
     assert moved_rm > 0       # silo 5's range lands on silos of other ranks at world 2 and 3
-    print(f"OK rank {rank}/{world}: received {m}, ok {int(ok.sum())}, handoff moved {moved_add} + {moved_rm}",
+    print(f"OK rank {rank}/{world}: received {m}, ok {int(ok.sum())}, forwarded-ok {n_fwd_ok}, "
+          f"handoff moved {moved_add} + {moved_rm}",
           flush=True)
     dist.destroy_process_group()
 

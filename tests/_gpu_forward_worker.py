@@ -1,0 +1,71 @@
+"""Worker for tests/test_gpu_multi.py::test_sharded_forward_two_ranks_one_gpu: one rank of
+orleans_amd.sharded.ShardedRouter with the product DeviceEngine (libgraindispatch on cuda:0) and
+route_bucket(forward=True).  Every rank shares cuda:0, so the exchange runs over gloo on host
+copies (stage_via_cpu); the partition, probe, forward partition (gd_pack_routes_by_rank_device)
+and bucketing are the GPU kernels.  Activations do not live on their directory owner: grain g's
+activation is on silo (5g + 1) % 8.  Results go to <dir>/fwd<r>.npz."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle as o                                    # noqa: E402
+
+TC = o.grain_type_code(o.PING_GRAIN_CLASS)
+G_TOTAL = 5000
+
+
+def batch_of(rank, n):
+    rng = np.random.default_rng(3000 + rank)
+    keys = o.grain_keys(TC, rng.integers(0, G_TOTAL + 300, size=n))   # ~6% unregistered -> MISS
+    keys[::101] = np.array(o.UniqueKey(0, 3, o.type_code_data(o.CAT_SYSTEM_TARGET, 1)).as_tuple(), dtype=np.uint64)
+    return keys
+
+
+def directory(world):
+    """(keys, owner silo, activation silo, activation id on its host rank) for every grain."""
+    spec = o.ring_spec(o.bench_silos(8), "D")
+    reg = o.grain_keys(TC, np.arange(G_TOTAL))
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    act_silo = ((5 * np.arange(G_TOTAL) + 1) % 8).astype(np.uint32)
+    host = act_silo % world
+    act_id = np.zeros(G_TOTAL, np.uint32)
+    for r in range(world):
+        act_id[host == r] = np.arange(int((host == r).sum()))
+    return spec, reg, own, act_silo, act_id
+
+
+def main():
+    out_dir, world, rank, n = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+    import torch
+    import torch.distributed as dist
+    from orleans_amd import graindispatch as g
+    from orleans_amd.sharded import DeviceEngine, ShardedRouter
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(out_dir, "pg"), world_size=world, rank=rank)
+    spec, reg, own, act_silo, act_id = directory(world)
+    mine = own % world == rank
+    e = g.GrainDispatch(device=0, table_capacity=1 << 13, my_silo=rank)
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in o.bench_silos(8)])
+    e.register(reg[mine], act_id[mine], act_silo[mine])
+    dev = torch.device("cuda:0")
+    eng = DeviceEngine(e, dev)
+    router = ShardedRouter(eng, stage_via_cpu=True)
+    n_act = int((act_silo % world == rank).sum())
+    keys = torch.from_numpy(batch_of(rank, n).view(np.int64).copy()).to(dev)
+    with torch.cuda.stream(eng.stream):
+        res = router.route_bucket(keys, n_act, forward=True)
+    torch.cuda.synchronize()
+    u32 = lambda t: t.cpu().numpy().view(np.uint32)
+    np.savez(os.path.join(out_dir, f"fwd{rank}.npz"), recv_keys=res.recv_keys.cpu().numpy().view(np.uint64),
+             recv_idx=u32(res.recv_idx), recv_src=u32(res.recv_src), status=res.status.cpu().numpy(),
+             silo=u32(res.silo), act=u32(res.act), perm=u32(res.perm), offsets=u32(res.offsets))
+    dist.destroy_process_group()
+    e.close()
+    print(f"rank {rank}: ok, received {res.recv_keys.shape[0]}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

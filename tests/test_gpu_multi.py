@@ -302,3 +302,115 @@ def test_ring_owner_ext_is_the_partition_owner(gd, mode):
     want = np.where(owner == o.M32, 5, owner)          # KEYEXT kept here -> my silo
     np.testing.assert_array_equal(got, want)
     e.close()
+
+
+@pytest.mark.parametrize("n", [0, 1, 70001])
+def test_route_multi_forward_world1(gd, n):
+    """GD_MULTI_FORWARD at world 1: the forward hop is a send to self, so the result equals the
+    co-located one (the activation silos here differ from the owners)."""
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "R")
+    G = 3000
+    reg, own, _ = _directory(G, 1, 0, spec)
+    act_silo = ((5 * np.arange(G) + 1) % 8).astype(np.uint32)
+    rng = np.random.default_rng(n + 5)
+    keys = o.grain_keys(TC, rng.integers(0, G + 200, size=n))
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 13, my_silo=4)
+    e.ring_set_silos("R", [(s.ip, s.port, s.gen) for s in silos])
+    e.register(reg, np.arange(G), act_silo)
+    e.comm_init(gd.GrainDispatch.comm_unique_id(), 1, 0)
+    st, silo, act, _, _ = o.route_batch_np(keys, spec, o.DirectoryArrays(reg, np.arange(G), act_silo), my_silo=4)
+    wp, wo = o.bucket_stable(act, G)
+    for ret in (False, True):
+        r = e.route_multi(keys, G, return_routes=ret, forward=True)
+        np.testing.assert_array_equal(r["recv_keys"], keys)
+        np.testing.assert_array_equal(r["recv_idx"], np.arange(n, dtype=np.uint32))
+        np.testing.assert_array_equal(r["recv_src"], np.zeros(n, np.uint32))
+        np.testing.assert_array_equal(r["status"], st)
+        np.testing.assert_array_equal(r["silo"], silo)
+        np.testing.assert_array_equal(r["act"], act)
+        np.testing.assert_array_equal(r["perm"], wp)
+        np.testing.assert_array_equal(r["offsets"], wo)
+        if ret:
+            np.testing.assert_array_equal(r["ret_act"], act)
+    e.comm_destroy()
+    e.close()
+
+
+@pytest.mark.parametrize("W", [1, 2, 3, 8, 256])
+def test_pack_routes_by_rank(gd, W):
+    """gd_pack_routes_by_rank_device: stable partition by silo % W for directory hits, my_rank for
+    every other status."""
+    import torch
+    rng = np.random.default_rng(W)
+    for n in (0, 1, 2047, 2048, 2049, 300001):
+        my_rank = int(rng.integers(0, W))
+        keys = rng.integers(0, 1 << 62, size=(n, 3), dtype=np.uint64)
+        st = rng.choice(np.array([0, 0, 0, 1, 2, 3, 4, 7], np.uint8), size=n)
+        silo = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+        e = gd.GrainDispatch(device=0, table_capacity=64)
+        dk = torch.from_numpy(keys.view(np.int64).copy()).cuda()
+        ds = torch.from_numpy(st.copy()).cuda()
+        dl = torch.from_numpy(silo.view(np.int32).copy()).cuda()
+        sk = torch.empty_like(dk)
+        sp = torch.empty(n, dtype=torch.int32, device="cuda")
+        cnt = torch.empty(W, dtype=torch.int32, device="cuda")
+        e.pack_routes_by_rank_device(dk.data_ptr(), ds.data_ptr(), dl.data_ptr(), n, W, my_rank, sk.data_ptr(),
+                                     sp.data_ptr(), cnt.data_ptr())
+        e.synchronize()
+        dest = np.where(st == 0, silo % W, my_rank).astype(np.uint32)
+        wp, wo = o.bucket_stable(dest, W)
+        np.testing.assert_array_equal(sp.cpu().numpy().view(np.uint32), wp)
+        np.testing.assert_array_equal(sk.cpu().numpy().view(np.uint64), keys[wp])
+        np.testing.assert_array_equal(cnt.cpu().numpy(), np.diff(wo[:W + 1]))
+        e.close()
+    with pytest.raises(gd.GrainDispatchError):
+        gd.GrainDispatch(device=0, table_capacity=64).pack_routes_by_rank_device(0, 0, 0, 0, W, W, 0, 0, 0)
+
+
+def test_sharded_forward_two_ranks_one_gpu(tmp_path):
+    """ShardedRouter.route_bucket(forward=True) with the device engine, two ranks on cuda:0 over
+    gloo (host-staged): every message ends on the rank hosting its activation (directory hits) or
+    on its owner (the rest), with the owner's route, and each activation sees its messages in
+    (sender rank, sender batch order)."""
+    world, n = 2, 30011
+    procs = [subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "_gpu_forward_worker.py"), str(tmp_path),
+                               str(world), str(r), str(n)], cwd=ROOT, env=dict(os.environ), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=100)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("forward worker timed out")
+        outs.append(out)
+    assert [p.returncode for p in procs] == [0] * world, outs
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _gpu_forward_worker as w
+    spec, reg, own, act_silo, act_id = w.directory(world)
+    full = o.DirectoryArrays(reg, act_id, act_silo)
+    batches = [w.batch_of(r, n) for r in range(world)]
+    expect = {r: [] for r in range(world)}
+    for s in range(world):
+        st, silo, act, owner, _ = o.route_batch_np(batches[s], spec, full, my_silo=s)
+        orank = np.where(owner == o.M32, s, owner % world)
+        final = np.where(st == o.ST_OK, silo % world, orank)
+        for i in range(n):
+            expect[int(final[i])].append((int(orank[i]), s, i))
+    for r in range(world):
+        res = dict(np.load(tmp_path / f"fwd{r}.npz"))
+        ex = sorted(expect[r])
+        np.testing.assert_array_equal(res["recv_src"], np.array([x[1] for x in ex], np.uint32))
+        np.testing.assert_array_equal(res["recv_idx"], np.array([x[2] for x in ex], np.uint32))
+        rk = np.concatenate([batches[x[1]][x[2]:x[2] + 1] for x in ex]) if ex else np.zeros((0, 3), np.uint64)
+        np.testing.assert_array_equal(res["recv_keys"], rk)
+        st, silo, act, _, _ = o.route_batch_np(rk, spec, full, my_silo=r)
+        np.testing.assert_array_equal(res["status"], st)
+        np.testing.assert_array_equal(res["silo"], silo)
+        np.testing.assert_array_equal(res["act"], act)
+        n_act = int((act_silo % world == r).sum())
+        wp, wo = o.bucket_stable(act, n_act)
+        np.testing.assert_array_equal(res["perm"], wp)
+        np.testing.assert_array_equal(res["offsets"], wo)
