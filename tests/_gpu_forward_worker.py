@@ -2,8 +2,9 @@
 orleans_amd.sharded.ShardedRouter with the product DeviceEngine (libgraindispatch on cuda:0) and
 route_bucket(forward=True).  Every rank shares cuda:0, so the exchange runs over gloo on host
 copies (stage_via_cpu); the partition, probe, forward partition (gd_pack_routes_by_rank_device)
-and bucketing are the GPU kernels.  Activations do not live on their directory owner: grain g's
-activation is on silo (5g + 1) % 8.  Results go to <dir>/fwd<r>.npz."""
+and bucketing are the GPU kernels.  The same batch also runs without the forward hop (probe +
+bucket on the owner, the bench's N > 1 torch path).  Activations do not live on their directory
+owner: grain g's activation is on silo (5g + 1) % 8.  Results go to <dir>/fwd<r>.npz and <dir>/own<r>.npz."""
 import os
 import sys
 
@@ -55,13 +56,14 @@ def main():
     router = ShardedRouter(eng, stage_via_cpu=True)
     n_act = int((act_silo % world == rank).sum())
     keys = torch.from_numpy(batch_of(rank, n).view(np.int64).copy()).to(dev)
-    with torch.cuda.stream(eng.stream):
-        res = router.route_bucket(keys, n_act, forward=True)
-    torch.cuda.synchronize()
     u32 = lambda t: t.cpu().numpy().view(np.uint32)
-    np.savez(os.path.join(out_dir, f"fwd{rank}.npz"), recv_keys=res.recv_keys.cpu().numpy().view(np.uint64),
-             recv_idx=u32(res.recv_idx), recv_src=u32(res.recv_src), status=res.status.cpu().numpy(),
-             silo=u32(res.silo), act=u32(res.act), perm=u32(res.perm), offsets=u32(res.offsets))
+    for name, fwd, na in (("fwd", True, n_act), ("own", False, G_TOTAL)):
+        with torch.cuda.stream(eng.stream):
+            res = router.route_bucket(keys, na, forward=fwd)
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, f"{name}{rank}.npz"), recv_keys=res.recv_keys.cpu().numpy().view(np.uint64),
+                 recv_idx=u32(res.recv_idx), recv_src=u32(res.recv_src), status=res.status.cpu().numpy(),
+                 silo=u32(res.silo), act=u32(res.act), perm=u32(res.perm), offsets=u32(res.offsets))
     dist.destroy_process_group()
     e.close()
     print(f"rank {rank}: ok, received {res.recv_keys.shape[0]}", flush=True)

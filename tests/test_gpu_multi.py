@@ -414,3 +414,22 @@ def test_sharded_forward_two_ranks_one_gpu(tmp_path):
         wp, wo = o.bucket_stable(act, n_act)
         np.testing.assert_array_equal(res["perm"], wp)
         np.testing.assert_array_equal(res["offsets"], wo)
+    # without the forward hop: everything stays on its owner (ShardedRouter.exchange + route_bucket)
+    for r in range(world):
+        res = dict(np.load(tmp_path / f"own{r}.npz"))
+        ks, ids, srcs = [], [], []
+        for s in range(world):
+            _, _, _, owner, _ = o.route_batch_np(batches[s], spec, full, my_silo=s)
+            sel = np.nonzero(np.where(owner == o.M32, s, owner % world) == r)[0]
+            ks.append(batches[s][sel]), ids.append(sel), srcs.append(np.full(len(sel), s))
+        rk = np.concatenate(ks)
+        np.testing.assert_array_equal(res["recv_keys"], rk)
+        np.testing.assert_array_equal(res["recv_idx"], np.concatenate(ids).astype(np.uint32))
+        np.testing.assert_array_equal(res["recv_src"], np.concatenate(srcs).astype(np.uint32))
+        st, silo, act, _, _ = o.route_batch_np(rk, spec, full, my_silo=r)
+        np.testing.assert_array_equal(res["status"], st)
+        np.testing.assert_array_equal(res["silo"], silo)
+        np.testing.assert_array_equal(res["act"], act)
+        wp, wo = o.bucket_stable(act, w.G_TOTAL)
+        np.testing.assert_array_equal(res["perm"], wp)
+        np.testing.assert_array_equal(res["offsets"], wo)
