@@ -299,6 +299,12 @@ int gd_pack_routes_by_rank_device(gd_handle* h, const gd_key* d_keys, const uint
 #define GD_COMM_ID_BYTES 128
 int gd_comm_unique_id(uint8_t out_id[GD_COMM_ID_BYTES]);
 int gd_comm_init(gd_handle* h, const uint8_t id[GD_COMM_ID_BYTES], int n_ranks, int rank);
+/* Rehearsal transport: hs[0..n_ranks) (handles of this process, any devices, one host thread
+ * driving each) become ranks 0..n_ranks-1 of an in-process communicator whose send/recv are
+ * device-to-device copies with RCCL's matching and stream-ordering rules (gd_localcomm.h).  It
+ * runs the W > 1 exchange on one GPU, which RCCL refuses (one rank per device).  Each handle
+ * leaves it with gd_comm_destroy / gd_destroy. */
+int gd_comm_init_local(gd_handle* const* hs, int n_ranks);
 int gd_comm_destroy(gd_handle* h);
 
 /* Results of the last gd_route_multi* call on a handle: device pointers into library-owned

@@ -19,6 +19,7 @@
 #include "gd_cache.h"
 #include "gd_shard.h"
 #include "gd_comm.h"
+#include "gd_localcomm.h"
 #include "gd_keyext.h"
 #include "gd_frames.h"
 #include "graindispatch.h"
@@ -94,6 +95,7 @@ struct gd_handle {
     // the RCCL rounds run on xstream; probe + bucketing on `stream`; batch i's exchange overlaps
     // batch i-1's probe + bucketing (receive/result buffers double-buffered by batch parity).
     ncclComm_t comm = nullptr;
+    const Rccl* net = nullptr;        // the transport behind comm: RCCL, or the in-process one
     int n_ranks = 0, rank = -1;
     hipStream_t xstream = nullptr;
     hipStream_t pstream = nullptr;    // the partition (pack) of the next batch, beside this one's rounds
@@ -2177,7 +2179,7 @@ namespace {
     do {                                                                                           \
         ncclResult_t r_ = (expr);                                                                  \
         if (r_ != ncclSuccess)                                                                     \
-            return set_err((h), GD_ERCCL, "%s: %s", #expr, rccl().GetErrorString(r_));             \
+            return set_err((h), GD_ERCCL, "%s: %s", #expr, (h)->net->GetErrorString(r_));          \
     } while (0)
 
 // Launches inside the scope go to the exchange stream (launch() uses h->stream), with the
@@ -2212,8 +2214,9 @@ struct OnPStream : OnStream {
 void comm_release(gd_handle* h) {
     if (h->pstream) (void)hipStreamSynchronize(h->pstream);
     if (h->xstream) (void)hipStreamSynchronize(h->xstream);
-    if (h->comm) (void)rccl().CommDestroy(h->comm);
+    if (h->comm) (void)h->net->CommDestroy(h->comm);
     h->comm = nullptr;
+    h->net = nullptr;
     for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
                           &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1], &h->x_fwd[0], &h->x_fwd[1]})
         if (*e) {
@@ -2244,6 +2247,21 @@ void comm_release(gd_handle* h) {
     h->rank = -1;
 }
 
+// Streams, events and the pinned count buffer of a communicator (any previous one released).
+int comm_setup(gd_handle* h) {
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(sync(h));
+    comm_release(h);
+    HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 6 * 256 * sizeof(uint32_t)));
+    HIP_TRY(h, hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
+    HIP_TRY(h, hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
+                          &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1],
+                          &h->x_fwd[0], &h->x_fwd[1]})
+        HIP_TRY(h, hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return GD_OK;
+}
+
 int need_comm(gd_handle* h) {
     if (!h->comm) return set_err(h, GD_ESTATE, "no communicator (gd_comm_init)");
     return GD_OK;
@@ -2272,7 +2290,7 @@ struct Lane {
 
 int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uint64_t* soff, const uint32_t* rc,
                    const uint64_t* roff, const Lane* lanes, int n_lanes) {
-    const Rccl& R = rccl();
+    const Rccl& R = *h->net;
     hipEvent_t a = nullptr, b = nullptr;
     if (h->timing) {
         a = take_event(h);
@@ -2307,7 +2325,7 @@ int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uin
 // owner's routes on entry (probe enqueued, x_route[s] recorded) and the forwarded result on exit.
 int forward_multi(gd_handle* h, int s, uint32_t n_act, gd_multi_result& r) {
     const int W = h->n_ranks;
-    const Rccl& R = rccl();
+    const Rccl& R = *h->net;
     const uint32_t m = r.n_recv;
     DevBuf* F = h->mf[s];
     const size_t m4 = (size_t)m * 4 + 4;
@@ -2386,7 +2404,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     GD_TRY(check_ring(h));
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
     const int W = h->n_ranks;
-    const Rccl& R = rccl();
+    const Rccl& R = *h->net;
     const int s = (int)(h->mcalls & 1);
     DevBuf* B = h->mx[s];
     const bool ret = (flags & GD_MULTI_RETURN_ROUTES) != 0;
@@ -2582,15 +2600,7 @@ int gd_comm_init(gd_handle* h, const uint8_t id[GD_COMM_ID_BYTES], int n_ranks, 
         return set_err(h, GD_EINVAL, "rank %d of %d: need 0 <= rank < n_ranks <= 256", rank, n_ranks);
     const Rccl& R = rccl();
     if (!R.ok) return set_err(h, GD_ERCCL, "%s", R.why);
-    HIP_TRY(h, hipSetDevice(h->device));
-    GD_TRY(sync(h));
-    comm_release(h);
-    HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 6 * 256 * sizeof(uint32_t)));
-    HIP_TRY(h, hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
-    HIP_TRY(h, hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
-                          &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1], &h->x_fwd[0], &h->x_fwd[1]})
-        HIP_TRY(h, hipEventCreateWithFlags(e, hipEventDisableTiming));
+    GD_TRY(comm_setup(h));
     ncclUniqueId uid;
     std::memcpy(&uid, id, GD_COMM_ID_BYTES);
     const ncclResult_t e = R.CommInitRank(&h->comm, n_ranks, uid, rank);
@@ -2599,8 +2609,30 @@ int gd_comm_init(gd_handle* h, const uint8_t id[GD_COMM_ID_BYTES], int n_ranks, 
         comm_release(h);
         return set_err(h, GD_ERCCL, "ncclCommInitRank(%d of %d): %s", rank, n_ranks, R.GetErrorString(e));
     }
+    h->net = &R;
     h->n_ranks = n_ranks;
     h->rank = rank;
+    return GD_OK;
+}
+
+int gd_comm_init_local(gd_handle* const* hs, int n_ranks) {
+    if (!hs || n_ranks < 1 || n_ranks > 256) return set_err(nullptr, GD_EINVAL, "need 1 <= n_ranks <= 256 handles");
+    for (int r = 0; r < n_ranks; ++r) {
+        if (!hs[r]) return set_err(nullptr, GD_EINVAL, "null handle %d", r);
+        for (int q = 0; q < r; ++q)
+            if (hs[q] == hs[r]) return set_err(nullptr, GD_EINVAL, "handle %d given twice", r);
+    }
+    for (int r = 0; r < n_ranks; ++r) {
+        HIP_TRY(hs[r], hipSetDevice(hs[r]->device));
+        GD_TRY(comm_setup(hs[r]));
+    }
+    const std::vector<ncclComm_t> comms = local_comms(n_ranks);
+    for (int r = 0; r < n_ranks; ++r) {
+        hs[r]->comm = comms[r];
+        hs[r]->net = &local_net();
+        hs[r]->n_ranks = n_ranks;
+        hs[r]->rank = r;
+    }
     return GD_OK;
 }
 

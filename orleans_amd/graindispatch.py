@@ -48,7 +48,8 @@ EXPORTED_SYMBOLS = [
     "gd_route_frames_ext_device", "gd_route_frames_ext",
     "gd_dir_register_ext", "gd_dir_unregister_ext", "gd_dir_lookup_ext", "gd_uniform_hashes_ext",
     "gd_dir_ext_stats", "gd_route_ext", "gd_route_bucket_ext", "gd_route_ext_device", "gd_route_bucket_ext_device",
-    "gd_comm_unique_id", "gd_comm_init", "gd_comm_destroy", "gd_route_multi_device", "gd_route_multi",
+    "gd_comm_unique_id", "gd_comm_init", "gd_comm_init_local", "gd_comm_destroy", "gd_route_multi_device",
+    "gd_route_multi",
     "gd_multi_fetch", "gd_route_multi_ext_device", "gd_route_multi_ext", "gd_ring_owner_ext",
     "gd_dir_split_ext", "gd_dir_upsert",
 ]
@@ -243,6 +244,7 @@ def _load() -> C.CDLL:
         "gd_route_bucket_ext_device": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, U32, P, P, P, P, P]),
         "gd_comm_unique_id": (C.c_int, [P]),
         "gd_comm_init": (C.c_int, [P, P, C.c_int, C.c_int]),
+        "gd_comm_init_local": (C.c_int, [P, C.c_int]),
         "gd_comm_destroy": (C.c_int, [P]),
         "gd_route_multi_device": (C.c_int, [P, P, U32, U32, C.c_int, C.POINTER(gd_multi_result)]),
         "gd_route_multi": (C.c_int, [P, P, U32, U32, C.c_int, C.POINTER(gd_multi_result)]),
@@ -753,6 +755,13 @@ class GrainDispatch:
         assert len(unique_id) == GD_COMM_ID_BYTES
         buf = (C.c_uint8 * GD_COMM_ID_BYTES).from_buffer_copy(unique_id)
         self._c(lib.gd_comm_init(self.h, buf, n_ranks, rank))
+
+    @staticmethod
+    def comm_init_local(engines: Sequence["GrainDispatch"]):
+        """gd_comm_init_local: the engines become ranks 0..W-1 of an in-process communicator (the
+        W > 1 exchange rehearsed on one GPU; drive each engine from its own thread)."""
+        arr = (C.c_void_p * len(engines))(*[e.h.value for e in engines])
+        _check(None, lib.gd_comm_init_local(arr, len(engines)))
 
     def comm_destroy(self):
         self._c(lib.gd_comm_destroy(self.h))

@@ -138,3 +138,14 @@ def test_rccl_loads_at_run_time_and_issues_unique_ids():
     assert "librccl" not in needed
     a, b = g.GrainDispatch.comm_unique_id(), g.GrainDispatch.comm_unique_id()
     assert len(a) == g.GD_COMM_ID_BYTES == 128 and a != b
+
+
+def test_comm_init_local_rejects_bad_args():
+    """gd_comm_init_local validates its handle list before touching a device."""
+    import ctypes as C
+    from orleans_amd import graindispatch as g
+    assert g.lib.gd_comm_init_local(None, 2) == g.GD_EINVAL
+    arr = (C.c_void_p * 2)(None, None)
+    assert g.lib.gd_comm_init_local(arr, 2) == g.GD_EINVAL
+    assert g.lib.gd_comm_init_local(arr, 0) == g.GD_EINVAL
+    assert g.lib.gd_comm_init_local(arr, 257) == g.GD_EINVAL

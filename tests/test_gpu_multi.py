@@ -213,8 +213,9 @@ def test_route_multi_pipelined_batches(gd):
 
 
 class _Cai:
-    def __init__(self, ptr, n):
-        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i4", "data": (int(ptr), False), "version": 3,
+    def __init__(self, ptr, n, typestr="<i4"):
+        shape = n if isinstance(n, tuple) else (n,)
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (int(ptr), False), "version": 3,
                                          "strides": None}
 
 
@@ -433,3 +434,247 @@ def test_sharded_forward_two_ranks_one_gpu(tmp_path):
         wp, wo = o.bucket_stable(act, w.G_TOTAL)
         np.testing.assert_array_equal(res["perm"], wp)
         np.testing.assert_array_equal(res["offsets"], wo)
+
+
+# ---- W > 1 in one process (gd_comm_init_local): the library exchange at several ranks ----------
+def _run_ranks(fns):
+    """Run fns[r]() on one thread per rank; re-raise the first failure."""
+    import threading
+    out, err = [None] * len(fns), [None] * len(fns)
+
+    def body(r):
+        try:
+            out[r] = fns[r]()
+        except BaseException as ex:           # noqa: BLE001 -- re-raised below
+            err[r] = ex
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(len(fns))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=110)
+    for r, ex in enumerate(err):
+        if ex is not None:
+            raise AssertionError(f"rank {r}") from ex
+    assert all(not t.is_alive() for t in ts), "a rank did not finish"
+    return out
+
+
+def _local_world(gd, W, spec_mode, silos, reg, act, silo_of, my_silos=None):
+    """W engines on cuda:0, rank r holding the directory entries whose ring owner lives on r."""
+    spec = o.ring_spec(silos, spec_mode)
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    es = []
+    for r in range(W):
+        e = gd.GrainDispatch(device=0, table_capacity=1 << 13, my_silo=r if my_silos is None else my_silos[r])
+        e.ring_set_silos(spec_mode, [(s.ip, s.port, s.gen) for s in silos])
+        mine = own % W == r
+        e.register(reg[mine], act[mine], silo_of[mine])
+        es.append(e)
+    gd.GrainDispatch.comm_init_local(es)
+    return spec, own, es
+
+
+def _expected_owner_side(batches, spec, full, W, r):
+    """Messages rank r owns, in arrival order (sender rank, sender order), and their routes."""
+    ks, ids, srcs = [], [], []
+    for s, k in enumerate(batches):
+        _, _, _, owner, _ = o.route_batch_np(k, spec, full, my_silo=s)
+        sel = np.nonzero(np.where(owner == o.M32, s, owner % W) == r)[0]
+        ks.append(k[sel]), ids.append(sel), srcs.append(np.full(len(sel), s))
+    rk = np.concatenate(ks)
+    st, silo, act, _, _ = o.route_batch_np(rk, spec, full, my_silo=r)
+    return rk, np.concatenate(ids).astype(np.uint32), np.concatenate(srcs).astype(np.uint32), st, silo, act
+
+
+@pytest.mark.parametrize("W", [2, 3, 5])
+def test_route_multi_local_world(gd, W):
+    """gd_route_multi at W ranks (in-process transport): owner-side arrival order, routes and
+    per-activation buckets, and the routes returned to every sender in batch order."""
+    silos = o.bench_silos(8)
+    G = 6000
+    reg = o.grain_keys(TC, np.arange(G))
+    spec = o.ring_spec(silos, "D")
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    act = np.zeros(G, np.uint32)
+    for r in range(W):                     # activation ids local to the owner rank
+        act[own % W == r] = np.arange(int((own % W == r).sum()))
+    spec, own, es = _local_world(gd, W, "D", silos, reg, act, own)
+    rng = np.random.default_rng(W)
+    batches = []
+    for r in range(W):
+        k = o.grain_keys(TC, rng.integers(0, G + 400, size=int(rng.integers(0, 40000)) if r else 33333))
+        if len(k) > 50:
+            k[::41] = np.array(o.UniqueKey(0, 7, o.type_code_data(o.CAT_SYSTEM_TARGET, 1)).as_tuple(), np.uint64)
+        batches.append(k)
+    n_act = [int((own % W == r).sum()) for r in range(W)]
+    res = _run_ranks([lambda r=r: es[r].route_multi(batches[r], n_act[r], return_routes=True) for r in range(W)])
+    full = o.DirectoryArrays(reg, act, own)
+    for r in range(W):
+        rk, ids, srcs, st, silo, a = _expected_owner_side(batches, spec, full, W, r)
+        np.testing.assert_array_equal(res[r]["recv_keys"], rk)
+        np.testing.assert_array_equal(res[r]["recv_idx"], ids)
+        np.testing.assert_array_equal(res[r]["recv_src"], srcs)
+        np.testing.assert_array_equal(res[r]["status"], st)
+        np.testing.assert_array_equal(res[r]["silo"], silo)
+        np.testing.assert_array_equal(res[r]["act"], a)
+        wp, wo = o.bucket_stable(a, n_act[r])
+        np.testing.assert_array_equal(res[r]["perm"], wp)
+        np.testing.assert_array_equal(res[r]["offsets"], wo)
+        # routes back at sender r, in batch order = the owner's answer (system targets: r itself)
+        st, silo, a, _, _ = o.route_batch_np(batches[r], spec, full, my_silo=r)
+        np.testing.assert_array_equal(res[r]["ret_status"], st)
+        np.testing.assert_array_equal(res[r]["ret_silo"], silo)
+        np.testing.assert_array_equal(res[r]["ret_act"], a)
+    for e in es:
+        e.comm_destroy()
+        e.close()
+
+
+def test_route_multi_local_pipelined_and_forward(gd):
+    """W = 4: five pipelined device batches per rank (GD_MULTI_KEYS_READY, results checked one
+    call later), then the forward hop with activations away from their owners."""
+    import torch
+    W, G = 4, 5000
+    silos = o.bench_silos(8)
+    reg = o.grain_keys(TC, np.arange(G))
+    spec = o.ring_spec(silos, "V")
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    act_silo = ((5 * np.arange(G) + 1) % 8).astype(np.uint32)
+    host = act_silo % W
+    act = np.zeros(G, np.uint32)
+    for r in range(W):
+        act[host == r] = np.arange(int((host == r).sum()))
+    spec, own, es = _local_world(gd, W, "V", silos, reg, act, act_silo)
+    full = o.DirectoryArrays(reg, act, act_silo)
+    streams = [torch.cuda.Stream() for _ in range(W)]
+    for r in range(W):
+        es[r].set_stream(streams[r].cuda_stream)
+    rng = np.random.default_rng(77)
+    batches = [[o.grain_keys(TC, rng.integers(0, G + 300, size=int(rng.integers(1, 30000)))) for _ in range(5)]
+               for _ in range(W)]
+
+    def read(rp):
+        m = rp.n_recv
+        dev = lambda ptr, shape, t: torch.as_tensor(_Cai(ptr, shape, t), device="cuda").cpu().numpy()
+        return {"recv_keys": dev(rp.recv_keys, (m, 3), "<i8").view(np.uint64),
+                "recv_idx": dev(rp.recv_idx, (m,), "<i4").view(np.uint32),
+                "act": dev(rp.act, (m,), "<i4").view(np.uint32), "perm": dev(rp.perm, (m,), "<i4").view(np.uint32),
+                "offsets": dev(rp.offsets, (G + 2,), "<i4").view(np.uint32)}
+
+    def pipelined(r):
+        dk = [torch.from_numpy(b.view(np.int64).copy()).cuda() for b in batches[r]]
+        torch.cuda.synchronize()
+        got, prev = [], None
+        for i in range(6):
+            cur = None
+            if i < 5:
+                with torch.cuda.stream(streams[r]):
+                    cur = es[r].route_multi_device(dk[i].data_ptr(), len(batches[r][i]), G, keys_ready=True)
+            if prev is not None:           # batch i-1's result, read after batch i was enqueued
+                es[r].synchronize()
+                got.append(read(prev))
+            prev = cur
+        return got
+
+    res = _run_ranks([lambda r=r: pipelined(r) for r in range(W)])
+    for i in range(5):
+        for r in range(W):
+            rk, ids, srcs, st, silo, a = _expected_owner_side([batches[s][i] for s in range(W)], spec, full, W, r)
+            np.testing.assert_array_equal(res[r][i]["recv_keys"], rk, err_msg=f"batch {i} rank {r}")
+            np.testing.assert_array_equal(res[r][i]["recv_idx"], ids)
+            np.testing.assert_array_equal(res[r][i]["act"], a)
+            wp, wo = o.bucket_stable(a, G)
+            np.testing.assert_array_equal(res[r][i]["perm"], wp)
+            np.testing.assert_array_equal(res[r][i]["offsets"], wo)
+    # forward hop: each message ends on its activation's rank (hits) or its owner (the rest)
+    n_act = [int((host == r).sum()) for r in range(W)]
+    fb = [batches[r][0] for r in range(W)]
+    res = _run_ranks([lambda r=r: es[r].route_multi(fb[r], n_act[r], forward=True) for r in range(W)])
+    expect = {r: [] for r in range(W)}
+    for s in range(W):
+        st, silo, a, owner, _ = o.route_batch_np(fb[s], spec, full, my_silo=s)
+        orank = np.where(owner == o.M32, s, owner % W)
+        final = np.where(st == o.ST_OK, silo % W, orank)
+        for i in range(len(fb[s])):
+            expect[int(final[i])].append((int(orank[i]), s, i))
+    for r in range(W):
+        ex = sorted(expect[r])
+        np.testing.assert_array_equal(res[r]["recv_src"], np.array([x[1] for x in ex], np.uint32))
+        np.testing.assert_array_equal(res[r]["recv_idx"], np.array([x[2] for x in ex], np.uint32))
+        rk = np.array([fb[x[1]][x[2]] for x in ex], np.uint64).reshape(-1, 3)
+        np.testing.assert_array_equal(res[r]["recv_keys"], rk)
+        st, silo, a, _, _ = o.route_batch_np(rk, spec, full, my_silo=r)
+        np.testing.assert_array_equal(res[r]["status"], st)
+        np.testing.assert_array_equal(res[r]["act"], a)
+        wp, wo = o.bucket_stable(a, n_act[r])
+        np.testing.assert_array_equal(res[r]["perm"], wp)
+        np.testing.assert_array_equal(res[r]["offsets"], wo)
+    for e in es:
+        e.comm_destroy()
+        e.close()
+
+
+def test_route_multi_ext_local_world(gd):
+    """gd_route_multi_ext at W = 3: KeyExt grains go to the rank owning their KeyExt hash with
+    their strings (byte round), host-kept and system-target messages stay with their sender."""
+    import keyext as kx
+    W, G = 3, 3000
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "R")
+    reg = o.grain_keys(TC, np.arange(G))
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    spec, own, es = _local_world(gd, W, "R", silos, reg, np.arange(G, dtype=np.uint32), own)
+    stc = o.grain_type_code("UnitTests.GrainInterfaces.IStringKeyGrain")
+    tcd = o.type_code_data(o.CAT_KEYEXT_GRAIN, stc)
+    names = [(f"user/{i}" + "ü" * (i % 5) + "q" * (i % 40)).encode() for i in range(500)]
+    kxd = kx.KeyExtDirectory()
+    for i, nm in enumerate(names[:300]):
+        owner = int(o.ring_owner_np(spec, np.array([kx.ext_uniform_hash(0, 0, tcd, nm)], np.uint32))[0])
+        kxd.add_single_activation((0, 0, tcd), nm, G + i, owner)
+        es[owner % W].register_ext(np.array([[0, 0, tcd]], np.uint64), [nm], [G + i], [owner])
+    rng = np.random.default_rng(31)
+    batches, exts = [], []
+    for r in range(W):
+        n = 20000 + 777 * r
+        k = o.grain_keys(TC, rng.integers(0, G + 200, size=n))
+        x = [None] * n
+        for i in np.nonzero(rng.random(n) < 0.35)[0]:
+            k[i] = (0, 0, tcd)
+            x[i] = names[int(rng.integers(0, 500))] if i % 89 else kx.EXT_HOST
+        k[5::211] = np.array(o.UniqueKey(0, 7, o.type_code_data(o.CAT_SYSTEM_TARGET, 1)).as_tuple(), np.uint64)
+        for i in range(5, n, 211):
+            x[i] = None
+        batches.append(k)
+        exts.append(x)
+    bx = [[gd.GD_KEYEXT_HOST if (isinstance(v, str) and v == kx.EXT_HOST) else v for v in x] for x in exts]
+    res = _run_ranks([lambda r=r: es[r].route_multi_ext(batches[r], bx[r], G + 300, return_routes=True)
+                      for r in range(W)])
+    full = o.DirectoryArrays(reg, np.arange(G), own)
+    kx_ok = 0
+    for r in range(W):
+        ks, xs, ids, srcs = [], [], [], []
+        for s in range(W):
+            _, _, _, owner, _ = kx.route_batch_ext(batches[s], exts[s], spec, full, kxd, my_silo=s)
+            sel = np.nonzero(np.where(owner == o.M32, s, owner % W) == r)[0]
+            ks.append(batches[s][sel]), ids.append(sel), srcs.append(np.full(len(sel), s))
+            xs += [exts[s][i] for i in sel]
+        rk = np.concatenate(ks)
+        np.testing.assert_array_equal(res[r]["recv_keys"], rk)
+        np.testing.assert_array_equal(res[r]["recv_idx"], np.concatenate(ids).astype(np.uint32))
+        np.testing.assert_array_equal(res[r]["recv_src"], np.concatenate(srcs).astype(np.uint32))
+        st, silo, a, _, _ = kx.route_batch_ext(rk, xs, spec, full, kxd, my_silo=r)
+        np.testing.assert_array_equal(res[r]["status"], st)
+        np.testing.assert_array_equal(res[r]["silo"], silo)
+        np.testing.assert_array_equal(res[r]["act"], a)
+        wp, wo = o.bucket_stable(a, G + 300)
+        np.testing.assert_array_equal(res[r]["perm"], wp)
+        np.testing.assert_array_equal(res[r]["offsets"], wo)
+        kx_ok += int(((st == o.ST_OK) & (rk[:, 2] == np.uint64(tcd))).sum())
+        st, silo, a, _, _ = kx.route_batch_ext(batches[r], exts[r], spec, full, kxd, my_silo=r)
+        np.testing.assert_array_equal(res[r]["ret_status"], st)
+        np.testing.assert_array_equal(res[r]["ret_act"], a)
+    assert kx_ok > 5000            # string-keyed hits were routed on their (remote) owners
+    for e in es:
+        e.comm_destroy()
+        e.close()
