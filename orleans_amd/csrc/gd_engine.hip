@@ -114,7 +114,7 @@ struct gd_handle {
     DevBuf x_scratch[4];              // xstream's own scan partials + partition scratch
     DevBuf p_scratch[4];              // pstream's
     uint32_t* h_xcnt = nullptr;       // pinned: send/recv message counts, send/recv KeyExt byte counts,
-                                      // send/recv forward counts (6 x 256)
+                                      // key descriptors (mine, every peer's), forward counts (12 x 256)
     gd_multi_result mres[2] = {};
     uint32_t mres_n[2] = {0, 0};
     uint64_t mcalls = 0;
@@ -126,6 +126,7 @@ struct gd_handle {
     int radix_max_bits = 8;   // digit width cap (GD_RADIX_MAXBITS, 4..11)
     int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
+    bool compact_headers = true;   // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
     bool fused_starts = true;   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
 
@@ -518,31 +519,37 @@ int maybe_grow_table(gd_handle* h, uint64_t incoming) {
 // ---- exchange partition (gd_shard.h) -------------------------------------------------
 template <int MODE, bool NODES>
 int shard_hist_t(gd_handle* h, const void* recs, uint32_t n, uint64_t tcd, uint32_t n_shards, uint32_t bits,
-                 uint32_t tiles, uint8_t* dest, uint32_t* hist, const ExtArgs& ext) {
+                 uint32_t tiles, uint8_t* dest, uint32_t* hist, const ExtArgs& ext, uint32_t* kdesc) {
     return launch(h, "k_shard_hist", dim3(tiles), dim3(SH_NT), ring_lds(h), k_shard_hist<MODE, NODES>, recs, n, tcd,
-                  ring_args(h), n_shards, bits, tiles, dest, hist, ext);
+                  ring_args(h), n_shards, bits, tiles, dest, hist, ext, kdesc);
 }
 
 template <int BITS, bool NODES>
 int shard_scatter_t(gd_handle* h, const void* recs, const uint32_t* payload, const uint8_t* dest, uint32_t n,
-                    uint32_t n_shards, uint32_t tiles, const uint32_t* gscan, void* out, uint32_t* out_pay) {
+                    uint32_t n_shards, uint32_t tiles, const uint32_t* gscan, void* out, uint32_t* out_pay,
+                    const uint32_t* kdesc) {
     return launch(h, "k_shard_scatter", dim3(tiles), dim3(SH_NT), 0, k_shard_scatter<BITS, NODES>, recs, payload, dest,
-                  n, n_shards, tiles, gscan, out, out_pay);
+                  n, n_shards, tiles, gscan, out, out_pay, kdesc);
 }
 
 template <bool NODES>
 int shard_finish(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t n, uint32_t n_shards, uint32_t bits,
                  uint32_t tiles, const uint8_t* dest, uint32_t* hist, void* out_recs, uint32_t* out_pay,
-                 uint32_t* counts);
+                 uint32_t* counts, const uint32_t* kdesc = nullptr);
 
 // Stable partition of n records (gd_key or u32 node ids) by destination rank, payload alongside
-// (payload == nullptr: the batch index); counts[d] per destination.
+// (payload == nullptr: the batch index); counts[d] per destination.  kdesc != nullptr (keys): the
+// header-compaction descriptor (k_key_desc) is built, and a compact batch is written as N1 only.
 template <bool NODES>
 int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t n, uint64_t tcd, uint32_t n_shards,
-               void* out_recs, uint32_t* out_pay, uint32_t* counts, const ExtArgs& ext = ExtArgs{}) {
+               void* out_recs, uint32_t* out_pay, uint32_t* counts, const ExtArgs& ext = ExtArgs{},
+               uint32_t* kdesc = nullptr) {
     GD_TRY(check_ring(h));
-    if (n == 0)
+    if (kdesc) HIP_TRY(h, hipMemsetAsync(kdesc, 0, 16, h->stream));
+    if (n == 0) {
+        if (kdesc) GD_TRY(launch(h, "k_key_desc", dim3(1), dim3(64), 0, k_key_desc, (const gd_key*)recs, n, kdesc));
         return launch(h, "k_fill", dim3(1), dim3(BLOCK), 0, k_fill_u32, counts, n_shards, 0u);
+    }
     const uint32_t tiles = blocks_for(n, SH_TILE);
     if ((uint64_t)tiles * n_shards > 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "batch too large to partition");
     GD_TRY(ensure(h, h->shard_dest, (size_t)n));
@@ -553,15 +560,17 @@ int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t
     while ((1u << bits) < n_shards) ++bits;
     switch (h->ring_mode) {
         case GD_RING_DIRECTORY:
-            GD_TRY((shard_hist_t<GD_RING_DIRECTORY, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext)));
+            GD_TRY((shard_hist_t<GD_RING_DIRECTORY, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext, kdesc)));
             break;
         case GD_RING_CONSISTENT:
-            GD_TRY((shard_hist_t<GD_RING_CONSISTENT, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext)));
+            GD_TRY((shard_hist_t<GD_RING_CONSISTENT, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext, kdesc)));
             break;
         default:
-            GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext)));
+            GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext, kdesc)));
     }
-    return shard_finish<NODES>(h, recs, payload, n, n_shards, bits, tiles, dest, hist, out_recs, out_pay, counts);
+    if (kdesc) GD_TRY(launch(h, "k_key_desc", dim3(1), dim3(64), 0, k_key_desc, (const gd_key*)recs, n, kdesc));
+    return shard_finish<NODES>(h, recs, payload, n, n_shards, bits, tiles, dest, hist, out_recs, out_pay, counts,
+                               kdesc);
 }
 
 // Forward partition of routed messages by the rank hosting their activation (k_fwd_hist): keys
@@ -586,20 +595,28 @@ int fwd_pack(gd_handle* h, const gd_key* keys, const uint8_t* st, const uint32_t
 template <bool NODES>
 int shard_finish(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t n, uint32_t n_shards, uint32_t bits,
                  uint32_t tiles, const uint8_t* dest, uint32_t* hist, void* out_recs, uint32_t* out_pay,
-                 uint32_t* counts) {
+                 uint32_t* counts, const uint32_t* kdesc) {
     GD_TRY(scan_device<OpAdd>(h, hist, tiles * n_shards, false, false, "shard"));
     GD_TRY(launch(h, "k_shard_counts", dim3(1), dim3(256), 0, k_shard_counts, (const uint32_t*)hist, tiles, n_shards, n,
                   counts));
     const uint32_t* gs = hist;
     switch (bits) {
-        case 1: return shard_scatter_t<1, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
-        case 2: return shard_scatter_t<2, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
-        case 3: return shard_scatter_t<3, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
-        case 4: return shard_scatter_t<4, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
-        case 5: return shard_scatter_t<5, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
-        case 6: return shard_scatter_t<6, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
-        case 7: return shard_scatter_t<7, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
-        default: return shard_scatter_t<8, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay);
+        case 1: return shard_scatter_t<1, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay,
+                                                   kdesc);
+        case 2: return shard_scatter_t<2, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay,
+                                                   kdesc);
+        case 3: return shard_scatter_t<3, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay,
+                                                   kdesc);
+        case 4: return shard_scatter_t<4, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay,
+                                                   kdesc);
+        case 5: return shard_scatter_t<5, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay,
+                                                   kdesc);
+        case 6: return shard_scatter_t<6, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay,
+                                                   kdesc);
+        case 7: return shard_scatter_t<7, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay,
+                                                   kdesc);
+        default: return shard_scatter_t<8, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay,
+                                                  kdesc);
     }
 }
 
@@ -628,6 +645,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
     if (const char* v = std::getenv("GD_RADIX_RANK")) h->radix_rank_atomic = std::atoi(v) ? 1u : 0u;
     if (const char* v = std::getenv("GD_FUSED_STARTS")) h->fused_starts = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_COMPACT_HEADERS")) h->compact_headers = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_XCD_TILES")) h->xcd_tiles = std::atoi(v) ? 1u : 0u;
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
@@ -2252,7 +2270,7 @@ int comm_setup(gd_handle* h) {
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(sync(h));
     comm_release(h);
-    HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 6 * 256 * sizeof(uint32_t)));
+    HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 12 * 256 * sizeof(uint32_t)));
     HIP_TRY(h, hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
     HIP_TRY(h, hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking));
     for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
@@ -2286,6 +2304,8 @@ struct Lane {
     size_t elem;            // bytes per element
     ncclDataType_t type;
     size_t per;             // elements of `type` per element
+    const uint64_t* sb = nullptr;   // set: per-peer byte ranges [sb[r], sb[r+1]) sent to r and
+    const uint64_t* rb = nullptr;   // [rb[r], rb[r+1]) received from r (compact headers)
 };
 
 int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uint64_t* soff, const uint32_t* rc,
@@ -2301,12 +2321,22 @@ int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uin
     for (int r = 0; r < h->n_ranks; ++r) {
         for (int l = 0; l < n_lanes; ++l) {
             const Lane& L = lanes[l];
-            if (sc[r])
-                NCCL_TRY(h, R.Send((const uint8_t*)L.send + soff[r] * L.elem, (size_t)sc[r] * L.per, L.type, r,
-                                   h->comm, h->stream));
-            if (rc[r])
-                NCCL_TRY(h, R.Recv((uint8_t*)L.recv + roff[r] * L.elem, (size_t)rc[r] * L.per, L.type, r, h->comm,
-                                   h->stream));
+            if (sc[r]) {
+                if (L.sb)
+                    NCCL_TRY(h, R.Send((const uint8_t*)L.send + L.sb[r], (size_t)(L.sb[r + 1] - L.sb[r]), ncclUint8, r,
+                                       h->comm, h->stream));
+                else
+                    NCCL_TRY(h, R.Send((const uint8_t*)L.send + soff[r] * L.elem, (size_t)sc[r] * L.per, L.type, r,
+                                       h->comm, h->stream));
+            }
+            if (rc[r]) {
+                if (L.rb)
+                    NCCL_TRY(h, R.Recv((uint8_t*)L.recv + L.rb[r], (size_t)(L.rb[r + 1] - L.rb[r]), ncclUint8, r,
+                                       h->comm, h->stream));
+                else
+                    NCCL_TRY(h, R.Recv((uint8_t*)L.recv + roff[r] * L.elem, (size_t)rc[r] * L.per, L.type, r,
+                                       h->comm, h->stream));
+            }
         }
     }
     NCCL_TRY(h, R.GroupEnd());
@@ -2332,7 +2362,7 @@ int forward_multi(gd_handle* h, int s, uint32_t n_act, gd_multi_result& r) {
     const size_t want_s[8] = {(size_t)m * sizeof(gd_key) + 8, m4, m4, m4, m4, m4, (size_t)m + 4, (size_t)W * 8};
     for (int b = 0; b < 8; ++b) GD_TRY(grow(h, F[b], want_s[b]));
     uint32_t* fcnt = (uint32_t*)F[7].p;           // send [0,W), recv [W,2W)
-    uint32_t* hc = h->h_xcnt + 4 * 256;
+    uint32_t* hc = h->h_xcnt + 10 * 256;
     HIP_TRY(h, hipStreamWaitEvent(h->xstream, h->x_route[s], 0));
     {
         OnXStream on(h);
@@ -2416,7 +2446,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     //    buffers once batch i-2's rounds have read them; it runs beside batch i-1's header round
     GD_TRY(grow(h, SB[0], (size_t)n * sizeof(gd_key) + 8));
     GD_TRY(grow(h, SB[1], (size_t)n * 4 + 4));
-    GD_TRY(grow(h, SB[2], (size_t)W * 16));
+    GD_TRY(grow(h, SB[2], ((size_t)W * 8 + 4) * 4));
     if (has_ext) {
         GD_TRY(grow(h, SB[3], (size_t)n * 4 + 4));
         GD_TRY(grow(h, SB[4], (size_t)n * 4 + 4));
@@ -2428,12 +2458,17 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     if (h->x_sent_rec[s]) HIP_TRY(h, hipStreamWaitEvent(h->pstream, h->x_sent[s], 0));
     gd_key* send_keys = (gd_key*)SB[0].p;
     uint32_t* send_idx = (uint32_t*)SB[1].p;
-    uint32_t* dcnt = (uint32_t*)SB[2].p;           // send msgs [0,W), recv msgs [W,2W), send bytes, recv bytes
+    // send msgs [0,W), recv msgs [W,2W), send bytes, recv bytes, my key descriptor [4W,4W+4) (k_key_desc),
+    // the peers' descriptors [4W+4, 8W+4)
+    uint32_t* dcnt = (uint32_t*)SB[2].p;
+    uint32_t* kdesc = dcnt + 4 * W;
     int32_t* send_len = (int32_t*)SB[3].p;
     uint32_t* send_boff = (uint32_t*)SB[4].p;
     {
         OnPStream on(h);
-        GD_TRY(shard_pack<false>(h, d_keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt, x));
+        GD_TRY(shard_pack<false>(h, d_keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt, x,
+                                 h->compact_headers ? kdesc : nullptr));
+        if (!h->compact_headers) HIP_TRY(h, hipMemsetAsync(kdesc, 0, 16, h->stream));
         if (has_ext) {                 // KeyExt bytes per destination; lengths and byte offsets in send order
             HIP_TRY(h, hipMemsetAsync(dcnt + 2 * W, 0, (size_t)W * 4, h->stream));
             GD_TRY(launch(h, "k_dest_bytes", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_dest_bytes,
@@ -2452,13 +2487,15 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         for (int r = 0; r < W; ++r) {
             NCCL_TRY(h, R.Send(dcnt + r, 1, ncclUint32, r, h->comm, h->stream));
             NCCL_TRY(h, R.Recv(dcnt + W + r, 1, ncclUint32, r, h->comm, h->stream));
+            NCCL_TRY(h, R.Send(kdesc, 4, ncclUint32, r, h->comm, h->stream));
+            NCCL_TRY(h, R.Recv(kdesc + 4 + 4 * r, 4, ncclUint32, r, h->comm, h->stream));
             if (has_ext) {
                 NCCL_TRY(h, R.Send(dcnt + 2 * W + r, 1, ncclUint32, r, h->comm, h->stream));
                 NCCL_TRY(h, R.Recv(dcnt + 3 * W + r, 1, ncclUint32, r, h->comm, h->stream));
             }
         }
         NCCL_TRY(h, R.GroupEnd());
-        HIP_TRY(h, hipMemcpyAsync(h->h_xcnt, dcnt, (size_t)W * (has_ext ? 16 : 8), hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipMemcpyAsync(h->h_xcnt, dcnt, ((size_t)W * 8 + 4) * 4, hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(h, hipStreamSynchronize(h->stream));
     }
     ncclResult_t async_err = ncclSuccess;
@@ -2483,13 +2520,25 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         return set_err(h, GD_EINVAL, "%llu messages / %llu KeyExt bytes received: more than a batch can hold",
                        (unsigned long long)roff[W], (unsigned long long)rboff[W]);
     const uint32_t m = (uint32_t)roff[W];
+    // header bytes per peer: 8 (N1 only) when that side's batch is compact (k_key_desc), else 24
+    const uint32_t* hd = h->h_xcnt + 4 * W;        // my descriptor, then the peers'
+    const uint64_t my_esz = hd[0] ? 8 : 24;
+    std::vector<uint64_t> hsb(W + 1, 0), hrb(W + 1, 0);
+    bool any_compact = false;
+    for (int r = 0; r < W; ++r) {
+        const bool c = hd[4 + 4 * r] != 0;
+        any_compact |= c && rc[r];
+        hsb[r + 1] = hsb[r] + sc[r] * my_esz;
+        hrb[r + 1] = hrb[r] + rc[r] * (c ? 8 : 24);
+    }
     // 2. this parity's buffers: batch i-2 must be done with them (probe/bucket and routes round)
     const size_t m4 = (size_t)m * 4 + 4, n4 = (size_t)n * 4 + 4;
     const size_t want[20] = {(size_t)m * sizeof(gd_key) + 8, m4, m4, m4, m4, (size_t)m + 4, m4,
                              ((size_t)n_act + 2) * 4, n4, n4, (size_t)n + 4, n4, n4, (size_t)n + 4,
-                             m4, (size_t)rboff[W] + 16, m4, (size_t)m * 8 + 8, 0, 0};
+                             m4, (size_t)rboff[W] + 16, m4, (size_t)m * 8 + 8, (size_t)hrb[W] + 16, 0};
     for (int b = 0; b < 20; ++b)
-        if (want[b] && (b < 8 || (ret && b < 14) || (has_ext && b >= 14))) GD_TRY(grow(h, B[b], want[b]));
+        if (want[b] && (b < 8 || (ret && b < 14) || (has_ext && b >= 14 && b < 18) || (any_compact && b == 18)))
+            GD_TRY(grow(h, B[b], want[b]));
     if (has_ext) GD_TRY(grow(h, SB[5], (size_t)sboff[W] + 16));
     gd_key* recv_keys = (gd_key*)B[0].p;
     uint32_t* recv_idx = (uint32_t*)B[1].p;
@@ -2505,7 +2554,10 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         if (has_ext)
             GD_TRY(launch(h, "k_gather_ext", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_gather_ext,
                           (const uint32_t*)send_idx, n, x, (const uint32_t*)send_boff, (uint8_t*)SB[5].p));
-        const Lane lanes[3] = {{send_keys, recv_keys, sizeof(gd_key), ncclUint64, 3},
+        // keys: byte ranges per peer (compact chunks are 8 B a header); with any compact peer they
+        // land in a staging buffer that k_recv_expand turns back into 24-B keys
+        const Lane lanes[3] = {{send_keys, any_compact ? B[18].p : (void*)recv_keys, 1, ncclUint8, 1, hsb.data(),
+                                hrb.data()},
                                {send_idx, recv_idx, 4, ncclUint32, 1},
                                {send_len, B[14].p, 4, ncclInt32, 1}};
         GD_TRY(exchange_round(h, "rccl_headers", sc.data(), soff.data(), rc.data(), roff.data(), lanes,
@@ -2519,8 +2571,13 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
             GD_TRY(launch(h, "k_u32_to_u64", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_u32_to_u64,
                           (const uint32_t*)B[16].p, m, (uint64_t*)B[17].p));
         }
-        GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
-                      (const uint32_t*)(dcnt + W), (uint32_t)W, m, recv_src));
+        if (any_compact)
+            GD_TRY(launch(h, "k_recv_expand", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_expand,
+                          (const uint8_t*)B[18].p, (const uint32_t*)(dcnt + W), (const uint32_t*)(kdesc + 4),
+                          (uint32_t)W, m, recv_keys, recv_src));
+        else
+            GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
+                          (const uint32_t*)(dcnt + W), (uint32_t)W, m, recv_src));
         HIP_TRY(h, hipEventRecord(h->x_hdr[s], h->xstream));
         if (!ret) {                    // this parity's send buffers are free for batch i+2's partition
             HIP_TRY(h, hipEventRecord(h->x_sent[s], h->xstream));

@@ -63,7 +63,8 @@ template <int MODE, bool NODES>
 __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ recs, uint32_t n, uint64_t tcd,
                                                       RingArgs ring, uint32_t n_shards, uint32_t bits,
                                                       uint32_t tiles, uint8_t* __restrict__ dest,
-                                                      uint32_t* __restrict__ hist, ExtArgs ext) {
+                                                      uint32_t* __restrict__ hist, ExtArgs ext,
+                                                      uint32_t* __restrict__ kdesc) {
     constexpr int NW = SH_NT / WAVE;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     __shared__ uint32_t s_wc[NW][256];
@@ -76,6 +77,11 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
     const uint32_t base = blockIdx.x * SH_TILE;
     const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     const unsigned long long lt = (1ull << lane) - 1ull;
+    // header compaction (kdesc != nullptr): does every key have N0 == 0 and the first key's TCD?
+    uint64_t ref_tcd = 0;
+    if constexpr (!NODES)
+        if (kdesc && n) ref_tcd = reinterpret_cast<const uint64_t*>(recs)[2];
+    bool wide = false;
 #pragma unroll
     for (int r = 0; r < SH_IT; ++r) {
         const uint32_t i = base + (w * SH_IT + r) * WAVE + lane;
@@ -88,6 +94,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
             } else {
                 const uint64_t* kp = reinterpret_cast<const uint64_t*>(recs) + 3ull * i;
                 d = key_dest<MODE>(kp[0], kp[1], kp[2], s_pts, s_own, ring, n_shards, ext, i);
+                wide |= kp[0] != 0 || kp[2] != ref_tcd;
             }
             dest[i] = (uint8_t)d;
         }
@@ -99,6 +106,8 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
         }
         if (valid && (peers & lt) == 0) s_wc[w][d] += (uint32_t)__popcll(peers);
     }
+    if constexpr (!NODES)
+        if (kdesc && __ballot(wide) && lane == 0) atomicOr(&kdesc[1], 1u);
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < n_shards; d += SH_NT) {
         uint32_t t = 0;
@@ -106,6 +115,69 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
         for (int ww = 0; ww < NW; ++ww) t += s_wc[ww][d];
         hist[d * tiles + blockIdx.x] = t;
     }
+}
+
+// Header compaction for the exchange (gd_route_multi*): a batch whose keys all have N0 == 0 and one
+// TypeCodeData -- long-keyed grains of one type (GrainId.GetGrainId(typeCode, long), GrainId.cs:
+// 72-77), the common case -- sends 8 B (N1) per header instead of 24.  kdesc = {compact, wide flag
+// (k_shard_hist), TCD lo, TCD hi}: the descriptor every peer receives with the counts.
+__global__ void k_key_desc(const gd_key* __restrict__ keys, uint32_t n, uint32_t* __restrict__ kdesc) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint64_t tcd = n ? reinterpret_cast<const uint64_t*>(keys)[2] : 0ull;
+    kdesc[0] = kdesc[1] == 0u ? 1u : 0u;
+    kdesc[2] = (uint32_t)tcd;
+    kdesc[3] = (uint32_t)(tcd >> 32);
+}
+
+// Receiver of a header round where some peer sent compact headers: raw = the peers' chunks back to
+// back (8 B or 24 B per header by each peer's descriptor); rebuild the 24-B keys and the sender
+// rank of every received message (k_recv_src's job otherwise).
+__global__ void __launch_bounds__(BLOCK) k_recv_expand(const uint8_t* __restrict__ raw,
+                                                       const uint32_t* __restrict__ rcount,
+                                                       const uint32_t* __restrict__ rdesc, uint32_t world,
+                                                       uint32_t m, gd_key* __restrict__ keys,
+                                                       uint32_t* __restrict__ src) {
+    __shared__ uint32_t s_off[257];
+    __shared__ uint64_t s_boff[256];
+    __shared__ uint64_t s_tcd[256];
+    __shared__ uint32_t s_compact[256];
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        uint64_t brun = 0;
+        for (uint32_t r = 0; r < world; ++r) {
+            const uint32_t c = rdesc[4 * r];
+            s_off[r] = run;
+            s_boff[r] = brun;
+            s_compact[r] = c;
+            s_tcd[r] = (uint64_t)rdesc[4 * r + 2] | ((uint64_t)rdesc[4 * r + 3] << 32);
+            run += rcount[r];
+            brun += (uint64_t)rcount[r] * (c ? 8u : 24u);
+        }
+        s_off[world] = run;
+    }
+    __syncthreads();
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= m) return;
+    uint32_t lo = 0, hi = world;          // largest r with s_off[r] <= i
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_off[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    const uint64_t j = i - s_off[lo];
+    uint64_t* out = reinterpret_cast<uint64_t*>(keys + i);
+    if (s_compact[lo]) {
+        const uint64_t n1 = reinterpret_cast<const uint64_t*>(raw + s_boff[lo])[j];
+        out[0] = 0;
+        out[1] = n1;
+        out[2] = s_tcd[lo];
+    } else {
+        const uint64_t* kp = reinterpret_cast<const uint64_t*>(raw + s_boff[lo]) + 3 * j;
+        out[0] = kp[0];
+        out[1] = kp[1];
+        out[2] = kp[2];
+    }
+    src[i] = lo;
 }
 
 // Forward partition (SURVEY 8 e, the owner != activation silo case): after the probe on the owner,
@@ -180,7 +252,8 @@ __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict_
                                                          uint32_t n_shards, uint32_t tiles,
                                                          const uint32_t* __restrict__ gscan,
                                                          void* __restrict__ out_recs,
-                                                         uint32_t* __restrict__ out_payload) {
+                                                         uint32_t* __restrict__ out_payload,
+                                                         const uint32_t* __restrict__ kdesc) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = SH_NT / WAVE;
     constexpr int RW = NODES ? 1 : 3;           // 8-B words per record (keys) / one u32 (nodes)
@@ -284,6 +357,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict_
         }
     }
     __syncthreads();
+    const bool compact = !NODES && kdesc && kdesc[0];   // headers as N1 only (k_key_desc)
 #pragma unroll
     for (int j = 0; j < SH_IT; ++j) {
         const uint32_t p = j * SH_NT + threadIdx.x;
@@ -293,6 +367,8 @@ __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict_
             if (g < n) {            // always true when the scan is right; never write out of bounds
                 if constexpr (NODES) {
                     reinterpret_cast<uint32_t*>(out_recs)[g] = s_node[p];
+                } else if (compact) {
+                    reinterpret_cast<uint64_t*>(out_recs)[g] = s_key[1][p];
                 } else {
                     uint64_t* o = reinterpret_cast<uint64_t*>(out_recs) + 3ull * g;
                     o[0] = s_key[0][p];

@@ -678,3 +678,55 @@ def test_route_multi_ext_local_world(gd):
     for e in es:
         e.comm_destroy()
         e.close()
+
+
+@pytest.mark.parametrize("compact", ["1", "0"])
+def test_route_multi_local_mixed_headers(gd, compact, monkeypatch):
+    """Exchange header compaction: a batch of one grain type with long keys travels as 8-B N1s
+    (k_key_desc / k_recv_expand).  Ranks here send: one type (compact), another type (compact,
+    other TCD), guid grains mixed in (full 24-B headers), nothing at all; with compaction off
+    (GD_COMPACT_HEADERS=0) everything goes as 24 B.  The results are identical either way."""
+    monkeypatch.setenv("GD_COMPACT_HEADERS", compact)
+    W = 4
+    silos = o.bench_silos(8)
+    tc2 = o.grain_type_code("UnitTests.Grains.SimpleGrain")
+    ka = o.grain_keys(TC, np.arange(3000))
+    kb = o.grain_keys(tc2, np.arange(2000))
+    kg = np.array([o.guid_key(f"0d2b3e5a-1111-4c3b-9f4e-aa{i:010d}", o.CAT_GRAIN, TC).as_tuple() for i in range(300)],
+                  np.uint64)
+    reg = np.concatenate([ka, kb, kg])
+    spec = o.ring_spec(silos, "D")
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    act = np.zeros(len(reg), np.uint32)
+    for r in range(W):
+        act[own % W == r] = np.arange(int((own % W == r).sum()))
+    spec, own, es = _local_world(gd, W, "D", silos, reg, act, own)
+    rng = np.random.default_rng(8)
+    batches = [ka[rng.integers(0, 3000, size=25000)],
+               np.concatenate([kb, o.grain_keys(tc2, np.arange(5000, 5100))])[rng.integers(0, 2100, size=17000)],
+               reg[rng.integers(0, len(reg), size=21000)],
+               np.zeros((0, 3), np.uint64)]
+    n_act = [int((own % W == r).sum()) for r in range(W)]
+    for e in es:
+        e.set_kernel_timing(True)
+    res = _run_ranks([lambda r=r: es[r].route_multi(batches[r], n_act[r], return_routes=True) for r in range(W)])
+    # every rank receives from the compact ranks 0 and 1 unless compaction is off
+    for e in es:
+        assert ("k_recv_expand" in e.kernel_times()) == (compact == "1")
+    full = o.DirectoryArrays(reg, act, own)
+    for r in range(W):
+        rk, ids, srcs, st, silo, a = _expected_owner_side(batches, spec, full, W, r)
+        np.testing.assert_array_equal(res[r]["recv_keys"], rk)
+        np.testing.assert_array_equal(res[r]["recv_idx"], ids)
+        np.testing.assert_array_equal(res[r]["recv_src"], srcs)
+        np.testing.assert_array_equal(res[r]["status"], st)
+        np.testing.assert_array_equal(res[r]["act"], a)
+        wp, wo = o.bucket_stable(a, n_act[r])
+        np.testing.assert_array_equal(res[r]["perm"], wp)
+        np.testing.assert_array_equal(res[r]["offsets"], wo)
+        st, silo, a, _, _ = o.route_batch_np(batches[r], spec, full, my_silo=r)
+        np.testing.assert_array_equal(res[r]["ret_status"], st)
+        np.testing.assert_array_equal(res[r]["ret_act"], a)
+    for e in es:
+        e.comm_destroy()
+        e.close()
