@@ -172,9 +172,13 @@ def main():
             dist.all_reduce(agree, op=dist.ReduceOp.MIN)
             if int(agree.item()) == 1:
                 # keys are resident and complete: batch i+1's exchange overlaps batch i's probe + bucket
+                # timed batches: messages are known by (sender, index); the probe reads the compact
+                # 8-B headers as they arrive and no 24-B key copy is rebuilt (GD_MULTI_NO_KEYS)
                 router = lib_router
                 lib_router.keys_ready = True
-                exchange = "libgraindispatch gd_route_multi_device (grouped RCCL send/recv)"
+                lib_router.no_keys = True
+                exchange = ("libgraindispatch gd_route_multi_device (grouped RCCL send/recv, compact headers, "
+                            "GD_MULTI_NO_KEYS)")
             else:
                 exchange = "torch.distributed all_to_all_single (RCCL); library exchange disagreed on batch 1"
                 assert args.exchange != "library", "library exchange disagrees with the torch exchange"
@@ -213,7 +217,7 @@ def main():
     value = total_msgs / wall_max
 
     # received (owner-side) message count, for the byte model
-    m_recv = int(res.recv_keys.shape[0])
+    m_recv = int(res.status.shape[0])
     st_ok = int((res.status == 0).sum().item())
 
     # ---- per-kernel durations (separate steps, HIP events around every launch) -----

@@ -100,7 +100,7 @@ struct gd_handle {
     hipStream_t xstream = nullptr;
     hipStream_t pstream = nullptr;    // the partition (pack) of the next batch, beside this one's rounds
     hipEvent_t x_in = nullptr, x_hdr[2] = {}, x_route[2] = {}, x_ret[2] = {}, x_done[2] = {};
-    hipEvent_t p_packed = nullptr, x_sent[2] = {}, x_fwd[2] = {};
+    hipEvent_t p_packed = nullptr, x_sent[2] = {}, x_fwd[2] = {}, x_keys[2] = {};
     bool x_done_rec[2] = {false, false}, x_sent_rec[2] = {false, false};
     DevBuf mx_send[2][6];             // per batch parity: send keys, send idx, counts (send/recv messages,
                                       // send/recv KeyExt bytes: 4 x [W]), KeyExt lengths, KeyExt byte
@@ -287,7 +287,27 @@ unsigned long long pow2_at_least(unsigned long long x) {
 template <int MODE, int M, bool NT>
 int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
     return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h), k_route_m<MODE, M, NT>, keys,
-                  n, ring_args(h), table_args(h), silo, act, status);
+                  n, ring_args(h), table_args(h), silo, act, status, 0ull);
+}
+
+// Keys given as N1 alone with one TypeCodeData (a compact exchange receive); not in cache mode.
+int route_n1_device(gd_handle* h, const uint64_t* n1s, uint64_t tcd, uint32_t n, uint32_t* silo, uint32_t* act,
+                    uint8_t* status) {
+    GD_TRY(check_ring(h));
+    h->routed += n;
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    const gd_key* k = reinterpret_cast<const gd_key*>(n1s);
+    switch (h->ring_mode) {
+        case GD_RING_DIRECTORY:
+            return launch(h, "k_route", g, b, ring_lds(h), k_route_m<GD_RING_DIRECTORY, 1, false, true>, k, n,
+                          ring_args(h), table_args(h), silo, act, status, tcd);
+        case GD_RING_CONSISTENT:
+            return launch(h, "k_route", g, b, ring_lds(h), k_route_m<GD_RING_CONSISTENT, 1, false, true>, k, n,
+                          ring_args(h), table_args(h), silo, act, status, tcd);
+        default:
+            return launch(h, "k_route", g, b, ring_lds(h), k_route_m<GD_RING_VIRTUAL_BUCKETS, 1, false, true>, k, n,
+                          ring_args(h), table_args(h), silo, act, status, tcd);
+    }
 }
 
 template <int MODE>
@@ -2236,7 +2256,8 @@ void comm_release(gd_handle* h) {
     h->comm = nullptr;
     h->net = nullptr;
     for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
-                          &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1], &h->x_fwd[0], &h->x_fwd[1]})
+                          &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1], &h->x_fwd[0], &h->x_fwd[1],
+                          &h->x_keys[0], &h->x_keys[1]})
         if (*e) {
             (void)hipEventDestroy(*e);
             *e = nullptr;
@@ -2275,7 +2296,7 @@ int comm_setup(gd_handle* h) {
     HIP_TRY(h, hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking));
     for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
                           &h->x_ret[1], &h->x_done[0], &h->x_done[1], &h->p_packed, &h->x_sent[0], &h->x_sent[1],
-                          &h->x_fwd[0], &h->x_fwd[1]})
+                          &h->x_fwd[0], &h->x_fwd[1], &h->x_keys[0], &h->x_keys[1]})
         HIP_TRY(h, hipEventCreateWithFlags(e, hipEventDisableTiming));
     return GD_OK;
 }
@@ -2439,6 +2460,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     DevBuf* B = h->mx[s];
     const bool ret = (flags & GD_MULTI_RETURN_ROUTES) != 0;
     const bool fwd = (flags & GD_MULTI_FORWARD) != 0;
+    const bool keep_keys = fwd || !(flags & GD_MULTI_NO_KEYS);   // the forward hop moves the keys on
     const bool has_ext = ext && n && !h->cache_max;      // KeyExt strings travel with their messages
     const ExtArgs x = has_ext ? ExtArgs{ext->bytes, ext->offset, ext->length, ext->bytes_len} : ExtArgs{};
     DevBuf* SB = h->mx_send[s];
@@ -2525,11 +2547,22 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     const uint64_t my_esz = hd[0] ? 8 : 24;
     std::vector<uint64_t> hsb(W + 1, 0), hrb(W + 1, 0);
     bool any_compact = false;
+    // every received chunk compact with one TypeCodeData: the probe reads the N1s as they arrive
+    // (8 B a key instead of a 24-B rebuilt key); not with KeyExt strings or in cache mode
+    bool n1_path = !has_ext && !h->cache_max && m > 0;
+    uint64_t n1_tcd = 0;
+    bool n1_first = true;
     for (int r = 0; r < W; ++r) {
         const bool c = hd[4 + 4 * r] != 0;
         any_compact |= c && rc[r];
         hsb[r + 1] = hsb[r] + sc[r] * my_esz;
         hrb[r + 1] = hrb[r] + rc[r] * (c ? 8 : 24);
+        if (rc[r]) {
+            const uint64_t t = (uint64_t)hd[4 + 4 * r + 2] | ((uint64_t)hd[4 + 4 * r + 3] << 32);
+            if (!c || (!n1_first && t != n1_tcd)) n1_path = false;
+            n1_tcd = t;
+            n1_first = false;
+        }
     }
     // 2. this parity's buffers: batch i-2 must be done with them (probe/bucket and routes round)
     const size_t m4 = (size_t)m * 4 + 4, n4 = (size_t)n * 4 + 4;
@@ -2571,7 +2604,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
             GD_TRY(launch(h, "k_u32_to_u64", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_u32_to_u64,
                           (const uint32_t*)B[16].p, m, (uint64_t*)B[17].p));
         }
-        if (any_compact)
+        if (any_compact && !n1_path)
             GD_TRY(launch(h, "k_recv_expand", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_expand,
                           (const uint8_t*)B[18].p, (const uint32_t*)(dcnt + W), (const uint32_t*)(kdesc + 4),
                           (uint32_t)W, m, recv_keys, recv_src));
@@ -2579,6 +2612,12 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
             GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
                           (const uint32_t*)(dcnt + W), (uint32_t)W, m, recv_src));
         HIP_TRY(h, hipEventRecord(h->x_hdr[s], h->xstream));
+        if (n1_path && keep_keys) {    // the 24-B keys for the result, beside the probe
+            GD_TRY(launch(h, "k_recv_expand", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_expand,
+                          (const uint8_t*)B[18].p, (const uint32_t*)(dcnt + W), (const uint32_t*)(kdesc + 4),
+                          (uint32_t)W, m, recv_keys, recv_src));
+            HIP_TRY(h, hipEventRecord(h->x_keys[s], h->xstream));
+        }
         if (!ret) {                    // this parity's send buffers are free for batch i+2's partition
             HIP_TRY(h, hipEventRecord(h->x_sent[s], h->xstream));
             h->x_sent_rec[s] = true;
@@ -2586,7 +2625,8 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     }
     // 3. probe + bucket on the owner (the handle's stream)
     HIP_TRY(h, hipStreamWaitEvent(h->stream, h->x_hdr[s], 0));
-    if (m) GD_TRY(route_device(h, recv_keys, m, silo, act, st));
+    if (n1_path) GD_TRY(route_n1_device(h, (const uint64_t*)B[18].p, n1_tcd, m, silo, act, st));
+    else if (m) GD_TRY(route_device(h, recv_keys, m, silo, act, st));
     if (m && has_ext)                  // the received strings: KeyExt grains are routed on their owner
         GD_TRY(keyext_pass(h, recv_keys,
                            ExtArgs{(const uint8_t*)B[15].p, (const uint64_t*)B[17].p, (const int32_t*)B[14].p,
@@ -2616,9 +2656,10 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         r.ret_act = (const uint32_t*)B[12].p;
         r.ret_status = (const uint8_t*)B[13].p;
     }
+    if (n1_path && keep_keys) HIP_TRY(h, hipStreamWaitEvent(h->stream, h->x_keys[s], 0));
     r.n_recv = m;
     r.n_act = n_act;
-    r.recv_keys = recv_keys;
+    r.recv_keys = keep_keys ? recv_keys : nullptr;
     r.recv_idx = recv_idx;
     r.recv_src = recv_src;
     r.silo = silo;
@@ -2704,14 +2745,14 @@ int gd_comm_destroy(gd_handle* h) {
 int gd_route_multi_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int flags,
                           gd_multi_result* out) {
     if (!h || (n && !d_keys)) return set_err(h, GD_EINVAL, "null argument");
-    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD | GD_MULTI_NO_KEYS)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
     HIP_TRY(h, hipSetDevice(h->device));
     return route_multi(h, d_keys, n, n_act, flags, out);
 }
 
 int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, int flags, gd_multi_result* out) {
     if (!h || (n && !keys)) return set_err(h, GD_EINVAL, "null argument");
-    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD | GD_MULTI_NO_KEYS)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(need_comm(h));
     // the batch goes to the device on the exchange stream, so the partition needs no other wait
@@ -2725,7 +2766,7 @@ int gd_route_multi(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act,
 int gd_route_multi_ext_device(gd_handle* h, const gd_key* d_keys, const gd_key_ext* d_ext, uint32_t n, uint32_t n_act,
                               int flags, gd_multi_result* out) {
     if (!h || (n && (!d_keys || !d_ext || !d_ext->offset || !d_ext->length))) return set_err(h, GD_EINVAL, "null argument");
-    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD | GD_MULTI_NO_KEYS)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
     HIP_TRY(h, hipSetDevice(h->device));
     return route_multi(h, d_keys, n, n_act, flags, out, d_ext);
 }
@@ -2733,7 +2774,7 @@ int gd_route_multi_ext_device(gd_handle* h, const gd_key* d_keys, const gd_key_e
 int gd_route_multi_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint32_t n_act, int flags,
                        gd_multi_result* out) {
     if (!h || (n && (!keys || !ext || !ext->offset || !ext->length))) return set_err(h, GD_EINVAL, "null argument");
-    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
+    if (flags & ~(GD_MULTI_RETURN_ROUTES | GD_MULTI_KEYS_READY | GD_MULTI_FORWARD | GD_MULTI_NO_KEYS)) return set_err(h, GD_EINVAL, "unknown flags 0x%x", flags);
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(need_comm(h));
     // the batch and its strings go to the device on the exchange stream
@@ -2770,7 +2811,9 @@ int gd_multi_fetch(gd_handle* h, gd_key* recv_keys, uint32_t* recv_idx, uint32_t
         if (dst && bytes) HIP_TRY(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream));
         return GD_OK;
     };
-    GD_TRY(cp(recv_keys, r.recv_keys, m * sizeof(gd_key)));
+    if (recv_keys && m && !r.recv_keys)
+        return set_err(h, GD_EINVAL, "the last gd_route_multi ran with GD_MULTI_NO_KEYS");
+    if (r.recv_keys) GD_TRY(cp(recv_keys, r.recv_keys, m * sizeof(gd_key)));
     GD_TRY(cp(recv_idx, r.recv_idx, m * 4));
     GD_TRY(cp(recv_src, r.recv_src, m * 4));
     GD_TRY(cp(silo, r.silo, m * 4));

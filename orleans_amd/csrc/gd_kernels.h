@@ -218,11 +218,13 @@ __device__ __forceinline__ void st(T* p, T v) {
 // that each lane keeps M random 32-B slot reads in flight.  NT streams the key
 // reads and result writes non-temporally so they do not push the table out of
 // the caches it shares with them.
-template <int MODE, int M, bool NT>
+// N1: the keys arrive as N1 alone (8 B each; N0 = 0, TypeCodeData = tcd_u for all), the form a
+// compact exchange header round delivers (k_key_desc, gd_shard.h).
+template <int MODE, int M, bool NT, bool N1 = false>
 __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                    TableArgs tab, uint32_t* __restrict__ out_silo,
                                                    uint32_t* __restrict__ out_act,
-                                                   uint8_t* __restrict__ out_status) {
+                                                   uint8_t* __restrict__ out_status, uint64_t tcd_u) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
@@ -239,10 +241,15 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
         const uint32_t i = base + j * BLOCK;
         n0[j] = n1[j] = tcd[j] = 0;
         if (i < n) {
-            const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
-            n0[j] = ld<NT>(kp);
-            n1[j] = ld<NT>(kp + 1);
-            tcd[j] = ld<NT>(kp + 2);
+            if constexpr (N1) {
+                n1[j] = ld<NT>(reinterpret_cast<const uint64_t*>(keys) + i);
+                tcd[j] = tcd_u;
+            } else {
+                const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
+                n0[j] = ld<NT>(kp);
+                n1[j] = ld<NT>(kp + 1);
+                tcd[j] = ld<NT>(kp + 2);
+            }
         }
     }
 #pragma unroll

@@ -146,6 +146,7 @@ class KeyExtBatch:
 GD_MULTI_RETURN_ROUTES = 1
 GD_MULTI_KEYS_READY = 2
 GD_MULTI_FORWARD = 4
+GD_MULTI_NO_KEYS = 8
 
 
 class GrainDispatchError(RuntimeError):
@@ -767,21 +768,24 @@ class GrainDispatch:
         self._c(lib.gd_comm_destroy(self.h))
 
     def route_multi_device(self, d_keys: int, n: int, n_act: int, return_routes: bool = False,
-                           keys_ready: bool = False, forward: bool = False) -> gd_multi_result:
+                           keys_ready: bool = False, forward: bool = False,
+                           no_keys: bool = False) -> gd_multi_result:
         """Returns after the counts round; the rest is enqueued.  The result holds device pointers
         into library-owned buffers, valid through the next call (two batches in flight)."""
         r = gd_multi_result()
         flags = ((GD_MULTI_RETURN_ROUTES if return_routes else 0) | (GD_MULTI_KEYS_READY if keys_ready else 0)
-                 | (GD_MULTI_FORWARD if forward else 0))
+                 | (GD_MULTI_FORWARD if forward else 0) | (GD_MULTI_NO_KEYS if no_keys else 0))
         self._c(lib.gd_route_multi_device(self.h, C.c_void_p(d_keys), n, n_act, flags, C.byref(r)))
         return r
 
-    def route_multi(self, keys, n_act: int, return_routes: bool = False, forward: bool = False) -> dict:
+    def route_multi(self, keys, n_act: int, return_routes: bool = False, forward: bool = False,
+                    no_keys: bool = False) -> dict:
         """Host batch in, host results out (gd_route_multi + gd_multi_fetch)."""
         k = keys_array(keys)
         n = k.shape[0]
         r = gd_multi_result()
-        flags = (GD_MULTI_RETURN_ROUTES if return_routes else 0) | (GD_MULTI_FORWARD if forward else 0)
+        flags = ((GD_MULTI_RETURN_ROUTES if return_routes else 0) | (GD_MULTI_FORWARD if forward else 0)
+                 | (GD_MULTI_NO_KEYS if no_keys else 0))
         self._c(lib.gd_route_multi(self.h, _ptr(k), n, n_act, flags, C.byref(r)))
         return self.multi_fetch(r, n)
 
@@ -824,7 +828,7 @@ class GrainDispatch:
     def multi_fetch(self, r: gd_multi_result, n: int) -> dict:
         """Host copies of the last gd_route_multi* result (n = this rank's batch size)."""
         m = r.n_recv
-        out = {"recv_keys": np.empty((m, 3), np.uint64), "recv_idx": np.empty(m, np.uint32),
+        out = {"recv_keys": np.empty((m, 3), np.uint64) if r.recv_keys else None, "recv_idx": np.empty(m, np.uint32),
                "recv_src": np.empty(m, np.uint32), "silo": np.empty(m, np.uint32), "act": np.empty(m, np.uint32),
                "status": np.empty(m, np.uint8), "perm": np.empty(m, np.uint32),
                "offsets": np.empty(r.n_act + 2, np.uint32)}
@@ -832,7 +836,8 @@ class GrainDispatch:
             out.update(ret_silo=np.empty(n, np.uint32), ret_act=np.empty(n, np.uint32), ret_status=np.empty(n, np.uint8))
         names = ("recv_keys", "recv_idx", "recv_src", "silo", "act", "status", "perm", "offsets", "ret_silo",
                  "ret_act", "ret_status")
-        self._c(lib.gd_multi_fetch(self.h, *[C.c_void_p(_ptr(out[f])) if f in out else None for f in names]))
+        self._c(lib.gd_multi_fetch(self.h, *[C.c_void_p(_ptr(out[f])) if out.get(f) is not None else None
+                                             for f in names]))
         return out
 
     # -- header decode -------------------------------------------------

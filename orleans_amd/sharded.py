@@ -25,7 +25,7 @@ from . import graindispatch as g
 
 @dataclass
 class ShardedResult:
-    recv_keys: torch.Tensor     # (M,3) int64 -- message headers this rank owns, arrival order
+    recv_keys: Optional[torch.Tensor]  # (M,3) int64 -- headers this rank owns, arrival order (None: no_keys)
     recv_idx: Optional[torch.Tensor]   # (M,) int32 -- index in the sender's batch (None: world 1, identity)
     recv_src: Optional[torch.Tensor]   # (M,) int32 -- sender rank (None: world 1, all rank 0)
     status: torch.Tensor        # (M,) uint8
@@ -255,6 +255,7 @@ class LibraryRouter:
         dist.broadcast(t, src=0, group=group)
         engine.gd.comm_init(bytes(t.cpu().numpy().tobytes()), self.world, self.rank)
         self.keys_ready = False
+        self.no_keys = False        # GD_MULTI_NO_KEYS: recv_keys None, messages known by (src, idx)
 
     def route_bucket(self, keys: torch.Tensor, n_act: int, return_routes: bool = False,
                      keys_ready: Optional[bool] = None) -> ShardedResult:
@@ -263,9 +264,11 @@ class LibraryRouter:
         returned views stay valid through the next call.  None: the router's `keys_ready`."""
         n = keys.shape[0]
         keys_ready = self.keys_ready if keys_ready is None else keys_ready
-        r = self.engine.gd.route_multi_device(keys.data_ptr(), n, n_act, return_routes, keys_ready)
+        r = self.engine.gd.route_multi_device(keys.data_ptr(), n, n_act, return_routes, keys_ready,
+                                              no_keys=self.no_keys)
         m, dev = r.n_recv, self.engine.device
-        return ShardedResult(_view(r.recv_keys, (m, 3), "<i8", dev), _view(r.recv_idx, (m,), "<i4", dev),
+        rk = _view(r.recv_keys, (m, 3), "<i8", dev) if r.recv_keys or m == 0 else None
+        return ShardedResult(rk, _view(r.recv_idx, (m,), "<i4", dev),
                              _view(r.recv_src, (m,), "<i4", dev), _view(r.status, (m,), "|u1", dev),
                              _view(r.silo, (m,), "<i4", dev), _view(r.act, (m,), "<i4", dev),
                              _view(r.perm, (m,), "<i4", dev), _view(r.offsets, (n_act + 2,), "<i4", dev))

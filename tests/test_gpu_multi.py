@@ -730,3 +730,44 @@ def test_route_multi_local_mixed_headers(gd, compact, monkeypatch):
     for e in es:
         e.comm_destroy()
         e.close()
+
+
+@pytest.mark.parametrize("two_types", [False, True])
+def test_route_multi_local_no_keys(gd, two_types):
+    """GD_MULTI_NO_KEYS at W = 3: with one grain type everywhere the probe reads the compact N1s
+    as received (route_n1_device); with two types the keys are rebuilt first.  Results other than
+    recv_keys (left unset) are the same either way."""
+    W, G = 3, 4000
+    silos = o.bench_silos(8)
+    tc2 = o.grain_type_code("UnitTests.Grains.SimpleGrain")
+    reg = np.concatenate([o.grain_keys(TC, np.arange(G)), o.grain_keys(tc2, np.arange(G))])
+    spec = o.ring_spec(silos, "D")
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    act = np.zeros(len(reg), np.uint32)
+    for r in range(W):
+        act[own % W == r] = np.arange(int((own % W == r).sum()))
+    spec, own, es = _local_world(gd, W, "D", silos, reg, act, own)
+    rng = np.random.default_rng(12)
+    batches = [o.grain_keys(tc2 if (two_types and r == 1) else TC, rng.integers(0, G + 300, size=30000 + r))
+               for r in range(W)]
+    n_act = [int((own % W == r).sum()) for r in range(W)]
+    res = _run_ranks([lambda r=r: es[r].route_multi(batches[r], n_act[r], no_keys=True) for r in range(W)])
+    full = o.DirectoryArrays(reg, act, own)
+    for r in range(W):
+        rk, ids, srcs, st, silo, a = _expected_owner_side(batches, spec, full, W, r)
+        assert res[r]["recv_keys"] is None
+        np.testing.assert_array_equal(res[r]["recv_idx"], ids)
+        np.testing.assert_array_equal(res[r]["recv_src"], srcs)
+        np.testing.assert_array_equal(res[r]["status"], st)
+        np.testing.assert_array_equal(res[r]["silo"], silo)
+        np.testing.assert_array_equal(res[r]["act"], a)
+        wp, wo = o.bucket_stable(a, n_act[r])
+        np.testing.assert_array_equal(res[r]["perm"], wp)
+        np.testing.assert_array_equal(res[r]["offsets"], wo)
+        assert (st == o.ST_OK).sum() > 20000 * 0.9 / W
+        with pytest.raises(gd.GrainDispatchError):        # the keys were not kept
+            buf = np.empty((len(ids), 3), np.uint64)
+            es[r]._c(gd.lib.gd_multi_fetch(es[r].h, gd._ptr(buf), *([None] * 10)))
+    for e in es:
+        e.comm_destroy()
+        e.close()
