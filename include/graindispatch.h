@@ -141,6 +141,12 @@ const char* gd_last_error(const gd_handle* h);   /* never NULL; h may be NULL   
 int         gd_abi_version(void);
 int         gd_set_stream(gd_handle* h, void* hip_stream); /* NULL = library stream */
 void*       gd_get_stream(gd_handle* h);
+/* Pinned (page-locked) host memory for batch buffers.  The host-pointer entry points overlap
+ * their PCIe copies with the kernels for large batches (gd_route_bucket: keys up, routes down
+ * while later chunks are probed); the copies are asynchronous only from pinned memory.  A C# host
+ * allocates its batch arrays here once and reuses them (Span<T> over the pointer). */
+int         gd_host_alloc(size_t bytes, void** out);
+int         gd_host_free(void* p);
 int         gd_synchronize(gd_handle* h);
 int         gd_stats_get(gd_handle* h, gd_stats* out);
 

@@ -31,7 +31,8 @@ RING_MODES = {"D": RING_DIRECTORY, "R": RING_CONSISTENT, "V": RING_VIRTUAL_BUCKE
 # C-ABI symbols the header declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
     "gd_create", "gd_destroy", "gd_last_error", "gd_abi_version", "gd_set_stream", "gd_get_stream",
-    "gd_synchronize", "gd_stats_get", "gd_jenkins_hash_bytes", "gd_jenkins_hash_u64x3", "gd_uniform_hash",
+    "gd_synchronize", "gd_stats_get", "gd_host_alloc", "gd_host_free", "gd_jenkins_hash_bytes",
+    "gd_jenkins_hash_u64x3", "gd_uniform_hash",
     "gd_calculate_id_hash", "gd_silo_consistent_hash", "gd_silo_uniform_hashes", "gd_silo_compare",
     "gd_ring_build", "gd_ring_set", "gd_ring_owner", "gd_ring_lookup_hashes", "gd_dir_register",
     "gd_dir_unregister", "gd_dir_lookup", "gd_dir_clear", "gd_dir_rehash", "gd_route", "gd_bucket",
@@ -176,6 +177,8 @@ def _load() -> C.CDLL:
         "gd_abi_version": (C.c_int, []),
         "gd_set_stream": (C.c_int, [P, P]),
         "gd_get_stream": (P, [P]),
+        "gd_host_alloc": (C.c_int, [C.c_size_t, P]),
+        "gd_host_free": (C.c_int, [P]),
         "gd_synchronize": (C.c_int, [P]),
         "gd_stats_get": (C.c_int, [P, C.POINTER(gd_stats)]),
         "gd_jenkins_hash_bytes": (U32, [P, C.c_size_t]),

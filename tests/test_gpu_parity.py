@@ -837,3 +837,50 @@ def test_randomized_configurations(gd):
             np.testing.assert_array_equal(mb.offsets(), wo, err_msg=msg)
             mb.close()
         e.close()
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_route_bucket_host_pipelined(gd, pinned, monkeypatch):
+    """gd_route_bucket's pipelined host path (chunked H2D / probe / D2H on three streams, then the
+    bucketing of the whole batch), forced on with small chunks (GD_HOST_CHUNK), from pageable and
+    from gd_host_alloc'd pinned buffers; a ragged last chunk."""
+    import ctypes as C
+    monkeypatch.setenv("GD_HOST_CHUNK", "4096")
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "V")
+    e = _engine(gd, silos, "V", cap=1 << 15, my_silo=2)
+    G = 9000
+    reg = o.grain_keys(TC, np.arange(G))
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    e.register(reg, np.arange(G), own)
+    n = 4096 * 7 + 123
+    keys = o.grain_keys(TC, np.random.default_rng(17).integers(0, G + 900, size=n))
+    keys[::37] = _special_keys()[np.arange(len(keys[::37])) % 8]
+    bufs = []
+
+    def arr(shape, dt):
+        if not pinned:
+            return np.zeros(shape, dt)
+        p = C.c_void_p()
+        nb = int(np.prod(shape)) * np.dtype(dt).itemsize
+        assert gd.lib.gd_host_alloc(nb, C.byref(p)) == 0
+        bufs.append(p)
+        return np.ctypeslib.as_array((C.c_uint8 * nb).from_address(p.value)).view(dt).reshape(shape)
+
+    k = arr((n, 3), np.uint64)
+    k[:] = keys
+    silo, act, perm = arr(n, np.uint32), arr(n, np.uint32), arr(n, np.uint32)
+    st, off = arr(n, np.uint8), arr(G + 2, np.uint32)
+    for _ in range(2):                                  # the streams and events are reused
+        e._c(gd.lib.gd_route_bucket(e.h, k.ctypes.data, n, G, silo.ctypes.data, act.ctypes.data, st.ctypes.data,
+                                    perm.ctypes.data, off.ctypes.data))
+        wst, wsilo, wact, _, _ = o.route_batch_np(keys, spec, o.DirectoryArrays(reg, np.arange(G), own), my_silo=2)
+        np.testing.assert_array_equal(st, wst)
+        np.testing.assert_array_equal(silo, wsilo)
+        np.testing.assert_array_equal(act, wact)
+        wp, wo = o.bucket_stable(wact, G)
+        np.testing.assert_array_equal(perm, wp)
+        np.testing.assert_array_equal(off, wo)
+    e.close()
+    for p in bufs:
+        assert gd.lib.gd_host_free(p) == 0
