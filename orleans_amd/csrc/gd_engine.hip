@@ -660,7 +660,8 @@ bool host_pinned(const void* p) {
 // copy-in stream while chunk k-1 is probed on the handle's stream and chunk k-2's routes come
 // down on the copy-out stream (PCIe is full duplex); the bucketing needs the whole batch, so only
 // perm and offsets are copied after it.  Bounded by the 24-B-a-message upload instead of the sum
-// of both directions.  Used when the keys and perm buffers are pinned (gd_host_alloc).
+// of both directions.  Used when the caller's buffers are pinned (gd_host_alloc).  out_perm ==
+// nullptr: gd_route (routes only, no bucketing).
 int route_bucket_host_pipelined(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, uint32_t* out_silo,
                                 uint32_t* out_act, uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets) {
     if (!h->cin) HIP_TRY(h, hipStreamCreateWithFlags(&h->cin, hipStreamNonBlocking));
@@ -676,8 +677,11 @@ int route_bucket_host_pipelined(gd_handle* h, const gd_key* keys, uint32_t n, ui
     GD_TRY(ensure(h, h->out_a, (size_t)n * 4 + 4));
     GD_TRY(ensure(h, h->out_b, (size_t)n * 4 + 4));
     GD_TRY(ensure(h, h->out_c, (size_t)n + 4));
-    GD_TRY(ensure(h, h->u8_a, (size_t)n * 4 + 4));
-    GD_TRY(ensure(h, h->offs, ((size_t)n_act + 2) * 4));
+    const bool bucket = out_perm != nullptr;        // gd_route: routes only
+    if (bucket) {
+        GD_TRY(ensure(h, h->u8_a, (size_t)n * 4 + 4));
+        GD_TRY(ensure(h, h->offs, ((size_t)n_act + 2) * 4));
+    }
     gd_key* dk = (gd_key*)h->keys_in.p;
     uint32_t* silo = (uint32_t*)h->out_a.p;
     uint32_t* act = (uint32_t*)h->out_b.p;
@@ -697,6 +701,10 @@ int route_bucket_host_pipelined(gd_handle* h, const gd_key* keys, uint32_t n, ui
         HIP_TRY(h, hipMemcpyAsync(out_silo + off, silo + off, (size_t)cnt * 4, hipMemcpyDeviceToHost, h->cout));
         HIP_TRY(h, hipMemcpyAsync(out_act + off, act + off, (size_t)cnt * 4, hipMemcpyDeviceToHost, h->cout));
         HIP_TRY(h, hipMemcpyAsync(out_status + off, st + off, cnt, hipMemcpyDeviceToHost, h->cout));
+    }
+    if (!bucket) {
+        HIP_TRY(h, hipStreamSynchronize(h->cout));
+        return sync(h);
     }
     GD_TRY(bucket_device(h, act, n, n_act, (uint32_t*)h->u8_a.p, (uint32_t*)h->offs.p));
     HIP_TRY(h, hipEventRecord(ev[2 * nch + 1], h->stream));
@@ -1112,6 +1120,8 @@ int gd_route(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* out_silo, u
     if (!h || (n && (!keys || !out_silo || !out_act || !out_status))) return set_err(h, GD_EINVAL, "null argument");
     if (n == 0) return GD_OK;
     HIP_TRY(h, hipSetDevice(h->device));
+    if (h->host_chunk && n >= 2 * h->host_chunk && !h->cache_max && host_pinned(keys) && host_pinned(out_silo))
+        return route_bucket_host_pipelined(h, keys, n, 0, out_silo, out_act, out_status, nullptr, nullptr);
     GD_TRY(h2d(h, h->keys_in, keys, n));
     GD_TRY(ensure(h, h->out_a, (size_t)n * 4));
     GD_TRY(ensure(h, h->out_b, (size_t)n * 4));

@@ -881,6 +881,11 @@ def test_route_bucket_host_pipelined(gd, pinned, monkeypatch):
         wp, wo = o.bucket_stable(wact, G)
         np.testing.assert_array_equal(perm, wp)
         np.testing.assert_array_equal(off, wo)
+        silo[:], act[:], st[:] = 7, 7, 7                 # gd_route: routes only, same pipeline
+        e._c(gd.lib.gd_route(e.h, k.ctypes.data, n, silo.ctypes.data, act.ctypes.data, st.ctypes.data))
+        np.testing.assert_array_equal(st, wst)
+        np.testing.assert_array_equal(silo, wsilo)
+        np.testing.assert_array_equal(act, wact)
     e.close()
     for p in bufs:
         assert gd.lib.gd_host_free(p) == 0

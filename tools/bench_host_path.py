@@ -77,15 +77,22 @@ def main():
         def step():
             e._c(g.lib.gd_route_bucket(e.h, ptr(keys), n, G, ptr(silo), ptr(act), ptr(st), ptr(perm), ptr(off)))
 
-        for _ in range(args.warmup):
-            step()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        dt = (time.perf_counter() - t0) / args.steps
+        def route_only():
+            e._c(g.lib.gd_route(e.h, ptr(keys), n, ptr(silo), ptr(act), ptr(st)))
+
+        def timed(fn):
+            for _ in range(args.warmup):
+                fn()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                fn()
+            return (time.perf_counter() - t0) / args.steps
+
+        dt = timed(step)
         assert int((st == 0).sum()) == n
-        out[kind] = {"value": n / dt, "ms_per_call": dt * 1e3,
-                     "pcie_GBps": n * (24 + 17) / dt / 1e9}
+        dr = timed(route_only)
+        out[kind] = {"value": n / dt, "ms_per_call": dt * 1e3, "pcie_GBps": n * (24 + 17) / dt / 1e9,
+                     "route_only": {"value": n / dr, "ms_per_call": dr * 1e3, "pcie_GBps": n * (24 + 9) / dr / 1e9}}
     out["value"] = out["pinned"]["value"]
     print(json.dumps(out), flush=True)
 
