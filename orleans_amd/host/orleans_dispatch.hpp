@@ -781,4 +781,62 @@ private:
     gd_handle* h_;
 };
 
+// ------------------------------------------------------------------ whole-node exchange
+// One silo per GPU (SURVEY 8 e).  Exchange() takes the messages this silo's batcher addressed,
+// moves each to the silo owning its grain's directory partition (the per-target-silo outbound
+// queues of OutboundMessageQueue.SendMessage, OutboundMessageQueue.cs:54-131), looks it up there
+// (GrainDirectoryPartition.cs:385-441) and queues it per activation (ActivationData.cs:566-606).
+// With forward = true a hit travels on to the silo hosting its activation (the send to
+// ActivationAddress.Silo after a remote lookup, LocalGrainDirectory.cs:920,
+// OutboundMessageQueue.cs:125).  Every silo calls Exchange for every batch (collective).
+struct Delivery {                        // the messages this silo received, in arrival order
+    std::vector<uint32_t> SenderSilo;    // silo index of the sender
+    std::vector<uint32_t> SenderIndex;   // position in the sender's batch
+    std::vector<uint8_t> Status;         // GD_ROUTE_* from the owner's lookup
+    std::vector<uint32_t> Activation;    // activation index (GD_NO_ACTIVATION unless OK)
+    std::vector<std::vector<uint32_t>> PerActivation;   // arrival positions per activation, FIFO
+    std::vector<uint32_t> Unrouted;      // arrival positions with no activation here
+};
+
+class SiloMessageCenter {
+public:
+    // RCCL communicator: silo 0 creates the id (gd_comm_unique_id) and publishes it to the others.
+    SiloMessageCenter(gd_handle* h, const uint8_t id[GD_COMM_ID_BYTES], int nSilos, int myIndex) : h_(h) {
+        Check(h, gd_comm_init(h, id, nSilos, myIndex));
+    }
+    // Handles already joined (gd_comm_init_local: every silo of the group in this process).
+    explicit SiloMessageCenter(gd_handle* h) : h_(h) {}
+    static void JoinInProcess(const std::vector<gd_handle*>& silos) {
+        Check(nullptr, gd_comm_init_local(silos.data(), (int)silos.size()));
+    }
+    ~SiloMessageCenter() { gd_comm_destroy(h_); }
+    SiloMessageCenter(const SiloMessageCenter&) = delete;
+    SiloMessageCenter& operator=(const SiloMessageCenter&) = delete;
+
+    Delivery Exchange(const std::vector<GrainId>& targets, uint32_t numActivations, bool forward = false) {
+        std::vector<gd_key> keys(targets.size());
+        for (size_t i = 0; i < targets.size(); ++i) keys[i] = targets[i].Key.ToNative();
+        gd_multi_result r{};
+        Check(h_, gd_route_multi(h_, keys.data(), (uint32_t)keys.size(), numActivations,
+                                 forward ? GD_MULTI_FORWARD : 0, &r));
+        const uint32_t m = r.n_recv;
+        Delivery d;
+        d.SenderSilo.resize(m);
+        d.SenderIndex.resize(m);
+        d.Status.resize(m);
+        d.Activation.resize(m);
+        std::vector<uint32_t> perm(m), off((size_t)numActivations + 2);
+        Check(h_, gd_multi_fetch(h_, nullptr, d.SenderIndex.data(), d.SenderSilo.data(), nullptr, d.Activation.data(),
+                                 d.Status.data(), perm.data(), off.data(), nullptr, nullptr, nullptr));
+        d.PerActivation.resize(numActivations);
+        for (uint32_t a = 0; a < numActivations; ++a)
+            d.PerActivation[a].assign(perm.begin() + off[a], perm.begin() + off[a + 1]);
+        d.Unrouted.assign(perm.begin() + off[numActivations], perm.begin() + off[numActivations + 1]);
+        return d;
+    }
+
+private:
+    gd_handle* h_;
+};
+
 }  // namespace orleans

@@ -14,6 +14,7 @@
 #include <random>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "orleans_dispatch.hpp"
@@ -501,6 +502,112 @@ static void RoutingDump(const char* path) {
         f << (int64_t)grains[i].Key.N1 << " " << (int)owners[i].Ip[15] << "\n";
 }
 
+// Whole-node exchange (SURVEY 8 e) with three silos in this process (gd_comm_init_local), one
+// thread each: every message is delivered exactly once, to the silo owning its grain (or, with
+// forward, to the silo hosting its activation), and each activation's queue keeps (sender silo,
+// sender order) -- the order one IncomingMessageAgent thread per silo produces.
+static void WholeNodeExchange() {
+    const int W = 3, G = 3000, N = 20000;
+    const int tc = gd_calculate_id_hash("BenchmarkGrains.Ping.PingGrain");
+    std::vector<SiloAddress> silos;
+    for (int i = 1; i <= W; ++i) silos.push_back(SiloAddress::New(10, 0, 0, (uint8_t)i, 11111, 1));
+    std::vector<gd_silo_addr> addrs;
+    for (const auto& s : silos) addrs.push_back(s.ToNative());
+    std::vector<uint32_t> pts(64), own(64);
+    uint32_t npts = 0;
+    Check(nullptr, gd_ring_build(GD_RING_DIRECTORY, addrs.data(), W, 0, pts.data(), own.data(), &npts));
+    std::vector<std::unique_ptr<DispatchHandle>> hs;
+    std::vector<gd_handle*> raw;
+    for (int r = 0; r < W; ++r) {
+        hs.push_back(std::make_unique<DispatchHandle>(0, 1 << 13, (uint32_t)r));
+        raw.push_back(hs.back()->get());
+        Check(raw[r], gd_ring_set(raw[r], GD_RING_DIRECTORY, pts.data(), own.data(), npts));
+    }
+    // grain k: directory owner from the ring; activation on silo (k * 7 + 1) % W, numbered per silo
+    const int K = G + 200;                  // grains G.. are never registered: MISS on their owner
+    std::vector<gd_key> gk(K);
+    for (int k = 0; k < K; ++k) gk[k] = GrainId::GetGrainId(tc, k).Key.ToNative();
+    std::vector<uint32_t> owner(K), actSilo(G), actIdx(G), perSilo(W, 0);
+    Check(raw[0], gd_ring_owner(raw[0], gk.data(), K, owner.data()));
+    for (int k = 0; k < G; ++k) {
+        actSilo[k] = (uint32_t)((k * 7 + 1) % W);
+        actIdx[k] = perSilo[actSilo[k]]++;
+    }
+    for (int r = 0; r < W; ++r) {
+        std::vector<gd_key> mk;
+        std::vector<gd_val> mv;
+        for (int k = 0; k < G; ++k)
+            if ((int)owner[k] == r) {
+                mk.push_back(gk[k]);
+                mv.push_back(gd_val{actIdx[k], actSilo[k]});
+            }
+        std::vector<gd_val> win(mk.size());
+        std::vector<uint8_t> ins(mk.size());
+        Check(raw[r], gd_dir_register(raw[r], mk.data(), mv.data(), (uint32_t)mk.size(), win.data(), ins.data()));
+    }
+    SiloMessageCenter::JoinInProcess(raw);
+    std::vector<std::vector<GrainId>> batch(W);
+    std::vector<std::vector<int>> batchK(W);
+    std::mt19937 rng(11);
+    for (int r = 0; r < W; ++r)
+        for (int i = 0; i < N + r * 100; ++i) {
+            const int k = (int)(rng() % K);
+            batch[r].push_back(GrainId::GetGrainId(tc, k));
+            batchK[r].push_back(k);
+        }
+    std::vector<std::unique_ptr<SiloMessageCenter>> mc;      // destroying one leaves the group
+    for (int r = 0; r < W; ++r) mc.push_back(std::make_unique<SiloMessageCenter>(raw[r]));
+    for (bool forward : {false, true}) {
+        std::vector<Delivery> got(W);
+        std::vector<std::string> err(W);
+        std::vector<std::thread> th;
+        for (int r = 0; r < W; ++r)
+            th.emplace_back([&, r] {
+                try {
+                    got[r] = mc[r]->Exchange(batch[r], perSilo[r], forward);
+                } catch (const std::exception& e) {
+                    err[r] = e.what();
+                }
+            });
+        for (auto& t : th) t.join();
+        bool ok = true;
+        for (int r = 0; r < W; ++r)
+            if (!err[r].empty()) {
+                std::fprintf(stderr, "  silo %d: %s\n", r, err[r].c_str());
+                ok = false;
+            }
+        EXPECT(ok);
+        if (!ok) return;
+        std::set<std::pair<uint32_t, uint32_t>> seen;
+        size_t total = 0;
+        for (int r = 0; r < W; ++r) {
+            const Delivery& d = got[r];
+            total += d.SenderSilo.size();
+            for (size_t j = 0; j < d.SenderSilo.size(); ++j) {
+                EXPECT(seen.insert({d.SenderSilo[j], d.SenderIndex[j]}).second);
+                const int k = batchK[d.SenderSilo[j]][d.SenderIndex[j]];
+                if (k < G) {
+                    EXPECT(d.Status[j] == GD_ROUTE_OK && d.Activation[j] == actIdx[k]);
+                    EXPECT((forward ? actSilo[k] : owner[k]) == (uint32_t)r);
+                } else {
+                    EXPECT(d.Status[j] == GD_ROUTE_MISS && owner[k] == (uint32_t)r);
+                }
+            }
+            if (!forward) continue;
+            for (uint32_t a = 0; a < perSilo[r]; ++a)
+                for (size_t q = 1; q < d.PerActivation[a].size(); ++q) {
+                    const uint32_t x = d.PerActivation[a][q - 1], y = d.PerActivation[a][q];
+                    EXPECT(d.Activation[y] == a);
+                    EXPECT(std::make_pair(d.SenderSilo[x], d.SenderIndex[x]) <
+                           std::make_pair(d.SenderSilo[y], d.SenderIndex[y]));
+                }
+        }
+        size_t sent = 0;
+        for (int r = 0; r < W; ++r) sent += batch[r].size();
+        EXPECT(total == sent);
+    }
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "all";
     Run("ID_HashCorrectness", ID_HashCorrectness);
@@ -532,6 +639,7 @@ int main(int argc, char** argv) {
         Run("LruMaximumSizeTest", LruMaximumSizeTest);
         Run("LruUsageTest", LruUsageTest);
         Run("PerSiloLocalLookup", PerSiloLocalLookup);
+        Run("WholeNodeExchange", WholeNodeExchange);
         if (argc > 2) Run("RoutingDump", [&] { RoutingDump(argv[2]); });
     }
     std::printf("%s (%d failure%s)\n", g_failures ? "FAILED" : "OK", g_failures, g_failures == 1 ? "" : "s");
