@@ -130,6 +130,7 @@ struct gd_handle {
     int radix_max_bits = 8;   // digit width cap (GD_RADIX_MAXBITS, 4..11)
     int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
+    uint32_t hist_tpb = 1;      // tiles per workgroup in the radix histogram, 1/4/8 (GD_HIST_TPB)
     bool compact_headers = true;   // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
     bool fused_starts = true;   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
@@ -427,8 +428,20 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
     const uint32_t R = 1u << BITS;
     GD_TRY(ensure(h, h->hist, (size_t)R * tiles * sizeof(uint32_t)));
     uint32_t* hist = (uint32_t*)h->hist.p;
-    GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_radix_hist<BITS, NT, IT>, kin, n, clamp, shift, tiles,
-                  hist));
+    if constexpr (BITS <= 8) {
+        if (h->hist_tpb == 4)
+            GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0, k_radix_hist_multi<BITS, NT, IT, 4>,
+                          kin, n, clamp, shift, tiles, hist));
+        else if (h->hist_tpb == 8)
+            GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 8)), dim3(NT), 0, k_radix_hist_multi<BITS, NT, IT, 8>,
+                          kin, n, clamp, shift, tiles, hist));
+        else
+            GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_radix_hist<BITS, NT, IT>, kin, n, clamp, shift,
+                          tiles, hist));
+    } else {
+        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_radix_hist<BITS, NT, IT>, kin, n, clamp, shift, tiles,
+                      hist));
+    }
     GD_TRY(scan_device<OpAdd>(h, hist, R * tiles, false, false, "hist"));
     if (first)
         return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, true, NT, IT>, kin, vin, n,
@@ -743,6 +756,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_COMPACT_HEADERS")) h->compact_headers = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_HOST_CHUNK")) h->host_chunk = (uint32_t)std::strtoul(v, nullptr, 10);
     if (const char* v = std::getenv("GD_XCD_TILES")) h->xcd_tiles = std::atoi(v) ? 1u : 0u;
+    if (const char* v = std::getenv("GD_HIST_TPB")) h->hist_tpb = (uint32_t)std::atoi(v);
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));

@@ -662,7 +662,7 @@ __global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ 
         const unsigned long long act = __ballot(valid);
         if (act == 0) continue;
         const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
-        const uint32_t d0 = __shfl(d, lead, WAVE);
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
         const unsigned long long hot = __ballot(valid && d == d0);
         if (valid) {
             if (d != d0) atomicAdd(&my_cnt[d], 1u);
@@ -675,6 +675,66 @@ __global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ 
 #pragma unroll
         for (int w = 0; w < NW; ++w) c += s_cnt[w * R + d];
         hist[d * tiles + blockIdx.x] = c;
+    }
+}
+
+// Multi-tile histogram: one workgroup counts TPB consecutive tiles, with every tile's 16-B key
+// loads issued before the first count, and one counter set per tile shared by the waves.  The
+// digit-major counts it writes for one digit are then TPB consecutive words, instead of one word
+// every `tiles` words per workgroup.  Same output as k_radix_hist.
+template <int BITS, int NT, int IT, int TPB>
+__global__ void __launch_bounds__(NT) k_radix_hist_multi(const uint32_t* __restrict__ keys, uint32_t n,
+                                                         uint32_t clamp, uint32_t shift, uint32_t tiles,
+                                                         uint32_t* __restrict__ hist) {
+    constexpr uint32_t R = 1u << BITS;
+    constexpr uint32_t TILE = NT * IT;
+    static_assert(IT % 4 == 0, "16-B loads");
+    __shared__ uint32_t s_cnt[TPB][R];
+    for (uint32_t x = threadIdx.x; x < TPB * R; x += NT) (&s_cnt[0][0])[x] = 0;
+    __syncthreads();
+    const uint32_t t0 = blockIdx.x * TPB;
+    const uint32_t lane = lane_id();
+    const bool aligned = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
+    uint32_t k[TPB][IT];
+#pragma unroll
+    for (int t = 0; t < TPB; ++t) {
+        const uint64_t base = (uint64_t)(t0 + t) * TILE;
+        const bool vec = aligned && base + TILE <= n;
+#pragma unroll
+        for (int j = 0; j < IT / 4; ++j) {
+            const uint64_t i0 = base + 4 * (j * NT + threadIdx.x);
+            if (vec) {
+                const uint4 v = *reinterpret_cast<const uint4*>(keys + i0);
+                k[t][4 * j] = v.x; k[t][4 * j + 1] = v.y; k[t][4 * j + 2] = v.z; k[t][4 * j + 3] = v.w;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) k[t][4 * j + q] = (i0 + q < n) ? keys[i0 + q] : NONE32;
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < TPB; ++t) {
+        const uint64_t base = (uint64_t)(t0 + t) * TILE;
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const uint64_t i = base + 4 * ((j / 4) * NT + threadIdx.x) + (j % 4);
+            const bool valid = i < n;
+            const uint32_t d = (min(k[t][j], clamp) >> shift) & (R - 1);
+            const unsigned long long act = __ballot(valid);
+            if (act == 0) continue;
+            const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
+            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
+            const unsigned long long hot = __ballot(valid && d == d0);
+            if (valid) {
+                if (d != d0) atomicAdd(&s_cnt[t][d], 1u);
+                else if (lane == lead) atomicAdd(&s_cnt[t][d], (uint32_t)__popcll(hot));
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < TPB * R; x += NT) {
+        const uint32_t t = x % TPB, d = x / TPB;
+        if (t0 + t < tiles) hist[d * tiles + t0 + t] = s_cnt[t][d];
     }
 }
 
