@@ -130,7 +130,7 @@ struct gd_handle {
     int radix_max_bits = 8;   // digit width cap (GD_RADIX_MAXBITS, 4..11)
     int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
-    uint32_t hist_tpb = 1;      // tiles per workgroup in the radix histogram, 1/4/8 (GD_HIST_TPB)
+    uint32_t hist_tpb = 4;      // tiles per workgroup in the radix histogram, 1/4/8 (GD_HIST_TPB)
     bool compact_headers = true;   // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
     bool fused_starts = true;   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)

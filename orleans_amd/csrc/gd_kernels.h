@@ -696,21 +696,27 @@ __global__ void __launch_bounds__(NT) k_radix_hist_multi(const uint32_t* __restr
     const uint32_t lane = lane_id();
     const bool aligned = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
     uint32_t k[TPB][IT];
+    // One workgroup-uniform branch: in a full, aligned range every 16-B load is unconditional, so
+    // all TPB * IT / 4 of them are issued before the first wait (a per-tile branch around them
+    // makes the compiler wait at each).
+    if (aligned && (uint64_t)(t0 + TPB) * TILE <= n) {
 #pragma unroll
-    for (int t = 0; t < TPB; ++t) {
-        const uint64_t base = (uint64_t)(t0 + t) * TILE;
-        const bool vec = aligned && base + TILE <= n;
+        for (int t = 0; t < TPB; ++t)
 #pragma unroll
-        for (int j = 0; j < IT / 4; ++j) {
-            const uint64_t i0 = base + 4 * (j * NT + threadIdx.x);
-            if (vec) {
+            for (int j = 0; j < IT / 4; ++j) {
+                const uint64_t i0 = (uint64_t)(t0 + t) * TILE + 4 * (j * NT + threadIdx.x);
                 const uint4 v = *reinterpret_cast<const uint4*>(keys + i0);
                 k[t][4 * j] = v.x; k[t][4 * j + 1] = v.y; k[t][4 * j + 2] = v.z; k[t][4 * j + 3] = v.w;
-            } else {
+            }
+    } else {
+#pragma unroll
+        for (int t = 0; t < TPB; ++t)
+#pragma unroll
+            for (int j = 0; j < IT / 4; ++j) {
+                const uint64_t i0 = (uint64_t)(t0 + t) * TILE + 4 * (j * NT + threadIdx.x);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) k[t][4 * j + q] = (i0 + q < n) ? keys[i0 + q] : NONE32;
             }
-        }
     }
 #pragma unroll
     for (int t = 0; t < TPB; ++t) {
