@@ -131,7 +131,7 @@ struct gd_handle {
     int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
     uint32_t hist_tpb = 0;      // tiles per workgroup in the radix histogram, 1/4/8 (GD_HIST_TPB);
-                                // 0 = by size: 4 up to 4096 tiles (16M keys), else 1 (A/B)
+                                // 0 = by size: 4 for 1024..4096 tiles (4M..16M keys), else 1 (A/B)
     bool compact_headers = true;   // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
     bool fused_starts = true;   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
@@ -429,7 +429,8 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
     const uint32_t R = 1u << BITS;
     GD_TRY(ensure(h, h->hist, (size_t)R * tiles * sizeof(uint32_t)));
     uint32_t* hist = (uint32_t*)h->hist.p;
-    const uint32_t tpb = h->hist_tpb ? h->hist_tpb : (tiles <= 4096 ? 4u : 1u);
+    // below 1024 tiles, 4 per workgroup would leave fewer workgroups than the 256 CUs
+    const uint32_t tpb = h->hist_tpb ? h->hist_tpb : (tiles >= 1024 && tiles <= 4096 ? 4u : 1u);
     if constexpr (BITS <= 8) {
         if (tpb == 4)
             GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0, k_radix_hist_multi<BITS, NT, IT, 4>,
