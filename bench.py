@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 from orleans_amd import graindispatch as g          # noqa: E402
 from orleans_amd.sharded import DeviceEngine, LibraryRouter, ShardedRouter, same_result  # noqa: E402
+from orleans_amd.workloads import zipf_keys_torch  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # 8 silos 10.0.0.{1..8}:11111.  "literal" = generation 1; its ring gives
@@ -70,25 +71,15 @@ def kernel_bytes(name: str, n: int, n_act: int, passes: int, world: int) -> floa
 
 def zipf_keys(tcd: int, n_grains: int, n: int, seed: int, dev) -> torch.Tensor:
     """(n, 3) int64 keys on `dev`: grain k ~ Zipf(s=1.1) over ranks 0..n_grains-1 by inverse CDF
-    (SURVEY 8 d cfg 3), sampled on the GPU; grain k is GrainId(Ping type, k)."""
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(seed)
-    cdf = torch.arange(1, n_grains + 1, dtype=torch.float64, device=dev).pow_(-1.1).cumsum_(0)
-    cdf /= cdf[-1].clone()
-    u = torch.rand(n, dtype=torch.float64, device=dev, generator=gen)
-    k = torch.searchsorted(cdf, u).clamp_(max=n_grains - 1)
-    del cdf, u
-    keys = torch.zeros((n, 3), dtype=torch.int64, device=dev)
-    keys[:, 1] = k
-    keys[:, 2] = np.uint64(tcd).astype(np.int64).item()
-    return keys
+    (SURVEY 8 d cfg 3), sampled on the GPU (orleans_amd/workloads.py)."""
+    return zipf_keys_torch(tcd, n_grains, n, seed, dev)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3"],
                     help="cfg2: 16M uniform msgs/GPU over 2^20 grains/GPU (weak scaling); cfg3: 64M Zipf(1.1) "
                          "msgs over 100M grains for the whole node (strong scaling)")
@@ -96,7 +87,7 @@ def main():
     ap.add_argument("--grains", type=int, default=None, help="grains per GPU (cfg2 default 2^20)")
     ap.add_argument("--mode", default="D", choices=["D", "R", "V"])
     ap.add_argument("--silos", default="balanced", choices=sorted(SILO_SETS))
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline budget")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0, help="bounded CPU baseline budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=5, help="extra steps with per-kernel events")
     ap.add_argument("--exchange", default="auto", choices=["auto", "library", "torch"],
@@ -331,36 +322,111 @@ def workload_name(w: str, world: int, n: int, g_total: int) -> str:
     return f"cfg2 per GPU (16M msgs/GPU over {g_total} grains), directory sharded by ring owner, RCCL all-to-all-v"
 
 
+def usable_cores() -> int:
+    """CPUs this process may actually run on: the affinity set, capped by a cgroup v2 CPU quota.
+    (os.cpu_count() reports the whole host -- 256 on the GPU box -- not the job's share.)"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def _timed(fn, budget: float, unit: int):
+    """Repeat fn() (each call = `unit` messages) for about `budget` seconds: (messages/s, messages)."""
+    done, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        done += unit
+        if time.perf_counter() - t0 >= budget:
+            break
+    return done / (time.perf_counter() - t0), done
+
+
 def cpu_baseline(args, tcd, G_total, pts, own, owner):
+    """The C restatement (oracle/cpu_ref.c, test infrastructure) timed on this host's cores, on
+    bounded samples of the bench workload: route (ring + directory probe) + per-activation bucketing
+    of the same messages.  faithful = the reference's data structures (linear ring scan under
+    lock(membershipCache), chained Dictionary under lock(lockable), per-activation FIFO append on the
+    single IncomingMessageAgent thread); fast = binary search, open addressing, parallel counting
+    sort.  `value` is the strongest CPU configuration measured (fast, all usable cores)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpu_ref  # test-infrastructure checker, timed here as the CPU baseline only
 
-    nthreads = min(16, os.cpu_count() or 1)
+    cores = usable_cores()
+    host = os.cpu_count() or 1
+    budget = args.cpu_seconds / 6
     sample = 1 << 22
     rng = np.random.default_rng(0x5EED0001)
     keys = grain_keys(tcd, rng.integers(0, G_total, size=sample, dtype=np.int64))
     all_keys = grain_keys(tcd, np.arange(G_total, dtype=np.int64))
     res = {}
-    for label, faithful, thr in (("faithful", True, 1), ("fast", False, nthreads)):
-        d = cpu_ref.CpuDirectory(faithful, G_total)
-        d.register(all_keys, np.arange(G_total, dtype=np.uint32), owner)
-        done, t0 = 0, time.perf_counter()
-        budget = args.cpu_seconds / 2
-        while True:
-            st, silo, act = d.route(args.mode, pts, own, keys, nthreads=thr)
-            perm, off = cpu_ref.bucket(act, G_total, faithful=faithful, nthreads=thr)
-            done += sample
-            if time.perf_counter() - t0 >= budget:
-                break
-        res[label] = (done / (time.perf_counter() - t0), thr, done)
+    runs = [("faithful_1", True, 1, 1), ("faithful_n", True, cores, 1), ("fast_1", False, 1, 1),
+            ("fast_n", False, cores, cores)]
+    if host != cores:
+        runs.append(("fast_host", False, host, host))
+    dirs = {}
+    for label, faithful, thr_route, thr_bucket in runs:
+        d = dirs.get(faithful)
+        if d is None:
+            d = dirs[faithful] = cpu_ref.CpuDirectory(faithful, G_total)
+            d.register(all_keys, np.arange(G_total, dtype=np.uint32), owner)
+
+        def one(d=d, faithful=faithful, thr_route=thr_route, thr_bucket=thr_bucket):
+            st, silo, act = d.route(args.mode, pts, own, keys, nthreads=thr_route)
+            cpu_ref.bucket(act, G_total, faithful=faithful, nthreads=thr_bucket)
+        v, done = _timed(one, budget, sample)
+        res[label] = {"value": round(v, 1), "route_threads": thr_route, "bucket_threads": thr_bucket,
+                      "messages": done}
+    dirs.clear()
+    # BASELINE cfg 1's shape (PingBenchmark: 1M calls over 10k grains, one silo), same restatement
+    G1, N1 = 10_000, 1 << 20
+    k1 = grain_keys(tcd, np.random.default_rng(0x5EED0101).integers(0, G1, size=N1, dtype=np.int64))
+    reg1 = grain_keys(tcd, np.arange(G1, dtype=np.int64))
+    cfg1 = {}
+    for label, faithful, thr in (("faithful_1", True, 1), ("fast_n", False, cores)):
+        d = cpu_ref.CpuDirectory(faithful, G1)
+        d.register(reg1, np.arange(G1, dtype=np.uint32), np.zeros(G1, np.uint32))
+
+        def one1(d=d, faithful=faithful, thr=thr):
+            _, _, act = d.route("D", np.zeros(1, np.uint32), np.zeros(1, np.uint32), k1, nthreads=thr)
+            cpu_ref.bucket(act, G1, faithful=faithful, nthreads=thr)
+        v, done = _timed(one1, budget / 2, N1)
+        cfg1[label] = {"value": round(v, 1), "threads": thr, "messages": done}
         del d
-    v, thr, done = res["faithful"]
-    return {"value": round(v, 1), "unit": "messages/s", "cores": thr, "kind": "port",
-            "sample": f"{done} messages (cfg2 distribution, {sample}-message batches repeated) through the C "
-                      f"restatement in faithful mode (linear ring scan under a mutex, chained Dictionary-style "
-                      f"map, per-activation FIFO append), 1 thread",
-            "fast_value": round(res["fast"][0], 1), "fast_cores": res["fast"][1],
-            "host_cpus": os.cpu_count()}
+    # BASELINE cfg 5's latency path: one 4096-message micro-batch, faithful, single thread
+    d = cpu_ref.CpuDirectory(True, G_total)
+    d.register(all_keys, np.arange(G_total, dtype=np.uint32), owner)
+    runs = cpu_ref.BucketRuns(G_total, 4096)
+    lat = []
+    t_end = time.perf_counter() + budget / 2
+    i = 0
+    while time.perf_counter() < t_end or len(lat) < 50:
+        kb = np.ascontiguousarray(keys[(i * 4096) % sample:(i * 4096) % sample + 4096])
+        t0 = time.perf_counter()
+        _, _, act = d.route(args.mode, pts, own, kb, nthreads=1)
+        runs(act)
+        lat.append(time.perf_counter() - t0)
+        i += 1
+    del d
+    lat_us = np.asarray(lat) * 1e6
+    best = res["fast_n"]
+    return {"value": best["value"], "unit": "messages/s", "cores": cores, "kind": "port",
+            "sample": f"{best['messages']} messages (cfg2 distribution, {sample}-message batches repeated) through "
+                      f"the C restatement (oracle/cpu_ref.c) in fast mode (binary-search ring, open addressing, "
+                      f"parallel stable counting sort) on {cores} threads = this job's usable cores "
+                      f"(affinity + cgroup quota; os.cpu_count() = {host})",
+            "modes": res, "host_cpus": host,
+            "cfg1_ping_shape": cfg1,
+            "cfg5_latency_us": {"batch": 4096, "n_batches": len(lat),
+                                "mode": "faithful route (linear ring scan + chained map under locks) + per-activation "
+                                        "FIFO runs of the batch (cpu_bucket_runs), 1 thread",
+                                "p50": round(float(np.percentile(lat_us, 50)), 1),
+                                "p99": round(float(np.percentile(lat_us, 99)), 1)}}
 
 
 if __name__ == "__main__":

@@ -183,6 +183,12 @@ int gd_ring_lookup_hashes(gd_handle* h, const uint32_t* hashes, uint32_t n, uint
  * out_inserted 1 for the item that created the entry.  Host pointers. */
 int gd_dir_register(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t n,
                     gd_val* out_vals, uint8_t* out_inserted);
+/* gd_dir_register with device arrays (keys, values and the optional outputs, which may be NULL):
+ * bulk population of a partition whose grains are already in HBM (activation tables built on
+ * the GPU, a handoff received over RCCL).  Waits for work enqueued on the handle's stream, runs
+ * synchronously.  A value with silo > 0xFFFE fails the call with GD_EINVAL. */
+int gd_dir_register_device(gd_handle* h, const gd_key* d_keys, const gd_val* d_vals, uint32_t n,
+                           gd_val* d_out_vals, uint8_t* d_out_inserted);
 /* Overwrite for a batch, applied in batch order (the last item of a grain wins): how the host
  * mirrors GrainDirectoryPartition.AddActivation (GrainDirectoryPartition.cs:274-302; GrainInfo
  * .AddActivation :89-108) for multi-instance grains: one instance -> {act, silo}, two or more ->

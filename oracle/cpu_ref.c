@@ -320,3 +320,38 @@ int cpu_bucket(int faithful, const uint32_t* act, uint64_t n, uint32_t n_act, ui
     free(hist);
     return 0;
 }
+
+/* Micro-batch form of the bucketing (BASELINE cfg 5, the CPU side of gd_microbatch_run): the
+ * activations present in a small batch, ascending, each with its messages in arrival order
+ * (ActivationData.waiting FIFO append, ActivationData.cs:604-605).  Work is O(n + k log k) for k
+ * distinct activations -- no O(n_act) pass per batch.  counts[n_act + 1] is caller scratch that is
+ * zero on entry and left zero on return. */
+static int cmp_u32(const void* a, const void* b) {
+    const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+int cpu_bucket_runs(const uint32_t* act, uint64_t n, uint32_t n_act, uint32_t* counts, uint32_t* perm,
+                    uint32_t* run_act, uint32_t* run_start, uint32_t* n_runs) {
+    uint32_t k = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t a = act[i] < n_act ? act[i] : n_act;
+        if (counts[a]++ == 0) run_act[k++] = a;
+    }
+    qsort(run_act, k, sizeof(uint32_t), cmp_u32);
+    uint32_t pos = 0;
+    for (uint32_t r = 0; r < k; ++r) {
+        const uint32_t c = counts[run_act[r]];
+        run_start[r] = pos;
+        counts[run_act[r]] = pos;   /* now the write cursor */
+        pos += c;
+    }
+    run_start[k] = pos;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t a = act[i] < n_act ? act[i] : n_act;
+        perm[counts[a]++] = (uint32_t)i;
+    }
+    for (uint32_t r = 0; r < k; ++r) counts[run_act[r]] = 0;
+    *n_runs = k;
+    return 0;
+}

@@ -24,6 +24,7 @@ def _load():
     lib.cpu_dir_register.argtypes = [P, P, P, P, U64, P, P, P]
     lib.cpu_route.argtypes = [P, C.c_int, C.c_int, P, P, U32, P, U64, U32, U32, P, P, P, C.c_int]
     lib.cpu_bucket.argtypes = [C.c_int, P, U64, U32, P, P, C.c_int]
+    lib.cpu_bucket_runs.argtypes = [P, U64, U32, P, P, P, P, P]
     lib.cpu_jenkins_u64x3.restype = U32
     lib.cpu_jenkins_u64x3.argtypes = [U64, U64, U64]
     return lib
@@ -43,7 +44,7 @@ class CpuDirectory:
         self.d = lib.cpu_dir_new(1 if faithful else 0, capacity_hint)
 
     def __del__(self):
-        if getattr(self, "d", None):
+        if getattr(self, "d", None) and lib is not None:
             lib.cpu_dir_free(self.d)
             self.d = None
 
@@ -73,3 +74,23 @@ def bucket(acts, n_act, faithful=True, nthreads=1):
     off = np.zeros(n_act + 2, np.uint32)
     lib.cpu_bucket(1 if faithful else 0, _p(a), len(a), n_act, _p(perm), _p(off), nthreads)
     return perm, off
+
+
+class BucketRuns:
+    """cpu_bucket_runs with its per-activation scratch kept across batches (the micro-batch form:
+    the activations present, ascending, each run in arrival order)."""
+
+    def __init__(self, n_act: int, capacity: int):
+        self.n_act = n_act
+        self.counts = np.zeros(n_act + 1, np.uint32)
+        self.perm = np.zeros(capacity, np.uint32)
+        self.run_act = np.zeros(capacity, np.uint32)
+        self.run_start = np.zeros(capacity + 1, np.uint32)
+        self.n_runs = np.zeros(1, np.uint32)
+
+    def __call__(self, acts):
+        a = np.ascontiguousarray(np.asarray(acts, dtype=np.uint32))
+        lib.cpu_bucket_runs(_p(a), len(a), self.n_act, _p(self.counts), _p(self.perm), _p(self.run_act),
+                            _p(self.run_start), _p(self.n_runs))
+        r = int(self.n_runs[0])
+        return self.perm[:len(a)], self.run_act[:r], self.run_start[:r + 1]

@@ -946,27 +946,22 @@ int gd_ring_lookup_hashes(gd_handle* h, const uint32_t* hashes, uint32_t n, uint
     return sync(h);
 }
 
-int gd_dir_register(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t n, gd_val* out_vals,
-                    uint8_t* out_inserted) {
-    if (!h || (n && (!keys || !vals || !out_vals || !out_inserted))) return set_err(h, GD_EINVAL, "null argument");
-    for (uint32_t i = 0; i < n; ++i)
-        if (vals[i].silo > 0xFFFEu) return set_err(h, GD_EINVAL, "silo index %u out of range at %u", vals[i].silo, i);
-    if (n == 0) return GD_OK;
-    HIP_TRY(h, hipSetDevice(h->device));
+}  // extern "C"
+
+namespace {
+// AddSingleActivation for a batch of device-resident keys / values (first registration wins, batch
+// order); out_vals / out_ins are device arrays (either may be null).  Synchronous.
+int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t n, gd_val* out_vals,
+                  uint8_t* out_ins) {
     GD_TRY(maybe_grow_table(h, n));
-    GD_TRY(h2d(h, h->keys_in, keys, n));
-    GD_TRY(h2d(h, h->out_c, vals, n));     // gd_val staging
     GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));   // slot_of
     GD_TRY(ensure(h, h->u32_b, (size_t)n * 4));   // win
     GD_TRY(ensure(h, h->u8_a, (size_t)n));        // is_new
-    GD_TRY(ensure(h, h->out_a, (size_t)n * sizeof(gd_val)));
-    GD_TRY(ensure(h, h->out_b, (size_t)n));
     HIP_TRY(h, hipMemsetAsync(h->u8_a.p, 0, n, h->stream));
     const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
     uint32_t* slot_of = (uint32_t*)h->u32_a.p;
     uint32_t* win = (uint32_t*)h->u32_b.p;
     uint8_t* is_new = (uint8_t*)h->u8_a.p;
-    const gd_key* dk = (const gd_key*)h->keys_in.p;
     const unsigned long long mask = h->capacity - 1;
     // claim pass, then relaunches for the items that met an unpublished claim
     for (uint32_t pass = 0;; ++pass) {
@@ -980,19 +975,50 @@ int gd_dir_register(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32
     GD_TRY(launch(h, "k_reg_minwin", g, b, 0, k_reg_minwin, (const uint32_t*)slot_of, (const uint8_t*)is_new, n, h->slots));
     GD_TRY(launch(h, "k_reg_resolve", g, b, 0, k_reg_resolve, (const uint32_t*)slot_of, (const uint8_t*)is_new, n,
                   (const Slot*)h->slots, win));
-    GD_TRY(launch(h, "k_reg_commit", g, b, 0, k_reg_commit, (const uint32_t*)slot_of, (const uint32_t*)win,
-                  (const gd_val*)h->out_c.p, n, h->slots, h->ctr));
-    GD_TRY(launch(h, "k_reg_report", g, b, 0, k_reg_report, (const uint32_t*)slot_of, (const uint32_t*)win, n,
-                  (const Slot*)h->slots, (gd_val*)h->out_a.p, (uint8_t*)h->out_b.p));
-    GD_TRY(d2h(h, out_vals, h->out_a, n));
-    GD_TRY(d2h(h, out_inserted, h->out_b, n));
+    GD_TRY(launch(h, "k_reg_commit", g, b, 0, k_reg_commit, (const uint32_t*)slot_of, (const uint32_t*)win, dvals, n,
+                  h->slots, h->ctr));
+    if (out_vals || out_ins)
+        GD_TRY(launch(h, "k_reg_report", g, b, 0, k_reg_report, (const uint32_t*)slot_of, (const uint32_t*)win, n,
+                      (const Slot*)h->slots, out_vals, out_ins));
     GD_TRY(pull_counters(h));
     if (h->ctr_host.err) {
         const uint32_t e = h->ctr_host.err;
         HIP_TRY(h, hipMemsetAsync(&h->ctr->err, 0, sizeof(uint32_t), h->stream));
-        return set_err(h, (e & 2) ? GD_EFULL : GD_ETIMEOUT, "gd_dir_register: device error bits 0x%x", e);
+        GD_TRY(sync(h));
+        return set_err(h, (e & 2) ? GD_EFULL : (e & 4) ? GD_EINVAL : GD_ETIMEOUT,
+                       "gd_dir_register: device error bits 0x%x (2: table full, 4: silo index > 0xFFFE)", e);
     }
     return GD_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gd_dir_register(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t n, gd_val* out_vals,
+                    uint8_t* out_inserted) {
+    if (!h || (n && (!keys || !vals || !out_vals || !out_inserted))) return set_err(h, GD_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n; ++i)
+        if (vals[i].silo > 0xFFFEu) return set_err(h, GD_EINVAL, "silo index %u out of range at %u", vals[i].silo, i);
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(h2d(h, h->out_c, vals, n));     // gd_val staging
+    GD_TRY(ensure(h, h->out_a, (size_t)n * sizeof(gd_val)));
+    GD_TRY(ensure(h, h->out_b, (size_t)n));
+    GD_TRY(register_core(h, (const gd_key*)h->keys_in.p, (const gd_val*)h->out_c.p, n, (gd_val*)h->out_a.p,
+                         (uint8_t*)h->out_b.p));
+    GD_TRY(d2h(h, out_vals, h->out_a, n));
+    GD_TRY(d2h(h, out_inserted, h->out_b, n));
+    return sync(h);
+}
+
+int gd_dir_register_device(gd_handle* h, const gd_key* d_keys, const gd_val* d_vals, uint32_t n, gd_val* d_out_vals,
+                           uint8_t* d_out_inserted) {
+    if (!h || (n && (!d_keys || !d_vals))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(sync(h));                       // the caller's producers of d_keys / d_vals ran on this stream
+    return register_core(h, d_keys, d_vals, n, d_out_vals, d_out_inserted);
 }
 
 int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t n, uint8_t* out_inserted) {
@@ -1349,7 +1375,10 @@ int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
     if (n > mb->capacity) return set_err(h, GD_EINVAL, "n %u above micro-batch capacity %u", n, mb->capacity);
     GD_TRY(check_ring(h));
     HIP_TRY(h, hipSetDevice(h->device));
-    if (!use_graph) {
+    // LocalLookup (cache) mode routes through k_route_cached, whose scratch, cache table and silo
+    // masks can be reallocated between runs (gd_cache_add rehashes, gd_cache_set_silos, larger
+    // gd_route* calls); a captured graph would replay freed pointers.  That mode runs eagerly.
+    if (!use_graph || h->cache_max) {
         GD_TRY(mb_enqueue(mb, n));
         return sync(h);
     }
@@ -1366,10 +1395,12 @@ int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
         const bool timing = h->timing;
         h->timing = false;
         hipGraph_t graph = nullptr;
+        const uint64_t routed = h->routed;       // counted per replay below, not at capture
         HIP_TRY(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
         const int rc = mb_enqueue(mb, n);
         const hipError_t ec = hipStreamEndCapture(h->stream, &graph);
         h->timing = timing;
+        h->routed = routed;
         if (rc != GD_OK) {
             if (graph) (void)hipGraphDestroy(graph);
             return rc;
@@ -1381,6 +1412,7 @@ int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
         mb->graphs.emplace_back(n, exec);
     }
     HIP_TRY(h, hipGraphLaunch(exec, h->stream));
+    h->routed += n;
     return sync(h);
 }
 

@@ -431,6 +431,7 @@ __global__ void __launch_bounds__(BLOCK) k_reg_commit(const uint32_t* __restrict
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n || win[i] != i) return;
     Slot& sl = slots[slot_of[i]];
+    if (vals[i].silo > 0xFFFEu) atomicOr(&ctr->err, 4u);   // silo index out of range (device-side values)
     sl.act = vals[i].act;
     sl.meta = make_meta(SLOT_LIVE, vals[i].silo);
     atomicAdd(&ctr->live, 1ull);
@@ -477,13 +478,13 @@ __global__ void __launch_bounds__(BLOCK) k_reg_report(const uint32_t* __restrict
     if (i >= n) return;
     const uint32_t s = slot_of[i];
     if (s >= SLOT_RETRY) {
-        out_vals[i] = gd_val{NONE32, NONE32};
-        out_inserted[i] = 0;
+        if (out_vals) out_vals[i] = gd_val{NONE32, NONE32};
+        if (out_inserted) out_inserted[i] = 0;
         return;
     }
     const Slot sl = slots[s];
-    out_vals[i] = gd_val{sl.act, slot_silo(sl.meta)};
-    out_inserted[i] = (win[i] == i) ? 1 : 0;
+    if (out_vals) out_vals[i] = gd_val{sl.act, slot_silo(sl.meta)};
+    if (out_inserted) out_inserted[i] = (win[i] == i) ? 1 : 0;
 }
 
 // RemoveActivation (GrainDirectoryPartition.cs:335-363, Force): find the live entry

@@ -52,7 +52,7 @@ EXPORTED_SYMBOLS = [
     "gd_comm_unique_id", "gd_comm_init", "gd_comm_init_local", "gd_comm_destroy", "gd_route_multi_device",
     "gd_route_multi",
     "gd_multi_fetch", "gd_route_multi_ext_device", "gd_route_multi_ext", "gd_ring_owner_ext",
-    "gd_dir_split_ext", "gd_dir_upsert",
+    "gd_dir_split_ext", "gd_dir_upsert", "gd_dir_register_device",
 ]
 
 
@@ -194,6 +194,7 @@ def _load() -> C.CDLL:
         "gd_ring_lookup_hashes": (C.c_int, [P, P, U32, P]),
         "gd_dir_register": (C.c_int, [P, P, P, U32, P, P]),
         "gd_dir_unregister": (C.c_int, [P, P, P, U32, P]),
+        "gd_dir_register_device": (C.c_int, [P, P, P, U32, P, P]),
         "gd_dir_upsert": (C.c_int, [P, P, P, U32, P]),
         "gd_dir_lookup": (C.c_int, [P, P, U32, P, P]),
         "gd_dir_clear": (C.c_int, [P]),
@@ -417,6 +418,12 @@ class GrainDispatch:
         ins = np.zeros(n, dtype=np.uint8)
         self._c(lib.gd_dir_register(self.h, _ptr(k), _ptr(vals), n, _ptr(out), _ptr(ins)))
         return out[:, 0].copy(), out[:, 1].copy(), ins
+
+    def register_device(self, d_keys: int, d_vals: int, n: int, d_out_vals: Optional[int] = None,
+                        d_out_inserted: Optional[int] = None):
+        """gd_dir_register_device: keys (n,3) u64 and values (n,2) u32 [act, silo] in HBM."""
+        self._c(lib.gd_dir_register_device(self.h, C.c_void_p(d_keys), C.c_void_p(d_vals), n,
+                                           C.c_void_p(d_out_vals or 0), C.c_void_p(d_out_inserted or 0)))
 
     def upsert(self, keys, acts, silos) -> np.ndarray:
         """gd_dir_upsert: overwrite, the last item of a grain wins; acts may hold GD_ACT_MULTI."""

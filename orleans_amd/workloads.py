@@ -31,3 +31,42 @@ def power_law_graph(n_nodes: int, mean_deg: float, seed: int, max_deg: int = 1 <
     k = np.arange(E, dtype=np.int64) - row_off[item]
     dst = ((item + 1 + S[(r[item] + k) % L]) % n_nodes).astype(np.uint32)
     return row_off.astype(np.uint32), dst
+
+
+def zipf_cdf(n_grains: int, s: float = 1.1) -> np.ndarray:
+    """Normalised Zipf(s) CDF over ranks 0..n_grains-1 (rank r has weight (r+1)^-s)."""
+    cdf = np.cumsum(np.arange(1, n_grains + 1, dtype=np.float64) ** -s)
+    return cdf / cdf[-1]
+
+
+def zipf_ranks_np(n_grains: int, n: int, seed: int, s: float = 1.1) -> np.ndarray:
+    """n grain ranks ~ Zipf(s) by inverse CDF (SURVEY 8 d cfg 3), on the host."""
+    rng = np.random.default_rng(seed)
+    return np.minimum(np.searchsorted(zipf_cdf(n_grains, s), rng.random(n)), n_grains - 1).astype(np.int64)
+
+
+def zipf_keys_torch(tcd: int, n_grains: int, n: int, seed: int, dev, s: float = 1.1):
+    """(n, 3) int64 GrainId keys on `dev`: grain k ~ Zipf(s) over ranks 0..n_grains-1 by inverse
+    CDF, sampled on the GPU (BASELINE cfg 3); grain k is GrainId(type, k): [0, k, tcd]."""
+    import torch
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    cdf = torch.arange(1, n_grains + 1, dtype=torch.float64, device=dev).pow_(-s).cumsum_(0)
+    cdf /= cdf[-1].clone()
+    u = torch.rand(n, dtype=torch.float64, device=dev, generator=gen)
+    k = torch.searchsorted(cdf, u).clamp_(max=n_grains - 1)
+    del cdf, u
+    keys = torch.zeros((n, 3), dtype=torch.int64, device=dev)
+    keys[:, 1] = k
+    keys[:, 2] = int(np.uint64(tcd).astype(np.int64))
+    return keys
+
+
+def grain_keys_torch(tcd: int, ks, dev):
+    """(n, 3) int64 keys [0, k, tcd] on `dev` for a 1-D tensor (or range) of long keys."""
+    import torch
+    ks = torch.as_tensor(ks, device=dev, dtype=torch.int64)
+    keys = torch.zeros((ks.shape[0], 3), dtype=torch.int64, device=dev)
+    keys[:, 1] = ks
+    keys[:, 2] = int(np.uint64(tcd).astype(np.int64))
+    return keys

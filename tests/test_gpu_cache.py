@@ -197,3 +197,60 @@ def test_lru_reference_tests(gd):
     assert len(ent) == 10 and tuple(int(x) for x in k(10)[0]) not in ent
     assert all(tuple(int(x) for x in k(i)[0]) in ent for i in range(1, 10))
     e.close()
+
+
+def test_microbatch_in_cache_mode_survives_rehash(gd):
+    """A micro-batch (gd_microbatch_run, use_graph=1) on a handle in LocalLookup mode, then a
+    gd_cache_add large enough to rehash the cache table (its device memory moves), then the same
+    micro-batch again: routes, runs and the LRU state match the oracle both times (the cache mode
+    runs the micro-batch eagerly, so nothing replays freed pointers)."""
+    rng = np.random.default_rng(5)
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    local, valid = {1, 4}, set(range(8))
+    G = 120000
+    reg = _keys(np.arange(G))
+    owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    mine = np.nonzero(np.isin(owner, list(local)))[0]
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 17, my_silo=1)
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+    e.register(reg[mine], mine.astype(np.uint32), owner[mine])
+    dirmap = {tuple(int(x) for x in reg[i]): (int(i), int(owner[i])) for i in mine}
+    M = 20000
+    e.cache_configure(M, sorted(local), 8)
+    oc = co.DirectoryCacheOracle(M)
+    remote = np.nonzero(~np.isin(owner, list(local)))[0]
+
+    def add(ids):
+        a_act = (ids + 500000).astype(np.uint32)
+        a_silo = (ids % 8).astype(np.uint32)
+        a_ver = (ids % 97).astype(np.int32)
+        e.cache_add(reg[ids], a_act, a_silo, a_ver)
+        for i, gi in enumerate(ids):
+            oc.add_or_update(tuple(int(x) for x in reg[gi]), int(a_act[i]), int(a_silo[i]), int(a_ver[i]))
+
+    add(rng.choice(remote, size=300))
+    cap0 = e.cache_stats()["capacity"]
+    mb = gd.MicroBatch(e, 4096, G)
+    n = 4096
+    for rnd in range(3):
+        ids = rng.integers(0, G, size=n)
+        mb.keys[:n] = reg[ids]
+        mb.run(n, use_graph=True)
+        kt = [tuple(int(x) for x in r) for r in reg[ids]]
+        want = co.local_lookup_route(kt, [int(owner[i]) for i in ids], local, valid, dirmap.get, oc)
+        w_st = np.array([o.ST_OK if w[0] == "OK" else o.ST_MISS for w in want], np.uint8)
+        w_silo = np.array([w[1] for w in want], np.uint32)
+        w_act = np.array([o.M32 if w[2] is None else w[2] for w in want], np.uint32)
+        np.testing.assert_array_equal(mb.status[:n], w_st)
+        np.testing.assert_array_equal(mb.silo[:n], w_silo)
+        np.testing.assert_array_equal(mb.act[:n], w_act)
+        wp, wo = o.bucket_stable(w_act, G)
+        np.testing.assert_array_equal(mb.perm[:n], wp)
+        np.testing.assert_array_equal(mb.offsets(), wo)
+        _check(e, oc)
+        if rnd == 0:
+            add(remote[: 40000])                 # past the rehash threshold: the cache table moves
+            assert e.cache_stats()["capacity"] > cap0
+    mb.close()
+    e.close()

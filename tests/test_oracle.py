@@ -256,3 +256,23 @@ def test_c_restatement_matches_oracle(faithful, mode):
     perm, off = cpu_ref.bucket(act, G, faithful=faithful, nthreads=3)
     wp, wo = o.bucket_stable(act, G)
     assert np.array_equal(perm, wp) and np.array_equal(off, wo)
+
+
+def test_c_bucket_runs_matches_stable_partition():
+    """cpu_bucket_runs (the micro-batch form of the CPU bucketing, cfg 5 baseline) = the stable
+    partition restricted to the activations present, across reused scratch."""
+    import cpu_ref
+    rng = np.random.default_rng(12)
+    br = cpu_ref.BucketRuns(1000, 5000)
+    for n in (0, 1, 17, 4096, 5000):
+        acts = rng.integers(0, 1100, size=n).astype(np.uint32)
+        acts[rng.random(n) < 0.05] = o.M32
+        perm, ra, rs = br(acts)
+        wp, wo = o.bucket_stable(acts, 1000)
+        np.testing.assert_array_equal(perm, wp)
+        c = np.minimum(acts.astype(np.int64), 1000)
+        ua = np.unique(c)
+        np.testing.assert_array_equal(ra, ua)
+        np.testing.assert_array_equal(np.diff(rs), np.bincount(c, minlength=1001)[ua])
+        assert rs[0] == 0 and rs[-1] == n
+    assert not br.counts.any()

@@ -10,10 +10,12 @@ import sys
 
 
 def load(dirs):
+    import glob
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for d in dirs:
-        for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-            agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for path in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+            for r in csv.DictReader(open(path)):
+                agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
 
 
