@@ -250,7 +250,7 @@ def test_microbatch_in_cache_mode_survives_rehash(gd):
         np.testing.assert_array_equal(mb.offsets(), wo)
         _check(e, oc)
         if rnd == 0:
-            add(remote[: 40000])                 # past the rehash threshold: the cache table moves
+            add(remote[: 60000])                 # past the rehash threshold: the cache table moves
             assert e.cache_stats()["capacity"] > cap0
     mb.close()
     e.close()

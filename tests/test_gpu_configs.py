@@ -77,7 +77,12 @@ def test_cfg3_full_size_one_gpu(gd):
     G, N = 100_000_000, 1 << 26
     e = gd.GrainDispatch(device=0, table_capacity=1 << 28)
     e.ring_set_silos("D", _tuples(silos))
-    e.set_stream(torch.cuda.current_stream().cuda_stream)
+    # a dedicated stream: torch's legacy default stream has handle 0, which gd_set_stream reads as
+    # "the library's own (non-blocking) stream" -- torch's writes would then race the library
+    stream = torch.cuda.Stream(dev)
+    e.set_stream(stream.cuda_stream)
+    ctx = torch.cuda.stream(stream)
+    ctx.__enter__()
     owner = torch.empty(G, dtype=torch.int32, device=dev)
     chunk = 1 << 25
     for c0 in range(0, G, chunk):                    # the 100M registrations, in 32M chunks
@@ -133,6 +138,7 @@ def test_cfg3_full_size_one_gpu(gd):
     n0 = int(counts[0])
     assert n0 > N // 20
     assert bool((p[:n0] == torch.nonzero(k == 0).flatten()).all())
+    ctx.__exit__(None, None, None)
     e.close()
 
 
@@ -281,14 +287,16 @@ def test_bucket_hist_variants_unaligned(gd, monkeypatch, tpb, n, n_act):
     acts[rng.random(n) < 0.01] = o.M32
     wp, wo = o.bucket_stable(acts, n_act)
     e = gd.GrainDispatch(device=0, table_capacity=1024)
-    e.set_stream(torch.cuda.current_stream().cuda_stream)
     dev = torch.device("cuda:0")
+    stream = torch.cuda.Stream(dev)
+    e.set_stream(stream.cuda_stream)
     for shift in (1, 0):
-        buf = torch.zeros(n + 4, dtype=torch.int32, device=dev)
-        buf[shift:shift + n] = torch.from_numpy(acts.view(np.int32)).to(dev)
-        perm = torch.empty(n, dtype=torch.int32, device=dev)
-        off = torch.empty(n_act + 2, dtype=torch.int32, device=dev)
-        e.bucket_device(buf.data_ptr() + 4 * shift, n, n_act, perm.data_ptr(), off.data_ptr())
+        with torch.cuda.stream(stream):
+            buf = torch.zeros(n + 4, dtype=torch.int32, device=dev)
+            buf[shift:shift + n] = torch.from_numpy(acts.view(np.int32)).to(dev)
+            perm = torch.empty(n, dtype=torch.int32, device=dev)
+            off = torch.empty(n_act + 2, dtype=torch.int32, device=dev)
+            e.bucket_device(buf.data_ptr() + 4 * shift, n, n_act, perm.data_ptr(), off.data_ptr())
         torch.cuda.synchronize()
         np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), wp, err_msg=f"shift {shift}")
         np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), wo)

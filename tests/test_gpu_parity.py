@@ -314,7 +314,9 @@ def test_full_size_cfg2_properties(gd):
     st = torch.empty(N, dtype=torch.uint8, device=dev)
     perm = torch.empty(N, dtype=torch.int32, device=dev)
     off = torch.empty(G + 2, dtype=torch.int32, device=dev)
-    e.set_stream(torch.cuda.current_stream().cuda_stream)
+    stream = torch.cuda.Stream(dev)          # not torch's null stream (handle 0 = the library's own stream)
+    stream.wait_stream(torch.cuda.current_stream())
+    e.set_stream(stream.cuda_stream)
     e.route_bucket_device(keys.data_ptr(), N, G, silo.data_ptr(), act.data_ptr(), st.data_ptr(),
                           perm.data_ptr(), off.data_ptr())
     torch.cuda.synchronize()
