@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 from orleans_amd import graindispatch as g          # noqa: E402
 from orleans_amd.sharded import DeviceEngine, LibraryRouter, ShardedRouter, same_result  # noqa: E402
-from orleans_amd.workloads import zipf_keys_torch  # noqa: E402
+from orleans_amd.workloads import grain_keys_torch, zipf_keys_torch  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # 8 silos 10.0.0.{1..8}:11111.  "literal" = generation 1; its ring gives
@@ -75,6 +75,127 @@ def zipf_keys(tcd: int, n_grains: int, n: int, seed: int, dev) -> torch.Tensor:
     return zipf_keys_torch(tcd, n_grains, n, seed, dev)
 
 
+def setup_workload(args, workload, world, rank, local, dev, tcd, msgs, grains):
+    """Directory + resident message batch + router for one workload on this rank.
+
+    The directory is built in HBM: grain keys generated on the GPU, ring owner by
+    gd_ring_owner_device, this rank's grains (owner silo % world == rank) registered with
+    gd_dir_register_device (act = running index over this rank's grains, silo = owner)."""
+    if workload == "cfg3":
+        # BASELINE cfg 3 (SURVEY 8 d): 67,108,864 messages for the whole node, k ~ Zipf(1.1) over
+        # 100,000,000 grains, directory sharded by mode-D owner
+        G_total = grains * world if grains else 100_000_000
+        N = msgs or (1 << 26) // world
+        Gr = -(-G_total // world)
+    else:
+        N, Gr = msgs or 1 << 24, grains or 1 << 20
+        G_total = Gr * world
+    cap = 2 * Gr if workload == "cfg2" else 1 << int(np.ceil(np.log2(2 * Gr)))
+    e = g.GrainDispatch(device=local, table_capacity=cap, my_silo=rank % 8, kernel_timing=False)
+    silos = SILO_SETS[args.silos]
+    pts, own = e.ring_set_silos(args.mode, silos)
+    engine = DeviceEngine(e, dev)
+    stream = engine.stream
+    counts = torch.zeros(world, dtype=torch.int64, device=dev)
+    n_act = 0
+    chunk = 1 << 25
+    with torch.cuda.stream(stream):
+        for c0 in range(0, G_total, chunk):
+            c1 = min(G_total, c0 + chunk)
+            rk = grain_keys_torch(tcd, torch.arange(c0, c1, device=dev), dev)
+            owner = torch.empty(c1 - c0, dtype=torch.int32, device=dev)
+            e.ring_owner_device(rk.data_ptr(), c1 - c0, owner.data_ptr())
+            sel = (owner % world) == rank
+            counts += torch.bincount((owner % world).long(), minlength=world)
+            m = int(sel.sum().item())
+            if m:
+                vals = torch.stack([torch.arange(n_act, n_act + m, device=dev, dtype=torch.int32), owner[sel]],
+                                   dim=1).contiguous()
+                mk = rk[sel].contiguous()
+                e.register_device(mk.data_ptr(), vals.data_ptr(), m)
+                del vals, mk
+            n_act += m
+            del rk, owner, sel
+        # ---- synthetic message batch, resident in HBM ----------------------------------
+        if workload == "cfg3":
+            keys = zipf_keys(tcd, G_total, N, 0x5EED0003 + rank, dev)
+        else:
+            rng = np.random.default_rng(0x5EED0001 + rank)
+            ks = rng.integers(0, G_total, size=N, dtype=np.int64)
+            keys = torch.from_numpy(grain_keys(tcd, ks).view(np.int64)).to(dev)
+            del ks
+    torch.cuda.synchronize()
+    owner_share = float(counts.max().item()) / G_total
+    # the same share under the other silo set (generation 1 literal vs balanced), from a sample
+    by_set = {}
+    for name, ss in SILO_SETS.items():
+        sp, so = g.ring_build(args.mode, ss)
+        e2 = g.GrainDispatch(device=local, table_capacity=1024)
+        e2.ring_set(args.mode, sp, so)
+        sample = np.random.default_rng(5).integers(0, G_total, size=1 << 20)
+        o2 = e2.ring_owner(grain_keys(tcd, sample))
+        e2.close()
+        by_set[name] = round(float(np.bincount(o2 % world, minlength=world).max()) / len(sample), 4)
+
+    router = ShardedRouter(engine, stage_via_cpu=args.rehearse_one_gpu)
+    exchange = "none" if world == 1 else (
+        "rehearsal: gloo all_to_all on host-staged copies (every rank on cuda:0)" if args.rehearse_one_gpu
+        else "torch.distributed all_to_all_single (RCCL)")
+    if not args.rehearse_one_gpu and ((world > 1 and args.exchange != "torch") or args.exchange == "library"):
+        # the in-library exchange, checked bit for bit against the torch exchange on the first batch
+        try:
+            lib_router = LibraryRouter(engine)
+            with torch.cuda.stream(stream):
+                ok = same_result(lib_router.route_bucket(keys, n_act), router.route_bucket(keys, n_act))
+                torch.cuda.synchronize()
+            agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(agree, op=dist.ReduceOp.MIN)
+            if int(agree.item()) == 1:
+                # keys are resident and complete: batch i+1's exchange overlaps batch i's probe + bucket
+                # timed batches: messages are known by (sender, index); the probe reads the compact
+                # 8-B headers as they arrive and no 24-B key copy is rebuilt (GD_MULTI_NO_KEYS)
+                router = lib_router
+                lib_router.keys_ready = True
+                lib_router.no_keys = True
+                exchange = ("libgraindispatch gd_route_multi_device (grouped RCCL send/recv, compact headers, "
+                            "GD_MULTI_NO_KEYS); first batch bit-identical to the torch.distributed exchange")
+            else:
+                exchange = "torch.distributed all_to_all_single (RCCL); library exchange disagreed on batch 1"
+                assert args.exchange != "library", "library exchange disagrees with the torch exchange"
+        except Exception as ex:   # noqa: BLE001 -- reported in the JSON line, torch exchange used instead
+            if args.exchange == "library":
+                raise
+            exchange = f"torch.distributed all_to_all_single (RCCL); library exchange failed: {ex!r}"[:300]
+    return {"e": e, "engine": engine, "router": router, "stream": stream, "keys": keys, "N": N, "n_act": n_act,
+            "G_total": G_total, "cap": cap, "pts": pts, "own": own, "exchange": exchange,
+            "owner_share_max": round(owner_share, 4), "owner_share_by_set": by_set}
+
+
+def timed_steps(router, keys, n_act, stream, steps, warmup):
+    """W untimed steps, then exactly K steps bracketed by barrier + synchronize; max over ranks."""
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            router.route_bucket(keys, n_act)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        res = None
+        for _ in range(steps):
+            res = router.route_bucket(keys, n_act)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()), ev0.elapsed_time(ev1), res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,6 +214,9 @@ def main():
     ap.add_argument("--exchange", default="auto", choices=["auto", "library", "torch"],
                     help="N>1: RCCL exchange inside libgraindispatch (gd_route_multi_device) or torch.distributed "
                          "all_to_all_single; auto = library once it matches torch bit for bit on the first batch")
+    ap.add_argument("--no-secondary", action="store_true", help="N>1: skip the cfg3 strong-scaling measurement")
+    ap.add_argument("--msgs3", type=int, default=None, help="secondary cfg3: messages per GPU (default 2^26 / N)")
+    ap.add_argument("--grains3", type=int, default=None, help="secondary cfg3: grains per GPU (default 1e8 / N)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo, host-staged all-to-all")
     args = ap.parse_args()
@@ -114,98 +238,30 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29571")
         dist.init_process_group("gloo", rank=0, world_size=1)
 
-    if args.workload == "cfg3":
-        # BASELINE cfg 3 (SURVEY 8 d): 67,108,864 messages for the whole node, k ~ Zipf(1.1) over
-        # 100,000,000 grains, directory sharded by mode-D owner
-        G_total = args.grains * world if args.grains else 100_000_000
-        N = args.msgs or (1 << 26) // world
-        Gr = -(-G_total // world)
-    else:
-        N, Gr = args.msgs or 1 << 24, args.grains or 1 << 20
-        G_total = Gr * world
     tc = g.calculate_id_hash(PING_GRAIN_CLASS)
     tcd = (3 << 56) + ((tc & 0xFFFFFFFFFFFFFFFF) & 0x00FFFFFFFFFFFFFF)
-
-    # ---- directory: this rank owns the grains whose owner silo lives here -----
-    all_keys = grain_keys(tcd, np.arange(G_total, dtype=np.int64))
-    cap = 2 * Gr if args.workload == "cfg2" else 1 << int(np.ceil(np.log2(2 * Gr)))
-    e = g.GrainDispatch(device=local, table_capacity=cap, my_silo=rank % 8, kernel_timing=False)
-    silos = SILO_SETS[args.silos]
-    pts, own = e.ring_set_silos(args.mode, silos)
-    owner = e.ring_owner(all_keys)
-    mine = np.nonzero(owner % world == rank)[0]
-    n_act = len(mine)
-    e.register(all_keys[mine], np.arange(n_act, dtype=np.uint32), owner[mine])
-    del all_keys
-
-    # ---- synthetic message batch, resident in HBM ----------------------------------
-    if args.workload == "cfg3":
-        keys = zipf_keys(tcd, G_total, N, 0x5EED0003 + rank, dev)
-    else:
-        rng = np.random.default_rng(0x5EED0001 + rank)
-        ks = rng.integers(0, G_total, size=N, dtype=np.int64)
-        keys = torch.from_numpy(grain_keys(tcd, ks).view(np.int64)).to(dev)
-        del ks
-    torch.cuda.synchronize()
-
-    engine = DeviceEngine(e, dev)
-    router = ShardedRouter(engine, stage_via_cpu=args.rehearse_one_gpu)
-    stream = engine.stream
-    exchange = "none" if world == 1 else "torch.distributed all_to_all_single (RCCL)"
-    if not args.rehearse_one_gpu and ((world > 1 and args.exchange != "torch") or args.exchange == "library"):
-        # the in-library exchange, checked bit for bit against the torch exchange on the first batch
-        try:
-            lib_router = LibraryRouter(engine)
-            with torch.cuda.stream(stream):
-                ok = same_result(lib_router.route_bucket(keys, n_act), router.route_bucket(keys, n_act))
-                torch.cuda.synchronize()
-            agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-            dist.all_reduce(agree, op=dist.ReduceOp.MIN)
-            if int(agree.item()) == 1:
-                # keys are resident and complete: batch i+1's exchange overlaps batch i's probe + bucket
-                # timed batches: messages are known by (sender, index); the probe reads the compact
-                # 8-B headers as they arrive and no 24-B key copy is rebuilt (GD_MULTI_NO_KEYS)
-                router = lib_router
-                lib_router.keys_ready = True
-                lib_router.no_keys = True
-                exchange = ("libgraindispatch gd_route_multi_device (grouped RCCL send/recv, compact headers, "
-                            "GD_MULTI_NO_KEYS)")
-            else:
-                exchange = "torch.distributed all_to_all_single (RCCL); library exchange disagreed on batch 1"
-                assert args.exchange != "library", "library exchange disagrees with the torch exchange"
-        except Exception as ex:   # noqa: BLE001 -- reported in the JSON line, torch exchange used instead
-            if args.exchange == "library":
-                raise
-            exchange = f"torch.distributed all_to_all_single (RCCL); library exchange failed: {ex!r}"[:300]
-
-    def step():
-        return router.route_bucket(keys, n_act)
-
-    with torch.cuda.stream(stream):
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        routed_local = 0
-        for _ in range(args.steps):
-            res = step()
-            routed_local += N
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        wall = time.perf_counter() - t0
-    t = torch.tensor([wall], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
-    gpu_ms = ev0.elapsed_time(ev1)
-    total_msgs = routed_local * world
-    value = total_msgs / wall_max
+    w = setup_workload(args, args.workload, world, rank, local, dev, tcd, args.msgs, args.grains)
+    e, N, n_act, G_total, cap, router, stream, keys = (w["e"], w["N"], w["n_act"], w["G_total"], w["cap"],
+                                                        w["router"], w["stream"], w["keys"])
+    exchange = w["exchange"]
+    wall_max, gpu_ms, res = timed_steps(router, keys, n_act, stream, args.steps, args.warmup)
+    value = N * args.steps * world / wall_max
+    secondary = {}
+    if world > 1 and args.workload == "cfg2" and not args.no_secondary:
+        # BASELINE cfg 3 is the node-level configuration: 64M Zipf(1.1) messages over 100M grains
+        # for the whole node (strong scaling), measured by the same harness beside the weak line
+        w3 = setup_workload(args, "cfg3", world, rank, local, dev, tcd, args.msgs3, args.grains3)
+        wall3, gpu3, _ = timed_steps(w3["router"], w3["keys"], w3["n_act"], w3["stream"],
+                                     max(10, args.steps // 10), max(3, args.warmup // 4))
+        steps3 = max(10, args.steps // 10)
+        secondary["cfg3_strong"] = {
+            "value": round(w3["N"] * steps3 * world / wall3, 1), "unit": "messages/s",
+            "ms_per_step": round(wall3 / steps3 * 1e3, 4), "steps": steps3,
+            "workload": workload_name("cfg3", world, w3["N"], w3["G_total"]), "msgs_per_gpu": w3["N"],
+            "scaling": "strong", "exchange": w3["exchange"], "owner_share_max": w3["owner_share_max"],
+            "owner_share_max_by_silo_set": w3["owner_share_by_set"]}
+        w3["e"].close()
+        del w3
 
     # received (owner-side) message count, for the byte model
     m_recv = int(res.status.shape[0])
@@ -277,7 +333,8 @@ def main():
     # ---- CPU baseline: the C restatement (oracle/cpu_ref.c), bounded sample ---------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "cfg2":
-        cpu = cpu_baseline(args, tcd, G_total, pts, own, owner)
+        owner = e.ring_owner(grain_keys(tcd, np.arange(G_total, dtype=np.int64)))
+        cpu = cpu_baseline(args, tcd, G_total, w["pts"], w["own"], owner)
 
     if rank == 0:
         line = {
@@ -299,7 +356,8 @@ def main():
             "config": {"workload": workload_name(args.workload, world, N, G_total),
                        "msgs_per_gpu": N, "grains_total": G_total, "ring_mode": args.mode,
                        "silos": f"8 x 10.0.0.{{1..8}}:11111, {args.silos} generations",
-                       "owner_share_max": round(float(np.bincount(owner % world, minlength=world).max()) / G_total, 4),
+                       "owner_share_max": w["owner_share_max"],
+                       "owner_share_max_by_silo_set": w["owner_share_by_set"],
                        "table_load": round(n_act / cap, 3), "parallelism": f"shard{world}"},
             "routed_ok_last_step_rank0": st_ok,
             "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
@@ -308,6 +366,8 @@ def main():
             "kernels": kernels,
             "cpu_baseline": cpu,
         }
+        if secondary:
+            line["secondary"] = secondary
         print(json.dumps(line), flush=True)
     e.close()
     dist.destroy_process_group()
