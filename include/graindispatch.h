@@ -457,7 +457,9 @@ int gd_decode_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const u
                      const gd_frame_fields* out);
 /* Decode -> route -> (optional) bucket, device pointers, enqueue only.  d_out receives the
  * decoded fields (flags + target_grain required).  Statuses are gd_route's plus
- * GD_ROUTE_ADDRESSED / GD_ROUTE_UNDECODED (silo = act = GD_NO_*, trailing bucket).
+ * GD_ROUTE_ADDRESSED / GD_ROUTE_UNDECODED (silo = act = GD_NO_*, trailing bucket).  With an
+ * ActivationDirectory (gd_actdir_add), an ADDRESSED frame whose TargetActivation FindTarget finds
+ * Valid gets that context as its act and is bucketed with it (IncomingMessageAgent.cs:131-152).
  * d_perm / d_offsets NULL = no bucketing. */
 int gd_route_frames_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
                            uint32_t n, uint32_t n_act, const gd_frame_fields* d_out, uint32_t* d_silo,
@@ -584,6 +586,127 @@ int gd_cache_stats_get(gd_handle* h, gd_cache_stats* out);
 /* KeyValues (:111-127) with each entry's generation, in slot order; keys NULL = size query. */
 int gd_cache_entries(gd_handle* h, gd_key* keys, gd_val* vals, int32_t* versions, uint64_t* generations,
                      uint64_t capacity, uint64_t* out_n);
+
+/* ---- membership change: IsValidSilo, VersionTag, silo removal, handoff merge ----
+ * GrainDirectoryPartition.IsValidSilo (GrainDirectoryPartition.cs:242-245, the membership oracle's
+ * IsFunctionalDirectory): valid[s] != 0 for every silo index s < n_silos that is a functional
+ * directory member; silo indices >= n_silos count as valid; n_silos = 0 = every silo valid (the
+ * default).  With the mask set:
+ *   - gd_dir_register / gd_dir_register_device / gd_dir_register_ext (AddSingleActivation, :304-326)
+ *     and gd_dir_upsert (AddActivation, :274-302) skip an item whose silo is not valid (no entry, out
+ *     value {GD_NO_ACTIVATION, GD_NO_SILO}, not inserted);
+ *   - LookUpActivations (:385-441) filters an entry on an invalid silo: routes give GD_ROUTE_MISS (an
+ *     empty address list fails FastLookup, Catalog.cs:1321-1330), gd_dir_lookup_tagged reports it. */
+int gd_dir_set_valid_silos(gd_handle* h, const uint8_t* valid, uint32_t n_silos);
+/* LookUpActivations with its VersionTag: out_found[i] = 0 no entry (tag 0, the AddressesAndTag
+ * default), 1 an entry with a valid address (out_vals), 2 an entry whose activation's silo is not
+ * valid (empty address list; tag still given).  VersionTags are non-negative int32.  The reference
+ * draws a fresh rand.Next() whenever a grain's entry changes (GrainInfo :106,120,135,154); this
+ * library gives a deterministic 31-bit function of (the mutating call's sequence number, the grain's
+ * uniform hash), changed exactly where the reference draws one.  Host pointers. */
+int gd_dir_lookup_tagged(gd_handle* h, const gd_key* keys, uint32_t n, gd_val* out_vals, int32_t* out_tags,
+                         uint8_t* out_found);
+/* RemoveServer's AdjustLocalDirectory (LocalGrainDirectory.cs:340-361): every entry whose activation
+ * lives on one of the removed silos is dropped (RemoveActivation, Force; single-activation grains lose
+ * their grain).  Multi-activation entries (GD_ACT_MULTI) are counted in *out_multi and left to the host
+ * (their instance silos live in C#).  In LocalLookup mode (gd_cache_configure) also AdjustLocalCache
+ * (:371-385) under the installed ring -- install the ring without the removed silos first: cache
+ * entries pointing at a removed silo or whose grain a local silo now owns are removed
+ * (*out_cache_removed).  KeyExt entries follow the same rule.  Any out pointer may be NULL. */
+int gd_dir_remove_silos(gd_handle* h, const uint32_t* silos, uint32_t n_silos, uint64_t* out_removed,
+                        uint64_t* out_multi, uint64_t* out_cache_removed);
+/* The ActivationId (ActivationId.cs; a UniqueKey, NewId = Guid with Category None) of host activation
+ * indices: ids[i] for acts[i].  gd_dir_merge orders activations by it (UniqueKey.CompareTo,
+ * UniqueKey.cs:255-265: TypeCodeData, N0, N1).  Host pointers. */
+int gd_activation_ids_set(gd_handle* h, const uint32_t* acts, const gd_key* ids, uint32_t n);
+/* GrainDirectoryPartition.Merge (GrainDirectoryPartition.cs:497-522) of a received partition (the copy
+ * merged by GrainDirectoryHandoffManager.ProcessSiloRemoveEvent, :125-158): one item per grain (a
+ * duplicated grain fails with GD_EINVAL and changes nothing).  Per item:
+ *   GD_MERGE_INSERTED  the grain was absent: the incoming entry is added with its VersionTag
+ *                      (tags[i]; tags NULL = a new tag)
+ *   GD_MERGE_SAME      the same activation is registered: nothing changes (GrainInfo.Merge :146)
+ *   GD_MERGE_KEPT      single-activation grain, the incoming ActivationId is the lower: it replaces the
+ *                      existing entry (GrainInfo.Merge :159-176); out_dropped[i] = the displaced one
+ *   GD_MERGE_DROPPED   the existing ActivationId is the lower: out_dropped[i] = the incoming activation
+ *   GD_MERGE_HOST      a multi-activation grain on either side (instance lists are unioned by C#)
+ * out_dropped lists what Catalog.DeleteActivations gets per silo (:514-518); {GD_NO_*} otherwise.  Both
+ * activations of a conflict need an ActivationId (gd_activation_ids_set), else GD_EINVAL.  No
+ * IsValidSilo check (Merge has none).  Host pointers; out_dropped may be NULL. */
+#define GD_MERGE_INSERTED 0
+#define GD_MERGE_KEPT     1
+#define GD_MERGE_SAME     2
+#define GD_MERGE_DROPPED  3
+#define GD_MERGE_HOST     4
+int gd_dir_merge(gd_handle* h, const gd_key* keys, const gd_val* vals, const int32_t* tags, uint32_t n,
+                 uint8_t* out_status, gd_val* out_dropped);
+
+/* ---- receive path: ActivationDirectory + IncomingMessageAgent -----------------
+ * ActivationDirectory (src/Orleans.Runtime/Catalog/ActivationDirectory.cs): ActivationId -> the
+ * host's scheduling-context index + flags, in an HBM table.  Activations (RecordNewTarget :86-93) and
+ * system targets (RecordNewSystemTarget :95-98, flag GD_ACTDIR_SYSTEM_TARGET) share one table and
+ * one context index space; FindTarget (:41-45) sees only activations, FindSystemTarget (:47-51) only
+ * system targets.  Use the grain directory's activation index as the context index of a local
+ * activation, so gd_route_frames' addressed frames and gd_bucket agree. */
+#define GD_ACTDIR_VALID            1u  /* ActivationData.State == Valid                          */
+#define GD_ACTDIR_SYSTEM_TARGET    2u  /* an entry of systemTargets                               */
+#define GD_ACTDIR_STATELESS_WORKER 4u  /* IsStatelessWorker: the *_StatelessWorker limits apply    */
+/* TryAdd (first add of an ActivationId wins); out_added may be NULL. */
+int gd_actdir_add(gd_handle* h, const gd_key* act_ids, const uint32_t* ctx, const uint8_t* flags, uint32_t n,
+                  uint8_t* out_added);
+/* TryRemove (RemoveTarget :116-131); out_removed may be NULL. */
+int gd_actdir_remove(gd_handle* h, const gd_key* act_ids, uint32_t n, uint8_t* out_removed);
+/* State changes (ActivationData.SetState): new flags, batch order (last wins); out_found may be NULL. */
+int gd_actdir_set_flags(gd_handle* h, const gd_key* act_ids, const uint8_t* flags, uint32_t n, uint8_t* out_found);
+int gd_actdir_lookup(gd_handle* h, const gd_key* act_ids, uint32_t n, uint32_t* out_ctx, uint8_t* out_flags,
+                     uint8_t* out_found);
+int gd_actdir_clear(gd_handle* h);
+int gd_actdir_count(gd_handle* h, uint64_t* out_live);
+
+/* IncomingMessageAgent.ReceiveMessage (IncomingMessageAgent.cs:92-170) for a batch in arrival order.
+ * Per message, from TargetGrain (its category), TargetActivation and Direction (NULL array = every
+ * message a Request; 0xFF = header absent = Request, Message.cs:113-116):
+ *   GD_RECV_ACTIVATION      FindTarget found a Valid activation: enqueued on its context
+ *   GD_RECV_SYSTEM_TARGET   FindSystemTarget found it, Request or Response: enqueued on its context
+ *   GD_RECV_NULL_CONTEXT    no activation, or not Valid: EnqueueReceiveMessage(msg, null, null)
+ *   GD_RECV_REJECT_UNKNOWN  system target not active here: rejection response (Unrecoverable)
+ *   GD_RECV_REJECT_OVERLOADED  CheckOverloaded's hard limit (ActivationData.cs:616-649), see limits
+ *   GD_RECV_DROPPED         system target message neither Request nor Response (logged, dropped)
+ *   GD_RECV_UNDECODED       (frames) no complete decoded address: C# deserializes it
+ * out_ctx[i] = the bucket it is enqueued in: the context index (< n_ctx), n_ctx for the null context,
+ * GD_NO_ACTIVATION when not enqueued.  perm / offsets (both or neither): the stable bucketing of the
+ * batch over n_ctx + 2 buckets -- contexts, the null context, then the messages not enqueued -- each
+ * in arrival order (WorkItemGroup FIFO, WorkItemGroup.cs:174-201); offsets has n_ctx + 3 entries.
+ * limits (NULL = none, the default options): request_count[c] = GetRequestCount() of context c when
+ * the batch starts (n_ctx entries), hard limits as SiloMessagingOptions' MaxEnqueuedRequestsHardLimit
+ * (_StatelessWorker); <= 0 = no limit.  Every enqueued message of an activation counts
+ * (IncrementEnqueuedOnDispatcherCount), as when the agent thread enqueues the batch before a worker
+ * runs any of it. */
+#define GD_RECV_ACTIVATION        0
+#define GD_RECV_SYSTEM_TARGET     1
+#define GD_RECV_NULL_CONTEXT      2
+#define GD_RECV_REJECT_UNKNOWN    3
+#define GD_RECV_REJECT_OVERLOADED 4
+#define GD_RECV_DROPPED           5
+#define GD_RECV_UNDECODED         6
+typedef struct gd_recv_limits {
+    const uint32_t* request_count;   /* [n_ctx]; device memory for the *_device entry points */
+    int32_t hard_limit;
+    int32_t hard_limit_stateless_worker;
+} gd_recv_limits;
+int gd_receive(gd_handle* h, const gd_key* target_grain, const gd_key* target_activation, const uint8_t* direction,
+               uint32_t n, uint32_t n_ctx, const gd_recv_limits* limits, uint32_t* out_ctx, uint8_t* out_status,
+               uint32_t* out_perm, uint32_t* out_offsets);
+int gd_receive_device(gd_handle* h, const gd_key* d_target_grain, const gd_key* d_target_activation,
+                      const uint8_t* d_direction, uint32_t n, uint32_t n_ctx, const gd_recv_limits* limits,
+                      uint32_t* d_ctx, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets);
+/* The same straight from the receive buffer (frames as gd_route_frames): decode -> ReceiveMessage ->
+ * bucketing.  d_out may be NULL or name the decoded fields wanted. */
+int gd_receive_frames_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
+                             uint32_t n, uint32_t n_ctx, const gd_recv_limits* limits, const gd_frame_fields* d_out,
+                             uint32_t* d_ctx, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets);
+int gd_receive_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
+                      uint32_t n_ctx, const gd_recv_limits* limits, const gd_frame_fields* out, uint32_t* out_ctx,
+                      uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets);
 
 /* ---- per-kernel timing (cfg.flags & GD_CFG_KERNEL_TIMING) ----------------------- */
 /* Up to max entries of {name, launches, total_ms} accumulated since the last reset. */

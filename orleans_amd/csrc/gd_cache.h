@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_cached(const gd_key* __restrict
                 if (probe(tab.slots, tab.mask, max_probe, h, n0, n1, tcd, a, meta)) {
                     if (a == GD_ACT_MULTI) {
                         status = GD_ROUTE_MULTI_ACT;          // RandomPlacementDirector.cs:33-53, in C#
-                    } else {
+                    } else if (tab_silo_valid(tab, slot_silo(meta))) {   // LookUpActivations' filter (:431)
                         act = a;
                         silo = slot_silo(meta);
                         status = GD_ROUTE_OK;

@@ -1,0 +1,234 @@
+// gd_dirops.h -- gfx950 device code for the directory operations around a membership change
+// (SURVEY 8 f4): IsValidSilo, VersionTag, silo removal and the handoff merge.
+//
+//   k_dir_lookup_tagged   LookUpActivations with its VersionTag and the IsValidSilo filter
+//                         (GrainDirectoryPartition.cs:385-441)
+//   k_dir_remove_silos    LocalGrainDirectory.AdjustLocalDirectory (LocalGrainDirectory.cs:351-361):
+//                         drop every entry whose activation lives on a removed silo
+//   k_cache_adjust        LocalGrainDirectory.AdjustLocalCache (:371-385): drop cached entries that
+//                         point at a removed silo or whose grain this handle now owns
+//   k_merge_apply         GrainDirectoryPartition.Merge (:497-522) with GrainInfo.Merge's
+//                         single-instance rule (:139-179): the lowest ActivationId stays, the others
+//                         are reported for Catalog.DeleteActivations
+// Integer table walks and random slot updates: HBM-bound, no MFMA.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gd_cache.h"
+#include "gd_common.h"
+#include "gd_kernels.h"
+
+namespace gd {
+
+// found: 0 = no entry (AddressesAndTag default: no list, VersionTag 0), 1 = entry with a valid
+// address, 2 = entry whose activation's silo is not valid (the filtered list is empty, the tag
+// is still returned: GrainDirectoryPartition.cs:401,425-431).
+__global__ void __launch_bounds__(BLOCK) k_dir_lookup_tagged(const gd_key* __restrict__ keys, uint32_t n,
+                                                             TableArgs tab, const uint32_t* __restrict__ vtag,
+                                                             gd_val* __restrict__ out_vals,
+                                                             int32_t* __restrict__ out_tags,
+                                                             uint8_t* __restrict__ out_found) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
+    const uint32_t h = uniform_hash(n0, n1, tcd);
+    unsigned long long s = fmix32(h) & tab.mask;
+    const uint32_t max_probe = tab.ctr->max_probe;
+    gd_val v{NONE32, NONE32};
+    int32_t tag = 0;
+    uint8_t f = 0;
+    for (uint32_t p = 0; p <= max_probe; ++p) {
+        const Slot sl = tab.slots[s];
+        const uint32_t st = slot_state(sl.meta);
+        if (st == SLOT_EMPTY) break;
+        if (st == SLOT_LIVE && sl.n0 == n0 && sl.n1 == n1 && sl.tcd == tcd) {
+            tag = (int32_t)(vtag[s] & 0x7FFFFFFFu);
+            if (sl.act == GD_ACT_MULTI || tab_silo_valid(tab, slot_silo(sl.meta))) {
+                v = gd_val{sl.act, slot_silo(sl.meta)};
+                f = 1;
+            } else {
+                f = 2;
+            }
+            break;
+        }
+        s = (s + 1) & tab.mask;
+    }
+    out_vals[i] = v;
+    out_tags[i] = tag;
+    out_found[i] = f;
+}
+
+// Silo-set membership as a bitset over silo indices (65,536 bits max).
+__device__ __forceinline__ bool in_set(const uint32_t* set, uint32_t silo) {
+    return (set[silo >> 5] >> (silo & 31u)) & 1u;
+}
+
+// AdjustLocalDirectory: RemoveActivation(grain, act, Force) for every instance on a removed
+// silo; a single-activation grain loses its only instance and so the grain.  Multi-activation
+// entries (GD_ACT_MULTI) keep no per-instance silos here: they are counted, left to the host.
+__global__ void __launch_bounds__(BLOCK) k_dir_remove_silos(Slot* slots, unsigned long long cap,
+                                                            const uint32_t* __restrict__ set, DevCounters* ctr,
+                                                            unsigned long long* __restrict__ counts) {
+    const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
+    bool rm = false, multi = false;
+    if (j < cap) {
+        const uint32_t meta = slots[j].meta;
+        if (slot_state(meta) == SLOT_LIVE && in_set(set, slot_silo(meta))) {
+            if (slots[j].act == GD_ACT_MULTI) {
+                multi = true;
+            } else {
+                slots[j].meta = make_meta(SLOT_TOMB, 0);
+                rm = true;
+            }
+        }
+    }
+    const unsigned long long b_rm = __ballot(rm), b_mu = __ballot(multi);
+    if ((threadIdx.x & (WAVE - 1)) == 0) {
+        if (b_rm) {
+            const unsigned long long c = (unsigned long long)__popcll(b_rm);
+            atomicAdd(&ctr->live, 0ull - c);
+            atomicAdd(&ctr->tomb, c);
+            atomicAdd(&counts[0], c);
+        }
+        if (b_mu) atomicAdd(&counts[1], (unsigned long long)__popcll(b_mu));
+    }
+}
+
+// AdjustLocalCache over the cache table, under the ring installed after the removal: an entry
+// goes if its grain is now owned by a local silo (CalculateTargetSilo == MyAddress) or its
+// activation lives on a removed silo (RemoveActivations with t.Item1 == removedSilo).  Removal is
+// LRU.RemoveKey: no generation moves.
+template <int MODE>
+__global__ void __launch_bounds__(BLOCK) k_cache_adjust(CacheSlot* slots, unsigned long long cap, RingArgs ring,
+                                                        const uint8_t* __restrict__ local, uint32_t n_local,
+                                                        const uint32_t* __restrict__ set, CacheCounters* ctr,
+                                                        unsigned long long* __restrict__ counts) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    stage_ring(ring, s_pts, s_own);
+    const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
+    bool rm = false;
+    if (j < cap) {
+        const uint32_t meta = slots[j].meta;
+        if (slot_state(meta) == SLOT_LIVE) {
+            const CacheSlot& c = slots[j];
+            const uint32_t owner = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(c.n0, c.n1, c.tcd))];
+            rm = (owner < n_local && local[owner]) || in_set(set, slot_silo(meta));
+            if (rm) slots[j].meta = make_meta(SLOT_TOMB, 0);
+        }
+    }
+    const unsigned long long b = __ballot(rm);
+    if ((threadIdx.x & (WAVE - 1)) == 0 && b) {
+        const unsigned long long c = (unsigned long long)__popcll(b);
+        atomicAdd(&ctr->live, 0ull - c);
+        atomicAdd(&ctr->tomb, c);
+        atomicAdd(&counts[2], c);
+    }
+}
+
+// A merge batch is a partition (a Dictionary): one item per grain.  Items sharing a slot are
+// flagged (err bit 8).
+__global__ void __launch_bounds__(BLOCK) k_dup_mark(const uint32_t* __restrict__ slot_of, uint32_t n,
+                                                    uint32_t* __restrict__ last, DevCounters* ctr) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n || slot_of[i] >= SLOT_RETRY) return;
+    if (atomicAdd(&last[slot_of[i]], 1u) != 0) atomicOr(&ctr->err, 8u);
+}
+
+// A rejected merge batch leaves no half-made entry: its new claims become tombstones (probe chains
+// through them stay intact).
+__global__ void __launch_bounds__(BLOCK) k_reg_abort(const uint32_t* __restrict__ slot_of,
+                                                     const uint8_t* __restrict__ is_new, uint32_t n, Slot* slots,
+                                                     DevCounters* ctr) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n || !is_new[i] || slot_of[i] >= SLOT_RETRY) return;
+    uint32_t expected = make_meta(SLOT_PENDING, 0);
+    if (__hip_atomic_compare_exchange_strong(&slots[slot_of[i]].meta, &expected, make_meta(SLOT_TOMB, 0),
+                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicAdd(&ctr->tomb, 1ull);
+}
+
+// gd_activation_ids_set: ids[acts[i]] = the i-th ActivationId (batch order; the last of a repeated
+// index wins only if the host repeats it -- it should not).
+__global__ void __launch_bounds__(BLOCK) k_scatter_ids(const uint32_t* __restrict__ acts,
+                                                       const gd_key* __restrict__ in, uint32_t n,
+                                                       gd_key* __restrict__ ids) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n) ids[acts[i]] = in[i];
+}
+
+// UniqueKey.CompareTo (UniqueKey.cs:255-265): TypeCodeData, then N0, then N1 (ActivationIds carry
+// no KeyExt).  < 0 when a sorts first.
+__device__ __forceinline__ int key_cmp(const gd_key& a, const gd_key& b) {
+    if (a.type_code_data != b.type_code_data) return a.type_code_data < b.type_code_data ? -1 : 1;
+    if (a.n0 != b.n0) return a.n0 < b.n0 ? -1 : 1;
+    if (a.n1 != b.n1) return a.n1 < b.n1 ? -1 : 1;
+    return 0;
+}
+
+// GD_MERGE_* statuses (include/graindispatch.h)
+constexpr uint8_t MERGE_INSERTED = 0, MERGE_KEPT = 1, MERGE_SAME = 2, MERGE_DROPPED = 3, MERGE_HOST = 4;
+
+// One item per grain (k_dup_mark); slot_of / is_new from k_reg_claim.  out_dropped[i] = the
+// activation Catalog.DeleteActivations gets (KEPT: the displaced entry, DROPPED: the incoming
+// one), else none.  ids[act] = the
+// ActivationId of host activation index act (gd_activation_ids_set); an index without one sets
+// err bit 16.  in_tags: the incoming entries' VersionTags (NULL: a new tag).
+__global__ void __launch_bounds__(BLOCK) k_merge_apply(const gd_key* __restrict__ keys,
+                                                       const gd_val* __restrict__ vals,
+                                                       const int32_t* __restrict__ in_tags, uint32_t n,
+                                                       const uint32_t* __restrict__ slot_of,
+                                                       const uint8_t* __restrict__ is_new, Slot* slots,
+                                                       uint32_t* __restrict__ vtag, DevCounters* ctr,
+                                                       const gd_key* __restrict__ ids, unsigned long long n_ids,
+                                                       uint32_t op, uint8_t* __restrict__ out_status,
+                                                       gd_val* __restrict__ out_dropped) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slot_of[i];
+    const gd_val in = vals[i];
+    gd_val dropped{NONE32, NONE32};
+    uint8_t st = MERGE_HOST;
+    if (s < SLOT_RETRY) {
+        Slot& sl = slots[s];
+        const uint32_t h = uniform_hash(keys[i].n0, keys[i].n1, keys[i].type_code_data);
+        if (is_new[i]) {                              // partitionData.Add(pair.Key, pair.Value) (:509-512)
+            sl.act = in.act;
+            sl.meta = make_meta(SLOT_LIVE, in.silo);
+            const uint32_t single = in.act == GD_ACT_MULTI ? 0u : VTAG_SINGLE;
+            vtag[s] = single | (in_tags ? ((uint32_t)in_tags[i] & 0x7FFFFFFFu) : version_tag(op, h));
+            atomicAdd(&ctr->live, 1ull);
+            st = MERGE_INSERTED;
+        } else {
+            const uint32_t cur = sl.act;
+            if (cur == GD_ACT_MULTI || in.act == GD_ACT_MULTI || !(vtag[s] & VTAG_SINGLE)) {
+                st = MERGE_HOST;                      // instance lists are unioned by C# (GrainInfo.Merge :141-152)
+            } else if (cur == in.act) {
+                st = MERGE_SAME;                      // Instances.ContainsKey -> continue; not modified (:146)
+            } else if (cur >= n_ids || in.act >= n_ids) {
+                atomicOr(&ctr->err, 16u);
+                st = MERGE_HOST;
+            } else {
+                // modified: VersionTag = rand.Next() (:154-157), then keep the lowest ActivationId (:159-176)
+                const bool in_wins = key_cmp(ids[in.act], ids[cur]) < 0;
+                if (in_wins) {
+                    dropped = gd_val{cur, slot_silo(sl.meta)};
+                    sl.act = in.act;
+                    sl.meta = make_meta(SLOT_LIVE, in.silo);
+                    st = MERGE_KEPT;
+                } else {
+                    dropped = in;
+                    st = MERGE_DROPPED;
+                }
+                vtag[s] = VTAG_SINGLE | version_tag(op, h);
+            }
+        }
+    }
+    out_status[i] = st;
+    if (out_dropped) out_dropped[i] = dropped;
+}
+
+}  // namespace gd

@@ -22,6 +22,8 @@
 #include "gd_localcomm.h"
 #include "gd_keyext.h"
 #include "gd_frames.h"
+#include "gd_dirops.h"
+#include "gd_actdir.h"
 #include "graindispatch.h"
 
 using namespace gd;
@@ -83,6 +85,26 @@ struct gd_handle {
     DevBuf cbuf[8];                   // cache scratch
     DevBuf shard_dest, shard_hist;    // exchange partition scratch
     DevBuf up_last;                   // gd_dir_upsert: last batch item per table slot (zero between calls)
+
+    // IsValidSilo (gd_dir_set_valid_silos): bitset over silo indices [0, n_valid); VersionTag and
+    // GrainInfo.SingleInstance per slot (gd_dirops.h); dir_op numbers the mutating directory calls
+    DevBuf dir_valid;
+    uint32_t n_valid = 0;
+    std::vector<uint8_t> valid_host;
+    uint32_t* vtag = nullptr;
+    uint32_t dir_op = 0;
+    DevBuf act_ids;                   // ActivationId per host activation index (gd_activation_ids_set)
+    uint64_t n_act_ids = 0;
+    DevBuf dirop_buf[4];
+
+    // ActivationDirectory of the receive path (gd_actdir.h): ActivationId -> context, flags
+    Slot* ad_slots = nullptr;
+    unsigned long long ad_cap = 0;
+    DevCounters* ad_ctr = nullptr;
+    DevCounters ad_host{};
+    DevBuf ad_last;
+    DevBuf ad_buf[8];
+    DevBuf fr_recv[3];                // frames: TargetActivation / Direction scratch when the caller wants neither
 
     // KeyExt grains (gd_keyext.h): device table + heap, and the host index both are kept from
     KxSlot* kx_slots = nullptr;
@@ -260,7 +282,13 @@ RingArgs ring_args(gd_handle* h) {
                     h->cfg.my_silo, h->cfg.seed_silo};
 }
 
-TableArgs table_args(gd_handle* h) { return TableArgs{h->slots, h->capacity - 1, h->ctr}; }
+TableArgs table_args(gd_handle* h) {
+    return TableArgs{h->slots, h->capacity - 1, h->ctr, (const uint32_t*)h->dir_valid.p, h->n_valid};
+}
+
+bool host_silo_valid(const gd_handle* h, uint32_t silo) {
+    return h->n_valid == 0 || silo >= h->n_valid || h->valid_host[silo];
+}
 
 size_t ring_lds(gd_handle* h) { return (size_t)h->ring_n * 2 * sizeof(uint32_t); }
 
@@ -280,6 +308,19 @@ int alloc_table(gd_handle* h, unsigned long long cap, Slot** out) {
         return set_err(h, GD_EHIP, "table memset: %s", hipGetErrorString(e));
     }
     *out = s;
+    return GD_OK;
+}
+
+int alloc_vtag(gd_handle* h, unsigned long long cap, uint32_t** out) {
+    uint32_t* v = nullptr;
+    hipError_t e = hipMalloc(&v, cap * sizeof(uint32_t));
+    if (e != hipSuccess) return set_err(h, GD_ENOMEM, "version tags hipMalloc(%llu): %s", cap, hipGetErrorString(e));
+    e = hipMemsetAsync(v, 0, cap * sizeof(uint32_t), h->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(v);
+        return set_err(h, GD_EHIP, "version tags memset: %s", hipGetErrorString(e));
+    }
+    *out = v;
     return GD_OK;
 }
 
@@ -343,7 +384,8 @@ int route_device(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, u
 }
 
 KxArgs kx_args(gd_handle* h) {
-    return KxArgs{h->kx_slots, h->kx_cap ? h->kx_cap - 1 : 0ull, h->kx_maxp, (const uint8_t*)h->kx_heap.p};
+    return KxArgs{h->kx_slots, h->kx_cap ? h->kx_cap - 1 : 0ull, h->kx_maxp, (const uint8_t*)h->kx_heap.p,
+                  (const uint32_t*)h->dir_valid.p, h->n_valid};
 }
 
 template <int MODE>
@@ -775,6 +817,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     h->stream = h->own_stream;
     h->capacity = pow2_at_least(cfg->table_capacity ? cfg->table_capacity : (1ull << 20));
     int r = alloc_table(h, h->capacity, &h->slots);
+    if (r == GD_OK) r = alloc_vtag(h, h->capacity, &h->vtag);
     if (r == GD_OK) {
         e = hipMalloc(&h->ctr, sizeof(DevCounters));
         if (e != hipSuccess) r = set_err(nullptr, GD_ENOMEM, "counters: %s", hipGetErrorString(e));
@@ -823,6 +866,15 @@ void gd_destroy(gd_handle* h) {
     if (h->cctr) (void)hipFree(h->cctr);
     if (h->slots) (void)hipFree(h->slots);
     if (h->ctr) (void)hipFree(h->ctr);
+    if (h->vtag) (void)hipFree(h->vtag);
+    free_buf(h->dir_valid);
+    free_buf(h->act_ids);
+    for (DevBuf& b : h->dirop_buf) free_buf(b);
+    if (h->ad_slots) (void)hipFree(h->ad_slots);
+    if (h->ad_ctr) (void)hipFree(h->ad_ctr);
+    free_buf(h->ad_last);
+    for (DevBuf& b : h->ad_buf) free_buf(b);
+    for (DevBuf& b : h->fr_recv) free_buf(b);
     for (auto& t : h->pending) {
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
@@ -954,6 +1006,7 @@ namespace {
 int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t n, gd_val* out_vals,
                   uint8_t* out_ins) {
     GD_TRY(maybe_grow_table(h, n));
+    const uint32_t op = ++h->dir_op;
     GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));   // slot_of
     GD_TRY(ensure(h, h->u32_b, (size_t)n * 4));   // win
     GD_TRY(ensure(h, h->u8_a, (size_t)n));        // is_new
@@ -967,7 +1020,7 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
     for (uint32_t pass = 0;; ++pass) {
         HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
         GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
-                      (uint32_t)(pass > 0)));
+                      (uint32_t)(pass > 0), dvals, table_args(h)));
         GD_TRY(pull_counters(h));
         if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
         if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_register: claims did not settle");
@@ -976,7 +1029,7 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
     GD_TRY(launch(h, "k_reg_resolve", g, b, 0, k_reg_resolve, (const uint32_t*)slot_of, (const uint8_t*)is_new, n,
                   (const Slot*)h->slots, win));
     GD_TRY(launch(h, "k_reg_commit", g, b, 0, k_reg_commit, (const uint32_t*)slot_of, (const uint32_t*)win, dvals, n,
-                  h->slots, h->ctr));
+                  h->slots, h->ctr, h->vtag, op));
     if (out_vals || out_ins)
         GD_TRY(launch(h, "k_reg_report", g, b, 0, k_reg_report, (const uint32_t*)slot_of, (const uint32_t*)win, n,
                       (const Slot*)h->slots, out_vals, out_ins));
@@ -1028,6 +1081,7 @@ int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t
     if (n == 0) return GD_OK;
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(maybe_grow_table(h, n));
+    const uint32_t op = ++h->dir_op;
     GD_TRY(h2d(h, h->keys_in, keys, n));
     GD_TRY(h2d(h, h->out_c, vals, n));            // gd_val staging
     GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));   // slot_of
@@ -1047,14 +1101,15 @@ int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t
     for (uint32_t pass = 0;; ++pass) {            // the registration's claim protocol (k_reg_claim)
         HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
         GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
-                      (uint32_t)(pass > 0)));
+                      (uint32_t)(pass > 0), (const gd_val*)h->out_c.p, table_args(h)));
         GD_TRY(pull_counters(h));
         if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
         if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_upsert: claims did not settle");
     }
     GD_TRY(launch(h, "k_up_last", g, b, 0, k_up_last, (const uint32_t*)slot_of, n, last));
     GD_TRY(launch(h, "k_up_apply", g, b, 0, k_up_apply, (const uint32_t*)slot_of, (const uint8_t*)is_new,
-                  (const gd_val*)h->out_c.p, n, (const uint32_t*)last, h->slots, h->ctr, (uint8_t*)h->out_b.p));
+                  (const gd_val*)h->out_c.p, n, (const uint32_t*)last, h->slots, h->ctr, (uint8_t*)h->out_b.p,
+                  h->vtag, op));
     GD_TRY(launch(h, "k_up_clear", g, b, 0, k_up_clear, (const uint32_t*)slot_of, n, last));
     if (out_inserted) GD_TRY(d2h(h, out_inserted, h->out_b, n));
     GD_TRY(pull_counters(h));
@@ -1105,6 +1160,7 @@ int gd_dir_clear(gd_handle* h) {
     if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, hipMemsetAsync(h->slots, 0, h->capacity * sizeof(Slot), h->stream));
+    HIP_TRY(h, hipMemsetAsync(h->vtag, 0, h->capacity * sizeof(uint32_t), h->stream));
     HIP_TRY(h, hipMemsetAsync(h->ctr, 0, sizeof(DevCounters), h->stream));
     if (h->kx_cap) {                   // KeyExt entries go too
         h->kx_m.assign(h->kx_cap, KxSlot{});
@@ -1125,14 +1181,22 @@ int gd_dir_rehash(gd_handle* h, uint64_t new_capacity) {
     if (cap < h->ctr_host.live) return set_err(h, GD_EINVAL, "capacity %llu below live entries", cap);
     Slot* ns = nullptr;
     GD_TRY(alloc_table(h, cap, &ns));
+    uint32_t* nv = nullptr;
+    if (alloc_vtag(h, cap, &nv) != GD_OK) {
+        (void)hipFree(ns);
+        return GD_ENOMEM;
+    }
     DevCounters fresh{};
     HIP_TRY(h, hipMemcpyAsync(h->ctr, &fresh, sizeof fresh, hipMemcpyHostToDevice, h->stream));
     const unsigned long long old_cap = h->capacity;
     const uint32_t g = (uint32_t)((old_cap + BLOCK - 1) / BLOCK);
-    GD_TRY(launch(h, "k_rehash", dim3(g), dim3(BLOCK), 0, k_rehash, (const Slot*)h->slots, old_cap, ns, cap - 1, h->ctr));
+    GD_TRY(launch(h, "k_rehash", dim3(g), dim3(BLOCK), 0, k_rehash, (const Slot*)h->slots, old_cap, ns, cap - 1, h->ctr,
+                  (const uint32_t*)h->vtag, nv));
     GD_TRY(sync(h));
     HIP_TRY(h, hipFree(h->slots));
+    HIP_TRY(h, hipFree(h->vtag));
     h->slots = ns;
+    h->vtag = nv;
     h->capacity = cap;
     h->layout_gen++;
     GD_TRY(pull_counters(h));
@@ -1460,19 +1524,33 @@ int decode_frames_device(gd_handle* h, const uint8_t* buf, uint64_t len, const u
 }
 
 // ext: KeyExt targets (string-keyed grains) are routed too, their strings read from buf itself.
+AdArgs ad_args(gd_handle* h);
+
+// ext: KeyExt targets (string-keyed grains) are routed too, their strings read from buf itself.  With an
+// ActivationDirectory (gd_actdir_add), a frame whose address is complete (GD_ROUTE_ADDRESSED) gets the
+// context of its TargetActivation as its act (k_frame_addressed_act), so it is bucketed with it.
 int route_frames_device(gd_handle* h, const uint8_t* buf, uint64_t len, const uint64_t* off, uint32_t n,
                         uint32_t n_act, const gd_frame_fields* out, uint32_t* silo, uint32_t* act, uint8_t* status,
                         uint32_t* perm, uint32_t* offsets, bool ext = false) {
     if (n) {
         GD_TRY(check_ring(h));
-        GD_TRY(decode_frames_device(h, buf, len, off, n, out, ext));
-        GD_TRY(route_device(h, out->target_grain, n, silo, act, status));
+        gd_frame_fields o2 = *out;
+        if (h->ad_slots && !o2.target_activation) {
+            GD_TRY(ensure(h, h->fr_recv[0], (size_t)n * sizeof(gd_key) + 8));
+            o2.target_activation = (gd_key*)h->fr_recv[0].p;
+        }
+        GD_TRY(decode_frames_device(h, buf, len, off, n, &o2, ext));
+        GD_TRY(route_device(h, o2.target_grain, n, silo, act, status));
         if (ext)
-            GD_TRY(keyext_pass(h, out->target_grain,
+            GD_TRY(keyext_pass(h, o2.target_grain,
                                ExtArgs{buf, (const uint64_t*)h->fr_ext[0].p, (const int32_t*)h->fr_ext[1].p, len}, n,
                                silo, act, status));
         GD_TRY(launch(h, "k_frame_status", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_frame_status,
-                      (const uint32_t*)out->flags, n, silo, act, status));
+                      (const uint32_t*)o2.flags, n, silo, act, status));
+        if (h->ad_slots)
+            GD_TRY(launch(h, "k_frame_addressed_act", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_frame_addressed_act,
+                          (const uint8_t*)status, (const gd_key*)o2.target_grain, (const gd_key*)o2.target_activation, n,
+                          ad_args(h), act));
     }
     if (perm && offsets) GD_TRY(bucket_device(h, act, n, n_act, perm, offsets));
     return GD_OK;
@@ -3177,6 +3255,11 @@ int gd_dir_register_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext,
         GD_TRY(host_ext(h, ext, i, s, len));
         uint64_t at = 0, free_at = 0;
         uint32_t dist = 0;
+        if (!host_silo_valid(h, vals[i].silo)) {    // AddSingleActivation's IsValidSilo check (:310-311)
+            if (out_vals) out_vals[i] = gd_val{NONE32, NONE32};
+            if (out_inserted) out_inserted[i] = 0;
+            continue;
+        }
         if (kx_find_host(h, keys[i], s, len, uh[i], &at, &free_at, &dist)) {     // first registration wins
             if (out_vals) out_vals[i] = gd_val{h->kx_m[at].act, slot_silo(h->kx_m[at].meta)};
             if (out_inserted) out_inserted[i] = 0;
@@ -3431,4 +3514,562 @@ int gd_dir_split_ext(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, in
     }
     return move ? kx_commit(h, dirty) : GD_OK;
 }
+}  // extern "C"
+
+// ================================================================== membership churn: IsValidSilo, VersionTag,
+// silo removal, handoff merge (gd_dirops.h)
+namespace {
+
+int set_bitset(gd_handle* h, DevBuf& b, const std::vector<uint32_t>& bits) {
+    GD_TRY(h2d(h, b, bits.data(), bits.size()));
+    return GD_OK;
+}
+
+int check_dir_err(gd_handle* h, const char* what) {
+    GD_TRY(pull_counters(h));
+    if (h->ctr_host.err) {
+        const uint32_t e = h->ctr_host.err;
+        HIP_TRY(h, hipMemsetAsync(&h->ctr->err, 0, sizeof(uint32_t), h->stream));
+        GD_TRY(sync(h));
+        if (e & 2) return set_err(h, GD_EFULL, "%s: table full (0x%x)", what, e);
+        if (e & 8) return set_err(h, GD_EINVAL, "%s: a grain appears twice in one merge batch (0x%x)", what, e);
+        if (e & 16) return set_err(h, GD_EINVAL, "%s: an activation index has no ActivationId (gd_activation_ids_set) (0x%x)", what, e);
+        return set_err(h, GD_EINVAL, "%s: device error bits 0x%x", what, e);
+    }
+    return GD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gd_dir_set_valid_silos(gd_handle* h, const uint8_t* valid, uint32_t n_silos) {
+    if (!h || (n_silos && !valid)) return set_err(h, GD_EINVAL, "null argument");
+    if (n_silos > 0x10000u) return set_err(h, GD_EINVAL, "n_silos %u above 65536", n_silos);
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(sync(h));
+    std::vector<uint32_t> bits((n_silos + 31) / 32 + 1, 0);
+    h->valid_host.assign(valid, valid + n_silos);
+    for (uint32_t s = 0; s < n_silos; ++s)
+        if (valid[s]) bits[s >> 5] |= 1u << (s & 31);
+    GD_TRY(set_bitset(h, h->dir_valid, bits));
+    GD_TRY(sync(h));
+    h->n_valid = n_silos;
+    h->layout_gen++;                  // captured micro-batch graphs bake TableArgs in
+    return GD_OK;
+}
+
+int gd_dir_lookup_tagged(gd_handle* h, const gd_key* keys, uint32_t n, gd_val* out_vals, int32_t* out_tags,
+                         uint8_t* out_found) {
+    if (!h || (n && (!keys || !out_vals || !out_tags || !out_found))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(ensure(h, h->dirop_buf[0], (size_t)n * sizeof(gd_val)));
+    GD_TRY(ensure(h, h->dirop_buf[1], (size_t)n * 4));
+    GD_TRY(ensure(h, h->dirop_buf[2], (size_t)n));
+    GD_TRY(launch(h, "k_dir_lookup_tagged", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_dir_lookup_tagged,
+                  (const gd_key*)h->keys_in.p, n, table_args(h), (const uint32_t*)h->vtag, (gd_val*)h->dirop_buf[0].p,
+                  (int32_t*)h->dirop_buf[1].p, (uint8_t*)h->dirop_buf[2].p));
+    HIP_TRY(h, hipMemcpyAsync(out_vals, h->dirop_buf[0].p, (size_t)n * sizeof(gd_val), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(out_tags, h->dirop_buf[1].p, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(out_found, h->dirop_buf[2].p, n, hipMemcpyDeviceToHost, h->stream));
+    return sync(h);
+}
+
+int gd_dir_remove_silos(gd_handle* h, const uint32_t* silos, uint32_t n_silos, uint64_t* out_removed,
+                        uint64_t* out_multi, uint64_t* out_cache_removed) {
+    if (!h || (n_silos && !silos)) return set_err(h, GD_EINVAL, "null argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    std::vector<uint32_t> bits(0x10000 / 32, 0);
+    for (uint32_t i = 0; i < n_silos; ++i) {
+        if (silos[i] > 0xFFFEu) return set_err(h, GD_EINVAL, "silo index %u out of range", silos[i]);
+        bits[silos[i] >> 5] |= 1u << (silos[i] & 31);
+    }
+    GD_TRY(set_bitset(h, h->dirop_buf[3], bits));
+    GD_TRY(ensure(h, h->dirop_buf[2], 32));
+    unsigned long long* cnt = (unsigned long long*)h->dirop_buf[2].p;
+    HIP_TRY(h, hipMemsetAsync(cnt, 0, 32, h->stream));
+    const uint32_t* set = (const uint32_t*)h->dirop_buf[3].p;
+    GD_TRY(launch(h, "k_dir_remove_silos", dim3((uint32_t)((h->capacity + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                  k_dir_remove_silos, h->slots, h->capacity, set, h->ctr, cnt));
+    if (h->cache_max) {               // AdjustLocalCache under the installed (post-removal) ring
+        GD_TRY(check_ring(h));
+        const dim3 g((uint32_t)((h->ccap + BLOCK - 1) / BLOCK)), b(BLOCK);
+        const RingArgs r = ring_args(h);
+        const uint8_t* loc = (const uint8_t*)h->cache_local.p;
+        switch (h->ring_mode) {
+            case GD_RING_DIRECTORY:
+                GD_TRY(launch(h, "k_cache_adjust", g, b, ring_lds(h), k_cache_adjust<GD_RING_DIRECTORY>, h->cslots,
+                              h->ccap, r, loc, h->cache_nsilos, set, h->cctr, cnt));
+                break;
+            case GD_RING_CONSISTENT:
+                GD_TRY(launch(h, "k_cache_adjust", g, b, ring_lds(h), k_cache_adjust<GD_RING_CONSISTENT>, h->cslots,
+                              h->ccap, r, loc, h->cache_nsilos, set, h->cctr, cnt));
+                break;
+            default:
+                GD_TRY(launch(h, "k_cache_adjust", g, b, ring_lds(h), k_cache_adjust<GD_RING_VIRTUAL_BUCKETS>, h->cslots,
+                              h->ccap, r, loc, h->cache_nsilos, set, h->cctr, cnt));
+        }
+    }
+    unsigned long long c[4] = {0, 0, 0, 0};
+    HIP_TRY(h, hipMemcpyAsync(c, cnt, 32, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(sync(h));
+    // KeyExt entries live in the host index: the same rule there
+    std::vector<uint64_t> dirty;
+    for (uint64_t j = 0; j < h->kx_cap; ++j) {
+        KxSlot& q = h->kx_m[j];
+        if (slot_state(q.meta) != SLOT_LIVE || !((bits[slot_silo(q.meta) >> 5] >> (slot_silo(q.meta) & 31)) & 1))
+            continue;
+        if (q.act == GD_ACT_MULTI) {
+            c[1]++;
+            continue;
+        }
+        q.meta = make_meta(SLOT_TOMB, slot_silo(q.meta));
+        h->kx_live--;
+        h->kx_tomb++;
+        c[0]++;
+        dirty.push_back(j);
+    }
+    if (!dirty.empty()) GD_TRY(kx_commit(h, dirty));
+    if (out_removed) *out_removed = c[0];
+    if (out_multi) *out_multi = c[1];
+    if (out_cache_removed) *out_cache_removed = c[2];
+    return GD_OK;
+}
+
+int gd_activation_ids_set(gd_handle* h, const uint32_t* acts, const gd_key* ids, uint32_t n) {
+    if (!h || (n && (!acts || !ids))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    uint64_t need = h->n_act_ids;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (acts[i] >= GD_ACT_MULTI) return set_err(h, GD_EINVAL, "activation index %u reserved", acts[i]);
+        need = std::max<uint64_t>(need, (uint64_t)acts[i] + 1);
+    }
+    if (need > h->n_act_ids) {        // grow, keeping the ids already set
+        DevBuf nb;
+        size_t cap = std::max<size_t>(need, 2 * h->n_act_ids) * sizeof(gd_key);
+        GD_TRY(ensure(h, nb, cap));
+        HIP_TRY(h, hipMemsetAsync(nb.p, 0, cap, h->stream));
+        if (h->n_act_ids)
+            HIP_TRY(h, hipMemcpyAsync(nb.p, h->act_ids.p, h->n_act_ids * sizeof(gd_key), hipMemcpyDeviceToDevice,
+                                      h->stream));
+        GD_TRY(sync(h));
+        free_buf(h->act_ids);
+        h->act_ids = nb;
+        h->n_act_ids = cap / sizeof(gd_key);
+    }
+    // scatter on the host side of a staging copy (small batches: registration is off the hot path)
+    GD_TRY(h2d(h, h->dirop_buf[0], acts, n));
+    GD_TRY(h2d(h, h->dirop_buf[1], ids, n));
+    GD_TRY(launch(h, "k_scatter_ids", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_scatter_ids,
+                  (const uint32_t*)h->dirop_buf[0].p, (const gd_key*)h->dirop_buf[1].p, n, (gd_key*)h->act_ids.p));
+    return sync(h);
+}
+
+int gd_dir_merge(gd_handle* h, const gd_key* keys, const gd_val* vals, const int32_t* tags, uint32_t n,
+                 uint8_t* out_status, gd_val* out_dropped) {
+    if (!h || (n && (!keys || !vals || !out_status))) return set_err(h, GD_EINVAL, "null argument");
+    for (uint32_t i = 0; i < n; ++i)
+        if (vals[i].silo > 0xFFFEu) return set_err(h, GD_EINVAL, "silo index %u out of range at %u", vals[i].silo, i);
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(maybe_grow_table(h, n));
+    const uint32_t op = ++h->dir_op;
+    GD_TRY(h2d(h, h->keys_in, keys, n));
+    GD_TRY(h2d(h, h->out_c, vals, n));
+    if (tags) GD_TRY(h2d(h, h->dirop_buf[1], tags, n));
+    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));   // slot_of
+    GD_TRY(ensure(h, h->u8_a, (size_t)n));        // is_new
+    GD_TRY(ensure(h, h->out_b, (size_t)n));
+    GD_TRY(ensure(h, h->out_a, (size_t)n * sizeof(gd_val)));
+    if (h->up_last.bytes < h->capacity * 4) {
+        GD_TRY(ensure(h, h->up_last, h->capacity * 4));
+        HIP_TRY(h, hipMemsetAsync(h->up_last.p, 0, h->up_last.bytes, h->stream));
+    }
+    HIP_TRY(h, hipMemsetAsync(h->u8_a.p, 0, n, h->stream));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    uint32_t* slot_of = (uint32_t*)h->u32_a.p;
+    uint8_t* is_new = (uint8_t*)h->u8_a.p;
+    const gd_key* dk = (const gd_key*)h->keys_in.p;
+    for (uint32_t pass = 0;; ++pass) {            // the registration's claim protocol; no IsValidSilo check in Merge
+        HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
+        GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, h->capacity - 1, h->ctr, slot_of,
+                      is_new, (uint32_t)(pass > 0), (const gd_val*)nullptr, table_args(h)));
+        GD_TRY(pull_counters(h));
+        if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
+        if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_merge: claims did not settle");
+    }
+    uint32_t* last = (uint32_t*)h->up_last.p;
+    GD_TRY(launch(h, "k_dup_mark", g, b, 0, k_dup_mark, (const uint32_t*)slot_of, n, last, h->ctr));
+    GD_TRY(launch(h, "k_up_clear", g, b, 0, k_up_clear, (const uint32_t*)slot_of, n, last));
+    GD_TRY(pull_counters(h));
+    if (h->ctr_host.err) {
+        // a duplicated grain: the pending claims of this batch must not stay half-made
+        GD_TRY(launch(h, "k_reg_abort", g, b, 0, k_reg_abort, (const uint32_t*)slot_of, (const uint8_t*)is_new, n,
+                      h->slots, h->ctr));
+        return check_dir_err(h, "gd_dir_merge");
+    }
+    GD_TRY(launch(h, "k_merge_apply", g, b, 0, k_merge_apply, dk, (const gd_val*)h->out_c.p,
+                  tags ? (const int32_t*)h->dirop_buf[1].p : (const int32_t*)nullptr, n, (const uint32_t*)slot_of,
+                  (const uint8_t*)is_new, h->slots, h->vtag, h->ctr, (const gd_key*)h->act_ids.p,
+                  (unsigned long long)h->n_act_ids, op, (uint8_t*)h->out_b.p, (gd_val*)h->out_a.p));
+    HIP_TRY(h, hipMemcpyAsync(out_status, h->out_b.p, n, hipMemcpyDeviceToHost, h->stream));
+    if (out_dropped)
+        HIP_TRY(h, hipMemcpyAsync(out_dropped, h->out_a.p, (size_t)n * sizeof(gd_val), hipMemcpyDeviceToHost, h->stream));
+    return check_dir_err(h, "gd_dir_merge");
+}
+
+}  // extern "C"
+
+// ================================================================== receive path: ActivationDirectory +
+// IncomingMessageAgent.ReceiveMessage (gd_actdir.h)
+namespace {
+
+AdArgs ad_args(gd_handle* h) { return AdArgs{h->ad_slots, h->ad_cap ? h->ad_cap - 1 : 0ull, h->ad_ctr}; }
+
+int receive_device(gd_handle* h, const gd_key* tg, const gd_key* ta, const uint8_t* dir, const uint32_t* fflags,
+                   uint32_t n, uint32_t n_ctx, const gd_recv_limits* lim, uint32_t* ctx, uint8_t* st, uint32_t* perm,
+                   uint32_t* offsets);
+
+// Frames -> decode (TargetGrain, TargetActivation, Direction into the caller's arrays or scratch)
+// -> ReceiveMessage -> bucketing.  Frames without a complete decoded address: RECV_UNDECODED.
+int receive_frames_device(gd_handle* h, const uint8_t* buf, uint64_t len, const uint64_t* off, uint32_t n,
+                          uint32_t n_ctx, const gd_recv_limits* lim, const gd_frame_fields* out, uint32_t* ctx,
+                          uint8_t* st, uint32_t* perm, uint32_t* offsets) {
+    gd_frame_fields o2 = *out;
+    if (n) {
+        if (!o2.target_activation) {
+            GD_TRY(ensure(h, h->fr_recv[0], (size_t)n * sizeof(gd_key) + 8));
+            o2.target_activation = (gd_key*)h->fr_recv[0].p;
+        }
+        if (!o2.direction) {
+            GD_TRY(ensure(h, h->fr_recv[1], (size_t)n + 8));
+            o2.direction = (uint8_t*)h->fr_recv[1].p;
+        }
+        GD_TRY(decode_frames_device(h, buf, len, off, n, &o2));
+    }
+    return receive_device(h, o2.target_grain, o2.target_activation, o2.direction, (const uint32_t*)o2.flags, n, n_ctx,
+                          lim, ctx, st, perm, offsets);
+}
+
+int ad_pull(gd_handle* h) {
+    HIP_TRY(h, hipMemcpyAsync(&h->ad_host, h->ad_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
+    return sync(h);
+}
+
+// (Re)build the ActivationDirectory table with cap slots (tombstones dropped).
+int ad_rehash(gd_handle* h, unsigned long long cap) {
+    Slot* ns = nullptr;
+    GD_TRY(alloc_table(h, cap, &ns));
+    if (!h->ad_ctr) {
+        hipError_t e = hipMalloc(&h->ad_ctr, sizeof(DevCounters));
+        if (e != hipSuccess) {
+            (void)hipFree(ns);
+            return set_err(h, GD_ENOMEM, "activation directory counters: %s", hipGetErrorString(e));
+        }
+    }
+    DevCounters fresh{};
+    HIP_TRY(h, hipMemcpyAsync(h->ad_ctr, &fresh, sizeof fresh, hipMemcpyHostToDevice, h->stream));
+    if (h->ad_slots) {
+        GD_TRY(launch(h, "k_rehash", dim3((uint32_t)((h->ad_cap + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, k_rehash,
+                      (const Slot*)h->ad_slots, h->ad_cap, ns, cap - 1, h->ad_ctr, (const uint32_t*)nullptr,
+                      (uint32_t*)nullptr));
+        GD_TRY(sync(h));
+        HIP_TRY(h, hipFree(h->ad_slots));
+    }
+    h->ad_slots = ns;
+    h->ad_cap = cap;
+    free_buf(h->ad_last);
+    GD_TRY(ensure(h, h->ad_last, cap * 4));
+    HIP_TRY(h, hipMemsetAsync(h->ad_last.p, 0, cap * 4, h->stream));
+    h->layout_gen++;
+    GD_TRY(ad_pull(h));
+    if (h->ad_host.err) return set_err(h, GD_EFULL, "activation directory rehash failed (0x%x)", h->ad_host.err);
+    return GD_OK;
+}
+
+int ad_reserve(gd_handle* h, uint64_t incoming) {
+    if (!h->ad_slots) return ad_rehash(h, pow2_at_least(std::max<uint64_t>(2 * incoming, 1024)));
+    GD_TRY(ad_pull(h));
+    if ((h->ad_host.live + h->ad_host.tomb + incoming) * 4 <= h->ad_cap * 3) return GD_OK;
+    unsigned long long cap = h->ad_cap;
+    while ((h->ad_host.live + incoming) * 2 > cap) cap <<= 1;
+    return ad_rehash(h, cap);
+}
+
+// ReceiveMessage for n messages already in HBM; ctx / status / perm / offsets device arrays.
+int receive_device(gd_handle* h, const gd_key* tg, const gd_key* ta, const uint8_t* dir, const uint32_t* fflags,
+                   uint32_t n, uint32_t n_ctx, const gd_recv_limits* lim, uint32_t* ctx, uint8_t* st, uint32_t* perm,
+                   uint32_t* offsets) {
+    if (n_ctx >= 0xFFFFFFFDu) return set_err(h, GD_EINVAL, "n_ctx too large");
+    if (!h->ad_slots) GD_TRY(ad_rehash(h, 1024));
+    const bool limits = lim && lim->request_count && (lim->hard_limit > 0 || lim->hard_limit_stateless_worker > 0);
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    if (n) {
+        if (limits)
+            GD_TRY(launch(h, "k_receive", g, b, 0, k_receive<true>, tg, ta, dir, fflags, n, n_ctx, ad_args(h), ctx, st));
+        else
+            GD_TRY(launch(h, "k_receive", g, b, 0, k_receive<false>, tg, ta, dir, fflags, n, n_ctx, ad_args(h), ctx, st));
+    }
+    if (!perm) return GD_OK;
+    // buckets 0..n_ctx-1 contexts, n_ctx the null context, n_ctx + 1 not enqueued (ctx NONE32 clamps there)
+    GD_TRY(bucket_device(h, ctx, n, n_ctx + 1, perm, offsets));
+    if (limits && n) {
+        GD_TRY(launch(h, "k_overload", g, b, 0, k_overload, (const uint32_t*)perm, (const uint32_t*)offsets, n_ctx, dir,
+                      lim->request_count, lim->hard_limit, lim->hard_limit_stateless_worker, ctx, st));
+        GD_TRY(bucket_device(h, ctx, n, n_ctx + 1, perm, offsets));
+    }
+    return GD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gd_actdir_add(gd_handle* h, const gd_key* act_ids, const uint32_t* ctx, const uint8_t* flags, uint32_t n,
+                  uint8_t* out_added) {
+    if (!h || (n && (!act_ids || !ctx || !flags))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(ad_reserve(h, n));
+    std::vector<gd_val> vals(n);
+    for (uint32_t i = 0; i < n; ++i) vals[i] = gd_val{ctx[i], flags[i]};
+    GD_TRY(h2d(h, h->ad_buf[0], act_ids, n));
+    GD_TRY(h2d(h, h->ad_buf[1], vals.data(), n));
+    GD_TRY(ensure(h, h->ad_buf[2], (size_t)n * 4));   // slot_of
+    GD_TRY(ensure(h, h->ad_buf[3], (size_t)n * 4));   // win
+    GD_TRY(ensure(h, h->ad_buf[4], (size_t)n));       // is_new
+    GD_TRY(ensure(h, h->ad_buf[5], (size_t)n));       // added
+    HIP_TRY(h, hipMemsetAsync(h->ad_buf[4].p, 0, n, h->stream));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    const gd_key* dk = (const gd_key*)h->ad_buf[0].p;
+    uint32_t* slot_of = (uint32_t*)h->ad_buf[2].p;
+    uint32_t* win = (uint32_t*)h->ad_buf[3].p;
+    uint8_t* is_new = (uint8_t*)h->ad_buf[4].p;
+    for (uint32_t pass = 0;; ++pass) {            // TryAdd: the registration's claim protocol, first add wins
+        HIP_TRY(h, hipMemsetAsync(&h->ad_ctr->retry, 0, sizeof(uint32_t), h->stream));
+        GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->ad_slots, h->ad_cap - 1, h->ad_ctr, slot_of,
+                      is_new, (uint32_t)(pass > 0), (const gd_val*)nullptr, TableArgs{}));
+        GD_TRY(ad_pull(h));
+        if (h->ad_host.retry == 0 || h->ad_host.err) break;
+        if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_actdir_add: claims did not settle");
+    }
+    GD_TRY(launch(h, "k_reg_minwin", g, b, 0, k_reg_minwin, (const uint32_t*)slot_of, (const uint8_t*)is_new, n,
+                  h->ad_slots));
+    GD_TRY(launch(h, "k_reg_resolve", g, b, 0, k_reg_resolve, (const uint32_t*)slot_of, (const uint8_t*)is_new, n,
+                  (const Slot*)h->ad_slots, win));
+    GD_TRY(launch(h, "k_reg_commit", g, b, 0, k_reg_commit, (const uint32_t*)slot_of, (const uint32_t*)win,
+                  (const gd_val*)h->ad_buf[1].p, n, h->ad_slots, h->ad_ctr, (uint32_t*)nullptr, 0u));
+    GD_TRY(launch(h, "k_reg_report", g, b, 0, k_reg_report, (const uint32_t*)slot_of, (const uint32_t*)win, n,
+                  (const Slot*)h->ad_slots, (gd_val*)nullptr, (uint8_t*)h->ad_buf[5].p));
+    if (out_added) HIP_TRY(h, hipMemcpyAsync(out_added, h->ad_buf[5].p, n, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(ad_pull(h));
+    if (h->ad_host.err) return set_err(h, GD_EFULL, "gd_actdir_add: device error bits 0x%x", h->ad_host.err);
+    return GD_OK;
+}
+
+int gd_actdir_remove(gd_handle* h, const gd_key* act_ids, uint32_t n, uint8_t* out_removed) {
+    if (!h || (n && !act_ids)) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->ad_slots) {
+        if (out_removed) std::memset(out_removed, 0, n);
+        return GD_OK;
+    }
+    GD_TRY(h2d(h, h->ad_buf[0], act_ids, n));
+    GD_TRY(ensure(h, h->ad_buf[2], (size_t)n * 4));
+    GD_TRY(ensure(h, h->ad_buf[5], (size_t)n));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    uint32_t* slot_of = (uint32_t*)h->ad_buf[2].p;
+    // TryRemove: the first item of a key removes it (the unregistration election, gd_kernels.h)
+    GD_TRY(launch(h, "k_ad_find", g, b, 0, k_ad_find, (const gd_key*)h->ad_buf[0].p, n, ad_args(h), slot_of));
+    GD_TRY(launch(h, "k_unreg_poison", g, b, 0, k_unreg_poison, (const uint32_t*)slot_of, n, h->ad_slots));
+    GD_TRY(launch(h, "k_unreg_min", g, b, 0, k_unreg_min, (const uint32_t*)slot_of, n, h->ad_slots));
+    GD_TRY(launch(h, "k_unreg_commit", g, b, 0, k_unreg_commit, (const uint32_t*)slot_of, n, h->ad_slots, h->ad_ctr,
+                  (uint8_t*)h->ad_buf[5].p));
+    if (out_removed) HIP_TRY(h, hipMemcpyAsync(out_removed, h->ad_buf[5].p, n, hipMemcpyDeviceToHost, h->stream));
+    return sync(h);
+}
+
+int gd_actdir_set_flags(gd_handle* h, const gd_key* act_ids, const uint8_t* flags, uint32_t n, uint8_t* out_found) {
+    if (!h || (n && (!act_ids || !flags))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->ad_slots) GD_TRY(ad_rehash(h, 1024));
+    GD_TRY(h2d(h, h->ad_buf[0], act_ids, n));
+    GD_TRY(h2d(h, h->ad_buf[1], flags, n));
+    GD_TRY(ensure(h, h->ad_buf[2], (size_t)n * 4));
+    GD_TRY(ensure(h, h->ad_buf[5], (size_t)n));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    uint32_t* slot_of = (uint32_t*)h->ad_buf[2].p;
+    uint32_t* last = (uint32_t*)h->ad_last.p;
+    GD_TRY(launch(h, "k_ad_find", g, b, 0, k_ad_find, (const gd_key*)h->ad_buf[0].p, n, ad_args(h), slot_of));
+    GD_TRY(launch(h, "k_up_last", g, b, 0, k_up_last, (const uint32_t*)slot_of, n, last));
+    GD_TRY(launch(h, "k_ad_setflags", g, b, 0, k_ad_setflags, (const uint32_t*)slot_of, (const uint8_t*)h->ad_buf[1].p, n,
+                  (const uint32_t*)last, h->ad_slots, (uint8_t*)h->ad_buf[5].p));
+    GD_TRY(launch(h, "k_up_clear", g, b, 0, k_up_clear, (const uint32_t*)slot_of, n, last));
+    if (out_found) HIP_TRY(h, hipMemcpyAsync(out_found, h->ad_buf[5].p, n, hipMemcpyDeviceToHost, h->stream));
+    return sync(h);
+}
+
+int gd_actdir_lookup(gd_handle* h, const gd_key* act_ids, uint32_t n, uint32_t* out_ctx, uint8_t* out_flags,
+                     uint8_t* out_found) {
+    if (!h || (n && (!act_ids || !out_ctx || !out_flags || !out_found))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->ad_slots) GD_TRY(ad_rehash(h, 1024));
+    GD_TRY(h2d(h, h->ad_buf[0], act_ids, n));
+    GD_TRY(ensure(h, h->ad_buf[2], (size_t)n * 4));
+    GD_TRY(ensure(h, h->ad_buf[4], (size_t)n));
+    GD_TRY(ensure(h, h->ad_buf[5], (size_t)n));
+    GD_TRY(launch(h, "k_ad_lookup", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_ad_lookup,
+                  (const gd_key*)h->ad_buf[0].p, n, ad_args(h), (uint32_t*)h->ad_buf[2].p, (uint8_t*)h->ad_buf[4].p,
+                  (uint8_t*)h->ad_buf[5].p));
+    HIP_TRY(h, hipMemcpyAsync(out_ctx, h->ad_buf[2].p, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(out_flags, h->ad_buf[4].p, n, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(out_found, h->ad_buf[5].p, n, hipMemcpyDeviceToHost, h->stream));
+    return sync(h);
+}
+
+int gd_actdir_clear(gd_handle* h) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (!h->ad_slots) return GD_OK;
+    HIP_TRY(h, hipMemsetAsync(h->ad_slots, 0, h->ad_cap * sizeof(Slot), h->stream));
+    HIP_TRY(h, hipMemsetAsync(h->ad_ctr, 0, sizeof(DevCounters), h->stream));
+    return sync(h);
+}
+
+int gd_actdir_count(gd_handle* h, uint64_t* out_live) {
+    if (!h || !out_live) return set_err(h, GD_EINVAL, "null argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    *out_live = 0;
+    if (!h->ad_slots) return GD_OK;
+    GD_TRY(ad_pull(h));
+    *out_live = h->ad_host.live;
+    return GD_OK;
+}
+
+int gd_receive_device(gd_handle* h, const gd_key* d_target_grain, const gd_key* d_target_activation,
+                      const uint8_t* d_direction, uint32_t n, uint32_t n_ctx, const gd_recv_limits* limits,
+                      uint32_t* d_ctx, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets) {
+    if (!h || (n && (!d_target_grain || !d_target_activation || !d_ctx || !d_status)))
+        return set_err(h, GD_EINVAL, "null argument");
+    if ((d_perm != nullptr) != (d_offsets != nullptr)) return set_err(h, GD_EINVAL, "perm and offsets go together");
+    HIP_TRY(h, hipSetDevice(h->device));
+    return receive_device(h, d_target_grain, d_target_activation, d_direction, nullptr, n, n_ctx, limits, d_ctx, d_status,
+                          d_perm, d_offsets);
+}
+
+int gd_receive(gd_handle* h, const gd_key* target_grain, const gd_key* target_activation, const uint8_t* direction,
+               uint32_t n, uint32_t n_ctx, const gd_recv_limits* limits, uint32_t* out_ctx, uint8_t* out_status,
+               uint32_t* out_perm, uint32_t* out_offsets) {
+    if (!h || (n && (!target_grain || !target_activation || !out_ctx || !out_status)))
+        return set_err(h, GD_EINVAL, "null argument");
+    if ((out_perm != nullptr) != (out_offsets != nullptr)) return set_err(h, GD_EINVAL, "perm and offsets go together");
+    if (n_ctx >= 0xFFFFFFFDu) return set_err(h, GD_EINVAL, "n_ctx too large");
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(h2d(h, h->keys_in, target_grain, n));
+    GD_TRY(h2d(h, h->ad_buf[6], target_activation, n));
+    const uint8_t* ddir = nullptr;
+    if (direction) {
+        GD_TRY(h2d(h, h->ad_buf[7], direction, n));
+        ddir = (const uint8_t*)h->ad_buf[7].p;
+    }
+    gd_recv_limits dl{};
+    const gd_recv_limits* pl = nullptr;
+    if (limits && limits->request_count) {
+        GD_TRY(h2d(h, h->dirop_buf[0], limits->request_count, n_ctx));
+        dl = *limits;
+        dl.request_count = (const uint32_t*)h->dirop_buf[0].p;
+        pl = &dl;
+    }
+    GD_TRY(ensure(h, h->out_a, (size_t)n * 4 + 4));
+    GD_TRY(ensure(h, h->out_c, (size_t)n + 4));
+    uint32_t* perm = nullptr;
+    uint32_t* offs = nullptr;
+    if (out_perm) {
+        GD_TRY(ensure(h, h->u8_a, (size_t)n * 4 + 4));
+        GD_TRY(ensure(h, h->offs, ((size_t)n_ctx + 3) * 4));
+        perm = (uint32_t*)h->u8_a.p;
+        offs = (uint32_t*)h->offs.p;
+    }
+    GD_TRY(receive_device(h, (const gd_key*)h->keys_in.p, (const gd_key*)h->ad_buf[6].p, ddir, nullptr, n, n_ctx, pl,
+                          (uint32_t*)h->out_a.p, (uint8_t*)h->out_c.p, perm, offs));
+    GD_TRY(d2h(h, out_ctx, h->out_a, n));
+    if (n) HIP_TRY(h, hipMemcpyAsync(out_status, h->out_c.p, n, hipMemcpyDeviceToHost, h->stream));
+    if (out_perm) {
+        GD_TRY(d2h(h, out_perm, h->u8_a, n));
+        HIP_TRY(h, hipMemcpyAsync(out_offsets, offs, ((size_t)n_ctx + 3) * 4, hipMemcpyDeviceToHost, h->stream));
+    }
+    return sync_checked(h);
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int gd_receive_frames_device(gd_handle* h, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* d_frame_off,
+                             uint32_t n, uint32_t n_ctx, const gd_recv_limits* limits, const gd_frame_fields* d_out,
+                             uint32_t* d_ctx, uint8_t* d_status, uint32_t* d_perm, uint32_t* d_offsets) {
+    GD_TRY(check_frames_args(h, d_buf, d_frame_off, n, d_out));
+    if (n && (!d_ctx || !d_status)) return set_err(h, GD_EINVAL, "null argument");
+    if ((d_perm != nullptr) != (d_offsets != nullptr)) return set_err(h, GD_EINVAL, "perm and offsets go together");
+    if (n_ctx >= 0xFFFFFFFDu) return set_err(h, GD_EINVAL, "n_ctx too large");
+    HIP_TRY(h, hipSetDevice(h->device));
+    gd_frame_fields none{};
+    return receive_frames_device(h, d_buf, buf_len, d_frame_off, n, n_ctx, limits, d_out ? d_out : &none, d_ctx, d_status,
+                                 d_perm, d_offsets);
+}
+
+int gd_receive_frames(gd_handle* h, const uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off, uint32_t n,
+                      uint32_t n_ctx, const gd_recv_limits* limits, const gd_frame_fields* out, uint32_t* out_ctx,
+                      uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (n && (!buf || !frame_off || !out_ctx || !out_status)) return set_err(h, GD_EINVAL, "null argument");
+    if ((out_perm != nullptr) != (out_offsets != nullptr)) return set_err(h, GD_EINVAL, "perm and offsets go together");
+    if (n_ctx >= 0xFFFFFFFDu) return set_err(h, GD_EINVAL, "n_ctx too large");
+    if (out && (((uintptr_t)out->target_silo | (uintptr_t)out->sending_silo) & 3))
+        return set_err(h, GD_EINVAL, "silo outputs must be 4-byte aligned");
+    HIP_TRY(h, hipSetDevice(h->device));
+    if (n) {
+        GD_TRY(h2d(h, h->fr[0], buf, (size_t)buf_len));
+        GD_TRY(h2d(h, h->fr[1], frame_off, n));
+    }
+    gd_frame_fields dev{};
+    GD_TRY(frame_scratch(h, n, out, &dev));
+    gd_recv_limits dl{};
+    const gd_recv_limits* pl = nullptr;
+    if (limits && limits->request_count) {
+        GD_TRY(h2d(h, h->dirop_buf[0], limits->request_count, n_ctx));
+        dl = *limits;
+        dl.request_count = (const uint32_t*)h->dirop_buf[0].p;
+        pl = &dl;
+    }
+    GD_TRY(ensure(h, h->fr[13], (size_t)n * 4 + 4));     // ctx
+    GD_TRY(ensure(h, h->fr[15], (size_t)n + 8));         // status
+    uint32_t* perm = nullptr;
+    uint32_t* offs = nullptr;
+    if (out_perm) {
+        GD_TRY(ensure(h, h->u8_a, (size_t)n * 4 + 4));
+        GD_TRY(ensure(h, h->offs, ((size_t)n_ctx + 3) * 4));
+        perm = (uint32_t*)h->u8_a.p;
+        offs = (uint32_t*)h->offs.p;
+    }
+    GD_TRY(receive_frames_device(h, (const uint8_t*)h->fr[0].p, buf_len, (const uint64_t*)h->fr[1].p, n, n_ctx, pl, &dev,
+                                 (uint32_t*)h->fr[13].p, (uint8_t*)h->fr[15].p, perm, offs));
+    GD_TRY(frame_results(h, n, out, &dev));
+    if (n) {
+        HIP_TRY(h, hipMemcpyAsync(out_ctx, h->fr[13].p, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipMemcpyAsync(out_status, h->fr[15].p, (size_t)n, hipMemcpyDeviceToHost, h->stream));
+    }
+    if (out_perm) {
+        if (n) HIP_TRY(h, hipMemcpyAsync(out_perm, perm, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipMemcpyAsync(out_offsets, offs, ((size_t)n_ctx + 3) * 4, hipMemcpyDeviceToHost, h->stream));
+    }
+    return sync_checked(h);
+}
+
 }  // extern "C"

@@ -152,6 +152,7 @@ __device__ __forceinline__ uint8_t route_node(uint32_t node, uint64_t tcd, const
     uint32_t a, meta;
     if (probe(tab.slots, tab.mask, max_probe, h, n0, n1, tcd, a, meta)) {
         if (a == GD_ACT_MULTI) return GD_ROUTE_MULTI_ACT;   // RandomPlacementDirector.cs:33-53, in C#
+        if (!tab_silo_valid(tab, slot_silo(meta))) return GD_ROUTE_MISS;   // IsValidSilo (:431)
         act = a;
         silo = slot_silo(meta);                    // ActivationAddress.Silo (Message.cs:629-639)
         return GD_ROUTE_OK;

@@ -110,7 +110,26 @@ struct TableArgs {
     const Slot* slots;
     unsigned long long mask;
     const DevCounters* ctr;
+    const uint32_t* valid;     // IsValidSilo bitset over silo indices [0, n_valid) (gd_dir_set_valid_silos)
+    uint32_t n_valid;          // 0: every silo valid
 };
+
+// GrainDirectoryPartition.IsValidSilo (GrainDirectoryPartition.cs:242-245): silos outside the
+// configured range count as valid.
+__device__ __forceinline__ bool valid_silo(const uint32_t* valid, uint32_t n_valid, uint32_t silo) {
+    return n_valid == 0 || silo >= n_valid || ((valid[silo >> 5] >> (silo & 31u)) & 1u);
+}
+__device__ __forceinline__ bool tab_silo_valid(const TableArgs& t, uint32_t silo) {
+    return valid_silo(t.valid, t.n_valid, silo);
+}
+
+// VersionTag side array (one u32 per table slot): bits 0..30 the tag (the reference draws
+// rand.Next() on every change, GrainDirectoryPartition.cs:106,120,135,154; here a deterministic
+// function of the change's sequence number and the grain), bit 31 = GrainInfo.SingleInstance.
+constexpr uint32_t VTAG_SINGLE = 0x80000000u;
+__device__ __host__ __forceinline__ uint32_t version_tag(uint32_t op, uint32_t h) {
+    return fmix32(h ^ (op * 0x9E3779B9u)) & 0x7FFFFFFFu;
+}
 
 __device__ __forceinline__ void stage_ring(const RingArgs& r, uint32_t* s_pts, uint32_t* s_own) {
     for (uint32_t i = threadIdx.x; i < r.n; i += blockDim.x) {
@@ -186,6 +205,8 @@ __global__ void __launch_bounds__(BLOCK) k_route(const gd_key* __restrict__ keys
             if (probe(tab.slots, tab.mask, max_probe, h, n0, n1, tcd, a, meta)) {
                 if (a == GD_ACT_MULTI) {
                     status = GD_ROUTE_MULTI_ACT;           // RandomPlacementDirector.cs:33-53, in C#
+                } else if (!tab_silo_valid(tab, slot_silo(meta))) {
+                    status = GD_ROUTE_MISS;                // LookUpActivations filters it (:431): no address
                 } else {
                     act = a;
                     silo = slot_silo(meta);                // ActivationAddress.Silo (Message.cs:629-639)
@@ -299,11 +320,11 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
             if (stt == SLOT_LIVE && k0 == n0[j] && k1 == n1[j] && k2 == tcd[j]) {
                 if (b.z == GD_ACT_MULTI) {                    // several activations: the C# random
                     status[j] = GD_ROUTE_MULTI_ACT;           // choice (RandomPlacementDirector.cs:33-53)
-                } else {
+                } else if (tab_silo_valid(tab, slot_silo(b.w))) {
                     act[j] = b.z;
                     silo[j] = slot_silo(b.w);                 // ActivationAddress.Silo (Message.cs:629-639)
                     status[j] = GD_ROUTE_OK;
-                }
+                }                                             // else: IsValidSilo filtered it (:431) -> MISS
                 break;
             }
             if (++p > max_probe) break;                        // miss: Dispatcher.cs:742 slow path
@@ -347,13 +368,21 @@ __global__ void __launch_bounds__(BLOCK) k_ring_hashes(const uint32_t* __restric
 // claim.
 constexpr uint32_t SLOT_RETRY = 0xFFFFFFFEu;
 
+// vals / valid (nullable): an item whose silo is not valid is skipped (slot_of = NONE32): the
+// IsValidSilo check of AddSingleActivation / AddActivation (GrainDirectoryPartition.cs:279,310).
 __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __restrict__ keys, uint32_t n, Slot* slots,
                                                      unsigned long long mask, DevCounters* ctr,
                                                      uint32_t* __restrict__ slot_of,
-                                                     uint8_t* __restrict__ is_new, uint32_t retry_only) {
+                                                     uint8_t* __restrict__ is_new, uint32_t retry_only,
+                                                     const gd_val* __restrict__ vals, TableArgs vt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     if (retry_only && slot_of[i] != SLOT_RETRY) return;
+    if (vals && !tab_silo_valid(vt, vals[i].silo)) {
+        slot_of[i] = NONE32;
+        is_new[i] = 0;
+        return;
+    }
     const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
     unsigned long long s = fmix32(uniform_hash(n0, n1, tcd)) & mask;
     unsigned long long dist = 0;
@@ -427,13 +456,15 @@ __global__ void __launch_bounds__(BLOCK) k_reg_resolve(const uint32_t* __restric
 __global__ void __launch_bounds__(BLOCK) k_reg_commit(const uint32_t* __restrict__ slot_of,
                                                       const uint32_t* __restrict__ win,
                                                       const gd_val* __restrict__ vals, uint32_t n, Slot* slots,
-                                                      DevCounters* ctr) {
+                                                      DevCounters* ctr, uint32_t* __restrict__ vtag, uint32_t op) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n || win[i] != i) return;
     Slot& sl = slots[slot_of[i]];
     if (vals[i].silo > 0xFFFEu) atomicOr(&ctr->err, 4u);   // silo index out of range (device-side values)
     sl.act = vals[i].act;
     sl.meta = make_meta(SLOT_LIVE, vals[i].silo);
+    // GrainInfo.AddSingleActivation: SingleInstance = true, VersionTag = rand.Next() (:110-124)
+    if (vtag) vtag[slot_of[i]] = VTAG_SINGLE | version_tag(op, uniform_hash(sl.n0, sl.n1, sl.tcd));
     atomicAdd(&ctr->live, 1ull);
 }
 
@@ -448,13 +479,18 @@ __global__ void __launch_bounds__(BLOCK) k_up_last(const uint32_t* __restrict__ 
 __global__ void __launch_bounds__(BLOCK) k_up_apply(const uint32_t* __restrict__ slot_of,
                                                     const uint8_t* __restrict__ is_new, const gd_val* __restrict__ vals,
                                                     uint32_t n, const uint32_t* __restrict__ last, Slot* slots,
-                                                    DevCounters* ctr, uint8_t* __restrict__ out_inserted) {
+                                                    DevCounters* ctr, uint8_t* __restrict__ out_inserted,
+                                                    uint32_t* __restrict__ vtag, uint32_t op) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = slot_of[i];
     uint8_t ins = 0;
     if (s < SLOT_RETRY && last[s] == i + 1) {
         Slot& sl = slots[s];
+        // GrainInfo.AddActivation (:89-108): a new tag unless the same activation is refreshed on the
+        // same silo; the entry is no longer in single-instance mode
+        const bool same = !is_new[i] && sl.act == vals[i].act && slot_silo(sl.meta) == vals[i].silo;
+        if (vtag && !same) vtag[s] = version_tag(op, uniform_hash(sl.n0, sl.n1, sl.tcd));
         sl.act = vals[i].act;
         sl.meta = make_meta(SLOT_LIVE, vals[i].silo);
         if (is_new[i]) {
@@ -555,7 +591,8 @@ __global__ void __launch_bounds__(BLOCK) k_dir_lookup(const gd_key* __restrict__
 // Rebuild: every live entry of the old table into the new one (keys are distinct,
 // so a claimer never needs to compare keys).
 __global__ void __launch_bounds__(BLOCK) k_rehash(const Slot* __restrict__ old_slots, unsigned long long old_cap,
-                                                  Slot* slots, unsigned long long mask, DevCounters* ctr) {
+                                                  Slot* slots, unsigned long long mask, DevCounters* ctr,
+                                                  const uint32_t* __restrict__ old_vtag, uint32_t* __restrict__ vtag) {
     const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
     if (j >= old_cap) return;
     const Slot sl = old_slots[j];
@@ -569,6 +606,7 @@ __global__ void __launch_bounds__(BLOCK) k_rehash(const Slot* __restrict__ old_s
             slots[s].n1 = sl.n1;
             slots[s].tcd = sl.tcd;
             slots[s].act = sl.act;
+            if (vtag) vtag[s] = old_vtag[j];
             __hip_atomic_store(&slots[s].meta, sl.meta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             atomicMax(&ctr->max_probe, dist);
             atomicAdd(&ctr->live, 1ull);

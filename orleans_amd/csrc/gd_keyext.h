@@ -29,6 +29,8 @@ struct KxArgs {
     unsigned long long mask;
     uint32_t max_probe;
     const uint8_t* heap;
+    const uint32_t* valid;     // IsValidSilo bitset (TableArgs::valid), n_valid 0 = all valid
+    uint32_t n_valid;
 };
 
 struct ExtArgs {
@@ -273,7 +275,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_keyext(const gd_key* __restrict
     bool found;
     const uint32_t uh = kx_hash_and_find(tab, n0, n1, tcd, s, len, found, act, meta);
     const uint32_t owner = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uh)];
-    if (found) {
+    if (found && valid_silo(tab.valid, tab.n_valid, slot_silo(meta))) {   // IsValidSilo filter (:431)
         out_silo[i] = slot_silo(meta);                 // ActivationAddress.Silo (Message.cs:629-639)
         out_act[i] = act;
         out_status[i] = GD_ROUTE_OK;

@@ -53,6 +53,9 @@ EXPORTED_SYMBOLS = [
     "gd_route_multi",
     "gd_multi_fetch", "gd_route_multi_ext_device", "gd_route_multi_ext", "gd_ring_owner_ext",
     "gd_dir_split_ext", "gd_dir_upsert", "gd_dir_register_device",
+    "gd_dir_set_valid_silos", "gd_dir_lookup_tagged", "gd_dir_remove_silos", "gd_activation_ids_set", "gd_dir_merge",
+    "gd_actdir_add", "gd_actdir_remove", "gd_actdir_set_flags", "gd_actdir_lookup", "gd_actdir_clear",
+    "gd_actdir_count", "gd_receive", "gd_receive_device", "gd_receive_frames_device", "gd_receive_frames",
 ]
 
 
@@ -106,6 +109,16 @@ class gd_multi_result(C.Structure):
     _fields_ = [("n_recv", C.c_uint32), ("n_act", C.c_uint32)] + [
         (f, C.c_void_p) for f in ("recv_keys", "recv_idx", "recv_src", "silo", "act", "status", "perm", "offsets",
                                   "ret_silo", "ret_act", "ret_status")]
+
+
+GD_MERGE_INSERTED, GD_MERGE_KEPT, GD_MERGE_SAME, GD_MERGE_DROPPED, GD_MERGE_HOST = 0, 1, 2, 3, 4
+ACTDIR_VALID, ACTDIR_SYSTEM_TARGET, ACTDIR_STATELESS_WORKER = 1, 2, 4
+(RECV_ACTIVATION, RECV_SYSTEM_TARGET, RECV_NULL_CONTEXT, RECV_REJECT_UNKNOWN, RECV_REJECT_OVERLOADED, RECV_DROPPED,
+ RECV_UNDECODED) = range(7)
+
+
+class gd_recv_limits(C.Structure):
+    _fields_ = [("request_count", C.c_void_p), ("hard_limit", C.c_int32), ("hard_limit_stateless_worker", C.c_int32)]
 
 
 GD_COMM_ID_BYTES = 128
@@ -195,6 +208,23 @@ def _load() -> C.CDLL:
         "gd_dir_register": (C.c_int, [P, P, P, U32, P, P]),
         "gd_dir_unregister": (C.c_int, [P, P, P, U32, P]),
         "gd_dir_register_device": (C.c_int, [P, P, P, U32, P, P]),
+        "gd_dir_set_valid_silos": (C.c_int, [P, P, U32]),
+        "gd_dir_lookup_tagged": (C.c_int, [P, P, U32, P, P, P]),
+        "gd_dir_remove_silos": (C.c_int, [P, P, U32, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]),
+        "gd_activation_ids_set": (C.c_int, [P, P, P, U32]),
+        "gd_dir_merge": (C.c_int, [P, P, P, P, U32, P, P]),
+        "gd_actdir_add": (C.c_int, [P, P, P, P, U32, P]),
+        "gd_actdir_remove": (C.c_int, [P, P, U32, P]),
+        "gd_actdir_set_flags": (C.c_int, [P, P, P, U32, P]),
+        "gd_actdir_lookup": (C.c_int, [P, P, U32, P, P, P]),
+        "gd_actdir_clear": (C.c_int, [P]),
+        "gd_actdir_count": (C.c_int, [P, C.POINTER(U64)]),
+        "gd_receive": (C.c_int, [P, P, P, P, U32, U32, C.POINTER(gd_recv_limits), P, P, P, P]),
+        "gd_receive_device": (C.c_int, [P, P, P, P, U32, U32, C.POINTER(gd_recv_limits), P, P, P, P]),
+        "gd_receive_frames_device": (C.c_int, [P, P, U64, P, U32, U32, C.POINTER(gd_recv_limits),
+                                               C.POINTER(gd_frame_fields), P, P, P, P]),
+        "gd_receive_frames": (C.c_int, [P, P, U64, P, U32, U32, C.POINTER(gd_recv_limits), C.POINTER(gd_frame_fields),
+                                        P, P, P, P]),
         "gd_dir_upsert": (C.c_int, [P, P, P, U32, P]),
         "gd_dir_lookup": (C.c_int, [P, P, U32, P, P]),
         "gd_dir_clear": (C.c_int, [P]),
@@ -424,6 +454,139 @@ class GrainDispatch:
         """gd_dir_register_device: keys (n,3) u64 and values (n,2) u32 [act, silo] in HBM."""
         self._c(lib.gd_dir_register_device(self.h, C.c_void_p(d_keys), C.c_void_p(d_vals), n,
                                            C.c_void_p(d_out_vals or 0), C.c_void_p(d_out_inserted or 0)))
+
+    # -- membership change: IsValidSilo, VersionTag, silo removal, merge (SURVEY 8 f4) ----------
+    def set_valid_silos(self, valid_silos, n_silos: int):
+        """gd_dir_set_valid_silos: the silos of [0, n_silos) that are valid (IsValidSilo); n_silos 0 =
+        every silo valid."""
+        m = np.zeros(max(n_silos, 1), dtype=np.uint8)
+        if n_silos:
+            m[[int(x) for x in valid_silos]] = 1
+        self._c(lib.gd_dir_set_valid_silos(self.h, _ptr(m), n_silos))
+
+    def lookup_tagged(self, keys):
+        """LookUpActivations with VersionTag: (act, silo, tag i32, found u8: 0 absent, 1 valid, 2 invalid silo)."""
+        k = keys_array(keys)
+        n = len(k)
+        vals = np.zeros((n, 2), np.uint32)
+        tags = np.zeros(n, np.int32)
+        found = np.zeros(n, np.uint8)
+        self._c(lib.gd_dir_lookup_tagged(self.h, _ptr(k), n, _ptr(vals), _ptr(tags), _ptr(found)))
+        return vals[:, 0].copy(), vals[:, 1].copy(), tags, found
+
+    def remove_silos(self, silos) -> dict:
+        """AdjustLocalDirectory (+ AdjustLocalCache in LocalLookup mode) for removed silos."""
+        a = np.ascontiguousarray(np.asarray(list(silos), dtype=np.uint32))
+        r, m, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._c(lib.gd_dir_remove_silos(self.h, _ptr(a) if len(a) else None, len(a), C.byref(r), C.byref(m),
+                                        C.byref(c)))
+        return {"removed": r.value, "multi": m.value, "cache_removed": c.value}
+
+    def activation_ids_set(self, acts, ids):
+        a = np.ascontiguousarray(np.asarray(acts, dtype=np.uint32))
+        k = keys_array(ids)
+        self._c(lib.gd_activation_ids_set(self.h, _ptr(a), _ptr(k), len(a)))
+
+    def merge(self, keys, acts, silos, tags=None):
+        """gd_dir_merge: (status u8, dropped act u32, dropped silo u32)."""
+        k = keys_array(keys)
+        n = len(k)
+        vals = np.zeros((n, 2), np.uint32)
+        vals[:, 0] = acts
+        vals[:, 1] = silos
+        t = None if tags is None else np.ascontiguousarray(np.asarray(tags, dtype=np.int32))
+        st = np.zeros(n, np.uint8)
+        dr = np.zeros((n, 2), np.uint32)
+        self._c(lib.gd_dir_merge(self.h, _ptr(k), _ptr(vals), None if t is None else _ptr(t), n, _ptr(st), _ptr(dr)))
+        return st, dr[:, 0].copy(), dr[:, 1].copy()
+
+    # -- receive path: ActivationDirectory + IncomingMessageAgent (SURVEY 8 a15) ------------------
+    def actdir_add(self, ids, ctx, flags) -> np.ndarray:
+        k = keys_array(ids)
+        c = np.ascontiguousarray(np.asarray(ctx, dtype=np.uint32))
+        f = np.ascontiguousarray(np.asarray(flags, dtype=np.uint8))
+        out = np.zeros(len(k), np.uint8)
+        self._c(lib.gd_actdir_add(self.h, _ptr(k), _ptr(c), _ptr(f), len(k), _ptr(out)))
+        return out
+
+    def actdir_remove(self, ids) -> np.ndarray:
+        k = keys_array(ids)
+        out = np.zeros(len(k), np.uint8)
+        self._c(lib.gd_actdir_remove(self.h, _ptr(k), len(k), _ptr(out)))
+        return out
+
+    def actdir_set_flags(self, ids, flags) -> np.ndarray:
+        k = keys_array(ids)
+        f = np.ascontiguousarray(np.asarray(flags, dtype=np.uint8))
+        out = np.zeros(len(k), np.uint8)
+        self._c(lib.gd_actdir_set_flags(self.h, _ptr(k), _ptr(f), len(k), _ptr(out)))
+        return out
+
+    def actdir_lookup(self, ids):
+        k = keys_array(ids)
+        n = len(k)
+        c = np.zeros(n, np.uint32)
+        f = np.zeros(n, np.uint8)
+        found = np.zeros(n, np.uint8)
+        self._c(lib.gd_actdir_lookup(self.h, _ptr(k), n, _ptr(c), _ptr(f), _ptr(found)))
+        return c, f, found
+
+    def actdir_clear(self):
+        self._c(lib.gd_actdir_clear(self.h))
+
+    def actdir_count(self) -> int:
+        v = C.c_uint64()
+        self._c(lib.gd_actdir_count(self.h, C.byref(v)))
+        return v.value
+
+    @staticmethod
+    def _limits(request_count, hard_limit, hard_limit_sw):
+        if request_count is None:
+            return None, None
+        rc = np.ascontiguousarray(np.asarray(request_count, dtype=np.uint32))
+        return gd_recv_limits(_ptr(rc), hard_limit, hard_limit_sw), rc
+
+    def receive(self, target_grain, target_activation, direction, n_ctx: int, request_count=None, hard_limit: int = 0,
+                hard_limit_sw: int = 0, bucket: bool = True):
+        """gd_receive: (ctx u32, status u8[, perm, offsets[n_ctx + 3]])."""
+        tg = keys_array(target_grain)
+        ta = keys_array(target_activation)
+        n = len(tg)
+        d = None if direction is None else np.ascontiguousarray(np.asarray(direction, dtype=np.uint8))
+        lim, keep = self._limits(request_count, hard_limit, hard_limit_sw)
+        ctx = np.zeros(n, np.uint32)
+        st = np.zeros(n, np.uint8)
+        perm = np.zeros(n, np.uint32) if bucket else None
+        off = np.zeros(n_ctx + 3, np.uint32) if bucket else None
+        self._c(lib.gd_receive(self.h, _ptr(tg), _ptr(ta), None if d is None else _ptr(d), n, n_ctx,
+                               None if lim is None else C.byref(lim), _ptr(ctx), _ptr(st),
+                               None if perm is None else _ptr(perm), None if off is None else _ptr(off)))
+        return (ctx, st, perm, off) if bucket else (ctx, st)
+
+    def receive_frames(self, buf: bytes, offsets, n_ctx: int, request_count=None, hard_limit: int = 0,
+                       hard_limit_sw: int = 0, fields: Optional[Iterable[str]] = ()):
+        """gd_receive_frames: (decoded fields, ctx, status, perm, offsets)."""
+        b = np.frombuffer(buf, dtype=np.uint8) if len(buf) else np.zeros(1, dtype=np.uint8)
+        off = np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
+        n = len(off)
+        arrs, ff = self._frame_host(n, fields)
+        lim, keep = self._limits(request_count, hard_limit, hard_limit_sw)
+        ctx = np.zeros(n, np.uint32)
+        st = np.zeros(n, np.uint8)
+        perm = np.zeros(n, np.uint32)
+        offs = np.zeros(n_ctx + 3, np.uint32)
+        self._c(lib.gd_receive_frames(self.h, _ptr(b), len(buf), _ptr(off), n, n_ctx,
+                                      None if lim is None else C.byref(lim), C.byref(ff), _ptr(ctx), _ptr(st),
+                                      _ptr(perm), _ptr(offs)))
+        return arrs, ctx, st, perm, offs
+
+    def receive_device(self, d_tg: int, d_ta: int, d_dir: Optional[int], n: int, n_ctx: int, d_ctx: int, d_status: int,
+                       d_perm: Optional[int], d_offsets: Optional[int], d_request_count: Optional[int] = None,
+                       hard_limit: int = 0, hard_limit_sw: int = 0):
+        lim = gd_recv_limits(d_request_count, hard_limit, hard_limit_sw) if d_request_count else None
+        self._c(lib.gd_receive_device(self.h, C.c_void_p(d_tg), C.c_void_p(d_ta), C.c_void_p(d_dir or 0), n, n_ctx,
+                                      None if lim is None else C.byref(lim), C.c_void_p(d_ctx), C.c_void_p(d_status),
+                                      C.c_void_p(d_perm or 0), C.c_void_p(d_offsets or 0)))
 
     def upsert(self, keys, acts, silos) -> np.ndarray:
         """gd_dir_upsert: overwrite, the last item of a grain wins; acts may hold GD_ACT_MULTI."""
