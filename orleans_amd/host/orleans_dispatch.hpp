@@ -14,6 +14,7 @@
 //   VirtualBucketsRingProvider          src/Orleans.Runtime/ConsistentRing/VirtualBucketsRingProvider.cs:122-293
 //   Dispatcher.AddressMessage           src/Orleans.Runtime/Core/Dispatcher.cs:715-767
 //   IncomingMessageAgent.ReceiveMessage src/Orleans.Runtime/Messaging/IncomingMessageAgent.cs:92-190
+//   ActivationDirectory                 src/Orleans.Runtime/Catalog/ActivationDirectory.cs:41-131
 //   AdaptiveGrainDirectoryCache         src/Orleans.Runtime/GrainDirectory/AdaptiveGrainDirectoryCache.cs:7-140
 //                                       (over LRU, src/Orleans.Core/Utils/LRU.cs)
 //
@@ -164,6 +165,10 @@ struct SiloAddress {
         return std::to_string(Ip[12]) + "." + std::to_string(Ip[13]) + "." + std::to_string(Ip[14]) + "." +
                std::to_string(Ip[15]) + ":" + std::to_string(Port) + "@" + std::to_string(Generation);
     }
+};
+
+struct SiloLess {            // SiloAddress.CompareTo order, for maps keyed by silo
+    bool operator()(const SiloAddress& a, const SiloAddress& b) const { return a.CompareTo(b) < 0; }
 };
 
 struct ActivationAddress {   // ActivationAddress.cs:6-34
@@ -365,8 +370,9 @@ class GrainDirectoryPartition {
 public:
     GrainDirectoryPartition(gd_handle* h, SiloTable& silos) : h_(h), silos_(silos) {}
 
-    // AddSingleActivation (GrainDirectoryPartition.cs:304-326): first registration wins.
-    // VersionTag is a random number in the reference (GrainInfo :121); here 0.
+    // AddSingleActivation (GrainDirectoryPartition.cs:304-326): first registration wins; an
+    // activation on a silo that is not valid (IsValidSilo, :310-311) is refused (no Address).
+    // VersionTag: the library's deterministic stand-in for GrainInfo's rand.Next() (:121).
     AddressAndTag AddSingleActivation(const GrainId& grain, const ActivationId& act, const SiloAddress& silo) {
         return AddSingleActivations({grain}, {act}, {silo}).at(0);
     }
@@ -401,9 +407,83 @@ public:
             for (size_t j = 0; j < idx.size(); ++j) out[idx[j]] = o[j];
         }
         std::vector<AddressAndTag> r(n);
-        for (size_t i = 0; i < n; ++i)
+        std::vector<gd_key> tk;
+        std::vector<size_t> ti;
+        for (size_t i = 0; i < n; ++i) {
+            if (out[i].act == GD_NO_ACTIVATION) continue;          // refused: IsValidSilo
             r[i].Address = ActivationAddress{silos_.At(out[i].silo), grains[i], acts_.at(out[i].act)};
+            if (!grains[i].Key.HasKeyExt()) {
+                tk.push_back(grains[i].Key.ToNative());
+                ti.push_back(i);
+            }
+        }
+        if (!tk.empty()) {
+            std::vector<gd_val> v(tk.size());
+            std::vector<int32_t> tags(tk.size());
+            std::vector<uint8_t> f(tk.size());
+            Check(h_, gd_dir_lookup_tagged(h_, tk.data(), (uint32_t)tk.size(), v.data(), tags.data(), f.data()));
+            for (size_t j = 0; j < ti.size(); ++j) r[ti[j]].VersionTag = tags[j];
+        }
         return r;
+    }
+
+    // GrainDirectoryPartition.Merge (GrainDirectoryPartition.cs:497-522) of a handed-off partition
+    // (distinct grains).  Conflicting single-activation grains keep the lowest ActivationId
+    // (GrainInfo.Merge :139-179); the activations to delete come back grouped per silo -- what the
+    // reference hands to Catalog.DeleteActivations on each silo (:514-518).  Multi-instance grains
+    // (AddActivation) are unioned here on the host.
+    std::map<SiloAddress, std::vector<ActivationAddress>, SiloLess> Merge(const std::vector<GrainId>& grains,
+                                                                          const std::vector<ActivationId>& acts,
+                                                                          const std::vector<SiloAddress>& silos) {
+        const size_t n = grains.size();
+        std::vector<gd_key> keys(n);
+        std::vector<gd_val> vals(n), dropped(n);
+        std::vector<uint8_t> st(n);
+        for (size_t i = 0; i < n; ++i) {
+            keys[i] = grains[i].Key.ToNative();
+            vals[i] = gd_val{ActIndex(acts[i]), silos_.IndexOf(silos[i])};
+        }
+        FlushIds();
+        if (n) Check(h_, gd_dir_merge(h_, keys.data(), vals.data(), nullptr, (uint32_t)n, st.data(), dropped.data()));
+        std::map<SiloAddress, std::vector<ActivationAddress>, SiloLess> del;
+        for (size_t i = 0; i < n; ++i) {
+            if (st[i] == GD_MERGE_KEPT || st[i] == GD_MERGE_DROPPED)
+                del[silos_.At(dropped[i].silo)].push_back(
+                    ActivationAddress{silos_.At(dropped[i].silo), grains[i], acts_.at(dropped[i].act)});
+            else if (st[i] == GD_MERGE_HOST && multi_.count(grains[i]))
+                AddActivation(grains[i], acts[i], silos[i]);
+        }
+        return del;
+    }
+
+    // LocalGrainDirectory.AdjustLocalDirectory (LocalGrainDirectory.cs:351-361): drop every
+    // instance located on the removed silo.  Returns the entries removed.
+    uint64_t RemoveActivationsOn(const SiloAddress& removed) {
+        const uint32_t s = silos_.IndexOf(removed);
+        uint64_t n = 0, multi = 0;
+        Check(h_, gd_dir_remove_silos(h_, &s, 1, &n, &multi, nullptr));
+        std::vector<GrainId> touched;
+        for (auto& kv : multi_)                        // multi-instance grains: their instances live here
+            for (auto it = kv.second.begin(); it != kv.second.end();)
+                if (it->second == removed) {
+                    it = kv.second.erase(it);
+                    touched.push_back(kv.first);
+                } else {
+                    ++it;
+                }
+        for (const auto& g : touched) {
+            auto& inst = multi_[g];
+            if (inst.empty()) {
+                const gd_key k = g.Key.ToNative();
+                const uint32_t a = GD_ACT_MULTI;
+                Check(h_, gd_dir_unregister(h_, &k, &a, 1, nullptr));
+                multi_.erase(g);
+                ++n;
+            } else {
+                Publish(g, inst);
+            }
+        }
+        return n;
     }
 
     // AddActivation (GrainDirectoryPartition.cs:274-302; GrainInfo.AddActivation :89-108): multi-
@@ -455,18 +535,25 @@ public:
         return removed != 0;
     }
 
-    // LookUpActivations (GrainDirectoryPartition.cs:385-441): null Addresses when absent.
+    // LookUpActivations (GrainDirectoryPartition.cs:385-441): null Addresses when absent; the
+    // addresses on silos that are not valid are filtered out (:431), the VersionTag stays.
     AddressesAndTag LookUpActivations(const GrainId& grain) const {
         const gd_key k = grain.Key.ToNative();
         gd_val v{};
         uint8_t found = 0;
+        int32_t tag = 0;
         if (grain.Key.HasKeyExt()) {
             KeyExtBatch kx({&grain.Key});
             Check(h_, gd_dir_lookup_ext(h_, &k, kx.get(), 1, &v, &found));
         } else {
-            Check(h_, gd_dir_lookup(h_, &k, 1, &v, &found));
+            Check(h_, gd_dir_lookup_tagged(h_, &k, 1, &v, &tag, &found));
         }
         AddressesAndTag r;
+        r.VersionTag = tag;
+        if (found == 2) {                              // only an invalid silo: an empty list
+            r.Addresses = std::vector<ActivationAddress>{};
+            return r;
+        }
         if (found && v.act == GD_ACT_MULTI) {          // every instance, from the host's list
             std::vector<ActivationAddress> all;
             for (const auto& kv : multi_.at(grain)) all.push_back(ActivationAddress{kv.second, grain, kv.first});
@@ -490,7 +577,16 @@ public:
         if (it != act_index_.end()) return it->second;
         acts_.push_back(a);
         act_index_.emplace(a, (uint32_t)acts_.size() - 1);
+        pending_ids_.push_back((uint32_t)acts_.size() - 1);
         return (uint32_t)acts_.size() - 1;
+    }
+    // The ActivationIds of new indices to the library (Merge orders by them).
+    void FlushIds() {
+        if (pending_ids_.empty()) return;
+        std::vector<gd_key> ids;
+        for (uint32_t i : pending_ids_) ids.push_back(acts_[i].ToNative());
+        Check(h_, gd_activation_ids_set(h_, pending_ids_.data(), ids.data(), (uint32_t)ids.size()));
+        pending_ids_.clear();
     }
     size_t ActivationCount() const { return acts_.size(); }
 
@@ -506,6 +602,7 @@ private:
     SiloTable& silos_;
     std::vector<ActivationId> acts_;
     std::map<ActivationId, uint32_t> act_index_;
+    std::vector<uint32_t> pending_ids_;
     std::map<GrainId, std::map<ActivationId, SiloAddress>> multi_;   // AddActivation grains
 };
 
@@ -607,10 +704,14 @@ public:
         m.push_back(s);
         Install(m);
     }
+    // RemoveServer (:311-345): the ring without the silo (membershipRingList.Remove), the valid silos
+    // without it, then AdjustLocalDirectory (:351-361) and, per-silo, AdjustLocalCache (:371-385).
     void RemoveServer(const SiloAddress& s) {
         auto m = ring_.Members();
+        if (std::find(m.begin(), m.end(), s) == m.end()) return;     // already removed
         m.erase(std::remove(m.begin(), m.end(), s), m.end());
         Install(m);
+        partition_.RemoveActivationsOn(s);
     }
 
     // CalculateTargetSilo (LocalGrainDirectory.cs:477-545) for a batch; excludeThisSiloIfStopping is
@@ -684,10 +785,9 @@ private:
         for (uint32_t o : ring_.Owners()) own.push_back(silos_.IndexOf(m[o]));
         std::vector<uint32_t> pts = ring_.Points();
         Check(h_, gd_ring_set(h_, GD_RING_DIRECTORY, pts.data(), own.data(), (uint32_t)pts.size()));
-        if (cacheOn_) {                    // membership changed: new IsValidSilo set
-            const auto mk = Masks();
-            Check(h_, gd_cache_set_silos(h_, mk.first.data(), mk.second.data(), (uint32_t)mk.first.size()));
-        }
+        const auto mk = Masks();           // membership changed: new IsValidSilo set (the members)
+        Check(h_, gd_dir_set_valid_silos(h_, mk.second.data(), (uint32_t)mk.second.size()));
+        if (cacheOn_) Check(h_, gd_cache_set_silos(h_, mk.first.data(), mk.second.data(), (uint32_t)mk.first.size()));
     }
     std::pair<std::vector<uint8_t>, std::vector<uint8_t>> Masks() {
         const uint32_t me = silos_.IndexOf(MyAddress);
@@ -761,12 +861,96 @@ private:
     LocalGrainDirectory& dir_;
 };
 
+// ActivationDirectory (src/Orleans.Runtime/Catalog/ActivationDirectory.cs): ActivationId -> the
+// scheduling context (index) of an activation or system target, with its state, in the GPU table.
+class ActivationDirectory {
+public:
+    explicit ActivationDirectory(gd_handle* h) : h_(h) {}
+    // RecordNewTarget (:86-93) / RecordNewSystemTarget (:95-98): TryAdd.
+    bool RecordNewTarget(const ActivationId& act, uint32_t context, bool valid, bool statelessWorker = false) {
+        return Add(act, context, (valid ? GD_ACTDIR_VALID : 0u) | (statelessWorker ? GD_ACTDIR_STATELESS_WORKER : 0u));
+    }
+    bool RecordNewSystemTarget(const ActivationId& act, uint32_t context) {
+        return Add(act, context, GD_ACTDIR_SYSTEM_TARGET | GD_ACTDIR_VALID);
+    }
+    bool RemoveTarget(const ActivationId& act) {       // :116-131, TryRemove
+        const gd_key k = act.ToNative();
+        uint8_t r = 0;
+        Check(h_, gd_actdir_remove(h_, &k, 1, &r));
+        return r != 0;
+    }
+    void SetValid(const ActivationId& act, bool valid) {   // ActivationData.SetState as the agent sees it
+        const gd_key k = act.ToNative();
+        uint32_t ctx = 0;
+        uint8_t fl = 0, found = 0;
+        Check(h_, gd_actdir_lookup(h_, &k, 1, &ctx, &fl, &found));
+        if (!found) return;
+        fl = (uint8_t)(valid ? (fl | GD_ACTDIR_VALID) : (fl & ~GD_ACTDIR_VALID));
+        Check(h_, gd_actdir_set_flags(h_, &k, &fl, 1, nullptr));
+    }
+    // FindTarget (:41-45): the context of a Valid-or-not activation, nullopt when absent.
+    std::optional<uint32_t> FindTarget(const ActivationId& act) const {
+        const gd_key k = act.ToNative();
+        uint32_t ctx = 0;
+        uint8_t fl = 0, found = 0;
+        Check(h_, gd_actdir_lookup(h_, &k, 1, &ctx, &fl, &found));
+        if (!found || (fl & GD_ACTDIR_SYSTEM_TARGET)) return std::nullopt;
+        return ctx;
+    }
+    int Count() const {
+        uint64_t n = 0;
+        Check(h_, gd_actdir_count(h_, &n));
+        return (int)n;
+    }
+
+private:
+    bool Add(const ActivationId& act, uint32_t context, uint32_t flags) {
+        const gd_key k = act.ToNative();
+        const uint8_t f = (uint8_t)flags;
+        uint8_t added = 0;
+        Check(h_, gd_actdir_add(h_, &k, &context, &f, 1, &added));
+        return added != 0;
+    }
+    gd_handle* h_;
+};
+
+// What IncomingMessageAgent.ReceiveMessage did with each message of a batch, and the per-context
+// FIFOs (WorkItemGroup.EnqueueTask, WorkItemGroup.cs:174-201).
+struct ReceiveResult {
+    std::vector<uint8_t> Status;                        // GD_RECV_*
+    std::vector<std::vector<uint32_t>> PerContext;      // batch positions per context, arrival order
+    std::vector<uint32_t> NullContext;                  // EnqueueReceiveMessage(msg, null, null)
+    std::vector<uint32_t> NotEnqueued;                  // rejections and drops
+};
+
 // Batched IncomingMessageAgent.ReceiveMessage (IncomingMessageAgent.cs:92-190) up to the
-// per-activation FIFO (ActivationData.EnqueueMessage, ActivationData.cs:566-606): returns, for each
-// activation index, the batch positions of its messages in arrival order.
+// per-activation FIFO (ActivationData.EnqueueMessage, ActivationData.cs:566-606).
 class IncomingMessageAgent {
 public:
     explicit IncomingMessageAgent(gd_handle* h) : h_(h) {}
+
+    // Messages by (TargetGrain, TargetActivation, Direction) against the ActivationDirectory.
+    ReceiveResult ReceiveMessages(const std::vector<GrainId>& targetGrain, const std::vector<ActivationId>& targetActivation,
+                                  const std::vector<uint8_t>& direction, uint32_t numContexts) {
+        const uint32_t n = (uint32_t)targetGrain.size();
+        std::vector<gd_key> tg(n), ta(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            tg[i] = targetGrain[i].Key.ToNative();
+            ta[i] = targetActivation[i].ToNative();
+        }
+        std::vector<uint32_t> ctx(n), perm(n), off((size_t)numContexts + 3);
+        ReceiveResult r;
+        r.Status.resize(n);
+        Check(h_, gd_receive(h_, tg.data(), ta.data(), direction.empty() ? nullptr : direction.data(), n, numContexts,
+                             nullptr, ctx.data(), r.Status.data(), perm.data(), off.data()));
+        r.PerContext.resize(numContexts);
+        for (uint32_t c = 0; c < numContexts; ++c) r.PerContext[c].assign(perm.begin() + off[c], perm.begin() + off[c + 1]);
+        r.NullContext.assign(perm.begin() + off[numContexts], perm.begin() + off[numContexts + 1]);
+        r.NotEnqueued.assign(perm.begin() + off[numContexts + 1], perm.begin() + off[numContexts + 2]);
+        return r;
+    }
+
+    // Activation indices already resolved (the whole-node path): the stable bucketing alone.
     std::vector<std::vector<uint32_t>> ReceiveMessages(const std::vector<uint32_t>& targetActivation,
                                                        uint32_t numActivations) {
         const uint32_t n = (uint32_t)targetActivation.size();

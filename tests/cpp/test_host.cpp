@@ -608,6 +608,100 @@ static void WholeNodeExchange() {
     }
 }
 
+// LocalGrainDirectory.RemoveServer (LocalGrainDirectory.cs:311-361): the ring loses the silo, it is
+// no longer a valid silo, and AdjustLocalDirectory drops the activations located on it; a second
+// removal is a no-op (membershipCache.Contains check, :318-322).
+static void SiloRemovalAdjustsDirectory() {
+    DispatchHandle h(0, 4096, 0);
+    const SiloAddress me = SiloAddress::New(10, 0, 0, 1, 11111, 1);
+    LocalGrainDirectory dir(h.get(), me);
+    std::vector<SiloAddress> silos{me};
+    for (int i = 2; i <= 6; ++i) {
+        silos.push_back(SiloAddress::New(10, 0, 0, (uint8_t)i, 11111, 1));
+        dir.AddServer(silos.back());
+    }
+    auto& part = dir.DirectoryPartition();
+    const int tc = gd_calculate_id_hash("BenchmarkGrains.Ping.PingGrain");
+    std::vector<GrainId> g;
+    for (int i = 0; i < 60; ++i) {
+        g.push_back(GrainId::GetGrainId(tc, i));
+        part.AddSingleActivation(g.back(), NewActivationId(100 + i), silos[i % 6]);
+    }
+    EXPECT(part.Count() == 60);
+    dir.RemoveServer(silos[3]);
+    EXPECT(part.Count() == 50);
+    for (int i = 0; i < 60; ++i) {
+        const auto r = dir.GetLocalDirectoryData(g[i]);
+        EXPECT((i % 6 == 3) ? !r.Addresses.has_value() : (r.Addresses && r.Addresses->size() == 1));
+        EXPECT(!(dir.CalculateTargetSilo(g[i]) == silos[3]));
+    }
+    // an activation on the removed silo is refused now (IsValidSilo, GrainDirectoryPartition.cs:310-311)
+    const auto refused = part.AddSingleActivation(GrainId::GetGrainId(tc, 999), NewActivationId(999), silos[3]);
+    EXPECT(!refused.Address.has_value());
+    dir.RemoveServer(silos[3]);
+    EXPECT(part.Count() == 50);
+}
+
+// GrainDirectoryPartition.Merge (:497-522): absent grains are added; for a grain held by both sides
+// the lowest ActivationId stays and the other goes to DeleteActivations on its silo.
+static void MergeKeepsLowestActivationId() {
+    DispatchHandle h(0, 4096, 0);
+    const SiloAddress me = SiloAddress::New(10, 0, 0, 1, 11111, 1), s2 = SiloAddress::New(10, 0, 0, 2, 11111, 1);
+    LocalGrainDirectory dir(h.get(), me);
+    dir.AddServer(s2);
+    auto& part = dir.DirectoryPartition();
+    const int tc = gd_calculate_id_hash("BenchmarkGrains.Ping.PingGrain");
+    const GrainId g1 = GrainId::GetGrainId(tc, 1), g2 = GrainId::GetGrainId(tc, 2), g3 = GrainId::GetGrainId(tc, 3);
+    ActivationId lo = NewActivationId(5), hi = NewActivationId(6);
+    lo.N0 = 1;
+    hi.N0 = 2;
+    part.AddSingleActivation(g1, hi, me);
+    part.AddSingleActivation(g2, lo, me);
+    const auto tag1 = part.LookUpActivations(g1).VersionTag;
+    const auto del = part.Merge({g1, g2, g3}, {lo, hi, NewActivationId(7)}, {s2, s2, s2});
+    const auto a1 = part.LookUpActivations(g1), a2 = part.LookUpActivations(g2), a3 = part.LookUpActivations(g3);
+    EXPECT(a1.Addresses && (*a1.Addresses)[0].Activation == lo && (*a1.Addresses)[0].Silo == s2);
+    EXPECT(a1.VersionTag != tag1);
+    EXPECT(a2.Addresses && (*a2.Addresses)[0].Activation == lo && (*a2.Addresses)[0].Silo == me);
+    EXPECT(a3.Addresses && (*a3.Addresses)[0].Silo == s2);
+    // hi on me (displaced from g1) and hi on s2 (the incoming one for g2) are deleted
+    EXPECT(del.size() == 2 && del.at(me).size() == 1 && del.at(s2).size() == 1);
+    EXPECT(del.at(me)[0].Activation == hi && del.at(me)[0].Grain == g1);
+    EXPECT(del.at(s2)[0].Activation == hi && del.at(s2)[0].Grain == g2);
+}
+
+// ActivationDirectory + IncomingMessageAgent.ReceiveMessage (IncomingMessageAgent.cs:92-170).
+static void ActivationDirectoryReceive() {
+    DispatchHandle h(0, 4096, 0);
+    ActivationDirectory ad(h.get());
+    IncomingMessageAgent agent(h.get());
+    const int tc = gd_calculate_id_hash("BenchmarkGrains.Ping.PingGrain");
+    const ActivationId a0 = NewActivationId(10), a1 = NewActivationId(11), a2 = NewActivationId(12);
+    EXPECT(ad.RecordNewTarget(a0, 0, true));
+    EXPECT(ad.RecordNewTarget(a1, 1, false));                  // not Valid yet
+    EXPECT(!ad.RecordNewTarget(a0, 7, true));                  // TryAdd: first wins
+    GrainId st;
+    st.Key = UniqueKey::NewKey(77, UniqueKey::Category::SystemTarget, 3);
+    EXPECT(ad.RecordNewSystemTarget(st.Key, 2));
+    EXPECT(ad.FindTarget(a0) == std::optional<uint32_t>(0) && !ad.FindTarget(st.Key) && !ad.FindTarget(a2));
+    const GrainId app = GrainId::GetGrainId(tc, 1);
+    std::vector<GrainId> tg{app, app, app, st, st, app, st};
+    std::vector<ActivationId> ta{a0, a1, a2, st.Key, st.Key, a0, a0};
+    std::vector<uint8_t> dir{0, 0, 0, 1, 2, 1, 0};
+    auto r = agent.ReceiveMessages(tg, ta, dir, 3);
+    EXPECT((r.Status == std::vector<uint8_t>{GD_RECV_ACTIVATION, GD_RECV_NULL_CONTEXT, GD_RECV_NULL_CONTEXT,
+                                             GD_RECV_SYSTEM_TARGET, GD_RECV_DROPPED, GD_RECV_ACTIVATION,
+                                             GD_RECV_REJECT_UNKNOWN}));
+    EXPECT((r.PerContext[0] == std::vector<uint32_t>{0, 5}) && r.PerContext[1].empty() &&
+           (r.PerContext[2] == std::vector<uint32_t>{3}));
+    EXPECT((r.NullContext == std::vector<uint32_t>{1, 2}) && (r.NotEnqueued == std::vector<uint32_t>{4, 6}));
+    ad.SetValid(a1, true);
+    EXPECT(ad.RemoveTarget(a0) && !ad.RemoveTarget(a0) && ad.Count() == 2);
+    r = agent.ReceiveMessages({app, app}, {a0, a1}, {}, 3);
+    EXPECT((r.Status == std::vector<uint8_t>{GD_RECV_NULL_CONTEXT, GD_RECV_ACTIVATION}));
+    EXPECT((r.PerContext[1] == std::vector<uint32_t>{1}));
+}
+
 int main(int argc, char** argv) {
     const std::string mode = argc > 1 ? argv[1] : "all";
     Run("ID_HashCorrectness", ID_HashCorrectness);
@@ -640,6 +734,9 @@ int main(int argc, char** argv) {
         Run("LruUsageTest", LruUsageTest);
         Run("PerSiloLocalLookup", PerSiloLocalLookup);
         Run("WholeNodeExchange", WholeNodeExchange);
+        Run("SiloRemovalAdjustsDirectory", SiloRemovalAdjustsDirectory);
+        Run("MergeKeepsLowestActivationId", MergeKeepsLowestActivationId);
+        Run("ActivationDirectoryReceive", ActivationDirectoryReceive);
         if (argc > 2) Run("RoutingDump", [&] { RoutingDump(argv[2]); });
     }
     std::printf("%s (%d failure%s)\n", g_failures ? "FAILED" : "OK", g_failures, g_failures == 1 ? "" : "s");
