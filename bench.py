@@ -217,6 +217,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true", help="N>1: skip the cfg3 strong-scaling measurement")
     ap.add_argument("--msgs3", type=int, default=None, help="secondary cfg3: messages per GPU (default 2^26 / N)")
     ap.add_argument("--grains3", type=int, default=None, help="secondary cfg3: grains per GPU (default 1e8 / N)")
+    ap.add_argument("--latency-batches", type=int, default=4000,
+                    help="N=1 cfg2: 4,096-message micro-batches timed for the cfg5 latency line (0: skip)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo, host-staged all-to-all")
     args = ap.parse_args()
@@ -330,6 +332,10 @@ def main():
                 "ms_per_launch": round(ceil_ms, 4), "source": "profiles/r01_ubench_random_ceiling.txt",
                 "frac_of_ceiling": round(ceil_ms / (d["ms_per_step"] / launches), 3)}
 
+    # ---- BASELINE cfg 5: 4,096-message micro-batch latency on this directory ---------
+    if world == 1 and args.workload == "cfg2" and args.latency_batches > 0:
+        secondary["cfg5_latency_us"] = micro_batch_latency(e, tcd, G_total, n_act, args.latency_batches)
+
     # ---- CPU baseline: the C restatement (oracle/cpu_ref.c), bounded sample ---------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "cfg2":
@@ -371,6 +377,36 @@ def main():
         print(json.dumps(line), flush=True)
     e.close()
     dist.destroy_process_group()
+
+
+def micro_batch_latency(e, tcd: int, G: int, n_act: int, batches: int, B: int = 4096) -> dict:
+    """BASELINE cfg 5: wall latency of one 4,096-message batch (uniform over the registered grains)
+    from keys in pinned host memory to statuses / silos / activations / per-activation runs back in
+    host memory (gd_microbatch_run: one hipGraph replay, or eager launches), p50 / p99 over
+    ``batches`` batches after 50 warmup batches.  The CPU restatement's p50 / p99 for the same batch
+    is cpu_baseline.cfg5_latency_us."""
+    mb = g.MicroBatch(e, B, n_act)
+    rng = np.random.default_rng(0x5EED0005)
+    pool = grain_keys(tcd, rng.integers(0, G, size=64 * B, dtype=np.int64)).reshape(64, B, 3)
+    out = {"batch": B, "batches": batches,
+           "path": "pinned host keys -> route -> one-workgroup radix sort + runs -> pinned host results"}
+    for use_graph in (True, False):
+        lat = np.empty(batches)
+        for i in range(50):
+            mb.keys[:] = pool[i % 64]
+            mb.run(B, use_graph)
+        for i in range(batches):
+            mb.keys[:] = pool[i % 64]
+            t0 = time.perf_counter()
+            mb.run(B, use_graph)
+            lat[i] = time.perf_counter() - t0
+        us = lat * 1e6
+        out["graph" if use_graph else "eager"] = {"p50": round(float(np.percentile(us, 50)), 1),
+                                                  "p99": round(float(np.percentile(us, 99)), 1),
+                                                  "max": round(float(us.max()), 1)}
+    out["zero_copy"] = os.environ.get("GD_MB_ZEROCOPY", "1") != "0"
+    mb.close()
+    return out
 
 
 def workload_name(w: str, world: int, n: int, g_total: int) -> str:

@@ -1339,6 +1339,17 @@ struct gd_microbatch {
     uint8_t* h_out = nullptr;      // pinned
     gd_key* d_keys = nullptr;
     uint8_t* d_out = nullptr;
+    // zero-copy (default; GD_MB_ZEROCOPY=0: staged copies): the route kernel reads the keys from the
+    // pinned host block and writes silo / status into the pinned output block, the sort kernel writes
+    // perm / runs / act there -- no H2D / D2H copy nodes; only act stays in HBM for the sort
+    bool zero_copy = true;
+    gd_key* h_keys_dev = nullptr;  // device view of h_keys
+    uint8_t* h_out_dev = nullptr;  // device view of h_out
+    uint32_t* d_act = nullptr;
+    uint32_t split = 8;                 // k_mb_sort_runs workgroups (redundant sorts, split stores; GD_MB_SPLIT)
+    uint32_t max_bits = MB_MAX_BITS;    // widest radix digit (GD_MB_MAXBITS)
+    unsigned long long* ts = nullptr;   // GD_MB_TRACE: per-phase tick sums (device), printed at destroy
+    uint64_t runs_done = 0;
     std::vector<std::pair<uint32_t, hipGraphExec_t>> graphs;
     uint64_t graphs_gen = 0;       // handle layout the cached graphs were captured against
 
@@ -1352,29 +1363,70 @@ struct gd_microbatch {
 
 namespace {
 
-// H2D keys -> route -> one-workgroup radix sort + runs -> one D2H of the whole output block.
+// H2D keys -> route -> one-workgroup radix sort + runs -> one D2H of the whole output block; or, zero-copy,
+// route (keys read from and silo / status written to pinned host memory) -> sort (perm / runs / act to host).
+template <int IT>
+int mb_launch_sort(gd_microbatch* mb, dim3 grid, uint32_t bits, const uint32_t* a, uint32_t n, uint32_t passes,
+                   uint32_t* pm, uint32_t* ra, uint32_t* rs, uint32_t* nr, uint32_t* ac) {
+    gd_handle* h = mb->h;
+    const dim3 b(MB_THREADS);
+    const uint32_t na = mb->n_act;
+    unsigned long long* ts = mb->ts;
+    switch (bits) {
+        case 4: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<4, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
+        case 5: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<5, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
+        case 6: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<6, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
+        case 7: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<7, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
+        case 8: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<8, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
+        case 9: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<9, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
+        case 10: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<10, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
+        default: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<11, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
+    }
+}
+
 int mb_enqueue(gd_microbatch* mb, uint32_t n) {
     gd_handle* h = mb->h;
-    uint8_t* d = mb->d_out;
-    if (n) {
-        HIP_TRY(h, hipMemcpyAsync(mb->d_keys, mb->h_keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice, h->stream));
-        GD_TRY(route_device(h, mb->d_keys, n, mb->out_u32(d, 0), mb->out_u32(d, 1), mb->out_status(d)));
-    }
+    const bool zc = mb->zero_copy;
+    uint8_t* d = zc ? mb->h_out_dev : mb->d_out;
+    uint32_t* act_dst = zc ? mb->d_act : mb->out_u32(d, 1);
+    // keys min(act, n_act) need key_bits; passes of at most max_bits, as even as the digits allow
     uint32_t key_bits = 1;
     while (key_bits < 32 && (mb->n_act >> key_bits) != 0) ++key_bits;
-    const uint32_t passes = (key_bits + 7) / 8;
+    const uint32_t passes = (key_bits + mb->max_bits - 1) / mb->max_bits;
     const uint32_t bits = std::max<uint32_t>(4, (key_bits + passes - 1) / passes);
-    const uint32_t* a = mb->out_u32(d, 1);
-    uint32_t *pm = mb->out_u32(d, 2), *ra = mb->out_u32(d, 5), *rs = mb->out_u32(d, 4), *nr = mb->out_u32(d, 3);
-    const dim3 g1(1), b1(MB_THREADS);
-    switch (bits) {
-        case 4: GD_TRY(launch(h, "k_mb_sort_runs", g1, b1, 0, k_mb_sort_runs<4>, a, n, passes, mb->n_act, pm, ra, rs, nr)); break;
-        case 5: GD_TRY(launch(h, "k_mb_sort_runs", g1, b1, 0, k_mb_sort_runs<5>, a, n, passes, mb->n_act, pm, ra, rs, nr)); break;
-        case 6: GD_TRY(launch(h, "k_mb_sort_runs", g1, b1, 0, k_mb_sort_runs<6>, a, n, passes, mb->n_act, pm, ra, rs, nr)); break;
-        case 7: GD_TRY(launch(h, "k_mb_sort_runs", g1, b1, 0, k_mb_sort_runs<7>, a, n, passes, mb->n_act, pm, ra, rs, nr)); break;
-        default: GD_TRY(launch(h, "k_mb_sort_runs", g1, b1, 0, k_mb_sort_runs<8>, a, n, passes, mb->n_act, pm, ra, rs, nr)); break;
+    if (n && zc && !h->cache_max) {
+        h->routed += n;
+        const dim3 g(blocks_for(n, MB_ROUTE_BLOCK)), b(MB_ROUTE_BLOCK);
+        const gd_key* k = mb->h_keys_dev;
+        uint32_t *so = mb->out_u32(d, 0);
+        uint8_t* st = mb->out_status(d);
+        switch (h->ring_mode) {
+            case GD_RING_DIRECTORY:
+                GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_DIRECTORY>, k, n, ring_args(h),
+                              table_args(h), so, act_dst, st, mb->ts));
+                break;
+            case GD_RING_CONSISTENT:
+                GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_CONSISTENT>, k, n, ring_args(h),
+                              table_args(h), so, act_dst, st, mb->ts));
+                break;
+            default:
+                GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_VIRTUAL_BUCKETS>, k, n,
+                              ring_args(h), table_args(h), so, act_dst, st, mb->ts));
+                break;
+        }
+    } else if (n) {
+        if (!zc)
+            HIP_TRY(h, hipMemcpyAsync(mb->d_keys, mb->h_keys, (size_t)n * sizeof(gd_key), hipMemcpyHostToDevice,
+                                      h->stream));
+        GD_TRY(route_device(h, zc ? mb->h_keys_dev : mb->d_keys, n, mb->out_u32(d, 0), act_dst, mb->out_status(d)));
     }
-    HIP_TRY(h, hipMemcpyAsync(mb->h_out, d, mb->out_bytes, hipMemcpyDeviceToHost, h->stream));
+    const uint32_t* a = act_dst;
+    uint32_t *pm = mb->out_u32(d, 2), *ra = mb->out_u32(d, 5), *rs = mb->out_u32(d, 4), *nr = mb->out_u32(d, 3);
+    uint32_t* ac = zc ? mb->out_u32(d, 1) : nullptr;
+    const dim3 g1(zc ? std::max<uint32_t>(1, std::min(mb->split, std::max<uint32_t>(1, n / 256))) : 1);
+    if (n <= MB_THREADS * 4) GD_TRY(mb_launch_sort<4>(mb, g1, bits, a, n, passes, pm, ra, rs, nr, ac));
+    else GD_TRY(mb_launch_sort<8>(mb, g1, bits, a, n, passes, pm, ra, rs, nr, ac));
+    if (!zc) HIP_TRY(h, hipMemcpyAsync(mb->h_out, d, mb->out_bytes, hipMemcpyDeviceToHost, h->stream));
     return GD_OK;
 }
 
@@ -1385,11 +1437,27 @@ extern "C" {
 void gd_microbatch_destroy(gd_microbatch* mb) {
     if (!mb) return;
     if (mb->h) (void)hipStreamSynchronize(mb->h->stream);
+    if (mb->ts) {
+        unsigned long long t[16] = {};
+        if (hipMemcpy(t, mb->ts, sizeof(t), hipMemcpyDeviceToHost) == hipSuccess && mb->runs_done) {
+            static const char* names[16] = {"", "route.ring", "route.core", "route.fence", "sort.p0.rank",
+                                            "sort.pass0.gather", "sort.pass1", "sort.pass2", "sort.pass3",
+                                            "sort.runs", "sort.stores", "sort.fence", "sort.clk", "sort.wall",
+                                            "sort.p0.scan", "sort.p0.scatter"};
+            std::fprintf(stderr, "[gd micro-batch trace] %llu runs, us per run:", (unsigned long long)mb->runs_done);
+            for (int k = 0; k < 16; ++k)
+                if (t[k]) std::fprintf(stderr, " %s=%.2f", names[k], t[k] * 0.01 / mb->runs_done);
+            std::fprintf(stderr, "\n");
+        }
+        (void)hipFree(mb->ts);
+    }
     for (auto& g : mb->graphs) (void)hipGraphExecDestroy(g.second);
     if (mb->h_keys) (void)hipHostFree(mb->h_keys);
     if (mb->h_out) (void)hipHostFree(mb->h_out);
     if (mb->d_keys) (void)hipFree(mb->d_keys);
     if (mb->d_out) (void)hipFree(mb->d_out);
+    if (mb->d_act) (void)hipFree(mb->d_act);
+
     delete mb;
 }
 
@@ -1405,9 +1473,21 @@ int gd_microbatch_create(gd_handle* h, uint32_t capacity, uint32_t n_act, gd_mic
     mb->n_act = n_act;
     mb->out_bytes = (5 * (size_t)capacity + 2) * 4 + capacity;
     const size_t kb = (size_t)capacity * sizeof(gd_key);
-    bool ok = hipHostMalloc((void**)&mb->h_keys, kb) == hipSuccess &&
-              hipHostMalloc((void**)&mb->h_out, mb->out_bytes) == hipSuccess &&
-              hipMalloc((void**)&mb->d_keys, kb) == hipSuccess && hipMalloc((void**)&mb->d_out, mb->out_bytes) == hipSuccess;
+    if (const char* v = std::getenv("GD_MB_ZEROCOPY")) mb->zero_copy = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_MB_MAXBITS")) mb->max_bits = (uint32_t)std::max(4, std::min(MB_MAX_BITS, std::atoi(v)));
+    if (const char* v = std::getenv("GD_MB_TRACE"))
+        if (std::atoi(v) != 0 && hipMalloc((void**)&mb->ts, 16 * sizeof(unsigned long long)) == hipSuccess)
+            (void)hipMemset(mb->ts, 0, 16 * sizeof(unsigned long long));
+    if (const char* v = std::getenv("GD_MB_SPLIT")) mb->split = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
+    // coherent (fine-grained) pinned memory: kernel stores reach the host without a cache flush
+    const unsigned hf = mb->zero_copy ? hipHostMallocCoherent : hipHostMallocDefault;
+    bool ok = hipHostMalloc((void**)&mb->h_keys, kb, hf) == hipSuccess &&
+              hipHostMalloc((void**)&mb->h_out, mb->out_bytes, hf) == hipSuccess &&
+              hipMalloc((void**)&mb->d_keys, kb) == hipSuccess && hipMalloc((void**)&mb->d_out, mb->out_bytes) == hipSuccess &&
+              hipMalloc((void**)&mb->d_act, (size_t)capacity * 4 + 4) == hipSuccess;
+    if (ok && mb->zero_copy)
+        ok = hipHostGetDevicePointer((void**)&mb->h_keys_dev, mb->h_keys, 0) == hipSuccess &&
+             hipHostGetDevicePointer((void**)&mb->h_out_dev, mb->h_out, 0) == hipSuccess;
     if (!ok) {
         gd_microbatch_destroy(mb);
         return set_err(h, GD_ENOMEM, "gd_microbatch_create: allocation failed");
@@ -1442,6 +1522,7 @@ int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
     // LocalLookup (cache) mode routes through k_route_cached, whose scratch, cache table and silo
     // masks can be reallocated between runs (gd_cache_add rehashes, gd_cache_set_silos, larger
     // gd_route* calls); a captured graph would replay freed pointers.  That mode runs eagerly.
+    ++mb->runs_done;
     if (!use_graph || h->cache_max) {
         GD_TRY(mb_enqueue(mb, n));
         return sync(h);

@@ -168,25 +168,13 @@ __device__ __forceinline__ bool probe(const Slot* slots, unsigned long long mask
 }
 
 // ------------------------------------------------------------------ K0+K1+K2: route
-// One message per thread.  PROBE=false gives CalculateTargetSilo only.
+// One message: ring owner (ring staged in LDS) and, PROBE, the directory entry.
 template <int MODE, bool PROBE>
-__global__ void __launch_bounds__(BLOCK) k_route(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
-                                                 TableArgs tab, uint32_t* __restrict__ out_silo,
-                                                 uint32_t* __restrict__ out_act,
-                                                 uint8_t* __restrict__ out_status) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
-    uint32_t* s_pts = s_ring;
-    uint32_t* s_own = s_ring + ring.n;
-    stage_ring(ring, s_pts, s_own);
-    const uint32_t max_probe = PROBE ? tab.ctr->max_probe : 0;
-
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
-    const uint64_t n0 = kp[0], n1 = kp[1], tcd = kp[2];
+__device__ __forceinline__ void route_one(uint64_t n0, uint64_t n1, uint64_t tcd, const RingArgs& ring,
+                                          const uint32_t* s_pts, const uint32_t* s_own, const TableArgs& tab,
+                                          uint32_t max_probe, uint32_t& silo, uint32_t& act, uint8_t& status) {
     const uint32_t cat = (uint32_t)(tcd >> 56);
-    uint32_t silo, act = NONE32;
-    uint8_t status;
+    act = NONE32;
     if (cat == CAT_SYSTEM_TARGET) {                        // LocalGrainDirectory.cs:480-485
         silo = ring.my_silo;
         status = GD_ROUTE_SYSTEM_TARGET;
@@ -216,6 +204,26 @@ __global__ void __launch_bounds__(BLOCK) k_route(const gd_key* __restrict__ keys
             }
         }
     }
+}
+
+// One message per thread.  PROBE=false gives CalculateTargetSilo only.
+template <int MODE, bool PROBE>
+__global__ void __launch_bounds__(BLOCK) k_route(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+                                                 TableArgs tab, uint32_t* __restrict__ out_silo,
+                                                 uint32_t* __restrict__ out_act,
+                                                 uint8_t* __restrict__ out_status) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    stage_ring(ring, s_pts, s_own);
+    const uint32_t max_probe = PROBE ? tab.ctr->max_probe : 0;
+
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
+    uint32_t silo, act;
+    uint8_t status;
+    route_one<MODE, PROBE>(kp[0], kp[1], kp[2], ring, s_pts, s_own, tab, max_probe, silo, act, status);
     out_silo[i] = silo;
     if constexpr (PROBE) {
         out_act[i] = act;
@@ -241,17 +249,14 @@ __device__ __forceinline__ void st(T* p, T v) {
 // the caches it shares with them.
 // N1: the keys arrive as N1 alone (8 B each; N0 = 0, TypeCodeData = tcd_u for all), the form a
 // compact exchange header round delivers (k_key_desc, gd_shard.h).
-template <int MODE, int M, bool NT, bool N1 = false>
-__global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
-                                                   TableArgs tab, uint32_t* __restrict__ out_silo,
-                                                   uint32_t* __restrict__ out_act,
-                                                   uint8_t* __restrict__ out_status, uint64_t tcd_u) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
-    uint32_t* s_pts = s_ring;
-    uint32_t* s_own = s_ring + ring.n;
-    stage_ring(ring, s_pts, s_own);
-    const uint32_t max_probe = tab.ctr->max_probe;
-    const uint32_t base = blockIdx.x * (BLOCK * M) + threadIdx.x;
+// The per-thread part: messages base + j * STRIDE, j < M; lds_act (optional) gets act too.
+template <int MODE, int M, int STRIDE, bool NT, bool N1>
+__device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, uint32_t n, uint32_t base,
+                                             const RingArgs& ring, const uint32_t* s_pts, const uint32_t* s_own,
+                                             const TableArgs& tab, uint32_t max_probe,
+                                             uint32_t* __restrict__ out_silo, uint32_t* __restrict__ out_act,
+                                             uint8_t* __restrict__ out_status, uint64_t tcd_u,
+                                             uint32_t* lds_act, uint32_t lds_stride) {
 
     uint64_t n0[M], n1[M], tcd[M];
     uint32_t h[M], silo[M], act[M];
@@ -259,7 +264,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
     bool need[M];
 #pragma unroll
     for (int j = 0; j < M; ++j) {
-        const uint32_t i = base + j * BLOCK;
+        const uint32_t i = base + j * STRIDE;
         n0[j] = n1[j] = tcd[j] = 0;
         if (i < n) {
             if constexpr (N1) {
@@ -336,13 +341,64 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
     }
 #pragma unroll
     for (int j = 0; j < M; ++j) {
-        const uint32_t i = base + j * BLOCK;
+        const uint32_t i = base + j * STRIDE;
         if (i < n) {
             st<NT>(out_silo + i, silo[j]);
             st<NT>(out_act + i, act[j]);
             st<NT>(out_status + i, status[j]);
+            if (lds_act) lds_act[(size_t)i * lds_stride] = act[j];
         }
     }
+}
+
+// Micro-batch route over keys in pinned host memory: one-wave workgroups, so the host reads (and
+// the host stores of silo / status) of a 4,096-message batch spread over 64 CUs.
+constexpr int MB_ROUTE_BLOCK = 64;
+
+// GD_MB_TRACE: workgroup 0, thread 0 adds phase durations (100-MHz wall clock ticks) into ts[]
+__device__ __forceinline__ void mb_mark(unsigned long long* ts, int k, unsigned long long& t) {
+    if (ts && blockIdx.x == 0 && threadIdx.x == 0) {
+        const unsigned long long now = wall_clock64();
+        if (k > 0) atomicAdd(ts + k, now - t);
+        t = now;
+    }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(MB_ROUTE_BLOCK) k_mb_route(const gd_key* __restrict__ keys, uint32_t n,
+                                                            RingArgs ring, TableArgs tab,
+                                                            uint32_t* __restrict__ out_silo,
+                                                            uint32_t* __restrict__ out_act,
+                                                            uint8_t* __restrict__ out_status,
+                                                            unsigned long long* ts) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    unsigned long long t = 0;
+    mb_mark(ts, 0, t);
+    stage_ring(ring, s_pts, s_own);
+    mb_mark(ts, 1, t);
+    route_m_core<MODE, 1, MB_ROUTE_BLOCK, false, false>(keys, n, blockIdx.x * MB_ROUTE_BLOCK + threadIdx.x, ring,
+                                                        s_pts, s_own, tab, tab.ctr->max_probe, out_silo, out_act,
+                                                        out_status, 0, nullptr, 0);
+    mb_mark(ts, 2, t);
+    if (ts) {
+        __threadfence_system();
+        mb_mark(ts, 3, t);
+    }
+}
+
+template <int MODE, int M, bool NT, bool N1 = false>
+__global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+                                                   TableArgs tab, uint32_t* __restrict__ out_silo,
+                                                   uint32_t* __restrict__ out_act,
+                                                   uint8_t* __restrict__ out_status, uint64_t tcd_u) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    stage_ring(ring, s_pts, s_own);
+    route_m_core<MODE, M, BLOCK, NT, N1>(keys, n, blockIdx.x * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own, tab,
+                                         tab.ctr->max_probe, out_silo, out_act, out_status, tcd_u, nullptr, 0);
 }
 
 // GetPrimaryTargetSilo(uint key) over raw ring keys.
@@ -1114,134 +1170,192 @@ __global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_
 }
 
 // ------------------------------------------------------------------ micro-batch bucketing (f3)
-// One workgroup sorts the whole micro-batch: LSD radix passes of BITS-bit digits of
-// min(act, n_act), each pass ranking stably inside the block (the same wave-ballot ranking as
-// k_radix_scatter, item (w, r, lane) <-> position (w * IT + r) * 64 + lane) and exchanging the
-// (key, index) pairs through LDS.  Then the runs of equal keys are compacted with ballots.
-// For micro-batches this replaces the multi-launch radix pipeline and the O(n_act) offsets:
-// the host gets perm[n] and, per activation present, run_act[r] / run_start[r]
-// (run_start[n_runs] = n), each run in arrival order (ActivationData.cs:566-606).
+// One workgroup sorts the whole micro-batch: LSD radix passes of BITS-bit digits (up to 11, so
+// 2^20..2^22 activations take 2 passes) of min(act, n_act), each pass ranking stably inside the
+// block and exchanging the (key, index) pairs through LDS.  Item (w, r, lane) <-> position
+// (w * IT + r) * 64 + lane; IT = 4 for batches up to 4,096 messages (all 16 waves busy), 8 above.
+// Ranking: per row, the wave-ballot ranking of k_radix_scatter into per-(digit, wave) counters
+// kept as packed u16 pairs in digit-major order, so ONE block-wide exclusive scan of the counters
+// gives every (digit, wave) its output base (the digits' starts and the waves' offsets at once).
+// Then the runs of equal keys are compacted with ballots.  For micro-batches this replaces the
+// multi-launch radix pipeline and the O(n_act) offsets: the host gets perm[n] and, per activation
+// present, run_act[r] / run_start[r] (run_start[n_runs] = n), each run in arrival order
+// (ActivationData.cs:566-606).
 constexpr int MB_THREADS = 1024;
-constexpr int MB_IT = 8;
-constexpr uint32_t MB_MAX = MB_THREADS * MB_IT;   // 8192 messages
+constexpr int MB_NW = MB_THREADS / WAVE;
+constexpr uint32_t MB_MAX = MB_THREADS * 8;        // 8192 messages
+constexpr int MB_MAX_BITS = 11;
 
-template <int BITS>
-__global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32_t* __restrict__ act, uint32_t n,
-                                                              uint32_t passes, uint32_t n_act,
-                                                              uint32_t* __restrict__ perm,
-                                                              uint32_t* __restrict__ run_act,
-                                                              uint32_t* __restrict__ run_start,
-                                                              uint32_t* __restrict__ n_runs) {
+struct MbShared {
+    uint32_t cnt[(1u << MB_MAX_BITS) * MB_NW / 2];  // u16 (digit, wave) counters, digit-major, 2 per word
+    uint2 kv[MB_MAX];
+    uint32_t wsum[MB_NW];
+};
+
+// Wave-wide inclusive sum with DPP (row shifts, then the row broadcasts of lanes 15 and 31): no
+// LDS round trips, unlike ds_bpermute shuffles.
+__device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return x;
+}
+
+// Block-wide exclusive sum over MB_THREADS threads (two barriers).
+__device__ __forceinline__ uint32_t mb_block_excl_sum(uint32_t v, uint32_t* s_wsum) {
+    const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    const uint32_t x = wave_incl_sum_dpp(v);
+    if (lane == WAVE - 1) s_wsum[w] = x;
+    __syncthreads();
+    const uint32_t ws = lane < (uint32_t)MB_NW ? s_wsum[lane] : 0u;
+    const uint32_t wi = wave_incl_sum_dpp(lane < w ? ws : 0u);   // sum of the waves before w
+    const uint32_t wbase = (uint32_t)__builtin_amdgcn_readlane((int)wi, WAVE - 1);
+    __syncthreads();
+    return wbase + x - v;
+}
+
+// The sort + runs over keys kk (already clamped to n_act) and indices vv held in registers.
+// Outputs are written for positions in [lo, hi) only (the calling workgroup's share; n_runs and
+// run_start[n_runs] by the share holding n).
+template <int BITS, int IT>
+__device__ __forceinline__ void mb_sort_runs_core(MbShared& sh, uint32_t (&kk)[IT], uint32_t (&vv)[IT], uint32_t n,
+                                                  uint32_t passes, uint32_t* __restrict__ perm,
+                                                  uint32_t* __restrict__ run_act, uint32_t* __restrict__ run_start,
+                                                  uint32_t* __restrict__ n_runs, uint32_t lo, uint32_t hi,
+                                                  unsigned long long* ts) {
     constexpr uint32_t R = 1u << BITS;
-    constexpr int NW = MB_THREADS / WAVE;
-    __shared__ uint32_t s_wcnt[NW][R];
-    __shared__ uint32_t s_lstart[R];
-    __shared__ uint2 s_kv[MB_MAX];
-    __shared__ uint32_t s_wsum[NW];
+    constexpr uint32_t WORDS = R * MB_NW / 2;
+    constexpr uint32_t WPT = WORDS >= MB_THREADS ? WORDS / MB_THREADS : 1;   // counter words per thread
+    constexpr uint32_t COLS = WORDS / WPT;
+    // scan word q (q = thread * WPT + j) lives at word (q % WPT) * COLS + q / WPT: the scan's reads
+    // are unit-stride across lanes, the ranking atomics spread over the banks by digit
+    auto cw = [](uint32_t q) { return (q % WPT) * COLS + q / WPT; };
+    static_assert(BITS <= MB_MAX_BITS && IT * MB_THREADS <= (int)MB_MAX, "micro-batch shape");
+    uint32_t* s_cnt = sh.cnt;
+    uint2* s_kv = sh.kv;
+    uint32_t* s_wsum = sh.wsum;
     const uint32_t lane = lane_id(), w = threadIdx.x / WAVE;
     const unsigned long long lt = (1ull << lane) - 1ull;
-    uint32_t kk[MB_IT], vv[MB_IT];
-#pragma unroll
-    for (int r = 0; r < MB_IT; ++r) {
-        const uint32_t idx = (w * MB_IT + r) * WAVE + lane;
-        const uint32_t a = act[idx < n ? idx : (n ? n - 1 : 0)];
-        kk[r] = a < n_act ? a : n_act;
-        vv[r] = idx;
-    }
+    unsigned long long t = 0;
+    mb_mark(ts, 0, t);
+    const unsigned long long c0 = ts ? clock64() : 0, r0 = t;
+    for (uint32_t e = threadIdx.x * 4; e < WORDS; e += MB_THREADS * 4)
+        *reinterpret_cast<uint4*>(s_cnt + e) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const uint32_t shift = pass * BITS;
-        for (uint32_t d = threadIdx.x; d < R; d += MB_THREADS)
-#pragma unroll
-            for (int ww = 0; ww < NW; ++ww) s_wcnt[ww][d] = 0;
-        __syncthreads();
         // Stable in-wave rank by ds_add_rtn (lanes served in ascending order, wave LDS ops in program
         // order: the k_radix_scatter ranking); the first live lane's digit group takes one update.
-        // Rows past n are skipped wave-uniformly (a 4096-message batch fills half the rows).
-        uint32_t rk[MB_IT], lead[MB_IT];
-        unsigned long long hot[MB_IT];
+        // Rows past n are skipped wave-uniformly.
+        uint32_t rk[IT], lead[IT];
+        unsigned long long hot[IT];
 #pragma unroll
-        for (int r = 0; r < MB_IT; ++r) {
+        for (int r = 0; r < IT; ++r) {
             rk[r] = 0;
             hot[r] = 0;
             lead[r] = 0;
-            if ((uint32_t)(w * MB_IT + r) * WAVE >= n) continue;
-            const bool valid = (w * MB_IT + r) * WAVE + lane < n;
+            if ((uint32_t)(w * IT + r) * WAVE >= n) continue;
+            const bool valid = (w * IT + r) * WAVE + lane < n;
             const uint32_t d = (kk[r] >> shift) & (R - 1);
             const unsigned long long live = __ballot(valid);
             lead[r] = (uint32_t)__ffsll((long long)live) - 1;
             const uint32_t hd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead[r]);
             hot[r] = __ballot(valid && d == hd);
-            if (valid && (d != hd || lane == lead[r]))
-                rk[r] = atomicAdd(&s_wcnt[w][d], lane == lead[r] ? (uint32_t)__popcll(hot[r]) : 1u);
+            if (valid && (d != hd || lane == lead[r])) {
+                const uint32_t e = d * MB_NW + w, sh16 = (e & 1u) * 16u;
+                const uint32_t inc = lane == lead[r] ? (uint32_t)__popcll(hot[r]) : 1u;
+                rk[r] = (atomicAdd(&s_cnt[cw(e >> 1)], inc << sh16) >> sh16) & 0xFFFFu;
+            }
         }
 #pragma unroll
-        for (int r = 0; r < MB_IT; ++r) {
-            if ((uint32_t)(w * MB_IT + r) * WAVE >= n) continue;
+        for (int r = 0; r < IT; ++r) {
+            if ((uint32_t)(w * IT + r) * WAVE >= n) continue;
             const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)rk[r], (int)lead[r]);
             if ((hot[r] >> lane) & 1ull) rk[r] = b0 + (uint32_t)__popcll(hot[r] & lt);
         }
         __syncthreads();
-        uint32_t total = 0;
-        if (threadIdx.x < R) {
-            uint32_t run = 0;
+        if (pass == 0) mb_mark(ts, 4, t);
+        // exclusive scan of the counters in (digit, wave) order: base of every (digit, wave)
+        {
+            const bool mine = threadIdx.x < COLS;
+            uint32_t cv[WPT];
+            uint32_t sum = 0;
 #pragma unroll
-            for (int ww = 0; ww < NW; ++ww) {
-                const uint32_t t = s_wcnt[ww][threadIdx.x];
-                s_wcnt[ww][threadIdx.x] = run;
-                run += t;
+            for (uint32_t j = 0; j < WPT; ++j) {
+                cv[j] = mine ? s_cnt[j * COLS + threadIdx.x] : 0u;
+                sum += (cv[j] & 0xFFFFu) + (cv[j] >> 16);
             }
-            total = run;
-        }
-        const uint32_t ex = block_excl_scan_add_n<MB_THREADS>(total, s_wsum);
-        if (threadIdx.x < R) s_lstart[threadIdx.x] = ex;
-        __syncthreads();
+            uint32_t run = mb_block_excl_sum(sum, s_wsum);
+            if (mine) {
 #pragma unroll
-        for (int r = 0; r < MB_IT; ++r) {
-            if ((w * MB_IT + r) * WAVE + lane < n) {
+                for (uint32_t j = 0; j < WPT; ++j) {
+                    const uint32_t a = run;
+                    run += cv[j] & 0xFFFFu;
+                    s_cnt[j * COLS + threadIdx.x] = a | (run << 16);
+                    run += cv[j] >> 16;
+                }
+            }
+        }
+        __syncthreads();
+        if (pass == 0) mb_mark(ts, 14, t);
+#pragma unroll
+        for (int r = 0; r < IT; ++r) {
+            if ((w * IT + r) * WAVE + lane < n) {
                 const uint32_t d = (kk[r] >> shift) & (R - 1);
-                s_kv[s_lstart[d] + s_wcnt[w][d] + rk[r]] = make_uint2(kk[r], vv[r]);
+                const uint32_t e = d * MB_NW + w;
+                const uint32_t base = (s_cnt[cw(e >> 1)] >> ((e & 1u) * 16u)) & 0xFFFFu;
+                s_kv[base + rk[r]] = make_uint2(kk[r], vv[r]);
             }
         }
         __syncthreads();
+        if (pass == 0) mb_mark(ts, 15, t);
 #pragma unroll
-        for (int r = 0; r < MB_IT; ++r) {
-            const uint32_t p = (w * MB_IT + r) * WAVE + lane;
+        for (int r = 0; r < IT; ++r) {
+            const uint32_t p = (w * IT + r) * WAVE + lane;
             if (p < n) {
                 const uint2 kv = s_kv[p];
                 kk[r] = kv.x;
                 vv[r] = kv.y;
             }
         }
+        if (pass + 1 < passes)       // the counters are free again: clear them for the next pass
+            for (uint32_t e = threadIdx.x * 4; e < WORDS; e += MB_THREADS * 4)
+                *reinterpret_cast<uint4*>(s_cnt + e) = make_uint4(0, 0, 0, 0);
         __syncthreads();
+        mb_mark(ts, 5 + (int)pass, t);
     }
     // runs: a head where the key changes; wave w owns positions [w * IT * 64, (w + 1) * IT * 64)
     // in (r, lane) order, so heads are counted per wave, scanned across waves, ranked in-wave.
-    uint32_t prev[MB_IT];
+    uint32_t prev[IT];
 #pragma unroll
-    for (int r = 0; r < MB_IT; ++r) {
-        const uint32_t p = (w * MB_IT + r) * WAVE + lane;
+    for (int r = 0; r < IT; ++r) {
+        const uint32_t p = (w * IT + r) * WAVE + lane;
         // key of position p - 1: lane - 1 of the same row, lane 63 of the previous row, or the
         // previous wave's last item (read through LDS, which still holds the sorted pairs)
         const uint32_t up = __shfl_up(kk[r], 1, WAVE);
         uint32_t pk = up;
-        if (lane == 0) pk = p > 0 ? s_kv[p - 1].x : ~0u;
+        if (lane == 0) pk = (p > 0 && p - 1 < n) ? s_kv[p - 1].x : ~0u;
         prev[r] = pk;
     }
     uint32_t heads_w = 0;
-    unsigned long long hb[MB_IT];
+    unsigned long long hb[IT];
 #pragma unroll
-    for (int r = 0; r < MB_IT; ++r) {
-        const uint32_t p = (w * MB_IT + r) * WAVE + lane;
+    for (int r = 0; r < IT; ++r) {
+        const uint32_t p = (w * IT + r) * WAVE + lane;
         hb[r] = __ballot(p < n && (p == 0 || prev[r] != kk[r]));
         heads_w += (uint32_t)__popcll(hb[r]);
     }
-    const uint32_t wbase = block_excl_scan_add_n<MB_THREADS>(lane == 0 ? heads_w : 0u, s_wsum);
+    const uint32_t wbase = mb_block_excl_sum(lane == 0 ? heads_w : 0u, s_wsum);
+    mb_mark(ts, 9, t);
     const uint32_t base = __shfl(wbase, 0, WAVE);
     uint32_t before = base;
 #pragma unroll
-    for (int r = 0; r < MB_IT; ++r) {
-        const uint32_t p = (w * MB_IT + r) * WAVE + lane;
-        if (p < n) {
+    for (int r = 0; r < IT; ++r) {
+        const uint32_t p = (w * IT + r) * WAVE + lane;
+        if (p < n && p >= lo && p < hi) {
             perm[p] = vv[r];
             if ((hb[r] >> lane) & 1ull) {
                 const uint32_t q = before + (uint32_t)__popcll(hb[r] & lt);
@@ -1251,11 +1365,48 @@ __global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32_t* __r
         }
         before += (uint32_t)__popcll(hb[r]);
     }
-    if (threadIdx.x == MB_THREADS - 1) {
+    if (threadIdx.x == MB_THREADS - 1 && n >= lo && n < hi) {
         const uint32_t tot = base + heads_w;   // last wave's base + its heads = all runs
         n_runs[0] = tot;
         run_start[tot] = n;
     }
+    mb_mark(ts, 10, t);
+    if (ts) {
+        __threadfence_system();
+        mb_mark(ts, 11, t);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {     // shader clocks vs wall ticks over the kernel
+            atomicAdd(ts + 12, clock64() - c0);
+            atomicAdd(ts + 13, t - r0);
+        }
+    }
+}
+
+// gridDim.x workgroups sort the same batch redundantly and each writes its 1/gridDim.x share of
+// the outputs: zero-copy stores to host memory are spread over as many CUs.  act_copy (optional):
+// the activations also go to the host block.
+template <int BITS, int IT>
+__global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32_t* __restrict__ act, uint32_t n,
+                                                              uint32_t passes, uint32_t n_act,
+                                                              uint32_t* __restrict__ perm,
+                                                              uint32_t* __restrict__ run_act,
+                                                              uint32_t* __restrict__ run_start,
+                                                              uint32_t* __restrict__ n_runs,
+                                                              uint32_t* __restrict__ act_copy,
+                                                              unsigned long long* ts) {
+    __shared__ MbShared sh;
+    const uint32_t lane = lane_id(), w = threadIdx.x / WAVE;
+    const uint32_t lo = (uint32_t)((uint64_t)n * blockIdx.x / gridDim.x);
+    const uint32_t hi = blockIdx.x + 1 == gridDim.x ? n + 1 : (uint32_t)((uint64_t)n * (blockIdx.x + 1) / gridDim.x);
+    uint32_t kk[IT], vv[IT];
+#pragma unroll
+    for (int r = 0; r < IT; ++r) {
+        const uint32_t idx = (w * IT + r) * WAVE + lane;
+        const uint32_t a = act[idx < n ? idx : (n ? n - 1 : 0)];
+        if (act_copy && idx < n && idx >= lo && idx < hi) act_copy[idx] = a;
+        kk[r] = a < n_act ? a : n_act;
+        vv[r] = idx;
+    }
+    mb_sort_runs_core<BITS, IT>(sh, kk, vv, n, passes, perm, run_act, run_start, n_runs, lo, hi, ts);
 }
 
 }  // namespace gd

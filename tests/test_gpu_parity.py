@@ -360,18 +360,33 @@ def _check_runs(mb, n, want_act, n_act):
     assert np.array_equal(np.diff(mb.run_start[:r + 1]), np.bincount(clamped, minlength=n_act + 1)[ua])
 
 
-def test_microbatch_graph_matches_eager_and_oracle(gd):
+MB_VARIANTS = {  # GD_MB_* switches read at gd_microbatch_create
+    "zero_copy": {},
+    "zero_copy_one_sorter": {"GD_MB_SPLIT": "1"},
+    "digits_7": {"GD_MB_MAXBITS": "7"},
+    "digits_4": {"GD_MB_MAXBITS": "4"},
+    "staged_copies": {"GD_MB_ZEROCOPY": "0"},
+}
+
+
+@pytest.mark.parametrize("variant,mode", [("zero_copy", "D"), ("zero_copy", "R"), ("zero_copy", "V"),
+                                          ("zero_copy_one_sorter", "V"), ("digits_7", "D"),
+                                          ("digits_4", "R"),
+                                          ("staged_copies", "V")])
+def test_microbatch_graph_matches_eager_and_oracle(gd, monkeypatch, variant, mode):
+    for k, v in MB_VARIANTS[variant].items():
+        monkeypatch.setenv(k, v)
     silos = o.bench_silos(8)
-    spec = o.ring_spec(silos, "D")
+    spec = o.ring_spec(silos, mode)
     G = 50000
-    e = _engine(gd, silos, "D", cap=1 << 17)
+    e = _engine(gd, silos, mode, cap=1 << 17)
     reg = o.grain_keys(TC, np.arange(G))
     owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1]))
     e.register(reg, np.arange(G), owner)
     d = o.DirectoryArrays(reg, np.arange(G), owner)
-    mb = gd.MicroBatch(e, 4096, G)
+    mb = gd.MicroBatch(e, 8192, G)
     rng = np.random.default_rng(55)
-    for n in (4096, 4096, 1000, 4096, 1, 0, 1000, 2):
+    for n in (4096, 8192, 1000, 4096, 1, 0, 4097, 2, 6000):
         hot = rng.integers(0, 64, size=n)                           # skewed: many messages per activation
         keys = o.grain_keys(TC, np.where(rng.random(n) < 0.5, hot, rng.integers(0, G + 300, size=n)))
         mb.keys[:n] = keys
