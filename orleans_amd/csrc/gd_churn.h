@@ -5,9 +5,13 @@
 // (GrainDirectoryHandoffManager.cs:212-218): "CalculateTargetSilo(grain) is not me", where "me"
 // is the set of silos whose partitions this handle holds.  The owner is computed under the
 // installed ring exactly as k_route computes it (LocalGrainDirectory.cs:477-545).  Entries are
-// emitted in slot order (a scan of per-slot flags), so the output is deterministic.  The merge on
-// the receiving side is a batched AddSingleActivation (gd_dir_register): first registration wins
-// and conflicts are reported, the mirror of GrainDirectoryPartition.Merge (:497-520).
+// emitted in slot order (a scan of per-slot flags), so the output is deterministic.  The receiving
+// side of a join is what ProcessSiloAddEvent sends the successor: RegisterMany(split,
+// singleActivation: true) (GrainDirectoryHandoffManager.cs:229 -> RemoteGrainDirectory.cs:31-43 ->
+// RegisterAsync -> AddSingleActivation), i.e. a batched gd_dir_register where the first
+// registration wins and the existing address is reported.  GrainDirectoryPartition.Merge
+// (:497-522, the lowest-ActivationId rule of GrainInfo.Merge :139-179) is the silo-REMOVAL path
+// (ProcessSiloRemoveEvent, GrainDirectoryHandoffManager.cs:125-158): gd_dir_merge, gd_dirops.h.
 #pragma once
 #include <hip/hip_runtime.h>
 
