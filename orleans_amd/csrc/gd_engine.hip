@@ -157,6 +157,11 @@ struct gd_handle {
     bool compact_headers = true;   // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
     bool fused_starts = true;   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
+    int fan_ilp = 2;                  // fan-out items per thread in flight together (GD_FAN_ILP: 1, 2, 4)
+
+    // pinned host scratch for small device -> host read-backs (counts, totals)
+    void* h_pin = nullptr;
+    size_t h_pin_bytes = 0;
 
     // per-kernel timing
     bool timing = false;
@@ -433,6 +438,16 @@ int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inc
                 uint32_t* out = nullptr) {
     if (n == 0) return GD_OK;
     if (!out) out = data;
+    // too many 1,024-entry tiles to fold but few 4,096-entry ones: the wide tiles, 2 launches
+    if (blocks_for(n, SCAN_TILE) > 2048 && blocks_for(n, 4 * SCAN_TILE) <= 4096) {
+        const uint32_t nbw = blocks_for(n, 4 * SCAN_TILE);
+        GD_TRY(ensure(h, h->partials, (size_t)nbw * sizeof(uint32_t)));
+        uint32_t* part = (uint32_t*)h->partials.p;
+        GD_TRY(launch(h, "k_scan_reduce", dim3(nbw), dim3(BLOCK), 0, k_scan_reduce<Op, 16>, (const uint32_t*)data, n,
+                      reverse, part));
+        return launch(h, "k_scan_down", dim3(nbw), dim3(BLOCK), 0, k_scan_down<Op, 16>, (const uint32_t*)data, out, n,
+                      reverse, inclusive, (const uint32_t*)part, nbw);
+    }
     const uint32_t nb = blocks_for(n, SCAN_TILE);
     GD_TRY(ensure(h, h->partials, (size_t)nb * sizeof(uint32_t)));
     uint32_t* part = (uint32_t*)h->partials.p;
@@ -574,6 +589,21 @@ int d2h(gd_handle* h, T* dst, const DevBuf& b, size_t count) {
 
 int sync(gd_handle* h) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
+    return GD_OK;
+}
+
+// h->h_pin holds at least `bytes` (page-locked: the small read-backs are true async copies).
+int pinned_scratch(gd_handle* h, size_t bytes) {
+    if (h->h_pin_bytes >= bytes) return GD_OK;
+    if (h->h_pin) {
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+        HIP_TRY(h, hipHostFree(h->h_pin));
+        h->h_pin = nullptr;
+        h->h_pin_bytes = 0;
+    }
+    const size_t b = std::max<size_t>(bytes, 64 * 1024);
+    HIP_TRY(h, hipHostMalloc(&h->h_pin, b));
+    h->h_pin_bytes = b;
     return GD_OK;
 }
 
@@ -802,6 +832,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_HOST_CHUNK")) h->host_chunk = (uint32_t)std::strtoul(v, nullptr, 10);
     if (const char* v = std::getenv("GD_XCD_TILES")) h->xcd_tiles = std::atoi(v) ? 1u : 0u;
     if (const char* v = std::getenv("GD_HIST_TPB")) h->hist_tpb = (uint32_t)std::atoi(v);
+    if (const char* v = std::getenv("GD_FAN_ILP")) h->fan_ilp = std::atoi(v);
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));
@@ -853,6 +884,7 @@ void gd_destroy(gd_handle* h) {
     for (DevBuf& b : h->churn) free_buf(b);
     for (DevBuf& b : h->fan) free_buf(b);
     for (DevBuf& b : h->cbuf) free_buf(b);
+    if (h->h_pin) (void)hipHostFree(h->h_pin);
     free_buf(h->cache_local);
     free_buf(h->shard_dest);
     free_buf(h->shard_hist);
@@ -1873,6 +1905,36 @@ int fan_count(gd_handle* h, const uint32_t* row_off, uint32_t n_nodes, const uin
     *total = 0;
     if (nf == 0) return GD_OK;
     GD_TRY(ensure(h, h->fan[0], (size_t)nf * 4));
+    // frontiers up to 16M publishers: degrees with the scan's tile sums, the down-sweep, and the
+    // partials back to the host (2 launches, one small pinned copy)
+    const uint32_t nb4 = blocks_for(nf, SCAN_TILE), nb16 = blocks_for(nf, 4 * SCAN_TILE);
+    if (nb4 <= 2048 || nb16 <= 4096) {
+        const bool wide = nb4 > 2048;
+        const uint32_t nb = wide ? nb16 : nb4;
+        GD_TRY(ensure(h, h->fan[1], (size_t)nb * 4));
+        GD_TRY(pinned_scratch(h, (size_t)nb * 4));
+        uint32_t* ends = (uint32_t*)h->fan[0].p;
+        uint32_t* part = (uint32_t*)h->fan[1].p;
+        if (wide) {
+            GD_TRY(launch(h, "k_fan_degree", dim3(nb), dim3(BLOCK), 0, k_fan_degree_tiles<16>, row_off, n_nodes, frontier,
+                          nf, ends, part));
+            GD_TRY(launch(h, "k_scan_down", dim3(nb), dim3(BLOCK), 0, k_scan_down<OpAdd, 16>, (const uint32_t*)ends, ends,
+                          nf, false, true, (const uint32_t*)part, nb));
+        } else {
+            GD_TRY(launch(h, "k_fan_degree", dim3(nb), dim3(BLOCK), 0, k_fan_degree_tiles<4>, row_off, n_nodes, frontier,
+                          nf, ends, part));
+            GD_TRY(launch(h, "k_scan_down", dim3(nb), dim3(BLOCK), 0, k_scan_down<OpAdd, 4>, (const uint32_t*)ends, ends,
+                          nf, false, true, (const uint32_t*)part, nb));
+        }
+        HIP_TRY(h, hipMemcpyAsync(h->h_pin, part, (size_t)nb * 4, hipMemcpyDeviceToHost, h->stream));
+        GD_TRY(sync(h));
+        uint64_t t = 0;
+        for (uint32_t b = 0; b < nb; ++b) t += ((const uint32_t*)h->h_pin)[b];
+        if (t > 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "fan-out of %llu messages exceeds 2^32 - 1",
+                                              (unsigned long long)t);
+        *total = t;
+        return GD_OK;
+    }
     GD_TRY(ensure(h, h->fan[1], 8));
     unsigned long long* dtot = (unsigned long long*)h->fan[1].p;
     HIP_TRY(h, hipMemsetAsync(dtot, 0, 8, h->stream));
@@ -1899,9 +1961,19 @@ template <int MODE>
 int fan_route_launch(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier, uint32_t nf,
                      uint32_t total, uint64_t tcd, uint32_t* target, uint32_t* sender, uint32_t* silo, uint32_t* act,
                      uint8_t* status) {
-    return launch(h, "k_fan_route", dim3(blocks_for(total, FAN_TILE)), dim3(BLOCK), ring_lds(h), k_fan_route<MODE>,
-                  row_off, dst, frontier, nf, (const uint32_t*)h->fan[0].p, total, tcd, ring_args(h), table_args(h),
-                  target, sender, silo, act, status);
+    const dim3 g(blocks_for(total, FAN_TILE)), b(BLOCK);
+    const uint32_t* ends = (const uint32_t*)h->fan[0].p;
+    switch (h->fan_ilp) {
+        case 1:
+            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 1>, row_off, dst, frontier, nf, ends,
+                          total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status);
+        case 4:
+            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 4>, row_off, dst, frontier, nf, ends,
+                          total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status);
+        default:
+            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2>, row_off, dst, frontier, nf, ends,
+                          total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status);
+    }
 }
 
 int fan_route(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier, uint32_t nf,
@@ -1941,24 +2013,25 @@ int route_nodes(gd_handle* h, const uint32_t* nodes, uint32_t n, uint64_t tcd, u
     }
 }
 
-// flag / scan / emit over n_act; returns the new frontier size.
+// count + compact over n_act (gd_fanout.h); returns the new frontier size.
 int frontier_next(gd_handle* h, const uint32_t* offsets, uint32_t n_act, uint8_t* visited, uint32_t* out,
                   uint32_t* out_n) {
     *out_n = 0;
     if (n_act == 0) return GD_OK;
-    GD_TRY(ensure(h, h->fan[2], (size_t)n_act * 4));
-    GD_TRY(ensure(h, h->fan[3], (size_t)n_act * 4));
-    uint32_t* flag = (uint32_t*)h->fan[2].p;
-    uint32_t* pos = (uint32_t*)h->fan[3].p;
-    const dim3 g(blocks_for(n_act, BLOCK)), b(BLOCK);
-    GD_TRY(launch(h, "k_frontier_flag", g, b, 0, k_frontier_flag, offsets, n_act, visited, flag));
-    GD_TRY(scan_device<OpAdd>(h, flag, n_act, false, true, "frontier", pos));
-    uint32_t cnt = 0;
-    HIP_TRY(h, hipMemcpyAsync(&cnt, pos + n_act - 1, 4, hipMemcpyDeviceToHost, h->stream));
-    GD_TRY(launch(h, "k_frontier_emit", g, b, 0, k_frontier_emit, (const uint32_t*)flag, (const uint32_t*)pos, n_act,
-                  out));
+    const uint32_t nb = blocks_for(n_act, FR_TILE);
+    GD_TRY(ensure(h, h->fan[2], (size_t)nb * BLOCK * sizeof(uint16_t)));
+    GD_TRY(ensure(h, h->fan[3], ((size_t)nb + 1) * 4));
+    uint16_t* flags = (uint16_t*)h->fan[2].p;
+    uint32_t* counts = (uint32_t*)h->fan[3].p;
+    uint32_t* total = counts + nb;
+    GD_TRY(launch(h, "k_frontier_count", dim3(nb), dim3(BLOCK), 0, k_frontier_count, offsets, n_act, visited, flags,
+                  counts));
+    GD_TRY(launch(h, "k_frontier_compact", dim3(nb), dim3(BLOCK), 0, k_frontier_compact, (const uint16_t*)flags,
+                  (const uint32_t*)counts, nb, out, total));
+    GD_TRY(pinned_scratch(h, 4));
+    HIP_TRY(h, hipMemcpyAsync(h->h_pin, total, 4, hipMemcpyDeviceToHost, h->stream));
     GD_TRY(sync(h));
-    *out_n = cnt;
+    *out_n = *(const uint32_t*)h->h_pin;
     return GD_OK;
 }
 

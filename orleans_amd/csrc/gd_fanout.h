@@ -55,6 +55,33 @@ __global__ void __launch_bounds__(BLOCK) k_fan_degree(const uint32_t* __restrict
     }
 }
 
+// The same as the first half of a scan: block b covers the scan tile b of k_scan_down<OpAdd, IPT>
+// (entries b * IPT * BLOCK ..), writes the degrees (coalesced: entry b * IPT * BLOCK + k * BLOCK + t
+// for thread t) and the tile's sum to part[b], so the inclusive scan of ends is the down-sweep
+// alone; the host adds the partials up for the u64 total.
+template <int IPT>
+__global__ void __launch_bounds__(BLOCK) k_fan_degree_tiles(const uint32_t* __restrict__ row_off, uint32_t n_nodes,
+                                                            const uint32_t* __restrict__ frontier, uint32_t n_front,
+                                                            uint32_t* __restrict__ ends, uint32_t* __restrict__ part) {
+    __shared__ uint32_t s_wsum[BLOCK / WAVE];
+    const uint32_t i0 = blockIdx.x * (BLOCK * IPT) + threadIdx.x;
+    uint32_t u[IPT], v = 0;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        const uint32_t i = i0 + k * BLOCK;
+        u[k] = i < n_front ? frontier[i] : n_nodes;
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+        const uint32_t i = i0 + k * BLOCK;
+        const uint32_t d = u[k] < n_nodes ? row_off[u[k] + 1] - row_off[u[k]] : 0u;
+        if (i < n_front) ends[i] = d;
+        v += d;
+    }
+    v = block_reduce<OpAdd>(v, s_wsum);
+    if (threadIdx.x == 0) part[blockIdx.x] = v;
+}
+
 // first i in [lo, hi) with a[i] > p  (hi if none)
 __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t p) {
     while (lo < hi) {
@@ -180,8 +207,10 @@ __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restric
     out_status[i] = st;
 }
 
-// Fused expansion + route.  out_target may be null.
-template <int MODE>
+// Fused expansion + route.  out_target may be null.  ILP items of a thread at a time: their
+// follower-list reads, then their first directory probes, are in flight together (one dependent
+// chain per item otherwise).
+template <int MODE, int ILP>
 __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict__ row_off,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint32_t* __restrict__ frontier, uint32_t n_front,
@@ -191,6 +220,7 @@ __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ out_sender,
                                                      uint32_t* __restrict__ out_silo, uint32_t* __restrict__ out_act,
                                                      uint8_t* __restrict__ out_status) {
+    static_assert(FAN_IT % ILP == 0, "whole rounds");
     __shared__ FanStage s;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     uint32_t* s_pts = s_ring;
@@ -200,39 +230,132 @@ __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict_
     const uint32_t p0 = blockIdx.x * FAN_TILE;
     const uint32_t p1 = min(p0 + FAN_TILE, total);
     fan_stage(s, row_off, frontier, n_front, ends, p0, p1);
-    for (int it = 0; it < FAN_IT; ++it) {
-        const uint32_t p = p0 + it * BLOCK + threadIdx.x;
-        if (p >= p1) break;
-        uint32_t j, sender, silo, act;
-        fan_item(s, row_off, frontier, n_front, ends, p, j, sender);
-        const uint32_t target = dst[j];
-        const uint8_t st = route_node<MODE>(target, tcd, s_pts, s_own, ring, tab, max_probe, silo, act);
-        if (out_target) out_target[p] = target;
-        out_sender[p] = sender;
-        out_silo[p] = silo;
-        out_act[p] = act;
-        out_status[p] = st;
+    for (int it0 = 0; it0 < FAN_IT; it0 += ILP) {
+        if (p0 + it0 * BLOCK >= p1) break;                 // block-uniform
+        uint32_t j[ILP], sender[ILP], target[ILP], h[ILP];
+        bool live[ILP];
+#pragma unroll
+        for (int q = 0; q < ILP; ++q) {
+            const uint32_t p = p0 + (it0 + q) * BLOCK + threadIdx.x;
+            live[q] = p < p1;
+            j[q] = 0;
+            sender[q] = 0;
+            if (live[q]) fan_item(s, row_off, frontier, n_front, ends, p, j[q], sender[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < ILP; ++q) target[q] = live[q] ? dst[j[q]] : 0u;
+        unsigned long long sl[ILP];
+        uint4 qa[ILP], qb[ILP];
+#pragma unroll
+        for (int q = 0; q < ILP; ++q) {
+            h[q] = uniform_hash(0, target[q], tcd);
+            sl[q] = fmix32(h[q]) & tab.mask;
+            if (live[q]) {
+                const uint4* a = reinterpret_cast<const uint4*>(tab.slots + sl[q]);
+                qa[q] = a[0];
+                qb[q] = a[1];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < ILP; ++q) {
+            if (!live[q]) continue;
+            const uint32_t p = p0 + (it0 + q) * BLOCK + threadIdx.x;
+            uint32_t silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[q])], act = NONE32;
+            uint8_t st = GD_ROUTE_MISS;
+            uint4 a = qa[q], b = qb[q];
+            for (uint32_t k = 0;;) {                        // the probe of route_node, from the first slot read
+                const uint32_t stt = slot_state(b.w);
+                if (stt == SLOT_EMPTY) break;
+                const uint64_t k0 = (uint64_t)a.x | ((uint64_t)a.y << 32);
+                const uint64_t k1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
+                const uint64_t k2 = (uint64_t)b.x | ((uint64_t)b.y << 32);
+                if (stt == SLOT_LIVE && k0 == 0 && k1 == target[q] && k2 == tcd) {
+                    if (b.z == GD_ACT_MULTI) {
+                        st = GD_ROUTE_MULTI_ACT;                 // RandomPlacementDirector.cs:33-53, in C#
+                    } else if (tab_silo_valid(tab, slot_silo(b.w))) {
+                        act = b.z;
+                        silo = slot_silo(b.w);                   // ActivationAddress.Silo (Message.cs:629-639)
+                        st = GD_ROUTE_OK;
+                    }                                            // else IsValidSilo (:431) -> MISS
+                    break;
+                }
+                if (++k > max_probe) break;                      // Dispatcher.cs:742 slow path
+                sl[q] = (sl[q] + 1) & tab.mask;
+                const uint4* n = reinterpret_cast<const uint4*>(tab.slots + sl[q]);
+                a = n[0];
+                b = n[1];
+            }
+            if (out_target) out_target[p] = target[q];
+            out_sender[p] = sender[q];
+            out_silo[p] = silo;
+            out_act[p] = act;
+            out_status[p] = st;
+        }
     }
 }
 
-// Next frontier (BFS over the cascade): activation a received >= 1 message this hop
-// (offsets[a+1] > offsets[a]) and has not published yet.  flag[a] in {0,1}; visited updated.
-__global__ void __launch_bounds__(BLOCK) k_frontier_flag(const uint32_t* __restrict__ offsets, uint32_t n_act,
-                                                         uint8_t* __restrict__ visited, uint32_t* __restrict__ flag) {
-    const uint32_t a = blockIdx.x * BLOCK + threadIdx.x;
-    if (a >= n_act) return;
-    const bool got = offsets[a + 1] > offsets[a];
-    const bool fresh = got && visited[a] == 0;
-    if (fresh) visited[a] = 1;
-    flag[a] = fresh ? 1u : 0u;
+// The next frontier in two launches (instead of flag + a 4-launch scan + emit over n_act).
+// k_frontier_count: thread t of block b looks at activations a0 .. a0 + 15 (a0 = b * FR_TILE +
+// 16 t): fresh = got a message this hop (offsets[a + 1] > offsets[a]) and not visited yet; marks
+// them visited, keeps the 16 flags as one u16 and the block's count.  k_frontier_compact: every
+// block folds the counts of the blocks before it, ranks its flags and writes its fresh activations
+// in activation order (the order the oracle's next_frontier gives); the last thread of the last
+// block writes the total.
+constexpr uint32_t FR_ITEMS = 16;
+constexpr uint32_t FR_TILE = BLOCK * FR_ITEMS;
+
+__global__ void __launch_bounds__(BLOCK) k_frontier_count(const uint32_t* __restrict__ offsets, uint32_t n_act,
+                                                          uint8_t* __restrict__ visited, uint16_t* __restrict__ flags,
+                                                          uint32_t* __restrict__ counts) {
+    __shared__ uint32_t s_wsum[BLOCK / WAVE];
+    const uint32_t a0 = blockIdx.x * FR_TILE + threadIdx.x * FR_ITEMS;
+    uint32_t m = 0;
+    if (a0 + FR_ITEMS <= n_act && (reinterpret_cast<uintptr_t>(offsets) & 15) == 0 &&
+        (reinterpret_cast<uintptr_t>(visited) & 15) == 0) {
+        uint32_t o[FR_ITEMS + 1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 u = *reinterpret_cast<const uint4*>(offsets + a0 + 4 * q);
+            o[4 * q] = u.x; o[4 * q + 1] = u.y; o[4 * q + 2] = u.z; o[4 * q + 3] = u.w;
+        }
+        o[FR_ITEMS] = offsets[a0 + FR_ITEMS];            // offsets has n_act + 2 entries
+        uint4 vis = *reinterpret_cast<const uint4*>(visited + a0);
+        uint8_t* vb = reinterpret_cast<uint8_t*>(&vis);
+#pragma unroll
+        for (int k = 0; k < (int)FR_ITEMS; ++k)
+            if (o[k + 1] > o[k] && vb[k] == 0) {
+                vb[k] = 1;
+                m |= 1u << k;
+            }
+        if (m) *reinterpret_cast<uint4*>(visited + a0) = vis;
+    } else {
+        for (uint32_t k = 0; k < FR_ITEMS; ++k) {
+            const uint32_t a = a0 + k;
+            if (a < n_act && offsets[a + 1] > offsets[a] && visited[a] == 0) {
+                visited[a] = 1;
+                m |= 1u << k;
+            }
+        }
+    }
+    flags[blockIdx.x * BLOCK + threadIdx.x] = (uint16_t)m;
+    const uint32_t c = block_reduce<OpAdd>((uint32_t)__popc(m), s_wsum);
+    if (threadIdx.x == 0) counts[blockIdx.x] = c;
 }
 
-// Compaction: pos = inclusive scan of flag, so a flagged activation goes to pos[a] - 1.
-__global__ void __launch_bounds__(BLOCK) k_frontier_emit(const uint32_t* __restrict__ flag,
-                                                         const uint32_t* __restrict__ pos, uint32_t n_act,
-                                                         uint32_t* __restrict__ out) {
-    const uint32_t a = blockIdx.x * BLOCK + threadIdx.x;
-    if (a < n_act && flag[a]) out[pos[a] - 1] = a;
+__global__ void __launch_bounds__(BLOCK) k_frontier_compact(const uint16_t* __restrict__ flags,
+                                                            const uint32_t* __restrict__ counts, uint32_t nb,
+                                                            uint32_t* __restrict__ out, uint32_t* __restrict__ total) {
+    __shared__ uint32_t s_wsum[BLOCK / WAVE];
+    uint32_t acc = 0;
+    for (uint32_t j = threadIdx.x; j < blockIdx.x; j += BLOCK) acc += counts[j];
+    const uint32_t prefix = block_reduce<OpAdd>(acc, s_wsum);
+    const uint32_t m = flags[blockIdx.x * BLOCK + threadIdx.x];
+    const uint32_t c = (uint32_t)__popc(m);
+    uint32_t pos = prefix + block_excl_scan<OpAdd>(c, s_wsum);
+    const uint32_t a0 = blockIdx.x * FR_TILE + threadIdx.x * FR_ITEMS;
+    for (uint32_t k = 0; k < FR_ITEMS; ++k)
+        if ((m >> k) & 1u) out[pos++] = a0 + k;
+    if (blockIdx.x + 1 == nb && threadIdx.x == BLOCK - 1) *total = pos;
 }
 
 }  // namespace gd

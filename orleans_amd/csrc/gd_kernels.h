@@ -1067,43 +1067,52 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wsum
 }
 
 // Tiles are physical: block b scans physical tile T = b (forward) or nb - 1 - b (reverse), and
-// thread t the 4 entries at T * SCAN_TILE + 4c with c = t (forward) or BLOCK - 1 - t (reverse),
-// taken high to low in a reverse scan.  Every thread's entries are then one aligned 16-B load /
-// store; a reverse scan meets the entries past n (identity) first, which changes nothing.
-static_assert(SCAN_ITEMS == 4, "scan tiles are read as one uint4 per thread");
+// thread t the IPT entries at T * IPT * BLOCK + IPT * c with c = t (forward) or BLOCK - 1 - t
+// (reverse), taken high to low in a reverse scan.  Every thread's entries are then IPT / 4 aligned
+// 16-B loads / stores; a reverse scan meets the entries past n (identity) first, which changes
+// nothing.  IPT = 4 (1,024-entry tiles: enough blocks to fill the chip) or 16 (4,096-entry tiles,
+// for arrays whose 1,024-entry tiles would be too many aggregates to fold in the down-sweep).
+static_assert(SCAN_ITEMS == 4, "scan tiles are read as uint4 per thread");
 
+template <int IPT>
 __device__ __forceinline__ uint32_t scan_chunk_base(uint32_t n, bool rev) {
-    const uint32_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    constexpr uint32_t TILE = BLOCK * IPT;
+    const uint32_t nb = (n + TILE - 1) / TILE;
     const uint32_t tile = rev ? nb - 1 - blockIdx.x : blockIdx.x;
     const uint32_t c = rev ? BLOCK - 1 - threadIdx.x : threadIdx.x;
-    return tile * SCAN_TILE + 4 * c;
+    return tile * TILE + IPT * c;
 }
 
-// The thread's 4 entries in scan order (identity past n).
-template <class Op>
-__device__ __forceinline__ void scan_load4(const uint32_t* in, uint32_t n, bool rev, uint32_t p0, uint32_t (&v)[4]) {
-    uint32_t x[4];
-    if (p0 + 3 < n && (reinterpret_cast<uintptr_t>(in) & 15) == 0) {
-        const uint4 q = *reinterpret_cast<const uint4*>(in + p0);
-        x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w;
+// The thread's IPT entries in scan order (identity past n).
+template <class Op, int IPT>
+__device__ __forceinline__ void scan_load(const uint32_t* in, uint32_t n, bool rev, uint32_t p0, uint32_t (&v)[IPT]) {
+    uint32_t x[IPT];
+    if (p0 + IPT - 1 < n && (reinterpret_cast<uintptr_t>(in) & 15) == 0) {
+#pragma unroll
+        for (int q = 0; q < IPT / 4; ++q) {
+            const uint4 u = *reinterpret_cast<const uint4*>(in + p0 + 4 * q);
+            x[4 * q] = u.x; x[4 * q + 1] = u.y; x[4 * q + 2] = u.z; x[4 * q + 3] = u.w;
+        }
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {                   // clamped loads: no per-item branch
+        for (int k = 0; k < IPT; ++k) {                 // clamped loads: no per-item branch
             const uint32_t y = in[min(p0 + k, n - 1)];
             x[k] = p0 + k < n ? y : Op::identity;
         }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = rev ? x[3 - k] : x[k];
+    for (int k = 0; k < IPT; ++k) v[k] = rev ? x[IPT - 1 - k] : x[k];
 }
 
-template <class Op>
+template <class Op, int IPT = SCAN_ITEMS>
 __global__ void __launch_bounds__(BLOCK) k_scan_reduce(const uint32_t* __restrict__ in, uint32_t n, bool rev,
                                                        uint32_t* __restrict__ partials) {
     __shared__ uint32_t s_wsum[BLOCK / WAVE];
-    uint32_t v[4];
-    scan_load4<Op>(in, n, rev, scan_chunk_base(n, rev), v);
-    uint32_t acc = Op::apply(Op::apply(v[0], v[1]), Op::apply(v[2], v[3]));
+    uint32_t v[IPT];
+    scan_load<Op, IPT>(in, n, rev, scan_chunk_base<IPT>(n, rev), v);
+    uint32_t acc = Op::identity;
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) acc = Op::apply(acc, v[k]);
     acc = block_reduce<Op>(acc, s_wsum);
     if (threadIdx.x == 0) partials[blockIdx.x] = acc;
 }
@@ -1127,7 +1136,7 @@ __global__ void __launch_bounds__(BLOCK) k_scan_partials(uint32_t* partials, uin
     }
 }
 
-template <class Op>
+template <class Op, int IPT = SCAN_ITEMS>
 __global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_t* out, uint32_t n, bool rev,
                                                      bool inclusive, const uint32_t* __restrict__ partials,
                                                      uint32_t n_partials_raw) {
@@ -1145,26 +1154,30 @@ __global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_
     }
     __syncthreads();
     const uint32_t prefix = s_prefix;
-    const uint32_t p0 = scan_chunk_base(n, rev);
-    uint32_t v[4];
-    scan_load4<Op>(in, n, rev, p0, v);
-    const uint32_t acc = Op::apply(Op::apply(v[0], v[1]), Op::apply(v[2], v[3]));
-    uint32_t run = Op::apply(prefix, block_excl_scan<Op>(acc, s_wsum));
-    uint32_t r[4];
+    const uint32_t p0 = scan_chunk_base<IPT>(n, rev);
+    uint32_t v[IPT];
+    scan_load<Op, IPT>(in, n, rev, p0, v);
+    uint32_t acc = Op::identity;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < IPT; ++k) acc = Op::apply(acc, v[k]);
+    uint32_t run = Op::apply(prefix, block_excl_scan<Op>(acc, s_wsum));
+    uint32_t r[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
         const uint32_t next = Op::apply(run, v[k]);
         r[k] = inclusive ? next : run;
         run = next;
     }
-    uint32_t x[4];                                      // back to physical order
+    uint32_t x[IPT];                                    // back to physical order
 #pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = rev ? r[3 - k] : r[k];
-    if (p0 + 3 < n && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
-        *reinterpret_cast<uint4*>(out + p0) = make_uint4(x[0], x[1], x[2], x[3]);
+    for (int k = 0; k < IPT; ++k) x[k] = rev ? r[IPT - 1 - k] : r[k];
+    if (p0 + IPT - 1 < n && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+#pragma unroll
+        for (int q = 0; q < IPT / 4; ++q)
+            *reinterpret_cast<uint4*>(out + p0 + 4 * q) = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < IPT; ++k)
             if (p0 + k < n) out[p0 + k] = x[k];
     }
 }
