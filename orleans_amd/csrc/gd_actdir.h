@@ -142,20 +142,20 @@ __global__ void __launch_bounds__(BLOCK) k_receive(const gd_key* __restrict__ ta
     out_status[i] = st;
 }
 
-// CheckOverloaded's hard limit (ActivationData.cs:616-649) after the first bucketing: the message
-// at position j of its activation's arrival order is rejected iff it is not a response and
+// CheckOverloaded's hard limit (ActivationData.cs:616-649) after the first bucketing, in message
+// order: rank[i] = message i's output position, so j = rank[i] - offsets[c] is its place in its
+// activation's arrival order; it is rejected iff it is not a response and
 // j >= limit + 1 - request_count[c] (every earlier message was enqueued and counted by
 // IncrementEnqueuedOnDispatcherCount until the first rejection; after it the count stays over the
 // limit).  Rejected messages get ctx NONE32; the caller rebuckets.
-__global__ void __launch_bounds__(BLOCK) k_overload(const uint32_t* __restrict__ perm,
-                                                    const uint32_t* __restrict__ offsets, uint32_t n_ctx,
+__global__ void __launch_bounds__(BLOCK) k_overload(const uint32_t* __restrict__ rank,
+                                                    const uint32_t* __restrict__ offsets, uint32_t n,
                                                     const uint8_t* __restrict__ direction,
                                                     const uint32_t* __restrict__ request_count, int32_t hard_limit,
                                                     int32_t hard_limit_sw, uint32_t* __restrict__ ctx,
                                                     uint8_t* __restrict__ status) {
-    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
-    if (p >= offsets[n_ctx]) return;                   // context buckets only (null context, rejects follow)
-    const uint32_t i = perm[p];
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
     const uint8_t st = status[i];
     if ((st & 0x7F) != RECV_ACTIVATION) return;
     const bool sw = st & RECV_STATELESS_BIT;
@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(BLOCK) k_overload(const uint32_t* __restrict__
     const int64_t limit = sw ? hard_limit_sw : hard_limit;
     if (d == DIR_RESPONSE || limit <= 0) return;       // responses are not checked (:140); no limit set (:627)
     const uint32_t c = ctx[i];
-    const int64_t j = (int64_t)(p - offsets[c]);
+    const int64_t j = (int64_t)(rank[i] - offsets[c]);
     if (j >= limit + 1 - (int64_t)request_count[c]) {
         status[i] = RECV_REJECT_OVERLOADED;
         ctx[i] = NONE32;

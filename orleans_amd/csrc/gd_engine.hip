@@ -480,7 +480,7 @@ int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inc
 template <int BITS, int NT, int IT>
 int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
                  uint32_t* kout, uint32_t* vout, bool first,
-                 uint32_t* offsets) {
+                 uint32_t* offsets, uint32_t* rank_out) {
     constexpr uint32_t TILE = NT * IT;
     const uint32_t tiles = blocks_for(n, TILE);
     const uint32_t R = 1u << BITS;
@@ -505,43 +505,47 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
     GD_TRY(scan_device<OpAdd>(h, hist, R * tiles, false, false, "hist"));
     if (first)
         return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, true, NT, IT>, kin, vin, n,
-                      clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets, h->xcd_tiles);
+                      clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets, h->xcd_tiles,
+                      rank_out);
     return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, false, NT, IT>, kin, vin, n,
-                  clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets, h->xcd_tiles);
+                  clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets, h->xcd_tiles,
+                      rank_out);
 }
 
 template <int BITS>
 int radix_pass(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
                uint32_t* kout, uint32_t* vout, bool first,
-                 uint32_t* offsets) {
+                 uint32_t* offsets, uint32_t* rank_out) {
     switch (h->radix_cfg) {
-        case 1: return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+        case 1: return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
         case 2:
-            if constexpr (BITS <= 8) return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
-            else return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
-        case 3: return radix_pass_t<BITS, 512, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
-        default: return radix_pass_t<BITS, 256, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+            if constexpr (BITS <= 8) return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+            else return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+        case 3: return radix_pass_t<BITS, 512, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+        default: return radix_pass_t<BITS, 256, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
     }
 }
 
 int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp,
                    uint32_t shift, uint32_t* kout, uint32_t* vout, bool first,
-                 uint32_t* offsets) {
+                 uint32_t* offsets, uint32_t* rank_out) {
     switch (bits) {
-        case 4: return radix_pass<4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
-        case 5: return radix_pass<5>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
-        case 6: return radix_pass<6>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
-        case 7: return radix_pass<7>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
-        case 8: return radix_pass<8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
-        case 9: return radix_pass<9>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
-        case 10: return radix_pass<10>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
-        default: return radix_pass<11>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets);
+        case 4: return radix_pass<4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+        case 5: return radix_pass<5>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+        case 6: return radix_pass<6>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+        case 7: return radix_pass<7>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+        case 8: return radix_pass<8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+        case 9: return radix_pass<9>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+        case 10: return radix_pass<10>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+        default: return radix_pass<11>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
     }
 }
 
 // Stable partition of indices 0..n-1 by min(acts[i], n_act):
-// LSD passes of <= 8 bits, then bucket offsets from the sorted keys.
-int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets) {
+// LSD passes of <= 8 bits, then bucket offsets from the sorted keys.  rank_out (optional): the
+// inverse permutation, rank_out[perm[p]] = p.
+int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
+                  uint32_t* rank_out = nullptr) {
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
     const uint32_t n_off = n_act + 2;
     GD_TRY(launch(h, "k_fill", dim3(blocks_for(n_off, BLOCK)), dim3(BLOCK), 0, k_fill_u32, offsets, n_off, n));
@@ -564,7 +568,7 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
         // the last pass writes the bucket starts itself (no sorted keys, no k_bucket_starts)
         const bool last = p + 1 == passes && h->fused_starts;
         GD_TRY(radix_dispatch(h, (int)bits, kin, vin, n, n_act, p * bits, kout, vout, p == 0,
-                              last ? offsets : nullptr));
+                              last ? offsets : nullptr, p + 1 == passes ? rank_out : nullptr));
         kin = kout;
         vin = vout;
     }
@@ -3969,9 +3973,14 @@ int receive_device(gd_handle* h, const gd_key* tg, const gd_key* ta, const uint8
     }
     if (!perm) return GD_OK;
     // buckets 0..n_ctx-1 contexts, n_ctx the null context, n_ctx + 1 not enqueued (ctx NONE32 clamps there)
-    GD_TRY(bucket_device(h, ctx, n, n_ctx + 1, perm, offsets));
+    uint32_t* rank = nullptr;
     if (limits && n) {
-        GD_TRY(launch(h, "k_overload", g, b, 0, k_overload, (const uint32_t*)perm, (const uint32_t*)offsets, n_ctx, dir,
+        GD_TRY(ensure(h, h->fr_recv[2], (size_t)n * 4));
+        rank = (uint32_t*)h->fr_recv[2].p;
+    }
+    GD_TRY(bucket_device(h, ctx, n, n_ctx + 1, perm, offsets, rank));
+    if (limits && n) {
+        GD_TRY(launch(h, "k_overload", g, b, 0, k_overload, (const uint32_t*)rank, (const uint32_t*)offsets, n, dir,
                       lim->request_count, lim->hard_limit, lim->hard_limit_stateless_worker, ctx, st));
         GD_TRY(bucket_device(h, ctx, n, n_ctx + 1, perm, offsets));
     }

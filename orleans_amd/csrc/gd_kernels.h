@@ -295,12 +295,11 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
             status[j] = GD_ROUTE_KEYEXT;
         } else {
             h[j] = uniform_hash(n0[j], n1[j], tcd[j]);
-            silo[j] = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[j])];
             status[j] = GD_ROUTE_MISS;
             need[j] = true;
         }
     }
-    // first probe of every message, all in flight together
+    // first probe of every message, all in flight together; the ring search (LDS) runs under them
     unsigned long long s[M];
     uint4 qa[M], qb[M];
 #pragma unroll
@@ -312,6 +311,9 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
             qb[j] = q[1];
         }
     }
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+        if (need[j]) silo[j] = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[j])];
 #pragma unroll
     for (int j = 0; j < M; ++j) {
         if (!need[j]) continue;
@@ -862,7 +864,8 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ gscan,
                                                       uint32_t* __restrict__ keys_out,
                                                       uint32_t* __restrict__ vals_out, uint32_t rank_atomic,
-                                                      uint32_t* __restrict__ starts, uint32_t xcd) {
+                                                      uint32_t* __restrict__ starts, uint32_t xcd,
+                                                      uint32_t* __restrict__ rank_out) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = NT / WAVE;
     constexpr uint32_t TILE = NT * IT;
@@ -1002,6 +1005,7 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
                     keys_out[g] = kv.x;
                 }
                 vals_out[g] = kv.y;
+                if (rank_out) rank_out[kv.y] = g;     // the inverse permutation (last pass, on request)
             }
         }
     }
