@@ -142,30 +142,34 @@ def setup_workload(args, workload, world, rank, local, dev, tcd, msgs, grains):
         "rehearsal: gloo all_to_all on host-staged copies (every rank on cuda:0)" if args.rehearse_one_gpu
         else "torch.distributed all_to_all_single (RCCL)")
     if not args.rehearse_one_gpu and ((world > 1 and args.exchange != "torch") or args.exchange == "library"):
-        # the in-library exchange, checked bit for bit against the torch exchange on the first batch
+        # the in-library exchange, checked bit for bit against the torch exchange on the first batch;
+        # every rank reaches the agreement all-reduce, whatever happened on it (no rank left waiting)
+        ok, err = False, None
         try:
             lib_router = LibraryRouter(engine)
             with torch.cuda.stream(stream):
                 ok = same_result(lib_router.route_bucket(keys, n_act), router.route_bucket(keys, n_act))
                 torch.cuda.synchronize()
-            agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-            dist.all_reduce(agree, op=dist.ReduceOp.MIN)
-            if int(agree.item()) == 1:
-                # keys are resident and complete: batch i+1's exchange overlaps batch i's probe + bucket
-                # timed batches: messages are known by (sender, index); the probe reads the compact
-                # 8-B headers as they arrive and no 24-B key copy is rebuilt (GD_MULTI_NO_KEYS)
-                router = lib_router
-                lib_router.keys_ready = True
-                lib_router.no_keys = True
-                exchange = ("libgraindispatch gd_route_multi_device (grouped RCCL send/recv, compact headers, "
-                            "GD_MULTI_NO_KEYS); first batch bit-identical to the torch.distributed exchange")
-            else:
-                exchange = "torch.distributed all_to_all_single (RCCL); library exchange disagreed on batch 1"
-                assert args.exchange != "library", "library exchange disagrees with the torch exchange"
         except Exception as ex:   # noqa: BLE001 -- reported in the JSON line, torch exchange used instead
             if args.exchange == "library":
                 raise
-            exchange = f"torch.distributed all_to_all_single (RCCL); library exchange failed: {ex!r}"[:300]
+            err = f"{ex!r}"[:200]
+        agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(agree, op=dist.ReduceOp.MIN)
+        if int(agree.item()) == 1:
+            # keys are resident and complete: batch i+1's exchange overlaps batch i's probe + bucket
+            # timed batches: messages are known by (sender, index); the probe reads the compact
+            # 8-B headers as they arrive and no 24-B key copy is rebuilt (GD_MULTI_NO_KEYS)
+            router = lib_router
+            lib_router.keys_ready = True
+            lib_router.no_keys = True
+            exchange = ("libgraindispatch gd_route_multi_device (grouped RCCL send/recv, compact headers, "
+                        "GD_MULTI_NO_KEYS); first batch bit-identical to the torch.distributed exchange")
+        elif err is not None:
+            exchange = f"torch.distributed all_to_all_single (RCCL); library exchange failed here: {err}"
+        else:
+            exchange = "torch.distributed all_to_all_single (RCCL); library exchange disagreed on batch 1 (some rank)"
+            assert args.exchange != "library", "library exchange disagrees with the torch exchange"
     return {"e": e, "engine": engine, "router": router, "stream": stream, "keys": keys, "N": N, "n_act": n_act,
             "G_total": G_total, "cap": cap, "pts": pts, "own": own, "exchange": exchange,
             "owner_share_max": round(owner_share, 4), "owner_share_by_set": by_set}
