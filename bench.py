@@ -221,7 +221,7 @@ def main():
     ap.add_argument("--no-secondary", action="store_true", help="N>1: skip the cfg3 strong-scaling measurement")
     ap.add_argument("--msgs3", type=int, default=None, help="secondary cfg3: messages per GPU (default 2^26 / N)")
     ap.add_argument("--grains3", type=int, default=None, help="secondary cfg3: grains per GPU (default 1e8 / N)")
-    ap.add_argument("--latency-batches", type=int, default=4000,
+    ap.add_argument("--latency-batches", type=int, default=10000,
                     help="N=1 cfg2: 4,096-message micro-batches timed for the cfg5 latency line (0: skip)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo, host-staged all-to-all")

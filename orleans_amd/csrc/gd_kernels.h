@@ -893,8 +893,8 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
     for (int r = 0; r < IT; ++r) {
         const uint32_t idx = base + (w * IT + r) * WAVE + lane;
         const uint32_t li = min(idx, n - 1);
-        kk[r] = keys_in[li];
-        if constexpr (!FIRST) vv[r] = vals_in[li];
+        kk[r] = __builtin_nontemporal_load(keys_in + li);          // read once: stream past the caches
+        if constexpr (!FIRST) vv[r] = __builtin_nontemporal_load(vals_in + li);
     }
 #pragma unroll
     for (int r = 0; r < IT; ++r) {

@@ -292,13 +292,20 @@ def test_route_bucket_fused(gd):
 
 
 # ----------------------------------------------------------------------------- device API + full size
-def test_full_size_cfg2_properties(gd):
+BALANCED_GENS = [138558, 165678, 215136, 61804, 17808, 48728, 207265, 76820]   # bench.py SILO_SETS["balanced"]
+
+
+@pytest.mark.parametrize("silo_set", ["literal", "balanced"])
+def test_full_size_cfg2_properties(gd, silo_set):
     """BASELINE config 2 at full size (16M messages over 1M grains): route checked
     against the known directory (act == grain index, silo == ring owner), a
     100k sample against the oracle, and the bucketing by size-independent
-    properties (permutation, sorted, stable, offsets = counts)."""
+    properties (permutation, sorted, stable, offsets = counts).  Both silo sets bench.py
+    reports: SURVEY 8(d)'s literal generation-1 silos and the balanced generations the
+    benchmark line is timed on."""
     import torch
-    silos = o.bench_silos(8)
+    silos = o.bench_silos(8) if silo_set == "literal" else \
+        [o.Silo(f"10.0.0.{i + 1}", 11111, gen) for i, gen in enumerate(BALANCED_GENS)]
     spec = o.ring_spec(silos, "D")
     G, N = 1 << 20, 1 << 24
     e = _engine(gd, silos, "D", cap=2 * G)
