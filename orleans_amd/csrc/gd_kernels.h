@@ -250,7 +250,7 @@ __device__ __forceinline__ void st(T* p, T v) {
 // N1: the keys arrive as N1 alone (8 B each; N0 = 0, TypeCodeData = tcd_u for all), the form a
 // compact exchange header round delivers (k_key_desc, gd_shard.h).
 // The per-thread part: messages base + j * STRIDE, j < M; lds_act (optional) gets act too.
-template <int MODE, int M, int STRIDE, bool NT, bool N1>
+template <int MODE, int M, int STRIDE, bool NT, bool N1, bool NT_SIDE = false>
 __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, uint32_t n, uint32_t base,
                                              const RingArgs& ring, const uint32_t* s_pts, const uint32_t* s_own,
                                              const TableArgs& tab, uint32_t max_probe,
@@ -345,9 +345,9 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
     for (int j = 0; j < M; ++j) {
         const uint32_t i = base + j * STRIDE;
         if (i < n) {
-            st<NT>(out_silo + i, silo[j]);
-            st<NT>(out_act + i, act[j]);
-            st<NT>(out_status + i, status[j]);
+            st<NT || NT_SIDE>(out_silo + i, silo[j]);      // silo / status: not read again on the device
+            st<NT>(out_act + i, act[j]);                    // act: the bucketing's input, next
+            st<NT || NT_SIDE>(out_status + i, status[j]);
             if (lds_act) lds_act[(size_t)i * lds_stride] = act[j];
         }
     }
@@ -399,8 +399,9 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
     stage_ring(ring, s_pts, s_own);
-    route_m_core<MODE, M, BLOCK, NT, N1>(keys, n, blockIdx.x * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own, tab,
-                                         tab.ctr->max_probe, out_silo, out_act, out_status, tcd_u, nullptr, 0);
+    route_m_core<MODE, M, BLOCK, NT, N1, true>(keys, n, blockIdx.x * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own,
+                                               tab, tab.ctr->max_probe, out_silo, out_act, out_status, tcd_u, nullptr,
+                                               0);
 }
 
 // GetPrimaryTargetSilo(uint key) over raw ring keys.
