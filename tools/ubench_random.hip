@@ -34,6 +34,26 @@ __global__ void __launch_bounds__(256) k_probe(const uint4* __restrict__ table, 
     out[i] = a.x ^ a.y ^ b.z ^ b.w;
 }
 
+// XCD-regioned: workgroup b probes only region b % 8 of the table (one eighth, contiguous).  With
+// workgroups dispatched round-robin over the 8 XCDs, each XCD's L2 then serves one region.
+template <bool KEYS>
+__global__ void __launch_bounds__(256) k_probe_region(const uint4* __restrict__ table, unsigned long long region_mask,
+                                                      unsigned long long region_slots,
+                                                      const uint64_t* __restrict__ keys, uint32_t n,
+                                                      uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t h = mix(i * 2654435761u);
+    if constexpr (KEYS) {
+        const uint64_t* kp = keys + 3ull * i;
+        h ^= (uint32_t)(kp[0] ^ kp[1] ^ kp[2]);
+    }
+    const unsigned long long s = (unsigned long long)(blockIdx.x & 7u) * region_slots + (mix(h) & region_mask);
+    const uint4 a = table[2 * s];
+    const uint4 b = table[2 * s + 1];
+    out[i] = a.x ^ a.y ^ b.z ^ b.w;
+}
+
 __global__ void __launch_bounds__(256) k_copy(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n16) {
     for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) out[i] = in[i];
 }
@@ -72,6 +92,26 @@ int main() {
             ms /= reps;
             std::printf("%8zu  %4d  %9.4f  %15.1f  %15.1f  %6.1f\n", mb, withKeys, ms, n * 32.0 / ms / 1e6,
                         n * 64.0 / ms / 1e6, n / ms / 1e6);
+        }
+        for (int withKeys = 0; withKeys < 2; ++withKeys) {       // XCD-regioned probes
+            const unsigned long long rs = slots / 8;
+            auto launch = [&] {
+                if (withKeys)
+                    hipLaunchKernelGGL(k_probe_region<true>, dim3(n / 256), dim3(256), 0, 0, table, rs - 1, rs, keys, n, out);
+                else
+                    hipLaunchKernelGGL(k_probe_region<false>, dim3(n / 256), dim3(256), 0, 0, table, rs - 1, rs, keys, n, out);
+            };
+            for (int w = 0; w < 3; ++w) launch();
+            CK(hipEventRecord(e0));
+            const int reps = 20;
+            for (int r = 0; r < reps; ++r) launch();
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ms /= reps;
+            std::printf("%8zu  %4d  %9.4f  %15.1f  %15.1f  %6.1f  xcd-regioned\n", mb, withKeys, ms,
+                        n * 32.0 / ms / 1e6, n * 64.0 / ms / 1e6, n / ms / 1e6);
         }
         CK(hipFree(table));
     }
