@@ -340,6 +340,10 @@ def main():
     if world == 1 and args.workload == "cfg2" and args.latency_batches > 0:
         secondary["cfg5_latency_us"] = micro_batch_latency(e, tcd, G_total, n_act, args.latency_batches)
 
+    # ---- BASELINE cfg 1's shape on the GPU: 1M calls over 10k grains, one silo ---------
+    if world == 1 and args.workload == "cfg2" and args.latency_batches > 0:
+        secondary["cfg1_ping_shape"] = ping_shape(tcd, dev, args.mode)
+
     # ---- CPU baseline: the C restatement (oracle/cpu_ref.c), bounded sample ---------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "cfg2":
@@ -381,6 +385,43 @@ def main():
         print(json.dumps(line), flush=True)
     e.close()
     dist.destroy_process_group()
+
+
+def ping_shape(tcd: int, dev, mode: str, G: int = 10_000, N: int = 1 << 20, steps: int = 200) -> dict:
+    """BASELINE cfg 1's shape (PingBenchmark: 1M calls over 10k grains, one silo) through
+    gd_route_bucket_device, inputs resident in HBM; the CPU restatement's rate for the same shape
+    is cpu_baseline.cfg1_ping_shape."""
+    e1 = g.GrainDispatch(device=dev.index or 0, table_capacity=1 << 15, my_silo=0, kernel_timing=False)
+    e1.ring_set_silos(mode, SILO_SETS["literal"][:1])
+    reg = grain_keys(tcd, np.arange(G, dtype=np.int64))
+    e1.register(reg, np.arange(G, dtype=np.uint32), np.zeros(G, np.uint32))
+    ks = np.random.default_rng(0x5EED0101).integers(0, G, size=N, dtype=np.int64)
+    keys = torch.from_numpy(grain_keys(tcd, ks).view(np.int64)).to(dev)
+    silo = torch.empty(N, dtype=torch.int32, device=dev)
+    act = torch.empty(N, dtype=torch.int32, device=dev)
+    st = torch.empty(N, dtype=torch.uint8, device=dev)
+    perm = torch.empty(N, dtype=torch.int32, device=dev)
+    off = torch.empty(G + 2, dtype=torch.int32, device=dev)
+    stream = torch.cuda.Stream(dev)
+    stream.wait_stream(torch.cuda.current_stream())
+    e1.set_stream(stream.cuda_stream)
+
+    def one():
+        e1.route_bucket_device(keys.data_ptr(), N, G, silo.data_ptr(), act.data_ptr(), st.data_ptr(),
+                               perm.data_ptr(), off.data_ptr())
+    for _ in range(10):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ok = int((st == 0).sum().item())
+    e1.close()
+    return {"value": round(N * steps / wall, 1), "unit": "messages/s", "ms_per_step": round(wall / steps * 1e3, 4),
+            "steps": steps, "workload": f"{N} calls uniform over {G} grains, 1 silo, ring {mode}",
+            "routed_ok_last_step": ok}
 
 
 def micro_batch_latency(e, tcd: int, G: int, n_act: int, batches: int, B: int = 4096) -> dict:
