@@ -1439,15 +1439,15 @@ int mb_enqueue(gd_microbatch* mb, uint32_t n) {
         switch (h->ring_mode) {
             case GD_RING_DIRECTORY:
                 GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_DIRECTORY>, k, n, ring_args(h),
-                              table_args(h), so, act_dst, st, mb->ts));
+                              table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts));
                 break;
             case GD_RING_CONSISTENT:
                 GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_CONSISTENT>, k, n, ring_args(h),
-                              table_args(h), so, act_dst, st, mb->ts));
+                              table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts));
                 break;
             default:
                 GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_VIRTUAL_BUCKETS>, k, n,
-                              ring_args(h), table_args(h), so, act_dst, st, mb->ts));
+                              ring_args(h), table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts));
                 break;
         }
     } else if (n) {
@@ -1458,7 +1458,8 @@ int mb_enqueue(gd_microbatch* mb, uint32_t n) {
     }
     const uint32_t* a = act_dst;
     uint32_t *pm = mb->out_u32(d, 2), *ra = mb->out_u32(d, 5), *rs = mb->out_u32(d, 4), *nr = mb->out_u32(d, 3);
-    uint32_t* ac = zc ? mb->out_u32(d, 1) : nullptr;
+    // act to the host block: k_mb_route wrote it already; the LocalLookup route did not
+    uint32_t* ac = zc && h->cache_max ? mb->out_u32(d, 1) : nullptr;
     const dim3 g1(zc ? std::max<uint32_t>(1, std::min(mb->split, std::max<uint32_t>(1, n / 256))) : 1);
     if (n <= MB_THREADS * 4) GD_TRY(mb_launch_sort<4>(mb, g1, bits, a, n, passes, pm, ra, rs, nr, ac));
     else GD_TRY(mb_launch_sort<8>(mb, g1, bits, a, n, passes, pm, ra, rs, nr, ac));

@@ -372,6 +372,7 @@ __global__ void __launch_bounds__(MB_ROUTE_BLOCK) k_mb_route(const gd_key* __res
                                                             uint32_t* __restrict__ out_silo,
                                                             uint32_t* __restrict__ out_act,
                                                             uint8_t* __restrict__ out_status,
+                                                            uint32_t* __restrict__ act_host,
                                                             unsigned long long* ts) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     uint32_t* s_pts = s_ring;
@@ -380,9 +381,10 @@ __global__ void __launch_bounds__(MB_ROUTE_BLOCK) k_mb_route(const gd_key* __res
     mb_mark(ts, 0, t);
     stage_ring(ring, s_pts, s_own);
     mb_mark(ts, 1, t);
+    // act goes to HBM for the sort and, from these 64 workgroups, to the host block as well
     route_m_core<MODE, 1, MB_ROUTE_BLOCK, false, false>(keys, n, blockIdx.x * MB_ROUTE_BLOCK + threadIdx.x, ring,
                                                         s_pts, s_own, tab, tab.ctr->max_probe, out_silo, out_act,
-                                                        out_status, 0, nullptr, 0);
+                                                        out_status, 0, act_host, act_host ? 1u : 0u);
     mb_mark(ts, 2, t);
     if (ts) {
         __threadfence_system();
