@@ -155,7 +155,12 @@ struct gd_handle {
     uint32_t hist_tpb = 0;      // tiles per workgroup in the radix histogram, 1/4/8 (GD_HIST_TPB);
                                 // 0 = by size: 4 for 1024..4096 tiles (4M..16M keys), else 1 (A/B)
     bool compact_headers = true;   // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
-    bool fused_starts = true;   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
+    bool fused_starts = true;
+    bool radix_rowscan = true;  // one scan launch per radix pass, digit rows (GD_RADIX_ROWSCAN=0: reduce + down)
+    bool fill_in_hist = true;
+    bool range_scan = true;     // bucket starts: one range-scan launch when it applies (GD_RANGE_SCAN=0: reduce + down)
+    const uint32_t* last_totals = nullptr;   // the last radix pass's digit totals (row scans), and their count
+    uint32_t last_digits = 0;   // the first histogram pre-fills the bucket starts (GD_FILL_IN_HIST=0: k_fill)   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
     int fan_ilp = 2;                  // fan-out items per thread in flight together (GD_FAN_ILP: 1, 2, 4)
 
@@ -480,64 +485,77 @@ int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inc
 template <int BITS, int NT, int IT>
 int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
                  uint32_t* kout, uint32_t* vout, bool first,
-                 uint32_t* offsets, uint32_t* rank_out) {
+                 uint32_t* offsets, uint32_t* rank_out, FillArgs fill) {
     constexpr uint32_t TILE = NT * IT;
     const uint32_t tiles = blocks_for(n, TILE);
     const uint32_t R = 1u << BITS;
-    GD_TRY(ensure(h, h->hist, (size_t)R * tiles * sizeof(uint32_t)));
+    // the digit-major counts, then (row scans) the R digit totals
+    GD_TRY(ensure(h, h->hist, ((size_t)R * tiles + R) * sizeof(uint32_t)));
     uint32_t* hist = (uint32_t*)h->hist.p;
     // below 1024 tiles, 4 per workgroup would leave fewer workgroups than the 256 CUs
     const uint32_t tpb = h->hist_tpb ? h->hist_tpb : (tiles >= 1024 && tiles <= 4096 ? 4u : 1u);
     if constexpr (BITS <= 8) {
         if (tpb == 4)
             GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0, k_radix_hist_multi<BITS, NT, IT, 4>,
-                          kin, n, clamp, shift, tiles, hist));
+                          kin, n, clamp, shift, tiles, hist, fill));
         else if (tpb == 8)
             GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 8)), dim3(NT), 0, k_radix_hist_multi<BITS, NT, IT, 8>,
-                          kin, n, clamp, shift, tiles, hist));
+                          kin, n, clamp, shift, tiles, hist, fill));
         else
             GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_radix_hist<BITS, NT, IT>, kin, n, clamp, shift,
-                          tiles, hist));
+                          tiles, hist, fill));
     } else {
         GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_radix_hist<BITS, NT, IT>, kin, n, clamp, shift, tiles,
-                      hist));
+                      hist, fill));
     }
-    GD_TRY(scan_device<OpAdd>(h, hist, R * tiles, false, false, "hist"));
+    // one scan launch per digit row (the scatter adds the digit bases), or the device-wide
+    // reduce + down-sweep over all R * tiles counts (GD_RADIX_ROWSCAN=0)
+    const uint32_t* totals = nullptr;
+    h->last_totals = nullptr;
+    if (h->radix_rowscan) {
+        totals = hist + (size_t)R * tiles;
+        h->last_totals = totals;
+        h->last_digits = R;
+        GD_TRY(launch(h, "k_radix_rowscan", dim3(R), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles,
+                      hist + (size_t)R * tiles));
+    } else {
+        GD_TRY(scan_device<OpAdd>(h, hist, R * tiles, false, false, "hist"));
+    }
     if (first)
         return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, true, NT, IT>, kin, vin, n,
                       clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets, h->xcd_tiles,
-                      rank_out);
+                      rank_out, totals);
     return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, false, NT, IT>, kin, vin, n,
                   clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets, h->xcd_tiles,
-                      rank_out);
+                  rank_out, totals);
 }
 
 template <int BITS>
 int radix_pass(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
                uint32_t* kout, uint32_t* vout, bool first,
-                 uint32_t* offsets, uint32_t* rank_out) {
+                 uint32_t* offsets, uint32_t* rank_out, FillArgs fill) {
     switch (h->radix_cfg) {
-        case 1: return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+        case 1: return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
         case 2:
-            if constexpr (BITS <= 8) return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
-            else return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
-        case 3: return radix_pass_t<BITS, 512, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
-        default: return radix_pass_t<BITS, 256, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+            if constexpr (BITS <= 8) return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+            else return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+        case 3: return radix_pass_t<BITS, 512, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+        default: return radix_pass_t<BITS, 256, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
     }
 }
 
 int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp,
                    uint32_t shift, uint32_t* kout, uint32_t* vout, bool first,
-                 uint32_t* offsets, uint32_t* rank_out) {
+                 uint32_t* offsets, uint32_t* rank_out, FillArgs fill) {
     switch (bits) {
-        case 4: return radix_pass<4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
-        case 5: return radix_pass<5>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
-        case 6: return radix_pass<6>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
-        case 7: return radix_pass<7>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
-        case 8: return radix_pass<8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
-        case 9: return radix_pass<9>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
-        case 10: return radix_pass<10>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
-        default: return radix_pass<11>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out);
+        case 4: return radix_pass<4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+        case 5: return radix_pass<5>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+        case 6: return radix_pass<6>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+        case 7: return radix_pass<7>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+        case 8: return radix_pass<8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+        case 9: return radix_pass<9>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+        case 10: return radix_pass<10>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+        default: return radix_pass<11>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
     }
 }
 
@@ -548,8 +566,11 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
                   uint32_t* rank_out = nullptr) {
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
     const uint32_t n_off = n_act + 2;
-    GD_TRY(launch(h, "k_fill", dim3(blocks_for(n_off, BLOCK)), dim3(BLOCK), 0, k_fill_u32, offsets, n_off, n));
+    if (n == 0 || !h->fill_in_hist)
+        GD_TRY(launch(h, "k_fill", dim3(blocks_for(n_off, BLOCK)), dim3(BLOCK), 0, k_fill_u32, offsets, n_off, n));
     if (n == 0) return GD_OK;
+    // otherwise the first pass's histogram fills the starts (n = the empty-bucket value)
+    const FillArgs fill{h->fill_in_hist ? offsets : nullptr, n_off, n};
     uint32_t key_bits = 1;
     while (key_bits < 32 && (n_act >> key_bits) != 0) ++key_bits;
     const uint32_t passes = (key_bits + h->radix_max_bits - 1) / h->radix_max_bits;
@@ -568,13 +589,20 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
         // the last pass writes the bucket starts itself (no sorted keys, no k_bucket_starts)
         const bool last = p + 1 == passes && h->fused_starts;
         GD_TRY(radix_dispatch(h, (int)bits, kin, vin, n, n_act, p * bits, kout, vout, p == 0,
-                              last ? offsets : nullptr, p + 1 == passes ? rank_out : nullptr));
+                              last ? offsets : nullptr, p + 1 == passes ? rank_out : nullptr,
+                              p == 0 ? fill : FillArgs{nullptr, 0u, 0u}));
         kin = kout;
         vin = vout;
     }
     if (!h->fused_starts)
         GD_TRY(launch(h, "k_bucket_starts", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_bucket_starts, kin, n,
                       offsets));
+    // the last pass's digit spans <= RS_RANGE activations: one workgroup per digit range, carried by
+    // the pass's digit bases (GD_RANGE_SCAN=0: the device-wide scan)
+    const uint32_t last_shift = (passes - 1) * bits;
+    if (h->range_scan && h->last_totals && last_shift < 32 && (1u << last_shift) <= RS_RANGE)
+        return launch(h, "k_starts_rangescan", dim3((n_act >> last_shift) + 1), dim3(RS_THREADS), 0, k_starts_rangescan,
+                      offsets, n_act + 1, last_shift, h->last_totals, h->last_digits);
     return scan_device<OpMin>(h, offsets, n_act + 1, true, true, "offsets");
 }
 
@@ -832,6 +860,9 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
     if (const char* v = std::getenv("GD_RADIX_RANK")) h->radix_rank_atomic = std::atoi(v) ? 1u : 0u;
     if (const char* v = std::getenv("GD_FUSED_STARTS")) h->fused_starts = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_RADIX_ROWSCAN")) h->radix_rowscan = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_FILL_IN_HIST")) h->fill_in_hist = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_RANGE_SCAN")) h->range_scan = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_COMPACT_HEADERS")) h->compact_headers = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_HOST_CHUNK")) h->host_chunk = (uint32_t)std::strtoul(v, nullptr, 10);
     if (const char* v = std::getenv("GD_XCD_TILES")) h->xcd_tiles = std::atoi(v) ? 1u : 0u;

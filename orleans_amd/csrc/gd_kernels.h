@@ -725,12 +725,55 @@ __device__ __forceinline__ uint32_t block_excl_scan_add_n(uint32_t v, uint32_t* 
     return wbase + x - v;
 }
 
+// Two block-wide exclusive add-scans (one value each per thread) sharing one pair of barriers.
+template <int NTH>
+__device__ __forceinline__ void block_excl_scan_add2(uint32_t a, uint32_t b, uint32_t* s_wsum2, uint32_t& ea,
+                                                     uint32_t& eb) {
+    const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    uint32_t x = a, y = b;
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        const uint32_t xa = __shfl_up(x, off, WAVE), yb = __shfl_up(y, off, WAVE);
+        if (lane >= (uint32_t)off) {
+            x += xa;
+            y += yb;
+        }
+    }
+    if (lane == WAVE - 1) {
+        s_wsum2[w] = x;
+        s_wsum2[NTH / WAVE + w] = y;
+    }
+    __syncthreads();
+    uint32_t wa = 0, wb = 0;
+#pragma unroll
+    for (int k = 0; k < NTH / WAVE; ++k)
+        if ((uint32_t)k < w) {
+            wa += s_wsum2[k];
+            wb += s_wsum2[NTH / WAVE + k];
+        }
+    __syncthreads();
+    ea = wa + x - a;
+    eb = wb + y - b;
+}
+
+// p[0..n) = v by the whole grid, at the end of a kernel that has other work: the first pass's
+// histogram pre-fills the bucket starts this way (one launch fewer per bucketing).
+struct FillArgs {
+    uint32_t* p;
+    uint32_t n, v;
+};
+__device__ __forceinline__ void fill_grid(const FillArgs& f, uint32_t nt) {
+    if (!f.p) return;
+    for (uint32_t i = blockIdx.x * nt + threadIdx.x; i < f.n; i += gridDim.x * nt) f.p[i] = f.v;
+}
+
 // Histogram.  Keys are read 16 B per lane (order is irrelevant here).  Equal
 // digits within a wave instruction: the lanes sharing the first active lane's
 // digit (the hot key under Zipf skew) are folded into one LDS atomic.
 template <int BITS, int NT, int IT>
 __global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t clamp,
-                                                   uint32_t shift, uint32_t tiles, uint32_t* __restrict__ hist) {
+                                                   uint32_t shift, uint32_t tiles, uint32_t* __restrict__ hist,
+                                                   FillArgs fill) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = NT / WAVE;
     constexpr uint32_t TILE = NT * IT;
@@ -776,6 +819,7 @@ __global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ 
         for (int w = 0; w < NW; ++w) c += s_cnt[w * R + d];
         hist[d * tiles + blockIdx.x] = c;
     }
+    fill_grid(fill, NT);
 }
 
 // Multi-tile histogram: one workgroup counts TPB consecutive tiles, with every tile's 16-B key
@@ -785,7 +829,7 @@ __global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ 
 template <int BITS, int NT, int IT, int TPB>
 __global__ void __launch_bounds__(NT) k_radix_hist_multi(const uint32_t* __restrict__ keys, uint32_t n,
                                                          uint32_t clamp, uint32_t shift, uint32_t tiles,
-                                                         uint32_t* __restrict__ hist) {
+                                                         uint32_t* __restrict__ hist, FillArgs fill) {
     constexpr uint32_t R = 1u << BITS;
     constexpr uint32_t TILE = NT * IT;
     static_assert(IT % 4 == 0, "16-B loads");
@@ -842,6 +886,7 @@ __global__ void __launch_bounds__(NT) k_radix_hist_multi(const uint32_t* __restr
         const uint32_t t = x % TPB, d = x / TPB;
         if (t0 + t < tiles) hist[d * tiles + t0 + t] = s_cnt[t][d];
     }
+    fill_grid(fill, NT);
 }
 
 // Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each with its own
@@ -868,7 +913,8 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
                                                       uint32_t* __restrict__ keys_out,
                                                       uint32_t* __restrict__ vals_out, uint32_t rank_atomic,
                                                       uint32_t* __restrict__ starts, uint32_t xcd,
-                                                      uint32_t* __restrict__ rank_out) {
+                                                      uint32_t* __restrict__ rank_out,
+                                                      const uint32_t* __restrict__ totals) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = NT / WAVE;
     constexpr uint32_t TILE = NT * IT;
@@ -876,7 +922,7 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
     __shared__ uint32_t s_lstart[R];
     __shared__ uint32_t s_gbase[R];
     __shared__ uint2 s_kv[TILE];
-    __shared__ uint32_t s_wsum[NW];
+    __shared__ uint32_t s_wsum[2 * NW];
 
     const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, xcd);
     const uint32_t base = tile * TILE;
@@ -889,6 +935,8 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
     const uint32_t lane = lane_id();
     const uint32_t w = threadIdx.x / WAVE;
     const unsigned long long lt = (1ull << lane) - 1ull;
+    // thread t owns digits [t*DPT, (t+1)*DPT) in the digit-total scans below
+    constexpr uint32_t DPT = (R + NT - 1) / NT;
     uint32_t rk[IT], kk[IT], vv[IT];
     // Branch-free loads (clamped index, masked after): a per-item `if (valid)` around
     // each load makes hipcc wait vmcnt(0) after every one of them.
@@ -898,6 +946,16 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
         const uint32_t li = min(idx, n - 1);
         kk[r] = __builtin_nontemporal_load(keys_in + li);          // read once: stream past the caches
         if constexpr (!FIRST) vv[r] = __builtin_nontemporal_load(vals_in + li);
+    }
+    // totals != nullptr: k_radix_rowscan left gscan per digit row only, and the digit's base (the
+    // exclusive prefix of the R row totals) is added below, in the tile-local digit scan; the
+    // totals are loaded here, beside the keys
+    uint32_t tv[DPT], my_g = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < DPT; ++q) {
+        const uint32_t d = threadIdx.x * DPT + q;
+        tv[q] = totals && d < R ? totals[d] : 0u;
+        my_g += tv[q];
     }
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
@@ -953,8 +1011,6 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
     }
     __syncthreads();
     // cross-wave exclusive prefix per digit, then tile-local digit starts
-    // (thread t owns digits [t*DPT, (t+1)*DPT))
-    constexpr uint32_t DPT = (R + NT - 1) / NT;
     uint32_t my_total = 0;
 #pragma unroll
     for (uint32_t q = 0; q < DPT; ++q) {
@@ -971,9 +1027,10 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
             my_total += run;
         }
     }
-    const uint32_t ex = block_excl_scan_add_n<NT>(my_total, s_wsum);
+    uint32_t ex, exg;
+    block_excl_scan_add2<NT>(my_total, my_g, s_wsum, ex, exg);     // its barrier orders s_gbase's stores
     {
-        uint32_t run = ex;
+        uint32_t run = ex, rung = exg;
 #pragma unroll
         for (uint32_t q = 0; q < DPT; ++q) {
             const uint32_t d = threadIdx.x * DPT + q;
@@ -981,6 +1038,8 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
                 const uint32_t t = s_lstart[d];
                 s_lstart[d] = run;
                 run += t;
+                if (totals) s_gbase[d] += rung;
+                rung += tv[q];
             }
         }
     }
@@ -1186,6 +1245,135 @@ __global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_
 #pragma unroll
         for (int k = 0; k < IPT; ++k)
             if (p0 + k < n) out[p0 + k] = x[k];
+    }
+}
+
+// One workgroup per digit d (the radix pass's counts are digit-major): exclusive add-scan of the
+// row hist[d * tiles, (d + 1) * tiles) in place, and the row total into totals[d].  The scatter
+// adds the digit's base (the exclusive prefix of the totals) itself, so a pass takes one scan
+// launch here instead of a device-wide reduce + down-sweep.
+__global__ void __launch_bounds__(BLOCK) k_radix_rowscan(uint32_t* __restrict__ hist, uint32_t tiles,
+                                                         uint32_t* __restrict__ totals) {
+    constexpr int IPT = 16;
+    constexpr uint32_t CH = BLOCK * IPT;
+    __shared__ uint32_t s_wsum[BLOCK / WAVE];
+    uint32_t* row = hist + (size_t)blockIdx.x * tiles;
+    const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15u) == 0;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < tiles; c0 += CH) {
+        const uint32_t p0 = c0 + IPT * threadIdx.x;
+        const bool vec = aligned && p0 + IPT <= tiles;
+        uint32_t v[IPT];
+        if (vec) {
+#pragma unroll
+            for (int q = 0; q < IPT / 4; ++q) {
+                const uint4 u = *reinterpret_cast<const uint4*>(row + p0 + 4 * q);
+                v[4 * q] = u.x; v[4 * q + 1] = u.y; v[4 * q + 2] = u.z; v[4 * q + 3] = u.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < IPT; ++k) v[k] = p0 + k < tiles ? row[p0 + k] : 0u;
+        }
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) acc += v[k];
+        uint32_t run = carry + block_excl_scan<OpAdd>(acc, s_wsum);
+        uint32_t chunk = 0;
+#pragma unroll
+        for (int k = 0; k < BLOCK / WAVE; ++k) chunk += s_wsum[k];
+        uint32_t r[IPT];
+#pragma unroll
+        for (int k = 0; k < IPT; ++k) {
+            r[k] = run;
+            run += v[k];
+        }
+        if (vec) {
+#pragma unroll
+            for (int q = 0; q < IPT / 4; ++q)
+                *reinterpret_cast<uint4*>(row + p0 + 4 * q) = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < IPT; ++k)
+                if (p0 + k < tiles) row[p0 + k] = r[k];
+        }
+        carry += chunk;
+        __syncthreads();                    // s_wsum is rewritten by the next chunk's scan
+    }
+    if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+}
+
+// The bucket starts' reverse inclusive min-scan in one launch, when the last radix pass's digit
+// covers at most RS_RANGE activations (1 << shift): workgroup d scans the activations
+// [d << shift, (d + 1) << shift) of offsets[0, n_scan) alone.  Its carry -- the first start past
+// the range -- is the last pass's digit base base(d + 1) = the number of messages whose (clamped)
+// key lies below the range's end (n when there is none): the starts of non-empty activations
+// increase with the activation, and the empty ones hold n.
+constexpr uint32_t RS_THREADS = 1024;
+constexpr uint32_t RS_IPT = 16;
+constexpr uint32_t RS_RANGE = RS_THREADS * RS_IPT;      // 16,384 activations per workgroup
+__global__ void __launch_bounds__(RS_THREADS) k_starts_rangescan(uint32_t* __restrict__ offsets, uint32_t n_scan,
+                                                                 uint32_t shift, const uint32_t* __restrict__ totals,
+                                                                 uint32_t n_digits) {
+    constexpr uint32_t NW = RS_THREADS / WAVE;
+    __shared__ uint32_t s_w[2][NW];
+    const uint32_t d = blockIdx.x;
+    const uint32_t lo = d << shift;
+    const uint32_t hi = min(lo + (1u << shift), n_scan);
+    // thread t takes chunk c = RS_THREADS - 1 - t, so a forward exclusive scan over the threads is
+    // the minimum over the chunks after c; the loads go out first
+    const uint32_t c = RS_THREADS - 1 - threadIdx.x;
+    const uint32_t p0 = lo + c * RS_IPT;
+    uint32_t v[RS_IPT];
+    const bool vec = p0 + RS_IPT <= hi && (reinterpret_cast<uintptr_t>(offsets + p0) & 15u) == 0;
+    if (vec) {
+#pragma unroll
+        for (uint32_t q = 0; q < RS_IPT / 4; ++q) {
+            const uint4 u = *reinterpret_cast<const uint4*>(offsets + p0 + 4 * q);
+            v[4 * q] = u.x; v[4 * q + 1] = u.y; v[4 * q + 2] = u.z; v[4 * q + 3] = u.w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < RS_IPT; ++k) v[k] = p0 + k < hi ? offsets[min(p0 + k, n_scan - 1)] : 0xFFFFFFFFu;
+    }
+    uint32_t part = 0;                                   // this thread's share of base(d + 1)
+    for (uint32_t j = threadIdx.x; j <= d && j < n_digits; j += RS_THREADS) part += totals[j];
+    uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t k = 0; k < RS_IPT; ++k) m = min(m, v[k]);
+    // one pass over the waves: the digit base's sum and the exclusive min-scan of the chunk minima
+    const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    uint32_t x = m;
+#pragma unroll
+    for (int off = 1; off < WAVE; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, WAVE);
+        if (lane >= (uint32_t)off) x = min(x, y);
+        part += __shfl_xor(part, off, WAVE);
+    }
+    uint32_t ex = __shfl_up(x, 1, WAVE);
+    if (lane == 0) ex = 0xFFFFFFFFu;
+    if (lane == WAVE - 1) s_w[0][w] = x;
+    if (lane == 0) s_w[1][w] = part;
+    __syncthreads();
+    uint32_t carry = 0, wmin = 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t k = 0; k < NW; ++k) {
+        carry += s_w[1][k];
+        if (k < w) wmin = min(wmin, s_w[0][k]);
+    }
+    uint32_t run = min(carry, min(wmin, ex));
+#pragma unroll
+    for (int k = RS_IPT - 1; k >= 0; --k) {
+        run = min(run, v[k]);
+        v[k] = run;
+    }
+    if (vec) {
+#pragma unroll
+        for (uint32_t q = 0; q < RS_IPT / 4; ++q)
+            *reinterpret_cast<uint4*>(offsets + p0 + 4 * q) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < RS_IPT; ++k)
+            if (p0 + k < hi) offsets[p0 + k] = v[k];
     }
 }
 

@@ -245,6 +245,30 @@ def test_bucket_matches_oracle(gd, n, n_act):
     e.close()
 
 
+@pytest.mark.parametrize("shape", ["first", "last", "ends", "trailing_only"])
+@pytest.mark.parametrize("n_act", [1 << 20, 100_000, 16_383, 3])
+def test_bucket_starts_empty_runs(gd, shape, n_act):
+    """Bucket starts across long runs of empty activations: the reverse min-scan's carries
+    (k_starts_rangescan's digit-base carry, or the device-wide scan) must cross whole empty digit
+    ranges, and an empty tail takes n."""
+    n = 50_000
+    rng = np.random.default_rng(n_act + len(shape))
+    if shape == "first":
+        acts = np.zeros(n, np.uint32)
+    elif shape == "last":
+        acts = np.full(n, n_act - 1, np.uint32)
+    elif shape == "ends":
+        acts = np.where(rng.random(n) < 0.5, 0, n_act - 1).astype(np.uint32)
+    else:
+        acts = np.full(n, o.M32, np.uint32)                     # every message unrouted
+    e = _engine(gd, o.bench_silos(8))
+    perm, off = e.bucket(acts, n_act)
+    wp, wo = o.bucket_stable(acts, n_act)
+    np.testing.assert_array_equal(perm, wp)
+    np.testing.assert_array_equal(off, wo)
+    e.close()
+
+
 def test_bucket_fifo_loop_small(gd):
     rng = np.random.default_rng(2)
     acts = rng.integers(0, 9, size=3000).astype(np.uint32)
