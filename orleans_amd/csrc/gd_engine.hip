@@ -158,7 +158,8 @@ struct gd_handle {
     bool fused_starts = true;
     bool radix_rowscan = true;  // one scan launch per radix pass, digit rows (GD_RADIX_ROWSCAN=0: reduce + down)
     bool fill_in_hist = true;
-    bool range_scan = true;     // bucket starts: one range-scan launch when it applies (GD_RANGE_SCAN=0: reduce + down)
+    bool range_scan = true;
+    bool shard_gather = true;   // exchange partition of keys: k_shard_gather (GD_SHARD_GATHER=0: k_shard_scatter, staged keys)     // bucket starts: one range-scan launch when it applies (GD_RANGE_SCAN=0: reduce + down)
     const uint32_t* last_totals = nullptr;   // the last radix pass's digit totals (row scans), and their count
     uint32_t last_digits = 0;   // the first histogram pre-fills the bucket starts (GD_FILL_IN_HIST=0: k_fill)   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
@@ -672,6 +673,15 @@ template <int BITS, bool NODES>
 int shard_scatter_t(gd_handle* h, const void* recs, const uint32_t* payload, const uint8_t* dest, uint32_t n,
                     uint32_t n_shards, uint32_t tiles, const uint32_t* gscan, void* out, uint32_t* out_pay,
                     const uint32_t* kdesc) {
+    // keys with a compaction descriptor: the compact case by k_shard_gather, the other by the staged
+    // kernel (each returns at once in the other's case)
+    if constexpr (!NODES)
+        if (h->shard_gather && kdesc) {
+            GD_TRY(launch(h, "k_shard_scatter", dim3(tiles), dim3(SH_NT), 0, k_shard_gather<BITS>,
+                          (const gd_key*)recs, payload, dest, n, n_shards, tiles, gscan, out, out_pay, kdesc));
+            return launch(h, "k_shard_scatter", dim3(tiles), dim3(SH_NT), 0, k_shard_scatter<BITS, false, true>, recs,
+                          payload, dest, n, n_shards, tiles, gscan, out, out_pay, kdesc);
+        }
     return launch(h, "k_shard_scatter", dim3(tiles), dim3(SH_NT), 0, k_shard_scatter<BITS, NODES>, recs, payload, dest,
                   n, n_shards, tiles, gscan, out, out_pay, kdesc);
 }
@@ -863,6 +873,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_RADIX_ROWSCAN")) h->radix_rowscan = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_FILL_IN_HIST")) h->fill_in_hist = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_RANGE_SCAN")) h->range_scan = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_SHARD_GATHER")) h->shard_gather = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_COMPACT_HEADERS")) h->compact_headers = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_HOST_CHUNK")) h->host_chunk = (uint32_t)std::strtoul(v, nullptr, 10);
     if (const char* v = std::getenv("GD_XCD_TILES")) h->xcd_tiles = std::atoi(v) ? 1u : 0u;

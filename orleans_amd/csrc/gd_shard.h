@@ -82,6 +82,21 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
     if constexpr (!NODES)
         if (kdesc && n) ref_tcd = reinterpret_cast<const uint64_t*>(recs)[2];
     bool wide = false;
+    // every record of the thread is loaded before the first hash (one wait, not one per record)
+    constexpr int RW = NODES ? 1 : 3;
+    uint64_t kv[SH_IT][RW];
+#pragma unroll
+    for (int r = 0; r < SH_IT; ++r) {
+        const uint32_t li = min(base + (w * SH_IT + r) * WAVE + lane, n - 1);
+        if constexpr (NODES) {
+            kv[r][0] = reinterpret_cast<const uint32_t*>(recs)[li];
+        } else {
+            const uint64_t* kp = reinterpret_cast<const uint64_t*>(recs) + 3ull * li;
+            kv[r][0] = kp[0];
+            kv[r][1] = kp[1];
+            kv[r][2] = kp[2];
+        }
+    }
 #pragma unroll
     for (int r = 0; r < SH_IT; ++r) {
         const uint32_t i = base + (w * SH_IT + r) * WAVE + lane;
@@ -89,12 +104,11 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
         uint32_t d = 0;
         if (valid) {
             if constexpr (NODES) {
-                const uint32_t node = reinterpret_cast<const uint32_t*>(recs)[i];
+                const uint32_t node = (uint32_t)kv[r][0];
                 d = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(0, node, tcd))] % n_shards;
             } else {
-                const uint64_t* kp = reinterpret_cast<const uint64_t*>(recs) + 3ull * i;
-                d = key_dest<MODE>(kp[0], kp[1], kp[2], s_pts, s_own, ring, n_shards, ext, i);
-                wide |= kp[0] != 0 || kp[2] != ref_tcd;
+                d = key_dest<MODE>(kv[r][0], kv[r][1], kv[r][2], s_pts, s_own, ring, n_shards, ext, i);
+                wide |= kv[r][0] != 0 || kv[r][2] != ref_tcd;
             }
             dest[i] = (uint8_t)d;
         }
@@ -245,7 +259,7 @@ __global__ void __launch_bounds__(BLOCK) k_fwd_gather(const uint32_t* __restrict
 }
 
 // payload_in == nullptr: the payload is the record's batch index (the origin index).
-template <int BITS, bool NODES>
+template <int BITS, bool NODES, bool SKIP_COMPACT = false>
 __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict__ recs,
                                                          const uint32_t* __restrict__ payload_in,
                                                          const uint8_t* __restrict__ dest, uint32_t n,
@@ -257,6 +271,8 @@ __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict_
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = SH_NT / WAVE;
     constexpr int RW = NODES ? 1 : 3;           // 8-B words per record (keys) / one u32 (nodes)
+    if constexpr (SKIP_COMPACT)
+        if (kdesc[0]) return;                   // compact: k_shard_gather's case
     __shared__ uint32_t s_wcnt[NW][R];
     __shared__ uint32_t s_lstart[R];
     __shared__ uint32_t s_gbase[R];
@@ -379,6 +395,128 @@ __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict_
             }
         }
     }
+}
+
+// A compact batch (k_key_desc: every key N0 == 0 with one TypeCodeData, sent as N1 alone) without
+// staging the keys in LDS: the tile is ranked from its destination bytes alone, LDS keeps each
+// output slot's source record (u16) and destination, and the write phase reads each N1 straight
+// from the batch and writes the runs coalesced.  6 KB of LDS per workgroup instead of the 58 KB
+// of k_shard_scatter's staged 24-B keys: several times the waves per CU.  Returns at once for a
+// batch that is not compact (k_shard_scatter<.., SKIP_COMPACT> runs beside it and takes that
+// case; gathering whole 24-B records measured slower than staging them: 0.18-0.24 vs 0.16 ms per
+// 16M keys at 1-8 destinations).  Same output as k_shard_scatter<BITS, false>.
+template <int BITS>
+__global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict__ recs,
+                                                        const uint32_t* __restrict__ payload_in,
+                                                        const uint8_t* __restrict__ dest, uint32_t n,
+                                                        uint32_t n_shards, uint32_t tiles,
+                                                        const uint32_t* __restrict__ gscan,
+                                                        void* __restrict__ out_recs,
+                                                        uint32_t* __restrict__ out_payload,
+                                                        const uint32_t* __restrict__ kdesc) {
+    constexpr uint32_t R = 1u << BITS;
+    constexpr int NW = SH_NT / WAVE;
+    if (!kdesc[0]) return;                      // not compact: k_shard_scatter's case
+    __shared__ uint32_t s_wcnt[NW][R];
+    __shared__ uint32_t s_lstart[R];
+    __shared__ uint32_t s_gbase[R];
+    __shared__ uint32_t s_wsum[NW];
+    __shared__ uint16_t s_src[SH_TILE];
+    __shared__ uint8_t s_dig[SH_TILE];
+    static_assert(SH_TILE <= 65536, "u16 source slots");
+
+    const uint32_t tile = blockIdx.x;
+    const uint32_t base = tile * SH_TILE;
+    const uint32_t cnt_tile = min(SH_TILE, n - base);
+    for (uint32_t d = threadIdx.x; d < R; d += SH_NT) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) s_wcnt[w][d] = 0;
+        s_gbase[d] = d < n_shards ? gscan[d * tiles + tile] : 0u;
+    }
+    const uint32_t lane = lane_id();
+    const uint32_t w = threadIdx.x / WAVE;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    uint32_t dd[SH_IT], rk[SH_IT];
+#pragma unroll
+    for (int r = 0; r < SH_IT; ++r) dd[r] = dest[min(base + (w * SH_IT + r) * WAVE + lane, n - 1)];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SH_IT; ++r) {
+        const uint32_t idx = base + (w * SH_IT + r) * WAVE + lane;
+        const bool valid = idx < n;
+        const uint32_t d = dd[r] & (R - 1);
+        const unsigned long long peers = match_digit<BITS>(d, valid);
+        uint32_t c = 0;
+        if (valid) c = s_wcnt[w][d];
+        rk[r] = c + (uint32_t)__popcll(peers & lt);
+        if (valid && (peers & lt) == 0) s_wcnt[w][d] = c + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    constexpr uint32_t DPT = (R + SH_NT - 1) / SH_NT;
+    uint32_t my_total = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < DPT; ++q) {
+        const uint32_t d = threadIdx.x * DPT + q;
+        if (d < R) {
+            uint32_t run = 0;
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) {
+                const uint32_t t = s_wcnt[ww][d];
+                s_wcnt[ww][d] = run;
+                run += t;
+            }
+            s_lstart[d] = run;
+            my_total += run;
+        }
+    }
+    const uint32_t ex = block_excl_scan_add_n<SH_NT>(my_total, s_wsum);
+    {
+        uint32_t run = ex;
+#pragma unroll
+        for (uint32_t q = 0; q < DPT; ++q) {
+            const uint32_t d = threadIdx.x * DPT + q;
+            if (d < R) {
+                const uint32_t t = s_lstart[d];
+                s_lstart[d] = run;
+                run += t;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SH_IT; ++r) {
+        const uint32_t loc = (w * SH_IT + r) * WAVE + lane;
+        if (base + loc < n) {
+            const uint32_t d = dd[r] & (R - 1);
+            const uint32_t p = s_lstart[d] + s_wcnt[w][d] + rk[r];
+            s_src[p] = (uint16_t)loc;
+            s_dig[p] = (uint8_t)d;
+        }
+    }
+    __syncthreads();
+    const uint64_t* k64 = reinterpret_cast<const uint64_t*>(recs);
+    uint64_t* o64 = reinterpret_cast<uint64_t*>(out_recs);
+    // one 8-B N1 and the payload per output slot; every gather of the thread before the stores
+    uint64_t kv[SH_IT];
+    uint32_t pay[SH_IT], gg[SH_IT];
+#pragma unroll
+    for (int j = 0; j < SH_IT; ++j) {
+        const uint32_t p = j * SH_NT + threadIdx.x;
+        gg[j] = 0xFFFFFFFFu;
+        if (p < cnt_tile) {
+            const uint32_t i = base + s_src[p];
+            const uint32_t d = s_dig[p];
+            gg[j] = s_gbase[d] + (p - s_lstart[d]);
+            kv[j] = k64[3ull * i + 1];
+            pay[j] = payload_in ? payload_in[i] : i;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < SH_IT; ++j)
+        if (gg[j] < n) {            // ~0: no record here; else always in bounds when the scan is right
+            o64[gg[j]] = kv[j];
+            out_payload[gg[j]] = pay[j];
+        }
 }
 
 // counts[d] = records for destination d, from the scanned (dest, tile) bases.
