@@ -240,10 +240,11 @@ class Silo:
     gen: int
 
     def endpoint_str(self) -> str:
-        # IPEndPoint.ToString(): "a.b.c.d:port" / "[v6]:port"
+        # IPEndPoint.ToString(): "a.b.c.d:port" / "[v6]:port" (canonical text of the parsed address;
+        # the IPv6 form is an unpinned assumption)
         addr = ipaddress.ip_address(self.ip)
         if addr.version == 4:
-            return f"{self.ip}:{self.port}"
+            return f"{addr}:{self.port}"
         if addr.ipv4_mapped is not None:        # .NET prints mapped addresses as ::ffff:a.b.c.d
             return f"[::ffff:{addr.ipv4_mapped}]:{self.port}"
         return f"[{addr.compressed}]:{self.port}"
