@@ -53,17 +53,36 @@ def grain_keys(type_code_data: int, ks: np.ndarray) -> np.ndarray:
     return out
 
 
+def radix_layout(n: int, n_act: int):
+    """(passes, digit bits, packed) of libgraindispatch's bucketing for n messages over n_act
+    activations (gd_engine.hip bucket_device): <= 8-bit digits; records packed to 6 B between the
+    passes (GD_RADIX_PACK, on by default) when the key bits above the first digit fit a u16 and the
+    message index fits a u32 beside the first digit."""
+    key_bits = max(1, int(n_act).bit_length())
+    passes = (key_bits + 7) // 8
+    bits = max(4, -(-key_bits // passes))
+    ib = max(1, int(max(n, 1) - 1).bit_length())
+    packed = (passes >= 2 and bits <= 8 and key_bits - bits <= 16 and ib + bits <= 32
+              and os.environ.get("GD_RADIX_PACK", "1") != "0")
+    return passes, bits, packed
+
+
 def kernel_bytes(name: str, n: int, n_act: int, passes: int, world: int) -> float:
     """Algorithmic HBM bytes of one step for a kernel (all launches of it), per
     DESIGN.md 'Byte model'."""
+    _, _, packed = radix_layout(n, n_act)
     if name == "k_route":
         return n * (24 + 32 + 4 + 4 + 1)          # key, one slot, silo+act+status
     if name == "k_radix_scatter":
         # pass 1 reads act, writes (key, idx); middle passes move (key, idx); the last pass reads
-        # (key, idx) and writes idx only (it emits the bucket starts instead of the sorted keys)
-        return n * 8 if passes == 1 else n * (12 + 16 * (passes - 2) + 12)
+        # (key, idx) and writes idx only (it emits the bucket starts instead of the sorted keys).
+        # Packed: (key, idx) is 6 B (u32 index + first digit, u16 higher key bits).
+        if passes == 1:
+            return n * 8
+        return n * (10 + 12 * (passes - 2) + 10) if packed else n * (12 + 16 * (passes - 2) + 12)
     if name == "k_radix_hist":
-        return n * 4 * passes
+        # pass 1 reads act; packed, the later passes read the u16 high-key array alone
+        return n * (4 + 2 * (passes - 1)) if packed else n * 4 * passes
     if name == "k_bucket_starts":
         return n * 4 + (n_act + 2) * 4
     return 0.0
@@ -294,8 +313,7 @@ def main():
         kt = e.kernel_times()
         e.set_kernel_timing(False)
 
-    key_bits = max(1, int(n_act).bit_length())
-    passes = (key_bits + 7) // 8
+    passes, _, packed = radix_layout(m_recv, n_act)
     kernels = {}
     for name, (launches, ms) in kt.items():
         if launches == 0:
@@ -334,7 +352,10 @@ def main():
                 "kernel": "k_radix_scatter", "achieved": sc["alg_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": sc["frac_hbm"], "traffic": sc_traffic, "launches_per_step": sl,
                 "alg_bytes_per_launch": kernel_bytes("k_radix_scatter", m_recv, n_act, passes, world) / sl,
-                "avg_launch_ms": round(sc["ms_per_step"] / sl, 5)}
+                "avg_launch_ms": round(sc["ms_per_step"] / sl, 5), "packed_records": packed,
+                # SURVEY 8(d)'s own definition: 16 B per record per pass (8 read + 8 written)
+                "frac_survey_model": round(16.0 * passes * m_recv / (sc["ms_per_step"] * 1e-3) / 1e9
+                                           / PEAK_HBM_GBS, 4) if sc["ms_per_step"] > 0 else None}
         if dom == "k_route" and args.workload == "cfg2":
             # k_route is one random 32-B slot read per message beside the 24-B key stream: its
             # real ceiling is the random-probe rate, measured on MI355X by tools/ubench_random.hip
@@ -581,8 +602,11 @@ def cpu_baseline(args, tcd, G_total, pts, own, owner):
 
 # ---- BASELINE cfg 4: Chirper-style follower fan-out cascade -------------------------------------
 
-def fan_kernel_bytes(name, msgs, n_front, n_act, passes, keep_target, n_hops):
-    """Algorithmic HBM bytes over all launches of a cfg 4 kernel in one cascade."""
+def fan_kernel_bytes(name, msgs, n_front, n_act, passes, keep_target, n_hops, hop_msgs=None):
+    """Algorithmic HBM bytes over all launches of a cfg 4 kernel in one cascade.
+    hop_msgs: the bucketing kernels per hop, by the main byte model (packed records where they fit)."""
+    if hop_msgs is not None and name in ("k_radix_scatter", "k_radix_hist"):
+        return float(sum(kernel_bytes(name, m, n_act, radix_layout(m, n_act)[0], 1) for m in hop_msgs if m))
     if name == "k_fan_route":
         # dst read 4 + one slot 32 + sender/silo/act 12 + status 1 (+ target 4); per publisher 16
         return msgs * (49 + (4 if keep_target else 0)) + n_front * 16
@@ -674,7 +698,8 @@ def run_cfg4(args, world, rank, local, dev):
             if not launches:
                 continue
             per = ms / args.profile_steps
-            b = fan_kernel_bytes(name, msgs_step, sum(hop_front), n, passes, not args.no_target, len(hops))
+            b = fan_kernel_bytes(name, msgs_step, sum(hop_front), n, passes, not args.no_target, len(hops),
+                                 hop_msgs)
             gbs = b / (per * 1e-3) / 1e9 if b and per > 0 else None
             kernels[name] = {"launches_per_step": launches // args.profile_steps, "ms_per_step": round(per, 4),
                              "alg_GBps": round(gbs, 1) if gbs else None,

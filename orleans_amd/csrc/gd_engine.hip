@@ -156,6 +156,7 @@ struct gd_handle {
                                 // 0 = by size: 4 for 1024..4096 tiles (4M..16M keys), else 1 (A/B)
     bool compact_headers = true;   // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
     bool fused_starts = true;
+    bool radix_pack = true;     // 6-B packed records between radix passes when they fit (GD_RADIX_PACK)
     bool radix_rowscan = true;  // one scan launch per radix pass, digit rows (GD_RADIX_ROWSCAN=0: reduce + down)
     bool fill_in_hist = true;
     bool range_scan = true;
@@ -486,7 +487,7 @@ int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inc
 template <int BITS, int NT, int IT>
 int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
                  uint32_t* kout, uint32_t* vout, bool first,
-                 uint32_t* offsets, uint32_t* rank_out, FillArgs fill) {
+                 uint32_t* offsets, uint32_t* rank_out, FillArgs fill, Pack pk) {
     constexpr uint32_t TILE = NT * IT;
     const uint32_t tiles = blocks_for(n, TILE);
     const uint32_t R = 1u << BITS;
@@ -495,7 +496,21 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
     uint32_t* hist = (uint32_t*)h->hist.p;
     // below 1024 tiles, 4 per workgroup would leave fewer workgroups than the 256 CUs
     const uint32_t tpb = h->hist_tpb ? h->hist_tpb : (tiles >= 1024 && tiles <= 4096 ? 4u : 1u);
-    if constexpr (BITS <= 8) {
+    if (pk.in) {
+        // packed records: the histogram reads the u16 high-key array (bucket_device enables the
+        // packing only for the 512 x 8 tiles and digits of at most 8 bits)
+        if constexpr (BITS <= 8 && NT == 512 && IT == 8) {
+            const uint16_t* kb16 = reinterpret_cast<const uint16_t*>(vin);
+            if (tpb == 4)
+                GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0, k_radix_hist16<BITS, NT, IT, 4>,
+                              kb16, n, shift - pk.b1, tiles, hist));
+            else
+                GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_radix_hist16<BITS, NT, IT, 1>, kb16, n,
+                              shift - pk.b1, tiles, hist));
+        } else {
+            return set_err(h, GD_EINVAL, "packed radix records need 512 x 8 tiles and <= 8-bit digits");
+        }
+    } else if constexpr (BITS <= 8) {
         if (tpb == 4)
             GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0, k_radix_hist_multi<BITS, NT, IT, 4>,
                           kin, n, clamp, shift, tiles, hist, fill));
@@ -525,38 +540,38 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
     if (first)
         return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, true, NT, IT>, kin, vin, n,
                       clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets, h->xcd_tiles,
-                      rank_out, totals);
+                      rank_out, totals, pk);
     return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, false, NT, IT>, kin, vin, n,
                   clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets, h->xcd_tiles,
-                  rank_out, totals);
+                  rank_out, totals, pk);
 }
 
 template <int BITS>
 int radix_pass(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
                uint32_t* kout, uint32_t* vout, bool first,
-                 uint32_t* offsets, uint32_t* rank_out, FillArgs fill) {
+                 uint32_t* offsets, uint32_t* rank_out, FillArgs fill, Pack pk) {
     switch (h->radix_cfg) {
-        case 1: return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+        case 1: return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
         case 2:
-            if constexpr (BITS <= 8) return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
-            else return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
-        case 3: return radix_pass_t<BITS, 512, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
-        default: return radix_pass_t<BITS, 256, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+            if constexpr (BITS <= 8) return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
+            else return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
+        case 3: return radix_pass_t<BITS, 512, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
+        default: return radix_pass_t<BITS, 256, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
     }
 }
 
 int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp,
                    uint32_t shift, uint32_t* kout, uint32_t* vout, bool first,
-                 uint32_t* offsets, uint32_t* rank_out, FillArgs fill) {
+                 uint32_t* offsets, uint32_t* rank_out, FillArgs fill, Pack pk) {
     switch (bits) {
-        case 4: return radix_pass<4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
-        case 5: return radix_pass<5>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
-        case 6: return radix_pass<6>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
-        case 7: return radix_pass<7>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
-        case 8: return radix_pass<8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
-        case 9: return radix_pass<9>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
-        case 10: return radix_pass<10>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
-        default: return radix_pass<11>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill);
+        case 4: return radix_pass<4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
+        case 5: return radix_pass<5>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
+        case 6: return radix_pass<6>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
+        case 7: return radix_pass<7>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
+        case 8: return radix_pass<8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
+        case 9: return radix_pass<9>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
+        case 10: return radix_pass<10>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
+        default: return radix_pass<11>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
     }
 }
 
@@ -584,14 +599,21 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
     uint32_t* vb[2] = {(uint32_t*)h->u32_c.p, (uint32_t*)h->u32_d.p};
     const uint32_t* kin = acts;
     const uint32_t* vin = nullptr;
+    // packed records between the passes (gd_kernels.h Pack): the key bits above the first digit fit
+    // a u16 and the index fits beside the first digit in a u32 (BASELINE cfg 2: 14 + 24 + 7 bits)
+    uint32_t ib = 1;
+    while (ib < 32 && ((n - 1) >> ib) != 0) ++ib;
+    const bool pack = h->radix_pack && passes >= 2 && h->fused_starts && h->radix_cfg == 1 && bits <= 8 &&
+                      key_bits - bits <= 16 && ib + bits <= 32;
     for (uint32_t p = 0; p < passes; ++p) {
         uint32_t* kout = kb[p & 1];
         uint32_t* vout = (p + 1 == passes) ? perm : vb[p & 1];
         // the last pass writes the bucket starts itself (no sorted keys, no k_bucket_starts)
         const bool last = p + 1 == passes && h->fused_starts;
+        const Pack pk{ib, bits, pack && p > 0, pack && p + 1 < passes};
         GD_TRY(radix_dispatch(h, (int)bits, kin, vin, n, n_act, p * bits, kout, vout, p == 0,
                               last ? offsets : nullptr, p + 1 == passes ? rank_out : nullptr,
-                              p == 0 ? fill : FillArgs{nullptr, 0u, 0u}));
+                              p == 0 ? fill : FillArgs{nullptr, 0u, 0u}, pk));
         kin = kout;
         vin = vout;
     }
@@ -870,6 +892,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
     if (const char* v = std::getenv("GD_RADIX_RANK")) h->radix_rank_atomic = std::atoi(v) ? 1u : 0u;
     if (const char* v = std::getenv("GD_FUSED_STARTS")) h->fused_starts = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_RADIX_PACK")) h->radix_pack = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_RADIX_ROWSCAN")) h->radix_rowscan = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_FILL_IN_HIST")) h->fill_in_hist = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_RANGE_SCAN")) h->range_scan = std::atoi(v) != 0;

@@ -889,6 +889,73 @@ __global__ void __launch_bounds__(NT) k_radix_hist_multi(const uint32_t* __restr
     fill_grid(fill, NT);
 }
 
+// Histogram of a packed pass (k_radix_scatter with Pack::in): the key bits above the first pass's
+// digit are a u16 array (8 keys per 16-B load), already clamped by the first pass.  TPB tiles per
+// workgroup as k_radix_hist_multi (TPB = 1: k_radix_hist's layout).  Same output as those for the
+// full keys.
+template <int BITS, int NT, int IT, int TPB>
+__global__ void __launch_bounds__(NT) k_radix_hist16(const uint16_t* __restrict__ keys, uint32_t n, uint32_t shift,
+                                                     uint32_t tiles, uint32_t* __restrict__ hist) {
+    constexpr uint32_t R = 1u << BITS;
+    constexpr uint32_t TILE = NT * IT;
+    static_assert(IT % 8 == 0, "16-B loads of 8 keys");
+    __shared__ uint32_t s_cnt[TPB][R];
+    for (uint32_t x = threadIdx.x; x < TPB * R; x += NT) (&s_cnt[0][0])[x] = 0;
+    __syncthreads();
+    const uint32_t t0 = blockIdx.x * TPB;
+    const uint32_t lane = lane_id();
+    const bool aligned = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
+    uint32_t k[TPB][IT];
+    if (aligned && (uint64_t)(t0 + TPB) * TILE <= n) {
+#pragma unroll
+        for (int t = 0; t < TPB; ++t)
+#pragma unroll
+            for (int j = 0; j < IT / 8; ++j) {
+                const uint64_t i0 = (uint64_t)(t0 + t) * TILE + 8 * (j * NT + threadIdx.x);
+                const uint4 v = *reinterpret_cast<const uint4*>(keys + i0);
+                const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    k[t][8 * j + 2 * q] = u[q] & 0xFFFFu;
+                    k[t][8 * j + 2 * q + 1] = u[q] >> 16;
+                }
+            }
+    } else {
+#pragma unroll
+        for (int t = 0; t < TPB; ++t)
+#pragma unroll
+            for (int j = 0; j < IT / 8; ++j) {
+                const uint64_t i0 = (uint64_t)(t0 + t) * TILE + 8 * (j * NT + threadIdx.x);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) k[t][8 * j + q] = (i0 + q < n) ? keys[i0 + q] : 0u;
+            }
+    }
+#pragma unroll
+    for (int t = 0; t < TPB; ++t) {
+        const uint64_t base = (uint64_t)(t0 + t) * TILE;
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const uint64_t i = base + 8 * ((j / 8) * NT + threadIdx.x) + (j % 8);
+            const bool valid = i < n;
+            const uint32_t d = (k[t][j] >> shift) & (R - 1);
+            const unsigned long long act = __ballot(valid);
+            if (act == 0) continue;
+            const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
+            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
+            const unsigned long long hot = __ballot(valid && d == d0);
+            if (valid) {
+                if (d != d0) atomicAdd(&s_cnt[t][d], 1u);
+                else if (lane == lead) atomicAdd(&s_cnt[t][d], (uint32_t)__popcll(hot));
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < TPB * R; x += NT) {
+        const uint32_t t = x % TPB, d = x / TPB;
+        if (t0 + t < tiles) hist[d * tiles + t0 + t] = s_cnt[t][d];
+    }
+}
+
 // Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each with its own
 // L2.  With xcd != 0 block b processes tile start(b % 8) + b / 8, so every XCD owns a contiguous
 // tile range: the digit-run fragments that consecutive tiles write next to each other in the
@@ -898,6 +965,16 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb, uint32_t x
     const uint32_t x = b & 7u, k = b >> 3, q = nb >> 3, rem = nb & 7u;
     return x * q + min(x, rem) + k;
 }
+
+// Packed records between radix passes (bucket_device, when the key bits above the first pass's
+// digit fit 16 bits and the message index fits beside that digit in 32): A = (key's low b1 bits)
+// << ib | index, in the keys array, and B = key >> b1 as u16, in the values array.  6 B a record
+// instead of 8, and the later histograms read B alone (2 B).  in: this pass reads packed records;
+// out: it writes them (never the last pass, which writes the permutation and the starts).
+struct Pack {
+    uint32_t ib, b1;
+    bool in, out;
+};
 
 // Downsweep.  FIRST: values are the message indices themselves.  The keys are
 // clamped to `clamp` (unrouted messages -> trailing bucket).
@@ -914,7 +991,7 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
                                                       uint32_t* __restrict__ vals_out, uint32_t rank_atomic,
                                                       uint32_t* __restrict__ starts, uint32_t xcd,
                                                       uint32_t* __restrict__ rank_out,
-                                                      const uint32_t* __restrict__ totals) {
+                                                      const uint32_t* __restrict__ totals, Pack pk) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = NT / WAVE;
     constexpr uint32_t TILE = NT * IT;
@@ -945,8 +1022,21 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
         const uint32_t idx = base + (w * IT + r) * WAVE + lane;
         const uint32_t li = min(idx, n - 1);
         kk[r] = __builtin_nontemporal_load(keys_in + li);          // read once: stream past the caches
-        if constexpr (!FIRST) vv[r] = __builtin_nontemporal_load(vals_in + li);
+        if constexpr (!FIRST) {
+            if (pk.in) vv[r] = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(vals_in) + li);
+            else vv[r] = __builtin_nontemporal_load(vals_in + li);
+        }
     }
+    if constexpr (!FIRST)
+        if (pk.in) {                       // (A, B) -> (key, index)
+            const uint32_t imask = (1u << pk.ib) - 1u;
+#pragma unroll
+            for (int r = 0; r < IT; ++r) {
+                const uint32_t a = kk[r];
+                kk[r] = (vv[r] << pk.b1) | (a >> pk.ib);
+                vv[r] = a & imask;
+            }
+        }
     // totals != nullptr: k_radix_rowscan left gscan per digit row only, and the digit's base (the
     // exclusive prefix of the R row totals) is added below, in the tile-local digit scan; the
     // totals are loaded here, beside the keys
@@ -1063,10 +1153,14 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
             if (g < n) {            // always true when the scan is right; never write out of bounds
                 if (starts) {
                     if (p == s_lstart[d] || s_kv[p - 1].x != kv.x) atomicMin(&starts[kv.x], g);
+                    vals_out[g] = kv.y;
+                } else if (pk.out) {
+                    keys_out[g] = ((kv.x & ((1u << pk.b1) - 1u)) << pk.ib) | kv.y;
+                    reinterpret_cast<uint16_t*>(vals_out)[g] = (uint16_t)(kv.x >> pk.b1);
                 } else {
                     keys_out[g] = kv.x;
+                    vals_out[g] = kv.y;
                 }
-                vals_out[g] = kv.y;
                 if (rank_out) rank_out[kv.y] = g;     // the inverse permutation (last pass, on request)
             }
         }

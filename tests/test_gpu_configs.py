@@ -301,3 +301,38 @@ def test_bucket_hist_variants_unaligned(gd, monkeypatch, tpb, n, n_act):
         np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), wp, err_msg=f"shift {shift}")
         np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), wo)
     e.close()
+
+
+# ----------------------------------------------------------------------------- packed radix records
+@pytest.mark.parametrize("pack", ["0", "1"])
+@pytest.mark.parametrize("n,n_act,skew", [(70001, 1 << 20, False), (5_000_003, 1 << 20, True),
+                                          (1 << 24, 1 << 20, False), (3_000_001, (1 << 16) + 5, False),
+                                          (200_000, (1 << 23) + 3, True), (33_554_431, 1 << 20, False)])
+def test_bucket_packed_records(gd, monkeypatch, pack, n, n_act, skew):
+    """Records packed to 6 B between the radix passes (GD_RADIX_PACK, read at gd_create): index and
+    first digit in a u32, the higher key bits in a u16 that the later histograms read alone.  The
+    shapes cover the u16 histogram with 1 and 4 tiles per workgroup, ragged tails, a u16 holding all
+    16 bits (2^23 + 3 activations, 8-bit digits), an index and first digit filling all 32 bits
+    (2^25 - 1 messages, 7-bit digits), unrouted messages and a hot key; the same output with and
+    without packing, against the oracle."""
+    import torch
+    monkeypatch.setenv("GD_RADIX_PACK", pack)
+    rng = np.random.default_rng(n ^ n_act)
+    acts = rng.integers(0, n_act + n_act // 8 + 1, size=n).astype(np.uint32)
+    if skew:
+        acts[rng.random(n) < 0.3] = np.uint32(n_act // 3)
+    acts[rng.random(n) < 0.01] = o.M32
+    wp, wo = o.bucket_stable(acts, n_act)
+    e = gd.GrainDispatch(device=0, table_capacity=1024)
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.Stream(dev)
+    e.set_stream(stream.cuda_stream)
+    with torch.cuda.stream(stream):
+        a = torch.from_numpy(acts.view(np.int32)).to(dev)
+        perm = torch.empty(n, dtype=torch.int32, device=dev)
+        off = torch.empty(n_act + 2, dtype=torch.int32, device=dev)
+        e.bucket_device(a.data_ptr(), n, n_act, perm.data_ptr(), off.data_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), wp)
+    np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), wo)
+    e.close()
