@@ -22,25 +22,35 @@ def main():
         base = name.split("<")[0].replace("gd::", "")
         if "rd_bytes_ea" not in row or "wr_bytes_ea" not in row:
             continue
-        fam.setdefault(base, []).append((name, row))
-    out = {}
-    for base, members in fam.items():
-        if base not in ("k_route_m", "k_radix_scatter", "k_radix_hist", "k_radix_hist_multi", "k_route_hist"):
+        if base not in ("k_route_m", "k_radix_scatter", "k_radix_hist", "k_radix_hist_multi", "k_radix_hist16",
+                        "k_route_hist"):
             continue
-        rd_raw = sum(r["rd_bytes_ea"] for _, r in members) / len(members)
-        wr = sum(r["wr_bytes_ea"] for _, r in members) / len(members)
-        if base in ("k_route_m", "k_route_hist"):
+        key = "k_route" if base == "k_route_m" else ("k_radix_hist" if base.startswith("k_radix_hist") else base)
+        # launches per cfg 2 step (3 radix passes): the first pass's scatter (FIRST = true) and
+        # histogram (32-bit keys) once, the later passes' instantiations twice
+        w = 1.0
+        if key == "k_radix_scatter" and ", false," in name:
+            w = 2.0
+        if base == "k_radix_hist16":
+            w = 2.0
+        fam.setdefault(key, []).append((name, row, w))
+    out = {}
+    for key, members in fam.items():
+        wsum = sum(w for _, _, w in members)
+        rd_raw = sum(r["rd_bytes_ea"] * w for _, r, w in members) / wsum
+        wr = sum(r["wr_bytes_ea"] * w for _, r, w in members) / wsum
+        if key == "k_route" or key == "k_route_hist":
             rd = rd_raw + 24 * n / 2
             how = "random slot probes as issued (64-B requests) + the 24-B/message key stream added back at half"
         else:
             rd = 2 * rd_raw
             how = "streamed reads doubled (gfx950 tallies a wide coalesced read at half its bytes)"
-        key = "k_route" if base == "k_route_m" else ("k_radix_hist" if base.startswith("k_radix_hist") else base)
-        out[key] = {"kernel": key, "instantiations": [m for m, _ in members],
+        out[key] = {"kernel": key, "instantiations": [m for m, _, _ in members],
                     "hbm_bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                     "raw_read_bytes_per_launch": rd_raw, "source": tag,
                     "method": "EA request counts x request size, separate --pmc passes; " + how +
-                              "; averaged over the instantiations (one per radix pass kind)"}
+                              "; averaged over the instantiations weighted by their launches per cfg 2 step "
+                              "(first radix pass once, later passes twice)"}
     for key, v in out.items():
         with open(f"profiles/pmc_{key}.json", "w") as f:
             json.dump(v, f, indent=1)
