@@ -154,7 +154,8 @@ struct gd_handle {
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
     uint32_t hist_tpb = 0;      // tiles per workgroup in the radix histogram, 1/4/8 (GD_HIST_TPB);
                                 // 0 = by size: 4 for 1024..4096 tiles (4M..16M keys), else 1 (A/B)
-    bool compact_headers = true;   // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
+    bool compact_headers = true;
+    bool narrow_headers = true;     // compact headers as u32 N1s when every N1 < 2^32 (GD_NARROW_HEADERS=0: u64)   // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
     bool fused_starts = true;
     bool radix_pack = true;     // 6-B packed records between radix passes when they fit (GD_RADIX_PACK)
     bool radix_rowscan = true;  // one scan launch per radix pass, digit rows (GD_RADIX_ROWSCAN=0: reduce + down)
@@ -349,23 +350,28 @@ int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, u
                   n, ring_args(h), table_args(h), silo, act, status, 0ull);
 }
 
-// Keys given as N1 alone with one TypeCodeData (a compact exchange receive); not in cache mode.
-int route_n1_device(gd_handle* h, const uint64_t* n1s, uint64_t tcd, uint32_t n, uint32_t* silo, uint32_t* act,
-                    uint8_t* status) {
+// Keys given as N1 alone (u64, or u32 with n1w = 4) with one TypeCodeData (a compact exchange
+// receive); not in cache mode.
+template <int MODE>
+int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uint32_t n, uint32_t* silo,
+                  uint32_t* act, uint8_t* status) {
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    if (n1w == 4)
+        return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4>, k, n, ring_args(h), table_args(h),
+                      silo, act, status, tcd);
+    return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8>, k, n, ring_args(h), table_args(h),
+                  silo, act, status, tcd);
+}
+
+int route_n1_device(gd_handle* h, const void* n1s, uint32_t n1w, uint64_t tcd, uint32_t n, uint32_t* silo,
+                    uint32_t* act, uint8_t* status) {
     GD_TRY(check_ring(h));
     h->routed += n;
-    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
     const gd_key* k = reinterpret_cast<const gd_key*>(n1s);
     switch (h->ring_mode) {
-        case GD_RING_DIRECTORY:
-            return launch(h, "k_route", g, b, ring_lds(h), k_route_m<GD_RING_DIRECTORY, 1, false, true>, k, n,
-                          ring_args(h), table_args(h), silo, act, status, tcd);
-        case GD_RING_CONSISTENT:
-            return launch(h, "k_route", g, b, ring_lds(h), k_route_m<GD_RING_CONSISTENT, 1, false, true>, k, n,
-                          ring_args(h), table_args(h), silo, act, status, tcd);
-        default:
-            return launch(h, "k_route", g, b, ring_lds(h), k_route_m<GD_RING_VIRTUAL_BUCKETS, 1, false, true>, k, n,
-                          ring_args(h), table_args(h), silo, act, status, tcd);
+        case GD_RING_DIRECTORY: return route_n1_mode<GD_RING_DIRECTORY>(h, k, n1w, tcd, n, silo, act, status);
+        case GD_RING_CONSISTENT: return route_n1_mode<GD_RING_CONSISTENT>(h, k, n1w, tcd, n, silo, act, status);
+        default: return route_n1_mode<GD_RING_VIRTUAL_BUCKETS>(h, k, n1w, tcd, n, silo, act, status);
     }
 }
 
@@ -723,7 +729,9 @@ int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t
     GD_TRY(check_ring(h));
     if (kdesc) HIP_TRY(h, hipMemsetAsync(kdesc, 0, 16, h->stream));
     if (n == 0) {
-        if (kdesc) GD_TRY(launch(h, "k_key_desc", dim3(1), dim3(64), 0, k_key_desc, (const gd_key*)recs, n, kdesc));
+        if (kdesc)
+            GD_TRY(launch(h, "k_key_desc", dim3(1), dim3(64), 0, k_key_desc, (const gd_key*)recs, n, kdesc,
+                          h->narrow_headers ? 1u : 0u));
         return launch(h, "k_fill", dim3(1), dim3(BLOCK), 0, k_fill_u32, counts, n_shards, 0u);
     }
     const uint32_t tiles = blocks_for(n, SH_TILE);
@@ -744,7 +752,9 @@ int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t
         default:
             GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext, kdesc)));
     }
-    if (kdesc) GD_TRY(launch(h, "k_key_desc", dim3(1), dim3(64), 0, k_key_desc, (const gd_key*)recs, n, kdesc));
+    if (kdesc)
+        GD_TRY(launch(h, "k_key_desc", dim3(1), dim3(64), 0, k_key_desc, (const gd_key*)recs, n, kdesc,
+                      h->narrow_headers ? 1u : 0u));
     return shard_finish<NODES>(h, recs, payload, n, n_shards, bits, tiles, dest, hist, out_recs, out_pay, counts,
                                kdesc);
 }
@@ -898,6 +908,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_RANGE_SCAN")) h->range_scan = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_SHARD_GATHER")) h->shard_gather = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_COMPACT_HEADERS")) h->compact_headers = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_NARROW_HEADERS")) h->narrow_headers = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_HOST_CHUNK")) h->host_chunk = (uint32_t)std::strtoul(v, nullptr, 10);
     if (const char* v = std::getenv("GD_XCD_TILES")) h->xcd_tiles = std::atoi(v) ? 1u : 0u;
     if (const char* v = std::getenv("GD_HIST_TPB")) h->hist_tpb = (uint32_t)std::atoi(v);
@@ -2994,25 +3005,27 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         return set_err(h, GD_EINVAL, "%llu messages / %llu KeyExt bytes received: more than a batch can hold",
                        (unsigned long long)roff[W], (unsigned long long)rboff[W]);
     const uint32_t m = (uint32_t)roff[W];
-    // header bytes per peer: 8 (N1 only) when that side's batch is compact (k_key_desc), else 24
+    // header bytes per peer: 8 or 4 (N1 only) when that side's batch is compact (k_key_desc), else 24
     const uint32_t* hd = h->h_xcnt + 4 * W;        // my descriptor, then the peers'
-    const uint64_t my_esz = hd[0] ? 8 : 24;
+    const uint64_t my_esz = header_bytes(hd[0]);
     std::vector<uint64_t> hsb(W + 1, 0), hrb(W + 1, 0);
     bool any_compact = false;
     // every received chunk compact with one TypeCodeData: the probe reads the N1s as they arrive
     // (8 B a key instead of a 24-B rebuilt key); not with KeyExt strings or in cache mode
     bool n1_path = !has_ext && !h->cache_max && m > 0;
     uint64_t n1_tcd = 0;
+    uint32_t n1_mode = 0;                          // every received chunk in one compact mode (u64 / u32)
     bool n1_first = true;
     for (int r = 0; r < W; ++r) {
-        const bool c = hd[4 + 4 * r] != 0;
+        const uint32_t c = hd[4 + 4 * r];
         any_compact |= c && rc[r];
         hsb[r + 1] = hsb[r] + sc[r] * my_esz;
-        hrb[r + 1] = hrb[r] + rc[r] * (c ? 8 : 24);
+        hrb[r + 1] = hrb[r] + rc[r] * header_bytes(c);
         if (rc[r]) {
             const uint64_t t = (uint64_t)hd[4 + 4 * r + 2] | ((uint64_t)hd[4 + 4 * r + 3] << 32);
-            if (!c || (!n1_first && t != n1_tcd)) n1_path = false;
+            if (!c || (!n1_first && (t != n1_tcd || c != n1_mode))) n1_path = false;
             n1_tcd = t;
+            n1_mode = c;
             n1_first = false;
         }
     }
@@ -3077,7 +3090,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     }
     // 3. probe + bucket on the owner (the handle's stream)
     HIP_TRY(h, hipStreamWaitEvent(h->stream, h->x_hdr[s], 0));
-    if (n1_path) GD_TRY(route_n1_device(h, (const uint64_t*)B[18].p, n1_tcd, m, silo, act, st));
+    if (n1_path) GD_TRY(route_n1_device(h, B[18].p, header_bytes(n1_mode), n1_tcd, m, silo, act, st));
     else if (m) GD_TRY(route_device(h, recv_keys, m, silo, act, st));
     if (m && has_ext)                  // the received strings: KeyExt grains are routed on their owner
         GD_TRY(keyext_pass(h, recv_keys,

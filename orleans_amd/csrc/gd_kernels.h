@@ -247,10 +247,10 @@ __device__ __forceinline__ void st(T* p, T v) {
 // that each lane keeps M random 32-B slot reads in flight.  NT streams the key
 // reads and result writes non-temporally so they do not push the table out of
 // the caches it shares with them.
-// N1: the keys arrive as N1 alone (8 B each; N0 = 0, TypeCodeData = tcd_u for all), the form a
-// compact exchange header round delivers (k_key_desc, gd_shard.h).
+// N1W: 0 = 24-B keys; 8 / 4 = the keys arrive as N1 alone (u64 / u32 each; N0 = 0, TypeCodeData =
+// tcd_u for all), the forms a compact exchange header round delivers (k_key_desc, gd_shard.h).
 // The per-thread part: messages base + j * STRIDE, j < M; lds_act (optional) gets act too.
-template <int MODE, int M, int STRIDE, bool NT, bool N1, bool NT_SIDE = false>
+template <int MODE, int M, int STRIDE, bool NT, int N1W, bool NT_SIDE = false>
 __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, uint32_t n, uint32_t base,
                                              const RingArgs& ring, const uint32_t* s_pts, const uint32_t* s_own,
                                              const TableArgs& tab, uint32_t max_probe,
@@ -267,8 +267,11 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
         const uint32_t i = base + j * STRIDE;
         n0[j] = n1[j] = tcd[j] = 0;
         if (i < n) {
-            if constexpr (N1) {
+            if constexpr (N1W == 8) {
                 n1[j] = ld<NT>(reinterpret_cast<const uint64_t*>(keys) + i);
+                tcd[j] = tcd_u;
+            } else if constexpr (N1W == 4) {
+                n1[j] = ld<NT>(reinterpret_cast<const uint32_t*>(keys) + i);
                 tcd[j] = tcd_u;
             } else {
                 const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
@@ -382,7 +385,7 @@ __global__ void __launch_bounds__(MB_ROUTE_BLOCK) k_mb_route(const gd_key* __res
     stage_ring(ring, s_pts, s_own);
     mb_mark(ts, 1, t);
     // act goes to HBM for the sort and, from these 64 workgroups, to the host block as well
-    route_m_core<MODE, 1, MB_ROUTE_BLOCK, false, false>(keys, n, blockIdx.x * MB_ROUTE_BLOCK + threadIdx.x, ring,
+    route_m_core<MODE, 1, MB_ROUTE_BLOCK, false, 0>(keys, n, blockIdx.x * MB_ROUTE_BLOCK + threadIdx.x, ring,
                                                         s_pts, s_own, tab, tab.ctr->max_probe, out_silo, out_act,
                                                         out_status, 0, act_host, act_host ? 1u : 0u);
     mb_mark(ts, 2, t);
@@ -392,7 +395,7 @@ __global__ void __launch_bounds__(MB_ROUTE_BLOCK) k_mb_route(const gd_key* __res
     }
 }
 
-template <int MODE, int M, bool NT, bool N1 = false>
+template <int MODE, int M, bool NT, int N1W = 0>
 __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                    TableArgs tab, uint32_t* __restrict__ out_silo,
                                                    uint32_t* __restrict__ out_act,
@@ -401,7 +404,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
     stage_ring(ring, s_pts, s_own);
-    route_m_core<MODE, M, BLOCK, NT, N1, true>(keys, n, blockIdx.x * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own,
+    route_m_core<MODE, M, BLOCK, NT, N1W, true>(keys, n, blockIdx.x * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own,
                                                tab, tab.ctr->max_probe, out_silo, out_act, out_status, tcd_u, nullptr,
                                                0);
 }

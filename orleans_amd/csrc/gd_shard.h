@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
     uint64_t ref_tcd = 0;
     if constexpr (!NODES)
         if (kdesc && n) ref_tcd = reinterpret_cast<const uint64_t*>(recs)[2];
-    bool wide = false;
+    bool wide = false, big = false;
     // every record of the thread is loaded before the first hash (one wait, not one per record)
     constexpr int RW = NODES ? 1 : 3;
     uint64_t kv[SH_IT][RW];
@@ -109,6 +109,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
             } else {
                 d = key_dest<MODE>(kv[r][0], kv[r][1], kv[r][2], s_pts, s_own, ring, n_shards, ext, i);
                 wide |= kv[r][0] != 0 || kv[r][2] != ref_tcd;
+                big |= (kv[r][1] >> 32) != 0;
             }
             dest[i] = (uint8_t)d;
         }
@@ -121,7 +122,10 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
         if (valid && (peers & lt) == 0) s_wc[w][d] += (uint32_t)__popcll(peers);
     }
     if constexpr (!NODES)
-        if (kdesc && __ballot(wide) && lane == 0) atomicOr(&kdesc[1], 1u);
+        if (kdesc) {
+            const bool any_wide = __ballot(wide) != 0, any_big = __ballot(big) != 0;
+            if (lane == 0 && (any_wide || any_big)) atomicOr(&kdesc[1], (any_wide ? 1u : 0u) | (any_big ? 2u : 0u));
+        }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < n_shards; d += SH_NT) {
         uint32_t t = 0;
@@ -133,15 +137,22 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
 
 // Header compaction for the exchange (gd_route_multi*): a batch whose keys all have N0 == 0 and one
 // TypeCodeData -- long-keyed grains of one type (GrainId.GetGrainId(typeCode, long), GrainId.cs:
-// 72-77), the common case -- sends 8 B (N1) per header instead of 24.  kdesc = {compact, wide flag
-// (k_shard_hist), TCD lo, TCD hi}: the descriptor every peer receives with the counts.
-__global__ void k_key_desc(const gd_key* __restrict__ keys, uint32_t n, uint32_t* __restrict__ kdesc) {
+// 72-77), the common case -- sends N1 alone per header instead of 24 B: 4 B when every N1 is below
+// 2^32 (narrow_ok), else 8 B.  kdesc = {mode (0 full, 1 u64 N1, 2 u32 N1), flags from k_shard_hist
+// (bit 0 wide, bit 1 some N1 >= 2^32), TCD lo, TCD hi}: the descriptor every peer receives with the
+// counts.
+__global__ void k_key_desc(const gd_key* __restrict__ keys, uint32_t n, uint32_t* __restrict__ kdesc,
+                           uint32_t narrow_ok) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const uint64_t tcd = n ? reinterpret_cast<const uint64_t*>(keys)[2] : 0ull;
-    kdesc[0] = kdesc[1] == 0u ? 1u : 0u;
+    const uint32_t f = kdesc[1];
+    kdesc[0] = (f & 1u) ? 0u : ((narrow_ok && !(f & 2u)) ? 2u : 1u);
     kdesc[2] = (uint32_t)tcd;
     kdesc[3] = (uint32_t)(tcd >> 32);
 }
+
+// Header bytes of a chunk by its sender's descriptor mode.
+__host__ __device__ __forceinline__ uint32_t header_bytes(uint32_t mode) { return mode == 2 ? 4u : mode ? 8u : 24u; }
 
 // Receiver of a header round where some peer sent compact headers: raw = the peers' chunks back to
 // back (8 B or 24 B per header by each peer's descriptor); rebuild the 24-B keys and the sender
@@ -165,7 +176,7 @@ __global__ void __launch_bounds__(BLOCK) k_recv_expand(const uint8_t* __restrict
             s_compact[r] = c;
             s_tcd[r] = (uint64_t)rdesc[4 * r + 2] | ((uint64_t)rdesc[4 * r + 3] << 32);
             run += rcount[r];
-            brun += (uint64_t)rcount[r] * (c ? 8u : 24u);
+            brun += (uint64_t)rcount[r] * header_bytes(c);
         }
         s_off[world] = run;
     }
@@ -181,7 +192,8 @@ __global__ void __launch_bounds__(BLOCK) k_recv_expand(const uint8_t* __restrict
     const uint64_t j = i - s_off[lo];
     uint64_t* out = reinterpret_cast<uint64_t*>(keys + i);
     if (s_compact[lo]) {
-        const uint64_t n1 = reinterpret_cast<const uint64_t*>(raw + s_boff[lo])[j];
+        const uint64_t n1 = s_compact[lo] == 2 ? (uint64_t)reinterpret_cast<const uint32_t*>(raw + s_boff[lo])[j]
+                                               : reinterpret_cast<const uint64_t*>(raw + s_boff[lo])[j];
         out[0] = 0;
         out[1] = n1;
         out[2] = s_tcd[lo];
@@ -373,7 +385,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict_
         }
     }
     __syncthreads();
-    const bool compact = !NODES && kdesc && kdesc[0];   // headers as N1 only (k_key_desc)
+    const uint32_t compact = !NODES && kdesc ? kdesc[0] : 0u;   // headers as N1 only (k_key_desc)
 #pragma unroll
     for (int j = 0; j < SH_IT; ++j) {
         const uint32_t p = j * SH_NT + threadIdx.x;
@@ -383,6 +395,8 @@ __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict_
             if (g < n) {            // always true when the scan is right; never write out of bounds
                 if constexpr (NODES) {
                     reinterpret_cast<uint32_t*>(out_recs)[g] = s_node[p];
+                } else if (compact == 2) {
+                    reinterpret_cast<uint32_t*>(out_recs)[g] = (uint32_t)s_key[1][p];
                 } else if (compact) {
                     reinterpret_cast<uint64_t*>(out_recs)[g] = s_key[1][p];
                 } else {
@@ -496,7 +510,9 @@ __global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict
     __syncthreads();
     const uint64_t* k64 = reinterpret_cast<const uint64_t*>(recs);
     uint64_t* o64 = reinterpret_cast<uint64_t*>(out_recs);
-    // one 8-B N1 and the payload per output slot; every gather of the thread before the stores
+    uint32_t* o32 = reinterpret_cast<uint32_t*>(out_recs);
+    const bool narrow = kdesc[0] == 2;          // every N1 below 2^32: 4 B a header
+    // one N1 (8 or 4 B) and the payload per output slot; every gather of the thread before the stores
     uint64_t kv[SH_IT];
     uint32_t pay[SH_IT], gg[SH_IT];
 #pragma unroll
@@ -514,7 +530,8 @@ __global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict
 #pragma unroll
     for (int j = 0; j < SH_IT; ++j)
         if (gg[j] < n) {            // ~0: no record here; else always in bounds when the scan is right
-            o64[gg[j]] = kv[j];
+            if (narrow) o32[gg[j]] = (uint32_t)kv[j];
+            else o64[gg[j]] = kv[j];
             out_payload[gg[j]] = pay[j];
         }
 }

@@ -680,18 +680,20 @@ def test_route_multi_ext_local_world(gd):
         e.close()
 
 
-@pytest.mark.parametrize("compact", ["1", "0"])
-def test_route_multi_local_mixed_headers(gd, compact, monkeypatch):
-    """Exchange header compaction: a batch of one grain type with long keys travels as 8-B N1s
-    (k_key_desc / k_recv_expand).  Ranks here send: one type (compact), another type (compact,
-    other TCD), guid grains mixed in (full 24-B headers), nothing at all; with compaction off
+@pytest.mark.parametrize("compact,narrow", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_route_multi_local_mixed_headers(gd, compact, narrow, monkeypatch):
+    """Exchange header compaction: a batch of one grain type with long keys travels as N1s alone
+    (k_key_desc / k_recv_expand), 4 B each when every N1 is below 2^32 (GD_NARROW_HEADERS), else 8.
+    Ranks here send: one type with small keys (u32 N1s), another type with keys above 2^32 (u64
+    N1s, other TCD), guid grains mixed in (full 24-B headers), nothing at all; with compaction off
     (GD_COMPACT_HEADERS=0) everything goes as 24 B.  The results are identical either way."""
     monkeypatch.setenv("GD_COMPACT_HEADERS", compact)
+    monkeypatch.setenv("GD_NARROW_HEADERS", narrow)
     W = 4
     silos = o.bench_silos(8)
     tc2 = o.grain_type_code("UnitTests.Grains.SimpleGrain")
     ka = o.grain_keys(TC, np.arange(3000))
-    kb = o.grain_keys(tc2, np.arange(2000))
+    kb = o.grain_keys(tc2, np.arange(2000) + (1 << 33) + 12345)
     kg = np.array([o.guid_key(f"0d2b3e5a-1111-4c3b-9f4e-aa{i:010d}", o.CAT_GRAIN, TC).as_tuple() for i in range(300)],
                   np.uint64)
     reg = np.concatenate([ka, kb, kg])
@@ -703,7 +705,8 @@ def test_route_multi_local_mixed_headers(gd, compact, monkeypatch):
     spec, own, es = _local_world(gd, W, "D", silos, reg, act, own)
     rng = np.random.default_rng(8)
     batches = [ka[rng.integers(0, 3000, size=25000)],
-               np.concatenate([kb, o.grain_keys(tc2, np.arange(5000, 5100))])[rng.integers(0, 2100, size=17000)],
+               np.concatenate([kb, o.grain_keys(tc2, np.arange(5000, 5100) + (1 << 33))])[rng.integers(0, 2100,
+                                                                                                size=17000)],
                reg[rng.integers(0, len(reg), size=21000)],
                np.zeros((0, 3), np.uint64)]
     n_act = [int((own % W == r).sum()) for r in range(W)]
@@ -732,15 +735,17 @@ def test_route_multi_local_mixed_headers(gd, compact, monkeypatch):
         e.close()
 
 
-@pytest.mark.parametrize("two_types", [False, True])
-def test_route_multi_local_no_keys(gd, two_types):
+@pytest.mark.parametrize("two_types,big", [(False, False), (True, False), (False, True), (False, "all")])
+def test_route_multi_local_no_keys(gd, two_types, big):
     """GD_MULTI_NO_KEYS at W = 3: with one grain type everywhere the probe reads the compact N1s
-    as received (route_n1_device); with two types the keys are rebuilt first.  Results other than
-    recv_keys (left unset) are the same either way."""
+    as received (route_n1_device: u32 N1s, or u64 when every sender has a key above 2^32); with two
+    types, or u32 and u64 chunks mixed (one sender with big keys), the keys are rebuilt first.
+    Results other than recv_keys (left unset) are the same either way."""
     W, G = 3, 4000
     silos = o.bench_silos(8)
     tc2 = o.grain_type_code("UnitTests.Grains.SimpleGrain")
-    reg = np.concatenate([o.grain_keys(TC, np.arange(G)), o.grain_keys(tc2, np.arange(G))])
+    reg = np.concatenate([o.grain_keys(TC, np.arange(G)), o.grain_keys(tc2, np.arange(G)),
+                          o.grain_keys(TC, np.arange(G) + (1 << 32))])
     spec = o.ring_spec(silos, "D")
     own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
     act = np.zeros(len(reg), np.uint32)
@@ -750,6 +755,9 @@ def test_route_multi_local_no_keys(gd, two_types):
     rng = np.random.default_rng(12)
     batches = [o.grain_keys(tc2 if (two_types and r == 1) else TC, rng.integers(0, G + 300, size=30000 + r))
                for r in range(W)]
+    for r in range(W):
+        if big == "all" or (big and r == 1):      # some keys above 2^32: that sender's N1s go as u64
+            batches[r][::3, 1] += np.uint64(1 << 32)
     n_act = [int((own % W == r).sum()) for r in range(W)]
     res = _run_ranks([lambda r=r: es[r].route_multi(batches[r], n_act[r], no_keys=True) for r in range(W)])
     full = o.DirectoryArrays(reg, act, own)
