@@ -361,9 +361,10 @@ typedef struct gd_multi_result {
  *        owner). */
 #define GD_MULTI_FORWARD       4
 /* GD_MULTI_NO_KEYS -- the result's recv_keys stay unset (NULL): the receiver identifies each
- *        message by (recv_src, recv_idx).  When every received header was compact (8-B N1, one
- *        TypeCodeData: the batches of every sender held long-keyed grains of one type) the probe
- *        reads the N1s directly and the 24-B keys are never rebuilt.  Ignored with
+ *        message by (recv_src, recv_idx).  When every received header was compact in one form
+ *        (N1 alone, 4 B when all of a sender's N1s are below 2^32, else 8 B; one TypeCodeData: the
+ *        batches of every sender held long-keyed grains of one type) the probe reads the N1s
+ *        directly and the 24-B keys are never rebuilt.  Ignored with
  *        GD_MULTI_FORWARD (the keys move on). */
 #define GD_MULTI_NO_KEYS       8
 int gd_route_multi_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, int flags,
