@@ -191,17 +191,18 @@ __global__ void __launch_bounds__(BLOCK) k_recv_expand(const uint8_t* __restrict
     }
     const uint64_t j = i - s_off[lo];
     uint64_t* out = reinterpret_cast<uint64_t*>(keys + i);
+    // a chunk starts 4-B aligned only (a u32 chunk of odd length before it): read in u32 words
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(raw + s_boff[lo]);
+    auto u64_at = [&](uint64_t w) { return (uint64_t)cw[w] | ((uint64_t)cw[w + 1] << 32); };
     if (s_compact[lo]) {
-        const uint64_t n1 = s_compact[lo] == 2 ? (uint64_t)reinterpret_cast<const uint32_t*>(raw + s_boff[lo])[j]
-                                               : reinterpret_cast<const uint64_t*>(raw + s_boff[lo])[j];
+        const uint64_t n1 = s_compact[lo] == 2 ? (uint64_t)cw[j] : u64_at(2 * j);
         out[0] = 0;
         out[1] = n1;
         out[2] = s_tcd[lo];
     } else {
-        const uint64_t* kp = reinterpret_cast<const uint64_t*>(raw + s_boff[lo]) + 3 * j;
-        out[0] = kp[0];
-        out[1] = kp[1];
-        out[2] = kp[2];
+        out[0] = u64_at(6 * j);
+        out[1] = u64_at(6 * j + 2);
+        out[2] = u64_at(6 * j + 4);
     }
     src[i] = lo;
 }
