@@ -84,6 +84,8 @@ struct gd_handle {
     DevBuf cache_local, cache_valid;
     DevBuf cbuf[8];                   // cache scratch
     DevBuf shard_dest, shard_hist;    // exchange partition scratch
+    DevBuf shard_n1;                  // low N1 words of the batch (k_shard_hist -> k_shard_gather, compact u32)
+    bool shard_n1_copy = true;        // GD_SHARD_N1=0: the gather reads N1 from the 24-B keys
     DevBuf up_last;                   // gd_dir_upsert: last batch item per table slot (zero between calls)
 
     // IsValidSilo (gd_dir_set_valid_silos): bitset over silo indices [0, n_valid); VersionTag and
@@ -693,8 +695,9 @@ int maybe_grow_table(gd_handle* h, uint64_t incoming) {
 template <int MODE, bool NODES>
 int shard_hist_t(gd_handle* h, const void* recs, uint32_t n, uint64_t tcd, uint32_t n_shards, uint32_t bits,
                  uint32_t tiles, uint8_t* dest, uint32_t* hist, const ExtArgs& ext, uint32_t* kdesc) {
+    uint32_t* n1lo = !NODES && kdesc && h->shard_n1_copy ? (uint32_t*)h->shard_n1.p : nullptr;
     return launch(h, "k_shard_hist", dim3(tiles), dim3(SH_NT), ring_lds(h), k_shard_hist<MODE, NODES>, recs, n, tcd,
-                  ring_args(h), n_shards, bits, tiles, dest, hist, ext, kdesc);
+                  ring_args(h), n_shards, bits, tiles, dest, hist, ext, kdesc, n1lo);
 }
 
 template <int BITS, bool NODES>
@@ -706,7 +709,8 @@ int shard_scatter_t(gd_handle* h, const void* recs, const uint32_t* payload, con
     if constexpr (!NODES)
         if (h->shard_gather && kdesc) {
             GD_TRY(launch(h, "k_shard_scatter", dim3(tiles), dim3(SH_NT), 0, k_shard_gather<BITS>,
-                          (const gd_key*)recs, payload, dest, n, n_shards, tiles, gscan, out, out_pay, kdesc));
+                          (const gd_key*)recs, payload, dest, n, n_shards, tiles, gscan, out, out_pay, kdesc,
+                          h->shard_n1_copy ? (const uint32_t*)h->shard_n1.p : nullptr));
             return launch(h, "k_shard_scatter", dim3(tiles), dim3(SH_NT), 0, k_shard_scatter<BITS, false, true>, recs,
                           payload, dest, n, n_shards, tiles, gscan, out, out_pay, kdesc);
         }
@@ -738,6 +742,7 @@ int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t
     if ((uint64_t)tiles * n_shards > 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "batch too large to partition");
     GD_TRY(ensure(h, h->shard_dest, (size_t)n));
     GD_TRY(ensure(h, h->shard_hist, (size_t)tiles * n_shards * 4));
+    if (!NODES && kdesc) GD_TRY(ensure(h, h->shard_n1, (size_t)n * 4));
     uint8_t* dest = (uint8_t*)h->shard_dest.p;
     uint32_t* hist = (uint32_t*)h->shard_hist.p;
     uint32_t bits = 1;
@@ -909,6 +914,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_SHARD_GATHER")) h->shard_gather = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_COMPACT_HEADERS")) h->compact_headers = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_NARROW_HEADERS")) h->narrow_headers = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_SHARD_N1")) h->shard_n1_copy = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_HOST_CHUNK")) h->host_chunk = (uint32_t)std::strtoul(v, nullptr, 10);
     if (const char* v = std::getenv("GD_XCD_TILES")) h->xcd_tiles = std::atoi(v) ? 1u : 0u;
     if (const char* v = std::getenv("GD_HIST_TPB")) h->hist_tpb = (uint32_t)std::atoi(v);

@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
                                                       RingArgs ring, uint32_t n_shards, uint32_t bits,
                                                       uint32_t tiles, uint8_t* __restrict__ dest,
                                                       uint32_t* __restrict__ hist, ExtArgs ext,
-                                                      uint32_t* __restrict__ kdesc) {
+                                                      uint32_t* __restrict__ kdesc, uint32_t* __restrict__ n1lo) {
     constexpr int NW = SH_NT / WAVE;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     __shared__ uint32_t s_wc[NW][256];
@@ -110,6 +110,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
                 d = key_dest<MODE>(kv[r][0], kv[r][1], kv[r][2], s_pts, s_own, ring, n_shards, ext, i);
                 wide |= kv[r][0] != 0 || kv[r][2] != ref_tcd;
                 big |= (kv[r][1] >> 32) != 0;
+                if (n1lo) n1lo[i] = (uint32_t)kv[r][1];   // the gather's 4-B header source (mode 2)
             }
             dest[i] = (uint8_t)d;
         }
@@ -428,7 +429,8 @@ __global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict
                                                         const uint32_t* __restrict__ gscan,
                                                         void* __restrict__ out_recs,
                                                         uint32_t* __restrict__ out_payload,
-                                                        const uint32_t* __restrict__ kdesc) {
+                                                        const uint32_t* __restrict__ kdesc,
+                                                        const uint32_t* __restrict__ n1lo) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = SH_NT / WAVE;
     if (!kdesc[0]) return;                      // not compact: k_shard_scatter's case
@@ -524,7 +526,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict
             const uint32_t i = base + s_src[p];
             const uint32_t d = s_dig[p];
             gg[j] = s_gbase[d] + (p - s_lstart[d]);
-            kv[j] = k64[3ull * i + 1];
+            kv[j] = narrow && n1lo ? (uint64_t)n1lo[i] : k64[3ull * i + 1];   // 4 B (k_shard_hist's copy) or the key's N1
             pay[j] = payload_in ? payload_in[i] : i;
         }
     }
