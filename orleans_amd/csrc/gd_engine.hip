@@ -757,9 +757,6 @@ int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t
         default:
             GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext, kdesc)));
     }
-    if (kdesc)
-        GD_TRY(launch(h, "k_key_desc", dim3(1), dim3(64), 0, k_key_desc, (const gd_key*)recs, n, kdesc,
-                      h->narrow_headers ? 1u : 0u));
     return shard_finish<NODES>(h, recs, payload, n, n_shards, bits, tiles, dest, hist, out_recs, out_pay, counts,
                                kdesc);
 }
@@ -788,8 +785,10 @@ int shard_finish(gd_handle* h, const void* recs, const uint32_t* payload, uint32
                  uint32_t tiles, const uint8_t* dest, uint32_t* hist, void* out_recs, uint32_t* out_pay,
                  uint32_t* counts, const uint32_t* kdesc) {
     GD_TRY(scan_device<OpAdd>(h, hist, tiles * n_shards, false, false, "shard"));
+    // k_shard_counts also completes the compaction descriptor (kdesc, keys only)
     GD_TRY(launch(h, "k_shard_counts", dim3(1), dim3(256), 0, k_shard_counts, (const uint32_t*)hist, tiles, n_shards, n,
-                  counts));
+                  counts, NODES ? nullptr : (const gd_key*)recs, NODES ? nullptr : const_cast<uint32_t*>(kdesc),
+                  h->narrow_headers ? 1u : 0u));
     const uint32_t* gs = hist;
     switch (bits) {
         case 1: return shard_scatter_t<1, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay,

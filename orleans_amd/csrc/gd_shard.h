@@ -540,9 +540,19 @@ __global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict
 }
 
 // counts[d] = records for destination d, from the scanned (dest, tile) bases.
+// kdesc != nullptr: thread 0 also completes the header-compaction descriptor (k_key_desc's work;
+// k_shard_hist's flags are final by now), one launch fewer on the partition stream.
 __global__ void k_shard_counts(const uint32_t* __restrict__ gscan, uint32_t tiles, uint32_t n_shards, uint32_t n,
-                               uint32_t* __restrict__ counts) {
+                               uint32_t* __restrict__ counts, const gd_key* __restrict__ keys,
+                               uint32_t* __restrict__ kdesc, uint32_t narrow_ok) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (kdesc && d == 0) {
+        const uint64_t tcd = n ? reinterpret_cast<const uint64_t*>(keys)[2] : 0ull;
+        const uint32_t f = kdesc[1];
+        kdesc[0] = (f & 1u) ? 0u : ((narrow_ok && !(f & 2u)) ? 2u : 1u);
+        kdesc[2] = (uint32_t)tcd;
+        kdesc[3] = (uint32_t)(tcd >> 32);
+    }
     if (d >= n_shards) return;
     const uint32_t start = gscan[d * tiles];
     const uint32_t end = d + 1 < n_shards ? gscan[(d + 1) * tiles] : n;
