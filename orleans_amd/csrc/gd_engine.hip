@@ -628,10 +628,10 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
     if (!h->fused_starts)
         GD_TRY(launch(h, "k_bucket_starts", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_bucket_starts, kin, n,
                       offsets));
-    // the last pass's digit spans <= RS_RANGE activations: one workgroup per digit range, carried by
-    // the pass's digit bases (GD_RANGE_SCAN=0: the device-wide scan)
+    // the last pass's digit spans <= RS_RANGE * RS_MAX_SUB activations: one workgroup per digit
+    // range, carried by the pass's digit bases (GD_RANGE_SCAN=0: the device-wide scan)
     const uint32_t last_shift = (passes - 1) * bits;
-    if (h->range_scan && h->last_totals && last_shift < 32 && (1u << last_shift) <= RS_RANGE)
+    if (h->range_scan && h->last_totals && last_shift < 32 && (1u << last_shift) <= RS_RANGE * RS_MAX_SUB)
         return launch(h, "k_starts_rangescan", dim3((n_act >> last_shift) + 1), dim3(RS_THREADS), 0, k_starts_rangescan,
                       offsets, n_act + 1, last_shift, h->last_totals, h->last_digits);
     return scan_device<OpMin>(h, offsets, n_act + 1, true, true, "offsets");

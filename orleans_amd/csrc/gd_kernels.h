@@ -1400,77 +1400,92 @@ __global__ void __launch_bounds__(BLOCK) k_radix_rowscan(uint32_t* __restrict__ 
 }
 
 // The bucket starts' reverse inclusive min-scan in one launch, when the last radix pass's digit
-// covers at most RS_RANGE activations (1 << shift): workgroup d scans the activations
-// [d << shift, (d + 1) << shift) of offsets[0, n_scan) alone.  Its carry -- the first start past
-// the range -- is the last pass's digit base base(d + 1) = the number of messages whose (clamped)
-// key lies below the range's end (n when there is none): the starts of non-empty activations
-// increase with the activation, and the empty ones hold n.
+// covers at most RS_RANGE * RS_MAX_SUB activations (1 << shift): workgroup d scans the activations
+// [d << shift, (d + 1) << shift) of offsets[0, n_scan) alone, RS_RANGE at a time from the top.  Its
+// carry -- the first start past the range -- is the last pass's digit base base(d + 1) = the
+// number of messages whose (clamped) key lies below the range's end (n when there is none): the
+// starts of non-empty activations increase with the activation, and the empty ones hold n.  Each
+// lower sub-range then carries the minimum of the ones above it.
 constexpr uint32_t RS_THREADS = 1024;
 constexpr uint32_t RS_IPT = 16;
-constexpr uint32_t RS_RANGE = RS_THREADS * RS_IPT;      // 16,384 activations per workgroup
+constexpr uint32_t RS_RANGE = RS_THREADS * RS_IPT;      // 16,384 activations per sub-range
+constexpr uint32_t RS_MAX_SUB = 16;                      // digit ranges up to 2^18 activations
 __global__ void __launch_bounds__(RS_THREADS) k_starts_rangescan(uint32_t* __restrict__ offsets, uint32_t n_scan,
                                                                  uint32_t shift, const uint32_t* __restrict__ totals,
                                                                  uint32_t n_digits) {
     constexpr uint32_t NW = RS_THREADS / WAVE;
     __shared__ uint32_t s_w[2][NW];
     const uint32_t d = blockIdx.x;
-    const uint32_t lo = d << shift;
-    const uint32_t hi = min(lo + (1u << shift), n_scan);
-    // thread t takes chunk c = RS_THREADS - 1 - t, so a forward exclusive scan over the threads is
-    // the minimum over the chunks after c; the loads go out first
-    const uint32_t c = RS_THREADS - 1 - threadIdx.x;
-    const uint32_t p0 = lo + c * RS_IPT;
-    uint32_t v[RS_IPT];
-    const bool vec = p0 + RS_IPT <= hi && (reinterpret_cast<uintptr_t>(offsets + p0) & 15u) == 0;
-    if (vec) {
-#pragma unroll
-        for (uint32_t q = 0; q < RS_IPT / 4; ++q) {
-            const uint4 u = *reinterpret_cast<const uint4*>(offsets + p0 + 4 * q);
-            v[4 * q] = u.x; v[4 * q + 1] = u.y; v[4 * q + 2] = u.z; v[4 * q + 3] = u.w;
-        }
-    } else {
-#pragma unroll
-        for (uint32_t k = 0; k < RS_IPT; ++k) v[k] = p0 + k < hi ? offsets[min(p0 + k, n_scan - 1)] : 0xFFFFFFFFu;
-    }
-    uint32_t part = 0;                                   // this thread's share of base(d + 1)
-    for (uint32_t j = threadIdx.x; j <= d && j < n_digits; j += RS_THREADS) part += totals[j];
-    uint32_t m = 0xFFFFFFFFu;
-#pragma unroll
-    for (uint32_t k = 0; k < RS_IPT; ++k) m = min(m, v[k]);
-    // one pass over the waves: the digit base's sum and the exclusive min-scan of the chunk minima
+    const uint64_t lo64 = (uint64_t)d << shift;
+    if (lo64 >= n_scan) return;                          // workgroup-uniform: an empty top range
+    const uint32_t lo = (uint32_t)lo64;
+    const uint32_t hi = (uint32_t)min<uint64_t>(lo64 + (1ull << shift), n_scan);
     const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
-    uint32_t x = m;
+    // base(d + 1), the carry into the range's top
+    uint32_t part = 0;
+    for (uint32_t j = threadIdx.x; j <= d && j < n_digits; j += RS_THREADS) part += totals[j];
 #pragma unroll
-    for (int off = 1; off < WAVE; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off, WAVE);
-        if (lane >= (uint32_t)off) x = min(x, y);
-        part += __shfl_xor(part, off, WAVE);
-    }
-    uint32_t ex = __shfl_up(x, 1, WAVE);
-    if (lane == 0) ex = 0xFFFFFFFFu;
-    if (lane == WAVE - 1) s_w[0][w] = x;
+    for (int off = 1; off < WAVE; off <<= 1) part += __shfl_xor(part, off, WAVE);
     if (lane == 0) s_w[1][w] = part;
     __syncthreads();
-    uint32_t carry = 0, wmin = 0xFFFFFFFFu;
+    uint32_t carry = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < NW; ++k) {
-        carry += s_w[1][k];
-        if (k < w) wmin = min(wmin, s_w[0][k]);
-    }
-    uint32_t run = min(carry, min(wmin, ex));
+    for (uint32_t k = 0; k < NW; ++k) carry += s_w[1][k];
+    // thread t takes chunk c = RS_THREADS - 1 - t of a sub-range, so a forward exclusive scan over
+    // the threads is the minimum over the chunks above c; the loads go out first
+    const uint32_t c = RS_THREADS - 1 - threadIdx.x;
+    const uint32_t n_sub = (hi - lo + RS_RANGE - 1) / RS_RANGE;
+    for (uint32_t sub = n_sub; sub-- > 0;) {
+        const uint32_t p0 = lo + sub * RS_RANGE + c * RS_IPT;
+        uint32_t v[RS_IPT];
+        const bool vec = p0 + RS_IPT <= hi && (reinterpret_cast<uintptr_t>(offsets + p0) & 15u) == 0;
+        if (vec) {
 #pragma unroll
-    for (int k = RS_IPT - 1; k >= 0; --k) {
-        run = min(run, v[k]);
-        v[k] = run;
-    }
-    if (vec) {
+            for (uint32_t q = 0; q < RS_IPT / 4; ++q) {
+                const uint4 u = *reinterpret_cast<const uint4*>(offsets + p0 + 4 * q);
+                v[4 * q] = u.x; v[4 * q + 1] = u.y; v[4 * q + 2] = u.z; v[4 * q + 3] = u.w;
+            }
+        } else {
 #pragma unroll
-        for (uint32_t q = 0; q < RS_IPT / 4; ++q)
-            *reinterpret_cast<uint4*>(offsets + p0 + 4 * q) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-    } else {
+            for (uint32_t k = 0; k < RS_IPT; ++k) v[k] = p0 + k < hi ? offsets[min(p0 + k, n_scan - 1)] : 0xFFFFFFFFu;
+        }
+        uint32_t m = 0xFFFFFFFFu;
 #pragma unroll
-        for (uint32_t k = 0; k < RS_IPT; ++k)
-            if (p0 + k < hi) offsets[p0 + k] = v[k];
+        for (uint32_t k = 0; k < RS_IPT; ++k) m = min(m, v[k]);
+        uint32_t x = m;
+#pragma unroll
+        for (int off = 1; off < WAVE; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off, WAVE);
+            if (lane >= (uint32_t)off) x = min(x, y);
+        }
+        uint32_t ex = __shfl_up(x, 1, WAVE);
+        if (lane == 0) ex = 0xFFFFFFFFu;
+        if (lane == WAVE - 1) s_w[0][w] = x;
+        __syncthreads();
+        uint32_t wmin = 0xFFFFFFFFu, bmin = 0xFFFFFFFFu;
+#pragma unroll
+        for (uint32_t k = 0; k < NW; ++k) {
+            const uint32_t t = s_w[0][k];
+            if (k < w) wmin = min(wmin, t);
+            bmin = min(bmin, t);
+        }
+        uint32_t run = min(carry, min(wmin, ex));
+#pragma unroll
+        for (int k = RS_IPT - 1; k >= 0; --k) {
+            run = min(run, v[k]);
+            v[k] = run;
+        }
+        if (vec) {
+#pragma unroll
+            for (uint32_t q = 0; q < RS_IPT / 4; ++q)
+                *reinterpret_cast<uint4*>(offsets + p0 + 4 * q) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < RS_IPT; ++k)
+                if (p0 + k < hi) offsets[p0 + k] = v[k];
+        }
+        carry = min(carry, bmin);
+        __syncthreads();                                 // s_w[0] is rewritten by the next sub-range
     }
 }
 

@@ -307,14 +307,16 @@ def test_bucket_hist_variants_unaligned(gd, monkeypatch, tpb, n, n_act):
 @pytest.mark.parametrize("pack", ["0", "1"])
 @pytest.mark.parametrize("n,n_act,skew", [(70001, 1 << 20, False), (5_000_003, 1 << 20, True),
                                           (1 << 24, 1 << 20, False), (3_000_001, (1 << 16) + 5, False),
-                                          (200_000, (1 << 23) + 3, True), (33_554_431, 1 << 20, False)])
+                                          (200_000, (1 << 23) + 3, True), (33_554_431, 1 << 20, False),
+                                          (300_001, (1 << 24) - 5, False)])
 def test_bucket_packed_records(gd, monkeypatch, pack, n, n_act, skew):
     """Records packed to 6 B between the radix passes (GD_RADIX_PACK, read at gd_create): index and
     first digit in a u32, the higher key bits in a u16 that the later histograms read alone.  The
     shapes cover the u16 histogram with 1 and 4 tiles per workgroup, ragged tails, a u16 holding all
     16 bits (2^23 + 3 activations, 8-bit digits), an index and first digit filling all 32 bits
     (2^25 - 1 messages, 7-bit digits), unrouted messages and a hot key; the same output with and
-    without packing, against the oracle."""
+    without packing, against the oracle.  The 8-bit shapes end in 2^16-activation digit ranges that
+    the one-launch range scan covers in 4 sub-ranges (most of them empty at 2^24 - 5)."""
     import torch
     monkeypatch.setenv("GD_RADIX_PACK", pack)
     rng = np.random.default_rng(n ^ n_act)
