@@ -1421,6 +1421,26 @@ __global__ void __launch_bounds__(RS_THREADS) k_starts_rangescan(uint32_t* __res
     const uint32_t lo = (uint32_t)lo64;
     const uint32_t hi = (uint32_t)min<uint64_t>(lo64 + (1ull << shift), n_scan);
     const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    // thread t takes chunk c = RS_THREADS - 1 - t of a sub-range, so a forward exclusive scan over
+    // the threads is the minimum over the chunks above c.  The next sub-range's loads go out before
+    // the current one is scanned (the top one's before the carry is summed).
+    const uint32_t c = RS_THREADS - 1 - threadIdx.x;
+    const uint32_t n_sub = (hi - lo + RS_RANGE - 1) / RS_RANGE;
+    auto load = [&](uint32_t sub, uint32_t (&v)[RS_IPT]) {
+        const uint32_t p0 = lo + sub * RS_RANGE + c * RS_IPT;
+        if (p0 + RS_IPT <= hi && (reinterpret_cast<uintptr_t>(offsets + p0) & 15u) == 0) {
+#pragma unroll
+            for (uint32_t q = 0; q < RS_IPT / 4; ++q) {
+                const uint4 u = *reinterpret_cast<const uint4*>(offsets + p0 + 4 * q);
+                v[4 * q] = u.x; v[4 * q + 1] = u.y; v[4 * q + 2] = u.z; v[4 * q + 3] = u.w;
+            }
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < RS_IPT; ++k) v[k] = p0 + k < hi ? offsets[min(p0 + k, n_scan - 1)] : 0xFFFFFFFFu;
+        }
+    };
+    uint32_t v[RS_IPT], nx[RS_IPT];
+    load(n_sub - 1, v);
     // base(d + 1), the carry into the range's top
     uint32_t part = 0;
     for (uint32_t j = threadIdx.x; j <= d && j < n_digits; j += RS_THREADS) part += totals[j];
@@ -1431,24 +1451,10 @@ __global__ void __launch_bounds__(RS_THREADS) k_starts_rangescan(uint32_t* __res
     uint32_t carry = 0;
 #pragma unroll
     for (uint32_t k = 0; k < NW; ++k) carry += s_w[1][k];
-    // thread t takes chunk c = RS_THREADS - 1 - t of a sub-range, so a forward exclusive scan over
-    // the threads is the minimum over the chunks above c; the loads go out first
-    const uint32_t c = RS_THREADS - 1 - threadIdx.x;
-    const uint32_t n_sub = (hi - lo + RS_RANGE - 1) / RS_RANGE;
     for (uint32_t sub = n_sub; sub-- > 0;) {
+        if (sub > 0) load(sub - 1, nx);
         const uint32_t p0 = lo + sub * RS_RANGE + c * RS_IPT;
-        uint32_t v[RS_IPT];
         const bool vec = p0 + RS_IPT <= hi && (reinterpret_cast<uintptr_t>(offsets + p0) & 15u) == 0;
-        if (vec) {
-#pragma unroll
-            for (uint32_t q = 0; q < RS_IPT / 4; ++q) {
-                const uint4 u = *reinterpret_cast<const uint4*>(offsets + p0 + 4 * q);
-                v[4 * q] = u.x; v[4 * q + 1] = u.y; v[4 * q + 2] = u.z; v[4 * q + 3] = u.w;
-            }
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < RS_IPT; ++k) v[k] = p0 + k < hi ? offsets[min(p0 + k, n_scan - 1)] : 0xFFFFFFFFu;
-        }
         uint32_t m = 0xFFFFFFFFu;
 #pragma unroll
         for (uint32_t k = 0; k < RS_IPT; ++k) m = min(m, v[k]);
@@ -1485,6 +1491,8 @@ __global__ void __launch_bounds__(RS_THREADS) k_starts_rangescan(uint32_t* __res
                 if (p0 + k < hi) offsets[p0 + k] = v[k];
         }
         carry = min(carry, bmin);
+#pragma unroll
+        for (uint32_t k = 0; k < RS_IPT; ++k) v[k] = nx[k];
         __syncthreads();                                 // s_w[0] is rewritten by the next sub-range
     }
 }
