@@ -154,7 +154,8 @@ struct gd_handle {
     int radix_max_bits = 8;   // digit width cap (GD_RADIX_MAXBITS, 4..11)
     int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
-    uint32_t hist_tpb = 0;      // tiles per workgroup in the radix histogram, 1/4/8 (GD_HIST_TPB);
+    uint32_t hist_tpb = 0;
+    bool hist_xcd = true;       // multi-tile histograms in reverse XCD tile order (GD_HIST_XCD)      // tiles per workgroup in the radix histogram, 1/4/8 (GD_HIST_TPB);
                                 // 0 = by size: 4 for 1024..4096 tiles (4M..16M keys), else 1 (A/B)
     bool compact_headers = true;
     bool narrow_headers = true;     // compact headers as u32 N1s when every N1 < 2^32 (GD_NARROW_HEADERS=0: u64)   // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
@@ -504,6 +505,8 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
     uint32_t* hist = (uint32_t*)h->hist.p;
     // below 1024 tiles, 4 per workgroup would leave fewer workgroups than the 256 CUs
     const uint32_t tpb = h->hist_tpb ? h->hist_tpb : (tiles >= 1024 && tiles <= 4096 ? 4u : 1u);
+    // multi-tile histograms walk the scatter's XCD tile ranges backwards (hist_t0)
+    const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
     if (pk.in) {
         // packed records: the histogram reads the u16 high-key array (bucket_device enables the
         // packing only for the 512 x 8 tiles and digits of at most 8 bits)
@@ -511,20 +514,20 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
             const uint16_t* kb16 = reinterpret_cast<const uint16_t*>(vin);
             if (tpb == 4)
                 GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0, k_radix_hist16<BITS, NT, IT, 4>,
-                              kb16, n, shift - pk.b1, tiles, hist));
+                              kb16, n, shift - pk.b1, tiles, hist, hxr));
             else
                 GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_radix_hist16<BITS, NT, IT, 1>, kb16, n,
-                              shift - pk.b1, tiles, hist));
+                              shift - pk.b1, tiles, hist, hxr));
         } else {
             return set_err(h, GD_EINVAL, "packed radix records need 512 x 8 tiles and <= 8-bit digits");
         }
     } else if constexpr (BITS <= 8) {
         if (tpb == 4)
             GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0, k_radix_hist_multi<BITS, NT, IT, 4>,
-                          kin, n, clamp, shift, tiles, hist, fill));
+                          kin, n, clamp, shift, tiles, hist, fill, hxr));
         else if (tpb == 8)
             GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 8)), dim3(NT), 0, k_radix_hist_multi<BITS, NT, IT, 8>,
-                          kin, n, clamp, shift, tiles, hist, fill));
+                          kin, n, clamp, shift, tiles, hist, fill, hxr));
         else
             GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_radix_hist<BITS, NT, IT>, kin, n, clamp, shift,
                           tiles, hist, fill));
@@ -917,6 +920,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_HOST_CHUNK")) h->host_chunk = (uint32_t)std::strtoul(v, nullptr, 10);
     if (const char* v = std::getenv("GD_XCD_TILES")) h->xcd_tiles = std::atoi(v) ? 1u : 0u;
     if (const char* v = std::getenv("GD_HIST_TPB")) h->hist_tpb = (uint32_t)std::atoi(v);
+    if (const char* v = std::getenv("GD_HIST_XCD")) h->hist_xcd = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_FAN_ILP")) h->fan_ilp = std::atoi(v);
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {

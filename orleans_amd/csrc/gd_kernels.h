@@ -825,6 +825,16 @@ __global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ 
     fill_grid(fill, NT);
 }
 
+// First tile of a TPB-tile histogram workgroup.  xcd_rev: workgroup b runs on XCD b % 8 (round-robin
+// dispatch) and counts tiles from the XCD's range of the scatter's tile order (xcd_tile) in reverse,
+// so the tiles the XCD's scatter workgroups read first are the ones its histogram read last -- still
+// in that XCD's L2.  Only when the ranges split evenly (tiles a multiple of 8 * TPB).
+__device__ __forceinline__ uint32_t hist_t0(uint32_t b, uint32_t nb, uint32_t tpb, uint32_t tiles, uint32_t xcd_rev) {
+    if (!xcd_rev || (tiles % (8u * tpb)) != 0 || (nb & 7u) != 0) return b * tpb;
+    const uint32_t per = nb >> 3, x = b & 7u, g = b >> 3;
+    return (x * per + (per - 1u - g)) * tpb;
+}
+
 // Multi-tile histogram: one workgroup counts TPB consecutive tiles, with every tile's 16-B key
 // loads issued before the first count, and one counter set per tile shared by the waves.  The
 // digit-major counts it writes for one digit are then TPB consecutive words, instead of one word
@@ -832,14 +842,15 @@ __global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ 
 template <int BITS, int NT, int IT, int TPB>
 __global__ void __launch_bounds__(NT) k_radix_hist_multi(const uint32_t* __restrict__ keys, uint32_t n,
                                                          uint32_t clamp, uint32_t shift, uint32_t tiles,
-                                                         uint32_t* __restrict__ hist, FillArgs fill) {
+                                                         uint32_t* __restrict__ hist, FillArgs fill,
+                                                         uint32_t xcd_rev) {
     constexpr uint32_t R = 1u << BITS;
     constexpr uint32_t TILE = NT * IT;
     static_assert(IT % 4 == 0, "16-B loads");
     __shared__ uint32_t s_cnt[TPB][R];
     for (uint32_t x = threadIdx.x; x < TPB * R; x += NT) (&s_cnt[0][0])[x] = 0;
     __syncthreads();
-    const uint32_t t0 = blockIdx.x * TPB;
+    const uint32_t t0 = hist_t0(blockIdx.x, gridDim.x, TPB, tiles, xcd_rev);
     const uint32_t lane = lane_id();
     const bool aligned = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
     uint32_t k[TPB][IT];
@@ -898,14 +909,14 @@ __global__ void __launch_bounds__(NT) k_radix_hist_multi(const uint32_t* __restr
 // full keys.
 template <int BITS, int NT, int IT, int TPB>
 __global__ void __launch_bounds__(NT) k_radix_hist16(const uint16_t* __restrict__ keys, uint32_t n, uint32_t shift,
-                                                     uint32_t tiles, uint32_t* __restrict__ hist) {
+                                                     uint32_t tiles, uint32_t* __restrict__ hist, uint32_t xcd_rev) {
     constexpr uint32_t R = 1u << BITS;
     constexpr uint32_t TILE = NT * IT;
     static_assert(IT % 8 == 0, "16-B loads of 8 keys");
     __shared__ uint32_t s_cnt[TPB][R];
     for (uint32_t x = threadIdx.x; x < TPB * R; x += NT) (&s_cnt[0][0])[x] = 0;
     __syncthreads();
-    const uint32_t t0 = blockIdx.x * TPB;
+    const uint32_t t0 = hist_t0(blockIdx.x, gridDim.x, TPB, tiles, xcd_rev);
     const uint32_t lane = lane_id();
     const bool aligned = (reinterpret_cast<uintptr_t>(keys) & 15u) == 0;
     uint32_t k[TPB][IT];
