@@ -151,6 +151,7 @@ struct gd_handle {
     // kernel tuning (defaults measured on MI355X; GD_ROUTE_M / GD_ROUTE_NT override for A/B runs)
     int route_m = 1;
     bool route_nt = false;
+    bool route_xcd = true;      // route workgroups over XCD-contiguous message ranges (GD_ROUTE_XCD)
     int radix_max_bits = 8;   // digit width cap (GD_RADIX_MAXBITS, 4..11)
     int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
@@ -350,7 +351,7 @@ unsigned long long pow2_at_least(unsigned long long x) {
 template <int MODE, int M, bool NT>
 int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
     return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h), k_route_m<MODE, M, NT>, keys,
-                  n, ring_args(h), table_args(h), silo, act, status, 0ull);
+                  n, ring_args(h), table_args(h), silo, act, status, 0ull, h->route_xcd ? 1u : 0u);
 }
 
 // Keys given as N1 alone (u64, or u32 with n1w = 4) with one TypeCodeData (a compact exchange
@@ -361,9 +362,9 @@ int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uin
     const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
     if (n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4>, k, n, ring_args(h), table_args(h),
-                      silo, act, status, tcd);
+                      silo, act, status, tcd, h->route_xcd ? 1u : 0u);
     return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8>, k, n, ring_args(h), table_args(h),
-                  silo, act, status, tcd);
+                  silo, act, status, tcd, h->route_xcd ? 1u : 0u);
 }
 
 int route_n1_device(gd_handle* h, const void* n1s, uint32_t n1w, uint64_t tcd, uint32_t n, uint32_t* silo,
@@ -905,6 +906,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     h->timing = (cfg->flags & GD_CFG_KERNEL_TIMING) != 0;
     if (const char* v = std::getenv("GD_ROUTE_M")) h->route_m = std::atoi(v);
     if (const char* v = std::getenv("GD_ROUTE_NT")) h->route_nt = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_ROUTE_XCD")) h->route_xcd = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
     if (const char* v = std::getenv("GD_RADIX_RANK")) h->radix_rank_atomic = std::atoi(v) ? 1u : 0u;

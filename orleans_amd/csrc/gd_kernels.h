@@ -395,16 +395,29 @@ __global__ void __launch_bounds__(MB_ROUTE_BLOCK) k_mb_route(const gd_key* __res
     }
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each with its own
+// L2.  With xcd != 0 block b processes tile start(b % 8) + b / 8, so every XCD owns a contiguous
+// tile range: the digit-run fragments that consecutive tiles write next to each other in the
+// output meet in one L2 instead of being written back as partial lines by two.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb, uint32_t xcd) {
+    if (!xcd) return b;
+    const uint32_t x = b & 7u, k = b >> 3, q = nb >> 3, rem = nb & 7u;
+    return x * q + min(x, rem) + k;
+}
+
 template <int MODE, int M, bool NT, int N1W = 0>
 __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                    TableArgs tab, uint32_t* __restrict__ out_silo,
                                                    uint32_t* __restrict__ out_act,
-                                                   uint8_t* __restrict__ out_status, uint64_t tcd_u) {
+                                                   uint8_t* __restrict__ out_status, uint64_t tcd_u, uint32_t xcd) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
     stage_ring(ring, s_pts, s_own);
-    route_m_core<MODE, M, BLOCK, NT, N1W, true>(keys, n, blockIdx.x * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own,
+    // xcd: each XCD routes a contiguous message range (xcd_tile), so the act it writes is the act the
+    // same XCD's histogram and scatter workgroups read next (their XCD tile ranges match)
+    const uint32_t blk = xcd_tile(blockIdx.x, gridDim.x, xcd);
+    route_m_core<MODE, M, BLOCK, NT, N1W, true>(keys, n, blk * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own,
                                                tab, tab.ctr->max_probe, out_silo, out_act, out_status, tcd_u, nullptr,
                                                0);
 }
@@ -970,15 +983,6 @@ __global__ void __launch_bounds__(NT) k_radix_hist16(const uint16_t* __restrict_
     }
 }
 
-// Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), each with its own
-// L2.  With xcd != 0 block b processes tile start(b % 8) + b / 8, so every XCD owns a contiguous
-// tile range: the digit-run fragments that consecutive tiles write next to each other in the
-// output meet in one L2 instead of being written back as partial lines by two.
-__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb, uint32_t xcd) {
-    if (!xcd) return b;
-    const uint32_t x = b & 7u, k = b >> 3, q = nb >> 3, rem = nb & 7u;
-    return x * q + min(x, rem) + k;
-}
 
 // Packed records between radix passes (bucket_device, when the key bits above the first pass's
 // digit fit 16 bits and the message index fits beside that digit in 32): A = (key's low b1 bits)
