@@ -504,8 +504,10 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
     // the digit-major counts, then (row scans) the R digit totals
     GD_TRY(ensure(h, h->hist, ((size_t)R * tiles + R) * sizeof(uint32_t)));
     uint32_t* hist = (uint32_t*)h->hist.p;
-    // below 1024 tiles, 4 per workgroup would leave fewer workgroups than the 256 CUs
-    const uint32_t tpb = h->hist_tpb ? h->hist_tpb : (tiles >= 1024 && tiles <= 4096 ? 4u : 1u);
+    // below 1024 tiles, 4 per workgroup would leave fewer workgroups than the 256 CUs; up to 12,288
+    // tiles (48M keys) 4 per workgroup in reverse XCD order also leaves the scatter's keys in L2
+    // (f2 hop 3, 43M keys: bucketing -8%); at cfg 3's 16,384 tiles it is neutral, one stays
+    const uint32_t tpb = h->hist_tpb ? h->hist_tpb : (tiles >= 1024 && tiles <= 12288 ? 4u : 1u);
     // multi-tile histograms walk the scatter's XCD tile ranges backwards (hist_t0)
     const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
     if (pk.in) {
