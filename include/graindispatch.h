@@ -681,7 +681,10 @@ int gd_actdir_count(gd_handle* h, uint64_t* out_live);
  * the batch starts (n_ctx entries), hard limits as SiloMessagingOptions' MaxEnqueuedRequestsHardLimit
  * (_StatelessWorker); <= 0 = no limit.  Every enqueued message of an activation counts
  * (IncrementEnqueuedOnDispatcherCount), as when the agent thread enqueues the batch before a worker
- * runs any of it. */
+ * runs any of it.  The limits apply whether or not perm / offsets are asked for.
+ * Every context index gd_actdir_add stored for an entry the batch finds must be < n_ctx: a larger one
+ * fails the call with GD_EINVAL (the *_device forms: the next gd_synchronize), the message left
+ * un-enqueued with GD_RECV_UNDECODED. */
 #define GD_RECV_ACTIVATION        0
 #define GD_RECV_SYSTEM_TARGET     1
 #define GD_RECV_NULL_CONTEXT      2

@@ -29,6 +29,7 @@ constexpr uint8_t RECV_ACTIVATION = 0, RECV_SYSTEM_TARGET = 1, RECV_NULL_CONTEXT
                   RECV_REJECT_OVERLOADED = 4, RECV_DROPPED = 5, RECV_UNDECODED = 6;
 constexpr uint8_t RECV_STATELESS_BIT = 0x80;   // transient mark for the overload pass
 constexpr uint8_t DIR_RESPONSE = 1;
+constexpr uint32_t ERR_CTX_RANGE = 32u;       // DevCounters.err: an entry's context index >= the call's n_ctx
 
 struct AdArgs {
     const Slot* slots;
@@ -95,13 +96,16 @@ __global__ void __launch_bounds__(BLOCK) k_ad_setflags(const uint32_t* __restric
 // Request (Message.Direction's default, Message.cs:113-116).  frame_flags (nullable): a frame whose
 // target address was not decoded completely goes back to C# (RECV_UNDECODED).  MARK_STATELESS: a
 // message enqueued on a stateless-worker activation carries RECV_STATELESS_BIT for k_overload.
+// An entry whose context index is not below n_ctx (gd_actdir_add stored it; n_ctx is per call) is a
+// caller error: ERR_CTX_RANGE in *err (the call fails with GD_EINVAL) and the message is left
+// un-enqueued (ctx NONE32, RECV_UNDECODED), so no later pass indexes past the n_ctx arrays.
 template <bool MARK_STATELESS>
 __global__ void __launch_bounds__(BLOCK) k_receive(const gd_key* __restrict__ target_grain,
                                                    const gd_key* __restrict__ target_activation,
                                                    const uint8_t* __restrict__ direction,
                                                    const uint32_t* __restrict__ frame_flags, uint32_t n, uint32_t n_ctx,
                                                    AdArgs t, uint32_t* __restrict__ out_ctx,
-                                                   uint8_t* __restrict__ out_status) {
+                                                   uint8_t* __restrict__ out_status, uint32_t* __restrict__ err) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     uint32_t ctx = NONE32;
@@ -136,6 +140,11 @@ __global__ void __launch_bounds__(BLOCK) k_receive(const gd_key* __restrict__ ta
         } else {
             st = RECV_NULL_CONTEXT;                    // EnqueueReceiveMessage(msg, null, null) (:154-167)
             ctx = n_ctx;
+        }
+        if (ctx != NONE32 && ctx >= n_ctx && st != RECV_NULL_CONTEXT) {
+            atomicOr(err, ERR_CTX_RANGE);
+            ctx = NONE32;
+            st = RECV_UNDECODED;
         }
     }
     out_ctx[i] = ctx;

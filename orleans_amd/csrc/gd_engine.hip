@@ -107,6 +107,7 @@ struct gd_handle {
     DevBuf ad_last;
     DevBuf ad_buf[8];
     DevBuf fr_recv[3];                // frames: TargetActivation / Direction scratch when the caller wants neither
+    DevBuf recv_scr[2];               // receive with limits but no buckets wanted: perm / offsets scratch
 
     // KeyExt grains (gd_keyext.h): device table + heap, and the host index both are kept from
     KxSlot* kx_slots = nullptr;
@@ -683,6 +684,8 @@ int sync_checked(gd_handle* h) {
         const uint32_t e = h->ctr_host.err;
         HIP_TRY(h, hipMemsetAsync(&h->ctr->err, 0, sizeof(uint32_t), h->stream));
         GD_TRY(sync(h));
+        if (e == ERR_CTX_RANGE)
+            return set_err(h, GD_EINVAL, "an ActivationDirectory entry's context index is not below n_ctx");
         return set_err(h, GD_EFULL, "device error bits 0x%x", e);
     }
     return GD_OK;
@@ -1000,6 +1003,7 @@ void gd_destroy(gd_handle* h) {
     free_buf(h->ad_last);
     for (DevBuf& b : h->ad_buf) free_buf(b);
     for (DevBuf& b : h->fr_recv) free_buf(b);
+    for (DevBuf& b : h->recv_scr) free_buf(b);
     for (auto& t : h->pending) {
         (void)hipEventDestroy(t.a);
         (void)hipEventDestroy(t.b);
@@ -4059,11 +4063,22 @@ int receive_device(gd_handle* h, const gd_key* tg, const gd_key* ta, const uint8
     const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
     if (n) {
         if (limits)
-            GD_TRY(launch(h, "k_receive", g, b, 0, k_receive<true>, tg, ta, dir, fflags, n, n_ctx, ad_args(h), ctx, st));
+            GD_TRY(launch(h, "k_receive", g, b, 0, k_receive<true>, tg, ta, dir, fflags, n, n_ctx, ad_args(h), ctx, st,
+                          &h->ctr->err));
         else
-            GD_TRY(launch(h, "k_receive", g, b, 0, k_receive<false>, tg, ta, dir, fflags, n, n_ctx, ad_args(h), ctx, st));
+            GD_TRY(launch(h, "k_receive", g, b, 0, k_receive<false>, tg, ta, dir, fflags, n, n_ctx, ad_args(h), ctx, st,
+                          &h->ctr->err));
     }
-    if (!perm) return GD_OK;
+    if (!perm && !(limits && n)) return GD_OK;
+    const bool want_buckets = perm != nullptr;
+    if (!want_buckets) {
+        // CheckOverloaded needs each message's place in its activation's FIFO: bucket into scratch
+        // (the caller asked for statuses only), then drop the buckets.
+        GD_TRY(ensure(h, h->recv_scr[0], (size_t)n * 4 + 4));
+        GD_TRY(ensure(h, h->recv_scr[1], ((size_t)n_ctx + 3) * 4));
+        perm = (uint32_t*)h->recv_scr[0].p;
+        offsets = (uint32_t*)h->recv_scr[1].p;
+    }
     // buckets 0..n_ctx-1 contexts, n_ctx the null context, n_ctx + 1 not enqueued (ctx NONE32 clamps there)
     uint32_t* rank = nullptr;
     if (limits && n) {
@@ -4074,7 +4089,7 @@ int receive_device(gd_handle* h, const gd_key* tg, const gd_key* ta, const uint8
     if (limits && n) {
         GD_TRY(launch(h, "k_overload", g, b, 0, k_overload, (const uint32_t*)rank, (const uint32_t*)offsets, n, dir,
                       lim->request_count, lim->hard_limit, lim->hard_limit_stateless_worker, ctx, st));
-        GD_TRY(bucket_device(h, ctx, n, n_ctx + 1, perm, offsets));
+        if (want_buckets) GD_TRY(bucket_device(h, ctx, n, n_ctx + 1, perm, offsets));
     }
     return GD_OK;
 }

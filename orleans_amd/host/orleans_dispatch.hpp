@@ -436,22 +436,55 @@ public:
                                                                           const std::vector<ActivationId>& acts,
                                                                           const std::vector<SiloAddress>& silos) {
         const size_t n = grains.size();
-        std::vector<gd_key> keys(n);
-        std::vector<gd_val> vals(n), dropped(n);
-        std::vector<uint8_t> st(n);
-        for (size_t i = 0; i < n; ++i) {
-            keys[i] = grains[i].Key.ToNative();
-            vals[i] = gd_val{ActIndex(acts[i]), silos_.IndexOf(silos[i])};
+        std::map<SiloAddress, std::vector<ActivationAddress>, SiloLess> del;
+        // KeyExt grains (string / compound keys) live in the KeyExt table, which gd_dir_merge does not
+        // probe: they are merged here, by the same rule, as AddSingleActivations splits them.
+        std::vector<size_t> main, ext;
+        for (size_t i = 0; i < n; ++i) (grains[i].Key.HasKeyExt() ? ext : main).push_back(i);
+        std::vector<gd_key> keys(main.size());
+        std::vector<gd_val> vals(main.size()), dropped(main.size());
+        std::vector<uint8_t> st(main.size());
+        for (size_t j = 0; j < main.size(); ++j) {
+            keys[j] = grains[main[j]].Key.ToNative();
+            vals[j] = gd_val{ActIndex(acts[main[j]]), silos_.IndexOf(silos[main[j]])};
         }
         FlushIds();
-        if (n) Check(h_, gd_dir_merge(h_, keys.data(), vals.data(), nullptr, (uint32_t)n, st.data(), dropped.data()));
-        std::map<SiloAddress, std::vector<ActivationAddress>, SiloLess> del;
-        for (size_t i = 0; i < n; ++i) {
-            if (st[i] == GD_MERGE_KEPT || st[i] == GD_MERGE_DROPPED)
-                del[silos_.At(dropped[i].silo)].push_back(
-                    ActivationAddress{silos_.At(dropped[i].silo), grains[i], acts_.at(dropped[i].act)});
-            else if (st[i] == GD_MERGE_HOST && multi_.count(grains[i]))
+        if (!main.empty())
+            Check(h_, gd_dir_merge(h_, keys.data(), vals.data(), nullptr, (uint32_t)main.size(), st.data(),
+                                   dropped.data()));
+        for (size_t j = 0; j < main.size(); ++j) {
+            const size_t i = main[j];
+            if (st[j] == GD_MERGE_KEPT || st[j] == GD_MERGE_DROPPED)
+                del[silos_.At(dropped[j].silo)].push_back(
+                    ActivationAddress{silos_.At(dropped[j].silo), grains[i], acts_.at(dropped[j].act)});
+            else if (st[j] == GD_MERGE_HOST && multi_.count(grains[i]))
                 AddActivation(grains[i], acts[i], silos[i]);
+        }
+        for (size_t i : ext) {
+            const gd_key k = grains[i].Key.ToNative();
+            KeyExtBatch kx({&grains[i].Key});
+            gd_val cur{};
+            uint8_t found = 0;
+            Check(h_, gd_dir_lookup_ext(h_, &k, kx.get(), 1, &cur, &found));
+            const gd_val in{ActIndex(acts[i]), silos_.IndexOf(silos[i])};
+            if (!found) {                                  // partitionData.Add (:517-520)
+                gd_val o{};
+                uint8_t ins = 0;
+                Check(h_, gd_dir_register_ext(h_, &k, kx.get(), &in, 1, &o, &ins));
+                continue;
+            }
+            if (cur.act == in.act) continue;               // the same activation: nothing to drop
+            const ActivationId& have = acts_.at(cur.act);
+            if (acts[i] < have) {                          // OrderBy(ActivationId).First() stays (:160-163)
+                uint8_t removed = 0;
+                Check(h_, gd_dir_unregister_ext(h_, &k, kx.get(), &cur.act, 1, &removed));
+                gd_val o{};
+                uint8_t ins = 0;
+                Check(h_, gd_dir_register_ext(h_, &k, kx.get(), &in, 1, &o, &ins));
+                del[silos_.At(cur.silo)].push_back(ActivationAddress{silos_.At(cur.silo), grains[i], have});
+            } else {
+                del[silos[i]].push_back(ActivationAddress{silos[i], grains[i], acts[i]});
+            }
         }
         return del;
     }
@@ -474,11 +507,14 @@ public:
         for (const auto& g : touched) {
             auto& inst = multi_[g];
             if (inst.empty()) {
+                // the GPU entry is GD_ACT_MULTI unless one instance was left, and that one lived on
+                // the removed silo: gd_dir_remove_silos already dropped and counted it
                 const gd_key k = g.Key.ToNative();
                 const uint32_t a = GD_ACT_MULTI;
-                Check(h_, gd_dir_unregister(h_, &k, &a, 1, nullptr));
+                uint8_t removed = 0;
+                Check(h_, gd_dir_unregister(h_, &k, &a, 1, &removed));
                 multi_.erase(g);
-                ++n;
+                if (removed) ++n;
             } else {
                 Publish(g, inst);
             }

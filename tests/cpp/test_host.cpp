@@ -678,6 +678,58 @@ static void MergeKeepsLowestActivationId() {
     EXPECT(del.at(s2)[0].Activation == hi && del.at(s2)[0].Grain == g2);
 }
 
+// Merge with string-keyed grains: they live in the KeyExt table and merge by the same rule
+// (they used to land in the main table, where LookUpActivations never looks).
+static void MergeStringKeyGrains() {
+    DispatchHandle h(0, 4096, 0);
+    const SiloAddress me = SiloAddress::New(10, 0, 0, 1, 11111, 1), s2 = SiloAddress::New(10, 0, 0, 2, 11111, 1);
+    LocalGrainDirectory dir(h.get(), me);
+    dir.AddServer(s2);
+    auto& part = dir.DirectoryPartition();
+    const int tc = gd_calculate_id_hash("UnitTests.GrainInterfaces.IStringKeyGrain");
+    const GrainId g1 = GrainId::GetGrainId(tc, std::string("alice")), g2 = GrainId::GetGrainId(tc, std::string("bob"));
+    const GrainId g3 = GrainId::GetGrainId(tc, std::string("carol-with-a-name-longer-than-24-bytes"));
+    ActivationId lo = NewActivationId(5), hi = NewActivationId(6);
+    lo.N0 = 1;
+    hi.N0 = 2;
+    part.AddSingleActivation(g1, hi, me);
+    part.AddSingleActivation(g2, lo, me);
+    const int before = part.Count();
+    const auto del = part.Merge({g1, g2, g3}, {lo, hi, NewActivationId(7)}, {s2, s2, s2});
+    const auto a1 = part.LookUpActivations(g1), a2 = part.LookUpActivations(g2), a3 = part.LookUpActivations(g3);
+    EXPECT(a1.Addresses && (*a1.Addresses)[0].Activation == lo && (*a1.Addresses)[0].Silo == s2);
+    EXPECT(a2.Addresses && (*a2.Addresses)[0].Activation == lo && (*a2.Addresses)[0].Silo == me);
+    EXPECT(a3.Addresses && (*a3.Addresses)[0].Silo == s2);
+    EXPECT(part.Count() == before + 1);
+    EXPECT(del.size() == 2 && del.at(me).size() == 1 && del.at(s2).size() == 1);
+    EXPECT(del.at(me)[0].Activation == hi && del.at(me)[0].Grain == g1);
+    EXPECT(del.at(s2)[0].Activation == hi && del.at(s2)[0].Grain == g2);
+    // a plain long-keyed grain with the same type is a different grain: untouched by the KeyExt merge
+    const GrainId plain = GrainId::GetGrainId(tc, (int64_t)0);
+    EXPECT(!part.LookUpActivations(plain).Addresses);
+}
+
+// AdjustLocalDirectory counts each removed grain once, also a multi-instance grain whose last
+// instance lived on the removed silo (it was counted twice).
+static void RemoveLastInstanceCountsOnce() {
+    DispatchHandle h(0, 4096, 0);
+    const SiloAddress me = SiloAddress::New(10, 0, 0, 1, 11111, 1);
+    const SiloAddress s2 = SiloAddress::New(10, 0, 0, 2, 11111, 1), s3 = SiloAddress::New(10, 0, 0, 3, 11111, 1);
+    LocalGrainDirectory dir(h.get(), me);
+    dir.AddServer(s2);
+    dir.AddServer(s3);
+    auto& part = dir.DirectoryPartition();
+    const int tc = gd_calculate_id_hash("UnitTests.Grains.StatelessWorkerGrain");
+    const GrainId one = GrainId::GetGrainId(tc, 1), two = GrainId::GetGrainId(tc, 2);
+    EXPECT(part.AddActivation(one, NewActivationId(71), s2));          // one instance, on s2
+    EXPECT(part.AddActivation(two, NewActivationId(72), s2));          // two instances, one on s2
+    EXPECT(part.AddActivation(two, NewActivationId(73), s3));
+    EXPECT(part.RemoveActivationsOn(s2) == 1);
+    EXPECT(!part.LookUpActivations(one).Addresses);
+    const auto r = part.LookUpActivations(two);
+    EXPECT(r.Addresses && r.Addresses->size() == 1 && (*r.Addresses)[0].Silo == s3);
+}
+
 // ActivationDirectory + IncomingMessageAgent.ReceiveMessage (IncomingMessageAgent.cs:92-170).
 static void ActivationDirectoryReceive() {
     DispatchHandle h(0, 4096, 0);
@@ -744,6 +796,8 @@ int main(int argc, char** argv) {
         Run("WholeNodeExchange", WholeNodeExchange);
         Run("SiloRemovalAdjustsDirectory", SiloRemovalAdjustsDirectory);
         Run("MergeKeepsLowestActivationId", MergeKeepsLowestActivationId);
+        Run("MergeStringKeyGrains", MergeStringKeyGrains);
+        Run("RemoveLastInstanceCountsOnce", RemoveLastInstanceCountsOnce);
         Run("ActivationDirectoryReceive", ActivationDirectoryReceive);
         if (argc > 2) Run("RoutingDump", [&] { RoutingDump(argv[2]); });
     }

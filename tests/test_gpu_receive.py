@@ -81,6 +81,32 @@ def test_receive_vs_oracle(gd, limits):
     w2 = rv.receive_batch(tg, ta, np.zeros(len(tg), np.uint8), ad, n_ctx)
     np.testing.assert_array_equal(st2, w2[0])
     np.testing.assert_array_equal(ctx2, w2[1])
+    # limits without buckets: CheckOverloaded still applies (it used to be skipped)
+    ctx3, st3 = e.receive(tg, ta, direction, n_ctx, rc, hl, hls, bucket=False)
+    np.testing.assert_array_equal(st3, w[0])
+    np.testing.assert_array_equal(ctx3, w[1])
+    assert int(st3.max()) <= 6                     # no transient stateless-worker mark leaks out
+    e.close()
+
+
+def test_receive_context_out_of_range(gd):
+    """An ActivationDirectory entry whose context index is not below the call's n_ctx is a caller
+    error (GD_EINVAL), never an out-of-bounds read of request_count / offsets."""
+    rng, keys, ctxs, flags, tg, ta, direction = _world(7, 500, 8, 4000)
+    n_ctx = len(keys)
+    e = gd.GrainDispatch(device=0, table_capacity=1024)
+    e.actdir_add(keys, ctxs, flags)
+    rc = np.zeros(n_ctx - 100, np.uint32)
+    with pytest.raises(gd.GrainDispatchError):
+        e.receive(tg, ta, direction, n_ctx - 100, rc, 3, 2)
+    # the handle stays usable, and a correct n_ctx routes as before
+    ctx, st, perm, off = e.receive(tg, ta, direction, n_ctx)
+    ad = rv.ActivationDirectory()
+    for k, c, f in zip(keys, ctxs, flags):
+        ad.add(tuple(int(x) for x in k), int(c), int(f))
+    w = rv.receive_batch(tg, ta, direction, ad, n_ctx)
+    np.testing.assert_array_equal(st, w[0])
+    np.testing.assert_array_equal(perm, w[2])
     e.close()
 
 
