@@ -635,8 +635,10 @@ def run_cfg4(args, world, rank, local, dev):
     owner + directory probe) -> bucket per activation -> next frontier.  Value = messages routed
     (all hops, all ranks) / max-over-ranks wall time of the cascade, graph and directory resident in
     HBM.  N = 1: fused expand+route kernel (k_fan_route) per hop.  N > 1: directory sharded by ring
-    owner, (target, sender) pairs exchanged with one all-to-all-v per hop (ShardedFanout over RCCL)."""
-    from orleans_amd.fanout import (CHIRPER_ACCOUNT_CLASS, DeviceFanoutEngine, FanoutCascade,
+    owner, (target, sender) pairs exchanged with one grouped RCCL send/recv round per hop inside the
+    library (gd_fanout_multi_device, LibraryFanout), checked on the first cascade against the
+    torch.distributed all-to-all-v path (ShardedFanout); the torch path is timed only if they differ."""
+    from orleans_amd.fanout import (CHIRPER_ACCOUNT_CLASS, DeviceFanoutEngine, FanoutCascade, LibraryFanout,
                                     ShardedFanout, upload_graph)
     from orleans_amd.workloads import power_law_graph
 
@@ -663,6 +665,32 @@ def run_cfg4(args, world, rank, local, dev):
     setup_s = time.perf_counter() - t_setup
     runner = (FanoutCascade(eng, graph, n) if world == 1 else
               ShardedFanout(eng, graph, n, stage_via_cpu=args.rehearse_one_gpu))
+    exchange = "none" if world == 1 else "torch.distributed all_to_all_single (RCCL)"
+    if world > 1 and not args.rehearse_one_gpu and args.exchange != "torch":
+        ok, err = False, None
+        try:
+            lib_runner = LibraryFanout(eng, graph, n)
+            want = runner.run(t_seeds, args.hops)
+            got = lib_runner.fetch(lib_runner.run(t_seeds, args.hops))
+            u = lambda t: t.cpu().numpy().view(np.uint32)  # noqa: E731
+            ok = len(got) == len(want) and all(
+                np.array_equal(gh["frontier"], u(wh.frontier)) and np.array_equal(gh["act"], u(wh.act)) and
+                np.array_equal(gh["perm"], u(wh.perm)) and np.array_equal(gh["offsets"], u(wh.offsets)) and
+                np.array_equal(gh["sender"], u(wh.sender)) for gh, wh in zip(got, want))
+        except Exception as ex:   # noqa: BLE001 -- reported in the JSON line, torch exchange used instead
+            if args.exchange == "library":
+                raise
+            err = f"{ex!r}"[:200]
+        agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(agree, op=dist.ReduceOp.MIN)
+        if int(agree.item()) == 1:
+            runner = lib_runner
+            exchange = ("libgraindispatch gd_fanout_multi_device (grouped RCCL send/recv of (target, sender) "
+                        "per hop); first cascade bit-identical to the torch.distributed all-to-all-v path")
+        else:
+            assert args.exchange != "library", "library fan-out disagrees with the torch path"
+            exchange = ("torch.distributed all_to_all_single (RCCL); library fan-out " +
+                        (f"failed here: {err}" if err else "disagreed on the first cascade (some rank)"))
 
     def step():
         return runner.run(t_seeds, args.hops)
@@ -687,7 +715,7 @@ def run_cfg4(args, world, rank, local, dev):
     dist.all_reduce(ts, op=dist.ReduceOp.SUM)
     wall_max, msgs_total = float(tw[0]), float(ts[1])
     hop_msgs = [h.messages for h in hops]
-    hop_front = [int(h.frontier.shape[0]) for h in hops]
+    hop_front = [h.n_frontier if hasattr(h, "n_frontier") else int(h.frontier.shape[0]) for h in hops]
 
     kernels, roofline = {}, None
     if args.profile_steps > 0:
@@ -717,7 +745,7 @@ def run_cfg4(args, world, rank, local, dev):
                     "avg_launch_ms": round(d["ms_per_step"] / max(1, d["launches_per_step"]), 5)}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and hops[-1].target is not None:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and getattr(hops[-1], "target", None) is not None:
         cpu = cpu_baseline_cfg4(args, hops, tcd, owner, pts, own, n)
 
     if rank == 0:
@@ -734,7 +762,7 @@ def run_cfg4(args, world, rank, local, dev):
                        "silos": f"8 x 10.0.0.{{1..8}}:11111, {args.silos} generations",
                        "parallelism": f"shard{world}" + ("-rehearsal" if args.rehearse_one_gpu else "")},
             "messages_per_step": int(msgs_total / args.steps), "hop_messages_rank0": hop_msgs,
-            "hop_publishers_rank0": hop_front, "setup_s": round(setup_s, 1),
+            "hop_publishers_rank0": hop_front, "setup_s": round(setup_s, 1), "exchange": exchange,
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

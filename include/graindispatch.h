@@ -551,6 +551,46 @@ int gd_pack_nodes_by_shard_device(gd_handle* h, const uint32_t* d_nodes, const u
 int gd_frontier_next_device(gd_handle* h, const uint32_t* d_offsets, uint32_t n_act, uint8_t* d_visited,
                             uint32_t* d_out, uint32_t* out_n);
 
+/* ---- the sharded fan-out cascade (BASELINE cfg 4 across GPUs: SURVEY 8 f2 over 8 e) ---------
+ * Over the library's communicator (gd_comm_init / gd_comm_init_local): rank r owns the directory
+ * partitions of silos s % n_ranks == r, as in gd_route_multi; the follower graph is replicated.
+ * From `seeds` (the same array on every rank) each rank takes the seeds whose grain it owns, in seed
+ * order, and marks them published.  Then per hop, on every rank:
+ *   expand its publishers (ChirperAccount.cs:131-134, as gd_fanout_expand_device) -> stable
+ *   partition of the (target, sender) pairs by the target's owner rank (the per-silo outbound
+ *   queues, OutboundMessageQueue.cs:54-131) -> one grouped send/recv round, 8 B a message ->
+ *   route the targets and bucket per activation on the owner, in arrival order = (sender rank,
+ *   sender emission order) -> the next publishers: this rank's activations that received a chirp
+ *   and have not published yet, ascending (gd_frontier_next_device).
+ * Collective: every rank calls it with the same seeds, hops and n_act.  out[hops] (may be NULL):
+ * device pointers into library-owned buffers, valid until the next call on the handle,
+ * gd_comm_destroy or gd_destroy.  Blocks the host twice per hop (the hop's size, the counts round). */
+typedef struct gd_fanout_hop {
+    uint32_t        n_frontier;   /* this rank's publishers of the hop                        */
+    const uint32_t* frontier;
+    uint64_t        n_sent;       /* messages they emitted                                    */
+    uint32_t        n_recv;       /* messages delivered here (this rank owns their grain)     */
+    const uint32_t* target;       /* [n_recv] follower node, arrival order                    */
+    const uint32_t* sender;       /* [n_recv] publisher node                                  */
+    const uint32_t* src;          /* [n_recv] sending rank                                    */
+    const uint32_t* silo;         /* [n_recv] route results (as gd_route_nodes_device)        */
+    const uint32_t* act;
+    const uint8_t*  status;
+    const uint32_t* perm;         /* [n_recv] stable per-activation order                     */
+    const uint32_t* offsets;      /* [n_act + 2]                                              */
+} gd_fanout_hop;
+int gd_fanout_multi_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_nodes,
+                           const uint32_t* d_seeds, uint32_t n_seeds, int32_t type_code, uint32_t n_act,
+                           uint32_t hops, gd_fanout_hop* out);
+/* Host graph and seeds (uploaded per call); returns with the cascade done. */
+int gd_fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint32_t n_nodes,
+                    const uint32_t* seeds, uint32_t n_seeds, int32_t type_code, uint32_t n_act, uint32_t hops,
+                    gd_fanout_hop* out);
+/* Copy hop `hop` of the last cascade to host arrays sized from its gd_fanout_hop (any may be NULL). */
+int gd_fanout_multi_fetch(gd_handle* h, uint32_t hop, uint32_t* frontier, uint32_t* target, uint32_t* sender,
+                          uint32_t* src, uint32_t* silo, uint32_t* act, uint8_t* status, uint32_t* perm,
+                          uint32_t* offsets);
+
 /* ---- non-owner directory cache -------------------------------------------
  * AdaptiveGrainDirectoryCache over LRU<GrainId, entry> (src/Orleans.Runtime/GrainDirectory/
  * AdaptiveGrainDirectoryCache.cs:7-140, src/Orleans.Core/Utils/LRU.cs) on the LocalLookup path
@@ -638,8 +678,55 @@ int gd_activation_ids_set(gd_handle* h, const uint32_t* acts, const gd_key* ids,
 #define GD_MERGE_SAME     2
 #define GD_MERGE_DROPPED  3
 #define GD_MERGE_HOST     4
+/* tags[i] | GD_MERGE_TAG_MULTI_INSTANCE: the incoming GrainInfo is not SingleInstance (an AddActivation
+ * grain holding one instance); partitionData.Add keeps it so (tags NULL: single unless GD_ACT_MULTI). */
+#define GD_MERGE_TAG_MULTI_INSTANCE 0x80000000u
 int gd_dir_merge(gd_handle* h, const gd_key* keys, const gd_val* vals, const int32_t* tags, uint32_t n,
                  uint8_t* out_status, gd_val* out_dropped);
+
+/* ---- multi-rank directory handoff (SURVEY 8 f4 over 8 e) ------------------------------------------
+ * After a membership change (the new ring installed on every rank with gd_ring_set), each rank splits
+ * off the entries whose new owner silo it does not host (keep_silo as gd_dir_split, removed here), they
+ * travel to the owner's rank (silo % n_ranks) in one grouped round over the library's communicator with
+ * their ActivationId (gd_activation_ids_set) and VersionTag, and the receiver applies them as the
+ * reference distinguishes the two events (GrainDirectoryHandoffManager.cs):
+ *   GD_HANDOFF_ADD     ProcessSiloAddEvent (:195-245): RegisterMany(singleActivation: true) --
+ *                      AddSingleActivation, the first registration wins (GrainDirectoryPartition.cs:304-326)
+ *   GD_HANDOFF_REMOVE  ProcessSiloRemoveEvent (:125-158): GrainDirectoryPartition.Merge (:497-522) --
+ *                      GrainInfo.Merge keeps the lowest ActivationId (:139-179), the incoming VersionTag
+ *                      and SingleInstance flag travel with the entry
+ * Received entries take this handle's activation indices act_base + j (j = arrival position; their
+ * ActivationIds are set at those indices as by gd_activation_ids_set); multi-activation entries stay
+ * GD_ACT_MULTI (their instance lists are the host's).  Per received entry, status:
+ *   GD_MERGE_INSERTED  the grain was absent here: the entry is added
+ *   GD_MERGE_SAME      the same ActivationId already holds the grain
+ *   GD_MERGE_KEPT      (REMOVE) the incoming ActivationId is the lower: it replaces the holder;
+ *                      dropped = the displaced {act, silo} (Catalog.DeleteActivations on that silo)
+ *   GD_MERGE_DROPPED   REMOVE: the holder's ActivationId is the lower, dropped = the incoming entry;
+ *                      ADD: another activation holds the grain (first registration wins) or the silo is
+ *                      not valid, dropped = the holder (none when refused)
+ *   GD_MERGE_HOST      a multi-activation entry on either side: C# unions the instance lists
+ * Collective over the communicator; synchronous.  The result's device arrays (arrival order = sender
+ * rank, sender slot order) stay valid until the next call, gd_comm_destroy or gd_destroy. */
+#define GD_HANDOFF_ADD    0
+#define GD_HANDOFF_REMOVE 1
+typedef struct gd_handoff_result {
+    uint64_t        n_sent;       /* entries this rank split off and sent              */
+    uint32_t        n_recv;       /* entries received                                  */
+    const gd_key*   recv_keys;    /* [n_recv] GrainIds                                 */
+    const gd_key*   recv_ids;     /* [n_recv] ActivationIds (zero for multi-activation) */
+    const uint32_t* recv_act;     /* [n_recv] activation index here (GD_ACT_MULTI kept) */
+    const uint32_t* recv_silo;    /* [n_recv] silo index (bit 31: a multi-activation entry) */
+    const uint32_t* recv_src;     /* [n_recv] sending rank                             */
+    const uint8_t*  status;       /* [n_recv] GD_MERGE_*                               */
+    const gd_val*   dropped;      /* [n_recv] see above; {GD_NO_*} otherwise           */
+} gd_handoff_result;
+int gd_dir_handoff_multi(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int event, uint32_t act_base,
+                         gd_handoff_result* out);
+/* Host copies of the last handoff's received entries (any pointer may be NULL; silos without the
+ * multi-activation mark). */
+int gd_dir_handoff_fetch(gd_handle* h, gd_key* keys, gd_key* ids, uint32_t* acts, uint32_t* silos, uint32_t* src,
+                         uint8_t* status, gd_val* dropped);
 
 /* ---- receive path: ActivationDirectory + IncomingMessageAgent -----------------
  * ActivationDirectory (src/Orleans.Runtime/Catalog/ActivationDirectory.cs): ActivationId -> the

@@ -159,21 +159,23 @@ class DirectoryState:
             self.ids[int(a)] = tuple(int(x) for x in k)
 
     def merge(self, keys, acts, silos, tags=None):
-        """Merge of a partition (distinct grains).  Returns [(status, dropped act, dropped silo)]."""
+        """Merge of a partition (distinct grains).  Returns [(status, dropped act, dropped silo)].
+        tags[i] bit 31 (GD_MERGE_TAG_MULTI_INSTANCE): the incoming GrainInfo is not SingleInstance."""
         self.op += 1
         out = []
         for i, k in enumerate(keys):
             k = tuple(int(x) for x in k)
             a, s = int(acts[i]), int(silos[i])
             e = self.entries.get(k)
-            if e is None:                                   # partitionData.Add (:509-512)
+            if e is None:                                   # partitionData.Add (:509-512): the GrainInfo as it is
                 tag = (int(tags[i]) & 0x7FFFFFFF) if tags is not None else version_tag(self.op, k)
-                self.entries[k] = [a, s, tag, a != ACT_MULTI]
+                multi_flag = tags is not None and (int(tags[i]) & 0x80000000) != 0
+                self.entries[k] = [a, s, tag, a != ACT_MULTI and not multi_flag]
                 out.append((MERGE_INSERTED, M32, M32))
             elif e[0] == ACT_MULTI or a == ACT_MULTI or not e[3]:
                 out.append((MERGE_HOST, M32, M32))
-            elif e[0] == a:
-                out.append((MERGE_SAME, M32, M32))          # ContainsKey -> continue, not modified
+            elif e[0] == a or self.ids[a] == self.ids[e[0]]:
+                out.append((MERGE_SAME, M32, M32))          # ContainsKey(ActivationId) -> continue (:146)
             else:
                 e[2] = version_tag(self.op, k)              # modified -> rand.Next()
                 if key_order(self.ids[a]) < key_order(self.ids[e[0]]):
@@ -181,6 +183,31 @@ class DirectoryState:
                     e[0], e[1] = a, s
                 else:
                     out.append((MERGE_DROPPED, a, s))
+        return out
+
+    def register_handoff(self, keys, acts, silos):
+        """ProcessSiloAddEvent's RegisterMany(singleActivation: true) on the receiver
+        (GrainDirectoryHandoffManager.cs:212-233): AddSingleActivation per entry, reported as
+        [(status, dropped act, dropped silo)] -- INSERTED, SAME (that ActivationId holds the grain),
+        DROPPED (another activation holds it: first registration wins; or the silo is not valid),
+        HOST (a multi-activation entry on either side)."""
+        out = []
+        keys = [tuple(int(x) for x in k) for k in keys]
+        pre = [self.entries.get(k) for k in keys]
+        pre = [None if e is None else list(e) for e in pre]
+        res = self.register(keys, acts, silos)
+        for k, a, s, e0, (ga, gs, ins) in zip(keys, acts, silos, pre, res):
+            a = int(a)
+            if a == ACT_MULTI or ga == ACT_MULTI:
+                out.append((MERGE_HOST, M32, M32))
+            elif ins:
+                out.append((MERGE_INSERTED, M32, M32))
+            elif ga == M32:
+                out.append((MERGE_DROPPED, M32, M32))
+            elif self.ids.get(ga) == self.ids.get(a):
+                out.append((MERGE_SAME, M32, M32))
+            else:
+                out.append((MERGE_DROPPED, ga, gs))
         return out
 
     def as_arrays(self):

@@ -171,12 +171,15 @@ __device__ __forceinline__ int key_cmp(const gd_key& a, const gd_key& b) {
 
 // GD_MERGE_* statuses (include/graindispatch.h)
 constexpr uint8_t MERGE_INSERTED = 0, MERGE_KEPT = 1, MERGE_SAME = 2, MERGE_DROPPED = 3, MERGE_HOST = 4;
+constexpr uint32_t MERGE_TAG_MULTI = 0x80000000u;   // GD_MERGE_TAG_MULTI_INSTANCE
 
 // One item per grain (k_dup_mark); slot_of / is_new from k_reg_claim.  out_dropped[i] = the
 // activation Catalog.DeleteActivations gets (KEPT: the displaced entry, DROPPED: the incoming
 // one), else none.  ids[act] = the
 // ActivationId of host activation index act (gd_activation_ids_set); an index without one sets
-// err bit 16.  in_tags: the incoming entries' VersionTags (NULL: a new tag).
+// err bit 16.  in_tags: the incoming entries' VersionTags (NULL: a new tag); bit 31 (MERGE_TAG_MULTI)
+// marks an incoming GrainInfo whose SingleInstance is false (an AddActivation grain with one
+// instance), which partitionData.Add keeps as it is (:517-520).
 __global__ void __launch_bounds__(BLOCK) k_merge_apply(const gd_key* __restrict__ keys,
                                                        const gd_val* __restrict__ vals,
                                                        const int32_t* __restrict__ in_tags, uint32_t n,
@@ -198,7 +201,8 @@ __global__ void __launch_bounds__(BLOCK) k_merge_apply(const gd_key* __restrict_
         if (is_new[i]) {                              // partitionData.Add(pair.Key, pair.Value) (:509-512)
             sl.act = in.act;
             sl.meta = make_meta(SLOT_LIVE, in.silo);
-            const uint32_t single = in.act == GD_ACT_MULTI ? 0u : VTAG_SINGLE;
+            const bool in_multi = in_tags && ((uint32_t)in_tags[i] & MERGE_TAG_MULTI);
+            const uint32_t single = (in.act == GD_ACT_MULTI || in_multi) ? 0u : VTAG_SINGLE;
             vtag[s] = single | (in_tags ? ((uint32_t)in_tags[i] & 0x7FFFFFFFu) : version_tag(op, h));
             atomicAdd(&ctr->live, 1ull);
             st = MERGE_INSERTED;
@@ -211,6 +215,8 @@ __global__ void __launch_bounds__(BLOCK) k_merge_apply(const gd_key* __restrict_
             } else if (cur >= n_ids || in.act >= n_ids) {
                 atomicOr(&ctr->err, 16u);
                 st = MERGE_HOST;
+            } else if (key_cmp(ids[in.act], ids[cur]) == 0) {
+                st = MERGE_SAME;                      // the same ActivationId under another host index
             } else {
                 // modified: VersionTag = rand.Next() (:154-157), then keep the lowest ActivationId (:159-176)
                 const bool in_wins = key_cmp(ids[in.act], ids[cur]) < 0;
@@ -229,6 +235,101 @@ __global__ void __launch_bounds__(BLOCK) k_merge_apply(const gd_key* __restrict_
     }
     out_status[i] = st;
     if (out_dropped) out_dropped[i] = dropped;
+}
+
+// ---- the multi-rank handoff (gd_dir_handoff_multi) -----------------------------------------------
+// Split entries with what travels: the ActivationId of their activation index (ids[act]; none for a
+// multi-activation entry) and their VersionTag in the public merge form (bit 31 = not SingleInstance).
+// `flag` / `pos` from k_split_mark + scan, as k_split_emit; move = tombstone the slot.
+__global__ void __launch_bounds__(BLOCK) k_split_emit_tagged(Slot* __restrict__ slots, unsigned long long cap,
+                                                             const uint32_t* __restrict__ flag,
+                                                             const uint32_t* __restrict__ pos, int move,
+                                                             const uint32_t* __restrict__ vtag,
+                                                             const gd_key* __restrict__ ids, unsigned long long n_ids,
+                                                             gd_key* __restrict__ out_keys, gd_key* __restrict__ out_ids,
+                                                             uint32_t* __restrict__ out_silo,
+                                                             uint32_t* __restrict__ out_tag, DevCounters* ctr) {
+    const unsigned long long i = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= cap || !flag[i]) return;
+    const Slot sl = slots[i];
+    const uint32_t p = pos[i];
+    out_keys[p] = gd_key{sl.n0, sl.n1, sl.tcd};
+    gd_key id{0, 0, 0};
+    if (sl.act != GD_ACT_MULTI) {
+        if (sl.act < n_ids) id = ids[sl.act];
+        else atomicOr(&ctr->err, 16u);
+    }
+    out_ids[p] = id;
+    out_silo[p] = sl.act == GD_ACT_MULTI ? (slot_silo(sl.meta) | 0x80000000u) : slot_silo(sl.meta);
+    const uint32_t t = vtag[i];
+    out_tag[p] = (t & 0x7FFFFFFFu) | ((t & VTAG_SINGLE) ? 0u : MERGE_TAG_MULTI);
+    if (move) {
+        slots[i].meta = make_meta(SLOT_TOMB, 0);
+        atomicAdd(&ctr->live, ~0ull);
+        atomicAdd(&ctr->tomb, 1ull);
+    }
+}
+
+// Partition order: the split's fields by the positions k_shard_scatter left (send_idx).
+__global__ void __launch_bounds__(BLOCK) k_gather_handoff(const uint32_t* __restrict__ idx, uint32_t n,
+                                                          const gd_key* __restrict__ ids,
+                                                          const uint32_t* __restrict__ silo,
+                                                          const uint32_t* __restrict__ tag,
+                                                          gd_key* __restrict__ o_ids, uint32_t* __restrict__ o_silo,
+                                                          uint32_t* __restrict__ o_tag) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t j = idx[i];
+    o_ids[i] = ids[j];
+    o_silo[i] = silo[j];
+    o_tag[i] = tag[j];
+}
+
+// Received entries take the receiver's activation indices act_base + j (their ActivationIds are
+// appended to its index -> ActivationId map); multi-activation entries stay GD_ACT_MULTI.
+__global__ void __launch_bounds__(BLOCK) k_handoff_vals(const gd_key* __restrict__ rids,
+                                                        const uint32_t* __restrict__ rsilo, uint32_t m,
+                                                        uint32_t act_base, gd_key* __restrict__ ids,
+                                                        gd_val* __restrict__ vals, uint32_t* __restrict__ acts) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= m) return;
+    const uint32_t s = rsilo[j];
+    const bool multi = s & 0x80000000u;
+    const uint32_t a = multi ? GD_ACT_MULTI : act_base + j;
+    vals[j] = gd_val{a, s & 0xFFFFu};
+    acts[j] = a;
+    if (!multi) ids[act_base + j] = rids[j];
+}
+
+// ProcessSiloAddEvent's RegisterMany(singleActivation: true) on the receiver (first registration
+// wins, AddSingleActivation :304-326): INSERTED, SAME (the same ActivationId was there), DROPPED
+// (another activation holds the grain: the incoming one is not registered; dropped = the holder),
+// HOST (a multi-activation entry: C# unions its instances).
+__global__ void __launch_bounds__(BLOCK) k_handoff_add_status(const gd_val* __restrict__ in,
+                                                              const gd_val* __restrict__ got,
+                                                              const uint8_t* __restrict__ ins, uint32_t m,
+                                                              const gd_key* __restrict__ ids,
+                                                              unsigned long long n_ids, uint8_t* __restrict__ status,
+                                                              gd_val* __restrict__ dropped) {
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= m) return;
+    const gd_val v = in[j], g = got[j];
+    uint8_t st;
+    gd_val d{NONE32, NONE32};
+    if (v.act == GD_ACT_MULTI || g.act == GD_ACT_MULTI) {
+        st = MERGE_HOST;
+    } else if (ins[j]) {
+        st = MERGE_INSERTED;
+    } else if (g.act == NONE32) {
+        st = MERGE_DROPPED;                          // refused: the silo is not valid (IsValidSilo)
+    } else if (g.act < n_ids && v.act < n_ids && key_cmp(ids[g.act], ids[v.act]) == 0) {
+        st = MERGE_SAME;
+    } else {
+        st = MERGE_DROPPED;
+        d = g;
+    }
+    status[j] = st;
+    dropped[j] = d;
 }
 
 }  // namespace gd

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -145,6 +146,18 @@ struct gd_handle {
     uint32_t* h_xcnt = nullptr;       // pinned: send/recv message counts, send/recv KeyExt byte counts,
                                       // key descriptors (mine, every peer's), forward counts (12 x 256)
     gd_multi_result mres[2] = {};
+    // sharded fan-out cascade (gd_fanout_multi_device): per hop the frontier and the owner-side
+    // results, kept for the caller; shared expansion / partition scratch
+    std::vector<std::array<DevBuf, 10>> fm_hop;
+    std::vector<gd_fanout_hop> fm_res;
+    uint32_t fm_n_act = 0;
+    DevBuf fm_scr[6];                 // expand target / sender, partitioned target / sender, counts, visited
+    DevBuf fm_graph[3];               // host-form entry point: row_off, dst, seeds
+    // multi-rank directory handoff (gd_dir_handoff_multi): split / send scratch, received entries
+    DevBuf ho_send[10];
+    DevBuf ho_recv[11];
+    gd_handoff_result ho_res{};
+    bool ho_valid = false;
     uint32_t mres_n[2] = {0, 0};
     uint64_t mcalls = 0;
     uint64_t routed = 0;
@@ -2756,6 +2769,15 @@ void comm_release(gd_handle* h) {
     free_buf(h->mx_keys);
     for (DevBuf& b : h->mx_ext) free_buf(b);
     for (DevBuf& b : h->x_scratch) free_buf(b);
+    for (auto& hop : h->fm_hop)
+        for (DevBuf& b : hop) free_buf(b);
+    h->fm_hop.clear();
+    h->fm_res.clear();
+    for (DevBuf& b : h->fm_scr) free_buf(b);
+    for (DevBuf& b : h->fm_graph) free_buf(b);
+    for (DevBuf& b : h->ho_send) free_buf(b);
+    for (DevBuf& b : h->ho_recv) free_buf(b);
+    h->ho_valid = false;
     if (h->h_xcnt) (void)hipHostFree(h->h_xcnt);
     h->h_xcnt = nullptr;
     h->x_done_rec[0] = h->x_done_rec[1] = false;
@@ -3311,6 +3333,205 @@ int gd_multi_fetch(gd_handle* h, gd_key* recv_keys, uint32_t* recv_idx, uint32_t
     return sync(h);
 }
 
+// ================================================================== sharded fan-out cascade (SURVEY 8 f2 + 8 e)
+// BASELINE cfg 4 across GPUs: ChirperAccount.PublishMessage (ChirperAccount.cs:106-147) on every
+// rank for the publishers it owns; each NewChirp goes to its follower's directory owner over the
+// library's communicator (OutboundMessageQueue.cs:54-131 per target silo), is routed there and
+// enqueued on the follower's activation in arrival order (sender rank, sender emission order).
+namespace {
+
+// counts[W] (device, this rank's sends per peer) -> host send / receive counts; one grouped round.
+int counts_round(gd_handle* h, uint32_t* dcnt, std::vector<uint32_t>& sc, std::vector<uint32_t>& rc) {
+    const int W = h->n_ranks;
+    const Rccl& R = *h->net;
+    NCCL_TRY(h, R.GroupStart());
+    for (int r = 0; r < W; ++r) {
+        NCCL_TRY(h, R.Send(dcnt + r, 1, ncclUint32, r, h->comm, h->stream));
+        NCCL_TRY(h, R.Recv(dcnt + W + r, 1, ncclUint32, r, h->comm, h->stream));
+    }
+    NCCL_TRY(h, R.GroupEnd());
+    uint32_t* hc = h->h_xcnt + 11 * 256;
+    HIP_TRY(h, hipMemcpyAsync(hc, dcnt, (size_t)W * 8, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    ncclResult_t async_err = ncclSuccess;
+    NCCL_TRY(h, R.CommGetAsyncError(h->comm, &async_err));
+    if (async_err != ncclSuccess) return set_err(h, GD_ERCCL, "RCCL async error: %s", R.GetErrorString(async_err));
+    sc.assign(hc, hc + W);
+    rc.assign(hc + W, hc + 2 * W);
+    return GD_OK;
+}
+
+int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint32_t n_nodes, const uint32_t* seeds,
+                 uint32_t n_seeds, int32_t type_code, uint32_t n_act, uint32_t hops, gd_fanout_hop* out) {
+    GD_TRY(need_comm(h));
+    GD_TRY(check_ring(h));
+    if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    const int W = h->n_ranks;
+    const uint64_t tcd = grain_tcd(type_code);
+    GD_TRY(sync(h));                                   // the previous call's results may be in use
+    if (h->fm_hop.size() < hops) h->fm_hop.resize(hops);
+    h->fm_res.assign(hops, gd_fanout_hop{});
+    h->fm_n_act = n_act;
+    DevBuf* S = h->fm_scr;
+    GD_TRY(ensure(h, S[4], (size_t)W * 8 + 16));
+    GD_TRY(ensure(h, S[5], (size_t)n_act + 16));
+    uint32_t* dcnt = (uint32_t*)S[4].p;
+    uint8_t* visited = (uint8_t*)S[5].p;
+    HIP_TRY(h, hipMemsetAsync(visited, 0, (size_t)n_act + 16, h->stream));
+    // hop 0's publishers: the seeds this rank owns, in seed order (a stable partition of the seeds by
+    // owner rank, then this rank's chunk)
+    uint32_t nf = 0;
+    {
+        std::array<DevBuf, 10>& H0 = h->fm_hop[0];
+        GD_TRY(ensure(h, S[0], (size_t)n_seeds * 4 + 16));
+        GD_TRY(ensure(h, S[1], (size_t)n_seeds * 4 + 16));
+        GD_TRY(shard_pack<true>(h, seeds, seeds, n_seeds, tcd, (uint32_t)W, S[0].p, (uint32_t*)S[1].p, dcnt));
+        uint32_t* hc = h->h_xcnt + 11 * 256;
+        HIP_TRY(h, hipMemcpyAsync(hc, dcnt, (size_t)W * 4, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+        uint64_t lo = 0;
+        for (int r = 0; r < h->rank; ++r) lo += hc[r];
+        nf = hc[h->rank];
+        GD_TRY(ensure(h, H0[0], ((size_t)std::max(nf, n_act) + 4) * 4));
+        if (nf) {
+            HIP_TRY(h, hipMemcpyAsync(H0[0].p, (const uint32_t*)S[0].p + lo, (size_t)nf * 4, hipMemcpyDeviceToDevice,
+                                      h->stream));
+            GD_TRY(launch(h, "k_mark_visited", dim3(blocks_for(nf, BLOCK)), dim3(BLOCK), 0, k_mark_visited,
+                          (const uint32_t*)H0[0].p, nf, n_act, visited));
+        }
+    }
+    for (uint32_t hp = 0; hp < hops; ++hp) {
+        std::array<DevBuf, 10>& H = h->fm_hop[hp];
+        const uint32_t* frontier = (const uint32_t*)H[0].p;
+        gd_fanout_hop& res = h->fm_res[hp];
+        res.n_frontier = nf;
+        res.frontier = frontier;
+        // 1. expand this rank's publishers (follower lists in enumeration order)
+        uint64_t total = 0;
+        GD_TRY(fan_count(h, row_off, n_nodes, frontier, nf, &total));
+        const uint32_t n = (uint32_t)total;
+        res.n_sent = total;
+        GD_TRY(ensure(h, S[0], (size_t)n * 4 + 16));
+        GD_TRY(ensure(h, S[1], (size_t)n * 4 + 16));
+        GD_TRY(ensure(h, S[2], (size_t)n * 4 + 16));
+        GD_TRY(ensure(h, S[3], (size_t)n * 4 + 16));
+        if (n)
+            GD_TRY(launch(h, "k_fan_expand", dim3(blocks_for(n, FAN_TILE)), dim3(BLOCK), 0, k_fan_expand, row_off,
+                          dst, frontier, nf, (const uint32_t*)h->fan[0].p, n, (uint32_t*)S[0].p, (uint32_t*)S[1].p));
+        // 2. stable partition of (target, sender) by the target's owner rank
+        GD_TRY(shard_pack<true>(h, S[0].p, (const uint32_t*)S[1].p, n, tcd, (uint32_t)W, S[2].p, (uint32_t*)S[3].p,
+                                dcnt));
+        // 3. counts, then one grouped round of 8 B a message
+        std::vector<uint32_t> sc, rc;
+        GD_TRY(counts_round(h, dcnt, sc, rc));
+        std::vector<uint64_t> soff(W + 1, 0), roff(W + 1, 0);
+        for (int r = 0; r < W; ++r) {
+            soff[r + 1] = soff[r] + sc[r];
+            roff[r + 1] = roff[r] + rc[r];
+        }
+        if (soff[W] != n)
+            return set_err(h, GD_ERCCL, "fan-out partition counts sum to %llu, hop emitted %u",
+                           (unsigned long long)soff[W], n);
+        if (roff[W] >= 0xFFFFFFFFull)
+            return set_err(h, GD_EINVAL, "%llu messages received in one hop", (unsigned long long)roff[W]);
+        const uint32_t m = (uint32_t)roff[W];
+        const size_t m4 = (size_t)m * 4 + 16;
+        const size_t want[10] = {0, m4, m4, m4, m4, m4, (size_t)m + 16, m4, ((size_t)n_act + 2) * 4, 0};
+        for (int b = 1; b < 9; ++b) GD_TRY(ensure(h, H[b], want[b]));
+        uint32_t* target = (uint32_t*)H[1].p;
+        uint32_t* sender = (uint32_t*)H[2].p;
+        uint32_t* src = (uint32_t*)H[3].p;
+        uint32_t* silo = (uint32_t*)H[4].p;
+        uint32_t* act = (uint32_t*)H[5].p;
+        uint8_t* st = (uint8_t*)H[6].p;
+        uint32_t* perm = (uint32_t*)H[7].p;
+        uint32_t* offs = (uint32_t*)H[8].p;
+        const Lane lanes[2] = {{S[2].p, target, 4, ncclUint32, 1}, {S[3].p, sender, 4, ncclUint32, 1}};
+        GD_TRY(exchange_round(h, "rccl_fanout", sc.data(), soff.data(), rc.data(), roff.data(), lanes, 2));
+        if (m)
+            GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
+                          (const uint32_t*)(dcnt + W), (uint32_t)W, m, src));
+        // 4. route + bucket on the owner
+        if (m) GD_TRY(route_nodes(h, target, m, tcd, silo, act, st));
+        GD_TRY(bucket_device(h, act, m, n_act, perm, offs));
+        res.n_recv = m;
+        res.target = target;
+        res.sender = sender;
+        res.src = src;
+        res.silo = silo;
+        res.act = act;
+        res.status = st;
+        res.perm = perm;
+        res.offsets = offs;
+        // 5. the next publishers: this rank's activations that got a chirp and have not published
+        if (hp + 1 < hops) {
+            std::array<DevBuf, 10>& N = h->fm_hop[hp + 1];
+            GD_TRY(ensure(h, N[0], ((size_t)n_act + 4) * 4));
+            GD_TRY(frontier_next(h, offs, n_act, visited, (uint32_t*)N[0].p, &nf));
+        }
+    }
+    if (out) std::copy(h->fm_res.begin(), h->fm_res.end(), out);
+    return GD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gd_fanout_multi_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_nodes,
+                           const uint32_t* d_seeds, uint32_t n_seeds, int32_t type_code, uint32_t n_act, uint32_t hops,
+                           gd_fanout_hop* out) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (n_seeds && !d_seeds) return set_err(h, GD_EINVAL, "null seeds");
+    if (!d_row_off || (!d_dst && n_nodes)) return set_err(h, GD_EINVAL, "null graph");
+    if (hops == 0 || hops > 64) return set_err(h, GD_EINVAL, "hops %u not in [1, 64]", hops);
+    HIP_TRY(h, hipSetDevice(h->device));
+    return fanout_multi(h, d_row_off, d_dst, n_nodes, d_seeds, n_seeds, type_code, n_act, hops, out);
+}
+
+int gd_fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint32_t n_nodes,
+                    const uint32_t* seeds, uint32_t n_seeds, int32_t type_code, uint32_t n_act, uint32_t hops,
+                    gd_fanout_hop* out) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (!row_off || (n_seeds && !seeds)) return set_err(h, GD_EINVAL, "null argument");
+    if (hops == 0 || hops > 64) return set_err(h, GD_EINVAL, "hops %u not in [1, 64]", hops);
+    HIP_TRY(h, hipSetDevice(h->device));
+    const uint64_t edges = row_off[n_nodes];
+    if (edges && !dst) return set_err(h, GD_EINVAL, "null graph");
+    GD_TRY(h2d(h, h->fm_graph[0], row_off, (size_t)n_nodes + 1));
+    GD_TRY(h2d(h, h->fm_graph[1], dst ? dst : row_off, edges ? edges : 1));
+    GD_TRY(h2d(h, h->fm_graph[2], seeds ? seeds : row_off, n_seeds ? n_seeds : 1));
+    GD_TRY(fanout_multi(h, (const uint32_t*)h->fm_graph[0].p, (const uint32_t*)h->fm_graph[1].p, n_nodes,
+                        (const uint32_t*)h->fm_graph[2].p, n_seeds, type_code, n_act, hops, out));
+    return sync_checked(h);
+}
+
+int gd_fanout_multi_fetch(gd_handle* h, uint32_t hop, uint32_t* frontier, uint32_t* target, uint32_t* sender,
+                          uint32_t* src, uint32_t* silo, uint32_t* act, uint8_t* status, uint32_t* perm,
+                          uint32_t* offsets) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (hop >= h->fm_res.size()) return set_err(h, GD_ESTATE, "no hop %u in the last gd_fanout_multi* result", hop);
+    HIP_TRY(h, hipSetDevice(h->device));
+    const gd_fanout_hop& r = h->fm_res[hop];
+    const size_t m = r.n_recv;
+    auto cp = [&](void* d, const void* s, size_t bytes) -> int {
+        if (d && bytes) HIP_TRY(h, hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToHost, h->stream));
+        return GD_OK;
+    };
+    GD_TRY(cp(frontier, r.frontier, (size_t)r.n_frontier * 4));
+    GD_TRY(cp(target, r.target, m * 4));
+    GD_TRY(cp(sender, r.sender, m * 4));
+    GD_TRY(cp(src, r.src, m * 4));
+    GD_TRY(cp(silo, r.silo, m * 4));
+    GD_TRY(cp(act, r.act, m * 4));
+    GD_TRY(cp(status, r.status, m));
+    GD_TRY(cp(perm, r.perm, m * 4));
+    GD_TRY(cp(offsets, r.offsets, ((size_t)h->fm_n_act + 2) * 4));
+    return sync(h);
+}
+
+}  // extern "C"
+
 // ================================================================== KeyExt grains (gd_keyext.h)
 namespace {
 
@@ -3779,6 +4000,23 @@ int set_bitset(gd_handle* h, DevBuf& b, const std::vector<uint32_t>& bits) {
     return GD_OK;
 }
 
+// Room for activation indices [0, need) in the index -> ActivationId map, keeping the ids set.
+int grow_act_ids(gd_handle* h, uint64_t need) {
+    if (need <= h->n_act_ids) return GD_OK;
+    DevBuf nb;
+    size_t cap = std::max<size_t>(need, 2 * h->n_act_ids) * sizeof(gd_key);
+    GD_TRY(ensure(h, nb, cap));
+    HIP_TRY(h, hipMemsetAsync(nb.p, 0, cap, h->stream));
+    if (h->n_act_ids)
+        HIP_TRY(h, hipMemcpyAsync(nb.p, h->act_ids.p, h->n_act_ids * sizeof(gd_key), hipMemcpyDeviceToDevice,
+                                  h->stream));
+    GD_TRY(sync(h));
+    free_buf(h->act_ids);
+    h->act_ids = nb;
+    h->n_act_ids = cap / sizeof(gd_key);
+    return GD_OK;
+}
+
 int check_dir_err(gd_handle* h, const char* what) {
     GD_TRY(pull_counters(h));
     if (h->ctr_host.err) {
@@ -3791,6 +4029,46 @@ int check_dir_err(gd_handle* h, const char* what) {
         return set_err(h, GD_EINVAL, "%s: device error bits 0x%x", what, e);
     }
     return GD_OK;
+}
+
+// GrainDirectoryPartition.Merge over device arrays (one item per grain): claims, the duplicate
+// check, then k_merge_apply.  Synchronous up to the apply (which stays enqueued); errors through
+// check_dir_err.
+int merge_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, const int32_t* dtags, uint32_t n,
+               uint8_t* d_status, gd_val* d_dropped) {
+    GD_TRY(maybe_grow_table(h, n));
+    const uint32_t op = ++h->dir_op;
+    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));   // slot_of
+    GD_TRY(ensure(h, h->u8_a, (size_t)n));        // is_new
+    if (h->up_last.bytes < h->capacity * 4) {
+        GD_TRY(ensure(h, h->up_last, h->capacity * 4));
+        HIP_TRY(h, hipMemsetAsync(h->up_last.p, 0, h->up_last.bytes, h->stream));
+    }
+    HIP_TRY(h, hipMemsetAsync(h->u8_a.p, 0, n, h->stream));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    uint32_t* slot_of = (uint32_t*)h->u32_a.p;
+    uint8_t* is_new = (uint8_t*)h->u8_a.p;
+    for (uint32_t pass = 0;; ++pass) {            // the registration's claim protocol; no IsValidSilo check in Merge
+        HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
+        GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, h->capacity - 1, h->ctr, slot_of,
+                      is_new, (uint32_t)(pass > 0), (const gd_val*)nullptr, table_args(h)));
+        GD_TRY(pull_counters(h));
+        if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
+        if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_merge: claims did not settle");
+    }
+    uint32_t* last = (uint32_t*)h->up_last.p;
+    GD_TRY(launch(h, "k_dup_mark", g, b, 0, k_dup_mark, (const uint32_t*)slot_of, n, last, h->ctr));
+    GD_TRY(launch(h, "k_up_clear", g, b, 0, k_up_clear, (const uint32_t*)slot_of, n, last));
+    GD_TRY(pull_counters(h));
+    if (h->ctr_host.err) {
+        // a duplicated grain: the pending claims of this batch must not stay half-made
+        GD_TRY(launch(h, "k_reg_abort", g, b, 0, k_reg_abort, (const uint32_t*)slot_of, (const uint8_t*)is_new, n,
+                      h->slots, h->ctr));
+        return check_dir_err(h, "gd_dir_merge");
+    }
+    return launch(h, "k_merge_apply", g, b, 0, k_merge_apply, dk, dvals, dtags, n, (const uint32_t*)slot_of,
+                  (const uint8_t*)is_new, h->slots, h->vtag, h->ctr, (const gd_key*)h->act_ids.p,
+                  (unsigned long long)h->n_act_ids, op, d_status, d_dropped);
 }
 
 }  // namespace
@@ -3901,19 +4179,7 @@ int gd_activation_ids_set(gd_handle* h, const uint32_t* acts, const gd_key* ids,
         if (acts[i] >= GD_ACT_MULTI) return set_err(h, GD_EINVAL, "activation index %u reserved", acts[i]);
         need = std::max<uint64_t>(need, (uint64_t)acts[i] + 1);
     }
-    if (need > h->n_act_ids) {        // grow, keeping the ids already set
-        DevBuf nb;
-        size_t cap = std::max<size_t>(need, 2 * h->n_act_ids) * sizeof(gd_key);
-        GD_TRY(ensure(h, nb, cap));
-        HIP_TRY(h, hipMemsetAsync(nb.p, 0, cap, h->stream));
-        if (h->n_act_ids)
-            HIP_TRY(h, hipMemcpyAsync(nb.p, h->act_ids.p, h->n_act_ids * sizeof(gd_key), hipMemcpyDeviceToDevice,
-                                      h->stream));
-        GD_TRY(sync(h));
-        free_buf(h->act_ids);
-        h->act_ids = nb;
-        h->n_act_ids = cap / sizeof(gd_key);
-    }
+    GD_TRY(grow_act_ids(h, need));
     // scatter on the host side of a staging copy (small batches: registration is off the hot path)
     GD_TRY(h2d(h, h->dirop_buf[0], acts, n));
     GD_TRY(h2d(h, h->dirop_buf[1], ids, n));
@@ -3929,50 +4195,177 @@ int gd_dir_merge(gd_handle* h, const gd_key* keys, const gd_val* vals, const int
         if (vals[i].silo > 0xFFFEu) return set_err(h, GD_EINVAL, "silo index %u out of range at %u", vals[i].silo, i);
     if (n == 0) return GD_OK;
     HIP_TRY(h, hipSetDevice(h->device));
-    GD_TRY(maybe_grow_table(h, n));
-    const uint32_t op = ++h->dir_op;
     GD_TRY(h2d(h, h->keys_in, keys, n));
     GD_TRY(h2d(h, h->out_c, vals, n));
     if (tags) GD_TRY(h2d(h, h->dirop_buf[1], tags, n));
-    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));   // slot_of
-    GD_TRY(ensure(h, h->u8_a, (size_t)n));        // is_new
     GD_TRY(ensure(h, h->out_b, (size_t)n));
     GD_TRY(ensure(h, h->out_a, (size_t)n * sizeof(gd_val)));
-    if (h->up_last.bytes < h->capacity * 4) {
-        GD_TRY(ensure(h, h->up_last, h->capacity * 4));
-        HIP_TRY(h, hipMemsetAsync(h->up_last.p, 0, h->up_last.bytes, h->stream));
-    }
-    HIP_TRY(h, hipMemsetAsync(h->u8_a.p, 0, n, h->stream));
-    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
-    uint32_t* slot_of = (uint32_t*)h->u32_a.p;
-    uint8_t* is_new = (uint8_t*)h->u8_a.p;
-    const gd_key* dk = (const gd_key*)h->keys_in.p;
-    for (uint32_t pass = 0;; ++pass) {            // the registration's claim protocol; no IsValidSilo check in Merge
-        HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
-        GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, h->capacity - 1, h->ctr, slot_of,
-                      is_new, (uint32_t)(pass > 0), (const gd_val*)nullptr, table_args(h)));
-        GD_TRY(pull_counters(h));
-        if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
-        if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_merge: claims did not settle");
-    }
-    uint32_t* last = (uint32_t*)h->up_last.p;
-    GD_TRY(launch(h, "k_dup_mark", g, b, 0, k_dup_mark, (const uint32_t*)slot_of, n, last, h->ctr));
-    GD_TRY(launch(h, "k_up_clear", g, b, 0, k_up_clear, (const uint32_t*)slot_of, n, last));
-    GD_TRY(pull_counters(h));
-    if (h->ctr_host.err) {
-        // a duplicated grain: the pending claims of this batch must not stay half-made
-        GD_TRY(launch(h, "k_reg_abort", g, b, 0, k_reg_abort, (const uint32_t*)slot_of, (const uint8_t*)is_new, n,
-                      h->slots, h->ctr));
-        return check_dir_err(h, "gd_dir_merge");
-    }
-    GD_TRY(launch(h, "k_merge_apply", g, b, 0, k_merge_apply, dk, (const gd_val*)h->out_c.p,
-                  tags ? (const int32_t*)h->dirop_buf[1].p : (const int32_t*)nullptr, n, (const uint32_t*)slot_of,
-                  (const uint8_t*)is_new, h->slots, h->vtag, h->ctr, (const gd_key*)h->act_ids.p,
-                  (unsigned long long)h->n_act_ids, op, (uint8_t*)h->out_b.p, (gd_val*)h->out_a.p));
+    GD_TRY(merge_core(h, (const gd_key*)h->keys_in.p, (const gd_val*)h->out_c.p,
+                      tags ? (const int32_t*)h->dirop_buf[1].p : nullptr, n, (uint8_t*)h->out_b.p,
+                      (gd_val*)h->out_a.p));
     HIP_TRY(h, hipMemcpyAsync(out_status, h->out_b.p, n, hipMemcpyDeviceToHost, h->stream));
     if (out_dropped)
         HIP_TRY(h, hipMemcpyAsync(out_dropped, h->out_a.p, (size_t)n * sizeof(gd_val), hipMemcpyDeviceToHost, h->stream));
     return check_dir_err(h, "gd_dir_merge");
+}
+
+}  // extern "C"
+
+// ================================================================== multi-rank directory handoff (SURVEY 8 f4 over 8 e)
+// A membership change moves directory entries between the ranks' partitions: every rank splits off
+// the entries whose new owner (the installed ring) lives on another rank, they travel in one grouped
+// round with their ActivationId and VersionTag, and the receiver applies them the way the reference
+// distinguishes the two events (GrainDirectoryHandoffManager.cs):
+//   GD_HANDOFF_ADD     ProcessSiloAddEvent (:195-245): RegisterMany(singleActivation: true) on the new
+//                      owner -- AddSingleActivation, the first registration wins (:304-326)
+//   GD_HANDOFF_REMOVE  ProcessSiloRemoveEvent (:125-158): GrainDirectoryPartition.Merge of the removed
+//                      silo's partition (:497-522) -- GrainInfo.Merge keeps the lowest ActivationId
+//                      (:139-179) and the loser goes to Catalog.DeleteActivations on its silo
+namespace {
+
+int handoff_multi(gd_handle* h, const uint8_t* keep, uint32_t n_keep, int event, uint32_t act_base,
+                  gd_handoff_result* out) {
+    GD_TRY(need_comm(h));
+    GD_TRY(check_ring(h));
+    const int W = h->n_ranks;
+    GD_TRY(sync(h));
+    h->ho_valid = false;
+    // 1. split: the entries this rank no longer owns, with ActivationId and tag, removed here
+    uint64_t total = 0;
+    GD_TRY(split_count(h, keep, n_keep, &total));
+    if (total >= 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "handoff of %llu entries", (unsigned long long)total);
+    const uint32_t n = (uint32_t)total;
+    DevBuf* S = h->ho_send;
+    const size_t n4 = (size_t)n * 4 + 16, nk = (size_t)n * sizeof(gd_key) + 16;
+    const size_t want_s[10] = {nk, nk, n4, n4, nk, n4, nk, (size_t)W * 8 + 16, n4, n4};
+    for (int b = 0; b < 10; ++b) GD_TRY(ensure(h, S[b], want_s[b]));
+    gd_key* keys = (gd_key*)S[0].p;             // split (slot) order
+    gd_key* ids = (gd_key*)S[1].p;
+    uint32_t* silo = (uint32_t*)S[2].p;
+    uint32_t* tag = (uint32_t*)S[3].p;
+    gd_key* send_keys = (gd_key*)S[4].p;        // partition order
+    uint32_t* send_idx = (uint32_t*)S[5].p;
+    gd_key* send_ids = (gd_key*)S[6].p;
+    uint32_t* dcnt = (uint32_t*)S[7].p;
+    uint32_t* send_silo = (uint32_t*)S[8].p;
+    uint32_t* send_tag = (uint32_t*)S[9].p;
+    if (n) {
+        const unsigned long long cap = h->capacity;
+        GD_TRY(launch(h, "k_split_emit_tagged", dim3(blocks_for(cap, BLOCK)), dim3(BLOCK), 0, k_split_emit_tagged,
+                      h->slots, cap, (const uint32_t*)h->churn[1].p, (const uint32_t*)h->churn[2].p, 1,
+                      (const uint32_t*)h->vtag, (const gd_key*)h->act_ids.p, (unsigned long long)h->n_act_ids, keys,
+                      ids, silo, tag, h->ctr));
+        GD_TRY(check_dir_err(h, "gd_dir_handoff_multi (split)"));
+    }
+    // 2. stable partition by the new owner's rank (slot order kept per destination), fields alongside
+    GD_TRY(shard_pack<false>(h, keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt));
+    if (n)
+        GD_TRY(launch(h, "k_gather_handoff", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_gather_handoff,
+                      (const uint32_t*)send_idx, n, (const gd_key*)ids, (const uint32_t*)silo, (const uint32_t*)tag,
+                      send_ids, send_silo, send_tag));
+    std::vector<uint32_t> sc, rc;
+    // 3. counts, then one grouped round: key 24 B + ActivationId 24 B + silo 4 B + tag 4 B an entry
+    GD_TRY(counts_round(h, dcnt, sc, rc));
+    std::vector<uint64_t> soff(W + 1, 0), roff(W + 1, 0);
+    for (int r = 0; r < W; ++r) {
+        soff[r + 1] = soff[r] + sc[r];
+        roff[r + 1] = roff[r] + rc[r];
+    }
+    if (soff[W] != n)
+        return set_err(h, GD_ERCCL, "handoff partition counts sum to %llu, split %u", (unsigned long long)soff[W], n);
+    if (roff[W] >= 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "%llu entries received", (unsigned long long)roff[W]);
+    const uint32_t m = (uint32_t)roff[W];
+    if ((uint64_t)act_base + m >= GD_ACT_MULTI)
+        return set_err(h, GD_EINVAL, "activation indices %u + %u run into the reserved range", act_base, m);
+    DevBuf* R = h->ho_recv;
+    const size_t m4 = (size_t)m * 4 + 16, mk = (size_t)m * sizeof(gd_key) + 16, mv = (size_t)m * sizeof(gd_val) + 16;
+    const size_t want_r[11] = {mk, mk, m4, m4, m4, m4, (size_t)m + 16, mv, mv, mv, (size_t)m + 16};
+    for (int b = 0; b < 11; ++b) GD_TRY(ensure(h, R[b], want_r[b]));
+    gd_key* rkeys = (gd_key*)R[0].p;
+    gd_key* rids = (gd_key*)R[1].p;
+    uint32_t* rsilo = (uint32_t*)R[2].p;
+    uint32_t* rtag = (uint32_t*)R[3].p;
+    uint32_t* rsrc = (uint32_t*)R[4].p;
+    uint32_t* racts = (uint32_t*)R[5].p;
+    uint8_t* rst = (uint8_t*)R[6].p;
+    gd_val* rdrop = (gd_val*)R[7].p;
+    gd_val* vals = (gd_val*)R[8].p;
+    gd_val* got = (gd_val*)R[9].p;
+    uint8_t* ins = (uint8_t*)R[10].p;
+    const Lane lanes[4] = {{send_keys, rkeys, sizeof(gd_key), ncclUint64, 3},
+                           {send_ids, rids, sizeof(gd_key), ncclUint64, 3},
+                           {send_silo, rsilo, 4, ncclUint32, 1},
+                           {send_tag, rtag, 4, ncclUint32, 1}};
+    GD_TRY(exchange_round(h, "rccl_handoff", sc.data(), soff.data(), rc.data(), roff.data(), lanes, 4));
+    if (m)
+        GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
+                      (const uint32_t*)(dcnt + W), (uint32_t)W, m, rsrc));
+    // 4. apply on the receiver: activation indices act_base + j, then Register or Merge
+    if (m) {
+        GD_TRY(grow_act_ids(h, (uint64_t)act_base + m));
+        GD_TRY(launch(h, "k_handoff_vals", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_handoff_vals,
+                      (const gd_key*)rids, (const uint32_t*)rsilo, m, act_base, (gd_key*)h->act_ids.p, vals, racts));
+        if (event == GD_HANDOFF_REMOVE) {
+            GD_TRY(merge_core(h, rkeys, vals, (const int32_t*)rtag, m, rst, rdrop));
+            GD_TRY(check_dir_err(h, "gd_dir_handoff_multi (merge)"));
+        } else {
+            GD_TRY(register_core(h, rkeys, vals, m, got, ins));
+            GD_TRY(launch(h, "k_handoff_add_status", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_handoff_add_status,
+                          (const gd_val*)vals, (const gd_val*)got, (const uint8_t*)ins, m, (const gd_key*)h->act_ids.p,
+                          (unsigned long long)h->n_act_ids, rst, rdrop));
+        }
+    }
+    GD_TRY(sync(h));
+    gd_handoff_result& r = h->ho_res;
+    r = gd_handoff_result{};
+    r.n_sent = n;
+    r.n_recv = m;
+    r.recv_keys = rkeys;
+    r.recv_ids = rids;
+    r.recv_act = racts;
+    r.recv_silo = rsilo;
+    r.recv_src = rsrc;
+    r.status = rst;
+    r.dropped = rdrop;
+    h->ho_valid = true;
+    if (out) *out = r;
+    return GD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gd_dir_handoff_multi(gd_handle* h, const uint8_t* keep_silo, uint32_t n_keep, int event, uint32_t act_base,
+                         gd_handoff_result* out) {
+    if (!h || (n_keep && !keep_silo)) return set_err(h, GD_EINVAL, "null argument");
+    if (event != GD_HANDOFF_ADD && event != GD_HANDOFF_REMOVE) return set_err(h, GD_EINVAL, "unknown event %d", event);
+    HIP_TRY(h, hipSetDevice(h->device));
+    return handoff_multi(h, keep_silo, n_keep, event, act_base, out);
+}
+
+int gd_dir_handoff_fetch(gd_handle* h, gd_key* keys, gd_key* ids, uint32_t* acts, uint32_t* silos, uint32_t* src,
+                         uint8_t* status, gd_val* dropped) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (!h->ho_valid) return set_err(h, GD_ESTATE, "no gd_dir_handoff_multi result on this handle");
+    HIP_TRY(h, hipSetDevice(h->device));
+    const gd_handoff_result& r = h->ho_res;
+    const size_t m = r.n_recv;
+    auto cp = [&](void* d, const void* sp, size_t bytes) -> int {
+        if (d && bytes) HIP_TRY(h, hipMemcpyAsync(d, sp, bytes, hipMemcpyDeviceToHost, h->stream));
+        return GD_OK;
+    };
+    GD_TRY(cp(keys, r.recv_keys, m * sizeof(gd_key)));
+    GD_TRY(cp(ids, r.recv_ids, m * sizeof(gd_key)));
+    GD_TRY(cp(acts, r.recv_act, m * 4));
+    GD_TRY(cp(silos, r.recv_silo, m * 4));
+    GD_TRY(cp(src, r.recv_src, m * 4));
+    GD_TRY(cp(status, r.status, m));
+    GD_TRY(cp(dropped, r.dropped, m * sizeof(gd_val)));
+    GD_TRY(sync(h));
+    if (silos)                                     // the multi-activation mark is internal
+        for (size_t j = 0; j < m; ++j) silos[j] &= 0xFFFFu;
+    return GD_OK;
 }
 
 }  // extern "C"

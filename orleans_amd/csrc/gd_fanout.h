@@ -358,4 +358,11 @@ __global__ void __launch_bounds__(BLOCK) k_frontier_compact(const uint16_t* __re
     if (blockIdx.x + 1 == nb && threadIdx.x == BLOCK - 1) *total = pos;
 }
 
+// The seeds of a cascade have published: visited[u] = 1 for u < n_act (gd_fanout_multi_device).
+__global__ void __launch_bounds__(BLOCK) k_mark_visited(const uint32_t* __restrict__ nodes, uint32_t n, uint32_t n_act,
+                                                        uint8_t* __restrict__ visited) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n && nodes[i] < n_act) visited[nodes[i]] = 1;
+}
+
 }  // namespace gd

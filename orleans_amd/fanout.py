@@ -12,6 +12,8 @@ activation index in the directory is u (the bench registers it so).
 
 * `FanoutCascade` -- one GPU: per hop one fused expand+route call
   (gd_fanout_route_bucket_device), the activation bucketing, and gd_frontier_next_device.
+* `LibraryFanout` -- N GPUs, the whole sharded cascade inside libgraindispatch
+  (gd_fanout_multi_device over the library's RCCL communicator): the path a C# host drives.
 * `ShardedFanout` -- N GPUs (one process each): the directory is sharded by ring owner as in
   orleans_amd.sharded; each rank expands its own publishers (gd_fanout_expand_device),
   partitions the (target, sender) pairs by owner rank (gd_pack_nodes_by_shard_device),
@@ -180,6 +182,54 @@ class FanoutCascade:
             out.append(HopResult(frontier, target, sender, None, st, silo, act, perm, off))
             frontier = eng.frontier_next(off, self.n_act, visited)
         return out
+
+
+class LibraryHop:
+    """One hop of gd_fanout_multi_device on this rank: counts, plus the library's device pointers
+    (valid until the next cascade on the handle)."""
+
+    def __init__(self, raw: "g.gd_fanout_hop"):
+        self.raw = raw
+        self.n_frontier = int(raw.n_frontier)
+        self.n_recv = int(raw.n_recv)
+        self.n_sent = int(raw.n_sent)
+
+    @property
+    def messages(self) -> int:
+        return self.n_recv
+
+
+class LibraryFanout:
+    """The sharded cascade inside libgraindispatch (gd_comm_init + gd_fanout_multi_device): expand,
+    partition by owner rank, one grouped RCCL send/recv round per hop, route + bucket on the owner,
+    next frontier -- all in the library on the engine's stream.  torch.distributed only hands the
+    RCCL unique id to the other ranks."""
+
+    def __init__(self, engine: DeviceFanoutEngine, graph: FollowerGraph, n_act: int,
+                 group: Optional[dist.ProcessGroup] = None):
+        self.engine, self.graph, self.n_act = engine, graph, n_act
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        uid = torch.zeros(g.GD_COMM_ID_BYTES, dtype=torch.uint8)
+        if rank == 0:
+            uid = torch.frombuffer(bytearray(g.GrainDispatch.comm_unique_id()), dtype=torch.uint8)
+        t = uid.to(engine.device) if dist.get_backend(group) == "nccl" else uid
+        dist.broadcast(t, src=0, group=group)
+        engine.gd.comm_init(bytes(t.cpu().numpy().tobytes()), world, rank)
+
+    def run(self, seeds: torch.Tensor, hops: int) -> List[LibraryHop]:
+        ns = int(seeds.shape[0])
+        with self.engine.context():
+            raw = self.engine.gd.fanout_multi_device(self.graph.row_off.data_ptr(), self.graph.dst.data_ptr(),
+                                                     self.graph.n_nodes, seeds.data_ptr() if ns else 0, ns,
+                                                     self.engine.type_code, self.n_act, hops)
+        return [LibraryHop(r) for r in raw]
+
+    def fetch(self, hops: List[LibraryHop]) -> List[dict]:
+        """Host copies of every hop of the last cascade (gd_fanout_multi_fetch)."""
+        return [self.engine.gd.fanout_multi_fetch(i, h.raw, self.n_act) for i, h in enumerate(hops)]
+
+    def close(self):
+        self.engine.gd.comm_destroy()
 
 
 class ShardedFanout:

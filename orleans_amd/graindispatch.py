@@ -56,6 +56,8 @@ EXPORTED_SYMBOLS = [
     "gd_dir_set_valid_silos", "gd_dir_lookup_tagged", "gd_dir_remove_silos", "gd_activation_ids_set", "gd_dir_merge",
     "gd_actdir_add", "gd_actdir_remove", "gd_actdir_set_flags", "gd_actdir_lookup", "gd_actdir_clear",
     "gd_actdir_count", "gd_receive", "gd_receive_device", "gd_receive_frames_device", "gd_receive_frames",
+    "gd_fanout_multi_device", "gd_fanout_multi", "gd_fanout_multi_fetch", "gd_dir_handoff_multi",
+    "gd_dir_handoff_fetch",
 ]
 
 
@@ -111,6 +113,18 @@ class gd_multi_result(C.Structure):
                                   "ret_silo", "ret_act", "ret_status")]
 
 
+class gd_fanout_hop(C.Structure):
+    _fields_ = [("n_frontier", C.c_uint32), ("frontier", C.c_void_p), ("n_sent", C.c_uint64), ("n_recv", C.c_uint32)] + [
+        (f, C.c_void_p) for f in ("target", "sender", "src", "silo", "act", "status", "perm", "offsets")]
+
+
+class gd_handoff_result(C.Structure):
+    _fields_ = [("n_sent", C.c_uint64), ("n_recv", C.c_uint32)] + [
+        (f, C.c_void_p) for f in ("recv_keys", "recv_ids", "recv_act", "recv_silo", "recv_src", "status", "dropped")]
+
+
+GD_HANDOFF_ADD, GD_HANDOFF_REMOVE = 0, 1
+GD_MERGE_TAG_MULTI_INSTANCE = 0x80000000
 GD_MERGE_INSERTED, GD_MERGE_KEPT, GD_MERGE_SAME, GD_MERGE_DROPPED, GD_MERGE_HOST = 0, 1, 2, 3, 4
 ACTDIR_VALID, ACTDIR_SYSTEM_TARGET, ACTDIR_STATELESS_WORKER = 1, 2, 4
 (RECV_ACTIVATION, RECV_SYSTEM_TARGET, RECV_NULL_CONTEXT, RECV_REJECT_UNKNOWN, RECV_REJECT_OVERLOADED, RECV_DROPPED,
@@ -289,6 +303,11 @@ def _load() -> C.CDLL:
         "gd_ring_owner_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, P]),
         "gd_dir_split_ext": (C.c_int, [P, P, U32, C.c_int, P, P, P, P, P, U64, U64, C.POINTER(U64), C.POINTER(U64)]),
         "gd_route_multi_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, U32, C.c_int, C.POINTER(gd_multi_result)]),
+        "gd_fanout_multi_device": (C.c_int, [P, P, P, U32, P, U32, C.c_int32, U32, U32, P]),
+        "gd_fanout_multi": (C.c_int, [P, P, P, U32, P, U32, C.c_int32, U32, U32, P]),
+        "gd_fanout_multi_fetch": (C.c_int, [P, U32] + [P] * 9),
+        "gd_dir_handoff_multi": (C.c_int, [P, P, U32, C.c_int, U32, C.POINTER(gd_handoff_result)]),
+        "gd_dir_handoff_fetch": (C.c_int, [P] + [P] * 7),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -961,6 +980,54 @@ class GrainDispatch:
                  | (GD_MULTI_NO_KEYS if no_keys else 0))
         self._c(lib.gd_route_multi(self.h, _ptr(k), n, n_act, flags, C.byref(r)))
         return self.multi_fetch(r, n)
+
+    # -- sharded fan-out cascade (gd_fanout_multi*) ------------------------------------
+    def fanout_multi_device(self, d_row_off: int, d_dst: int, n_nodes: int, d_seeds: int, n_seeds: int,
+                            type_code: int, n_act: int, hops: int):
+        """gd_fanout_multi_device (collective over the communicator): a list of gd_fanout_hop with
+        device pointers into library-owned buffers, valid until the next call."""
+        out = (gd_fanout_hop * hops)()
+        self._c(lib.gd_fanout_multi_device(self.h, C.c_void_p(d_row_off), C.c_void_p(d_dst), n_nodes,
+                                           C.c_void_p(d_seeds or 0), n_seeds, type_code, n_act, hops, out))
+        return list(out)
+
+    def fanout_multi(self, row_off, dst, seeds, type_code: int, n_act: int, hops: int) -> List[dict]:
+        """gd_fanout_multi (host graph and seeds) + gd_fanout_multi_fetch of every hop."""
+        ro = np.ascontiguousarray(row_off, dtype=np.uint32)
+        d = np.ascontiguousarray(dst, dtype=np.uint32)
+        sd = np.ascontiguousarray(seeds, dtype=np.uint32)
+        out = (gd_fanout_hop * hops)()
+        self._c(lib.gd_fanout_multi(self.h, _ptr(ro), _ptr(d) if d.size else None, len(ro) - 1,
+                                    _ptr(sd) if sd.size else None, sd.size, type_code, n_act, hops, out))
+        return [self.fanout_multi_fetch(i, out[i], n_act) for i in range(hops)]
+
+    def fanout_multi_fetch(self, hop: int, r: gd_fanout_hop, n_act: int) -> dict:
+        m = r.n_recv
+        res = {"frontier": np.empty(r.n_frontier, np.uint32), "target": np.empty(m, np.uint32),
+               "sender": np.empty(m, np.uint32), "src": np.empty(m, np.uint32), "silo": np.empty(m, np.uint32),
+               "act": np.empty(m, np.uint32), "status": np.empty(m, np.uint8), "perm": np.empty(m, np.uint32),
+               "offsets": np.empty(n_act + 2, np.uint32)}
+        names = ("frontier", "target", "sender", "src", "silo", "act", "status", "perm", "offsets")
+        self._c(lib.gd_fanout_multi_fetch(self.h, hop, *[C.c_void_p(_ptr(res[f])) if res[f].size else None
+                                                         for f in names]))
+        res["n_sent"] = int(r.n_sent)
+        return res
+
+    # -- multi-rank directory handoff (gd_dir_handoff_multi) ----------------------------
+    def handoff_multi(self, keep_silos, n_silos: int, event: int, act_base: int) -> dict:
+        """gd_dir_handoff_multi (collective) + gd_dir_handoff_fetch: the entries this rank received,
+        in arrival order, with their activation index here, status and dropped address."""
+        keep = self.keep_mask(keep_silos, n_silos)
+        r = gd_handoff_result()
+        self._c(lib.gd_dir_handoff_multi(self.h, _ptr(keep), len(keep), event, act_base, C.byref(r)))
+        m = r.n_recv
+        out = {"keys": np.empty((m, 3), np.uint64), "ids": np.empty((m, 3), np.uint64), "act": np.empty(m, np.uint32),
+               "silo": np.empty(m, np.uint32), "src": np.empty(m, np.uint32), "status": np.empty(m, np.uint8),
+               "dropped": np.empty((m, 2), np.uint32)}
+        names = ("keys", "ids", "act", "silo", "src", "status", "dropped")
+        self._c(lib.gd_dir_handoff_fetch(self.h, *[C.c_void_p(_ptr(out[f])) if m else None for f in names]))
+        out["n_sent"] = int(r.n_sent)
+        return out
 
     def split_ext(self, keep_silos, n_silos: int, move: bool = True):
         """gd_dir_split_ext: (keys (m,3) u64, acts, silos, KeyExt list (bytes / None)) in slot order."""

@@ -1,0 +1,225 @@
+"""GPU parity for the sharded fan-out cascade behind the C ABI (gd_fanout_multi*, BASELINE cfg 4
+across GPUs: SURVEY 8 f2 over 8 e) against oracle/fanout.py, and cfg 4 at its BASELINE size.
+
+* W = 8 (and 3) ranks on one GPU through the in-process transport (gd_comm_init_local): every
+  hop's frontier, owner-side arrival order (sender rank, sender emission order), routes, buckets.
+* W = 1 over RCCL: the sharded cascade equals the one-GPU fused cascade bit for bit.
+* cfg 4 at full size (10M grains, ~100M follower edges, 65,536 seeds, 3 hops) on one GPU:
+  size-independent properties of every hop plus an oracle sample of each hop.
+Reference: Samples/Chirper/ChirperGrains/ChirperAccount.cs:106-147 (publish loop :131-134)."""
+import numpy as np
+import pytest
+
+import fanout as fo
+import oracle as o
+from orleans_amd.workloads import power_law_graph
+
+pytestmark = pytest.mark.gpu
+
+TC = o.grain_type_code(fo.CHIRPER_ACCOUNT_CLASS)
+
+
+@pytest.fixture(scope="module")
+def gd():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from orleans_amd import graindispatch as g
+    return g
+
+
+def _run_ranks(fns):
+    import threading
+    out, err = [None] * len(fns), [None] * len(fns)
+
+    def body(r):
+        try:
+            out[r] = fns[r]()
+        except BaseException as ex:           # noqa: BLE001 -- re-raised below
+            err[r] = ex
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(len(fns))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=110)
+    for r, ex in enumerate(err):
+        if ex is not None:
+            raise AssertionError(f"rank {r}") from ex
+    assert all(not t.is_alive() for t in ts), "a rank did not finish"
+    return out
+
+
+def _owners_of(spec, nodes):
+    reg = o.grain_keys(TC, np.asarray(nodes, dtype=np.int64))
+    return o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+
+
+def _owners(spec, n):
+    return _owners_of(spec, np.arange(n))
+
+
+@pytest.mark.parametrize("W,mode", [(8, "D"), (3, "V")])
+def test_fanout_multi_local_world_vs_oracle(gd, W, mode):
+    n, hops = 20000, 4
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, mode)
+    ro, dst = power_law_graph(n, 6.0, seed=41 + W, max_deg=4000)
+    own = _owners(spec, n)
+    registered = np.arange(n)[np.arange(n) % 23 != 4]              # some followers have no activation
+    es = []
+    for r in range(W):
+        e = gd.GrainDispatch(device=0, table_capacity=1 << 14, my_silo=r)
+        e.ring_set_silos(mode, [(s.ip, s.port, s.gen) for s in silos])
+        mine = registered[own[registered] % W == r]
+        e.register(o.grain_keys(TC, mine), mine.astype(np.uint32), own[mine])
+        es.append(e)
+    gd.GrainDispatch.comm_init_local(es)
+    seeds = np.random.default_rng(W).integers(0, n, 40).astype(np.uint32)
+    seeds = np.concatenate([seeds, seeds[:3], [n + 7]]).astype(np.uint32)   # duplicates, a node past the graph
+    res = _run_ranks([lambda r=r: es[r].fanout_multi(ro, dst, seeds, TC, n, hops) for r in range(W)])
+    full = o.DirectoryArrays(o.grain_keys(TC, registered), registered.astype(np.uint32), own[registered])
+    want = fo.cascade(ro, dst, seeds, hops, spec, full, n, TC)
+    own_rank = own % W
+    assert sum(w["target"].size for w in want) > 20000
+    for h in range(hops):
+        fronts = [res[r][h]["frontier"] for r in range(W)]
+        if h == 0:
+            seed_rank = _owners_of(spec, seeds) % W
+            for r in range(W):       # each rank publishes the seeds it owns, in seed order (duplicates too)
+                assert fronts[r].tolist() == seeds[seed_rank == r].tolist(), (h, r)
+        else:
+            assert sorted(np.concatenate(fronts).tolist()) == want[h]["frontier"].tolist(), h
+            for r in range(W):
+                assert (own_rank[fronts[r]] == r).all()
+                assert (np.diff(fronts[r].astype(np.int64)) > 0).all()
+        for r in range(W):
+            tt, ss, src = [], [], []
+            for q in range(W):
+                t, s = fo.expand(ro, dst, fronts[q])
+                keep = own_rank[t] == r
+                tt.append(t[keep]), ss.append(s[keep]), src.append(np.full(int(keep.sum()), q, np.uint32))
+            t, s = np.concatenate(tt), np.concatenate(ss)
+            got = res[r][h]
+            np.testing.assert_array_equal(got["target"], t, err_msg=f"hop {h} rank {r} target")
+            np.testing.assert_array_equal(got["sender"], s, err_msg=f"hop {h} rank {r} sender")
+            np.testing.assert_array_equal(got["src"], np.concatenate(src), err_msg=f"hop {h} rank {r} src")
+            assert got["n_sent"] == fo.expand(ro, dst, fronts[r])[0].size
+            st, silo, act, _, _ = o.route_batch_np(o.grain_keys(TC, t.astype(np.int64)), spec, full, my_silo=r)
+            np.testing.assert_array_equal(got["status"], st, err_msg=f"hop {h} rank {r} status")
+            np.testing.assert_array_equal(got["silo"], silo)
+            np.testing.assert_array_equal(got["act"], act)
+            wp, wo = o.bucket_stable(act, n)
+            np.testing.assert_array_equal(got["perm"], wp, err_msg=f"hop {h} rank {r} perm")
+            np.testing.assert_array_equal(got["offsets"], wo, err_msg=f"hop {h} rank {r} offsets")
+        assert sum(res[r][h]["target"].size for r in range(W)) == want[h]["target"].size
+    for e in es:
+        e.comm_destroy()
+        e.close()
+
+
+def test_fanout_multi_world1_rccl_equals_fused_cascade(gd):
+    """W = 1 over RCCL (a send/recv to self): the sharded cascade gives exactly the one-GPU fused
+    cascade's hops (same emission order, same frontiers)."""
+    import torch
+    from orleans_amd.fanout import DeviceFanoutEngine, FanoutCascade, upload_graph
+    n, hops = 200000, 3
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    ro, dst = power_law_graph(n, 8.0, seed=5, max_deg=20000)
+    own = _owners(spec, n)
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 19, my_silo=0)
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+    e.register(o.grain_keys(TC, np.arange(n)), np.arange(n, dtype=np.uint32), own)
+    e.comm_init(gd.GrainDispatch.comm_unique_id(), 1, 0)
+    dev = torch.device("cuda", 0)
+    eng = DeviceFanoutEngine(e, dev, TC)
+    g = upload_graph(ro, dst, dev)
+    seeds = np.unique(np.random.default_rng(6).integers(0, n, 500)).astype(np.uint32)
+    t_seeds = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    with eng.context():
+        hr = e.fanout_multi_device(g.row_off.data_ptr(), g.dst.data_ptr(), n, t_seeds.data_ptr(), seeds.size, TC, n,
+                                   hops)
+        got = [e.fanout_multi_fetch(h, hr[h], n) for h in range(hops)]
+        ref = FanoutCascade(eng, g, n).run(t_seeds, hops)
+    eng.synchronize()
+    u = lambda t: t.cpu().numpy().view(np.uint32)  # noqa: E731
+    assert sum(x["target"].size for x in got) > 100000
+    for h in range(hops):
+        np.testing.assert_array_equal(got[h]["frontier"], u(ref[h].frontier), err_msg=f"hop {h}")
+        for k in ("target", "sender", "silo", "act", "perm", "offsets"):
+            np.testing.assert_array_equal(got[h][k], u(getattr(ref[h], k)), err_msg=f"hop {h} {k}")
+        np.testing.assert_array_equal(got[h]["status"], ref[h].status.cpu().numpy())
+        assert (got[h]["src"] == 0).all() and got[h]["n_sent"] == got[h]["target"].size
+    e.comm_destroy()
+    e.close()
+
+
+def test_cfg4_full_size_properties(gd):
+    """BASELINE cfg 4 at its size on one GPU: 10M grains, ~100M follower edges (power law, mean 10,
+    cap 65,536; the bench's graph), 65,536 seeds, 3 hops.  Size-independent properties of every hop
+    (each message is a follower edge of its publisher in enumeration order, counts add up, buckets
+    sorted and stable, frontiers new and distinct) plus the oracle on a sample of each hop's
+    publishers."""
+    import torch
+    from orleans_amd.fanout import DeviceFanoutEngine, FanoutCascade, upload_graph
+    n, hops = 10_000_000, 3
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    ro, dst = power_law_graph(n, 10.0, seed=0x5EED0004, max_deg=1 << 16)
+    assert ro[-1] > 90_000_000
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 25, my_silo=0)
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+    keys = o.grain_keys(TC, np.arange(n))
+    owner = e.ring_owner(keys)
+    e.register(keys, np.arange(n, dtype=np.uint32), owner)
+    del keys
+    dev = torch.device("cuda", 0)
+    eng = DeviceFanoutEngine(e, dev, TC)
+    g = upload_graph(ro, dst, dev)
+    seeds = np.random.default_rng(0x5EED0004).choice(n, size=1 << 16, replace=False).astype(np.uint32)
+    hops_r = FanoutCascade(eng, g, n).run(torch.from_numpy(seeds.view(np.int32)).to(dev), hops)
+    eng.synchronize()
+    seen = np.zeros(n, dtype=bool)
+    seen[seeds] = True
+    ro64 = ro.astype(np.int64)
+    total = 0
+    samples = []
+    for h, hr in enumerate(hops_r):
+        fr = hr.frontier.cpu().numpy().view(np.uint32)
+        t = hr.target.cpu().numpy().view(np.uint32)
+        s = hr.sender.cpu().numpy().view(np.uint32)
+        act = hr.act.cpu().numpy().view(np.uint32)
+        st = hr.status.cpu().numpy()
+        perm = hr.perm.cpu().numpy().view(np.uint32)
+        off = hr.offsets.cpu().numpy().view(np.uint32)
+        deg = ro64[fr.astype(np.int64) + 1] - ro64[fr]
+        assert t.size == int(deg.sum())
+        total += t.size
+        assert (st == o.ST_OK).all() and np.array_equal(act, t)          # every grain registered, act = node
+        np.testing.assert_array_equal(np.repeat(fr, deg), s)             # publisher order, degree each
+        starts = np.repeat(ro64[fr] - np.concatenate([[0], np.cumsum(deg)[:-1]]), deg)
+        np.testing.assert_array_equal(dst[starts + np.arange(t.size)], t)
+        sa = act[perm].astype(np.int64)
+        assert (np.diff(sa) >= 0).all()
+        assert (np.diff(perm.astype(np.int64))[np.diff(sa) == 0] > 0).all()
+        cnt = np.bincount(act, minlength=n + 1)
+        np.testing.assert_array_equal(np.diff(off[:n + 1].astype(np.int64)), cnt[:n])
+        assert off[n] == t.size and off[n + 1] == t.size
+        if h:
+            assert not seen[fr].any() and np.unique(fr).size == fr.size and (np.diff(fr.astype(np.int64)) > 0).all()
+            seen[fr] = True
+        samples.append(fr[:: max(1, fr.size // 200)][:200])
+        del t, s, act, st, perm, off
+    assert total > 40_000_000
+    # the oracle on a sample of each hop's publishers (the directory restricted to the grains they reach)
+    for h, fs in enumerate(samples):
+        t, s = fo.expand(ro, dst, fs)
+        nodes = np.unique(t)
+        d = o.DirectoryArrays(o.grain_keys(TC, nodes), nodes.astype(np.uint32), owner[nodes])
+        want = dict(zip(("status", "silo", "act"), o.route_batch_np(o.grain_keys(TC, t.astype(np.int64)), spec, d)[:3]))
+        got = e.fanout_route_bucket(ro, dst, fs, TC, None)
+        np.testing.assert_array_equal(got["target"], t, err_msg=f"hop {h}")
+        np.testing.assert_array_equal(got["sender"], s)
+        for k in want:
+            np.testing.assert_array_equal(got[k], want[k], err_msg=f"hop {h} {k}")
+    e.close()
