@@ -313,23 +313,26 @@ __global__ void __launch_bounds__(BLOCK) k_handoff_add_status(const gd_val* __re
                                                               gd_val* __restrict__ dropped) {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= m) return;
-    const gd_val v = in[j], g = got[j];
+    const uint32_t v_act = in[j].act, g_act = got[j].act, g_silo = got[j].silo;
     uint8_t st;
-    gd_val d{NONE32, NONE32};
-    if (v.act == GD_ACT_MULTI || g.act == GD_ACT_MULTI) {
+    uint32_t d_act = NONE32, d_silo = NONE32;
+    // (written as a select: an if / else-if chain assigning the struct in two branches lost the silo
+    // half of `got` on this compiler -- the ISA reused its register for the id comparison)
+    if (v_act == GD_ACT_MULTI || g_act == GD_ACT_MULTI) {
         st = MERGE_HOST;
     } else if (ins[j]) {
         st = MERGE_INSERTED;
-    } else if (g.act == NONE32) {
+    } else if (g_act == NONE32) {
         st = MERGE_DROPPED;                          // refused: the silo is not valid (IsValidSilo)
-    } else if (g.act < n_ids && v.act < n_ids && key_cmp(ids[g.act], ids[v.act]) == 0) {
-        st = MERGE_SAME;
     } else {
-        st = MERGE_DROPPED;
-        d = g;
+        bool same = false;
+        if (g_act < n_ids && v_act < n_ids) same = key_cmp(ids[g_act], ids[v_act]) == 0;
+        st = same ? MERGE_SAME : MERGE_DROPPED;
+        d_act = same ? NONE32 : g_act;
+        d_silo = same ? NONE32 : g_silo;
     }
     status[j] = st;
-    dropped[j] = d;
+    dropped[j] = gd_val{d_act, d_silo};
 }
 
 }  // namespace gd
