@@ -25,6 +25,7 @@
 #include "gd_frames.h"
 #include "gd_dirops.h"
 #include "gd_actdir.h"
+#include "gd_bucket2.h"
 #include "graindispatch.h"
 
 using namespace gd;
@@ -184,6 +185,7 @@ struct gd_handle {
     uint32_t last_digits = 0;   // the first histogram pre-fills the bucket starts (GD_FILL_IN_HIST=0: k_fill)   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
     int fan_ilp = 2;                  // fan-out items per thread in flight together (GD_FAN_ILP: 1, 2, 4)
+    bool bucket2 = false;             // two wide-digit passes on 16K-item tiles (GD_BUCKET2=1; measured slower)
 
     // pinned host scratch for small device -> host read-backs (counts, totals)
     void* h_pin = nullptr;
@@ -603,12 +605,64 @@ int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* 
     }
 }
 
+// The two wide-digit passes of gd_bucket2.h: key & 1023, then key >> 10, on 16K-item tiles, for keys
+// in [0, n_act] with (n_act >> 10) + 1 <= B2_RMAX2.  Starts pre-filled by the first histogram, lowered
+// by the second scatter, min-scanned per 1,024-activation range.
+int bucket2_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
+                   uint32_t* rank_out) {
+    const uint32_t n_off = n_act + 2;
+    const FillArgs fill{offsets, n_off, n};
+    const uint32_t tiles = blocks_for(n, B2_TILE);
+    const uint32_t R1 = B2_R1, R2 = (n_act >> B2_LOW_BITS) + 1;
+    GD_TRY(ensure(h, h->hist, ((size_t)std::max(R1, R2) * tiles + std::max(R1, R2)) * sizeof(uint32_t)));
+    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
+    GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
+    uint32_t* hist = (uint32_t*)h->hist.p;
+    uint32_t* k1 = (uint32_t*)h->u32_a.p;
+    uint32_t* v1 = (uint32_t*)h->u32_c.p;
+    const uint32_t xcd = h->xcd_tiles;
+    const uint32_t tpb = tiles >= 1024 ? 4u : 1u;
+    const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
+    // pass 1: key & 1023
+    if (tpb == 4)
+        GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(1024), 0, k_b2_hist<1024, 16, 4, B2_R1, true>,
+                      acts, n, n_act, R1, tiles, hist, fill, hxr));
+    else
+        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(1024), 0, k_b2_hist<1024, 16, 1, B2_R1, true>, acts, n,
+                      n_act, R1, tiles, hist, fill, hxr));
+    const uint32_t* tot1 = hist + (size_t)R1 * tiles;
+    GD_TRY(launch(h, "k_radix_rowscan", dim3(R1), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R1 * tiles));
+    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(1024), 0, k_b2_scatter<1024, 16, B2_R1, true>, acts,
+                  (const uint32_t*)nullptr, n, n_act, R1, tiles, (const uint32_t*)hist, tot1, k1, v1, (uint32_t*)nullptr,
+                  (uint32_t*)nullptr, xcd));
+    // pass 2: key >> 10, the permutation and the starts
+    if (tpb == 4)
+        GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(1024), 0,
+                      k_b2_hist<1024, 16, 4, B2_RMAX2, false>, (const uint32_t*)k1, n, n_act, R2, tiles, hist,
+                      FillArgs{nullptr, 0u, 0u}, hxr));
+    else
+        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(1024), 0, k_b2_hist<1024, 16, 1, B2_RMAX2, false>,
+                      (const uint32_t*)k1, n, n_act, R2, tiles, hist, FillArgs{nullptr, 0u, 0u}, hxr));
+    const uint32_t* tot2 = hist + (size_t)R2 * tiles;
+    GD_TRY(launch(h, "k_radix_rowscan", dim3(R2), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R2 * tiles));
+    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(512), 0, k_b2_scatter<512, 32, B2_RMAX2, false>,
+                  (const uint32_t*)k1, (const uint32_t*)v1, n, n_act, R2, tiles, (const uint32_t*)hist, tot2,
+                  (uint32_t*)nullptr, perm, offsets, rank_out, xcd));
+    h->last_totals = tot2;
+    h->last_digits = R2;
+    return launch(h, "k_starts_rangescan", dim3(R2), dim3(RS_THREADS), 0, k_starts_rangescan, offsets, n_act + 1,
+                  B2_LOW_BITS, tot2, R2);
+}
+
 // Stable partition of indices 0..n-1 by min(acts[i], n_act):
 // LSD passes of <= 8 bits, then bucket offsets from the sorted keys.  rank_out (optional): the
 // inverse permutation, rank_out[perm[p]] = p.
 int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                   uint32_t* rank_out = nullptr) {
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    // keys of 17..21 bits with at most B2_RMAX2 high digits, batches of at least 64 tiles: two wide passes
+    if (h->bucket2 && n >= 64 * B2_TILE && n_act >= (1u << 16) && (n_act >> B2_LOW_BITS) + 1 <= B2_RMAX2)
+        return bucket2_device(h, acts, n, n_act, perm, offsets, rank_out);
     const uint32_t n_off = n_act + 2;
     if (n == 0 || !h->fill_in_hist)
         GD_TRY(launch(h, "k_fill", dim3(blocks_for(n_off, BLOCK)), dim3(BLOCK), 0, k_fill_u32, offsets, n_off, n));
@@ -942,6 +996,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_HIST_TPB")) h->hist_tpb = (uint32_t)std::atoi(v);
     if (const char* v = std::getenv("GD_HIST_XCD")) h->hist_xcd = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_FAN_ILP")) h->fan_ilp = std::atoi(v);
+    if (const char* v = std::getenv("GD_BUCKET2")) h->bucket2 = std::atoi(v) != 0;
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));
