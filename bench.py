@@ -219,6 +219,9 @@ def timed_steps(router, keys, n_act, stream, steps, warmup):
     return float(t.item()), ev0.elapsed_time(ev1), res
 
 
+T_START = time.perf_counter()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -238,7 +241,8 @@ def main():
     ap.add_argument("--exchange", default="auto", choices=["auto", "library", "torch"],
                     help="N>1: RCCL exchange inside libgraindispatch (gd_route_multi_device) or torch.distributed "
                          "all_to_all_single; auto = library once it matches torch bit for bit on the first batch")
-    ap.add_argument("--no-secondary", action="store_true", help="N>1: skip the cfg3 strong-scaling measurement")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary configs (N>1: cfg3 strong scaling; N=1: cfg3 and cfg4 on one GPU)")
     ap.add_argument("--msgs3", type=int, default=None, help="secondary cfg3: messages per GPU (default 2^26 / N)")
     ap.add_argument("--grains3", type=int, default=None, help="secondary cfg3: grains per GPU (default 1e8 / N)")
     ap.add_argument("--latency-batches", type=int, default=10000,
@@ -296,6 +300,28 @@ def main():
             "owner_share_max_by_silo_set": w3["owner_share_by_set"]}
         w3["e"].close()
         del w3
+
+    if world == 1 and args.workload == "cfg2" and not args.no_secondary:
+        # BASELINE cfg 3 on one GPU (64M Zipf(1.1) messages over 100M grains) and cfg 4 (the Chirper
+        # fan-out cascade), each with its bounded CPU baseline; the cfg 2 handle stays open
+        w3 = setup_workload(args, "cfg3", 1, 0, local, dev, tcd, args.msgs3, args.grains3)
+        steps3 = max(10, args.steps // 10)
+        wall3, gpu3, _ = timed_steps(w3["router"], w3["keys"], w3["n_act"], w3["stream"], steps3,
+                                     max(3, args.warmup // 4))
+        c3 = None
+        if not args.no_cpu_baseline:
+            c3 = cpu_baseline_cfg3(args, w3, tcd)
+        secondary["cfg3"] = {
+            "value": round(w3["N"] * steps3 / wall3, 1), "unit": "messages/s",
+            "ms_per_step": round(wall3 / steps3 * 1e3, 4), "steps": steps3,
+            "workload": workload_name("cfg3", 1, w3["N"], w3["G_total"]), "msgs_per_gpu": w3["N"],
+            "cpu_baseline": c3}
+        w3["e"].close()
+        del w3
+        torch.cuda.empty_cache()
+        secondary["cfg4"] = measure_cfg4(args, 1, 0, local, dev, steps=max(5, args.steps // 20),
+                                         warmup=max(2, args.warmup // 5), profile_steps=0,
+                                         with_cpu=not args.no_cpu_baseline)
 
     # received (owner-side) message count, for the byte model
     m_recv = int(res.status.shape[0])
@@ -418,6 +444,7 @@ def main():
         }
         if secondary:
             line["secondary"] = secondary
+        line["bench_wall_s"] = round(time.perf_counter() - T_START, 1)
         print(json.dumps(line), flush=True)
     e.close()
     dist.destroy_process_group()
@@ -606,6 +633,39 @@ def cpu_baseline(args, tcd, G_total, pts, own, owner):
                                 "p99": round(float(np.percentile(lat_us, 99)), 1)}}
 
 
+def cpu_baseline_cfg3(args, w3, tcd):
+    """cfg 3's CPU baseline: the C restatement (oracle/cpu_ref.c, test infrastructure) routing +
+    bucketing a bounded prefix of the GPU's own Zipf(1.1) batch.  The CPU directory holds the
+    sample's distinct grains only (registering all 100M would take minutes and ~8 GB): a smaller
+    table than the GPU's 8.6 GB one, which favours the CPU."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_ref  # test-infrastructure checker, timed here as the CPU baseline only
+
+    cores = usable_cores()
+    sample = 1 << 21
+    keys = w3["keys"][:sample].cpu().numpy().view(np.uint64).copy()
+    ks = keys[:, 1].astype(np.int64)
+    grains = np.unique(ks)
+    reg = grain_keys(tcd, grains)
+    owner = w3["e"].ring_owner(reg)
+    res = {}
+    for label, faithful, thr in (("faithful_1", True, 1), ("fast_n", False, cores)):
+        d = cpu_ref.CpuDirectory(faithful, len(grains))
+        d.register(reg, grains.astype(np.uint32), owner)
+
+        def one(d=d, faithful=faithful, thr=thr):
+            _, _, act = d.route(args.mode, w3["pts"], w3["own"], keys, nthreads=thr)
+            cpu_ref.bucket(act, w3["n_act"], faithful=faithful, nthreads=thr)
+        v, done = _timed(one, args.cpu_seconds / 4, sample)
+        res[label] = {"value": round(v, 1), "threads": thr, "messages": done}
+        del d
+    best = res["fast_n"]
+    return {"value": best["value"], "unit": "messages/s", "cores": cores, "kind": "port",
+            "sample": f"{best['messages']} messages (the first {sample} of the GPU's Zipf(1.1) batch, repeated; "
+                      f"{len(grains)} distinct grains registered on the CPU of the 100M) through the C restatement "
+                      f"in fast mode on {cores} threads", "modes": res}
+
+
 # ---- BASELINE cfg 4: Chirper-style follower fan-out cascade -------------------------------------
 
 def fan_kernel_bytes(name, msgs, n_front, n_act, passes, keep_target, n_hops, hop_msgs=None):
@@ -630,6 +690,16 @@ def fan_kernel_bytes(name, msgs, n_front, n_act, passes, keep_target, n_hops, ho
 
 
 def run_cfg4(args, world, rank, local, dev):
+    """--workload cfg4: the cascade line (measure_cfg4) printed on rank 0."""
+    line = measure_cfg4(args, world, rank, local, dev, args.steps, args.warmup, args.profile_steps,
+                        with_cpu=not args.no_cpu_baseline)
+    if rank == 0:
+        line["bench_wall_s"] = round(time.perf_counter() - T_START, 1)
+        print(json.dumps(line), flush=True)
+    dist.destroy_process_group()
+
+
+def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, with_cpu):
     """One step = one whole cascade: `--hops` publish rounds from `--seeds` publishers, each round =
     expand the frontier's follower lists (ChirperAccount.cs:131-134) -> route every NewChirp (ring
     owner + directory probe) -> bucket per activation -> next frontier.  Value = messages routed
@@ -695,14 +765,14 @@ def run_cfg4(args, world, rank, local, dev):
     def step():
         return runner.run(t_seeds, args.hops)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     msgs_local = 0
-    for _ in range(args.steps):
+    for _ in range(steps):
         hops = step()
         msgs_local += sum(h.messages for h in hops)
     torch.cuda.synchronize()
@@ -718,10 +788,10 @@ def run_cfg4(args, world, rank, local, dev):
     hop_front = [h.n_frontier if hasattr(h, "n_frontier") else int(h.frontier.shape[0]) for h in hops]
 
     kernels, roofline = {}, None
-    if args.profile_steps > 0:
+    if profile_steps > 0:
         e.set_kernel_timing(True)
         e.kernel_times_reset()
-        for _ in range(args.profile_steps):
+        for _ in range(profile_steps):
             step()
         torch.cuda.synchronize()
         kt = e.kernel_times()
@@ -731,11 +801,11 @@ def run_cfg4(args, world, rank, local, dev):
         for name, (launches, ms) in kt.items():
             if not launches:
                 continue
-            per = ms / args.profile_steps
+            per = ms / profile_steps
             b = fan_kernel_bytes(name, msgs_step, sum(hop_front), n, passes, not args.no_target, len(hops),
                                  hop_msgs)
             gbs = b / (per * 1e-3) / 1e9 if b and per > 0 else None
-            kernels[name] = {"launches_per_step": launches // args.profile_steps, "ms_per_step": round(per, 4),
+            kernels[name] = {"launches_per_step": launches // profile_steps, "ms_per_step": round(per, 4),
                              "alg_GBps": round(gbs, 1) if gbs else None,
                              "frac_hbm": round(gbs / PEAK_HBM_GBS, 4) if gbs else None}
         dom = max((k for k in kernels if not k.startswith("rccl_")), key=lambda k: kernels[k]["ms_per_step"])
@@ -745,15 +815,14 @@ def run_cfg4(args, world, rank, local, dev):
                     "avg_launch_ms": round(d["ms_per_step"] / max(1, d["launches_per_step"]), 5)}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and getattr(hops[-1], "target", None) is not None:
+    if rank == 0 and world == 1 and with_cpu and getattr(hops[-1], "target", None) is not None:
         cpu = cpu_baseline_cfg4(args, hops, tcd, owner, pts, own, n)
 
-    if rank == 0:
-        line = {
+    line = {
             "metric": "routed messages/sec (fan-out cascade: expand+lookup+bucket, whole node)",
             "value": round(msgs_total / wall_max, 1), "unit": "messages/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(wall_max / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+            "steps": steps, "warmup": warmup,
+            "ms_per_step": round(wall_max / steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "u32/u64 integer",
             "data": f"synthetic power-law follower graph (alpha 2.5, mean {args.mean_deg}, cap {args.max_deg}), "
                     f"seed 0x5EED0004",
@@ -761,13 +830,14 @@ def run_cfg4(args, world, rank, local, dev):
                                    f"{args.hops} hops", "ring_mode": args.mode,
                        "silos": f"8 x 10.0.0.{{1..8}}:11111, {args.silos} generations",
                        "parallelism": f"shard{world}" + ("-rehearsal" if args.rehearse_one_gpu else "")},
-            "messages_per_step": int(msgs_total / args.steps), "hop_messages_rank0": hop_msgs,
+            "messages_per_step": int(msgs_total / steps), "hop_messages_rank0": hop_msgs,
             "hop_publishers_rank0": hop_front, "setup_s": round(setup_s, 1), "exchange": exchange,
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
     e.close()
-    dist.destroy_process_group()
+    del graph, eng
+    torch.cuda.empty_cache()
+    return line
 
 
 def cpu_baseline_cfg4(args, hops, tcd, owner, pts, own, n):

@@ -669,7 +669,8 @@ int gd_activation_ids_set(gd_handle* h, const uint32_t* acts, const gd_key* ids,
  *   GD_MERGE_KEPT      single-activation grain, the incoming ActivationId is the lower: it replaces the
  *                      existing entry (GrainInfo.Merge :159-176); out_dropped[i] = the displaced one
  *   GD_MERGE_DROPPED   the existing ActivationId is the lower: out_dropped[i] = the incoming activation
- *   GD_MERGE_HOST      a multi-activation grain on either side (instance lists are unioned by C#)
+ *   GD_MERGE_UNION     a multi-instance grain holding one instance here meets another: both kept (below)
+ *   GD_MERGE_HOST      a grain with several instances on either side (its lists are unioned by C#)
  * out_dropped lists what Catalog.DeleteActivations gets per silo (:514-518); {GD_NO_*} otherwise.  Both
  * activations of a conflict need an ActivationId (gd_activation_ids_set), else GD_EINVAL.  No
  * IsValidSilo check (Merge has none).  Host pointers; out_dropped may be NULL. */
@@ -678,6 +679,11 @@ int gd_activation_ids_set(gd_handle* h, const uint32_t* acts, const gd_key* ids,
 #define GD_MERGE_SAME     2
 #define GD_MERGE_DROPPED  3
 #define GD_MERGE_HOST     4
+/* GD_MERGE_UNION     the grain here is a multi-instance one (AddActivation, SingleInstance false) holding
+ *                    one instance, and the incoming instance is another: GrainInfo.Merge unions the lists
+ *                    (:141-152) and keeps both; the entry becomes GD_ACT_MULTI with a new VersionTag and
+ *                    the host adds the incoming instance to its list */
+#define GD_MERGE_UNION    5
 /* tags[i] | GD_MERGE_TAG_MULTI_INSTANCE: the incoming GrainInfo is not SingleInstance (an AddActivation
  * grain holding one instance); partitionData.Add keeps it so (tags NULL: single unless GD_ACT_MULTI). */
 #define GD_MERGE_TAG_MULTI_INSTANCE 0x80000000u

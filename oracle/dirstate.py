@@ -38,7 +38,7 @@ M32 = 0xFFFFFFFF
 ACT_MULTI = 0xFFFFFFFE
 Key = Tuple[int, int, int]
 
-MERGE_INSERTED, MERGE_KEPT, MERGE_SAME, MERGE_DROPPED, MERGE_HOST = 0, 1, 2, 3, 4
+MERGE_INSERTED, MERGE_KEPT, MERGE_SAME, MERGE_DROPPED, MERGE_HOST, MERGE_UNION = 0, 1, 2, 3, 4, 5
 
 
 def fmix32(h: int) -> int:
@@ -172,8 +172,14 @@ class DirectoryState:
                 multi_flag = tags is not None and (int(tags[i]) & 0x80000000) != 0
                 self.entries[k] = [a, s, tag, a != ACT_MULTI and not multi_flag]
                 out.append((MERGE_INSERTED, M32, M32))
-            elif e[0] == ACT_MULTI or a == ACT_MULTI or not e[3]:
+            elif e[0] == ACT_MULTI or a == ACT_MULTI:
                 out.append((MERGE_HOST, M32, M32))
+            elif not e[3]:                                  # multi-instance grain with one instance: union (:141-152)
+                if e[0] == a or self.ids[a] == self.ids[e[0]]:
+                    out.append((MERGE_SAME, M32, M32))
+                else:
+                    e[0], e[2] = ACT_MULTI, version_tag(self.op, k)
+                    out.append((MERGE_UNION, M32, M32))
             elif e[0] == a or self.ids[a] == self.ids[e[0]]:
                 out.append((MERGE_SAME, M32, M32))          # ContainsKey(ActivationId) -> continue (:146)
             else:

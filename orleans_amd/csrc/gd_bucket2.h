@@ -200,15 +200,18 @@ __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ 
     uint32_t ex, exg;
     block_excl_scan_add2<NT>(my_total, my_g, s_wsum, ex, exg);
     {
+        // the pair prefixes become absolute tile positions (+ the digit's tile start, both halves), and
+        // the write-out's base is gbase - lstart: one LDS lookup per item on each side
         uint32_t run = ex, rung = exg;
 #pragma unroll
         for (uint32_t q = 0; q < DPT; ++q) {
             const uint32_t d = threadIdx.x * DPT + q;
             if (d < RMAX) {
                 const uint32_t t = s_lstart[d];
-                s_lstart[d] = run;
+#pragma unroll
+                for (int p = 0; p < NW / 2; ++p) s_cnt[p][d] += run | (run << 16);
+                s_gbase[d] = s_gbase[d] + rung - run;
                 run += t;
-                s_gbase[d] += rung;
                 rung += tv[q];
             }
         }
@@ -219,7 +222,7 @@ __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ 
         const uint32_t pos = (w * IT + r) * WAVE + lane;
         if (base + pos < n) {
             const uint32_t d = FIRST ? (kk[r] & (B2_R1 - 1)) : (kk[r] >> B2_LOW_BITS);
-            const uint32_t at = s_lstart[d] + ((s_cnt[w >> 1][d] >> half) & 0xFFFFu) + rk[r];
+            const uint32_t at = ((s_cnt[w >> 1][d] >> half) & 0xFFFFu) + rk[r];
             s_key[at] = kk[r];
             s_val[at] = (Val)vv[r];
         }
@@ -231,14 +234,14 @@ __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ 
         if (p < cnt_tile) {
             const uint32_t k = s_key[p];
             const uint32_t d = FIRST ? (k & (B2_R1 - 1)) : (k >> B2_LOW_BITS);
-            const uint32_t g = s_gbase[d] + (p - s_lstart[d]);
+            const uint32_t g = s_gbase[d] + p;
             if (g < n) {                  // always true when the counts are right; never write out of bounds
                 if constexpr (FIRST) {
                     keys_out[g] = k;
                     vals_out[g] = base + (uint32_t)s_val[p];
                 } else {
                     const uint32_t v = s_val[p];
-                    if (p == s_lstart[d] || s_key[p - 1] != k) atomicMin(&starts[k], g);
+                    if (p == 0 || s_key[p - 1] != k) atomicMin(&starts[k], g);
                     vals_out[g] = v;
                     if (rank_out) rank_out[v] = g;
                 }

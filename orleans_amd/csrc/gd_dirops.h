@@ -170,7 +170,8 @@ __device__ __forceinline__ int key_cmp(const gd_key& a, const gd_key& b) {
 }
 
 // GD_MERGE_* statuses (include/graindispatch.h)
-constexpr uint8_t MERGE_INSERTED = 0, MERGE_KEPT = 1, MERGE_SAME = 2, MERGE_DROPPED = 3, MERGE_HOST = 4;
+constexpr uint8_t MERGE_INSERTED = 0, MERGE_KEPT = 1, MERGE_SAME = 2, MERGE_DROPPED = 3, MERGE_HOST = 4,
+                  MERGE_UNION = 5;
 constexpr uint32_t MERGE_TAG_MULTI = 0x80000000u;   // GD_MERGE_TAG_MULTI_INSTANCE
 
 // One item per grain (k_dup_mark); slot_of / is_new from k_reg_claim.  out_dropped[i] = the
@@ -208,8 +209,18 @@ __global__ void __launch_bounds__(BLOCK) k_merge_apply(const gd_key* __restrict_
             st = MERGE_INSERTED;
         } else {
             const uint32_t cur = sl.act;
-            if (cur == GD_ACT_MULTI || in.act == GD_ACT_MULTI || !(vtag[s] & VTAG_SINGLE)) {
+            if (cur == GD_ACT_MULTI || in.act == GD_ACT_MULTI) {
                 st = MERGE_HOST;                      // instance lists are unioned by C# (GrainInfo.Merge :141-152)
+            } else if (!(vtag[s] & VTAG_SINGLE)) {
+                // a multi-instance grain (AddActivation) holding one instance: Merge unions the lists
+                // (:141-152) and keeps both -- no lowest-id rule, SingleInstance is false (:159)
+                if (cur == in.act || (cur < n_ids && in.act < n_ids && key_cmp(ids[in.act], ids[cur]) == 0)) {
+                    st = MERGE_SAME;                  // Instances.ContainsKey -> not modified
+                } else {
+                    sl.act = GD_ACT_MULTI;            // two instances now: routes answer MULTI_ACT
+                    vtag[s] = version_tag(op, h);     // modified -> VersionTag = rand.Next() (:154-157)
+                    st = MERGE_UNION;
+                }
             } else if (cur == in.act) {
                 st = MERGE_SAME;                      // Instances.ContainsKey -> continue; not modified (:146)
             } else if (cur >= n_ids || in.act >= n_ids) {

@@ -1138,15 +1138,18 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
     uint32_t ex, exg;
     block_excl_scan_add2<NT>(my_total, my_g, s_wsum, ex, exg);     // its barrier orders s_gbase's stores
     {
+        // one LDS lookup per item on each side below: the waves' prefixes become absolute tile
+        // positions (s_wcnt += the digit's tile start), and the write-out's base is gbase - lstart
         uint32_t run = ex, rung = exg;
 #pragma unroll
         for (uint32_t q = 0; q < DPT; ++q) {
             const uint32_t d = threadIdx.x * DPT + q;
             if (d < R) {
                 const uint32_t t = s_lstart[d];
-                s_lstart[d] = run;
+#pragma unroll
+                for (int ww = 0; ww < NW; ++ww) s_wcnt[ww][d] += run;
+                s_gbase[d] = s_gbase[d] + (totals ? rung : 0u) - run;
                 run += t;
-                if (totals) s_gbase[d] += rung;
                 rung += tv[q];
             }
         }
@@ -1157,7 +1160,7 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
         const uint32_t idx = base + (w * IT + r) * WAVE + lane;
         if (idx < n) {
             const uint32_t d = (kk[r] >> shift) & (R - 1);
-            s_kv[s_lstart[d] + s_wcnt[w][d] + rk[r]] = make_uint2(kk[r], vv[r]);
+            s_kv[s_wcnt[w][d] + rk[r]] = make_uint2(kk[r], vv[r]);
         }
     }
     __syncthreads();
@@ -1167,10 +1170,12 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
         if (p < cnt_tile) {
             const uint2 kv = s_kv[p];
             const uint32_t d = (kv.x >> shift) & (R - 1);
-            const uint32_t g = s_gbase[d] + (p - s_lstart[d]);
+            const uint32_t g = s_gbase[d] + p;       // s_gbase holds the digit's global base - its tile start
             if (g < n) {            // always true when the scan is right; never write out of bounds
                 if (starts) {
-                    if (p == s_lstart[d] || s_kv[p - 1].x != kv.x) atomicMin(&starts[kv.x], g);
+                    // a key's first item in the tile: the item before it holds another key (a digit
+                    // boundary is a key boundary too)
+                    if (p == 0 || s_kv[p - 1].x != kv.x) atomicMin(&starts[kv.x], g);
                     vals_out[g] = kv.y;
                 } else if (pk.out) {
                     keys_out[g] = ((kv.x & ((1u << pk.b1) - 1u)) << pk.ib) | kv.y;

@@ -125,7 +125,7 @@ class gd_handoff_result(C.Structure):
 
 GD_HANDOFF_ADD, GD_HANDOFF_REMOVE = 0, 1
 GD_MERGE_TAG_MULTI_INSTANCE = 0x80000000
-GD_MERGE_INSERTED, GD_MERGE_KEPT, GD_MERGE_SAME, GD_MERGE_DROPPED, GD_MERGE_HOST = 0, 1, 2, 3, 4
+GD_MERGE_INSERTED, GD_MERGE_KEPT, GD_MERGE_SAME, GD_MERGE_DROPPED, GD_MERGE_HOST, GD_MERGE_UNION = 0, 1, 2, 3, 4, 5
 ACTDIR_VALID, ACTDIR_SYSTEM_TARGET, ACTDIR_STATELESS_WORKER = 1, 2, 4
 (RECV_ACTIVATION, RECV_SYSTEM_TARGET, RECV_NULL_CONTEXT, RECV_REJECT_UNKNOWN, RECV_REJECT_OVERLOADED, RECV_DROPPED,
  RECV_UNDECODED) = range(7)

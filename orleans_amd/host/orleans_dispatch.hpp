@@ -457,6 +457,8 @@ public:
             if (st[j] == GD_MERGE_KEPT || st[j] == GD_MERGE_DROPPED)
                 del[silos_.At(dropped[j].silo)].push_back(
                     ActivationAddress{silos_.At(dropped[j].silo), grains[i], acts_.at(dropped[j].act)});
+            else if (st[j] == GD_MERGE_UNION)            // the device entry is GD_ACT_MULTI already
+                multi_[grains[i]][acts[i]] = silos[i];
             else if (st[j] == GD_MERGE_HOST && multi_.count(grains[i]))
                 AddActivation(grains[i], acts[i], silos[i]);
         }

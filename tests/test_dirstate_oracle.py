@@ -72,13 +72,17 @@ def test_merge_rules():
     keys = [_k(1), _k(2), _k(3), _k(5), _k(1 << 20)]
     acts = [11, 21, 60, 51, 20]
     silos = [2, 3, 4, 5, 6]
-    tag1 = st.entries[_k(1)][2]
+    tag1, tag5 = st.entries[_k(1)][2], st.entries[_k(5)][2]
     out = st.merge(keys[:4], acts[:4], silos[:4], tags=[0, 0, 123, 0])
     assert out[0] == (ds.MERGE_KEPT, 10, 0)               # incoming 11 (N0 4) < existing 10 (N0 5): the incoming stays
     assert st.entries[_k(1)][:2] == [11, 2] and st.entries[_k(1)][2] != tag1
     assert out[1] == (ds.MERGE_DROPPED, 21, 3)            # incoming 21 (N1 2) > existing 20 (N1 1): dropped
     assert st.entries[_k(2)][:2] == [20, 0]
     assert out[2] == (ds.MERGE_INSERTED, M32, M32) and st.entries[_k(3)][2] == 123   # absent: added with its tag
-    assert out[3] == (ds.MERGE_HOST, M32, M32)            # a multi-instance side: the host merges the lists
+    # a multi-instance grain (AddActivation) holding one instance meets another: the lists are unioned
+    # and both instances stay (GrainInfo.Merge :141-152, SingleInstance false): GD_ACT_MULTI, new tag
+    assert out[3] == (ds.MERGE_UNION, M32, M32) and st.entries[_k(5)][0] == ds.ACT_MULTI
+    assert st.entries[_k(5)][2] != tag5
+    assert st.merge([_k(5)], [50], [0]) == [(ds.MERGE_HOST, M32, M32)]   # several instances now: the host's
     same = st.merge([_k(1)], [11], [2])
     assert same == [(ds.MERGE_SAME, M32, M32)]

@@ -167,6 +167,15 @@ def test_merge_rules_and_duplicates(gd):
     assert (got[1][0], got[2][0]) == (0, 1) and (got[1][1], got[2][1]) == (4, 3)
     universe = _keys(np.arange(8, 20))
     _check_state(e, st, universe)
+    # multi-instance grains (AddActivation) holding one instance: another instance -> the lists are
+    # unioned (GD_MERGE_UNION, the entry becomes GD_ACT_MULTI with a new tag); the same one -> SAME
+    mi = _keys([18, 19])
+    e.upsert(mi, [5, 4], [1, 2])
+    st.upsert(mi, [5, 4], [1, 2])
+    got = e.merge(mi, [2, 4], [0, 2])
+    want = st.merge(mi, [2, 4], [0, 2])
+    assert got[0].tolist() == [ds.MERGE_UNION, ds.MERGE_SAME] == [w[0] for w in want]
+    _check_state(e, st, universe)
     live = e.stats()["table_live"]
     with pytest.raises(gd.GrainDispatchError):
         e.merge(_keys([16, 17, 16]), [1, 2, 3], [0, 0, 0])

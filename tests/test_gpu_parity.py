@@ -417,12 +417,15 @@ def test_microbatch_graph_matches_eager_and_oracle(gd, monkeypatch, variant, mod
     d = o.DirectoryArrays(reg, np.arange(G), owner)
     mb = gd.MicroBatch(e, 8192, G)
     rng = np.random.default_rng(55)
+    routed0, routed = e.stats()["routed"], 0
     for n in (4096, 8192, 1000, 4096, 1, 0, 4097, 2, 6000):
         hot = rng.integers(0, 64, size=n)                           # skewed: many messages per activation
         keys = o.grain_keys(TC, np.where(rng.random(n) < 0.5, hot, rng.integers(0, G + 300, size=n)))
         mb.keys[:n] = keys
         for use_graph in (True, False):
             mb.run(n, use_graph)
+            routed += n
+            assert e.stats()["routed"] - routed0 == routed      # every replay counts its messages
             want = o.route_batch_np(keys, spec, d)
             assert np.array_equal(mb.status[:n], want[0]) and np.array_equal(mb.silo[:n], want[1])
             assert np.array_equal(mb.act[:n], want[2])
