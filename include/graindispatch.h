@@ -321,8 +321,14 @@ int gd_comm_destroy(gd_handle* h);
 
 /* Results of the last gd_route_multi* call on a handle: device pointers into library-owned
  * buffers, valid until the next gd_route_multi* / gd_comm_destroy / gd_destroy.  The received
- * messages are in arrival order = (sender rank, sender batch order); perm / offsets are the
- * stable per-activation bucketing of that order (offsets: n_act + 2 entries). */
+ * messages are in arrival order = (sender rank, table region, sender batch order): each sender
+ * groups its chunk for an owner by the eighth of the owner's directory table the grain's home slot
+ * lies in (region 0 for system targets, the membership grain and KeyExt grains), so the owner's
+ * probe maps one region to one XCD.  Without header compaction (GD_COMPACT_HEADERS=0) or with
+ * GD_REGION_PROBE=0 on the sender, or more than 32 ranks, the order is (sender rank, sender batch
+ * order).  One grain has one region, so every activation's messages are in (sender rank, sender
+ * batch order) either way; perm / offsets are the stable per-activation bucketing of the arrival
+ * order (offsets: n_act + 2 entries). */
 typedef struct gd_multi_result {
     uint32_t        n_recv;       /* messages this rank owns in this batch            */
     uint32_t        n_act;

@@ -669,3 +669,39 @@ def route_batch_np(keys: np.ndarray, spec: RingSpec, directory: DirectoryArrays,
     status[mtm] = ST_MEMBERSHIP; silo[mtm] = seed_silo; owner[mtm] = seed_silo; act[mtm] = M32
     status[is_st] = ST_SYSTEM_TARGET; silo[is_st] = my_silo; owner[is_st] = my_silo; act[is_st] = M32
     return status, silo, act, owner, h
+
+
+def fmix32_np(h: np.ndarray) -> np.ndarray:
+    """MurmurHash3's 32-bit finaliser, vectorised (the table's home-slot mix, gd_common.h fmix32)."""
+    h = np.asarray(h, dtype=np.uint64) & np.uint64(M32)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & np.uint64(M32)
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & np.uint64(M32)
+    h ^= h >> np.uint64(16)
+    return h.astype(np.uint32)
+
+
+N_REGIONS = 8
+
+
+def table_region_np(keys: np.ndarray) -> np.ndarray:
+    """The owner's table region of each message (not a reference concept: the library's exchange
+    order): the top 3 bits of fmix32(uniform hash) for a grain the owner probes in its
+    directory table -- the eighth of the table its home slot falls in -- and 0 for system targets,
+    the membership grain and KeyExt / geo-client grains (LocalGrainDirectory.cs:480-503 route
+    those without the table)."""
+    keys = np.asarray(keys, dtype=np.uint64).reshape(-1, 3)
+    n0, n1, tcd = keys[:, 0], keys[:, 1], keys[:, 2]
+    cat = (tcd >> np.uint64(56)).astype(np.uint32)
+    mt = MEMBERSHIP_TABLE_ID
+    special = ((cat == CAT_SYSTEM_TARGET) | (cat == CAT_KEYEXT_GRAIN) | (cat == CAT_GEO_CLIENT) |
+               ((n0 == np.uint64(mt.n0)) & (n1 == np.uint64(mt.n1)) & (tcd == np.uint64(mt.tcd))))
+    reg = fmix32_np(jenkins_u64x3_np(tcd, n0, n1)) >> np.uint32(32 - 3)
+    return np.where(special, 0, reg).astype(np.uint32)
+
+
+def region_order(keys: np.ndarray) -> np.ndarray:
+    """Positions of one sender's chunk in the order the owner receives them from gd_route_multi:
+    stable by table region (table_region_np), batch order within a region."""
+    return np.argsort(table_region_np(keys), kind="stable")

@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(BLOCK) k_ad_find(const gd_key* __restrict__ ke
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
-    unsigned long long s = fmix32(uniform_hash(n0, n1, tcd)) & t.mask;
+    unsigned long long s = home_slot(uniform_hash(n0, n1, tcd), t.mask);
     uint32_t res = NONE32;
     for (uint32_t p = 0; p <= t.ctr->max_probe; ++p) {
         const Slot sl = t.slots[s];

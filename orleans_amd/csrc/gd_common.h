@@ -104,4 +104,24 @@ GD_HD uint32_t fmix32(uint32_t h) {
     return h;
 }
 
+// Home slot of a grain in a directory table of mask + 1 slots (a power of two, at most 2^32): the
+// TOP bits of fmix32(uniform hash) (multiply-shift), so that the table's eighths hold the grains of
+// region fmix32(h) >> 29 whatever its size -- the region the exchange groups messages by, and the
+// owner's probe workgroups are mapped by (one region per XCD, its L2 serving one eighth of the table).
+// The home slot is the first of an aligned group of SLOT_GROUP slots (2 x 32 B = one 64-B DRAM
+// atom): linear probing from the group start, so the lookup (route_m_core) reads a whole group per
+// round trip.  At load 0.5 a 64-lane wave waits on the longest chain of its lanes: ~7.7 dependent
+// rounds with one slot a round, ~4.1 with two (tools/sim_probe_rounds.py).  Measured on cfg 2:
+// k_route 0.385 (1 slot) / 0.366 (2) / 0.382 (4) / 0.675 ms (8).
+#ifndef GD_SLOT_GROUP
+#define GD_SLOT_GROUP 2
+#endif
+constexpr uint32_t SLOT_GROUP = GD_SLOT_GROUP;
+static_assert((SLOT_GROUP & (SLOT_GROUP - 1)) == 0 && SLOT_GROUP <= 1024, "slot group: a power of two <= 1024");
+GD_HD unsigned long long home_slot(uint32_t h, unsigned long long mask) {
+    return (((unsigned long long)fmix32(h) * (mask + 1ull)) >> 32) & ~(unsigned long long)(SLOT_GROUP - 1);
+}
+constexpr uint32_t N_REGIONS = 8;
+GD_HD uint32_t grain_region(uint32_t h) { return fmix32(h) >> 29; }
+
 }  // namespace gd

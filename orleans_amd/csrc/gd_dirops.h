@@ -34,7 +34,7 @@ __global__ void __launch_bounds__(BLOCK) k_dir_lookup_tagged(const gd_key* __res
     if (i >= n) return;
     const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
     const uint32_t h = uniform_hash(n0, n1, tcd);
-    unsigned long long s = fmix32(h) & tab.mask;
+    unsigned long long s = home_slot(h, tab.mask);
     const uint32_t max_probe = tab.ctr->max_probe;
     gd_val v{NONE32, NONE32};
     int32_t tag = 0;

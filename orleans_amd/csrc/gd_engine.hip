@@ -170,11 +170,11 @@ struct gd_handle {
     int radix_max_bits = 8;   // digit width cap (GD_RADIX_MAXBITS, 4..11)
     int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
-    uint32_t hist_tpb = 0;
-    bool hist_xcd = true;       // multi-tile histograms in reverse XCD tile order (GD_HIST_XCD)      // tiles per workgroup in the radix histogram, 1/4/8 (GD_HIST_TPB);
-                                // 0 = by size: 4 for 1024..4096 tiles (4M..16M keys), else 1 (A/B)
-    bool compact_headers = true;
-    bool narrow_headers = true;     // compact headers as u32 N1s when every N1 < 2^32 (GD_NARROW_HEADERS=0: u64)   // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
+    uint32_t hist_tpb = 0;      // tiles per workgroup in the radix histogram, 1/4/8 (GD_HIST_TPB); 0 = by size
+    bool hist_xcd = true;       // multi-tile histograms in reverse XCD tile order (GD_HIST_XCD)
+    bool compact_headers = true;    // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
+    bool region_probe = false;      // gd_route_multi: chunks ordered by table region, region-mapped probe (GD_REGION_PROBE)
+    bool narrow_headers = true;     // compact headers as u32 N1s when every N1 < 2^32 (GD_NARROW_HEADERS=0: u64)
     bool fused_starts = true;
     bool radix_pack = true;     // 6-B packed records between radix passes when they fit (GD_RADIX_PACK)
     bool radix_rowscan = true;  // one scan launch per radix pass, digit rows (GD_RADIX_ROWSCAN=0: reduce + down)
@@ -332,6 +332,7 @@ int pull_counters(gd_handle* h) {
 }
 
 int alloc_table(gd_handle* h, unsigned long long cap, Slot** out) {
+    if (cap > (1ull << 32)) return set_err(h, GD_EINVAL, "table of %llu slots: at most 2^32 (home_slot)", cap);
     Slot* s = nullptr;
     hipError_t e = hipMalloc(&s, cap * sizeof(Slot));
     if (e != hipSuccess) return set_err(h, GD_ENOMEM, "table hipMalloc(%llu slots): %s", cap, hipGetErrorString(e));
@@ -376,11 +377,12 @@ template <int MODE>
 int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uint32_t n, uint32_t* silo,
                   uint32_t* act, uint8_t* status) {
     const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    const uint32_t xcd = h->route_xcd ? 1u : 0u;
     if (n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4>, k, n, ring_args(h), table_args(h),
-                      silo, act, status, tcd, h->route_xcd ? 1u : 0u);
+                      silo, act, status, tcd, xcd);
     return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8>, k, n, ring_args(h), table_args(h),
-                  silo, act, status, tcd, h->route_xcd ? 1u : 0u);
+                  silo, act, status, tcd, xcd);
 }
 
 int route_n1_device(gd_handle* h, const void* n1s, uint32_t n1w, uint64_t tcd, uint32_t n, uint32_t* silo,
@@ -392,6 +394,37 @@ int route_n1_device(gd_handle* h, const void* n1s, uint32_t n1w, uint64_t tcd, u
         case GD_RING_DIRECTORY: return route_n1_mode<GD_RING_DIRECTORY>(h, k, n1w, tcd, n, silo, act, status);
         case GD_RING_CONSISTENT: return route_n1_mode<GD_RING_CONSISTENT>(h, k, n1w, tcd, n, silo, act, status);
         default: return route_n1_mode<GD_RING_VIRTUAL_BUCKETS>(h, k, n1w, tcd, n, silo, act, status);
+    }
+}
+
+// The owner's region-mapped probe (k_route_region) over m received messages: 24-B keys (n1w = 0) or
+// N1s with one TypeCodeData; seg from k_region_segments.  Not in cache mode.
+template <int MODE>
+int route_region_mode(gd_handle* h, const void* k, uint32_t n1w, uint64_t tcd, uint32_t m, const uint32_t* seg,
+                      uint32_t world, uint32_t* silo, uint32_t* act, uint8_t* status) {
+    const dim3 g(N_REGIONS * std::max<uint32_t>(1, blocks_for(m, N_REGIONS * BLOCK))), b(BLOCK);
+    const gd_key* kk = reinterpret_cast<const gd_key*>(k);
+    if (n1w == 4)
+        return launch(h, "k_route", g, b, ring_lds(h), k_route_region<MODE, 4>, kk, m, ring_args(h), table_args(h),
+                      silo, act, status, tcd, seg, world);
+    if (n1w == 8)
+        return launch(h, "k_route", g, b, ring_lds(h), k_route_region<MODE, 8>, kk, m, ring_args(h), table_args(h),
+                      silo, act, status, tcd, seg, world);
+    return launch(h, "k_route", g, b, ring_lds(h), k_route_region<MODE, 0>, kk, m, ring_args(h), table_args(h), silo,
+                  act, status, 0ull, seg, world);
+}
+
+int route_region_device(gd_handle* h, const void* k, uint32_t n1w, uint64_t tcd, uint32_t m, const uint32_t* seg,
+                        uint32_t world, uint32_t* silo, uint32_t* act, uint8_t* status) {
+    GD_TRY(check_ring(h));
+    h->routed += m;
+    switch (h->ring_mode) {
+        case GD_RING_DIRECTORY:
+            return route_region_mode<GD_RING_DIRECTORY>(h, k, n1w, tcd, m, seg, world, silo, act, status);
+        case GD_RING_CONSISTENT:
+            return route_region_mode<GD_RING_CONSISTENT>(h, k, n1w, tcd, m, seg, world, silo, act, status);
+        default:
+            return route_region_mode<GD_RING_VIRTUAL_BUCKETS>(h, k, n1w, tcd, m, seg, world, silo, act, status);
     }
 }
 
@@ -770,10 +803,10 @@ int maybe_grow_table(gd_handle* h, uint64_t incoming) {
 // ---- exchange partition (gd_shard.h) -------------------------------------------------
 template <int MODE, bool NODES>
 int shard_hist_t(gd_handle* h, const void* recs, uint32_t n, uint64_t tcd, uint32_t n_shards, uint32_t bits,
-                 uint32_t tiles, uint8_t* dest, uint32_t* hist, const ExtArgs& ext, uint32_t* kdesc) {
+                 uint32_t tiles, uint8_t* dest, uint32_t* hist, const ExtArgs& ext, uint32_t* kdesc, uint32_t regions) {
     uint32_t* n1lo = !NODES && kdesc && h->shard_n1_copy ? (uint32_t*)h->shard_n1.p : nullptr;
     return launch(h, "k_shard_hist", dim3(tiles), dim3(SH_NT), ring_lds(h), k_shard_hist<MODE, NODES>, recs, n, tcd,
-                  ring_args(h), n_shards, bits, tiles, dest, hist, ext, kdesc, n1lo);
+                  ring_args(h), n_shards, bits, tiles, dest, hist, ext, kdesc, n1lo, regions);
 }
 
 template <int BITS, bool NODES>
@@ -797,15 +830,17 @@ int shard_scatter_t(gd_handle* h, const void* recs, const uint32_t* payload, con
 template <bool NODES>
 int shard_finish(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t n, uint32_t n_shards, uint32_t bits,
                  uint32_t tiles, const uint8_t* dest, uint32_t* hist, void* out_recs, uint32_t* out_pay,
-                 uint32_t* counts, const uint32_t* kdesc = nullptr);
+                 uint32_t* counts, const uint32_t* kdesc = nullptr, uint32_t group = 1);
 
 // Stable partition of n records (gd_key or u32 node ids) by destination rank, payload alongside
 // (payload == nullptr: the batch index); counts[d] per destination.  kdesc != nullptr (keys): the
 // header-compaction descriptor (k_key_desc) is built, and a compact batch is written as N1 only.
+// regions = N_REGIONS (keys): each rank's chunk is ordered by the grains' table region on the owner
+// (then batch order), for the owner's region-mapped probe; counts stay per rank.
 template <bool NODES>
 int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t n, uint64_t tcd, uint32_t n_shards,
                void* out_recs, uint32_t* out_pay, uint32_t* counts, const ExtArgs& ext = ExtArgs{},
-               uint32_t* kdesc = nullptr) {
+               uint32_t* kdesc = nullptr, uint32_t regions = 1) {
     GD_TRY(check_ring(h));
     if (kdesc) HIP_TRY(h, hipMemsetAsync(kdesc, 0, 16, h->stream));
     if (n == 0) {
@@ -814,27 +849,32 @@ int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t
                           h->narrow_headers ? 1u : 0u));
         return launch(h, "k_fill", dim3(1), dim3(BLOCK), 0, k_fill_u32, counts, n_shards, 0u);
     }
+    if (NODES || n_shards * regions > 256) regions = 1;
+    const uint32_t n_dest = n_shards * regions;
     const uint32_t tiles = blocks_for(n, SH_TILE);
-    if ((uint64_t)tiles * n_shards > 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "batch too large to partition");
+    if ((uint64_t)tiles * n_dest > 0xFFFFFFFFull) return set_err(h, GD_EINVAL, "batch too large to partition");
     GD_TRY(ensure(h, h->shard_dest, (size_t)n));
-    GD_TRY(ensure(h, h->shard_hist, (size_t)tiles * n_shards * 4));
+    GD_TRY(ensure(h, h->shard_hist, (size_t)tiles * n_dest * 4));
     if (!NODES && kdesc) GD_TRY(ensure(h, h->shard_n1, (size_t)n * 4));
     uint8_t* dest = (uint8_t*)h->shard_dest.p;
     uint32_t* hist = (uint32_t*)h->shard_hist.p;
     uint32_t bits = 1;
-    while ((1u << bits) < n_shards) ++bits;
+    while ((1u << bits) < n_dest) ++bits;
     switch (h->ring_mode) {
         case GD_RING_DIRECTORY:
-            GD_TRY((shard_hist_t<GD_RING_DIRECTORY, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext, kdesc)));
+            GD_TRY((shard_hist_t<GD_RING_DIRECTORY, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext, kdesc,
+                                                           regions)));
             break;
         case GD_RING_CONSISTENT:
-            GD_TRY((shard_hist_t<GD_RING_CONSISTENT, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext, kdesc)));
+            GD_TRY((shard_hist_t<GD_RING_CONSISTENT, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext,
+                                                            kdesc, regions)));
             break;
         default:
-            GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist, ext, kdesc)));
+            GD_TRY((shard_hist_t<GD_RING_VIRTUAL_BUCKETS, NODES>(h, recs, n, tcd, n_shards, bits, tiles, dest, hist,
+                                                                 ext, kdesc, regions)));
     }
     return shard_finish<NODES>(h, recs, payload, n, n_shards, bits, tiles, dest, hist, out_recs, out_pay, counts,
-                               kdesc);
+                               kdesc, regions);
 }
 
 // Forward partition of routed messages by the rank hosting their activation (k_fwd_hist): keys
@@ -859,13 +899,14 @@ int fwd_pack(gd_handle* h, const gd_key* keys, const uint8_t* st, const uint32_t
 template <bool NODES>
 int shard_finish(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t n, uint32_t n_shards, uint32_t bits,
                  uint32_t tiles, const uint8_t* dest, uint32_t* hist, void* out_recs, uint32_t* out_pay,
-                 uint32_t* counts, const uint32_t* kdesc) {
-    GD_TRY(scan_device<OpAdd>(h, hist, tiles * n_shards, false, false, "shard"));
+                 uint32_t* counts, const uint32_t* kdesc, uint32_t group) {
+    GD_TRY(scan_device<OpAdd>(h, hist, tiles * n_shards * group, false, false, "shard"));
     // k_shard_counts also completes the compaction descriptor (kdesc, keys only)
     GD_TRY(launch(h, "k_shard_counts", dim3(1), dim3(256), 0, k_shard_counts, (const uint32_t*)hist, tiles, n_shards, n,
                   counts, NODES ? nullptr : (const gd_key*)recs, NODES ? nullptr : const_cast<uint32_t*>(kdesc),
-                  h->narrow_headers ? 1u : 0u));
+                  h->narrow_headers ? 1u : 0u, group));
     const uint32_t* gs = hist;
+    n_shards *= group;                  // the scatter's destinations: (rank, region) pairs
     switch (bits) {
         case 1: return shard_scatter_t<1, NODES>(h, recs, payload, dest, n, n_shards, tiles, gs, out_recs, out_pay,
                                                    kdesc);
@@ -997,6 +1038,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_HIST_XCD")) h->hist_xcd = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_FAN_ILP")) h->fan_ilp = std::atoi(v);
     if (const char* v = std::getenv("GD_BUCKET2")) h->bucket2 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_REGION_PROBE")) h->region_probe = std::atoi(v) != 0;
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));
@@ -3043,15 +3085,18 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     uint32_t* kdesc = dcnt + 4 * W;
     int32_t* send_len = (int32_t*)SB[3].p;
     uint32_t* send_boff = (uint32_t*)SB[4].p;
+    uint32_t regions = 1;
     {
         OnPStream on(h);
+        // region order needs the descriptor: its flag tells the owners (k_shard_counts)
+        regions = h->region_probe && h->compact_headers && !h->cache_max && W * N_REGIONS <= 256 ? N_REGIONS : 1u;
         GD_TRY(shard_pack<false>(h, d_keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt, x,
-                                 h->compact_headers ? kdesc : nullptr));
+                                 h->compact_headers ? kdesc : nullptr, regions));
         if (!h->compact_headers) HIP_TRY(h, hipMemsetAsync(kdesc, 0, 16, h->stream));
         if (has_ext) {                 // KeyExt bytes per destination; lengths and byte offsets in send order
             HIP_TRY(h, hipMemsetAsync(dcnt + 2 * W, 0, (size_t)W * 4, h->stream));
             GD_TRY(launch(h, "k_dest_bytes", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_dest_bytes,
-                          (const uint8_t*)h->shard_dest.p, n, x, (uint32_t)W, dcnt + 2 * W));
+                          (const uint8_t*)h->shard_dest.p, n, x, (uint32_t)W, dcnt + 2 * W, regions));
             GD_TRY(launch(h, "k_send_lengths", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_send_lengths,
                           (const uint32_t*)send_idx, n, x, send_len, send_boff));
             GD_TRY(scan_device<OpAdd>(h, send_boff, n, false, false, "ext_offsets"));
@@ -3110,8 +3155,11 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     uint64_t n1_tcd = 0;
     uint32_t n1_mode = 0;                          // every received chunk in one compact mode (u64 / u32)
     bool n1_first = true;
+    // every non-empty chunk ordered by region (descriptor flag 4): the region-mapped probe
+    bool by_region = !h->cache_max && m > 0;
     for (int r = 0; r < W; ++r) {
         const uint32_t c = hd[4 + 4 * r];
+        if (rc[r] && !(hd[4 + 4 * r + 1] & KD_REGIONS)) by_region = false;
         any_compact |= c && rc[r];
         hsb[r + 1] = hsb[r] + sc[r] * my_esz;
         hrb[r + 1] = hrb[r] + rc[r] * header_bytes(c);
@@ -3127,9 +3175,11 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     const size_t m4 = (size_t)m * 4 + 4, n4 = (size_t)n * 4 + 4;
     const size_t want[20] = {(size_t)m * sizeof(gd_key) + 8, m4, m4, m4, m4, (size_t)m + 4, m4,
                              ((size_t)n_act + 2) * 4, n4, n4, (size_t)n + 4, n4, n4, (size_t)n + 4,
-                             m4, (size_t)rboff[W] + 16, m4, (size_t)m * 8 + 8, (size_t)hrb[W] + 16, 0};
+                             m4, (size_t)rboff[W] + 16, m4, (size_t)m * 8 + 8, (size_t)hrb[W] + 16,
+                             (size_t)W * (N_REGIONS + 1) * 4};
     for (int b = 0; b < 20; ++b)
-        if (want[b] && (b < 8 || (ret && b < 14) || (has_ext && b >= 14 && b < 18) || (any_compact && b == 18)))
+        if (want[b] && (b < 8 || (ret && b < 14) || (has_ext && b >= 14 && b < 18) || (any_compact && b == 18) ||
+                        (by_region && b == 19)))
             GD_TRY(grow(h, B[b], want[b]));
     if (has_ext) GD_TRY(grow(h, SB[5], (size_t)sboff[W] + 16));
     gd_key* recv_keys = (gd_key*)B[0].p;
@@ -3170,6 +3220,21 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         else
             GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
                           (const uint32_t*)(dcnt + W), (uint32_t)W, m, recv_src));
+        if (by_region) {               // where each sender's region runs start (binary search per chunk)
+            const uint32_t nt = (uint32_t)W * (N_REGIONS + 1);
+            const uint32_t* rcnt = dcnt + W;
+            uint32_t* seg = (uint32_t*)B[19].p;
+            const uint32_t w1 = n1_path ? header_bytes(n1_mode) : 0u;
+            if (w1 == 4)
+                GD_TRY(launch(h, "k_region_segments", dim3(blocks_for(nt, 64)), dim3(64), 0, k_region_segments<4>,
+                              (const void*)B[18].p, rcnt, (uint32_t)W, n1_tcd, seg));
+            else if (w1 == 8)
+                GD_TRY(launch(h, "k_region_segments", dim3(blocks_for(nt, 64)), dim3(64), 0, k_region_segments<8>,
+                              (const void*)B[18].p, rcnt, (uint32_t)W, n1_tcd, seg));
+            else
+                GD_TRY(launch(h, "k_region_segments", dim3(blocks_for(nt, 64)), dim3(64), 0, k_region_segments<0>,
+                              (const void*)recv_keys, rcnt, (uint32_t)W, 0ull, seg));
+        }
         HIP_TRY(h, hipEventRecord(h->x_hdr[s], h->xstream));
         if (n1_path && keep_keys) {    // the 24-B keys for the result, beside the probe
             GD_TRY(launch(h, "k_recv_expand", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_expand,
@@ -3184,7 +3249,10 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     }
     // 3. probe + bucket on the owner (the handle's stream)
     HIP_TRY(h, hipStreamWaitEvent(h->stream, h->x_hdr[s], 0));
-    if (n1_path) GD_TRY(route_n1_device(h, B[18].p, header_bytes(n1_mode), n1_tcd, m, silo, act, st));
+    if (by_region)
+        GD_TRY(route_region_device(h, n1_path ? B[18].p : (const void*)recv_keys, n1_path ? header_bytes(n1_mode) : 0u,
+                                   n1_tcd, m, (const uint32_t*)B[19].p, (uint32_t)W, silo, act, st));
+    else if (n1_path) GD_TRY(route_n1_device(h, B[18].p, header_bytes(n1_mode), n1_tcd, m, silo, act, st));
     else if (m) GD_TRY(route_device(h, recv_keys, m, silo, act, st));
     if (m && has_ext)                  // the received strings: KeyExt grains are routed on their owner
         GD_TRY(keyext_pass(h, recv_keys,

@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict_
 #pragma unroll
         for (int q = 0; q < ILP; ++q) {
             h[q] = uniform_hash(0, target[q], tcd);
-            sl[q] = fmix32(h[q]) & tab.mask;
+            sl[q] = home_slot(h[q], tab.mask);
             if (live[q]) {
                 const uint4* a = reinterpret_cast<const uint4*>(tab.slots + sl[q]);
                 qa[q] = a[0];

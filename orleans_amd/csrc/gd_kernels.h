@@ -147,7 +147,7 @@ __device__ __forceinline__ bool is_membership(uint64_t n0, uint64_t n1, uint64_t
 __device__ __forceinline__ bool probe(const Slot* slots, unsigned long long mask, uint32_t max_probe,
                                       uint32_t h, uint64_t n0, uint64_t n1, uint64_t tcd,
                                       uint32_t& act, uint32_t& meta) {
-    unsigned long long s = fmix32(h) & mask;
+    unsigned long long s = home_slot(h, mask);
     for (uint32_t p = 0; p <= max_probe; ++p) {
         const uint4* q = reinterpret_cast<const uint4*>(slots + s);
         const uint4 a = q[0];
@@ -302,16 +302,18 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
             need[j] = true;
         }
     }
-    // first probe of every message, all in flight together; the ring search (LDS) runs under them
+    // first probe of every message, all in flight together; the ring search (LDS) runs under them.
+    // A round reads the whole aligned group of SLOT_GROUP slots (home_slot) and walks it in order.
+    constexpr int RG = (int)SLOT_GROUP;
     unsigned long long s[M];
-    uint4 qa[M], qb[M];
+    uint4 q[M][2 * RG];
 #pragma unroll
     for (int j = 0; j < M; ++j) {
-        s[j] = fmix32(h[j]) & tab.mask;
+        s[j] = home_slot(h[j], tab.mask);
         if (need[j]) {
-            const uint4* q = reinterpret_cast<const uint4*>(tab.slots + s[j]);
-            qa[j] = q[0];
-            qb[j] = q[1];
+            const uint4* qp = reinterpret_cast<const uint4*>(tab.slots + s[j]);
+#pragma unroll
+            for (int g = 0; g < 2 * RG; ++g) q[j][g] = qp[g];
         }
     }
 #pragma unroll
@@ -320,28 +322,36 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
 #pragma unroll
     for (int j = 0; j < M; ++j) {
         if (!need[j]) continue;
-        uint4 a = qa[j], b = qb[j];
+        bool done = false;
         for (uint32_t p = 0;;) {
-            const uint32_t stt = slot_state(b.w);
-            if (stt == SLOT_EMPTY) break;
-            const uint64_t k0 = (uint64_t)a.x | ((uint64_t)a.y << 32);
-            const uint64_t k1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
-            const uint64_t k2 = (uint64_t)b.x | ((uint64_t)b.y << 32);
-            if (stt == SLOT_LIVE && k0 == n0[j] && k1 == n1[j] && k2 == tcd[j]) {
-                if (b.z == GD_ACT_MULTI) {                    // several activations: the C# random
-                    status[j] = GD_ROUTE_MULTI_ACT;           // choice (RandomPlacementDirector.cs:33-53)
-                } else if (tab_silo_valid(tab, slot_silo(b.w))) {
-                    act[j] = b.z;
-                    silo[j] = slot_silo(b.w);                 // ActivationAddress.Silo (Message.cs:629-639)
-                    status[j] = GD_ROUTE_OK;
-                }                                             // else: IsValidSilo filtered it (:431) -> MISS
-                break;
+#pragma unroll
+            for (int g = 0; g < RG; ++g) {
+                if (done) continue;
+                const uint4 a = q[j][2 * g], b = q[j][2 * g + 1];
+                const uint32_t stt = slot_state(b.w);
+                const uint64_t k0 = (uint64_t)a.x | ((uint64_t)a.y << 32);
+                const uint64_t k1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
+                const uint64_t k2 = (uint64_t)b.x | ((uint64_t)b.y << 32);
+                if (stt == SLOT_EMPTY) {
+                    done = true;                                  // miss
+                } else if (stt == SLOT_LIVE && k0 == n0[j] && k1 == n1[j] && k2 == tcd[j]) {
+                    if (b.z == GD_ACT_MULTI) {                    // several activations: the C# random
+                        status[j] = GD_ROUTE_MULTI_ACT;           // choice (RandomPlacementDirector.cs:33-53)
+                    } else if (tab_silo_valid(tab, slot_silo(b.w))) {
+                        act[j] = b.z;
+                        silo[j] = slot_silo(b.w);                 // ActivationAddress.Silo (Message.cs:629-639)
+                        status[j] = GD_ROUTE_OK;
+                    }                                             // else: IsValidSilo filtered it (:431) -> MISS
+                    done = true;
+                } else if (++p > max_probe) {
+                    done = true;                                  // miss: Dispatcher.cs:742 slow path
+                }
             }
-            if (++p > max_probe) break;                        // miss: Dispatcher.cs:742 slow path
-            s[j] = (s[j] + 1) & tab.mask;
-            const uint4* q = reinterpret_cast<const uint4*>(tab.slots + s[j]);
-            a = q[0];
-            b = q[1];
+            if (done) break;
+            s[j] = (s[j] + RG) & tab.mask;
+            const uint4* qp = reinterpret_cast<const uint4*>(tab.slots + s[j]);
+#pragma unroll
+            for (int g = 0; g < 2 * RG; ++g) q[j][g] = qp[g];
         }
     }
 #pragma unroll
@@ -422,6 +432,53 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
                                                0);
 }
 
+// The owner's probe over received chunks grouped by region (gd_route_multi with regions, SURVEY 8 e):
+// workgroup b takes region g = b % 8.  Workgroups are dispatched round-robin over the 8 XCDs (b -> XCD
+// b % 8), so all of one XCD's workgroups probe one eighth of the table (home_slot's top bits) and its
+// 4-MB L2 serves that eighth alone (tools/ubench_random.hip: 16M probes of a 64-MB table 0.344 ->
+// 0.224 ms).  The region's messages are W segments, one per sender (seg: k_region_segments); the
+// G = gridDim.x / 8 workgroups of a region take its blocks of BLOCK messages grid-stride.
+template <int MODE, int N1W>
+__global__ void __launch_bounds__(BLOCK) k_route_region(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+                                                        TableArgs tab, uint32_t* __restrict__ out_silo,
+                                                        uint32_t* __restrict__ out_act,
+                                                        uint8_t* __restrict__ out_status, uint64_t tcd_u,
+                                                        const uint32_t* __restrict__ seg, uint32_t world) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    __shared__ uint32_t s_beg[257], s_pre[257];
+    uint32_t* s_pts = s_ring;
+    uint32_t* s_own = s_ring + ring.n;
+    const uint32_t g = blockIdx.x % N_REGIONS, G = gridDim.x / N_REGIONS;
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t q = 0; q < world; ++q) {
+            const uint32_t b = seg[q * (N_REGIONS + 1) + g], e = seg[q * (N_REGIONS + 1) + g + 1];
+            s_beg[q] = b;
+            s_pre[q] = run;
+            run += e - b;
+        }
+        s_pre[world] = run;
+    }
+    stage_ring(ring, s_pts, s_own);                   // its barrier publishes s_beg / s_pre too
+    const uint32_t total = s_pre[world];
+    const uint32_t max_probe = tab.ctr->max_probe;
+    for (uint32_t k = blockIdx.x / N_REGIONS; k * BLOCK < total; k += G) {
+        const uint32_t e = k * BLOCK + threadIdx.x;
+        uint32_t i = n;                                // past the region: route_m_core skips it
+        if (e < total) {
+            uint32_t lo = 0, hi = world;               // largest q with s_pre[q] <= e
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_pre[mid] <= e) lo = mid;
+                else hi = mid;
+            }
+            i = s_beg[lo] + (e - s_pre[lo]);
+        }
+        route_m_core<MODE, 1, BLOCK, false, N1W, true>(keys, n, i, ring, s_pts, s_own, tab, max_probe, out_silo,
+                                                      out_act, out_status, tcd_u, nullptr, 0);
+    }
+}
+
 // GetPrimaryTargetSilo(uint key) over raw ring keys.
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK) k_ring_hashes(const uint32_t* __restrict__ hashes, uint32_t n,
@@ -461,7 +518,7 @@ __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __restrict__ 
         return;
     }
     const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
-    unsigned long long s = fmix32(uniform_hash(n0, n1, tcd)) & mask;
+    unsigned long long s = home_slot(uniform_hash(n0, n1, tcd), mask);
     unsigned long long dist = 0;
     uint32_t res = NONE32;
     uint8_t fresh = 0;
@@ -610,7 +667,7 @@ __global__ void __launch_bounds__(BLOCK) k_unreg_find(const gd_key* __restrict__
     if (i >= n) return;
     const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
     const uint32_t h = uniform_hash(n0, n1, tcd);
-    unsigned long long s = fmix32(h) & mask;
+    unsigned long long s = home_slot(h, mask);
     uint32_t res = NONE32;
     for (uint32_t p = 0; p <= ctr->max_probe; ++p) {
         const Slot sl = slots[s];
@@ -674,7 +731,7 @@ __global__ void __launch_bounds__(BLOCK) k_rehash(const Slot* __restrict__ old_s
     if (j >= old_cap) return;
     const Slot sl = old_slots[j];
     if (slot_state(sl.meta) != SLOT_LIVE) return;
-    unsigned long long s = fmix32(uniform_hash(sl.n0, sl.n1, sl.tcd)) & mask;
+    unsigned long long s = home_slot(uniform_hash(sl.n0, sl.n1, sl.tcd), mask);
     for (uint32_t dist = 0; dist <= mask; ++dist) {
         uint32_t expected = make_meta(SLOT_EMPTY, 0);
         if (__hip_atomic_compare_exchange_strong(&slots[s].meta, &expected, make_meta(SLOT_CLAIMED, 0),

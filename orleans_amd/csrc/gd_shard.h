@@ -29,12 +29,15 @@ constexpr uint32_t SH_TILE = SH_NT * SH_IT;   // 2048 records per tile
 
 // Owner rank of message i.  KeyExt grains go to the owner of their KeyExt hash when the batch's
 // strings are given (ext.len != nullptr, gd_route_multi_ext), else they stay here (KEYEXT).
+// region (optional): the grain's table region on its owner (grain_region of its uniform hash) for a
+// grain the owner probes in its directory table, 0 for everything else.
 template <int MODE>
 __device__ __forceinline__ uint32_t key_dest(uint64_t n0, uint64_t n1, uint64_t tcd, const uint32_t* s_pts,
                                              const uint32_t* s_own, const RingArgs& ring, uint32_t n_shards,
-                                             const ExtArgs& ext, uint32_t i) {
+                                             const ExtArgs& ext, uint32_t i, uint32_t* region = nullptr) {
     const uint32_t cat = (uint32_t)(tcd >> 56);
     uint32_t silo;
+    if (region) *region = 0;
     const uint8_t* s;
     int32_t len;
     if ((cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) && ext.len && ext_of(ext, i, s, len)) {
@@ -51,7 +54,11 @@ __device__ __forceinline__ uint32_t key_dest(uint64_t n0, uint64_t n1, uint64_t 
         silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uh)];
     } else if (cat == CAT_SYSTEM_TARGET || cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) silo = ring.my_silo;
     else if (is_membership(n0, n1, tcd)) silo = ring.seed_silo;
-    else silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(n0, n1, tcd))];
+    else {
+        const uint32_t uh = uniform_hash(n0, n1, tcd);
+        silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uh)];
+        if (region) *region = grain_region(uh);
+    }
     return (silo == NONE32 ? ring.my_silo : silo) % n_shards;
 }
 
@@ -59,12 +66,15 @@ __device__ __forceinline__ uint32_t key_dest(uint64_t n0, uint64_t n1, uint64_t 
 // Counts per wave by ballot matching (the lowest lane of each destination group adds the group's
 // size), not per-lane LDS atomics: with few destinations every lane of a wave would hit one
 // counter.  `bits` = destination bits (n_shards <= 1 << bits).
+// regions (keys only; 1 or N_REGIONS): destination = owner rank * regions + the grain's table region,
+// so each rank's chunk arrives grouped by region (gd_route_multi's region-mapped probe).
 template <int MODE, bool NODES>
 __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ recs, uint32_t n, uint64_t tcd,
                                                       RingArgs ring, uint32_t n_shards, uint32_t bits,
                                                       uint32_t tiles, uint8_t* __restrict__ dest,
                                                       uint32_t* __restrict__ hist, ExtArgs ext,
-                                                      uint32_t* __restrict__ kdesc, uint32_t* __restrict__ n1lo) {
+                                                      uint32_t* __restrict__ kdesc, uint32_t* __restrict__ n1lo,
+                                                      uint32_t regions) {
     constexpr int NW = SH_NT / WAVE;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     __shared__ uint32_t s_wc[NW][256];
@@ -107,7 +117,9 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
                 const uint32_t node = (uint32_t)kv[r][0];
                 d = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(0, node, tcd))] % n_shards;
             } else {
-                d = key_dest<MODE>(kv[r][0], kv[r][1], kv[r][2], s_pts, s_own, ring, n_shards, ext, i);
+                uint32_t reg = 0;
+                d = key_dest<MODE>(kv[r][0], kv[r][1], kv[r][2], s_pts, s_own, ring, n_shards, ext, i,
+                                   regions > 1 ? &reg : nullptr) * regions + reg;
                 wide |= kv[r][0] != 0 || kv[r][2] != ref_tcd;
                 big |= (kv[r][1] >> 32) != 0;
                 if (n1lo) n1lo[i] = (uint32_t)kv[r][1];   // the gather's 4-B header source (mode 2)
@@ -128,7 +140,8 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
             if (lane == 0 && (any_wide || any_big)) atomicOr(&kdesc[1], (any_wide ? 1u : 0u) | (any_big ? 2u : 0u));
         }
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < n_shards; d += SH_NT) {
+    const uint32_t n_dest = NODES ? n_shards : n_shards * regions;
+    for (uint32_t d = threadIdx.x; d < n_dest; d += SH_NT) {
         uint32_t t = 0;
 #pragma unroll
         for (int ww = 0; ww < NW; ++ww) t += s_wc[ww][d];
@@ -151,6 +164,9 @@ __global__ void k_key_desc(const gd_key* __restrict__ keys, uint32_t n, uint32_t
     kdesc[2] = (uint32_t)tcd;
     kdesc[3] = (uint32_t)(tcd >> 32);
 }
+
+// Descriptor flag (kdesc[1]): every chunk of the sender is ordered by region (k_shard_hist with regions).
+constexpr uint32_t KD_REGIONS = 4u;
 
 // Header bytes of a chunk by its sender's descriptor mode.
 __host__ __device__ __forceinline__ uint32_t header_bytes(uint32_t mode) { return mode == 2 ? 4u : mode ? 8u : 24u; }
@@ -542,9 +558,11 @@ __global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict
 // counts[d] = records for destination d, from the scanned (dest, tile) bases.
 // kdesc != nullptr: thread 0 also completes the header-compaction descriptor (k_key_desc's work;
 // k_shard_hist's flags are final by now), one launch fewer on the partition stream.
+// counts[d] for the n_shards ranks; with regions, rank d's destinations are d * group .. (d + 1) * group
+// - 1 (its region chunks, contiguous in the send buffer).
 __global__ void k_shard_counts(const uint32_t* __restrict__ gscan, uint32_t tiles, uint32_t n_shards, uint32_t n,
                                uint32_t* __restrict__ counts, const gd_key* __restrict__ keys,
-                               uint32_t* __restrict__ kdesc, uint32_t narrow_ok) {
+                               uint32_t* __restrict__ kdesc, uint32_t narrow_ok, uint32_t group) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (kdesc && d == 0) {
         const uint64_t tcd = n ? reinterpret_cast<const uint64_t*>(keys)[2] : 0ull;
@@ -553,10 +571,51 @@ __global__ void k_shard_counts(const uint32_t* __restrict__ gscan, uint32_t tile
         kdesc[2] = (uint32_t)tcd;
         kdesc[3] = (uint32_t)(tcd >> 32);
     }
+    if (kdesc && d == 0 && group > 1) kdesc[1] |= KD_REGIONS;
     if (d >= n_shards) return;
-    const uint32_t start = gscan[d * tiles];
-    const uint32_t end = d + 1 < n_shards ? gscan[(d + 1) * tiles] : n;
+    const uint32_t start = gscan[(size_t)d * group * tiles];
+    const uint32_t end = d + 1 < n_shards ? gscan[(size_t)(d + 1) * group * tiles] : n;
     counts[d] = end - start;
+}
+
+// Region segments of the received chunks (gd_route_multi with regions): every sender's chunk arrives
+// sorted by region (k_shard_hist with regions), so thread (q, g) binary-searches chunk q for the first
+// message of region >= g.  seg[q * (N_REGIONS + 1) + g] = that position in the receive order
+// (seg[.. + N_REGIONS] = the chunk's end).  Keys: 24-B (N1W = 0) or N1s (N1W = 4 / 8, N0 = 0, tcd).
+template <int N1W>
+__global__ void k_region_segments(const void* __restrict__ keys, const uint32_t* __restrict__ rcount,
+                                  uint32_t world, uint64_t tcd, uint32_t* __restrict__ seg) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= world * (N_REGIONS + 1)) return;
+    const uint32_t q = t / (N_REGIONS + 1), g = t % (N_REGIONS + 1);
+    uint32_t lo = 0;
+    for (uint32_t r = 0; r < q; ++r) lo += rcount[r];
+    uint32_t hi = lo + rcount[q];
+    if (g == N_REGIONS) {
+        seg[t] = hi;
+        return;
+    }
+    auto region_at = [&](uint32_t i) -> uint32_t {
+        uint64_t n0 = 0, n1, c = tcd;
+        if constexpr (N1W == 8) n1 = reinterpret_cast<const uint64_t*>(keys)[i];
+        else if constexpr (N1W == 4) n1 = reinterpret_cast<const uint32_t*>(keys)[i];
+        else {
+            const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys) + 3ull * i;
+            n0 = kp[0];
+            n1 = kp[1];
+            c = kp[2];
+        }
+        const uint32_t cat = (uint32_t)(c >> 56);
+        if (cat == CAT_SYSTEM_TARGET || cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT || is_membership(n0, n1, c))
+            return 0u;
+        return grain_region(uniform_hash(n0, n1, c));
+    };
+    while (lo < hi) {                                  // first i in [lo, hi) with region_at(i) >= g
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if (region_at(mid) < g) lo = mid + 1;
+        else hi = mid;
+    }
+    seg[t] = lo;
 }
 
 // recv_src[i] = the rank chunk i of the receive buffer came from: off[r] <= i < off[r + 1], off =
@@ -621,16 +680,17 @@ __device__ __forceinline__ uint32_t ext_bytes(const ExtArgs& e, uint32_t i) {
     return l > 0 ? (uint32_t)l : 0u;
 }
 
-// Per destination: bytes of KeyExt payload (LDS per block, one atomic per destination per block).
+// Per destination rank: bytes of KeyExt payload (LDS per block, one atomic per destination per
+// block).  group: destinations per rank in dest (N_REGIONS with a region-ordered partition).
 __global__ void __launch_bounds__(BLOCK) k_dest_bytes(const uint8_t* __restrict__ dest, uint32_t n, ExtArgs ext,
-                                                      uint32_t n_shards, uint32_t* __restrict__ out) {
+                                                      uint32_t n_shards, uint32_t* __restrict__ out, uint32_t group) {
     __shared__ uint32_t s_b[256];
     for (uint32_t d = threadIdx.x; d < 256; d += BLOCK) s_b[d] = 0;
     __syncthreads();
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i < n) {
         const uint32_t b = ext_bytes(ext, i);
-        if (b) atomicAdd(&s_b[dest[i]], b);
+        if (b) atomicAdd(&s_b[dest[i] / group], b);
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < n_shards; d += BLOCK)

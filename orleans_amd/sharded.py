@@ -277,15 +277,35 @@ class LibraryRouter:
         self.engine.gd.comm_destroy()
 
 
+def _canonical(r: ShardedResult):
+    """The owner-side result keyed by message identity (sender rank, index in the sender's batch),
+    free of the arrival order: the messages sorted by identity with their keys and routes, and each
+    activation's queue as the identities of its messages in bucket order."""
+    m = r.status.shape[0]
+    dev = r.status.device
+    idx = r.recv_idx.long() if r.recv_idx is not None else torch.arange(m, device=dev)
+    src = r.recv_src.long() if r.recv_src is not None else torch.zeros(m, dtype=torch.long, device=dev)
+    ident = src * (1 << 32) + idx
+    order = torch.argsort(ident)
+    q = ident[r.perm.long()]
+    # the trailing bucket (unrouted messages, many grains) holds them in arrival order: compare as a set
+    u = int(r.offsets[-2]) if r.offsets.numel() >= 2 else m
+    q = torch.cat([q[:u], torch.sort(q[u:]).values])
+    out = [ident[order], r.status[order], r.silo[order], r.act[order], q, r.offsets]
+    if r.recv_keys is not None:
+        out.append(r.recv_keys[order])
+    return out
+
+
 def same_result(a: ShardedResult, b: ShardedResult) -> bool:
-    """Bit-identical owner-side results (both routers on the same batch)."""
-    if a.recv_keys.shape != b.recv_keys.shape:
+    """The same owner-side results for the same batch (both routers): every message with the same
+    key and route, every activation's queue with the same messages in the same order, the same
+    offsets.  The two routers' arrival orders may differ (gd_route_multi groups a sender's chunk
+    by table region; the per-activation order (sender rank, sender order) is the same)."""
+    if a.status.shape != b.status.shape:
         return False
-    pairs = [(a.recv_keys, b.recv_keys), (a.status, b.status), (a.silo, b.silo), (a.act, b.act), (a.perm, b.perm),
-             (a.offsets, b.offsets)]
-    if a.recv_idx is not None and b.recv_idx is not None:
-        pairs += [(a.recv_idx, b.recv_idx), (a.recv_src, b.recv_src)]
-    return all(torch.equal(x, y) for x, y in pairs)
+    ca, cb = _canonical(a), _canonical(b)
+    return len(ca) == len(cb) and all(torch.equal(x, y) for x, y in zip(ca, cb))
 
 
 def silo_rank(silo: int, world: int) -> int:

@@ -26,6 +26,13 @@ TC = o.grain_type_code(o.PING_GRAIN_CLASS)
 TCD = o.type_code_data(o.CAT_GRAIN, TC)
 
 
+@pytest.fixture(autouse=True)
+def _region_order(monkeypatch):
+    """These tests expect the region-grouped arrival order (GD_REGION_PROBE=1, the sender's switch);
+    test_route_multi_local_world_plain_order runs the other."""
+    monkeypatch.setenv("GD_REGION_PROBE", "1")
+
+
 @pytest.fixture(scope="module")
 def gd():
     import torch
@@ -199,6 +206,7 @@ def test_cfg3_exchange_w8_zipf(gd):
         for s, k in enumerate(bs):
             _, _, _, owner, _ = o.route_batch_np(k, spec, full, my_silo=s)
             sel = np.nonzero(owner % W == r)[0]
+            sel = sel[o.region_order(k[sel])]     # arrival: (sender, table region, sender order)
             ks.append(k[sel]), ids.append(sel), srcs.append(np.full(len(sel), s))
         rk = np.concatenate(ks)
         stt, sl, a, _, _ = o.route_batch_np(rk, spec, full, my_silo=r)

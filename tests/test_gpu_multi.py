@@ -19,6 +19,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TC = o.grain_type_code(o.PING_GRAIN_CLASS)
 
 
+@pytest.fixture(autouse=True)
+def _region_order(monkeypatch):
+    """These tests expect the region-grouped arrival order (GD_REGION_PROBE=1, the sender's switch);
+    test_route_multi_local_world_plain_order runs the other."""
+    monkeypatch.setenv("GD_REGION_PROBE", "1")
+
+
 @pytest.fixture(scope="module")
 def gd():
     import torch
@@ -48,19 +55,20 @@ def test_route_multi_world1(gd, n):
     e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
     e.register(reg, np.arange(G), own)
     e.comm_init(gd.GrainDispatch.comm_unique_id(), 1, 0)
+    ro = o.region_order(keys)              # arrival order: by table region, batch order within one
     for ret in (False, True):
         r = e.route_multi(keys, G, return_routes=ret)
         st, silo, act, _, _ = o.route_batch_np(keys, spec, o.DirectoryArrays(reg, np.arange(G), own), my_silo=2)
-        np.testing.assert_array_equal(r["recv_keys"], keys)
-        np.testing.assert_array_equal(r["recv_idx"], np.arange(n, dtype=np.uint32))
+        np.testing.assert_array_equal(r["recv_keys"], keys[ro])
+        np.testing.assert_array_equal(r["recv_idx"], ro.astype(np.uint32))
         np.testing.assert_array_equal(r["recv_src"], np.zeros(n, np.uint32))
-        np.testing.assert_array_equal(r["status"], st)
-        np.testing.assert_array_equal(r["silo"], silo)
-        np.testing.assert_array_equal(r["act"], act)
-        wp, wo = o.bucket_stable(act, G)
+        np.testing.assert_array_equal(r["status"], st[ro])
+        np.testing.assert_array_equal(r["silo"], silo[ro])
+        np.testing.assert_array_equal(r["act"], act[ro])
+        wp, wo = o.bucket_stable(act[ro], G)
         np.testing.assert_array_equal(r["perm"], wp)
         np.testing.assert_array_equal(r["offsets"], wo)
-        if ret:
+        if ret:                            # back in the sender's batch order
             np.testing.assert_array_equal(r["ret_status"], st)
             np.testing.assert_array_equal(r["ret_silo"], silo)
             np.testing.assert_array_equal(r["ret_act"], act)
@@ -92,10 +100,11 @@ def test_route_multi_device_pointers(gd):
     assert r.n_recv == n and r.ret_act and r.perm
     got = e.multi_fetch(r, n)
     st, silo, act, _, _ = o.route_batch_np(keys, spec, o.DirectoryArrays(reg, np.arange(G), own))
-    np.testing.assert_array_equal(got["act"], act)
+    ro = o.region_order(keys)
+    np.testing.assert_array_equal(got["act"], act[ro])
     np.testing.assert_array_equal(got["ret_act"], act)
     np.testing.assert_array_equal(got["ret_silo"], silo)
-    wp, wo = o.bucket_stable(act, G)
+    wp, wo = o.bucket_stable(act[ro], G)
     np.testing.assert_array_equal(got["perm"], wp)
     np.testing.assert_array_equal(got["offsets"], wo)
     e.comm_destroy()
@@ -139,6 +148,7 @@ def test_route_multi_two_ranks_one_gpu(tmp_path):
             k = batches[s]
             _, _, _, owner, _ = o.route_batch_np(k, spec, o.DirectoryArrays(np.zeros((0, 3), np.uint64), [], []))
             sel = np.nonzero(owner % world == r)[0]
+            sel = sel[o.region_order(k[sel])]
             exp_keys.append(k[sel]), exp_idx.append(sel), exp_src.append(np.full(len(sel), s))
         ek = np.concatenate(exp_keys)
         np.testing.assert_array_equal(res[r]["recv_keys"], ek)
@@ -200,8 +210,9 @@ def test_route_multi_pipelined_batches(gd):
             perm = torch.as_tensor(_Cai(rp.perm, m), device="cuda").cpu().numpy().view(np.uint32)
             offs = torch.as_tensor(_Cai(rp.offsets, G + 2), device="cuda").cpu().numpy().view(np.uint32)
             st, silo, want_act, _, _ = o.route_batch_np(batches[j], spec, d, my_silo=1)
-            np.testing.assert_array_equal(act, want_act)
-            wp, wo = o.bucket_stable(want_act, G)
+            ro = o.region_order(batches[j])
+            np.testing.assert_array_equal(act, want_act[ro])
+            wp, wo = o.bucket_stable(want_act[ro], G)
             np.testing.assert_array_equal(perm, wp)
             np.testing.assert_array_equal(offs, wo)
             if j % 2 == 1:
@@ -252,11 +263,12 @@ def test_route_multi_ext_world1(gd, n):
     bexts = [gd.GD_KEYEXT_HOST if (isinstance(x, str) and x == kx.EXT_HOST) else x for x in exts]
     r = e.route_multi_ext(keys, bexts, G + 200, return_routes=True)
     st, silo, act, _, _ = kx.route_batch_ext(keys, exts, spec, o.DirectoryArrays(reg, np.arange(G), own), d, my_silo=4)
-    np.testing.assert_array_equal(r["recv_keys"], keys)
-    np.testing.assert_array_equal(r["status"], st)
-    np.testing.assert_array_equal(r["silo"], silo)
-    np.testing.assert_array_equal(r["act"], act)
-    wp, wo = o.bucket_stable(act, G + 200)
+    ro = o.region_order(keys)              # KeyExt grains: region 0
+    np.testing.assert_array_equal(r["recv_keys"], keys[ro])
+    np.testing.assert_array_equal(r["status"], st[ro])
+    np.testing.assert_array_equal(r["silo"], silo[ro])
+    np.testing.assert_array_equal(r["act"], act[ro])
+    wp, wo = o.bucket_stable(act[ro], G + 200)
     np.testing.assert_array_equal(r["perm"], wp)
     np.testing.assert_array_equal(r["offsets"], wo)
     np.testing.assert_array_equal(r["ret_act"], act)
@@ -321,15 +333,16 @@ def test_route_multi_forward_world1(gd, n):
     e.register(reg, np.arange(G), act_silo)
     e.comm_init(gd.GrainDispatch.comm_unique_id(), 1, 0)
     st, silo, act, _, _ = o.route_batch_np(keys, spec, o.DirectoryArrays(reg, np.arange(G), act_silo), my_silo=4)
-    wp, wo = o.bucket_stable(act, G)
+    ro = o.region_order(keys)
+    wp, wo = o.bucket_stable(act[ro], G)
     for ret in (False, True):
         r = e.route_multi(keys, G, return_routes=ret, forward=True)
-        np.testing.assert_array_equal(r["recv_keys"], keys)
-        np.testing.assert_array_equal(r["recv_idx"], np.arange(n, dtype=np.uint32))
+        np.testing.assert_array_equal(r["recv_keys"], keys[ro])
+        np.testing.assert_array_equal(r["recv_idx"], ro.astype(np.uint32))
         np.testing.assert_array_equal(r["recv_src"], np.zeros(n, np.uint32))
-        np.testing.assert_array_equal(r["status"], st)
-        np.testing.assert_array_equal(r["silo"], silo)
-        np.testing.assert_array_equal(r["act"], act)
+        np.testing.assert_array_equal(r["status"], st[ro])
+        np.testing.assert_array_equal(r["silo"], silo[ro])
+        np.testing.assert_array_equal(r["act"], act[ro])
         np.testing.assert_array_equal(r["perm"], wp)
         np.testing.assert_array_equal(r["offsets"], wo)
         if ret:
@@ -475,22 +488,28 @@ def _local_world(gd, W, spec_mode, silos, reg, act, silo_of, my_silos=None):
     return spec, own, es
 
 
-def _expected_owner_side(batches, spec, full, W, r):
-    """Messages rank r owns, in arrival order (sender rank, sender order), and their routes."""
+def _expected_owner_side(batches, spec, full, W, r, by_region=True):
+    """Messages rank r owns, in arrival order (sender rank, table region, sender order), and their
+    routes.  by_region=False: (sender rank, sender order), the order without header compaction."""
     ks, ids, srcs = [], [], []
     for s, k in enumerate(batches):
         _, _, _, owner, _ = o.route_batch_np(k, spec, full, my_silo=s)
         sel = np.nonzero(np.where(owner == o.M32, s, owner % W) == r)[0]
+        if by_region:
+            sel = sel[o.region_order(k[sel])]
         ks.append(k[sel]), ids.append(sel), srcs.append(np.full(len(sel), s))
     rk = np.concatenate(ks)
     st, silo, act, _, _ = o.route_batch_np(rk, spec, full, my_silo=r)
     return rk, np.concatenate(ids).astype(np.uint32), np.concatenate(srcs).astype(np.uint32), st, silo, act
 
 
-@pytest.mark.parametrize("W", [2, 3, 5])
-def test_route_multi_local_world(gd, W):
+@pytest.mark.parametrize("W,by_region", [(2, True), (3, True), (5, True), (3, False)])
+def test_route_multi_local_world(gd, W, by_region, monkeypatch):
     """gd_route_multi at W ranks (in-process transport): owner-side arrival order, routes and
-    per-activation buckets, and the routes returned to every sender in batch order."""
+    per-activation buckets, and the routes returned to every sender in batch order.  by_region:
+    GD_REGION_PROBE (senders group each chunk by table region, the owner probes region by XCD);
+    without it the arrival order is (sender rank, sender order)."""
+    monkeypatch.setenv("GD_REGION_PROBE", "1" if by_region else "0")
     silos = o.bench_silos(8)
     G = 6000
     reg = o.grain_keys(TC, np.arange(G))
@@ -511,7 +530,7 @@ def test_route_multi_local_world(gd, W):
     res = _run_ranks([lambda r=r: es[r].route_multi(batches[r], n_act[r], return_routes=True) for r in range(W)])
     full = o.DirectoryArrays(reg, act, own)
     for r in range(W):
-        rk, ids, srcs, st, silo, a = _expected_owner_side(batches, spec, full, W, r)
+        rk, ids, srcs, st, silo, a = _expected_owner_side(batches, spec, full, W, r, by_region=by_region)
         np.testing.assert_array_equal(res[r]["recv_keys"], rk)
         np.testing.assert_array_equal(res[r]["recv_idx"], ids)
         np.testing.assert_array_equal(res[r]["recv_src"], srcs)
@@ -596,13 +615,14 @@ def test_route_multi_local_pipelined_and_forward(gd):
         st, silo, a, owner, _ = o.route_batch_np(fb[s], spec, full, my_silo=s)
         orank = np.where(owner == o.M32, s, owner % W)
         final = np.where(st == o.ST_OK, silo % W, orank)
-        for i in range(len(fb[s])):
-            expect[int(final[i])].append((int(orank[i]), s, i))
+        reg_ = o.table_region_np(fb[s])
+        for i in range(len(fb[s])):        # (owner rank, sender, region on the owner, sender order)
+            expect[int(final[i])].append((int(orank[i]), s, int(reg_[i]), i))
     for r in range(W):
         ex = sorted(expect[r])
         np.testing.assert_array_equal(res[r]["recv_src"], np.array([x[1] for x in ex], np.uint32))
-        np.testing.assert_array_equal(res[r]["recv_idx"], np.array([x[2] for x in ex], np.uint32))
-        rk = np.array([fb[x[1]][x[2]] for x in ex], np.uint64).reshape(-1, 3)
+        np.testing.assert_array_equal(res[r]["recv_idx"], np.array([x[3] for x in ex], np.uint32))
+        rk = np.array([fb[x[1]][x[3]] for x in ex], np.uint64).reshape(-1, 3)
         np.testing.assert_array_equal(res[r]["recv_keys"], rk)
         st, silo, a, _, _ = o.route_batch_np(rk, spec, full, my_silo=r)
         np.testing.assert_array_equal(res[r]["status"], st)
@@ -657,6 +677,7 @@ def test_route_multi_ext_local_world(gd):
         for s in range(W):
             _, _, _, owner, _ = kx.route_batch_ext(batches[s], exts[s], spec, full, kxd, my_silo=s)
             sel = np.nonzero(np.where(owner == o.M32, s, owner % W) == r)[0]
+            sel = sel[o.region_order(batches[s][sel])]
             ks.append(batches[s][sel]), ids.append(sel), srcs.append(np.full(len(sel), s))
             xs += [exts[s][i] for i in sel]
         rk = np.concatenate(ks)
@@ -718,7 +739,7 @@ def test_route_multi_local_mixed_headers(gd, compact, narrow, monkeypatch):
         assert ("k_recv_expand" in e.kernel_times()) == (compact == "1")
     full = o.DirectoryArrays(reg, act, own)
     for r in range(W):
-        rk, ids, srcs, st, silo, a = _expected_owner_side(batches, spec, full, W, r)
+        rk, ids, srcs, st, silo, a = _expected_owner_side(batches, spec, full, W, r, by_region=compact == "1")
         np.testing.assert_array_equal(res[r]["recv_keys"], rk)
         np.testing.assert_array_equal(res[r]["recv_idx"], ids)
         np.testing.assert_array_equal(res[r]["recv_src"], srcs)
