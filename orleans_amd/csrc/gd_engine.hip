@@ -133,10 +133,10 @@ struct gd_handle {
     hipEvent_t x_in = nullptr, x_hdr[2] = {}, x_route[2] = {}, x_ret[2] = {}, x_done[2] = {};
     hipEvent_t p_packed = nullptr, x_sent[2] = {}, x_fwd[2] = {}, x_keys[2] = {};
     bool x_done_rec[2] = {false, false}, x_sent_rec[2] = {false, false};
-    DevBuf mx_send[2][6];             // per batch parity: send keys, send idx, counts (send/recv messages,
+    DevBuf mx_send[2][7];             // per batch parity: send keys, send idx, counts (send/recv messages,
                                       // send/recv KeyExt bytes: 4 x [W]), KeyExt lengths, KeyExt byte
-                                      // offsets, KeyExt blob
-    DevBuf mx[2][20];                 // per batch parity: receive / result buffers
+                                      // offsets, KeyExt blob, block starts of 2-B origin indices
+    DevBuf mx[2][22];                 // per batch parity: receive / result buffers
     DevBuf mf[2][16];                 // per batch parity, GD_MULTI_FORWARD: forward send (keys, pos, idx,
                                       // src, silo, act, status, counts), forward receive (keys, idx, src,
                                       // silo, act, status), perm, offsets
@@ -174,6 +174,8 @@ struct gd_handle {
     bool hist_xcd = true;       // multi-tile histograms in reverse XCD tile order (GD_HIST_XCD)
     bool compact_headers = true;    // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
     bool region_probe = false;      // gd_route_multi: chunks ordered by table region, region-mapped probe (GD_REGION_PROBE)
+    bool idx16 = true;              // gd_route_multi: 2-B origin indices on the wire (KD_IDX16, GD_IDX16)
+    bool pack_pay16 = false;        // set by route_multi around its partition: the scatter writes u16 payloads
     bool narrow_headers = true;     // compact headers as u32 N1s when every N1 < 2^32 (GD_NARROW_HEADERS=0: u64)
     bool fused_starts = true;
     bool radix_pack = true;     // 6-B packed records between radix passes when they fit (GD_RADIX_PACK)
@@ -368,32 +370,37 @@ unsigned long long pow2_at_least(unsigned long long x) {
 template <int MODE, int M, bool NT>
 int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
     return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h), k_route_m<MODE, M, NT>, keys,
-                  n, ring_args(h), table_args(h), silo, act, status, 0ull, h->route_xcd ? 1u : 0u);
+                  n, ring_args(h), table_args(h), silo, act, status, 0ull, h->route_xcd ? 1u : 0u,
+                  (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr);
 }
 
 // Keys given as N1 alone (u64, or u32 with n1w = 4) with one TypeCodeData (a compact exchange
 // receive); not in cache mode.
 template <int MODE>
 int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uint32_t n, uint32_t* silo,
-                  uint32_t* act, uint8_t* status) {
+                  uint32_t* act, uint8_t* status, const uint32_t* rcnt, uint32_t world, uint32_t* src) {
     const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
     const uint32_t xcd = h->route_xcd ? 1u : 0u;
     if (n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4>, k, n, ring_args(h), table_args(h),
-                      silo, act, status, tcd, xcd);
+                      silo, act, status, tcd, xcd, rcnt, world, src);
     return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8>, k, n, ring_args(h), table_args(h),
-                  silo, act, status, tcd, xcd);
+                  silo, act, status, tcd, xcd, rcnt, world, src);
 }
 
+// src (optional): also the sender rank of every message, from the per-sender counts rcnt[world].
 int route_n1_device(gd_handle* h, const void* n1s, uint32_t n1w, uint64_t tcd, uint32_t n, uint32_t* silo,
-                    uint32_t* act, uint8_t* status) {
+                    uint32_t* act, uint8_t* status, const uint32_t* rcnt = nullptr, uint32_t world = 0,
+                    uint32_t* src = nullptr) {
     GD_TRY(check_ring(h));
     h->routed += n;
     const gd_key* k = reinterpret_cast<const gd_key*>(n1s);
     switch (h->ring_mode) {
-        case GD_RING_DIRECTORY: return route_n1_mode<GD_RING_DIRECTORY>(h, k, n1w, tcd, n, silo, act, status);
-        case GD_RING_CONSISTENT: return route_n1_mode<GD_RING_CONSISTENT>(h, k, n1w, tcd, n, silo, act, status);
-        default: return route_n1_mode<GD_RING_VIRTUAL_BUCKETS>(h, k, n1w, tcd, n, silo, act, status);
+        case GD_RING_DIRECTORY:
+            return route_n1_mode<GD_RING_DIRECTORY>(h, k, n1w, tcd, n, silo, act, status, rcnt, world, src);
+        case GD_RING_CONSISTENT:
+            return route_n1_mode<GD_RING_CONSISTENT>(h, k, n1w, tcd, n, silo, act, status, rcnt, world, src);
+        default: return route_n1_mode<GD_RING_VIRTUAL_BUCKETS>(h, k, n1w, tcd, n, silo, act, status, rcnt, world, src);
     }
 }
 
@@ -816,6 +823,20 @@ int shard_scatter_t(gd_handle* h, const void* recs, const uint32_t* payload, con
     // keys with a compaction descriptor: the compact case by k_shard_gather, the other by the staged
     // kernel (each returns at once in the other's case)
     if constexpr (!NODES)
+        if (h->pack_pay16) {         // route_multi's 2-B origin indices (KD_IDX16); keys with a descriptor
+            uint16_t* op = reinterpret_cast<uint16_t*>(out_pay);
+            if (h->shard_gather)
+                GD_TRY(launch(h, "k_shard_scatter", dim3(tiles), dim3(SH_NT), 0, k_shard_gather<BITS, uint16_t>,
+                              (const gd_key*)recs, payload, dest, n, n_shards, tiles, gscan, out, op, kdesc,
+                              h->shard_n1_copy ? (const uint32_t*)h->shard_n1.p : nullptr));
+            if (h->shard_gather)
+                return launch(h, "k_shard_scatter", dim3(tiles), dim3(SH_NT), 0,
+                              k_shard_scatter<BITS, false, true, uint16_t>, recs, payload, dest, n, n_shards, tiles,
+                              gscan, out, op, kdesc);
+            return launch(h, "k_shard_scatter", dim3(tiles), dim3(SH_NT), 0, k_shard_scatter<BITS, false, false, uint16_t>,
+                          recs, payload, dest, n, n_shards, tiles, gscan, out, op, kdesc);
+        }
+    if constexpr (!NODES)
         if (h->shard_gather && kdesc) {
             GD_TRY(launch(h, "k_shard_scatter", dim3(tiles), dim3(SH_NT), 0, k_shard_gather<BITS>,
                           (const gd_key*)recs, payload, dest, n, n_shards, tiles, gscan, out, out_pay, kdesc,
@@ -1039,6 +1060,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_FAN_ILP")) h->fan_ilp = std::atoi(v);
     if (const char* v = std::getenv("GD_BUCKET2")) h->bucket2 = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_REGION_PROBE")) h->region_probe = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_IDX16")) h->idx16 = std::atoi(v) != 0;
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));
@@ -2926,6 +2948,7 @@ struct Lane {
     size_t per;             // elements of `type` per element
     const uint64_t* sb = nullptr;   // set: per-peer byte ranges [sb[r], sb[r+1]) sent to r and
     const uint64_t* rb = nullptr;   // [rb[r], rb[r+1]) received from r (compact headers)
+    const uint64_t* rsz = nullptr;  // set (with rb): bytes received from r at rb[r] (padded layouts)
 };
 
 int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uint64_t* soff, const uint32_t* rc,
@@ -2942,18 +2965,19 @@ int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uin
         for (int l = 0; l < n_lanes; ++l) {
             const Lane& L = lanes[l];
             if (sc[r]) {
-                if (L.sb)
-                    NCCL_TRY(h, R.Send((const uint8_t*)L.send + L.sb[r], (size_t)(L.sb[r + 1] - L.sb[r]), ncclUint8, r,
-                                       h->comm, h->stream));
-                else
+                if (L.sb) {                // byte ranges: an empty one is no send (the peer expects none)
+                    if (L.sb[r + 1] > L.sb[r])
+                        NCCL_TRY(h, R.Send((const uint8_t*)L.send + L.sb[r], (size_t)(L.sb[r + 1] - L.sb[r]),
+                                           ncclUint8, r, h->comm, h->stream));
+                } else
                     NCCL_TRY(h, R.Send((const uint8_t*)L.send + soff[r] * L.elem, (size_t)sc[r] * L.per, L.type, r,
                                        h->comm, h->stream));
             }
             if (rc[r]) {
-                if (L.rb)
-                    NCCL_TRY(h, R.Recv((uint8_t*)L.recv + L.rb[r], (size_t)(L.rb[r + 1] - L.rb[r]), ncclUint8, r,
-                                       h->comm, h->stream));
-                else
+                if (L.rb) {
+                    const uint64_t nb = L.rsz ? L.rsz[r] : L.rb[r + 1] - L.rb[r];
+                    if (nb) NCCL_TRY(h, R.Recv((uint8_t*)L.recv + L.rb[r], (size_t)nb, ncclUint8, r, h->comm, h->stream));
+                } else
                     NCCL_TRY(h, R.Recv((uint8_t*)L.recv + roff[r] * L.elem, (size_t)rc[r] * L.per, L.type, r,
                                        h->comm, h->stream));
             }
@@ -3067,7 +3091,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     //    buffers once batch i-2's rounds have read them; it runs beside batch i-1's header round
     GD_TRY(grow(h, SB[0], (size_t)n * sizeof(gd_key) + 8));
     GD_TRY(grow(h, SB[1], (size_t)n * 4 + 4));
-    GD_TRY(grow(h, SB[2], ((size_t)W * 8 + 4) * 4));
+    GD_TRY(grow(h, SB[2], ((size_t)W * 9 + 6) * 4));
     if (has_ext) {
         GD_TRY(grow(h, SB[3], (size_t)n * 4 + 4));
         GD_TRY(grow(h, SB[4], (size_t)n * 4 + 4));
@@ -3080,19 +3104,35 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     gd_key* send_keys = (gd_key*)SB[0].p;
     uint32_t* send_idx = (uint32_t*)SB[1].p;
     // send msgs [0,W), recv msgs [W,2W), send bytes, recv bytes, my key descriptor [4W,4W+4) (k_key_desc),
-    // the peers' descriptors [4W+4, 8W+4)
+    // the peers' descriptors [4W+4, 8W+4), my 2-B index block count [8W+4], the peers' [8W+5, 9W+5)
     uint32_t* dcnt = (uint32_t*)SB[2].p;
     uint32_t* kdesc = dcnt + 4 * W;
     int32_t* send_len = (int32_t*)SB[3].p;
     uint32_t* send_boff = (uint32_t*)SB[4].p;
     uint32_t regions = 1;
+    // region order needs the descriptor: its flag tells the owners (k_shard_counts)
+    regions = h->region_probe && h->compact_headers && !h->cache_max && W * N_REGIONS <= 256 ? N_REGIONS : 1u;
+    // 2-B origin indices (KD_IDX16): the senders' own 4-B copy is needed for returned routes and
+    // KeyExt lengths; region order breaks the increasing order within a rank's chunk
+    // (W > 1 only: at world 1 nothing crosses a link and the rebuild costs more HBM than it saves)
+    const bool idx16 = h->idx16 && W > 1 && !ret && !has_ext && regions == 1 && n > 0;
+    const uint32_t nblk = idx16 ? (uint32_t)(((uint64_t)n + 65535u) >> 16) : 0u;
+    if (idx16) GD_TRY(grow(h, SB[6], (size_t)W * nblk * 4 + 16));
+    uint32_t* nb_mine = dcnt + 8 * W + 4;
     {
         OnPStream on(h);
-        // region order needs the descriptor: its flag tells the owners (k_shard_counts)
-        regions = h->region_probe && h->compact_headers && !h->cache_max && W * N_REGIONS <= 256 ? N_REGIONS : 1u;
-        GD_TRY(shard_pack<false>(h, d_keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt, x,
-                                 h->compact_headers ? kdesc : nullptr, regions));
+        h->pack_pay16 = idx16;
+        const int prc = shard_pack<false>(h, d_keys, nullptr, n, 0, (uint32_t)W, send_keys, send_idx, dcnt, x,
+                                          h->compact_headers ? kdesc : nullptr, regions);
+        h->pack_pay16 = false;
+        GD_TRY(prc);
         if (!h->compact_headers) HIP_TRY(h, hipMemsetAsync(kdesc, 0, 16, h->stream));
+        if (idx16)                     // block starts per rank from the partition's scan; descriptor flag
+            GD_TRY(launch(h, "k_block_prefix", dim3(blocks_for((uint64_t)W * nblk, BLOCK)), dim3(BLOCK), 0,
+                          k_block_prefix, (const uint32_t*)h->shard_hist.p, blocks_for(n, SH_TILE), (uint32_t)W, nblk,
+                          (uint32_t*)SB[6].p, kdesc, nb_mine));
+        else
+            HIP_TRY(h, hipMemsetAsync(nb_mine, 0, 4, h->stream));
         if (has_ext) {                 // KeyExt bytes per destination; lengths and byte offsets in send order
             HIP_TRY(h, hipMemsetAsync(dcnt + 2 * W, 0, (size_t)W * 4, h->stream));
             GD_TRY(launch(h, "k_dest_bytes", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_dest_bytes,
@@ -3113,13 +3153,15 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
             NCCL_TRY(h, R.Recv(dcnt + W + r, 1, ncclUint32, r, h->comm, h->stream));
             NCCL_TRY(h, R.Send(kdesc, 4, ncclUint32, r, h->comm, h->stream));
             NCCL_TRY(h, R.Recv(kdesc + 4 + 4 * r, 4, ncclUint32, r, h->comm, h->stream));
+            NCCL_TRY(h, R.Send(nb_mine, 1, ncclUint32, r, h->comm, h->stream));
+            NCCL_TRY(h, R.Recv(nb_mine + 1 + r, 1, ncclUint32, r, h->comm, h->stream));
             if (has_ext) {
                 NCCL_TRY(h, R.Send(dcnt + 2 * W + r, 1, ncclUint32, r, h->comm, h->stream));
                 NCCL_TRY(h, R.Recv(dcnt + 3 * W + r, 1, ncclUint32, r, h->comm, h->stream));
             }
         }
         NCCL_TRY(h, R.GroupEnd());
-        HIP_TRY(h, hipMemcpyAsync(h->h_xcnt, dcnt, ((size_t)W * 8 + 4) * 4, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipMemcpyAsync(h->h_xcnt, dcnt, ((size_t)W * 9 + 6) * 4, hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(h, hipStreamSynchronize(h->stream));
     }
     ncclResult_t async_err = ncclSuccess;
@@ -3171,15 +3213,33 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
             n1_first = false;
         }
     }
+    // origin indices: 2 B a message from KD_IDX16 senders (+ their block starts), else 4 B.  With any
+    // 2-B peer every chunk lands in a staging buffer at 4-B aligned offsets and k_recv_idx16 rebuilds
+    // them; otherwise the 4-B chunks land in recv_idx directly.
+    bool any16 = false;
+    std::vector<uint64_t> isb(W + 1, 0), irb(W + 1, 0), irs(W, 0), psb(W + 1, 0), prb(W + 1, 0), prs(W, 0);
+    const uint32_t* rnb = h->h_xcnt + 8 * W + 5;
+    for (int r = 0; r < W; ++r) {
+        const bool w16 = rc[r] && (hd[4 + 4 * r + 1] & KD_IDX16);
+        any16 |= w16;
+        isb[r + 1] = isb[r] + (uint64_t)sc[r] * (idx16 ? 2 : 4);
+        irs[r] = (uint64_t)rc[r] * (w16 ? 2 : 4);
+        irb[r + 1] = irb[r] + ((irs[r] + 3) & ~3ull);
+        psb[r + 1] = psb[r] + (idx16 && sc[r] ? (uint64_t)nblk * 4 : 0);
+        prs[r] = w16 ? (uint64_t)rnb[r] * 4 : 0;
+        prb[r + 1] = prb[r] + prs[r];
+    }
+    // the probe of compact N1s writes the sender ranks itself (no k_recv_src pass over the batch)
+    const bool src_in_probe = n1_path && !any16 && !by_region;
     // 2. this parity's buffers: batch i-2 must be done with them (probe/bucket and routes round)
     const size_t m4 = (size_t)m * 4 + 4, n4 = (size_t)n * 4 + 4;
-    const size_t want[20] = {(size_t)m * sizeof(gd_key) + 8, m4, m4, m4, m4, (size_t)m + 4, m4,
+    const size_t want[22] = {(size_t)m * sizeof(gd_key) + 8, m4, m4, m4, m4, (size_t)m + 4, m4,
                              ((size_t)n_act + 2) * 4, n4, n4, (size_t)n + 4, n4, n4, (size_t)n + 4,
                              m4, (size_t)rboff[W] + 16, m4, (size_t)m * 8 + 8, (size_t)hrb[W] + 16,
-                             (size_t)W * (N_REGIONS + 1) * 4};
-    for (int b = 0; b < 20; ++b)
+                             (size_t)W * (N_REGIONS + 1) * 4, (size_t)irb[W] + 16, (size_t)prb[W] + 16};
+    for (int b = 0; b < 22; ++b)
         if (want[b] && (b < 8 || (ret && b < 14) || (has_ext && b >= 14 && b < 18) || (any_compact && b == 18) ||
-                        (by_region && b == 19)))
+                        (by_region && b == 19) || (any16 && b >= 20)))
             GD_TRY(grow(h, B[b], want[b]));
     if (has_ext) GD_TRY(grow(h, SB[5], (size_t)sboff[W] + 16));
     gd_key* recv_keys = (gd_key*)B[0].p;
@@ -3198,12 +3258,15 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
                           (const uint32_t*)send_idx, n, x, (const uint32_t*)send_boff, (uint8_t*)SB[5].p));
         // keys: byte ranges per peer (compact chunks are 8 B a header); with any compact peer they
         // land in a staging buffer that k_recv_expand turns back into 24-B keys
-        const Lane lanes[3] = {{send_keys, any_compact ? B[18].p : (void*)recv_keys, 1, ncclUint8, 1, hsb.data(),
-                                hrb.data()},
-                               {send_idx, recv_idx, 4, ncclUint32, 1},
-                               {send_len, B[14].p, 4, ncclInt32, 1}};
-        GD_TRY(exchange_round(h, "rccl_headers", sc.data(), soff.data(), rc.data(), roff.data(), lanes,
-                              has_ext ? 3 : 2));
+        // keys, origin indices, KeyExt lengths, the block starts of 2-B origin indices
+        Lane lanes[4];
+        int nl = 0;
+        lanes[nl++] = {send_keys, any_compact ? B[18].p : (void*)recv_keys, 1, ncclUint8, 1, hsb.data(), hrb.data()};
+        lanes[nl++] = {send_idx, any16 ? B[20].p : (void*)recv_idx, 4, ncclUint32, 1, idx16 ? isb.data() : nullptr,
+                       any16 ? irb.data() : nullptr, any16 ? irs.data() : nullptr};
+        if (has_ext) lanes[nl++] = {send_len, B[14].p, 4, ncclInt32, 1};
+        if (idx16 || any16) lanes[nl++] = {SB[6].p, B[21].p, 4, ncclUint32, 1, psb.data(), prb.data(), prs.data()};
+        GD_TRY(exchange_round(h, "rccl_headers", sc.data(), soff.data(), rc.data(), roff.data(), lanes, nl));
         if (has_ext) {                 // the KeyExt strings, then their offsets in the receive blob
             const Lane bl[1] = {{SB[5].p, B[15].p, 1, ncclUint8, 1}};
             GD_TRY(exchange_round(h, "rccl_keyext", sbc.data(), sboff.data(), rbc.data(), rboff.data(), bl, 1));
@@ -3217,9 +3280,14 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
             GD_TRY(launch(h, "k_recv_expand", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_expand,
                           (const uint8_t*)B[18].p, (const uint32_t*)(dcnt + W), (const uint32_t*)(kdesc + 4),
                           (uint32_t)W, m, recv_keys, recv_src));
-        else
+        else if (!any16 && !src_in_probe)
             GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
                           (const uint32_t*)(dcnt + W), (uint32_t)W, m, recv_src));
+        if (any16)                     // 4-B origin indices and sender ranks from the 2-B form
+            GD_TRY(launch(h, "k_recv_idx16", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_idx16,
+                          (const uint8_t*)B[20].p, (const uint32_t*)(dcnt + W), (const uint32_t*)(kdesc + 4),
+                          (const uint32_t*)B[21].p, (const uint32_t*)(nb_mine + 1), (uint32_t)W, m, recv_idx,
+                          recv_src));
         if (by_region) {               // where each sender's region runs start (binary search per chunk)
             const uint32_t nt = (uint32_t)W * (N_REGIONS + 1);
             const uint32_t* rcnt = dcnt + W;
@@ -3239,7 +3307,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         if (n1_path && keep_keys) {    // the 24-B keys for the result, beside the probe
             GD_TRY(launch(h, "k_recv_expand", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_expand,
                           (const uint8_t*)B[18].p, (const uint32_t*)(dcnt + W), (const uint32_t*)(kdesc + 4),
-                          (uint32_t)W, m, recv_keys, recv_src));
+                          (uint32_t)W, m, recv_keys, src_in_probe ? nullptr : recv_src));
             HIP_TRY(h, hipEventRecord(h->x_keys[s], h->xstream));
         }
         if (!ret) {                    // this parity's send buffers are free for batch i+2's partition
@@ -3252,7 +3320,10 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     if (by_region)
         GD_TRY(route_region_device(h, n1_path ? B[18].p : (const void*)recv_keys, n1_path ? header_bytes(n1_mode) : 0u,
                                    n1_tcd, m, (const uint32_t*)B[19].p, (uint32_t)W, silo, act, st));
-    else if (n1_path) GD_TRY(route_n1_device(h, B[18].p, header_bytes(n1_mode), n1_tcd, m, silo, act, st));
+    else if (n1_path)
+        GD_TRY(route_n1_device(h, B[18].p, header_bytes(n1_mode), n1_tcd, m, silo, act, st,
+                               src_in_probe ? (const uint32_t*)(dcnt + W) : nullptr, (uint32_t)W,
+                               src_in_probe ? recv_src : nullptr));
     else if (m) GD_TRY(route_device(h, recv_keys, m, silo, act, st));
     if (m && has_ext)                  // the received strings: KeyExt grains are routed on their owner
         GD_TRY(keyext_pass(h, recv_keys,

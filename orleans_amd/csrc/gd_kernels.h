@@ -415,21 +415,48 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb, uint32_t x
     return x * q + min(x, rem) + k;
 }
 
+// src_out (optional, the exchange's receive side): message i's sender rank, from the per-sender
+// receive counts rcnt[world] (k_recv_src's job, done here beside the probe's own writes).
 template <int MODE, int M, bool NT, int N1W = 0>
 __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                    TableArgs tab, uint32_t* __restrict__ out_silo,
                                                    uint32_t* __restrict__ out_act,
-                                                   uint8_t* __restrict__ out_status, uint64_t tcd_u, uint32_t xcd) {
+                                                   uint8_t* __restrict__ out_status, uint64_t tcd_u, uint32_t xcd,
+                                                   const uint32_t* __restrict__ rcnt = nullptr, uint32_t world = 0,
+                                                   uint32_t* __restrict__ src_out = nullptr) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
+    __shared__ uint32_t s_soff[257];
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
-    stage_ring(ring, s_pts, s_own);
+    if (src_out && threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t q = 0; q < world; ++q) {
+            s_soff[q] = run;
+            run += rcnt[q];
+        }
+        s_soff[world] = run;
+    }
+    stage_ring(ring, s_pts, s_own);                    // its barrier publishes s_soff too
     // xcd: each XCD routes a contiguous message range (xcd_tile), so the act it writes is the act the
     // same XCD's histogram and scatter workgroups read next (their XCD tile ranges match)
     const uint32_t blk = xcd_tile(blockIdx.x, gridDim.x, xcd);
     route_m_core<MODE, M, BLOCK, NT, N1W, true>(keys, n, blk * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own,
                                                tab, tab.ctr->max_probe, out_silo, out_act, out_status, tcd_u, nullptr,
                                                0);
+    if (src_out) {
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const uint32_t i = blk * (BLOCK * M) + j * BLOCK + threadIdx.x;
+            if (i >= n) continue;
+            uint32_t lo = 0, hi = world;               // largest q with s_soff[q] <= i
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_soff[mid] <= i) lo = mid;
+                else hi = mid;
+            }
+            st<true>(src_out + i, lo);
+        }
+    }
 }
 
 // The owner's probe over received chunks grouped by region (gd_route_multi with regions, SURVEY 8 e):

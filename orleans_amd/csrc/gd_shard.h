@@ -167,6 +167,88 @@ __global__ void k_key_desc(const gd_key* __restrict__ keys, uint32_t n, uint32_t
 
 // Descriptor flag (kdesc[1]): every chunk of the sender is ordered by region (k_shard_hist with regions).
 constexpr uint32_t KD_REGIONS = 4u;
+// Descriptor flag: the sender's origin indices travel as their low 16 bits (2 B a message), with,
+// per receiving rank, the chunk position where each 65,536-index block of the sender's batch starts
+// (k_block_prefix); k_recv_idx16 rebuilds them.  Origin indices increase along a chunk (the
+// partition is stable), so block b's messages are a contiguous run of it.
+constexpr uint32_t KD_IDX16 = 8u;
+constexpr uint32_t IDX16_BLOCK_TILES = 65536u / SH_TILE;
+
+// Sender, after the partition's scan (gscan: exclusive over (dest, tile), rank-major): for rank r
+// and block b (tiles 32b .. 32b + 31), the position in r's chunk where block b starts.  Thread 0
+// also flags the descriptor and stores this sender's block count (the counts round sends it).
+__global__ void k_block_prefix(const uint32_t* __restrict__ gscan, uint32_t tiles, uint32_t n_shards,
+                               uint32_t nblk, uint32_t* __restrict__ out, uint32_t* __restrict__ kdesc,
+                               uint32_t* __restrict__ nblk_out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t == 0) {
+        kdesc[1] |= KD_IDX16;
+        *nblk_out = nblk;
+    }
+    if (t >= n_shards * nblk) return;
+    const uint32_t r = t / nblk, b = t % nblk;
+    out[t] = gscan[(size_t)r * tiles + (size_t)b * IDX16_BLOCK_TILES] - gscan[(size_t)r * tiles];
+}
+
+// Receiver of a header round with 2-B origin indices from some peers: raw = the peers' index chunks
+// back to back (2 or 4 B a message by the sender's descriptor, each chunk padded to 4 B), pcol =
+// the 2-B senders' block starts back to back (rnblk[q] each).  Writes the 4-B origin index and the
+// sender rank of every received message (k_recv_src's job).
+__global__ void __launch_bounds__(BLOCK) k_recv_idx16(const uint8_t* __restrict__ raw,
+                                                      const uint32_t* __restrict__ rcount,
+                                                      const uint32_t* __restrict__ rdesc,
+                                                      const uint32_t* __restrict__ pcol,
+                                                      const uint32_t* __restrict__ rnblk, uint32_t world, uint32_t m,
+                                                      uint32_t* __restrict__ idx, uint32_t* __restrict__ src) {
+    constexpr uint32_t LDS_COL = 4096;   // block starts staged in LDS when they fit (16M-message batches at W <= 16)
+    __shared__ uint32_t s_off[257], s_boff[256], s_coff[256], s_nb[256], s_col[LDS_COL];
+    __shared__ uint32_t s_ncol;
+    if (threadIdx.x == 0) {
+        uint32_t run = 0, brun = 0, crun = 0;
+        for (uint32_t q = 0; q < world; ++q) {
+            const bool w16 = (rdesc[4 * q + 1] & KD_IDX16) != 0;
+            s_off[q] = run;
+            s_boff[q] = brun;
+            s_coff[q] = crun;
+            s_nb[q] = w16 ? rnblk[q] : 0u;
+            run += rcount[q];
+            brun += w16 ? (2u * rcount[q] + 3u) & ~3u : 4u * rcount[q];
+            crun += w16 ? rnblk[q] : 0u;
+        }
+        s_off[world] = run;
+        s_ncol = crun;
+    }
+    __syncthreads();
+    const bool in_lds = s_ncol <= LDS_COL;
+    if (in_lds)
+        for (uint32_t k = threadIdx.x; k < s_ncol; k += BLOCK) s_col[k] = pcol[k];
+    __syncthreads();
+    const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
+    if (j >= m) return;
+    uint32_t lo = 0, hi = world;          // largest q with s_off[q] <= j
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_off[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t q = lo, jj = j - s_off[q], nb = s_nb[q];
+    uint32_t v;
+    if (nb) {
+        const uint32_t low = reinterpret_cast<const uint16_t*>(raw + s_boff[q])[jj];
+        const uint32_t* col = (in_lds ? s_col : pcol) + s_coff[q];
+        uint32_t b = 0, e = nb;           // largest b with col[b] <= jj (col[0] = 0)
+        while (e - b > 1) {
+            const uint32_t mid = (b + e) >> 1;
+            if (col[mid] <= jj) b = mid;
+            else e = mid;
+        }
+        v = (b << 16) | low;
+    } else {
+        v = reinterpret_cast<const uint32_t*>(raw + s_boff[q])[jj];
+    }
+    idx[j] = v;
+    src[j] = q;
+}
 
 // Header bytes of a chunk by its sender's descriptor mode.
 __host__ __device__ __forceinline__ uint32_t header_bytes(uint32_t mode) { return mode == 2 ? 4u : mode ? 8u : 24u; }
@@ -221,7 +303,7 @@ __global__ void __launch_bounds__(BLOCK) k_recv_expand(const uint8_t* __restrict
         out[1] = u64_at(6 * j + 2);
         out[2] = u64_at(6 * j + 4);
     }
-    src[i] = lo;
+    if (src) src[i] = lo;
 }
 
 // Forward partition (SURVEY 8 e, the owner != activation silo case): after the probe on the owner,
@@ -288,15 +370,16 @@ __global__ void __launch_bounds__(BLOCK) k_fwd_gather(const uint32_t* __restrict
     st[j] = st_in[i];
 }
 
-// payload_in == nullptr: the payload is the record's batch index (the origin index).
-template <int BITS, bool NODES, bool SKIP_COMPACT = false>
+// payload_in == nullptr: the payload is the record's batch index (the origin index).  PT = uint16_t:
+// the payload is written as its low 16 bits (origin indices for the exchange, KD_IDX16).
+template <int BITS, bool NODES, bool SKIP_COMPACT = false, typename PT = uint32_t>
 __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict__ recs,
                                                          const uint32_t* __restrict__ payload_in,
                                                          const uint8_t* __restrict__ dest, uint32_t n,
                                                          uint32_t n_shards, uint32_t tiles,
                                                          const uint32_t* __restrict__ gscan,
                                                          void* __restrict__ out_recs,
-                                                         uint32_t* __restrict__ out_payload,
+                                                         PT* __restrict__ out_payload,
                                                          const uint32_t* __restrict__ kdesc) {
     constexpr uint32_t R = 1u << BITS;
     constexpr int NW = SH_NT / WAVE;
@@ -423,7 +506,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict_
                     o[1] = s_key[1][p];
                     o[2] = s_key[2][p];
                 }
-                out_payload[g] = s_pay[p];
+                out_payload[g] = (PT)s_pay[p];
             }
         }
     }
@@ -437,14 +520,14 @@ __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict_
 // batch that is not compact (k_shard_scatter<.., SKIP_COMPACT> runs beside it and takes that
 // case; gathering whole 24-B records measured slower than staging them: 0.18-0.24 vs 0.16 ms per
 // 16M keys at 1-8 destinations).  Same output as k_shard_scatter<BITS, false>.
-template <int BITS>
+template <int BITS, typename PT = uint32_t>
 __global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict__ recs,
                                                         const uint32_t* __restrict__ payload_in,
                                                         const uint8_t* __restrict__ dest, uint32_t n,
                                                         uint32_t n_shards, uint32_t tiles,
                                                         const uint32_t* __restrict__ gscan,
                                                         void* __restrict__ out_recs,
-                                                        uint32_t* __restrict__ out_payload,
+                                                        PT* __restrict__ out_payload,
                                                         const uint32_t* __restrict__ kdesc,
                                                         const uint32_t* __restrict__ n1lo) {
     constexpr uint32_t R = 1u << BITS;
@@ -551,7 +634,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict
         if (gg[j] < n) {            // ~0: no record here; else always in bounds when the scan is right
             if (narrow) o32[gg[j]] = (uint32_t)kv[j];
             else o64[gg[j]] = kv[j];
-            out_payload[gg[j]] = pay[j];
+            out_payload[gg[j]] = (PT)pay[j];
         }
 }
 

@@ -550,10 +550,13 @@ def test_route_multi_local_world(gd, W, by_region, monkeypatch):
         e.close()
 
 
-def test_route_multi_local_pipelined_and_forward(gd):
+@pytest.mark.parametrize("by_region", [True, False])
+def test_route_multi_local_pipelined_and_forward(gd, by_region, monkeypatch):
     """W = 4: five pipelined device batches per rank (GD_MULTI_KEYS_READY, results checked one
-    call later), then the forward hop with activations away from their owners."""
+    call later), then the forward hop with activations away from their owners.  Without the region
+    order the batches travel with 2-B origin indices (KD_IDX16), which the forward hop carries on."""
     import torch
+    monkeypatch.setenv("GD_REGION_PROBE", "1" if by_region else "0")
     W, G = 4, 5000
     silos = o.bench_silos(8)
     reg = o.grain_keys(TC, np.arange(G))
@@ -599,7 +602,8 @@ def test_route_multi_local_pipelined_and_forward(gd):
     res = _run_ranks([lambda r=r: pipelined(r) for r in range(W)])
     for i in range(5):
         for r in range(W):
-            rk, ids, srcs, st, silo, a = _expected_owner_side([batches[s][i] for s in range(W)], spec, full, W, r)
+            rk, ids, srcs, st, silo, a = _expected_owner_side([batches[s][i] for s in range(W)], spec, full, W, r,
+                                                              by_region=by_region)
             np.testing.assert_array_equal(res[r][i]["recv_keys"], rk, err_msg=f"batch {i} rank {r}")
             np.testing.assert_array_equal(res[r][i]["recv_idx"], ids)
             np.testing.assert_array_equal(res[r][i]["act"], a)
@@ -615,7 +619,7 @@ def test_route_multi_local_pipelined_and_forward(gd):
         st, silo, a, owner, _ = o.route_batch_np(fb[s], spec, full, my_silo=s)
         orank = np.where(owner == o.M32, s, owner % W)
         final = np.where(st == o.ST_OK, silo % W, orank)
-        reg_ = o.table_region_np(fb[s])
+        reg_ = o.table_region_np(fb[s]) if by_region else np.zeros(len(fb[s]), np.uint32)
         for i in range(len(fb[s])):        # (owner rank, sender, region on the owner, sender order)
             expect[int(final[i])].append((int(orank[i]), s, int(reg_[i]), i))
     for r in range(W):
@@ -757,11 +761,13 @@ def test_route_multi_local_mixed_headers(gd, compact, narrow, monkeypatch):
 
 
 @pytest.mark.parametrize("two_types,big", [(False, False), (True, False), (False, True), (False, "all")])
-def test_route_multi_local_no_keys(gd, two_types, big):
+def test_route_multi_local_no_keys(gd, two_types, big, monkeypatch):
     """GD_MULTI_NO_KEYS at W = 3: with one grain type everywhere the probe reads the compact N1s
     as received (route_n1_device: u32 N1s, or u64 when every sender has a key above 2^32); with two
     types, or u32 and u64 chunks mixed (one sender with big keys), the keys are rebuilt first.
     Results other than recv_keys (left unset) are the same either way."""
+    by_region = not big                               # the big-key cases run with 2-B origin indices
+    monkeypatch.setenv("GD_REGION_PROBE", "1" if by_region else "0")
     W, G = 3, 4000
     silos = o.bench_silos(8)
     tc2 = o.grain_type_code("UnitTests.Grains.SimpleGrain")
@@ -783,7 +789,7 @@ def test_route_multi_local_no_keys(gd, two_types, big):
     res = _run_ranks([lambda r=r: es[r].route_multi(batches[r], n_act[r], no_keys=True) for r in range(W)])
     full = o.DirectoryArrays(reg, act, own)
     for r in range(W):
-        rk, ids, srcs, st, silo, a = _expected_owner_side(batches, spec, full, W, r)
+        rk, ids, srcs, st, silo, a = _expected_owner_side(batches, spec, full, W, r, by_region=by_region)
         assert res[r]["recv_keys"] is None
         np.testing.assert_array_equal(res[r]["recv_idx"], ids)
         np.testing.assert_array_equal(res[r]["recv_src"], srcs)
@@ -797,6 +803,58 @@ def test_route_multi_local_no_keys(gd, two_types, big):
         with pytest.raises(gd.GrainDispatchError):        # the keys were not kept
             buf = np.empty((len(ids), 3), np.uint64)
             es[r]._c(gd.lib.gd_multi_fetch(es[r].h, gd._ptr(buf), *([None] * 10)))
+    for e in es:
+        e.comm_destroy()
+        e.close()
+
+
+@pytest.mark.parametrize("idx16", ["1", "0"])
+def test_route_multi_local_idx16_mixed(gd, idx16, monkeypatch):
+    """2-B origin indices on the wire (KD_IDX16: low 16 bits + per-rank block starts, rebuilt by
+    k_recv_idx16) at W = 3 with senders of both widths in one round: rank 1's handle was created
+    with GD_IDX16=0 (4-B indices), ranks 0 and 2 with the parameter; rank 0's batch spans four
+    65,536-index blocks with a long one-owner stretch (empty blocks for the other owners), rank 2
+    sends nothing.  Owner-side order (sender rank, sender order), routes and buckets against the
+    oracle."""
+    monkeypatch.setenv("GD_REGION_PROBE", "0")
+    W, G = 3, 5000
+    silos = o.bench_silos(8)
+    reg = o.grain_keys(TC, np.arange(G))
+    spec = o.ring_spec(silos, "D")
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    act = np.zeros(G, np.uint32)
+    for r in range(W):
+        act[own % W == r] = np.arange(int((own % W == r).sum()))
+    es = []
+    for r in range(W):
+        monkeypatch.setenv("GD_IDX16", "0" if r == 1 else idx16)
+        e = gd.GrainDispatch(device=0, table_capacity=1 << 13, my_silo=r)
+        e.ring_set_silos("D", [(x.ip, x.port, x.gen) for x in silos])
+        mine = own % W == r
+        e.register(reg[mine], act[mine], own[mine])
+        e.set_kernel_timing(True)
+        es.append(e)
+    gd.GrainDispatch.comm_init_local(es)
+    rng = np.random.default_rng(16)
+    g0 = rng.integers(0, G + 200, size=230_000)
+    by_rank = [np.nonzero(own % W == r)[0] for r in range(W)]
+    g0[70_000:150_000] = rng.choice(by_rank[1], size=80_000)      # one owner only: empty blocks elsewhere
+    batches = [o.grain_keys(TC, g0), o.grain_keys(TC, rng.integers(0, G, size=40_000)), np.zeros((0, 3), np.uint64)]
+    n_act = [int((own % W == r).sum()) for r in range(W)]
+    res = _run_ranks([lambda r=r: es[r].route_multi(batches[r], n_act[r]) for r in range(W)])
+    for e in es:                       # every rank receives from rank 0
+        assert ("k_recv_idx16" in e.kernel_times()) == (idx16 == "1")
+    full = o.DirectoryArrays(reg, act, own)
+    for r in range(W):
+        rk, ids, srcs, st, silo, a = _expected_owner_side(batches, spec, full, W, r, by_region=False)
+        np.testing.assert_array_equal(res[r]["recv_keys"], rk)
+        np.testing.assert_array_equal(res[r]["recv_idx"], ids)
+        np.testing.assert_array_equal(res[r]["recv_src"], srcs)
+        np.testing.assert_array_equal(res[r]["status"], st)
+        np.testing.assert_array_equal(res[r]["act"], a)
+        wp, wo = o.bucket_stable(a, n_act[r])
+        np.testing.assert_array_equal(res[r]["perm"], wp)
+        np.testing.assert_array_equal(res[r]["offsets"], wo)
     for e in es:
         e.comm_destroy()
         e.close()
