@@ -137,9 +137,9 @@ struct gd_handle {
                                       // send/recv KeyExt bytes: 4 x [W]), KeyExt lengths, KeyExt byte
                                       // offsets, KeyExt blob, block starts of 2-B origin indices
     DevBuf mx[2][22];                 // per batch parity: receive / result buffers
-    DevBuf mf[2][16];                 // per batch parity, GD_MULTI_FORWARD: forward send (keys, pos, idx,
+    DevBuf mf[2][17];                 // per batch parity, GD_MULTI_FORWARD: forward send (keys, pos, idx,
                                       // src, silo, act, status, counts), forward receive (keys, idx, src,
-                                      // silo, act, status), perm, offsets
+                                      // silo, act, status), perm, offsets, compact key staging
     DevBuf mx_keys;                   // host-keys entry point: the batch, on xstream
     DevBuf mx_ext[3];                 // host-keys entry point: its KeyExt blob, offsets, lengths
     DevBuf x_scratch[4];              // xstream's own scan partials + partition scratch
@@ -900,8 +900,9 @@ int shard_pack(gd_handle* h, const void* recs, const uint32_t* payload, uint32_t
 
 // Forward partition of routed messages by the rank hosting their activation (k_fwd_hist): keys
 // move, out_pos[j] = the message's position in the input.
+// n1 (optional): the messages' keys are u32 N1s (one TypeCodeData, N0 = 0) and move as such.
 int fwd_pack(gd_handle* h, const gd_key* keys, const uint8_t* st, const uint32_t* silo, uint32_t n, uint32_t n_shards,
-             uint32_t my_rank, gd_key* out_keys, uint32_t* out_pos, uint32_t* counts) {
+             uint32_t my_rank, void* out_keys, uint32_t* out_pos, uint32_t* counts, const uint32_t* n1 = nullptr) {
     if (n == 0)
         return launch(h, "k_fill", dim3(1), dim3(BLOCK), 0, k_fill_u32, counts, n_shards, 0u);
     const uint32_t tiles = blocks_for(n, SH_TILE);
@@ -914,6 +915,7 @@ int fwd_pack(gd_handle* h, const gd_key* keys, const uint8_t* st, const uint32_t
     while ((1u << bits) < n_shards) ++bits;
     GD_TRY(launch(h, "k_fwd_hist", dim3(tiles), dim3(SH_NT), 0, k_fwd_hist, st, silo, n, n_shards, my_rank, bits, tiles,
                   dest, hist));
+    if (n1) return shard_finish<true>(h, n1, nullptr, n, n_shards, bits, tiles, dest, hist, out_keys, out_pos, counts);
     return shard_finish<false>(h, keys, nullptr, n, n_shards, bits, tiles, dest, hist, out_keys, out_pos, counts);
 }
 
@@ -2912,7 +2914,7 @@ int comm_setup(gd_handle* h) {
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(sync(h));
     comm_release(h);
-    HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 12 * 256 * sizeof(uint32_t)));
+    HIP_TRY(h, hipHostMalloc((void**)&h->h_xcnt, 20 * 256 * sizeof(uint32_t)));
     HIP_TRY(h, hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
     HIP_TRY(h, hipStreamCreateWithFlags(&h->pstream, hipStreamNonBlocking));
     for (hipEvent_t* e : {&h->x_in, &h->x_hdr[0], &h->x_hdr[1], &h->x_route[0], &h->x_route[1], &h->x_ret[0],
@@ -2997,21 +2999,33 @@ int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uin
 // origin rank; every other status stays here.  All messages of one grain pass through its one
 // owner, so each activation's arrival order stays (sender rank, sender batch order).  r holds the
 // owner's routes on entry (probe enqueued, x_route[s] recorded) and the forwarded result on exit.
-int forward_multi(gd_handle* h, int s, uint32_t n_act, gd_multi_result& r) {
+// n1 (optional): the received keys as u32 N1s with one TypeCodeData tcd (a compact header round in
+// mode 2): the forward round moves them as such (4 B instead of 24; descriptor in the counts round)
+// and the final receiver rebuilds the 24-B keys (k_recv_expand).
+int forward_multi(gd_handle* h, int s, uint32_t n_act, gd_multi_result& r, const uint32_t* n1 = nullptr,
+                  uint64_t tcd = 0) {
     const int W = h->n_ranks;
     const Rccl& R = *h->net;
     const uint32_t m = r.n_recv;
     DevBuf* F = h->mf[s];
     const size_t m4 = (size_t)m * 4 + 4;
-    const size_t want_s[8] = {(size_t)m * sizeof(gd_key) + 8, m4, m4, m4, m4, m4, (size_t)m + 4, (size_t)W * 8};
+    const size_t want_s[8] = {(size_t)m * sizeof(gd_key) + 8, m4, m4, m4, m4, m4, (size_t)m + 4,
+                              ((size_t)W * 6 + 4) * 4};
     for (int b = 0; b < 8; ++b) GD_TRY(grow(h, F[b], want_s[b]));
-    uint32_t* fcnt = (uint32_t*)F[7].p;           // send [0,W), recv [W,2W)
+    uint32_t* fcnt = (uint32_t*)F[7].p;           // send [0,W), recv [W,2W), my descriptor, the peers'
+    uint32_t* fdesc = fcnt + 2 * W;
     uint32_t* hc = h->h_xcnt + 10 * 256;
+    uint32_t* mydesc = h->h_xcnt + 19 * 256;      // pinned; read by the copy before the sync below
+    mydesc[0] = n1 ? 2u : 0u;
+    mydesc[1] = 0u;
+    mydesc[2] = (uint32_t)tcd;
+    mydesc[3] = (uint32_t)(tcd >> 32);
     HIP_TRY(h, hipStreamWaitEvent(h->xstream, h->x_route[s], 0));
     {
         OnXStream on(h);
-        GD_TRY(fwd_pack(h, r.recv_keys, r.status, r.silo, m, (uint32_t)W, (uint32_t)h->rank, (gd_key*)F[0].p,
-                        (uint32_t*)F[1].p, fcnt));
+        HIP_TRY(h, hipMemcpyAsync(fdesc, mydesc, 16, hipMemcpyHostToDevice, h->stream));
+        GD_TRY(fwd_pack(h, r.recv_keys, r.status, r.silo, m, (uint32_t)W, (uint32_t)h->rank, F[0].p,
+                        (uint32_t*)F[1].p, fcnt, n1));
         if (m)
             GD_TRY(launch(h, "k_fwd_gather", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_fwd_gather,
                           (const uint32_t*)F[1].p, m, r.recv_idx, r.recv_src, r.silo, r.act, r.status,
@@ -3021,9 +3035,11 @@ int forward_multi(gd_handle* h, int s, uint32_t n_act, gd_multi_result& r) {
         for (int q = 0; q < W; ++q) {
             NCCL_TRY(h, R.Send(fcnt + q, 1, ncclUint32, q, h->comm, h->stream));
             NCCL_TRY(h, R.Recv(fcnt + W + q, 1, ncclUint32, q, h->comm, h->stream));
+            NCCL_TRY(h, R.Send(fdesc, 4, ncclUint32, q, h->comm, h->stream));
+            NCCL_TRY(h, R.Recv(fdesc + 4 + 4 * q, 4, ncclUint32, q, h->comm, h->stream));
         }
         NCCL_TRY(h, R.GroupEnd());
-        HIP_TRY(h, hipMemcpyAsync(hc, fcnt, (size_t)W * 8, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipMemcpyAsync(hc, fcnt, ((size_t)W * 6 + 4) * 4, hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(h, hipStreamSynchronize(h->stream));
     }
     std::vector<uint32_t> sc(hc, hc + W), rc(hc + W, hc + 2 * W);
@@ -3037,19 +3053,35 @@ int forward_multi(gd_handle* h, int s, uint32_t n_act, gd_multi_result& r) {
     if (roff[W] >= 0xFFFFFFFFull)
         return set_err(h, GD_EINVAL, "%llu forwarded messages: more than a batch can hold", (unsigned long long)roff[W]);
     const uint32_t m2 = (uint32_t)roff[W];
+    // key bytes per peer: 4 (u32 N1s) or 24 by each side's descriptor; with any compact peer the
+    // keys land in staging and k_recv_expand rebuilds them
+    const uint32_t* hdsc = hc + 2 * W;             // mine, then the peers'
+    std::vector<uint64_t> ksb(W + 1, 0), krb(W + 1, 0);
+    bool any_c = false;
+    for (int q = 0; q < W; ++q) {
+        const uint32_t c = hdsc[4 + 4 * q];
+        any_c |= c && rc[q];
+        ksb[q + 1] = ksb[q] + (uint64_t)sc[q] * header_bytes(hdsc[0]);
+        krb[q + 1] = krb[q] + (uint64_t)rc[q] * header_bytes(c);
+    }
     const size_t q4 = (size_t)m2 * 4 + 4;
-    const size_t want_r[8] = {(size_t)m2 * sizeof(gd_key) + 8, q4, q4, q4, q4, (size_t)m2 + 4, q4,
-                              ((size_t)n_act + 2) * 4};
-    for (int b = 0; b < 8; ++b) GD_TRY(grow(h, F[8 + b], want_r[b]));
+    const size_t want_r[9] = {(size_t)m2 * sizeof(gd_key) + 8, q4, q4, q4, q4, (size_t)m2 + 4, q4,
+                              ((size_t)n_act + 2) * 4, any_c ? (size_t)krb[W] + 16 : 0};
+    for (int b = 0; b < 9; ++b)
+        if (want_r[b]) GD_TRY(grow(h, F[8 + b], want_r[b]));
     {
         OnXStream on(h);
-        const Lane lanes[6] = {{F[0].p, F[8].p, sizeof(gd_key), ncclUint64, 3},
+        const Lane lanes[6] = {{F[0].p, any_c ? F[16].p : F[8].p, 1, ncclUint8, 1, ksb.data(), krb.data()},
                                {F[2].p, F[9].p, 4, ncclUint32, 1},
                                {F[3].p, F[10].p, 4, ncclUint32, 1},
                                {F[4].p, F[11].p, 4, ncclUint32, 1},
                                {F[5].p, F[12].p, 4, ncclUint32, 1},
                                {F[6].p, F[13].p, 1, ncclUint8, 1}};
         GD_TRY(exchange_round(h, "rccl_forward", sc.data(), soff.data(), rc.data(), roff.data(), lanes, 6));
+        if (any_c && m2)
+            GD_TRY(launch(h, "k_recv_expand", dim3(blocks_for(m2, BLOCK)), dim3(BLOCK), 0, k_recv_expand,
+                          (const uint8_t*)F[16].p, (const uint32_t*)(fcnt + W), (const uint32_t*)(fdesc + 4),
+                          (uint32_t)W, m2, (gd_key*)F[8].p, (uint32_t*)nullptr));
         HIP_TRY(h, hipEventRecord(h->x_fwd[s], h->xstream));
     }
     HIP_TRY(h, hipStreamWaitEvent(h->stream, h->x_fwd[s], 0));
@@ -3365,7 +3397,9 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
     r.status = st;
     r.perm = perm;
     r.offsets = offs;
-    if (fwd) GD_TRY(forward_multi(h, s, n_act, r));
+    // compact forward keys: every received header a u32 N1 of one type (the probe's N1 path)
+    if (fwd)
+        GD_TRY(forward_multi(h, s, n_act, r, n1_path && n1_mode == 2 ? (const uint32_t*)B[18].p : nullptr, n1_tcd));
     HIP_TRY(h, hipEventRecord(h->x_done[s], h->stream));
     h->x_done_rec[s] = true;
     h->mres[s] = r;

@@ -317,10 +317,12 @@ def test_ring_owner_ext_is_the_partition_owner(gd, mode):
     e.close()
 
 
-@pytest.mark.parametrize("n", [0, 1, 70001])
-def test_route_multi_forward_world1(gd, n):
+@pytest.mark.parametrize("n,mixed", [(0, False), (1, False), (70001, False), (70001, True)])
+def test_route_multi_forward_world1(gd, n, mixed):
     """GD_MULTI_FORWARD at world 1: the forward hop is a send to self, so the result equals the
-    co-located one (the activation silos here differ from the owners)."""
+    co-located one (the activation silos here differ from the owners).  One grain type with small
+    keys: the forward round moves u32 N1s (descriptor mode 2) and the keys are rebuilt; mixed
+    (system targets among them): 24-B keys."""
     silos = o.bench_silos(8)
     spec = o.ring_spec(silos, "R")
     G = 3000
@@ -328,6 +330,8 @@ def test_route_multi_forward_world1(gd, n):
     act_silo = ((5 * np.arange(G) + 1) % 8).astype(np.uint32)
     rng = np.random.default_rng(n + 5)
     keys = o.grain_keys(TC, rng.integers(0, G + 200, size=n))
+    if mixed:
+        keys[::17] = np.array(o.UniqueKey(0, 7, o.type_code_data(o.CAT_SYSTEM_TARGET, 1)).as_tuple(), np.uint64)
     e = gd.GrainDispatch(device=0, table_capacity=1 << 13, my_silo=4)
     e.ring_set_silos("R", [(s.ip, s.port, s.gen) for s in silos])
     e.register(reg, np.arange(G), act_silo)
