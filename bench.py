@@ -272,7 +272,15 @@ def main():
     else:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29571")
-        dist.init_process_group("gloo", rank=0, world_size=1)
+        # gloo's connect message goes to fd 1: keep stdout for the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=0, world_size=1)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     if args.workload == "cfg4":
         return run_cfg4(args, world, rank, local, dev)
 

@@ -607,8 +607,9 @@ int gd_fanout_multi_fetch(gd_handle* h, uint32_t hop, uint32_t* frontier, uint32
  * GD_ROUTE_MISS, as is a cache miss (silo = ring owner, act = GD_NO_ACTIVATION).  The LRU is the
  * reference's exactly: every hit and every add takes the next generation (hits in batch order),
  * AdjustSize evicts the lowest generation while count >= max_size.  max_size 0 = no cache
- * (whole-node mode: every grain is probed in this handle's table).  The specialised paths
- * (frames, micro-batch, fan-out) do not consult the cache. */
+ * (whole-node mode: every grain is probed in this handle's table).  The frame and micro-batch
+ * paths run LocalLookup too (the micro-batch eagerly in this mode); the fan-out paths do not
+ * consult the cache. */
 typedef struct gd_cache_stats {
     uint64_t count;             /* live entries (LRU.Count)                       */
     uint64_t accesses;          /* NumAccesses                                     */
@@ -633,6 +634,26 @@ int gd_cache_stats_get(gd_handle* h, gd_cache_stats* out);
 /* KeyValues (:111-127) with each entry's generation, in slot order; keys NULL = size query. */
 int gd_cache_entries(gd_handle* h, gd_key* keys, gd_val* vals, int32_t* versions, uint64_t* generations,
                      uint64_t capacity, uint64_t* out_n);
+/* KeyExt grains (string, compound keys, geo clients: UniqueKey.HasKeyExt) in the cache, keyed by their
+ * KeyExt as UniqueKey.Equals is (UniqueKey.cs:245-251) and homed by the KeyExt uniform hash
+ * (UniqueKey.cs:272-336).  gd_route_ext / gd_route_bucket_ext[_device] / gd_route_frames_ext* in
+ * LocalLookup mode route KeyExt grains the same way as the three-word ones: the owner by the KeyExt
+ * hash, a local owner's grains in this handle's KeyExt partition (gd_dir_register_ext), the others
+ * in the cache (AdaptiveGrainDirectoryCache.cs:93-110), every hit of the batch numbered in batch
+ * order.  One LRU holds both kinds (one generation sequence, one max_size).  `ext` is read for
+ * KeyExt-category keys only; GD_KEYEXT_NULL there is the three-word entry, GD_KEYEXT_HOST is
+ * GD_EINVAL.  The plain forms above treat a KeyExt-category key as KeyExt null. */
+int gd_cache_add_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, const gd_val* vals,
+                     const int32_t* versions, uint32_t n);
+int gd_cache_remove_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, uint8_t* out_removed);
+int gd_cache_lookup_ext(gd_handle* h, const gd_key* keys, const gd_key_ext* ext, uint32_t n, gd_val* out_vals,
+                        int32_t* out_versions, uint8_t* out_found);
+/* gd_cache_entries with each entry's KeyExt: ext_len[k] (GD_KEYEXT_NULL for a three-word key), its
+ * UTF-8 bytes at ext_bytes + ext_off[k]; *out_bytes = the bytes all strings need.  keys NULL = size
+ * query (*out_n, *out_bytes). */
+int gd_cache_entries_ext(gd_handle* h, gd_key* keys, gd_val* vals, int32_t* versions, uint64_t* generations,
+                         int32_t* ext_len, uint64_t* ext_off, uint8_t* ext_bytes, uint64_t capacity,
+                         uint64_t bytes_capacity, uint64_t* out_n, uint64_t* out_bytes);
 
 /* ---- membership change: IsValidSilo, VersionTag, silo removal, handoff merge ----
  * GrainDirectoryPartition.IsValidSilo (GrainDirectoryPartition.cs:242-245, the membership oracle's

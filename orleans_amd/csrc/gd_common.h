@@ -31,6 +31,11 @@ constexpr uint32_t CAT_SYSTEM_GRAIN = 2;
 constexpr uint32_t CAT_GRAIN = 3;
 constexpr uint32_t CAT_KEYEXT_GRAIN = 6;
 constexpr uint32_t CAT_GEO_CLIENT = 7;
+// Categories whose keys carry a KeyExt (UniqueKey.HasKeyExt, Orleans.Core.Abstractions/IDs/UniqueKey.cs:61-68).
+GD_HD bool is_keyext_tcd(uint64_t tcd) {
+    const uint32_t c = (uint32_t)(tcd >> 56);
+    return c == CAT_KEYEXT_GRAIN || c == CAT_GEO_CLIENT;
+}
 
 // Constants.SystemMembershipTableId (src/Orleans.Core/Runtime/Constants.cs:52):
 // SystemGrain key of Guid 01145FEC-C21E-11E0-9105-D0FB4724019B in Guid.ToByteArray

@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(BLOCK) k_cache_adjust(CacheSlot* slots, unsign
         const uint32_t meta = slots[j].meta;
         if (slot_state(meta) == SLOT_LIVE) {
             const CacheSlot& c = slots[j];
-            const uint32_t owner = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(c.n0, c.n1, c.tcd))];
+            const uint32_t owner = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, cache_slot_hash(c))];
             rm = (owner < n_local && local[owner]) || in_set(set, slot_silo(meta));
             if (rm) slots[j].meta = make_meta(SLOT_TOMB, 0);
         }

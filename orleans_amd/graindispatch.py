@@ -45,7 +45,8 @@ EXPORTED_SYMBOLS = [
     "gd_fanout_expand_device", "gd_fanout_route_bucket_device", "gd_fanout_route_bucket", "gd_route_nodes_device",
     "gd_pack_nodes_by_shard_device", "gd_frontier_next_device",
     "gd_cache_configure", "gd_cache_set_silos", "gd_cache_add", "gd_cache_remove", "gd_cache_lookup",
-    "gd_cache_clear", "gd_cache_stats_get", "gd_cache_entries",
+    "gd_cache_clear", "gd_cache_stats_get", "gd_cache_entries", "gd_cache_add_ext", "gd_cache_remove_ext",
+    "gd_cache_lookup_ext", "gd_cache_entries_ext",
     "gd_route_frames_ext_device", "gd_route_frames_ext",
     "gd_dir_register_ext", "gd_dir_unregister_ext", "gd_dir_lookup_ext", "gd_uniform_hashes_ext",
     "gd_dir_ext_stats", "gd_route_ext", "gd_route_bucket_ext", "gd_route_ext_device", "gd_route_bucket_ext_device",
@@ -282,6 +283,10 @@ def _load() -> C.CDLL:
         "gd_cache_clear": (C.c_int, [P]),
         "gd_cache_stats_get": (C.c_int, [P, C.POINTER(gd_cache_stats)]),
         "gd_cache_entries": (C.c_int, [P, P, P, P, P, U64, C.POINTER(U64)]),
+        "gd_cache_add_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), P, P, U32]),
+        "gd_cache_remove_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, P]),
+        "gd_cache_lookup_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, P, P, P]),
+        "gd_cache_entries_ext": (C.c_int, [P, P, P, P, P, P, P, P, U64, U64, C.POINTER(U64), C.POINTER(U64)]),
         "gd_dir_register_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), P, U32, P, P]),
         "gd_dir_unregister_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), P, U32, P]),
         "gd_dir_lookup_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, P, P]),
@@ -802,29 +807,43 @@ class GrainDispatch:
         val = self._silo_mask(valid_silos, n_silos, 1)
         self._c(lib.gd_cache_set_silos(self.h, _ptr(loc), _ptr(val), n_silos))
 
-    def cache_add(self, keys, acts, silos, versions):
+    def cache_add(self, keys, acts, silos, versions, exts=None):
+        """AddOrUpdate in order; exts (one per key, see KeyExtBatch) keys KeyExt grains by their string."""
         k = keys_array(keys)
         n = len(k)
         vals = np.zeros((n, 2), dtype=np.uint32)
         vals[:, 0] = acts
         vals[:, 1] = silos
         ver = np.ascontiguousarray(np.asarray(versions, dtype=np.int32))
-        self._c(lib.gd_cache_add(self.h, _ptr(k), _ptr(vals), _ptr(ver), n))
+        if exts is None:
+            self._c(lib.gd_cache_add(self.h, _ptr(k), _ptr(vals), _ptr(ver), n))
+        else:
+            x = self._ext(exts, n)
+            self._c(lib.gd_cache_add_ext(self.h, _ptr(k), C.byref(x.struct), _ptr(vals), _ptr(ver), n))
 
-    def cache_remove(self, keys) -> np.ndarray:
+    def cache_remove(self, keys, exts=None) -> np.ndarray:
         k = keys_array(keys)
         out = np.zeros(len(k), dtype=np.uint8)
-        self._c(lib.gd_cache_remove(self.h, _ptr(k), len(k), _ptr(out)))
+        if exts is None:
+            self._c(lib.gd_cache_remove(self.h, _ptr(k), len(k), _ptr(out)))
+        else:
+            x = self._ext(exts, len(k))
+            self._c(lib.gd_cache_remove_ext(self.h, _ptr(k), C.byref(x.struct), len(k), _ptr(out)))
         return out
 
-    def cache_lookup(self, keys):
+    def cache_lookup(self, keys, exts=None):
         """Returns (found u8, act u32, silo u32, version i32)."""
         k = keys_array(keys)
         n = len(k)
         vals = np.zeros((n, 2), dtype=np.uint32)
         ver = np.zeros(n, dtype=np.int32)
         found = np.zeros(n, dtype=np.uint8)
-        self._c(lib.gd_cache_lookup(self.h, _ptr(k), n, _ptr(vals), _ptr(ver), _ptr(found)))
+        if exts is None:
+            self._c(lib.gd_cache_lookup(self.h, _ptr(k), n, _ptr(vals), _ptr(ver), _ptr(found)))
+        else:
+            x = self._ext(exts, n)
+            self._c(lib.gd_cache_lookup_ext(self.h, _ptr(k), C.byref(x.struct), n, _ptr(vals), _ptr(ver),
+                                            _ptr(found)))
         return found, vals[:, 0].copy(), vals[:, 1].copy(), ver
 
     def cache_clear(self):
@@ -848,6 +867,30 @@ class GrainDispatch:
             self._c(lib.gd_cache_entries(self.h, _ptr(k), _ptr(v), _ptr(ver), _ptr(gen), m, C.byref(n)))
         return {tuple(int(x) for x in k[i]): (int(v[i, 0]), int(v[i, 1]), int(ver[i]), int(gen[i]))
                 for i in range(m)}
+
+    def cache_entries_ext(self) -> dict:
+        """(n0, n1, tcd) or (n0, n1, tcd, KeyExt bytes) -> (act, silo, version, generation)."""
+        n, nb = C.c_uint64(0), C.c_uint64(0)
+        self._c(lib.gd_cache_entries_ext(self.h, None, None, None, None, None, None, None, 0, 0, C.byref(n),
+                                         C.byref(nb)))
+        m, b = n.value, nb.value
+        k = np.zeros((max(m, 1), 3), dtype=np.uint64)
+        v = np.zeros((max(m, 1), 2), dtype=np.uint32)
+        ver = np.zeros(max(m, 1), dtype=np.int32)
+        gen = np.zeros(max(m, 1), dtype=np.uint64)
+        xl = np.zeros(max(m, 1), dtype=np.int32)
+        xo = np.zeros(max(m, 1), dtype=np.uint64)
+        blob = np.zeros(max(b, 1), dtype=np.uint8)
+        if m:
+            self._c(lib.gd_cache_entries_ext(self.h, _ptr(k), _ptr(v), _ptr(ver), _ptr(gen), _ptr(xl), _ptr(xo),
+                                             _ptr(blob), m, b, C.byref(n), C.byref(nb)))
+        out = {}
+        for i in range(m):
+            key = tuple(int(x) for x in k[i])
+            if xl[i] >= 0:
+                key = key + (bytes(blob[int(xo[i]):int(xo[i]) + int(xl[i])]),)
+            out[key] = (int(v[i, 0]), int(v[i, 1]), int(ver[i]), int(gen[i]))
+        return out
 
     # -- follower fan-out (SURVEY 8 f2) ----------------------------------------------
     def fanout_route_bucket(self, row_off, dst, frontier, type_code: int, n_act: Optional[int]):

@@ -646,7 +646,8 @@ private:
 
 // AdaptiveGrainDirectoryCache<IReadOnlyList<Tuple<SiloAddress, ActivationId>>> for
 // single-activation grains (AdaptiveGrainDirectoryCache.cs:7-140 over LRU.cs): the handle's GPU
-// cache, exact LRU generations.  Owned by a LocalGrainDirectory in per-silo mode.
+// cache, exact LRU generations, string-keyed grains keyed by their KeyExt (gd_cache_*_ext).
+// Owned by a LocalGrainDirectory in per-silo mode.
 class AdaptiveGrainDirectoryCache {
 public:
     using Value = std::pair<SiloAddress, ActivationId>;
@@ -663,25 +664,30 @@ public:
         std::vector<gd_key> k(n);
         std::vector<gd_val> v(n);
         std::vector<int32_t> ver(versions.begin(), versions.end());
+        std::vector<const UniqueKey*> uk(n);
         for (size_t i = 0; i < n; ++i) {
             k[i] = keys[i].Key.ToNative();
+            uk[i] = &keys[i].Key;
             v[i] = gd_val{acts_.ActIndex(values[i].second), silos_.IndexOf(values[i].first)};
         }
-        if (n) Check(h_, gd_cache_add(h_, k.data(), v.data(), ver.data(), (uint32_t)n));
+        KeyExtBatch kx(uk);
+        if (n) Check(h_, gd_cache_add_ext(h_, k.data(), kx.get(), v.data(), ver.data(), (uint32_t)n));
     }
     bool Remove(const GrainId& key) {                   // :79-83
         const gd_key k = key.Key.ToNative();
+        KeyExtBatch kx({&key.Key});
         uint8_t removed = 0;
-        Check(h_, gd_cache_remove(h_, &k, 1, &removed));
+        Check(h_, gd_cache_remove_ext(h_, &k, kx.get(), 1, &removed));
         return removed != 0;
     }
     void Clear() { Check(h_, gd_cache_clear(h_)); }     // :85-88
     bool LookUp(const GrainId& key, Value& result, int& version) {   // :90-109
         const gd_key k = key.Key.ToNative();
+        KeyExtBatch kx({&key.Key});
         gd_val v{};
         int32_t ver = 0;
         uint8_t found = 0;
-        Check(h_, gd_cache_lookup(h_, &k, 1, &v, &ver, &found));
+        Check(h_, gd_cache_lookup_ext(h_, &k, kx.get(), 1, &v, &ver, &found));
         if (!found) return false;
         result = Value{silos_.At(v.silo), acts_.ActivationAt(v.act)};
         version = ver;
@@ -689,19 +695,24 @@ public:
     }
     // KeyValues (:111-127)
     std::vector<std::tuple<GrainId, Value, int>> KeyValues() const {
-        uint64_t n = 0;
-        Check(h_, gd_cache_entries(h_, nullptr, nullptr, nullptr, nullptr, 0, &n));
+        uint64_t n = 0, nb = 0;
+        Check(h_, gd_cache_entries_ext(h_, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, &n,
+                                       &nb));
         std::vector<gd_key> k(n);
         std::vector<gd_val> v(n);
-        std::vector<int32_t> ver(n);
-        std::vector<uint64_t> gen(n);
-        if (n) Check(h_, gd_cache_entries(h_, k.data(), v.data(), ver.data(), gen.data(), n, &n));
+        std::vector<int32_t> ver(n), xl(n);
+        std::vector<uint64_t> gen(n), xo(n);
+        std::vector<uint8_t> bytes(nb + 1);
+        if (n)
+            Check(h_, gd_cache_entries_ext(h_, k.data(), v.data(), ver.data(), gen.data(), xl.data(), xo.data(),
+                                           bytes.data(), n, nb, &n, &nb));
         std::vector<std::tuple<GrainId, Value, int>> r;
         for (uint64_t i = 0; i < n; ++i) {
             GrainId g;
             g.Key.N0 = k[i].n0;
             g.Key.N1 = k[i].n1;
             g.Key.TypeCodeData = k[i].type_code_data;
+            if (xl[i] >= 0) g.Key.KeyExt = std::string(reinterpret_cast<const char*>(bytes.data() + xo[i]), (size_t)xl[i]);
             r.emplace_back(g, Value{silos_.At(v[i].silo), acts_.ActivationAt(v[i].act)}, ver[i]);
         }
         return r;
@@ -799,7 +810,8 @@ public:
         const gd_key k = grain.Key.ToNative();
         uint32_t silo = 0, act = 0;
         uint8_t st = 0;
-        Check(h_, gd_route(h_, &k, 1, &silo, &act, &st));
+        KeyExtBatch kx({&grain.Key});                 // string-keyed grains: KeyExt owner, partition or cache
+        Check(h_, gd_route_ext(h_, &k, kx.get(), 1, &silo, &act, &st));
         result = AddressesAndTag{};
         if (st != GD_ROUTE_OK) return false;
         result.Addresses = std::vector<ActivationAddress>{{silos_.At(silo), grain, partition_.ActivationAt(act)}};

@@ -496,6 +496,43 @@ static void PerSiloLocalLookup() {           // LocalGrainDirectory.LocalLookup,
     EXPECT(c.Count() == 0 && !c.Remove(f.Key(theirs)));
 }
 
+// LocalLookup of string-keyed grains in the per-silo model: the owner by the KeyExt uniform hash,
+// this silo's KeyExt partition for its own grains, the cache for the others -- keyed by the string
+// (UniqueKey.Equals, UniqueKey.cs:245-251): "alice" and "alice!" of one type are different entries.
+static void PerSiloLocalLookupStringKeys() {
+    CacheFixture f(100);
+    auto& part = f.dir.DirectoryPartition();
+    auto& c = f.dir.DirectoryCache();
+    const int stc = gd_calculate_id_hash("UnitTests.StringKeyGrain");
+    std::vector<GrainId> mine, theirs;
+    for (int k = 0; k < 400 && (mine.size() < 2 || theirs.size() < 2); ++k) {
+        const GrainId g = GrainId::GetGrainId(stc, std::string("user/") + std::to_string(k));
+        (f.dir.CalculateTargetSilo(g) == f.dir.MyAddress ? mine : theirs).push_back(g);
+    }
+    EXPECT(mine.size() >= 2 && theirs.size() >= 2);
+    part.AddSingleActivation(mine[0], NewActivationId(11), f.dir.MyAddress);
+    AddressesAndTag r;
+    EXPECT(f.dir.LocalLookup(mine[0], r) && (*r.Addresses)[0].Activation == NewActivationId(11));
+    EXPECT(!f.dir.LocalLookup(mine[1], r));                    // owned, not registered
+    EXPECT(!f.dir.LocalLookup(theirs[0], r));                  // not owned, not cached
+    const SiloAddress s3 = SiloAddress::New(10, 0, 0, 3, 11111, 1);
+    c.AddOrUpdate(theirs[0], {s3, NewActivationId(12)}, 5);
+    EXPECT(f.dir.LocalLookup(theirs[0], r) && (*r.Addresses)[0].Silo == s3 &&
+           (*r.Addresses)[0].Activation == NewActivationId(12));
+    GrainId other = theirs[0];
+    other.Key.KeyExt = *other.Key.KeyExt + "!";                // same words, another KeyExt
+    AdaptiveGrainDirectoryCache::Value v;
+    int ver = 0;
+    EXPECT(!c.LookUp(other, v, ver));
+    EXPECT(c.LookUp(theirs[0], v, ver) && ver == 5 && v.second == NewActivationId(12));
+    bool dumped = false;                                        // KeyValues returns the string key
+    for (const auto& kv : c.KeyValues()) dumped = dumped || std::get<0>(kv) == theirs[0];
+    EXPECT(dumped && c.Count() == 1);
+    EXPECT(c.NumAccesses() == 4 && c.NumHits() == 2);
+    EXPECT(c.Remove(theirs[0]) && !c.Remove(theirs[0]) && c.Count() == 0);
+    EXPECT(!f.dir.LocalLookup(theirs[0], r));
+}
+
 static void RoutingDump(const char* path) {
     // bench silos, ring D, 20000 grains of the Ping type: owner silo index per grain (oracle-checked)
     DispatchHandle h(0, 1 << 15, 0);
@@ -793,6 +830,7 @@ int main(int argc, char** argv) {
         Run("LruMaximumSizeTest", LruMaximumSizeTest);
         Run("LruUsageTest", LruUsageTest);
         Run("PerSiloLocalLookup", PerSiloLocalLookup);
+        Run("PerSiloLocalLookupStringKeys", PerSiloLocalLookupStringKeys);
         Run("WholeNodeExchange", WholeNodeExchange);
         Run("SiloRemovalAdjustsDirectory", SiloRemovalAdjustsDirectory);
         Run("MergeKeepsLowestActivationId", MergeKeepsLowestActivationId);

@@ -34,8 +34,9 @@ def test_host_cpp_gpu(tmp_path):
     assert p.returncode == 0, p.stdout + p.stderr
     for name in ("RingStandalone_Basic", "RingStandalone_Failures", "RingStandalone_Joins", "RingStandalone_Mixed",
                  "VirtualBucketsRanges", "DirectorySemantics", "DispatcherAndAgent", "StringKeyGrains", "MultiActivationGrains", "LruCountTest",
-                 "LruMaximumSizeTest", "LruUsageTest", "PerSiloLocalLookup", "WholeNodeExchange", "SiloRemovalAdjustsDirectory",
-                 "MergeKeepsLowestActivationId", "ActivationDirectoryReceive", "RoutingDump"):
+                 "LruMaximumSizeTest", "LruUsageTest", "PerSiloLocalLookup", "PerSiloLocalLookupStringKeys", "WholeNodeExchange", "SiloRemovalAdjustsDirectory",
+                 "MergeKeepsLowestActivationId", "MergeStringKeyGrains", "RemoveLastInstanceCountsOnce",
+                 "ActivationDirectoryReceive", "RoutingDump"):
         assert f"PASS {name}" in p.stdout, p.stdout + p.stderr
     rows = np.loadtxt(dump, dtype=np.int64)
     tc = o.grain_type_code(o.PING_GRAIN_CLASS)
