@@ -18,6 +18,7 @@
 #include "gd_churn.h"
 #include "gd_fanout.h"
 #include "gd_cache.h"
+#include "gd_cx.h"
 #include "gd_shard.h"
 #include "gd_comm.h"
 #include "gd_localcomm.h"
@@ -169,6 +170,14 @@ struct gd_handle {
     int route_m = 1;
     bool route_nt = false;
     bool route_xcd = true;      // route workgroups over XCD-contiguous message ranges (GD_ROUTE_XCD)
+    // compact probe index (gd_cx.h): derived from the table, rebuilt after any change of it (GD_CX=0: off)
+    bool cx_on = true;
+    uint64_t tab_gen = 0;       // bumped by every launch that takes the table as a writable Slot*
+    bool cx_built = false, cx_ok = false;
+    const Slot* cx_slots_at = nullptr;
+    uint64_t cx_cap_at = 0, cx_gen_at = 0;
+    uint32_t cx_rounds = 0;
+    DevBuf cxi_tab, cxi_types, cxi_ctr;
     int radix_max_bits = 8;   // digit width cap (GD_RADIX_MAXBITS, 4..11)
     int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
@@ -271,10 +280,17 @@ hipEvent_t take_event(gd_handle* h) {
     return e;
 }
 
-// Launch a kernel on the handle's stream; with GD_CFG_KERNEL_TIMING bracket it by events.
+// A launch argument that is the directory table as a writable Slot* (the kernel may change it).
+template <typename T>
+bool writes_table(const gd_handle*, const T&) { return false; }
+bool writes_table(const gd_handle* h, Slot* p) { return p != nullptr && p == h->slots; }
+
+// Launch a kernel on the handle's stream; with GD_CFG_KERNEL_TIMING bracket it by events.  A kernel
+// handed the table as a writable Slot* invalidates the compact probe index (tab_gen).
 template <typename K, typename... Args>
 int launch(gd_handle* h, const char* name, dim3 grid, dim3 block, size_t lds, K kernel, Args... args) {
     if (grid.x == 0) return GD_OK;
+    if ((writes_table(h, args) || ...)) h->tab_gen++;
     hipEvent_t a = nullptr, b = nullptr;
     if (h->timing) {
         a = take_event(h);
@@ -368,12 +384,60 @@ unsigned long long pow2_at_least(unsigned long long x) {
     return c;
 }
 
+// ---- compact probe index (gd_cx.h) ----------------------------------------------
+// The index for the current table: rebuilt (two passes + one host sync) when the table changed since
+// the last build; false when the table is not eligible (an N0 != 0 key, too many types) or GD_CX=0.
+int cx_ensure(gd_handle* h, bool* ok) {
+    *ok = false;
+    if (!h->cx_on || !h->slots || h->capacity < CX_GROUP) return GD_OK;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;   // a captured graph keeps the directory probe
+    HIP_TRY(h, hipStreamIsCapturing(h->stream, &cs));
+    if (cs != hipStreamCaptureStatusNone) return GD_OK;
+    if (h->cx_built && h->cx_slots_at == h->slots && h->cx_cap_at == h->capacity && h->cx_gen_at == h->tab_gen) {
+        *ok = h->cx_ok;
+        return GD_OK;
+    }
+    const unsigned long long cap = h->capacity;
+    GD_TRY(ensure(h, h->cxi_tab, cap * 16));
+    GD_TRY(ensure(h, h->cxi_types, CX_TYPES * 8));
+    GD_TRY(ensure(h, h->cxi_ctr, sizeof(CxCounters)));
+    HIP_TRY(h, hipMemsetAsync(h->cxi_tab.p, 0, cap * 16, h->stream));
+    HIP_TRY(h, hipMemsetAsync(h->cxi_types.p, 0xFF, CX_TYPES * 8, h->stream));
+    HIP_TRY(h, hipMemsetAsync(h->cxi_ctr.p, 0, sizeof(CxCounters), h->stream));
+    const dim3 g(blocks_for(cap, BLOCK)), b(BLOCK);
+    GD_TRY(launch(h, "k_cx_types", g, b, 0, k_cx_types, (const Slot*)h->slots, cap,
+                  (unsigned long long*)h->cxi_types.p, (CxCounters*)h->cxi_ctr.p));
+    GD_TRY(launch(h, "k_cx_build", g, b, 0, k_cx_build, (const Slot*)h->slots, cap,
+                  (const unsigned long long*)h->cxi_types.p, (uint4*)h->cxi_tab.p, cap, (CxCounters*)h->cxi_ctr.p));
+    CxCounters c{};
+    HIP_TRY(h, hipMemcpyAsync(&c, h->cxi_ctr.p, sizeof c, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    h->cx_built = true;
+    h->cx_ok = c.flag == 0 && c.full == 0;
+    h->cx_rounds = c.max_rounds;
+    h->cx_slots_at = h->slots;
+    h->cx_cap_at = h->capacity;
+    h->cx_gen_at = h->tab_gen;
+    *ok = h->cx_ok;
+    return GD_OK;
+}
+
+CxArgs cx_args(gd_handle* h) {
+    return CxArgs{(const uint4*)h->cxi_tab.p, h->capacity, (const unsigned long long*)h->cxi_types.p, h->cx_rounds};
+}
+
 // ---- route -------------------------------------------------------------------
 template <int MODE, int M, bool NT>
 int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
+    bool cx = false;
+    GD_TRY(cx_ensure(h, &cx));
+    if (cx)
+        return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h),
+                      k_route_m<MODE, M, NT, 0, true>, keys, n, ring_args(h), table_args(h), silo, act, status, 0ull,
+                      h->route_xcd ? 1u : 0u, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, cx_args(h));
     return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h), k_route_m<MODE, M, NT>, keys,
                   n, ring_args(h), table_args(h), silo, act, status, 0ull, h->route_xcd ? 1u : 0u,
-                  (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr);
+                  (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, CxArgs{});
 }
 
 // Keys given as N1 alone (u64, or u32 with n1w = 4) with one TypeCodeData (a compact exchange
@@ -383,11 +447,19 @@ int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uin
                   uint32_t* act, uint8_t* status, const uint32_t* rcnt, uint32_t world, uint32_t* src) {
     const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
     const uint32_t xcd = h->route_xcd ? 1u : 0u;
+    bool cx = false;
+    GD_TRY(cx_ensure(h, &cx));
+    if (cx && n1w == 4)
+        return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4, true>, k, n, ring_args(h),
+                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h));
+    if (cx)
+        return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8, true>, k, n, ring_args(h),
+                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h));
     if (n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4>, k, n, ring_args(h), table_args(h),
-                      silo, act, status, tcd, xcd, rcnt, world, src);
+                      silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{});
     return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8>, k, n, ring_args(h), table_args(h),
-                  silo, act, status, tcd, xcd, rcnt, world, src);
+                  silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{});
 }
 
 // src (optional): also the sender rank of every message, from the per-sender counts rcnt[world].
@@ -1053,6 +1125,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_ROUTE_M")) h->route_m = std::atoi(v);
     if (const char* v = std::getenv("GD_ROUTE_NT")) h->route_nt = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_ROUTE_XCD")) h->route_xcd = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_CX")) h->cx_on = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
     if (const char* v = std::getenv("GD_RADIX_RANK")) h->radix_rank_atomic = std::atoi(v) ? 1u : 0u;
@@ -1136,6 +1209,9 @@ void gd_destroy(gd_handle* h) {
     free_buf(h->cache_valid);
     if (h->cslots) (void)hipFree(h->cslots);
     free_buf(h->cx_heap);
+    free_buf(h->cxi_tab);
+    free_buf(h->cxi_types);
+    free_buf(h->cxi_ctr);
     if (h->cctr) (void)hipFree(h->cctr);
     if (h->slots) (void)hipFree(h->slots);
     if (h->ctr) (void)hipFree(h->ctr);
@@ -1434,6 +1510,7 @@ int gd_dir_clear(gd_handle* h) {
     if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
     HIP_TRY(h, hipSetDevice(h->device));
     HIP_TRY(h, hipMemsetAsync(h->slots, 0, h->capacity * sizeof(Slot), h->stream));
+    h->tab_gen++;
     HIP_TRY(h, hipMemsetAsync(h->vtag, 0, h->capacity * sizeof(uint32_t), h->stream));
     HIP_TRY(h, hipMemsetAsync(h->ctr, 0, sizeof(DevCounters), h->stream));
     if (h->kx_cap) {                   // KeyExt entries go too
@@ -1473,6 +1550,7 @@ int gd_dir_rehash(gd_handle* h, uint64_t new_capacity) {
     h->vtag = nv;
     h->capacity = cap;
     h->layout_gen++;
+    h->tab_gen++;
     GD_TRY(pull_counters(h));
     if (h->ctr_host.err) return set_err(h, GD_EFULL, "rehash failed (0x%x)", h->ctr_host.err);
     return GD_OK;

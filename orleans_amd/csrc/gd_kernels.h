@@ -143,6 +143,42 @@ __device__ __forceinline__ bool is_membership(uint64_t n0, uint64_t n1, uint64_t
     return n0 == MEMBERSHIP_N0 && n1 == MEMBERSHIP_N1 && tcd == MEMBERSHIP_TCD;
 }
 
+// ---- compact probe index (gd_cx.h builds it) ------------------------------------------------
+// A derived, read-only copy of the directory for the probe, built when every live entry has N0 = 0
+// (long-keyed grains, GrainId.GetGrainId(typeCode, long), GrainId.cs:72-77) and at most 256 distinct
+// TypeCodeData: 16-B slots {N1, act, meta = silo | type index << 16 | CX_LIVE}, 4 to a 64-B DRAM
+// atom, so one read a round covers 4 slots of a table half the directory's size.  Homed by the
+// same uniform hash (multiply-shift over any capacity), linear probing in aligned 4-slot groups,
+// no tombstones (rebuilt, never updated).  The types: 256 u64 TypeCodeData slots (open addressing,
+// CX_NO_TYPE empty) staged in LDS by the route kernel.
+constexpr uint32_t CX_GROUP = 4;
+constexpr uint32_t CX_LIVE = 1u << 24;
+constexpr uint32_t CX_TYPES = 256;
+constexpr unsigned long long CX_NO_TYPE = ~0ull;
+struct CxArgs {
+    const uint4* slots;
+    unsigned long long cap;        // slots, a multiple of CX_GROUP
+    const unsigned long long* types;
+    uint32_t max_rounds;           // groups past the home group any entry sits
+};
+__host__ __device__ __forceinline__ uint32_t cx_type_home(uint64_t tcd) {
+    return fmix32((uint32_t)tcd ^ fmix32((uint32_t)(tcd >> 32))) & (CX_TYPES - 1);
+}
+__host__ __device__ __forceinline__ unsigned long long cx_home(uint32_t h, unsigned long long cap) {
+    return (((unsigned long long)fmix32(h) * cap) >> 32) & ~(unsigned long long)(CX_GROUP - 1);
+}
+// Type index of tcd in the staged type set, or -1.
+__device__ __forceinline__ int cx_type_index(const unsigned long long* s_types, uint64_t tcd) {
+    uint32_t t = cx_type_home(tcd);
+    for (uint32_t k = 0; k < CX_TYPES; ++k) {
+        const unsigned long long v = s_types[t];
+        if (v == tcd) return (int)t;
+        if (v == CX_NO_TYPE) return -1;
+        t = (t + 1) & (CX_TYPES - 1);
+    }
+    return -1;
+}
+
 // Linear probe of the open-addressing directory for a live entry with this key.
 __device__ __forceinline__ bool probe(const Slot* slots, unsigned long long mask, uint32_t max_probe,
                                       uint32_t h, uint64_t n0, uint64_t n1, uint64_t tcd,
@@ -250,13 +286,15 @@ __device__ __forceinline__ void st(T* p, T v) {
 // N1W: 0 = 24-B keys; 8 / 4 = the keys arrive as N1 alone (u64 / u32 each; N0 = 0, TypeCodeData =
 // tcd_u for all), the forms a compact exchange header round delivers (k_key_desc, gd_shard.h).
 // The per-thread part: messages base + j * STRIDE, j < M; lds_act (optional) gets act too.
-template <int MODE, int M, int STRIDE, bool NT, int N1W, bool NT_SIDE = false>
+// CX: probe the compact index (cx, its type set staged in s_types) instead of the directory.
+template <int MODE, int M, int STRIDE, bool NT, int N1W, bool NT_SIDE = false, bool CX = false>
 __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, uint32_t n, uint32_t base,
                                              const RingArgs& ring, const uint32_t* s_pts, const uint32_t* s_own,
                                              const TableArgs& tab, uint32_t max_probe,
                                              uint32_t* __restrict__ out_silo, uint32_t* __restrict__ out_act,
                                              uint8_t* __restrict__ out_status, uint64_t tcd_u,
-                                             uint32_t* lds_act, uint32_t lds_stride) {
+                                             uint32_t* lds_act, uint32_t lds_stride, const CxArgs* cx = nullptr,
+                                             const unsigned long long* s_types = nullptr) {
 
     uint64_t n0[M], n1[M], tcd[M];
     uint32_t h[M], silo[M], act[M];
@@ -302,6 +340,57 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
             need[j] = true;
         }
     }
+    if constexpr (CX) {
+        // Every directory entry has N0 = 0 and one of the staged types: any other key is a miss.
+        uint32_t want[M];
+        unsigned long long s[M];
+        uint4 q[M][CX_GROUP];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            want[j] = 0;
+            if (need[j]) {
+                const int t = n0[j] == 0 ? cx_type_index(s_types, tcd[j]) : -1;
+                want[j] = t < 0 ? 0u : (CX_LIVE | ((uint32_t)t << 16)) >> 16;
+            }
+            s[j] = cx_home(h[j], cx->cap);
+            if (want[j]) {
+#pragma unroll
+                for (int g = 0; g < (int)CX_GROUP; ++g) q[j][g] = cx->slots[s[j] + g];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+            if (need[j]) silo[j] = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[j])];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            if (!want[j]) continue;
+            bool done = false;
+            for (uint32_t p = 0;;) {
+#pragma unroll
+                for (int g = 0; g < (int)CX_GROUP; ++g) {
+                    if (done) continue;
+                    const uint4 v = q[j][g];
+                    if (v.w == 0) {
+                        done = true;                                      // miss
+                    } else if ((v.w >> 16) == want[j] && ((uint64_t)v.x | ((uint64_t)v.y << 32)) == n1[j]) {
+                        if (v.z == GD_ACT_MULTI) {                        // RandomPlacementDirector.cs:33-53
+                            status[j] = GD_ROUTE_MULTI_ACT;
+                        } else if (tab_silo_valid(tab, slot_silo(v.w))) {
+                            act[j] = v.z;
+                            silo[j] = slot_silo(v.w);                     // Message.cs:629-639
+                            status[j] = GD_ROUTE_OK;
+                        }                                                 // else IsValidSilo (:431) -> MISS
+                        done = true;
+                    }
+                }
+                if (done || ++p > cx->max_rounds) break;
+                s[j] += CX_GROUP;
+                if (s[j] >= cx->cap) s[j] = 0;
+#pragma unroll
+                for (int g = 0; g < (int)CX_GROUP; ++g) q[j][g] = cx->slots[s[j] + g];
+            }
+        }
+    } else {
     // first probe of every message, all in flight together; the ring search (LDS) runs under them.
     // A round reads the whole aligned group of SLOT_GROUP slots (home_slot) and walks it in order.
     constexpr int RG = (int)SLOT_GROUP;
@@ -353,6 +442,7 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
 #pragma unroll
             for (int g = 0; g < 2 * RG; ++g) q[j][g] = qp[g];
         }
+    }
     }
 #pragma unroll
     for (int j = 0; j < M; ++j) {
@@ -417,17 +507,20 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb, uint32_t x
 
 // src_out (optional, the exchange's receive side): message i's sender rank, from the per-sender
 // receive counts rcnt[world] (k_recv_src's job, done here beside the probe's own writes).
-template <int MODE, int M, bool NT, int N1W = 0>
+template <int MODE, int M, bool NT, int N1W = 0, bool CX = false>
 __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                    TableArgs tab, uint32_t* __restrict__ out_silo,
                                                    uint32_t* __restrict__ out_act,
                                                    uint8_t* __restrict__ out_status, uint64_t tcd_u, uint32_t xcd,
                                                    const uint32_t* __restrict__ rcnt = nullptr, uint32_t world = 0,
-                                                   uint32_t* __restrict__ src_out = nullptr) {
+                                                   uint32_t* __restrict__ src_out = nullptr, CxArgs cx = CxArgs{}) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     __shared__ uint32_t s_soff[257];
+    __shared__ unsigned long long s_types[CX ? CX_TYPES : 1];
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
+    if constexpr (CX)
+        for (uint32_t t = threadIdx.x; t < CX_TYPES; t += BLOCK) s_types[t] = cx.types[t];
     if (src_out && threadIdx.x == 0) {
         uint32_t run = 0;
         for (uint32_t q = 0; q < world; ++q) {
@@ -436,13 +529,13 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
         }
         s_soff[world] = run;
     }
-    stage_ring(ring, s_pts, s_own);                    // its barrier publishes s_soff too
+    stage_ring(ring, s_pts, s_own);                    // its barrier publishes s_soff (and s_types) too
     // xcd: each XCD routes a contiguous message range (xcd_tile), so the act it writes is the act the
     // same XCD's histogram and scatter workgroups read next (their XCD tile ranges match)
     const uint32_t blk = xcd_tile(blockIdx.x, gridDim.x, xcd);
-    route_m_core<MODE, M, BLOCK, NT, N1W, true>(keys, n, blk * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own,
-                                               tab, tab.ctr->max_probe, out_silo, out_act, out_status, tcd_u, nullptr,
-                                               0);
+    route_m_core<MODE, M, BLOCK, NT, N1W, true, CX>(keys, n, blk * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own,
+                                                   tab, CX ? 0u : tab.ctr->max_probe, out_silo, out_act, out_status,
+                                                   tcd_u, nullptr, 0, &cx, s_types);
     if (src_out) {
 #pragma unroll
         for (int j = 0; j < M; ++j) {

@@ -1,0 +1,141 @@
+"""The compact probe index (gd_cx.h, GD_CX): a derived copy of the directory table for the route
+probe, rebuilt after every change of the table.  Routes through it must equal routes through the
+directory table itself (GD_CX=0) and the oracle, after every kind of directory change
+(registration, RemoveActivation, AddActivation / multi-activation upserts, silo removal, handoff
+Merge, split-and-move, clear, rehash), with the IsValidSilo filter, and when the table is not
+eligible (an N0 != 0 key, more than 256 TypeCodeData) or the batch holds keys the index cannot
+hold (N0 != 0, unknown types, special categories)."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as o
+
+pytestmark = pytest.mark.gpu
+
+TC = o.grain_type_code(o.PING_GRAIN_CLASS)
+
+
+@pytest.fixture(scope="module")
+def gd():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from orleans_amd import graindispatch as g
+    return g
+
+
+def _pair(gd, mode, cap, **kw):
+    silos = o.bench_silos(8)
+    out = []
+    for cx in ("1", "0"):
+        os.environ["GD_CX"] = cx
+        try:
+            e = gd.GrainDispatch(device=0, table_capacity=cap, **kw)
+        finally:
+            os.environ.pop("GD_CX", None)
+        e.ring_set_silos(mode, [(s.ip, s.port, s.gen) for s in silos])
+        out.append(e)
+    return out, o.ring_spec(silos, mode)
+
+
+def _same(a, b, keys, n_act=None):
+    if n_act is None:
+        ra, rb = a.route(keys), b.route(keys)
+    else:
+        ra, rb = a.route_bucket(keys, n_act), b.route_bucket(keys, n_act)
+    for x, y in zip(ra, rb):
+        np.testing.assert_array_equal(x, y)
+    return ra
+
+
+def _both(engines, fn):
+    return [fn(e) for e in engines]
+
+
+@pytest.mark.parametrize("mode", ["D", "R", "V"])
+def test_cx_matches_directory_through_changes(gd, mode):
+    rng = np.random.default_rng(41)
+    (a, b), spec = _pair(gd, mode, 1 << 14)
+    tc2 = o.grain_type_code("UnitTests.OtherGrain")
+    G = 5000
+    reg = np.concatenate([o.grain_keys(TC, np.arange(G)), o.grain_keys(tc2, np.arange(G // 2))])
+    owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    acts = np.arange(len(reg), dtype=np.uint32) + 3
+
+    def batch(n=20000):
+        ids = rng.integers(0, len(reg) + 300, size=n)
+        k = np.concatenate([reg, o.grain_keys(TC, np.arange(G, G + 300))])[ids]
+        k[::97, 0] = 5                                                   # N0 != 0: never registered
+        k[::89, 2] = np.uint64(o.type_code_data(o.CAT_GRAIN, 0x777))     # a type nobody registered
+        k[::211] = np.array(o.UniqueKey(0, 7, o.type_code_data(o.CAT_SYSTEM_TARGET, 1)).as_tuple(), np.uint64)
+        return k
+
+    _both((a, b), lambda e: e.register(reg[: G], acts[: G], owner[: G]))
+    q = batch()
+    st, silo, act = _same(a, b, q)
+    want = o.route_batch_np(q, spec, o.DirectoryArrays(reg[:G], acts[:G], owner[:G]))
+    np.testing.assert_array_equal(st, want[0])
+    np.testing.assert_array_equal(silo, want[1])
+    np.testing.assert_array_equal(act, want[2])
+    _same(a, b, batch(), n_act=len(reg) + 10)
+    _both((a, b), lambda e: e.register(reg[G:], acts[G:], owner[G:]))        # a second type
+    _same(a, b, batch(), n_act=len(reg) + 10)
+    _both((a, b), lambda e: e.unregister(reg[: G: 3], acts[: G: 3]))
+    _same(a, b, batch())
+    up = rng.choice(len(reg), size=400, replace=False)
+    ua = acts[up].copy()
+    ua[::2] = gd.GD_ACT_MULTI if hasattr(gd, "GD_ACT_MULTI") else 0xFFFFFFFE
+    _both((a, b), lambda e: e.upsert(reg[up], ua, owner[up]))
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.set_valid_silos([s for s in range(8) if s != 3], 8))
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.remove_silos([5]))
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.set_valid_silos([], 0))
+    mk = o.grain_keys(TC, np.arange(G - 100, G + 200))
+    ms = rng.integers(0, 8, size=len(mk)).astype(np.uint32)
+    _both((a, b), lambda e: e.merge(mk, np.arange(len(mk), dtype=np.uint32) + 90000, ms))
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.split([0, 1, 2, 3], move=True))
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.rehash(1 << 15))
+    _same(a, b, batch(), n_act=len(reg) + 10)
+    _both((a, b), lambda e: e.clear())
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.register(reg, acts, owner))
+    _same(a, b, batch(), n_act=len(reg) + 10)
+    a.close()
+    b.close()
+
+
+def test_cx_ineligible_tables_fall_back(gd):
+    """An N0 != 0 grain (a Guid key) or more than 256 types: the route keeps the directory probe,
+    and the index returns once the table is eligible again."""
+    rng = np.random.default_rng(9)
+    (a, b), spec = _pair(gd, "D", 1 << 14)
+    G = 3000
+    reg = o.grain_keys(TC, np.arange(G))
+    owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    guid = np.array([[0x1234, 77, reg[0, 2]]], np.uint64)
+    gown = o.ring_owner_np(spec, o.jenkins_u64x3_np(guid[:, 2], guid[:, 0], guid[:, 1])).astype(np.uint32)
+    _both((a, b), lambda e: e.register(reg, np.arange(G), owner))
+    _both((a, b), lambda e: e.register(guid, [999], gown))
+    q = np.concatenate([reg[rng.integers(0, G, size=5000)], guid])
+    st, silo, act = _same(a, b, q)
+    assert act[-1] == 999 and st[-1] == o.ST_OK
+    _both((a, b), lambda e: e.unregister(guid, [999]))
+    st, _, act = _same(a, b, q)
+    assert st[-1] == o.ST_MISS
+    # 300 types of one grain number each
+    many = np.concatenate([o.grain_keys(o.grain_type_code(f"T.Grain{t}"), np.array([t])) for t in range(300)])
+    mown = o.ring_owner_np(spec, o.jenkins_u64x3_np(many[:, 2], many[:, 0], many[:, 1])).astype(np.uint32)
+    _both((a, b), lambda e: e.register(many, np.arange(300) + 5000, mown))
+    q2 = np.concatenate([q, many])
+    st, _, act = _same(a, b, q2)
+    assert (st[-300:] == o.ST_OK).all() and (act[-300:] == np.arange(300) + 5000).all()
+    _both((a, b), lambda e: e.unregister(many[:100], np.arange(100) + 5000))   # 200 types + Ping: eligible
+    st, _, act = _same(a, b, q2)
+    assert (st[-300:-200] == o.ST_MISS).all() and (st[-200:] == o.ST_OK).all()
+    a.close()
+    b.close()
