@@ -396,7 +396,18 @@ def main():
                 "avg_launch_ms": round(sc["ms_per_step"] / sl, 5), "packed_records": packed,
                 "impl_bytes_per_launch": impl,
                 "frac_impl": round(impl / t_launch / 1e9 / PEAK_HBM_GBS, 4) if t_launch > 0 else None}
-        if dom == "k_route" and args.workload == "cfg2":
+        if dom == "k_route":
+            roofline["bytes_model"] = "SURVEY 8(d): key 24 + one 32-B directory slot + silo/act/status 9 B"
+            if os.environ.get("GD_CX", "1") != "0":
+                # the probe reads the compact index (gd_cx.h): 16-B slots, 4 to a 64-B read; the bytes it
+                # needs per message are key 24 + one 16-B slot + 9 (reported beside the SURVEY model)
+                impl = m_recv * (24 + 16 + 9) / launches
+                t_l = d["ms_per_step"] / launches * 1e-3
+                roofline["probe_index"] = {
+                    "slot_bytes": 16, "group_slots": 4, "impl_bytes_per_launch": impl,
+                    "frac_impl": round(impl / t_l / 1e9 / PEAK_HBM_GBS, 4) if t_l > 0 else None,
+                    "ubench": "profiles/r03_ubench_mirror.txt"}
+        if dom == "k_route" and args.workload == "cfg2" and os.environ.get("GD_CX", "1") == "0":
             # k_route is one random 32-B slot read per message beside the 24-B key stream: its
             # real ceiling is the random-probe rate, measured on MI355X by tools/ubench_random.hip
             # for this shape (16M probes, 64-MiB table, key stream on): 0.3453 ms per launch

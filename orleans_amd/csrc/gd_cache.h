@@ -255,32 +255,29 @@ __global__ void __launch_bounds__(BLOCK) k_route_cached_keyext(const gd_key* __r
         uint32_t w[KX_FAST_WORDS];
         const uint32_t uh = keyext_hash(n0, n1, tcd, s, len, w);
         const uint32_t owner = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uh)];
-        uint32_t silo = owner, act = NONE32, a = NONE32, meta = 0;
-        uint8_t status = GD_ROUTE_MISS;
-        if (silo_flag(cache.local, cache.n_silos, owner)) {            // we own the grain (:806-821)
-            bool found = false;
-            if (kx.slots) {
-                if (len <= KX_FAST_BYTES) found = kx_find<true>(kx, n0, n1, tcd, s, len, uh, w, a, meta);
-                else found = kx_find<false>(kx, n0, n1, tcd, s, len, uh, w, a, meta);
-            }
-            if (found && valid_silo(kx.valid, kx.n_valid, slot_silo(meta))) {   // IsValidSilo filter (:431)
-                act = a;
-                silo = slot_silo(meta);
-                status = GD_ROUTE_OK;
-            }
-        } else {                                                         // cache (:823-836)
-            access = true;
-            uint32_t slot = NONE32;
-            if (cache_find_any(cache, cache.ctr->max_probe, uh, n0, n1, tcd, s, len, w, slot, a, meta)) {
-                hit[i] = 1;
-                cslot[i] = slot;
-                if (silo_flag(cache.valid, cache.n_silos, slot_silo(meta))) {   // IsValidSilo (:848)
-                    act = a;
-                    silo = slot_silo(meta);
-                    status = GD_ROUTE_OK;
-                }
-            }
+        // (select form: the branch form lost the partition hit's activation in this compiler's
+        // codegen -- status OK with act unset; cf. k_handoff_add_status)
+        const bool local = silo_flag(cache.local, cache.n_silos, owner);
+        uint32_t ka = NONE32, km = 0, ca = NONE32, cm = 0, slot = NONE32;
+        bool kfound = false, cfound = false;
+        if (local && kx.slots) {                                        // we own the grain (:806-821)
+            if (len <= KX_FAST_BYTES) kfound = kx_find<true>(kx, n0, n1, tcd, s, len, uh, w, ka, km);
+            else kfound = kx_find<false>(kx, n0, n1, tcd, s, len, uh, w, ka, km);
         }
+        if (!local) {                                                   // cache (:823-836)
+            access = true;
+            cfound = cache_find_any(cache, cache.ctr->max_probe, uh, n0, n1, tcd, s, len, w, slot, ca, cm);
+        }
+        const bool kok = kfound && valid_silo(kx.valid, kx.n_valid, slot_silo(km));   // IsValidSilo (:431)
+        const bool cok = cfound && silo_flag(cache.valid, cache.n_silos, slot_silo(cm));   // (:848)
+        const uint32_t a = local ? ka : ca, m = local ? km : cm;
+        const bool ok = local ? kok : cok;
+        if (cfound) {
+            hit[i] = 1;
+            cslot[i] = slot;
+        }
+        const uint32_t silo = ok ? slot_silo(m) : owner, act = ok ? a : NONE32;
+        const uint8_t status = ok ? (uint8_t)GD_ROUTE_OK : (uint8_t)GD_ROUTE_MISS;
         out_silo[i] = silo;
         out_act[i] = act;
         out_status[i] = status;

@@ -95,6 +95,10 @@ def test_cx_matches_directory_through_changes(gd, mode):
     _both((a, b), lambda e: e.set_valid_silos([], 0))
     mk = o.grain_keys(TC, np.arange(G - 100, G + 200))
     ms = rng.integers(0, 8, size=len(mk)).astype(np.uint32)
+    n_ids = 90000 + len(mk)                                              # Merge compares ActivationIds
+    ids = np.zeros((n_ids, 3), np.uint64)
+    ids[:, 1] = rng.permutation(n_ids).astype(np.uint64)
+    _both((a, b), lambda e: e.activation_ids_set(np.arange(n_ids), ids))
     _both((a, b), lambda e: e.merge(mk, np.arange(len(mk), dtype=np.uint32) + 90000, ms))
     _same(a, b, batch())
     _both((a, b), lambda e: e.split([0, 1, 2, 3], move=True))
