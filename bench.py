@@ -678,11 +678,15 @@ def cpu_baseline_cfg3(args, w3, tcd):
         v, done = _timed(one, args.cpu_seconds / 4, sample)
         res[label] = {"value": round(v, 1), "threads": thr, "messages": done}
         del d
-    best = res["fast_n"]
-    return {"value": best["value"], "unit": "messages/s", "cores": cores, "kind": "port",
+    # the faster mode is the baseline: at n_act = 100M the fast mode's parallel counting sort pays
+    # O(n_act) per thread per batch, which a 2M-message sample does not amortise
+    label = max(res, key=lambda k: res[k]["value"])
+    best = res[label]
+    return {"value": best["value"], "unit": "messages/s", "cores": best["threads"], "kind": "port",
             "sample": f"{best['messages']} messages (the first {sample} of the GPU's Zipf(1.1) batch, repeated; "
                       f"{len(grains)} distinct grains registered on the CPU of the 100M) through the C restatement "
-                      f"in fast mode on {cores} threads", "modes": res}
+                      f"in {'faithful' if label.startswith('faithful') else 'fast'} mode on {best['threads']} "
+                      f"thread(s), the faster of the two modes", "modes": res, "usable_cores": cores}
 
 
 # ---- BASELINE cfg 4: Chirper-style follower fan-out cascade -------------------------------------

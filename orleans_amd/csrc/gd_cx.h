@@ -58,32 +58,40 @@ __global__ void __launch_bounds__(BLOCK) k_cx_types(const Slot* __restrict__ slo
 __global__ void __launch_bounds__(BLOCK) k_cx_build(const Slot* __restrict__ slots, unsigned long long cap,
                                                     const unsigned long long* __restrict__ types, uint4* cx,
                                                     unsigned long long cx_cap, CxCounters* ctr) {
-    if (ctr->flag) return;                             // not eligible: nothing to build
+    if (ctr->flag) return;                             // not eligible (uniform): nothing to build
     const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
-    if (j >= cap) return;
-    const uint4* q = reinterpret_cast<const uint4*>(slots + j);
-    const uint4 a = q[0], b = q[1];
-    if (slot_state(b.w) != SLOT_LIVE) return;
-    const uint64_t n1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
-    const uint64_t tcd = (uint64_t)b.x | ((uint64_t)b.y << 32);
-    uint32_t t = cx_type_home(tcd);
-    while (types[t] != tcd) t = (t + 1) & (CX_TYPES - 1);     // present: k_cx_types put it there
-    const uint32_t meta = CX_LIVE | (t << 16) | slot_silo(b.w);
-    const unsigned long long home = cx_home(uniform_hash(0, n1, tcd), cx_cap);
-    unsigned long long s = home;
-    for (unsigned long long d = 0; d < cx_cap; ++d) {
-        uint32_t* mp = &cx[s].w;
-        if (atomicCAS(mp, 0u, meta) == 0u) {
-            cx[s].x = (uint32_t)n1;
-            cx[s].y = (uint32_t)(n1 >> 32);
-            cx[s].z = b.z;
-            const unsigned long long dist = s >= home ? s - home : s + cx_cap - home;
-            atomicMax(&ctr->max_rounds, (uint32_t)(dist / CX_GROUP));
-            return;
+    uint32_t rounds = 0;
+    bool placed = false, live = false;
+    if (j < cap) {
+        const uint4* q = reinterpret_cast<const uint4*>(slots + j);
+        const uint4 a = q[0], b = q[1];
+        live = slot_state(b.w) == SLOT_LIVE;
+        if (live) {
+            const uint64_t n1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
+            const uint64_t tcd = (uint64_t)b.x | ((uint64_t)b.y << 32);
+            uint32_t t = cx_type_home(tcd);
+            while (types[t] != tcd) t = (t + 1) & (CX_TYPES - 1);     // present: k_cx_types put it there
+            const uint32_t meta = CX_LIVE | (t << 16) | slot_silo(b.w);
+            const unsigned long long home = cx_home(uniform_hash(0, n1, tcd), cx_cap);
+            unsigned long long s = home;
+            for (unsigned long long d = 0; d < cx_cap; ++d) {
+                if (atomicCAS(&cx[s].w, 0u, meta) == 0u) {
+                    cx[s].x = (uint32_t)n1;
+                    cx[s].y = (uint32_t)(n1 >> 32);
+                    cx[s].z = b.z;
+                    rounds = (uint32_t)((s >= home ? s - home : s + cx_cap - home) / CX_GROUP);
+                    placed = true;
+                    break;
+                }
+                s = s + 1 == cx_cap ? 0 : s + 1;
+            }
+            if (!placed) atomicOr(&ctr->full, 1u);
         }
-        s = s + 1 == cx_cap ? 0 : s + 1;
     }
-    atomicOr(&ctr->full, 1u);
+    // one atomicMax per wave on the shared counter (one per entry serialises a million of them);
+    // every lane of the wave takes part in the reduction
+    for (int off = WAVE / 2; off > 0; off >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor(rounds, off, WAVE));
+    if (lane_id() == 0 && rounds) atomicMax(&ctr->max_rounds, rounds);
 }
 
 }  // namespace gd

@@ -12,7 +12,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 # --latency-batches 0: no cfg 5 / cfg 1 secondary lines (their small launches would mix into the
 # cfg 2 kernels' statistics and counters)
-BENCH=(python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --profile-steps 0 --latency-batches 0 "$@")
+BENCH=(python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-secondary --profile-steps 0 --latency-batches 0 "$@")
 cd /tmp || exit 1
 echo "[profile $TAG] kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- "${BENCH[@]}" \
