@@ -172,6 +172,7 @@ struct gd_handle {
     bool route_xcd = true;      // route workgroups over XCD-contiguous message ranges (GD_ROUTE_XCD)
     // compact probe index (gd_cx.h): derived from the table, rebuilt after any change of it (GD_CX=0: off)
     bool cx_on = true;
+    uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
     uint64_t tab_gen = 0;       // bumped by every launch that takes the table as a writable Slot*
     bool cx_built = false, cx_ok = false;
     const Slot* cx_slots_at = nullptr;
@@ -393,21 +394,22 @@ int cx_ensure(gd_handle* h, bool* ok) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;   // a captured graph keeps the directory probe
     HIP_TRY(h, hipStreamIsCapturing(h->stream, &cs));
     if (cs != hipStreamCaptureStatusNone) return GD_OK;
-    if (h->cx_built && h->cx_slots_at == h->slots && h->cx_cap_at == h->capacity && h->cx_gen_at == h->tab_gen) {
+    if (h->cx_built && h->cx_slots_at == h->slots && h->cx_cap_at == h->capacity * h->cx_scale &&
+        h->cx_gen_at == h->tab_gen) {
         *ok = h->cx_ok;
         return GD_OK;
     }
-    const unsigned long long cap = h->capacity;
+    const unsigned long long cap = h->capacity * h->cx_scale;
     GD_TRY(ensure(h, h->cxi_tab, cap * 16));
     GD_TRY(ensure(h, h->cxi_types, CX_TYPES * 8));
     GD_TRY(ensure(h, h->cxi_ctr, sizeof(CxCounters)));
     HIP_TRY(h, hipMemsetAsync(h->cxi_tab.p, 0, cap * 16, h->stream));
     HIP_TRY(h, hipMemsetAsync(h->cxi_types.p, 0xFF, CX_TYPES * 8, h->stream));
     HIP_TRY(h, hipMemsetAsync(h->cxi_ctr.p, 0, sizeof(CxCounters), h->stream));
-    const dim3 g(blocks_for(cap, BLOCK)), b(BLOCK);
-    GD_TRY(launch(h, "k_cx_types", g, b, 0, k_cx_types, (const Slot*)h->slots, cap,
+    const dim3 g(blocks_for(h->capacity, BLOCK)), b(BLOCK);
+    GD_TRY(launch(h, "k_cx_types", g, b, 0, k_cx_types, (const Slot*)h->slots, (unsigned long long)h->capacity,
                   (unsigned long long*)h->cxi_types.p, (CxCounters*)h->cxi_ctr.p));
-    GD_TRY(launch(h, "k_cx_build", g, b, 0, k_cx_build, (const Slot*)h->slots, cap,
+    GD_TRY(launch(h, "k_cx_build", g, b, 0, k_cx_build, (const Slot*)h->slots, (unsigned long long)h->capacity,
                   (const unsigned long long*)h->cxi_types.p, (uint4*)h->cxi_tab.p, cap, (CxCounters*)h->cxi_ctr.p));
     CxCounters c{};
     HIP_TRY(h, hipMemcpyAsync(&c, h->cxi_ctr.p, sizeof c, hipMemcpyDeviceToHost, h->stream));
@@ -416,14 +418,15 @@ int cx_ensure(gd_handle* h, bool* ok) {
     h->cx_ok = c.flag == 0 && c.full == 0;
     h->cx_rounds = c.max_rounds;
     h->cx_slots_at = h->slots;
-    h->cx_cap_at = h->capacity;
+    h->cx_cap_at = cap;
     h->cx_gen_at = h->tab_gen;
     *ok = h->cx_ok;
     return GD_OK;
 }
 
 CxArgs cx_args(gd_handle* h) {
-    return CxArgs{(const uint4*)h->cxi_tab.p, h->capacity, (const unsigned long long*)h->cxi_types.p, h->cx_rounds};
+    return CxArgs{(const uint4*)h->cxi_tab.p, h->capacity * h->cx_scale, (const unsigned long long*)h->cxi_types.p,
+                  h->cx_rounds};
 }
 
 // ---- route -------------------------------------------------------------------
@@ -1126,6 +1129,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_ROUTE_NT")) h->route_nt = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_ROUTE_XCD")) h->route_xcd = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_CX")) h->cx_on = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_CX_SCALE")) h->cx_scale = std::atoi(v) == 2 ? 2u : 1u;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
     if (const char* v = std::getenv("GD_RADIX_RANK")) h->radix_rank_atomic = std::atoi(v) ? 1u : 0u;
@@ -2278,23 +2282,37 @@ int fan_args_ok(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint
     return GD_OK;
 }
 
+template <int MODE, bool CX>
+int fan_route_launch_cx(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier,
+                        uint32_t nf, uint32_t total, uint64_t tcd, uint32_t* target, uint32_t* sender, uint32_t* silo,
+                        uint32_t* act, uint8_t* status) {
+    const dim3 g(blocks_for(total, FAN_TILE)), b(BLOCK);
+    const uint32_t* ends = (const uint32_t*)h->fan[0].p;
+    const CxArgs cx = CX ? cx_args(h) : CxArgs{};
+    switch (h->fan_ilp) {
+        case 1:
+            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 1, CX>, row_off, dst, frontier, nf,
+                          ends, total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx);
+        case 4:
+            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 4, CX>, row_off, dst, frontier, nf,
+                          ends, total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx);
+        default:
+            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2, CX>, row_off, dst, frontier, nf,
+                          ends, total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx);
+    }
+}
+
 template <int MODE>
 int fan_route_launch(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier, uint32_t nf,
                      uint32_t total, uint64_t tcd, uint32_t* target, uint32_t* sender, uint32_t* silo, uint32_t* act,
                      uint8_t* status) {
-    const dim3 g(blocks_for(total, FAN_TILE)), b(BLOCK);
-    const uint32_t* ends = (const uint32_t*)h->fan[0].p;
-    switch (h->fan_ilp) {
-        case 1:
-            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 1>, row_off, dst, frontier, nf, ends,
-                          total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status);
-        case 4:
-            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 4>, row_off, dst, frontier, nf, ends,
-                          total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status);
-        default:
-            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2>, row_off, dst, frontier, nf, ends,
-                          total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status);
-    }
+    bool cx = false;
+    GD_TRY(cx_ensure(h, &cx));
+    if (cx)
+        return fan_route_launch_cx<MODE, true>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo, act,
+                                               status);
+    return fan_route_launch_cx<MODE, false>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo, act,
+                                            status);
 }
 
 int fan_route(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier, uint32_t nf,
@@ -2314,23 +2332,27 @@ int fan_route(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const 
     }
 }
 
+template <int MODE>
+int route_nodes_mode(gd_handle* h, const uint32_t* nodes, uint32_t n, uint64_t tcd, uint32_t* silo, uint32_t* act,
+                     uint8_t* status, bool cx) {
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    if (cx)
+        return launch(h, "k_route_nodes", g, b, ring_lds(h), k_route_nodes<MODE, true>, nodes, n, tcd, ring_args(h),
+                      table_args(h), silo, act, status, cx_args(h));
+    return launch(h, "k_route_nodes", g, b, ring_lds(h), k_route_nodes<MODE, false>, nodes, n, tcd, ring_args(h),
+                  table_args(h), silo, act, status, CxArgs{});
+}
+
 int route_nodes(gd_handle* h, const uint32_t* nodes, uint32_t n, uint64_t tcd, uint32_t* silo, uint32_t* act,
                 uint8_t* status) {
     GD_TRY(check_ring(h));
     h->routed += n;
-    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
-    const RingArgs r = ring_args(h);
-    const TableArgs t = table_args(h);
+    bool cx = false;
+    GD_TRY(cx_ensure(h, &cx));
     switch (h->ring_mode) {
-        case GD_RING_DIRECTORY:
-            return launch(h, "k_route_nodes", g, b, ring_lds(h), k_route_nodes<GD_RING_DIRECTORY>, nodes, n, tcd, r, t,
-                          silo, act, status);
-        case GD_RING_CONSISTENT:
-            return launch(h, "k_route_nodes", g, b, ring_lds(h), k_route_nodes<GD_RING_CONSISTENT>, nodes, n, tcd, r, t,
-                          silo, act, status);
-        default:
-            return launch(h, "k_route_nodes", g, b, ring_lds(h), k_route_nodes<GD_RING_VIRTUAL_BUCKETS>, nodes, n, tcd,
-                          r, t, silo, act, status);
+        case GD_RING_DIRECTORY: return route_nodes_mode<GD_RING_DIRECTORY>(h, nodes, n, tcd, silo, act, status, cx);
+        case GD_RING_CONSISTENT: return route_nodes_mode<GD_RING_CONSISTENT>(h, nodes, n, tcd, silo, act, status, cx);
+        default: return route_nodes_mode<GD_RING_VIRTUAL_BUCKETS>(h, nodes, n, tcd, silo, act, status, cx);
     }
 }
 

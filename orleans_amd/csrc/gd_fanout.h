@@ -187,21 +187,74 @@ __device__ __forceinline__ uint8_t route_node(uint32_t node, uint64_t tcd, const
     return GD_ROUTE_MISS;                          // Dispatcher.cs:742 slow path
 }
 
+// The compact probe index's walk (gd_kernels.h CxArgs) from a group already read: the status of
+// GrainId(tcd, n1) given its type's `want` (0x100 | type index; 0: the type holds no entry).
+__device__ __forceinline__ uint8_t cx_walk_node(const CxArgs& cx, const TableArgs& tab, uint32_t want, uint64_t n1,
+                                                unsigned long long s, uint4 (&q)[CX_GROUP], uint32_t& silo,
+                                                uint32_t& act) {
+    uint8_t st = GD_ROUTE_MISS;
+    bool done = want == 0;
+    for (uint32_t p = 0; !done;) {
+#pragma unroll
+        for (int g = 0; g < (int)CX_GROUP; ++g) {
+            if (done) continue;
+            const uint4 v = q[g];
+            if (v.w == 0) {
+                done = true;
+            } else if ((v.w >> 16) == want && ((uint64_t)v.x | ((uint64_t)v.y << 32)) == n1) {
+                const bool ok = v.z != GD_ACT_MULTI && tab_silo_valid(tab, slot_silo(v.w));
+                st = v.z == GD_ACT_MULTI ? (uint8_t)GD_ROUTE_MULTI_ACT : (ok ? (uint8_t)GD_ROUTE_OK : st);
+                act = ok ? v.z : act;
+                silo = ok ? slot_silo(v.w) : silo;
+                done = true;
+            }
+        }
+        if (done || ++p > cx.max_rounds) break;
+        s += CX_GROUP;
+        if (s >= cx.cap) s = 0;
+#pragma unroll
+        for (int g = 0; g < (int)CX_GROUP; ++g) q[g] = cx.slots[s + g];
+    }
+    return st;
+}
+
+__device__ __forceinline__ uint32_t cx_want(const CxArgs& cx, uint64_t tcd) {
+    const int t = cx_type_index(cx.types, tcd);
+    return t < 0 ? 0u : (0x100u | (uint32_t)t);
+}
+
 // Route a batch of node ids (GrainId(typeCode, node), the owner side of the sharded fan-out).
-template <int MODE>
+// CX: through the compact probe index.
+template <int MODE, bool CX = false>
 __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restrict__ nodes, uint32_t n, uint64_t tcd,
                                                        RingArgs ring, TableArgs tab, uint32_t* __restrict__ out_silo,
                                                        uint32_t* __restrict__ out_act,
-                                                       uint8_t* __restrict__ out_status) {
+                                                       uint8_t* __restrict__ out_status, CxArgs cx = CxArgs{}) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
     stage_ring(ring, s_pts, s_own);
-    const uint32_t max_probe = tab.ctr->max_probe;
+    const uint32_t max_probe = CX ? 0u : tab.ctr->max_probe;
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     uint32_t silo, act;
-    const uint8_t st = route_node<MODE>(nodes[i], tcd, s_pts, s_own, ring, tab, max_probe, silo, act);
+    uint8_t st;
+    if constexpr (CX) {
+        const uint32_t want = cx_want(cx, tcd);
+        const uint32_t node = nodes[i];
+        const uint32_t h = uniform_hash(0, node, tcd);
+        const unsigned long long s0 = cx_home(h, cx.cap);
+        uint4 q[CX_GROUP];
+        if (want) {
+#pragma unroll
+            for (int g = 0; g < (int)CX_GROUP; ++g) q[g] = cx.slots[s0 + g];
+        }
+        silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h)];
+        act = NONE32;
+        st = cx_walk_node(cx, tab, want, node, s0, q, silo, act);
+    } else {
+        st = route_node<MODE>(nodes[i], tcd, s_pts, s_own, ring, tab, max_probe, silo, act);
+    }
     out_silo[i] = silo;
     out_act[i] = act;
     out_status[i] = st;
@@ -210,7 +263,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restric
 // Fused expansion + route.  out_target may be null.  ILP items of a thread at a time: their
 // follower-list reads, then their first directory probes, are in flight together (one dependent
 // chain per item otherwise).
-template <int MODE, int ILP>
+template <int MODE, int ILP, bool CX = false>
 __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict__ row_off,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint32_t* __restrict__ frontier, uint32_t n_front,
@@ -219,7 +272,7 @@ __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ out_target,
                                                      uint32_t* __restrict__ out_sender,
                                                      uint32_t* __restrict__ out_silo, uint32_t* __restrict__ out_act,
-                                                     uint8_t* __restrict__ out_status) {
+                                                     uint8_t* __restrict__ out_status, CxArgs cx = CxArgs{}) {
     static_assert(FAN_IT % ILP == 0, "whole rounds");
     __shared__ FanStage s;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
@@ -244,6 +297,33 @@ __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict_
         }
 #pragma unroll
         for (int q = 0; q < ILP; ++q) target[q] = live[q] ? dst[j[q]] : 0u;
+        if constexpr (CX) {                                   // the compact probe index (gd_kernels.h)
+            const uint32_t want = cx_want(cx, tcd);
+            unsigned long long sc[ILP];
+            uint4 qc[ILP][CX_GROUP];
+#pragma unroll
+            for (int q = 0; q < ILP; ++q) {
+                h[q] = uniform_hash(0, target[q], tcd);
+                sc[q] = cx_home(h[q], cx.cap);
+                if (live[q] && want) {
+#pragma unroll
+                    for (int g = 0; g < (int)CX_GROUP; ++g) qc[q][g] = cx.slots[sc[q] + g];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < ILP; ++q) {
+                if (!live[q]) continue;
+                const uint32_t p = p0 + (it0 + q) * BLOCK + threadIdx.x;
+                uint32_t silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[q])], act = NONE32;
+                const uint8_t st = cx_walk_node(cx, tab, want, target[q], sc[q], qc[q], silo, act);
+                if (out_target) out_target[p] = target[q];
+                out_sender[p] = sender[q];
+                out_silo[p] = silo;
+                out_act[p] = act;
+                out_status[p] = st;
+            }
+            continue;
+        }
         unsigned long long sl[ILP];
         uint4 qa[ILP], qb[ILP];
 #pragma unroll
