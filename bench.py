@@ -395,7 +395,10 @@ def main():
                 "launches_per_step": sl, "alg_bytes_per_launch": alg, "bytes_model": "SURVEY 8(d): 16 B/record/pass",
                 "avg_launch_ms": round(sc["ms_per_step"] / sl, 5), "packed_records": packed,
                 "impl_bytes_per_launch": impl,
-                "frac_impl": round(impl / t_launch / 1e9 / PEAK_HBM_GBS, 4) if t_launch > 0 else None}
+                "frac_impl": round(impl / t_launch / 1e9 / PEAK_HBM_GBS, 4) if t_launch > 0 else None,
+                # on the HBM bytes the PMC counters saw per launch (profiles/pmc_k_radix_scatter.json)
+                "frac_pmc": round(sc_traffic / t_launch / 1e9 / PEAK_HBM_GBS, 4) if sc_traffic and t_launch > 0
+                else None}
         if dom == "k_route":
             roofline["bytes_model"] = "SURVEY 8(d): key 24 + one 32-B directory slot + silo/act/status 9 B"
             if os.environ.get("GD_CX", "1") != "0":
