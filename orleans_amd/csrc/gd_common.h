@@ -117,9 +117,12 @@ GD_HD uint32_t fmix32(uint32_t h) {
 // atom): linear probing from the group start, so the lookup (route_m_core) reads a whole group per
 // round trip.  At load 0.5 a 64-lane wave waits on the longest chain of its lanes: ~7.7 dependent
 // rounds with one slot a round, ~4.1 with two (tools/sim_probe_rounds.py).  Measured on cfg 2:
-// k_route 0.385 (1 slot) / 0.366 (2) / 0.382 (4) / 0.675 ms (8).
+// k_route 0.385 (1 slot) / 0.366 (2) / 0.382 (4) / 0.675 ms (8).  But on cfg 3 (Zipf(1.1)
+// over 100M grains) the 64-B reads double the hot set's cache traffic: k_route 1.24 (1 slot) vs
+// 2.25 ms (2) (profiles/r03_cfg3_group_ab.txt).  Uniform batches take the compact probe index
+// (gd_cx.h) instead, so the directory keeps one slot a round.
 #ifndef GD_SLOT_GROUP
-#define GD_SLOT_GROUP 2
+#define GD_SLOT_GROUP 1
 #endif
 constexpr uint32_t SLOT_GROUP = GD_SLOT_GROUP;
 static_assert((SLOT_GROUP & (SLOT_GROUP - 1)) == 0 && SLOT_GROUP <= 1024, "slot group: a power of two <= 1024");

@@ -171,8 +171,16 @@ struct gd_handle {
     bool route_nt = false;
     bool route_xcd = true;      // route workgroups over XCD-contiguous message ranges (GD_ROUTE_XCD)
     // compact probe index (gd_cx.h): derived from the table, rebuilt after any change of it (GD_CX=0: off)
-    bool cx_on = true;
+    int cx_mode = 1;            // 0 off, 1 measured per launch kind (default), 2 always (GD_CX)
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
+    struct CxTune {             // per launch kind: index vs directory probe, timed on live launches
+        int pick = -1;          // -1 measuring, 0 index, 1 directory
+        int round = 0;
+        float best[2] = {1e30f, 1e30f};
+        hipEvent_t a[2] = {nullptr, nullptr}, b[2] = {nullptr, nullptr};
+        bool pending[2] = {false, false};
+        uint64_t n[2] = {0, 0};
+    } cx_tune[4];
     uint64_t tab_gen = 0;       // bumped by every launch that takes the table as a writable Slot*
     bool cx_built = false, cx_ok = false;
     const Slot* cx_slots_at = nullptr;
@@ -390,7 +398,7 @@ unsigned long long pow2_at_least(unsigned long long x) {
 // the last build; false when the table is not eligible (an N0 != 0 key, too many types) or GD_CX=0.
 int cx_ensure(gd_handle* h, bool* ok) {
     *ok = false;
-    if (!h->cx_on || !h->slots || h->capacity < CX_GROUP) return GD_OK;
+    if (!h->cx_mode || !h->slots || h->capacity < CX_GROUP) return GD_OK;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;   // a captured graph keeps the directory probe
     HIP_TRY(h, hipStreamIsCapturing(h->stream, &cs));
     if (cs != hipStreamCaptureStatusNone) return GD_OK;
@@ -416,6 +424,14 @@ int cx_ensure(gd_handle* h, bool* ok) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     h->cx_built = true;
     h->cx_ok = c.flag == 0 && c.full == 0;
+    for (auto& t : h->cx_tune) {                    // a new table: measure both probes again
+        for (int v = 0; v < 2; ++v)
+            if (t.pending[v]) (void)hipEventSynchronize(t.b[v]);
+        t.pick = -1;
+        t.round = 0;
+        t.best[0] = t.best[1] = 1e30f;
+        t.pending[0] = t.pending[1] = false;
+    }
     h->cx_rounds = c.max_rounds;
     h->cx_slots_at = h->slots;
     h->cx_cap_at = cap;
@@ -423,6 +439,56 @@ int cx_ensure(gd_handle* h, bool* ok) {
     *ok = h->cx_ok;
     return GD_OK;
 }
+
+// Index or directory probe for a launch of `kind` (0 keys, 1 N1s, 2 fan-out, 3 node ids) when the index
+// is available: GD_CX=2 always the index; GD_CX=1 times the two on the first four eligible launches of
+// the kind (index, directory, index, directory; HIP events, read back without a stream sync at the
+// next choice) and keeps the faster per message.  Both give the same results; which is faster
+// depends on the key distribution (a Zipf-hot set favours the directory's 32-B reads, a uniform one the
+// index's smaller table).  *meas: the tune slot this launch is timed into, or -1.
+bool cx_choose(gd_handle* h, int kind, int* meas) {
+    *meas = -1;
+    if (h->cx_mode == 2) return true;
+    auto& t = h->cx_tune[kind];
+    for (int v = 0; v < 2; ++v) {
+        if (!t.pending[v]) continue;
+        if (hipEventQuery(t.b[v]) != hipSuccess && t.pick < 0 && t.round >= 4) (void)hipEventSynchronize(t.b[v]);
+        if (hipEventQuery(t.b[v]) == hipSuccess) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, t.a[v], t.b[v]) == hipSuccess && t.n[v])
+                t.best[v] = std::min(t.best[v], ms / (float)t.n[v]);
+            t.pending[v] = false;
+        }
+    }
+    if (t.pick < 0 && t.round >= 4 && !t.pending[0] && !t.pending[1])
+        t.pick = t.best[0] <= t.best[1] ? 0 : 1;
+    if (t.pick >= 0) return t.pick == 0;
+    const int v = t.round & 1;
+    if (t.round < 4 && !t.pending[v]) {
+        if (!t.a[v]) (void)hipEventCreate(&t.a[v]);
+        if (!t.b[v]) (void)hipEventCreate(&t.b[v]);
+        *meas = kind * 2 + v;
+        ++t.round;
+    }
+    return v == 0;
+}
+
+// Brackets a launch chosen by cx_choose with the tune slot's events.
+struct CxMeasure {
+    gd_handle* h;
+    int slot;
+    uint64_t n;
+    CxMeasure(gd_handle* hh, int sl, uint64_t nn) : h(hh), slot(sl), n(nn) {
+        if (slot >= 0) (void)hipEventRecord(h->cx_tune[slot / 2].a[slot & 1], h->stream);
+    }
+    ~CxMeasure() {
+        if (slot < 0) return;
+        auto& t = h->cx_tune[slot / 2];
+        (void)hipEventRecord(t.b[slot & 1], h->stream);
+        t.n[slot & 1] = n;
+        t.pending[slot & 1] = true;
+    }
+};
 
 CxArgs cx_args(gd_handle* h) {
     return CxArgs{(const uint4*)h->cxi_tab.p, h->capacity * h->cx_scale, (const unsigned long long*)h->cxi_types.p,
@@ -434,6 +500,9 @@ template <int MODE, int M, bool NT>
 int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
+    int meas = -1;
+    if (cx) cx = cx_choose(h, 0, &meas);
+    CxMeasure m(h, meas, n);
     if (cx)
         return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h),
                       k_route_m<MODE, M, NT, 0, true>, keys, n, ring_args(h), table_args(h), silo, act, status, 0ull,
@@ -452,6 +521,9 @@ int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uin
     const uint32_t xcd = h->route_xcd ? 1u : 0u;
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
+    int meas = -1;
+    if (cx) cx = cx_choose(h, 1, &meas);
+    CxMeasure m(h, meas, n);
     if (cx && n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4, true>, k, n, ring_args(h),
                       table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h));
@@ -1128,7 +1200,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_ROUTE_M")) h->route_m = std::atoi(v);
     if (const char* v = std::getenv("GD_ROUTE_NT")) h->route_nt = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_ROUTE_XCD")) h->route_xcd = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_CX")) h->cx_on = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_CX")) h->cx_mode = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("GD_CX_SCALE")) h->cx_scale = std::atoi(v) == 2 ? 2u : 1u;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
@@ -1216,6 +1288,11 @@ void gd_destroy(gd_handle* h) {
     free_buf(h->cxi_tab);
     free_buf(h->cxi_types);
     free_buf(h->cxi_ctr);
+    for (auto& t : h->cx_tune)
+        for (int v = 0; v < 2; ++v) {
+            if (t.a[v]) (void)hipEventDestroy(t.a[v]);
+            if (t.b[v]) (void)hipEventDestroy(t.b[v]);
+        }
     if (h->cctr) (void)hipFree(h->cctr);
     if (h->slots) (void)hipFree(h->slots);
     if (h->ctr) (void)hipFree(h->ctr);
@@ -2308,6 +2385,9 @@ int fan_route_launch(gd_handle* h, const uint32_t* row_off, const uint32_t* dst,
                      uint8_t* status) {
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
+    int meas = -1;
+    if (cx) cx = cx_choose(h, 2, &meas);
+    CxMeasure m(h, meas, total);
     if (cx)
         return fan_route_launch_cx<MODE, true>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo, act,
                                                status);
@@ -2349,6 +2429,9 @@ int route_nodes(gd_handle* h, const uint32_t* nodes, uint32_t n, uint64_t tcd, u
     h->routed += n;
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
+    int meas = -1;
+    if (cx) cx = cx_choose(h, 3, &meas);
+    CxMeasure m(h, meas, n);
     switch (h->ring_mode) {
         case GD_RING_DIRECTORY: return route_nodes_mode<GD_RING_DIRECTORY>(h, nodes, n, tcd, silo, act, status, cx);
         case GD_RING_CONSISTENT: return route_nodes_mode<GD_RING_CONSISTENT>(h, nodes, n, tcd, silo, act, status, cx);
