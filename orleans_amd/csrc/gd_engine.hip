@@ -10,6 +10,7 @@
 #include <cstring>
 #include <mutex>
 #include <queue>
+#include <map>
 #include <unordered_map>
 #include <string>
 #include <vector>
@@ -173,14 +174,15 @@ struct gd_handle {
     // compact probe index (gd_cx.h): derived from the table, rebuilt after any change of it (GD_CX=0: off)
     int cx_mode = 1;            // 0 off, 1 measured per launch kind (default), 2 always (GD_CX)
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
-    struct CxTune {             // per launch kind: index vs directory probe, timed on live launches
+    struct CxTune {             // per launch kind and size class: index vs directory probe, timed live
         int pick = -1;          // -1 measuring, 0 index, 1 directory
         int round = 0;
         float best[2] = {1e30f, 1e30f};
         hipEvent_t a[2] = {nullptr, nullptr}, b[2] = {nullptr, nullptr};
         bool pending[2] = {false, false};
         uint64_t n[2] = {0, 0};
-    } cx_tune[4];
+    };
+    std::map<int, CxTune> cx_tune;   // key: kind * 64 + size class (bit length of n)
     uint64_t tab_gen = 0;       // bumped by every launch that takes the table as a writable Slot*
     bool cx_built = false, cx_ok = false;
     const Slot* cx_slots_at = nullptr;
@@ -424,7 +426,8 @@ int cx_ensure(gd_handle* h, bool* ok) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     h->cx_built = true;
     h->cx_ok = c.flag == 0 && c.full == 0;
-    for (auto& t : h->cx_tune) {                    // a new table: measure both probes again
+    for (auto& kt : h->cx_tune) {                   // a new table: measure both probes again
+        auto& t = kt.second;
         for (int v = 0; v < 2; ++v)
             if (t.pending[v]) (void)hipEventSynchronize(t.b[v]);
         t.pick = -1;
@@ -440,16 +443,21 @@ int cx_ensure(gd_handle* h, bool* ok) {
     return GD_OK;
 }
 
-// Index or directory probe for a launch of `kind` (0 keys, 1 N1s, 2 fan-out, 3 node ids) when the index
-// is available: GD_CX=2 always the index; GD_CX=1 times the two on the first four eligible launches of
-// the kind (index, directory, index, directory; HIP events, read back without a stream sync at the
-// next choice) and keeps the faster per message.  Both give the same results; which is faster
-// depends on the key distribution (a Zipf-hot set favours the directory's 32-B reads, a uniform one the
-// index's smaller table).  *meas: the tune slot this launch is timed into, or -1.
-bool cx_choose(gd_handle* h, int kind, int* meas) {
+// Index or directory probe for a launch of `kind` (0 keys, 1 N1s, 2 fan-out, 3 node ids) over n
+// messages when the index is available: GD_CX=2 always the index; GD_CX=1 times the two on the first
+// four eligible launches of the kind and size class (bit length of n: the fan-out's hops differ 10x in
+// size, and per-message cost with them) -- index, directory, index, directory, between HIP events read
+// back without a stream sync at the next choice -- and keeps the faster per message.  Both give the
+// same results; which is faster depends on the key distribution (a Zipf-hot set favours the
+// directory's 32-B reads, a uniform one the index's smaller table).  *meas: the tune entry
+// this launch is timed into (key), or -1.
+bool cx_choose(gd_handle* h, int kind, uint64_t n, int* meas) {
     *meas = -1;
     if (h->cx_mode == 2) return true;
-    auto& t = h->cx_tune[kind];
+    int cls = 0;
+    while (cls < 63 && (n >> cls) > 1) ++cls;
+    const int key = kind * 64 + cls;
+    auto& t = h->cx_tune[key];
     for (int v = 0; v < 2; ++v) {
         if (!t.pending[v]) continue;
         if (hipEventQuery(t.b[v]) != hipSuccess && t.pick < 0 && t.round >= 4) (void)hipEventSynchronize(t.b[v]);
@@ -467,7 +475,7 @@ bool cx_choose(gd_handle* h, int kind, int* meas) {
     if (t.round < 4 && !t.pending[v]) {
         if (!t.a[v]) (void)hipEventCreate(&t.a[v]);
         if (!t.b[v]) (void)hipEventCreate(&t.b[v]);
-        *meas = kind * 2 + v;
+        *meas = key * 2 + v;
         ++t.round;
     }
     return v == 0;
@@ -501,7 +509,7 @@ int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, u
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
     int meas = -1;
-    if (cx) cx = cx_choose(h, 0, &meas);
+    if (cx) cx = cx_choose(h, 0, n, &meas);
     CxMeasure m(h, meas, n);
     if (cx)
         return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h),
@@ -522,7 +530,7 @@ int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uin
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
     int meas = -1;
-    if (cx) cx = cx_choose(h, 1, &meas);
+    if (cx) cx = cx_choose(h, 1, n, &meas);
     CxMeasure m(h, meas, n);
     if (cx && n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4, true>, k, n, ring_args(h),
@@ -1288,8 +1296,9 @@ void gd_destroy(gd_handle* h) {
     free_buf(h->cxi_tab);
     free_buf(h->cxi_types);
     free_buf(h->cxi_ctr);
-    for (auto& t : h->cx_tune)
+    for (auto& kt : h->cx_tune)
         for (int v = 0; v < 2; ++v) {
+            auto& t = kt.second;
             if (t.a[v]) (void)hipEventDestroy(t.a[v]);
             if (t.b[v]) (void)hipEventDestroy(t.b[v]);
         }
@@ -2386,7 +2395,7 @@ int fan_route_launch(gd_handle* h, const uint32_t* row_off, const uint32_t* dst,
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
     int meas = -1;
-    if (cx) cx = cx_choose(h, 2, &meas);
+    if (cx) cx = cx_choose(h, 2, total, &meas);
     CxMeasure m(h, meas, total);
     if (cx)
         return fan_route_launch_cx<MODE, true>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo, act,
@@ -2430,7 +2439,7 @@ int route_nodes(gd_handle* h, const uint32_t* nodes, uint32_t n, uint64_t tcd, u
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
     int meas = -1;
-    if (cx) cx = cx_choose(h, 3, &meas);
+    if (cx) cx = cx_choose(h, 3, n, &meas);
     CxMeasure m(h, meas, n);
     switch (h->ring_mode) {
         case GD_RING_DIRECTORY: return route_nodes_mode<GD_RING_DIRECTORY>(h, nodes, n, tcd, silo, act, status, cx);
