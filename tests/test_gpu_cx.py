@@ -25,10 +25,11 @@ def gd():
     return g
 
 
-def _pair(gd, mode, cap, **kw):
+def _pair(gd, mode, cap, cx_mode="2", **kw):
+    """(engine with the index: GD_CX=cx_mode, 2 always / 1 measured choice; engine without: GD_CX=0)."""
     silos = o.bench_silos(8)
     out = []
-    for cx in ("1", "0"):
+    for cx in (cx_mode, "0"):
         os.environ["GD_CX"] = cx
         try:
             e = gd.GrainDispatch(device=0, table_capacity=cap, **kw)
@@ -53,10 +54,10 @@ def _both(engines, fn):
     return [fn(e) for e in engines]
 
 
-@pytest.mark.parametrize("mode", ["D", "R", "V"])
-def test_cx_matches_directory_through_changes(gd, mode):
+@pytest.mark.parametrize("mode,cx_mode", [("D", "2"), ("R", "2"), ("V", "2"), ("D", "1")])
+def test_cx_matches_directory_through_changes(gd, mode, cx_mode):
     rng = np.random.default_rng(41)
-    (a, b), spec = _pair(gd, mode, 1 << 14)
+    (a, b), spec = _pair(gd, mode, 1 << 14, cx_mode)
     tc2 = o.grain_type_code("UnitTests.OtherGrain")
     G = 5000
     reg = np.concatenate([o.grain_keys(TC, np.arange(G)), o.grain_keys(tc2, np.arange(G // 2))])

@@ -2,6 +2,7 @@
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
 OUT=gpurun_out/r03_cfg4_tune_ab.txt
+timeout -k 10 300 python -u -m pytest tests/test_gpu_cx.py tests/test_gpu_fanout.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r03_cx_tests2.log 2>&1 || exit 1
 : > $OUT
 for rep in 1 2; do
 for cx in 1 2 0; do
