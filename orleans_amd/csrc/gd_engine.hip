@@ -172,15 +172,18 @@ struct gd_handle {
     bool route_nt = false;
     bool route_xcd = true;      // route workgroups over XCD-contiguous message ranges (GD_ROUTE_XCD)
     // compact probe index (gd_cx.h): derived from the table, rebuilt after any change of it (GD_CX=0: off)
-    int cx_mode = 1;            // 0 off, 1 measured per launch kind (default), 2 always (GD_CX)
+    int cx_mode = 1;            // 0 off, 1 measured (default), 2 index group reads, 3 index slot reads (GD_CX)
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
-    struct CxTune {             // per launch kind and size class: index vs directory probe, timed live
-        int pick = -1;          // -1 measuring, 0 index, 1 directory
+    // per launch kind and size class: the probe variant, timed on live launches.  Variants: 0 the index
+    // in 64-B group reads, 1 the directory, 2 the index in 16-B slot reads
+    static constexpr int CXV = 3;
+    struct CxTune {
+        int pick = -1;          // -1 measuring, else the variant
         int round = 0;
-        float best[2] = {1e30f, 1e30f};
-        hipEvent_t a[2] = {nullptr, nullptr}, b[2] = {nullptr, nullptr};
-        bool pending[2] = {false, false};
-        uint64_t n[2] = {0, 0};
+        float best[CXV] = {1e30f, 1e30f, 1e30f};
+        hipEvent_t a[CXV] = {}, b[CXV] = {};
+        bool pending[CXV] = {};
+        uint64_t n[CXV] = {};
     };
     std::map<int, CxTune> cx_tune;   // key: kind * 64 + size class (bit length of n)
     uint64_t tab_gen = 0;       // bumped by every launch that takes the table as a writable Slot*
@@ -426,14 +429,15 @@ int cx_ensure(gd_handle* h, bool* ok) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     h->cx_built = true;
     h->cx_ok = c.flag == 0 && c.full == 0;
-    for (auto& kt : h->cx_tune) {                   // a new table: measure both probes again
+    for (auto& kt : h->cx_tune) {                   // a new table: measure the probes again
         auto& t = kt.second;
-        for (int v = 0; v < 2; ++v)
+        for (int v = 0; v < gd_handle::CXV; ++v) {
             if (t.pending[v]) (void)hipEventSynchronize(t.b[v]);
+            t.best[v] = 1e30f;
+            t.pending[v] = false;
+        }
         t.pick = -1;
         t.round = 0;
-        t.best[0] = t.best[1] = 1e30f;
-        t.pending[0] = t.pending[1] = false;
     }
     h->cx_rounds = c.max_rounds;
     h->cx_slots_at = h->slots;
@@ -443,58 +447,67 @@ int cx_ensure(gd_handle* h, bool* ok) {
     return GD_OK;
 }
 
-// Index or directory probe for a launch of `kind` (0 keys, 1 N1s, 2 fan-out, 3 node ids) over n
-// messages when the index is available: GD_CX=2 always the index; GD_CX=1 times the two on the first
-// four eligible launches of the kind and size class (bit length of n: the fan-out's hops differ 10x in
-// size, and per-message cost with them) -- index, directory, index, directory, between HIP events read
-// back without a stream sync at the next choice -- and keeps the faster per message.  Both give the
-// same results; which is faster depends on the key distribution (a Zipf-hot set favours the
-// directory's 32-B reads, a uniform one the index's smaller table).  *meas: the tune entry
-// this launch is timed into (key), or -1.
-bool cx_choose(gd_handle* h, int kind, uint64_t n, int* meas) {
+// The probe variant for a launch of `kind` (0 keys, 1 N1s, 2 fan-out, 3 node ids) over n messages when
+// the index is available: 0 the index read in 64-B groups, 1 the directory, 2 the index read one 16-B
+// slot at a time.  GD_CX=2: always 0.  GD_CX=1 times the three on the first six eligible launches of the
+// kind and size class (bit length of n: the fan-out's hops differ 10x in size, and per-message cost
+// with them), twice each in turn, between HIP events read back without a stream sync at the next
+// choice, and keeps the fastest per message.  All give the same results; which is fastest depends on
+// the key distribution (a Zipf-hot set favours small reads, a uniform one the index's group reads,
+// DESIGN 5).  nvar: the variants this launch kind has (2: no 16-B-read form).  *meas: the tune entry
+// this launch is timed into (key * CXV + variant), or -1.
+int cx_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar = gd_handle::CXV) {
+    constexpr int V = gd_handle::CXV;
     *meas = -1;
-    if (h->cx_mode == 2) return true;
+    if (h->cx_mode == 2) return 0;
+    if (h->cx_mode == 3) return nvar > 2 ? 2 : 0;
     int cls = 0;
     while (cls < 63 && (n >> cls) > 1) ++cls;
     const int key = kind * 64 + cls;
     auto& t = h->cx_tune[key];
-    for (int v = 0; v < 2; ++v) {
+    bool any_pending = false;
+    for (int v = 0; v < V; ++v) {
         if (!t.pending[v]) continue;
-        if (hipEventQuery(t.b[v]) != hipSuccess && t.pick < 0 && t.round >= 4) (void)hipEventSynchronize(t.b[v]);
+        if (hipEventQuery(t.b[v]) != hipSuccess && t.pick < 0 && t.round >= 2 * nvar) (void)hipEventSynchronize(t.b[v]);
         if (hipEventQuery(t.b[v]) == hipSuccess) {
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, t.a[v], t.b[v]) == hipSuccess && t.n[v])
                 t.best[v] = std::min(t.best[v], ms / (float)t.n[v]);
             t.pending[v] = false;
         }
+        any_pending = any_pending || t.pending[v];
     }
-    if (t.pick < 0 && t.round >= 4 && !t.pending[0] && !t.pending[1])
-        t.pick = t.best[0] <= t.best[1] ? 0 : 1;
-    if (t.pick >= 0) return t.pick == 0;
-    const int v = t.round & 1;
-    if (t.round < 4 && !t.pending[v]) {
+    if (t.pick < 0 && t.round >= 2 * nvar && !any_pending) {
+        t.pick = 0;
+        for (int v = 1; v < nvar; ++v)
+            if (t.best[v] < t.best[t.pick]) t.pick = v;
+    }
+    if (t.pick >= 0) return t.pick;
+    const int v = t.round % nvar;
+    if (t.round < 2 * nvar && !t.pending[v]) {
         if (!t.a[v]) (void)hipEventCreate(&t.a[v]);
         if (!t.b[v]) (void)hipEventCreate(&t.b[v]);
-        *meas = key * 2 + v;
+        *meas = key * V + v;
         ++t.round;
     }
-    return v == 0;
+    return v;
 }
 
-// Brackets a launch chosen by cx_choose with the tune slot's events.
+// Brackets a launch chosen by cx_choose with the tune entry's events.
 struct CxMeasure {
     gd_handle* h;
     int slot;
     uint64_t n;
     CxMeasure(gd_handle* hh, int sl, uint64_t nn) : h(hh), slot(sl), n(nn) {
-        if (slot >= 0) (void)hipEventRecord(h->cx_tune[slot / 2].a[slot & 1], h->stream);
+        if (slot >= 0) (void)hipEventRecord(h->cx_tune[slot / gd_handle::CXV].a[slot % gd_handle::CXV], h->stream);
     }
     ~CxMeasure() {
         if (slot < 0) return;
-        auto& t = h->cx_tune[slot / 2];
-        (void)hipEventRecord(t.b[slot & 1], h->stream);
-        t.n[slot & 1] = n;
-        t.pending[slot & 1] = true;
+        auto& t = h->cx_tune[slot / gd_handle::CXV];
+        const int v = slot % gd_handle::CXV;
+        (void)hipEventRecord(t.b[v], h->stream);
+        t.n[v] = n;
+        t.pending[v] = true;
     }
 };
 
@@ -509,12 +522,16 @@ int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, u
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
     int meas = -1;
-    if (cx) cx = cx_choose(h, 0, n, &meas);
+    const int var = cx ? cx_choose(h, 0, n, &meas) : 1;
     CxMeasure m(h, meas, n);
-    if (cx)
+    if (var == 0)
         return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h),
                       k_route_m<MODE, M, NT, 0, true>, keys, n, ring_args(h), table_args(h), silo, act, status, 0ull,
                       h->route_xcd ? 1u : 0u, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, cx_args(h));
+    if (var == 2)
+        return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h),
+                      k_route_m<MODE, M, NT, 0, true, 1>, keys, n, ring_args(h), table_args(h), silo, act, status,
+                      0ull, h->route_xcd ? 1u : 0u, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, cx_args(h));
     return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h), k_route_m<MODE, M, NT>, keys,
                   n, ring_args(h), table_args(h), silo, act, status, 0ull, h->route_xcd ? 1u : 0u,
                   (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, CxArgs{});
@@ -530,13 +547,19 @@ int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uin
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
     int meas = -1;
-    if (cx) cx = cx_choose(h, 1, n, &meas);
+    const int var = cx ? cx_choose(h, 1, n, &meas) : 1;
     CxMeasure m(h, meas, n);
-    if (cx && n1w == 4)
+    if (var == 0 && n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4, true>, k, n, ring_args(h),
                       table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h));
-    if (cx)
+    if (var == 0)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8, true>, k, n, ring_args(h),
+                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h));
+    if (var == 2 && n1w == 4)
+        return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4, true, 1>, k, n, ring_args(h),
+                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h));
+    if (var == 2)
+        return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8, true, 1>, k, n, ring_args(h),
                       table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h));
     if (n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4>, k, n, ring_args(h), table_args(h),
@@ -1208,7 +1231,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_ROUTE_M")) h->route_m = std::atoi(v);
     if (const char* v = std::getenv("GD_ROUTE_NT")) h->route_nt = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_ROUTE_XCD")) h->route_xcd = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_CX")) h->cx_mode = std::max(0, std::min(2, std::atoi(v)));
+    if (const char* v = std::getenv("GD_CX")) h->cx_mode = std::max(0, std::min(3, std::atoi(v)));
     if (const char* v = std::getenv("GD_CX_SCALE")) h->cx_scale = std::atoi(v) == 2 ? 2u : 1u;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
@@ -2395,7 +2418,7 @@ int fan_route_launch(gd_handle* h, const uint32_t* row_off, const uint32_t* dst,
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
     int meas = -1;
-    if (cx) cx = cx_choose(h, 2, total, &meas);
+    if (cx) cx = cx_choose(h, 2, total, &meas, 2) == 0;
     CxMeasure m(h, meas, total);
     if (cx)
         return fan_route_launch_cx<MODE, true>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo, act,
@@ -2439,7 +2462,7 @@ int route_nodes(gd_handle* h, const uint32_t* nodes, uint32_t n, uint64_t tcd, u
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx));
     int meas = -1;
-    if (cx) cx = cx_choose(h, 3, n, &meas);
+    if (cx) cx = cx_choose(h, 3, n, &meas, 2) == 0;
     CxMeasure m(h, meas, n);
     switch (h->ring_mode) {
         case GD_RING_DIRECTORY: return route_nodes_mode<GD_RING_DIRECTORY>(h, nodes, n, tcd, silo, act, status, cx);

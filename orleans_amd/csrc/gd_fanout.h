@@ -189,14 +189,16 @@ __device__ __forceinline__ uint8_t route_node(uint32_t node, uint64_t tcd, const
 
 // The compact probe index's walk (gd_kernels.h CxArgs) from a group already read: the status of
 // GrainId(tcd, n1) given its type's `want` (0x100 | type index; 0: the type holds no entry).
+template <int RG>
 __device__ __forceinline__ uint8_t cx_walk_node(const CxArgs& cx, const TableArgs& tab, uint32_t want, uint64_t n1,
-                                                unsigned long long s, uint4 (&q)[CX_GROUP], uint32_t& silo,
+                                                unsigned long long s, uint4 (&q)[RG], uint32_t& silo,
                                                 uint32_t& act) {
+    const uint32_t bound = (cx.max_rounds + 1) * (CX_GROUP / RG) - 1;   // reads of RG slots
     uint8_t st = GD_ROUTE_MISS;
     bool done = want == 0;
     for (uint32_t p = 0; !done;) {
 #pragma unroll
-        for (int g = 0; g < (int)CX_GROUP; ++g) {
+        for (int g = 0; g < RG; ++g) {
             if (done) continue;
             const uint4 v = q[g];
             if (v.w == 0) {
@@ -209,11 +211,11 @@ __device__ __forceinline__ uint8_t cx_walk_node(const CxArgs& cx, const TableArg
                 done = true;
             }
         }
-        if (done || ++p > cx.max_rounds) break;
-        s += CX_GROUP;
+        if (done || ++p > bound) break;
+        s += RG;
         if (s >= cx.cap) s = 0;
 #pragma unroll
-        for (int g = 0; g < (int)CX_GROUP; ++g) q[g] = cx.slots[s + g];
+        for (int g = 0; g < RG; ++g) q[g] = cx.slots[s + g];
     }
     return st;
 }
@@ -225,7 +227,7 @@ __device__ __forceinline__ uint32_t cx_want(const CxArgs& cx, uint64_t tcd) {
 
 // Route a batch of node ids (GrainId(typeCode, node), the owner side of the sharded fan-out).
 // CX: through the compact probe index.
-template <int MODE, bool CX = false>
+template <int MODE, bool CX = false, int RG = (int)CX_GROUP>
 __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restrict__ nodes, uint32_t n, uint64_t tcd,
                                                        RingArgs ring, TableArgs tab, uint32_t* __restrict__ out_silo,
                                                        uint32_t* __restrict__ out_act,
@@ -244,14 +246,14 @@ __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restric
         const uint32_t node = nodes[i];
         const uint32_t h = uniform_hash(0, node, tcd);
         const unsigned long long s0 = cx_home(h, cx.cap);
-        uint4 q[CX_GROUP];
+        uint4 q[RG];
         if (want) {
 #pragma unroll
-            for (int g = 0; g < (int)CX_GROUP; ++g) q[g] = cx.slots[s0 + g];
+            for (int g = 0; g < RG; ++g) q[g] = cx.slots[s0 + g];
         }
         silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h)];
         act = NONE32;
-        st = cx_walk_node(cx, tab, want, node, s0, q, silo, act);
+        st = cx_walk_node<RG>(cx, tab, want, node, s0, q, silo, act);
     } else {
         st = route_node<MODE>(nodes[i], tcd, s_pts, s_own, ring, tab, max_probe, silo, act);
     }
@@ -263,7 +265,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restric
 // Fused expansion + route.  out_target may be null.  ILP items of a thread at a time: their
 // follower-list reads, then their first directory probes, are in flight together (one dependent
 // chain per item otherwise).
-template <int MODE, int ILP, bool CX = false>
+template <int MODE, int ILP, bool CX = false, int RG = (int)CX_GROUP>
 __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict__ row_off,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint32_t* __restrict__ frontier, uint32_t n_front,
@@ -300,14 +302,14 @@ __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict_
         if constexpr (CX) {                                   // the compact probe index (gd_kernels.h)
             const uint32_t want = cx_want(cx, tcd);
             unsigned long long sc[ILP];
-            uint4 qc[ILP][CX_GROUP];
+            uint4 qc[ILP][RG];
 #pragma unroll
             for (int q = 0; q < ILP; ++q) {
                 h[q] = uniform_hash(0, target[q], tcd);
                 sc[q] = cx_home(h[q], cx.cap);
                 if (live[q] && want) {
 #pragma unroll
-                    for (int g = 0; g < (int)CX_GROUP; ++g) qc[q][g] = cx.slots[sc[q] + g];
+                    for (int g = 0; g < RG; ++g) qc[q][g] = cx.slots[sc[q] + g];
                 }
             }
 #pragma unroll
@@ -315,7 +317,7 @@ __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict_
                 if (!live[q]) continue;
                 const uint32_t p = p0 + (it0 + q) * BLOCK + threadIdx.x;
                 uint32_t silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[q])], act = NONE32;
-                const uint8_t st = cx_walk_node(cx, tab, want, target[q], sc[q], qc[q], silo, act);
+                const uint8_t st = cx_walk_node<RG>(cx, tab, want, target[q], sc[q], qc[q], silo, act);
                 if (out_target) out_target[p] = target[q];
                 out_sender[p] = sender[q];
                 out_silo[p] = silo;

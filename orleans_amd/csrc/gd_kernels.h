@@ -286,8 +286,10 @@ __device__ __forceinline__ void st(T* p, T v) {
 // N1W: 0 = 24-B keys; 8 / 4 = the keys arrive as N1 alone (u64 / u32 each; N0 = 0, TypeCodeData =
 // tcd_u for all), the forms a compact exchange header round delivers (k_key_desc, gd_shard.h).
 // The per-thread part: messages base + j * STRIDE, j < M; lds_act (optional) gets act too.
-// CX: probe the compact index (cx, its type set staged in s_types) instead of the directory.
-template <int MODE, int M, int STRIDE, bool NT, int N1W, bool NT_SIDE = false, bool CX = false>
+// CX: probe the compact index (cx, its type set staged in s_types) instead of the directory, RG slots
+// (16 B each) a read: CX_GROUP (one 64-B atom, the layout's group) or 1 (16 B, for hot key sets).
+template <int MODE, int M, int STRIDE, bool NT, int N1W, bool NT_SIDE = false, bool CX = false,
+          int RG_CX = (int)CX_GROUP>
 __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, uint32_t n, uint32_t base,
                                              const RingArgs& ring, const uint32_t* s_pts, const uint32_t* s_own,
                                              const TableArgs& tab, uint32_t max_probe,
@@ -342,9 +344,12 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
     }
     if constexpr (CX) {
         // Every directory entry has N0 = 0 and one of the staged types: any other key is a miss.
+        static_assert(RG_CX == 1 || RG_CX == (int)CX_GROUP, "index reads: one slot or one group");
+        // the probe bound in reads of RG_CX slots: every entry sits within max_rounds groups of its home
+        const uint32_t bound = (cx->max_rounds + 1) * (CX_GROUP / RG_CX) - 1;
         uint32_t want[M];
         unsigned long long s[M];
-        uint4 q[M][CX_GROUP];
+        uint4 q[M][RG_CX];
 #pragma unroll
         for (int j = 0; j < M; ++j) {
             want[j] = 0;
@@ -355,7 +360,7 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
             s[j] = cx_home(h[j], cx->cap);
             if (want[j]) {
 #pragma unroll
-                for (int g = 0; g < (int)CX_GROUP; ++g) q[j][g] = cx->slots[s[j] + g];
+                for (int g = 0; g < RG_CX; ++g) q[j][g] = cx->slots[s[j] + g];
             }
         }
 #pragma unroll
@@ -367,7 +372,7 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
             bool done = false;
             for (uint32_t p = 0;;) {
 #pragma unroll
-                for (int g = 0; g < (int)CX_GROUP; ++g) {
+                for (int g = 0; g < RG_CX; ++g) {
                     if (done) continue;
                     const uint4 v = q[j][g];
                     if (v.w == 0) {
@@ -383,11 +388,11 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
                         done = true;
                     }
                 }
-                if (done || ++p > cx->max_rounds) break;
-                s[j] += CX_GROUP;
+                if (done || ++p > bound) break;
+                s[j] += RG_CX;
                 if (s[j] >= cx->cap) s[j] = 0;
 #pragma unroll
-                for (int g = 0; g < (int)CX_GROUP; ++g) q[j][g] = cx->slots[s[j] + g];
+                for (int g = 0; g < RG_CX; ++g) q[j][g] = cx->slots[s[j] + g];
             }
         }
     } else {
@@ -507,7 +512,7 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb, uint32_t x
 
 // src_out (optional, the exchange's receive side): message i's sender rank, from the per-sender
 // receive counts rcnt[world] (k_recv_src's job, done here beside the probe's own writes).
-template <int MODE, int M, bool NT, int N1W = 0, bool CX = false>
+template <int MODE, int M, bool NT, int N1W = 0, bool CX = false, int RG_CX = (int)CX_GROUP>
 __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                    TableArgs tab, uint32_t* __restrict__ out_silo,
                                                    uint32_t* __restrict__ out_act,
@@ -533,7 +538,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
     // xcd: each XCD routes a contiguous message range (xcd_tile), so the act it writes is the act the
     // same XCD's histogram and scatter workgroups read next (their XCD tile ranges match)
     const uint32_t blk = xcd_tile(blockIdx.x, gridDim.x, xcd);
-    route_m_core<MODE, M, BLOCK, NT, N1W, true, CX>(keys, n, blk * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own,
+    route_m_core<MODE, M, BLOCK, NT, N1W, true, CX, RG_CX>(keys, n, blk * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own,
                                                    tab, CX ? 0u : tab.ctr->max_probe, out_silo, out_act, out_status,
                                                    tcd_u, nullptr, 0, &cx, s_types);
     if (src_out) {

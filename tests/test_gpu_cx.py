@@ -26,7 +26,8 @@ def gd():
 
 
 def _pair(gd, mode, cap, cx_mode="2", **kw):
-    """(engine with the index: GD_CX=cx_mode, 2 always / 1 measured choice; engine without: GD_CX=0)."""
+    """(engine with the index: GD_CX=cx_mode -- 2 group reads, 3 slot reads, 1 measured choice; engine
+    without: GD_CX=0)."""
     silos = o.bench_silos(8)
     out = []
     for cx in (cx_mode, "0"):
@@ -54,7 +55,7 @@ def _both(engines, fn):
     return [fn(e) for e in engines]
 
 
-@pytest.mark.parametrize("mode,cx_mode", [("D", "2"), ("R", "2"), ("V", "2"), ("D", "1")])
+@pytest.mark.parametrize("mode,cx_mode", [("D", "2"), ("R", "2"), ("V", "2"), ("D", "1"), ("V", "3")])
 def test_cx_matches_directory_through_changes(gd, mode, cx_mode):
     rng = np.random.default_rng(41)
     (a, b), spec = _pair(gd, mode, 1 << 14, cx_mode)
