@@ -269,7 +269,11 @@ int gd_route_bucket(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act
                     uint32_t* out_silo, uint32_t* out_act, uint8_t* out_status,
                     uint32_t* out_perm, uint32_t* out_offsets);
 
-/* Device-pointer forms (enqueue only).  Same semantics as above. */
+/* Device-pointer forms (enqueue only).  Same semantics as above.  One exception to "enqueue only": the
+ * first route after a change of the directory table rebuilds the library's compact probe index (two
+ * kernels over the table) and synchronises the handle's stream once to learn whether the
+ * table qualifies; routes in between changes enqueue only.  GD_CX=0 in the environment at gd_create
+ * turns the index off. */
 int gd_route_device(gd_handle* h, const gd_key* d_keys, uint32_t n,
                     uint32_t* d_silo, uint32_t* d_act, uint8_t* d_status);
 int gd_bucket_device(gd_handle* h, const uint32_t* d_acts, uint32_t n, uint32_t n_act,
