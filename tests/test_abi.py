@@ -149,3 +149,11 @@ def test_comm_init_local_rejects_bad_args():
     assert g.lib.gd_comm_init_local(arr, 2) == g.GD_EINVAL
     assert g.lib.gd_comm_init_local(arr, 0) == g.GD_EINVAL
     assert g.lib.gd_comm_init_local(arr, 257) == g.GD_EINVAL
+
+
+def test_calculate_id_hash_matches_the_reference_assertions():
+    """gd_calculate_id_hash (host, C ABI) on the reference's own known answers
+    (CodeGeneratorTests_RequiringSilo.cs:32,47; tests/golden/reference_kat.json)."""
+    kat = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_kat.json")))
+    for row in kat["grain_class_type_codes"]:
+        assert g.calculate_id_hash(row["class"]) == row["base_type_code"], row["class"]

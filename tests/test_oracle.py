@@ -276,3 +276,21 @@ def test_c_bucket_runs_matches_stable_partition():
         np.testing.assert_array_equal(np.diff(rs), np.bincount(c, minlength=1001)[ua])
         assert rs[0] == 0 and rs[-1] == n
     assert not br.counts.any()
+
+
+def test_type_codes_match_the_reference_assertions():
+    """Known answers the reference's own tests hold: the GrainId of GetGrain<ITestGrain>(k) has
+    BaseTypeCode 1146670029 and that of GetGrain<ICollectionTestGrain>(k) 1381240679
+    (test/DefaultCluster.Tests/CodeGenTests/CodeGeneratorTests_RequiringSilo.cs:32,47).  The class's type
+    code is GrainInterfaceUtils.GetTypeCode = Utils.CalculateIdHash(class full name) (no
+    [TypeCodeOverride]; GrainInterfaceUtils.cs:400-415, Utils.cs:184-203), it goes into the key's
+    TypeCodeData (GrainId.GetGrainId(typeCode, long), GrainId.cs:72-77, UniqueKey.cs:112-128) and
+    BaseTypeCode reads its low 32 bits back (UniqueKey.cs:11,36-39).  This pins the SHA-256-of-UTF-16LE
+    fold and the key layout every routed message carries."""
+    kat = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kat.json")))
+    for row in kat["grain_class_type_codes"]:
+        tc = o.grain_type_code(row["class"])
+        assert tc == row["base_type_code"], row["class"]
+        key = o.grain_keys(tc, np.array([12345]))[0]
+        assert int(key[2]) >> 56 == o.CAT_GRAIN
+        assert int(key[2]) & 0xFFFFFFFF == row["base_type_code"]
