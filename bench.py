@@ -194,10 +194,19 @@ def setup_workload(args, workload, world, rank, local, dev, tcd, msgs, grains):
             "owner_share_max": round(owner_share, 4), "owner_share_by_set": by_set}
 
 
+# Untimed steps before the W warmup steps: libgraindispatch times its probe variants (compact index in
+# group reads, directory, index in slot reads) on the first 2 x 3 eligible launches of each launch kind
+# and size, then keeps the fastest (gd_engine.hip cx_choose).  These steps let that
+# measurement finish before the timed region with any --warmup (the driver uses 5): every timed step
+# then runs the variant the library keeps.
+SETTLE_STEPS = 8
+
+
 def timed_steps(router, keys, n_act, stream, steps, warmup):
-    """W untimed steps, then exactly K steps bracketed by barrier + synchronize; max over ranks."""
+    """W untimed steps (after SETTLE_STEPS), then exactly K steps bracketed by barrier + synchronize;
+    max over ranks."""
     with torch.cuda.stream(stream):
-        for _ in range(warmup):
+        for _ in range(SETTLE_STEPS + warmup):
             router.route_bucket(keys, n_act)
         torch.cuda.synchronize()
         dist.barrier()
@@ -441,7 +450,7 @@ def main():
             "unit": "messages/s",
             "n_gpus": world,
             "steps": args.steps,
-            "warmup": args.warmup,
+            "warmup": args.warmup, "settle_steps": SETTLE_STEPS,
             "ms_per_step": round(wall_max / args.steps * 1e3, 4),
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
             "higher_is_better": True,
@@ -791,7 +800,7 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     def step():
         return runner.run(t_seeds, args.hops)
 
-    for _ in range(warmup):
+    for _ in range(SETTLE_STEPS // 2 + warmup):     # cascades: the probe choice per hop size (SETTLE_STEPS)
         step()
     torch.cuda.synchronize()
     dist.barrier()
