@@ -220,9 +220,11 @@ def timed_steps(router, keys, n_act, stream, steps, warmup):
             res = router.route_bucket(keys, n_act)
         ev1.record(stream)
         torch.cuda.synchronize()
+        # this rank's K steps end when its device is done; the closing barrier aligns the ranks and the
+        # max over ranks below takes the slowest
+        wall = time.perf_counter() - t0
         dist.barrier()
         torch.cuda.synchronize()
-        wall = time.perf_counter() - t0
     t = torch.tensor([wall], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item()), ev0.elapsed_time(ev1), res
@@ -811,9 +813,9 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
         hops = step()
         msgs_local += sum(h.messages for h in hops)
     torch.cuda.synchronize()
+    wall = time.perf_counter() - t0                  # this rank's steps; the max over ranks below
     dist.barrier()
     torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
     t = torch.tensor([wall, msgs_local], dtype=torch.float64)
     tw, ts = t.clone(), t.clone()
     dist.all_reduce(tw, op=dist.ReduceOp.MAX)
