@@ -20,6 +20,7 @@
 #include "gd_fanout.h"
 #include "gd_cache.h"
 #include "gd_cx.h"
+#include "gd_msd.h"
 #include "gd_shard.h"
 #include "gd_comm.h"
 #include "gd_localcomm.h"
@@ -173,6 +174,7 @@ struct gd_handle {
     bool route_xcd = true;      // route workgroups over XCD-contiguous message ranges (GD_ROUTE_XCD)
     // compact probe index (gd_cx.h): derived from the table, rebuilt after any change of it (GD_CX=0: off)
     int cx_mode = 1;            // 0 off, 1 measured (default), 2 index group reads, 3 index slot reads (GD_CX)
+    int msd_mode = 1;           // two-level bucketing (gd_msd.h): 0 off, 1 measured (default), 2 always (GD_MSD)
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
     // per launch kind and size class: the probe variant, timed on live launches.  Variants: 0 the index
     // in 64-B group reads, 1 the directory, 2 the index in 16-B slot reads
@@ -456,11 +458,9 @@ int cx_ensure(gd_handle* h, bool* ok) {
 // the key distribution (a Zipf-hot set favours small reads, a uniform one the index's group reads,
 // DESIGN 5).  nvar: the variants this launch kind has (2: no 16-B-read form).  *meas: the tune entry
 // this launch is timed into (key * CXV + variant), or -1.
-int cx_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar = gd_handle::CXV) {
+int tune_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar) {
     constexpr int V = gd_handle::CXV;
     *meas = -1;
-    if (h->cx_mode == 2) return 0;
-    if (h->cx_mode == 3) return nvar > 2 ? 2 : 0;
     int cls = 0;
     while (cls < 63 && (n >> cls) > 1) ++cls;
     const int key = kind * 64 + cls;
@@ -493,7 +493,14 @@ int cx_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar = gd_handl
     return v;
 }
 
-// Brackets a launch chosen by cx_choose with the tune entry's events.
+int cx_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar = gd_handle::CXV) {
+    *meas = -1;
+    if (h->cx_mode == 2) return 0;
+    if (h->cx_mode == 3) return nvar > 2 ? 2 : 0;
+    return tune_choose(h, kind, n, meas, nvar);
+}
+
+// Brackets a launch chosen by cx_choose / tune_choose with the tune entry's events.
 struct CxMeasure {
     gd_handle* h;
     int slot;
@@ -882,12 +889,49 @@ int bucket2_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_ac
                   B2_LOW_BITS, tot2, R2);
 }
 
-// Stable partition of indices 0..n-1 by min(acts[i], n_act):
-// LSD passes of <= 8 bits, then bucket offsets from the sorted keys.  rank_out (optional): the
-// inverse permutation, rank_out[perm[p]] = p.
+// The two-level bucketing (gd_msd.h): a stable 9-bit MSD pass into ranges of 4,096 activations
+// (the LSD kernels with shift 12), then k_msd_local sorts each range in LDS and writes its starts.
+int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
+               uint32_t* rank_out) {
+    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
+    GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
+    uint32_t* k1 = (uint32_t*)h->u32_a.p;
+    uint32_t* v1 = (uint32_t*)h->u32_c.p;
+    uint32_t ib = 1;
+    while (ib < 32 && ((n - 1) >> ib) != 0) ++ib;
+    GD_TRY(radix_dispatch(h, 9, acts, nullptr, n, n_act, MSD_SHIFT, k1, v1, true, nullptr, nullptr,
+                          FillArgs{nullptr, 0u, 0u}, Pack{ib, 9u, false, false}));
+    if (!h->last_totals || h->last_digits < (n_act >> MSD_SHIFT) + 1)
+        return set_err(h, GD_ESTATE, "two-level bucketing needs the row-scan digit totals");
+    return launch(h, "k_msd_local", dim3((n_act >> MSD_SHIFT) + 1), dim3(MSD_NT), 0, k_msd_local, (const uint32_t*)k1,
+                  (const uint32_t*)v1, h->last_totals, n, n_act, perm, offsets, rank_out);
+}
+
+int bucket_lsd(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
+               uint32_t* rank_out);
+
+// Stable partition of indices 0..n-1 by min(acts[i], n_act).  rank_out (optional): the inverse
+// permutation, rank_out[perm[p]] = p.  Two forms with identical output: LSD passes of <= 8 bits plus
+// the bucket starts (bucket_lsd), or, for n_act < 2^21 and batches of at least 2^20 messages, the
+// two-level MSD + in-LDS form (msd_bucket); GD_MSD=1 (default) times both on the first launches of
+// each batch size (tune_choose, kind 4) and keeps the faster, 2 always takes the two-level form.
 int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                   uint32_t* rank_out = nullptr) {
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    const bool msd_ok = h->msd_mode && n >= (1u << 20) && n_act < (MSD_MAX_RANGES << MSD_SHIFT) && h->radix_rowscan &&
+                        h->radix_cfg == 1 && !h->bucket2;
+    if (msd_ok) {
+        int meas = -1;
+        const int var = h->msd_mode == 2 ? 1 : tune_choose(h, 4, n, &meas, 2);
+        CxMeasure m(h, meas, n);
+        if (var == 1) return msd_bucket(h, acts, n, n_act, perm, offsets, rank_out);
+        return bucket_lsd(h, acts, n, n_act, perm, offsets, rank_out);
+    }
+    return bucket_lsd(h, acts, n, n_act, perm, offsets, rank_out);
+}
+
+int bucket_lsd(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
+               uint32_t* rank_out) {
     // keys of 17..21 bits with at most B2_RMAX2 high digits, batches of at least 64 tiles: two wide passes
     if (h->bucket2 && n >= 64 * B2_TILE && n_act >= (1u << 16) && (n_act >> B2_LOW_BITS) + 1 <= B2_RMAX2)
         return bucket2_device(h, acts, n, n_act, perm, offsets, rank_out);
@@ -1232,6 +1276,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_ROUTE_NT")) h->route_nt = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_ROUTE_XCD")) h->route_xcd = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_CX")) h->cx_mode = std::max(0, std::min(3, std::atoi(v)));
+    if (const char* v = std::getenv("GD_MSD")) h->msd_mode = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("GD_CX_SCALE")) h->cx_scale = std::atoi(v) == 2 ? 2u : 1u;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
