@@ -33,8 +33,9 @@ constexpr uint32_t B2_TILE = 16384;                      // items per tile, both
 
 // Histogram of TPB consecutive tiles per workgroup (NT x IT = B2_TILE), digit-major counts
 // hist[d * tiles + t] for d < R.  FIRST: the digit of min(key, clamp) & 1023, and the grid pre-fills
-// the bucket starts (fill); else (pass 2) the digit of the already clamped key, key >> 10.
-template <int NT, int IT, int TPB, int RMAX, bool FIRST>
+// the bucket starts (fill); else (pass 2) the digit of the already clamped key, key >> 10.  HI with
+// FIRST (the MSD pass of gd_msd.h): the raw keys clamped, their high digit.
+template <int NT, int IT, int TPB, int RMAX, bool FIRST, bool HI = !FIRST>
 __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t clamp,
                                                 uint32_t R, uint32_t tiles, uint32_t* __restrict__ hist, FillArgs fill,
                                                 uint32_t xcd_rev) {
@@ -68,7 +69,8 @@ __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restrict__ key
         for (int j = 0; j < IT; ++j) {
             const uint64_t i = base + 4 * ((j / 4) * NT + threadIdx.x) + (j % 4);
             const bool valid = i < n;
-            const uint32_t d = FIRST ? (min(k[j], clamp) & (B2_R1 - 1)) : (k[j] >> B2_LOW_BITS);
+            const uint32_t kc = FIRST ? min(k[j], clamp) : k[j];
+            const uint32_t d = HI ? (kc >> B2_LOW_BITS) : (kc & (B2_R1 - 1));
             const unsigned long long act = __ballot(valid);
             if (act == 0) continue;
             const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
@@ -93,8 +95,9 @@ __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restrict__ key
 // (key, index) in, the index out in digit order of key >> 10 -- the permutation -- and the bucket
 // starts (the first item of each key in a tile's digit run lowers starts[key] with atomicMin; the
 // run is sorted by the whole key because pass 1 ordered it), rank_out[index] = position on request.
-// gscan: the row-scanned counts (k_radix_rowscan), totals: the digit totals.
-template <int NT, int IT, int RMAX, bool FIRST>
+// gscan: the row-scanned counts (k_radix_rowscan), totals: the digit totals.  HI with FIRST (the MSD
+// pass of gd_msd.h): pass 1's inputs and outputs, ordered by the high digit key >> 10.
+template <int NT, int IT, int RMAX, bool FIRST, bool HI = !FIRST>
 __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ keys_in,
                                                    const uint32_t* __restrict__ vals_in, uint32_t n, uint32_t clamp,
                                                    uint32_t R, uint32_t tiles, const uint32_t* __restrict__ gscan,
@@ -160,7 +163,7 @@ __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ 
         for (int r = r0; r < r0 + 8; ++r) {
             const uint32_t idx = base + (w * IT + r) * WAVE + lane;
             const bool valid = idx < n;
-            const uint32_t d = FIRST ? (kk[r] & (B2_R1 - 1)) : (kk[r] >> B2_LOW_BITS);
+            const uint32_t d = HI ? (kk[r] >> B2_LOW_BITS) : (kk[r] & (B2_R1 - 1));
             const unsigned long long live = __ballot(valid);
             const uint32_t ld = live ? (uint32_t)__ffsll((long long)live) - 1 : 0u;
             const uint32_t hd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)ld);
@@ -221,7 +224,7 @@ __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ 
     for (int r = 0; r < IT; ++r) {
         const uint32_t pos = (w * IT + r) * WAVE + lane;
         if (base + pos < n) {
-            const uint32_t d = FIRST ? (kk[r] & (B2_R1 - 1)) : (kk[r] >> B2_LOW_BITS);
+            const uint32_t d = HI ? (kk[r] >> B2_LOW_BITS) : (kk[r] & (B2_R1 - 1));
             const uint32_t at = ((s_cnt[w >> 1][d] >> half) & 0xFFFFu) + rk[r];
             s_key[at] = kk[r];
             s_val[at] = (Val)vv[r];
@@ -233,7 +236,7 @@ __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ 
         const uint32_t p = j * NT + threadIdx.x;
         if (p < cnt_tile) {
             const uint32_t k = s_key[p];
-            const uint32_t d = FIRST ? (k & (B2_R1 - 1)) : (k >> B2_LOW_BITS);
+            const uint32_t d = HI ? (k >> B2_LOW_BITS) : (k & (B2_R1 - 1));
             const uint32_t g = s_gbase[d] + p;
             if (g < n) {                  // always true when the counts are right; never write out of bounds
                 if constexpr (FIRST) {

@@ -175,6 +175,8 @@ struct gd_handle {
     // compact probe index (gd_cx.h): derived from the table, rebuilt after any change of it (GD_CX=0: off)
     int cx_mode = 1;            // 0 off, 1 measured (default), 2 index group reads, 3 index slot reads (GD_CX)
     int msd_mode = 1;           // two-level bucketing (gd_msd.h): 0 off, 1 measured (default), 2 always (GD_MSD)
+    bool msd_g16 = false;       // its range staging: u32 indices, 1 workgroup a CU (GD_MSD_G16=1: u16 positions, 2;
+                                // measured slower, profiles/r03_msd_ab.txt)
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
     // per launch kind and size class: the probe variant, timed on live launches.  Variants: 0 the index
     // in 64-B group reads, 1 the directory, 2 the index in 16-B slot reads
@@ -204,14 +206,14 @@ struct gd_handle {
     bool idx16 = true;              // gd_route_multi: 2-B origin indices on the wire (KD_IDX16, GD_IDX16)
     bool pack_pay16 = false;        // set by route_multi around its partition: the scatter writes u16 payloads
     bool narrow_headers = true;     // compact headers as u32 N1s when every N1 < 2^32 (GD_NARROW_HEADERS=0: u64)
-    bool fused_starts = true;
+    bool fused_starts = true;   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
     bool radix_pack = true;     // 6-B packed records between radix passes when they fit (GD_RADIX_PACK)
     bool radix_rowscan = true;  // one scan launch per radix pass, digit rows (GD_RADIX_ROWSCAN=0: reduce + down)
-    bool fill_in_hist = true;
-    bool range_scan = true;
-    bool shard_gather = true;   // exchange partition of keys: k_shard_gather (GD_SHARD_GATHER=0: k_shard_scatter, staged keys)     // bucket starts: one range-scan launch when it applies (GD_RANGE_SCAN=0: reduce + down)
+    bool fill_in_hist = true;   // the first histogram pre-fills the bucket starts (GD_FILL_IN_HIST=0: k_fill)
+    bool range_scan = true;     // bucket starts: one range-scan launch when it applies (GD_RANGE_SCAN=0: reduce + down)
+    bool shard_gather = true;   // exchange partition of keys: k_shard_gather (GD_SHARD_GATHER=0: k_shard_scatter, staged keys)
     const uint32_t* last_totals = nullptr;   // the last radix pass's digit totals (row scans), and their count
-    uint32_t last_digits = 0;   // the first histogram pre-fills the bucket starts (GD_FILL_IN_HIST=0: k_fill)   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
+    uint32_t last_digits = 0;
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
     int fan_ilp = 2;                  // fan-out items per thread in flight together (GD_FAN_ILP: 1, 2, 4)
     bool bucket2 = false;             // two wide-digit passes on 16K-item tiles (GD_BUCKET2=1; measured slower)
@@ -775,7 +777,7 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
         } else {
             return set_err(h, GD_EINVAL, "packed radix records need 512 x 8 tiles and <= 8-bit digits");
         }
-    } else if constexpr (BITS <= 8) {
+    } else if constexpr (BITS <= 9) {
         if (tpb == 4)
             GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0, k_radix_hist_multi<BITS, NT, IT, 4>,
                           kin, n, clamp, shift, tiles, hist, fill, hxr));
@@ -889,22 +891,40 @@ int bucket2_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_ac
                   B2_LOW_BITS, tot2, R2);
 }
 
-// The two-level bucketing (gd_msd.h): a stable 9-bit MSD pass into ranges of 4,096 activations
-// (the LSD kernels with shift 12), then k_msd_local sorts each range in LDS and writes its starts.
+// The two-level bucketing (gd_msd.h): a stable MSD pass on the high digit min(act, n_act) >> 10 over
+// 16K-item tiles (the gd_bucket2.h kernels), then k_msd_local sorts each 1,024-activation range in
+// LDS and writes its starts.  Needs (n_act >> 10) + 1 <= B2_RMAX2.
 int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                uint32_t* rank_out) {
+    const uint32_t tiles = blocks_for(n, B2_TILE);
+    const uint32_t R = (n_act >> MSD_SHIFT) + 1;
+    if (R > MSD_MAX_RANGES) return set_err(h, GD_EINVAL, "two-level bucketing: n_act too large");
+    GD_TRY(ensure(h, h->hist, ((size_t)R * tiles + R) * sizeof(uint32_t)));
     GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
     GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
+    uint32_t* hist = (uint32_t*)h->hist.p;
     uint32_t* k1 = (uint32_t*)h->u32_a.p;
     uint32_t* v1 = (uint32_t*)h->u32_c.p;
-    uint32_t ib = 1;
-    while (ib < 32 && ((n - 1) >> ib) != 0) ++ib;
-    GD_TRY(radix_dispatch(h, 9, acts, nullptr, n, n_act, MSD_SHIFT, k1, v1, true, nullptr, nullptr,
-                          FillArgs{nullptr, 0u, 0u}, Pack{ib, 9u, false, false}));
-    if (!h->last_totals || h->last_digits < (n_act >> MSD_SHIFT) + 1)
-        return set_err(h, GD_ESTATE, "two-level bucketing needs the row-scan digit totals");
-    return launch(h, "k_msd_local", dim3((n_act >> MSD_SHIFT) + 1), dim3(MSD_NT), 0, k_msd_local, (const uint32_t*)k1,
-                  (const uint32_t*)v1, h->last_totals, n, n_act, perm, offsets, rank_out);
+    const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
+    if (tiles >= 1024)
+        GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(1024), 0,
+                      k_b2_hist<1024, 16, 4, B2_RMAX2, true, true>, acts, n, n_act, R, tiles, hist,
+                      FillArgs{nullptr, 0u, 0u}, hxr));
+    else
+        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(1024), 0, k_b2_hist<1024, 16, 1, B2_RMAX2, true, true>, acts,
+                      n, n_act, R, tiles, hist, FillArgs{nullptr, 0u, 0u}, hxr));
+    const uint32_t* tot = hist + (size_t)R * tiles;
+    GD_TRY(launch(h, "k_radix_rowscan", dim3(R), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R * tiles));
+    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(1024), 0, k_b2_scatter<1024, 16, B2_RMAX2, true, true>, acts,
+                  (const uint32_t*)nullptr, n, n_act, R, tiles, (const uint32_t*)hist, tot, k1, v1, (uint32_t*)nullptr,
+                  (uint32_t*)nullptr, h->xcd_tiles));
+    h->last_totals = tot;
+    h->last_digits = R;
+    if (h->msd_g16)
+        return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<true>, (const uint32_t*)k1,
+                      (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
+    return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<false>, (const uint32_t*)k1,
+                  (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
 }
 
 int bucket_lsd(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
@@ -912,14 +932,13 @@ int bucket_lsd(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, u
 
 // Stable partition of indices 0..n-1 by min(acts[i], n_act).  rank_out (optional): the inverse
 // permutation, rank_out[perm[p]] = p.  Two forms with identical output: LSD passes of <= 8 bits plus
-// the bucket starts (bucket_lsd), or, for n_act < 2^21 and batches of at least 2^20 messages, the
-// two-level MSD + in-LDS form (msd_bucket); GD_MSD=1 (default) times both on the first launches of
+// the bucket starts (bucket_lsd), or, for n_act < 1056 x 1024 and batches of at least 2^20 messages,
+// the two-level MSD + in-LDS form (msd_bucket); GD_MSD=1 (default) times both on the first launches of
 // each batch size (tune_choose, kind 4) and keeps the faster, 2 always takes the two-level form.
 int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                   uint32_t* rank_out = nullptr) {
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
-    const bool msd_ok = h->msd_mode && n >= (1u << 20) && n_act < (MSD_MAX_RANGES << MSD_SHIFT) && h->radix_rowscan &&
-                        h->radix_cfg == 1 && !h->bucket2;
+    const bool msd_ok = h->msd_mode && n >= (1u << 20) && (n_act >> MSD_SHIFT) + 1 <= MSD_MAX_RANGES && !h->bucket2;
     if (msd_ok) {
         int meas = -1;
         const int var = h->msd_mode == 2 ? 1 : tune_choose(h, 4, n, &meas, 2);
@@ -1277,6 +1296,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_ROUTE_XCD")) h->route_xcd = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_CX")) h->cx_mode = std::max(0, std::min(3, std::atoi(v)));
     if (const char* v = std::getenv("GD_MSD")) h->msd_mode = std::max(0, std::min(2, std::atoi(v)));
+    if (const char* v = std::getenv("GD_MSD_G16")) h->msd_g16 = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_CX_SCALE")) h->cx_scale = std::atoi(v) == 2 ? 2u : 1u;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));

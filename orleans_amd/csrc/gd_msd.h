@@ -1,31 +1,37 @@
 // gd_msd.h -- gfx950 device code for the two-level bucketing (the per-activation FIFO;
-// VERDICT r02 item 3): an MSD radix pass into ranges of MSD_L = 4,096 activations, then one
+// VERDICT r02 item 3): an MSD radix pass into ranges of MSD_L = 1,024 activations, then one
 // workgroup per range sorts it stably inside LDS and writes the range's bucket starts itself.
 //
-//   pass 1  k_radix_hist / row scan / k_radix_scatter with 9-bit digits = min(act, n_act) >> 12
-//           (the LSD kernels of gd_kernels.h, used as a stable MSD partition): every range's messages
-//           contiguous, in message order, keys and message indices 8 B a record;
-//   pass 2  k_msd_local, one 1,024-thread workgroup per range (<= 512 ranges: n_act < 2^21):
-//             sweep 1   the range's histogram over its <= 4,096 activations in LDS (32-bit counters),
-//                       exclusive scan -> the activations' bucket starts, written to offsets
-//                       (every activation of the range once, empty ones included: no min-scan);
-//             then in chunks of <= 16 x 4,095 messages, each wave taking a contiguous 1/16 of it:
-//             sweep 2a  per-wave counts (u16 pairs packed in u32 words: 16 x 2,048 words, 128 KB);
-//             prefix    per activation over the 16 waves (the owner thread of a word does both
-//                       halves), so a wave's counter now holds its first position in the chunk;
-//             sweep 2b  the same items again in the same order: ds_add_rtn on the wave's counter
-//                       returns the stable rank (a wave's lanes are served in lane order, its rows in
-//                       program order), perm[range base + start + rank] = message index.
-// Per message: pass 1 reads 4 + 4 B and writes 8 B; pass 2 reads the key 3 x 4 B (mostly from the
-// MALL) and the index 4 B and writes 4 B -- against 3 LSD passes, 3 histograms and a min-scan.
-// Output identical to the LSD path (both are the stable partition by min(act, n_act)).  A range's
-// workgroup processes all of its messages, so a Zipf-hot range is one workgroup's work: the library
-// times both paths per batch size and keeps the faster (bucket_device).
+//   pass 1  k_b2_hist / row scan / k_b2_scatter (gd_bucket2.h, 16K-item tiles) with the high digit
+//           min(act, n_act) >> 10 (<= B2_RMAX2 ranges): every range's messages contiguous, in message
+//           order, keys and message indices 8 B a record;
+//   pass 2  k_msd_local, one 1,024-thread workgroup per range.  A range of <= MSD_CAP messages (the
+//           uniform case: 16 K for BASELINE cfg 2) is held in registers, 24 rows a lane:
+//             count     per-wave counts (u16 pairs packed in u32 words: 16 x 512 words, 32 KB);
+//             prefix    per activation over the 16 waves (the owner thread of a word does both halves),
+//                       so a wave's counter holds its first position; the activations' totals are
+//                       scanned into the bucket starts, written to offsets (every activation of the
+//                       range once, empty ones included: no min-scan);
+//             rank      ds_add_rtn on the wave's counter returns the stable rank (a wave's lanes are
+//                       served in lane order, its rows in program order); the message index goes to
+//                       its sorted place in an LDS copy of the range (96 KB);
+//             write     the range's permutation slice leaves LDS in order: coalesced 4-B stores.
+//           A larger range (a Zipf-hot one) is histogrammed first and ranked in chunks of MSD_CAP with
+//           the index stored straight to its global position.
+// Why the range is staged: the first form of this pass (ranges of 4,096 activations, 64 K messages,
+// too many for LDS) stored each index straight to global memory, and those 16 M scattered 4-B stores
+// cost 0.18 ms of its 0.25 ms (measured with the stores removed: profiles/r03_msd4k_nostore_exp.txt);
+// staged, the pass takes 0.054 ms at cfg 2 (profiles/r03_msd_ab.txt).
+// Per message: pass 1 reads 4 B twice (histogram, scatter) and writes 8 B; pass 2 reads 8 B and
+// writes 4 B in order -- 24 B over 4 launches, against 40 B over 11 for three packed 7-bit LSD passes.  Output identical to the LSD path (both are the stable
+// partition by min(act, n_act)); the library times both per batch size and keeps the faster.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
+#include "gd_bucket2.h"
 #include "gd_common.h"
 #include "gd_kernels.h"
 
@@ -33,21 +39,53 @@ namespace gd {
 
 constexpr int MSD_NT = 1024;
 constexpr int MSD_NW = MSD_NT / WAVE;              // 16 waves
-constexpr uint32_t MSD_SHIFT = 12;
-constexpr uint32_t MSD_L = 1u << MSD_SHIFT;        // activations per range (range b: keys with b = key >> 12)
+constexpr uint32_t MSD_SHIFT = B2_LOW_BITS;        // range b: keys with key >> 10 == b
+constexpr uint32_t MSD_L = 1u << MSD_SHIFT;        // activations per range
 constexpr uint32_t MSD_LW = MSD_L / 2;             // u16-pair words per wave
-constexpr uint32_t MSD_SEG = 4095;                 // messages per wave per chunk: u16 counts never carry
-constexpr uint32_t MSD_CHUNK = MSD_NW * MSD_SEG;
-constexpr uint32_t MSD_MAX_RANGES = 512;           // the 9-bit MSD digit
+constexpr int MSD_G = 8;                           // rows whose message indices are loaded together
+constexpr uint32_t MSD_MAX_RANGES = B2_RMAX2;      // the high digit of pass 1
 
-__global__ void __launch_bounds__(MSD_NT) k_msd_local(const uint32_t* __restrict__ keys,
-                                                      const uint32_t* __restrict__ idx,
-                                                      const uint32_t* __restrict__ totals, uint32_t n,
-                                                      uint32_t n_act, uint32_t* __restrict__ perm,
-                                                      uint32_t* __restrict__ offsets,
-                                                      uint32_t* __restrict__ rank_out) {
+// G16 = false (the default): the staging copy holds the message indices (4 bytes a message, 24 rows
+// a lane, one workgroup a CU).  G16: u16 positions in the range (2 bytes, 20 rows a lane, two
+// workgroups a CU at <= 64 VGPRs) and the write-out gathers the indices from the range's slice --
+// measured slower at cfg 2 (0.088 against 0.054 ms, profiles/r03_msd_ab.txt), kept for A/B.
+template <bool G16>
+struct MsdCfg {
+    static constexpr int RW = G16 ? 20 : 24;                      // rows of 64 messages a wave holds
+    static constexpr uint32_t CAP = RW * MSD_NT;                  // messages per chunk (<= 1,536 a wave)
+    static constexpr int WPE = G16 ? 8 : 4;                       // waves per SIMD: 2 or 1 workgroups a CU
+    using Out = typename std::conditional<G16, uint16_t, uint32_t>::type;
+};
+
+// The per-wave counts (u16 pairs, wc[wave * MSD_LW + word]) become each wave's first position per
+// activation (an exclusive prefix over the waves); thread t < MSD_LW owns word t (activations 2t,
+// 2t + 1) and returns the two totals.
+__device__ __forceinline__ void msd_wave_prefix(uint32_t* wc, uint32_t tid, uint32_t& tlo, uint32_t& thi) {
+    tlo = 0;
+    thi = 0;
+    if (tid >= MSD_LW) return;
+#pragma unroll
+    for (int ww = 0; ww < MSD_NW; ++ww) {
+        const uint32_t v = wc[ww * MSD_LW + tid];
+        wc[ww * MSD_LW + tid] = tlo | (thi << 16);
+        tlo += v & 0xFFFFu;
+        thi += v >> 16;
+    }
+}
+
+template <bool G16>
+__global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const uint32_t* __restrict__ keys,
+                                                                      const uint32_t* __restrict__ idx,
+                                                                      const uint32_t* __restrict__ totals,
+                                                                      uint32_t n, uint32_t n_act,
+                                                                      uint32_t* __restrict__ perm,
+                                                                      uint32_t* __restrict__ offsets,
+                                                                      uint32_t* __restrict__ rank_out) {
+    constexpr int MSD_RW = MsdCfg<G16>::RW;
+    constexpr uint32_t MSD_CAP = MsdCfg<G16>::CAP;
     __shared__ uint32_t s_run[MSD_L];
     __shared__ uint32_t s_wc[MSD_NW][MSD_LW];
+    __shared__ typename MsdCfg<G16>::Out s_out[MSD_CAP];
     __shared__ uint32_t s_red[MSD_NW];
     __shared__ uint32_t s_base;
     const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
@@ -56,7 +94,7 @@ __global__ void __launch_bounds__(MSD_NT) k_msd_local(const uint32_t* __restrict
     for (uint32_t d = tid; d < b; d += MSD_NT) part += totals[d];
     for (int off = WAVE / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, WAVE);
     if (lane == 0) s_red[w] = part;
-    for (uint32_t k = tid; k < MSD_L; k += MSD_NT) s_run[k] = 0;
+    s_run[tid] = 0;
     __syncthreads();
     if (tid == 0) {
         uint32_t t = 0;
@@ -70,74 +108,125 @@ __global__ void __launch_bounds__(MSD_NT) k_msd_local(const uint32_t* __restrict
     const uint32_t L = min(MSD_L, n_act + 1 - k0);       // activations of this range
     const uint32_t* rk = keys + base;
     const uint32_t* ri = idx + base;
-    // sweep 1: counts, then starts (each thread 4 consecutive activations)
+    if (tid == 0 && b == (n_act >> MSD_SHIFT)) offsets[n_act + 1] = n;   // the range holding n_act: the end
+    for (uint32_t x = tid; x < MSD_NW * MSD_LW; x += MSD_NT) (&s_wc[0][0])[x] = 0;
+    if (S <= MSD_CAP) {
+        // staged: wave w takes the contiguous segment [s0, s1) of the range, the range-local keys
+        // (< 1,024; 0xFFFF past the segment) two to a register, every load in flight at once
+        const uint32_t seg = (S + MSD_NW - 1) / MSD_NW;
+        const uint32_t s0 = min(w * seg, S), s1 = min((w + 1) * seg, S);
+        uint32_t kp[MSD_RW / 2];
+#pragma unroll
+        for (int j = 0; j < MSD_RW / 2; ++j) kp[j] = 0xFFFFFFFFu;   // an empty range: no keys
+        if (S) {                                         // unconditional loads (clamped), selects after
+            const uint32_t last = S - 1;
+#pragma unroll
+            for (int r = 0; r < MSD_RW; r += 2) {
+                const uint32_t i = s0 + r * WAVE + lane;
+                const uint32_t a = rk[min(i, last)], c = rk[min(i + WAVE, last)];
+                kp[r / 2] = (i < s1 ? a - k0 : 0xFFFFu) | ((i + WAVE < s1 ? c - k0 : 0xFFFFu) << 16);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < MSD_RW; ++r) {
+            const uint32_t k = (kp[r / 2] >> (16 * (r & 1))) & 0xFFFFu;
+            if (k != 0xFFFFu) atomicAdd(&s_wc[w][k >> 1], 1u << (16 * (k & 1)));
+        }
+        // the rank sweep decodes the keys again rather than keeping the count sweep's addresses live
+        // across the barriers (that spilled)
+#pragma unroll
+        for (int j = 0; j < MSD_RW / 2; ++j) asm volatile("" : "+v"(kp[j]));
+        __syncthreads();
+        uint32_t tlo, thi;
+        msd_wave_prefix(&s_wc[0][0], tid, tlo, thi);
+        const uint32_t ex = block_excl_scan_add_n<MSD_NT>(tlo + thi, s_red);
+        if (tid < MSD_LW) {
+            s_run[2 * tid] = ex;
+            s_run[2 * tid + 1] = ex + tlo;
+            if (2 * tid < L) offsets[k0 + 2 * tid] = base + ex;
+            if (2 * tid + 1 < L) offsets[k0 + 2 * tid + 1] = base + ex + tlo;
+        }
+        __syncthreads();
+        // rows in order: the ranks stay stable.  G16 stages the message's place in the range, else the
+        // message index (loaded MSD_G rows at a time)
+#pragma unroll
+        for (int g = 0; g < MSD_RW; g += MSD_G) {
+            uint32_t mm[MSD_G];
+#pragma unroll
+            for (int r = 0; r < MSD_G && g + r < MSD_RW; ++r) {
+                const uint32_t i = s0 + (g + r) * WAVE + lane;
+                mm[r] = G16 ? i : (i < s1 ? ri[i] : 0u);
+            }
+#pragma unroll
+            for (int r = 0; r < MSD_G && g + r < MSD_RW; ++r) {
+                const uint32_t k = (kp[(g + r) / 2] >> (16 * ((g + r) & 1))) & 0xFFFFu;
+                if (k == 0xFFFFu) continue;
+                const uint32_t old = atomicAdd(&s_wc[w][k >> 1], 1u << (16 * (k & 1)));
+                s_out[s_run[k] + ((old >> (16 * (k & 1))) & 0xFFFFu)] = (typename MsdCfg<G16>::Out)mm[r];
+            }
+        }
+        __syncthreads();
+        constexpr int U = 4;                             // gathers in flight a lane
+        for (uint32_t i0 = 0; i0 < S; i0 += U * MSD_NT) {
+            uint32_t v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t i = i0 + u * MSD_NT + tid;
+                v[u] = i < S ? (G16 ? ri[s_out[i]] : (uint32_t)s_out[i]) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t i = i0 + u * MSD_NT + tid;
+                if (i < S) {
+                    perm[base + i] = v[u];
+                    if (rank_out) rank_out[v[u]] = base + i;
+                }
+            }
+        }
+        return;
+    }
+    // a hot range (a Zipf-hot activation): its whole histogram first, so every chunk knows each
+    // activation's start, then chunks of MSD_CAP ranked the same way with the indices stored straight
+    // to their global places (rolled loops reading the keys again: this form is not the common one)
     for (uint32_t i = tid; i < S; i += MSD_NT) atomicAdd(&s_run[rk[i] - k0], 1u);
     __syncthreads();
-    uint32_t c[4], sum = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        c[q] = s_run[4 * tid + q];
-        sum += c[q];
-    }
-    const uint32_t ex = block_excl_scan_add_n<MSD_NT>(sum, s_red);
     {
-        uint32_t run = ex;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t k = 4 * tid + q;
-            s_run[k] = run;
-            if (k < L) offsets[k0 + k] = base + run;
-            run += c[q];
-        }
+        const uint32_t ex = block_excl_scan_add_n<MSD_NT>(s_run[tid], s_red);
+        s_run[tid] = ex;
+        if (tid < L) offsets[k0 + tid] = base + ex;
     }
-    if (tid == 0 && b == (n_act >> MSD_SHIFT)) offsets[n_act + 1] = n;   // the range holding n_act: the end
-    __syncthreads();
-    // sweeps 2a / 2b over chunks of <= MSD_CHUNK messages
-    for (uint32_t c0 = 0; c0 < S; c0 += MSD_CHUNK) {
-        const uint32_t cs = min(MSD_CHUNK, S - c0);
+    for (uint32_t c0 = 0; c0 < S; c0 += MSD_CAP) {
+        const uint32_t cs = min(MSD_CAP, S - c0);
         const uint32_t seg = (cs + MSD_NW - 1) / MSD_NW;
         const uint32_t s0 = c0 + min(w * seg, cs), s1 = c0 + min((w + 1) * seg, cs);
-        for (uint32_t x = tid; x < MSD_NW * MSD_LW; x += MSD_NT) (&s_wc[0][0])[x] = 0;
         __syncthreads();
+#pragma unroll 1
         for (uint32_t i = s0 + lane; i < s1; i += WAVE) {
             const uint32_t k = rk[i] - k0;
             atomicAdd(&s_wc[w][k >> 1], 1u << (16 * (k & 1)));
         }
         __syncthreads();
-        // prefix over the waves: thread t owns words 2t, 2t + 1 (activations 4t .. 4t + 3)
-        uint32_t tot[2][2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint32_t word = 2 * tid + j;
-            uint32_t plo = 0, phi = 0;
-#pragma unroll
-            for (int ww = 0; ww < MSD_NW; ++ww) {
-                const uint32_t v = s_wc[ww][word];
-                s_wc[ww][word] = plo | (phi << 16);
-                plo += v & 0xFFFFu;
-                phi += v >> 16;
+        uint32_t tlo, thi;
+        msd_wave_prefix(&s_wc[0][0], tid, tlo, thi);
+        __syncthreads();
+#pragma unroll 1
+        for (uint32_t r0 = s0; r0 < s1; r0 += WAVE) {     // whole rows, so every lane keeps row order
+            const uint32_t i = r0 + lane;
+            if (i < s1) {
+                const uint32_t k = rk[i] - k0, m = ri[i];
+                const uint32_t old = atomicAdd(&s_wc[w][k >> 1], 1u << (16 * (k & 1)));
+                const uint32_t pos = base + s_run[k] + ((old >> (16 * (k & 1))) & 0xFFFFu);
+                perm[pos] = m;
+                if (rank_out) rank_out[m] = pos;
             }
-            tot[j][0] = plo;
-            tot[j][1] = phi;
         }
         __syncthreads();
-        for (uint32_t i = s0 + lane; i < s1; i += WAVE) {
-            const uint32_t k = rk[i] - k0;
-            const uint32_t old = atomicAdd(&s_wc[w][k >> 1], 1u << (16 * (k & 1)));
-            const uint32_t r = (old >> (16 * (k & 1))) & 0xFFFFu;
-            const uint32_t pos = base + s_run[k] + r;
-            const uint32_t m = ri[i];
-            perm[pos] = m;
-            if (rank_out) rank_out[m] = pos;
+        if (tid < MSD_LW) {
+            s_run[2 * tid] += tlo;
+            s_run[2 * tid + 1] += thi;
         }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint32_t word = 2 * tid + j;
-            s_run[2 * word] += tot[j][0];
-            s_run[2 * word + 1] += tot[j][1];
-        }
-        __syncthreads();
+        for (uint32_t x = tid; x < MSD_NW * MSD_LW; x += MSD_NT) (&s_wc[0][0])[x] = 0;
     }
 }
 

@@ -1,10 +1,11 @@
-"""The two-level bucketing (gd_msd.h, GD_MSD): a stable MSD pass into ranges of 4,096 activations,
+"""The two-level bucketing (gd_msd.h, GD_MSD): a stable MSD pass into ranges of 1,024 activations,
 then one workgroup per range sorting it in LDS and writing its bucket starts.  Its permutation and
 offsets must equal the stable partition of the oracle (o.bucket_stable: the per-activation FIFO,
 IncomingMessageAgent.cs:92-190, ActivationData.cs:566-606) and the LSD path's, for every shape the
-path takes: range edges, the unrouted bucket n_act, empty ranges, ranges over one u16 chunk (hot
-activations), and through the fused route + bucket and the receive path (which also asks for the
-inverse permutation)."""
+path takes: range edges, the unrouted bucket n_act, empty ranges, ranges staged in LDS and ranges
+over the staging capacity (hot activations: chunks stored straight to global memory), ranges either
+side of that capacity in one launch, the largest n_act the MSD digit takes, and through the fused
+route + bucket and the receive path (which also asks for the inverse permutation)."""
 import os
 
 import numpy as np
@@ -23,12 +24,14 @@ def gd():
     return g
 
 
-def _engine(gd, msd):
+def _engine(gd, msd, g16="0"):
     os.environ["GD_MSD"] = msd
+    os.environ["GD_MSD_G16"] = g16
     try:
         return gd.GrainDispatch(device=0, table_capacity=1 << 12)
     finally:
         os.environ.pop("GD_MSD", None)
+        os.environ.pop("GD_MSD_G16", None)
 
 
 SHAPES = [
@@ -37,7 +40,8 @@ SHAPES = [
     (1 << 22, 1 << 20, "uniform"),
     (3_000_017, 4096, "uniform"),
     (1_500_001, 4097, "uniform"),
-    (1 << 21, (1 << 21) - 1, "uniform"),
+    (1 << 21, 1056 * 1024 - 1, "uniform"),                     # the largest n_act of the MSD digit
+    (1 << 20, 43 * 1024 - 1, "uniform"),                       # ~24.4 K a range: either side of MSD_CAP
     (1 << 21, 1000, "uniform"),
     (1 << 21, 300_000, "unrouted"),
     (1 << 21, 1 << 20, "hot"),
@@ -59,10 +63,12 @@ def _acts(n, n_act, kind, seed):
     return a.astype(np.uint32)
 
 
+@pytest.mark.parametrize("g16", ["0", "1"])
 @pytest.mark.parametrize("n,n_act,kind", SHAPES)
-def test_msd_bucket_vs_oracle(gd, n, n_act, kind):
+def test_msd_bucket_vs_oracle(gd, n, n_act, kind, g16):
+    """g16: the range staging as the message indices (the default) or as u16 positions."""
     acts = _acts(n, n_act, kind, n + n_act)
-    e2, e0 = _engine(gd, "2"), _engine(gd, "0")
+    e2, e0 = _engine(gd, "2", g16), _engine(gd, "0")
     p2, off2 = e2.bucket(acts, n_act)
     p0, off0 = e0.bucket(acts, n_act)
     np.testing.assert_array_equal(p2, p0)
@@ -95,4 +101,37 @@ def test_msd_measured_choice_and_fused_route(gd):
         np.testing.assert_array_equal(act, want[2])
         np.testing.assert_array_equal(perm, wp)
         np.testing.assert_array_equal(off, wo)
+    e.close()
+
+
+def test_msd_receive_with_limits(gd):
+    """The receive path with overload limits asks the bucketing for the inverse permutation too
+    (each message's place in its context's FIFO, IncomingMessageAgent.cs:142 CheckOverloaded):
+    with the two-level form forced, statuses, contexts, permutation and offsets equal the oracle's."""
+    import torch
+    from test_gpu_receive import _world
+    import receive as rv
+    rng, keys, ctxs, flags, tg, ta, direction = _world(23, 1 << 18, 16, 1 << 21)
+    n_ctx, n = len(keys), len(tg)
+    e = _engine(gd, "2")
+    e.actdir_add(keys, ctxs, flags)
+    rc = rng.integers(0, 4, size=n_ctx).astype(np.uint32)
+    dev = torch.device("cuda:0")
+    d_tg = torch.from_numpy(tg.view(np.int64)).to(dev)
+    d_ta = torch.from_numpy(ta.view(np.int64)).to(dev)
+    d_dir = torch.from_numpy(direction).to(dev)
+    d_rc = torch.from_numpy(rc.view(np.int32)).to(dev)
+    ctx = torch.empty(n, dtype=torch.int32, device=dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    perm = torch.empty(n, dtype=torch.int32, device=dev)
+    off = torch.empty(n_ctx + 3, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    e.receive_device(d_tg.data_ptr(), d_ta.data_ptr(), d_dir.data_ptr(), n, n_ctx, ctx.data_ptr(), st.data_ptr(),
+                     perm.data_ptr(), off.data_ptr(), d_rc.data_ptr(), 2, 1)
+    e.synchronize()
+    w = rv.receive_batch_np(tg, ta, direction, keys, ctxs, flags, n_ctx, rc, 2, 1)
+    np.testing.assert_array_equal(st.cpu().numpy(), w[0])
+    np.testing.assert_array_equal(ctx.cpu().numpy().view(np.uint32), w[1])
+    np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), w[2])
+    np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), w[3])
     e.close()

@@ -1,11 +1,17 @@
-# Two-level bucketing (GD_MSD 0 LSD / 1 measured / 2 always): parity tests, then cfg 2 A/B.
+# Two-level bucketing (GD_MSD 0 LSD / 1 measured / 2 always; GD_MSD_G16 its staging form): parity
+# tests, then cfg 2 A/B.
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-.}
 OUT=gpurun_out/r03_msd_ab.txt
 : > $OUT
 timeout -k 10 400 python -u -m pytest tests/test_gpu_msd.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r03_msd_tests.log 2>&1 || { tail -40 gpurun_out/r03_msd_tests.log; exit 1; }
 for rep in 1 2; do
-for m in 0 2 1; do
-  GD_MSD=$m timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary --latency-batches 0 --steps 100 --warmup 10 > gpurun_out/ab.json 2>gpurun_out/ab.err || { tail -5 gpurun_out/ab.err; exit 2; }
-  echo "cfg2 GD_MSD=$m $(python -c "import json;d=json.loads(open('gpurun_out/ab.json').readlines()[-1]);print(round(d['value']/1e9,3), d['ms_per_step'], {k: v['ms_per_step'] for k, v in d.get('kernels', {}).items()})")" >> $OUT
+for m in "GD_MSD=0" "GD_MSD=2 GD_MSD_G16=0" "GD_MSD=2 GD_MSD_G16=1" "GD_MSD=1"; do
+  env $m timeout -k 10 300 python bench.py --no-cpu-baseline --no-secondary --latency-batches 0 --steps 100 --warmup 10 > gpurun_out/ab.json 2>gpurun_out/ab.err || { tail -5 gpurun_out/ab.err; exit 2; }
+  echo "cfg2 $m $(python -c "import json;d=json.loads(open('gpurun_out/ab.json').readlines()[-1]);print(round(d['value']/1e9,3), d['ms_per_step'], {k: v['ms_per_step'] for k, v in d.get('kernels', {}).items()})")" >> $OUT
+done; done
+for w in cfg3 cfg4; do
+for m in "GD_MSD=0" "GD_MSD=2" "GD_MSD=1"; do
+  env $m timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline --no-secondary --latency-batches 0 --steps 40 --warmup 10 > gpurun_out/ab.json 2>gpurun_out/ab.err || { tail -5 gpurun_out/ab.err; exit 2; }
+  echo "$w $m $(python -c "import json;d=json.loads(open('gpurun_out/ab.json').readlines()[-1]);print(round(d['value']/1e9,3), d['ms_per_step'], {k: v['ms_per_step'] for k, v in d.get('kernels', {}).items()})")" >> $OUT
 done; done
