@@ -67,12 +67,17 @@ def radix_layout(n: int, n_act: int):
     return passes, bits, packed
 
 
-def kernel_bytes(name: str, n: int, n_act: int, passes: int, world: int) -> float:
+def kernel_bytes(name: str, n: int, n_act: int, passes: int, world: int, form: str = "lsd") -> float:
     """Algorithmic HBM bytes of one step for a kernel (all launches of it), per
-    DESIGN.md 'Byte model'."""
+    DESIGN.md 'Byte model'.  form "msd": the two-level bucketing (gd_msd.h) -- one MSD pass reading
+    the activation (histogram, scatter) and writing (key, index), then k_msd_local reading (key,
+    index), writing the index in order and every bucket start once."""
     _, _, packed = radix_layout(n, n_act)
     if name == "k_route":
         return n * (24 + 32 + 4 + 4 + 1)          # key, one slot, silo+act+status
+    if form == "msd":
+        return {"k_radix_scatter": n * 12, "k_radix_hist": n * 4,
+                "k_msd_local": n * 12 + (n_act + 2) * 4}.get(name, 0.0)
     if name == "k_radix_scatter":
         # pass 1 reads act, writes (key, idx); middle passes move (key, idx); the last pass reads
         # (key, idx) and writes idx only (it emits the bucket starts instead of the sorted keys).
@@ -359,12 +364,13 @@ def main():
         e.set_kernel_timing(False)
 
     passes, _, packed = radix_layout(m_recv, n_act)
+    form = "msd" if kt.get("k_msd_local", (0, 0))[0] else "lsd"     # the bucketing form the library chose
     kernels = {}
     for name, (launches, ms) in kt.items():
         if launches == 0:
             continue
         per_step_ms = ms / args.profile_steps
-        b = kernel_bytes(name, m_recv, n_act, passes, world)
+        b = kernel_bytes(name, m_recv, n_act, passes, world, form)
         gbs = b / (per_step_ms * 1e-3) / 1e9 if b and per_step_ms > 0 else None
         kernels[name] = {"launches_per_step": launches // args.profile_steps, "ms_per_step": round(per_step_ms, 4),
                          "alg_GBps": round(gbs, 1) if gbs else None,
@@ -399,8 +405,8 @@ def main():
             alg = 16.0 * m_recv
             t_launch = sc["ms_per_step"] / sl * 1e-3
             ach = alg / t_launch / 1e9 if t_launch > 0 else None
-            impl = kernel_bytes("k_radix_scatter", m_recv, n_act, passes, world) / sl
-            roofline["bucketing_kernel"] = {
+            impl = kernel_bytes("k_radix_scatter", m_recv, n_act, passes, world, form) / sl
+            roofline["bucketing_kernel"] = {"form": form,
                 "kernel": "k_radix_scatter", "achieved": round(ach, 1) if ach else None, "peak": PEAK_HBM_GBS,
                 "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4) if ach else None, "traffic": sc_traffic,
                 "launches_per_step": sl, "alg_bytes_per_launch": alg, "bytes_model": "SURVEY 8(d): 16 B/record/pass",
@@ -410,6 +416,29 @@ def main():
                 # on the HBM bytes the PMC counters saw per launch (profiles/pmc_k_radix_scatter.json)
                 "frac_pmc": round(sc_traffic / t_launch / 1e9 / PEAK_HBM_GBS, 4) if sc_traffic and t_launch > 0
                 else None}
+            if form == "msd" and "k_msd_local" in kernels:
+                # the second level: each 1,024-activation range counting-sorted in LDS, written in order
+                ml = kernels["k_msd_local"]
+                t_ml = ml["ms_per_step"] / max(1, ml["launches_per_step"]) * 1e-3
+                ml_traffic = None
+                ml_pmc = os.path.join(ROOT, "profiles", "pmc_k_msd_local.json")
+                if os.path.exists(ml_pmc) and args.workload == "cfg2" and world == 1:
+                    with open(ml_pmc) as f:
+                        ml_traffic = json.load(f).get("hbm_bytes_per_launch")
+                roofline["bucketing_kernel"]["k_msd_local"] = {
+                    "impl_bytes_per_launch": kernel_bytes("k_msd_local", m_recv, n_act, passes, world, form),
+                    "avg_launch_ms": round(t_ml * 1e3, 5), "frac_impl": ml["frac_hbm"], "traffic": ml_traffic,
+                    "frac_pmc": round(ml_traffic / t_ml / 1e9 / PEAK_HBM_GBS, 4) if ml_traffic and t_ml > 0 else None}
+            # the whole bucketing stage against SURVEY 8(d)'s single-pass contract (read act, write perm:
+            # 12 B a message counting the 4-B bucket start the reference's per-activation FIFO implies)
+            stage = [k for k in ("k_radix_hist", "k_radix_rowscan", "k_radix_scatter", "k_msd_local",
+                                 "k_starts_rangescan", "k_bucket_starts", "k_scan_reduce", "k_scan_down") if k in kernels]
+            st_ms = sum(kernels[k]["ms_per_step"] for k in stage)
+            st_impl = sum(kernel_bytes(k, m_recv, n_act, passes, world, form) for k in stage)
+            roofline["bucketing_stage"] = {
+                "form": form, "kernels": stage, "ms_per_step": round(st_ms, 4),
+                "impl_bytes_per_message": round(st_impl / max(1, m_recv), 2), "contract_bytes_per_message": 12,
+                "frac_contract": round(12.0 * m_recv / (st_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4) if st_ms > 0 else None}
         if dom == "k_route":
             roofline["bytes_model"] = "SURVEY 8(d): key 24 + one 32-B directory slot + silo/act/status 9 B"
             if os.environ.get("GD_CX", "1") != "0":

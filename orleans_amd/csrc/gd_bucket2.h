@@ -31,7 +31,8 @@ constexpr uint32_t B2_R1 = 1u << B2_LOW_BITS;
 constexpr uint32_t B2_RMAX2 = 1056;                      // pass 2 digits: (n_act >> 10) + 1 <= 1056
 constexpr uint32_t B2_TILE = 16384;                      // items per tile, both passes
 
-// Histogram of TPB consecutive tiles per workgroup (NT x IT = B2_TILE), digit-major counts
+// Histogram of TPB consecutive tiles per workgroup (NT x IT items a tile: B2_TILE, or 8,192 for the
+// MSD pass's A/B form), digit-major counts
 // hist[d * tiles + t] for d < R.  FIRST: the digit of min(key, clamp) & 1023, and the grid pre-fills
 // the bucket starts (fill); else (pass 2) the digit of the already clamped key, key >> 10.  HI with
 // FIRST (the MSD pass of gd_msd.h): the raw keys clamped, their high digit.
@@ -40,7 +41,7 @@ __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restrict__ key
                                                 uint32_t R, uint32_t tiles, uint32_t* __restrict__ hist, FillArgs fill,
                                                 uint32_t xcd_rev) {
     constexpr uint32_t TILE = NT * IT;
-    static_assert(TILE == B2_TILE && IT % 4 == 0, "16-B loads over a B2 tile");
+    static_assert(TILE <= 65536 && IT % 4 == 0, "16-B loads, u16 tile positions");
     __shared__ uint32_t s_cnt[TPB][RMAX];
     for (uint32_t x = threadIdx.x; x < TPB * RMAX; x += NT) (&s_cnt[0][0])[x] = 0;
     __syncthreads();
@@ -107,7 +108,7 @@ __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ 
                                                    uint32_t xcd) {
     constexpr int NW = NT / WAVE;
     constexpr uint32_t TILE = NT * IT;
-    static_assert(TILE == B2_TILE && NW % 2 == 0, "B2 tiles, wave pairs");
+    static_assert(TILE <= 65536 && NW % 2 == 0, "u16 tile positions, wave pairs");
     constexpr uint32_t DPT = (RMAX + NT - 1) / NT;
     using Val = typename std::conditional<FIRST, uint16_t, uint32_t>::type;   // pass 1: position in the tile
     __shared__ uint32_t s_cnt[NW / 2][RMAX];             // wave pair (2p, 2p + 1): low / high 16 bits

@@ -175,6 +175,8 @@ struct gd_handle {
     // compact probe index (gd_cx.h): derived from the table, rebuilt after any change of it (GD_CX=0: off)
     int cx_mode = 1;            // 0 off, 1 measured (default), 2 index group reads, 3 index slot reads (GD_CX)
     int msd_mode = 1;           // two-level bucketing (gd_msd.h): 0 off, 1 measured (default), 2 always (GD_MSD)
+    uint32_t msd_tile = 8192;   // its MSD pass's tile: 8K items, two workgroups a CU (GD_MSD_TILE=16384: 16K, one;
+                                // measured slower, profiles/r03_msd_tile_ab.txt)
     bool msd_g16 = false;       // its range staging: u32 indices, 1 workgroup a CU (GD_MSD_G16=1: u16 positions, 2;
                                 // measured slower, profiles/r03_msd_ab.txt)
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
@@ -891,35 +893,47 @@ int bucket2_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_ac
                   B2_LOW_BITS, tot2, R2);
 }
 
-// The two-level bucketing (gd_msd.h): a stable MSD pass on the high digit min(act, n_act) >> 10 over
-// 16K-item tiles (the gd_bucket2.h kernels), then k_msd_local sorts each 1,024-activation range in
-// LDS and writes its starts.  Needs (n_act >> 10) + 1 <= B2_RMAX2.
-int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
-               uint32_t* rank_out) {
-    const uint32_t tiles = blocks_for(n, B2_TILE);
-    const uint32_t R = (n_act >> MSD_SHIFT) + 1;
-    if (R > MSD_MAX_RANGES) return set_err(h, GD_EINVAL, "two-level bucketing: n_act too large");
-    GD_TRY(ensure(h, h->hist, ((size_t)R * tiles + R) * sizeof(uint32_t)));
-    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
-    GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
-    uint32_t* hist = (uint32_t*)h->hist.p;
-    uint32_t* k1 = (uint32_t*)h->u32_a.p;
-    uint32_t* v1 = (uint32_t*)h->u32_c.p;
+// MSD pass on tiles of NT x 16 items: 8K (512 threads, two workgroups a CU, 32-B index runs at
+// R ~ 1,024; the default: 65 against 76 us at cfg 2) or 16K (1,024 threads, one a CU, 64-B runs).
+template <int NT>
+int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t R, uint32_t* hist, uint32_t* k1,
+             uint32_t* v1) {
+    constexpr uint32_t TILE = NT * 16;
+    const uint32_t tiles = blocks_for(n, TILE);
     const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
+    GD_TRY(ensure(h, h->hist, ((size_t)R * tiles + R) * sizeof(uint32_t)));
+    hist = (uint32_t*)h->hist.p;
     if (tiles >= 1024)
-        GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(1024), 0,
-                      k_b2_hist<1024, 16, 4, B2_RMAX2, true, true>, acts, n, n_act, R, tiles, hist,
+        GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0,
+                      k_b2_hist<NT, 16, 4, B2_RMAX2, true, true>, acts, n, n_act, R, tiles, hist,
                       FillArgs{nullptr, 0u, 0u}, hxr));
     else
-        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(1024), 0, k_b2_hist<1024, 16, 1, B2_RMAX2, true, true>, acts,
+        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_b2_hist<NT, 16, 1, B2_RMAX2, true, true>, acts,
                       n, n_act, R, tiles, hist, FillArgs{nullptr, 0u, 0u}, hxr));
     const uint32_t* tot = hist + (size_t)R * tiles;
     GD_TRY(launch(h, "k_radix_rowscan", dim3(R), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R * tiles));
-    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(1024), 0, k_b2_scatter<1024, 16, B2_RMAX2, true, true>, acts,
+    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_b2_scatter<NT, 16, B2_RMAX2, true, true>, acts,
                   (const uint32_t*)nullptr, n, n_act, R, tiles, (const uint32_t*)hist, tot, k1, v1, (uint32_t*)nullptr,
                   (uint32_t*)nullptr, h->xcd_tiles));
     h->last_totals = tot;
     h->last_digits = R;
+    return GD_OK;
+}
+
+// The two-level bucketing (gd_msd.h): a stable MSD pass on the high digit min(act, n_act) >> 10 (the
+// gd_bucket2.h kernels), then k_msd_local sorts each 1,024-activation range in LDS and writes its
+// starts.  Needs (n_act >> 10) + 1 <= B2_RMAX2.
+int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
+               uint32_t* rank_out) {
+    const uint32_t R = (n_act >> MSD_SHIFT) + 1;
+    if (R > MSD_MAX_RANGES) return set_err(h, GD_EINVAL, "two-level bucketing: n_act too large");
+    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
+    GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
+    uint32_t* k1 = (uint32_t*)h->u32_a.p;
+    uint32_t* v1 = (uint32_t*)h->u32_c.p;
+    if (h->msd_tile == 8192) GD_TRY(msd_pass<512>(h, acts, n, n_act, R, nullptr, k1, v1));
+    else GD_TRY(msd_pass<1024>(h, acts, n, n_act, R, nullptr, k1, v1));
+    const uint32_t* tot = h->last_totals;
     if (h->msd_g16)
         return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<true>, (const uint32_t*)k1,
                       (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
@@ -1297,6 +1311,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_CX")) h->cx_mode = std::max(0, std::min(3, std::atoi(v)));
     if (const char* v = std::getenv("GD_MSD")) h->msd_mode = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("GD_MSD_G16")) h->msd_g16 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_MSD_TILE")) h->msd_tile = std::atoi(v) == 16384 ? 16384u : 8192u;
     if (const char* v = std::getenv("GD_CX_SCALE")) h->cx_scale = std::atoi(v) == 2 ? 2u : 1u;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
     if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));

@@ -2,7 +2,7 @@
 // VERDICT r02 item 3): an MSD radix pass into ranges of MSD_L = 1,024 activations, then one
 // workgroup per range sorts it stably inside LDS and writes the range's bucket starts itself.
 //
-//   pass 1  k_b2_hist / row scan / k_b2_scatter (gd_bucket2.h, 16K-item tiles) with the high digit
+//   pass 1  k_b2_hist / row scan / k_b2_scatter (gd_bucket2.h, 8K-item tiles) with the high digit
 //           min(act, n_act) >> 10 (<= B2_RMAX2 ranges): every range's messages contiguous, in message
 //           order, keys and message indices 8 B a record;
 //   pass 2  k_msd_local, one 1,024-thread workgroup per range.  A range of <= MSD_CAP messages (the
@@ -21,7 +21,7 @@
 // Why the range is staged: the first form of this pass (ranges of 4,096 activations, 64 K messages,
 // too many for LDS) stored each index straight to global memory, and those 16 M scattered 4-B stores
 // cost 0.18 ms of its 0.25 ms (measured with the stores removed: profiles/r03_msd4k_nostore_exp.txt);
-// staged, the pass takes 0.054 ms at cfg 2 (profiles/r03_msd_ab.txt).
+// staged, the pass takes 0.054 ms at cfg 2 (profiles/r03_msd_ab.txt), the whole stage 0.148 ms.
 // Per message: pass 1 reads 4 B twice (histogram, scatter) and writes 8 B; pass 2 reads 8 B and
 // writes 4 B in order -- 24 B over 4 launches, against 40 B over 11 for three packed 7-bit LSD passes.  Output identical to the LSD path (both are the stable
 // partition by min(act, n_act)); the library times both per batch size and keeps the faster.

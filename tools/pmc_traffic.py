@@ -23,15 +23,26 @@ def main():
         for r in csv.DictReader(open(sys.argv[4])):
             nm = r["Name"].split("(")[0].replace("void ", "").replace("gd::", "")
             calls[nm] = calls.get(nm, 0) + int(r["Calls"])
+    # the bucketing form the library kept (its first launches time both): the two-level form
+    # (k_b2_hist / k_b2_scatter / k_msd_local, gd_msd.h) or the LSD passes (k_radix_*)
+    msd_calls = sum(v for k, v in calls.items() if k.startswith("k_msd_local"))
+    lsd_calls = max([v for k, v in calls.items() if k.startswith("k_radix_scatter<") and ", true," in k] or [0])
+    msd = msd_calls > lsd_calls if calls else any(k.startswith("gd::k_msd_local") for k in summ)
+    lsd_fams = ("k_radix_scatter", "k_radix_hist", "k_radix_hist_multi", "k_radix_hist16")
+    msd_fams = {"k_b2_scatter": "k_radix_scatter", "k_b2_hist": "k_radix_hist", "k_msd_local": "k_msd_local"}
     fam = {}
     for name, row in summ.items():
         base = name.split("<")[0].replace("gd::", "")
         if "rd_bytes_ea" not in row or "wr_bytes_ea" not in row:
             continue
-        if base not in ("k_route_m", "k_radix_scatter", "k_radix_hist", "k_radix_hist_multi", "k_radix_hist16",
-                        "k_route_hist"):
+        if base in ("k_route_m", "k_route_hist"):
+            key = "k_route" if base == "k_route_m" else base
+        elif not msd and base in lsd_fams:
+            key = "k_radix_hist" if base.startswith("k_radix_hist") else base
+        elif msd and base in msd_fams:
+            key = msd_fams[base]
+        else:
             continue
-        key = "k_route" if base == "k_route_m" else ("k_radix_hist" if base.startswith("k_radix_hist") else base)
         # the route's probe variants (index group reads / directory / index slot reads) are each timed on
         # a few launches before the library keeps one: with the kernel-trace stats (4th argument) count
         # the steady-state one only, the instantiation with the most calls
@@ -39,12 +50,13 @@ def main():
             mine = calls.get(name.replace("void ", "").replace("gd::", ""), 0)
             if mine < max(v for k, v in calls.items() if k.startswith("k_route_m<")):
                 continue
-        # launches per cfg 2 step (3 radix passes): the first pass's scatter (FIRST = true) and
-        # histogram (32-bit keys) once, the later passes' instantiations twice
+        # launches per cfg 2 step (3 LSD passes): the first pass's scatter (FIRST = true) and
+        # histogram (32-bit keys) once, the later passes' instantiations twice; the two-level form
+        # launches each of its kernels once
         w = 1.0
-        if key == "k_radix_scatter" and ", false," in name:
+        if not msd and key == "k_radix_scatter" and ", false," in name:
             w = 2.0
-        if base == "k_radix_hist16":
+        if not msd and base == "k_radix_hist16":
             w = 2.0
         fam.setdefault(key, []).append((name, row, w))
     out = {}
@@ -63,7 +75,8 @@ def main():
                     "raw_read_bytes_per_launch": rd_raw, "source": tag,
                     "method": "EA request counts x request size, separate --pmc passes; " + how +
                               "; averaged over the instantiations weighted by their launches per cfg 2 step "
-                              "(first radix pass once, later passes twice)"}
+                              "(LSD: first radix pass once, later passes twice; two-level form: once each)",
+                    "bucketing_form": "msd" if msd else "lsd"}
     for key, v in out.items():
         with open(f"profiles/pmc_{key}.json", "w") as f:
             json.dump(v, f, indent=1)
