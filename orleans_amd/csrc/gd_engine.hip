@@ -177,6 +177,8 @@ struct gd_handle {
     int msd_mode = 1;           // two-level bucketing (gd_msd.h): 0 off, 1 measured (default), 2 always (GD_MSD)
     uint32_t msd_tile = 8192;   // its MSD pass's tile: 8K items, two workgroups a CU (GD_MSD_TILE=16384: 16K, one;
                                 // measured slower, profiles/r03_msd_tile_ab.txt)
+    bool msd_early = false;     // its message indices loaded with the keys (GD_MSD_EARLY=1; measured slower,
+                                // profiles/r03_msd_early_ab.txt) or in the rank sweep
     bool msd_g16 = false;       // its range staging: u32 indices, 1 workgroup a CU (GD_MSD_G16=1: u16 positions, 2;
                                 // measured slower, profiles/r03_msd_ab.txt)
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
@@ -937,6 +939,9 @@ int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, u
     if (h->msd_g16)
         return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<true>, (const uint32_t*)k1,
                       (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
+    if (h->msd_early)
+        return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<false, true>, (const uint32_t*)k1,
+                      (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
     return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<false>, (const uint32_t*)k1,
                   (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
 }
@@ -1311,6 +1316,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_CX")) h->cx_mode = std::max(0, std::min(3, std::atoi(v)));
     if (const char* v = std::getenv("GD_MSD")) h->msd_mode = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("GD_MSD_G16")) h->msd_g16 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_MSD_EARLY")) h->msd_early = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_MSD_TILE")) h->msd_tile = std::atoi(v) == 16384 ? 16384u : 8192u;
     if (const char* v = std::getenv("GD_CX_SCALE")) h->cx_scale = std::atoi(v) == 2 ? 2u : 1u;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);

@@ -73,7 +73,7 @@ __device__ __forceinline__ void msd_wave_prefix(uint32_t* wc, uint32_t tid, uint
     }
 }
 
-template <bool G16>
+template <bool G16, bool EARLY = false>
 __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const uint32_t* __restrict__ keys,
                                                                       const uint32_t* __restrict__ idx,
                                                                       const uint32_t* __restrict__ totals,
@@ -81,6 +81,7 @@ __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const ui
                                                                       uint32_t* __restrict__ perm,
                                                                       uint32_t* __restrict__ offsets,
                                                                       uint32_t* __restrict__ rank_out) {
+    static_assert(!(G16 && EARLY), "G16 stages positions: no indices to load early");
     constexpr int MSD_RW = MsdCfg<G16>::RW;
     constexpr uint32_t MSD_CAP = MsdCfg<G16>::CAP;
     __shared__ uint32_t s_run[MSD_L];
@@ -118,6 +119,11 @@ __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const ui
         uint32_t kp[MSD_RW / 2];
 #pragma unroll
         for (int j = 0; j < MSD_RW / 2; ++j) kp[j] = 0xFFFFFFFFu;   // an empty range: no keys
+        // EARLY: the message indices are loaded right behind the keys and stay in registers (122 VGPRs),
+        // their latency under the count, prefix and scan phases -- measured slower at cfg 2 (0.058
+        // against 0.054 ms, profiles/r03_msd_early_ab.txt): the key and index streams then compete
+        // for the CU's share of HBM in the same phase; kept for A/B
+        uint32_t mi[EARLY ? MSD_RW : 1] = {};
         if (S) {                                         // unconditional loads (clamped), selects after
             const uint32_t last = S - 1;
 #pragma unroll
@@ -125,6 +131,10 @@ __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const ui
                 const uint32_t i = s0 + r * WAVE + lane;
                 const uint32_t a = rk[min(i, last)], c = rk[min(i + WAVE, last)];
                 kp[r / 2] = (i < s1 ? a - k0 : 0xFFFFu) | ((i + WAVE < s1 ? c - k0 : 0xFFFFu) << 16);
+            }
+            if constexpr (EARLY) {
+#pragma unroll
+                for (int r = 0; r < MSD_RW; ++r) mi[r] = ri[min(s0 + r * WAVE + lane, last)];
             }
         }
         __syncthreads();
@@ -156,7 +166,8 @@ __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const ui
 #pragma unroll
             for (int r = 0; r < MSD_G && g + r < MSD_RW; ++r) {
                 const uint32_t i = s0 + (g + r) * WAVE + lane;
-                mm[r] = G16 ? i : (i < s1 ? ri[i] : 0u);
+                if constexpr (EARLY) mm[r] = mi[g + r];
+                else mm[r] = G16 ? i : (i < s1 ? ri[i] : 0u);
             }
 #pragma unroll
             for (int r = 0; r < MSD_G && g + r < MSD_RW; ++r) {

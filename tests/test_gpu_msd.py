@@ -24,14 +24,20 @@ def gd():
     return g
 
 
-def _engine(gd, msd, g16="0"):
-    os.environ["GD_MSD"] = msd
-    os.environ["GD_MSD_G16"] = g16
+# the range staging forms of k_msd_local: the message indices loaded in the rank sweep (the default),
+# loaded with the keys, u16 positions with the indices gathered at write-out
+FORMS = {"late": {"GD_MSD_G16": "0", "GD_MSD_EARLY": "0"}, "early": {"GD_MSD_G16": "0", "GD_MSD_EARLY": "1"},
+         "g16": {"GD_MSD_G16": "1", "GD_MSD_EARLY": "0"}}
+
+
+def _engine(gd, msd, form="late"):
+    env = dict(FORMS[form], GD_MSD=msd)
+    os.environ.update(env)
     try:
         return gd.GrainDispatch(device=0, table_capacity=1 << 12)
     finally:
-        os.environ.pop("GD_MSD", None)
-        os.environ.pop("GD_MSD_G16", None)
+        for k in env:
+            os.environ.pop(k, None)
 
 
 SHAPES = [
@@ -63,12 +69,11 @@ def _acts(n, n_act, kind, seed):
     return a.astype(np.uint32)
 
 
-@pytest.mark.parametrize("g16", ["0", "1"])
+@pytest.mark.parametrize("form", list(FORMS))
 @pytest.mark.parametrize("n,n_act,kind", SHAPES)
-def test_msd_bucket_vs_oracle(gd, n, n_act, kind, g16):
-    """g16: the range staging as the message indices (the default) or as u16 positions."""
+def test_msd_bucket_vs_oracle(gd, n, n_act, kind, form):
     acts = _acts(n, n_act, kind, n + n_act)
-    e2, e0 = _engine(gd, "2", g16), _engine(gd, "0")
+    e2, e0 = _engine(gd, "2", form), _engine(gd, "0")
     p2, off2 = e2.bucket(acts, n_act)
     p0, off0 = e0.bucket(acts, n_act)
     np.testing.assert_array_equal(p2, p0)
