@@ -70,14 +70,15 @@ def radix_layout(n: int, n_act: int):
 def kernel_bytes(name: str, n: int, n_act: int, passes: int, world: int, form: str = "lsd") -> float:
     """Algorithmic HBM bytes of one step for a kernel (all launches of it), per
     DESIGN.md 'Byte model'.  form "msd": the two-level bucketing (gd_msd.h) -- one MSD pass reading
-    the activation (histogram, scatter) and writing (key, index), then k_msd_local reading (key,
-    index), writing the index in order and every bucket start once."""
+    the activation (histogram, scatter) and writing (index, range-local key) 6-B records, then
+    k_msd_local reading them, writing the index in order and every bucket start once."""
     _, _, packed = radix_layout(n, n_act)
     if name == "k_route":
         return n * (24 + 32 + 4 + 4 + 1)          # key, one slot, silo+act+status
     if form == "msd":
-        return {"k_radix_scatter": n * 12, "k_radix_hist": n * 4,
-                "k_msd_local": n * 12 + (n_act + 2) * 4}.get(name, 0.0)
+        rec = 6 if os.environ.get("GD_MSD_K16", "1") != "0" else 8      # u32 index + u16 (or u32) key
+        return {"k_radix_scatter": n * (4 + rec), "k_radix_hist": n * 4,
+                "k_msd_local": n * (rec + 4) + (n_act + 2) * 4}.get(name, 0.0)
     if name == "k_radix_scatter":
         # pass 1 reads act, writes (key, idx); middle passes move (key, idx); the last pass reads
         # (key, idx) and writes idx only (it emits the bucket starts instead of the sorted keys).

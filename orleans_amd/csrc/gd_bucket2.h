@@ -97,8 +97,9 @@ __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restrict__ key
 // starts (the first item of each key in a tile's digit run lowers starts[key] with atomicMin; the
 // run is sorted by the whole key because pass 1 ordered it), rank_out[index] = position on request.
 // gscan: the row-scanned counts (k_radix_rowscan), totals: the digit totals.  HI with FIRST (the MSD
-// pass of gd_msd.h): pass 1's inputs and outputs, ordered by the high digit key >> 10.
-template <int NT, int IT, int RMAX, bool FIRST, bool HI = !FIRST>
+// pass of gd_msd.h): pass 1's inputs and outputs, ordered by the high digit key >> 10; K16 writes
+// only the key's low 10 bits, as u16 (its digit is implied by the range it lands in).
+template <int NT, int IT, int RMAX, bool FIRST, bool HI = !FIRST, bool K16 = false>
 __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ keys_in,
                                                    const uint32_t* __restrict__ vals_in, uint32_t n, uint32_t clamp,
                                                    uint32_t R, uint32_t tiles, const uint32_t* __restrict__ gscan,
@@ -241,7 +242,8 @@ __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ 
             const uint32_t g = s_gbase[d] + p;
             if (g < n) {                  // always true when the counts are right; never write out of bounds
                 if constexpr (FIRST) {
-                    keys_out[g] = k;
+                    if constexpr (K16) reinterpret_cast<uint16_t*>(keys_out)[g] = (uint16_t)(k & (B2_R1 - 1));
+                    else keys_out[g] = k;
                     vals_out[g] = base + (uint32_t)s_val[p];
                 } else {
                     const uint32_t v = s_val[p];

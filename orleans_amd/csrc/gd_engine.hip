@@ -179,6 +179,7 @@ struct gd_handle {
                                 // measured slower, profiles/r03_msd_tile_ab.txt)
     bool msd_early = false;     // its message indices loaded with the keys (GD_MSD_EARLY=1; measured slower,
                                 // profiles/r03_msd_early_ab.txt) or in the rank sweep
+    bool msd_k16 = true;        // its MSD pass writes the range-local keys as u16 (GD_MSD_K16=0: u32 keys)
     bool msd_g16 = false;       // its range staging: u32 indices, 1 workgroup a CU (GD_MSD_G16=1: u16 positions, 2;
                                 // measured slower, profiles/r03_msd_ab.txt)
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
@@ -897,7 +898,7 @@ int bucket2_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_ac
 
 // MSD pass on tiles of NT x 16 items: 8K (512 threads, two workgroups a CU, 32-B index runs at
 // R ~ 1,024; the default: 65 against 76 us at cfg 2) or 16K (1,024 threads, one a CU, 64-B runs).
-template <int NT>
+template <int NT, bool K16>
 int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t R, uint32_t* hist, uint32_t* k1,
              uint32_t* v1) {
     constexpr uint32_t TILE = NT * 16;
@@ -914,7 +915,7 @@ int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uin
                       n, n_act, R, tiles, hist, FillArgs{nullptr, 0u, 0u}, hxr));
     const uint32_t* tot = hist + (size_t)R * tiles;
     GD_TRY(launch(h, "k_radix_rowscan", dim3(R), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R * tiles));
-    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_b2_scatter<NT, 16, B2_RMAX2, true, true>, acts,
+    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_b2_scatter<NT, 16, B2_RMAX2, true, true, K16>, acts,
                   (const uint32_t*)nullptr, n, n_act, R, tiles, (const uint32_t*)hist, tot, k1, v1, (uint32_t*)nullptr,
                   (uint32_t*)nullptr, h->xcd_tiles));
     h->last_totals = tot;
@@ -933,9 +934,18 @@ int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, u
     GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
     uint32_t* k1 = (uint32_t*)h->u32_a.p;
     uint32_t* v1 = (uint32_t*)h->u32_c.p;
-    if (h->msd_tile == 8192) GD_TRY(msd_pass<512>(h, acts, n, n_act, R, nullptr, k1, v1));
-    else GD_TRY(msd_pass<1024>(h, acts, n, n_act, R, nullptr, k1, v1));
+    const bool k16 = h->msd_k16 && !h->msd_g16 && !h->msd_early;
+    if (h->msd_tile == 8192) {
+        if (k16) GD_TRY((msd_pass<512, true>(h, acts, n, n_act, R, nullptr, k1, v1)));
+        else GD_TRY((msd_pass<512, false>(h, acts, n, n_act, R, nullptr, k1, v1)));
+    } else {
+        if (k16) GD_TRY((msd_pass<1024, true>(h, acts, n, n_act, R, nullptr, k1, v1)));
+        else GD_TRY((msd_pass<1024, false>(h, acts, n, n_act, R, nullptr, k1, v1)));
+    }
     const uint32_t* tot = h->last_totals;
+    if (k16)
+        return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<false, false, true>, (const uint32_t*)k1,
+                      (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
     if (h->msd_g16)
         return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<true>, (const uint32_t*)k1,
                       (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
@@ -1317,6 +1327,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_MSD")) h->msd_mode = std::max(0, std::min(2, std::atoi(v)));
     if (const char* v = std::getenv("GD_MSD_G16")) h->msd_g16 = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_MSD_EARLY")) h->msd_early = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_MSD_K16")) h->msd_k16 = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_MSD_TILE")) h->msd_tile = std::atoi(v) == 16384 ? 16384u : 8192u;
     if (const char* v = std::getenv("GD_CX_SCALE")) h->cx_scale = std::atoi(v) == 2 ? 2u : 1u;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);

@@ -4,7 +4,7 @@
 //
 //   pass 1  k_b2_hist / row scan / k_b2_scatter (gd_bucket2.h, 8K-item tiles) with the high digit
 //           min(act, n_act) >> 10 (<= B2_RMAX2 ranges): every range's messages contiguous, in message
-//           order, keys and message indices 8 B a record;
+//           order, message indices and range-local keys (key & 1023, u16) 6 B a record;
 //   pass 2  k_msd_local, one 1,024-thread workgroup per range.  A range of <= MSD_CAP messages (the
 //           uniform case: 16 K for BASELINE cfg 2) is held in registers, 24 rows a lane:
 //             count     per-wave counts (u16 pairs packed in u32 words: 16 x 512 words, 32 KB);
@@ -22,7 +22,7 @@
 // too many for LDS) stored each index straight to global memory, and those 16 M scattered 4-B stores
 // cost 0.18 ms of its 0.25 ms (measured with the stores removed: profiles/r03_msd4k_nostore_exp.txt);
 // staged, the pass takes 0.054 ms at cfg 2 (profiles/r03_msd_ab.txt), the whole stage 0.148 ms.
-// Per message: pass 1 reads 4 B twice (histogram, scatter) and writes 8 B; pass 2 reads 8 B and
+// Per message: pass 1 reads 4 B twice (histogram, scatter) and writes 6 B; pass 2 reads 6 B and
 // writes 4 B in order -- 24 B over 4 launches, against 40 B over 11 for three packed 7-bit LSD passes.  Output identical to the LSD path (both are the stable
 // partition by min(act, n_act)); the library times both per batch size and keeps the faster.
 #pragma once
@@ -73,7 +73,7 @@ __device__ __forceinline__ void msd_wave_prefix(uint32_t* wc, uint32_t tid, uint
     }
 }
 
-template <bool G16, bool EARLY = false>
+template <bool G16, bool EARLY = false, bool K16 = false>
 __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const uint32_t* __restrict__ keys,
                                                                       const uint32_t* __restrict__ idx,
                                                                       const uint32_t* __restrict__ totals,
@@ -107,7 +107,10 @@ __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const ui
     const uint32_t S = totals[b];
     const uint32_t k0 = b << MSD_SHIFT;
     const uint32_t L = min(MSD_L, n_act + 1 - k0);       // activations of this range
-    const uint32_t* rk = keys + base;
+    // K16: pass 1 wrote the range-local keys (key & 1023) as u16, 6 B a record instead of 8
+    using KT = typename std::conditional<K16, uint16_t, uint32_t>::type;
+    const KT* rk = reinterpret_cast<const KT*>(keys) + base;
+    const uint32_t koff = K16 ? 0u : k0;                 // what turns a stored key into a range-local one
     const uint32_t* ri = idx + base;
     if (tid == 0 && b == (n_act >> MSD_SHIFT)) offsets[n_act + 1] = n;   // the range holding n_act: the end
     for (uint32_t x = tid; x < MSD_NW * MSD_LW; x += MSD_NT) (&s_wc[0][0])[x] = 0;
@@ -130,7 +133,7 @@ __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const ui
             for (int r = 0; r < MSD_RW; r += 2) {
                 const uint32_t i = s0 + r * WAVE + lane;
                 const uint32_t a = rk[min(i, last)], c = rk[min(i + WAVE, last)];
-                kp[r / 2] = (i < s1 ? a - k0 : 0xFFFFu) | ((i + WAVE < s1 ? c - k0 : 0xFFFFu) << 16);
+                kp[r / 2] = (i < s1 ? a - koff : 0xFFFFu) | ((i + WAVE < s1 ? c - koff : 0xFFFFu) << 16);
             }
             if constexpr (EARLY) {
 #pragma unroll
@@ -200,7 +203,7 @@ __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const ui
     // a hot range (a Zipf-hot activation): its whole histogram first, so every chunk knows each
     // activation's start, then chunks of MSD_CAP ranked the same way with the indices stored straight
     // to their global places (rolled loops reading the keys again: this form is not the common one)
-    for (uint32_t i = tid; i < S; i += MSD_NT) atomicAdd(&s_run[rk[i] - k0], 1u);
+    for (uint32_t i = tid; i < S; i += MSD_NT) atomicAdd(&s_run[rk[i] - koff], 1u);
     __syncthreads();
     {
         const uint32_t ex = block_excl_scan_add_n<MSD_NT>(s_run[tid], s_red);
@@ -214,7 +217,7 @@ __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const ui
         __syncthreads();
 #pragma unroll 1
         for (uint32_t i = s0 + lane; i < s1; i += WAVE) {
-            const uint32_t k = rk[i] - k0;
+            const uint32_t k = rk[i] - koff;
             atomicAdd(&s_wc[w][k >> 1], 1u << (16 * (k & 1)));
         }
         __syncthreads();
@@ -225,7 +228,7 @@ __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const ui
         for (uint32_t r0 = s0; r0 < s1; r0 += WAVE) {     // whole rows, so every lane keeps row order
             const uint32_t i = r0 + lane;
             if (i < s1) {
-                const uint32_t k = rk[i] - k0, m = ri[i];
+                const uint32_t k = rk[i] - koff, m = ri[i];
                 const uint32_t old = atomicAdd(&s_wc[w][k >> 1], 1u << (16 * (k & 1)));
                 const uint32_t pos = base + s_run[k] + ((old >> (16 * (k & 1))) & 0xFFFFu);
                 perm[pos] = m;

@@ -24,10 +24,13 @@ def gd():
     return g
 
 
-# the range staging forms of k_msd_local: the message indices loaded in the rank sweep (the default),
-# loaded with the keys, u16 positions with the indices gathered at write-out
-FORMS = {"late": {"GD_MSD_G16": "0", "GD_MSD_EARLY": "0"}, "early": {"GD_MSD_G16": "0", "GD_MSD_EARLY": "1"},
-         "g16": {"GD_MSD_G16": "1", "GD_MSD_EARLY": "0"}}
+# the forms of the second level: the message indices loaded in k_msd_local's rank sweep and the
+# range-local keys as u16 records (the default); the same on u32 keys; the indices loaded with the
+# keys; u16 positions staged with the indices gathered at write-out
+FORMS = {"late": {"GD_MSD_G16": "0", "GD_MSD_EARLY": "0", "GD_MSD_K16": "1"},
+         "late32": {"GD_MSD_G16": "0", "GD_MSD_EARLY": "0", "GD_MSD_K16": "0"},
+         "early": {"GD_MSD_G16": "0", "GD_MSD_EARLY": "1", "GD_MSD_K16": "0"},
+         "g16": {"GD_MSD_G16": "1", "GD_MSD_EARLY": "0", "GD_MSD_K16": "0"}}
 
 
 def _engine(gd, msd, form="late"):
