@@ -899,13 +899,12 @@ int bucket2_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_ac
 // MSD pass on tiles of NT x 16 items: 8K (512 threads, two workgroups a CU, 32-B index runs at
 // R ~ 1,024; the default: 65 against 76 us at cfg 2) or 16K (1,024 threads, one a CU, 64-B runs).
 template <int NT, bool K16>
-int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t R, uint32_t* hist, uint32_t* k1,
-             uint32_t* v1) {
+int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t R, uint32_t* k1, uint32_t* v1) {
     constexpr uint32_t TILE = NT * 16;
     const uint32_t tiles = blocks_for(n, TILE);
     const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
     GD_TRY(ensure(h, h->hist, ((size_t)R * tiles + R) * sizeof(uint32_t)));
-    hist = (uint32_t*)h->hist.p;
+    uint32_t* hist = (uint32_t*)h->hist.p;
     if (tiles >= 1024)
         GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0,
                       k_b2_hist<NT, 16, 4, B2_RMAX2, true, true>, acts, n, n_act, R, tiles, hist,
@@ -936,11 +935,11 @@ int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, u
     uint32_t* v1 = (uint32_t*)h->u32_c.p;
     const bool k16 = h->msd_k16 && !h->msd_g16 && !h->msd_early;
     if (h->msd_tile == 8192) {
-        if (k16) GD_TRY((msd_pass<512, true>(h, acts, n, n_act, R, nullptr, k1, v1)));
-        else GD_TRY((msd_pass<512, false>(h, acts, n, n_act, R, nullptr, k1, v1)));
+        if (k16) GD_TRY((msd_pass<512, true>(h, acts, n, n_act, R, k1, v1)));
+        else GD_TRY((msd_pass<512, false>(h, acts, n, n_act, R, k1, v1)));
     } else {
-        if (k16) GD_TRY((msd_pass<1024, true>(h, acts, n, n_act, R, nullptr, k1, v1)));
-        else GD_TRY((msd_pass<1024, false>(h, acts, n, n_act, R, nullptr, k1, v1)));
+        if (k16) GD_TRY((msd_pass<1024, true>(h, acts, n, n_act, R, k1, v1)));
+        else GD_TRY((msd_pass<1024, false>(h, acts, n, n_act, R, k1, v1)));
     }
     const uint32_t* tot = h->last_totals;
     if (k16)

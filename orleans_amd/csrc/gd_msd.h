@@ -82,6 +82,7 @@ __global__ void __launch_bounds__(MSD_NT, MsdCfg<G16>::WPE) k_msd_local(const ui
                                                                       uint32_t* __restrict__ offsets,
                                                                       uint32_t* __restrict__ rank_out) {
     static_assert(!(G16 && EARLY), "G16 stages positions: no indices to load early");
+    static_assert(MSD_NT == (int)MSD_L && MSD_LW <= (uint32_t)MSD_NT, "one thread per activation of a range");
     constexpr int MSD_RW = MsdCfg<G16>::RW;
     constexpr uint32_t MSD_CAP = MsdCfg<G16>::CAP;
     __shared__ uint32_t s_run[MSD_L];
