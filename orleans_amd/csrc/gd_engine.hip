@@ -194,7 +194,7 @@ struct gd_handle {
         bool pending[CXV] = {};
         uint64_t n[CXV] = {};
     };
-    std::map<int, CxTune> cx_tune;   // key: kind * 64 + size class (bit length of n)
+    std::map<int, CxTune> cx_tune;   // key: (kind * 64 + size class (bit length of n)) * 32 + a second class
     uint64_t tab_gen = 0;       // bumped by every launch that takes the table as a writable Slot*
     bool cx_built = false, cx_ok = false;
     const Slot* cx_slots_at = nullptr;
@@ -465,12 +465,12 @@ int cx_ensure(gd_handle* h, bool* ok) {
 // the key distribution (a Zipf-hot set favours small reads, a uniform one the index's group reads,
 // DESIGN 5).  nvar: the variants this launch kind has (2: no 16-B-read form).  *meas: the tune entry
 // this launch is timed into (key * CXV + variant), or -1.
-int tune_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar) {
+int tune_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar, int sub = 0) {
     constexpr int V = gd_handle::CXV;
     *meas = -1;
     int cls = 0;
     while (cls < 63 && (n >> cls) > 1) ++cls;
-    const int key = kind * 64 + cls;
+    const int key = (kind * 64 + cls) * 32 + std::max(0, std::min(31, sub));   // sub: a second shape class
     auto& t = h->cx_tune[key];
     bool any_pending = false;
     for (int v = 0; v < V; ++v) {
@@ -969,7 +969,12 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
     const bool msd_ok = h->msd_mode && n >= (1u << 20) && (n_act >> MSD_SHIFT) + 1 <= MSD_MAX_RANGES && !h->bucket2;
     if (msd_ok) {
         int meas = -1;
-        const int var = h->msd_mode == 2 ? 1 : tune_choose(h, 4, n, &meas, 2);
+        // keyed by the batch size and by the messages a range holds (which decide whether ranges are
+        // staged in LDS): a handle bucketing 16M messages over 1M and over 10k activations keeps one
+        // choice for each
+        int per_range = 0;
+        while (per_range < 31 && ((uint64_t)n / ((n_act >> MSD_SHIFT) + 1) >> per_range) > 1) ++per_range;
+        const int var = h->msd_mode == 2 ? 1 : tune_choose(h, 4, n, &meas, 2, per_range);
         CxMeasure m(h, meas, n);
         if (var == 1) return msd_bucket(h, acts, n, n_act, perm, offsets, rank_out);
         return bucket_lsd(h, acts, n, n_act, perm, offsets, rank_out);
@@ -1416,7 +1421,7 @@ void gd_destroy(gd_handle* h) {
     free_buf(h->cxi_types);
     free_buf(h->cxi_ctr);
     for (auto& kt : h->cx_tune)
-        for (int v = 0; v < 2; ++v) {
+        for (int v = 0; v < gd_handle::CXV; ++v) {
             auto& t = kt.second;
             if (t.a[v]) (void)hipEventDestroy(t.a[v]);
             if (t.b[v]) (void)hipEventDestroy(t.b[v]);

@@ -143,3 +143,18 @@ def test_msd_receive_with_limits(gd):
     np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), w[2])
     np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), w[3])
     e.close()
+
+
+def test_msd_measured_choice_per_shape(gd):
+    """The measured choice is kept per batch size and per messages-a-range class: one handle
+    alternating 2^21 messages over 2^20 activations (ranges staged in LDS) and over 10,000 (ranges
+    far over the staging capacity) stays bit-exact on every launch, through both forms' timing."""
+    e = _engine(gd, "1")
+    shapes = [(_acts(1 << 21, 1 << 20, "uniform", 5), 1 << 20), (_acts(1 << 21, 10000, "uniform", 6), 10000)]
+    want = [o.bucket_stable(a, na) for a, na in shapes]
+    for i in range(10):
+        a, na = shapes[i % 2]
+        p, off = e.bucket(a, na)
+        np.testing.assert_array_equal(p, want[i % 2][0])
+        np.testing.assert_array_equal(off, want[i % 2][1])
+    e.close()
