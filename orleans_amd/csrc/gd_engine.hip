@@ -179,6 +179,7 @@ struct gd_handle {
                                 // measured slower, profiles/r03_msd_tile_ab.txt)
     bool msd_early = false;     // its message indices loaded with the keys (GD_MSD_EARLY=1; measured slower,
                                 // profiles/r03_msd_early_ab.txt) or in the rank sweep
+    uint32_t msd_htpb = 4;      // its MSD histogram's tiles a workgroup from 1,024 tiles up (GD_MSD_HTPB: 1, 2, 4)
     bool msd_k16 = true;        // its MSD pass writes the range-local keys as u16 (GD_MSD_K16=0: u32 keys)
     bool msd_g16 = false;       // its range staging: u32 indices, 1 workgroup a CU (GD_MSD_G16=1: u16 positions, 2;
                                 // measured slower, profiles/r03_msd_ab.txt)
@@ -905,9 +906,14 @@ int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uin
     const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
     GD_TRY(ensure(h, h->hist, ((size_t)R * tiles + R) * sizeof(uint32_t)));
     uint32_t* hist = (uint32_t*)h->hist.p;
-    if (tiles >= 1024)
+    const uint32_t tpb = tiles >= 1024 ? h->msd_htpb : 1u;
+    if (tpb == 4)
         GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0,
                       k_b2_hist<NT, 16, 4, B2_RMAX2, true, true>, acts, n, n_act, R, tiles, hist,
+                      FillArgs{nullptr, 0u, 0u}, hxr));
+    else if (tpb == 2)
+        GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 2)), dim3(NT), 0,
+                      k_b2_hist<NT, 16, 2, B2_RMAX2, true, true>, acts, n, n_act, R, tiles, hist,
                       FillArgs{nullptr, 0u, 0u}, hxr));
     else
         GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_b2_hist<NT, 16, 1, B2_RMAX2, true, true>, acts,
@@ -1332,6 +1338,10 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (const char* v = std::getenv("GD_MSD_G16")) h->msd_g16 = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_MSD_EARLY")) h->msd_early = std::atoi(v) != 0;
     if (const char* v = std::getenv("GD_MSD_K16")) h->msd_k16 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("GD_MSD_HTPB")) {
+        const int t = std::atoi(v);
+        h->msd_htpb = t == 1 || t == 2 ? (uint32_t)t : 4u;
+    }
     if (const char* v = std::getenv("GD_MSD_TILE")) h->msd_tile = std::atoi(v) == 16384 ? 16384u : 8192u;
     if (const char* v = std::getenv("GD_CX_SCALE")) h->cx_scale = std::atoi(v) == 2 ? 2u : 1u;
     if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
