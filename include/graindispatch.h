@@ -847,6 +847,56 @@ int gd_kernel_times(gd_handle* h, gd_kernel_time* out, uint32_t max, uint32_t* o
 int gd_kernel_times_reset(gd_handle* h);
 int gd_set_kernel_timing(gd_handle* h, int enable);
 
+/* ---- handle options (no reference counterpart: the reference has no device kernels) ------------
+ * Round 4 replaces the library's GD_* environment switches: a host's behaviour no longer depends on
+ * its environment, only on these calls.  Every option changes speed only, never results (the parity
+ * tests run both sides of each one that changes a data layout); the defaults are the measured
+ * winners.  Exchange options are per sender and may differ between ranks. */
+#define GD_OPT_PROBE        1   /* route probe: 0 directory, 1 measured per launch kind (default),
+                                   2 compact index in 64-B group reads, 3 compact index in 16-B slot reads */
+#define GD_OPT_BUCKET       2   /* bucketing: 0 LSD passes, 1 measured (default), 2 the two-level form
+                                   wherever it applies (batches >= 2^20 messages, n_act < 2^28) */
+#define GD_OPT_L2_SMALL     3   /* two-level three-pass form: ranges of at most this many messages are
+                                   sorted one wave a range (default 1024) */
+#define GD_OPT_STABLE_RANK  4   /* LSD passes' in-tile rank: 1 ds_add_rtn (default when the creation
+                                   self-check passed), 0 ballots (stable by construction) */
+#define GD_OPT_WIRE_HEADERS 5   /* exchange headers of one-type long-key batches: 0 24-B keys, 1 u64
+                                   N1s, 2 u32 N1s when every N1 < 2^32 (default) */
+#define GD_OPT_REGION_PROBE 6   /* exchange: (rank, region) partition + region-mapped owner probe: 0 (default) / 1 */
+#define GD_OPT_IDX16        7   /* exchange at W > 1: 2-B origin indices on the wire: 1 (default) / 0 */
+#define GD_OPT_HOST_CHUNK   8   /* host-pointer gd_route / gd_route_bucket: messages a pipelined chunk
+                                   (default 2,097,152; 0 = one chunk, the serial copies) */
+#define GD_OPT_MB_ZEROCOPY  9   /* micro-batches created after: I/O from / to pinned host memory: 1 (default)
+                                   / 0 staged copies */
+#define GD_OPT_MB_SPLIT     10  /* micro-batches created after: redundant sorters splitting the host stores (8) */
+#define GD_OPT_MB_TRACE     11  /* micro-batches created after: per-phase timestamps printed at destroy (0) */
+int gd_option_set(gd_handle* h, int option, int64_t value);
+int gd_option_get(const gd_handle* h, int option, int64_t* value);
+
+/* ---- measured choices -------------------------------------------------------------------------
+ * With GD_OPT_PROBE / GD_OPT_BUCKET at 1 the library times its interchangeable variants on the first
+ * launches of each launch kind and size class (HIP events, read without a stream sync) and keeps the
+ * fastest per message.  These calls let a host see, pin and share those choices, so that performance
+ * is deterministic: pinned choices run from the first launch; gd_tune_agree makes every rank of the
+ * communicator run the same variant. */
+#define GD_TUNE_PROBE_KEYS   0  /* k_route over 24-B keys: 0 index groups, 1 directory, 2 index slots */
+#define GD_TUNE_PROBE_N1     1  /* the exchange owner's probe over received N1s: same variants */
+#define GD_TUNE_PROBE_FANOUT 2  /* k_fan_route: 0 index groups, 1 directory */
+#define GD_TUNE_PROBE_NODES  3  /* the sharded fan-out owner's probe: 0 index groups, 1 directory */
+#define GD_TUNE_BUCKET       4  /* bucketing: 0 LSD passes, 1 the two-level form */
+#define GD_TUNE_KINDS        5
+int gd_tune_reset(gd_handle* h);                         /* forget every measured choice */
+/* Pin kind's choice for every size (variant >= 0), or return it to measuring (-1). */
+int gd_tune_set(gd_handle* h, int kind, int variant);
+/* The choice a launch of kind over n messages (sub: the bucketing's messages-a-range class, else 0)
+ * would take: the pinned or measured variant, or -1 while still measuring. */
+int gd_tune_get(gd_handle* h, int kind, uint64_t n, uint32_t sub, int* variant);
+/* Collective over the handle's communicator (gd_comm_init*): every rank contributes its finished
+ * measurements (best time per message of each variant of each kind and size class) and every rank
+ * keeps, per entry any rank finished, the variant with the least summed time -- the same pick on every
+ * rank.  Entries no rank finished keep measuring. */
+int gd_tune_agree(gd_handle* h);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,6 +21,7 @@
 #include "gd_cache.h"
 #include "gd_cx.h"
 #include "gd_msd.h"
+#include "gd_msd2.h"
 #include "gd_shard.h"
 #include "gd_comm.h"
 #include "gd_localcomm.h"
@@ -169,20 +170,17 @@ struct gd_handle {
     uint64_t routed = 0;
 
     // kernel tuning (defaults measured on MI355X; GD_ROUTE_M / GD_ROUTE_NT override for A/B runs)
-    int route_m = 1;
-    bool route_nt = false;
     bool route_xcd = true;      // route workgroups over XCD-contiguous message ranges (GD_ROUTE_XCD)
     // compact probe index (gd_cx.h): derived from the table, rebuilt after any change of it (GD_CX=0: off)
     int cx_mode = 1;            // 0 off, 1 measured (default), 2 index group reads, 3 index slot reads (GD_CX)
-    int msd_mode = 1;           // two-level bucketing (gd_msd.h): 0 off, 1 measured (default), 2 always (GD_MSD)
-    uint32_t msd_tile = 8192;   // its MSD pass's tile: 8K items, two workgroups a CU (GD_MSD_TILE=16384: 16K, one;
-                                // measured slower, profiles/r03_msd_tile_ab.txt)
-    bool msd_early = false;     // its message indices loaded with the keys (GD_MSD_EARLY=1; measured slower,
-                                // profiles/r03_msd_early_ab.txt) or in the rank sweep
-    uint32_t msd_htpb = 4;      // its MSD histogram's tiles a workgroup from 1,024 tiles up (GD_MSD_HTPB: 1, 2, 4)
-    bool msd_k16 = true;        // its MSD pass writes the range-local keys as u16 (GD_MSD_K16=0: u32 keys)
-    bool msd_g16 = false;       // its range staging: u32 indices, 1 workgroup a CU (GD_MSD_G16=1: u16 positions, 2;
-                                // measured slower, profiles/r03_msd_ab.txt)
+    bool mb_zero_copy = true;   // micro-batches: I/O from / to pinned host memory (GD_OPT_MB_ZEROCOPY)
+    uint32_t mb_split = 8;      // micro-batches: redundant sorters splitting the host stores (GD_OPT_MB_SPLIT)
+    bool mb_trace = false;      // micro-batches: per-phase timestamps (GD_OPT_MB_TRACE)
+    int tune_pin[GD_TUNE_KINDS] = {-1, -1, -1, -1, -1};   // gd_tune_set: pinned variant per kind, -1 measured
+    int msd_mode = 1;           // two-level bucketing (gd_msd.h, gd_msd2.h): 0 off, 1 measured (default), 2 always (GD_MSD)
+    uint32_t l2_small = 1024;   // three-pass form: ranges of at most this many messages are sorted one wave a range
+    DevBuf m3[12];              // three-pass form's scratch (msd3_bucket)
+    DevBuf tune_buf;            // gd_tune_agree's send / receive records
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
     // per launch kind and size class: the probe variant, timed on live launches.  Variants: 0 the index
     // in 64-B group reads, 1 the directory, 2 the index in 16-B slot reads
@@ -202,27 +200,17 @@ struct gd_handle {
     uint64_t cx_cap_at = 0, cx_gen_at = 0;
     uint32_t cx_rounds = 0;
     DevBuf cxi_tab, cxi_types, cxi_ctr;
-    int radix_max_bits = 8;   // digit width cap (GD_RADIX_MAXBITS, 4..11)
-    int radix_cfg = 1;   // 512-thread tiles of 8 messages per thread (A/B: tools/ab_bucket.py)
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
-    uint32_t hist_tpb = 0;      // tiles per workgroup in the radix histogram, 1/4/8 (GD_HIST_TPB); 0 = by size
     bool hist_xcd = true;       // multi-tile histograms in reverse XCD tile order (GD_HIST_XCD)
     bool compact_headers = true;    // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
     bool region_probe = false;      // gd_route_multi: chunks ordered by table region, region-mapped probe (GD_REGION_PROBE)
     bool idx16 = true;              // gd_route_multi: 2-B origin indices on the wire (KD_IDX16, GD_IDX16)
     bool pack_pay16 = false;        // set by route_multi around its partition: the scatter writes u16 payloads
     bool narrow_headers = true;     // compact headers as u32 N1s when every N1 < 2^32 (GD_NARROW_HEADERS=0: u64)
-    bool fused_starts = true;   // last radix pass emits the bucket starts (GD_FUSED_STARTS=0: k_bucket_starts)
-    bool radix_pack = true;     // 6-B packed records between radix passes when they fit (GD_RADIX_PACK)
-    bool radix_rowscan = true;  // one scan launch per radix pass, digit rows (GD_RADIX_ROWSCAN=0: reduce + down)
-    bool fill_in_hist = true;   // the first histogram pre-fills the bucket starts (GD_FILL_IN_HIST=0: k_fill)
-    bool range_scan = true;     // bucket starts: one range-scan launch when it applies (GD_RANGE_SCAN=0: reduce + down)
     bool shard_gather = true;   // exchange partition of keys: k_shard_gather (GD_SHARD_GATHER=0: k_shard_scatter, staged keys)
     const uint32_t* last_totals = nullptr;   // the last radix pass's digit totals (row scans), and their count
     uint32_t last_digits = 0;
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
-    int fan_ilp = 2;                  // fan-out items per thread in flight together (GD_FAN_ILP: 1, 2, 4)
-    bool bucket2 = false;             // two wide-digit passes on 16K-item tiles (GD_BUCKET2=1; measured slower)
 
     // pinned host scratch for small device -> host read-backs (counts, totals)
     void* h_pin = nullptr;
@@ -411,7 +399,10 @@ unsigned long long pow2_at_least(unsigned long long x) {
 // ---- compact probe index (gd_cx.h) ----------------------------------------------
 // The index for the current table: rebuilt (two passes + one host sync) when the table changed since
 // the last build; false when the table is not eligible (an N0 != 0 key, too many types) or GD_CX=0.
-int cx_ensure(gd_handle* h, bool* ok) {
+// n: the messages of the launch asking.  A stale index is rebuilt only for a launch of at least
+// capacity / 16 messages: a small route after a directory write takes the directory probe instead of a
+// full-table pass and a host sync; the next large launch rebuilds.
+int cx_ensure(gd_handle* h, bool* ok, uint64_t n) {
     *ok = false;
     if (!h->cx_mode || !h->slots || h->capacity < CX_GROUP) return GD_OK;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;   // a captured graph keeps the directory probe
@@ -422,6 +413,7 @@ int cx_ensure(gd_handle* h, bool* ok) {
         *ok = h->cx_ok;
         return GD_OK;
     }
+    if (h->cx_mode == 1 && n < h->capacity / 16) return GD_OK;
     const unsigned long long cap = h->capacity * h->cx_scale;
     GD_TRY(ensure(h, h->cxi_tab, cap * 16));
     GD_TRY(ensure(h, h->cxi_types, CX_TYPES * 8));
@@ -439,7 +431,8 @@ int cx_ensure(gd_handle* h, bool* ok) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     h->cx_built = true;
     h->cx_ok = c.flag == 0 && c.full == 0;
-    for (auto& kt : h->cx_tune) {                   // a new table: measure the probes again
+    for (auto& kt : h->cx_tune) {                   // a new table: measure the probes again (not the bucketing)
+        if (kt.first / (64 * 32) == GD_TUNE_BUCKET) continue;
         auto& t = kt.second;
         for (int v = 0; v < gd_handle::CXV; ++v) {
             if (t.pending[v]) (void)hipEventSynchronize(t.b[v]);
@@ -466,13 +459,20 @@ int cx_ensure(gd_handle* h, bool* ok) {
 // the key distribution (a Zipf-hot set favours small reads, a uniform one the index's group reads,
 // DESIGN 5).  nvar: the variants this launch kind has (2: no 16-B-read form).  *meas: the tune entry
 // this launch is timed into (key * CXV + variant), or -1.
-int tune_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar, int sub = 0) {
-    constexpr int V = gd_handle::CXV;
-    *meas = -1;
+// The tune entry's key: kind, size class (bit length of n), a second shape class.
+int tune_key(int kind, uint64_t n, int sub) {
     int cls = 0;
     while (cls < 63 && (n >> cls) > 1) ++cls;
-    const int key = (kind * 64 + cls) * 32 + std::max(0, std::min(31, sub));   // sub: a second shape class
-    auto& t = h->cx_tune[key];
+    return (kind * 64 + cls) * 32 + std::max(0, std::min(31, sub));
+}
+
+// Variants of a tune kind (GD_TUNE_*): the 24-B-key and N1 probes have three, the rest two.
+int tune_nvar(int kind) { return kind <= 1 ? gd_handle::CXV : 2; }
+
+// Folds the entry's finished timings in (events read without a stream sync, unless the entry has
+// timed every variant twice and only waits for them) and picks when every variant is timed.
+void tune_resolve(gd_handle::CxTune& t, int nvar) {
+    constexpr int V = gd_handle::CXV;
     bool any_pending = false;
     for (int v = 0; v < V; ++v) {
         if (!t.pending[v]) continue;
@@ -490,6 +490,25 @@ int tune_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar, int sub
         for (int v = 1; v < nvar; ++v)
             if (t.best[v] < t.best[t.pick]) t.pick = v;
     }
+}
+
+// The probe variant for a launch of `kind` (0 keys, 1 N1s, 2 fan-out, 3 node ids) over n messages when
+// the index is available: 0 the index read in 64-B groups, 1 the directory, 2 the index read one 16-B
+// slot at a time; kind 4: the bucketing form.  A variant pinned by gd_tune_set is taken at once.
+// Else the first launches of the kind and size class (bit length of n: the fan-out's hops differ 10x
+// in size, and per-message cost with them) time the variants, twice each in turn, between HIP events
+// read back without a stream sync at the next choice, and the fastest per message is kept (or the one
+// gd_tune_agree settled on).  All give the same results; which is fastest depends on the key
+// distribution (a Zipf-hot set favours small reads, a uniform one the index's group reads).
+// nvar: the variants this launch kind has.  *meas: the tune entry this launch is timed into
+// (key * CXV + variant), or -1.
+int tune_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar, int sub = 0) {
+    constexpr int V = gd_handle::CXV;
+    *meas = -1;
+    if (h->tune_pin[kind] >= 0 && h->tune_pin[kind] < nvar) return h->tune_pin[kind];
+    const int key = tune_key(kind, n, sub);
+    auto& t = h->cx_tune[key];
+    tune_resolve(t, nvar);
     if (t.pick >= 0) return t.pick;
     const int v = t.round % nvar;
     if (t.round < 2 * nvar && !t.pending[v]) {
@@ -535,7 +554,7 @@ CxArgs cx_args(gd_handle* h) {
 template <int MODE, int M, bool NT>
 int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
     bool cx = false;
-    GD_TRY(cx_ensure(h, &cx));
+    GD_TRY(cx_ensure(h, &cx, n));
     int meas = -1;
     const int var = cx ? cx_choose(h, 0, n, &meas) : 1;
     CxMeasure m(h, meas, n);
@@ -560,7 +579,7 @@ int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uin
     const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
     const uint32_t xcd = h->route_xcd ? 1u : 0u;
     bool cx = false;
-    GD_TRY(cx_ensure(h, &cx));
+    GD_TRY(cx_ensure(h, &cx, n));
     int meas = -1;
     const int var = cx ? cx_choose(h, 1, n, &meas) : 1;
     CxMeasure m(h, meas, n);
@@ -630,17 +649,11 @@ int route_region_device(gd_handle* h, const void* k, uint32_t n1w, uint64_t tcd,
     }
 }
 
+// One message a thread, plain (temporal) key reads: 2 a thread and non-temporal streams measured no
+// faster (0.533 / 0.533-0.535 against 0.530-0.531 ms a cfg 2 step, profiles/r03_route_cx_ab.txt).
 template <int MODE>
 int route_mode(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
-    const bool nt = h->route_nt;
-    switch (h->route_m) {
-        case 1: return nt ? route_launch<MODE, 1, true>(h, keys, n, silo, act, status)
-                          : route_launch<MODE, 1, false>(h, keys, n, silo, act, status);
-        case 4: return nt ? route_launch<MODE, 4, true>(h, keys, n, silo, act, status)
-                          : route_launch<MODE, 4, false>(h, keys, n, silo, act, status);
-        default: return nt ? route_launch<MODE, 2, true>(h, keys, n, silo, act, status)
-                           : route_launch<MODE, 2, false>(h, keys, n, silo, act, status);
-    }
+    return route_launch<MODE, 1, false>(h, keys, n, silo, act, status);
 }
 
 int route_cached(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status,
@@ -766,7 +779,7 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
     // below 1024 tiles, 4 per workgroup would leave fewer workgroups than the 256 CUs; up to 12,288
     // tiles (48M keys) 4 per workgroup in reverse XCD order also leaves the scatter's keys in L2
     // (f2 hop 3, 43M keys: bucketing -8%); at cfg 3's 16,384 tiles it is neutral, one stays
-    const uint32_t tpb = h->hist_tpb ? h->hist_tpb : (tiles >= 1024 && tiles <= 12288 ? 4u : 1u);
+    const uint32_t tpb = tiles >= 1024 && tiles <= 12288 ? 4u : 1u;
     // multi-tile histograms walk the scatter's XCD tile ranges backwards (hist_t0)
     const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
     if (pk.in) {
@@ -787,9 +800,6 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
         if (tpb == 4)
             GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0, k_radix_hist_multi<BITS, NT, IT, 4>,
                           kin, n, clamp, shift, tiles, hist, fill, hxr));
-        else if (tpb == 8)
-            GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 8)), dim3(NT), 0, k_radix_hist_multi<BITS, NT, IT, 8>,
-                          kin, n, clamp, shift, tiles, hist, fill, hxr));
         else
             GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_radix_hist<BITS, NT, IT>, kin, n, clamp, shift,
                           tiles, hist, fill));
@@ -799,17 +809,10 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
     }
     // one scan launch per digit row (the scatter adds the digit bases), or the device-wide
     // reduce + down-sweep over all R * tiles counts (GD_RADIX_ROWSCAN=0)
-    const uint32_t* totals = nullptr;
-    h->last_totals = nullptr;
-    if (h->radix_rowscan) {
-        totals = hist + (size_t)R * tiles;
-        h->last_totals = totals;
-        h->last_digits = R;
-        GD_TRY(launch(h, "k_radix_rowscan", dim3(R), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles,
-                      hist + (size_t)R * tiles));
-    } else {
-        GD_TRY(scan_device<OpAdd>(h, hist, R * tiles, false, false, "hist"));
-    }
+    const uint32_t* totals = hist + (size_t)R * tiles;
+    h->last_totals = totals;
+    h->last_digits = R;
+    GD_TRY(launch(h, "k_radix_rowscan", dim3(R), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R * tiles));
     if (first)
         return launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_radix_scatter<BITS, true, NT, IT>, kin, vin, n,
                       clamp, shift, tiles, (const uint32_t*)hist, kout, vout, h->radix_rank_atomic, offsets, h->xcd_tiles,
@@ -821,16 +824,9 @@ int radix_pass_t(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_
 
 template <int BITS>
 int radix_pass(gd_handle* h, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp, uint32_t shift,
-               uint32_t* kout, uint32_t* vout, bool first,
-                 uint32_t* offsets, uint32_t* rank_out, FillArgs fill, Pack pk) {
-    switch (h->radix_cfg) {
-        case 1: return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
-        case 2:
-            if constexpr (BITS <= 8) return radix_pass_t<BITS, 1024, 4>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
-            else return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
-        case 3: return radix_pass_t<BITS, 512, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
-        default: return radix_pass_t<BITS, 256, 16>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
-    }
+               uint32_t* kout, uint32_t* vout, bool first, uint32_t* offsets, uint32_t* rank_out, FillArgs fill, Pack pk) {
+    // 512 threads x 8 messages (tools/ab_bucket.py: beat 256 x 16, 1024 x 4 and 512 x 16 by 10-20 %)
+    return radix_pass_t<BITS, 512, 8>(h, kin, vin, n, clamp, shift, kout, vout, first, offsets, rank_out, fill, pk);
 }
 
 int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* vin, uint32_t n, uint32_t clamp,
@@ -848,89 +844,37 @@ int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* 
     }
 }
 
-// The two wide-digit passes of gd_bucket2.h: key & 1023, then key >> 10, on 16K-item tiles, for keys
-// in [0, n_act] with (n_act >> 10) + 1 <= B2_RMAX2.  Starts pre-filled by the first histogram, lowered
-// by the second scatter, min-scanned per 1,024-activation range.
-int bucket2_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
-                   uint32_t* rank_out) {
-    const uint32_t n_off = n_act + 2;
-    const FillArgs fill{offsets, n_off, n};
+// The one-pass form's MSD pass (gd_bucket2.h): 8K-item tiles (512 threads, two workgroups a CU, 32-B
+// index runs at R ~ 1,024; 65 against 76 us on 16K tiles at cfg 2), digit min(act, n_act) >> shift.
+// K16: the range-local keys as u16 (the one-pass form); else the whole clamped key as u32 (pass A of
+// the three-pass form).  Leaves the digit totals in last_totals.
+template <int RMAX, bool K16>
+int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t R, uint32_t shift, uint32_t* k1,
+             uint32_t* v1) {
     const uint32_t tiles = blocks_for(n, B2_TILE);
-    const uint32_t R1 = B2_R1, R2 = (n_act >> B2_LOW_BITS) + 1;
-    GD_TRY(ensure(h, h->hist, ((size_t)std::max(R1, R2) * tiles + std::max(R1, R2)) * sizeof(uint32_t)));
-    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
-    GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
-    uint32_t* hist = (uint32_t*)h->hist.p;
-    uint32_t* k1 = (uint32_t*)h->u32_a.p;
-    uint32_t* v1 = (uint32_t*)h->u32_c.p;
-    const uint32_t xcd = h->xcd_tiles;
-    const uint32_t tpb = tiles >= 1024 ? 4u : 1u;
-    const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
-    // pass 1: key & 1023
-    if (tpb == 4)
-        GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(1024), 0, k_b2_hist<1024, 16, 4, B2_R1, true>,
-                      acts, n, n_act, R1, tiles, hist, fill, hxr));
-    else
-        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(1024), 0, k_b2_hist<1024, 16, 1, B2_R1, true>, acts, n,
-                      n_act, R1, tiles, hist, fill, hxr));
-    const uint32_t* tot1 = hist + (size_t)R1 * tiles;
-    GD_TRY(launch(h, "k_radix_rowscan", dim3(R1), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R1 * tiles));
-    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(1024), 0, k_b2_scatter<1024, 16, B2_R1, true>, acts,
-                  (const uint32_t*)nullptr, n, n_act, R1, tiles, (const uint32_t*)hist, tot1, k1, v1, (uint32_t*)nullptr,
-                  (uint32_t*)nullptr, xcd));
-    // pass 2: key >> 10, the permutation and the starts
-    if (tpb == 4)
-        GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(1024), 0,
-                      k_b2_hist<1024, 16, 4, B2_RMAX2, false>, (const uint32_t*)k1, n, n_act, R2, tiles, hist,
-                      FillArgs{nullptr, 0u, 0u}, hxr));
-    else
-        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(1024), 0, k_b2_hist<1024, 16, 1, B2_RMAX2, false>,
-                      (const uint32_t*)k1, n, n_act, R2, tiles, hist, FillArgs{nullptr, 0u, 0u}, hxr));
-    const uint32_t* tot2 = hist + (size_t)R2 * tiles;
-    GD_TRY(launch(h, "k_radix_rowscan", dim3(R2), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R2 * tiles));
-    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(512), 0, k_b2_scatter<512, 32, B2_RMAX2, false>,
-                  (const uint32_t*)k1, (const uint32_t*)v1, n, n_act, R2, tiles, (const uint32_t*)hist, tot2,
-                  (uint32_t*)nullptr, perm, offsets, rank_out, xcd));
-    h->last_totals = tot2;
-    h->last_digits = R2;
-    return launch(h, "k_starts_rangescan", dim3(R2), dim3(RS_THREADS), 0, k_starts_rangescan, offsets, n_act + 1,
-                  B2_LOW_BITS, tot2, R2);
-}
-
-// MSD pass on tiles of NT x 16 items: 8K (512 threads, two workgroups a CU, 32-B index runs at
-// R ~ 1,024; the default: 65 against 76 us at cfg 2) or 16K (1,024 threads, one a CU, 64-B runs).
-template <int NT, bool K16>
-int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t R, uint32_t* k1, uint32_t* v1) {
-    constexpr uint32_t TILE = NT * 16;
-    const uint32_t tiles = blocks_for(n, TILE);
     const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
     GD_TRY(ensure(h, h->hist, ((size_t)R * tiles + R) * sizeof(uint32_t)));
     uint32_t* hist = (uint32_t*)h->hist.p;
-    const uint32_t tpb = tiles >= 1024 ? h->msd_htpb : 1u;
-    if (tpb == 4)
-        GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(NT), 0,
-                      k_b2_hist<NT, 16, 4, B2_RMAX2, true, true>, acts, n, n_act, R, tiles, hist,
-                      FillArgs{nullptr, 0u, 0u}, hxr));
-    else if (tpb == 2)
-        GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 2)), dim3(NT), 0,
-                      k_b2_hist<NT, 16, 2, B2_RMAX2, true, true>, acts, n, n_act, R, tiles, hist,
-                      FillArgs{nullptr, 0u, 0u}, hxr));
+    // 4 tiles a histogram workgroup from 1,024 tiles up (20.3 / 21.3 / 24.7 us at cfg 2 for 1 / 2 / 4,
+    // profiles/r03_msd_htpb_ab.txt: 4 is the fastest; fewer tiles leave CUs idle)
+    if (tiles >= 1024)
+        GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(B2_NT), 0, k_b2_hist<B2_NT, B2_IT, 4, RMAX>,
+                      acts, n, n_act, R, tiles, hist, shift, hxr));
     else
-        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(NT), 0, k_b2_hist<NT, 16, 1, B2_RMAX2, true, true>, acts,
-                      n, n_act, R, tiles, hist, FillArgs{nullptr, 0u, 0u}, hxr));
+        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(B2_NT), 0, k_b2_hist<B2_NT, B2_IT, 1, RMAX>, acts, n, n_act,
+                      R, tiles, hist, shift, hxr));
     const uint32_t* tot = hist + (size_t)R * tiles;
     GD_TRY(launch(h, "k_radix_rowscan", dim3(R), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R * tiles));
-    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(NT), 0, k_b2_scatter<NT, 16, B2_RMAX2, true, true, K16>, acts,
-                  (const uint32_t*)nullptr, n, n_act, R, tiles, (const uint32_t*)hist, tot, k1, v1, (uint32_t*)nullptr,
-                  (uint32_t*)nullptr, h->xcd_tiles));
+    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(B2_NT), 0, k_b2_scatter<B2_NT, B2_IT, RMAX, K16>, acts, n,
+                  n_act, R, tiles, (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles));
     h->last_totals = tot;
     h->last_digits = R;
     return GD_OK;
 }
 
-// The two-level bucketing (gd_msd.h): a stable MSD pass on the high digit min(act, n_act) >> 10 (the
-// gd_bucket2.h kernels), then k_msd_local sorts each 1,024-activation range in LDS and writes its
-// starts.  Needs (n_act >> 10) + 1 <= B2_RMAX2.
+// The one-pass two-level bucketing (gd_msd.h): a stable MSD pass on the high digit min(act, n_act) >> 10,
+// then k_msd_local sorts each 1,024-activation range in LDS and writes its starts.  Needs (n_act >> 10)
+// + 1 <= B2_RMAX2.
 int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                uint32_t* rank_out) {
     const uint32_t R = (n_act >> MSD_SHIFT) + 1;
@@ -939,41 +883,115 @@ int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, u
     GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
     uint32_t* k1 = (uint32_t*)h->u32_a.p;
     uint32_t* v1 = (uint32_t*)h->u32_c.p;
-    const bool k16 = h->msd_k16 && !h->msd_g16 && !h->msd_early;
-    if (h->msd_tile == 8192) {
-        if (k16) GD_TRY((msd_pass<512, true>(h, acts, n, n_act, R, k1, v1)));
-        else GD_TRY((msd_pass<512, false>(h, acts, n, n_act, R, k1, v1)));
-    } else {
-        if (k16) GD_TRY((msd_pass<1024, true>(h, acts, n, n_act, R, k1, v1)));
-        else GD_TRY((msd_pass<1024, false>(h, acts, n, n_act, R, k1, v1)));
-    }
-    const uint32_t* tot = h->last_totals;
-    if (k16)
-        return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<false, false, true>, (const uint32_t*)k1,
-                      (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
-    if (h->msd_g16)
-        return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<true>, (const uint32_t*)k1,
-                      (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
-    if (h->msd_early)
-        return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<false, true>, (const uint32_t*)k1,
-                      (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
-    return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local<false>, (const uint32_t*)k1,
-                  (const uint32_t*)v1, tot, n, n_act, perm, offsets, rank_out);
+    GD_TRY((msd_pass<B2_RMAX2, true>(h, acts, n, n_act, R, MSD_SHIFT, k1, v1)));
+    return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local, (const uint16_t*)k1, (const uint32_t*)v1,
+                  h->last_totals, n, n_act, perm, offsets, rank_out);
+}
+
+// Three-pass form's split of k' = n_act >> 10: pass B's digit bits a (low part), pass A's kb - a.
+// False when the one-pass form applies or k' needs more than 18 bits (n_act >= 2^28).
+bool msd3_split(uint32_t n_act, uint32_t* a_out, uint32_t* ra_out) {
+    const uint32_t km = n_act >> MSD_SHIFT;
+    if (km + 1 <= MSD_MAX_RANGES) return false;
+    uint32_t kb = 0;
+    while (kb < 32 && (km >> kb) != 0) ++kb;
+    if (kb > 18) return false;
+    const uint32_t a = (kb + 1) / 2;
+    *a_out = a;
+    *ra_out = (km >> a) + 1;
+    return true;
+}
+
+// The three-pass two-level bucketing (gd_msd2.h), for n_act past the one-pass form's digit: pass A
+// (MSD on d2 = k' >> a), pass B (segmented MSD on d1 = k' & (2^a - 1), one flat scan for the
+// positions), then the level-2 work lists (thin ranges a wave each, staged ranges a workgroup each,
+// hot ranges in chunks).  Grids of the level-2 kernels are bounded and loop over device-side counts.
+int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
+                uint32_t* rank_out) {
+    uint32_t a = 0, RA = 0;
+    if (!msd3_split(n_act, &a, &RA)) return set_err(h, GD_EINVAL, "three-pass bucketing: n_act out of range");
+    const uint32_t R = (n_act >> MSD_SHIFT) + 1, RB = 1u << a;
+    const uint32_t tilesA = blocks_for(n, B2_TILE);
+    const uint32_t tbound = blocks_for(n, SEG_TILE) + RA;
+    const uint32_t cr_bound = n / (MSD_CAP + 1) + 1;
+    const uint32_t ch_bound = n / CH_CAP + cr_bound;
+    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
+    GD_TRY(ensure(h, h->u32_b, (size_t)n * 4));
+    GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
+    GD_TRY(ensure(h, h->u32_d, (size_t)n * 4));
+    DevBuf* m = h->m3;
+    GD_TRY(ensure(h, m[0], (size_t)(RA + 1) * 4));                 // segment starts
+    GD_TRY(ensure(h, m[1], (size_t)(RA + 1) * 4));                 // segment tile bases
+    GD_TRY(ensure(h, m[2], (size_t)tbound * 4));                   // tile -> segment
+    GD_TRY(ensure(h, m[3], (size_t)RB * tbound * 4));              // pass B counts, flat-scanned
+    GD_TRY(ensure(h, m[4], (size_t)(R + 1) * 4));                  // range starts
+    GD_TRY(ensure(h, m[5], (size_t)L2_CTR_WORDS * 4));
+    GD_TRY(ensure(h, m[6], (size_t)R * 4));                        // thin ranges
+    GD_TRY(ensure(h, m[7], (size_t)R * 4));                        // staged ranges
+    GD_TRY(ensure(h, m[8], (size_t)cr_bound * 3 * 4));             // chunked ranges
+    GD_TRY(ensure(h, m[9], (size_t)ch_bound * 4));                 // chunk -> chunked range
+    GD_TRY(ensure(h, m[10], (size_t)ch_bound * MSD_L * 4));        // per-chunk activation counts
+    GD_TRY(ensure(h, m[11], (size_t)cr_bound * MSD_L * 4));        // per-range activation totals
+    uint32_t* kA = (uint32_t*)h->u32_a.p;
+    uint32_t* vA = (uint32_t*)h->u32_c.p;
+    uint16_t* kB = (uint16_t*)h->u32_b.p;
+    uint32_t* vB = (uint32_t*)h->u32_d.p;
+    uint32_t* seg_start = (uint32_t*)m[0].p;
+    uint32_t* seg_tb = (uint32_t*)m[1].p;
+    uint32_t* tile_seg = (uint32_t*)m[2].p;
+    uint32_t* hseg = (uint32_t*)m[3].p;
+    (void)tilesA;
+    // pass A: d2 = k' >> a, whole keys out
+    GD_TRY((msd_pass<SEG_RMAX, false>(h, acts, n, n_act, RA, MSD_SHIFT + a, kA, vA)));
+    GD_TRY(launch(h, "k_seg_table", dim3(1), dim3(1024), 0, k_seg_table, h->last_totals, RA, tbound, seg_start, seg_tb,
+                  tile_seg, (uint32_t*)m[5].p));
+    // pass B: d1 inside each d2 segment; one flat scan gives every (segment, digit, tile) its position
+    GD_TRY(launch(h, "k_seg_hist", dim3(tbound), dim3(SEG_NT), 0, k_seg_hist, (const uint32_t*)kA,
+                  (const uint32_t*)tile_seg, (const uint32_t*)seg_start, (const uint32_t*)seg_tb, RB, hseg));
+    GD_TRY(scan_device<OpAdd>(h, hseg, RB * tbound, false, false, "seg"));
+    GD_TRY(launch(h, "k_seg_scatter", dim3(tbound), dim3(SEG_NT), 0, k_seg_scatter, (const uint32_t*)kA,
+                  (const uint32_t*)vA, (const uint32_t*)tile_seg, (const uint32_t*)seg_start, (const uint32_t*)seg_tb, RB,
+                  (const uint32_t*)hseg, kB, vB, h->xcd_tiles));
+    // level 2
+    uint32_t* cr = (uint32_t*)m[8].p;
+    const L2Lists l{(uint32_t*)m[4].p, (uint32_t*)m[6].p, (uint32_t*)m[7].p, cr, cr + cr_bound, cr + 2 * cr_bound,
+                    (uint32_t*)m[9].p, (uint32_t*)m[5].p};
+    GD_TRY(launch(h, "k_l2_classify", dim3(blocks_for(R, BLOCK)), dim3(BLOCK), 0, k_l2_classify, (const uint32_t*)hseg,
+                  (const uint32_t*)seg_start, (const uint32_t*)seg_tb, a, R, n, h->l2_small, l));
+    GD_TRY(launch(h, "k_l2_small", dim3(std::min<uint32_t>(blocks_for(R, L2_SMALL_WAVES), 2048)),
+                  dim3(L2_SMALL_WAVES * WAVE), 0, k_l2_small, (const uint16_t*)kB, (const uint32_t*)vB, l, n, n_act, perm,
+                  offsets, rank_out));
+    GD_TRY(launch(h, "k_msd_local", dim3(std::min<uint32_t>(R, 512)), dim3(MSD_NT), 0, k_msd_local_list,
+                  (const uint16_t*)kB, (const uint32_t*)vB, (const uint32_t*)l.rs, (const uint32_t*)l.staged,
+                  (const uint32_t*)(l.ctr + 1), n, n_act, perm, offsets, rank_out));
+    uint32_t* hh = (uint32_t*)m[10].p;
+    uint32_t* tot = (uint32_t*)m[11].p;
+    GD_TRY(launch(h, "k_l2_chunk_hist", dim3(std::min<uint32_t>(ch_bound, 1024)), dim3(MSD_NT), 0, k_l2_chunk_hist,
+                  (const uint16_t*)kB, l, hh));
+    GD_TRY(launch(h, "k_l2_chunk_scan", dim3(std::min<uint32_t>(cr_bound * (MSD_L / CS_COLS), 1024)), dim3(MSD_NT), 0,
+                  k_l2_chunk_scan, l, hh, tot));
+    return launch(h, "k_l2_chunk_scatter", dim3(std::min<uint32_t>(ch_bound, 512)), dim3(MSD_NT), 0, k_l2_chunk_scatter,
+                  (const uint16_t*)kB, (const uint32_t*)vB, l, (const uint32_t*)hh, (const uint32_t*)tot, n, n_act, perm,
+                  offsets, rank_out);
 }
 
 int bucket_lsd(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                uint32_t* rank_out);
 
 // Stable partition of indices 0..n-1 by min(acts[i], n_act).  rank_out (optional): the inverse
-// permutation, rank_out[perm[p]] = p.  Two forms with identical output: LSD passes of <= 8 bits plus
-// the bucket starts (bucket_lsd), or, for n_act < 1056 x 1024 and batches of at least 2^20 messages,
-// the two-level MSD + in-LDS form (msd_bucket); GD_MSD=1 (default) times both on the first launches of
-// each batch size (tune_choose, kind 4) and keeps the faster, 2 always takes the two-level form.
+// permutation, rank_out[perm[p]] = p.  Forms with identical output: LSD passes of <= 8 bits plus the
+// bucket starts (bucket_lsd); for batches of at least 2^20 messages the two-level forms -- one MSD pass
+// + the in-LDS range sort for n_act < 1056 x 1024 (msd_bucket), two MSD passes + the level-2 work lists
+// up to n_act < 2^28 (msd3_bucket).  GD_MSD=1 (default) times the two-level form against the LSD
+// passes on the first launches of each batch shape (tune_choose, kind 4) and keeps the faster, 2
+// always takes the two-level form.
 int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                   uint32_t* rank_out = nullptr) {
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
-    const bool msd_ok = h->msd_mode && n >= (1u << 20) && (n_act >> MSD_SHIFT) + 1 <= MSD_MAX_RANGES && !h->bucket2;
-    if (msd_ok) {
+    uint32_t a3 = 0, ra3 = 0;
+    const bool one = (n_act >> MSD_SHIFT) + 1 <= MSD_MAX_RANGES;
+    const bool three = !one && msd3_split(n_act, &a3, &ra3);
+    if (h->msd_mode && n >= (1u << 20) && (one || three)) {
         int meas = -1;
         // keyed by the batch size and by the messages a range holds (which decide whether ranges are
         // staged in LDS): a handle bucketing 16M messages over 1M and over 10k activations keeps one
@@ -981,27 +999,25 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
         int per_range = 0;
         while (per_range < 31 && ((uint64_t)n / ((n_act >> MSD_SHIFT) + 1) >> per_range) > 1) ++per_range;
         const int var = h->msd_mode == 2 ? 1 : tune_choose(h, 4, n, &meas, 2, per_range);
-        CxMeasure m(h, meas, n);
-        if (var == 1) return msd_bucket(h, acts, n, n_act, perm, offsets, rank_out);
+        CxMeasure mm(h, meas, n);
+        if (var == 1) return one ? msd_bucket(h, acts, n, n_act, perm, offsets, rank_out)
+                                 : msd3_bucket(h, acts, n, n_act, perm, offsets, rank_out);
         return bucket_lsd(h, acts, n, n_act, perm, offsets, rank_out);
     }
     return bucket_lsd(h, acts, n, n_act, perm, offsets, rank_out);
 }
 
+constexpr uint32_t RADIX_MAX_BITS = 8;   // widest LSD digit (9- and 10-bit digits measured slower at cfg 3)
+
 int bucket_lsd(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                uint32_t* rank_out) {
-    // keys of 17..21 bits with at most B2_RMAX2 high digits, batches of at least 64 tiles: two wide passes
-    if (h->bucket2 && n >= 64 * B2_TILE && n_act >= (1u << 16) && (n_act >> B2_LOW_BITS) + 1 <= B2_RMAX2)
-        return bucket2_device(h, acts, n, n_act, perm, offsets, rank_out);
     const uint32_t n_off = n_act + 2;
-    if (n == 0 || !h->fill_in_hist)
-        GD_TRY(launch(h, "k_fill", dim3(blocks_for(n_off, BLOCK)), dim3(BLOCK), 0, k_fill_u32, offsets, n_off, n));
-    if (n == 0) return GD_OK;
-    // otherwise the first pass's histogram fills the starts (n = the empty-bucket value)
-    const FillArgs fill{h->fill_in_hist ? offsets : nullptr, n_off, n};
+    if (n == 0) return launch(h, "k_fill", dim3(blocks_for(n_off, BLOCK)), dim3(BLOCK), 0, k_fill_u32, offsets, n_off, n);
+    // the first pass's histogram fills the starts (n = the empty-bucket value)
+    const FillArgs fill{offsets, n_off, n};
     uint32_t key_bits = 1;
     while (key_bits < 32 && (n_act >> key_bits) != 0) ++key_bits;
-    const uint32_t passes = (key_bits + h->radix_max_bits - 1) / h->radix_max_bits;
+    const uint32_t passes = (key_bits + RADIX_MAX_BITS - 1) / RADIX_MAX_BITS;
     const uint32_t bits = std::max<uint32_t>(4, (key_bits + passes - 1) / passes);
     GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
     GD_TRY(ensure(h, h->u32_b, (size_t)n * 4));
@@ -1015,13 +1031,13 @@ int bucket_lsd(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, u
     // a u16 and the index fits beside the first digit in a u32 (BASELINE cfg 2: 14 + 24 + 7 bits)
     uint32_t ib = 1;
     while (ib < 32 && ((n - 1) >> ib) != 0) ++ib;
-    const bool pack = h->radix_pack && passes >= 2 && h->fused_starts && h->radix_cfg == 1 && bits <= 8 &&
+    const bool pack = passes >= 2 && bits <= 8 &&
                       key_bits - bits <= 16 && ib + bits <= 32;
     for (uint32_t p = 0; p < passes; ++p) {
         uint32_t* kout = kb[p & 1];
         uint32_t* vout = (p + 1 == passes) ? perm : vb[p & 1];
         // the last pass writes the bucket starts itself (no sorted keys, no k_bucket_starts)
-        const bool last = p + 1 == passes && h->fused_starts;
+        const bool last = p + 1 == passes;
         const Pack pk{ib, bits, pack && p > 0, pack && p + 1 < passes};
         GD_TRY(radix_dispatch(h, (int)bits, kin, vin, n, n_act, p * bits, kout, vout, p == 0,
                               last ? offsets : nullptr, p + 1 == passes ? rank_out : nullptr,
@@ -1029,13 +1045,10 @@ int bucket_lsd(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, u
         kin = kout;
         vin = vout;
     }
-    if (!h->fused_starts)
-        GD_TRY(launch(h, "k_bucket_starts", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_bucket_starts, kin, n,
-                      offsets));
     // the last pass's digit spans <= RS_RANGE * RS_MAX_SUB activations: one workgroup per digit
     // range, carried by the pass's digit bases (GD_RANGE_SCAN=0: the device-wide scan)
     const uint32_t last_shift = (passes - 1) * bits;
-    if (h->range_scan && h->last_totals && last_shift < 32 && (1u << last_shift) <= RS_RANGE * RS_MAX_SUB)
+    if (h->last_totals && last_shift < 32 && (1u << last_shift) <= RS_RANGE * RS_MAX_SUB)
         return launch(h, "k_starts_rangescan", dim3((n_act >> last_shift) + 1), dim3(RS_THREADS), 0, k_starts_rangescan,
                       offsets, n_act + 1, last_shift, h->last_totals, h->last_digits);
     return scan_device<OpMin>(h, offsets, n_act + 1, true, true, "offsets");
@@ -1330,40 +1343,6 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     h->cfg = *cfg;
     h->device = cfg->device;
     h->timing = (cfg->flags & GD_CFG_KERNEL_TIMING) != 0;
-    if (const char* v = std::getenv("GD_ROUTE_M")) h->route_m = std::atoi(v);
-    if (const char* v = std::getenv("GD_ROUTE_NT")) h->route_nt = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_ROUTE_XCD")) h->route_xcd = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_CX")) h->cx_mode = std::max(0, std::min(3, std::atoi(v)));
-    if (const char* v = std::getenv("GD_MSD")) h->msd_mode = std::max(0, std::min(2, std::atoi(v)));
-    if (const char* v = std::getenv("GD_MSD_G16")) h->msd_g16 = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_MSD_EARLY")) h->msd_early = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_MSD_K16")) h->msd_k16 = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_MSD_HTPB")) {
-        const int t = std::atoi(v);
-        h->msd_htpb = t == 1 || t == 2 ? (uint32_t)t : 4u;
-    }
-    if (const char* v = std::getenv("GD_MSD_TILE")) h->msd_tile = std::atoi(v) == 16384 ? 16384u : 8192u;
-    if (const char* v = std::getenv("GD_CX_SCALE")) h->cx_scale = std::atoi(v) == 2 ? 2u : 1u;
-    if (const char* v = std::getenv("GD_RADIX_CFG")) h->radix_cfg = std::atoi(v);
-    if (const char* v = std::getenv("GD_RADIX_MAXBITS")) h->radix_max_bits = std::min(11, std::max(4, std::atoi(v)));
-    if (const char* v = std::getenv("GD_RADIX_RANK")) h->radix_rank_atomic = std::atoi(v) ? 1u : 0u;
-    if (const char* v = std::getenv("GD_FUSED_STARTS")) h->fused_starts = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_RADIX_PACK")) h->radix_pack = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_RADIX_ROWSCAN")) h->radix_rowscan = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_FILL_IN_HIST")) h->fill_in_hist = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_RANGE_SCAN")) h->range_scan = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_SHARD_GATHER")) h->shard_gather = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_COMPACT_HEADERS")) h->compact_headers = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_NARROW_HEADERS")) h->narrow_headers = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_SHARD_N1")) h->shard_n1_copy = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_HOST_CHUNK")) h->host_chunk = (uint32_t)std::strtoul(v, nullptr, 10);
-    if (const char* v = std::getenv("GD_XCD_TILES")) h->xcd_tiles = std::atoi(v) ? 1u : 0u;
-    if (const char* v = std::getenv("GD_HIST_TPB")) h->hist_tpb = (uint32_t)std::atoi(v);
-    if (const char* v = std::getenv("GD_HIST_XCD")) h->hist_xcd = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_FAN_ILP")) h->fan_ilp = std::atoi(v);
-    if (const char* v = std::getenv("GD_BUCKET2")) h->bucket2 = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_REGION_PROBE")) h->region_probe = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_IDX16")) h->idx16 = std::atoi(v) != 0;
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));
@@ -1411,6 +1390,8 @@ void gd_destroy(gd_handle* h) {
                       &h->out_a, &h->out_b, &h->out_c, &h->hist, &h->partials, &h->partials2, &h->offs})
         free_buf(*b);
     for (DevBuf& b : h->fr) free_buf(b);
+    for (DevBuf& b : h->m3) free_buf(b);
+    free_buf(h->tune_buf);
     for (DevBuf& b : h->fr_ext) free_buf(b);
     for (DevBuf& b : h->churn) free_buf(b);
     for (DevBuf& b : h->fan) free_buf(b);
@@ -1902,6 +1883,120 @@ int gd_kernel_times_reset(gd_handle* h) {
     return GD_OK;
 }
 
+int gd_option_set(gd_handle* h, int option, int64_t v) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    auto in = [&](int64_t lo, int64_t hi) { return v >= lo && v <= hi; };
+    switch (option) {
+        case GD_OPT_PROBE:
+            if (!in(0, 3)) break;
+            h->cx_mode = (int)v;
+            return GD_OK;
+        case GD_OPT_BUCKET:
+            if (!in(0, 2)) break;
+            h->msd_mode = (int)v;
+            return GD_OK;
+        case GD_OPT_L2_SMALL:
+            if (!in(0, MSD_CAP)) break;
+            h->l2_small = (uint32_t)v;
+            return GD_OK;
+        case GD_OPT_STABLE_RANK:
+            if (!in(0, 1)) break;
+            h->radix_rank_atomic = (uint32_t)v;
+            return GD_OK;
+        case GD_OPT_WIRE_HEADERS:
+            if (!in(0, 2)) break;
+            h->compact_headers = v >= 1;
+            h->narrow_headers = v == 2;
+            return GD_OK;
+        case GD_OPT_REGION_PROBE:
+            if (!in(0, 1)) break;
+            h->region_probe = v != 0;
+            return GD_OK;
+        case GD_OPT_IDX16:
+            if (!in(0, 1)) break;
+            h->idx16 = v != 0;
+            return GD_OK;
+        case GD_OPT_HOST_CHUNK:
+            if (!in(0, 1ll << 30)) break;
+            h->host_chunk = (uint32_t)v;
+            return GD_OK;
+        case GD_OPT_MB_ZEROCOPY:
+            if (!in(0, 1)) break;
+            h->mb_zero_copy = v != 0;
+            return GD_OK;
+        case GD_OPT_MB_SPLIT:
+            if (!in(1, 64)) break;
+            h->mb_split = (uint32_t)v;
+            return GD_OK;
+        case GD_OPT_MB_TRACE:
+            if (!in(0, 1)) break;
+            h->mb_trace = v != 0;
+            return GD_OK;
+        default: return set_err(h, GD_EINVAL, "gd_option_set: unknown option %d", option);
+    }
+    return set_err(h, GD_EINVAL, "gd_option_set: option %d: value %lld out of range", option, (long long)v);
+}
+
+int gd_option_get(const gd_handle* hc, int option, int64_t* v) {
+    gd_handle* h = const_cast<gd_handle*>(hc);
+    if (!h || !v) return set_err(h, GD_EINVAL, "null argument");
+    switch (option) {
+        case GD_OPT_PROBE: *v = h->cx_mode; return GD_OK;
+        case GD_OPT_BUCKET: *v = h->msd_mode; return GD_OK;
+        case GD_OPT_L2_SMALL: *v = h->l2_small; return GD_OK;
+        case GD_OPT_STABLE_RANK: *v = h->radix_rank_atomic; return GD_OK;
+        case GD_OPT_WIRE_HEADERS: *v = h->compact_headers ? (h->narrow_headers ? 2 : 1) : 0; return GD_OK;
+        case GD_OPT_REGION_PROBE: *v = h->region_probe; return GD_OK;
+        case GD_OPT_IDX16: *v = h->idx16; return GD_OK;
+        case GD_OPT_HOST_CHUNK: *v = h->host_chunk; return GD_OK;
+        case GD_OPT_MB_ZEROCOPY: *v = h->mb_zero_copy; return GD_OK;
+        case GD_OPT_MB_SPLIT: *v = h->mb_split; return GD_OK;
+        case GD_OPT_MB_TRACE: *v = h->mb_trace; return GD_OK;
+        default: return set_err(h, GD_EINVAL, "gd_option_get: unknown option %d", option);
+    }
+}
+
+int gd_tune_reset(gd_handle* h) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    for (auto& kt : h->cx_tune) {
+        auto& t = kt.second;
+        for (int v = 0; v < gd_handle::CXV; ++v) {
+            if (t.pending[v]) (void)hipEventSynchronize(t.b[v]);
+            t.best[v] = 1e30f;
+            t.pending[v] = false;
+        }
+        t.pick = -1;
+        t.round = 0;
+    }
+    return GD_OK;
+}
+
+int gd_tune_set(gd_handle* h, int kind, int variant) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (kind < 0 || kind >= GD_TUNE_KINDS) return set_err(h, GD_EINVAL, "gd_tune_set: kind %d", kind);
+    if (variant < -1 || variant >= tune_nvar(kind))
+        return set_err(h, GD_EINVAL, "gd_tune_set: kind %d has no variant %d", kind, variant);
+    h->tune_pin[kind] = variant;
+    return GD_OK;
+}
+
+int gd_tune_get(gd_handle* h, int kind, uint64_t n, uint32_t sub, int* variant) {
+    if (!h || !variant) return set_err(h, GD_EINVAL, "null argument");
+    if (kind < 0 || kind >= GD_TUNE_KINDS) return set_err(h, GD_EINVAL, "gd_tune_get: kind %d", kind);
+    if (h->tune_pin[kind] >= 0) {
+        *variant = h->tune_pin[kind];
+        return GD_OK;
+    }
+    auto it = h->cx_tune.find(tune_key(kind, n, (int)sub));
+    if (it == h->cx_tune.end()) {
+        *variant = -1;
+        return GD_OK;
+    }
+    tune_resolve(it->second, tune_nvar(kind));
+    *variant = it->second.pick;
+    return GD_OK;
+}
+
 }  // extern "C"
 
 // ================================================================== micro-batch latency path
@@ -1922,8 +2017,8 @@ struct gd_microbatch {
     gd_key* h_keys_dev = nullptr;  // device view of h_keys
     uint8_t* h_out_dev = nullptr;  // device view of h_out
     uint32_t* d_act = nullptr;
-    uint32_t split = 8;                 // k_mb_sort_runs workgroups (redundant sorts, split stores; GD_MB_SPLIT)
-    uint32_t max_bits = MB_MAX_BITS;    // widest radix digit (GD_MB_MAXBITS)
+    uint32_t split = 8;                 // k_mb_sort_runs workgroups (redundant sorts, split stores; GD_OPT_MB_SPLIT)
+    uint32_t max_bits = MB_MAX_BITS;    // widest radix digit (11: two passes at n_act = 2^20)
     unsigned long long* ts = nullptr;   // GD_MB_TRACE: per-phase tick sums (device), printed at destroy
     uint64_t runs_done = 0;
     std::vector<std::pair<uint32_t, hipGraphExec_t>> graphs;
@@ -2050,12 +2145,10 @@ int gd_microbatch_create(gd_handle* h, uint32_t capacity, uint32_t n_act, gd_mic
     mb->n_act = n_act;
     mb->out_bytes = (5 * (size_t)capacity + 2) * 4 + capacity;
     const size_t kb = (size_t)capacity * sizeof(gd_key);
-    if (const char* v = std::getenv("GD_MB_ZEROCOPY")) mb->zero_copy = std::atoi(v) != 0;
-    if (const char* v = std::getenv("GD_MB_MAXBITS")) mb->max_bits = (uint32_t)std::max(4, std::min(MB_MAX_BITS, std::atoi(v)));
-    if (const char* v = std::getenv("GD_MB_TRACE"))
-        if (std::atoi(v) != 0 && hipMalloc((void**)&mb->ts, 16 * sizeof(unsigned long long)) == hipSuccess)
-            (void)hipMemset(mb->ts, 0, 16 * sizeof(unsigned long long));
-    if (const char* v = std::getenv("GD_MB_SPLIT")) mb->split = (uint32_t)std::max(1, std::min(64, std::atoi(v)));
+    mb->zero_copy = h->mb_zero_copy;
+    mb->split = h->mb_split;
+    if (h->mb_trace && hipMalloc((void**)&mb->ts, 16 * sizeof(unsigned long long)) == hipSuccess)
+        (void)hipMemset(mb->ts, 0, 16 * sizeof(unsigned long long));
     // coherent (fine-grained) pinned memory: kernel stores reach the host without a cache flush
     const unsigned hf = mb->zero_copy ? hipHostMallocCoherent : hipHostMallocDefault;
     bool ok = hipHostMalloc((void**)&mb->h_keys, kb, hf) == hipSuccess &&
@@ -2509,17 +2602,10 @@ int fan_route_launch_cx(gd_handle* h, const uint32_t* row_off, const uint32_t* d
     const dim3 g(blocks_for(total, FAN_TILE)), b(BLOCK);
     const uint32_t* ends = (const uint32_t*)h->fan[0].p;
     const CxArgs cx = CX ? cx_args(h) : CxArgs{};
-    switch (h->fan_ilp) {
-        case 1:
-            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 1, CX>, row_off, dst, frontier, nf,
-                          ends, total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx);
-        case 4:
-            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 4, CX>, row_off, dst, frontier, nf,
-                          ends, total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx);
-        default:
-            return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2, CX>, row_off, dst, frontier, nf,
-                          ends, total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx);
-    }
+    // 2 outputs a thread in flight (1: 2.95 ms, 4: 3.03 ms against 2.87 ms a cfg 4 cascade,
+    // profiles/r02_v1_fanout_cfg4_ilp_ab.jsonl)
+    return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2, CX>, row_off, dst, frontier, nf, ends,
+                  total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx);
 }
 
 template <int MODE>
@@ -2527,7 +2613,7 @@ int fan_route_launch(gd_handle* h, const uint32_t* row_off, const uint32_t* dst,
                      uint32_t total, uint64_t tcd, uint32_t* target, uint32_t* sender, uint32_t* silo, uint32_t* act,
                      uint8_t* status) {
     bool cx = false;
-    GD_TRY(cx_ensure(h, &cx));
+    GD_TRY(cx_ensure(h, &cx, total));
     int meas = -1;
     if (cx) cx = cx_choose(h, 2, total, &meas, 2) == 0;
     CxMeasure m(h, meas, total);
@@ -2571,7 +2657,7 @@ int route_nodes(gd_handle* h, const uint32_t* nodes, uint32_t n, uint64_t tcd, u
     GD_TRY(check_ring(h));
     h->routed += n;
     bool cx = false;
-    GD_TRY(cx_ensure(h, &cx));
+    GD_TRY(cx_ensure(h, &cx, n));
     int meas = -1;
     if (cx) cx = cx_choose(h, 3, n, &meas, 2) == 0;
     CxMeasure m(h, meas, n);
@@ -4067,6 +4153,71 @@ int gd_comm_destroy(gd_handle* h) {
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(sync(h));
     comm_release(h);
+    return GD_OK;
+}
+
+// One all-gather of every rank's finished tune entries (key, best time a message per variant) in a
+// grouped send/recv round, then the same reduction on every rank: per key, the summed times of the
+// ranks that finished it (in rank order, so the floats agree bit for bit), argmin -> the pick.
+int gd_tune_agree(gd_handle* h) {
+    if (!h) return set_err(h, GD_EINVAL, "null argument");
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(need_comm(h));
+    struct Rec {
+        uint32_t key;
+        float best[gd_handle::CXV];
+    };
+    static_assert(sizeof(Rec) == 16, "16-B records");
+    constexpr uint32_t MAXE = 1023;                      // entries a rank contributes (+ a count record)
+    const int W = h->n_ranks;
+    std::vector<Rec> mine(MAXE + 1, Rec{0, {0.f, 0.f, 0.f}});
+    uint32_t ne = 0;
+    for (auto& kt : h->cx_tune) {
+        const int nvar = tune_nvar(kt.first / (64 * 32));
+        auto& t = kt.second;
+        tune_resolve(t, nvar);
+        bool done = true;
+        for (int v = 0; v < nvar; ++v) done = done && t.best[v] < 1e29f;
+        if (!done || ne == MAXE) continue;
+        Rec& r = mine[1 + ne++];
+        r.key = (uint32_t)kt.first;
+        for (int v = 0; v < gd_handle::CXV; ++v) r.best[v] = v < nvar ? t.best[v] : 0.f;
+    }
+    mine[0].key = ne;
+    const size_t bytes = (size_t)(MAXE + 1) * sizeof(Rec);
+    DevBuf& buf = h->tune_buf;
+    GD_TRY(sync(h));
+    GD_TRY(ensure(h, buf, bytes * (W + 1)));
+    uint8_t* d = (uint8_t*)buf.p;
+    HIP_TRY(h, hipMemcpyAsync(d, mine.data(), bytes, hipMemcpyHostToDevice, h->stream));
+    const Rccl& R = *h->net;
+    NCCL_TRY(h, R.GroupStart());
+    for (int r = 0; r < W; ++r) {
+        NCCL_TRY(h, R.Send(d, bytes, ncclUint8, r, h->comm, h->stream));
+        NCCL_TRY(h, R.Recv(d + bytes * (r + 1), bytes, ncclUint8, r, h->comm, h->stream));
+    }
+    NCCL_TRY(h, R.GroupEnd());
+    std::vector<Rec> all((size_t)(MAXE + 1) * W);
+    HIP_TRY(h, hipMemcpyAsync(all.data(), d + bytes, bytes * W, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(sync(h));
+    std::map<uint32_t, std::array<double, gd_handle::CXV>> sum;
+    for (int r = 0; r < W; ++r) {
+        const Rec* rr = all.data() + (size_t)(MAXE + 1) * r;
+        const uint32_t cnt = std::min(rr[0].key, MAXE);
+        for (uint32_t i = 0; i < cnt; ++i) {
+            auto& s = sum.try_emplace(rr[1 + i].key, std::array<double, gd_handle::CXV>{0.0, 0.0, 0.0}).first->second;
+            for (int v = 0; v < gd_handle::CXV; ++v) s[v] += (double)rr[1 + i].best[v];
+        }
+    }
+    for (const auto& ks : sum) {
+        const int kind = (int)ks.first / (64 * 32), nvar = tune_nvar(kind);
+        int pick = 0;
+        for (int v = 1; v < nvar; ++v)
+            if (ks.second[v] < ks.second[pick]) pick = v;
+        auto& t = h->cx_tune[(int)ks.first];
+        t.pick = pick;
+        t.round = std::max(t.round, 2 * nvar);
+    }
     return GD_OK;
 }
 

@@ -1,0 +1,592 @@
+// gd_msd2.h -- gfx950 device code for the three-pass form of the two-level bucketing (SURVEY 8 a16,
+// the per-activation FIFO): the stable partition of message indices by
+// min(act, n_act) when n_act is past the one-pass form's digit (n_act >= 1,081,344: BASELINE cfg 3's
+// 100M activations, 12.5M a GPU at W = 8, cfg 4's 10M), up to n_act < 2^28.
+//
+// Ranges of 1,024 activations, k' = min(act, n_act) >> 10 (17 bits at cfg 3), split k' = (d2, d1):
+//   pass A  k_b2_hist / row scan / k_b2_scatter (gd_bucket2.h) on d2 = k' >> a (<= 512 digits):
+//           every d2 segment contiguous, in message order; the whole clamped key (u32) and the index
+//           (u32) written, 8 B a record;
+//   pass B  segmented MSD on d1 = k' & (2^a - 1) (<= 512 digits) inside each d2 segment: tiles never
+//           cross a segment (k_seg_table lays them out), counts laid out [segment][digit][tile], and ONE
+//           flat exclusive scan of that array gives every (segment, digit, tile) its absolute output
+//           position -- so each range's start is a lookup, with no atomics and no min-scan over
+//           the activations.  Writes the range-local key (key & 1023, u16) and the index (u32), 6 B;
+//   level 2 k_l2_classify sorts the ranges into three work lists by their message count S:
+//             S <= t_small      k_l2_small, one wave a range (its 1,024 counters in 4 KB of LDS);
+//             S <= MSD_CAP      k_msd_local_list (gd_msd.h), one workgroup a range, staged in LDS;
+//             S >  MSD_CAP      chunks of CH_CAP messages, several workgroups a range: k_l2_chunk_hist
+//                               (per-chunk activation counts) -> k_l2_chunk_scan (exclusive prefix of
+//                               each activation's counts over the range's chunks, 16-activation columns
+//                               scanned in LDS) -> k_l2_chunk_scatter (ranked and staged in LDS like a
+//                               range, written at each activation's base for that chunk).
+//           Every level-2 kernel writes the bucket starts of the activations it owns (empty ones
+//           included), so offsets is written exactly once.
+// A Zipf-hot range (BASELINE cfg 3: acts 0..1,023 take ~60 % of a batch) is spread over as many
+// workgroups as it has chunks: no range serialises on one CU.
+// Per message: 4 + 12 (pass A: histogram, scatter) + 4 + 14 (pass B) + 6 + 4 (level 2) B, plus 4 B a
+// activation for the starts -- 44 B + 4 n_act / n, against 4 x (4 + 16) B + three passes over the
+// starts (fill, lowered, min-scanned) for four 7-bit LSD passes at cfg 3.  Stability: every pass ranks
+// a tile in index order (ds_add_rtn serves the lanes of one instruction in lane order), the
+// level-2 forms rank rows in order, chunks in order.  HBM-bound, no MFMA.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gd_bucket2.h"
+#include "gd_kernels.h"
+#include "gd_msd.h"
+
+namespace gd {
+
+constexpr int SEG_NT = 512;                    // pass B tile: 512 threads x 16 items (as pass A)
+constexpr int SEG_IT = 16;
+constexpr uint32_t SEG_TILE = SEG_NT * SEG_IT;
+constexpr uint32_t SEG_RMAX = 512;             // digits of either pass (a, kb - a <= 9 bits)
+constexpr uint32_t L2_SMALL_WAVES = 8;         // k_l2_small: waves a workgroup, one range each
+constexpr uint32_t CH_CAP = 16384;             // messages a chunk of a hot range (16 rows x 1,024 lanes)
+constexpr uint32_t CH_RW = CH_CAP / MSD_NT;
+constexpr uint32_t L2_CTR_WORDS = 8;           // [0] small ranges, [1] staged ranges, [2] chunks, [3] chunked ranges
+
+// Wave-local LDS hand-off: the wave's earlier LDS writes are complete and visible to its other lanes.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One workgroup: the d2 segments' starts (exclusive prefix of pass A's digit totals) and tile bases
+// (exclusive prefix of ceil(size / SEG_TILE)), every pass-B tile's segment (NONE32 past the last), and
+// the level-2 counters zeroed.  ra <= SEG_RMAX.
+__global__ void __launch_bounds__(1024) k_seg_table(const uint32_t* __restrict__ totals, uint32_t ra,
+                                                    uint32_t tbound, uint32_t* __restrict__ seg_start,
+                                                    uint32_t* __restrict__ seg_tb, uint32_t* __restrict__ tile_seg,
+                                                    uint32_t* __restrict__ ctr) {
+    __shared__ uint32_t s_wsum[2 * 1024 / WAVE];
+    __shared__ uint32_t s_tb[SEG_RMAX + 1];
+    const uint32_t t = threadIdx.x;
+    const uint32_t v = t < ra ? totals[t] : 0u;
+    const uint32_t nt = (v + SEG_TILE - 1) / SEG_TILE;
+    uint32_t es, et;
+    block_excl_scan_add2<1024>(v, nt, s_wsum, es, et);
+    if (t < ra) {
+        seg_start[t] = es;
+        seg_tb[t] = et;
+        s_tb[t] = et;
+    }
+    if (t == ra - 1) {
+        seg_start[ra] = es + v;
+        seg_tb[ra] = et + nt;
+        s_tb[ra] = et + nt;
+    }
+    if (t < L2_CTR_WORDS) ctr[t] = 0;
+    __syncthreads();
+    const uint32_t total = s_tb[ra];
+    for (uint32_t j = t; j < tbound; j += 1024) {
+        uint32_t s = NONE32;
+        if (j < total) {
+            uint32_t lo = 0, hi = ra;                // largest s < ra with s_tb[s] <= j
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_tb[mid] <= j) lo = mid;
+                else hi = mid;
+            }
+            s = lo;
+        }
+        tile_seg[j] = s;
+    }
+}
+
+// A pass-B tile: its segment s, the tile's index in the segment tl, the segment's tiles ts and tile
+// base tb, its first item and item count.
+struct SegTile {
+    uint32_t s, tl, ts, tb, base, cnt;
+};
+__device__ __forceinline__ bool seg_tile(uint32_t j, const uint32_t* tile_seg, const uint32_t* seg_start,
+                                         const uint32_t* seg_tb, SegTile& st) {
+    st.s = tile_seg[j];
+    if (st.s == NONE32) return false;
+    st.tb = seg_tb[st.s];
+    st.ts = seg_tb[st.s + 1] - st.tb;
+    st.tl = j - st.tb;
+    st.base = seg_start[st.s] + st.tl * SEG_TILE;
+    st.cnt = min(SEG_TILE, seg_start[st.s + 1] - st.base);
+    return true;
+}
+
+// Pass B histogram: tile j's counts of d1 = (key >> 10) & (rb - 1), written at
+// hseg[tb * rb + d * ts + tl] (segment-major, then digit-major, then tile).
+__global__ void __launch_bounds__(SEG_NT) k_seg_hist(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ tile_seg,
+                                                     const uint32_t* __restrict__ seg_start,
+                                                     const uint32_t* __restrict__ seg_tb, uint32_t rb,
+                                                     uint32_t* __restrict__ hseg) {
+    __shared__ uint32_t s_cnt[SEG_RMAX];
+    SegTile st;
+    if (!seg_tile(blockIdx.x, tile_seg, seg_start, seg_tb, st)) return;
+    for (uint32_t d = threadIdx.x; d < SEG_RMAX; d += SEG_NT) s_cnt[d] = 0;
+    const uint32_t lane = lane_id();
+    uint32_t k[SEG_IT];
+#pragma unroll
+    for (int r = 0; r < SEG_IT; ++r) {
+        const uint32_t i = r * SEG_NT + threadIdx.x;
+        k[r] = keys[st.base + min(i, st.cnt - 1)];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SEG_IT; ++r) {
+        const bool valid = r * SEG_NT + threadIdx.x < st.cnt;
+        const uint32_t d = (k[r] >> B2_LOW_BITS) & (rb - 1);
+        const unsigned long long act = __ballot(valid);
+        if (act == 0) continue;
+        const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
+        const unsigned long long hot = __ballot(valid && d == d0);
+        if (valid) {
+            if (d != d0) atomicAdd(&s_cnt[d], 1u);
+            else if (lane == lead) atomicAdd(&s_cnt[d], (uint32_t)__popcll(hot));
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < rb; d += SEG_NT) hseg[(size_t)st.tb * rb + (size_t)d * st.ts + st.tl] = s_cnt[d];
+}
+
+// Pass B scatter: tile j's (key, index) records ranked stably by d1 and written at the flat-scanned
+// positions hseg[tb * rb + d * ts + tl] + rank: the range-local key (key & 1023) as u16 and the index.
+__global__ void __launch_bounds__(SEG_NT) k_seg_scatter(const uint32_t* __restrict__ keys_in,
+                                                        const uint32_t* __restrict__ vals_in,
+                                                        const uint32_t* __restrict__ tile_seg,
+                                                        const uint32_t* __restrict__ seg_start,
+                                                        const uint32_t* __restrict__ seg_tb, uint32_t rb,
+                                                        const uint32_t* __restrict__ hseg,
+                                                        uint16_t* __restrict__ keys_out,
+                                                        uint32_t* __restrict__ vals_out, uint32_t xcd) {
+    constexpr int NW = SEG_NT / WAVE;
+    constexpr int IT = SEG_IT;
+    __shared__ uint32_t s_cnt[NW / 2][SEG_RMAX];         // wave pair (2p, 2p + 1): low / high 16 bits
+    __shared__ uint32_t s_gbase[SEG_RMAX];
+    __shared__ uint32_t s_key[SEG_TILE];
+    __shared__ uint32_t s_val[SEG_TILE];
+    __shared__ uint32_t s_wsum[NW];
+    SegTile st;
+    if (!seg_tile(xcd_tile(blockIdx.x, gridDim.x, xcd), tile_seg, seg_start, seg_tb, st)) return;
+    const uint32_t mask = rb - 1;
+    for (uint32_t d = threadIdx.x; d < SEG_RMAX; d += SEG_NT) {
+#pragma unroll
+        for (int p = 0; p < NW / 2; ++p) s_cnt[p][d] = 0;
+        s_gbase[d] = d < rb ? hseg[(size_t)st.tb * rb + (size_t)d * st.ts + st.tl] : 0u;
+    }
+    const uint32_t lane = lane_id();
+    const uint32_t w = threadIdx.x / WAVE;
+    const uint32_t half = (w & 1u) * 16u;
+    const uint32_t one = 1u << half;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    uint32_t kk[IT], vv[IT], rk[IT];
+#pragma unroll
+    for (int r = 0; r < IT; ++r) {
+        const uint32_t p = min((w * IT + r) * WAVE + lane, st.cnt - 1);
+        kk[r] = __builtin_nontemporal_load(keys_in + st.base + p);
+        vv[r] = __builtin_nontemporal_load(vals_in + st.base + p);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r0 = 0; r0 < IT; r0 += 8) {
+        unsigned long long hot[8];
+        uint32_t lead[8];
+#pragma unroll
+        for (int r = r0; r < r0 + 8; ++r) {
+            const bool valid = (w * IT + r) * WAVE + lane < st.cnt;
+            const uint32_t d = (kk[r] >> B2_LOW_BITS) & mask;
+            const unsigned long long live = __ballot(valid);
+            const uint32_t ld = live ? (uint32_t)__ffsll((long long)live) - 1 : 0u;
+            const uint32_t hd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)ld);
+            hot[r - r0] = __ballot(valid && d == hd);
+            lead[r - r0] = ld;
+            rk[r] = 0;
+            if (valid && (d != hd || lane == ld))
+                rk[r] = atomicAdd(&s_cnt[w >> 1][d], lane == ld ? (uint32_t)__popcll(hot[r - r0]) << half : one);
+        }
+#pragma unroll
+        for (int r = r0; r < r0 + 8; ++r) {
+            const uint32_t mine = (rk[r] >> half) & 0xFFFFu;
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)lead[r - r0]);
+            rk[r] = ((hot[r - r0] >> lane) & 1ull) ? b0 + (uint32_t)__popcll(hot[r - r0] & lt) : mine;
+        }
+    }
+    __syncthreads();
+    // per digit (one a thread): the waves' exclusive prefix into the halves, the tile-local digit start
+    uint32_t run = 0;
+    {
+        const uint32_t d = threadIdx.x;
+#pragma unroll
+        for (int p = 0; p < NW / 2; ++p) {
+            const uint32_t c = s_cnt[p][d];
+            const uint32_t lo = c & 0xFFFFu, hi = c >> 16;
+            s_cnt[p][d] = run | ((run + lo) << 16);
+            run += lo + hi;
+        }
+    }
+    const uint32_t ex = block_excl_scan_add_n<SEG_NT>(run, s_wsum);
+    {
+        const uint32_t d = threadIdx.x;
+#pragma unroll
+        for (int p = 0; p < NW / 2; ++p) s_cnt[p][d] += ex | (ex << 16);
+        s_gbase[d] -= ex;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < IT; ++r) {
+        if ((w * IT + r) * WAVE + lane < st.cnt) {
+            const uint32_t d = (kk[r] >> B2_LOW_BITS) & mask;
+            const uint32_t at = ((s_cnt[w >> 1][d] >> half) & 0xFFFFu) + rk[r];
+            s_key[at] = kk[r];
+            s_val[at] = vv[r];
+        }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < IT; ++j) {
+        const uint32_t p = j * SEG_NT + threadIdx.x;
+        if (p < st.cnt) {
+            const uint32_t k = s_key[p];
+            const uint32_t g = s_gbase[(k >> B2_LOW_BITS) & mask] + p;
+            keys_out[g] = (uint16_t)(k & ((1u << B2_LOW_BITS) - 1));
+            vals_out[g] = s_val[p];
+        }
+    }
+}
+
+// Start of range b in pass B's output: the flat-scanned count of its (segment, digit) row's first
+// tile, or the segment start when the segment has no tile.
+__device__ __forceinline__ uint32_t range_start(uint32_t b, uint32_t a, const uint32_t* hseg,
+                                                const uint32_t* seg_start, const uint32_t* seg_tb) {
+    const uint32_t s = b >> a, d = b & ((1u << a) - 1);
+    const uint32_t tb = seg_tb[s], ts = seg_tb[s + 1] - tb;
+    return ts ? hseg[(size_t)tb * (1u << a) + (size_t)d * ts] : seg_start[s];
+}
+
+struct L2Lists {
+    uint32_t* rs;          // [R + 1] range starts
+    uint32_t* small;       // [R]
+    uint32_t* staged;      // [R]
+    uint32_t* cr_b;        // chunked ranges: range, first chunk, chunks
+    uint32_t* cr_cb;
+    uint32_t* cr_n;
+    uint32_t* chunk_r;     // chunk -> chunked range
+    uint32_t* ctr;         // L2_CTR_WORDS
+};
+
+// Range b's start and size, and its work list (wave-aggregated appends: one atomic a wave and list).
+// A chunked range reserves its chunks and its entry with one 64-bit atomic (chunks in the low word,
+// ranges in the high word), so the chunked ranges' first chunks increase with their entries.
+__global__ void __launch_bounds__(BLOCK) k_l2_classify(const uint32_t* __restrict__ hseg,
+                                                       const uint32_t* __restrict__ seg_start,
+                                                       const uint32_t* __restrict__ seg_tb, uint32_t a, uint32_t R,
+                                                       uint32_t n, uint32_t t_small, L2Lists l) {
+    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t lane = lane_id();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const bool valid = b < R;
+    uint32_t S = 0, cls = 3;
+    if (valid) {
+        const uint32_t r0 = range_start(b, a, hseg, seg_start, seg_tb);
+        const uint32_t r1 = b + 1 < R ? range_start(b + 1, a, hseg, seg_start, seg_tb) : n;
+        l.rs[b] = r0;
+        if (b + 1 == R) l.rs[R] = n;
+        S = r1 - r0;
+        cls = S <= t_small ? 0u : (S <= MSD_CAP ? 1u : 2u);
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < 2; ++c) {
+        const unsigned long long m = __ballot(cls == c);
+        if (m == 0) continue;
+        const uint32_t lead = (uint32_t)__ffsll((long long)m) - 1;
+        uint32_t base = 0;
+        if (lane == lead) base = atomicAdd(&l.ctr[c], (uint32_t)__popcll(m));
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)lead);
+        if (cls == c) (c == 0 ? l.small : l.staged)[base + (uint32_t)__popcll(m & lt)] = b;
+    }
+    const unsigned long long mc = __ballot(cls == 2);
+    if (mc == 0) return;
+    const uint32_t C = cls == 2 ? (S + CH_CAP - 1) / CH_CAP : 0u;
+    const uint32_t incl = wave_incl_sum_dpp(C);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
+    unsigned long long old = 0;
+    if (lane == 0)
+        old = atomicAdd(reinterpret_cast<unsigned long long*>(l.ctr + 2),
+                        ((unsigned long long)__popcll(mc) << 32) | total);
+    const uint32_t olo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)old, 0);
+    const uint32_t ohi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(old >> 32), 0);
+    const uint32_t my_r = ohi + (uint32_t)__popcll(mc & lt), my_cb = olo + incl - C;
+    if (cls == 2) {
+        l.cr_b[my_r] = b;
+        l.cr_cb[my_r] = my_cb;
+        l.cr_n[my_r] = C;
+    }
+    // the chunk -> range map, written by the whole wave one chunked lane at a time
+    unsigned long long rem = mc;
+    while (rem) {
+        const uint32_t src = (uint32_t)__ffsll((long long)rem) - 1;
+        rem &= rem - 1;
+        const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)my_r, (int)src);
+        const uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)my_cb, (int)src);
+        const uint32_t cn = (uint32_t)__builtin_amdgcn_readlane((int)C, (int)src);
+        for (uint32_t c = lane; c < cn; c += WAVE) l.chunk_r[cb + c] = r;
+    }
+}
+
+// Level 2, thin ranges (S <= t_small): one wave a range, its 1,024 counters in the wave's 4 KB of LDS:
+// count, exclusive scan (16 DPP wave scans, written out as the range's bucket starts), then rows in
+// order ranked by ds_add_rtn (stable) and stored at their places in the range's slice of perm.
+__global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16_t* __restrict__ keys16,
+                                                                   const uint32_t* __restrict__ idx, L2Lists l,
+                                                                   uint32_t n, uint32_t n_act,
+                                                                   uint32_t* __restrict__ perm,
+                                                                   uint32_t* __restrict__ offsets,
+                                                                   uint32_t* __restrict__ rank_out) {
+    __shared__ uint32_t s_cnt[L2_SMALL_WAVES][MSD_L];
+    const uint32_t lane = lane_id(), w = threadIdx.x / WAVE;
+    uint32_t* cnt = s_cnt[w];
+    const uint32_t m = l.ctr[0];
+    constexpr uint32_t U = 4;
+    for (uint32_t i = blockIdx.x * L2_SMALL_WAVES + w; i < m; i += gridDim.x * L2_SMALL_WAVES) {
+        const uint32_t b = l.small[i];
+        const uint32_t base = l.rs[b], S = l.rs[b + 1] - base;
+        const uint32_t k0 = b << MSD_SHIFT;
+        const uint32_t L = min(MSD_L, n_act + 1 - k0);
+        const uint16_t* rk = keys16 + base;
+        const uint32_t* ri = idx + base;
+#pragma unroll
+        for (uint32_t q = 0; q < MSD_L / (4 * WAVE); ++q) reinterpret_cast<uint4*>(cnt)[q * WAVE + lane] = make_uint4(0, 0, 0, 0);
+        wave_lds_sync();
+        for (uint32_t i0 = 0; i0 < S; i0 += U * WAVE) {
+            uint32_t k[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t j = i0 + u * WAVE + lane;
+                k[u] = j < S ? (uint32_t)rk[j] : NONE32;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u)
+                if (k[u] != NONE32) atomicAdd(&cnt[k[u]], 1u);
+        }
+        wave_lds_sync();
+        uint32_t carry = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < MSD_L / WAVE; ++q) {
+            const uint32_t x = cnt[q * WAVE + lane];
+            const uint32_t inc = wave_incl_sum_dpp(x);
+            const uint32_t e = carry + inc - x;
+            cnt[q * WAVE + lane] = e;
+            if (q * WAVE + lane < L) offsets[k0 + q * WAVE + lane] = base + e;
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, WAVE - 1);
+        }
+        if (lane == 0 && b == (n_act >> MSD_SHIFT)) offsets[n_act + 1] = n;
+        wave_lds_sync();
+        for (uint32_t i0 = 0; i0 < S; i0 += U * WAVE) {
+            uint32_t k[U], v[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t j = i0 + u * WAVE + lane;
+                k[u] = j < S ? (uint32_t)rk[j] : NONE32;
+                v[u] = j < S ? ri[j] : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                if (k[u] == NONE32) continue;
+                const uint32_t p = base + atomicAdd(&cnt[k[u]], 1u);
+                perm[p] = v[u];
+                if (rank_out) rank_out[v[u]] = p;
+            }
+        }
+        wave_lds_sync();
+    }
+}
+
+// Level 2, hot ranges: chunk j's activation counts, hh[j * 1,024 + a].
+__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_hist(const uint16_t* __restrict__ keys16, L2Lists l,
+                                                          uint32_t* __restrict__ hh) {
+    __shared__ uint32_t s_cnt[MSD_L];
+    const uint32_t tid = threadIdx.x, lane = lane_id();
+    const uint32_t m = l.ctr[2];
+    for (uint32_t j = blockIdx.x; j < m; j += gridDim.x) {
+        const uint32_t r = l.chunk_r[j], b = l.cr_b[r];
+        const uint32_t rsb = l.rs[b], c = j - l.cr_cb[r];
+        const uint32_t start = rsb + c * CH_CAP, cs = min(CH_CAP, l.rs[b + 1] - start);
+        s_cnt[tid] = 0;
+        uint32_t k[CH_RW];
+#pragma unroll
+        for (uint32_t q = 0; q < CH_RW; ++q) k[q] = keys16[start + min(q * MSD_NT + tid, cs - 1)];
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < CH_RW; ++q) {
+            const bool valid = q * MSD_NT + tid < cs;
+            const unsigned long long act = __ballot(valid);
+            if (act == 0) continue;
+            const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
+            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)k[q], (int)lead);
+            const unsigned long long hot = __ballot(valid && k[q] == d0);
+            if (valid) {
+                if (k[q] != d0) atomicAdd(&s_cnt[k[q]], 1u);
+                else if (lane == lead) atomicAdd(&s_cnt[k[q]], (uint32_t)__popcll(hot));
+            }
+        }
+        __syncthreads();
+        hh[(size_t)j * MSD_L + tid] = s_cnt[tid];
+        __syncthreads();
+    }
+}
+
+// Level 2, hot ranges: for chunked range r and activations [16 g, 16 g + 16), the exclusive prefix of
+// each activation's chunk counts over the range's chunks, in place (hh), and its total (tot).  The
+// 16-column slab of up to 1,024 chunks goes through LDS (rows padded to 17 words: the column scans
+// are conflict-free), one wave a column, 16 DPP scans of 64 rows each.
+constexpr uint32_t CS_COLS = 16;
+constexpr uint32_t CS_ROWS = 1024;
+__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_scan(L2Lists l, uint32_t* __restrict__ hh,
+                                                          uint32_t* __restrict__ tot) {
+    __shared__ uint32_t s_m[CS_ROWS * (CS_COLS + 1)];
+    const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / WAVE;
+    const uint32_t items = l.ctr[3] * (MSD_L / CS_COLS);
+    for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const uint32_t r = it / (MSD_L / CS_COLS), g = it % (MSD_L / CS_COLS);
+        const uint32_t cb = l.cr_cb[r], C = l.cr_n[r];
+        uint32_t carry = 0;                              // wave w: column w
+        for (uint32_t c0 = 0; c0 < C; c0 += CS_ROWS) {
+            const uint32_t rows = min(CS_ROWS, C - c0);
+            uint32_t* src = hh + (size_t)(cb + c0 + tid) * MSD_L + g * CS_COLS;
+            if (tid < rows) {
+#pragma unroll
+                for (uint32_t q = 0; q < CS_COLS / 4; ++q) {
+                    const uint4 v = reinterpret_cast<const uint4*>(src)[q];
+                    uint32_t* d = s_m + tid * (CS_COLS + 1) + 4 * q;
+                    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (uint32_t q = 0; q < CS_COLS; ++q) s_m[tid * (CS_COLS + 1) + q] = 0;
+            }
+            __syncthreads();
+#pragma unroll 4
+            for (uint32_t q = 0; q < CS_ROWS / WAVE; ++q) {
+                uint32_t* p = s_m + (q * WAVE + lane) * (CS_COLS + 1) + w;
+                const uint32_t x = *p;
+                const uint32_t inc = wave_incl_sum_dpp(x);
+                *p = carry + inc - x;
+                carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, WAVE - 1);
+            }
+            __syncthreads();
+            if (tid < rows) {
+#pragma unroll
+                for (uint32_t q = 0; q < CS_COLS / 4; ++q) {
+                    const uint32_t* d = s_m + tid * (CS_COLS + 1) + 4 * q;
+                    reinterpret_cast<uint4*>(src)[q] = make_uint4(d[0], d[1], d[2], d[3]);
+                }
+            }
+            __syncthreads();
+        }
+        if (lane == 0) tot[(size_t)r * MSD_L + g * CS_COLS + w] = carry;
+    }
+}
+
+// Level 2, hot ranges: chunk j = chunk c of range b, ranked and staged in LDS like a range
+// (msd_range), each activation's items written at its start in the range + its count in the earlier
+// chunks.  Chunk 0 writes the range's bucket starts.
+struct ChunkShared {
+    uint32_t out[CH_CAP];
+    uint16_t key[CH_CAP];
+    uint32_t wc[MSD_NW][MSD_LW];
+    uint32_t run[MSD_L];
+    uint32_t delta[MSD_L];
+    uint32_t red[MSD_NW];
+};
+__global__ void __launch_bounds__(MSD_NT, 4) k_l2_chunk_scatter(const uint16_t* __restrict__ keys16,
+                                                                const uint32_t* __restrict__ idx, L2Lists l,
+                                                                const uint32_t* __restrict__ hh,
+                                                                const uint32_t* __restrict__ tot, uint32_t n,
+                                                                uint32_t n_act, uint32_t* __restrict__ perm,
+                                                                uint32_t* __restrict__ offsets,
+                                                                uint32_t* __restrict__ rank_out) {
+    __shared__ ChunkShared sh;
+    const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+    const uint32_t m = l.ctr[2];
+    for (uint32_t j = blockIdx.x; j < m; j += gridDim.x) {
+        const uint32_t r = l.chunk_r[j], b = l.cr_b[r];
+        const uint32_t rsb = l.rs[b], c = j - l.cr_cb[r];
+        const uint32_t start = rsb + c * CH_CAP, cs = min(CH_CAP, l.rs[b + 1] - start);
+        const uint32_t k0 = b << MSD_SHIFT;
+        const uint32_t L = min(MSD_L, n_act + 1 - k0);
+        // activation tid: its start in the range (scan of the totals) and its base for this chunk
+        const uint32_t as = block_excl_scan_add_n<MSD_NT>(tot[(size_t)r * MSD_L + tid], sh.red);
+        const uint32_t gb = rsb + as + hh[(size_t)j * MSD_L + tid];
+        if (c == 0) {
+            if (tid < L) offsets[k0 + tid] = rsb + as;
+            if (tid == 0 && b == (n_act >> MSD_SHIFT)) offsets[n_act + 1] = n;
+        }
+        for (uint32_t x = tid; x < MSD_NW * MSD_LW; x += MSD_NT) (&sh.wc[0][0])[x] = 0;
+        const uint32_t seg = (cs + MSD_NW - 1) / MSD_NW;
+        const uint32_t s0 = min(w * seg, cs), s1 = min((w + 1) * seg, cs);
+        const uint16_t* rk = keys16 + start;
+        const uint32_t* ri = idx + start;
+        uint32_t kp[CH_RW / 2];
+        {
+            const uint32_t last = cs - 1;
+#pragma unroll
+            for (uint32_t q = 0; q < CH_RW; q += 2) {
+                const uint32_t i = s0 + q * WAVE + lane;
+                const uint32_t x = rk[min(i, last)], y = rk[min(i + WAVE, last)];
+                kp[q / 2] = (i < s1 ? x : 0xFFFFu) | ((i + WAVE < s1 ? y : 0xFFFFu) << 16);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < CH_RW; ++q) {
+            const uint32_t k = (kp[q / 2] >> (16 * (q & 1))) & 0xFFFFu;
+            if (k != 0xFFFFu) atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < CH_RW / 2; ++q) asm volatile("" : "+v"(kp[q]));
+        __syncthreads();
+        uint32_t tlo, thi;
+        msd_wave_prefix(&sh.wc[0][0], tid, tlo, thi);
+        const uint32_t ex = block_excl_scan_add_n<MSD_NT>(tlo + thi, sh.red);
+        if (tid < MSD_LW) {
+            sh.run[2 * tid] = ex;
+            sh.run[2 * tid + 1] = ex + tlo;
+        }
+        __syncthreads();
+        sh.delta[tid] = gb - sh.run[tid];                // chunk-local position -> global position
+#pragma unroll
+        for (uint32_t g = 0; g < CH_RW; g += MSD_G) {
+            uint32_t mm[MSD_G];
+#pragma unroll
+            for (uint32_t q = 0; q < (uint32_t)MSD_G; ++q) {
+                const uint32_t i = s0 + (g + q) * WAVE + lane;
+                mm[q] = i < s1 ? ri[i] : 0u;
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < (uint32_t)MSD_G; ++q) {
+                const uint32_t k = (kp[(g + q) / 2] >> (16 * ((g + q) & 1))) & 0xFFFFu;
+                if (k == 0xFFFFu) continue;
+                const uint32_t old = atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
+                const uint32_t at = sh.run[k] + ((old >> (16 * (k & 1))) & 0xFFFFu);
+                sh.out[at] = mm[q];
+                sh.key[at] = (uint16_t)k;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < CH_RW; ++q) {
+            const uint32_t i = q * MSD_NT + tid;
+            if (i < cs) {
+                const uint32_t v = sh.out[i];
+                const uint32_t p = sh.delta[sh.key[i]] + i;
+                perm[p] = v;
+                if (rank_out) rank_out[v] = p;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace gd

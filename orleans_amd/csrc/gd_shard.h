@@ -206,7 +206,9 @@ __global__ void __launch_bounds__(BLOCK) k_recv_idx16(const uint8_t* __restrict_
     if (threadIdx.x == 0) {
         uint32_t run = 0, brun = 0, crun = 0;
         for (uint32_t q = 0; q < world; ++q) {
-            const bool w16 = (rdesc[4 * q + 1] & KD_IDX16) != 0;
+            // the host's rule (route_multi): a sender that sent this rank nothing sent no block starts
+            // either, whatever its descriptor says (one descriptor goes to every peer)
+            const bool w16 = rcount[q] != 0 && (rdesc[4 * q + 1] & KD_IDX16) != 0;
             s_off[q] = run;
             s_boff[q] = brun;
             s_coff[q] = crun;

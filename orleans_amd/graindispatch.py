@@ -39,6 +39,7 @@ EXPORTED_SYMBOLS = [
     "gd_route_bucket", "gd_route_device", "gd_bucket_device", "gd_route_bucket_device",
     "gd_ring_owner_device", "gd_pack_by_shard_device", "gd_pack_routes_by_rank_device", "gd_kernel_times",
     "gd_kernel_times_reset",
+    "gd_option_set", "gd_option_get", "gd_tune_reset", "gd_tune_set", "gd_tune_get", "gd_tune_agree",
     "gd_set_kernel_timing", "gd_microbatch_create", "gd_microbatch_destroy", "gd_microbatch_keys",
     "gd_microbatch_outputs", "gd_microbatch_run", "gd_decode_frames_device", "gd_decode_frames",
     "gd_route_frames_device", "gd_route_frames", "gd_dir_split", "gd_dir_split_device",
@@ -313,6 +314,12 @@ def _load() -> C.CDLL:
         "gd_fanout_multi_fetch": (C.c_int, [P, U32] + [P] * 9),
         "gd_dir_handoff_multi": (C.c_int, [P, P, U32, C.c_int, U32, C.POINTER(gd_handoff_result)]),
         "gd_dir_handoff_fetch": (C.c_int, [P] + [P] * 7),
+        "gd_option_set": (C.c_int, [P, C.c_int, C.c_int64]),
+        "gd_option_get": (C.c_int, [P, C.c_int, C.POINTER(C.c_int64)]),
+        "gd_tune_reset": (C.c_int, [P]),
+        "gd_tune_set": (C.c_int, [P, C.c_int, C.c_int]),
+        "gd_tune_get": (C.c_int, [P, C.c_int, U64, U32, C.POINTER(C.c_int)]),
+        "gd_tune_agree": (C.c_int, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -389,6 +396,15 @@ def _check(h, rc: int):
         raise GrainDispatchError(rc, msg.decode() if msg else "")
 
 
+# ---- handle options (include/graindispatch.h GD_OPT_*) and measured choices (GD_TUNE_*) -----------
+OPTIONS = {"probe": 1, "bucket": 2, "l2_small": 3, "stable_rank": 4, "wire_headers": 5, "region_probe": 6,
+           "idx16": 7, "host_chunk": 8, "mb_zerocopy": 9, "mb_split": 10, "mb_trace": 11}
+TUNE_KINDS = {"probe_keys": 0, "probe_n1": 1, "probe_fanout": 2, "probe_nodes": 3, "bucket": 4}
+# Options applied to every handle this process creates, before its own `options=` (the test and tool
+# harness sets these; a C# host calls gd_option_set on its handle instead).
+DEFAULT_OPTIONS: dict = {}
+
+
 # ---- the handle --------------------------------------------------------------------
 
 class GrainDispatch:
@@ -396,13 +412,39 @@ class GrainDispatch:
     GPU owns + scratch, on one HIP stream."""
 
     def __init__(self, device: int = 0, table_capacity: int = 1 << 20, my_silo: int = 0,
-                 seed_silo: int = NO_SILO, kernel_timing: bool = False):
+                 seed_silo: int = NO_SILO, kernel_timing: bool = False, options: Optional[dict] = None):
         cfg = gd_config(C.sizeof(gd_config), device, table_capacity, my_silo, seed_silo, 0,
                         CFG_KERNEL_TIMING if kernel_timing else 0)
         h = C.c_void_p()
         _check(None, lib.gd_create(C.byref(cfg), C.byref(h)))
         self.h = h
         self.device = device
+        for k, v in {**DEFAULT_OPTIONS, **(options or {})}.items():
+            self.set_option(k, v)
+
+    # -- options and measured choices ------------------------------------------
+    def set_option(self, name, value: int):
+        self._c(lib.gd_option_set(self.h, OPTIONS[name] if isinstance(name, str) else name, int(value)))
+
+    def get_option(self, name) -> int:
+        v = C.c_int64(0)
+        self._c(lib.gd_option_get(self.h, OPTIONS[name] if isinstance(name, str) else name, C.byref(v)))
+        return v.value
+
+    def tune_reset(self):
+        self._c(lib.gd_tune_reset(self.h))
+
+    def tune_set(self, kind, variant: int):
+        self._c(lib.gd_tune_set(self.h, TUNE_KINDS[kind] if isinstance(kind, str) else kind, variant))
+
+    def tune_get(self, kind, n: int, sub: int = 0) -> int:
+        v = C.c_int(0)
+        self._c(lib.gd_tune_get(self.h, TUNE_KINDS[kind] if isinstance(kind, str) else kind, n, sub, C.byref(v)))
+        return v.value
+
+    def tune_agree(self):
+        """Collective over the handle's communicator: every rank keeps the same measured choices."""
+        self._c(lib.gd_tune_agree(self.h))
 
     def close(self):
         if getattr(self, "h", None):

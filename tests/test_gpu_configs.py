@@ -28,9 +28,9 @@ TCD = o.type_code_data(o.CAT_GRAIN, TC)
 
 @pytest.fixture(autouse=True)
 def _region_order(monkeypatch):
-    """These tests expect the region-grouped arrival order (GD_REGION_PROBE=1, the sender's switch);
+    """These tests expect the region-grouped arrival order (GD_OPT_REGION_PROBE = 1, the sender's option);
     test_route_multi_local_world_plain_order runs the other."""
-    monkeypatch.setenv("GD_REGION_PROBE", "1")
+    monkeypatch.setitem(gd.DEFAULT_OPTIONS, "region_probe", 1)
 
 
 @pytest.fixture(scope="module")
@@ -282,15 +282,14 @@ def test_cfg3_exchange_w8_zipf(gd):
 
 
 # ----------------------------------------------------------------------------- histogram variants
-@pytest.mark.parametrize("tpb", ["1", "4", "8"])
-@pytest.mark.parametrize("n,n_act", [(4097, 17), (12345, 256), (70001, 1 << 20), (5_000_003, 1 << 20)])
-def test_bucket_hist_variants_unaligned(gd, monkeypatch, tpb, n, n_act):
-    """The radix histogram with 1, 4 and 8 tiles per workgroup (GD_HIST_TPB, read at gd_create) on
-    ragged sizes, from an activation array that starts 4 bytes past a 16-B boundary (the unaligned
-    branch) and from an aligned one."""
+@pytest.mark.parametrize("n,n_act", [(4097, 17), (12345, 256), (70001, 1 << 20), (5_000_003, 1 << 20),
+                                     (5_000_003, 3_000_000)])
+def test_bucket_hist_variants_unaligned(gd, monkeypatch, n, n_act):
+    """The LSD path's radix histogram with 1 tile per workgroup (below 1,024 tiles) and 4 (5M
+    messages), and the two-level forms' MSD histograms, on ragged sizes, from an activation array
+    that starts 4 bytes past a 16-B boundary (the unaligned branch) and from an aligned one."""
     import torch
-    monkeypatch.setenv("GD_HIST_TPB", tpb)
-    rng = np.random.default_rng(n + int(tpb))
+    rng = np.random.default_rng(n + 4)
     acts = rng.integers(0, n_act + n_act // 8 + 1, size=n).astype(np.uint32)
     acts[rng.random(n) < 0.01] = o.M32
     wp, wo = o.bucket_stable(acts, n_act)
@@ -312,21 +311,22 @@ def test_bucket_hist_variants_unaligned(gd, monkeypatch, tpb, n, n_act):
 
 
 # ----------------------------------------------------------------------------- packed radix records
-@pytest.mark.parametrize("pack", ["0", "1"])
+@pytest.mark.parametrize("bucket", [0, 2])
 @pytest.mark.parametrize("n,n_act,skew", [(70001, 1 << 20, False), (5_000_003, 1 << 20, True),
                                           (1 << 24, 1 << 20, False), (3_000_001, (1 << 16) + 5, False),
                                           (200_000, (1 << 23) + 3, True), (33_554_431, 1 << 20, False),
-                                          (300_001, (1 << 24) - 5, False)])
-def test_bucket_packed_records(gd, monkeypatch, pack, n, n_act, skew):
-    """Records packed to 6 B between the radix passes (GD_RADIX_PACK, read at gd_create): index and
-    first digit in a u32, the higher key bits in a u16 that the later histograms read alone.  The
+                                          (300_001, (1 << 24) - 5, False), (6_000_001, (1 << 24) - 5, True)])
+def test_bucket_packed_records(gd, monkeypatch, bucket, n, n_act, skew):
+    """The LSD passes (GD_OPT_BUCKET 0) pack records to 6 B between the passes where they fit: index
+    and first digit in a u32, the higher key bits in a u16 that the later histograms read alone.  The
     shapes cover the u16 histogram with 1 and 4 tiles per workgroup, ragged tails, a u16 holding all
     16 bits (2^23 + 3 activations, 8-bit digits), an index and first digit filling all 32 bits
-    (2^25 - 1 messages, 7-bit digits), unrouted messages and a hot key; the same output with and
-    without packing, against the oracle.  The 8-bit shapes end in 2^16-activation digit ranges that
-    the one-launch range scan covers in 4 sub-ranges (most of them empty at 2^24 - 5)."""
+    (2^25 - 1 messages, 7-bit digits), unrouted messages and a hot key.  The same shapes through the
+    two-level forms where they apply (GD_OPT_BUCKET 2: batches of 2^20 messages and up), against the
+    oracle.  The 8-bit shapes end in 2^16-activation digit ranges that the one-launch range scan
+    covers in 4 sub-ranges (most of them empty at 2^24 - 5)."""
     import torch
-    monkeypatch.setenv("GD_RADIX_PACK", pack)
+    monkeypatch.setitem(gd.DEFAULT_OPTIONS, "bucket", bucket)
     rng = np.random.default_rng(n ^ n_act)
     acts = rng.integers(0, n_act + n_act // 8 + 1, size=n).astype(np.uint32)
     if skew:

@@ -1,6 +1,6 @@
-"""The compact probe index (gd_cx.h, GD_CX): a derived copy of the directory table for the route
+"""The compact probe index (gd_cx.h, GD_OPT_PROBE): a derived copy of the directory table for the route
 probe, rebuilt after every change of the table.  Routes through it must equal routes through the
-directory table itself (GD_CX=0) and the oracle, after every kind of directory change
+directory table itself (GD_OPT_PROBE 0) and the oracle, after every kind of directory change
 (registration, RemoveActivation, AddActivation / multi-activation upserts, silo removal, handoff
 Merge, split-and-move, clear, rehash), with the IsValidSilo filter, and when the table is not
 eligible (an N0 != 0 key, more than 256 TypeCodeData) or the batch holds keys the index cannot
@@ -26,16 +26,12 @@ def gd():
 
 
 def _pair(gd, mode, cap, cx_mode="2", **kw):
-    """(engine with the index: GD_CX=cx_mode -- 2 group reads, 3 slot reads, 1 measured choice; engine
-    without: GD_CX=0)."""
+    """(engine with the index: GD_OPT_PROBE = cx_mode -- 2 group reads, 3 slot reads, 1 measured choice;
+    engine without: 0)."""
     silos = o.bench_silos(8)
     out = []
     for cx in (cx_mode, "0"):
-        os.environ["GD_CX"] = cx
-        try:
-            e = gd.GrainDispatch(device=0, table_capacity=cap, **kw)
-        finally:
-            os.environ.pop("GD_CX", None)
+        e = gd.GrainDispatch(device=0, table_capacity=cap, options={"probe": int(cx)}, **kw)
         e.ring_set_silos(mode, [(s.ip, s.port, s.gen) for s in silos])
         out.append(e)
     return out, o.ring_spec(silos, mode)

@@ -1,13 +1,16 @@
-"""The two-level bucketing (gd_msd.h, GD_MSD): a stable MSD pass into ranges of 1,024 activations,
-then one workgroup per range sorting it in LDS and writing its bucket starts.  Its permutation and
-offsets must equal the stable partition of the oracle (o.bucket_stable: the per-activation FIFO,
-IncomingMessageAgent.cs:92-190, ActivationData.cs:566-606) and the LSD path's, for every shape the
-path takes: range edges, the unrouted bucket n_act, empty ranges, ranges staged in LDS and ranges
-over the staging capacity (hot activations: chunks stored straight to global memory), ranges either
-side of that capacity in one launch, the largest n_act the MSD digit takes, and through the fused
-route + bucket and the receive path (which also asks for the inverse permutation)."""
-import os
+"""The two-level bucketing (GD_OPT_BUCKET): ranges of 1,024 activations, each sorted stably in LDS.
 
+One-pass form (gd_msd.h, n_act < 1,081,344): one MSD pass into the ranges, one workgroup a range.
+Three-pass form (gd_msd2.h, n_act up to 2^28): two MSD passes (the second segmented, its positions
+from one flat scan), then the ranges in three work lists -- thin ranges one wave each, staged ranges
+one workgroup each, hot ranges in chunks over several workgroups.
+
+The permutation and offsets must equal the stable partition of the oracle (o.bucket_stable: the
+per-activation FIFO, IncomingMessageAgent.cs:92-190, ActivationData.cs:566-606) and the LSD path's,
+for every shape the forms take: range edges, the unrouted bucket n_act, empty ranges, ranges either
+side of each class boundary (the thin-range threshold, the staging capacity 24,576, whole numbers of
+16,384-message chunks), Zipf-hot ranges, the largest n_act of each form, and through the fused route +
+bucket and the receive path (which also asks for the inverse permutation)."""
 import numpy as np
 import pytest
 
@@ -24,37 +27,36 @@ def gd():
     return g
 
 
-# the forms of the second level: the message indices loaded in k_msd_local's rank sweep and the
-# range-local keys as u16 records (the default); the same on u32 keys; the indices loaded with the
-# keys; u16 positions staged with the indices gathered at write-out
-FORMS = {"late": {"GD_MSD_G16": "0", "GD_MSD_EARLY": "0", "GD_MSD_K16": "1"},
-         "late32": {"GD_MSD_G16": "0", "GD_MSD_EARLY": "0", "GD_MSD_K16": "0"},
-         "early": {"GD_MSD_G16": "0", "GD_MSD_EARLY": "1", "GD_MSD_K16": "0"},
-         "g16": {"GD_MSD_G16": "1", "GD_MSD_EARLY": "0", "GD_MSD_K16": "0"}}
+def _engine(gd, bucket, **opts):
+    """GD_OPT_BUCKET: 0 the LSD passes, 1 measured, 2 the two-level form wherever it applies."""
+    return gd.GrainDispatch(device=0, table_capacity=1 << 12, options=dict(opts, bucket=int(bucket)))
 
 
-def _engine(gd, msd, form="late"):
-    env = dict(FORMS[form], GD_MSD=msd)
-    os.environ.update(env)
-    try:
-        return gd.GrainDispatch(device=0, table_capacity=1 << 12)
-    finally:
-        for k in env:
-            os.environ.pop(k, None)
-
-
-SHAPES = [
+ONE_PASS = [
     # (n, n_act, kind)
     (1 << 20, 1 << 20, "uniform"),
     (1 << 22, 1 << 20, "uniform"),
     (3_000_017, 4096, "uniform"),
     (1_500_001, 4097, "uniform"),
-    (1 << 21, 1056 * 1024 - 1, "uniform"),                     # the largest n_act of the MSD digit
+    (1 << 21, 1056 * 1024 - 1, "uniform"),                     # the largest n_act of the one-pass form
     (1 << 20, 43 * 1024 - 1, "uniform"),                       # ~24.4 K a range: either side of MSD_CAP
     (1 << 21, 1000, "uniform"),
     (1 << 21, 300_000, "unrouted"),
     (1 << 21, 1 << 20, "hot"),
     (1 << 22, 1 << 16, "sparse"),
+]
+
+THREE_PASS = [
+    (1 << 20, 1056 * 1024, "uniform"),                         # the smallest n_act of the three-pass form
+    (1 << 21, 1 << 21, "uniform"),                             # ~1,024 a range: thin / staged boundary
+    (1 << 22, 1 << 21, "zipf"),                                # hot ranges in chunks
+    (1 << 22, 1 << 21, "hot"),                                 # one activation with 70 % of the batch
+    (1 << 22, 10_000_000, "zipf"),                             # BASELINE cfg 4's n_act
+    (1 << 22, 100_000_000, "zipf"),                            # BASELINE cfg 3's n_act
+    (1 << 21, 100_000_000, "uniform"),                         # ~21 messages a range
+    (3_000_017, 5_000_000, "unrouted"),
+    (1 << 21, 1 << 21, "edges"),                               # ranges of exactly 24,576 / 24,577 / 32,768 ...
+    (1 << 20, (1 << 27) + 5, "uniform"),                       # 18-bit ranges: 9 + 9 digit bits
 ]
 
 
@@ -65,31 +67,77 @@ def _acts(n, n_act, kind, seed):
         a[rng.random(n) < 0.2] = 0xFFFFFFFF                     # GD_NO_ACTIVATION: the trailing bucket
         a[rng.random(n) < 0.05] = n_act + rng.integers(0, 5, size=n)[0]
     elif kind == "hot":
-        a[rng.random(n) < 0.7] = 4095                           # one activation over many u16 chunks
+        a[rng.random(n) < 0.7] = 4095                           # one activation over many chunks
         a[rng.random(n) < 0.1] = 4096 * 7 + 3
     elif kind == "sparse":
         a = rng.choice(np.arange(0, n_act, 4099), size=n)       # most ranges empty or thin
+    elif kind == "zipf":
+        a = (rng.zipf(1.1, size=n) - 1) % n_act                 # Zipf(1.1): low activations hot
+    elif kind == "edges":
+        # whole ranges of chosen sizes around the class boundaries, the rest thin
+        sizes = {5: 24576, 7: 24577, 9: 32768, 11: 32769, 13: 16384, 17: 1024, 19: 1025, 23: 49153}
+        parts = [rng.integers(b * 1024, b * 1024 + 1024, size=s) for b, s in sizes.items()]
+        rest = n - sum(sizes.values())
+        r = rng.integers(0, n_act, size=rest)
+        r = r[~np.isin(r >> 10, list(sizes))]
+        a = np.concatenate(parts + [r])
+        rng.shuffle(a)
     return a.astype(np.uint32)
 
 
-@pytest.mark.parametrize("form", list(FORMS))
-@pytest.mark.parametrize("n,n_act,kind", SHAPES)
-def test_msd_bucket_vs_oracle(gd, n, n_act, kind, form):
-    acts = _acts(n, n_act, kind, n + n_act)
-    e2, e0 = _engine(gd, "2", form), _engine(gd, "0")
+def _check(gd, acts, n_act, **opts):
+    e2, e0 = _engine(gd, 2, **opts), _engine(gd, 0)
     p2, off2 = e2.bucket(acts, n_act)
     p0, off0 = e0.bucket(acts, n_act)
-    np.testing.assert_array_equal(p2, p0)
-    np.testing.assert_array_equal(off2, off0)
     wp, wo = o.bucket_stable(acts, n_act)
     np.testing.assert_array_equal(p2, wp)
     np.testing.assert_array_equal(off2, wo)
+    np.testing.assert_array_equal(p0, wp)
+    np.testing.assert_array_equal(off0, wo)
+    return e2, e0
+
+
+@pytest.mark.parametrize("n,n_act,kind", ONE_PASS)
+def test_msd_one_pass_vs_oracle(gd, n, n_act, kind):
+    e2, e0 = _check(gd, _acts(n, n_act, kind, n + n_act), n_act)
     e2.close()
     e0.close()
 
 
+@pytest.mark.parametrize("n,n_act,kind", THREE_PASS)
+def test_msd_three_pass_vs_oracle(gd, n, n_act, kind):
+    e2, e0 = _check(gd, _acts(n, n_act, kind, n + n_act + 3), n_act)
+    e2.close()
+    e0.close()
+
+
+@pytest.mark.parametrize("small", [0, 300, 24576])
+def test_msd_three_pass_class_threshold(gd, small):
+    """The thin-range threshold moves ranges between the wave form and the workgroup form (0: every
+    non-empty range staged; 24,576: every non-hot range a wave); the result never changes."""
+    acts = _acts(1 << 21, 3 << 20, "zipf", 77)
+    e2, e0 = _check(gd, acts, 3 << 20, l2_small=small)
+    e2.close()
+    e0.close()
+
+
+def test_msd_three_pass_kernels(gd):
+    """The three-pass form runs its own kernels (not the LSD passes) when forced."""
+    acts = _acts(1 << 21, 5_000_000, "zipf", 9)
+    e = _engine(gd, "2")
+    e.set_kernel_timing(True)
+    p, off = e.bucket(acts, 5_000_000)
+    names = set(e.kernel_times())
+    assert {"k_seg_hist", "k_seg_scatter", "k_l2_classify", "k_l2_small", "k_l2_chunk_scatter"} <= names, names
+    assert "k_starts_rangescan" not in names
+    wp, wo = o.bucket_stable(acts, 5_000_000)
+    np.testing.assert_array_equal(p, wp)
+    np.testing.assert_array_equal(off, wo)
+    e.close()
+
+
 def test_msd_measured_choice_and_fused_route(gd):
-    """GD_MSD=1 (the default): the first launches of a batch size alternate the two forms; every
+    """GD_OPT_BUCKET 1 (the default): the first launches of a batch size alternate the two forms; every
     result along the way is the stable partition."""
     silos = o.bench_silos(8)
     spec = o.ring_spec(silos, "D")
@@ -112,14 +160,16 @@ def test_msd_measured_choice_and_fused_route(gd):
     e.close()
 
 
-def test_msd_receive_with_limits(gd):
+@pytest.mark.parametrize("n_ctx", [1 << 18, 1_200_000])
+def test_msd_receive_with_limits(gd, n_ctx):
     """The receive path with overload limits asks the bucketing for the inverse permutation too
     (each message's place in its context's FIFO, IncomingMessageAgent.cs:142 CheckOverloaded):
-    with the two-level form forced, statuses, contexts, permutation and offsets equal the oracle's."""
+    with the two-level form forced (one-pass at 2^18 contexts, three-pass at 1.2M), statuses,
+    contexts, permutation and offsets equal the oracle's."""
     import torch
     from test_gpu_receive import _world
     import receive as rv
-    rng, keys, ctxs, flags, tg, ta, direction = _world(23, 1 << 18, 16, 1 << 21)
+    rng, keys, ctxs, flags, tg, ta, direction = _world(23, n_ctx, 16, 1 << 21)
     n_ctx, n = len(keys), len(tg)
     e = _engine(gd, "2")
     e.actdir_add(keys, ctxs, flags)
@@ -147,14 +197,16 @@ def test_msd_receive_with_limits(gd):
 
 def test_msd_measured_choice_per_shape(gd):
     """The measured choice is kept per batch size and per messages-a-range class: one handle
-    alternating 2^21 messages over 2^20 activations (ranges staged in LDS) and over 10,000 (ranges
-    far over the staging capacity) stays bit-exact on every launch, through both forms' timing."""
+    alternating 2^21 messages over 2^20 activations (ranges staged in LDS), over 10,000 (ranges far
+    over the staging capacity) and over 3M (the three-pass form) stays bit-exact on every launch,
+    through every form's timing."""
     e = _engine(gd, "1")
-    shapes = [(_acts(1 << 21, 1 << 20, "uniform", 5), 1 << 20), (_acts(1 << 21, 10000, "uniform", 6), 10000)]
+    shapes = [(_acts(1 << 21, 1 << 20, "uniform", 5), 1 << 20), (_acts(1 << 21, 10000, "uniform", 6), 10000),
+              (_acts(1 << 21, 3_000_000, "zipf", 7), 3_000_000)]
     want = [o.bucket_stable(a, na) for a, na in shapes]
-    for i in range(10):
-        a, na = shapes[i % 2]
+    for i in range(15):
+        a, na = shapes[i % 3]
         p, off = e.bucket(a, na)
-        np.testing.assert_array_equal(p, want[i % 2][0])
-        np.testing.assert_array_equal(off, want[i % 2][1])
+        np.testing.assert_array_equal(p, want[i % 3][0])
+        np.testing.assert_array_equal(off, want[i % 3][1])
     e.close()

@@ -21,9 +21,9 @@ TC = o.grain_type_code(o.PING_GRAIN_CLASS)
 
 @pytest.fixture(autouse=True)
 def _region_order(monkeypatch):
-    """These tests expect the region-grouped arrival order (GD_REGION_PROBE=1, the sender's switch);
+    """These tests expect the region-grouped arrival order (GD_OPT_REGION_PROBE = 1, the sender's option);
     test_route_multi_local_world_plain_order runs the other."""
-    monkeypatch.setenv("GD_REGION_PROBE", "1")
+    monkeypatch.setitem(gd.DEFAULT_OPTIONS, "region_probe", 1)
 
 
 @pytest.fixture(scope="module")
@@ -511,9 +511,9 @@ def _expected_owner_side(batches, spec, full, W, r, by_region=True):
 def test_route_multi_local_world(gd, W, by_region, monkeypatch):
     """gd_route_multi at W ranks (in-process transport): owner-side arrival order, routes and
     per-activation buckets, and the routes returned to every sender in batch order.  by_region:
-    GD_REGION_PROBE (senders group each chunk by table region, the owner probes region by XCD);
+    GD_OPT_REGION_PROBE (senders group each chunk by table region, the owner probes region by XCD);
     without it the arrival order is (sender rank, sender order)."""
-    monkeypatch.setenv("GD_REGION_PROBE", "1" if by_region else "0")
+    monkeypatch.setitem(gd.DEFAULT_OPTIONS, "region_probe", 1 if by_region else 0)
     silos = o.bench_silos(8)
     G = 6000
     reg = o.grain_keys(TC, np.arange(G))
@@ -560,7 +560,7 @@ def test_route_multi_local_pipelined_and_forward(gd, by_region, monkeypatch):
     call later), then the forward hop with activations away from their owners.  Without the region
     order the batches travel with 2-B origin indices (KD_IDX16), which the forward hop carries on."""
     import torch
-    monkeypatch.setenv("GD_REGION_PROBE", "1" if by_region else "0")
+    monkeypatch.setitem(gd.DEFAULT_OPTIONS, "region_probe", 1 if by_region else 0)
     W, G = 4, 5000
     silos = o.bench_silos(8)
     reg = o.grain_keys(TC, np.arange(G))
@@ -712,12 +712,11 @@ def test_route_multi_ext_local_world(gd):
 @pytest.mark.parametrize("compact,narrow", [("1", "1"), ("1", "0"), ("0", "1")])
 def test_route_multi_local_mixed_headers(gd, compact, narrow, monkeypatch):
     """Exchange header compaction: a batch of one grain type with long keys travels as N1s alone
-    (k_key_desc / k_recv_expand), 4 B each when every N1 is below 2^32 (GD_NARROW_HEADERS), else 8.
+    (k_key_desc / k_recv_expand), 4 B each when every N1 is below 2^32 (GD_OPT_WIRE_HEADERS 2), else 8.
     Ranks here send: one type with small keys (u32 N1s), another type with keys above 2^32 (u64
     N1s, other TCD), guid grains mixed in (full 24-B headers), nothing at all; with compaction off
-    (GD_COMPACT_HEADERS=0) everything goes as 24 B.  The results are identical either way."""
-    monkeypatch.setenv("GD_COMPACT_HEADERS", compact)
-    monkeypatch.setenv("GD_NARROW_HEADERS", narrow)
+    (GD_OPT_WIRE_HEADERS 0) everything goes as 24 B.  The results are identical either way."""
+    monkeypatch.setitem(gd.DEFAULT_OPTIONS, "wire_headers", 0 if compact == "0" else (2 if narrow == "1" else 1))
     W = 4
     silos = o.bench_silos(8)
     tc2 = o.grain_type_code("UnitTests.Grains.SimpleGrain")
@@ -771,7 +770,7 @@ def test_route_multi_local_no_keys(gd, two_types, big, monkeypatch):
     types, or u32 and u64 chunks mixed (one sender with big keys), the keys are rebuilt first.
     Results other than recv_keys (left unset) are the same either way."""
     by_region = not big                               # the big-key cases run with 2-B origin indices
-    monkeypatch.setenv("GD_REGION_PROBE", "1" if by_region else "0")
+    monkeypatch.setitem(gd.DEFAULT_OPTIONS, "region_probe", 1 if by_region else 0)
     W, G = 3, 4000
     silos = o.bench_silos(8)
     tc2 = o.grain_type_code("UnitTests.Grains.SimpleGrain")
@@ -816,11 +815,11 @@ def test_route_multi_local_no_keys(gd, two_types, big, monkeypatch):
 def test_route_multi_local_idx16_mixed(gd, idx16, monkeypatch):
     """2-B origin indices on the wire (KD_IDX16: low 16 bits + per-rank block starts, rebuilt by
     k_recv_idx16) at W = 3 with senders of both widths in one round: rank 1's handle was created
-    with GD_IDX16=0 (4-B indices), ranks 0 and 2 with the parameter; rank 0's batch spans four
+    with GD_OPT_IDX16 0 (4-B indices), ranks 0 and 2 with the parameter; rank 0's batch spans four
     65,536-index blocks with a long one-owner stretch (empty blocks for the other owners), rank 2
     sends nothing.  Owner-side order (sender rank, sender order), routes and buckets against the
     oracle."""
-    monkeypatch.setenv("GD_REGION_PROBE", "0")
+    monkeypatch.setitem(gd.DEFAULT_OPTIONS, "region_probe", 0)
     W, G = 3, 5000
     silos = o.bench_silos(8)
     reg = o.grain_keys(TC, np.arange(G))
@@ -831,8 +830,8 @@ def test_route_multi_local_idx16_mixed(gd, idx16, monkeypatch):
         act[own % W == r] = np.arange(int((own % W == r).sum()))
     es = []
     for r in range(W):
-        monkeypatch.setenv("GD_IDX16", "0" if r == 1 else idx16)
-        e = gd.GrainDispatch(device=0, table_capacity=1 << 13, my_silo=r)
+        e = gd.GrainDispatch(device=0, table_capacity=1 << 13, my_silo=r,
+                             options={"idx16": 0 if r == 1 else int(idx16)})
         e.ring_set_silos("D", [(x.ip, x.port, x.gen) for x in silos])
         mine = own % W == r
         e.register(reg[mine], act[mine], own[mine])
@@ -859,6 +858,58 @@ def test_route_multi_local_idx16_mixed(gd, idx16, monkeypatch):
         wp, wo = o.bucket_stable(a, n_act[r])
         np.testing.assert_array_equal(res[r]["perm"], wp)
         np.testing.assert_array_equal(res[r]["offsets"], wo)
+    for e in es:
+        e.comm_destroy()
+        e.close()
+
+
+def test_route_multi_local_idx16_silent_sender(gd, monkeypatch):
+    """a 2-B-index sender with a non-empty batch that sends one owner nothing,
+    followed by a higher-ranked 2-B sender whose chunk for that owner spans blocks past 65,536.
+    k_recv_idx16 must skip the silent sender's block starts (it sent none) exactly as the host
+    layout does, or every later chunk's high 16 bits come from the wrong column.  W = 3, every
+    handle with 2-B indices: rank 0 sends only to ranks 0 and 1, rank 1 sends ~100k messages to
+    rank 2."""
+    monkeypatch.setitem(gd.DEFAULT_OPTIONS, "region_probe", 0)
+    monkeypatch.setitem(gd.DEFAULT_OPTIONS, "idx16", 1)
+    W, G = 3, 6000
+    silos = o.bench_silos(8)
+    reg = o.grain_keys(TC, np.arange(G))
+    spec = o.ring_spec(silos, "D")
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    act = np.zeros(G, np.uint32)
+    for r in range(W):
+        act[own % W == r] = np.arange(int((own % W == r).sum()))
+    es = []
+    for r in range(W):
+        e = gd.GrainDispatch(device=0, table_capacity=1 << 14, my_silo=r)
+        e.ring_set_silos("D", [(x.ip, x.port, x.gen) for x in silos])
+        mine = own % W == r
+        e.register(reg[mine], act[mine], own[mine])
+        e.set_kernel_timing(True)
+        es.append(e)
+    gd.GrainDispatch.comm_init_local(es)
+    rng = np.random.default_rng(161)
+    by_rank = [np.nonzero(own % W == r)[0] for r in range(W)]
+    not2 = np.concatenate([by_rank[0], by_rank[1]])
+    b0 = rng.choice(not2, size=90_000)                           # n > 0, nothing for owner 2
+    b1 = rng.integers(0, G, size=300_000)                        # ~100k for owner 2: blocks 0..4
+    b2 = rng.integers(0, G, size=1_000)
+    batches = [o.grain_keys(TC, b0), o.grain_keys(TC, b1), o.grain_keys(TC, b2)]
+    n_act = [int((own % W == r).sum()) for r in range(W)]
+    res = _run_ranks([lambda r=r: es[r].route_multi(batches[r], n_act[r]) for r in range(W)])
+    assert "k_recv_idx16" in es[2].kernel_times()
+    full = o.DirectoryArrays(reg, act, own)
+    for r in range(W):
+        rk, ids, srcs, st, silo, a = _expected_owner_side(batches, spec, full, W, r, by_region=False)
+        np.testing.assert_array_equal(res[r]["recv_idx"], ids)
+        np.testing.assert_array_equal(res[r]["recv_src"], srcs)
+        np.testing.assert_array_equal(res[r]["status"], st)
+        np.testing.assert_array_equal(res[r]["act"], a)
+        wp, wo = o.bucket_stable(a, n_act[r])
+        np.testing.assert_array_equal(res[r]["perm"], wp)
+        np.testing.assert_array_equal(res[r]["offsets"], wo)
+    assert int((res[2]["recv_src"] == 1).sum()) > 65_536
     for e in es:
         e.comm_destroy()
         e.close()

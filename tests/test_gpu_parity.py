@@ -391,22 +391,18 @@ def _check_runs(mb, n, want_act, n_act):
     assert np.array_equal(np.diff(mb.run_start[:r + 1]), np.bincount(clamped, minlength=n_act + 1)[ua])
 
 
-MB_VARIANTS = {  # GD_MB_* switches read at gd_microbatch_create
+MB_VARIANTS = {  # GD_OPT_MB_* options, read at gd_microbatch_create
     "zero_copy": {},
-    "zero_copy_one_sorter": {"GD_MB_SPLIT": "1"},
-    "digits_7": {"GD_MB_MAXBITS": "7"},
-    "digits_4": {"GD_MB_MAXBITS": "4"},
-    "staged_copies": {"GD_MB_ZEROCOPY": "0"},
+    "zero_copy_one_sorter": {"mb_split": 1},
+    "staged_copies": {"mb_zerocopy": 0},
 }
 
 
 @pytest.mark.parametrize("variant,mode", [("zero_copy", "D"), ("zero_copy", "R"), ("zero_copy", "V"),
-                                          ("zero_copy_one_sorter", "V"), ("digits_7", "D"),
-                                          ("digits_4", "R"),
-                                          ("staged_copies", "V")])
+                                          ("zero_copy_one_sorter", "V"), ("staged_copies", "V")])
 def test_microbatch_graph_matches_eager_and_oracle(gd, monkeypatch, variant, mode):
     for k, v in MB_VARIANTS[variant].items():
-        monkeypatch.setenv(k, v)
+        monkeypatch.setitem(gd.DEFAULT_OPTIONS, k, v)
     silos = o.bench_silos(8)
     spec = o.ring_spec(silos, mode)
     G = 50000
@@ -893,10 +889,10 @@ def test_randomized_configurations(gd):
 @pytest.mark.parametrize("pinned", [False, True])
 def test_route_bucket_host_pipelined(gd, pinned, monkeypatch):
     """gd_route_bucket's pipelined host path (chunked H2D / probe / D2H on three streams, then the
-    bucketing of the whole batch), forced on with small chunks (GD_HOST_CHUNK), from pageable and
+    bucketing of the whole batch), forced on with small chunks (GD_OPT_HOST_CHUNK), from pageable and
     from gd_host_alloc'd pinned buffers; a ragged last chunk."""
     import ctypes as C
-    monkeypatch.setenv("GD_HOST_CHUNK", "4096")
+    monkeypatch.setitem(gd.DEFAULT_OPTIONS, "host_chunk", 4096)
     silos = o.bench_silos(8)
     spec = o.ring_spec(silos, "V")
     e = _engine(gd, silos, "V", cap=1 << 15, my_silo=2)

@@ -4,7 +4,7 @@
 4,096-message batches of the cfg2 distribution (uniform over 2^20 registered grains,
 8 silos, ring D), each batch = keys in pinned host memory -> k_mb_route (reads them in
 place) -> k_mb_sort_runs -> results written straight to pinned host memory (zero-copy;
-GD_MB_ZEROCOPY=0 for the staged H2D / D2H form), replayed as one hipGraph
+GD_OPT_MB_ZEROCOPY 0 for the staged H2D / D2H form), replayed as one hipGraph
 (gd_microbatch_run(..., use_graph=1)) or launched eagerly.  Reports p50/p99/max wall
 latency per batch over --batches batches, and checks a sample of graph replays bit-exact
 against the library's gd_route_bucket.  bench.py reports the same measurement with the CPU
