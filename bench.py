@@ -54,44 +54,176 @@ def grain_keys(type_code_data: int, ks: np.ndarray) -> np.ndarray:
 
 
 def radix_layout(n: int, n_act: int):
-    """(passes, digit bits, packed) of libgraindispatch's bucketing for n messages over n_act
-    activations (gd_engine.hip bucket_device): <= 8-bit digits; records packed to 6 B between the
-    passes (GD_RADIX_PACK, on by default) when the key bits above the first digit fit a u16 and the
-    message index fits a u32 beside the first digit."""
+    """(passes, digit bits, packed) of libgraindispatch's LSD bucketing for n messages over n_act
+    activations (gd_engine.hip bucket_lsd): <= 8-bit digits; records packed to 6 B between the passes
+    when the key bits above the first digit fit a u16 and the message index fits a u32 beside the
+    first digit."""
     key_bits = max(1, int(n_act).bit_length())
     passes = (key_bits + 7) // 8
     bits = max(4, -(-key_bits // passes))
     ib = max(1, int(max(n, 1) - 1).bit_length())
-    packed = (passes >= 2 and bits <= 8 and key_bits - bits <= 16 and ib + bits <= 32
-              and os.environ.get("GD_RADIX_PACK", "1") != "0")
+    packed = passes >= 2 and bits <= 8 and key_bits - bits <= 16 and ib + bits <= 32
     return passes, bits, packed
 
 
-def kernel_bytes(name: str, n: int, n_act: int, passes: int, world: int, form: str = "lsd") -> float:
-    """Algorithmic HBM bytes of one step for a kernel (all launches of it), per
-    DESIGN.md 'Byte model'.  form "msd": the two-level bucketing (gd_msd.h) -- one MSD pass reading
-    the activation (histogram, scatter) and writing (index, range-local key) 6-B records, then
-    k_msd_local reading them, writing the index in order and every bucket start once."""
-    _, _, packed = radix_layout(n, n_act)
-    if name == "k_route":
-        return n * (24 + 32 + 4 + 4 + 1)          # key, one slot, silo+act+status
-    if form == "msd":
-        rec = 6 if os.environ.get("GD_MSD_K16", "1") != "0" else 8      # u32 index + u16 (or u32) key
-        return {"k_radix_scatter": n * (4 + rec), "k_radix_hist": n * 4,
-                "k_msd_local": n * (rec + 4) + (n_act + 2) * 4}.get(name, 0.0)
-    if name == "k_radix_scatter":
-        # pass 1 reads act, writes (key, idx); middle passes move (key, idx); the last pass reads
-        # (key, idx) and writes idx only (it emits the bucket starts instead of the sorted keys).
-        # Packed: (key, idx) is 6 B (u32 index + first digit, u16 higher key bits).
+MSD_CAP, CH_CAP, L2_SMALL = 24576, 16384, 1024     # gd_msd.h / gd_msd2.h
+
+
+def bucket_form(names) -> str:
+    """The bucketing form a step ran, from its kernel names: "msd3" (the three-pass two-level form,
+    gd_msd2.h), "msd" (the one-pass two-level form, gd_msd.h) or "lsd" (the LSD radix passes)."""
+    if "k_seg_scatter" in names:
+        return "msd3"
+    if "k_msd_local" in names:
+        return "msd"
+    return "lsd"
+
+
+def l2_classes(acts: np.ndarray, n_act: int, t_small: int = L2_SMALL) -> dict:
+    """The three-pass form's level-2 work (gd_msd2.h k_l2_classify) for one batch: per class, the
+    messages and activations it owns; chunks and ranges of the hot class."""
+    k = np.minimum(acts.astype(np.int64), n_act) >> 10
+    R = (n_act >> 10) + 1
+    S = np.bincount(k, minlength=R)
+    per = np.full(R, 1024, np.int64)
+    per[-1] = n_act + 1 - (R - 1) * 1024
+    small, hot = S <= t_small, S > MSD_CAP
+    staged = ~small & ~hot
+    return {"small": (int(S[small].sum()), int(per[small].sum())),
+            "staged": (int(S[staged].sum()), int(per[staged].sum())),
+            "hot": (int(S[hot].sum()), int(per[hot].sum())), "chunks": int(((S[hot] + CH_CAP - 1) // CH_CAP).sum()),
+            "hot_ranges": int(hot.sum()), "ranges": R}
+
+
+def bucket_bytes(form: str, n: int, n_act: int, acts=None) -> dict:
+    """Algorithmic HBM bytes of one bucketing of n messages over n_act activations, per kernel name
+    (all its launches), for the form the library ran (DESIGN 5 byte tables).  Every form writes the
+    permutation (4 B a message) and the n_act + 2 bucket starts (4 B each)."""
+    off = (n_act + 2) * 4
+    if form == "lsd":
+        passes, _, packed = radix_layout(n, n_act)
         if passes == 1:
-            return n * 8
-        return n * (10 + 12 * (passes - 2) + 10) if packed else n * (12 + 16 * (passes - 2) + 12)
-    if name == "k_radix_hist":
-        # pass 1 reads act; packed, the later passes read the u16 high-key array alone
-        return n * (4 + 2 * (passes - 1)) if packed else n * 4 * passes
-    if name == "k_bucket_starts":
-        return n * 4 + (n_act + 2) * 4
-    return 0.0
+            sc = n * 8.0
+        else:
+            sc = n * (10 + 12 * (passes - 2) + 10) if packed else n * (12 + 16 * (passes - 2) + 12)
+        # the first histogram fills the starts, the last scatter lowers them, one range scan reads and
+        # writes them
+        return {"k_radix_hist": (n * (4 + 2 * (passes - 1)) if packed else n * 4 * passes) + off,
+                "k_radix_scatter": sc, "k_starts_rangescan": 2 * off}
+    if form == "msd":
+        # one MSD pass (activation read twice, 6-B record written), the in-LDS range sort (record read,
+        # index written in order, every start written once)
+        return {"k_radix_hist": n * 4.0, "k_radix_scatter": n * 10.0, "k_msd_local": n * 10.0 + off}
+    # msd3: pass A (activation read twice, 8-B record written), pass B (key read for the histogram,
+    # the record read, a 6-B record written; its [segment][digit][tile] counts flat-scanned), level 2
+    # (record read, index written in order, starts written once, per class)
+    kb = max(1, (n_act >> 10).bit_length())
+    a = (kb + 1) // 2
+    tiles = -(-n // 8192) + (n_act >> (10 + a)) + 1
+    cnt = (1 << a) * tiles * 4.0
+    c = l2_classes(acts, n_act) if acts is not None else None
+    out = {"k_radix_hist": n * 4.0, "k_radix_scatter": n * 12.0, "k_seg_hist": n * 4.0 + cnt,
+           "k_scan_reduce": cnt, "k_scan_down": 2 * cnt, "k_seg_scatter": n * 14.0 + cnt,
+           "k_l2_classify": ((n_act >> 10) + 1) * 12.0}
+    if c is None:
+        out["k_l2_small"] = n * 10.0 + off      # unknown split: all charged to one kernel
+        return out
+    out.update({"k_l2_small": c["small"][0] * 10.0 + c["small"][1] * 4.0,
+                "k_msd_local": c["staged"][0] * 10.0 + c["staged"][1] * 4.0,
+                "k_l2_chunk_hist": c["hot"][0] * 2.0 + c["chunks"] * 4096.0,
+                "k_l2_chunk_scan": c["chunks"] * 8192.0 + c["hot_ranges"] * 4096.0,
+                "k_l2_chunk_scatter": c["hot"][0] * 10.0 + c["hot"][1] * 4.0 + c["chunks"] * 8192.0})
+    if (n_act + 1) % 1024:
+        out["k_l2_small"] += 8.0                # offsets[n_act + 1]
+    return out
+
+
+# The kernels of a bucketing stage (every form), for the stage total
+BUCKET_KERNELS = ("k_radix_hist", "k_radix_rowscan", "k_radix_scatter", "k_msd_local", "k_starts_rangescan",
+                  "k_scan_reduce", "k_scan_down", "k_fill", "k_seg_table", "k_seg_hist", "k_seg_scatter",
+                  "k_l2_classify", "k_l2_small", "k_l2_chunk_hist", "k_l2_chunk_scan", "k_l2_chunk_scatter")
+
+
+def kernel_bytes(name: str, n: int, n_act: int, form: str = "lsd", acts=None) -> float:
+    """Algorithmic HBM bytes of one step for a kernel (all launches of it), per DESIGN.md's byte
+    tables: the route (key 24 + one 32-B directory slot + silo/act/status 9 B) and the
+    bucketing form's kernels (bucket_bytes)."""
+    if name == "k_route":
+        return n * (24 + 32 + 4 + 4 + 1)
+    return float(bucket_bytes(form, n, n_act, acts).get(name, 0.0))
+
+
+def load_pmc(tag: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary profiles/pmc_<tag>_<kernel>.json
+    (cfg2: profiles/pmc_<kernel>.json), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{kernel}.json" if tag == "cfg2" else f"pmc_{tag}_{kernel}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get("hbm_bytes_per_launch")
+
+
+def roofline_of(kt: dict, steps: int, n: int, n_act: int, acts, tag, world: int = 1, bytes_fn=None):
+    """(kernels, roofline) from in-library HIP-event kernel times kt {name: (launches, ms)} over `steps`
+    steps of one workload: per kernel its algorithmic GB/s and fraction of HBM peak; the dominant
+    kernel's roofline with its PMC traffic (profiles/pmc_*.json at this workload, N = 1) and the ratio
+    of that traffic to the algorithmic bytes; the bucketing kernels (the MSD scatter and the level-2
+    range sort, or the LSD scatter) on their implementation bytes -- `frac` -- with SURVEY 8(d)'s
+    16 B/record/pass model beside them; and the whole bucketing stage against the 12-B contract.
+    bytes_fn(name, form): a kernel's bytes a step when a step is not one batch (the cfg 4 cascade)."""
+    form = bucket_form(kt)
+    kernels = {}
+    for name, (launches, ms) in kt.items():
+        if launches == 0:
+            continue
+        per_step_ms = ms / steps
+        b = bytes_fn(name, form) if bytes_fn else kernel_bytes(name, n, n_act, form, acts)
+        gbs = b / (per_step_ms * 1e-3) / 1e9 if b and per_step_ms > 0 else None
+        kernels[name] = {"launches_per_step": launches // steps, "ms_per_step": round(per_step_ms, 4),
+                         "alg_bytes_per_step": b or None, "alg_GBps": round(gbs, 1) if gbs else None,
+                         "frac_hbm": round(gbs / PEAK_HBM_GBS, 4) if gbs else None}
+    if not kernels:
+        return kernels, None
+    pmc_tag = tag if world == 1 else None
+
+    def entry(name):
+        d = kernels[name]
+        launches = max(1, d["launches_per_step"])
+        t = d["ms_per_step"] / launches * 1e-3
+        alg = (d["alg_bytes_per_step"] or 0.0) / launches
+        traffic = load_pmc(pmc_tag, name) if pmc_tag else None
+        return {"kernel": name, "achieved": d["alg_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": d["frac_hbm"], "traffic": traffic, "alg_bytes_per_launch": alg,
+                "traffic_ratio": round(traffic / alg, 3) if traffic and alg else None,
+                "frac_pmc": round(traffic / t / 1e9 / PEAK_HBM_GBS, 4) if traffic and t > 0 else None,
+                "avg_launch_ms": round(t * 1e3, 5), "launches_per_step": launches}
+
+    dom = max((k for k in kernels if not k.startswith("rccl_")), key=lambda k: kernels[k]["ms_per_step"])
+    roofline = dict(entry(dom), bound="hbm")
+    if dom == "k_route":
+        roofline["bytes_model"] = "SURVEY 8(d): key 24 + one 32-B directory slot + silo/act/status 9 B"
+    bk = {}
+    for name in ("k_radix_scatter", "k_msd_local", "k_seg_scatter", "k_l2_small", "k_l2_chunk_scatter"):
+        if name in kernels and kernels[name]["alg_bytes_per_step"]:
+            e = entry(name)
+            launches = e["launches_per_step"]
+            if name in ("k_radix_scatter", "k_seg_scatter"):
+                # SURVEY 8(d)'s model: 16 B per record per radix pass, side field
+                sm = 16.0 * n / max(1, kernels[name]["launches_per_step"])
+                e["frac_survey_model"] = round(sm / (e["avg_launch_ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+            bk[name] = e
+    if bk:
+        roofline["bucketing_kernel"] = dict(form=form, bytes_model="implementation bytes (DESIGN 5); frac_pmc on "
+                                            "the PMC counters' bytes where profiles/ holds them", **bk)
+    stage = [k for k in BUCKET_KERNELS if k in kernels]
+    st_ms = sum(kernels[k]["ms_per_step"] for k in stage)
+    st_b = sum(kernels[k]["alg_bytes_per_step"] or 0.0 for k in stage)
+    roofline["bucketing_stage"] = {
+        "form": form, "kernels": stage, "ms_per_step": round(st_ms, 4),
+        "impl_bytes_per_message": round(st_b / max(1, n), 2), "contract_bytes_per_message": 12,
+        "frac_impl": round(st_b / (st_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4) if st_ms > 0 else None,
+        "frac_contract": round(12.0 * n / (st_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4) if st_ms > 0 else None}
+    return kernels, roofline
 
 
 def zipf_keys(tcd: int, n_grains: int, n: int, seed: int, dev) -> torch.Tensor:
@@ -117,6 +249,7 @@ def setup_workload(args, workload, world, rank, local, dev, tcd, msgs, grains):
         G_total = Gr * world
     cap = 2 * Gr if workload == "cfg2" else 1 << int(np.ceil(np.log2(2 * Gr)))
     e = g.GrainDispatch(device=local, table_capacity=cap, my_silo=rank % 8, kernel_timing=False)
+    pin_choices(e, args, workload)
     silos = SILO_SETS[args.silos]
     pts, own = e.ring_set_silos(args.mode, silos)
     engine = DeviceEngine(e, dev)
@@ -195,7 +328,10 @@ def setup_workload(args, workload, world, rank, local, dev, tcd, msgs, grains):
         else:
             exchange = "torch.distributed all_to_all_single (RCCL); library exchange disagreed on batch 1 (some rank)"
             assert args.exchange != "library", "library exchange disagrees with the torch exchange"
+    agree = e if world > 1 and router is not None and isinstance(router, LibraryRouter) and args.tune == "measured" \
+        else None
     return {"e": e, "engine": engine, "router": router, "stream": stream, "keys": keys, "N": N, "n_act": n_act,
+            "agree": agree,
             "G_total": G_total, "cap": cap, "pts": pts, "own": own, "exchange": exchange,
             "owner_share_max": round(owner_share, 4), "owner_share_by_set": by_set}
 
@@ -206,13 +342,34 @@ def setup_workload(args, workload, world, rank, local, dev, tcd, msgs, grains):
 # measurement finish before the timed region with any --warmup (the driver uses 5): every timed step
 # then runs the variant the library keeps.
 SETTLE_STEPS = 8
+# --tune pinned: the variants each workload's measured runs settle on, fixed with
+# gd_tune_set before the first launch -- no settle steps, the same variant on every rank
+PINNED = {"cfg2": {"probe_keys": 0, "probe_n1": 0, "bucket": 1},
+          "cfg3": {"probe_keys": 2, "probe_n1": 2, "bucket": 1},
+          "cfg4": {"probe_fanout": 0, "probe_nodes": 0, "bucket": 1}}
 
 
-def timed_steps(router, keys, n_act, stream, steps, warmup):
-    """W untimed steps (after SETTLE_STEPS), then exactly K steps bracketed by barrier + synchronize;
-    max over ranks."""
+def settle_steps(args) -> int:
+    return 0 if args.tune == "pinned" else SETTLE_STEPS
+
+
+def pin_choices(e, args, workload: str):
+    if args.tune == "pinned":
+        for kind, v in PINNED[workload].items():
+            e.tune_set(kind, v)
+
+
+def timed_steps(router, keys, n_act, stream, steps, warmup, settle=SETTLE_STEPS, agree=None):
+    """W untimed steps (after `settle` steps for the library's measured choices, then gd_tune_agree
+    on `agree`'s communicator at N > 1), then exactly K steps bracketed by barrier + synchronize; max
+    over ranks."""
     with torch.cuda.stream(stream):
-        for _ in range(SETTLE_STEPS + warmup):
+        for _ in range(settle):
+            router.route_bucket(keys, n_act)
+        if agree is not None:
+            torch.cuda.synchronize()
+            agree.tune_agree()
+        for _ in range(warmup):
             router.route_bucket(keys, n_act)
         torch.cuda.synchronize()
         dist.barrier()
@@ -272,7 +429,16 @@ def main():
     ap.add_argument("--no-target", action="store_true", help="cfg4: do not write the target node per message")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo, host-staged all-to-all")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="a handle option for every handle (graindispatch.OPTIONS: GD_OPT_*), e.g. bucket=2")
+    ap.add_argument("--tune", default="measured", choices=["measured", "pinned"],
+                    help="measured: the library times its variants on the first launches (settle steps, then "
+                         "gd_tune_agree across ranks at N > 1); pinned: the variants fixed up front "
+                         "(gd_tune_set: compact-index group reads, two-level bucketing), no settle steps")
     args = ap.parse_args()
+    for kv in args.opt:
+        k, v = kv.split("=", 1)
+        g.DEFAULT_OPTIONS[k] = int(v)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -307,17 +473,21 @@ def main():
     e, N, n_act, G_total, cap, router, stream, keys = (w["e"], w["N"], w["n_act"], w["G_total"], w["cap"],
                                                         w["router"], w["stream"], w["keys"])
     exchange = w["exchange"]
-    wall_max, gpu_ms, res = timed_steps(router, keys, n_act, stream, args.steps, args.warmup)
+    wall_max, gpu_ms, res = timed_steps(router, keys, n_act, stream, args.steps, args.warmup, settle_steps(args),
+                                        w["agree"])
     value = N * args.steps * world / wall_max
     secondary = {}
     if world > 1 and args.workload == "cfg2" and not args.no_secondary:
         # BASELINE cfg 3 is the node-level configuration: 64M Zipf(1.1) messages over 100M grains
         # for the whole node (strong scaling), measured by the same harness beside the weak line
         w3 = setup_workload(args, "cfg3", world, rank, local, dev, tcd, args.msgs3, args.grains3)
-        wall3, gpu3, _ = timed_steps(w3["router"], w3["keys"], w3["n_act"], w3["stream"],
-                                     max(10, args.steps // 10), max(3, args.warmup // 4))
+        wall3, gpu3, r3 = timed_steps(w3["router"], w3["keys"], w3["n_act"], w3["stream"],
+                                      max(10, args.steps // 10), max(3, args.warmup // 4), settle_steps(args),
+                                      w3["agree"])
         steps3 = max(10, args.steps // 10)
+        k3, rf3 = secondary_roofline(w3, r3, args, "cfg3", world)
         secondary["cfg3_strong"] = {
+            "roofline": rf3, "kernels": k3,
             "value": round(w3["N"] * steps3 * world / wall3, 1), "unit": "messages/s",
             "ms_per_step": round(wall3 / steps3 * 1e3, 4), "steps": steps3,
             "workload": workload_name("cfg3", world, w3["N"], w3["G_total"]), "msgs_per_gpu": w3["N"],
@@ -331,8 +501,9 @@ def main():
         # fan-out cascade), each with its bounded CPU baseline; the cfg 2 handle stays open
         w3 = setup_workload(args, "cfg3", 1, 0, local, dev, tcd, args.msgs3, args.grains3)
         steps3 = max(10, args.steps // 10)
-        wall3, gpu3, _ = timed_steps(w3["router"], w3["keys"], w3["n_act"], w3["stream"], steps3,
-                                     max(3, args.warmup // 4))
+        wall3, gpu3, r3 = timed_steps(w3["router"], w3["keys"], w3["n_act"], w3["stream"], steps3,
+                                      max(3, args.warmup // 4), settle_steps(args))
+        k3, rf3 = secondary_roofline(w3, r3, args, "cfg3", 1)
         c3 = None
         if not args.no_cpu_baseline:
             c3 = cpu_baseline_cfg3(args, w3, tcd)
@@ -340,12 +511,12 @@ def main():
             "value": round(w3["N"] * steps3 / wall3, 1), "unit": "messages/s",
             "ms_per_step": round(wall3 / steps3 * 1e3, 4), "steps": steps3,
             "workload": workload_name("cfg3", 1, w3["N"], w3["G_total"]), "msgs_per_gpu": w3["N"],
-            "cpu_baseline": c3}
+            "roofline": rf3, "kernels": k3, "cpu_baseline": c3}
         w3["e"].close()
         del w3
         torch.cuda.empty_cache()
         secondary["cfg4"] = measure_cfg4(args, 1, 0, local, dev, steps=max(5, args.steps // 20),
-                                         warmup=max(2, args.warmup // 5), profile_steps=0,
+                                         warmup=max(2, args.warmup // 5), profile_steps=2,
                                          with_cpu=not args.no_cpu_baseline)
 
     # received (owner-side) message count, for the byte model
@@ -353,113 +524,11 @@ def main():
     st_ok = int((res.status == 0).sum().item())
 
     # ---- per-kernel durations (separate steps, HIP events around every launch) -----
-    kt = {}
-    if args.profile_steps > 0:
-        e.set_kernel_timing(True)
-        e.kernel_times_reset()
-        with torch.cuda.stream(stream):
-            for _ in range(args.profile_steps):
-                router.route_bucket(keys, n_act)
-        torch.cuda.synchronize()
-        kt = e.kernel_times()
-        e.set_kernel_timing(False)
-
-    passes, _, packed = radix_layout(m_recv, n_act)
-    form = "msd" if kt.get("k_msd_local", (0, 0))[0] else "lsd"     # the bucketing form the library chose
-    kernels = {}
-    for name, (launches, ms) in kt.items():
-        if launches == 0:
-            continue
-        per_step_ms = ms / args.profile_steps
-        b = kernel_bytes(name, m_recv, n_act, passes, world, form)
-        gbs = b / (per_step_ms * 1e-3) / 1e9 if b and per_step_ms > 0 else None
-        kernels[name] = {"launches_per_step": launches // args.profile_steps, "ms_per_step": round(per_step_ms, 4),
-                         "alg_GBps": round(gbs, 1) if gbs else None,
-                         "frac_hbm": round(gbs / PEAK_HBM_GBS, 4) if gbs else None}
-    roofline = None
-    if kernels:
-        dom = max((k for k in kernels if not k.startswith("rccl_")), key=lambda k: kernels[k]["ms_per_step"])
-        d = kernels[dom]
-        launches = max(1, d["launches_per_step"])
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{dom}.json")   # collected on cfg2 at N = 1
-        if os.path.exists(pmc_path) and args.workload == "cfg2" and world == 1:
-            with open(pmc_path) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        roofline = {"bound": "hbm", "kernel": dom,
-                    "achieved": d["alg_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": d["frac_hbm"], "traffic": traffic,
-                    "alg_bytes_per_launch": kernel_bytes(dom, m_recv, n_act, passes, world) / launches,
-                    "avg_launch_ms": round(d["ms_per_step"] / launches, 5)}
-        if "k_radix_scatter" in kernels:
-            # the north star's "bucketing kernel" target (>= 50% of HBM peak), next to the dominant one
-            sc = kernels["k_radix_scatter"]
-            sl = max(1, sc["launches_per_step"])
-            sc_traffic = None
-            sc_pmc = os.path.join(ROOT, "profiles", "pmc_k_radix_scatter.json")
-            if os.path.exists(sc_pmc) and args.workload == "cfg2" and world == 1:
-                with open(sc_pmc) as f:
-                    sc_traffic = json.load(f).get("hbm_bytes_per_launch")
-            # algorithmic bytes per SURVEY 8(d): 16 B per record per radix pass (read act/key u32 +
-            # message index u32, write both); the bytes this implementation moves (packed 6-B records
-            # between passes, the last pass writing the index alone) are reported beside
-            alg = 16.0 * m_recv
-            t_launch = sc["ms_per_step"] / sl * 1e-3
-            ach = alg / t_launch / 1e9 if t_launch > 0 else None
-            impl = kernel_bytes("k_radix_scatter", m_recv, n_act, passes, world, form) / sl
-            roofline["bucketing_kernel"] = {"form": form,
-                "kernel": "k_radix_scatter", "achieved": round(ach, 1) if ach else None, "peak": PEAK_HBM_GBS,
-                "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4) if ach else None, "traffic": sc_traffic,
-                "launches_per_step": sl, "alg_bytes_per_launch": alg, "bytes_model": "SURVEY 8(d): 16 B/record/pass",
-                "avg_launch_ms": round(sc["ms_per_step"] / sl, 5), "packed_records": packed,
-                "impl_bytes_per_launch": impl,
-                "frac_impl": round(impl / t_launch / 1e9 / PEAK_HBM_GBS, 4) if t_launch > 0 else None,
-                # on the HBM bytes the PMC counters saw per launch (profiles/pmc_k_radix_scatter.json)
-                "frac_pmc": round(sc_traffic / t_launch / 1e9 / PEAK_HBM_GBS, 4) if sc_traffic and t_launch > 0
-                else None}
-            if form == "msd" and "k_msd_local" in kernels:
-                # the second level: each 1,024-activation range counting-sorted in LDS, written in order
-                ml = kernels["k_msd_local"]
-                t_ml = ml["ms_per_step"] / max(1, ml["launches_per_step"]) * 1e-3
-                ml_traffic = None
-                ml_pmc = os.path.join(ROOT, "profiles", "pmc_k_msd_local.json")
-                if os.path.exists(ml_pmc) and args.workload == "cfg2" and world == 1:
-                    with open(ml_pmc) as f:
-                        ml_traffic = json.load(f).get("hbm_bytes_per_launch")
-                roofline["bucketing_kernel"]["k_msd_local"] = {
-                    "impl_bytes_per_launch": kernel_bytes("k_msd_local", m_recv, n_act, passes, world, form),
-                    "avg_launch_ms": round(t_ml * 1e3, 5), "frac_impl": ml["frac_hbm"], "traffic": ml_traffic,
-                    "frac_pmc": round(ml_traffic / t_ml / 1e9 / PEAK_HBM_GBS, 4) if ml_traffic and t_ml > 0 else None}
-            # the whole bucketing stage against SURVEY 8(d)'s single-pass contract (read act, write perm:
-            # 12 B a message counting the 4-B bucket start the reference's per-activation FIFO implies)
-            stage = [k for k in ("k_radix_hist", "k_radix_rowscan", "k_radix_scatter", "k_msd_local",
-                                 "k_starts_rangescan", "k_bucket_starts", "k_scan_reduce", "k_scan_down") if k in kernels]
-            st_ms = sum(kernels[k]["ms_per_step"] for k in stage)
-            st_impl = sum(kernel_bytes(k, m_recv, n_act, passes, world, form) for k in stage)
-            roofline["bucketing_stage"] = {
-                "form": form, "kernels": stage, "ms_per_step": round(st_ms, 4),
-                "impl_bytes_per_message": round(st_impl / max(1, m_recv), 2), "contract_bytes_per_message": 12,
-                "frac_contract": round(12.0 * m_recv / (st_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4) if st_ms > 0 else None}
-        if dom == "k_route":
-            roofline["bytes_model"] = "SURVEY 8(d): key 24 + one 32-B directory slot + silo/act/status 9 B"
-            if os.environ.get("GD_CX", "1") != "0":
-                # the probe reads the compact index (gd_cx.h): 16-B slots, 4 to a 64-B read; the bytes it
-                # needs per message are key 24 + one 16-B slot + 9 (reported beside the SURVEY model)
-                impl = m_recv * (24 + 16 + 9) / launches
-                t_l = d["ms_per_step"] / launches * 1e-3
-                roofline["probe_index"] = {
-                    "slot_bytes": 16, "group_slots": 4, "impl_bytes_per_launch": impl,
-                    "frac_impl": round(impl / t_l / 1e9 / PEAK_HBM_GBS, 4) if t_l > 0 else None,
-                    "ubench": "profiles/r03_ubench_mirror.txt"}
-        if dom == "k_route" and args.workload == "cfg2" and os.environ.get("GD_CX", "1") == "0":
-            # k_route is one random 32-B slot read per message beside the 24-B key stream: its
-            # real ceiling is the random-probe rate, measured on MI355X by tools/ubench_random.hip
-            # for this shape (16M probes, 64-MiB table, key stream on): 0.3453 ms per launch
-            # (profiles/r01_ubench_random_ceiling.txt).
-            ceil_ms = 0.3453 * (m_recv / (1 << 24))
-            roofline["random_probe_ceiling"] = {
-                "ms_per_launch": round(ceil_ms, 4), "source": "profiles/r01_ubench_random_ceiling.txt",
-                "frac_of_ceiling": round(ceil_ms / (d["ms_per_step"] / launches), 3)}
+    acts_np = res.act.cpu().numpy().view(np.uint32)
+    kt = profile_kernels(e, router, keys, n_act, stream, args.profile_steps)
+    kernels, roofline = roofline_of(kt, max(1, args.profile_steps), m_recv, n_act, acts_np, args.workload, world)
+    if roofline and roofline["kernel"] == "k_route":
+        route_extras(roofline, e, m_recv, args.workload, world)
 
     # ---- BASELINE cfg 5: 4,096-message micro-batch latency on this directory ---------
     if world == 1 and args.workload == "cfg2" and args.latency_batches > 0:
@@ -482,7 +551,7 @@ def main():
             "unit": "messages/s",
             "n_gpus": world,
             "steps": args.steps,
-            "warmup": args.warmup, "settle_steps": SETTLE_STEPS,
+            "warmup": args.warmup, "settle_steps": settle_steps(args), "tune": args.tune,
             "ms_per_step": round(wall_max / args.steps * 1e3, 4),
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
             "higher_is_better": True,
@@ -511,6 +580,57 @@ def main():
         print(json.dumps(line), flush=True)
     e.close()
     dist.destroy_process_group()
+
+
+def secondary_roofline(w, res, args, tag: str, world: int):
+    """(kernels, roofline) of a secondary workload's steps (its own profiled steps)."""
+    m = int(res.status.shape[0])
+    acts = res.act.cpu().numpy().view(np.uint32)
+    kt = profile_kernels(w["e"], w["router"], w["keys"], w["n_act"], w["stream"], 3)
+    k, rf = roofline_of(kt, 3, m, w["n_act"], acts, tag, world)
+    if rf and rf["kernel"] == "k_route":
+        route_extras(rf, w["e"], m, tag, world)
+    return k, rf
+
+
+def profile_kernels(e, router, keys, n_act, stream, steps: int) -> dict:
+    """{kernel: (launches, total ms)} over `steps` extra steps with HIP events around every launch in
+    the library (gd_set_kernel_timing; events inside the timed region would perturb it)."""
+    if steps <= 0:
+        return {}
+    e.set_kernel_timing(True)
+    e.kernel_times_reset()
+    with torch.cuda.stream(stream):
+        for _ in range(steps):
+            router.route_bucket(keys, n_act)
+    torch.cuda.synchronize()
+    kt = e.kernel_times()
+    e.set_kernel_timing(False)
+    return kt
+
+
+def route_extras(roofline: dict, e, m_recv: int, tag: str, world: int):
+    """k_route's side fields: the probe variant the library runs (gd_tune_get), the compact index's
+    own bytes when it is the index, and (cfg2, N = 1) the measured random-probe ceiling."""
+    kind = "probe_keys" if world == 1 else "probe_n1"
+    v = e.tune_get(kind, m_recv)
+    roofline["probe_variant"] = {0: "compact index, 64-B group reads", 1: "directory table, 32-B slots",
+                                 2: "compact index, 16-B slot reads", -1: "still measuring"}.get(v, str(v))
+    t_l = roofline["avg_launch_ms"] * 1e-3
+    if v in (0, 2):
+        # the probe reads the compact index (gd_cx.h): 16-B slots; per message key 24 + one 16-B slot + 9
+        impl = m_recv * (24 + 16 + 9)
+        roofline["probe_index"] = {"slot_bytes": 16, "group_slots": 4 if v == 0 else 1, "impl_bytes_per_launch": impl,
+                                   "frac_impl": round(impl / t_l / 1e9 / PEAK_HBM_GBS, 4) if t_l > 0 else None,
+                                   "ubench": "profiles/r03_ubench_mirror.txt"}
+    if tag == "cfg2" and world == 1:
+        # one random slot read per message beside the 24-B key stream: its real ceiling is the
+        # random-probe rate, measured on MI355X by tools/ubench_random.hip for this shape (16M probes,
+        # 64-MiB table, key stream on): 0.3453 ms a launch (profiles/r01_ubench_random_ceiling.txt)
+        ceil_ms = 0.3453 * (m_recv / (1 << 24))
+        roofline["random_probe_ceiling"] = {"ms_per_launch": round(ceil_ms, 4),
+                                            "source": "profiles/r01_ubench_random_ceiling.txt",
+                                            "frac_of_ceiling": round(ceil_ms / (t_l * 1e3), 3) if t_l > 0 else None}
 
 
 def ping_shape(tcd: int, dev, mode: str, G: int = 10_000, N: int = 1 << 20, steps: int = 200) -> dict:
@@ -575,7 +695,7 @@ def micro_batch_latency(e, tcd: int, G: int, n_act: int, batches: int, B: int = 
         out["graph" if use_graph else "eager"] = {"p50": round(float(np.percentile(us, 50)), 1),
                                                   "p99": round(float(np.percentile(us, 99)), 1),
                                                   "max": round(float(us.max()), 1)}
-    out["zero_copy"] = os.environ.get("GD_MB_ZEROCOPY", "1") != "0"
+    out["zero_copy"] = bool(e.get_option("mb_zerocopy"))
     mb.close()
     return out
 
@@ -735,11 +855,9 @@ def cpu_baseline_cfg3(args, w3, tcd):
 
 # ---- BASELINE cfg 4: Chirper-style follower fan-out cascade -------------------------------------
 
-def fan_kernel_bytes(name, msgs, n_front, n_act, passes, keep_target, n_hops, hop_msgs=None):
-    """Algorithmic HBM bytes over all launches of a cfg 4 kernel in one cascade.
-    hop_msgs: the bucketing kernels per hop, by the main byte model (packed records where they fit)."""
-    if hop_msgs is not None and name in ("k_radix_scatter", "k_radix_hist"):
-        return float(sum(kernel_bytes(name, m, n_act, radix_layout(m, n_act)[0], 1) for m in hop_msgs if m))
+def fan_kernel_bytes(name, msgs, n_front, keep_target):
+    """Algorithmic HBM bytes over all launches of a cfg 4 expansion / route kernel in one cascade
+    (DESIGN.md 5.3); the bucketing kernels follow bucket_bytes per hop."""
     if name == "k_fan_route":
         # dst read 4 + one slot 32 + sender/silo/act 12 + status 1 (+ target 4); per publisher 16
         return msgs * (49 + (4 if keep_target else 0)) + n_front * 16
@@ -747,13 +865,21 @@ def fan_kernel_bytes(name, msgs, n_front, n_act, passes, keep_target, n_hops, ho
         return msgs * (4 + 32 + 9)
     if name == "k_fan_expand":
         return msgs * (4 + 8) + n_front * 16
-    if name == "k_radix_scatter":
-        return msgs * (12 + 16 * (passes - 1))
-    if name == "k_radix_hist":
-        return msgs * 4 * passes
-    if name == "k_bucket_starts":
-        return msgs * 4 + n_hops * (n_act + 2) * 4
     return 0.0
+
+
+def hop_form(e, m: int, n_act: int) -> str:
+    """The bucketing form the library keeps for m messages over n_act activations (gd_tune_get,
+    GD_TUNE_BUCKET; the two-level forms only from 2^20 messages)."""
+    if m < (1 << 20):
+        return "lsd"
+    q, sub = m // ((n_act >> 10) + 1), 0
+    while sub < 31 and (q >> sub) > 1:
+        sub += 1
+    v = e.tune_get("bucket", m, sub)
+    if v != 1:
+        return "lsd"
+    return "msd" if (n_act >> 10) + 1 <= 1056 else "msd3"
 
 
 def run_cfg4(args, world, rank, local, dev):
@@ -789,6 +915,7 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     keys = grain_keys(tcd, np.arange(n, dtype=np.int64))
     e = g.GrainDispatch(device=local, table_capacity=1 << int(np.ceil(np.log2(2 * n / world + 1))),
                         my_silo=rank % 8)
+    pin_choices(e, args, "cfg4")
     pts, own = e.ring_set_silos(args.mode, SILO_SETS[args.silos])
     owner = e.ring_owner(keys)
     mine = np.nonzero(owner % world == rank)[0]
@@ -832,7 +959,12 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     def step():
         return runner.run(t_seeds, args.hops)
 
-    for _ in range(SETTLE_STEPS // 2 + warmup):     # cascades: the probe choice per hop size (SETTLE_STEPS)
+    for _ in range(settle_steps(args) // 2):         # cascades: the measured choices per hop size
+        step()
+    if world > 1 and args.tune == "measured" and runner is not None and isinstance(runner, LibraryFanout):
+        torch.cuda.synchronize()
+        e.tune_agree()
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     dist.barrier()
@@ -856,6 +988,8 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
 
     kernels, roofline = {}, None
     if profile_steps > 0:
+        hop_acts = [h.act.cpu().numpy().view(np.uint32) if getattr(h, "act", None) is not None else None
+                    for h in hops]
         e.set_kernel_timing(True)
         e.kernel_times_reset()
         for _ in range(profile_steps):
@@ -863,23 +997,17 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
         torch.cuda.synchronize()
         kt = e.kernel_times()
         e.set_kernel_timing(False)
-        passes = (max(1, n.bit_length()) + 7) // 8
         msgs_step = sum(hop_msgs)
-        for name, (launches, ms) in kt.items():
-            if not launches:
-                continue
-            per = ms / profile_steps
-            b = fan_kernel_bytes(name, msgs_step, sum(hop_front), n, passes, not args.no_target, len(hops),
-                                 hop_msgs)
-            gbs = b / (per * 1e-3) / 1e9 if b and per > 0 else None
-            kernels[name] = {"launches_per_step": launches // profile_steps, "ms_per_step": round(per, 4),
-                             "alg_GBps": round(gbs, 1) if gbs else None,
-                             "frac_hbm": round(gbs / PEAK_HBM_GBS, 4) if gbs else None}
-        dom = max((k for k in kernels if not k.startswith("rccl_")), key=lambda k: kernels[k]["ms_per_step"])
-        d = kernels[dom]
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": d["alg_GBps"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": d["frac_hbm"], "traffic": None,
-                    "avg_launch_ms": round(d["ms_per_step"] / max(1, d["launches_per_step"]), 5)}
+
+        def cfg4_bytes(name, _form):
+            if name in ("k_fan_route", "k_route_nodes", "k_fan_expand"):
+                return fan_kernel_bytes(name, msgs_step, sum(hop_front), not args.no_target)
+            # the bucketing kernels: each hop's batch in the form the library keeps for its shape
+            return float(sum(bucket_bytes(hop_form(e, m, n), m, n, a).get(name, 0.0)
+                             for m, a in zip(hop_msgs, hop_acts) if m))
+        kernels, roofline = roofline_of(kt, profile_steps, msgs_step, n, None, "cfg4", world, bytes_fn=cfg4_bytes)
+        if roofline:
+            roofline["hop_bucket_forms"] = [hop_form(e, m, n) for m in hop_msgs]
 
     cpu = None
     if rank == 0 and world == 1 and with_cpu and getattr(hops[-1], "target", None) is not None:

@@ -897,6 +897,13 @@ int gd_tune_get(gd_handle* h, int kind, uint64_t n, uint32_t sub, int* variant);
  * rank.  Entries no rank finished keep measuring. */
 int gd_tune_agree(gd_handle* h);
 
+/* The handle's communicator: its rank count and this handle's rank as the transport reports them
+ * (RCCL: ncclCommCount / ncclCommUserRank), and the transport. */
+#define GD_COMM_NONE  0
+#define GD_COMM_RCCL  1   /* gd_comm_init */
+#define GD_COMM_LOCAL 2   /* gd_comm_init_local (in-process device copies) */
+int gd_comm_info(gd_handle* h, int* n_ranks, int* rank, int* transport);
+
 #ifdef __cplusplus
 }
 #endif

@@ -25,6 +25,8 @@ struct Rccl {
     decltype(&ncclRecv) Recv = nullptr;
     decltype(&ncclGetErrorString) GetErrorString = nullptr;
     decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+    decltype(&ncclCommCount) CommCount = nullptr;          // optional (gd_comm_info)
+    decltype(&ncclCommUserRank) CommUserRank = nullptr;    // optional (gd_comm_info)
 };
 
 inline const Rccl& rccl() {
@@ -60,6 +62,8 @@ inline const Rccl& rccl() {
         sym(r.GetErrorString, "ncclGetErrorString");
         sym(r.CommGetAsyncError, "ncclCommGetAsyncError");
         r.ok = all;
+        r.CommCount = reinterpret_cast<decltype(&ncclCommCount)>(dlsym(lib, "ncclCommCount"));
+        r.CommUserRank = reinterpret_cast<decltype(&ncclCommUserRank)>(dlsym(lib, "ncclCommUserRank"));
     });
     return r;
 }

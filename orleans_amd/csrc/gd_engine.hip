@@ -4156,6 +4156,28 @@ int gd_comm_destroy(gd_handle* h) {
     return GD_OK;
 }
 
+int gd_comm_info(gd_handle* h, int* n_ranks, int* rank, int* transport) {
+    if (!h || !n_ranks || !rank || !transport) return set_err(h, GD_EINVAL, "null argument");
+    *n_ranks = 0;
+    *rank = -1;
+    *transport = GD_COMM_NONE;
+    if (!h->comm) return GD_OK;
+    const Rccl& R = rccl();
+    if (h->net == &R) {
+        *transport = GD_COMM_RCCL;
+        int c = h->n_ranks, u = h->rank;
+        if (R.CommCount) NCCL_TRY(h, R.CommCount(h->comm, &c));       // the count RCCL itself reports
+        if (R.CommUserRank) NCCL_TRY(h, R.CommUserRank(h->comm, &u));
+        *n_ranks = c;
+        *rank = u;
+        return GD_OK;
+    }
+    *transport = GD_COMM_LOCAL;
+    *n_ranks = h->n_ranks;
+    *rank = h->rank;
+    return GD_OK;
+}
+
 // One all-gather of every rank's finished tune entries (key, best time a message per variant) in a
 // grouped send/recv round, then the same reduction on every rank: per key, the summed times of the
 // ranks that finished it (in rank order, so the floats agree bit for bit), argmin -> the pick.

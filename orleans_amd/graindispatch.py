@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = [
     "gd_ring_owner_device", "gd_pack_by_shard_device", "gd_pack_routes_by_rank_device", "gd_kernel_times",
     "gd_kernel_times_reset",
     "gd_option_set", "gd_option_get", "gd_tune_reset", "gd_tune_set", "gd_tune_get", "gd_tune_agree",
+    "gd_comm_info",
     "gd_set_kernel_timing", "gd_microbatch_create", "gd_microbatch_destroy", "gd_microbatch_keys",
     "gd_microbatch_outputs", "gd_microbatch_run", "gd_decode_frames_device", "gd_decode_frames",
     "gd_route_frames_device", "gd_route_frames", "gd_dir_split", "gd_dir_split_device",
@@ -320,6 +321,7 @@ def _load() -> C.CDLL:
         "gd_tune_set": (C.c_int, [P, C.c_int, C.c_int]),
         "gd_tune_get": (C.c_int, [P, C.c_int, U64, U32, C.POINTER(C.c_int)]),
         "gd_tune_agree": (C.c_int, [P]),
+        "gd_comm_info": (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -445,6 +447,13 @@ class GrainDispatch:
     def tune_agree(self):
         """Collective over the handle's communicator: every rank keeps the same measured choices."""
         self._c(lib.gd_tune_agree(self.h))
+
+    def comm_info(self) -> dict:
+        """{"n_ranks", "rank", "transport"} of the handle's communicator (RCCL's own count)."""
+        nr, rk, tr = C.c_int(0), C.c_int(0), C.c_int(0)
+        self._c(lib.gd_comm_info(self.h, C.byref(nr), C.byref(rk), C.byref(tr)))
+        return {"n_ranks": nr.value, "rank": rk.value,
+                "transport": {0: "none", 1: "rccl", 2: "in-process"}.get(tr.value, str(tr.value))}
 
     def close(self):
         if getattr(self, "h", None):

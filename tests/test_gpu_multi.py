@@ -20,7 +20,7 @@ TC = o.grain_type_code(o.PING_GRAIN_CLASS)
 
 
 @pytest.fixture(autouse=True)
-def _region_order(monkeypatch):
+def _region_order(monkeypatch, gd):
     """These tests expect the region-grouped arrival order (GD_OPT_REGION_PROBE = 1, the sender's option);
     test_route_multi_local_world_plain_order runs the other."""
     monkeypatch.setitem(gd.DEFAULT_OPTIONS, "region_probe", 1)
