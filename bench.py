@@ -121,9 +121,13 @@ def bucket_bytes(form: str, n: int, n_act: int, acts=None) -> dict:
     a = (kb + 1) // 2
     tiles = -(-n // 8192) + (n_act >> (10 + a)) + 1
     cnt = (1 << a) * tiles * 4.0
+    # pass A's records: 6 B (u16 + the index word's spare bits) when the index leaves room, else 8 B
+    hb, ib = max(0, a + 10 - 16), max(1, int(max(n, 1) - 1).bit_length())
+    rec = 6.0 if hb == 0 or ib + hb <= 32 else 8.0
     c = l2_classes(acts, n_act) if acts is not None else None
-    out = {"k_radix_hist": n * 4.0, "k_radix_scatter": n * 12.0, "k_seg_hist": n * 4.0 + cnt,
-           "k_scan_reduce": cnt, "k_scan_down": 2 * cnt, "k_seg_scatter": n * 14.0 + cnt,
+    out = {"k_radix_hist": n * 4.0, "k_radix_scatter": n * (4.0 + rec),
+           "k_seg_hist": n * (2.0 if rec == 6.0 else 4.0) + cnt,
+           "k_scan_reduce": cnt, "k_scan_down": 2 * cnt, "k_seg_scatter": n * (rec + 6.0) + cnt,
            "k_l2_classify": ((n_act >> 10) + 1) * 12.0}
     if c is None:
         out["k_l2_small"] = n * 10.0 + off      # unknown split: all charged to one kernel
@@ -899,10 +903,8 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     (all hops, all ranks) / max-over-ranks wall time of the cascade, graph and directory resident in
     HBM.  N = 1: fused expand+route kernel (k_fan_route) per hop.  N > 1: directory sharded by ring
     owner, (target, sender) pairs exchanged with one grouped RCCL send/recv round per hop inside the
-    library (gd_fanout_multi_device, LibraryFanout), checked on the first cascade against the
-    torch.distributed all-to-all-v path (ShardedFanout); the torch path is timed only if they differ."""
-    from orleans_amd.fanout import (CHIRPER_ACCOUNT_CLASS, DeviceFanoutEngine, FanoutCascade, LibraryFanout,
-                                    ShardedFanout, upload_graph)
+    library (gd_fanout_multi_device, LibraryFanout)."""
+    from orleans_amd.fanout import CHIRPER_ACCOUNT_CLASS, DeviceFanoutEngine, FanoutCascade, LibraryFanout, upload_graph
     from orleans_amd.workloads import power_law_graph
 
     t_setup = time.perf_counter()
@@ -927,34 +929,12 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     t_seeds = torch.from_numpy(seeds.view(np.int32)).to(dev)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
-    runner = (FanoutCascade(eng, graph, n) if world == 1 else
-              ShardedFanout(eng, graph, n, stage_via_cpu=args.rehearse_one_gpu))
-    exchange = "none" if world == 1 else "torch.distributed all_to_all_single (RCCL)"
-    if world > 1 and not args.rehearse_one_gpu and args.exchange != "torch":
-        ok, err = False, None
-        try:
-            lib_runner = LibraryFanout(eng, graph, n)
-            want = runner.run(t_seeds, args.hops)
-            got = lib_runner.fetch(lib_runner.run(t_seeds, args.hops))
-            u = lambda t: t.cpu().numpy().view(np.uint32)  # noqa: E731
-            ok = len(got) == len(want) and all(
-                np.array_equal(gh["frontier"], u(wh.frontier)) and np.array_equal(gh["act"], u(wh.act)) and
-                np.array_equal(gh["perm"], u(wh.perm)) and np.array_equal(gh["offsets"], u(wh.offsets)) and
-                np.array_equal(gh["sender"], u(wh.sender)) for gh, wh in zip(got, want))
-        except Exception as ex:   # noqa: BLE001 -- reported in the JSON line, torch exchange used instead
-            if args.exchange == "library":
-                raise
-            err = f"{ex!r}"[:200]
-        agree = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(agree, op=dist.ReduceOp.MIN)
-        if int(agree.item()) == 1:
-            runner = lib_runner
-            exchange = ("libgraindispatch gd_fanout_multi_device (grouped RCCL send/recv of (target, sender) "
-                        "per hop); first cascade bit-identical to the torch.distributed all-to-all-v path")
-        else:
-            assert args.exchange != "library", "library fan-out disagrees with the torch path"
-            exchange = ("torch.distributed all_to_all_single (RCCL); library fan-out " +
-                        (f"failed here: {err}" if err else "disagreed on the first cascade (some rank)"))
+    # N > 1: the sharded cascade inside the library (gd_fanout_multi_device), bit-exact against
+    # oracle/fanout.py in tests/test_gpu_fanout_multi.py (W = 8 and 3 in process)
+    assert not (world > 1 and args.rehearse_one_gpu), "cfg4 at N > 1 runs the library's RCCL cascade only"
+    runner = FanoutCascade(eng, graph, n) if world == 1 else LibraryFanout(eng, graph, n)
+    exchange = "none" if world == 1 else ("libgraindispatch gd_fanout_multi_device (grouped RCCL send/recv of "
+                                          "(target, sender) per hop)")
 
     def step():
         return runner.run(t_seeds, args.hops)

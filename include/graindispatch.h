@@ -870,6 +870,9 @@ int gd_set_kernel_timing(gd_handle* h, int enable);
                                    / 0 staged copies */
 #define GD_OPT_MB_SPLIT     10  /* micro-batches created after: redundant sorters splitting the host stores (8) */
 #define GD_OPT_MB_TRACE     11  /* micro-batches created after: per-phase timestamps printed at destroy (0) */
+#define GD_OPT_L2_STAGED    12  /* two-level three-pass form: ranges of at most this many messages (and more
+                                   than GD_OPT_L2_SMALL) sorted one workgroup a range, larger ones in 8K
+                                   chunks over several workgroups (default 24,576, the staging capacity) */
 int gd_option_set(gd_handle* h, int option, int64_t value);
 int gd_option_get(const gd_handle* h, int option, int64_t* value);
 

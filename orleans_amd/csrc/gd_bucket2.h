@@ -10,9 +10,9 @@
 // counters in one u32 (16-bit halves).
 //
 // Per item: the histogram reads the activation (4 B), the scatter reads it again and writes the
-// message index (u32) plus either the range-local key (key & 1023, u16: K16, the one-pass form for
-// n_act < 1,081,344) or the whole clamped key (u32: the first pass of the three-pass form for larger
-// n_act, gd_msd2.h).  Stability: a tile is ranked in index order (wave-striped rows, ds_add_rtn
+// message index (u32) plus a key (B2Out): the range-local key (key & 1023, u16: the one-pass form for
+// n_act < 1,081,344), or for the first pass of the three-pass form (larger n_act, gd_msd2.h) the key
+// bits the second pass needs packed into 6 B, or the whole clamped key (u32).  Stability: a tile is ranked in index order (wave-striped rows, ds_add_rtn
 // serves the lanes of one instruction in lane order -- checked on the device at handle creation,
 // DESIGN 5), tiles in order by the row-scanned counts.  HBM-bound, no MFMA.
 //
@@ -89,16 +89,26 @@ __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restrict__ key
     }
 }
 
-// The MSD pass's scatter: keys_in = the activations (clamped here), writes the message index to
-// vals_out and the key to keys_out in digit order of min(key, clamp) >> shift -- as u16 (key & 1023,
-// K16) or u32 (the whole clamped key).  gscan: the row-scanned counts (k_radix_rowscan), totals: the
-// digit totals.
-template <int NT, int IT, int RMAX, bool K16>
+// What the MSD scatter writes beside each message index.
+enum B2Out : int {
+    B2_KEY32 = 0,    // the whole clamped key, u32 (8-B records)
+    B2_KEY16 = 1,    // the range-local key key & 1023, u16 (the one-pass form: 6-B records)
+    B2_PACK = 2,     // the key's low pbits bits P: P >> hb as u16, P's low hb bits above the index's ib
+                     // bits in the u32 (the three-pass form's pass A: 6-B records)
+};
+struct B2Pack {
+    uint32_t pbits, hb, ib;
+};
+
+// The MSD pass's scatter: keys_in = the activations (clamped here), writes the message index and the
+// key (B2Out form) in digit order of min(key, clamp) >> shift.  gscan: the row-scanned counts
+// (k_radix_rowscan), totals: the digit totals.
+template <int NT, int IT, int RMAX, int KOUT>
 __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ keys_in, uint32_t n, uint32_t clamp,
                                                    uint32_t R, uint32_t tiles, const uint32_t* __restrict__ gscan,
                                                    const uint32_t* __restrict__ totals,
                                                    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                   uint32_t shift, uint32_t xcd) {
+                                                   uint32_t shift, uint32_t xcd, B2Pack pk) {
     constexpr int NW = NT / WAVE;
     constexpr uint32_t TILE = NT * IT;
     static_assert(TILE <= 65536 && NW % 2 == 0, "u16 tile positions, wave pairs");
@@ -227,9 +237,18 @@ __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ 
             const uint32_t k = s_key[p];
             const uint32_t g = s_gbase[k >> shift] + p;
             if (g < n) {                  // always true when the counts are right; never write out of bounds
-                if constexpr (K16) reinterpret_cast<uint16_t*>(keys_out)[g] = (uint16_t)(k & ((1u << B2_LOW_BITS) - 1));
-                else keys_out[g] = k;
-                vals_out[g] = base + (uint32_t)s_val[p];
+                const uint32_t idx = base + (uint32_t)s_val[p];
+                if constexpr (KOUT == B2_KEY16) {
+                    reinterpret_cast<uint16_t*>(keys_out)[g] = (uint16_t)(k & ((1u << B2_LOW_BITS) - 1));
+                    vals_out[g] = idx;
+                } else if constexpr (KOUT == B2_PACK) {
+                    const uint32_t P = k & ((1u << pk.pbits) - 1u);
+                    reinterpret_cast<uint16_t*>(keys_out)[g] = (uint16_t)(P >> pk.hb);
+                    vals_out[g] = pk.hb ? idx | ((P & ((1u << pk.hb) - 1u)) << pk.ib) : idx;
+                } else {
+                    keys_out[g] = k;
+                    vals_out[g] = idx;
+                }
             }
         }
     }

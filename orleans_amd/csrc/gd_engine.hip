@@ -179,7 +179,9 @@ struct gd_handle {
     int tune_pin[GD_TUNE_KINDS] = {-1, -1, -1, -1, -1};   // gd_tune_set: pinned variant per kind, -1 measured
     int msd_mode = 1;           // two-level bucketing (gd_msd.h, gd_msd2.h): 0 off, 1 measured (default), 2 always (GD_MSD)
     uint32_t l2_small = 1024;   // three-pass form: ranges of at most this many messages are sorted one wave a range
-    DevBuf m3[12];              // three-pass form's scratch (msd3_bucket)
+    uint32_t l2_staged = MSD_CAP;  // three-pass form: ranges up to this many messages one workgroup each, more: chunks
+    uint32_t n_cu = 256;        // compute units (hipDeviceProp_t::multiProcessorCount): persistent grids
+    DevBuf m3[14];              // three-pass form's scratch (msd3_bucket)
     DevBuf tune_buf;            // gd_tune_agree's send / receive records
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
     // per launch kind and size class: the probe variant, timed on live launches.  Variants: 0 the index
@@ -848,9 +850,9 @@ int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* 
 // index runs at R ~ 1,024; 65 against 76 us on 16K tiles at cfg 2), digit min(act, n_act) >> shift.
 // K16: the range-local keys as u16 (the one-pass form); else the whole clamped key as u32 (pass A of
 // the three-pass form).  Leaves the digit totals in last_totals.
-template <int RMAX, bool K16>
+template <int RMAX, int KOUT>
 int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t R, uint32_t shift, uint32_t* k1,
-             uint32_t* v1) {
+             uint32_t* v1, B2Pack pk = B2Pack{0, 0, 32}) {
     const uint32_t tiles = blocks_for(n, B2_TILE);
     const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
     GD_TRY(ensure(h, h->hist, ((size_t)R * tiles + R) * sizeof(uint32_t)));
@@ -865,8 +867,8 @@ int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uin
                       R, tiles, hist, shift, hxr));
     const uint32_t* tot = hist + (size_t)R * tiles;
     GD_TRY(launch(h, "k_radix_rowscan", dim3(R), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R * tiles));
-    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(B2_NT), 0, k_b2_scatter<B2_NT, B2_IT, RMAX, K16>, acts, n,
-                  n_act, R, tiles, (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles));
+    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(B2_NT), 0, k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT>, acts, n,
+                  n_act, R, tiles, (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk));
     h->last_totals = tot;
     h->last_digits = R;
     return GD_OK;
@@ -883,7 +885,7 @@ int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, u
     GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
     uint32_t* k1 = (uint32_t*)h->u32_a.p;
     uint32_t* v1 = (uint32_t*)h->u32_c.p;
-    GD_TRY((msd_pass<B2_RMAX2, true>(h, acts, n, n_act, R, MSD_SHIFT, k1, v1)));
+    GD_TRY((msd_pass<B2_RMAX2, B2_KEY16>(h, acts, n, n_act, R, MSD_SHIFT, k1, v1)));
     return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local, (const uint16_t*)k1, (const uint32_t*)v1,
                   h->last_totals, n, n_act, perm, offsets, rank_out);
 }
@@ -928,10 +930,14 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     GD_TRY(ensure(h, m[5], (size_t)L2_CTR_WORDS * 4));
     GD_TRY(ensure(h, m[6], (size_t)R * 4));                        // thin ranges
     GD_TRY(ensure(h, m[7], (size_t)R * 4));                        // staged ranges
-    GD_TRY(ensure(h, m[8], (size_t)cr_bound * 3 * 4));             // chunked ranges
+    GD_TRY(ensure(h, m[8], (size_t)cr_bound * 4 * 4));             // chunked ranges
+    // chunk-scan items: 1 a range of <= CS_DIRECT chunks, else CS_SLABS a piece of CS_ROWS chunks
+    const uint32_t it_bound = cr_bound + CS_SLABS * (ch_bound / CS_DIRECT + blocks_for(ch_bound, CS_ROWS));
+    GD_TRY(ensure(h, m[13], (size_t)it_bound * 4));
     GD_TRY(ensure(h, m[9], (size_t)ch_bound * 4));                 // chunk -> chunked range
     GD_TRY(ensure(h, m[10], (size_t)ch_bound * MSD_L * 4));        // per-chunk activation counts
     GD_TRY(ensure(h, m[11], (size_t)cr_bound * MSD_L * 4));        // per-range activation totals
+    GD_TRY(ensure(h, m[12], (size_t)cr_bound * blocks_for(ch_bound, CS_ROWS) * MSD_L * 4));   // per-piece sums
     uint32_t* kA = (uint32_t*)h->u32_a.p;
     uint32_t* vA = (uint32_t*)h->u32_c.p;
     uint16_t* kB = (uint16_t*)h->u32_b.p;
@@ -941,36 +947,64 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     uint32_t* tile_seg = (uint32_t*)m[2].p;
     uint32_t* hseg = (uint32_t*)m[3].p;
     (void)tilesA;
-    // pass A: d2 = k' >> a, whole keys out
-    GD_TRY((msd_pass<SEG_RMAX, false>(h, acts, n, n_act, RA, MSD_SHIFT + a, kA, vA)));
+    // pass A: d2 = k' >> a.  Pass B needs the key's low a + 10 bits P: as a u16 of P's high bits with
+    // the hb bits below them in the index word's spare top bits (6-B records) when the index leaves
+    // room (BASELINE cfg 3: P 19 bits, 26-bit indices), else the whole key (8-B records)
+    uint32_t ib = 1;
+    while (ib < 32 && ((n - 1) >> ib) != 0) ++ib;
+    const uint32_t pbits = a + MSD_SHIFT, hb = pbits > 16 ? pbits - 16 : 0;
+    const bool pk = hb == 0 || ib + hb <= 32;
+    const B2Pack bp{pbits, hb, hb ? ib : 32u};
+    if (pk) GD_TRY((msd_pass<SEG_RMAX, B2_PACK>(h, acts, n, n_act, RA, MSD_SHIFT + a, kA, vA, bp)));
+    else GD_TRY((msd_pass<SEG_RMAX, B2_KEY32>(h, acts, n, n_act, RA, MSD_SHIFT + a, kA, vA)));
+    const SegIn in{(const uint16_t*)kA, (const uint32_t*)kA, (const uint32_t*)vA, hb, bp.ib};
     GD_TRY(launch(h, "k_seg_table", dim3(1), dim3(1024), 0, k_seg_table, h->last_totals, RA, tbound, seg_start, seg_tb,
                   tile_seg, (uint32_t*)m[5].p));
     // pass B: d1 inside each d2 segment; one flat scan gives every (segment, digit, tile) its position
-    GD_TRY(launch(h, "k_seg_hist", dim3(tbound), dim3(SEG_NT), 0, k_seg_hist, (const uint32_t*)kA,
-                  (const uint32_t*)tile_seg, (const uint32_t*)seg_start, (const uint32_t*)seg_tb, RB, hseg));
+    if (pk)
+        GD_TRY(launch(h, "k_seg_hist", dim3(tbound), dim3(SEG_NT), 0, k_seg_hist<true>, in, (const uint32_t*)tile_seg,
+                      (const uint32_t*)seg_start, (const uint32_t*)seg_tb, RB, hseg));
+    else
+        GD_TRY(launch(h, "k_seg_hist", dim3(tbound), dim3(SEG_NT), 0, k_seg_hist<false>, in, (const uint32_t*)tile_seg,
+                      (const uint32_t*)seg_start, (const uint32_t*)seg_tb, RB, hseg));
     GD_TRY(scan_device<OpAdd>(h, hseg, RB * tbound, false, false, "seg"));
-    GD_TRY(launch(h, "k_seg_scatter", dim3(tbound), dim3(SEG_NT), 0, k_seg_scatter, (const uint32_t*)kA,
-                  (const uint32_t*)vA, (const uint32_t*)tile_seg, (const uint32_t*)seg_start, (const uint32_t*)seg_tb, RB,
-                  (const uint32_t*)hseg, kB, vB, h->xcd_tiles));
+    if (pk)
+        GD_TRY(launch(h, "k_seg_scatter", dim3(tbound), dim3(SEG_NT), 0, k_seg_scatter<true>, in,
+                      (const uint32_t*)tile_seg, (const uint32_t*)seg_start, (const uint32_t*)seg_tb, RB,
+                      (const uint32_t*)hseg, kB, vB, h->xcd_tiles));
+    else
+        GD_TRY(launch(h, "k_seg_scatter", dim3(tbound), dim3(SEG_NT), 0, k_seg_scatter<false>, in,
+                      (const uint32_t*)tile_seg, (const uint32_t*)seg_start, (const uint32_t*)seg_tb, RB,
+                      (const uint32_t*)hseg, kB, vB, h->xcd_tiles));
     // level 2
     uint32_t* cr = (uint32_t*)m[8].p;
     const L2Lists l{(uint32_t*)m[4].p, (uint32_t*)m[6].p, (uint32_t*)m[7].p, cr, cr + cr_bound, cr + 2 * cr_bound,
-                    (uint32_t*)m[9].p, (uint32_t*)m[5].p};
+                    (uint32_t*)m[9].p, cr + 3 * cr_bound, (uint32_t*)m[13].p, (uint32_t*)m[5].p};
     GD_TRY(launch(h, "k_l2_classify", dim3(blocks_for(R, BLOCK)), dim3(BLOCK), 0, k_l2_classify, (const uint32_t*)hseg,
-                  (const uint32_t*)seg_start, (const uint32_t*)seg_tb, a, R, n, h->l2_small, l));
-    GD_TRY(launch(h, "k_l2_small", dim3(std::min<uint32_t>(blocks_for(R, L2_SMALL_WAVES), 2048)),
+                  (const uint32_t*)seg_start, (const uint32_t*)seg_tb, a, R, n, h->l2_small,
+                  std::max(h->l2_small, h->l2_staged), l));
+    // persistent grids sized to what the chip holds at once (a second round of workgroups would wait for
+    // the first to finish its whole share): k_l2_small 4 a CU (32 KB of LDS, 8 waves each), the range
+    // sort 1 a CU (135 KB), the chunk scatter 2 (72 KB), the chunk histogram 4 and the scan 2 a CU
+    const uint32_t cu8 = (h->n_cu + 7) & ~7u;
+    GD_TRY(launch(h, "k_l2_small", dim3(std::min<uint32_t>(blocks_for(R, L2_SMALL_WAVES), 4 * cu8)),
                   dim3(L2_SMALL_WAVES * WAVE), 0, k_l2_small, (const uint16_t*)kB, (const uint32_t*)vB, l, n, n_act, perm,
                   offsets, rank_out));
-    GD_TRY(launch(h, "k_msd_local", dim3(std::min<uint32_t>(R, 512)), dim3(MSD_NT), 0, k_msd_local_list,
+    GD_TRY(launch(h, "k_msd_local", dim3(std::min<uint32_t>(R, cu8)), dim3(MSD_NT), 0, k_msd_local_list,
                   (const uint16_t*)kB, (const uint32_t*)vB, (const uint32_t*)l.rs, (const uint32_t*)l.staged,
                   (const uint32_t*)(l.ctr + 1), n, n_act, perm, offsets, rank_out));
     uint32_t* hh = (uint32_t*)m[10].p;
     uint32_t* tot = (uint32_t*)m[11].p;
-    GD_TRY(launch(h, "k_l2_chunk_hist", dim3(std::min<uint32_t>(ch_bound, 1024)), dim3(MSD_NT), 0, k_l2_chunk_hist,
+    // the chunk grids are multiples of 8 (chunk_walk: one contiguous chunk range an XCD)
+    GD_TRY(launch(h, "k_l2_chunk_hist", dim3(4 * cu8), dim3(CH_NT), 0, k_l2_chunk_hist,
                   (const uint16_t*)kB, l, hh));
-    GD_TRY(launch(h, "k_l2_chunk_scan", dim3(std::min<uint32_t>(cr_bound * (MSD_L / CS_COLS), 1024)), dim3(MSD_NT), 0,
-                  k_l2_chunk_scan, l, hh, tot));
-    return launch(h, "k_l2_chunk_scatter", dim3(std::min<uint32_t>(ch_bound, 512)), dim3(MSD_NT), 0, k_l2_chunk_scatter,
+    const uint32_t pmax = blocks_for(ch_bound, CS_ROWS);
+    uint32_t* ptot = (uint32_t*)m[12].p;
+    GD_TRY(launch(h, "k_l2_chunk_ptot", dim3(2 * cu8), dim3(MSD_NT), 0, k_l2_chunk_ptot, l, (const uint32_t*)hh, pmax,
+                  ptot));
+    GD_TRY(launch(h, "k_l2_chunk_scan", dim3(2 * cu8), dim3(MSD_NT), 0, k_l2_chunk_scan, l, hh, pmax,
+                  (const uint32_t*)ptot, tot));
+    return launch(h, "k_l2_chunk_scatter", dim3(2 * cu8), dim3(CH_NT), 0, k_l2_chunk_scatter,
                   (const uint16_t*)kB, (const uint32_t*)vB, l, (const uint32_t*)hh, (const uint32_t*)tot, n, n_act, perm,
                   offsets, rank_out);
 }
@@ -1348,6 +1382,11 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));
         delete h;
         return r;
+    }
+    {
+        int cu = 0;
+        if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, h->device) == hipSuccess && cu > 0)
+            h->n_cu = (uint32_t)cu;
     }
     e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -1932,6 +1971,10 @@ int gd_option_set(gd_handle* h, int option, int64_t v) {
             if (!in(0, 1)) break;
             h->mb_trace = v != 0;
             return GD_OK;
+        case GD_OPT_L2_STAGED:
+            if (!in(0, MSD_CAP)) break;
+            h->l2_staged = (uint32_t)v;
+            return GD_OK;
         default: return set_err(h, GD_EINVAL, "gd_option_set: unknown option %d", option);
     }
     return set_err(h, GD_EINVAL, "gd_option_set: option %d: value %lld out of range", option, (long long)v);
@@ -1952,6 +1995,7 @@ int gd_option_get(const gd_handle* hc, int option, int64_t* v) {
         case GD_OPT_MB_ZEROCOPY: *v = h->mb_zero_copy; return GD_OK;
         case GD_OPT_MB_SPLIT: *v = h->mb_split; return GD_OK;
         case GD_OPT_MB_TRACE: *v = h->mb_trace; return GD_OK;
+        case GD_OPT_L2_STAGED: *v = h->l2_staged; return GD_OK;
         default: return set_err(h, GD_EINVAL, "gd_option_get: unknown option %d", option);
     }
 }

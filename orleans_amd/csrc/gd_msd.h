@@ -81,10 +81,43 @@ __device__ __forceinline__ void msd_wave_prefix(uint32_t* wc, uint32_t tid, uint
     }
 }
 
+// Hot-key folding for the per-wave u16-pair counters (FOLD): the lanes of a row holding the first live
+// lane's key add to its counter with one LDS atomic by that lane, the others one each.  Under Zipf skew
+// many lanes of a row share a hot activation, and same-address LDS atomics serialise.  k = 0xFFFF: no
+// key.  msd_fold_count counts; msd_fold_rank returns this lane's place: its counter's value before the
+// add, plus its rank among the folded lanes (lane order: stable).
+__device__ __forceinline__ void msd_fold_count(uint32_t* wc, uint32_t k) {
+    const uint32_t lane = threadIdx.x & (WAVE - 1);
+    const bool valid = k != 0xFFFFu;
+    const unsigned long long live = __ballot(valid);
+    if (!live) return;
+    const uint32_t ld = (uint32_t)__ffsll((long long)live) - 1;
+    const uint32_t hk = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)ld);
+    const unsigned long long hot = __ballot(valid && k == hk);
+    if (valid && (k != hk || lane == ld))
+        atomicAdd(&wc[k >> 1], (lane == ld ? (uint32_t)__popcll(hot) : 1u) << (16 * (k & 1)));
+}
+__device__ __forceinline__ uint32_t msd_fold_rank(uint32_t* wc, uint32_t k) {
+    const uint32_t lane = threadIdx.x & (WAVE - 1);
+    const bool valid = k != 0xFFFFu;
+    const unsigned long long live = __ballot(valid);
+    const uint32_t ld = live ? (uint32_t)__ffsll((long long)live) - 1 : 0u;
+    const uint32_t hk = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)ld);
+    const unsigned long long hot = __ballot(valid && k == hk);
+    uint32_t r = 0;
+    if (valid && (k != hk || lane == ld)) {
+        const uint32_t old = atomicAdd(&wc[k >> 1], (lane == ld ? (uint32_t)__popcll(hot) : 1u) << (16 * (k & 1)));
+        r = (old >> (16 * (k & 1))) & 0xFFFFu;
+    }
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)ld);
+    return ((hot >> lane) & 1ull) ? b0 + (uint32_t)__popcll(hot & ((1ull << lane) - 1ull)) : r;
+}
+
 // Range b = activations [b << 10, (b << 10) + L) holding the S messages at [base, base + S) of the
 // MSD output (rk: range-local keys, u16; ri: message indices).  Writes perm[base, base + S), the
 // range's bucket starts offsets[b << 10, ... + L) and, for the range holding n_act, offsets[n_act + 1]
 // = n.  Called by all MSD_NT threads; LDS is free on entry and on return.
+template <bool FOLD>
 __device__ __forceinline__ void msd_range(MsdShared& sh, uint32_t b, uint32_t base, uint32_t S,
                                           const uint16_t* __restrict__ keys16, const uint32_t* __restrict__ idx,
                                           uint32_t n, uint32_t n_act, uint32_t* __restrict__ perm,
@@ -118,7 +151,8 @@ __device__ __forceinline__ void msd_range(MsdShared& sh, uint32_t b, uint32_t ba
 #pragma unroll
         for (int r = 0; r < MSD_RW; ++r) {
             const uint32_t k = (kp[r / 2] >> (16 * (r & 1))) & 0xFFFFu;
-            if (k != 0xFFFFu) atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
+            if constexpr (FOLD) msd_fold_count(sh.wc[w], k);
+            else if (k != 0xFFFFu) atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
         }
         // the rank sweep decodes the keys again rather than keeping the count sweep's addresses live
         // across the barriers (that spilled)
@@ -147,9 +181,14 @@ __device__ __forceinline__ void msd_range(MsdShared& sh, uint32_t b, uint32_t ba
 #pragma unroll
             for (int r = 0; r < MSD_G && g + r < MSD_RW; ++r) {
                 const uint32_t k = (kp[(g + r) / 2] >> (16 * ((g + r) & 1))) & 0xFFFFu;
-                if (k == 0xFFFFu) continue;
-                const uint32_t old = atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
-                sh.out[sh.run[k] + ((old >> (16 * (k & 1))) & 0xFFFFu)] = mm[r];
+                if constexpr (FOLD) {
+                    const uint32_t at = msd_fold_rank(sh.wc[w], k);
+                    if (k != 0xFFFFu) sh.out[sh.run[k] + at] = mm[r];
+                } else {
+                    if (k == 0xFFFFu) continue;
+                    const uint32_t old = atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
+                    sh.out[sh.run[k] + ((old >> (16 * (k & 1))) & 0xFFFFu)] = mm[r];
+                }
             }
         }
         __syncthreads();
@@ -240,7 +279,7 @@ __global__ void __launch_bounds__(MSD_NT, 4) k_msd_local(const uint16_t* __restr
         sh.base = t;
     }
     __syncthreads();
-    msd_range(sh, b, sh.base, totals[b], keys16, idx, n, n_act, perm, offsets, rank_out);
+    msd_range<false>(sh, b, sh.base, totals[b], keys16, idx, n, n_act, perm, offsets, rank_out);
 }
 
 // Three-pass form: the ranges of list[0, *count) (each <= MSD_CAP messages), range b at rs[b] .. rs[b + 1]
@@ -258,7 +297,7 @@ __global__ void __launch_bounds__(MSD_NT, 4) k_msd_local_list(const uint16_t* __
     for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
         const uint32_t b = list[i];
         const uint32_t base = rs[b];
-        msd_range(sh, b, base, rs[b + 1] - base, keys16, idx, n, n_act, perm, offsets, rank_out);
+        msd_range<true>(sh, b, base, rs[b + 1] - base, keys16, idx, n, n_act, perm, offsets, rank_out);
     }
 }
 

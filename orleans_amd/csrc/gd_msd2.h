@@ -14,8 +14,9 @@
 //           the activations.  Writes the range-local key (key & 1023, u16) and the index (u32), 6 B;
 //   level 2 k_l2_classify sorts the ranges into three work lists by their message count S:
 //             S <= t_small      k_l2_small, one wave a range (its 1,024 counters in 4 KB of LDS);
-//             S <= MSD_CAP      k_msd_local_list (gd_msd.h), one workgroup a range, staged in LDS;
-//             S >  MSD_CAP      chunks of CH_CAP messages, several workgroups a range: k_l2_chunk_hist
+//             S <= t_staged     k_msd_local_list (gd_msd.h), one workgroup a range, staged in LDS
+//                               (t_staged <= MSD_CAP);
+//             S >  t_staged     chunks of CH_CAP messages, several workgroups a range: k_l2_chunk_hist
 //                               (per-chunk activation counts) -> k_l2_chunk_scan (exclusive prefix of
 //                               each activation's counts over the range's chunks, 16-activation columns
 //                               scanned in LDS) -> k_l2_chunk_scatter (ranked and staged in LDS like a
@@ -45,9 +46,12 @@ constexpr int SEG_IT = 16;
 constexpr uint32_t SEG_TILE = SEG_NT * SEG_IT;
 constexpr uint32_t SEG_RMAX = 512;             // digits of either pass (a, kb - a <= 9 bits)
 constexpr uint32_t L2_SMALL_WAVES = 8;         // k_l2_small: waves a workgroup, one range each
-constexpr uint32_t CH_CAP = 16384;             // messages a chunk of a hot range (16 rows x 1,024 lanes)
-constexpr uint32_t CH_RW = CH_CAP / MSD_NT;
-constexpr uint32_t L2_CTR_WORDS = 8;           // [0] small ranges, [1] staged ranges, [2] chunks, [3] chunked ranges
+constexpr int CH_NT = 512;                     // chunk workgroups: 8 waves (two workgroups a CU, 72 KB of LDS each)
+constexpr int CH_NW = CH_NT / WAVE;
+constexpr uint32_t CH_CAP = 8192;              // messages a chunk of a hot range (16 rows x 512 lanes)
+constexpr uint32_t CH_RW = CH_CAP / CH_NT;
+constexpr uint32_t L2_CTR_WORDS = 8;           // [0] small ranges, [1] staged ranges, [2] chunks, [3] chunked ranges,
+                                               // [4] chunk-scan items
 
 // Wave-local LDS hand-off: the wave's earlier LDS writes are complete and visible to its other lanes.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -115,47 +119,78 @@ __device__ __forceinline__ bool seg_tile(uint32_t j, const uint32_t* tile_seg, c
     return true;
 }
 
+// Pass A's records as pass B reads them: PK (the default where the index leaves room): u16 keys16 =
+// P >> hb and the u32 index word idx | (P & (2^hb - 1)) << ib, P = key & (2^(a + 10) - 1) (6 B);
+// else the whole key (u32 keys32) and the index (8 B).
+struct SegIn {
+    const uint16_t* keys16;
+    const uint32_t* keys32;
+    const uint32_t* vals;
+    uint32_t hb, ib;
+};
+
 // Pass B histogram: tile j's counts of d1 = (key >> 10) & (rb - 1), written at
-// hseg[tb * rb + d * ts + tl] (segment-major, then digit-major, then tile).
-__global__ void __launch_bounds__(SEG_NT) k_seg_hist(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ tile_seg,
+// hseg[tb * rb + d * ts + tl] (segment-major, then digit-major, then tile).  PK reads the u16 keys
+// alone, 16 B a load from the 16-B boundary at or below the tile's first item (items outside the tile
+// masked): 2 B a message.
+template <bool PK>
+__global__ void __launch_bounds__(SEG_NT) k_seg_hist(SegIn in, const uint32_t* __restrict__ tile_seg,
                                                      const uint32_t* __restrict__ seg_start,
                                                      const uint32_t* __restrict__ seg_tb, uint32_t rb,
                                                      uint32_t* __restrict__ hseg) {
+    constexpr uint32_t PER = PK ? 8u : 4u;               // items a 16-B load
+    constexpr uint32_t NL = SEG_IT / PER;                // 16-B loads a thread covering the aligned tile
     __shared__ uint32_t s_cnt[SEG_RMAX];
     SegTile st;
-    if (!seg_tile(blockIdx.x, tile_seg, seg_start, seg_tb, st)) return;
+    // XCD-contiguous tiles (xcd_tile): the digit-major counts of neighbouring tiles share cache lines,
+    // which then fill in one L2 instead of going out as partial-line writes from eight
+    if (!seg_tile(xcd_tile(blockIdx.x, gridDim.x, 1u), tile_seg, seg_start, seg_tb, st)) return;
     for (uint32_t d = threadIdx.x; d < SEG_RMAX; d += SEG_NT) s_cnt[d] = 0;
     const uint32_t lane = lane_id();
-    uint32_t k[SEG_IT];
+    const uint32_t a0 = st.base & ~(PER - 1);            // aligned start: the loads cover [a0, a0 + TILE + PER)
+    const uint32_t dsh = PK ? B2_LOW_BITS - in.hb : B2_LOW_BITS;
+    uint4 v[NL + 1];
 #pragma unroll
-    for (int r = 0; r < SEG_IT; ++r) {
-        const uint32_t i = r * SEG_NT + threadIdx.x;
-        k[r] = keys[st.base + min(i, st.cnt - 1)];
+    for (uint32_t j = 0; j < NL; ++j) {                  // no load starts past the tile (the array may end there)
+        const uint32_t e = a0 + PER * (j * SEG_NT + threadIdx.x);
+        v[j] = make_uint4(0, 0, 0, 0);
+        if (e < st.base + st.cnt)
+            v[j] = PK ? *reinterpret_cast<const uint4*>(in.keys16 + e) : *reinterpret_cast<const uint4*>(in.keys32 + e);
     }
+    const uint32_t et = a0 + PER * (NL * SEG_NT + threadIdx.x);     // the tail past the aligned tile
+    v[NL] = make_uint4(0, 0, 0, 0);
+    if (threadIdx.x == 0 && et < st.base + st.cnt)
+        v[NL] = PK ? *reinterpret_cast<const uint4*>(in.keys16 + et) : *reinterpret_cast<const uint4*>(in.keys32 + et);
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < SEG_IT; ++r) {
-        const bool valid = r * SEG_NT + threadIdx.x < st.cnt;
-        const uint32_t d = (k[r] >> B2_LOW_BITS) & (rb - 1);
-        const unsigned long long act = __ballot(valid);
-        if (act == 0) continue;
-        const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
-        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
-        const unsigned long long hot = __ballot(valid && d == d0);
-        if (valid) {
-            if (d != d0) atomicAdd(&s_cnt[d], 1u);
-            else if (lane == lead) atomicAdd(&s_cnt[d], (uint32_t)__popcll(hot));
+    for (uint32_t j = 0; j <= NL; ++j) {
+        const uint32_t e0 = j < NL ? a0 + PER * (j * SEG_NT + threadIdx.x) : et;
+        const uint32_t w4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+        for (uint32_t q = 0; q < PER; ++q) {
+            const uint32_t e = e0 + q;
+            const bool valid = e >= st.base && e < st.base + st.cnt && (j < NL || threadIdx.x == 0);
+            const uint32_t k = PK ? (w4[q / 2] >> (16 * (q & 1))) & 0xFFFFu : w4[q];
+            const uint32_t d = (k >> dsh) & (rb - 1);
+            const unsigned long long act = __ballot(valid);
+            if (act == 0) continue;
+            const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
+            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
+            const unsigned long long hot = __ballot(valid && d == d0);
+            if (valid) {
+                if (d != d0) atomicAdd(&s_cnt[d], 1u);
+                else if (lane == lead) atomicAdd(&s_cnt[d], (uint32_t)__popcll(hot));
+            }
         }
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < rb; d += SEG_NT) hseg[(size_t)st.tb * rb + (size_t)d * st.ts + st.tl] = s_cnt[d];
 }
 
-// Pass B scatter: tile j's (key, index) records ranked stably by d1 and written at the flat-scanned
-// positions hseg[tb * rb + d * ts + tl] + rank: the range-local key (key & 1023) as u16 and the index.
-__global__ void __launch_bounds__(SEG_NT) k_seg_scatter(const uint32_t* __restrict__ keys_in,
-                                                        const uint32_t* __restrict__ vals_in,
-                                                        const uint32_t* __restrict__ tile_seg,
+// Pass B scatter: tile j's records ranked stably by d1 and written at the flat-scanned positions
+// hseg[tb * rb + d * ts + tl] + rank: the range-local key (key & 1023) as u16 and the index.
+template <bool PK>
+__global__ void __launch_bounds__(SEG_NT) k_seg_scatter(SegIn in, const uint32_t* __restrict__ tile_seg,
                                                         const uint32_t* __restrict__ seg_start,
                                                         const uint32_t* __restrict__ seg_tb, uint32_t rb,
                                                         const uint32_t* __restrict__ hseg,
@@ -165,7 +200,7 @@ __global__ void __launch_bounds__(SEG_NT) k_seg_scatter(const uint32_t* __restri
     constexpr int IT = SEG_IT;
     __shared__ uint32_t s_cnt[NW / 2][SEG_RMAX];         // wave pair (2p, 2p + 1): low / high 16 bits
     __shared__ uint32_t s_gbase[SEG_RMAX];
-    __shared__ uint32_t s_key[SEG_TILE];
+    __shared__ uint32_t s_key[SEG_TILE];                 // the key's low a + 10 bits
     __shared__ uint32_t s_val[SEG_TILE];
     __shared__ uint32_t s_wsum[NW];
     SegTile st;
@@ -181,12 +216,21 @@ __global__ void __launch_bounds__(SEG_NT) k_seg_scatter(const uint32_t* __restri
     const uint32_t half = (w & 1u) * 16u;
     const uint32_t one = 1u << half;
     const unsigned long long lt = (1ull << lane) - 1ull;
+    const uint32_t imask = PK ? (in.ib >= 32 ? 0xFFFFFFFFu : (1u << in.ib) - 1u) : 0xFFFFFFFFu;
     uint32_t kk[IT], vv[IT], rk[IT];
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
-        const uint32_t p = min((w * IT + r) * WAVE + lane, st.cnt - 1);
-        kk[r] = __builtin_nontemporal_load(keys_in + st.base + p);
-        vv[r] = __builtin_nontemporal_load(vals_in + st.base + p);
+        const uint32_t p = st.base + min((w * IT + r) * WAVE + lane, st.cnt - 1);
+        vv[r] = __builtin_nontemporal_load(in.vals + p);
+        if constexpr (PK) kk[r] = in.keys16[p];
+        else kk[r] = __builtin_nontemporal_load(in.keys32 + p);
+    }
+    if constexpr (PK) {
+#pragma unroll
+        for (int r = 0; r < IT; ++r) {                   // P = the u16 << hb | the index word's top hb bits
+            kk[r] = (kk[r] << in.hb) | (in.hb ? vv[r] >> in.ib : 0u);
+            vv[r] &= imask;
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -273,8 +317,18 @@ struct L2Lists {
     uint32_t* cr_cb;
     uint32_t* cr_n;
     uint32_t* chunk_r;     // chunk -> chunked range
+    uint32_t* cr_ib;       // chunked range -> its first chunk-scan item
+    uint32_t* item_r;      // chunk-scan item -> chunked range
     uint32_t* ctr;         // L2_CTR_WORDS
 };
+
+constexpr uint32_t CS_COLS = 16;               // k_l2_chunk_scan: activations a slab
+constexpr uint32_t CS_ROWS = 1024;             // chunks a piece
+constexpr uint32_t CS_DIRECT = 64;             // ranges of at most this many chunks: one item, no slabs
+constexpr uint32_t CS_SLABS = MSD_L / CS_COLS;
+__host__ __device__ __forceinline__ uint32_t cs_items(uint32_t C) {
+    return C <= CS_DIRECT ? 1u : CS_SLABS * ((C + CS_ROWS - 1) / CS_ROWS);
+}
 
 // Range b's start and size, and its work list (wave-aggregated appends: one atomic a wave and list).
 // A chunked range reserves its chunks and its entry with one 64-bit atomic (chunks in the low word,
@@ -282,7 +336,8 @@ struct L2Lists {
 __global__ void __launch_bounds__(BLOCK) k_l2_classify(const uint32_t* __restrict__ hseg,
                                                        const uint32_t* __restrict__ seg_start,
                                                        const uint32_t* __restrict__ seg_tb, uint32_t a, uint32_t R,
-                                                       uint32_t n, uint32_t t_small, L2Lists l) {
+                                                       uint32_t n, uint32_t t_small, uint32_t t_staged,
+                                                       L2Lists l) {
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t lane = lane_id();
     const unsigned long long lt = (1ull << lane) - 1ull;
@@ -294,7 +349,7 @@ __global__ void __launch_bounds__(BLOCK) k_l2_classify(const uint32_t* __restric
         l.rs[b] = r0;
         if (b + 1 == R) l.rs[R] = n;
         S = r1 - r0;
-        cls = S <= t_small ? 0u : (S <= MSD_CAP ? 1u : 2u);
+        cls = S <= t_small ? 0u : (S <= t_staged ? 1u : 2u);
     }
 #pragma unroll
     for (uint32_t c = 0; c < 2; ++c) {
@@ -318,10 +373,18 @@ __global__ void __launch_bounds__(BLOCK) k_l2_classify(const uint32_t* __restric
     const uint32_t olo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)old, 0);
     const uint32_t ohi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(old >> 32), 0);
     const uint32_t my_r = ohi + (uint32_t)__popcll(mc & lt), my_cb = olo + incl - C;
+    // chunk-scan work items (cs_items): one atomic a wave
+    const uint32_t ni = cls == 2 ? cs_items(C) : 0u;
+    const uint32_t iincl = wave_incl_sum_dpp(ni);
+    uint32_t ibase = 0;
+    if (lane == 0) ibase = atomicAdd(&l.ctr[4], (uint32_t)__builtin_amdgcn_readlane((int)iincl, WAVE - 1));
+    ibase = (uint32_t)__builtin_amdgcn_readlane((int)ibase, 0);
+    const uint32_t my_ib = ibase + iincl - ni;
     if (cls == 2) {
         l.cr_b[my_r] = b;
         l.cr_cb[my_r] = my_cb;
         l.cr_n[my_r] = C;
+        l.cr_ib[my_r] = my_ib;
     }
     // the chunk -> range map, written by the whole wave one chunked lane at a time
     unsigned long long rem = mc;
@@ -332,6 +395,9 @@ __global__ void __launch_bounds__(BLOCK) k_l2_classify(const uint32_t* __restric
         const uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)my_cb, (int)src);
         const uint32_t cn = (uint32_t)__builtin_amdgcn_readlane((int)C, (int)src);
         for (uint32_t c = lane; c < cn; c += WAVE) l.chunk_r[cb + c] = r;
+        const uint32_t ib = (uint32_t)__builtin_amdgcn_readlane((int)my_ib, (int)src);
+        const uint32_t in_ = (uint32_t)__builtin_amdgcn_readlane((int)ni, (int)src);
+        for (uint32_t i = lane; i < in_; i += WAVE) l.item_r[ib + i] = r;
     }
 }
 
@@ -358,8 +424,25 @@ __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16
         const uint32_t* ri = idx + base;
 #pragma unroll
         for (uint32_t q = 0; q < MSD_L / (4 * WAVE); ++q) reinterpret_cast<uint4*>(cnt)[q * WAVE + lane] = make_uint4(0, 0, 0, 0);
+        // a range of at most U rows (the thin ranges of a sparse batch) is loaded once, keys and indices
+        // together, and ranked from registers: one memory round trip instead of two
+        const bool reg = S <= U * WAVE;
+        uint32_t rk0[U], rv0[U];
+        if (reg) {
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                const uint32_t j = u * WAVE + lane;
+                rk0[u] = j < S ? (uint32_t)rk[j] : NONE32;
+                rv0[u] = j < S ? ri[j] : 0u;
+            }
+        }
         wave_lds_sync();
-        for (uint32_t i0 = 0; i0 < S; i0 += U * WAVE) {
+        if (reg) {
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u)
+                if (rk0[u] != NONE32) atomicAdd(&cnt[rk0[u]], 1u);
+        }
+        for (uint32_t i0 = 0; !reg && i0 < S; i0 += U * WAVE) {
             uint32_t k[U];
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
@@ -383,7 +466,16 @@ __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16
         }
         if (lane == 0 && b == (n_act >> MSD_SHIFT)) offsets[n_act + 1] = n;
         wave_lds_sync();
-        for (uint32_t i0 = 0; i0 < S; i0 += U * WAVE) {
+        if (reg) {
+#pragma unroll
+            for (uint32_t u = 0; u < U; ++u) {
+                if (rk0[u] == NONE32) continue;
+                const uint32_t p = base + atomicAdd(&cnt[rk0[u]], 1u);
+                perm[p] = rv0[u];
+                if (rank_out) rank_out[rv0[u]] = p;
+            }
+        }
+        for (uint32_t i0 = 0; !reg && i0 < S; i0 += U * WAVE) {
             uint32_t k[U], v[U];
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
@@ -403,128 +495,224 @@ __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16
     }
 }
 
+// Chunk order of the persistent level-2 grids: workgroup b runs on XCD b % 8 (round-robin dispatch),
+// and the workgroups of one XCD walk one contiguous eighth of the chunks together, so the neighbouring
+// chunks of a hot range -- whose runs of one activation lie side by side in perm -- meet in one L2.
+struct ChunkWalk {
+    uint32_t j, end, step;
+};
+__device__ __forceinline__ ChunkWalk chunk_walk(uint32_t m) {
+    const uint32_t g = gridDim.x;
+    if (g % 8u) return ChunkWalk{blockIdx.x, m, g};
+    const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3, per = g >> 3;
+    const uint32_t q = m >> 3, rem = m & 7u;
+    const uint32_t lo = x * q + min(x, rem), hi = lo + q + (x < rem ? 1u : 0u);
+    return ChunkWalk{lo + k, hi, per};
+}
+
 // Level 2, hot ranges: chunk j's activation counts, hh[j * 1,024 + a].
-__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_hist(const uint16_t* __restrict__ keys16, L2Lists l,
-                                                          uint32_t* __restrict__ hh) {
+__global__ void __launch_bounds__(CH_NT) k_l2_chunk_hist(const uint16_t* __restrict__ keys16, L2Lists l,
+                                                         uint32_t* __restrict__ hh) {
     __shared__ uint32_t s_cnt[MSD_L];
     const uint32_t tid = threadIdx.x, lane = lane_id();
-    const uint32_t m = l.ctr[2];
-    for (uint32_t j = blockIdx.x; j < m; j += gridDim.x) {
+    const ChunkWalk cw = chunk_walk(l.ctr[2]);
+    for (uint32_t j = cw.j; j < cw.end; j += cw.step) {
         const uint32_t r = l.chunk_r[j], b = l.cr_b[r];
         const uint32_t rsb = l.rs[b], c = j - l.cr_cb[r];
         const uint32_t start = rsb + c * CH_CAP, cs = min(CH_CAP, l.rs[b + 1] - start);
-        s_cnt[tid] = 0;
-        uint32_t k[CH_RW];
+        for (uint32_t x = tid; x < MSD_L; x += CH_NT) s_cnt[x] = 0;
+        // 16-B loads of 8 keys from the 16-B boundary at or below the chunk's first key (keys outside the
+        // chunk masked), 2 a thread, and one more for the tail past the aligned span
+        const uint32_t a0 = start & ~7u;
+        uint4 v[CH_RW / 8 + 1];
 #pragma unroll
-        for (uint32_t q = 0; q < CH_RW; ++q) k[q] = keys16[start + min(q * MSD_NT + tid, cs - 1)];
+        for (uint32_t q = 0; q < CH_RW / 8; ++q) {
+            const uint32_t e = a0 + 8 * (q * CH_NT + tid);
+            v[q] = e < start + cs ? *reinterpret_cast<const uint4*>(keys16 + e) : make_uint4(0, 0, 0, 0);
+        }
+        const uint32_t et = a0 + CH_CAP;
+        v[CH_RW / 8] = tid == 0 && et < start + cs ? *reinterpret_cast<const uint4*>(keys16 + et) : make_uint4(0, 0, 0, 0);
         __syncthreads();
 #pragma unroll
-        for (uint32_t q = 0; q < CH_RW; ++q) {
-            const bool valid = q * MSD_NT + tid < cs;
-            const unsigned long long act = __ballot(valid);
-            if (act == 0) continue;
-            const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
-            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)k[q], (int)lead);
-            const unsigned long long hot = __ballot(valid && k[q] == d0);
-            if (valid) {
-                if (k[q] != d0) atomicAdd(&s_cnt[k[q]], 1u);
-                else if (lane == lead) atomicAdd(&s_cnt[k[q]], (uint32_t)__popcll(hot));
+        for (uint32_t q = 0; q <= CH_RW / 8; ++q) {
+            const uint32_t e0 = q < CH_RW / 8 ? a0 + 8 * (q * CH_NT + tid) : et;
+            const uint32_t w4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+            for (uint32_t x = 0; x < 8; ++x) {
+                const uint32_t e = e0 + x;
+                const bool valid = e >= start && e < start + cs && (q < CH_RW / 8 || tid == 0);
+                const uint32_t k = (w4[x / 2] >> (16 * (x & 1))) & 0xFFFFu;
+                const unsigned long long act = __ballot(valid);
+                if (act == 0) continue;
+                const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
+                const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)lead);
+                const unsigned long long hot = __ballot(valid && k == d0);
+                if (valid) {
+                    if (k != d0) atomicAdd(&s_cnt[k], 1u);
+                    else if (lane == lead) atomicAdd(&s_cnt[k], (uint32_t)__popcll(hot));
+                }
             }
         }
         __syncthreads();
-        hh[(size_t)j * MSD_L + tid] = s_cnt[tid];
+        for (uint32_t x = tid; x < MSD_L; x += CH_NT) hh[(size_t)j * MSD_L + x] = s_cnt[x];
         __syncthreads();
     }
 }
 
-// Level 2, hot ranges: for chunked range r and activations [16 g, 16 g + 16), the exclusive prefix of
-// each activation's chunk counts over the range's chunks, in place (hh), and its total (tot).  The
-// 16-column slab of up to 1,024 chunks goes through LDS (rows padded to 17 words: the column scans
-// are conflict-free), one wave a column, 16 DPP scans of 64 rows each.
-constexpr uint32_t CS_COLS = 16;
-constexpr uint32_t CS_ROWS = 1024;
-__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_scan(L2Lists l, uint32_t* __restrict__ hh,
+// Level 2, hot ranges: the exclusive prefix of each activation's chunk counts over its range's chunks,
+// in place (hh), and each activation's total (tot).  A range of at most CS_DIRECT chunks is one work
+// item: thread a walks column a down the range's chunks (coalesced 4-KB rows, 8 loads in flight).  A
+// longer one (BASELINE cfg 3's hottest range: ~4,900 chunks) is cut into 64 slabs of 16 activations
+// (one 64-B line a chunk) x pieces of CS_ROWS chunks, every (slab, piece) an item of its own, in two
+// launches: k_l2_chunk_ptot sums each piece's columns, k_l2_chunk_scan scans each piece in LDS (rows
+// padded to 17 words: conflict-free column scans; one wave a column, DPP scans of 64 rows) starting
+// from the sum of the pieces before it.  (One item walking all of a slab's pieces left the hottest
+// range's ~5 pieces in series: 0.064 ms at cfg 3.)
+struct CsItem {
+    uint32_t r, g, p, cb, C, pieces;
+};
+// Item it (k_l2_classify laid the items out: cs_items a chunked range): its range, slab and piece.
+__device__ __forceinline__ void cs_item(const L2Lists& l, uint32_t it, CsItem& x) {
+    x.r = l.item_r[it];
+    x.cb = l.cr_cb[x.r];
+    x.C = l.cr_n[x.r];
+    x.pieces = x.C <= CS_DIRECT ? 1u : (x.C + CS_ROWS - 1) / CS_ROWS;
+    const uint32_t li = it - l.cr_ib[x.r];
+    x.g = li / x.pieces;
+    x.p = li % x.pieces;
+}
+
+// One piece of one slab into LDS (rows past the piece zero up to the next 64).  Returns the rows.
+__device__ __forceinline__ uint32_t cs_load(const uint32_t* hh, const CsItem& x, uint32_t* s_m) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t c0 = x.p * CS_ROWS, rows = min(CS_ROWS, x.C - c0);
+    const uint32_t rows64 = (rows + WAVE - 1) & ~(WAVE - 1);
+    uint32_t* d = s_m + tid * (CS_COLS + 1);             // CS_ROWS == MSD_NT: one row a thread
+    if (tid < rows) {
+        const uint4* src = reinterpret_cast<const uint4*>(hh + (size_t)(x.cb + c0 + tid) * MSD_L + x.g * CS_COLS);
+#pragma unroll
+        for (uint32_t q = 0; q < CS_COLS / 4; ++q) {
+            const uint4 v = src[q];
+            d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+        }
+    } else if (tid < rows64) {
+#pragma unroll
+        for (uint32_t q = 0; q < CS_COLS; ++q) d[q] = 0;
+    }
+    return rows;
+}
+
+__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_ptot(L2Lists l, const uint32_t* __restrict__ hh, uint32_t pmax,
+                                                          uint32_t* __restrict__ ptot) {
+    __shared__ uint32_t s_m[CS_ROWS * (CS_COLS + 1)];
+    const uint32_t lane = lane_id(), w = threadIdx.x / WAVE;
+    const uint32_t items = l.ctr[4];
+    for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+        CsItem x;
+        cs_item(l, it, x);
+        if (x.C <= CS_DIRECT) continue;                  // uniform over the workgroup
+        const uint32_t rows = cs_load(hh, x, s_m);
+        __syncthreads();
+        uint32_t sum = 0;                                // wave w: column w
+        for (uint32_t q = 0; q < (rows + WAVE - 1) / WAVE; ++q) sum += s_m[(q * WAVE + lane) * (CS_COLS + 1) + w];
+        sum = wave_incl_sum_dpp(sum);
+        if (lane == WAVE - 1) ptot[((size_t)x.r * pmax + x.p) * MSD_L + x.g * CS_COLS + w] = sum;
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_scan(L2Lists l, uint32_t* __restrict__ hh, uint32_t pmax,
+                                                          const uint32_t* __restrict__ ptot,
                                                           uint32_t* __restrict__ tot) {
     __shared__ uint32_t s_m[CS_ROWS * (CS_COLS + 1)];
     const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / WAVE;
-    const uint32_t items = l.ctr[3] * (MSD_L / CS_COLS);
+    const uint32_t items = l.ctr[4];
     for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
-        const uint32_t r = it / (MSD_L / CS_COLS), g = it % (MSD_L / CS_COLS);
-        const uint32_t cb = l.cr_cb[r], C = l.cr_n[r];
-        uint32_t carry = 0;                              // wave w: column w
-        for (uint32_t c0 = 0; c0 < C; c0 += CS_ROWS) {
-            const uint32_t rows = min(CS_ROWS, C - c0);
-            uint32_t* src = hh + (size_t)(cb + c0 + tid) * MSD_L + g * CS_COLS;
-            if (tid < rows) {
+        CsItem x;
+        cs_item(l, it, x);
+        if (x.C <= CS_DIRECT) {
+            uint32_t* col = hh + (size_t)x.cb * MSD_L + tid;
+            uint32_t run = 0;
+            for (uint32_t c0 = 0; c0 < x.C; c0 += 8) {
+                uint32_t v[8];
 #pragma unroll
-                for (uint32_t q = 0; q < CS_COLS / 4; ++q) {
-                    const uint4 v = reinterpret_cast<const uint4*>(src)[q];
-                    uint32_t* d = s_m + tid * (CS_COLS + 1) + 4 * q;
-                    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-                }
-            } else {
+                for (uint32_t q = 0; q < 8; ++q) v[q] = c0 + q < x.C ? col[(size_t)(c0 + q) * MSD_L] : 0u;
 #pragma unroll
-                for (uint32_t q = 0; q < CS_COLS; ++q) s_m[tid * (CS_COLS + 1) + q] = 0;
-            }
-            __syncthreads();
-#pragma unroll 4
-            for (uint32_t q = 0; q < CS_ROWS / WAVE; ++q) {
-                uint32_t* p = s_m + (q * WAVE + lane) * (CS_COLS + 1) + w;
-                const uint32_t x = *p;
-                const uint32_t inc = wave_incl_sum_dpp(x);
-                *p = carry + inc - x;
-                carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, WAVE - 1);
-            }
-            __syncthreads();
-            if (tid < rows) {
-#pragma unroll
-                for (uint32_t q = 0; q < CS_COLS / 4; ++q) {
-                    const uint32_t* d = s_m + tid * (CS_COLS + 1) + 4 * q;
-                    reinterpret_cast<uint4*>(src)[q] = make_uint4(d[0], d[1], d[2], d[3]);
+                for (uint32_t q = 0; q < 8; ++q) {
+                    if (c0 + q < x.C) col[(size_t)(c0 + q) * MSD_L] = run;
+                    run += v[q];
                 }
             }
-            __syncthreads();
+            tot[(size_t)x.r * MSD_L + tid] = run;
+            continue;
         }
-        if (lane == 0) tot[(size_t)r * MSD_L + g * CS_COLS + w] = carry;
+        // wave w: column w, carried in from the pieces before this one
+        uint32_t carry = 0;
+        for (uint32_t p = 0; p < x.p; ++p) carry += ptot[((size_t)x.r * pmax + p) * MSD_L + x.g * CS_COLS + w];
+        const uint32_t rows = cs_load(hh, x, s_m);
+        __syncthreads();
+        for (uint32_t q = 0; q < (rows + WAVE - 1) / WAVE; ++q) {
+            uint32_t* pp = s_m + (q * WAVE + lane) * (CS_COLS + 1) + w;
+            const uint32_t v = *pp;
+            const uint32_t inc = wave_incl_sum_dpp(v);
+            *pp = carry + inc - v;
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, WAVE - 1);
+        }
+        __syncthreads();
+        if (tid < rows) {
+            const uint32_t* d = s_m + tid * (CS_COLS + 1);
+            uint4* dst = reinterpret_cast<uint4*>(hh + (size_t)(x.cb + x.p * CS_ROWS + tid) * MSD_L + x.g * CS_COLS);
+#pragma unroll
+            for (uint32_t q = 0; q < CS_COLS / 4; ++q) dst[q] = make_uint4(d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]);
+        }
+        if (lane == 0 && x.p + 1 == x.pieces) tot[(size_t)x.r * MSD_L + x.g * CS_COLS + w] = carry;
+        __syncthreads();
     }
 }
 
 // Level 2, hot ranges: chunk j = chunk c of range b, ranked and staged in LDS like a range
 // (msd_range), each activation's items written at its start in the range + its count in the earlier
-// chunks.  Chunk 0 writes the range's bucket starts.
+// chunks.  Chunk 0 writes the range's bucket starts.  512 threads, 8K messages: 72 KB of LDS, so two
+// workgroups share a CU and one's memory phases run under the other's LDS phases (16K chunks on
+// 1,024 threads took 136 KB: one a CU, 0.24 ms at cfg 3).  Thread t owns activations 2t, 2t + 1.
 struct ChunkShared {
     uint32_t out[CH_CAP];
     uint16_t key[CH_CAP];
-    uint32_t wc[MSD_NW][MSD_LW];
+    uint32_t wc[CH_NW][MSD_LW];
     uint32_t run[MSD_L];
     uint32_t delta[MSD_L];
-    uint32_t red[MSD_NW];
+    uint32_t red[CH_NW];
 };
-__global__ void __launch_bounds__(MSD_NT, 4) k_l2_chunk_scatter(const uint16_t* __restrict__ keys16,
-                                                                const uint32_t* __restrict__ idx, L2Lists l,
-                                                                const uint32_t* __restrict__ hh,
-                                                                const uint32_t* __restrict__ tot, uint32_t n,
-                                                                uint32_t n_act, uint32_t* __restrict__ perm,
-                                                                uint32_t* __restrict__ offsets,
-                                                                uint32_t* __restrict__ rank_out) {
+__global__ void __launch_bounds__(CH_NT, 2) k_l2_chunk_scatter(const uint16_t* __restrict__ keys16,
+                                                               const uint32_t* __restrict__ idx, L2Lists l,
+                                                               const uint32_t* __restrict__ hh,
+                                                               const uint32_t* __restrict__ tot, uint32_t n,
+                                                               uint32_t n_act, uint32_t* __restrict__ perm,
+                                                               uint32_t* __restrict__ offsets,
+                                                               uint32_t* __restrict__ rank_out) {
+    static_assert(CH_NT == (int)MSD_LW, "one thread per u16-pair counter word");
     __shared__ ChunkShared sh;
     const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
-    const uint32_t m = l.ctr[2];
-    for (uint32_t j = blockIdx.x; j < m; j += gridDim.x) {
+    const ChunkWalk cw = chunk_walk(l.ctr[2]);
+    for (uint32_t j = cw.j; j < cw.end; j += cw.step) {
         const uint32_t r = l.chunk_r[j], b = l.cr_b[r];
         const uint32_t rsb = l.rs[b], c = j - l.cr_cb[r];
         const uint32_t start = rsb + c * CH_CAP, cs = min(CH_CAP, l.rs[b + 1] - start);
         const uint32_t k0 = b << MSD_SHIFT;
         const uint32_t L = min(MSD_L, n_act + 1 - k0);
-        // activation tid: its start in the range (scan of the totals) and its base for this chunk
-        const uint32_t as = block_excl_scan_add_n<MSD_NT>(tot[(size_t)r * MSD_L + tid], sh.red);
-        const uint32_t gb = rsb + as + hh[(size_t)j * MSD_L + tid];
+        // activations 2t, 2t + 1: their starts in the range (scan of the totals), their bases for this chunk
+        const uint2 t2 = reinterpret_cast<const uint2*>(tot + (size_t)r * MSD_L)[tid];
+        const uint2 h2 = reinterpret_cast<const uint2*>(hh + (size_t)j * MSD_L)[tid];
+        const uint32_t as0 = block_excl_scan_add_n<CH_NT>(t2.x + t2.y, sh.red), as1 = as0 + t2.x;
+        const uint32_t gb0 = rsb + as0 + h2.x, gb1 = rsb + as1 + h2.y;
         if (c == 0) {
-            if (tid < L) offsets[k0 + tid] = rsb + as;
+            if (2 * tid < L) offsets[k0 + 2 * tid] = rsb + as0;
+            if (2 * tid + 1 < L) offsets[k0 + 2 * tid + 1] = rsb + as1;
             if (tid == 0 && b == (n_act >> MSD_SHIFT)) offsets[n_act + 1] = n;
         }
-        for (uint32_t x = tid; x < MSD_NW * MSD_LW; x += MSD_NT) (&sh.wc[0][0])[x] = 0;
-        const uint32_t seg = (cs + MSD_NW - 1) / MSD_NW;
+#pragma unroll
+        for (int ww = 0; ww < CH_NW; ++ww) sh.wc[ww][tid] = 0;
+        const uint32_t seg = (cs + CH_NW - 1) / CH_NW;
         const uint32_t s0 = min(w * seg, cs), s1 = min((w + 1) * seg, cs);
         const uint16_t* rk = keys16 + start;
         const uint32_t* ri = idx + start;
@@ -540,22 +728,25 @@ __global__ void __launch_bounds__(MSD_NT, 4) k_l2_chunk_scatter(const uint16_t* 
         }
         __syncthreads();
 #pragma unroll
-        for (uint32_t q = 0; q < CH_RW; ++q) {
-            const uint32_t k = (kp[q / 2] >> (16 * (q & 1))) & 0xFFFFu;
-            if (k != 0xFFFFu) atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
-        }
+        for (uint32_t q = 0; q < CH_RW; ++q) msd_fold_count(sh.wc[w], (kp[q / 2] >> (16 * (q & 1))) & 0xFFFFu);
 #pragma unroll
         for (uint32_t q = 0; q < CH_RW / 2; ++q) asm volatile("" : "+v"(kp[q]));
         __syncthreads();
-        uint32_t tlo, thi;
-        msd_wave_prefix(&sh.wc[0][0], tid, tlo, thi);
-        const uint32_t ex = block_excl_scan_add_n<MSD_NT>(tlo + thi, sh.red);
-        if (tid < MSD_LW) {
-            sh.run[2 * tid] = ex;
-            sh.run[2 * tid + 1] = ex + tlo;
+        // each wave's first position per activation (exclusive prefix over the waves), the totals
+        uint32_t tlo = 0, thi = 0;
+#pragma unroll
+        for (int ww = 0; ww < CH_NW; ++ww) {
+            const uint32_t v = sh.wc[ww][tid];
+            sh.wc[ww][tid] = tlo | (thi << 16);
+            tlo += v & 0xFFFFu;
+            thi += v >> 16;
         }
+        const uint32_t ex = block_excl_scan_add_n<CH_NT>(tlo + thi, sh.red);
+        sh.run[2 * tid] = ex;
+        sh.run[2 * tid + 1] = ex + tlo;
+        sh.delta[2 * tid] = gb0 - ex;                    // chunk-local position -> global position
+        sh.delta[2 * tid + 1] = gb1 - ex - tlo;
         __syncthreads();
-        sh.delta[tid] = gb - sh.run[tid];                // chunk-local position -> global position
 #pragma unroll
         for (uint32_t g = 0; g < CH_RW; g += MSD_G) {
             uint32_t mm[MSD_G];
@@ -567,9 +758,9 @@ __global__ void __launch_bounds__(MSD_NT, 4) k_l2_chunk_scatter(const uint16_t* 
 #pragma unroll
             for (uint32_t q = 0; q < (uint32_t)MSD_G; ++q) {
                 const uint32_t k = (kp[(g + q) / 2] >> (16 * ((g + q) & 1))) & 0xFFFFu;
+                const uint32_t rr = msd_fold_rank(sh.wc[w], k);    // Zipf-hot ranges: fold the hot key
                 if (k == 0xFFFFu) continue;
-                const uint32_t old = atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
-                const uint32_t at = sh.run[k] + ((old >> (16 * (k & 1))) & 0xFFFFu);
+                const uint32_t at = sh.run[k] + rr;
                 sh.out[at] = mm[q];
                 sh.key[at] = (uint16_t)k;
             }
@@ -577,7 +768,7 @@ __global__ void __launch_bounds__(MSD_NT, 4) k_l2_chunk_scatter(const uint16_t* 
         __syncthreads();
 #pragma unroll
         for (uint32_t q = 0; q < CH_RW; ++q) {
-            const uint32_t i = q * MSD_NT + tid;
+            const uint32_t i = q * CH_NT + tid;
             if (i < cs) {
                 const uint32_t v = sh.out[i];
                 const uint32_t p = sh.delta[sh.key[i]] + i;

@@ -14,12 +14,7 @@ activation index in the directory is u (the bench registers it so).
   (gd_fanout_route_bucket_device), the activation bucketing, and gd_frontier_next_device.
 * `LibraryFanout` -- N GPUs, the whole sharded cascade inside libgraindispatch
   (gd_fanout_multi_device over the library's RCCL communicator): the path a C# host drives.
-* `ShardedFanout` -- N GPUs (one process each): the directory is sharded by ring owner as in
-  orleans_amd.sharded; each rank expands its own publishers (gd_fanout_expand_device),
-  partitions the (target, sender) pairs by owner rank (gd_pack_nodes_by_shard_device),
-  exchanges them with one all-to-all-v (RCCL over xGMI; gloo in the CPU tests), then routes
-  (gd_route_nodes_device), buckets and advances its share of the frontier.  The follower
-  graph is replicated on every rank (10M nodes + 100M edges = 0.44 GB of 288 GB).
+  (Round 4 removed the torch.distributed form of the same cascade, which duplicated it.)
 """
 from __future__ import annotations
 
@@ -230,70 +225,3 @@ class LibraryFanout:
 
     def close(self):
         self.engine.gd.comm_destroy()
-
-
-class ShardedFanout:
-    """All hops with the directory sharded by ring owner over the ranks of `group`.
-    `engine` follows DeviceFanoutEngine's contract (the CPU tests pass an oracle engine)."""
-
-    def __init__(self, engine, graph, n_act: int, group: Optional[dist.ProcessGroup] = None,
-                 stage_via_cpu: bool = False):
-        self.engine, self.graph, self.n_act = engine, graph, n_act
-        self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
-        self.stage_via_cpu = stage_via_cpu
-
-    def _a2a(self, out, inp, out_splits=None, in_splits=None):
-        if self.stage_via_cpu and out.device.type != "cpu":
-            o_cpu = torch.empty(out.shape, dtype=out.dtype)
-            dist.all_to_all_single(o_cpu, inp.cpu(), out_splits, in_splits, group=self.group)
-            out.copy_(o_cpu)
-        else:
-            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
-
-    def exchange(self, target: torch.Tensor, sender: torch.Tensor):
-        send_t, send_s, counts = self.engine.pack_nodes_by_shard(target, sender, self.world)
-        counts64 = counts.to(torch.int64)
-        recv_counts = torch.empty_like(counts64)
-        self._a2a(recv_counts, counts64)
-        in_splits, out_splits = counts64.tolist(), recv_counts.tolist()
-        m = int(sum(out_splits))
-        recv_t = torch.empty(m, dtype=target.dtype, device=target.device)
-        recv_s = torch.empty(m, dtype=sender.dtype, device=sender.device)
-        self._a2a(recv_t, send_t, out_splits, in_splits)
-        self._a2a(recv_s, send_s, out_splits, in_splits)
-        src = torch.repeat_interleave(torch.arange(self.world, dtype=torch.int32, device=target.device),
-                                      recv_counts.to(target.device))
-        return recv_t, recv_s, src
-
-    def local_seeds(self, seeds: torch.Tensor) -> torch.Tensor:
-        """The seeds this rank owns (their publisher activations live here), in seed order."""
-        if self.world == 1:
-            return seeds
-        ones = torch.zeros_like(seeds)
-        s_t, _, counts = self.engine.pack_nodes_by_shard(seeds, ones, self.world)
-        c = counts.to(torch.int64).cpu().tolist()
-        lo = sum(c[:self.rank])
-        return s_t[lo:lo + c[self.rank]]
-
-    def run(self, seeds: torch.Tensor, hops: int) -> List[HopResult]:
-        with self.engine.context():
-            return self._run(seeds, hops)
-
-    def _run(self, seeds: torch.Tensor, hops: int) -> List[HopResult]:
-        eng = self.engine
-        visited = eng.new_visited(self.n_act)
-        frontier = self.local_seeds(seeds)
-        eng.mark_visited(visited, frontier)
-        out = []
-        for _ in range(hops):
-            target, sender = eng.expand(self.graph, frontier)
-            if self.world > 1:
-                target, sender, src = self.exchange(target, sender)
-            else:
-                src = None
-            st, silo, act, perm, off = eng.route_nodes_bucket(target, self.n_act)
-            out.append(HopResult(frontier, target, sender, src, st, silo, act, perm, off))
-            frontier = eng.frontier_next(off, self.n_act, visited)
-        return out

@@ -8,7 +8,10 @@ partitioned by owner rank (stable), exchanged with one all-to-all-v, then
 routed (directory probe) and bucketed per activation on the owner.
 
 Exchange = torch.distributed all_to_all_single: RCCL over xGMI on MI355X
-(backend "nccl"), gloo in the CPU tests.  The local steps run through an
+(backend "nccl"), gloo in the CPU tests.  This is the cross-check of the library's own exchange
+(LibraryRouter: gd_route_multi_device, the product path); membership handoffs are the library's
+gd_dir_handoff_multi only (GrainInfo.Merge semantics, GrainDirectoryPartition.cs:139-179).
+The local steps run through an
 engine object; `DeviceEngine` is the product engine (libgraindispatch device
 entry points on torch-allocated HBM buffers).
 """
@@ -95,33 +98,6 @@ class DeviceEngine:
                                     perm.data_ptr(), off.data_ptr())
         return st, silo, act, perm, off
 
-    def split(self, keep_silos, n_silos: int):
-        """Move out the entries whose owner under the installed ring is not kept here
-        (gd_dir_split_device).  Returns device tensors keys (m,3) int64, vals (m,2) int32."""
-        keep = g.GrainDispatch.keep_mask(keep_silos, n_silos)
-        m = self.gd.split_device(keep, True, None, None, 0)
-        keys = torch.empty((m, 3), dtype=torch.int64, device=self.device)
-        vals = torch.empty((m, 2), dtype=torch.int32, device=self.device)
-        if m:
-            got = self.gd.split_device(keep, True, keys.data_ptr(), vals.data_ptr(), m)
-            assert got == m
-        return keys, vals
-
-    def register(self, keys: torch.Tensor, vals: torch.Tensor):
-        """Merge received entries (GrainDirectoryPartition.Merge as a batched
-        AddSingleActivation).  Returns (winning acts, winning silos, inserted) on the host."""
-        torch.cuda.current_stream(self.device).wait_stream(self.stream)
-        k = keys.cpu().numpy().view("uint64").reshape(-1, 3)
-        v = vals.cpu().numpy().view("uint32").reshape(-1, 2)
-        return self.gd.register(k, v[:, 0], v[:, 1])
-
-
-@dataclass
-class HandoffResult:
-    moved_out: int              # entries this rank split off
-    received: int               # entries merged into this rank
-    conflicts: int              # received entries whose grain was already registered here
-
 
 class ShardedRouter:
     """`stage_via_cpu` is a rehearsal mode only (several ranks sharing one GPU with
@@ -158,31 +134,6 @@ class ShardedRouter:
         recv_src = torch.repeat_interleave(torch.arange(self.world, dtype=torch.int32, device=keys.device),
                                            recv_counts.to(keys.device))
         return recv_keys, recv_idx, recv_src
-
-    def handoff(self, n_silos: int) -> HandoffResult:
-        """Directory handoff after a membership change: install the new ring on
-        every rank first.  Each rank splits off the entries whose new owner silo lives on
-        another rank (GrainDirectoryHandoffManager.ProcessSiloAddEvent / RemoveEvent,
-        GrainDirectoryHandoffManager.cs:125-245), exchanges them with one all-to-all-v (the
-        RegisterMany RPC of the reference) and merges what it receives."""
-        keep = [s for s in range(n_silos) if silo_rank(s, self.world) == self.rank]
-        keys, vals = self.engine.split(keep, n_silos)
-        moved = int(keys.shape[0])
-        if self.world == 1:
-            return HandoffResult(moved, 0, 0)
-        send_keys, send_idx, counts = self.engine.pack_by_shard(keys, self.world)
-        send_vals = vals[send_idx.long()]
-        counts64 = counts.to(torch.int64)
-        recv_counts = torch.empty_like(counts64)
-        self._a2a(recv_counts, counts64)
-        in_splits, out_splits = counts64.tolist(), recv_counts.tolist()
-        m = int(sum(out_splits))
-        recv_keys = torch.empty((m, 3), dtype=keys.dtype, device=keys.device)
-        self._a2a(recv_keys, send_keys, out_splits, in_splits)
-        recv_vals = torch.empty((m, 2), dtype=vals.dtype, device=vals.device)
-        self._a2a(recv_vals, send_vals, out_splits, in_splits)
-        _, _, inserted = self.engine.register(recv_keys, recv_vals)
-        return HandoffResult(moved, m, int((inserted == 0).sum()))
 
     def _a2a_v(self, tensors, in_splits, out_splits):
         outs = []

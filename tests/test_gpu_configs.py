@@ -346,3 +346,92 @@ def test_bucket_packed_records(gd, monkeypatch, bucket, n, n_act, skew):
     np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), wp)
     np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), wo)
     e.close()
+
+
+# ----------------------------------------------------------------------------- measured choices (GD_TUNE_*)
+def test_tune_pin_get_reset(gd):
+    """gd_tune_set pins a kind's variant from the first launch (the kernels that run show it), -1
+    returns it to measuring, gd_tune_get reports the choice, gd_tune_reset forgets the measured ones;
+    results never change."""
+    acts = np.random.default_rng(3).integers(0, 1 << 20, size=1 << 21).astype(np.uint32)
+    wp, wo = o.bucket_stable(acts, 1 << 20)
+    q = (1 << 21) // ((1 << 20 >> 10) + 1)
+    sub = 0
+    while sub < 31 and (q >> sub) > 1:
+        sub += 1
+    e = gd.GrainDispatch(device=0, table_capacity=1024)
+    e.set_kernel_timing(True)
+    for pin, want, absent in ((1, "k_msd_local", "k_starts_rangescan"), (0, "k_starts_rangescan", "k_msd_local")):
+        e.tune_set("bucket", pin)
+        assert e.tune_get("bucket", 1 << 21, sub) == pin
+        e.kernel_times_reset()
+        p, off = e.bucket(acts, 1 << 20)
+        names = {k for k, (launches, _) in e.kernel_times().items() if launches}
+        assert want in names and absent not in names, (pin, names)
+        np.testing.assert_array_equal(p, wp)
+        np.testing.assert_array_equal(off, wo)
+    e.tune_set("bucket", -1)
+    assert e.tune_get("bucket", 1 << 21, sub) == -1           # measuring
+    for _ in range(6):                                         # 2 x 2 timed launches, then the pick
+        p, off = e.bucket(acts, 1 << 20)
+        np.testing.assert_array_equal(p, wp)
+    assert e.tune_get("bucket", 1 << 21, sub) in (0, 1)
+    e.tune_reset()
+    assert e.tune_get("bucket", 1 << 21, sub) == -1
+    with pytest.raises(gd.GrainDispatchError):
+        e.tune_set("bucket", 2)                                # the bucketing has two variants
+    e.close()
+
+
+def test_tune_agree_w8(gd):
+    """gd_tune_agree at W = 8 (in-process transport): after each rank measured its own probe and
+    bucketing variants on live exchange batches, every rank keeps the same pick for every measured
+    entry -- the variant with the least summed time -- and results stay bit-exact afterwards.  The
+    communicator reports its 8 ranks (gd_comm_info)."""
+    W, G = 8, 1 << 20
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    reg = o.grain_keys(TC, np.arange(G))
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    act = np.zeros(G, np.uint32)
+    for r in range(W):
+        act[own % W == r] = np.arange(int((own % W == r).sum()))
+    n_act = [int((own % W == r).sum()) for r in range(W)]
+    es = []
+    for r in range(W):
+        # the plain owner probe (its index / directory variants are what is measured)
+        e = gd.GrainDispatch(device=0, table_capacity=1 << 19, my_silo=r, options={"region_probe": 0})
+        e.ring_set_silos("D", _tuples(silos))
+        mine = own % W == r
+        e.register(reg[mine], act[mine], own[mine])
+        es.append(e)
+    gd.GrainDispatch.comm_init_local(es)
+    for r in range(W):
+        info = es[r].comm_info()
+        assert info == {"n_ranks": W, "rank": r, "transport": "in-process"}, info
+    rng = np.random.default_rng(88)
+    n = 3 << 20
+    batches = [o.grain_keys(TC, rng.integers(0, G, size=n)) for _ in range(W)]
+    for _ in range(7):
+        res = _run_ranks([lambda r=r: es[r].route_multi(batches[r], n_act[r], no_keys=True) for r in range(W)])
+    m = [len(res[r]["act"]) for r in range(W)]
+    assert len({int(x).bit_length() for x in m}) == 1            # one size class on every rank
+    _run_ranks([lambda r=r: es[r].tune_agree() for r in range(W)])
+    q = m[0] // ((n_act[0] >> 10) + 1)
+    sub = 0
+    while sub < 31 and (q >> sub) > 1:
+        sub += 1
+    for kind in ("probe_n1", "bucket"):
+        picks = [es[r].tune_get(kind, m[r], sub if kind == "bucket" else 0) for r in range(W)]
+        assert len(set(picks)) == 1 and picks[0] >= 0, (kind, picks)
+    res = _run_ranks([lambda r=r: es[r].route_multi(batches[r], n_act[r]) for r in range(W)])
+    full = o.DirectoryArrays(reg, act, own)
+    for r in range(W):
+        wp, wo = o.bucket_stable(res[r]["act"], n_act[r])
+        np.testing.assert_array_equal(res[r]["perm"], wp)
+        np.testing.assert_array_equal(res[r]["offsets"], wo)
+        st, _, a, _, _ = o.route_batch_np(res[r]["recv_keys"], spec, full, my_silo=r)
+        np.testing.assert_array_equal(res[r]["act"], a)
+    for e in es:
+        e.comm_destroy()
+        e.close()

@@ -29,17 +29,3 @@ def test_sharded_exchange_gloo(world):
     assert p.returncode == 0, out[-4000:]
     for r in range(world):
         assert f"OK rank {r}/{world}" in out, out[-4000:]
-
-
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_fanout_gloo(world):
-    """SURVEY 8 f2 across ranks: orleans_amd.fanout.ShardedFanout with an oracle engine."""
-    env = dict(os.environ, OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "tests", "_gloo_fanout_worker.py")]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
-    out = p.stdout + p.stderr
-    assert p.returncode == 0, out[-4000:]
-    for r in range(world):
-        assert f"OK fanout rank {r}/{world}" in out, out[-4000:]
