@@ -353,6 +353,22 @@ PINNED = {"cfg2": {"probe_keys": 0, "probe_n1": 0, "bucket": 1},
           "cfg4": {"probe_fanout": 0, "probe_nodes": 0, "bucket": 1}}
 
 
+def silos_note(which: str) -> str:
+    if which == "literal":
+        return "8 x 10.0.0.{1..8}:11111 generation 1 (SURVEY 8(d)'s literal silo set)"
+    return ("8 x 10.0.0.{1..8}:11111, balanced generations (tools/balanced_silos.py: each silo owns 1/8 of the "
+            "ring; SURVEY 8(d) names generation 1 -- --silos literal -- whose ring gives one silo 35.7 %; "
+            "generations are arbitrary timestamps, SiloAddress.cs:72-76, and the per-message work is the same)")
+
+
+def comm_info(w) -> dict:
+    """The library communicator's own view (gd_comm_info: RCCL's ncclCommCount / ncclCommUserRank)."""
+    try:
+        return w["e"].comm_info()
+    except Exception as ex:   # noqa: BLE001 -- reporting only
+        return {"error": f"{ex!r}"[:120]}
+
+
 def settle_steps(args) -> int:
     return 0 if args.tune == "pinned" else SETTLE_STEPS
 
@@ -372,7 +388,10 @@ def timed_steps(router, keys, n_act, stream, steps, warmup, settle=SETTLE_STEPS,
             router.route_bucket(keys, n_act)
         if agree is not None:
             torch.cuda.synchronize()
-            agree.tune_agree()
+            try:
+                agree.tune_agree()
+            except Exception as ex:   # noqa: BLE001 -- speed only: every rank keeps its own choices
+                print(f"gd_tune_agree failed: {ex!r}", file=sys.stderr, flush=True)
         for _ in range(warmup):
             router.route_bucket(keys, n_act)
         torch.cuda.synchronize()
@@ -567,13 +586,14 @@ def main():
                 "Zipf(1.1) keys by inverse CDF on the GPU, seed 0x5EED0003+rank"),
             "config": {"workload": workload_name(args.workload, world, N, G_total),
                        "msgs_per_gpu": N, "grains_total": G_total, "ring_mode": args.mode,
-                       "silos": f"8 x 10.0.0.{{1..8}}:11111, {args.silos} generations",
+                       "silos": silos_note(args.silos),
                        "owner_share_max": w["owner_share_max"],
                        "owner_share_max_by_silo_set": w["owner_share_by_set"],
                        "table_load": round(n_act / cap, 3), "parallelism": f"shard{world}"},
             "routed_ok_last_step_rank0": st_ok,
             "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
             "exchange": exchange,
+            "comm": comm_info(w),
             "roofline": roofline,
             "kernels": kernels,
             "cpu_baseline": cpu,
@@ -943,7 +963,10 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
         step()
     if world > 1 and args.tune == "measured" and runner is not None and isinstance(runner, LibraryFanout):
         torch.cuda.synchronize()
-        e.tune_agree()
+        try:
+            e.tune_agree()
+        except Exception as ex:   # noqa: BLE001 -- speed only: every rank keeps its own choices
+            print(f"gd_tune_agree failed: {ex!r}", file=sys.stderr, flush=True)
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -1003,8 +1026,9 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
                     f"seed 0x5EED0004",
             "config": {"workload": f"cfg4: {n} grains, {int(ro[-1])} follower edges, {args.seeds} seeds, "
                                    f"{args.hops} hops", "ring_mode": args.mode,
-                       "silos": f"8 x 10.0.0.{{1..8}}:11111, {args.silos} generations",
+                       "silos": silos_note(args.silos),
                        "parallelism": f"shard{world}" + ("-rehearsal" if args.rehearse_one_gpu else "")},
+            "comm": e.comm_info(),
             "messages_per_step": int(msgs_total / steps), "hop_messages_rank0": hop_msgs,
             "hop_publishers_rank0": hop_front, "setup_s": round(setup_s, 1), "exchange": exchange,
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,

@@ -389,7 +389,10 @@ def test_tune_agree_w8(gd):
     entry -- the variant with the least summed time -- and results stay bit-exact afterwards.  The
     communicator reports its 8 ranks (gd_comm_info)."""
     W, G = 8, 1 << 20
-    silos = o.bench_silos(8)
+    # the bench's balanced silo set (every silo owns 1/8 of the ring): every rank receives a batch of
+    # one size class, so the ranks measure the same tune entries
+    gens = [138558, 165678, 215136, 61804, 17808, 48728, 207265, 76820]
+    silos = [o.Silo(f"10.0.0.{i + 1}", 11111, gens[i]) for i in range(8)]
     spec = o.ring_spec(silos, "D")
     reg = o.grain_keys(TC, np.arange(G))
     own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
