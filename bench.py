@@ -66,7 +66,7 @@ def radix_layout(n: int, n_act: int):
     return passes, bits, packed
 
 
-MSD_CAP, CH_CAP, L2_SMALL = 24576, 16384, 1024     # gd_msd.h / gd_msd2.h
+MSD_CAP, MSD_MID_CAP, CH_CAP, L2_SMALL = 24576, 8192, 8192, 1024     # gd_msd.h / gd_msd2.h
 
 
 def bucket_form(names) -> str:
@@ -88,8 +88,10 @@ def l2_classes(acts: np.ndarray, n_act: int, t_small: int = L2_SMALL) -> dict:
     per = np.full(R, 1024, np.int64)
     per[-1] = n_act + 1 - (R - 1) * 1024
     small, hot = S <= t_small, S > MSD_CAP
-    staged = ~small & ~hot
+    mid = ~small & (S <= MSD_MID_CAP)
+    staged = ~small & ~mid & ~hot
     return {"small": (int(S[small].sum()), int(per[small].sum())),
+            "mid": (int(S[mid].sum()), int(per[mid].sum())),
             "staged": (int(S[staged].sum()), int(per[staged].sum())),
             "hot": (int(S[hot].sum()), int(per[hot].sum())), "chunks": int(((S[hot] + CH_CAP - 1) // CH_CAP).sum()),
             "hot_ranges": int(hot.sum()), "ranges": R}
@@ -133,6 +135,7 @@ def bucket_bytes(form: str, n: int, n_act: int, acts=None) -> dict:
         out["k_l2_small"] = n * 10.0 + off      # unknown split: all charged to one kernel
         return out
     out.update({"k_l2_small": c["small"][0] * 10.0 + c["small"][1] * 4.0,
+                "k_msd_local_mid": c["mid"][0] * 10.0 + c["mid"][1] * 4.0,
                 "k_msd_local": c["staged"][0] * 10.0 + c["staged"][1] * 4.0,
                 "k_l2_chunk_hist": c["hot"][0] * 2.0 + c["chunks"] * 4096.0,
                 "k_l2_chunk_scan": c["chunks"] * 8192.0 + c["hot_ranges"] * 4096.0,
@@ -143,7 +146,8 @@ def bucket_bytes(form: str, n: int, n_act: int, acts=None) -> dict:
 
 
 # The kernels of a bucketing stage (every form), for the stage total
-BUCKET_KERNELS = ("k_radix_hist", "k_radix_rowscan", "k_radix_scatter", "k_msd_local", "k_starts_rangescan",
+BUCKET_KERNELS = ("k_radix_hist", "k_radix_rowscan", "k_radix_scatter", "k_msd_local", "k_msd_local_mid",
+                  "k_starts_rangescan",
                   "k_scan_reduce", "k_scan_down", "k_fill", "k_seg_table", "k_seg_hist", "k_seg_scatter",
                   "k_l2_classify", "k_l2_small", "k_l2_chunk_hist", "k_l2_chunk_scan", "k_l2_chunk_scatter")
 
@@ -207,7 +211,8 @@ def roofline_of(kt: dict, steps: int, n: int, n_act: int, acts, tag, world: int 
     if dom == "k_route":
         roofline["bytes_model"] = "SURVEY 8(d): key 24 + one 32-B directory slot + silo/act/status 9 B"
     bk = {}
-    for name in ("k_radix_scatter", "k_msd_local", "k_seg_scatter", "k_l2_small", "k_l2_chunk_scatter"):
+    for name in ("k_radix_scatter", "k_msd_local", "k_msd_local_mid", "k_seg_scatter", "k_l2_small",
+                 "k_l2_chunk_scatter"):
         if name in kernels and kernels[name]["alg_bytes_per_step"]:
             e = entry(name)
             launches = e["launches_per_step"]

@@ -873,6 +873,10 @@ int gd_set_kernel_timing(gd_handle* h, int enable);
 #define GD_OPT_L2_STAGED    12  /* two-level three-pass form: ranges of at most this many messages (and more
                                    than GD_OPT_L2_SMALL) sorted one workgroup a range, larger ones in 8K
                                    chunks over several workgroups (default 24,576, the staging capacity) */
+#define GD_OPT_L2_MID       13  /* two-level three-pass form: ranges of at most this many messages (and more
+                                   than GD_OPT_L2_SMALL) sorted by 512-thread workgroups, three a CU, the rest
+                                   of the staged class by 1,024-thread ones (default 8,192, the 512-thread
+                                   capacity; 0 = every staged range on the 1,024-thread sort) */
 int gd_option_set(gd_handle* h, int option, int64_t value);
 int gd_option_get(const gd_handle* h, int option, int64_t* value);
 

@@ -179,9 +179,10 @@ struct gd_handle {
     int tune_pin[GD_TUNE_KINDS] = {-1, -1, -1, -1, -1};   // gd_tune_set: pinned variant per kind, -1 measured
     int msd_mode = 1;           // two-level bucketing (gd_msd.h, gd_msd2.h): 0 off, 1 measured (default), 2 always (GD_MSD)
     uint32_t l2_small = 1024;   // three-pass form: ranges of at most this many messages are sorted one wave a range
+    uint32_t l2_mid = MSD_MID_CAP;  // three-pass form: staged ranges up to this many messages on the 512-thread sort
     uint32_t l2_staged = MSD_CAP;  // three-pass form: ranges up to this many messages one workgroup each, more: chunks
     uint32_t n_cu = 256;        // compute units (hipDeviceProp_t::multiProcessorCount): persistent grids
-    DevBuf m3[14];              // three-pass form's scratch (msd3_bucket)
+    DevBuf m3[15];              // three-pass form's scratch (msd3_bucket)
     DevBuf tune_buf;            // gd_tune_agree's send / receive records
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
     // per launch kind and size class: the probe variant, timed on live launches.  Variants: 0 the index
@@ -930,6 +931,7 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     GD_TRY(ensure(h, m[5], (size_t)L2_CTR_WORDS * 4));
     GD_TRY(ensure(h, m[6], (size_t)R * 4));                        // thin ranges
     GD_TRY(ensure(h, m[7], (size_t)R * 4));                        // staged ranges
+    GD_TRY(ensure(h, m[14], (size_t)R * 4));                       // mid ranges
     GD_TRY(ensure(h, m[8], (size_t)cr_bound * 4 * 4));             // chunked ranges
     // chunk-scan items: 1 a range of <= CS_DIRECT chunks, else CS_SLABS a piece of CS_ROWS chunks
     const uint32_t it_bound = cr_bound + CS_SLABS * (ch_bound / CS_DIRECT + blocks_for(ch_bound, CS_ROWS));
@@ -978,11 +980,12 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
                       (const uint32_t*)hseg, kB, vB, h->xcd_tiles));
     // level 2
     uint32_t* cr = (uint32_t*)m[8].p;
-    const L2Lists l{(uint32_t*)m[4].p, (uint32_t*)m[6].p, (uint32_t*)m[7].p, cr, cr + cr_bound, cr + 2 * cr_bound,
+    const L2Lists l{(uint32_t*)m[4].p, (uint32_t*)m[6].p, (uint32_t*)m[7].p, (uint32_t*)m[14].p, cr, cr + cr_bound,
+                    cr + 2 * cr_bound,
                     (uint32_t*)m[9].p, cr + 3 * cr_bound, (uint32_t*)m[13].p, (uint32_t*)m[5].p};
     GD_TRY(launch(h, "k_l2_classify", dim3(blocks_for(R, BLOCK)), dim3(BLOCK), 0, k_l2_classify, (const uint32_t*)hseg,
                   (const uint32_t*)seg_start, (const uint32_t*)seg_tb, a, R, n, h->l2_small,
-                  std::max(h->l2_small, h->l2_staged), l));
+                  std::max(h->l2_small, h->l2_mid), std::max(h->l2_small, h->l2_staged), l));
     // persistent grids sized to what the chip holds at once (a second round of workgroups would wait for
     // the first to finish its whole share): k_l2_small 4 a CU (32 KB of LDS, 8 waves each), the range
     // sort 1 a CU (135 KB), the chunk scatter 2 (72 KB), the chunk histogram 4 and the scan 2 a CU
@@ -990,7 +993,11 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     GD_TRY(launch(h, "k_l2_small", dim3(std::min<uint32_t>(blocks_for(R, L2_SMALL_WAVES), 4 * cu8)),
                   dim3(L2_SMALL_WAVES * WAVE), 0, k_l2_small, (const uint16_t*)kB, (const uint32_t*)vB, l, n, n_act, perm,
                   offsets, rank_out));
-    GD_TRY(launch(h, "k_msd_local", dim3(std::min<uint32_t>(R, cu8)), dim3(MSD_NT), 0, k_msd_local_list,
+    GD_TRY(launch(h, "k_msd_local_mid", dim3(std::min<uint32_t>(R, 3 * cu8)), dim3(MSD_MID_NT), 0,
+                  k_msd_local_list<MSD_MID_NT, MSD_MID_RW>, (const uint16_t*)kB, (const uint32_t*)vB,
+                  (const uint32_t*)l.rs, (const uint32_t*)l.mid, (const uint32_t*)(l.ctr + 5), n, n_act, perm, offsets,
+                  rank_out));
+    GD_TRY(launch(h, "k_msd_local", dim3(std::min<uint32_t>(R, cu8)), dim3(MSD_NT), 0, k_msd_local_list<MSD_NT, MSD_RW>,
                   (const uint16_t*)kB, (const uint32_t*)vB, (const uint32_t*)l.rs, (const uint32_t*)l.staged,
                   (const uint32_t*)(l.ctr + 1), n, n_act, perm, offsets, rank_out));
     uint32_t* hh = (uint32_t*)m[10].p;
@@ -1975,6 +1982,10 @@ int gd_option_set(gd_handle* h, int option, int64_t v) {
             if (!in(0, MSD_CAP)) break;
             h->l2_staged = (uint32_t)v;
             return GD_OK;
+        case GD_OPT_L2_MID:
+            if (!in(0, MSD_MID_CAP)) break;
+            h->l2_mid = (uint32_t)v;
+            return GD_OK;
         default: return set_err(h, GD_EINVAL, "gd_option_set: unknown option %d", option);
     }
     return set_err(h, GD_EINVAL, "gd_option_set: option %d: value %lld out of range", option, (long long)v);
@@ -1996,6 +2007,7 @@ int gd_option_get(const gd_handle* hc, int option, int64_t* v) {
         case GD_OPT_MB_SPLIT: *v = h->mb_split; return GD_OK;
         case GD_OPT_MB_TRACE: *v = h->mb_trace; return GD_OK;
         case GD_OPT_L2_STAGED: *v = h->l2_staged; return GD_OK;
+        case GD_OPT_L2_MID: *v = h->l2_mid; return GD_OK;
         default: return set_err(h, GD_EINVAL, "gd_option_get: unknown option %d", option);
     }
 }

@@ -56,24 +56,30 @@ constexpr int MSD_G = 8;                           // rows whose message indices
 constexpr uint32_t MSD_MAX_RANGES = B2_RMAX2;      // the high digit of the one-pass form
 constexpr int MSD_RW = 24;                         // rows of 64 messages a wave holds
 constexpr uint32_t MSD_CAP = MSD_RW * MSD_NT;      // messages a workgroup stages (24,576)
+constexpr int MSD_MID_NT = 512;                    // the three-pass form's mid-size ranges: 512 threads,
+constexpr int MSD_MID_RW = 16;                     // 16 rows a wave: 8,192 messages, 52 KB of LDS (3 a CU)
+constexpr uint32_t MSD_MID_CAP = MSD_MID_NT * MSD_MID_RW;
 
+template <int NT, int RW>
 struct MsdShared {
+    static constexpr int NW = NT / WAVE;
     uint32_t run[MSD_L];
-    uint32_t wc[MSD_NW][MSD_LW];
-    uint32_t out[MSD_CAP];
-    uint32_t red[MSD_NW];
+    uint32_t wc[NW][MSD_LW];
+    uint32_t out[NT * RW];
+    uint32_t red[NW];
     uint32_t base;
 };
 
 // The per-wave counts (u16 pairs, wc[wave * MSD_LW + word]) become each wave's first position per
-// activation (an exclusive prefix over the waves); thread t < MSD_LW owns word t (activations 2t,
+// activation (an exclusive prefix over the NW waves); thread t < MSD_LW owns word t (activations 2t,
 // 2t + 1) and returns the two totals.
+template <int NW = MSD_NW>
 __device__ __forceinline__ void msd_wave_prefix(uint32_t* wc, uint32_t tid, uint32_t& tlo, uint32_t& thi) {
     tlo = 0;
     thi = 0;
     if (tid >= MSD_LW) return;
 #pragma unroll
-    for (int ww = 0; ww < MSD_NW; ++ww) {
+    for (int ww = 0; ww < NW; ++ww) {
         const uint32_t v = wc[ww * MSD_LW + tid];
         wc[ww * MSD_LW + tid] = tlo | (thi << 16);
         tlo += v & 0xFFFFu;
@@ -117,31 +123,34 @@ __device__ __forceinline__ uint32_t msd_fold_rank(uint32_t* wc, uint32_t k) {
 // MSD output (rk: range-local keys, u16; ri: message indices).  Writes perm[base, base + S), the
 // range's bucket starts offsets[b << 10, ... + L) and, for the range holding n_act, offsets[n_act + 1]
 // = n.  Called by all MSD_NT threads; LDS is free on entry and on return.
-template <bool FOLD>
-__device__ __forceinline__ void msd_range(MsdShared& sh, uint32_t b, uint32_t base, uint32_t S,
+template <bool FOLD, int NT = MSD_NT, int RW = MSD_RW>
+__device__ __forceinline__ void msd_range(MsdShared<NT, RW>& sh, uint32_t b, uint32_t base, uint32_t S,
                                           const uint16_t* __restrict__ keys16, const uint32_t* __restrict__ idx,
                                           uint32_t n, uint32_t n_act, uint32_t* __restrict__ perm,
                                           uint32_t* __restrict__ offsets, uint32_t* __restrict__ rank_out) {
+    constexpr int NW = NT / WAVE;
+    constexpr uint32_t CAP = NT * RW;
+    static_assert(NT >= (int)MSD_LW, "a thread for every u16-pair counter word");
     const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
     const uint32_t k0 = b << MSD_SHIFT;
     const uint32_t L = min(MSD_L, n_act + 1 - k0);       // activations of this range
     const uint16_t* rk = keys16 + base;
     const uint32_t* ri = idx + base;
     if (tid == 0 && b == (n_act >> MSD_SHIFT)) offsets[n_act + 1] = n;   // the range holding n_act: the end
-    sh.run[tid] = 0;
-    for (uint32_t x = tid; x < MSD_NW * MSD_LW; x += MSD_NT) (&sh.wc[0][0])[x] = 0;
-    if (S <= MSD_CAP) {
+    for (uint32_t x = tid; x < MSD_L; x += NT) sh.run[x] = 0;
+    for (uint32_t x = tid; x < NW * MSD_LW; x += NT) (&sh.wc[0][0])[x] = 0;
+    if (S <= CAP) {
         // staged: wave w takes the contiguous segment [s0, s1) of the range, the range-local keys
         // (< 1,024; 0xFFFF past the segment) two to a register, every load in flight at once
-        const uint32_t seg = (S + MSD_NW - 1) / MSD_NW;
+        const uint32_t seg = (S + NW - 1) / NW;
         const uint32_t s0 = min(w * seg, S), s1 = min((w + 1) * seg, S);
-        uint32_t kp[MSD_RW / 2];
+        uint32_t kp[RW / 2];
 #pragma unroll
-        for (int j = 0; j < MSD_RW / 2; ++j) kp[j] = 0xFFFFFFFFu;   // an empty range: no keys
+        for (int j = 0; j < RW / 2; ++j) kp[j] = 0xFFFFFFFFu;   // an empty range: no keys
         if (S) {                                         // unconditional loads (clamped), selects after
             const uint32_t last = S - 1;
 #pragma unroll
-            for (int r = 0; r < MSD_RW; r += 2) {
+            for (int r = 0; r < RW; r += 2) {
                 const uint32_t i = s0 + r * WAVE + lane;
                 const uint32_t a = rk[min(i, last)], c = rk[min(i + WAVE, last)];
                 kp[r / 2] = (i < s1 ? a : 0xFFFFu) | ((i + WAVE < s1 ? c : 0xFFFFu) << 16);
@@ -149,7 +158,7 @@ __device__ __forceinline__ void msd_range(MsdShared& sh, uint32_t b, uint32_t ba
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < MSD_RW; ++r) {
+        for (int r = 0; r < RW; ++r) {
             const uint32_t k = (kp[r / 2] >> (16 * (r & 1))) & 0xFFFFu;
             if constexpr (FOLD) msd_fold_count(sh.wc[w], k);
             else if (k != 0xFFFFu) atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
@@ -157,11 +166,11 @@ __device__ __forceinline__ void msd_range(MsdShared& sh, uint32_t b, uint32_t ba
         // the rank sweep decodes the keys again rather than keeping the count sweep's addresses live
         // across the barriers (that spilled)
 #pragma unroll
-        for (int j = 0; j < MSD_RW / 2; ++j) asm volatile("" : "+v"(kp[j]));
+        for (int j = 0; j < RW / 2; ++j) asm volatile("" : "+v"(kp[j]));
         __syncthreads();
         uint32_t tlo, thi;
-        msd_wave_prefix(&sh.wc[0][0], tid, tlo, thi);
-        const uint32_t ex = block_excl_scan_add_n<MSD_NT>(tlo + thi, sh.red);
+        msd_wave_prefix<NW>(&sh.wc[0][0], tid, tlo, thi);
+        const uint32_t ex = block_excl_scan_add_n<NT>(tlo + thi, sh.red);
         if (tid < MSD_LW) {
             sh.run[2 * tid] = ex;
             sh.run[2 * tid + 1] = ex + tlo;
@@ -171,15 +180,15 @@ __device__ __forceinline__ void msd_range(MsdShared& sh, uint32_t b, uint32_t ba
         __syncthreads();
         // rows in order: the ranks stay stable; the message indices are loaded MSD_G rows at a time
 #pragma unroll
-        for (int g = 0; g < MSD_RW; g += MSD_G) {
+        for (int g = 0; g < RW; g += MSD_G) {
             uint32_t mm[MSD_G];
 #pragma unroll
-            for (int r = 0; r < MSD_G && g + r < MSD_RW; ++r) {
+            for (int r = 0; r < MSD_G && g + r < RW; ++r) {
                 const uint32_t i = s0 + (g + r) * WAVE + lane;
                 mm[r] = i < s1 ? ri[i] : 0u;
             }
 #pragma unroll
-            for (int r = 0; r < MSD_G && g + r < MSD_RW; ++r) {
+            for (int r = 0; r < MSD_G && g + r < RW; ++r) {
                 const uint32_t k = (kp[(g + r) / 2] >> (16 * ((g + r) & 1))) & 0xFFFFu;
                 if constexpr (FOLD) {
                     const uint32_t at = msd_fold_rank(sh.wc[w], k);
@@ -193,16 +202,16 @@ __device__ __forceinline__ void msd_range(MsdShared& sh, uint32_t b, uint32_t ba
         }
         __syncthreads();
         constexpr int U = 4;                             // gathers in flight a lane
-        for (uint32_t i0 = 0; i0 < S; i0 += U * MSD_NT) {
+        for (uint32_t i0 = 0; i0 < S; i0 += U * NT) {
             uint32_t v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t i = i0 + u * MSD_NT + tid;
+                const uint32_t i = i0 + u * NT + tid;
                 v[u] = i < S ? sh.out[i] : 0u;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t i = i0 + u * MSD_NT + tid;
+                const uint32_t i = i0 + u * NT + tid;
                 if (i < S) {
                     perm[base + i] = v[u];
                     if (rank_out) rank_out[v[u]] = base + i;
@@ -216,6 +225,7 @@ __device__ __forceinline__ void msd_range(MsdShared& sh, uint32_t b, uint32_t ba
     // chunk knows each activation's start, then chunks of MSD_CAP ranked the same way with the
     // indices stored straight to their global places (rolled loops reading the keys again: this form
     // is not the common one)
+    if constexpr (NT != MSD_NT) return;                  // the list forms never pass a range over CAP
     __syncthreads();
     for (uint32_t i = tid; i < S; i += MSD_NT) atomicAdd(&sh.run[rk[i]], 1u);
     __syncthreads();
@@ -266,7 +276,7 @@ __global__ void __launch_bounds__(MSD_NT, 4) k_msd_local(const uint16_t* __restr
                                                          uint32_t n_act, uint32_t* __restrict__ perm,
                                                          uint32_t* __restrict__ offsets,
                                                          uint32_t* __restrict__ rank_out) {
-    __shared__ MsdShared sh;
+    __shared__ MsdShared<MSD_NT, MSD_RW> sh;
     const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
     uint32_t part = 0;
     for (uint32_t d = tid; d < b; d += MSD_NT) part += totals[d];
@@ -282,22 +292,27 @@ __global__ void __launch_bounds__(MSD_NT, 4) k_msd_local(const uint16_t* __restr
     msd_range<false>(sh, b, sh.base, totals[b], keys16, idx, n, n_act, perm, offsets, rank_out);
 }
 
-// Three-pass form: the ranges of list[0, *count) (each <= MSD_CAP messages), range b at rs[b] .. rs[b + 1]
-// of the grouped output, a grid-stride loop (every workgroup exits when the list is done).
-__global__ void __launch_bounds__(MSD_NT, 4) k_msd_local_list(const uint16_t* __restrict__ keys16,
-                                                              const uint32_t* __restrict__ idx,
-                                                              const uint32_t* __restrict__ rs,
-                                                              const uint32_t* __restrict__ list,
-                                                              const uint32_t* __restrict__ count, uint32_t n,
-                                                              uint32_t n_act, uint32_t* __restrict__ perm,
-                                                              uint32_t* __restrict__ offsets,
-                                                              uint32_t* __restrict__ rank_out) {
-    __shared__ MsdShared sh;
+// Three-pass form: the ranges of list[0, *count) (each <= NT x RW messages), range b at rs[b] .. rs[b + 1]
+// of the grouped output, a grid-stride loop (every workgroup exits when the list is done).  <1024, 24>:
+// up to 24,576 messages, 135 KB of LDS (one a CU); <512, 16>: up to 8,192, 52 KB (three a CU) -- the
+// ranges of a few thousand messages of BASELINE cfg 4 (~4,400 a range) and cfg 3's mid ranks.  (Hot-key
+// folding measured slower here: 0.077 against 0.059 ms at cfg 3.)
+template <int NT, int RW>
+__global__ void __launch_bounds__(NT, (NT == MSD_NT ? 4 : 6)) k_msd_local_list(const uint16_t* __restrict__ keys16,
+                                                                              const uint32_t* __restrict__ idx,
+                                                                              const uint32_t* __restrict__ rs,
+                                                                              const uint32_t* __restrict__ list,
+                                                                              const uint32_t* __restrict__ count,
+                                                                              uint32_t n, uint32_t n_act,
+                                                                              uint32_t* __restrict__ perm,
+                                                                              uint32_t* __restrict__ offsets,
+                                                                              uint32_t* __restrict__ rank_out) {
+    __shared__ MsdShared<NT, RW> sh;
     const uint32_t m = *count;
     for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
         const uint32_t b = list[i];
         const uint32_t base = rs[b];
-        msd_range<true>(sh, b, base, rs[b + 1] - base, keys16, idx, n, n_act, perm, offsets, rank_out);
+        msd_range<false, NT, RW>(sh, b, base, rs[b + 1] - base, keys16, idx, n, n_act, perm, offsets, rank_out);
     }
 }
 

@@ -14,7 +14,9 @@
 //           the activations.  Writes the range-local key (key & 1023, u16) and the index (u32), 6 B;
 //   level 2 k_l2_classify sorts the ranges into three work lists by their message count S:
 //             S <= t_small      k_l2_small, one wave a range (its 1,024 counters in 4 KB of LDS);
-//             S <= t_staged     k_msd_local_list (gd_msd.h), one workgroup a range, staged in LDS
+//             S <= t_mid        k_msd_local_list<512, 16> (gd_msd.h), one 512-thread workgroup a
+//                               range, staged in LDS, three workgroups a CU (t_mid <= 8,192);
+//             S <= t_staged     k_msd_local_list<1024, 24>, one 1,024-thread workgroup a range
 //                               (t_staged <= MSD_CAP);
 //             S >  t_staged     chunks of CH_CAP messages, several workgroups a range: k_l2_chunk_hist
 //                               (per-chunk activation counts) -> k_l2_chunk_scan (exclusive prefix of
@@ -51,7 +53,7 @@ constexpr int CH_NW = CH_NT / WAVE;
 constexpr uint32_t CH_CAP = 8192;              // messages a chunk of a hot range (16 rows x 512 lanes)
 constexpr uint32_t CH_RW = CH_CAP / CH_NT;
 constexpr uint32_t L2_CTR_WORDS = 8;           // [0] small ranges, [1] staged ranges, [2] chunks, [3] chunked ranges,
-                                               // [4] chunk-scan items
+                                               // [4] chunk-scan items, [5] mid ranges
 
 // Wave-local LDS hand-off: the wave's earlier LDS writes are complete and visible to its other lanes.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -313,6 +315,7 @@ struct L2Lists {
     uint32_t* rs;          // [R + 1] range starts
     uint32_t* small;       // [R]
     uint32_t* staged;      // [R]
+    uint32_t* mid;         // [R]
     uint32_t* cr_b;        // chunked ranges: range, first chunk, chunks
     uint32_t* cr_cb;
     uint32_t* cr_n;
@@ -336,30 +339,33 @@ __host__ __device__ __forceinline__ uint32_t cs_items(uint32_t C) {
 __global__ void __launch_bounds__(BLOCK) k_l2_classify(const uint32_t* __restrict__ hseg,
                                                        const uint32_t* __restrict__ seg_start,
                                                        const uint32_t* __restrict__ seg_tb, uint32_t a, uint32_t R,
-                                                       uint32_t n, uint32_t t_small, uint32_t t_staged,
+                                                       uint32_t n, uint32_t t_small, uint32_t t_mid,
+                                                       uint32_t t_staged,
                                                        L2Lists l) {
     const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
     const uint32_t lane = lane_id();
     const unsigned long long lt = (1ull << lane) - 1ull;
     const bool valid = b < R;
-    uint32_t S = 0, cls = 3;
+    uint32_t S = 0, cls = 7;                         // 7: no range (past R)
     if (valid) {
         const uint32_t r0 = range_start(b, a, hseg, seg_start, seg_tb);
         const uint32_t r1 = b + 1 < R ? range_start(b + 1, a, hseg, seg_start, seg_tb) : n;
         l.rs[b] = r0;
         if (b + 1 == R) l.rs[R] = n;
         S = r1 - r0;
-        cls = S <= t_small ? 0u : (S <= t_staged ? 1u : 2u);
+        cls = S <= t_small ? 0u : (S <= min(t_mid, t_staged) ? 3u : (S <= t_staged ? 1u : 2u));
     }
 #pragma unroll
-    for (uint32_t c = 0; c < 2; ++c) {
+    for (uint32_t c = 0; c < 4; ++c) {
+        if (c == 2) continue;                            // chunked: below
         const unsigned long long m = __ballot(cls == c);
         if (m == 0) continue;
         const uint32_t lead = (uint32_t)__ffsll((long long)m) - 1;
+        const uint32_t ci = c == 3 ? 5u : c;             // its counter
         uint32_t base = 0;
-        if (lane == lead) base = atomicAdd(&l.ctr[c], (uint32_t)__popcll(m));
+        if (lane == lead) base = atomicAdd(&l.ctr[ci], (uint32_t)__popcll(m));
         base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)lead);
-        if (cls == c) (c == 0 ? l.small : l.staged)[base + (uint32_t)__popcll(m & lt)] = b;
+        if (cls == c) (c == 0 ? l.small : (c == 1 ? l.staged : l.mid))[base + (uint32_t)__popcll(m & lt)] = b;
     }
     const unsigned long long mc = __ballot(cls == 2);
     if (mc == 0) return;
