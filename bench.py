@@ -163,12 +163,17 @@ def kernel_bytes(name: str, n: int, n_act: int, form: str = "lsd", acts=None) ->
 
 def load_pmc(tag: str, kernel: str):
     """HBM bytes per launch of `kernel` from the committed PMC summary profiles/pmc_<tag>_<kernel>.json
-    (cfg2: profiles/pmc_<kernel>.json), or None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{kernel}.json" if tag == "cfg2" else f"pmc_{tag}_{kernel}.json")
-    if not os.path.exists(path):
+    (tools/pmc_traffic.py), or None."""
+    d = load_pmc_entry(tag, kernel)
+    return d.get("hbm_bytes_per_launch") if d else None
+
+
+def load_pmc_entry(tag: str, kernel: str):
+    path = os.path.join(ROOT, "profiles", f"pmc_{tag}_{kernel}.json")
+    if not tag or not os.path.exists(path):
         return None
     with open(path) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+        return json.load(f)
 
 
 def roofline_of(kt: dict, steps: int, n: int, n_act: int, acts, tag, world: int = 1, bytes_fn=None):
@@ -193,6 +198,20 @@ def roofline_of(kt: dict, steps: int, n: int, n_act: int, acts, tag, world: int 
     if not kernels:
         return kernels, None
     pmc_tag = tag if world == 1 else None
+    # every kernel's committed PMC figures at this workload (N = 1): HBM bytes as the counters saw
+    # them, their rate over this run's launch time, and the LDS bank-conflict ratio
+    for name, d in kernels.items():
+        p = load_pmc_entry(pmc_tag, name)
+        if not p or d["ms_per_step"] <= 0:
+            continue
+        t = d["ms_per_step"] / max(1, d["launches_per_step"]) * 1e-3
+        d["pmc_bytes_per_launch"] = round(p["hbm_bytes_per_launch"])
+        d["frac_pmc"] = round(p["hbm_bytes_per_launch"] / t / 1e9 / PEAK_HBM_GBS, 4)
+        if d["alg_bytes_per_step"]:
+            d["traffic_ratio"] = round(p["hbm_bytes_per_launch"] * max(1, d["launches_per_step"])
+                                       / d["alg_bytes_per_step"], 3)
+        if p.get("lds_conflict_ratio") is not None:
+            d["lds_conflict_ratio"] = p["lds_conflict_ratio"]
 
     def entry(name):
         d = kernels[name]

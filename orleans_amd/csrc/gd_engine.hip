@@ -983,7 +983,7 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     const L2Lists l{(uint32_t*)m[4].p, (uint32_t*)m[6].p, (uint32_t*)m[7].p, (uint32_t*)m[14].p, cr, cr + cr_bound,
                     cr + 2 * cr_bound,
                     (uint32_t*)m[9].p, cr + 3 * cr_bound, (uint32_t*)m[13].p, (uint32_t*)m[5].p};
-    GD_TRY(launch(h, "k_l2_classify", dim3(blocks_for(R, BLOCK)), dim3(BLOCK), 0, k_l2_classify, (const uint32_t*)hseg,
+    GD_TRY(launch(h, "k_l2_classify", dim3(blocks_for(R, CL_NT)), dim3(CL_NT), 0, k_l2_classify, (const uint32_t*)hseg,
                   (const uint32_t*)seg_start, (const uint32_t*)seg_tb, a, R, n, h->l2_small,
                   std::max(h->l2_small, h->l2_mid), std::max(h->l2_small, h->l2_staged), l));
     // persistent grids sized to what the chip holds at once (a second round of workgroups would wait for

@@ -333,59 +333,84 @@ __host__ __device__ __forceinline__ uint32_t cs_items(uint32_t C) {
     return C <= CS_DIRECT ? 1u : CS_SLABS * ((C + CS_ROWS - 1) / CS_ROWS);
 }
 
-// Range b's start and size, and its work list (wave-aggregated appends: one atomic a wave and list).
-// A chunked range reserves its chunks and its entry with one 64-bit atomic (chunks in the low word,
-// ranges in the high word), so the chunked ranges' first chunks increase with their entries.
-__global__ void __launch_bounds__(BLOCK) k_l2_classify(const uint32_t* __restrict__ hseg,
+// Range b's start and size, and its work list.  Appends are aggregated per workgroup (one atomic a
+// workgroup and counter: ~100 workgroups at cfg 3 instead of one atomic a wave and list, which queued
+// ~7,000 same-address device atomics); range b + 1's start comes from the next lane.  A chunked range
+// reserves its chunks and its entry with one 64-bit atomic (chunks in the low word, ranges in the high
+// word), so the chunked ranges' first chunks increase with their entries.
+constexpr int CL_NT = 1024;
+constexpr int CL_NW = CL_NT / WAVE;
+__global__ void __launch_bounds__(CL_NT) k_l2_classify(const uint32_t* __restrict__ hseg,
                                                        const uint32_t* __restrict__ seg_start,
                                                        const uint32_t* __restrict__ seg_tb, uint32_t a, uint32_t R,
                                                        uint32_t n, uint32_t t_small, uint32_t t_mid,
-                                                       uint32_t t_staged,
-                                                       L2Lists l) {
-    const uint32_t b = blockIdx.x * BLOCK + threadIdx.x;
-    const uint32_t lane = lane_id();
+                                                       uint32_t t_staged, L2Lists l) {
+    // per wave, then (exclusive-scanned) per workgroup: [0] small, [1] staged, [2] mid, [3] chunked
+    // ranges, [4] chunks, [5] chunk-scan items
+    __shared__ uint32_t s_c[6][CL_NW];
+    __shared__ uint32_t s_base[6];
+    const uint32_t b = blockIdx.x * CL_NT + threadIdx.x;
+    const uint32_t lane = lane_id(), w = threadIdx.x / WAVE;
     const unsigned long long lt = (1ull << lane) - 1ull;
     const bool valid = b < R;
+    const uint32_t r0 = valid ? range_start(b, a, hseg, seg_start, seg_tb) : n;
+    uint32_t r1 = __shfl_down(r0, 1, WAVE);
+    if (lane == WAVE - 1) r1 = b + 1 < R ? range_start(b + 1, a, hseg, seg_start, seg_tb) : n;
     uint32_t S = 0, cls = 7;                         // 7: no range (past R)
     if (valid) {
-        const uint32_t r0 = range_start(b, a, hseg, seg_start, seg_tb);
-        const uint32_t r1 = b + 1 < R ? range_start(b + 1, a, hseg, seg_start, seg_tb) : n;
         l.rs[b] = r0;
         if (b + 1 == R) l.rs[R] = n;
         S = r1 - r0;
         cls = S <= t_small ? 0u : (S <= min(t_mid, t_staged) ? 3u : (S <= t_staged ? 1u : 2u));
     }
-#pragma unroll
-    for (uint32_t c = 0; c < 4; ++c) {
-        if (c == 2) continue;                            // chunked: below
-        const unsigned long long m = __ballot(cls == c);
-        if (m == 0) continue;
-        const uint32_t lead = (uint32_t)__ffsll((long long)m) - 1;
-        const uint32_t ci = c == 3 ? 5u : c;             // its counter
-        uint32_t base = 0;
-        if (lane == lead) base = atomicAdd(&l.ctr[ci], (uint32_t)__popcll(m));
-        base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)lead);
-        if (cls == c) (c == 0 ? l.small : (c == 1 ? l.staged : l.mid))[base + (uint32_t)__popcll(m & lt)] = b;
-    }
+    const unsigned long long m0 = __ballot(cls == 0), m1 = __ballot(cls == 1), m3 = __ballot(cls == 3);
     const unsigned long long mc = __ballot(cls == 2);
-    if (mc == 0) return;
     const uint32_t C = cls == 2 ? (S + CH_CAP - 1) / CH_CAP : 0u;
-    const uint32_t incl = wave_incl_sum_dpp(C);
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, WAVE - 1);
-    unsigned long long old = 0;
-    if (lane == 0)
-        old = atomicAdd(reinterpret_cast<unsigned long long*>(l.ctr + 2),
-                        ((unsigned long long)__popcll(mc) << 32) | total);
-    const uint32_t olo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)old, 0);
-    const uint32_t ohi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(old >> 32), 0);
-    const uint32_t my_r = ohi + (uint32_t)__popcll(mc & lt), my_cb = olo + incl - C;
-    // chunk-scan work items (cs_items): one atomic a wave
     const uint32_t ni = cls == 2 ? cs_items(C) : 0u;
-    const uint32_t iincl = wave_incl_sum_dpp(ni);
-    uint32_t ibase = 0;
-    if (lane == 0) ibase = atomicAdd(&l.ctr[4], (uint32_t)__builtin_amdgcn_readlane((int)iincl, WAVE - 1));
-    ibase = (uint32_t)__builtin_amdgcn_readlane((int)ibase, 0);
-    const uint32_t my_ib = ibase + iincl - ni;
+    const uint32_t cincl = wave_incl_sum_dpp(C), iincl = wave_incl_sum_dpp(ni);
+    if (lane == WAVE - 1) {
+        s_c[0][w] = (uint32_t)__popcll(m0);
+        s_c[1][w] = (uint32_t)__popcll(m1);
+        s_c[2][w] = (uint32_t)__popcll(m3);
+        s_c[3][w] = (uint32_t)__popcll(mc);
+        s_c[4][w] = cincl;
+        s_c[5][w] = iincl;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const uint32_t c = threadIdx.x;
+        uint32_t run = 0;
+#pragma unroll
+        for (int q = 0; q < CL_NW; ++q) {
+            const uint32_t v = s_c[c][q];
+            s_c[c][q] = run;
+            run += v;
+        }
+        s_base[c] = run;                             // the workgroup's total, for now
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const uint32_t c = threadIdx.x;
+        const uint32_t tot = s_base[c];
+        uint32_t base = 0;
+        if (c == 3) {                                // ranges and chunks together
+            const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(l.ctr + 2),
+                                                     ((unsigned long long)tot << 32) | s_base[4]);
+            base = (uint32_t)(old >> 32);
+            s_base[4] = (uint32_t)old;               // c = 4 reads it after the barrier below
+        } else if (c != 4 && tot) {
+            base = atomicAdd(&l.ctr[c == 0 ? 0u : (c == 1 ? 1u : (c == 2 ? 5u : 4u))], tot);
+        }
+        if (c != 4) s_base[c] = base;
+    }
+    __syncthreads();
+    if (cls == 0) l.small[s_base[0] + s_c[0][w] + (uint32_t)__popcll(m0 & lt)] = b;
+    if (cls == 1) l.staged[s_base[1] + s_c[1][w] + (uint32_t)__popcll(m1 & lt)] = b;
+    if (cls == 3) l.mid[s_base[2] + s_c[2][w] + (uint32_t)__popcll(m3 & lt)] = b;
+    if (mc == 0) return;
+    const uint32_t my_r = s_base[3] + s_c[3][w] + (uint32_t)__popcll(mc & lt);
+    const uint32_t my_cb = s_base[4] + s_c[4][w] + cincl - C;
+    const uint32_t my_ib = s_base[5] + s_c[5][w] + iincl - ni;
     if (cls == 2) {
         l.cr_b[my_r] = b;
         l.cr_cb[my_r] = my_cb;
@@ -410,6 +435,10 @@ __global__ void __launch_bounds__(BLOCK) k_l2_classify(const uint32_t* __restric
 // Level 2, thin ranges (S <= t_small): one wave a range, its 1,024 counters in the wave's 4 KB of LDS:
 // count, exclusive scan (16 DPP wave scans, written out as the range's bucket starts), then rows in
 // order ranked by ds_add_rtn (stable) and stored at their places in the range's slice of perm.
+// A wave walks its ranges software-pipelined: the next range's records (when it has at most U rows)
+// are loaded while this one is scanned and written, and the range after that one's list entry and
+// starts before then -- each range is three dependent HBM round trips (list, starts, records), which
+// left the thin ranges of BASELINE cfg 3 (~96K ranges of ~60 messages) latency-bound.
 __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16_t* __restrict__ keys16,
                                                                    const uint32_t* __restrict__ idx, L2Lists l,
                                                                    uint32_t n, uint32_t n_act,
@@ -420,33 +449,36 @@ __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16
     const uint32_t lane = lane_id(), w = threadIdx.x / WAVE;
     uint32_t* cnt = s_cnt[w];
     const uint32_t m = l.ctr[0];
+    const uint32_t stride = gridDim.x * L2_SMALL_WAVES;
     constexpr uint32_t U = 4;
-    for (uint32_t i = blockIdx.x * L2_SMALL_WAVES + w; i < m; i += gridDim.x * L2_SMALL_WAVES) {
-        const uint32_t b = l.small[i];
-        const uint32_t base = l.rs[b], S = l.rs[b + 1] - base;
+    uint32_t i = blockIdx.x * L2_SMALL_WAVES + w;
+    if (i >= m) return;
+    // the pipeline: this range (b, base, S; its records in ck / cv when S <= U rows), the next (nb, nbase,
+    // nS), the one after (bb: its list entry only)
+    uint32_t b = l.small[i];
+    uint32_t base = l.rs[b], S = l.rs[b + 1] - base;
+    uint32_t nb = i + stride < m ? l.small[i + stride] : 0u;
+    uint32_t nbase = l.rs[nb], nS = l.rs[nb + 1] - nbase;
+    uint32_t ck[U], cv[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t j = u * WAVE + lane;
+        ck[u] = S <= U * WAVE && j < S ? (uint32_t)keys16[base + j] : NONE32;
+        cv[u] = S <= U * WAVE && j < S ? idx[base + j] : 0u;
+    }
+    for (; i < m; i += stride) {
         const uint32_t k0 = b << MSD_SHIFT;
         const uint32_t L = min(MSD_L, n_act + 1 - k0);
         const uint16_t* rk = keys16 + base;
         const uint32_t* ri = idx + base;
+        const bool reg = S <= U * WAVE;
 #pragma unroll
         for (uint32_t q = 0; q < MSD_L / (4 * WAVE); ++q) reinterpret_cast<uint4*>(cnt)[q * WAVE + lane] = make_uint4(0, 0, 0, 0);
-        // a range of at most U rows (the thin ranges of a sparse batch) is loaded once, keys and indices
-        // together, and ranked from registers: one memory round trip instead of two
-        const bool reg = S <= U * WAVE;
-        uint32_t rk0[U], rv0[U];
-        if (reg) {
-#pragma unroll
-            for (uint32_t u = 0; u < U; ++u) {
-                const uint32_t j = u * WAVE + lane;
-                rk0[u] = j < S ? (uint32_t)rk[j] : NONE32;
-                rv0[u] = j < S ? ri[j] : 0u;
-            }
-        }
         wave_lds_sync();
         if (reg) {
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u)
-                if (rk0[u] != NONE32) atomicAdd(&cnt[rk0[u]], 1u);
+                if (ck[u] != NONE32) atomicAdd(&cnt[ck[u]], 1u);
         }
         for (uint32_t i0 = 0; !reg && i0 < S; i0 += U * WAVE) {
             uint32_t k[U];
@@ -459,6 +491,17 @@ __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16
             for (uint32_t u = 0; u < U; ++u)
                 if (k[u] != NONE32) atomicAdd(&cnt[k[u]], 1u);
         }
+        // in flight during the scan and the ranking: the next range's records, the list entry after it
+        const bool has_next = i + stride < m;
+        const bool nreg = has_next && nS <= U * WAVE;
+        uint32_t nk[U], nv[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t j = u * WAVE + lane;
+            nk[u] = nreg && j < nS ? (uint32_t)keys16[nbase + j] : NONE32;
+            nv[u] = nreg && j < nS ? idx[nbase + j] : 0u;
+        }
+        const uint32_t bb = i + 2 * stride < m ? l.small[i + 2 * stride] : 0u;
         wave_lds_sync();
         uint32_t carry = 0;
 #pragma unroll
@@ -475,10 +518,10 @@ __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16
         if (reg) {
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
-                if (rk0[u] == NONE32) continue;
-                const uint32_t p = base + atomicAdd(&cnt[rk0[u]], 1u);
-                perm[p] = rv0[u];
-                if (rank_out) rank_out[rv0[u]] = p;
+                if (ck[u] == NONE32) continue;
+                const uint32_t p = base + atomicAdd(&cnt[ck[u]], 1u);
+                perm[p] = cv[u];
+                if (rank_out) rank_out[cv[u]] = p;
             }
         }
         for (uint32_t i0 = 0; !reg && i0 < S; i0 += U * WAVE) {
@@ -498,6 +541,18 @@ __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16
             }
         }
         wave_lds_sync();
+        // rotate: next -> this, the one after -> next (its starts loaded now)
+        b = nb;
+        base = nbase;
+        S = nS;
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            ck[u] = nk[u];
+            cv[u] = nv[u];
+        }
+        nb = bb;
+        nbase = l.rs[nb];
+        nS = l.rs[nb + 1] - nbase;
     }
 }
 

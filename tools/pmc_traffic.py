@@ -1,86 +1,94 @@
 #!/usr/bin/env python3
-"""HBM traffic per launch of the bench's dominant kernels from a pmc_summary.json (tools/pmc_summary.py),
-corrected as MI355X_MICROARCH.md §HBM prescribes, written to profiles/pmc_<kernel>.json for bench.py's
-roofline `traffic` field.
+"""HBM traffic and LDS conflict ratio per launch of every library kernel of one bench workload, from a
+pmc_summary.json (tools/pmc_summary.py) and the same command's rocprofv3 kernel_stats.csv, corrected as
+MI355X_MICROARCH.md §HBM prescribes; written to profiles/pmc_<workload>_<kernel>.json, where bench.py's
+roofline reads its `traffic` (load_pmc).
 
-    python tools/pmc_traffic.py PMC_SUMMARY.json SOURCE_TAG N_MESSAGES [KERNEL_STATS.csv]
+    python tools/pmc_traffic.py PMC_SUMMARY.json SOURCE_TAG WORKLOAD N_MESSAGES KERNEL_STATS.csv
+
+<kernel> is the library's launch name (the names of bench.py's `kernels`), not the template function:
+k_b2_hist / k_radix_hist16 are launched as k_radix_hist, k_b2_scatter as k_radix_scatter,
+k_msd_local_list<512, ...> as k_msd_local_mid and <1024, ...> as k_msd_local, k_route_m as k_route.
+Instantiations of one launch name are averaged weighted by their calls; instantiations with under a
+quarter of the busiest one's calls (variants the tuner timed and dropped) are left out.
 
 Counters: TCC_EA0_RDREQ[_32B]_sum x 64 B (32 B), TCC_EA0_WRREQ[_64B]_sum x 64 B (else 32 B), collected in
-separate passes.  gfx950: a wide coalesced streaming read is tallied at half its bytes, so streamed
-reads are doubled; k_route's random 32-B slot probes each move one 64-B request and are counted as
-issued, so only its 24-B/message key stream is added back at half.  Writes are counted as issued.
+separate passes.  gfx950 tallies a wide coalesced streaming read at half its bytes, so streamed reads
+are doubled; k_route's random 32-B slot probes each move one 64-B request and are counted as issued,
+so only its 24-B/message key stream is added back at half; k_fan_route (CSR and directory gathers) is
+reported as issued (a lower bound).  Writes are counted as issued.  LDS: SQ_LDS_BANK_CONFLICT (extra
+cycles) / SQ_LDS_IDX_ACTIVE (all LDS-array cycles).
 """
+import csv
 import json
+import os
 import sys
+
+RENAME = {"k_b2_hist": "k_radix_hist", "k_radix_hist16": "k_radix_hist", "k_radix_hist_multi": "k_radix_hist",
+          "k_b2_scatter": "k_radix_scatter",
+          "k_route_m": "k_route", "k_route_region": "k_route", "k_shard_gather": "k_shard_scatter",
+          "k_fill_u32": "k_fill", "k_fan_degree_tiles": "k_fan_degree"}
+GATHER = ("k_route", "k_fan_route")
+
+
+def launch_name(inst: str) -> str:
+    """gd::k_msd_local_list<512, 16> -> k_msd_local_mid; gd::k_b2_scatter<...> -> k_radix_scatter."""
+    s = inst.replace("void ", "").replace("gd::", "")
+    base = s.split("<")[0]
+    if base == "k_msd_local_list":
+        return "k_msd_local_mid" if s.split("<")[1].startswith("512") else "k_msd_local"
+    return RENAME.get(base, base)
+
+
+def short(name: str) -> str:
+    name = name.replace("void ", "").replace("gd::", "")
+    return name[: name.index("(")] if "(" in name else name
 
 
 def main():
     summ = json.load(open(sys.argv[1]))
-    tag, n = sys.argv[2], int(sys.argv[3])
+    src, workload, n = sys.argv[2], sys.argv[3], int(sys.argv[4])
     calls = {}
-    if len(sys.argv) > 4:                      # rocprof kernel_stats.csv: calls per instantiation
-        import csv
-        for r in csv.DictReader(open(sys.argv[4])):
-            nm = r["Name"].split("(")[0].replace("void ", "").replace("gd::", "")
-            calls[nm] = calls.get(nm, 0) + int(r["Calls"])
-    # the bucketing form the library kept (its first launches time both): the two-level form
-    # (k_b2_hist / k_b2_scatter / k_msd_local, gd_msd.h) or the LSD passes (k_radix_*)
-    msd_calls = sum(v for k, v in calls.items() if k.startswith("k_msd_local"))
-    lsd_calls = max([v for k, v in calls.items() if k.startswith("k_radix_scatter<") and ", true," in k] or [0])
-    msd = msd_calls > lsd_calls if calls else any(k.startswith("gd::k_msd_local") for k in summ)
-    lsd_fams = ("k_radix_scatter", "k_radix_hist", "k_radix_hist_multi", "k_radix_hist16")
-    msd_fams = {"k_b2_scatter": "k_radix_scatter", "k_b2_hist": "k_radix_hist", "k_msd_local": "k_msd_local"}
+    for r in csv.DictReader(open(sys.argv[5])):
+        nm = short(r["Name"])
+        calls[nm] = calls.get(nm, 0) + int(r["Calls"])
     fam = {}
     for name, row in summ.items():
-        base = name.split("<")[0].replace("gd::", "")
+        sn = short(name)
         if "rd_bytes_ea" not in row or "wr_bytes_ea" not in row:
             continue
-        if base in ("k_route_m", "k_route_hist"):
-            key = "k_route" if base == "k_route_m" else base
-        elif not msd and base in lsd_fams:
-            key = "k_radix_hist" if base.startswith("k_radix_hist") else base
-        elif msd and base in msd_fams:
-            key = msd_fams[base]
-        else:
-            continue
-        # the route's probe variants (index group reads / directory / index slot reads) are each timed on
-        # a few launches before the library keeps one: with the kernel-trace stats (4th argument) count
-        # the steady-state one only, the instantiation with the most calls
-        if key == "k_route" and calls:
-            mine = calls.get(name.replace("void ", "").replace("gd::", ""), 0)
-            if mine < max(v for k, v in calls.items() if k.startswith("k_route_m<")):
-                continue
-        # launches per cfg 2 step (3 LSD passes): the first pass's scatter (FIRST = true) and
-        # histogram (32-bit keys) once, the later passes' instantiations twice; the two-level form
-        # launches each of its kernels once
-        w = 1.0
-        if not msd and key == "k_radix_scatter" and ", false," in name:
-            w = 2.0
-        if not msd and base == "k_radix_hist16":
-            w = 2.0
-        fam.setdefault(key, []).append((name, row, w))
+        fam.setdefault(launch_name(sn), []).append((sn, row, calls.get(sn, 0)))
     out = {}
     for key, members in fam.items():
-        wsum = sum(w for _, _, w in members)
-        rd_raw = sum(r["rd_bytes_ea"] * w for _, r, w in members) / wsum
-        wr = sum(r["wr_bytes_ea"] * w for _, r, w in members) / wsum
-        if key == "k_route" or key == "k_route_hist":
+        top = max(c for _, _, c in members)
+        members = [m for m in members if m[2] * 4 >= top and m[2] > 0] or members
+        wsum = sum(max(c, 1) for _, _, c in members)
+        avg = lambda f: sum(f(r) * max(c, 1) for _, r, c in members) / wsum  # noqa: E731
+        rd_raw, wr = avg(lambda r: r["rd_bytes_ea"]), avg(lambda r: r["wr_bytes_ea"])
+        if key == "k_route":
             rd = rd_raw + 24 * n / 2
             how = "random slot probes as issued (64-B requests) + the 24-B/message key stream added back at half"
+        elif key in GATHER:
+            rd = rd_raw
+            how = "reads as issued (gathers; a lower bound)"
         else:
             rd = 2 * rd_raw
             how = "streamed reads doubled (gfx950 tallies a wide coalesced read at half its bytes)"
-        out[key] = {"kernel": key, "instantiations": [m for m, _, _ in members],
+        lds = None
+        if all("SQ_LDS_IDX_ACTIVE" in r and "SQ_LDS_BANK_CONFLICT" in r for _, r, _ in members):
+            act = avg(lambda r: r["SQ_LDS_IDX_ACTIVE"])
+            lds = round(avg(lambda r: r["SQ_LDS_BANK_CONFLICT"]) / act, 4) if act else None
+        out[key] = {"kernel": key, "workload": workload, "instantiations": [m for m, _, _ in members],
+                    "calls": [c for _, _, c in members],
                     "hbm_bytes_per_launch": rd + wr, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
-                    "raw_read_bytes_per_launch": rd_raw, "source": tag,
+                    "raw_read_bytes_per_launch": rd_raw, "lds_conflict_ratio": lds, "source": src,
                     "method": "EA request counts x request size, separate --pmc passes; " + how +
-                              "; averaged over the instantiations weighted by their launches per cfg 2 step "
-                              "(LSD: first radix pass once, later passes twice; two-level form: once each)",
-                    "bucketing_form": "msd" if msd else "lsd"}
-    for key, v in out.items():
-        with open(f"profiles/pmc_{key}.json", "w") as f:
+                              "; instantiations averaged weighted by calls"}
+    os.makedirs("profiles", exist_ok=True)
+    for key, v in sorted(out.items()):
+        with open(f"profiles/pmc_{workload}_{key}.json", "w") as f:
             json.dump(v, f, indent=1)
-        print(key, round(v["hbm_bytes_per_launch"] / 1e6, 1), "MB/launch")
+        print(f"{key:24s} {v['hbm_bytes_per_launch'] / 1e6:10.2f} MB/launch  lds_conflicts {v['lds_conflict_ratio']}")
 
 
 if __name__ == "__main__":
