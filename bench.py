@@ -948,7 +948,8 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     HBM.  N = 1: fused expand+route kernel (k_fan_route) per hop.  N > 1: directory sharded by ring
     owner, (target, sender) pairs exchanged with one grouped RCCL send/recv round per hop inside the
     library (gd_fanout_multi_device, LibraryFanout)."""
-    from orleans_amd.fanout import CHIRPER_ACCOUNT_CLASS, DeviceFanoutEngine, FanoutCascade, LibraryFanout, upload_graph
+    from orleans_amd.fanout import (CHIRPER_ACCOUNT_CLASS, DeviceFanoutEngine, FanoutCascade, LibraryFanout,
+                                    partition_graph_np, upload_graph)
     from orleans_amd.workloads import power_law_graph
 
     t_setup = time.perf_counter()
@@ -965,10 +966,23 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     pts, own = e.ring_set_silos(args.mode, SILO_SETS[args.silos])
     owner = e.ring_owner(keys)
     mine = np.nonzero(owner % world == rank)[0]
-    e.register(keys[mine], mine.astype(np.uint32), owner[mine])
+    # N > 1: the follower graph is partitioned (gd_fanout_multi_part_device): this rank keeps the rows
+    # of the grains it owns, row i = activation i (ascending node ids); N = 1: node u = activation u
+    e.register(keys[mine], (np.arange(mine.size) if world > 1 else mine).astype(np.uint32), owner[mine])
     del keys
     eng = DeviceFanoutEngine(e, dev, tc, keep_target=not args.no_target)
-    graph = upload_graph(ro, dst, dev)
+    node_of = None
+    n_act = n
+    if world > 1:
+        ro_l, dst_l, no = partition_graph_np(ro, dst, mine)
+        graph = upload_graph(ro_l, dst_l, dev)
+        node_of = torch.from_numpy(no.view(np.int32) if no.size else np.zeros(1, np.int32)).to(dev)
+        n_act = int(mine.size)
+        graph_edges_rank = int(dst_l.size)
+        del ro_l, dst_l, no
+    else:
+        graph = upload_graph(ro, dst, dev)
+        graph_edges_rank = int(dst.size)
     seeds = np.random.default_rng(0x5EED0004).choice(n, size=args.seeds, replace=False).astype(np.uint32)
     t_seeds = torch.from_numpy(seeds.view(np.int32)).to(dev)
     torch.cuda.synchronize()
@@ -976,9 +990,9 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     # N > 1: the sharded cascade inside the library (gd_fanout_multi_device), bit-exact against
     # oracle/fanout.py in tests/test_gpu_fanout_multi.py (W = 8 and 3 in process)
     assert not (world > 1 and args.rehearse_one_gpu), "cfg4 at N > 1 runs the library's RCCL cascade only"
-    runner = FanoutCascade(eng, graph, n) if world == 1 else LibraryFanout(eng, graph, n)
-    exchange = "none" if world == 1 else ("libgraindispatch gd_fanout_multi_device (grouped RCCL send/recv of "
-                                          "(target, sender) per hop)")
+    runner = FanoutCascade(eng, graph, n) if world == 1 else LibraryFanout(eng, graph, n_act, node_of=node_of)
+    exchange = "none" if world == 1 else ("libgraindispatch gd_fanout_multi_part_device (partitioned follower "
+                                          "graph; grouped RCCL send/recv of (target, sender) per hop)")
 
     def step():
         return runner.run(t_seeds, args.hops)
@@ -1030,11 +1044,12 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
             if name in ("k_fan_route", "k_route_nodes", "k_fan_expand"):
                 return fan_kernel_bytes(name, msgs_step, sum(hop_front), not args.no_target)
             # the bucketing kernels: each hop's batch in the form the library keeps for its shape
-            return float(sum(bucket_bytes(hop_form(e, m, n), m, n, a).get(name, 0.0)
+            return float(sum(bucket_bytes(hop_form(e, m, n_act), m, n_act, a).get(name, 0.0)
                              for m, a in zip(hop_msgs, hop_acts) if m))
-        kernels, roofline = roofline_of(kt, profile_steps, msgs_step, n, None, "cfg4", world, bytes_fn=cfg4_bytes)
+        kernels, roofline = roofline_of(kt, profile_steps, msgs_step, n_act, None, "cfg4", world,
+                                        bytes_fn=cfg4_bytes)
         if roofline:
-            roofline["hop_bucket_forms"] = [hop_form(e, m, n) for m in hop_msgs]
+            roofline["hop_bucket_forms"] = [hop_form(e, m, n_act) for m in hop_msgs]
 
     cpu = None
     if rank == 0 and world == 1 and with_cpu and getattr(hops[-1], "target", None) is not None:
@@ -1055,6 +1070,7 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
             "comm": e.comm_info(),
             "messages_per_step": int(msgs_total / steps), "hop_messages_rank0": hop_msgs,
             "hop_publishers_rank0": hop_front, "setup_s": round(setup_s, 1), "exchange": exchange,
+            "graph_edges_rank0": graph_edges_rank, "graph_edges_total": int(dst.size),
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
         }
     e.close()

@@ -592,6 +592,18 @@ typedef struct gd_fanout_hop {
 int gd_fanout_multi_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_nodes,
                            const uint32_t* d_seeds, uint32_t n_seeds, int32_t type_code, uint32_t n_act,
                            uint32_t hops, gd_fanout_hop* out);
+/* The same cascade over a partitioned follower graph: each rank holds only the
+ * follower lists of the grains it owns -- the publishers a rank expands are always its own activations
+ * (a chirp is enqueued on its follower's activation, on the follower's directory owner, which then
+ * publishes; ChirperAccount.cs:131-134) -- so per-rank graph memory is ~1/n_ranks.  Row i of this
+ * rank's CSR (d_row_off[n_rows + 1], d_dst = follower node ids) is local activation i, whose node is
+ * d_node_of[i]; the directory must map each owned node to its row (act = i), with rows in ascending
+ * node order so that publishers run in the replicated form's order (the hops are then bit-identical
+ * to gd_fanout_multi_device's).  Every seed needs a live activation on its owner (else GD_EINVAL).
+ * n_act = n_rows: buckets and offsets are over local rows; frontier, target and sender are node ids. */
+int gd_fanout_multi_part_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_rows,
+                                const uint32_t* d_node_of, const uint32_t* d_seeds, uint32_t n_seeds,
+                                int32_t type_code, uint32_t hops, gd_fanout_hop* out);
 /* Host graph and seeds (uploaded per call); returns with the cascade done. */
 int gd_fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint32_t n_nodes,
                     const uint32_t* seeds, uint32_t n_seeds, int32_t type_code, uint32_t n_act, uint32_t hops,
@@ -858,8 +870,8 @@ int gd_set_kernel_timing(gd_handle* h, int enable);
                                    wherever it applies (batches >= 2^20 messages, n_act < 2^28) */
 #define GD_OPT_L2_SMALL     3   /* two-level three-pass form: ranges of at most this many messages are
                                    sorted one wave a range (default 1024) */
-#define GD_OPT_STABLE_RANK  4   /* LSD passes' in-tile rank: 1 ds_add_rtn (default when the creation
-                                   self-check passed), 0 ballots (stable by construction) */
+#define GD_OPT_STABLE_RANK  4   /* LSD passes' in-tile rank: 1 ds_add_rtn (default; gd_create verifies the
+                                   lane order it relies on and refuses a device without it), 0 ballots */
 #define GD_OPT_WIRE_HEADERS 5   /* exchange headers of one-type long-key batches: 0 24-B keys, 1 u64
                                    N1s, 2 u32 N1s when every N1 < 2^32 (default) */
 #define GD_OPT_REGION_PROBE 6   /* exchange: (rank, region) partition + region-mapped owner probe: 0 (default) / 1 */

@@ -1375,6 +1375,29 @@ const char* gd_last_error(const gd_handle* h) {
     return g_tls_error.c_str();
 }
 
+// The stable ranks' hardware assumption (gd_msd.h k_lane_order_check): refuse the handle on a device
+// that does not serve one wave's same-address LDS atomics in lane order -- every bucketing would be
+// silently unstable there.
+static int lane_order_check(gd_handle* h) {
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, 256 * 4) != hipSuccess) return set_err(nullptr, GD_ENOMEM, "lane-order check buffer");
+    uint32_t hbad[256] = {};
+    hipLaunchKernelGGL(k_lane_order_check, dim3(1), dim3(256), 0, h->stream, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(hbad, d, sizeof(hbad), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return set_err(nullptr, GD_EHIP, "lane-order check: %s", hipGetErrorString(e));
+    uint64_t bad = 0;
+    for (uint32_t x : hbad) bad += x;
+    if (bad)
+        return set_err(nullptr, GD_EHIP,
+                       "this device does not serve same-address LDS atomics in lane order (%llu mismatches): "
+                       "the library's stable ranks would be wrong here",
+                       (unsigned long long)bad);
+    return GD_OK;
+}
+
 int gd_create(const gd_config* cfg, gd_handle** out) {
     if (!cfg || !out) return set_err(nullptr, GD_EINVAL, "gd_create: null argument");
     if (cfg->struct_size != sizeof(gd_config)) return set_err(nullptr, GD_EINVAL, "gd_create: struct_size mismatch");
@@ -1416,6 +1439,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
         (void)mb;  // scratch grows on demand; nothing pre-sized beyond the table
         r = sync(h);
     }
+    if (r == GD_OK) r = lane_order_check(h);
     if (r != GD_OK) {
         gd_destroy(h);
         return r;
@@ -2764,7 +2788,8 @@ int gd_fanout_expand_device(gd_handle* h, const uint32_t* d_row_off, const uint3
         return set_err(h, GD_EINVAL, "fan-out emits %llu messages, output holds %llu", (unsigned long long)total,
                        (unsigned long long)capacity);
     return launch(h, "k_fan_expand", dim3(blocks_for(total, FAN_TILE)), dim3(BLOCK), 0, k_fan_expand, d_row_off, d_dst,
-                  d_frontier, n_frontier, (const uint32_t*)h->fan[0].p, (uint32_t)total, d_target, d_sender);
+                  d_frontier, n_frontier, (const uint32_t*)h->fan[0].p, (uint32_t)total, d_target, d_sender,
+                  (const uint32_t*)nullptr);
 }
 
 int gd_fanout_route_bucket_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_nodes,
@@ -4012,8 +4037,13 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
                         (by_region && b == 19) || (any16 && b >= 20)))
             GD_TRY(grow(h, B[b], want[b]));
     if (has_ext) GD_TRY(grow(h, SB[5], (size_t)sboff[W] + 16));
-    gd_key* recv_keys = (gd_key*)B[0].p;
-    uint32_t* recv_idx = (uint32_t*)B[1].p;
+    // World 1 (the self-chunk skip): the one chunk is this rank's own, so the probe reads the send
+    // buffers in place -- no header round, no copy of the headers and origin indices -- and those
+    // buffers stay busy until this batch's probe and bucketing are done (x_sent below)
+    const bool alias = W == 1 && !has_ext && !any16 && !by_region && !ret && !fwd;
+    gd_key* recv_keys = alias && !any_compact ? send_keys : (gd_key*)B[0].p;
+    uint32_t* recv_idx = alias ? send_idx : (uint32_t*)B[1].p;
+    void* hdr = alias ? (void*)send_keys : (any_compact ? B[18].p : (void*)recv_keys);   // headers as received
     uint32_t* recv_src = (uint32_t*)B[2].p;
     uint32_t* silo = (uint32_t*)B[3].p;
     uint32_t* act = (uint32_t*)B[4].p;
@@ -4031,12 +4061,12 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         // keys, origin indices, KeyExt lengths, the block starts of 2-B origin indices
         Lane lanes[4];
         int nl = 0;
-        lanes[nl++] = {send_keys, any_compact ? B[18].p : (void*)recv_keys, 1, ncclUint8, 1, hsb.data(), hrb.data()};
+        lanes[nl++] = {send_keys, hdr, 1, ncclUint8, 1, hsb.data(), hrb.data()};
         lanes[nl++] = {send_idx, any16 ? B[20].p : (void*)recv_idx, 4, ncclUint32, 1, idx16 ? isb.data() : nullptr,
                        any16 ? irb.data() : nullptr, any16 ? irs.data() : nullptr};
         if (has_ext) lanes[nl++] = {send_len, B[14].p, 4, ncclInt32, 1};
         if (idx16 || any16) lanes[nl++] = {SB[6].p, B[21].p, 4, ncclUint32, 1, psb.data(), prb.data(), prs.data()};
-        GD_TRY(exchange_round(h, "rccl_headers", sc.data(), soff.data(), rc.data(), roff.data(), lanes, nl));
+        if (!alias) GD_TRY(exchange_round(h, "rccl_headers", sc.data(), soff.data(), rc.data(), roff.data(), lanes, nl));
         if (has_ext) {                 // the KeyExt strings, then their offsets in the receive blob
             const Lane bl[1] = {{SB[5].p, B[15].p, 1, ncclUint8, 1}};
             GD_TRY(exchange_round(h, "rccl_keyext", sbc.data(), sboff.data(), rbc.data(), rboff.data(), bl, 1));
@@ -4048,7 +4078,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         }
         if (any_compact && !n1_path)
             GD_TRY(launch(h, "k_recv_expand", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_expand,
-                          (const uint8_t*)B[18].p, (const uint32_t*)(dcnt + W), (const uint32_t*)(kdesc + 4),
+                          (const uint8_t*)hdr, (const uint32_t*)(dcnt + W), (const uint32_t*)(kdesc + 4),
                           (uint32_t)W, m, recv_keys, recv_src));
         else if (!any16 && !src_in_probe)
             GD_TRY(launch(h, "k_recv_src", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_src,
@@ -4076,11 +4106,11 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         HIP_TRY(h, hipEventRecord(h->x_hdr[s], h->xstream));
         if (n1_path && keep_keys) {    // the 24-B keys for the result, beside the probe
             GD_TRY(launch(h, "k_recv_expand", dim3(blocks_for(m, BLOCK)), dim3(BLOCK), 0, k_recv_expand,
-                          (const uint8_t*)B[18].p, (const uint32_t*)(dcnt + W), (const uint32_t*)(kdesc + 4),
+                          (const uint8_t*)hdr, (const uint32_t*)(dcnt + W), (const uint32_t*)(kdesc + 4),
                           (uint32_t)W, m, recv_keys, src_in_probe ? nullptr : recv_src));
             HIP_TRY(h, hipEventRecord(h->x_keys[s], h->xstream));
         }
-        if (!ret) {                    // this parity's send buffers are free for batch i+2's partition
+        if (!ret && !alias) {          // this parity's send buffers are free for batch i+2's partition
             HIP_TRY(h, hipEventRecord(h->x_sent[s], h->xstream));
             h->x_sent_rec[s] = true;
         }
@@ -4091,7 +4121,7 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         GD_TRY(route_region_device(h, n1_path ? B[18].p : (const void*)recv_keys, n1_path ? header_bytes(n1_mode) : 0u,
                                    n1_tcd, m, (const uint32_t*)B[19].p, (uint32_t)W, silo, act, st));
     else if (n1_path)
-        GD_TRY(route_n1_device(h, B[18].p, header_bytes(n1_mode), n1_tcd, m, silo, act, st,
+        GD_TRY(route_n1_device(h, hdr, header_bytes(n1_mode), n1_tcd, m, silo, act, st,
                                src_in_probe ? (const uint32_t*)(dcnt + W) : nullptr, (uint32_t)W,
                                src_in_probe ? recv_src : nullptr));
     else if (m) GD_TRY(route_device(h, recv_keys, m, silo, act, st, !has_ext));
@@ -4140,6 +4170,10 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         GD_TRY(forward_multi(h, s, n_act, r, n1_path && n1_mode == 2 ? (const uint32_t*)B[18].p : nullptr, n1_tcd));
     HIP_TRY(h, hipEventRecord(h->x_done[s], h->stream));
     h->x_done_rec[s] = true;
+    if (alias) {                       // the probe read the send buffers: free once it is done
+        HIP_TRY(h, hipEventRecord(h->x_sent[s], h->stream));
+        h->x_sent_rec[s] = true;
+    }
     h->mres[s] = r;
     h->mres_n[s] = n;
     h->mcalls += 1;
@@ -4414,8 +4448,12 @@ int counts_round(gd_handle* h, uint32_t* dcnt, std::vector<uint32_t>& sc, std::v
     return GD_OK;
 }
 
+// node_of == nullptr: the replicated graph (rows = node ids = activation indices, n_nodes rows).
+// node_of != nullptr: this rank's partition of the graph -- row i = local activation i, whose node
+// is node_of[i] (n_nodes = n_act rows); publishers are rows, messages still carry node ids.
 int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint32_t n_nodes, const uint32_t* seeds,
-                 uint32_t n_seeds, int32_t type_code, uint32_t n_act, uint32_t hops, gd_fanout_hop* out) {
+                 uint32_t n_seeds, int32_t type_code, uint32_t n_act, uint32_t hops, gd_fanout_hop* out,
+                 const uint32_t* node_of = nullptr) {
     GD_TRY(need_comm(h));
     GD_TRY(check_ring(h));
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
@@ -4446,9 +4484,31 @@ int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uin
         for (int r = 0; r < h->rank; ++r) lo += hc[r];
         nf = hc[h->rank];
         GD_TRY(ensure(h, H0[0], ((size_t)std::max(nf, n_act) + 4) * 4));
-        if (nf) {
+        if (nf && !node_of) {
             HIP_TRY(h, hipMemcpyAsync(H0[0].p, (const uint32_t*)S[0].p + lo, (size_t)nf * 4, hipMemcpyDeviceToDevice,
                                       h->stream));
+            GD_TRY(launch(h, "k_mark_visited", dim3(blocks_for(nf, BLOCK)), dim3(BLOCK), 0, k_mark_visited,
+                          (const uint32_t*)H0[0].p, nf, n_act, visited));
+        } else if (nf) {
+            // partitioned: the owned seeds' nodes (the hop's frontier as reported), their rows by the
+            // directory probe (every seed must have a live activation on its owner)
+            GD_TRY(ensure(h, H0[9], ((size_t)std::max(nf, n_act) + 4) * 4));
+            GD_TRY(ensure(h, S[2], (size_t)nf * 4 + 16));
+            GD_TRY(ensure(h, S[3], (size_t)nf * 5 + 16));
+            uint32_t* nodes = (uint32_t*)H0[9].p;
+            HIP_TRY(h, hipMemcpyAsync(nodes, (const uint32_t*)S[0].p + lo, (size_t)nf * 4, hipMemcpyDeviceToDevice,
+                                      h->stream));
+            uint32_t* acts = (uint32_t*)S[2].p;
+            uint8_t* sts = (uint8_t*)S[3].p + (size_t)nf * 4;
+            GD_TRY(route_nodes(h, nodes, nf, tcd, (uint32_t*)S[3].p, acts, sts));
+            HIP_TRY(h, hipMemsetAsync(dcnt + 2 * W, 0, 4, h->stream));
+            GD_TRY(launch(h, "k_seed_rows", dim3(blocks_for(nf, BLOCK)), dim3(BLOCK), 0, k_seed_rows, (const uint32_t*)acts,
+                          (const uint8_t*)sts, nf, n_act, (uint32_t*)H0[0].p, dcnt + 2 * W));
+            HIP_TRY(h, hipMemcpyAsync(hc, dcnt + 2 * W, 4, hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(h, hipStreamSynchronize(h->stream));
+            if (hc[0])
+                return set_err(h, GD_EINVAL, "%u seeds have no live activation on their owner (a partitioned "
+                               "graph's rows are activations)", hc[0]);
             GD_TRY(launch(h, "k_mark_visited", dim3(blocks_for(nf, BLOCK)), dim3(BLOCK), 0, k_mark_visited,
                           (const uint32_t*)H0[0].p, nf, n_act, visited));
         }
@@ -4459,6 +4519,15 @@ int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uin
         gd_fanout_hop& res = h->fm_res[hp];
         res.n_frontier = nf;
         res.frontier = frontier;
+        if (node_of) {                 // reported as nodes: hop 0's seeds are there already
+            if (hp > 0) {
+                GD_TRY(ensure(h, H[9], ((size_t)n_act + 4) * 4));
+                if (nf)
+                    GD_TRY(launch(h, "k_gather_u32", dim3(blocks_for(nf, BLOCK)), dim3(BLOCK), 0, k_gather_u32, frontier,
+                                  nf, node_of, (uint32_t*)H[9].p));
+            }
+            res.frontier = (const uint32_t*)H[9].p;
+        }
         // 1. expand this rank's publishers (follower lists in enumeration order)
         uint64_t total = 0;
         GD_TRY(fan_count(h, row_off, n_nodes, frontier, nf, &total));
@@ -4470,7 +4539,8 @@ int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uin
         GD_TRY(ensure(h, S[3], (size_t)n * 4 + 16));
         if (n)
             GD_TRY(launch(h, "k_fan_expand", dim3(blocks_for(n, FAN_TILE)), dim3(BLOCK), 0, k_fan_expand, row_off,
-                          dst, frontier, nf, (const uint32_t*)h->fan[0].p, n, (uint32_t*)S[0].p, (uint32_t*)S[1].p));
+                          dst, frontier, nf, (const uint32_t*)h->fan[0].p, n, (uint32_t*)S[0].p, (uint32_t*)S[1].p,
+                          node_of));
         // 2. stable partition of (target, sender) by the target's owner rank
         GD_TRY(shard_pack<true>(h, S[0].p, (const uint32_t*)S[1].p, n, tcd, (uint32_t)W, S[2].p, (uint32_t*)S[3].p,
                                 dcnt));
@@ -4540,6 +4610,19 @@ int gd_fanout_multi_device(gd_handle* h, const uint32_t* d_row_off, const uint32
     if (hops == 0 || hops > 64) return set_err(h, GD_EINVAL, "hops %u not in [1, 64]", hops);
     HIP_TRY(h, hipSetDevice(h->device));
     return fanout_multi(h, d_row_off, d_dst, n_nodes, d_seeds, n_seeds, type_code, n_act, hops, out);
+}
+
+int gd_fanout_multi_part_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_rows,
+                                const uint32_t* d_node_of, const uint32_t* d_seeds, uint32_t n_seeds,
+                                int32_t type_code, uint32_t hops, gd_fanout_hop* out) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (n_seeds && !d_seeds) return set_err(h, GD_EINVAL, "null seeds");
+    if (!d_row_off || (n_rows && (!d_dst || !d_node_of))) return set_err(h, GD_EINVAL, "null graph");
+    if (hops == 0 || hops > 64) return set_err(h, GD_EINVAL, "hops %u not in [1, 64]", hops);
+    HIP_TRY(h, hipSetDevice(h->device));
+    // an empty partition still needs a non-null node_of to select the partitioned form
+    return fanout_multi(h, d_row_off, d_dst, n_rows, d_seeds, n_seeds, type_code, n_rows, hops, out,
+                        d_node_of ? d_node_of : d_row_off);
 }
 
 int gd_fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint32_t n_nodes,

@@ -146,12 +146,15 @@ __device__ __forceinline__ void fan_item(const FanStage& s, const uint32_t* __re
 
 // Expansion only: (target, sender) per message -- the multi-GPU path ships these 8 B to the
 // owner instead of a 28-B header.
+// node_of (partitioned graphs, gd_fanout_multi_part_device): the frontier holds this rank's local rows
+// (activation indices); the sender written is the row's node.
 __global__ void __launch_bounds__(BLOCK) k_fan_expand(const uint32_t* __restrict__ row_off,
                                                       const uint32_t* __restrict__ dst,
                                                       const uint32_t* __restrict__ frontier, uint32_t n_front,
                                                       const uint32_t* __restrict__ ends, uint32_t total,
                                                       uint32_t* __restrict__ out_target,
-                                                      uint32_t* __restrict__ out_sender) {
+                                                      uint32_t* __restrict__ out_sender,
+                                                      const uint32_t* __restrict__ node_of) {
     __shared__ FanStage s;
     const uint32_t p0 = blockIdx.x * FAN_TILE;
     const uint32_t p1 = min(p0 + FAN_TILE, total);
@@ -162,7 +165,7 @@ __global__ void __launch_bounds__(BLOCK) k_fan_expand(const uint32_t* __restrict
         uint32_t j, sender;
         fan_item(s, row_off, frontier, n_front, ends, p, j, sender);
         out_target[p] = dst[j];
-        out_sender[p] = sender;
+        out_sender[p] = node_of ? node_of[sender] : sender;
     }
 }
 
@@ -438,6 +441,25 @@ __global__ void __launch_bounds__(BLOCK) k_frontier_compact(const uint16_t* __re
     for (uint32_t k = 0; k < FR_ITEMS; ++k)
         if ((m >> k) & 1u) out[pos++] = a0 + k;
     if (blockIdx.x + 1 == nb && threadIdx.x == BLOCK - 1) *total = pos;
+}
+
+// Partitioned graphs: this rank's seeds (node ids, routed on their owner) become local rows = their
+// activation indices; a seed without a live activation here counts in *bad (the host refuses the call).
+__global__ void __launch_bounds__(BLOCK) k_seed_rows(const uint32_t* __restrict__ act,
+                                                     const uint8_t* __restrict__ status, uint32_t n, uint32_t n_act,
+                                                     uint32_t* __restrict__ rows, uint32_t* __restrict__ bad) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const bool ok = status[i] == GD_ROUTE_OK && act[i] < n_act;
+    rows[i] = ok ? act[i] : 0u;
+    if (!ok) atomicAdd(bad, 1u);
+}
+
+// out[i] = table[in[i]] (a partitioned cascade's frontier rows -> their nodes).
+__global__ void __launch_bounds__(BLOCK) k_gather_u32(const uint32_t* __restrict__ in, uint32_t n,
+                                                      const uint32_t* __restrict__ table, uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n) out[i] = table[in[i]];
 }
 
 // The seeds of a cascade have published: visited[u] = 1 for u < n_act (gd_fanout_multi_device).

@@ -269,6 +269,47 @@ __device__ __forceinline__ void msd_range(MsdShared<NT, RW>& sh, uint32_t b, uin
     __syncthreads();
 }
 
+// The hardware property every stable rank of this library rests on (the LSD and MSD scatters, the
+// range sorts, the level-2 and micro-batch ranks): the lanes of one wave's LDS ds_add_rtn to one
+// address are served in ascending lane order, so each lane's returned value is the sum of the
+// increments of the lower active lanes with the same address.  The ISA does not document the order;
+// tools/ubench_lds_order.hip observed it on gfx950 and gd_create checks it here on the device it runs on
+// (patterns: one address, u16-pair increments, pseudo-random colliding addresses, partial EXEC),
+// refusing the handle when it fails.  One workgroup of 256 threads, 64 rounds; out[t] = thread t's
+// mismatches (vector stores, summed by the host).
+__global__ void __launch_bounds__(256) k_lane_order_check(uint32_t* __restrict__ out) {
+    __shared__ uint32_t s_w[4][16];
+    const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    uint32_t bad = 0;
+    for (uint32_t round = 0; round < 64; ++round) {
+        if (lane < 16) s_w[w][lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        uint32_t x = (lane + 1) * 0x9E3779B1u ^ (round * 0x85EBCA6Bu) ^ (w * 0xC2B2AE35u);
+        x ^= x >> 15;
+        x *= 0x2C1B3C6Du;
+        x ^= x >> 12;
+        const uint32_t mode = round & 3u;
+        const uint32_t addr = mode == 0 ? 0u : (mode == 1 ? (lane % 3u) : (x & (mode == 2 ? 7u : 15u)));
+        const uint32_t inc = mode == 1 ? (1u << (16 * (lane & 1))) : (mode == 3 ? (x >> 28) + 1u : 1u);
+        const bool active = mode != 3 || ((x >> 8) & 3u) != 0;      // partial EXEC in mode 3
+        uint32_t got = 0;
+        if (active) got = atomicAdd(&s_w[w][addr], inc);
+        // expected: the increments of the lower active lanes on the same address
+        uint32_t want = 0;
+        for (uint32_t j = 0; j < WAVE; ++j) {
+            const uint32_t aj = (uint32_t)__builtin_amdgcn_readlane((int)addr, (int)j);
+            const uint32_t ij = (uint32_t)__builtin_amdgcn_readlane((int)inc, (int)j);
+            const uint32_t vj = (uint32_t)__builtin_amdgcn_readlane((int)(active ? 1u : 0u), (int)j);
+            if (j < lane && vj && aj == addr) want += ij;
+        }
+        if (active && got != want) ++bad;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    out[threadIdx.x] = bad;
+}
+
 // One-pass form: range b = blockIdx.x; its first output position is the digit totals before it.
 __global__ void __launch_bounds__(MSD_NT, 4) k_msd_local(const uint16_t* __restrict__ keys16,
                                                          const uint32_t* __restrict__ idx,

@@ -13,7 +13,9 @@ activation index in the directory is u (the bench registers it so).
 * `FanoutCascade` -- one GPU: per hop one fused expand+route call
   (gd_fanout_route_bucket_device), the activation bucketing, and gd_frontier_next_device.
 * `LibraryFanout` -- N GPUs, the whole sharded cascade inside libgraindispatch
-  (gd_fanout_multi_device over the library's RCCL communicator): the path a C# host drives.
+  (gd_fanout_multi_device over the library's RCCL communicator): the path a C# host drives; with
+  `node_of`, over a partitioned follower graph (gd_fanout_multi_part_device: each rank holds the
+  follower lists of the grains it owns, ~1/N of the edges; partition_graph_np / _torch build it).
   (Round 4 removed the torch.distributed form of the same cascade, which duplicated it.)
 """
 from __future__ import annotations
@@ -39,6 +41,33 @@ class FollowerGraph:
     @property
     def edges(self) -> int:
         return int(self.dst.shape[0])
+
+
+def partition_graph_np(row_off: np.ndarray, dst: np.ndarray, nodes: np.ndarray):
+    """This rank's part of a follower graph for gd_fanout_multi_part_device: the rows of `nodes`
+    (ascending node ids, the grains this rank owns) as a local CSR (row i = local activation i) and
+    node_of[i] = nodes[i]."""
+    nodes = np.asarray(nodes, dtype=np.int64)
+    ro = np.asarray(row_off, dtype=np.int64)
+    deg = ro[nodes + 1] - ro[nodes]
+    ro_l = np.zeros(nodes.size + 1, np.int64)
+    np.cumsum(deg, out=ro_l[1:])
+    idx = np.repeat(ro[nodes] - ro_l[:-1], deg) + np.arange(int(ro_l[-1]), dtype=np.int64)
+    return ro_l.astype(np.uint32), np.asarray(dst, dtype=np.uint32)[idx], nodes.astype(np.uint32)
+
+
+def partition_graph_torch(row_off: torch.Tensor, dst: torch.Tensor, nodes: torch.Tensor):
+    """partition_graph_np on the device (int64 row offsets, int32 node ids): (row_off_local int32 bit
+    pattern, dst_local int32, node_of int32)."""
+    nodes = nodes.long()
+    ro = row_off.long()
+    deg = ro[nodes + 1] - ro[nodes]
+    ro_l = torch.zeros(nodes.numel() + 1, dtype=torch.int64, device=nodes.device)
+    torch.cumsum(deg, 0, out=ro_l[1:])
+    total = int(ro_l[-1].item())
+    idx = torch.repeat_interleave(ro[nodes] - ro_l[:-1], deg, output_size=total)
+    idx += torch.arange(total, dtype=torch.int64, device=nodes.device)
+    return ro_l.to(torch.int32), dst[idx].contiguous(), nodes.to(torch.int32)
 
 
 def upload_graph(row_off: np.ndarray, dst: np.ndarray, device) -> FollowerGraph:
@@ -201,8 +230,10 @@ class LibraryFanout:
     RCCL unique id to the other ranks."""
 
     def __init__(self, engine: DeviceFanoutEngine, graph: FollowerGraph, n_act: int,
-                 group: Optional[dist.ProcessGroup] = None):
-        self.engine, self.graph, self.n_act = engine, graph, n_act
+                 group: Optional[dist.ProcessGroup] = None, node_of: Optional[torch.Tensor] = None):
+        """node_of: `graph` is this rank's partition (partition_graph_*: row i = local activation i,
+        node node_of[i], n_act = its rows) -- gd_fanout_multi_part_device; None: the replicated graph."""
+        self.engine, self.graph, self.n_act, self.node_of = engine, graph, n_act, node_of
         world, rank = dist.get_world_size(group), dist.get_rank(group)
         uid = torch.zeros(g.GD_COMM_ID_BYTES, dtype=torch.uint8)
         if rank == 0:
@@ -214,9 +245,14 @@ class LibraryFanout:
     def run(self, seeds: torch.Tensor, hops: int) -> List[LibraryHop]:
         ns = int(seeds.shape[0])
         with self.engine.context():
-            raw = self.engine.gd.fanout_multi_device(self.graph.row_off.data_ptr(), self.graph.dst.data_ptr(),
-                                                     self.graph.n_nodes, seeds.data_ptr() if ns else 0, ns,
-                                                     self.engine.type_code, self.n_act, hops)
+            if self.node_of is not None:
+                raw = self.engine.gd.fanout_multi_part_device(
+                    self.graph.row_off.data_ptr(), self.graph.dst.data_ptr(), self.graph.n_nodes,
+                    self.node_of.data_ptr(), seeds.data_ptr() if ns else 0, ns, self.engine.type_code, hops)
+            else:
+                raw = self.engine.gd.fanout_multi_device(self.graph.row_off.data_ptr(), self.graph.dst.data_ptr(),
+                                                         self.graph.n_nodes, seeds.data_ptr() if ns else 0, ns,
+                                                         self.engine.type_code, self.n_act, hops)
         return [LibraryHop(r) for r in raw]
 
     def fetch(self, hops: List[LibraryHop]) -> List[dict]:

@@ -83,3 +83,31 @@ def test_cascade_small_by_hand():
     assert (hops[1]["status"] == o.ST_OK).all()
     assert hops[1]["act"].tolist() == [2, 3, 0]
     assert hops[1]["perm"].tolist() == [2, 0, 1]
+
+
+def test_partition_graph_rows():
+    """partition_graph_np / _torch (the partitioned follower graph of gd_fanout_multi_part_device):
+    local row i is node nodes[i]'s follower list, in enumeration order; the parts of all ranks hold
+    every edge exactly once."""
+    import torch
+    from orleans_amd.fanout import partition_graph_np, partition_graph_torch
+    from orleans_amd.workloads import power_law_graph
+    n, W = 5000, 4
+    ro, dst = power_law_graph(n, 5.0, seed=3, max_deg=300)
+    owner = np.random.default_rng(1).integers(0, W, n)
+    total = 0
+    for r in range(W):
+        nodes = np.nonzero(owner == r)[0]
+        ro_l, dst_l, node_of = partition_graph_np(ro, dst, nodes)
+        assert node_of.tolist() == nodes.tolist()
+        for i in range(0, nodes.size, 37):
+            u = nodes[i]
+            assert dst_l[ro_l[i]:ro_l[i + 1]].tolist() == dst[ro[u]:ro[u + 1]].tolist()
+        t_ro, t_dst, t_no = partition_graph_torch(torch.from_numpy(ro.astype(np.int64)),
+                                                  torch.from_numpy(dst.astype(np.int32)),
+                                                  torch.from_numpy(nodes.astype(np.int32)))
+        assert t_ro.numpy().astype(np.uint32).tolist() == ro_l.tolist()
+        assert t_dst.numpy().astype(np.uint32).tolist() == dst_l.tolist()
+        assert t_no.numpy().tolist() == nodes.tolist()
+        total += dst_l.size
+    assert total == dst.size

@@ -117,6 +117,75 @@ def test_fanout_multi_local_world_vs_oracle(gd, W, mode):
         e.close()
 
 
+def test_fanout_multi_partitioned_graph_w8(gd):
+    """The cascade over a partitioned follower graph (gd_fanout_multi_part_device): each of W = 8
+    in-process ranks holds only the rows of the grains it owns (~1/8 of the edges), its directory
+    maps each owned node to its local row.  Every hop equals the replicated-graph cascade's (itself
+    checked against the oracle above): frontier, target, sender, sending rank, status, silo, and
+    each activation's message list (perm slice) mapped row -> node."""
+    import torch
+    from orleans_amd.fanout import partition_graph_np
+    W, n, hops = 8, 20000, 4
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    ro, dst = power_law_graph(n, 6.0, seed=77, max_deg=4000)
+    own = _owners(spec, n)
+    registered = np.arange(n)[np.arange(n) % 23 != 4]
+    rep, part, parts = [], [], []
+    dev = torch.device("cuda", 0)
+    for r in range(W):
+        mine = registered[own[registered] % W == r]
+        a = gd.GrainDispatch(device=0, table_capacity=1 << 14, my_silo=r)
+        a.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+        a.register(o.grain_keys(TC, mine), mine.astype(np.uint32), own[mine])
+        rep.append(a)
+        b = gd.GrainDispatch(device=0, table_capacity=1 << 14, my_silo=r)
+        b.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+        b.register(o.grain_keys(TC, mine), np.arange(mine.size, dtype=np.uint32), own[mine])
+        part.append(b)
+        ro_l, dst_l, node_of = partition_graph_np(ro, dst, mine)
+        parts.append(tuple(torch.from_numpy(x.view(np.int32)).to(dev) if x.size else
+                           torch.zeros(1, dtype=torch.int32, device=dev) for x in (ro_l, dst_l, node_of)) +
+                     (mine.size, dst_l.size))
+    assert max(p[4] for p in parts) < 0.3 * dst.size            # ~1/8 of the edges a rank
+    gd.GrainDispatch.comm_init_local(rep)
+    gd.GrainDispatch.comm_init_local(part)
+    seeds = np.random.default_rng(8).choice(registered, 60).astype(np.uint32)
+    seeds = np.concatenate([seeds, seeds[:3]]).astype(np.uint32)                  # duplicates
+    t_seeds = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    torch.cuda.synchronize()
+    want = _run_ranks([lambda r=r: rep[r].fanout_multi(ro, dst, seeds, TC, n, hops) for r in range(W)])
+
+    def run_part(r):
+        ro_d, dst_d, no_d, rows, _ = parts[r]
+        hr = part[r].fanout_multi_part_device(ro_d.data_ptr(), dst_d.data_ptr(), rows, no_d.data_ptr(),
+                                              t_seeds.data_ptr(), seeds.size, TC, hops)
+        out = [part[r].fanout_multi_fetch(h, hr[h], rows) for h in range(hops)]
+        part[r].synchronize()
+        return out
+    got = _run_ranks([lambda r=r: run_part(r) for r in range(W)])
+    assert sum(want[r][h]["target"].size for r in range(W) for h in range(hops)) > 20000
+    for r in range(W):
+        node_of = parts[r][2].cpu().numpy().view(np.uint32)[:parts[r][3]]
+        for h in range(hops):
+            g, w = got[r][h], want[r][h]
+            for k in ("frontier", "target", "sender", "src", "status", "silo"):
+                np.testing.assert_array_equal(g[k], w[k], err_msg=f"hop {h} rank {r} {k}")
+            assert g["n_sent"] == w["n_sent"]
+            ok = g["status"] == 0
+            np.testing.assert_array_equal(node_of[g["act"][ok]], w["act"][ok], err_msg=f"hop {h} rank {r} act")
+            for i, u in enumerate(node_of):                       # each activation's messages, in order
+                np.testing.assert_array_equal(g["perm"][g["offsets"][i]:g["offsets"][i + 1]],
+                                              w["perm"][w["offsets"][u]:w["offsets"][u + 1]],
+                                              err_msg=f"hop {h} rank {r} row {i}")
+            rows = parts[r][3]
+            np.testing.assert_array_equal(g["perm"][g["offsets"][rows]:], w["perm"][w["offsets"][n]:],
+                                          err_msg=f"hop {h} rank {r} unrouted")
+    for e in rep + part:
+        e.comm_destroy()
+        e.close()
+
+
 def test_fanout_multi_world1_rccl_equals_fused_cascade(gd):
     """W = 1 over RCCL (a send/recv to self): the sharded cascade gives exactly the one-GPU fused
     cascade's hops (same emission order, same frontiers)."""
