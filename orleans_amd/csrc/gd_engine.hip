@@ -887,8 +887,8 @@ int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, u
     uint32_t* k1 = (uint32_t*)h->u32_a.p;
     uint32_t* v1 = (uint32_t*)h->u32_c.p;
     GD_TRY((msd_pass<B2_RMAX2, B2_KEY16>(h, acts, n, n_act, R, MSD_SHIFT, k1, v1)));
-    return launch(h, "k_msd_local", dim3(R), dim3(MSD_NT), 0, k_msd_local, (const uint16_t*)k1, (const uint32_t*)v1,
-                  h->last_totals, n, n_act, perm, offsets, rank_out);
+    return launch(h, "k_msd_local", dim3(std::min<uint32_t>(R, h->n_cu)), dim3(MSD_NT), 0, k_msd_local,
+                  (const uint16_t*)k1, (const uint32_t*)v1, h->last_totals, R, n, n_act, perm, offsets, rank_out);
 }
 
 // Three-pass form's split of k' = n_act >> 10: pass B's digit bits a (low part), pass A's kb - a.

@@ -123,11 +123,40 @@ __device__ __forceinline__ uint32_t msd_fold_rank(uint32_t* wc, uint32_t k) {
 // MSD output (rk: range-local keys, u16; ri: message indices).  Writes perm[base, base + S), the
 // range's bucket starts offsets[b << 10, ... + L) and, for the range holding n_act, offsets[n_act + 1]
 // = n.  Called by all MSD_NT threads; LDS is free on entry and on return.
-template <bool FOLD, int NT = MSD_NT, int RW = MSD_RW>
-__device__ __forceinline__ void msd_range(MsdShared<NT, RW>& sh, uint32_t b, uint32_t base, uint32_t S,
-                                          const uint16_t* __restrict__ keys16, const uint32_t* __restrict__ idx,
-                                          uint32_t n, uint32_t n_act, uint32_t* __restrict__ perm,
-                                          uint32_t* __restrict__ offsets, uint32_t* __restrict__ rank_out) {
+// The staged path's keys of a range of S <= NT x RW messages at rk: wave w takes the contiguous segment
+// [s0, s1) of the range, the range-local keys (< 1,024; 0xFFFF past the segment) two to a register,
+// every load in flight at once (unconditional loads, clamped; selects after).
+template <int NT, int RW>
+__device__ __forceinline__ void msd_load_keys(const uint16_t* __restrict__ rk, uint32_t S, uint32_t (&kp)[RW / 2]) {
+    constexpr int NW = NT / WAVE;
+    const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    const uint32_t seg = (S + NW - 1) / NW;
+    const uint32_t s0 = min(w * seg, S), s1 = min((w + 1) * seg, S);
+#pragma unroll
+    for (int j = 0; j < RW / 2; ++j) kp[j] = 0xFFFFFFFFu;   // an empty range: no keys
+    if (S == 0 || S > (uint32_t)(NT * RW)) return;
+    const uint32_t last = S - 1;
+#pragma unroll
+    for (int r = 0; r < RW; r += 2) {
+        const uint32_t i = s0 + r * WAVE + lane;
+        const uint32_t a = rk[min(i, last)], c = rk[min(i + WAVE, last)];
+        kp[r / 2] = (i < s1 ? a : 0xFFFFu) | ((i + WAVE < s1 ? c : 0xFFFFu) << 16);
+    }
+}
+
+struct MsdNoPrefetch {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+// msd_range with the staged path's keys already in kp (msd_load_keys); after() runs once the count
+// sweep is done with them -- the persistent form issues the next range's key loads there, so they
+// fly under this range's scan, ranking and write-out.
+template <bool FOLD, int NT, int RW, class After>
+__device__ __forceinline__ void msd_range_kp(MsdShared<NT, RW>& sh, uint32_t b, uint32_t base, uint32_t S,
+                                             const uint16_t* __restrict__ keys16, const uint32_t* __restrict__ idx,
+                                             uint32_t n, uint32_t n_act, uint32_t* __restrict__ perm,
+                                             uint32_t* __restrict__ offsets, uint32_t* __restrict__ rank_out,
+                                             uint32_t (&kp)[RW / 2], After after) {
     constexpr int NW = NT / WAVE;
     constexpr uint32_t CAP = NT * RW;
     static_assert(NT >= (int)MSD_LW, "a thread for every u16-pair counter word");
@@ -140,22 +169,8 @@ __device__ __forceinline__ void msd_range(MsdShared<NT, RW>& sh, uint32_t b, uin
     for (uint32_t x = tid; x < MSD_L; x += NT) sh.run[x] = 0;
     for (uint32_t x = tid; x < NW * MSD_LW; x += NT) (&sh.wc[0][0])[x] = 0;
     if (S <= CAP) {
-        // staged: wave w takes the contiguous segment [s0, s1) of the range, the range-local keys
-        // (< 1,024; 0xFFFF past the segment) two to a register, every load in flight at once
         const uint32_t seg = (S + NW - 1) / NW;
         const uint32_t s0 = min(w * seg, S), s1 = min((w + 1) * seg, S);
-        uint32_t kp[RW / 2];
-#pragma unroll
-        for (int j = 0; j < RW / 2; ++j) kp[j] = 0xFFFFFFFFu;   // an empty range: no keys
-        if (S) {                                         // unconditional loads (clamped), selects after
-            const uint32_t last = S - 1;
-#pragma unroll
-            for (int r = 0; r < RW; r += 2) {
-                const uint32_t i = s0 + r * WAVE + lane;
-                const uint32_t a = rk[min(i, last)], c = rk[min(i + WAVE, last)];
-                kp[r / 2] = (i < s1 ? a : 0xFFFFu) | ((i + WAVE < s1 ? c : 0xFFFFu) << 16);
-            }
-        }
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
@@ -167,6 +182,7 @@ __device__ __forceinline__ void msd_range(MsdShared<NT, RW>& sh, uint32_t b, uin
         // across the barriers (that spilled)
 #pragma unroll
         for (int j = 0; j < RW / 2; ++j) asm volatile("" : "+v"(kp[j]));
+        after();
         __syncthreads();
         uint32_t tlo, thi;
         msd_wave_prefix<NW>(&sh.wc[0][0], tid, tlo, thi);
@@ -269,6 +285,16 @@ __device__ __forceinline__ void msd_range(MsdShared<NT, RW>& sh, uint32_t b, uin
     __syncthreads();
 }
 
+template <bool FOLD, int NT = MSD_NT, int RW = MSD_RW>
+__device__ __forceinline__ void msd_range(MsdShared<NT, RW>& sh, uint32_t b, uint32_t base, uint32_t S,
+                                          const uint16_t* __restrict__ keys16, const uint32_t* __restrict__ idx,
+                                          uint32_t n, uint32_t n_act, uint32_t* __restrict__ perm,
+                                          uint32_t* __restrict__ offsets, uint32_t* __restrict__ rank_out) {
+    uint32_t kp[RW / 2];
+    msd_load_keys<NT, RW>(keys16 + base, S, kp);
+    msd_range_kp<FOLD, NT, RW>(sh, b, base, S, keys16, idx, n, n_act, perm, offsets, rank_out, kp, MsdNoPrefetch{});
+}
+
 // The hardware property every stable rank of this library rests on (the LSD and MSD scatters, the
 // range sorts, the level-2 and micro-batch ranks): the lanes of one wave's LDS ds_add_rtn to one
 // address are served in ascending lane order, so each lane's returned value is the sum of the
@@ -310,27 +336,44 @@ __global__ void __launch_bounds__(256) k_lane_order_check(uint32_t* __restrict__
     out[threadIdx.x] = bad;
 }
 
-// One-pass form: range b = blockIdx.x; its first output position is the digit totals before it.
-__global__ void __launch_bounds__(MSD_NT, 4) k_msd_local(const uint16_t* __restrict__ keys16,
-                                                         const uint32_t* __restrict__ idx,
-                                                         const uint32_t* __restrict__ totals, uint32_t n,
-                                                         uint32_t n_act, uint32_t* __restrict__ perm,
-                                                         uint32_t* __restrict__ offsets,
-                                                         uint32_t* __restrict__ rank_out) {
+// One-pass form, persistent: gridDim.x <= R workgroups (one a CU) walk the ranges b = blockIdx.x +
+// k x gridDim.x, every range's first position from one scan of the totals at the start, and each
+// range's key loads issued under the previous range's scan, ranking and write-out (msd_range_kp).
+// Against one workgroup a range (round 3): 0.0523 -> 0.0495 ms at cfg 2, stage 0.148 -> 0.146 ms
+// (3 interleaved rounds each).
+__global__ void __launch_bounds__(MSD_NT, 1) k_msd_local(const uint16_t* __restrict__ keys16,
+                                                            const uint32_t* __restrict__ idx,
+                                                            const uint32_t* __restrict__ totals, uint32_t R,
+                                                            uint32_t n, uint32_t n_act, uint32_t* __restrict__ perm,
+                                                            uint32_t* __restrict__ offsets,
+                                                            uint32_t* __restrict__ rank_out) {
     __shared__ MsdShared<MSD_NT, MSD_RW> sh;
-    const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
-    uint32_t part = 0;
-    for (uint32_t d = tid; d < b; d += MSD_NT) part += totals[d];
-    for (int off = WAVE / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, WAVE);
-    if (lane == 0) sh.red[w] = part;
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t t = 0;
-        for (int q = 0; q < MSD_NW; ++q) t += sh.red[q];
-        sh.base = t;
+    __shared__ uint32_t s_base[2 * MSD_NT];
+    const uint32_t tid = threadIdx.x;
+    {
+        const uint32_t t0 = 2 * tid < R ? totals[2 * tid] : 0u, t1 = 2 * tid + 1 < R ? totals[2 * tid + 1] : 0u;
+        const uint32_t ex = block_excl_scan_add_n<MSD_NT>(t0 + t1, sh.red);
+        s_base[2 * tid] = ex;
+        s_base[2 * tid + 1] = ex + t0;
     }
     __syncthreads();
-    msd_range<false>(sh, b, sh.base, totals[b], keys16, idx, n, n_act, perm, offsets, rank_out);
+    uint32_t b = blockIdx.x;
+    if (b >= R) return;                                  // uniform over the workgroup
+    uint32_t kp[MSD_RW / 2], kn[MSD_RW / 2];
+    uint32_t S = totals[b];
+    msd_load_keys<MSD_NT, MSD_RW>(keys16 + s_base[b], S, kp);
+    for (; b < R; b += gridDim.x) {
+        const uint32_t nb = b + gridDim.x;
+        const uint32_t nS = nb < R ? totals[nb] : 0u;
+        const uint32_t nbase = nb < R ? s_base[nb] : 0u;
+        auto next = [&] { msd_load_keys<MSD_NT, MSD_RW>(keys16 + nbase, nS, kn); };
+        msd_range_kp<false, MSD_NT, MSD_RW>(sh, b, s_base[b], S, keys16, idx, n, n_act, perm, offsets, rank_out, kp,
+                                            next);
+        if (S > MSD_CAP) next();                         // a hot range takes the chunked path: no after()
+#pragma unroll
+        for (int j = 0; j < MSD_RW / 2; ++j) kp[j] = kn[j];
+        S = nS;
+    }
 }
 
 // Three-pass form: the ranges of list[0, *count) (each <= NT x RW messages), range b at rs[b] .. rs[b + 1]
