@@ -1156,6 +1156,9 @@ template <int MODE, bool NODES>
 int shard_hist_t(gd_handle* h, const void* recs, uint32_t n, uint64_t tcd, uint32_t n_shards, uint32_t bits,
                  uint32_t tiles, uint8_t* dest, uint32_t* hist, const ExtArgs& ext, uint32_t* kdesc, uint32_t regions) {
     uint32_t* n1lo = !NODES && kdesc && h->shard_n1_copy ? (uint32_t*)h->shard_n1.p : nullptr;
+    if (!NODES && !ext.len)           // no KeyExt strings in the batch: the instantiation without their path
+        return launch(h, "k_shard_hist", dim3(tiles), dim3(SH_NT), ring_lds(h), k_shard_hist<MODE, NODES, false>, recs,
+                      n, tcd, ring_args(h), n_shards, bits, tiles, dest, hist, ext, kdesc, n1lo, regions);
     return launch(h, "k_shard_hist", dim3(tiles), dim3(SH_NT), ring_lds(h), k_shard_hist<MODE, NODES>, recs, n, tcd,
                   ring_args(h), n_shards, bits, tiles, dest, hist, ext, kdesc, n1lo, regions);
 }

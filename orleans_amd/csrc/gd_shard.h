@@ -31,7 +31,10 @@ constexpr uint32_t SH_TILE = SH_NT * SH_IT;   // 2048 records per tile
 // strings are given (ext.len != nullptr, gd_route_multi_ext), else they stay here (KEYEXT).
 // region (optional): the grain's table region on its owner (grain_region of its uniform hash) for a
 // grain the owner probes in its directory table, 0 for everything else.
-template <int MODE>
+// EXT = false: the batch carries no KeyExt strings (ext.len == nullptr); the string-hash path is
+// compiled out (k_shard_hist unrolls 8 records a thread: with it inlined the kernel was 14K
+// instructions, past the instruction cache).
+template <int MODE, bool EXT = true>
 __device__ __forceinline__ uint32_t key_dest(uint64_t n0, uint64_t n1, uint64_t tcd, const uint32_t* s_pts,
                                              const uint32_t* s_own, const RingArgs& ring, uint32_t n_shards,
                                              const ExtArgs& ext, uint32_t i, uint32_t* region = nullptr) {
@@ -40,7 +43,7 @@ __device__ __forceinline__ uint32_t key_dest(uint64_t n0, uint64_t n1, uint64_t 
     if (region) *region = 0;
     const uint8_t* s;
     int32_t len;
-    if ((cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) && ext.len && ext_of(ext, i, s, len)) {
+    if (EXT && (cat == CAT_KEYEXT_GRAIN || cat == CAT_GEO_CLIENT) && ext.len && ext_of(ext, i, s, len)) {
         uint32_t uh;
         if (len < 0) {
             uh = uniform_hash(n0, n1, tcd);
@@ -68,7 +71,7 @@ __device__ __forceinline__ uint32_t key_dest(uint64_t n0, uint64_t n1, uint64_t 
 // counter.  `bits` = destination bits (n_shards <= 1 << bits).
 // regions (keys only; 1 or N_REGIONS): destination = owner rank * regions + the grain's table region,
 // so each rank's chunk arrives grouped by region (gd_route_multi's region-mapped probe).
-template <int MODE, bool NODES>
+template <int MODE, bool NODES, bool EXT = true>
 __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ recs, uint32_t n, uint64_t tcd,
                                                       RingArgs ring, uint32_t n_shards, uint32_t bits,
                                                       uint32_t tiles, uint8_t* __restrict__ dest,
@@ -118,7 +121,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
                 d = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, uniform_hash(0, node, tcd))] % n_shards;
             } else {
                 uint32_t reg = 0;
-                d = key_dest<MODE>(kv[r][0], kv[r][1], kv[r][2], s_pts, s_own, ring, n_shards, ext, i,
+                d = key_dest<MODE, EXT>(kv[r][0], kv[r][1], kv[r][2], s_pts, s_own, ring, n_shards, ext, i,
                                    regions > 1 ? &reg : nullptr) * regions + reg;
                 wide |= kv[r][0] != 0 || kv[r][2] != ref_tcd;
                 big |= (kv[r][1] >> 32) != 0;
