@@ -121,6 +121,17 @@ def test_msd_three_pass_class_threshold(gd, small):
     e0.close()
 
 
+@pytest.mark.parametrize("mid", [0, 2000, 8192])
+def test_msd_three_pass_mid_class(gd, mid):
+    """The mid-range class (512-thread sorts, GD_OPT_L2_MID) takes staged ranges up to `mid` messages,
+    the 1,024-thread sort the rest (0: none mid); Zipf ranges from a few to 24K+ messages cover every
+    class at each setting; the result never changes."""
+    acts = _acts(1 << 22, 3 << 20, "zipf", 91)
+    e2, e0 = _check(gd, acts, 3 << 20, l2_mid=mid)
+    e2.close()
+    e0.close()
+
+
 def test_msd_three_pass_kernels(gd):
     """The three-pass form runs its own kernels (not the LSD passes) when forced."""
     acts = _acts(1 << 21, 5_000_000, "zipf", 9)
