@@ -966,14 +966,16 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     pts, own = e.ring_set_silos(args.mode, SILO_SETS[args.silos])
     owner = e.ring_owner(keys)
     mine = np.nonzero(owner % world == rank)[0]
-    # N > 1: the follower graph is partitioned (gd_fanout_multi_part_device): this rank keeps the rows
-    # of the grains it owns, row i = activation i (ascending node ids); N = 1: node u = activation u
-    e.register(keys[mine], (np.arange(mine.size) if world > 1 else mine).astype(np.uint32), owner[mine])
+    # N > 1 (or --exchange library at N = 1: the same path over a one-rank RCCL communicator): the
+    # follower graph is partitioned (gd_fanout_multi_part_device), this rank keeps the rows of the
+    # grains it owns, row i = activation i (ascending node ids); else node u = activation u
+    sharded = world > 1 or args.exchange == "library"
+    e.register(keys[mine], (np.arange(mine.size) if sharded else mine).astype(np.uint32), owner[mine])
     del keys
     eng = DeviceFanoutEngine(e, dev, tc, keep_target=not args.no_target)
     node_of = None
     n_act = n
-    if world > 1:
+    if sharded:
         ro_l, dst_l, no = partition_graph_np(ro, dst, mine)
         graph = upload_graph(ro_l, dst_l, dev)
         node_of = torch.from_numpy(no.view(np.int32) if no.size else np.zeros(1, np.int32)).to(dev)
@@ -990,9 +992,9 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     # N > 1: the sharded cascade inside the library (gd_fanout_multi_device), bit-exact against
     # oracle/fanout.py in tests/test_gpu_fanout_multi.py (W = 8 and 3 in process)
     assert not (world > 1 and args.rehearse_one_gpu), "cfg4 at N > 1 runs the library's RCCL cascade only"
-    runner = FanoutCascade(eng, graph, n) if world == 1 else LibraryFanout(eng, graph, n_act, node_of=node_of)
-    exchange = "none" if world == 1 else ("libgraindispatch gd_fanout_multi_part_device (partitioned follower "
-                                          "graph; grouped RCCL send/recv of (target, sender) per hop)")
+    runner = LibraryFanout(eng, graph, n_act, node_of=node_of) if sharded else FanoutCascade(eng, graph, n)
+    exchange = "none" if not sharded else ("libgraindispatch gd_fanout_multi_part_device (partitioned follower "
+                                           "graph; grouped RCCL send/recv of (target, sender) per hop)")
 
     def step():
         return runner.run(t_seeds, args.hops)
