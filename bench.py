@@ -120,7 +120,7 @@ def bucket_bytes(form: str, n: int, n_act: int, acts=None) -> dict:
     # the record read, a 6-B record written; its [segment][digit][tile] counts flat-scanned), level 2
     # (record read, index written in order, starts written once, per class)
     kb = max(1, (n_act >> 10).bit_length())
-    a = (kb + 1) // 2
+    a = kb // 2
     tiles = -(-n // 8192) + (n_act >> (10 + a)) + 1
     cnt = (1 << a) * tiles * 4.0
     # pass A's records: 6 B (u16 + the index word's spare bits) when the index leaves room, else 8 B

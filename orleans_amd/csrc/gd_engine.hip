@@ -899,7 +899,10 @@ bool msd3_split(uint32_t n_act, uint32_t* a_out, uint32_t* ra_out) {
     uint32_t kb = 0;
     while (kb < 32 && (km >> kb) != 0) ++kb;
     if (kb > 18) return false;
-    const uint32_t a = (kb + 1) / 2;
+    // pass B takes the smaller half: a 17-bit k' (BASELINE cfg 3) as 9 + 8 bits, pass B's 256 digits
+    // writing twice the run length of 512 (k_seg_scatter 0.240 -> 0.218 ms, step 2.094 -> 2.035 ms,
+    // profiles/r04_msd3_split_ab.jsonl)
+    const uint32_t a = kb / 2;
     *a_out = a;
     *ra_out = (km >> a) + 1;
     return true;
