@@ -438,3 +438,41 @@ def test_tune_agree_w8(gd):
     for e in es:
         e.comm_destroy()
         e.close()
+
+
+def test_options_roundtrip_and_range(gd, monkeypatch):
+    """gd_option_set / gd_option_get: every option reads back what was set, the defaults are the
+    documented ones, values out of range and unknown options are refused with an error
+    (the handle keeps its value)."""
+    monkeypatch.setattr(gd, "DEFAULT_OPTIONS", {})           # the library's own defaults, not this module's
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 12)   # creation ran the lane-order self-check
+    defaults = {"probe": 1, "bucket": 1, "l2_small": 1024, "stable_rank": 1, "wire_headers": 2,
+                "region_probe": 0, "idx16": 1, "host_chunk": 2097152, "mb_zerocopy": 1, "mb_split": 8,
+                "mb_trace": 0, "l2_staged": 24576, "l2_mid": 8192}
+    assert set(defaults) == set(gd.OPTIONS)
+    for k, v in defaults.items():
+        assert e.get_option(k) == v, k
+    for k, v in {"probe": 3, "bucket": 2, "l2_small": 300, "stable_rank": 0, "wire_headers": 0,
+                 "region_probe": 1, "idx16": 0, "l2_staged": 9000, "l2_mid": 2000}.items():
+        e.set_option(k, v)
+        assert e.get_option(k) == v, k
+    for k, bad in {"probe": 4, "bucket": -1, "l2_small": 24577, "l2_mid": 8193, "l2_staged": 1 << 20}.items():
+        before = e.get_option(k)
+        with pytest.raises(Exception):
+            e.set_option(k, bad)
+        assert e.get_option(k) == before, k
+    with pytest.raises(Exception):
+        e.set_option(99, 1)
+    e.close()
+
+
+def test_comm_info_world1_rccl(gd):
+    """gd_comm_info reports the communicator as RCCL sees it: none before gd_comm_init, one rank over
+    RCCL after, none again after gd_comm_destroy."""
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 12)
+    assert e.comm_info()["transport"] == "none"
+    e.comm_init(gd.GrainDispatch.comm_unique_id(), 1, 0)
+    assert e.comm_info() == {"n_ranks": 1, "rank": 0, "transport": "rccl"}
+    e.comm_destroy()
+    assert e.comm_info()["transport"] == "none"
+    e.close()
