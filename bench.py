@@ -948,7 +948,7 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     HBM.  N = 1: fused expand+route kernel (k_fan_route) per hop.  N > 1: directory sharded by ring
     owner, (target, sender) pairs exchanged with one grouped RCCL send/recv round per hop inside the
     library (gd_fanout_multi_device, LibraryFanout)."""
-    from orleans_amd.fanout import (CHIRPER_ACCOUNT_CLASS, DeviceFanoutEngine, FanoutCascade, LibraryFanout,
+    from orleans_amd.fanout import (CHIRPER_ACCOUNT_CLASS, DeviceFanoutEngine, LibraryCascade, LibraryFanout,
                                     partition_graph_np, upload_graph)
     from orleans_amd.workloads import power_law_graph
 
@@ -992,7 +992,8 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     # N > 1: the sharded cascade inside the library (gd_fanout_multi_device), bit-exact against
     # oracle/fanout.py in tests/test_gpu_fanout_multi.py (W = 8 and 3 in process)
     assert not (world > 1 and args.rehearse_one_gpu), "cfg4 at N > 1 runs the library's RCCL cascade only"
-    runner = LibraryFanout(eng, graph, n_act, node_of=node_of) if sharded else FanoutCascade(eng, graph, n)
+    # N = 1: the whole cascade inside the library (gd_fanout_cascade_device, one read-back a hop)
+    runner = LibraryFanout(eng, graph, n_act, node_of=node_of) if sharded else LibraryCascade(eng, graph, n)
     exchange = "none" if not sharded else ("libgraindispatch gd_fanout_multi_part_device (partitioned follower "
                                            "graph; grouped RCCL send/recv of (target, sender) per hop)")
 
@@ -1031,8 +1032,8 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
 
     kernels, roofline = {}, None
     if profile_steps > 0:
-        hop_acts = [h.act.cpu().numpy().view(np.uint32) if getattr(h, "act", None) is not None else None
-                    for h in hops]
+        hop_acts = ([f["act"] for f in runner.fetch(hops)] if isinstance(runner, LibraryCascade)
+                    else [None for _ in hops])
         e.set_kernel_timing(True)
         e.kernel_times_reset()
         for _ in range(profile_steps):
@@ -1054,8 +1055,8 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
             roofline["hop_bucket_forms"] = [hop_form(e, m, n_act) for m in hop_msgs]
 
     cpu = None
-    if rank == 0 and world == 1 and with_cpu and getattr(hops[-1], "target", None) is not None:
-        cpu = cpu_baseline_cfg4(args, hops, tcd, owner, pts, own, n)
+    if rank == 0 and world == 1 and with_cpu and isinstance(runner, LibraryCascade):
+        cpu = cpu_baseline_cfg4(args, runner.fetch(hops)[-1]["target"], tcd, owner, pts, own, n)
 
     line = {
             "metric": "routed messages/sec (fan-out cascade: expand+lookup+bucket, whole node)",
@@ -1081,13 +1082,13 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     return line
 
 
-def cpu_baseline_cfg4(args, hops, tcd, owner, pts, own, n):
+def cpu_baseline_cfg4(args, t, tcd, owner, pts, own, n):
     """cfg 4's CPU baseline: the C restatement (oracle/cpu_ref.c, test infrastructure, faithful
     mode, 1 thread) routing + bucketing a bounded sample of the cascade's last hop; the follower
     expansion itself is a numpy gather and is not timed."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpu_ref  # test-infrastructure checker, timed here as the CPU baseline only
-    t = hops[-1].target.cpu().numpy().view(np.uint32)
+    t = np.asarray(t, dtype=np.uint32)                 # the last hop's targets
     sample = min(t.size, 1 << 21)
     keys = grain_keys(tcd, t[:sample].astype(np.int64))
     d = cpu_ref.CpuDirectory(True, n)

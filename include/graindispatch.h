@@ -608,6 +608,17 @@ int gd_fanout_multi_part_device(gd_handle* h, const uint32_t* d_row_off, const u
 int gd_fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint32_t n_nodes,
                     const uint32_t* seeds, uint32_t n_seeds, int32_t type_code, uint32_t n_act, uint32_t hops,
                     gd_fanout_hop* out);
+/* The single-GPU cascade inside the library (BASELINE cfg 4 on one GPU; what gd_fanout_route_bucket
+ * + gd_frontier_next do hop by hop from the host): `seeds` publish in seed order, then per hop the
+ * fused expand + route (ChirperAccount.cs:131-134), the bucketing per activation and the next
+ * publishers (this handle's activations that received a chirp and have not published, ascending).
+ * Node u = activation u (n_act >= the nodes that have activations).  One host read-back a hop (the
+ * next hop's message and publisher counts together, the frontier's size staying on the device until
+ * then).  out[hops] (may be NULL): device pointers into library buffers as gd_fanout_multi_device's
+ * (src = NULL); gd_fanout_multi_fetch copies a hop out (src as zeros). */
+int gd_fanout_cascade_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_nodes,
+                             const uint32_t* d_seeds, uint32_t n_seeds, int32_t type_code, uint32_t n_act,
+                             uint32_t hops, gd_fanout_hop* out);
 /* Copy hop `hop` of the last cascade to host arrays sized from its gd_fanout_hop (any may be NULL). */
 int gd_fanout_multi_fetch(gd_handle* h, uint32_t hop, uint32_t* frontier, uint32_t* target, uint32_t* sender,
                           uint32_t* src, uint32_t* silo, uint32_t* act, uint8_t* status, uint32_t* perm,

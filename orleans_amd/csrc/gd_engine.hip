@@ -2641,12 +2641,12 @@ int fan_count(gd_handle* h, const uint32_t* row_off, uint32_t n_nodes, const uin
         uint32_t* part = (uint32_t*)h->fan[1].p;
         if (wide) {
             GD_TRY(launch(h, "k_fan_degree", dim3(nb), dim3(BLOCK), 0, k_fan_degree_tiles<16>, row_off, n_nodes, frontier,
-                          nf, ends, part));
+                          nf, ends, part, (const uint32_t*)nullptr));
             GD_TRY(launch(h, "k_scan_down", dim3(nb), dim3(BLOCK), 0, k_scan_down<OpAdd, 16>, (const uint32_t*)ends, ends,
                           nf, false, true, (const uint32_t*)part, nb));
         } else {
             GD_TRY(launch(h, "k_fan_degree", dim3(nb), dim3(BLOCK), 0, k_fan_degree_tiles<4>, row_off, n_nodes, frontier,
-                          nf, ends, part));
+                          nf, ends, part, (const uint32_t*)nullptr));
             GD_TRY(launch(h, "k_scan_down", dim3(nb), dim3(BLOCK), 0, k_scan_down<OpAdd, 4>, (const uint32_t*)ends, ends,
                           nf, false, true, (const uint32_t*)part, nb));
         }
@@ -2776,9 +2776,158 @@ int frontier_next(gd_handle* h, const uint32_t* offsets, uint32_t n_act, uint8_t
     return GD_OK;
 }
 
+// frontier_next without the read-back: the new frontier's length stays on the device (*d_nf).
+int frontier_next_dev(gd_handle* h, const uint32_t* offsets, uint32_t n_act, uint8_t* visited, uint32_t* out,
+                      const uint32_t** d_nf) {
+    const uint32_t nb = blocks_for(std::max<uint32_t>(n_act, 1), FR_TILE);
+    GD_TRY(ensure(h, h->fan[2], (size_t)nb * BLOCK * sizeof(uint16_t)));
+    GD_TRY(ensure(h, h->fan[3], ((size_t)nb + 1) * 4));
+    uint16_t* flags = (uint16_t*)h->fan[2].p;
+    uint32_t* counts = (uint32_t*)h->fan[3].p;
+    uint32_t* total = counts + nb;
+    *d_nf = total;
+    if (n_act == 0) {
+        HIP_TRY(h, hipMemsetAsync(total, 0, 4, h->stream));
+        return GD_OK;
+    }
+    GD_TRY(launch(h, "k_frontier_count", dim3(nb), dim3(BLOCK), 0, k_frontier_count, offsets, n_act, visited, flags,
+                  counts));
+    return launch(h, "k_frontier_compact", dim3(nb), dim3(BLOCK), 0, k_frontier_compact, (const uint16_t*)flags,
+                  (const uint32_t*)counts, nb, out, total);
+}
+
+// fan_count of a frontier whose length is on the device (*d_nf <= nf_max): the degree and scan grids
+// are sized for nf_max, and one read-back brings both the length and the total (instead of one for
+// each).  Past 16M rows it reads the length first and takes fan_count.
+int fan_count_dev(gd_handle* h, const uint32_t* row_off, uint32_t n_nodes, const uint32_t* frontier,
+                  const uint32_t* d_nf, uint32_t nf_max, uint32_t* nf, uint64_t* total) {
+    *nf = 0;
+    *total = 0;
+    if (nf_max == 0) return GD_OK;
+    const uint32_t nb4 = blocks_for(nf_max, SCAN_TILE), nb16 = blocks_for(nf_max, 4 * SCAN_TILE);
+    if (!(nb4 <= 2048 || nb16 <= 4096)) {
+        GD_TRY(pinned_scratch(h, 4));
+        HIP_TRY(h, hipMemcpyAsync(h->h_pin, d_nf, 4, hipMemcpyDeviceToHost, h->stream));
+        GD_TRY(sync(h));
+        *nf = *(const uint32_t*)h->h_pin;
+        return fan_count(h, row_off, n_nodes, frontier, *nf, total);
+    }
+    const bool wide = nb4 > 2048;
+    const uint32_t nb = wide ? nb16 : nb4;
+    GD_TRY(ensure(h, h->fan[0], (size_t)nf_max * 4));
+    GD_TRY(ensure(h, h->fan[1], (size_t)nb * 4));
+    GD_TRY(pinned_scratch(h, ((size_t)nb + 1) * 4));
+    uint32_t* ends = (uint32_t*)h->fan[0].p;
+    uint32_t* part = (uint32_t*)h->fan[1].p;
+    if (wide) {
+        GD_TRY(launch(h, "k_fan_degree", dim3(nb), dim3(BLOCK), 0, k_fan_degree_tiles<16>, row_off, n_nodes, frontier,
+                      nf_max, ends, part, d_nf));
+        GD_TRY(launch(h, "k_scan_down", dim3(nb), dim3(BLOCK), 0, k_scan_down<OpAdd, 16>, (const uint32_t*)ends, ends,
+                      nf_max, false, true, (const uint32_t*)part, nb));
+    } else {
+        GD_TRY(launch(h, "k_fan_degree", dim3(nb), dim3(BLOCK), 0, k_fan_degree_tiles<4>, row_off, n_nodes, frontier,
+                      nf_max, ends, part, d_nf));
+        GD_TRY(launch(h, "k_scan_down", dim3(nb), dim3(BLOCK), 0, k_scan_down<OpAdd, 4>, (const uint32_t*)ends, ends,
+                      nf_max, false, true, (const uint32_t*)part, nb));
+    }
+    uint32_t* pin = (uint32_t*)h->h_pin;
+    HIP_TRY(h, hipMemcpyAsync(pin, part, (size_t)nb * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(pin + nb, d_nf, 4, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(sync(h));
+    uint64_t t = 0;
+    for (uint32_t b = 0; b < nb; ++b) t += pin[b];
+    if (t > 0xFFFFFFFFull)
+        return set_err(h, GD_EINVAL, "fan-out of %llu messages exceeds 2^32 - 1", (unsigned long long)t);
+    *nf = pin[nb];
+    *total = t;
+    return GD_OK;
+}
+
+// The whole single-GPU cascade in the library (gd_fanout_cascade_device): per hop the fused
+// expand + route (k_fan_route), the bucketing and the next frontier, with one host read-back a hop
+// (the next hop's size and its publishers' count together).  Results in the handle's hop buffers
+// (fm_hop / fm_res, read by gd_fanout_multi_fetch).
+int fanout_cascade(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint32_t n_nodes, const uint32_t* seeds,
+                   uint32_t n_seeds, int32_t type_code, uint32_t n_act, uint32_t hops, gd_fanout_hop* out) {
+    GD_TRY(check_ring(h));
+    if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    const uint64_t tcd = grain_tcd(type_code);
+    GD_TRY(sync(h));                                   // the previous call's results may be in use
+    if (h->fm_hop.size() < hops) h->fm_hop.resize(hops);
+    h->fm_res.assign(hops, gd_fanout_hop{});
+    h->fm_n_act = n_act;
+    DevBuf* S = h->fm_scr;
+    GD_TRY(ensure(h, S[5], (size_t)n_act + 16));
+    uint8_t* visited = (uint8_t*)S[5].p;
+    HIP_TRY(h, hipMemsetAsync(visited, 0, (size_t)n_act + 16, h->stream));
+    uint32_t nf = n_seeds;
+    {
+        std::array<DevBuf, 10>& H0 = h->fm_hop[0];
+        GD_TRY(ensure(h, H0[0], ((size_t)std::max(nf, n_act) + 4) * 4));
+        if (nf) {
+            HIP_TRY(h, hipMemcpyAsync(H0[0].p, seeds, (size_t)nf * 4, hipMemcpyDeviceToDevice, h->stream));
+            GD_TRY(launch(h, "k_mark_visited", dim3(blocks_for(nf, BLOCK)), dim3(BLOCK), 0, k_mark_visited,
+                          (const uint32_t*)H0[0].p, nf, n_act, visited));
+        }
+    }
+    uint64_t total = 0;
+    GD_TRY(fan_count(h, row_off, n_nodes, (const uint32_t*)h->fm_hop[0][0].p, nf, &total));
+    for (uint32_t hp = 0; hp < hops; ++hp) {
+        std::array<DevBuf, 10>& H = h->fm_hop[hp];
+        const uint32_t* frontier = (const uint32_t*)H[0].p;
+        const uint32_t m = (uint32_t)total;
+        gd_fanout_hop& res = h->fm_res[hp];
+        res.n_frontier = nf;
+        res.frontier = frontier;
+        res.n_sent = total;
+        const size_t m4 = (size_t)m * 4 + 16;
+        const size_t want[10] = {0, m4, m4, 0, m4, m4, (size_t)m + 16, m4, ((size_t)n_act + 2) * 4, 0};
+        for (int b = 1; b < 9; ++b)
+            if (want[b]) GD_TRY(ensure(h, H[b], want[b]));
+        uint32_t* target = (uint32_t*)H[1].p;
+        uint32_t* sender = (uint32_t*)H[2].p;
+        uint32_t* silo = (uint32_t*)H[4].p;
+        uint32_t* act = (uint32_t*)H[5].p;
+        uint8_t* st = (uint8_t*)H[6].p;
+        uint32_t* perm = (uint32_t*)H[7].p;
+        uint32_t* offs = (uint32_t*)H[8].p;
+        if (m) GD_TRY(fan_route(h, row_off, dst, frontier, nf, m, tcd, target, sender, silo, act, st));
+        GD_TRY(bucket_device(h, act, m, n_act, perm, offs));
+        res.n_recv = m;
+        res.target = target;
+        res.sender = sender;
+        res.src = nullptr;
+        res.silo = silo;
+        res.act = act;
+        res.status = st;
+        res.perm = perm;
+        res.offsets = offs;
+        if (hp + 1 < hops) {
+            std::array<DevBuf, 10>& N = h->fm_hop[hp + 1];
+            GD_TRY(ensure(h, N[0], ((size_t)n_act + 4) * 4));
+            const uint32_t* d_nf = nullptr;
+            GD_TRY(frontier_next_dev(h, offs, n_act, visited, (uint32_t*)N[0].p, &d_nf));
+            GD_TRY(fan_count_dev(h, row_off, n_nodes, (const uint32_t*)N[0].p, d_nf, n_act, &nf, &total));
+        }
+    }
+    if (out) std::copy(h->fm_res.begin(), h->fm_res.end(), out);
+    return GD_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int gd_fanout_cascade_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_nodes,
+                             const uint32_t* d_seeds, uint32_t n_seeds, int32_t type_code, uint32_t n_act,
+                             uint32_t hops, gd_fanout_hop* out) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (n_seeds && !d_seeds) return set_err(h, GD_EINVAL, "null seeds");
+    if (!d_row_off || (!d_dst && n_nodes)) return set_err(h, GD_EINVAL, "null graph");
+    if (hops == 0 || hops > 64) return set_err(h, GD_EINVAL, "hops %u not in [1, 64]", hops);
+    HIP_TRY(h, hipSetDevice(h->device));
+    return fanout_cascade(h, d_row_off, d_dst, n_nodes, d_seeds, n_seeds, type_code, n_act, hops, out);
+}
 
 int gd_fanout_expand_device(gd_handle* h, const uint32_t* d_row_off, const uint32_t* d_dst, uint32_t n_nodes,
                             const uint32_t* d_frontier, uint32_t n_frontier, uint32_t* d_target, uint32_t* d_sender,
@@ -4663,7 +4812,8 @@ int gd_fanout_multi_fetch(gd_handle* h, uint32_t hop, uint32_t* frontier, uint32
     GD_TRY(cp(frontier, r.frontier, (size_t)r.n_frontier * 4));
     GD_TRY(cp(target, r.target, m * 4));
     GD_TRY(cp(sender, r.sender, m * 4));
-    GD_TRY(cp(src, r.src, m * 4));
+    if (r.src) GD_TRY(cp(src, r.src, m * 4));
+    else if (src) std::memset(src, 0, m * 4);           // the one-GPU cascade: every message is this rank's
     GD_TRY(cp(silo, r.silo, m * 4));
     GD_TRY(cp(act, r.act, m * 4));
     GD_TRY(cp(status, r.status, m));

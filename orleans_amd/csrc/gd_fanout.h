@@ -60,10 +60,14 @@ __global__ void __launch_bounds__(BLOCK) k_fan_degree(const uint32_t* __restrict
 // for thread t) and the tile's sum to part[b], so the inclusive scan of ends is the down-sweep
 // alone; the host adds the partials up for the u64 total.
 template <int IPT>
+// d_nf (optional): the frontier's length on the device (<= n_front, the grid's bound), as
+// k_frontier_compact left it -- the in-library cascade sizes a hop without reading it back first.
 __global__ void __launch_bounds__(BLOCK) k_fan_degree_tiles(const uint32_t* __restrict__ row_off, uint32_t n_nodes,
                                                             const uint32_t* __restrict__ frontier, uint32_t n_front,
-                                                            uint32_t* __restrict__ ends, uint32_t* __restrict__ part) {
+                                                            uint32_t* __restrict__ ends, uint32_t* __restrict__ part,
+                                                            const uint32_t* __restrict__ d_nf) {
     __shared__ uint32_t s_wsum[BLOCK / WAVE];
+    if (d_nf) n_front = min(n_front, *d_nf);
     const uint32_t i0 = blockIdx.x * (BLOCK * IPT) + threadIdx.x;
     uint32_t u[IPT], v = 0;
 #pragma unroll

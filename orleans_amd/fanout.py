@@ -208,6 +208,25 @@ class FanoutCascade:
         return out
 
 
+class LibraryCascade:
+    """All hops on one GPU inside libgraindispatch (gd_fanout_cascade_device): one host read-back a hop
+    instead of the two of FanoutCascade's per-hop calls.  Node u = activation u."""
+
+    def __init__(self, engine: DeviceFanoutEngine, graph: FollowerGraph, n_act: int):
+        self.engine, self.graph, self.n_act = engine, graph, n_act
+
+    def run(self, seeds: torch.Tensor, hops: int) -> List["LibraryHop"]:
+        ns = int(seeds.shape[0])
+        with self.engine.context():
+            raw = self.engine.gd.fanout_cascade_device(self.graph.row_off.data_ptr(), self.graph.dst.data_ptr(),
+                                                       self.graph.n_nodes, seeds.data_ptr() if ns else 0, ns,
+                                                       self.engine.type_code, self.n_act, hops)
+        return [LibraryHop(r) for r in raw]
+
+    def fetch(self, hops: List["LibraryHop"]) -> List[dict]:
+        return [self.engine.gd.fanout_multi_fetch(i, h.raw, self.n_act) for i, h in enumerate(hops)]
+
+
 class LibraryHop:
     """One hop of gd_fanout_multi_device on this rank: counts, plus the library's device pointers
     (valid until the next cascade on the handle)."""

@@ -60,7 +60,7 @@ EXPORTED_SYMBOLS = [
     "gd_actdir_add", "gd_actdir_remove", "gd_actdir_set_flags", "gd_actdir_lookup", "gd_actdir_clear",
     "gd_actdir_count", "gd_receive", "gd_receive_device", "gd_receive_frames_device", "gd_receive_frames",
     "gd_fanout_multi_device", "gd_fanout_multi", "gd_fanout_multi_fetch", "gd_dir_handoff_multi",
-    "gd_fanout_multi_part_device",
+    "gd_fanout_multi_part_device", "gd_fanout_cascade_device",
     "gd_dir_handoff_fetch",
 ]
 
@@ -313,6 +313,7 @@ def _load() -> C.CDLL:
         "gd_route_multi_ext": (C.c_int, [P, P, C.POINTER(gd_key_ext), U32, U32, C.c_int, C.POINTER(gd_multi_result)]),
         "gd_fanout_multi_device": (C.c_int, [P, P, P, U32, P, U32, C.c_int32, U32, U32, P]),
         "gd_fanout_multi_part_device": (C.c_int, [P, P, P, U32, P, P, U32, C.c_int32, U32, P]),
+        "gd_fanout_cascade_device": (C.c_int, [P, P, P, U32, P, U32, C.c_int32, U32, U32, P]),
         "gd_fanout_multi": (C.c_int, [P, P, P, U32, P, U32, C.c_int32, U32, U32, P]),
         "gd_fanout_multi_fetch": (C.c_int, [P, U32] + [P] * 9),
         "gd_dir_handoff_multi": (C.c_int, [P, P, U32, C.c_int, U32, C.POINTER(gd_handoff_result)]),
@@ -1097,6 +1098,15 @@ class GrainDispatch:
         self._c(lib.gd_fanout_multi_part_device(self.h, C.c_void_p(d_row_off), C.c_void_p(d_dst or 0), n_rows,
                                                 C.c_void_p(d_node_of or 0), C.c_void_p(d_seeds or 0), n_seeds,
                                                 type_code, hops, out))
+        return list(out)
+
+    def fanout_cascade_device(self, d_row_off: int, d_dst: int, n_nodes: int, d_seeds: int, n_seeds: int,
+                              type_code: int, n_act: int, hops: int):
+        """gd_fanout_cascade_device: the one-GPU cascade inside the library; gd_fanout_hop list (device
+        pointers into library buffers, src NULL), hops copied out with fanout_multi_fetch."""
+        out = (gd_fanout_hop * hops)()
+        self._c(lib.gd_fanout_cascade_device(self.h, C.c_void_p(d_row_off), C.c_void_p(d_dst or 0), n_nodes,
+                                             C.c_void_p(d_seeds or 0), n_seeds, type_code, n_act, hops, out))
         return list(out)
 
     def fanout_multi(self, row_off, dst, seeds, type_code: int, n_act: int, hops: int) -> List[dict]:

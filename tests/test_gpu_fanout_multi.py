@@ -225,6 +225,41 @@ def test_fanout_multi_world1_rccl_equals_fused_cascade(gd):
     e.close()
 
 
+def test_library_cascade_equals_host_driven_cascade(gd):
+    """gd_fanout_cascade_device (the one-GPU cascade inside the library, one read-back a hop) gives
+    exactly the host-driven cascade's hops (FanoutCascade: gd_fanout_route_bucket_device +
+    gd_frontier_next_device per hop): frontiers, targets, senders, routes, buckets."""
+    import torch
+    from orleans_amd.fanout import DeviceFanoutEngine, FanoutCascade, LibraryCascade, upload_graph
+    n, hops = 200000, 4
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    ro, dst = power_law_graph(n, 8.0, seed=15, max_deg=20000)
+    own = _owners(spec, n)
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 19, my_silo=0)
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+    reg = np.arange(n)[np.arange(n) % 17 != 3]                   # some followers have no activation
+    e.register(o.grain_keys(TC, reg), reg.astype(np.uint32), own[reg])
+    dev = torch.device("cuda", 0)
+    eng = DeviceFanoutEngine(e, dev, TC)
+    g = upload_graph(ro, dst, dev)
+    seeds = np.unique(np.random.default_rng(16).choice(reg, 700)).astype(np.uint32)
+    t_seeds = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    lc = LibraryCascade(eng, g, n)
+    got = lc.fetch(lc.run(t_seeds, hops))
+    ref = FanoutCascade(eng, g, n).run(t_seeds, hops)
+    eng.synchronize()
+    u = lambda t: t.cpu().numpy().view(np.uint32)  # noqa: E731
+    assert sum(x["target"].size for x in got) > 100000
+    for h in range(hops):
+        np.testing.assert_array_equal(got[h]["frontier"], u(ref[h].frontier), err_msg=f"hop {h}")
+        for k in ("target", "sender", "silo", "act", "perm", "offsets"):
+            np.testing.assert_array_equal(got[h][k], u(getattr(ref[h], k)), err_msg=f"hop {h} {k}")
+        np.testing.assert_array_equal(got[h]["status"], ref[h].status.cpu().numpy())
+        assert (got[h]["src"] == 0).all()
+    e.close()
+
+
 def test_cfg4_full_size_properties(gd):
     """BASELINE cfg 4 at its size on one GPU: 10M grains, ~100M follower edges (power law, mean 10,
     cap 65,536; the bench's graph), 65,536 seeds, 3 hops.  Size-independent properties of every hop
