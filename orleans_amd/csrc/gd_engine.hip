@@ -4668,6 +4668,7 @@ int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uin
                           (const uint32_t*)H0[0].p, nf, n_act, visited));
         }
     }
+    uint64_t total = 0;
     for (uint32_t hp = 0; hp < hops; ++hp) {
         std::array<DevBuf, 10>& H = h->fm_hop[hp];
         const uint32_t* frontier = (const uint32_t*)H[0].p;
@@ -4683,9 +4684,9 @@ int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uin
             }
             res.frontier = (const uint32_t*)H[9].p;
         }
-        // 1. expand this rank's publishers (follower lists in enumeration order)
-        uint64_t total = 0;
-        GD_TRY(fan_count(h, row_off, n_nodes, frontier, nf, &total));
+        // 1. expand this rank's publishers (follower lists in enumeration order); hop 0 counts here,
+        //    later hops were counted with the previous hop's frontier (one read-back for both)
+        if (hp == 0) GD_TRY(fan_count(h, row_off, n_nodes, frontier, nf, &total));
         const uint32_t n = (uint32_t)total;
         res.n_sent = total;
         GD_TRY(ensure(h, S[0], (size_t)n * 4 + 16));
@@ -4741,11 +4742,14 @@ int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uin
         res.status = st;
         res.perm = perm;
         res.offsets = offs;
-        // 5. the next publishers: this rank's activations that got a chirp and have not published
+        // 5. the next publishers: this rank's activations that got a chirp and have not published; their
+        //    count stays on the device until the next hop's degree scan reads it back with its total
         if (hp + 1 < hops) {
             std::array<DevBuf, 10>& N = h->fm_hop[hp + 1];
             GD_TRY(ensure(h, N[0], ((size_t)n_act + 4) * 4));
-            GD_TRY(frontier_next(h, offs, n_act, visited, (uint32_t*)N[0].p, &nf));
+            const uint32_t* d_nf = nullptr;
+            GD_TRY(frontier_next_dev(h, offs, n_act, visited, (uint32_t*)N[0].p, &d_nf));
+            GD_TRY(fan_count_dev(h, row_off, n_nodes, (const uint32_t*)N[0].p, d_nf, n_act, &nf, &total));
         }
     }
     if (out) std::copy(h->fm_res.begin(), h->fm_res.end(), out);
