@@ -2907,7 +2907,9 @@ int fanout_cascade(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, u
             GD_TRY(ensure(h, N[0], ((size_t)n_act + 4) * 4));
             const uint32_t* d_nf = nullptr;
             GD_TRY(frontier_next_dev(h, offs, n_act, visited, (uint32_t*)N[0].p, &d_nf));
-            GD_TRY(fan_count_dev(h, row_off, n_nodes, (const uint32_t*)N[0].p, d_nf, n_act, &nf, &total));
+            // every new publisher received at least one of this hop's m messages: the scan's bound
+            GD_TRY(fan_count_dev(h, row_off, n_nodes, (const uint32_t*)N[0].p, d_nf, std::min(n_act, m), &nf,
+                                 &total));
         }
     }
     if (out) std::copy(h->fm_res.begin(), h->fm_res.end(), out);
@@ -4749,7 +4751,9 @@ int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uin
             GD_TRY(ensure(h, N[0], ((size_t)n_act + 4) * 4));
             const uint32_t* d_nf = nullptr;
             GD_TRY(frontier_next_dev(h, offs, n_act, visited, (uint32_t*)N[0].p, &d_nf));
-            GD_TRY(fan_count_dev(h, row_off, n_nodes, (const uint32_t*)N[0].p, d_nf, n_act, &nf, &total));
+            // every new publisher received at least one of this hop's m messages: the scan's bound
+            GD_TRY(fan_count_dev(h, row_off, n_nodes, (const uint32_t*)N[0].p, d_nf, std::min(n_act, m), &nf,
+                                 &total));
         }
     }
     if (out) std::copy(h->fm_res.begin(), h->fm_res.end(), out);
