@@ -186,12 +186,13 @@ struct gd_handle {
     DevBuf tune_buf;            // gd_tune_agree's send / receive records
     uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
     // per launch kind and size class: the probe variant, timed on live launches.  Variants: 0 the index
-    // in 64-B group reads, 1 the directory, 2 the index in 16-B slot reads
-    static constexpr int CXV = 3;
+    // in 64-B group reads, 1 the directory, 2 the index in 16-B slot reads, 3 the 8-B index (24-B keys)
+    static constexpr int CXV = 4;
     struct CxTune {
         int pick = -1;          // -1 measuring, else the variant
         int round = 0;
-        float best[CXV] = {1e30f, 1e30f, 1e30f};
+        int nvar = 0;           // the variants this entry measures (the 8-B index only where it is built)
+        float best[CXV] = {1e30f, 1e30f, 1e30f, 1e30f};
         hipEvent_t a[CXV] = {}, b[CXV] = {};
         bool pending[CXV] = {};
         uint64_t n[CXV] = {};
@@ -203,6 +204,10 @@ struct gd_handle {
     uint64_t cx_cap_at = 0, cx_gen_at = 0;
     uint32_t cx_rounds = 0;
     DevBuf cxi_tab, cxi_types, cxi_ctr;
+    bool cx8_ok = false;        // the 8-B index (gd_cx.h k_cx8_build) is built and current with cx
+    uint32_t cx8_rounds = 0;
+    uint64_t cx8_tcd = 0;
+    DevBuf cx8_tab;
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
     bool hist_xcd = true;       // multi-tile histograms in reverse XCD tile order (GD_HIST_XCD)
     bool compact_headers = true;    // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
@@ -430,10 +435,31 @@ int cx_ensure(gd_handle* h, bool* ok, uint64_t n) {
     GD_TRY(launch(h, "k_cx_build", g, b, 0, k_cx_build, (const Slot*)h->slots, (unsigned long long)h->capacity,
                   (const unsigned long long*)h->cxi_types.p, (uint4*)h->cxi_tab.p, cap, (CxCounters*)h->cxi_ctr.p));
     CxCounters c{};
+    unsigned long long types[CX_TYPES];
     HIP_TRY(h, hipMemcpyAsync(&c, h->cxi_ctr.p, sizeof c, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(types, h->cxi_types.p, sizeof types, hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     h->cx_built = true;
     h->cx_ok = c.flag == 0 && c.full == 0;
+    // the 8-B index: one type, every N1 < 2^32, activation < 2^24 - 1, silo < 255
+    h->cx8_ok = false;
+    uint32_t ntypes = 0;
+    for (unsigned long long t : types)
+        if (t != CX_NO_TYPE) {
+            ++ntypes;
+            h->cx8_tcd = t;
+        }
+    if (h->cx_ok && c.flag8 == 0 && ntypes == 1) {
+        const unsigned long long cap8 = cap;           // as many 8-B slots as the 16-B index: half its bytes
+        GD_TRY(ensure(h, h->cx8_tab, cap8 * 8));
+        HIP_TRY(h, hipMemsetAsync(h->cx8_tab.p, 0, cap8 * 8, h->stream));
+        GD_TRY(launch(h, "k_cx8_build", g, b, 0, k_cx8_build, (const Slot*)h->slots, (unsigned long long)h->capacity,
+                      (unsigned long long*)h->cx8_tab.p, cap8, (CxCounters*)h->cxi_ctr.p));
+        HIP_TRY(h, hipMemcpyAsync(&c, h->cxi_ctr.p, sizeof c, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(h, hipStreamSynchronize(h->stream));
+        h->cx8_ok = c.full8 == 0;
+        h->cx8_rounds = c.max_rounds8;
+    }
     for (auto& kt : h->cx_tune) {                   // a new table: measure the probes again (not the bucketing)
         if (kt.first / (64 * 32) == GD_TUNE_BUCKET) continue;
         auto& t = kt.second;
@@ -470,7 +496,7 @@ int tune_key(int kind, uint64_t n, int sub) {
 }
 
 // Variants of a tune kind (GD_TUNE_*): the 24-B-key and N1 probes have three, the rest two.
-int tune_nvar(int kind) { return kind <= 1 ? gd_handle::CXV : 2; }
+int tune_nvar(int kind) { return kind == 0 ? 4 : (kind == 1 ? 3 : 2); }
 
 // Folds the entry's finished timings in (events read without a stream sync, unless the entry has
 // timed every variant twice and only waits for them) and picks when every variant is timed.
@@ -511,6 +537,7 @@ int tune_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar, int sub
     if (h->tune_pin[kind] >= 0 && h->tune_pin[kind] < nvar) return h->tune_pin[kind];
     const int key = tune_key(kind, n, sub);
     auto& t = h->cx_tune[key];
+    t.nvar = nvar;
     tune_resolve(t, nvar);
     if (t.pick >= 0) return t.pick;
     const int v = t.round % nvar;
@@ -527,6 +554,7 @@ int cx_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar = gd_handl
     *meas = -1;
     if (h->cx_mode == 2) return 0;
     if (h->cx_mode == 3) return nvar > 2 ? 2 : 0;
+    if (h->cx_mode == 4) return nvar > 3 ? 3 : 0;
     return tune_choose(h, kind, n, meas, nvar);
 }
 
@@ -548,6 +576,10 @@ struct CxMeasure {
     }
 };
 
+Cx8Args cx8_args(gd_handle* h) {
+    return Cx8Args{(const uint4*)h->cx8_tab.p, h->capacity * h->cx_scale, h->cx8_tcd, h->cx8_rounds};
+}
+
 CxArgs cx_args(gd_handle* h) {
     return CxArgs{(const uint4*)h->cxi_tab.p, h->capacity * h->cx_scale, (const unsigned long long*)h->cxi_types.p,
                   h->cx_rounds};
@@ -559,19 +591,24 @@ int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, u
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx, n));
     int meas = -1;
-    const int var = cx ? cx_choose(h, 0, n, &meas) : 1;
+    const int var = cx ? cx_choose(h, 0, n, &meas, h->cx8_ok ? 4 : 3) : 1;
     CxMeasure m(h, meas, n);
+    if (var == 3)
+        return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h),
+                      k_route_m<MODE, M, NT, 0, false, (int)CX_GROUP, true>, keys, n, ring_args(h), table_args(h), silo,
+                      act, status, 0ull, h->route_xcd ? 1u : 0u, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr,
+                      CxArgs{}, cx8_args(h));
     if (var == 0)
         return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h),
                       k_route_m<MODE, M, NT, 0, true>, keys, n, ring_args(h), table_args(h), silo, act, status, 0ull,
-                      h->route_xcd ? 1u : 0u, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, cx_args(h));
+                      h->route_xcd ? 1u : 0u, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, cx_args(h), Cx8Args{});
     if (var == 2)
         return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h),
                       k_route_m<MODE, M, NT, 0, true, 1>, keys, n, ring_args(h), table_args(h), silo, act, status,
-                      0ull, h->route_xcd ? 1u : 0u, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, cx_args(h));
+                      0ull, h->route_xcd ? 1u : 0u, (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, cx_args(h), Cx8Args{});
     return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h), k_route_m<MODE, M, NT>, keys,
                   n, ring_args(h), table_args(h), silo, act, status, 0ull, h->route_xcd ? 1u : 0u,
-                  (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, CxArgs{});
+                  (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, CxArgs{}, Cx8Args{});
 }
 
 // Keys given as N1 alone (u64, or u32 with n1w = 4) with one TypeCodeData (a compact exchange
@@ -584,25 +621,25 @@ int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uin
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx, n));
     int meas = -1;
-    const int var = cx ? cx_choose(h, 1, n, &meas) : 1;
+    const int var = cx ? cx_choose(h, 1, n, &meas, 3) : 1;
     CxMeasure m(h, meas, n);
     if (var == 0 && n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4, true>, k, n, ring_args(h),
-                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h));
+                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h), Cx8Args{});
     if (var == 0)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8, true>, k, n, ring_args(h),
-                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h));
+                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h), Cx8Args{});
     if (var == 2 && n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4, true, 1>, k, n, ring_args(h),
-                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h));
+                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h), Cx8Args{});
     if (var == 2)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8, true, 1>, k, n, ring_args(h),
-                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h));
+                      table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h), Cx8Args{});
     if (n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4>, k, n, ring_args(h), table_args(h),
-                      silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{});
+                      silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{}, Cx8Args{});
     return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8>, k, n, ring_args(h), table_args(h),
-                  silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{});
+                  silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{}, Cx8Args{});
 }
 
 // src (optional): also the sender rank of every message, from the per-sender counts rcnt[world].
@@ -1485,6 +1522,7 @@ void gd_destroy(gd_handle* h) {
     if (h->cslots) (void)hipFree(h->cslots);
     free_buf(h->cx_heap);
     free_buf(h->cxi_tab);
+    free_buf(h->cx8_tab);
     free_buf(h->cxi_types);
     free_buf(h->cxi_ctr);
     for (auto& kt : h->cx_tune)
@@ -1964,7 +2002,7 @@ int gd_option_set(gd_handle* h, int option, int64_t v) {
     auto in = [&](int64_t lo, int64_t hi) { return v >= lo && v <= hi; };
     switch (option) {
         case GD_OPT_PROBE:
-            if (!in(0, 3)) break;
+            if (!in(0, 4)) break;
             h->cx_mode = (int)v;
             return GD_OK;
         case GD_OPT_BUCKET:
@@ -4436,21 +4474,22 @@ int gd_tune_agree(gd_handle* h) {
         uint32_t key;
         float best[gd_handle::CXV];
     };
-    static_assert(sizeof(Rec) == 16, "16-B records");
+    static_assert(sizeof(Rec) == 4 + 4 * gd_handle::CXV, "packed records");
     constexpr uint32_t MAXE = 1023;                      // entries a rank contributes (+ a count record)
     const int W = h->n_ranks;
-    std::vector<Rec> mine(MAXE + 1, Rec{0, {0.f, 0.f, 0.f}});
+    std::vector<Rec> mine(MAXE + 1, Rec{0, {}});
     uint32_t ne = 0;
     for (auto& kt : h->cx_tune) {
-        const int nvar = tune_nvar(kt.first / (64 * 32));
         auto& t = kt.second;
+        const int nvar = t.nvar ? t.nvar : tune_nvar(kt.first / (64 * 32));
         tune_resolve(t, nvar);
         bool done = true;
         for (int v = 0; v < nvar; ++v) done = done && t.best[v] < 1e29f;
         if (!done || ne == MAXE) continue;
         Rec& r = mine[1 + ne++];
         r.key = (uint32_t)kt.first;
-        for (int v = 0; v < gd_handle::CXV; ++v) r.best[v] = v < nvar ? t.best[v] : 0.f;
+        // a variant this rank does not have (the 8-B index not built here) can never win the sum
+        for (int v = 0; v < gd_handle::CXV; ++v) r.best[v] = v < nvar ? t.best[v] : 1e30f;
     }
     mine[0].key = ne;
     const size_t bytes = (size_t)(MAXE + 1) * sizeof(Rec);
@@ -4474,12 +4513,12 @@ int gd_tune_agree(gd_handle* h) {
         const Rec* rr = all.data() + (size_t)(MAXE + 1) * r;
         const uint32_t cnt = std::min(rr[0].key, MAXE);
         for (uint32_t i = 0; i < cnt; ++i) {
-            auto& s = sum.try_emplace(rr[1 + i].key, std::array<double, gd_handle::CXV>{0.0, 0.0, 0.0}).first->second;
+            auto& s = sum.try_emplace(rr[1 + i].key, std::array<double, gd_handle::CXV>{}).first->second;
             for (int v = 0; v < gd_handle::CXV; ++v) s[v] += (double)rr[1 + i].best[v];
         }
     }
     for (const auto& ks : sum) {
-        const int kind = (int)ks.first / (64 * 32), nvar = tune_nvar(kind);
+        const int kind = (int)ks.first / (64 * 32), nvar = tune_nvar(kind);   // unavailable ones sum past 1e30
         int pick = 0;
         for (int v = 1; v < nvar; ++v)
             if (ks.second[v] < ks.second[pick]) pick = v;

@@ -167,6 +167,20 @@ __host__ __device__ __forceinline__ uint32_t cx_type_home(uint64_t tcd) {
 __host__ __device__ __forceinline__ unsigned long long cx_home(uint32_t h, unsigned long long cap) {
     return (((unsigned long long)fmix32(h) * cap) >> 32) & ~(unsigned long long)(CX_GROUP - 1);
 }
+// The 8-B index (round 4): when the directory holds one TypeCodeData, every N1 < 2^32, every
+// activation < 2^24 - 1 (or GD_ACT_MULTI) and every silo < 255, a slot is {N1 low word, (silo + 1) << 24 |
+// act} -- 0 = empty -- half the 16-B index at the same load, 8 slots a 64-B read (cx8 in gd_cx.h).
+constexpr uint32_t CX8_GROUP = 8;
+constexpr uint32_t CX8_ACT_MULTI = 0xFFFFFFu;
+struct Cx8Args {
+    const uint4* slots;            // two 8-B slots an uint4
+    unsigned long long cap;        // slots, a multiple of CX8_GROUP
+    uint64_t tcd;                  // the one TypeCodeData
+    uint32_t max_rounds;           // groups past the home group any entry sits
+};
+__host__ __device__ __forceinline__ unsigned long long cx8_home(uint32_t h, unsigned long long cap) {
+    return (((unsigned long long)fmix32(h) * cap) >> 32) & ~(unsigned long long)(CX8_GROUP - 1);
+}
 // Type index of tcd in the staged type set, or -1.
 __device__ __forceinline__ int cx_type_index(const unsigned long long* s_types, uint64_t tcd) {
     uint32_t t = cx_type_home(tcd);
@@ -288,15 +302,17 @@ __device__ __forceinline__ void st(T* p, T v) {
 // The per-thread part: messages base + j * STRIDE, j < M; lds_act (optional) gets act too.
 // CX: probe the compact index (cx, its type set staged in s_types) instead of the directory, RG slots
 // (16 B each) a read: CX_GROUP (one 64-B atom, the layout's group) or 1 (16 B, for hot key sets).
+// CX8: probe the 8-B index (cx8) instead, one 64-B group (8 slots) a read.
 template <int MODE, int M, int STRIDE, bool NT, int N1W, bool NT_SIDE = false, bool CX = false,
-          int RG_CX = (int)CX_GROUP>
+          int RG_CX = (int)CX_GROUP, bool CX8 = false>
 __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, uint32_t n, uint32_t base,
                                              const RingArgs& ring, const uint32_t* s_pts, const uint32_t* s_own,
                                              const TableArgs& tab, uint32_t max_probe,
                                              uint32_t* __restrict__ out_silo, uint32_t* __restrict__ out_act,
                                              uint8_t* __restrict__ out_status, uint64_t tcd_u,
                                              uint32_t* lds_act, uint32_t lds_stride, const CxArgs* cx = nullptr,
-                                             const unsigned long long* s_types = nullptr) {
+                                             const unsigned long long* s_types = nullptr,
+                                             const Cx8Args* cx8 = nullptr) {
 
     uint64_t n0[M], n1[M], tcd[M];
     uint32_t h[M], silo[M], act[M];
@@ -393,6 +409,59 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
                 if (s[j] >= cx->cap) s[j] = 0;
 #pragma unroll
                 for (int g = 0; g < RG_CX; ++g) q[j][g] = cx->slots[s[j] + g];
+            }
+        }
+    } else if constexpr (CX8) {
+        static_assert(!CX, "one index form a launch");
+        // one type, N1 < 2^32 in every entry: any other key is a miss without a probe
+        const uint32_t bound = cx8->max_rounds;
+        bool want[M];
+        unsigned long long s[M];
+        uint4 q[M][CX8_GROUP / 2];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            want[j] = need[j] && n0[j] == 0 && tcd[j] == cx8->tcd && (n1[j] >> 32) == 0;
+            s[j] = cx8_home(h[j], cx8->cap);
+            if (want[j]) {
+                const uint4* qp = cx8->slots + (s[j] >> 1);
+#pragma unroll
+                for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q[j][g] = qp[g];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < M; ++j)
+            if (need[j]) silo[j] = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[j])];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            if (!want[j]) continue;
+            const uint32_t key = (uint32_t)n1[j];
+            bool done = false;
+            for (uint32_t p = 0;;) {
+#pragma unroll
+                for (int g = 0; g < (int)CX8_GROUP; ++g) {
+                    if (done) continue;
+                    const uint4 v = q[j][g / 2];
+                    const uint32_t x = (g & 1) ? v.z : v.x, y = (g & 1) ? v.w : v.y;
+                    if (y == 0) {
+                        done = true;                                      // empty: miss
+                    } else if (x == key) {
+                        const uint32_t a = y & CX8_ACT_MULTI;
+                        if (a == CX8_ACT_MULTI) {                         // RandomPlacementDirector.cs:33-53
+                            status[j] = GD_ROUTE_MULTI_ACT;
+                        } else if (tab_silo_valid(tab, (y >> 24) - 1u)) {
+                            act[j] = a;
+                            silo[j] = (y >> 24) - 1u;                     // Message.cs:629-639
+                            status[j] = GD_ROUTE_OK;
+                        }                                                 // else IsValidSilo (:431) -> MISS
+                        done = true;
+                    }
+                }
+                if (done || ++p > bound) break;
+                s[j] += CX8_GROUP;
+                if (s[j] >= cx8->cap) s[j] = 0;
+                const uint4* qp = cx8->slots + (s[j] >> 1);
+#pragma unroll
+                for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q[j][g] = qp[g];
             }
         }
     } else {
@@ -512,13 +581,14 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb, uint32_t x
 
 // src_out (optional, the exchange's receive side): message i's sender rank, from the per-sender
 // receive counts rcnt[world] (k_recv_src's job, done here beside the probe's own writes).
-template <int MODE, int M, bool NT, int N1W = 0, bool CX = false, int RG_CX = (int)CX_GROUP>
+template <int MODE, int M, bool NT, int N1W = 0, bool CX = false, int RG_CX = (int)CX_GROUP, bool CX8 = false>
 __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                    TableArgs tab, uint32_t* __restrict__ out_silo,
                                                    uint32_t* __restrict__ out_act,
                                                    uint8_t* __restrict__ out_status, uint64_t tcd_u, uint32_t xcd,
                                                    const uint32_t* __restrict__ rcnt = nullptr, uint32_t world = 0,
-                                                   uint32_t* __restrict__ src_out = nullptr, CxArgs cx = CxArgs{}) {
+                                                   uint32_t* __restrict__ src_out = nullptr, CxArgs cx = CxArgs{},
+                                                   Cx8Args cx8 = Cx8Args{}) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     __shared__ uint32_t s_soff[257];
     __shared__ unsigned long long s_types[CX ? CX_TYPES : 1];
@@ -538,9 +608,9 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
     // xcd: each XCD routes a contiguous message range (xcd_tile), so the act it writes is the act the
     // same XCD's histogram and scatter workgroups read next (their XCD tile ranges match)
     const uint32_t blk = xcd_tile(blockIdx.x, gridDim.x, xcd);
-    route_m_core<MODE, M, BLOCK, NT, N1W, true, CX, RG_CX>(keys, n, blk * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own,
-                                                   tab, CX ? 0u : tab.ctr->max_probe, out_silo, out_act, out_status,
-                                                   tcd_u, nullptr, 0, &cx, s_types);
+    route_m_core<MODE, M, BLOCK, NT, N1W, true, CX, RG_CX, CX8>(keys, n, blk * (BLOCK * M) + threadIdx.x, ring, s_pts,
+                                                        s_own, tab, (CX || CX8) ? 0u : tab.ctr->max_probe, out_silo,
+                                                        out_act, out_status, tcd_u, nullptr, 0, &cx, s_types, &cx8);
     if (src_out) {
 #pragma unroll
         for (int j = 0; j < M; ++j) {

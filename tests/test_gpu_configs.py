@@ -452,11 +452,11 @@ def test_options_roundtrip_and_range(gd, monkeypatch):
     assert set(defaults) == set(gd.OPTIONS)
     for k, v in defaults.items():
         assert e.get_option(k) == v, k
-    for k, v in {"probe": 3, "bucket": 2, "l2_small": 300, "stable_rank": 0, "wire_headers": 0,
+    for k, v in {"probe": 4, "bucket": 2, "l2_small": 300, "stable_rank": 0, "wire_headers": 0,
                  "region_probe": 1, "idx16": 0, "l2_staged": 9000, "l2_mid": 2000}.items():
         e.set_option(k, v)
         assert e.get_option(k) == v, k
-    for k, bad in {"probe": 4, "bucket": -1, "l2_small": 24577, "l2_mid": 8193, "l2_staged": 1 << 20}.items():
+    for k, bad in {"probe": 5, "bucket": -1, "l2_small": 24577, "l2_mid": 8193, "l2_staged": 1 << 20}.items():
         before = e.get_option(k)
         with pytest.raises(Exception):
             e.set_option(k, bad)

@@ -141,3 +141,77 @@ def test_cx_ineligible_tables_fall_back(gd):
     assert (st[-300:-200] == o.ST_MISS).all() and (st[-200:] == o.ST_OK).all()
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("mode", ["D", "V"])
+def test_cx8_matches_directory_through_changes(gd, mode):
+    """The 8-B index (GD_OPT_PROBE = 4: one type, N1 < 2^32, activations < 2^24 - 1, silos < 255) gives
+    the directory probe's routes through every directory change -- registration, RemoveActivation,
+    multi-activation upserts (GD_ACT_MULTI), IsValidSilo, silo removal, Merge, split-and-move, rehash,
+    clear -- and through the changes that make it ineligible and eligible again (a second type, an
+    N1 past 2^32, an activation past 2^24): keys it cannot hold (other types, N0 != 0, large N1) miss
+    without a probe or fall back to the 16-B index."""
+    rng = np.random.default_rng(43)
+    (a, b), spec = _pair(gd, mode, 1 << 14, "4")
+    G = 6000
+    reg = o.grain_keys(TC, np.arange(G))
+    owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    acts = np.arange(G, dtype=np.uint32) * 7 + 1
+
+    def batch(n=20000, extra=None):
+        pool = np.concatenate([reg, o.grain_keys(TC, np.arange(G, G + 400))] + ([extra] if extra is not None else []))
+        k = pool[rng.integers(0, len(pool), size=n)]
+        k[::97, 0] = 5                                                   # N0 != 0
+        k[::89, 2] = np.uint64(o.type_code_data(o.CAT_GRAIN, 0x777))     # another type
+        k[::83, 1] += np.uint64(1 << 32)                                 # N1 past 2^32
+        return k
+
+    _both((a, b), lambda e: e.register(reg, acts, owner))
+    q = batch()
+    st, silo, act = _same(a, b, q)
+    want = o.route_batch_np(q, spec, o.DirectoryArrays(reg, acts, owner))
+    np.testing.assert_array_equal(st, want[0])
+    np.testing.assert_array_equal(silo, want[1])
+    np.testing.assert_array_equal(act, want[2])
+    _same(a, b, batch(), n_act=int(acts.max()) + 10)
+    _both((a, b), lambda e: e.unregister(reg[::3], acts[::3]))
+    _same(a, b, batch())
+    up = rng.choice(G, size=400, replace=False)
+    ua = acts[up].copy()
+    ua[::2] = 0xFFFFFFFE                                                 # GD_ACT_MULTI
+    _both((a, b), lambda e: e.upsert(reg[up], ua, owner[up]))
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.set_valid_silos([s for s in range(8) if s != 3], 8))
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.remove_silos([5]))
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.set_valid_silos([], 0))
+    # ineligible: an N1 past 2^32, then an activation past 2^24, then a second type; eligible again after
+    big = o.grain_keys(TC, np.array([(1 << 32) + 9]))
+    bown = o.ring_owner_np(spec, o.jenkins_u64x3_np(big[:, 2], big[:, 0], big[:, 1])).astype(np.uint32)
+    _both((a, b), lambda e: e.register(big, [42], bown))
+    st, _, act = _same(a, b, batch(extra=big))
+    _both((a, b), lambda e: e.unregister(big, [42]))
+    far = o.grain_keys(TC, np.array([G + 1000]))
+    fown = o.ring_owner_np(spec, o.jenkins_u64x3_np(far[:, 2], far[:, 0], far[:, 1])).astype(np.uint32)
+    _both((a, b), lambda e: e.register(far, [1 << 24], fown))
+    _same(a, b, batch(extra=far))
+    _both((a, b), lambda e: e.unregister(far, [1 << 24]))
+    other = o.grain_keys(o.grain_type_code("UnitTests.OtherGrain"), np.arange(50))
+    oown = o.ring_owner_np(spec, o.jenkins_u64x3_np(other[:, 2], other[:, 0], other[:, 1])).astype(np.uint32)
+    _both((a, b), lambda e: e.register(other, np.arange(50) + 90000, oown))
+    _same(a, b, batch(extra=other))
+    _both((a, b), lambda e: e.unregister(other, np.arange(50) + 90000))
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.split([0, 1, 2, 3], move=True))
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.rehash(1 << 15))
+    _same(a, b, batch(), n_act=int(acts.max()) + 10)
+    _both((a, b), lambda e: e.clear())
+    _same(a, b, batch())
+    _both((a, b), lambda e: e.register(reg, acts, owner))
+    st, silo, act = _same(a, b, q)
+    np.testing.assert_array_equal(st, want[0])
+    np.testing.assert_array_equal(act, want[2])
+    a.close()
+    b.close()
