@@ -372,8 +372,8 @@ def setup_workload(args, workload, world, rank, local, dev, tcd, msgs, grains):
 SETTLE_STEPS = 8
 # --tune pinned: the variants each workload's measured runs settle on, fixed with
 # gd_tune_set before the first launch -- no settle steps, the same variant on every rank
-PINNED = {"cfg2": {"probe_keys": 3, "probe_n1": 0, "bucket": 1},
-          "cfg3": {"probe_keys": 2, "probe_n1": 2, "bucket": 1},
+PINNED = {"cfg2": {"probe_keys": 3, "probe_n1": 3, "bucket": 1},
+          "cfg3": {"probe_keys": 3, "probe_n1": 3, "bucket": 1},
           "cfg4": {"probe_fanout": 0, "probe_nodes": 0, "bucket": 1}}
 
 

@@ -878,7 +878,7 @@ int gd_set_kernel_timing(gd_handle* h, int enable);
 #define GD_OPT_PROBE        1   /* route probe: 0 directory, 1 measured per launch kind (default),
                                    2 compact index in 64-B group reads, 3 compact index in 16-B slot reads,
                                    4 the 8-B index where the directory allows it (one type, N1 < 2^32,
-                                   activations < 2^24 - 1, silos < 255; else as 2) */
+                                   activation and silo numbers fitting a u32 together; else as 2) */
 #define GD_OPT_BUCKET       2   /* bucketing: 0 LSD passes, 1 measured (default), 2 the two-level form
                                    wherever it applies (batches >= 2^20 messages, n_act < 2^28) */
 #define GD_OPT_L2_SMALL     3   /* two-level three-pass form: ranges of at most this many messages are
@@ -913,7 +913,7 @@ int gd_option_get(const gd_handle* h, int option, int64_t* value);
  * communicator run the same variant. */
 #define GD_TUNE_PROBE_KEYS   0  /* k_route over 24-B keys: 0 index groups, 1 directory, 2 index slots,
                                    3 the 8-B index (when the directory allows it) */
-#define GD_TUNE_PROBE_N1     1  /* the exchange owner's probe over received N1s: same variants */
+#define GD_TUNE_PROBE_N1     1  /* the exchange owner's probe over received N1s: same variants (0..3) */
 #define GD_TUNE_PROBE_FANOUT 2  /* k_fan_route: 0 index groups, 1 directory */
 #define GD_TUNE_PROBE_NODES  3  /* the sharded fan-out owner's probe: 0 index groups, 1 directory */
 #define GD_TUNE_BUCKET       4  /* bucketing: 0 LSD passes, 1 the two-level form */

@@ -23,11 +23,11 @@ struct CxCounters {
     uint32_t flag;         // bit 0: an entry with N0 != 0; bit 1: more than CX_TYPES types
     uint32_t max_rounds;   // CxArgs::max_rounds
     uint32_t full;         // the index ran out of slots (cannot happen at cap >= live)
-    uint32_t flag8;        // the 8-B index: bit 0 an N1 >= 2^32, bit 1 an activation >= 2^24 - 1 (not
-                           // GD_ACT_MULTI), bit 2 a silo >= 255 (one type more: the host counts them)
+    uint32_t flag8;        // the 8-B index: bit 0 an N1 >= 2^32 (one type more: the host counts them)
     uint32_t max_rounds8;  // Cx8Args::max_rounds
     uint32_t full8;
-    uint32_t pad[2];
+    uint32_t act_max;      // the largest activation (GD_ACT_MULTI aside) and silo: the host's bit split
+    uint32_t silo_max;
 };
 
 __global__ void __launch_bounds__(BLOCK) k_cx_types(const Slot* __restrict__ slots, unsigned long long cap,
@@ -41,11 +41,9 @@ __global__ void __launch_bounds__(BLOCK) k_cx_types(const Slot* __restrict__ slo
         atomicOr(&ctr->flag, 1u);
         return;
     }
-    {
-        const uint32_t f8 = (a.w != 0 ? 1u : 0u) | (b.z >= CX8_ACT_MULTI && b.z != GD_ACT_MULTI ? 2u : 0u) |
-                            (slot_silo(b.w) >= 255u ? 4u : 0u);
-        if (f8) atomicOr(&ctr->flag8, f8);
-    }
+    if (a.w != 0) atomicOr(&ctr->flag8, 1u);
+    if (b.z != GD_ACT_MULTI) atomicMax(&ctr->act_max, b.z);
+    atomicMax(&ctr->silo_max, slot_silo(b.w));
     const unsigned long long tcd = (unsigned long long)b.x | ((unsigned long long)b.y << 32);
     // one insert per distinct type in the wave: lanes holding the first lane's type stand down
     const unsigned long long lead = __shfl(tcd, __ffsll((long long)__ballot(1)) - 1);
@@ -104,11 +102,12 @@ __global__ void __launch_bounds__(BLOCK) k_cx_build(const Slot* __restrict__ slo
 }
 
 // The 8-B index (Cx8Args), built after the 16-B one when the host found it eligible (flag8 == 0, one
-// type): slot = (silo + 1) << 24 | act (CX8_ACT_MULTI for a multi-activation grain) above the N1 low
-// word, placed by a 64-bit CAS in probe order from cx8_home.
+// type, activations and silos fitting a u32 together): slot = (silo + 1) << ab | act (all ab bits set
+// for a multi-activation grain) above the N1 low word, placed by a 64-bit CAS in probe order from
+// cx8_home.
 __global__ void __launch_bounds__(BLOCK) k_cx8_build(const Slot* __restrict__ slots, unsigned long long cap,
                                                      unsigned long long* cx8, unsigned long long cx8_cap,
-                                                     CxCounters* ctr) {
+                                                     uint32_t ab, CxCounters* ctr) {
     const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
     uint32_t rounds = 0;
     if (j < cap) {
@@ -117,7 +116,8 @@ __global__ void __launch_bounds__(BLOCK) k_cx8_build(const Slot* __restrict__ sl
         if (slot_state(b.w) == SLOT_LIVE) {
             const uint64_t n1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
             const uint64_t tcd = (uint64_t)b.x | ((uint64_t)b.y << 32);
-            const uint32_t y = ((slot_silo(b.w) + 1u) << 24) | (b.z == GD_ACT_MULTI ? CX8_ACT_MULTI : b.z);
+            const uint32_t am = (1u << ab) - 1u;
+            const uint32_t y = ((slot_silo(b.w) + 1u) << ab) | (b.z == GD_ACT_MULTI ? am : b.z);
             const unsigned long long v = ((unsigned long long)y << 32) | (uint32_t)n1;
             const unsigned long long home = cx8_home(uniform_hash(0, n1, tcd), cx8_cap);
             unsigned long long s = home;

@@ -205,7 +205,7 @@ struct gd_handle {
     uint32_t cx_rounds = 0;
     DevBuf cxi_tab, cxi_types, cxi_ctr;
     bool cx8_ok = false;        // the 8-B index (gd_cx.h k_cx8_build) is built and current with cx
-    uint32_t cx8_rounds = 0;
+    uint32_t cx8_rounds = 0, cx8_ab = 24;
     uint64_t cx8_tcd = 0;
     DevBuf cx8_tab;
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
@@ -441,7 +441,8 @@ int cx_ensure(gd_handle* h, bool* ok, uint64_t n) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     h->cx_built = true;
     h->cx_ok = c.flag == 0 && c.full == 0;
-    // the 8-B index: one type, every N1 < 2^32, activation < 2^24 - 1, silo < 255
+    // the 8-B index: one type, every N1 < 2^32, activation bits ab (all ones left for GD_ACT_MULTI) and
+    // silo + 1 above them in a u32
     h->cx8_ok = false;
     uint32_t ntypes = 0;
     for (unsigned long long t : types)
@@ -449,12 +450,16 @@ int cx_ensure(gd_handle* h, bool* ok, uint64_t n) {
             ++ntypes;
             h->cx8_tcd = t;
         }
-    if (h->cx_ok && c.flag8 == 0 && ntypes == 1) {
+    uint32_t ab = 1;
+    while (ab < 32 && ((uint64_t)c.act_max + 1) >> ab) ++ab;          // act_max < 2^ab - 1
+    const bool fits = ab < 32 && (((uint64_t)c.silo_max + 1) >> (32 - ab)) == 0;
+    h->cx8_ab = ab;
+    if (h->cx_ok && c.flag8 == 0 && ntypes == 1 && fits) {
         const unsigned long long cap8 = cap;           // as many 8-B slots as the 16-B index: half its bytes
         GD_TRY(ensure(h, h->cx8_tab, cap8 * 8));
         HIP_TRY(h, hipMemsetAsync(h->cx8_tab.p, 0, cap8 * 8, h->stream));
         GD_TRY(launch(h, "k_cx8_build", g, b, 0, k_cx8_build, (const Slot*)h->slots, (unsigned long long)h->capacity,
-                      (unsigned long long*)h->cx8_tab.p, cap8, (CxCounters*)h->cxi_ctr.p));
+                      (unsigned long long*)h->cx8_tab.p, cap8, ab, (CxCounters*)h->cxi_ctr.p));
         HIP_TRY(h, hipMemcpyAsync(&c, h->cxi_ctr.p, sizeof c, hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(h, hipStreamSynchronize(h->stream));
         h->cx8_ok = c.full8 == 0;
@@ -496,7 +501,7 @@ int tune_key(int kind, uint64_t n, int sub) {
 }
 
 // Variants of a tune kind (GD_TUNE_*): the 24-B-key and N1 probes have three, the rest two.
-int tune_nvar(int kind) { return kind == 0 ? 4 : (kind == 1 ? 3 : 2); }
+int tune_nvar(int kind) { return kind <= 1 ? 4 : 2; }
 
 // Folds the entry's finished timings in (events read without a stream sync, unless the entry has
 // timed every variant twice and only waits for them) and picks when every variant is timed.
@@ -577,7 +582,7 @@ struct CxMeasure {
 };
 
 Cx8Args cx8_args(gd_handle* h) {
-    return Cx8Args{(const uint4*)h->cx8_tab.p, h->capacity * h->cx_scale, h->cx8_tcd, h->cx8_rounds};
+    return Cx8Args{(const uint4*)h->cx8_tab.p, h->capacity * h->cx_scale, h->cx8_tcd, h->cx8_rounds, h->cx8_ab};
 }
 
 CxArgs cx_args(gd_handle* h) {
@@ -621,8 +626,16 @@ int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uin
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx, n));
     int meas = -1;
-    const int var = cx ? cx_choose(h, 1, n, &meas, 3) : 1;
+    const int var = cx ? cx_choose(h, 1, n, &meas, h->cx8_ok ? 4 : 3) : 1;
     CxMeasure m(h, meas, n);
+    if (var == 3 && n1w == 4)
+        return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4, false, (int)CX_GROUP, true>, k, n,
+                      ring_args(h), table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{},
+                      cx8_args(h));
+    if (var == 3)
+        return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 8, false, (int)CX_GROUP, true>, k, n,
+                      ring_args(h), table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{},
+                      cx8_args(h));
     if (var == 0 && n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4, true>, k, n, ring_args(h),
                       table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, cx_args(h), Cx8Args{});

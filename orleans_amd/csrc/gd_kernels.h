@@ -167,16 +167,17 @@ __host__ __device__ __forceinline__ uint32_t cx_type_home(uint64_t tcd) {
 __host__ __device__ __forceinline__ unsigned long long cx_home(uint32_t h, unsigned long long cap) {
     return (((unsigned long long)fmix32(h) * cap) >> 32) & ~(unsigned long long)(CX_GROUP - 1);
 }
-// The 8-B index (round 4): when the directory holds one TypeCodeData, every N1 < 2^32, every
-// activation < 2^24 - 1 (or GD_ACT_MULTI) and every silo < 255, a slot is {N1 low word, (silo + 1) << 24 |
-// act} -- 0 = empty -- half the 16-B index at the same load, 8 slots a 64-B read (cx8 in gd_cx.h).
+// The 8-B index (round 4): when the directory holds one TypeCodeData and every N1 < 2^32, a slot is
+// {N1 low word, (silo + 1) << ab | act} -- ab bits hold every activation with all ones left for
+// GD_ACT_MULTI, the 32 - ab above them silo + 1; 0 = empty -- half the 16-B index at the same load,
+// 8 slots a 64-B read (cx8 in gd_cx.h).
 constexpr uint32_t CX8_GROUP = 8;
-constexpr uint32_t CX8_ACT_MULTI = 0xFFFFFFu;
 struct Cx8Args {
     const uint4* slots;            // two 8-B slots an uint4
     unsigned long long cap;        // slots, a multiple of CX8_GROUP
     uint64_t tcd;                  // the one TypeCodeData
     uint32_t max_rounds;           // groups past the home group any entry sits
+    uint32_t ab;                   // activation bits
 };
 __host__ __device__ __forceinline__ unsigned long long cx8_home(uint32_t h, unsigned long long cap) {
     return (((unsigned long long)fmix32(h) * cap) >> 32) & ~(unsigned long long)(CX8_GROUP - 1);
@@ -445,12 +446,13 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
                     if (y == 0) {
                         done = true;                                      // empty: miss
                     } else if (x == key) {
-                        const uint32_t a = y & CX8_ACT_MULTI;
-                        if (a == CX8_ACT_MULTI) {                         // RandomPlacementDirector.cs:33-53
+                        const uint32_t am = (1u << cx8->ab) - 1u;
+                        const uint32_t a = y & am, sl = (y >> cx8->ab) - 1u;
+                        if (a == am) {                                    // RandomPlacementDirector.cs:33-53
                             status[j] = GD_ROUTE_MULTI_ACT;
-                        } else if (tab_silo_valid(tab, (y >> 24) - 1u)) {
+                        } else if (tab_silo_valid(tab, sl)) {
                             act[j] = a;
-                            silo[j] = (y >> 24) - 1u;                     // Message.cs:629-639
+                            silo[j] = sl;                                 // Message.cs:629-639
                             status[j] = GD_ROUTE_OK;
                         }                                                 // else IsValidSilo (:431) -> MISS
                         done = true;

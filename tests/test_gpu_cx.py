@@ -143,20 +143,21 @@ def test_cx_ineligible_tables_fall_back(gd):
     b.close()
 
 
-@pytest.mark.parametrize("mode", ["D", "V"])
-def test_cx8_matches_directory_through_changes(gd, mode):
-    """The 8-B index (GD_OPT_PROBE = 4: one type, N1 < 2^32, activations < 2^24 - 1, silos < 255) gives
+@pytest.mark.parametrize("mode,act_base", [("D", 0), ("V", 0), ("D", 1 << 26)])
+def test_cx8_matches_directory_through_changes(gd, mode, act_base):
+    """The 8-B index (GD_OPT_PROBE = 4: one type, N1 < 2^32, activation and silo numbers sharing a u32
+    -- act_base moves the activations to 27 bits, BASELINE cfg 3's range) gives
     the directory probe's routes through every directory change -- registration, RemoveActivation,
     multi-activation upserts (GD_ACT_MULTI), IsValidSilo, silo removal, Merge, split-and-move, rehash,
     clear -- and through the changes that make it ineligible and eligible again (a second type, an
-    N1 past 2^32, an activation past 2^24): keys it cannot hold (other types, N0 != 0, large N1) miss
-    without a probe or fall back to the 16-B index."""
+    N1 past 2^32) or change its bit split (an activation past 2^24): keys it cannot hold (other types,
+    N0 != 0, large N1) miss without a probe or fall back to the 16-B index."""
     rng = np.random.default_rng(43)
     (a, b), spec = _pair(gd, mode, 1 << 14, "4")
     G = 6000
     reg = o.grain_keys(TC, np.arange(G))
     owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
-    acts = np.arange(G, dtype=np.uint32) * 7 + 1
+    acts = (np.arange(G, dtype=np.uint32) * 7 + 1 + act_base).astype(np.uint32)
 
     def batch(n=20000, extra=None):
         pool = np.concatenate([reg, o.grain_keys(TC, np.arange(G, G + 400))] + ([extra] if extra is not None else []))
