@@ -501,7 +501,7 @@ int tune_key(int kind, uint64_t n, int sub) {
 }
 
 // Variants of a tune kind (GD_TUNE_*): the 24-B-key and N1 probes have three, the rest two.
-int tune_nvar(int kind) { return kind <= 1 ? 4 : 2; }
+int tune_nvar(int kind) { return kind <= 1 ? 4 : (kind == 2 ? 3 : 2); }
 
 // Folds the entry's finished timings in (events read without a stream sync, unless the entry has
 // timed every variant twice and only waits for them) and picks when every variant is timed.
@@ -557,9 +557,11 @@ int tune_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar, int sub
 
 int cx_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar = gd_handle::CXV) {
     *meas = -1;
+    // variants: 0 index groups, 1 directory; kinds 0 / 1: 2 index slots, 3 the 8-B index; kind 2: 2 the
+    // 8-B index (when built: nvar says)
     if (h->cx_mode == 2) return 0;
-    if (h->cx_mode == 3) return nvar > 2 ? 2 : 0;
-    if (h->cx_mode == 4) return nvar > 3 ? 3 : 0;
+    if (h->cx_mode == 3) return kind <= 1 && nvar > 2 ? 2 : 0;
+    if (h->cx_mode == 4) return kind <= 1 ? (nvar > 3 ? 3 : 0) : (kind == 2 && nvar > 2 ? 2 : 0);
     return tune_choose(h, kind, n, meas, nvar);
 }
 
@@ -2742,7 +2744,7 @@ int fan_route_launch_cx(gd_handle* h, const uint32_t* row_off, const uint32_t* d
     // 2 outputs a thread in flight (1: 2.95 ms, 4: 3.03 ms against 2.87 ms a cfg 4 cascade,
     // profiles/r02_v1_fanout_cfg4_ilp_ab.jsonl)
     return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2, CX>, row_off, dst, frontier, nf, ends,
-                  total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx);
+                  total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx, Cx8Args{});
 }
 
 template <int MODE>
@@ -2752,8 +2754,15 @@ int fan_route_launch(gd_handle* h, const uint32_t* row_off, const uint32_t* dst,
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx, total));
     int meas = -1;
-    if (cx) cx = cx_choose(h, 2, total, &meas, 2) == 0;
+    const int var = cx ? cx_choose(h, 2, total, &meas, h->cx8_ok ? 3 : 2) : 1;
+    cx = var == 0;
     CxMeasure m(h, meas, total);
+    if (var == 2) {                    // the 8-B index
+        const dim3 g(blocks_for(total, FAN_TILE)), b(BLOCK);
+        return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2, false, (int)CX_GROUP, true>, row_off,
+                      dst, frontier, nf, (const uint32_t*)h->fan[0].p, total, tcd, ring_args(h), table_args(h), target,
+                      sender, silo, act, status, CxArgs{}, cx8_args(h));
+    }
     if (cx)
         return fan_route_launch_cx<MODE, true>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo, act,
                                                status);

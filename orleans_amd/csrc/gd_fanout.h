@@ -227,6 +227,35 @@ __device__ __forceinline__ uint8_t cx_walk_node(const CxArgs& cx, const TableArg
     return st;
 }
 
+// The 8-B index's walk (Cx8Args) from a group already read (q: its 8 slots as 4 uint4): as cx_walk_node.
+__device__ __forceinline__ uint8_t cx8_walk_node(const Cx8Args& cx8, const TableArgs& tab, uint32_t key,
+                                                 unsigned long long s, uint4 (&q)[CX8_GROUP / 2], uint32_t& silo,
+                                                 uint32_t& act) {
+    const uint32_t am = (1u << cx8.ab) - 1u;
+    for (uint32_t p = 0;;) {
+#pragma unroll
+        for (int g = 0; g < (int)CX8_GROUP; ++g) {
+            const uint4 v = q[g / 2];
+            const uint32_t x = (g & 1) ? v.z : v.x, y = (g & 1) ? v.w : v.y;
+            if (y == 0) return GD_ROUTE_MISS;
+            if (x == key) {
+                const uint32_t a = y & am, sl = (y >> cx8.ab) - 1u;
+                if (a == am) return GD_ROUTE_MULTI_ACT;
+                if (!tab_silo_valid(tab, sl)) return GD_ROUTE_MISS;
+                act = a;
+                silo = sl;
+                return GD_ROUTE_OK;
+            }
+        }
+        if (++p > cx8.max_rounds) return GD_ROUTE_MISS;
+        s += CX8_GROUP;
+        if (s >= cx8.cap) s = 0;
+        const uint4* qp = cx8.slots + (s >> 1);
+#pragma unroll
+        for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q[g] = qp[g];
+    }
+}
+
 __device__ __forceinline__ uint32_t cx_want(const CxArgs& cx, uint64_t tcd) {
     const int t = cx_type_index(cx.types, tcd);
     return t < 0 ? 0u : (0x100u | (uint32_t)t);
@@ -272,7 +301,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restric
 // Fused expansion + route.  out_target may be null.  ILP items of a thread at a time: their
 // follower-list reads, then their first directory probes, are in flight together (one dependent
 // chain per item otherwise).
-template <int MODE, int ILP, bool CX = false, int RG = (int)CX_GROUP>
+template <int MODE, int ILP, bool CX = false, int RG = (int)CX_GROUP, bool CX8 = false>
 __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict__ row_off,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint32_t* __restrict__ frontier, uint32_t n_front,
@@ -281,7 +310,8 @@ __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ out_target,
                                                      uint32_t* __restrict__ out_sender,
                                                      uint32_t* __restrict__ out_silo, uint32_t* __restrict__ out_act,
-                                                     uint8_t* __restrict__ out_status, CxArgs cx = CxArgs{}) {
+                                                     uint8_t* __restrict__ out_status, CxArgs cx = CxArgs{},
+                                                     Cx8Args cx8 = Cx8Args{}) {
     static_assert(FAN_IT % ILP == 0, "whole rounds");
     __shared__ FanStage s;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
@@ -306,6 +336,35 @@ __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict_
         }
 #pragma unroll
         for (int q = 0; q < ILP; ++q) target[q] = live[q] ? dst[j[q]] : 0u;
+        if constexpr (CX8) {                                  // the 8-B index (gd_kernels.h Cx8Args)
+            const bool want = tcd == cx8.tcd;                 // node grains: N0 = 0, N1 = node < 2^32
+            unsigned long long s8[ILP];
+            uint4 q8[ILP][CX8_GROUP / 2];
+#pragma unroll
+            for (int q = 0; q < ILP; ++q) {
+                h[q] = uniform_hash(0, target[q], tcd);
+                s8[q] = cx8_home(h[q], cx8.cap);
+                if (live[q] && want) {
+                    const uint4* qp = cx8.slots + (s8[q] >> 1);
+#pragma unroll
+                    for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q8[q][g] = qp[g];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < ILP; ++q) {
+                if (!live[q]) continue;
+                const uint32_t p = p0 + (it0 + q) * BLOCK + threadIdx.x;
+                uint32_t silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[q])], act = NONE32;
+                const uint8_t st = want ? cx8_walk_node(cx8, tab, target[q], s8[q], q8[q], silo, act)
+                                        : (uint8_t)GD_ROUTE_MISS;
+                if (out_target) out_target[p] = target[q];
+                out_sender[p] = sender[q];
+                out_silo[p] = silo;
+                out_act[p] = act;
+                out_status[p] = st;
+            }
+            continue;
+        }
         if constexpr (CX) {                                   // the compact probe index (gd_kernels.h)
             const uint32_t want = cx_want(cx, tcd);
             unsigned long long sc[ILP];

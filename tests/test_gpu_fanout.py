@@ -20,13 +20,14 @@ def gd():
     return g
 
 
-def _setup(gd, n_nodes, mode="D", registered=None, cap=None):
+def _setup(gd, n_nodes, mode="D", registered=None, cap=None, probe=None):
     silos = o.bench_silos(8)
     spec = o.ring_spec(silos, mode)
     reg_nodes = np.arange(n_nodes) if registered is None else np.asarray(registered)
     reg = o.grain_keys(TC, reg_nodes)
     owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
-    e = gd.GrainDispatch(device=0, table_capacity=cap or max(1024, 2 * len(reg_nodes)))
+    e = gd.GrainDispatch(device=0, table_capacity=cap or max(1024, 2 * len(reg_nodes)),
+                         options=None if probe is None else {"probe": probe})
     e.ring_set_silos(mode, [(s.ip, s.port, s.gen) for s in silos])
     e.register(reg, reg_nodes.astype(np.uint32), owner)
     d = o.DirectoryArrays(reg, reg_nodes.astype(np.uint32), owner)
@@ -40,13 +41,14 @@ def _want_hop(ro, dst, frontier, spec, d, n_act):
     return dict(target=t, sender=s, status=st, silo=silo, act=act, perm=perm, offsets=off)
 
 
-@pytest.mark.parametrize("mode", ["D", "R", "V"])
-def test_fanout_hop_vs_oracle(gd, mode):
+@pytest.mark.parametrize("mode,probe", [("D", None), ("R", None), ("V", None), ("D", 0), ("D", 2), ("V", 4)])
+def test_fanout_hop_vs_oracle(gd, mode, probe):
+    """probe: the route's probe forced (0 directory, 2 the 16-B index, 4 the 8-B index), None measured."""
     n = 6000
     ro, dst = power_law_graph(n, 8.0, seed=11, max_deg=3000)
     rng = np.random.default_rng(12)
     registered = np.sort(rng.choice(n, size=int(n * 0.95), replace=False))     # 5% MISS
-    e, spec, d = _setup(gd, n, mode, registered)
+    e, spec, d = _setup(gd, n, mode, registered, probe=probe)
     frontier = np.concatenate([rng.integers(0, n, 700), [3, 3, 3], [n, n + 5, 0xFFFFFFF0]]).astype(np.uint32)
     got = e.fanout_route_bucket(ro, dst, frontier, TC, n)
     want = _want_hop(ro, dst, frontier, spec, d, n)
