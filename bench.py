@@ -374,7 +374,7 @@ SETTLE_STEPS = 8
 # gd_tune_set before the first launch -- no settle steps, the same variant on every rank
 PINNED = {"cfg2": {"probe_keys": 3, "probe_n1": 3, "bucket": 1},
           "cfg3": {"probe_keys": 3, "probe_n1": 3, "bucket": 1},
-          "cfg4": {"probe_fanout": 2, "probe_nodes": 0, "bucket": 1}}
+          "cfg4": {"probe_fanout": 2, "probe_nodes": 2, "bucket": 1}}
 
 
 def silos_note(which: str) -> str:

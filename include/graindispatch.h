@@ -915,7 +915,7 @@ int gd_option_get(const gd_handle* h, int option, int64_t* value);
                                    3 the 8-B index (when the directory allows it) */
 #define GD_TUNE_PROBE_N1     1  /* the exchange owner's probe over received N1s: same variants (0..3) */
 #define GD_TUNE_PROBE_FANOUT 2  /* k_fan_route: 0 index groups, 1 directory, 2 the 8-B index */
-#define GD_TUNE_PROBE_NODES  3  /* the sharded fan-out owner's probe: 0 index groups, 1 directory */
+#define GD_TUNE_PROBE_NODES  3  /* the sharded fan-out owner's probe: 0 index groups, 1 directory, 2 the 8-B index */
 #define GD_TUNE_BUCKET       4  /* bucketing: 0 LSD passes, 1 the two-level form */
 #define GD_TUNE_KINDS        5
 int gd_tune_reset(gd_handle* h);                         /* forget every measured choice */

@@ -501,7 +501,7 @@ int tune_key(int kind, uint64_t n, int sub) {
 }
 
 // Variants of a tune kind (GD_TUNE_*): the 24-B-key and N1 probes have three, the rest two.
-int tune_nvar(int kind) { return kind <= 1 ? 4 : (kind == 2 ? 3 : 2); }
+int tune_nvar(int kind) { return kind <= 1 ? 4 : (kind <= 3 ? 3 : 2); }
 
 // Folds the entry's finished timings in (events read without a stream sync, unless the entry has
 // timed every variant twice and only waits for them) and picks when every variant is timed.
@@ -557,11 +557,11 @@ int tune_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar, int sub
 
 int cx_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar = gd_handle::CXV) {
     *meas = -1;
-    // variants: 0 index groups, 1 directory; kinds 0 / 1: 2 index slots, 3 the 8-B index; kind 2: 2 the
-    // 8-B index (when built: nvar says)
+    // variants: 0 index groups, 1 directory; kinds 0 / 1: 2 index slots, 3 the 8-B index; kinds 2 / 3:
+    // 2 the 8-B index (when built: nvar says)
     if (h->cx_mode == 2) return 0;
     if (h->cx_mode == 3) return kind <= 1 && nvar > 2 ? 2 : 0;
-    if (h->cx_mode == 4) return kind <= 1 ? (nvar > 3 ? 3 : 0) : (kind == 2 && nvar > 2 ? 2 : 0);
+    if (h->cx_mode == 4) return kind <= 1 ? (nvar > 3 ? 3 : 0) : ((kind == 2 || kind == 3) && nvar > 2 ? 2 : 0);
     return tune_choose(h, kind, n, meas, nvar);
 }
 
@@ -2789,13 +2789,16 @@ int fan_route(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const 
 
 template <int MODE>
 int route_nodes_mode(gd_handle* h, const uint32_t* nodes, uint32_t n, uint64_t tcd, uint32_t* silo, uint32_t* act,
-                     uint8_t* status, bool cx) {
+                     uint8_t* status, bool cx, bool cx8 = false) {
     const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    if (cx8)
+        return launch(h, "k_route_nodes", g, b, ring_lds(h), k_route_nodes<MODE, false, (int)CX_GROUP, true>, nodes, n,
+                      tcd, ring_args(h), table_args(h), silo, act, status, CxArgs{}, cx8_args(h));
     if (cx)
         return launch(h, "k_route_nodes", g, b, ring_lds(h), k_route_nodes<MODE, true>, nodes, n, tcd, ring_args(h),
-                      table_args(h), silo, act, status, cx_args(h));
+                      table_args(h), silo, act, status, cx_args(h), Cx8Args{});
     return launch(h, "k_route_nodes", g, b, ring_lds(h), k_route_nodes<MODE, false>, nodes, n, tcd, ring_args(h),
-                  table_args(h), silo, act, status, CxArgs{});
+                  table_args(h), silo, act, status, CxArgs{}, Cx8Args{});
 }
 
 int route_nodes(gd_handle* h, const uint32_t* nodes, uint32_t n, uint64_t tcd, uint32_t* silo, uint32_t* act,
@@ -2805,12 +2808,16 @@ int route_nodes(gd_handle* h, const uint32_t* nodes, uint32_t n, uint64_t tcd, u
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx, n));
     int meas = -1;
-    if (cx) cx = cx_choose(h, 3, n, &meas, 2) == 0;
+    const int var = cx ? cx_choose(h, 3, n, &meas, h->cx8_ok ? 3 : 2) : 1;
+    cx = var == 0;
+    const bool cx8 = var == 2;
     CxMeasure m(h, meas, n);
     switch (h->ring_mode) {
-        case GD_RING_DIRECTORY: return route_nodes_mode<GD_RING_DIRECTORY>(h, nodes, n, tcd, silo, act, status, cx);
-        case GD_RING_CONSISTENT: return route_nodes_mode<GD_RING_CONSISTENT>(h, nodes, n, tcd, silo, act, status, cx);
-        default: return route_nodes_mode<GD_RING_VIRTUAL_BUCKETS>(h, nodes, n, tcd, silo, act, status, cx);
+        case GD_RING_DIRECTORY:
+            return route_nodes_mode<GD_RING_DIRECTORY>(h, nodes, n, tcd, silo, act, status, cx, cx8);
+        case GD_RING_CONSISTENT:
+            return route_nodes_mode<GD_RING_CONSISTENT>(h, nodes, n, tcd, silo, act, status, cx, cx8);
+        default: return route_nodes_mode<GD_RING_VIRTUAL_BUCKETS>(h, nodes, n, tcd, silo, act, status, cx, cx8);
     }
 }
 

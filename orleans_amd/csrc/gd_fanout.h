@@ -263,21 +263,36 @@ __device__ __forceinline__ uint32_t cx_want(const CxArgs& cx, uint64_t tcd) {
 
 // Route a batch of node ids (GrainId(typeCode, node), the owner side of the sharded fan-out).
 // CX: through the compact probe index.
-template <int MODE, bool CX = false, int RG = (int)CX_GROUP>
+template <int MODE, bool CX = false, int RG = (int)CX_GROUP, bool CX8 = false>
 __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restrict__ nodes, uint32_t n, uint64_t tcd,
                                                        RingArgs ring, TableArgs tab, uint32_t* __restrict__ out_silo,
                                                        uint32_t* __restrict__ out_act,
-                                                       uint8_t* __restrict__ out_status, CxArgs cx = CxArgs{}) {
+                                                       uint8_t* __restrict__ out_status, CxArgs cx = CxArgs{},
+                                                       Cx8Args cx8 = Cx8Args{}) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
     stage_ring(ring, s_pts, s_own);
-    const uint32_t max_probe = CX ? 0u : tab.ctr->max_probe;
+    const uint32_t max_probe = (CX || CX8) ? 0u : tab.ctr->max_probe;
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     uint32_t silo, act;
     uint8_t st;
-    if constexpr (CX) {
+    if constexpr (CX8) {                               // the 8-B index (gd_kernels.h Cx8Args)
+        const bool want = tcd == cx8.tcd;
+        const uint32_t node = nodes[i];
+        const uint32_t h = uniform_hash(0, node, tcd);
+        const unsigned long long s0 = cx8_home(h, cx8.cap);
+        uint4 q[CX8_GROUP / 2];
+        if (want) {
+            const uint4* qp = cx8.slots + (s0 >> 1);
+#pragma unroll
+            for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q[g] = qp[g];
+        }
+        silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h)];
+        act = NONE32;
+        st = want ? cx8_walk_node(cx8, tab, node, s0, q, silo, act) : (uint8_t)GD_ROUTE_MISS;
+    } else if constexpr (CX) {
         const uint32_t want = cx_want(cx, tcd);
         const uint32_t node = nodes[i];
         const uint32_t h = uniform_hash(0, node, tcd);

@@ -129,10 +129,12 @@ def test_cascade_device_vs_oracle(gd, mode):
     e.close()
 
 
-def test_route_nodes_pack_and_frontier_vs_oracle(gd):
+@pytest.mark.parametrize("probe", [None, 0, 4])
+def test_route_nodes_pack_and_frontier_vs_oracle(gd, probe):
+    """probe: the node route's probe forced (0 directory, 4 the 8-B index), None measured."""
     import torch
     n = 50000
-    e, spec, d = _setup(gd, n, "D", np.arange(0, n, 2))          # odd nodes unregistered
+    e, spec, d = _setup(gd, n, "D", np.arange(0, n, 2), probe=probe)   # odd nodes unregistered
     eng = _device(gd, e)
     rng = np.random.default_rng(9)
     nodes = rng.integers(0, n + 100, 100000).astype(np.uint32)
