@@ -1000,7 +1000,8 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     def step():
         return runner.run(t_seeds, args.hops)
 
-    for _ in range(settle_steps(args) // 2):         # cascades: the measured choices per hop size
+    for _ in range(settle_steps(args)):              # cascades: the measured choices per hop size (3 fan-out
+        #                                              probe variants x 2 launches each, then the pick)
         step()
     if world > 1 and args.tune == "measured" and runner is not None and isinstance(runner, LibraryFanout):
         torch.cuda.synchronize()
