@@ -229,7 +229,7 @@ __device__ __forceinline__ void msd_range_kp(MsdShared<NT, RW>& sh, uint32_t b, 
             for (int u = 0; u < U; ++u) {
                 const uint32_t i = i0 + u * NT + tid;
                 if (i < S) {
-                    perm[base + i] = v[u];
+                    __builtin_nontemporal_store(v[u], perm + base + i);
                     if (rank_out) rank_out[v[u]] = base + i;
                 }
             }

@@ -510,7 +510,7 @@ __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16
             const uint32_t inc = wave_incl_sum_dpp(x);
             const uint32_t e = carry + inc - x;
             cnt[q * WAVE + lane] = e;
-            if (q * WAVE + lane < L) offsets[k0 + q * WAVE + lane] = base + e;
+            if (q * WAVE + lane < L) __builtin_nontemporal_store(base + e, offsets + k0 + q * WAVE + lane);
             carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, WAVE - 1);
         }
         if (lane == 0 && b == (n_act >> MSD_SHIFT)) offsets[n_act + 1] = n;
