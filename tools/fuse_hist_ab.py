@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """A/B of the route kernel that also counts the one-pass MSD digits (option fuse_hist) at the cfg-2
-shape: bit-exact outputs with the option on and off, then interleaved timing.  Prints JSON lines."""
+shape: bit-exact outputs with the option on and off, then interleaved timing.  Prints JSON lines.
+The option was removed after this A/B; the script needs that experiment's build."""
 import json
 import os
 import sys
