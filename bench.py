@@ -149,7 +149,8 @@ def bucket_bytes(form: str, n: int, n_act: int, acts=None) -> dict:
 BUCKET_KERNELS = ("k_radix_hist", "k_radix_rowscan", "k_radix_scatter", "k_msd_local", "k_msd_local_mid",
                   "k_starts_rangescan",
                   "k_scan_reduce", "k_scan_down", "k_fill", "k_seg_table", "k_seg_hist", "k_seg_scatter",
-                  "k_l2_classify", "k_l2_small", "k_l2_chunk_hist", "k_l2_chunk_scan", "k_l2_chunk_scatter")
+                  "k_l2_classify", "k_l2_small", "k_l2_chunk_hist", "k_l2_chunk_ptot", "k_l2_chunk_scan",
+                  "k_l2_chunk_scatter")
 
 
 def kernel_bytes(name: str, n: int, n_act: int, form: str = "lsd", acts=None) -> float:
