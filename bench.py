@@ -443,6 +443,139 @@ def timed_steps(router, keys, n_act, stream, steps, warmup, settle=SETTLE_STEPS,
 
 T_START = time.perf_counter()
 
+# The one printed line must reach the driver whole: it keeps only the tail (~8 KB) of stdout, and round 4's
+# 21.5-KB line (every kernel table inline) was cut and went unparsed.  The line carries the headline and
+# compact roofline / baseline / secondary summaries; the full record (per-kernel tables of every config)
+# goes to --full-out.
+LINE_CAP = 6000
+
+
+def _pick(d, keys) -> dict:
+    return {k: d[k] for k in keys if d and d.get(k) is not None}
+
+
+ROOF_KEYS = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "traffic_ratio", "frac_pmc",
+             "avg_launch_ms", "launches_per_step", "alg_bytes_per_launch")
+
+
+def compact_roofline(rf, kernels, with_table=True):
+    """The line's roofline: the dominant kernel (BASELINE's fields: achieved / peak / frac / traffic, plus
+    frac_pmc and the traffic ratio), the bucketing stage's summary, its weakest kernel by name (lowest
+    frac_pmc -- else frac -- of the kernels taking >= 10 % of the stage), and (with_table) every stage
+    kernel as [ms a step, frac, frac_pmc, traffic_ratio]."""
+    if not rf:
+        return rf
+    out = _pick(rf, ROOF_KEYS)
+    if out.get("traffic") is not None:
+        out["traffic"] = round(out["traffic"])
+    for k in ("probe_variant", "probe_index_frac_impl"):
+        if rf.get(k) is not None:
+            out[k] = rf[k]
+    if rf.get("probe_index"):
+        out["probe_index_frac_impl"] = rf["probe_index"].get("frac_impl")
+    st = rf.get("bucketing_stage")
+    if st:
+        out["bucketing_stage"] = _pick(st, ("form", "ms_per_step", "impl_bytes_per_message", "frac_impl",
+                                            "frac_contract"))
+        stage_ms = st.get("ms_per_step") or 0.0
+        weakest, wkey = None, None
+        table = {}
+        for name in st.get("kernels", []):
+            d = (kernels or {}).get(name)
+            if not d or not d.get("frac_hbm"):
+                continue
+            table[name] = [d["ms_per_step"], d["frac_hbm"], d.get("frac_pmc"), d.get("traffic_ratio")]
+            key = d.get("frac_pmc") or d["frac_hbm"]
+            if d["ms_per_step"] >= 0.1 * stage_ms and (wkey is None or key < wkey):
+                weakest, wkey = name, key
+        if weakest:
+            d = kernels[weakest]
+            out["weakest_bucketing_kernel"] = dict(
+                kernel=weakest, **_pick(d, ("ms_per_step", "launches_per_step", "frac_hbm", "frac_pmc",
+                                            "traffic_ratio", "lds_conflict_ratio")))
+        if with_table and table:
+            out["bucketing_kernels"] = dict(cols="ms_per_step,frac,frac_pmc,traffic_ratio", **table)
+    return out
+
+
+def compact_cpu(c):
+    if not c:
+        return c
+    out = _pick(c, ("value", "unit", "cores", "kind", "mode"))
+    out["sample"] = (c.get("sample") or "")[:240]
+    return out
+
+
+def compact_secondary(sec: dict) -> dict:
+    out = {}
+    for name, v in (sec or {}).items():
+        if name == "cfg5_latency_us":
+            out[name] = {k: v[k] for k in ("batch", "graph", "eager", "zero_copy") if k in v}
+        elif name == "cfg1_ping_shape":
+            out[name] = _pick(v, ("value", "ms_per_step", "workload"))
+        else:
+            d = _pick(v, ("value", "unit", "ms_per_step", "steps", "workload", "n_gpus", "scaling",
+                          "messages_per_step"))
+            if isinstance(d.get("workload"), str):
+                d["workload"] = d["workload"][:160]
+            if v.get("config", {}).get("workload"):
+                d["workload"] = v["config"]["workload"][:160]
+            d["roofline"] = compact_roofline(v.get("roofline"), v.get("kernels"), with_table=False)
+            if v.get("cpu_baseline"):
+                d["cpu_baseline"] = compact_cpu(v["cpu_baseline"])
+            out[name] = d
+    return out
+
+
+def compact_line(full: dict, full_path=None) -> dict:
+    """The printed line from the full record (LINE_CAP bytes at most: secondary tables are dropped first,
+    then the main stage table)."""
+    line = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "settle_steps", "tune",
+                                 "ms_per_step", "gpu_event_ms_per_step", "higher_is_better", "scaling",
+                                 "vs_baseline", "dtype", "data") if k in full}
+    cfg = dict(full.get("config") or {})
+    if isinstance(cfg.get("silos"), str):
+        cfg["silos"] = cfg["silos"][:90]
+    cfg.pop("owner_share_max_by_silo_set", None)
+    line["config"] = cfg
+    for k in ("routed_ok_last_step_rank0", "rehearsal_one_gpu", "messages_per_step", "comm"):
+        if k in full:
+            line[k] = full[k]
+    if isinstance(full.get("exchange"), str):
+        line["exchange"] = full["exchange"][:120]
+    line["roofline"] = compact_roofline(full.get("roofline"), full.get("kernels"))
+    line["cpu_baseline"] = compact_cpu(full.get("cpu_baseline"))
+    if full.get("secondary"):
+        line["secondary"] = compact_secondary(full["secondary"])
+    if full_path:
+        line["full_record"] = full_path
+    if "bench_wall_s" in full:
+        line["bench_wall_s"] = full["bench_wall_s"]
+    if len(json.dumps(line)) > LINE_CAP and line["roofline"]:
+        line["roofline"].pop("bucketing_kernels", None)
+    for name in list((line.get("secondary") or {}).keys()):
+        if len(json.dumps(line)) <= LINE_CAP:
+            break
+        sec = line["secondary"][name]
+        if isinstance(sec, dict) and isinstance(sec.get("roofline"), dict):
+            sec["roofline"] = {k: sec["roofline"][k] for k in ("kernel", "frac", "frac_pmc")
+                               if k in sec["roofline"]}
+    return line
+
+
+def emit(full: dict, args):
+    """Writes the full record to --full-out, prints the compact line (one JSON line, <= LINE_CAP bytes)."""
+    path = args.full_out
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+    except OSError as ex:
+        print(f"bench: full record not written: {ex!r}", file=sys.stderr, flush=True)
+        path = None
+    line = compact_line(full, os.path.relpath(path, ROOT) if path else None)
+    print(json.dumps(line), flush=True)
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -477,6 +610,8 @@ def main():
     ap.add_argument("--no-target", action="store_true", help="cfg4: do not write the target node per message")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="rehearsal only: every rank on cuda:0, gloo, host-staged all-to-all")
+    ap.add_argument("--full-out", default=os.path.join(ROOT, "gpurun_out", "bench_full.json"),
+                    help="where the full record (every kernel table) is written; the printed line is its summary")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="a handle option for every handle (graindispatch.OPTIONS: GD_OPT_*), e.g. bucket=2")
     ap.add_argument("--tune", default="measured", choices=["measured", "pinned"],
@@ -626,7 +761,7 @@ def main():
         if secondary:
             line["secondary"] = secondary
         line["bench_wall_s"] = round(time.perf_counter() - T_START, 1)
-        print(json.dumps(line), flush=True)
+        emit(line, args)
     e.close()
     dist.destroy_process_group()
 
@@ -659,27 +794,24 @@ def profile_kernels(e, router, keys, n_act, stream, steps: int) -> dict:
 
 
 def route_extras(roofline: dict, e, m_recv: int, tag: str, world: int):
-    """k_route's side fields: the probe variant the library runs (gd_tune_get), the compact index's
-    own bytes when it is the index, and (cfg2, N = 1) the measured random-probe ceiling."""
+    """k_route's side fields: the probe variant the library runs (gd_tune_get) and, when it reads a
+    compact index (gd_cx.h), the index's own bytes a message.  (Round 1's random-probe "ceiling" was
+    measured for the 32-B slot table and does not bound the 8-B index probe: no longer reported.)"""
     kind = "probe_keys" if world == 1 else "probe_n1"
     v = e.tune_get(kind, m_recv)
-    roofline["probe_variant"] = {0: "compact index, 64-B group reads", 1: "directory table, 32-B slots",
-                                 2: "compact index, 16-B slot reads", -1: "still measuring"}.get(v, str(v))
+    roofline["probe_variant"] = PROBE_VARIANTS.get(v, str(v))
     t_l = roofline["avg_launch_ms"] * 1e-3
-    if v in (0, 2):
-        # the probe reads the compact index (gd_cx.h): 16-B slots; per message key 24 + one 16-B slot + 9
-        impl = m_recv * (24 + 16 + 9)
-        roofline["probe_index"] = {"slot_bytes": 16, "group_slots": 4 if v == 0 else 1, "impl_bytes_per_launch": impl,
-                                   "frac_impl": round(impl / t_l / 1e9 / PEAK_HBM_GBS, 4) if t_l > 0 else None,
-                                   "ubench": "profiles/r03_ubench_mirror.txt"}
-    if tag == "cfg2" and world == 1:
-        # one random slot read per message beside the 24-B key stream: its real ceiling is the
-        # random-probe rate, measured on MI355X by tools/ubench_random.hip for this shape (16M probes,
-        # 64-MiB table, key stream on): 0.3453 ms a launch (profiles/r01_ubench_random_ceiling.txt)
-        ceil_ms = 0.3453 * (m_recv / (1 << 24))
-        roofline["random_probe_ceiling"] = {"ms_per_launch": round(ceil_ms, 4),
-                                            "source": "profiles/r01_ubench_random_ceiling.txt",
-                                            "frac_of_ceiling": round(ceil_ms / (t_l * 1e3), 3) if t_l > 0 else None}
+    slot = {0: 16, 2: 16, 3: 8}.get(v)
+    if slot:
+        # per message: key 24 + one index slot + silo/act/status 9
+        impl = m_recv * (24 + slot + 9)
+        roofline["probe_index"] = {"slot_bytes": slot, "impl_bytes_per_launch": impl,
+                                   "frac_impl": round(impl / t_l / 1e9 / PEAK_HBM_GBS, 4) if t_l > 0 else None}
+
+
+# gd_tune_get variants of the 24-B-key / N1 probes (gd_engine.hip cx_choose)
+PROBE_VARIANTS = {0: "16-B index, 64-B group reads", 1: "directory table, 32-B slots",
+                  2: "16-B index, 16-B slot reads", 3: "8-B index, 64-B group reads", -1: "still measuring"}
 
 
 def ping_shape(tcd: int, dev, mode: str, G: int = 10_000, N: int = 1 << 20, steps: int = 200) -> dict:
@@ -851,7 +983,7 @@ def cpu_baseline(args, tcd, G_total, pts, own, owner):
     del d
     lat_us = np.asarray(lat) * 1e6
     best = res["fast_n"]
-    return {"value": best["value"], "unit": "messages/s", "cores": cores, "kind": "port",
+    return {"value": best["value"], "unit": "messages/s", "cores": cores, "kind": "port", "mode": "fast_n",
             "sample": f"{best['messages']} messages (cfg2 distribution, {sample}-message batches repeated) through "
                       f"the C restatement (oracle/cpu_ref.c) in fast mode (binary-search ring, open addressing, "
                       f"parallel stable counting sort) on {cores} threads = this job's usable cores "
@@ -891,11 +1023,12 @@ def cpu_baseline_cfg3(args, w3, tcd):
         v, done = _timed(one, args.cpu_seconds / 4, sample)
         res[label] = {"value": round(v, 1), "threads": thr, "messages": done}
         del d
-    # the faster mode is the baseline: at n_act = 100M the fast mode's parallel counting sort pays
-    # O(n_act) per thread per batch, which a 2M-message sample does not amortise
+    # the faster mode is the baseline (fast: binary-search ring, open addressing, the parallel two-level
+    # partition of cpu_ref.c -- O(n + n_act) work over all threads)
     label = max(res, key=lambda k: res[k]["value"])
     best = res[label]
     return {"value": best["value"], "unit": "messages/s", "cores": best["threads"], "kind": "port",
+            "mode": label,
             "sample": f"{best['messages']} messages (the first {sample} of the GPU's Zipf(1.1) batch, repeated; "
                       f"{len(grains)} distinct grains registered on the CPU of the 100M) through the C restatement "
                       f"in {'faithful' if label.startswith('faithful') else 'fast'} mode on {best['threads']} "
@@ -937,7 +1070,7 @@ def run_cfg4(args, world, rank, local, dev):
                         with_cpu=not args.no_cpu_baseline)
     if rank == 0:
         line["bench_wall_s"] = round(time.perf_counter() - T_START, 1)
-        print(json.dumps(line), flush=True)
+        emit(line, args)
     dist.destroy_process_group()
 
 
@@ -1085,24 +1218,35 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
 
 
 def cpu_baseline_cfg4(args, t, tcd, owner, pts, own, n):
-    """cfg 4's CPU baseline: the C restatement (oracle/cpu_ref.c, test infrastructure, faithful
-    mode, 1 thread) routing + bucketing a bounded sample of the cascade's last hop; the follower
-    expansion itself is a numpy gather and is not timed."""
+    """cfg 4's CPU baseline: the C restatement (oracle/cpu_ref.c, test infrastructure) routing +
+    bucketing a bounded sample of the cascade's last hop, in faithful mode on 1 thread and fast mode
+    on all usable cores; the faster is the baseline.  The follower expansion itself is a numpy gather
+    and is not timed."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpu_ref  # test-infrastructure checker, timed here as the CPU baseline only
     t = np.asarray(t, dtype=np.uint32)                 # the last hop's targets
     sample = min(t.size, 1 << 21)
     keys = grain_keys(tcd, t[:sample].astype(np.int64))
-    d = cpu_ref.CpuDirectory(True, n)
-    d.register(grain_keys(tcd, np.arange(n, dtype=np.int64)), np.arange(n, dtype=np.uint32), owner)
+    cores = usable_cores()
+    reg = grain_keys(tcd, np.arange(n, dtype=np.int64))
+    res = {}
+    for label, faithful, thr in (("faithful_1", True, 1), ("fast_n", False, cores)):
+        d = cpu_ref.CpuDirectory(faithful, n)
+        d.register(reg, np.arange(n, dtype=np.uint32), owner)
 
-    def one():
-        _, _, act = d.route(args.mode, pts, own, keys, nthreads=1)
-        cpu_ref.bucket(act, n, faithful=True, nthreads=1)
-    v, done = _timed(one, args.cpu_seconds / 2, sample)
-    return {"value": round(v, 1), "unit": "messages/s", "cores": 1, "kind": "port",
-            "sample": f"{done} NewChirp messages ({sample}-message prefix of the last hop, repeated) through the C "
-                      f"restatement in faithful mode (linear ring scan, chained map, per-activation FIFO)"}
+        def one(d=d, faithful=faithful, thr=thr):
+            _, _, act = d.route(args.mode, pts, own, keys, nthreads=thr)
+            cpu_ref.bucket(act, n, faithful=faithful, nthreads=thr)
+        v, done = _timed(one, args.cpu_seconds / 4, sample)
+        res[label] = {"value": round(v, 1), "threads": thr, "messages": done}
+        del d
+    label = max(res, key=lambda k: res[k]["value"])
+    best = res[label]
+    return {"value": best["value"], "unit": "messages/s", "cores": best["threads"], "kind": "port", "mode": label,
+            "sample": f"{best['messages']} NewChirp messages ({sample}-message prefix of the last hop, repeated) "
+                      f"through the C restatement in {'faithful' if label.startswith('faithful') else 'fast'} mode "
+                      f"on {best['threads']} thread(s), the faster of the two modes", "modes": res,
+            "usable_cores": cores}
 
 
 if __name__ == "__main__":

@@ -243,8 +243,14 @@ int cpu_route(cpu_dir* d, int faithful, int mode, const uint32_t* pts, const uin
 /* ------------------------------------------------------------------ bucketing */
 typedef struct { uint32_t* v; uint32_t len, cap; } fifo_t;
 
+/* Fast mode: a parallel two-level stable partition, O(n + n_act) work in all, no O(n_act) pass per
+ * thread.  Level 1: each thread counts the high digit key >> s of its contiguous slice (H <= 4,096
+ * digits), one serial scan over [digit][thread], each thread scatters (index, key) stably.  Level 2:
+ * the threads take high-digit buckets from a shared counter; a bucket's 2^s activations get a private
+ * counting sort (counts, exclusive scan written as their offsets, stable placement).  */
 typedef struct {
-    const uint32_t* act; uint64_t lo, hi; uint32_t n_act; uint64_t* hist; uint32_t* perm; int phase;
+    const uint32_t* act; uint64_t lo, hi; uint32_t n_act, shift, H; uint64_t* hist; uint32_t *tk, *ti, *perm, *off;
+    int phase; uint32_t* next; const uint64_t* bstart; uint32_t* cnt;
 } bk_job;
 
 static void* bucket_worker(void* arg) {
@@ -252,19 +258,47 @@ static void* bucket_worker(void* arg) {
     if (j->phase == 0) {
         for (uint64_t i = j->lo; i < j->hi; ++i) {
             const uint32_t a = j->act[i] < j->n_act ? j->act[i] : j->n_act;
-            j->hist[a]++;
+            j->hist[a >> j->shift]++;
         }
-    } else {
+    } else if (j->phase == 1) {
         for (uint64_t i = j->lo; i < j->hi; ++i) {
             const uint32_t a = j->act[i] < j->n_act ? j->act[i] : j->n_act;
-            j->perm[j->hist[a]++] = (uint32_t)i;
+            const uint64_t p = j->hist[a >> j->shift]++;
+            j->tk[p] = a;
+            j->ti[p] = (uint32_t)i;
+        }
+    } else {
+        const uint32_t L = 1u << j->shift;
+        for (;;) {
+            const uint32_t b = __atomic_fetch_add(j->next, 1u, __ATOMIC_RELAXED);
+            if (b >= j->H) break;
+            const uint64_t s0 = j->bstart[b], s1 = j->bstart[b + 1];
+            const uint64_t k0 = (uint64_t)b << j->shift;
+            const uint64_t nk = (uint64_t)j->n_act + 1 - k0 < L ? (uint64_t)j->n_act + 1 - k0 : L;
+            memset(j->cnt, 0, nk * sizeof(uint32_t));
+            for (uint64_t p = s0; p < s1; ++p) j->cnt[j->tk[p] - k0]++;
+            uint64_t run = s0;
+            for (uint64_t a = 0; a < nk; ++a) {
+                const uint32_t c = j->cnt[a];
+                j->off[k0 + a] = (uint32_t)run;
+                j->cnt[a] = (uint32_t)run;
+                run += c;
+            }
+            for (uint64_t p = s0; p < s1; ++p) j->perm[j->cnt[j->tk[p] - k0]++] = j->ti[p];
         }
     }
     return NULL;
 }
 
+static void run_jobs(bk_job* jobs, int nthreads) {
+    pthread_t th[256];
+    if (nthreads == 1) { bucket_worker(&jobs[0]); return; }
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, bucket_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
 /* Stable partition by activation: faithful = per-activation FIFO append
- * (ActivationData.cs:604-605), fast = parallel stable counting sort. */
+ * (ActivationData.cs:604-605), fast = the parallel two-level partition above. */
 int cpu_bucket(int faithful, const uint32_t* act, uint64_t n, uint32_t n_act, uint32_t* perm, uint32_t* off,
                int nthreads) {
     const uint64_t nb = (uint64_t)n_act + 1;
@@ -292,32 +326,40 @@ int cpu_bucket(int faithful, const uint32_t* act, uint64_t n, uint32_t n_act, ui
     }
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
-    uint64_t* hist = (uint64_t*)calloc((uint64_t)nthreads * nb, sizeof(uint64_t));
-    pthread_t th[256];
+    /* s: low bits sorted per bucket (2^s counters, <= 256 KB a thread), leaving <= 4,096 high digits */
+    uint32_t kb = 1;
+    while (kb < 32 && (nb - 1) >> kb) ++kb;
+    const uint32_t shift = kb > 12 ? (kb - 12 < 16 ? (kb - 12 > 6 ? kb - 12 : 6) : 16) : 6;
+    const uint32_t H = (uint32_t)(((nb - 1) >> shift) + 1);
+    uint64_t* hist = (uint64_t*)calloc((uint64_t)nthreads * H, sizeof(uint64_t));
+    uint64_t* bstart = (uint64_t*)malloc(((uint64_t)H + 1) * sizeof(uint64_t));
+    uint32_t* tk = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+    uint32_t* ti = (uint32_t*)malloc((n ? n : 1) * sizeof(uint32_t));
+    uint32_t* cnt = (uint32_t*)malloc((uint64_t)nthreads << shift << 2);
+    uint32_t next = 0;
     bk_job jobs[256];
-    for (int ph = 0; ph < 2; ++ph) {
-        if (ph == 1) {  /* column-major exclusive scan: bucket a, thread t */
-            uint64_t run = 0;
-            for (uint64_t a = 0; a < nb; ++a) {
-                off[a] = (uint32_t)run;
-                for (int t = 0; t < nthreads; ++t) {
-                    const uint64_t c = hist[(uint64_t)t * nb + a];
-                    hist[(uint64_t)t * nb + a] = run;
-                    run += c;
-                }
-            }
-            off[nb] = (uint32_t)run;
-        }
-        for (int t = 0; t < nthreads; ++t) {
-            bk_job j = {act, n * t / nthreads, n * (t + 1) / nthreads, n_act, hist + (uint64_t)t * nb, perm, ph};
-            jobs[t] = j;
-            if (nthreads == 1) bucket_worker(&jobs[0]);
-            else pthread_create(&th[t], NULL, bucket_worker, &jobs[t]);
-        }
-        if (nthreads > 1)
-            for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    for (int t = 0; t < nthreads; ++t) {
+        bk_job j = {act, n * t / nthreads, n * (t + 1) / nthreads, n_act, shift, H, hist + (uint64_t)t * H,
+                    tk, ti, perm, off, 0, &next, bstart, cnt + ((uint64_t)t << shift)};
+        jobs[t] = j;
     }
-    free(hist);
+    run_jobs(jobs, nthreads);
+    uint64_t run = 0;
+    for (uint32_t d = 0; d < H; ++d) {          /* [digit][thread]: thread slices in batch order */
+        bstart[d] = run;
+        for (int t = 0; t < nthreads; ++t) {
+            const uint64_t c = hist[(uint64_t)t * H + d];
+            hist[(uint64_t)t * H + d] = run;
+            run += c;
+        }
+    }
+    bstart[H] = run;
+    for (int t = 0; t < nthreads; ++t) jobs[t].phase = 1;
+    run_jobs(jobs, nthreads);
+    for (int t = 0; t < nthreads; ++t) jobs[t].phase = 2;
+    run_jobs(jobs, nthreads);
+    off[nb] = (uint32_t)n;
+    free(hist); free(bstart); free(tk); free(ti); free(cnt);
     return 0;
 }
 

@@ -503,6 +503,14 @@ int tune_key(int kind, uint64_t n, int sub) {
 // Variants of a tune kind (GD_TUNE_*): the 24-B-key and N1 probes have three, the rest two.
 int tune_nvar(int kind) { return kind <= 1 ? 4 : (kind <= 3 ? 3 : 2); }
 
+// Variants a launch of `kind` has on this handle now: kinds 0 / 1 and 2 / 3 have the 8-B index as their
+// last variant only where it is built (cx_ensure), kind 4 (the bucketing form) always two.
+int tune_nvar_now(const gd_handle* h, int kind) {
+    if (kind <= 1) return h->cx8_ok ? 4 : 3;
+    if (kind <= 3) return h->cx8_ok ? 3 : 2;
+    return 2;
+}
+
 // Folds the entry's finished timings in (events read without a stream sync, unless the entry has
 // timed every variant twice and only waits for them) and picks when every variant is timed.
 void tune_resolve(gd_handle::CxTune& t, int nvar) {
@@ -542,6 +550,19 @@ int tune_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar, int sub
     if (h->tune_pin[kind] >= 0 && h->tune_pin[kind] < nvar) return h->tune_pin[kind];
     const int key = tune_key(kind, n, sub);
     auto& t = h->cx_tune[key];
+    if (t.pick >= nvar || (t.pick < 0 && t.nvar && t.nvar != nvar)) {
+        // a pick (gd_tune_agree's, or this entry's own) of a variant this launch does not have -- the
+        // 8-B index not built here, or no longer -- or timings taken over another variant set: measure
+        // again over the variants this launch has
+        for (int v = 0; v < V; ++v) {
+            if (t.pending[v] && t.b[v]) (void)hipEventSynchronize(t.b[v]);
+            t.pending[v] = false;
+            t.best[v] = 1e30f;
+            t.n[v] = 0;
+        }
+        t.pick = -1;
+        t.round = 0;
+    }
     t.nvar = nvar;
     tune_resolve(t, nvar);
     if (t.pick >= 0) return t.pick;
@@ -971,7 +992,10 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     const uint32_t R = (n_act >> MSD_SHIFT) + 1, RB = 1u << a;
     const uint32_t tilesA = blocks_for(n, B2_TILE);
     const uint32_t tbound = blocks_for(n, SEG_TILE) + RA;
-    const uint32_t cr_bound = n / (MSD_CAP + 1) + 1;
+    // ranges past t_staged messages are chunked (k_l2_classify): at most n / (t_staged + 1) of them,
+    // whatever GD_OPT_L2_STAGED / GD_OPT_L2_SMALL say
+    const uint32_t t_staged = std::max(h->l2_small, h->l2_staged);
+    const uint32_t cr_bound = std::min(R, n / (t_staged + 1) + 1);
     const uint32_t ch_bound = n / CH_CAP + cr_bound;
     GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
     GD_TRY(ensure(h, h->u32_b, (size_t)n * 4));
@@ -994,7 +1018,7 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     GD_TRY(ensure(h, m[9], (size_t)ch_bound * 4));                 // chunk -> chunked range
     GD_TRY(ensure(h, m[10], (size_t)ch_bound * MSD_L * 4));        // per-chunk activation counts
     GD_TRY(ensure(h, m[11], (size_t)cr_bound * MSD_L * 4));        // per-range activation totals
-    GD_TRY(ensure(h, m[12], (size_t)cr_bound * blocks_for(ch_bound, CS_ROWS) * MSD_L * 4));   // per-piece sums
+    GD_TRY(ensure(h, m[12], (size_t)it_bound * CS_COLS * 4));        // per-item (slab x piece) column sums
     uint32_t* kA = (uint32_t*)h->u32_a.p;
     uint32_t* vA = (uint32_t*)h->u32_c.p;
     uint16_t* kB = (uint16_t*)h->u32_b.p;
@@ -1040,7 +1064,7 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
                     (uint32_t*)m[9].p, cr + 3 * cr_bound, (uint32_t*)m[13].p, (uint32_t*)m[5].p};
     GD_TRY(launch(h, "k_l2_classify", dim3(blocks_for(R, CL_NT)), dim3(CL_NT), 0, k_l2_classify, (const uint32_t*)hseg,
                   (const uint32_t*)seg_start, (const uint32_t*)seg_tb, a, R, n, h->l2_small,
-                  std::max(h->l2_small, h->l2_mid), std::max(h->l2_small, h->l2_staged), l));
+                  std::max(h->l2_small, h->l2_mid), t_staged, l));
     // persistent grids sized to what the chip holds at once (a second round of workgroups would wait for
     // the first to finish its whole share): k_l2_small 4 a CU (32 KB of LDS, 8 waves each), the range
     // sort 1 a CU (135 KB), the chunk scatter 2 (72 KB), the chunk histogram 4 and the scan 2 a CU
@@ -1060,12 +1084,10 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     // the chunk grids are multiples of 8 (chunk_walk: one contiguous chunk range an XCD)
     GD_TRY(launch(h, "k_l2_chunk_hist", dim3(4 * cu8), dim3(CH_NT), 0, k_l2_chunk_hist,
                   (const uint16_t*)kB, l, hh));
-    const uint32_t pmax = blocks_for(ch_bound, CS_ROWS);
     uint32_t* ptot = (uint32_t*)m[12].p;
-    GD_TRY(launch(h, "k_l2_chunk_ptot", dim3(2 * cu8), dim3(MSD_NT), 0, k_l2_chunk_ptot, l, (const uint32_t*)hh, pmax,
-                  ptot));
-    GD_TRY(launch(h, "k_l2_chunk_scan", dim3(2 * cu8), dim3(MSD_NT), 0, k_l2_chunk_scan, l, hh, pmax,
-                  (const uint32_t*)ptot, tot));
+    GD_TRY(launch(h, "k_l2_chunk_ptot", dim3(2 * cu8), dim3(MSD_NT), 0, k_l2_chunk_ptot, l, (const uint32_t*)hh, ptot));
+    GD_TRY(launch(h, "k_l2_chunk_scan", dim3(2 * cu8), dim3(MSD_NT), 0, k_l2_chunk_scan, l, hh, (const uint32_t*)ptot,
+                  tot));
     return launch(h, "k_l2_chunk_scatter", dim3(2 * cu8), dim3(CH_NT), 0, k_l2_chunk_scatter,
                   (const uint16_t*)kB, (const uint32_t*)vB, l, (const uint32_t*)hh, (const uint32_t*)tot, n, n_act, perm,
                   offsets, rank_out);
@@ -2131,7 +2153,7 @@ int gd_tune_get(gd_handle* h, int kind, uint64_t n, uint32_t sub, int* variant) 
         *variant = -1;
         return GD_OK;
     }
-    tune_resolve(it->second, tune_nvar(kind));
+    tune_resolve(it->second, it->second.nvar ? it->second.nvar : tune_nvar(kind));
     *variant = it->second.pick;
     return GD_OK;
 }
@@ -4551,9 +4573,16 @@ int gd_tune_agree(gd_handle* h) {
         int pick = 0;
         for (int v = 1; v < nvar; ++v)
             if (ks.second[v] < ks.second[pick]) pick = v;
+        // only a variant this handle can launch: the entry's own variant count where it measured it,
+        // else the count its launches have now (the 8-B index built or not); a later launch with
+        // fewer variants measures again (tune_choose).  Results agree whatever each rank runs.
+        auto it = h->cx_tune.find((int)ks.first);
+        const int local = it != h->cx_tune.end() && it->second.nvar ? it->second.nvar : tune_nvar_now(h, kind);
+        if (pick >= local) continue;
         auto& t = h->cx_tune[(int)ks.first];
         t.pick = pick;
-        t.round = std::max(t.round, 2 * nvar);
+        t.nvar = local;
+        t.round = std::max(t.round, 2 * local);
     }
     return GD_OK;
 }
@@ -4696,7 +4725,7 @@ int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uin
     HIP_TRY(h, hipMemsetAsync(visited, 0, (size_t)n_act + 16, h->stream));
     // hop 0's publishers: the seeds this rank owns, in seed order (a stable partition of the seeds by
     // owner rank, then this rank's chunk)
-    uint32_t nf = 0;
+    uint32_t nf = 0, seed_fail = 0;
     {
         std::array<DevBuf, 10>& H0 = h->fm_hop[0];
         GD_TRY(ensure(h, S[0], (size_t)n_seeds * 4 + 16));
@@ -4731,11 +4760,13 @@ int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uin
                           (const uint8_t*)sts, nf, n_act, (uint32_t*)H0[0].p, dcnt + 2 * W));
             HIP_TRY(h, hipMemcpyAsync(hc, dcnt + 2 * W, 4, hipMemcpyDeviceToHost, h->stream));
             HIP_TRY(h, hipStreamSynchronize(h->stream));
-            if (hc[0])
-                return set_err(h, GD_EINVAL, "%u seeds have no live activation on their owner (a partitioned "
-                               "graph's rows are activations)", hc[0]);
-            GD_TRY(launch(h, "k_mark_visited", dim3(blocks_for(nf, BLOCK)), dim3(BLOCK), 0, k_mark_visited,
-                          (const uint32_t*)H0[0].p, nf, n_act, visited));
+            // a seed without a live activation fails the whole cascade on every rank: this rank goes on
+            // with no publishers and flags its hop-0 counts (below), so no peer waits in a later round
+            seed_fail = hc[0];
+            if (seed_fail) nf = 0;
+            else
+                GD_TRY(launch(h, "k_mark_visited", dim3(blocks_for(nf, BLOCK)), dim3(BLOCK), 0, k_mark_visited,
+                              (const uint32_t*)H0[0].p, nf, n_act, visited));
         }
     }
     uint64_t total = 0;
@@ -4770,9 +4801,19 @@ int fanout_multi(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uin
         // 2. stable partition of (target, sender) by the target's owner rank
         GD_TRY(shard_pack<true>(h, S[0].p, (const uint32_t*)S[1].p, n, tcd, (uint32_t)W, S[2].p, (uint32_t*)S[3].p,
                                 dcnt));
-        // 3. counts, then one grouped round of 8 B a message
+        // 3. counts, then one grouped round of 8 B a message.  Hop 0's counts carry a failed seed
+        //    resolution to every peer (all ones: no real count, at most 2^32 - 2 messages a hop), and
+        //    every rank returns the error after this same round
+        if (hp == 0 && seed_fail) HIP_TRY(h, hipMemsetAsync(dcnt, 0xFF, (size_t)W * 4, h->stream));
         std::vector<uint32_t> sc, rc;
         GD_TRY(counts_round(h, dcnt, sc, rc));
+        if (hp == 0) {
+            for (int r = 0; r < W; ++r)
+                if (rc[r] == 0xFFFFFFFFu)
+                    return set_err(h, GD_EINVAL, "rank %d: %s seeds have no live activation on their owner (a "
+                                   "partitioned graph's rows are activations)", r,
+                                   r == h->rank ? std::to_string(seed_fail).c_str() : "some");
+        }
         std::vector<uint64_t> soff(W + 1, 0), roff(W + 1, 0);
         for (int r = 0; r < W; ++r) {
             soff[r + 1] = soff[r] + sc[r];

@@ -663,7 +663,8 @@ __device__ __forceinline__ uint32_t cs_load(const uint32_t* hh, const CsItem& x,
     return rows;
 }
 
-__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_ptot(L2Lists l, const uint32_t* __restrict__ hh, uint32_t pmax,
+// ptot: one CS_COLS-word row a chunk-scan item (its piece's column sums), at the item's index.
+__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_ptot(L2Lists l, const uint32_t* __restrict__ hh,
                                                           uint32_t* __restrict__ ptot) {
     __shared__ uint32_t s_m[CS_ROWS * (CS_COLS + 1)];
     const uint32_t lane = lane_id(), w = threadIdx.x / WAVE;
@@ -677,12 +678,12 @@ __global__ void __launch_bounds__(MSD_NT) k_l2_chunk_ptot(L2Lists l, const uint3
         uint32_t sum = 0;                                // wave w: column w
         for (uint32_t q = 0; q < (rows + WAVE - 1) / WAVE; ++q) sum += s_m[(q * WAVE + lane) * (CS_COLS + 1) + w];
         sum = wave_incl_sum_dpp(sum);
-        if (lane == WAVE - 1) ptot[((size_t)x.r * pmax + x.p) * MSD_L + x.g * CS_COLS + w] = sum;
+        if (lane == WAVE - 1) ptot[(size_t)it * CS_COLS + w] = sum;
         __syncthreads();
     }
 }
 
-__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_scan(L2Lists l, uint32_t* __restrict__ hh, uint32_t pmax,
+__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_scan(L2Lists l, uint32_t* __restrict__ hh,
                                                           const uint32_t* __restrict__ ptot,
                                                           uint32_t* __restrict__ tot) {
     __shared__ uint32_t s_m[CS_ROWS * (CS_COLS + 1)];
@@ -709,7 +710,8 @@ __global__ void __launch_bounds__(MSD_NT) k_l2_chunk_scan(L2Lists l, uint32_t* _
         }
         // wave w: column w, carried in from the pieces before this one
         uint32_t carry = 0;
-        for (uint32_t p = 0; p < x.p; ++p) carry += ptot[((size_t)x.r * pmax + p) * MSD_L + x.g * CS_COLS + w];
+        const uint32_t* pt = ptot + ((size_t)l.cr_ib[x.r] + (size_t)x.g * x.pieces) * CS_COLS + w;
+        for (uint32_t p = 0; p < x.p; ++p) carry += pt[(size_t)p * CS_COLS];
         const uint32_t rows = cs_load(hh, x, s_m);
         __syncthreads();
         for (uint32_t q = 0; q < (rows + WAVE - 1) / WAVE; ++q) {

@@ -440,6 +440,51 @@ def test_tune_agree_w8(gd):
         e.close()
 
 
+def test_tune_agree_rank_without_8b_index(gd):
+    """gd_tune_agree when one rank cannot build the 8-B probe index (an entry with N1 >= 2^32 on rank
+    0) and never measured the agreed entry: ranks 1..3 time their 24-B-key probe variants (the 8-B
+    index among them) on a size class rank 0 never routes, the agreement hands rank 0 a pick for that
+    entry, and rank 0's next launch of that size must run a variant it has -- never the 8-B probe over
+    an index it did not build -- with results equal to the oracle's."""
+    W, G = 4, 1 << 16
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    reg = o.grain_keys(TC, np.arange(G))
+    own = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    wide = o.grain_keys(TC, np.array([0], dtype=np.int64))
+    wide[0, 1] = np.uint64(1 << 33)                          # N1 >= 2^32: no 8-B index on rank 0
+    wide_own = o.ring_owner_np(spec, o.jenkins_u64x3_np(wide[:, 2], wide[:, 0], wide[:, 1])).astype(np.uint32)
+    es = []
+    for r in range(W):
+        e = gd.GrainDispatch(device=0, table_capacity=1 << 17, my_silo=r)
+        e.ring_set_silos("D", _tuples(silos))
+        e.register(reg, np.arange(G, dtype=np.uint32), own)
+        if r == 0:
+            e.register(wide, np.array([G], np.uint32), wide_own)
+        es.append(e)
+    gd.GrainDispatch.comm_init_local(es)
+    rng = np.random.default_rng(5)
+    keys = o.grain_keys(TC, rng.integers(0, G, size=1 << 20))
+    for r in range(1, W):                                    # 8 launches: every variant timed twice
+        for _ in range(10):
+            es[r].route(keys)
+    _run_ranks([lambda r=r: es[r].tune_agree() for r in range(W)])
+    picks = [es[r].tune_get("probe_keys", len(keys)) for r in range(1, W)]
+    assert len(set(picks)) == 1 and picks[0] >= 0, picks
+    full = o.DirectoryArrays(np.concatenate([reg, wide]), np.arange(G + 1, dtype=np.uint32),
+                             np.concatenate([own, wide_own]))
+    want = o.route_batch_np(keys, spec, full)
+    for _ in range(10):                                      # measuring again over rank 0's own variants
+        st, silo, act = es[0].route(keys)
+        np.testing.assert_array_equal(st, want[0])
+        np.testing.assert_array_equal(silo, want[1])
+        np.testing.assert_array_equal(act, want[2])
+    assert es[0].tune_get("probe_keys", len(keys)) in (-1, 0, 1, 2)
+    for e in es:
+        e.comm_destroy()
+        e.close()
+
+
 def test_options_roundtrip_and_range(gd, monkeypatch):
     """gd_option_set / gd_option_get: every option reads back what was set, the defaults are the
     documented ones, values out of range and unknown options are refused with an error

@@ -188,6 +188,57 @@ def test_fanout_multi_partitioned_graph_w8(gd):
         e.close()
 
 
+def test_fanout_multi_partitioned_bad_seed_fails_on_every_rank(gd):
+    """A seed without a live activation on its owner (a partitioned graph's rows are activations)
+    fails gd_fanout_multi_part_device on EVERY rank, together, after hop 0's counts round -- no rank
+    is left waiting in a later exchange round (W = 4, in-process transport).  The handles stay usable:
+    the next cascade with valid seeds runs on all ranks."""
+    import torch
+    from orleans_amd.fanout import partition_graph_np
+    W, n, hops = 4, 4000, 3
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    ro, dst = power_law_graph(n, 5.0, seed=91, max_deg=500)
+    own = _owners(spec, n)
+    registered = np.arange(n)[np.arange(n) % 17 != 3]
+    dev = torch.device("cuda", 0)
+    es, parts = [], []
+    for r in range(W):
+        mine = registered[own[registered] % W == r]
+        e = gd.GrainDispatch(device=0, table_capacity=1 << 12, my_silo=r)
+        e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+        e.register(o.grain_keys(TC, mine), np.arange(mine.size, dtype=np.uint32), own[mine])
+        es.append(e)
+        ro_l, dst_l, node_of = partition_graph_np(ro, dst, mine)
+        parts.append(tuple(torch.from_numpy(x.view(np.int32)).to(dev) if x.size else
+                           torch.zeros(1, dtype=torch.int32, device=dev) for x in (ro_l, dst_l, node_of)) +
+                     (mine.size,))
+    gd.GrainDispatch.comm_init_local(es)
+    good = np.random.default_rng(3).choice(registered, 20).astype(np.uint32)
+    bad = np.concatenate([good, [3]]).astype(np.uint32)          # node 3 has no activation
+    assert own[3] % W in range(W)
+
+    def run(r, seeds):
+        t = torch.from_numpy(seeds.view(np.int32)).to(dev)
+        torch.cuda.synchronize()
+        ro_d, dst_d, no_d, rows = parts[r]
+        try:
+            es[r].fanout_multi_part_device(ro_d.data_ptr(), dst_d.data_ptr(), rows, no_d.data_ptr(), t.data_ptr(),
+                                           seeds.size, TC, hops)
+            return None
+        except Exception as ex:   # noqa: BLE001 -- the error is the result here
+            return str(ex)
+    errs = _run_ranks([lambda r=r: run(r, bad) for r in range(W)])
+    for r in range(W):
+        assert errs[r] is not None and "no live activation" in errs[r], (r, errs[r])
+        assert f"rank {int(own[3] % W)}" in errs[r], (r, errs[r])
+    errs = _run_ranks([lambda r=r: run(r, good) for r in range(W)])
+    assert errs == [None] * W, errs
+    for e in es:
+        e.comm_destroy()
+        e.close()
+
+
 def test_fanout_multi_world1_rccl_equals_fused_cascade(gd):
     """W = 1 over RCCL (a send/recv to self): the sharded cascade gives exactly the one-GPU fused
     cascade's hops (same emission order, same frontiers)."""

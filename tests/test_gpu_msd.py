@@ -132,6 +132,22 @@ def test_msd_three_pass_mid_class(gd, mid):
     e0.close()
 
 
+@pytest.mark.parametrize("staged,small", [(2048, 1024), (0, 1024), (0, 0), (1100, 300)])
+def test_msd_three_pass_small_staged_threshold(gd, staged, small):
+    """GD_OPT_L2_STAGED below the staging capacity: every range over max(l2_small, l2_staged) messages
+    is chunked (k_l2_classify), far more chunked ranges than the default's n / 24,577 -- the chunk
+    buffers are sized from that threshold (msd3_bucket), and the result never changes.  Uniform
+    ~2K-message ranges: most ranges exceed 2,048 / 1,024 / 0."""
+    acts = _acts(1 << 22, 2 << 20, "uniform", 55)
+    e2, e0 = _check(gd, acts, 2 << 20, l2_staged=staged, l2_small=small)
+    e2.close()
+    e0.close()
+    acts = _acts(1 << 21, 3 << 20, "zipf", 56)
+    e2, e0 = _check(gd, acts, 3 << 20, l2_staged=staged, l2_small=small)
+    e2.close()
+    e0.close()
+
+
 def test_msd_three_pass_kernels(gd):
     """The three-pass form runs its own kernels (not the LSD passes) when forced."""
     acts = _acts(1 << 21, 5_000_000, "zipf", 9)

@@ -258,6 +258,25 @@ def test_c_restatement_matches_oracle(faithful, mode):
     assert np.array_equal(perm, wp) and np.array_equal(off, wo)
 
 
+@pytest.mark.parametrize("n,n_act", [(0, 10), (1, 1), (1000, 7), (100_000, 1000), (1 << 20, 1 << 20),
+                                     (1 << 19, 100_000_000), (300_017, 5_000_000)])
+def test_c_fast_bucket_two_level_matches_oracle(n, n_act):
+    """cpu_bucket fast mode (the CPU baseline's parallel two-level partition: high-digit scatter, then
+    a counting sort per bucket) = the stable partition, on 1, 3 and 8 threads, with unrouted and
+    clamped activations and Zipf-hot keys."""
+    import cpu_ref
+    rng = np.random.default_rng(n + n_act)
+    for kind in ("uniform", "zipf"):
+        a = (rng.integers(0, n_act + 3, size=n) if kind == "uniform" else (rng.zipf(1.1, size=n) - 1) % (n_act + 3))
+        a = a.astype(np.uint32)
+        a[rng.random(n) < 0.1] = o.M32
+        wp, wo = o.bucket_stable(a, n_act)
+        for thr in (1, 3, 8):
+            perm, off = cpu_ref.bucket(a, n_act, faithful=False, nthreads=thr)
+            np.testing.assert_array_equal(perm, wp, err_msg=f"{kind} {thr}")
+            np.testing.assert_array_equal(off, wo, err_msg=f"{kind} {thr}")
+
+
 def test_c_bucket_runs_matches_stable_partition():
     """cpu_bucket_runs (the micro-batch form of the CPU bucketing, cfg 5 baseline) = the stable
     partition restricted to the activations present, across reused scratch."""
