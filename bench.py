@@ -986,7 +986,7 @@ def cpu_baseline(args, tcd, G_total, pts, own, owner):
     return {"value": best["value"], "unit": "messages/s", "cores": cores, "kind": "port", "mode": "fast_n",
             "sample": f"{best['messages']} messages (cfg2 distribution, {sample}-message batches repeated) through "
                       f"the C restatement (oracle/cpu_ref.c) in fast mode (binary-search ring, open addressing, "
-                      f"parallel stable counting sort) on {cores} threads = this job's usable cores "
+                      f"parallel two-level stable partition) on {cores} threads = this job's usable cores "
                       f"(affinity + cgroup quota; os.cpu_count() = {host})",
             "modes": res, "host_cpus": host,
             "cfg1_ping_shape": cfg1,

@@ -10,7 +10,7 @@ for r in $(seq 1 "$ROUNDS"); do
     LIB=$A; [ $L = B ] && LIB=$B
     OUT="$ROOT/gpurun_out/abl_${TAG}_${L}_${r}.json"
     GRAINDISPATCH_LIB="$ROOT/$LIB" timeout -k 10 300 python3 "$ROOT/bench.py" $ARGS --no-cpu-baseline --latency-batches 0 \
-        --no-secondary > "$OUT" 2> "$OUT.err" || { echo "$L round $r failed"; tail -5 "$OUT.err"; exit 1; }
-    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); k=d.get('kernels',{}); print(sys.argv[2], 'round', sys.argv[3], round(d['value']/1e9,3), 'G/s', d['ms_per_step'], 'ms/step', {n: k[n]['ms_per_step'] for n in sorted(k, key=lambda n: -k[n]['ms_per_step'])[:6]})" "$OUT" "$L" "$r"
+        --no-secondary --full-out "$OUT.full" > "$OUT" 2> "$OUT.err" || { echo "$L round $r failed"; tail -5 "$OUT.err"; exit 1; }
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); k=json.load(open(sys.argv[1]+'.full')).get('kernels',{}); print(sys.argv[2], 'round', sys.argv[3], round(d['value']/1e9,3), 'G/s', d['ms_per_step'], 'ms/step', {n: k[n]['ms_per_step'] for n in sorted(k, key=lambda n: -k[n]['ms_per_step'])[:6]})" "$OUT" "$L" "$r"
   done
 done

@@ -8,8 +8,8 @@ for r in $(seq 1 "$ROUNDS"); do
   for L in A B; do
     O=$A; [ $L = B ] && O=$B
     OUT="$ROOT/gpurun_out/abo_${TAG}_${L}_${r}.json"
-    timeout -k 10 300 python3 "$ROOT/bench.py" $ARGS --no-cpu-baseline --latency-batches 0 --no-secondary --opt "$O" \
+    timeout -k 10 300 python3 "$ROOT/bench.py" $ARGS --no-cpu-baseline --latency-batches 0 --no-secondary --opt "$O" --full-out "$OUT.full" \
         > "$OUT" 2> "$OUT.err" || { echo "$L round $r failed"; tail -5 "$OUT.err"; exit 1; }
-    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); k=d.get('kernels',{}); print(sys.argv[2], 'round', sys.argv[3], round(d['value']/1e9,3), 'G/s', d['ms_per_step'], 'ms/step', {n: k[n]['ms_per_step'] for n in sorted(k, key=lambda n: -k[n]['ms_per_step'])[:4]})" "$OUT" "$O" "$r"
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); k=json.load(open(sys.argv[1]+'.full')).get('kernels',{}); print(sys.argv[2], 'round', sys.argv[3], round(d['value']/1e9,3), 'G/s', d['ms_per_step'], 'ms/step', {n: k[n]['ms_per_step'] for n in sorted(k, key=lambda n: -k[n]['ms_per_step'])[:4]})" "$OUT" "$O" "$r"
   done
 done
