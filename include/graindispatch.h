@@ -122,6 +122,9 @@ typedef struct gd_config {
 } gd_config;
 
 #define GD_CFG_KERNEL_TIMING 1u  /* record per-kernel HIP events (gd_kernel_times) */
+#define GD_CFG_NO_LANE_ORDER 2u  /* behave as on a device whose LDS atomics are not served in lane order:
+                                    every stable rank by ballots (GD_OPT_STABLE_RANK 0, 1 refused); the
+                                    library's own choice when gd_create's check fails (tests force it) */
 
 typedef struct gd_stats {
     uint64_t routed;          /* messages through gd_route*                          */
@@ -883,8 +886,10 @@ int gd_set_kernel_timing(gd_handle* h, int enable);
                                    wherever it applies (batches >= 2^20 messages, n_act < 2^28) */
 #define GD_OPT_L2_SMALL     3   /* two-level three-pass form: ranges of at most this many messages are
                                    sorted one wave a range (default 1024) */
-#define GD_OPT_STABLE_RANK  4   /* LSD passes' in-tile rank: 1 ds_add_rtn (default; gd_create verifies the
-                                   lane order it relies on and refuses a device without it), 0 ballots */
+#define GD_OPT_STABLE_RANK  4   /* every bucketing form's in-wave rank: 1 ds_add_rtn, whose same-address
+                                   lanes the hardware serves in lane order (default; gd_create checks that
+                                   order on the device), 0 ballots -- stable by construction; a device
+                                   failing the check gets 0 and refuses 1 */
 #define GD_OPT_WIRE_HEADERS 5   /* exchange headers of one-type long-key batches: 0 24-B keys, 1 u64
                                    N1s, 2 u32 N1s when every N1 < 2^32 (default) */
 #define GD_OPT_REGION_PROBE 6   /* exchange: (rank, region) partition + region-mapped owner probe: 0 (default) / 1 */

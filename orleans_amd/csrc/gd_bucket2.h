@@ -66,21 +66,20 @@ __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restrict__ key
                 for (int q = 0; q < 4; ++q) k[4 * j + q] = (i0 + q < n) ? keys[i0 + q] : 0u;
             }
         }
+        // the wave's hot digit (wave_hot_digit of its first row) counted in a register, the rest in LDS
+        const uint32_t h = wave_hot_digit(min(k[0], clamp) >> shift, base + 4 * threadIdx.x < n);
+        uint32_t hc = 0;
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
             const uint64_t i = base + 4 * ((j / 4) * NT + threadIdx.x) + (j % 4);
-            const bool valid = i < n;
             const uint32_t d = min(k[j], clamp) >> shift;
-            const unsigned long long act = __ballot(valid);
-            if (act == 0) continue;
-            const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
-            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
-            const unsigned long long hot = __ballot(valid && d == d0);
-            if (valid) {
-                if (d != d0) atomicAdd(&s_cnt[t][d], 1u);
-                else if (lane == lead) atomicAdd(&s_cnt[t][d], (uint32_t)__popcll(hot));
+            if (i < n) {
+                if (d == h) ++hc;
+                else atomicAdd(&s_cnt[t][d], 1u);
             }
         }
+        hc = wave_sum(hc);
+        if (lane == 0 && hc) atomicAdd(&s_cnt[t][h], hc);
     }
     __syncthreads();
     for (uint32_t x = threadIdx.x; x < TPB * R; x += NT) {
@@ -103,7 +102,7 @@ struct B2Pack {
 // The MSD pass's scatter: keys_in = the activations (clamped here), writes the message index and the
 // key (B2Out form) in digit order of min(key, clamp) >> shift.  gscan: the row-scanned counts
 // (k_radix_rowscan), totals: the digit totals.
-template <int NT, int IT, int RMAX, int KOUT>
+template <int NT, int IT, int RMAX, int KOUT, bool BALLOT = false>
 __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ keys_in, uint32_t n, uint32_t clamp,
                                                    uint32_t R, uint32_t tiles, const uint32_t* __restrict__ gscan,
                                                    const uint32_t* __restrict__ totals,
@@ -131,7 +130,6 @@ __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ 
     const uint32_t lane = lane_id();
     const uint32_t w = threadIdx.x / WAVE;
     const uint32_t half = (w & 1u) * 16u;
-    const uint32_t one = 1u << half;
     const unsigned long long lt = (1ull << lane) - 1ull;
     uint32_t kk[IT], rk[IT];
 #pragma unroll
@@ -152,34 +150,21 @@ __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ 
         kk[r] = base + pos < n ? min(kk[r], clamp) : 0u;
     }
     __syncthreads();
-    // stable rank within the wave: one ds_add_rtn per row on the wave's half of the pair counter (the
-    // lanes sharing the first live lane's digit fold into one update by that lane); 8 rows' updates
-    // go out before their hot lanes are resolved
+    // stable rank within the wave: the wave's hot digit (wave_hot_digit of its first row) by ballot in
+    // registers, every other item by its own update of the wave's half of the pair counter (row_rank16)
+    constexpr int DB = RMAX <= 512 ? 9 : 11;             // digit bits (BALLOT's matching)
+    const uint32_t h = wave_hot_digit(kk[0] >> shift, base + w * IT * WAVE + lane < n);
+    uint32_t hrun = 0;
 #pragma unroll
-    for (int r0 = 0; r0 < IT; r0 += 8) {
-        unsigned long long hot[8];
-        uint32_t lead[8];
-#pragma unroll
-        for (int r = r0; r < r0 + 8; ++r) {
-            const uint32_t idx = base + (w * IT + r) * WAVE + lane;
-            const bool valid = idx < n;
-            const uint32_t d = kk[r] >> shift;
-            const unsigned long long live = __ballot(valid);
-            const uint32_t ld = live ? (uint32_t)__ffsll((long long)live) - 1 : 0u;
-            const uint32_t hd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)ld);
-            hot[r - r0] = __ballot(valid && d == hd);
-            lead[r - r0] = ld;
-            rk[r] = 0;
-            if (valid && (d != hd || lane == ld))
-                rk[r] = atomicAdd(&s_cnt[w >> 1][d], lane == ld ? (uint32_t)__popcll(hot[r - r0]) << half : one);
-        }
-#pragma unroll
-        for (int r = r0; r < r0 + 8; ++r) {
-            const uint32_t mine = (rk[r] >> half) & 0xFFFFu;
-            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)lead[r - r0]);
-            rk[r] = ((hot[r - r0] >> lane) & 1ull) ? b0 + (uint32_t)__popcll(hot[r - r0] & lt) : mine;
-        }
+    for (int r = 0; r < IT; ++r) {
+        const bool valid = base + (w * IT + r) * WAVE + lane < n;
+        const uint32_t d = kk[r] >> shift;
+        const unsigned long long hm = __ballot(valid && d == h);
+        const uint32_t cr = row_rank16<BALLOT, DB>(&s_cnt[w >> 1][d], half, d, valid && d != h);
+        rk[r] = d == h ? hrun + (uint32_t)__popcll(hm & lt) : cr;
+        hrun += (uint32_t)__popcll(hm);
     }
+    if (lane == 0 && hrun) atomicAdd(&s_cnt[w >> 1][h], hrun << half);
     __syncthreads();
     // per digit: the waves' exclusive prefix (back into the halves), then tile-local digit starts and,
     // with the digit totals, the digit bases

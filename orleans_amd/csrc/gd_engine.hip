@@ -219,6 +219,8 @@ struct gd_handle {
     const uint32_t* last_totals = nullptr;   // the last radix pass's digit totals (row scans), and their count
     uint32_t last_digits = 0;
     uint32_t radix_rank_atomic = 1;   // stable in-wave rank by ds_add_rtn (1, A/B: ab_bucket.py) or ballots (0)
+    bool lane_order = true;           // gd_create's k_lane_order_check passed (else every rank by ballots)
+    bool lane_order_forced_off = false;   // GD_CFG_NO_LANE_ORDER: behave as on a device without it (tests)
 
     // pinned host scratch for small device -> host read-backs (counts, totals)
     void* h_pin = nullptr;
@@ -924,7 +926,7 @@ int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* 
 // index runs at R ~ 1,024; 65 against 76 us on 16K tiles at cfg 2), digit min(act, n_act) >> shift.
 // K16: the range-local keys as u16 (the one-pass form); else the whole clamped key as u32 (pass A of
 // the three-pass form).  Leaves the digit totals in last_totals.
-template <int RMAX, int KOUT>
+template <int RMAX, int KOUT, bool BALLOT>
 int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t R, uint32_t shift, uint32_t* k1,
              uint32_t* v1, B2Pack pk = B2Pack{0, 0, 32}) {
     const uint32_t tiles = blocks_for(n, B2_TILE);
@@ -941,7 +943,7 @@ int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uin
                       R, tiles, hist, shift, hxr));
     const uint32_t* tot = hist + (size_t)R * tiles;
     GD_TRY(launch(h, "k_radix_rowscan", dim3(R), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R * tiles));
-    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(B2_NT), 0, k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT>, acts, n,
+    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(B2_NT), 0, k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT, BALLOT>, acts, n,
                   n_act, R, tiles, (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk));
     h->last_totals = tot;
     h->last_digits = R;
@@ -951,6 +953,7 @@ int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uin
 // The one-pass two-level bucketing (gd_msd.h): a stable MSD pass on the high digit min(act, n_act) >> 10,
 // then k_msd_local sorts each 1,024-activation range in LDS and writes its starts.  Needs (n_act >> 10)
 // + 1 <= B2_RMAX2.
+template <bool BALLOT>
 int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                uint32_t* rank_out) {
     const uint32_t R = (n_act >> MSD_SHIFT) + 1;
@@ -959,8 +962,8 @@ int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, u
     GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
     uint32_t* k1 = (uint32_t*)h->u32_a.p;
     uint32_t* v1 = (uint32_t*)h->u32_c.p;
-    GD_TRY((msd_pass<B2_RMAX2, B2_KEY16>(h, acts, n, n_act, R, MSD_SHIFT, k1, v1)));
-    return launch(h, "k_msd_local", dim3(std::min<uint32_t>(R, h->n_cu)), dim3(MSD_NT), 0, k_msd_local,
+    GD_TRY((msd_pass<B2_RMAX2, B2_KEY16, BALLOT>(h, acts, n, n_act, R, MSD_SHIFT, k1, v1)));
+    return launch(h, "k_msd_local", dim3(std::min<uint32_t>(R, h->n_cu)), dim3(MSD_NT), 0, k_msd_local<BALLOT>,
                   (const uint16_t*)k1, (const uint32_t*)v1, h->last_totals, R, n, n_act, perm, offsets, rank_out);
 }
 
@@ -985,6 +988,7 @@ bool msd3_split(uint32_t n_act, uint32_t* a_out, uint32_t* ra_out) {
 // (MSD on d2 = k' >> a), pass B (segmented MSD on d1 = k' & (2^a - 1), one flat scan for the
 // positions), then the level-2 work lists (thin ranges a wave each, staged ranges a workgroup each,
 // hot ranges in chunks).  Grids of the level-2 kernels are bounded and loop over device-side counts.
+template <bool BALLOT>
 int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                 uint32_t* rank_out) {
     uint32_t a = 0, RA = 0;
@@ -1036,8 +1040,8 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     const uint32_t pbits = a + MSD_SHIFT, hb = pbits > 16 ? pbits - 16 : 0;
     const bool pk = hb == 0 || ib + hb <= 32;
     const B2Pack bp{pbits, hb, hb ? ib : 32u};
-    if (pk) GD_TRY((msd_pass<SEG_RMAX, B2_PACK>(h, acts, n, n_act, RA, MSD_SHIFT + a, kA, vA, bp)));
-    else GD_TRY((msd_pass<SEG_RMAX, B2_KEY32>(h, acts, n, n_act, RA, MSD_SHIFT + a, kA, vA)));
+    if (pk) GD_TRY((msd_pass<SEG_RMAX, B2_PACK, BALLOT>(h, acts, n, n_act, RA, MSD_SHIFT + a, kA, vA, bp)));
+    else GD_TRY((msd_pass<SEG_RMAX, B2_KEY32, BALLOT>(h, acts, n, n_act, RA, MSD_SHIFT + a, kA, vA)));
     const SegIn in{(const uint16_t*)kA, (const uint32_t*)kA, (const uint32_t*)vA, hb, bp.ib};
     GD_TRY(launch(h, "k_seg_table", dim3(1), dim3(1024), 0, k_seg_table, h->last_totals, RA, tbound, seg_start, seg_tb,
                   tile_seg, (uint32_t*)m[5].p));
@@ -1050,11 +1054,11 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
                       (const uint32_t*)seg_start, (const uint32_t*)seg_tb, RB, hseg));
     GD_TRY(scan_device<OpAdd>(h, hseg, RB * tbound, false, false, "seg"));
     if (pk)
-        GD_TRY(launch(h, "k_seg_scatter", dim3(tbound), dim3(SEG_NT), 0, k_seg_scatter<true>, in,
+        GD_TRY(launch(h, "k_seg_scatter", dim3(tbound), dim3(SEG_NT), 0, k_seg_scatter<true, BALLOT>, in,
                       (const uint32_t*)tile_seg, (const uint32_t*)seg_start, (const uint32_t*)seg_tb, RB,
                       (const uint32_t*)hseg, kB, vB, h->xcd_tiles));
     else
-        GD_TRY(launch(h, "k_seg_scatter", dim3(tbound), dim3(SEG_NT), 0, k_seg_scatter<false>, in,
+        GD_TRY(launch(h, "k_seg_scatter", dim3(tbound), dim3(SEG_NT), 0, k_seg_scatter<false, BALLOT>, in,
                       (const uint32_t*)tile_seg, (const uint32_t*)seg_start, (const uint32_t*)seg_tb, RB,
                       (const uint32_t*)hseg, kB, vB, h->xcd_tiles));
     // level 2
@@ -1070,13 +1074,13 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     // sort 1 a CU (135 KB), the chunk scatter 2 (72 KB), the chunk histogram 4 and the scan 2 a CU
     const uint32_t cu8 = (h->n_cu + 7) & ~7u;
     GD_TRY(launch(h, "k_l2_small", dim3(std::min<uint32_t>(blocks_for(R, L2_SMALL_WAVES), 4 * cu8)),
-                  dim3(L2_SMALL_WAVES * WAVE), 0, k_l2_small, (const uint16_t*)kB, (const uint32_t*)vB, l, n, n_act, perm,
+                  dim3(L2_SMALL_WAVES * WAVE), 0, k_l2_small<BALLOT>, (const uint16_t*)kB, (const uint32_t*)vB, l, n, n_act, perm,
                   offsets, rank_out));
     GD_TRY(launch(h, "k_msd_local_mid", dim3(std::min<uint32_t>(R, 3 * cu8)), dim3(MSD_MID_NT), 0,
-                  k_msd_local_list<MSD_MID_NT, MSD_MID_RW>, (const uint16_t*)kB, (const uint32_t*)vB,
+                  k_msd_local_list<MSD_MID_NT, MSD_MID_RW, BALLOT>, (const uint16_t*)kB, (const uint32_t*)vB,
                   (const uint32_t*)l.rs, (const uint32_t*)l.mid, (const uint32_t*)(l.ctr + 5), n, n_act, perm, offsets,
                   rank_out));
-    GD_TRY(launch(h, "k_msd_local", dim3(std::min<uint32_t>(R, cu8)), dim3(MSD_NT), 0, k_msd_local_list<MSD_NT, MSD_RW>,
+    GD_TRY(launch(h, "k_msd_local", dim3(std::min<uint32_t>(R, cu8)), dim3(MSD_NT), 0, k_msd_local_list<MSD_NT, MSD_RW, BALLOT>,
                   (const uint16_t*)kB, (const uint32_t*)vB, (const uint32_t*)l.rs, (const uint32_t*)l.staged,
                   (const uint32_t*)(l.ctr + 1), n, n_act, perm, offsets, rank_out));
     uint32_t* hh = (uint32_t*)m[10].p;
@@ -1088,7 +1092,7 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     GD_TRY(launch(h, "k_l2_chunk_ptot", dim3(2 * cu8), dim3(MSD_NT), 0, k_l2_chunk_ptot, l, (const uint32_t*)hh, ptot));
     GD_TRY(launch(h, "k_l2_chunk_scan", dim3(2 * cu8), dim3(MSD_NT), 0, k_l2_chunk_scan, l, hh, (const uint32_t*)ptot,
                   tot));
-    return launch(h, "k_l2_chunk_scatter", dim3(2 * cu8), dim3(CH_NT), 0, k_l2_chunk_scatter,
+    return launch(h, "k_l2_chunk_scatter", dim3(2 * cu8), dim3(CH_NT), 0, k_l2_chunk_scatter<BALLOT>,
                   (const uint16_t*)kB, (const uint32_t*)vB, l, (const uint32_t*)hh, (const uint32_t*)tot, n, n_act, perm,
                   offsets, rank_out);
 }
@@ -1118,8 +1122,14 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
         while (per_range < 31 && ((uint64_t)n / ((n_act >> MSD_SHIFT) + 1) >> per_range) > 1) ++per_range;
         const int var = h->msd_mode == 2 ? 1 : tune_choose(h, 4, n, &meas, 2, per_range);
         CxMeasure mm(h, meas, n);
-        if (var == 1) return one ? msd_bucket(h, acts, n, n_act, perm, offsets, rank_out)
-                                 : msd3_bucket(h, acts, n, n_act, perm, offsets, rank_out);
+        // ranks by ds_add_rtn lane order (default) or by ballots (GD_OPT_STABLE_RANK 0; gd_create's
+        // choice on a device without that order)
+        if (var == 1 && h->radix_rank_atomic)
+            return one ? msd_bucket<false>(h, acts, n, n_act, perm, offsets, rank_out)
+                       : msd3_bucket<false>(h, acts, n, n_act, perm, offsets, rank_out);
+        if (var == 1)
+            return one ? msd_bucket<true>(h, acts, n, n_act, perm, offsets, rank_out)
+                       : msd3_bucket<true>(h, acts, n, n_act, perm, offsets, rank_out);
         return bucket_lsd(h, acts, n, n_act, perm, offsets, rank_out);
     }
     return bucket_lsd(h, acts, n, n_act, perm, offsets, rank_out);
@@ -1455,9 +1465,9 @@ const char* gd_last_error(const gd_handle* h) {
     return g_tls_error.c_str();
 }
 
-// The stable ranks' hardware assumption (gd_msd.h k_lane_order_check): refuse the handle on a device
-// that does not serve one wave's same-address LDS atomics in lane order -- every bucketing would be
-// silently unstable there.
+// The stable ranks' hardware assumption (gd_msd.h k_lane_order_check): on a device that does not serve
+// one wave's same-address LDS atomics in lane order, the handle ranks by ballots instead (stable by
+// construction; GD_OPT_STABLE_RANK reads 0 and refuses 1 there).
 static int lane_order_check(gd_handle* h) {
     uint32_t* d = nullptr;
     if (hipMalloc(&d, 256 * 4) != hipSuccess) return set_err(nullptr, GD_ENOMEM, "lane-order check buffer");
@@ -1470,11 +1480,8 @@ static int lane_order_check(gd_handle* h) {
     if (e != hipSuccess) return set_err(nullptr, GD_EHIP, "lane-order check: %s", hipGetErrorString(e));
     uint64_t bad = 0;
     for (uint32_t x : hbad) bad += x;
-    if (bad)
-        return set_err(nullptr, GD_EHIP,
-                       "this device does not serve same-address LDS atomics in lane order (%llu mismatches): "
-                       "the library's stable ranks would be wrong here",
-                       (unsigned long long)bad);
+    h->lane_order = bad == 0 && !h->lane_order_forced_off;
+    if (!h->lane_order) h->radix_rank_atomic = 0;
     return GD_OK;
 }
 
@@ -1487,6 +1494,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     h->cfg = *cfg;
     h->device = cfg->device;
     h->timing = (cfg->flags & GD_CFG_KERNEL_TIMING) != 0;
+    h->lane_order_forced_off = (cfg->flags & GD_CFG_NO_LANE_ORDER) != 0;
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
         int r = set_err(nullptr, GD_EHIP, "hipSetDevice(%d): %s", h->device, hipGetErrorString(e));
@@ -2052,6 +2060,9 @@ int gd_option_set(gd_handle* h, int option, int64_t v) {
             return GD_OK;
         case GD_OPT_STABLE_RANK:
             if (!in(0, 1)) break;
+            if (v == 1 && !h->lane_order)
+                return set_err(h, GD_EINVAL, "gd_option_set: GD_OPT_STABLE_RANK 1 needs the LDS lane order this "
+                               "device lacks (gd_create's check): ranks stay on ballots");
             h->radix_rank_atomic = (uint32_t)v;
             return GD_OK;
         case GD_OPT_WIRE_HEADERS:
@@ -2204,15 +2215,16 @@ int mb_launch_sort(gd_microbatch* mb, dim3 grid, uint32_t bits, const uint32_t* 
     const dim3 b(MB_THREADS);
     const uint32_t na = mb->n_act;
     unsigned long long* ts = mb->ts;
+    const uint32_t bal = h->radix_rank_atomic ? 0u : 1u;
     switch (bits) {
-        case 4: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<4, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
-        case 5: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<5, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
-        case 6: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<6, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
-        case 7: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<7, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
-        case 8: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<8, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
-        case 9: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<9, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
-        case 10: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<10, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
-        default: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<11, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts);
+        case 4: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<4, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
+        case 5: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<5, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
+        case 6: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<6, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
+        case 7: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<7, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
+        case 8: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<8, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
+        case 9: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<9, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
+        case 10: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<10, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
+        default: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<11, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
     }
 }
 

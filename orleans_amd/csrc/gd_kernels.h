@@ -1806,6 +1806,78 @@ __device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t x) {
     return x;
 }
 
+// Wave-wide sum, uniform.
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(x), WAVE - 1);
+}
+
+// ---- row counts and ranks of the bucketing kernels (gd_bucket2.h, gd_msd.h, gd_msd2.h) ----------
+// A row is one wave instruction's 64 items, each with a digit d; counters are per wave.
+//
+// The wave's hot digit: the digit most of a row holds, of four candidate lanes' digits (lanes 0, 16,
+// 32, 48), when at least 8 of the row's valid lanes hold it; else NONE32.  Uniform over the wave.
+// Under Zipf skew (BASELINE cfg 3: one pass-A digit holds 86 % of the messages, one range 62 %) the
+// hot digit's items are then counted and ranked in registers by ballot -- no LDS atomic and none of the
+// same-address serialisation a hot counter costs (64 lanes on one LDS address take 64 cycles) -- and
+// every other item takes its own counter update.  A wave keeps one hot digit for all its rows of a tile.
+__device__ __forceinline__ uint32_t wave_hot_digit(uint32_t d, bool valid) {
+    uint32_t best = NONE32, bc = 7;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t cd = (uint32_t)__builtin_amdgcn_readlane((int)(valid ? d : NONE32), 16 * q);
+        const uint32_t c = (uint32_t)__popcll(__ballot(valid && d == cd));
+        if (cd != NONE32 && c > bc) {
+            bc = c;
+            best = cd;
+        }
+    }
+    return best;
+}
+
+// This lane's place among the wave's earlier items with its digit d, from the wave's u16 counter at
+// bit sh of *p, which this row's valid items then advance.  BALLOT = false: one ds_add_rtn a lane --
+// the lanes of one instruction on one address are served in ascending lane order (gd_create
+// checks it on the device).  BALLOT = true: stable by construction -- the lanes sharing d found by
+// ballots over its B bits (match_digit), the lowest of them adds the group's size, every lane of the
+// group takes the base from that lane (ds_bpermute) plus its count of lower peers (GD_OPT_STABLE_RANK
+// 0, and the library's choice when gd_create finds the lane order missing).  Call with every lane.
+template <bool BALLOT, int B>
+__device__ __forceinline__ uint32_t row_rank16(uint32_t* p, uint32_t sh, uint32_t d, bool valid) {
+    if constexpr (!BALLOT) {
+        uint32_t old = 0;
+        if (valid) old = atomicAdd(p, 1u << sh);
+        return (old >> sh) & 0xFFFFu;
+    } else {
+        const unsigned long long peers = match_digit<B>(d, valid);
+        const uint32_t lane = lane_id();
+        const uint32_t below = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+        uint32_t old = 0;
+        if (valid && below == 0) old = atomicAdd(p, (uint32_t)__popcll(peers) << sh);
+        const int src = peers ? __ffsll((long long)peers) - 1 : (int)lane;
+        old = (uint32_t)__shfl((int)old, src, WAVE);
+        return ((old >> sh) & 0xFFFFu) + below;
+    }
+}
+
+// row_rank16 over whole u32 counters.
+template <bool BALLOT, int B>
+__device__ __forceinline__ uint32_t row_rank32(uint32_t* p, uint32_t d, bool valid) {
+    if constexpr (!BALLOT) {
+        uint32_t old = 0;
+        if (valid) old = atomicAdd(p, 1u);
+        return old;
+    } else {
+        const unsigned long long peers = match_digit<B>(d, valid);
+        const uint32_t lane = lane_id();
+        const uint32_t below = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+        uint32_t old = 0;
+        if (valid && below == 0) old = atomicAdd(p, (uint32_t)__popcll(peers));
+        const int src = peers ? __ffsll((long long)peers) - 1 : (int)lane;
+        old = (uint32_t)__shfl((int)old, src, WAVE);
+        return old + below;
+    }
+}
+
 // Block-wide exclusive sum over MB_THREADS threads (two barriers).
 __device__ __forceinline__ uint32_t mb_block_excl_sum(uint32_t v, uint32_t* s_wsum) {
     const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
@@ -1827,7 +1899,7 @@ __device__ __forceinline__ void mb_sort_runs_core(MbShared& sh, uint32_t (&kk)[I
                                                   uint32_t passes, uint32_t* __restrict__ perm,
                                                   uint32_t* __restrict__ run_act, uint32_t* __restrict__ run_start,
                                                   uint32_t* __restrict__ n_runs, uint32_t lo, uint32_t hi,
-                                                  unsigned long long* ts) {
+                                                  unsigned long long* ts, bool ballot) {
     constexpr uint32_t R = 1u << BITS;
     constexpr uint32_t WORDS = R * MB_NW / 2;
     constexpr uint32_t WPT = WORDS >= MB_THREADS ? WORDS / MB_THREADS : 1;   // counter words per thread
@@ -1849,34 +1921,29 @@ __device__ __forceinline__ void mb_sort_runs_core(MbShared& sh, uint32_t (&kk)[I
     __syncthreads();
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const uint32_t shift = pass * BITS;
-        // Stable in-wave rank by ds_add_rtn (lanes served in ascending order, wave LDS ops in program
-        // order: the k_radix_scatter ranking); the first live lane's digit group takes one update.
-        // Rows past n are skipped wave-uniformly.
-        uint32_t rk[IT], lead[IT];
-        unsigned long long hot[IT];
+        // Stable in-wave rank: the wave's hot digit by ballot in registers, the others by row_rank16
+        // (ds_add_rtn in lane order, or ballots when `ballot`: GD_OPT_STABLE_RANK 0).  Rows past n are
+        // skipped wave-uniformly.
+        uint32_t rk[IT];
+        const uint32_t h = wave_hot_digit(kk[0] >> shift & (R - 1), (uint32_t)(w * IT) * WAVE + lane < n);
+        uint32_t hrun = 0;
 #pragma unroll
         for (int r = 0; r < IT; ++r) {
             rk[r] = 0;
-            hot[r] = 0;
-            lead[r] = 0;
             if ((uint32_t)(w * IT + r) * WAVE >= n) continue;
             const bool valid = (w * IT + r) * WAVE + lane < n;
             const uint32_t d = (kk[r] >> shift) & (R - 1);
-            const unsigned long long live = __ballot(valid);
-            lead[r] = (uint32_t)__ffsll((long long)live) - 1;
-            const uint32_t hd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead[r]);
-            hot[r] = __ballot(valid && d == hd);
-            if (valid && (d != hd || lane == lead[r])) {
-                const uint32_t e = d * MB_NW + w, sh16 = (e & 1u) * 16u;
-                const uint32_t inc = lane == lead[r] ? (uint32_t)__popcll(hot[r]) : 1u;
-                rk[r] = (atomicAdd(&s_cnt[cw(e >> 1)], inc << sh16) >> sh16) & 0xFFFFu;
-            }
+            const uint32_t e = d * MB_NW + w, sh16 = (e & 1u) * 16u;
+            const unsigned long long hm = __ballot(valid && d == h);
+            const bool cold = valid && d != h;
+            const uint32_t cr = ballot ? row_rank16<true, BITS>(&s_cnt[cw(e >> 1)], sh16, d, cold)
+                                       : row_rank16<false, BITS>(&s_cnt[cw(e >> 1)], sh16, d, cold);
+            rk[r] = d == h ? hrun + (uint32_t)__popcll(hm & lt) : cr;
+            hrun += (uint32_t)__popcll(hm);
         }
-#pragma unroll
-        for (int r = 0; r < IT; ++r) {
-            if ((uint32_t)(w * IT + r) * WAVE >= n) continue;
-            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)rk[r], (int)lead[r]);
-            if ((hot[r] >> lane) & 1ull) rk[r] = b0 + (uint32_t)__popcll(hot[r] & lt);
+        if (lane == 0 && hrun) {
+            const uint32_t e = h * MB_NW + w;
+            atomicAdd(&s_cnt[cw(e >> 1)], hrun << ((e & 1u) * 16u));
         }
         __syncthreads();
         if (pass == 0) mb_mark(ts, 4, t);
@@ -1994,7 +2061,7 @@ __global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32_t* __r
                                                               uint32_t* __restrict__ run_start,
                                                               uint32_t* __restrict__ n_runs,
                                                               uint32_t* __restrict__ act_copy,
-                                                              unsigned long long* ts) {
+                                                              unsigned long long* ts, uint32_t ballot) {
     __shared__ MbShared sh;
     const uint32_t lane = lane_id(), w = threadIdx.x / WAVE;
     const uint32_t lo = (uint32_t)((uint64_t)n * blockIdx.x / gridDim.x);
@@ -2008,7 +2075,7 @@ __global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32_t* __r
         kk[r] = a < n_act ? a : n_act;
         vv[r] = idx;
     }
-    mb_sort_runs_core<BITS, IT>(sh, kk, vv, n, passes, perm, run_act, run_start, n_runs, lo, hi, ts);
+    mb_sort_runs_core<BITS, IT>(sh, kk, vv, n, passes, perm, run_act, run_start, n_runs, lo, hi, ts, ballot != 0);
 }
 
 }  // namespace gd

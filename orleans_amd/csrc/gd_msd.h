@@ -87,38 +87,6 @@ __device__ __forceinline__ void msd_wave_prefix(uint32_t* wc, uint32_t tid, uint
     }
 }
 
-// Hot-key folding for the per-wave u16-pair counters (FOLD): the lanes of a row holding the first live
-// lane's key add to its counter with one LDS atomic by that lane, the others one each.  Under Zipf skew
-// many lanes of a row share a hot activation, and same-address LDS atomics serialise.  k = 0xFFFF: no
-// key.  msd_fold_count counts; msd_fold_rank returns this lane's place: its counter's value before the
-// add, plus its rank among the folded lanes (lane order: stable).
-__device__ __forceinline__ void msd_fold_count(uint32_t* wc, uint32_t k) {
-    const uint32_t lane = threadIdx.x & (WAVE - 1);
-    const bool valid = k != 0xFFFFu;
-    const unsigned long long live = __ballot(valid);
-    if (!live) return;
-    const uint32_t ld = (uint32_t)__ffsll((long long)live) - 1;
-    const uint32_t hk = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)ld);
-    const unsigned long long hot = __ballot(valid && k == hk);
-    if (valid && (k != hk || lane == ld))
-        atomicAdd(&wc[k >> 1], (lane == ld ? (uint32_t)__popcll(hot) : 1u) << (16 * (k & 1)));
-}
-__device__ __forceinline__ uint32_t msd_fold_rank(uint32_t* wc, uint32_t k) {
-    const uint32_t lane = threadIdx.x & (WAVE - 1);
-    const bool valid = k != 0xFFFFu;
-    const unsigned long long live = __ballot(valid);
-    const uint32_t ld = live ? (uint32_t)__ffsll((long long)live) - 1 : 0u;
-    const uint32_t hk = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)ld);
-    const unsigned long long hot = __ballot(valid && k == hk);
-    uint32_t r = 0;
-    if (valid && (k != hk || lane == ld)) {
-        const uint32_t old = atomicAdd(&wc[k >> 1], (lane == ld ? (uint32_t)__popcll(hot) : 1u) << (16 * (k & 1)));
-        r = (old >> (16 * (k & 1))) & 0xFFFFu;
-    }
-    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)r, (int)ld);
-    return ((hot >> lane) & 1ull) ? b0 + (uint32_t)__popcll(hot & ((1ull << lane) - 1ull)) : r;
-}
-
 // Range b = activations [b << 10, (b << 10) + L) holding the S messages at [base, base + S) of the
 // MSD output (rk: range-local keys, u16; ri: message indices).  Writes perm[base, base + S), the
 // range's bucket starts offsets[b << 10, ... + L) and, for the range holding n_act, offsets[n_act + 1]
@@ -151,7 +119,7 @@ struct MsdNoPrefetch {
 // msd_range with the staged path's keys already in kp (msd_load_keys); after() runs once the count
 // sweep is done with them -- the persistent form issues the next range's key loads there, so they
 // fly under this range's scan, ranking and write-out.
-template <bool FOLD, int NT, int RW, class After>
+template <bool BALLOT, int NT, int RW, class After>
 __device__ __forceinline__ void msd_range_kp(MsdShared<NT, RW>& sh, uint32_t b, uint32_t base, uint32_t S,
                                              const uint16_t* __restrict__ keys16, const uint32_t* __restrict__ idx,
                                              uint32_t n, uint32_t n_act, uint32_t* __restrict__ perm,
@@ -175,8 +143,7 @@ __device__ __forceinline__ void msd_range_kp(MsdShared<NT, RW>& sh, uint32_t b, 
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
             const uint32_t k = (kp[r / 2] >> (16 * (r & 1))) & 0xFFFFu;
-            if constexpr (FOLD) msd_fold_count(sh.wc[w], k);
-            else if (k != 0xFFFFu) atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
+            if (k != 0xFFFFu) atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
         }
         // the rank sweep decodes the keys again rather than keeping the count sweep's addresses live
         // across the barriers (that spilled)
@@ -206,14 +173,8 @@ __device__ __forceinline__ void msd_range_kp(MsdShared<NT, RW>& sh, uint32_t b, 
 #pragma unroll
             for (int r = 0; r < MSD_G && g + r < RW; ++r) {
                 const uint32_t k = (kp[(g + r) / 2] >> (16 * ((g + r) & 1))) & 0xFFFFu;
-                if constexpr (FOLD) {
-                    const uint32_t at = msd_fold_rank(sh.wc[w], k);
-                    if (k != 0xFFFFu) sh.out[sh.run[k] + at] = mm[r];
-                } else {
-                    if (k == 0xFFFFu) continue;
-                    const uint32_t old = atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
-                    sh.out[sh.run[k] + ((old >> (16 * (k & 1))) & 0xFFFFu)] = mm[r];
-                }
+                const uint32_t at = row_rank16<BALLOT, 10>(&sh.wc[w][k >> 1], 16 * (k & 1), k, k != 0xFFFFu);
+                if (k != 0xFFFFu) sh.out[sh.run[k] + at] = mm[r];
             }
         }
         __syncthreads();
@@ -267,10 +228,11 @@ __device__ __forceinline__ void msd_range_kp(MsdShared<NT, RW>& sh, uint32_t b, 
 #pragma unroll 1
         for (uint32_t r0 = s0; r0 < s1; r0 += WAVE) {     // whole rows, so every lane keeps row order
             const uint32_t i = r0 + lane;
-            if (i < s1) {
-                const uint32_t k = rk[i], m = ri[i];
-                const uint32_t old = atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
-                const uint32_t pos = base + sh.run[k] + ((old >> (16 * (k & 1))) & 0xFFFFu);
+            const bool valid = i < s1;
+            const uint32_t k = valid ? rk[i] : 0u, m = valid ? ri[i] : 0u;
+            const uint32_t at = row_rank16<BALLOT, 10>(&sh.wc[w][k >> 1], 16 * (k & 1), k, valid);
+            if (valid) {
+                const uint32_t pos = base + sh.run[k] + at;
                 perm[pos] = m;
                 if (rank_out) rank_out[m] = pos;
             }
@@ -285,14 +247,14 @@ __device__ __forceinline__ void msd_range_kp(MsdShared<NT, RW>& sh, uint32_t b, 
     __syncthreads();
 }
 
-template <bool FOLD, int NT = MSD_NT, int RW = MSD_RW>
+template <bool BALLOT, int NT = MSD_NT, int RW = MSD_RW>
 __device__ __forceinline__ void msd_range(MsdShared<NT, RW>& sh, uint32_t b, uint32_t base, uint32_t S,
                                           const uint16_t* __restrict__ keys16, const uint32_t* __restrict__ idx,
                                           uint32_t n, uint32_t n_act, uint32_t* __restrict__ perm,
                                           uint32_t* __restrict__ offsets, uint32_t* __restrict__ rank_out) {
     uint32_t kp[RW / 2];
     msd_load_keys<NT, RW>(keys16 + base, S, kp);
-    msd_range_kp<FOLD, NT, RW>(sh, b, base, S, keys16, idx, n, n_act, perm, offsets, rank_out, kp, MsdNoPrefetch{});
+    msd_range_kp<BALLOT, NT, RW>(sh, b, base, S, keys16, idx, n, n_act, perm, offsets, rank_out, kp, MsdNoPrefetch{});
 }
 
 // The hardware property every stable rank of this library rests on (the LSD and MSD scatters, the
@@ -341,6 +303,7 @@ __global__ void __launch_bounds__(256) k_lane_order_check(uint32_t* __restrict__
 // range's key loads issued under the previous range's scan, ranking and write-out (msd_range_kp).
 // Against one workgroup a range (round 3): 0.0523 -> 0.0495 ms at cfg 2, stage 0.148 -> 0.146 ms
 // (3 interleaved rounds each).
+template <bool BALLOT>
 __global__ void __launch_bounds__(MSD_NT, 1) k_msd_local(const uint16_t* __restrict__ keys16,
                                                             const uint32_t* __restrict__ idx,
                                                             const uint32_t* __restrict__ totals, uint32_t R,
@@ -367,7 +330,7 @@ __global__ void __launch_bounds__(MSD_NT, 1) k_msd_local(const uint16_t* __restr
         const uint32_t nS = nb < R ? totals[nb] : 0u;
         const uint32_t nbase = nb < R ? s_base[nb] : 0u;
         auto next = [&] { msd_load_keys<MSD_NT, MSD_RW>(keys16 + nbase, nS, kn); };
-        msd_range_kp<false, MSD_NT, MSD_RW>(sh, b, s_base[b], S, keys16, idx, n, n_act, perm, offsets, rank_out, kp,
+        msd_range_kp<BALLOT, MSD_NT, MSD_RW>(sh, b, s_base[b], S, keys16, idx, n, n_act, perm, offsets, rank_out, kp,
                                             next);
         if (S > MSD_CAP) next();                         // a hot range takes the chunked path: no after()
 #pragma unroll
@@ -381,7 +344,7 @@ __global__ void __launch_bounds__(MSD_NT, 1) k_msd_local(const uint16_t* __restr
 // up to 24,576 messages, 135 KB of LDS (one a CU); <512, 16>: up to 8,192, 52 KB (three a CU) -- the
 // ranges of a few thousand messages of BASELINE cfg 4 (~4,400 a range) and cfg 3's mid ranks.  (Hot-key
 // folding measured slower here: 0.077 against 0.059 ms at cfg 3.)
-template <int NT, int RW>
+template <int NT, int RW, bool BALLOT>
 __global__ void __launch_bounds__(NT, (NT == MSD_NT ? 4 : 6)) k_msd_local_list(const uint16_t* __restrict__ keys16,
                                                                               const uint32_t* __restrict__ idx,
                                                                               const uint32_t* __restrict__ rs,
@@ -396,7 +359,7 @@ __global__ void __launch_bounds__(NT, (NT == MSD_NT ? 4 : 6)) k_msd_local_list(c
     for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
         const uint32_t b = list[i];
         const uint32_t base = rs[b];
-        msd_range<false, NT, RW>(sh, b, base, rs[b + 1] - base, keys16, idx, n, n_act, perm, offsets, rank_out);
+        msd_range<BALLOT, NT, RW>(sh, b, base, rs[b + 1] - base, keys16, idx, n, n_act, perm, offsets, rank_out);
     }
 }
 

@@ -164,6 +164,14 @@ __global__ void __launch_bounds__(SEG_NT) k_seg_hist(SegIn in, const uint32_t* _
     if (threadIdx.x == 0 && et < st.base + st.cnt)
         v[NL] = PK ? *reinterpret_cast<const uint4*>(in.keys16 + et) : *reinterpret_cast<const uint4*>(in.keys32 + et);
     __syncthreads();
+    // the wave's hot digit (from its first load's last key: past a misaligned segment start) in a
+    // register, every other key one LDS add
+    uint32_t h, hc = 0;
+    {
+        const uint32_t e = a0 + PER * threadIdx.x + PER - 1;
+        const uint32_t k = PK ? v[0].w >> 16 : v[0].w;
+        h = wave_hot_digit((k >> dsh) & (rb - 1), e >= st.base && e < st.base + st.cnt);
+    }
 #pragma unroll
     for (uint32_t j = 0; j <= NL; ++j) {
         const uint32_t e0 = j < NL ? a0 + PER * (j * SEG_NT + threadIdx.x) : et;
@@ -174,24 +182,21 @@ __global__ void __launch_bounds__(SEG_NT) k_seg_hist(SegIn in, const uint32_t* _
             const bool valid = e >= st.base && e < st.base + st.cnt && (j < NL || threadIdx.x == 0);
             const uint32_t k = PK ? (w4[q / 2] >> (16 * (q & 1))) & 0xFFFFu : w4[q];
             const uint32_t d = (k >> dsh) & (rb - 1);
-            const unsigned long long act = __ballot(valid);
-            if (act == 0) continue;
-            const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
-            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)lead);
-            const unsigned long long hot = __ballot(valid && d == d0);
             if (valid) {
-                if (d != d0) atomicAdd(&s_cnt[d], 1u);
-                else if (lane == lead) atomicAdd(&s_cnt[d], (uint32_t)__popcll(hot));
+                if (d == h) ++hc;
+                else atomicAdd(&s_cnt[d], 1u);
             }
         }
     }
+    hc = wave_sum(hc);
+    if (lane == 0 && hc) atomicAdd(&s_cnt[h], hc);
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < rb; d += SEG_NT) hseg[(size_t)st.tb * rb + (size_t)d * st.ts + st.tl] = s_cnt[d];
 }
 
 // Pass B scatter: tile j's records ranked stably by d1 and written at the flat-scanned positions
 // hseg[tb * rb + d * ts + tl] + rank: the range-local key (key & 1023) as u16 and the index.
-template <bool PK>
+template <bool PK, bool BALLOT = false>
 __global__ void __launch_bounds__(SEG_NT) k_seg_scatter(SegIn in, const uint32_t* __restrict__ tile_seg,
                                                         const uint32_t* __restrict__ seg_start,
                                                         const uint32_t* __restrict__ seg_tb, uint32_t rb,
@@ -216,7 +221,6 @@ __global__ void __launch_bounds__(SEG_NT) k_seg_scatter(SegIn in, const uint32_t
     const uint32_t lane = lane_id();
     const uint32_t w = threadIdx.x / WAVE;
     const uint32_t half = (w & 1u) * 16u;
-    const uint32_t one = 1u << half;
     const unsigned long long lt = (1ull << lane) - 1ull;
     const uint32_t imask = PK ? (in.ib >= 32 ? 0xFFFFFFFFu : (1u << in.ib) - 1u) : 0xFFFFFFFFu;
     uint32_t kk[IT], vv[IT], rk[IT];
@@ -235,30 +239,19 @@ __global__ void __launch_bounds__(SEG_NT) k_seg_scatter(SegIn in, const uint32_t
         }
     }
     __syncthreads();
+    // stable rank within the wave: the wave's hot digit by ballot in registers, the rest by row_rank16
+    const uint32_t h = wave_hot_digit((kk[0] >> B2_LOW_BITS) & mask, w * IT * WAVE + lane < st.cnt);
+    uint32_t hrun = 0;
 #pragma unroll
-    for (int r0 = 0; r0 < IT; r0 += 8) {
-        unsigned long long hot[8];
-        uint32_t lead[8];
-#pragma unroll
-        for (int r = r0; r < r0 + 8; ++r) {
-            const bool valid = (w * IT + r) * WAVE + lane < st.cnt;
-            const uint32_t d = (kk[r] >> B2_LOW_BITS) & mask;
-            const unsigned long long live = __ballot(valid);
-            const uint32_t ld = live ? (uint32_t)__ffsll((long long)live) - 1 : 0u;
-            const uint32_t hd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)ld);
-            hot[r - r0] = __ballot(valid && d == hd);
-            lead[r - r0] = ld;
-            rk[r] = 0;
-            if (valid && (d != hd || lane == ld))
-                rk[r] = atomicAdd(&s_cnt[w >> 1][d], lane == ld ? (uint32_t)__popcll(hot[r - r0]) << half : one);
-        }
-#pragma unroll
-        for (int r = r0; r < r0 + 8; ++r) {
-            const uint32_t mine = (rk[r] >> half) & 0xFFFFu;
-            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)lead[r - r0]);
-            rk[r] = ((hot[r - r0] >> lane) & 1ull) ? b0 + (uint32_t)__popcll(hot[r - r0] & lt) : mine;
-        }
+    for (int r = 0; r < IT; ++r) {
+        const bool valid = (w * IT + r) * WAVE + lane < st.cnt;
+        const uint32_t d = (kk[r] >> B2_LOW_BITS) & mask;
+        const unsigned long long hm = __ballot(valid && d == h);
+        const uint32_t cr = row_rank16<BALLOT, 9>(&s_cnt[w >> 1][d], half, d, valid && d != h);
+        rk[r] = d == h ? hrun + (uint32_t)__popcll(hm & lt) : cr;
+        hrun += (uint32_t)__popcll(hm);
     }
+    if (lane == 0 && hrun) atomicAdd(&s_cnt[w >> 1][h], hrun << half);
     __syncthreads();
     // per digit (one a thread): the waves' exclusive prefix into the halves, the tile-local digit start
     uint32_t run = 0;
@@ -439,6 +432,7 @@ __global__ void __launch_bounds__(CL_NT) k_l2_classify(const uint32_t* __restric
 // are loaded while this one is scanned and written, and the range after that one's list entry and
 // starts before then -- each range is three dependent HBM round trips (list, starts, records), which
 // left the thin ranges of BASELINE cfg 3 (~96K ranges of ~60 messages) latency-bound.
+template <bool BALLOT>
 __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16_t* __restrict__ keys16,
                                                                    const uint32_t* __restrict__ idx, L2Lists l,
                                                                    uint32_t n, uint32_t n_act,
@@ -518,8 +512,10 @@ __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16
         if (reg) {
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
-                if (ck[u] == NONE32) continue;
-                const uint32_t p = base + atomicAdd(&cnt[ck[u]], 1u);
+                const bool valid = ck[u] != NONE32;
+                const uint32_t kq = valid ? ck[u] : 0u;
+                const uint32_t p = base + row_rank32<BALLOT, 10>(&cnt[kq], kq, valid);
+                if (!valid) continue;
                 perm[p] = cv[u];
                 if (rank_out) rank_out[cv[u]] = p;
             }
@@ -534,8 +530,10 @@ __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16
             }
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
-                if (k[u] == NONE32) continue;
-                const uint32_t p = base + atomicAdd(&cnt[k[u]], 1u);
+                const bool valid = k[u] != NONE32;
+                const uint32_t kq = valid ? k[u] : 0u;
+                const uint32_t p = base + row_rank32<BALLOT, 10>(&cnt[kq], kq, valid);
+                if (!valid) continue;
                 perm[p] = v[u];
                 if (rank_out) rank_out[v[u]] = p;
             }
@@ -594,6 +592,9 @@ __global__ void __launch_bounds__(CH_NT) k_l2_chunk_hist(const uint16_t* __restr
         const uint32_t et = a0 + CH_CAP;
         v[CH_RW / 8] = tid == 0 && et < start + cs ? *reinterpret_cast<const uint4*>(keys16 + et) : make_uint4(0, 0, 0, 0);
         __syncthreads();
+        // the wave's hot activation (its first load's last key) in a register, every other key one LDS add
+        const uint32_t h = wave_hot_digit(v[0].w >> 16, a0 + 8 * tid + 7 >= start && a0 + 8 * tid + 7 < start + cs);
+        uint32_t hc = 0;
 #pragma unroll
         for (uint32_t q = 0; q <= CH_RW / 8; ++q) {
             const uint32_t e0 = q < CH_RW / 8 ? a0 + 8 * (q * CH_NT + tid) : et;
@@ -603,17 +604,14 @@ __global__ void __launch_bounds__(CH_NT) k_l2_chunk_hist(const uint16_t* __restr
                 const uint32_t e = e0 + x;
                 const bool valid = e >= start && e < start + cs && (q < CH_RW / 8 || tid == 0);
                 const uint32_t k = (w4[x / 2] >> (16 * (x & 1))) & 0xFFFFu;
-                const unsigned long long act = __ballot(valid);
-                if (act == 0) continue;
-                const uint32_t lead = (uint32_t)__ffsll((long long)act) - 1;
-                const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)k, (int)lead);
-                const unsigned long long hot = __ballot(valid && k == d0);
                 if (valid) {
-                    if (k != d0) atomicAdd(&s_cnt[k], 1u);
-                    else if (lane == lead) atomicAdd(&s_cnt[k], (uint32_t)__popcll(hot));
+                    if (k == h) ++hc;
+                    else atomicAdd(&s_cnt[k], 1u);
                 }
             }
         }
+        hc = wave_sum(hc);
+        if (lane == 0 && hc) atomicAdd(&s_cnt[h], hc);
         __syncthreads();
         for (uint32_t x = tid; x < MSD_L; x += CH_NT) hh[(size_t)j * MSD_L + x] = s_cnt[x];
         __syncthreads();
@@ -746,6 +744,7 @@ struct ChunkShared {
     uint32_t delta[MSD_L];
     uint32_t red[CH_NW];
 };
+template <bool BALLOT>
 __global__ void __launch_bounds__(CH_NT, 2) k_l2_chunk_scatter(const uint16_t* __restrict__ keys16,
                                                                const uint32_t* __restrict__ idx, L2Lists l,
                                                                const uint32_t* __restrict__ hh,
@@ -790,8 +789,19 @@ __global__ void __launch_bounds__(CH_NT, 2) k_l2_chunk_scatter(const uint16_t* _
             }
         }
         __syncthreads();
+        // the wave's hot activation (of its first row; Zipf-hot ranges) counted and ranked in registers
+        const uint32_t hk = wave_hot_digit(kp[0] & 0xFFFFu, (kp[0] & 0xFFFFu) != 0xFFFFu);
+        {
+            uint32_t hc = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < CH_RW; ++q) msd_fold_count(sh.wc[w], (kp[q / 2] >> (16 * (q & 1))) & 0xFFFFu);
+            for (uint32_t q = 0; q < CH_RW; ++q) {
+                const uint32_t k = (kp[q / 2] >> (16 * (q & 1))) & 0xFFFFu;
+                if (k == hk) ++hc;
+                else if (k != 0xFFFFu) atomicAdd(&sh.wc[w][k >> 1], 1u << (16 * (k & 1)));
+            }
+            hc = wave_sum(hc);
+            if (lane == 0 && hc) atomicAdd(&sh.wc[w][hk >> 1], hc << (16 * (hk & 1)));
+        }
 #pragma unroll
         for (uint32_t q = 0; q < CH_RW / 2; ++q) asm volatile("" : "+v"(kp[q]));
         __syncthreads();
@@ -810,6 +820,10 @@ __global__ void __launch_bounds__(CH_NT, 2) k_l2_chunk_scatter(const uint16_t* _
         sh.delta[2 * tid] = gb0 - ex;                    // chunk-local position -> global position
         sh.delta[2 * tid + 1] = gb1 - ex - tlo;
         __syncthreads();
+        // the hot activation's ranks: this wave's first position among its items, then ballots
+        const uint32_t hk_s = hk == NONE32 ? 0u : hk;
+        uint32_t hrun = hk == NONE32 ? 0u : sh.run[hk_s] + ((sh.wc[w][hk_s >> 1] >> (16 * (hk_s & 1))) & 0xFFFFu);
+        const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
         for (uint32_t g = 0; g < CH_RW; g += MSD_G) {
             uint32_t mm[MSD_G];
@@ -821,9 +835,12 @@ __global__ void __launch_bounds__(CH_NT, 2) k_l2_chunk_scatter(const uint16_t* _
 #pragma unroll
             for (uint32_t q = 0; q < (uint32_t)MSD_G; ++q) {
                 const uint32_t k = (kp[(g + q) / 2] >> (16 * ((g + q) & 1))) & 0xFFFFu;
-                const uint32_t rr = msd_fold_rank(sh.wc[w], k);    // Zipf-hot ranges: fold the hot key
+                const unsigned long long hm = __ballot(k == hk);
+                const bool cold = k != 0xFFFFu && k != hk;
+                const uint32_t rr = row_rank16<BALLOT, 10>(&sh.wc[w][k >> 1], 16 * (k & 1), k, cold);
+                const uint32_t at = k == hk ? hrun + (uint32_t)__popcll(hm & lt) : sh.run[k] + rr;
+                hrun += (uint32_t)__popcll(hm);
                 if (k == 0xFFFFu) continue;
-                const uint32_t at = sh.run[k] + rr;
                 sh.out[at] = mm[q];
                 sh.key[at] = (uint16_t)k;
             }

@@ -25,6 +25,7 @@ FRAME_HAS_TARGET, FRAME_COMPLETE, FRAME_FALLBACK, FRAME_MALFORMED, FRAME_TARGET_
 NO_ACTIVATION = 0xFFFFFFFF
 NO_SILO = 0xFFFFFFFF
 CFG_KERNEL_TIMING = 1
+CFG_NO_LANE_ORDER = 2
 
 RING_MODES = {"D": RING_DIRECTORY, "R": RING_CONSISTENT, "V": RING_VIRTUAL_BUCKETS}
 
@@ -409,6 +410,9 @@ TUNE_KINDS = {"probe_keys": 0, "probe_n1": 1, "probe_fanout": 2, "probe_nodes": 
 # Options applied to every handle this process creates, before its own `options=` (the test and tool
 # harness sets these; a C# host calls gd_option_set on its handle instead).
 DEFAULT_OPTIONS: dict = {}
+# Every handle created as if its device failed gd_create's lane-order check (GD_CFG_NO_LANE_ORDER): the
+# test suite's ballot-rank run (tests/conftest.py, GD_TEST_BALLOT_RANKS=1) sets it
+FORCE_NO_LANE_ORDER = False
 
 
 # ---- the handle --------------------------------------------------------------------
@@ -418,9 +422,13 @@ class GrainDispatch:
     GPU owns + scratch, on one HIP stream."""
 
     def __init__(self, device: int = 0, table_capacity: int = 1 << 20, my_silo: int = 0,
-                 seed_silo: int = NO_SILO, kernel_timing: bool = False, options: Optional[dict] = None):
+                 seed_silo: int = NO_SILO, kernel_timing: bool = False, options: Optional[dict] = None,
+                 no_lane_order: bool = False):
+        """no_lane_order (GD_CFG_NO_LANE_ORDER): the handle behaves as on a device that fails gd_create's
+        LDS lane-order check -- every stable rank by ballots."""
         cfg = gd_config(C.sizeof(gd_config), device, table_capacity, my_silo, seed_silo, 0,
-                        CFG_KERNEL_TIMING if kernel_timing else 0)
+                        (CFG_KERNEL_TIMING if kernel_timing else 0) |
+                        (CFG_NO_LANE_ORDER if no_lane_order or FORCE_NO_LANE_ORDER else 0))
         h = C.c_void_p()
         _check(None, lib.gd_create(C.byref(cfg), C.byref(h)))
         self.h = h

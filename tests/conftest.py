@@ -11,6 +11,11 @@ for p in (ROOT, os.path.join(ROOT, "oracle")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libgraindispatch on cuda:0)")
+    if os.environ.get("GD_TEST_BALLOT_RANKS") == "1":
+        # the whole suite with every stable rank by ballots (GD_CFG_NO_LANE_ORDER on every handle): the
+        # library's path on a device without the LDS lane order
+        from orleans_amd import graindispatch
+        graindispatch.FORCE_NO_LANE_ORDER = True
     config.addinivalue_line("markers", "slow: larger CPU cases")
 
 

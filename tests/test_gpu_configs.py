@@ -485,13 +485,25 @@ def test_tune_agree_rank_without_8b_index(gd):
         e.close()
 
 
+def test_stable_rank_fallback_without_lane_order(gd):
+    """A handle on a device without the LDS lane order (GD_CFG_NO_LANE_ORDER stands in for a failed
+    gd_create check) is created, ranks by ballots (GD_OPT_STABLE_RANK reads 0) and refuses 1."""
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 12, no_lane_order=True)
+    assert e.get_option("stable_rank") == 0
+    with pytest.raises(Exception):
+        e.set_option("stable_rank", 1)
+    assert e.get_option("stable_rank") == 0
+    e.close()
+
+
 def test_options_roundtrip_and_range(gd, monkeypatch):
     """gd_option_set / gd_option_get: every option reads back what was set, the defaults are the
     documented ones, values out of range and unknown options are refused with an error
     (the handle keeps its value)."""
     monkeypatch.setattr(gd, "DEFAULT_OPTIONS", {})           # the library's own defaults, not this module's
     e = gd.GrainDispatch(device=0, table_capacity=1 << 12)   # creation ran the lane-order self-check
-    defaults = {"probe": 1, "bucket": 1, "l2_small": 1024, "stable_rank": 1, "wire_headers": 2,
+    defaults = {"probe": 1, "bucket": 1, "l2_small": 1024, "stable_rank": 0 if gd.FORCE_NO_LANE_ORDER else 1,
+                "wire_headers": 2,
                 "region_probe": 0, "idx16": 1, "host_chunk": 2097152, "mb_zerocopy": 1, "mb_split": 8,
                 "mb_trace": 0, "l2_staged": 24576, "l2_mid": 8192}
     assert set(defaults) == set(gd.OPTIONS)

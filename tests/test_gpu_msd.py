@@ -111,6 +111,24 @@ def test_msd_three_pass_vs_oracle(gd, n, n_act, kind):
     e0.close()
 
 
+@pytest.mark.parametrize("n,n_act,kind", [ONE_PASS[0], ONE_PASS[4], ONE_PASS[8], THREE_PASS[1], THREE_PASS[2],
+                                           THREE_PASS[3], THREE_PASS[5], THREE_PASS[8]])
+def test_msd_ballot_ranks_vs_oracle(gd, n, n_act, kind):
+    """Every bucketing form with its ranks by ballots (GD_CFG_NO_LANE_ORDER: the library's path on a
+    device whose LDS atomics are not served in lane order) -- stable by construction -- equals the
+    oracle: the one-pass and three-pass forms (thin, mid, staged and chunked ranges, the hot-key
+    register path) and the LSD passes."""
+    acts = _acts(n, n_act, kind, n + n_act + 11)
+    wp, wo = o.bucket_stable(acts, n_act)
+    for bucket in (2, 0):
+        e = gd.GrainDispatch(device=0, table_capacity=1 << 12, options={"bucket": bucket}, no_lane_order=True)
+        assert e.get_option("stable_rank") == 0
+        p, off = e.bucket(acts, n_act)
+        np.testing.assert_array_equal(p, wp, err_msg=f"bucket {bucket}")
+        np.testing.assert_array_equal(off, wo, err_msg=f"bucket {bucket}")
+        e.close()
+
+
 @pytest.mark.parametrize("small", [0, 300, 24576])
 def test_msd_three_pass_class_threshold(gd, small):
     """The thin-range threshold moves ranges between the wave form and the workgroup form (0: every

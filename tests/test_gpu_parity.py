@@ -399,9 +399,12 @@ MB_VARIANTS = {  # GD_OPT_MB_* options, read at gd_microbatch_create
 
 
 @pytest.mark.parametrize("variant,mode", [("zero_copy", "D"), ("zero_copy", "R"), ("zero_copy", "V"),
-                                          ("zero_copy_one_sorter", "V"), ("staged_copies", "V")])
+                                          ("zero_copy_one_sorter", "V"), ("staged_copies", "V"),
+                                          ("ballot_ranks", "D")])
 def test_microbatch_graph_matches_eager_and_oracle(gd, monkeypatch, variant, mode):
-    for k, v in MB_VARIANTS[variant].items():
+    if variant == "ballot_ranks":                # every rank by ballots (GD_CFG_NO_LANE_ORDER)
+        monkeypatch.setattr(gd, "FORCE_NO_LANE_ORDER", True)
+    for k, v in MB_VARIANTS.get(variant, {}).items():
         monkeypatch.setitem(gd.DEFAULT_OPTIONS, k, v)
     silos = o.bench_silos(8)
     spec = o.ring_spec(silos, mode)
