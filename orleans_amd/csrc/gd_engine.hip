@@ -1043,7 +1043,7 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
     if (pk) GD_TRY((msd_pass<SEG_RMAX, B2_PACK, BALLOT>(h, acts, n, n_act, RA, MSD_SHIFT + a, kA, vA, bp)));
     else GD_TRY((msd_pass<SEG_RMAX, B2_KEY32, BALLOT>(h, acts, n, n_act, RA, MSD_SHIFT + a, kA, vA)));
     const SegIn in{(const uint16_t*)kA, (const uint32_t*)kA, (const uint32_t*)vA, hb, bp.ib};
-    GD_TRY(launch(h, "k_seg_table", dim3(1), dim3(1024), 0, k_seg_table, h->last_totals, RA, tbound, seg_start, seg_tb,
+    GD_TRY(launch(h, "k_seg_table", dim3(blocks_for(tbound, 1024)), dim3(1024), 0, k_seg_table, h->last_totals, RA, tbound, seg_start, seg_tb,
                   tile_seg, (uint32_t*)m[5].p));
     // pass B: d1 inside each d2 segment; one flat scan gives every (segment, digit, tile) its position
     if (pk)

@@ -62,7 +62,7 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// One workgroup: the d2 segments' starts (exclusive prefix of pass A's digit totals) and tile bases
+// The d2 segments' starts (exclusive prefix of pass A's digit totals) and tile bases
 // (exclusive prefix of ceil(size / SEG_TILE)), every pass-B tile's segment (NONE32 past the last), and
 // the level-2 counters zeroed.  ra <= SEG_RMAX.
 __global__ void __launch_bounds__(1024) k_seg_table(const uint32_t* __restrict__ totals, uint32_t ra,
@@ -71,25 +71,32 @@ __global__ void __launch_bounds__(1024) k_seg_table(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ ctr) {
     __shared__ uint32_t s_wsum[2 * 1024 / WAVE];
     __shared__ uint32_t s_tb[SEG_RMAX + 1];
+    // every workgroup scans the <= 512 totals itself and fills its 1,024 tiles; workgroup 0 writes the
+    // segment tables and zeroes the counters
     const uint32_t t = threadIdx.x;
     const uint32_t v = t < ra ? totals[t] : 0u;
     const uint32_t nt = (v + SEG_TILE - 1) / SEG_TILE;
     uint32_t es, et;
     block_excl_scan_add2<1024>(v, nt, s_wsum, es, et);
+    const bool w0 = blockIdx.x == 0;
     if (t < ra) {
-        seg_start[t] = es;
-        seg_tb[t] = et;
+        if (w0) {
+            seg_start[t] = es;
+            seg_tb[t] = et;
+        }
         s_tb[t] = et;
     }
     if (t == ra - 1) {
-        seg_start[ra] = es + v;
-        seg_tb[ra] = et + nt;
+        if (w0) {
+            seg_start[ra] = es + v;
+            seg_tb[ra] = et + nt;
+        }
         s_tb[ra] = et + nt;
     }
-    if (t < L2_CTR_WORDS) ctr[t] = 0;
+    if (w0 && t < L2_CTR_WORDS) ctr[t] = 0;
     __syncthreads();
     const uint32_t total = s_tb[ra];
-    for (uint32_t j = t; j < tbound; j += 1024) {
+    for (uint32_t j = blockIdx.x * 1024 + t; j < tbound; j += gridDim.x * 1024) {
         uint32_t s = NONE32;
         if (j < total) {
             uint32_t lo = 0, hi = ra;                // largest s < ra with s_tb[s] <= j
@@ -172,22 +179,22 @@ __global__ void __launch_bounds__(SEG_NT) k_seg_hist(SegIn in, const uint32_t* _
         const uint32_t k = PK ? v[0].w >> 16 : v[0].w;
         h = wave_hot_digit((k >> dsh) & (rb - 1), e >= st.base && e < st.base + st.cnt);
     }
-#pragma unroll
-    for (uint32_t j = 0; j <= NL; ++j) {
-        const uint32_t e0 = j < NL ? a0 + PER * (j * SEG_NT + threadIdx.x) : et;
-        const uint32_t w4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+    auto count = [&](const uint4& vj, uint32_t e0) {
+        const uint32_t w4[4] = {vj.x, vj.y, vj.z, vj.w};
 #pragma unroll
         for (uint32_t q = 0; q < PER; ++q) {
             const uint32_t e = e0 + q;
-            const bool valid = e >= st.base && e < st.base + st.cnt && (j < NL || threadIdx.x == 0);
             const uint32_t k = PK ? (w4[q / 2] >> (16 * (q & 1))) & 0xFFFFu : w4[q];
             const uint32_t d = (k >> dsh) & (rb - 1);
-            if (valid) {
+            if (e >= st.base && e < st.base + st.cnt) {
                 if (d == h) ++hc;
                 else atomicAdd(&s_cnt[d], 1u);
             }
         }
-    }
+    };
+#pragma unroll
+    for (uint32_t j = 0; j < NL; ++j) count(v[j], a0 + PER * (j * SEG_NT + threadIdx.x));
+    if (threadIdx.x == 0) count(v[NL], et);              // the tail past the aligned tile: one thread
     hc = wave_sum(hc);
     if (lane == 0 && hc) atomicAdd(&s_cnt[h], hc);
     __syncthreads();
@@ -331,7 +338,7 @@ __host__ __device__ __forceinline__ uint32_t cs_items(uint32_t C) {
 // ~7,000 same-address device atomics); range b + 1's start comes from the next lane.  A chunked range
 // reserves its chunks and its entry with one 64-bit atomic (chunks in the low word, ranges in the high
 // word), so the chunked ranges' first chunks increase with their entries.
-constexpr int CL_NT = 1024;
+constexpr int CL_NT = 1024;                    // (256: 0.025 -> 0.031 ms at cfg 3, the list order less sequential)
 constexpr int CL_NW = CL_NT / WAVE;
 __global__ void __launch_bounds__(CL_NT) k_l2_classify(const uint32_t* __restrict__ hseg,
                                                        const uint32_t* __restrict__ seg_start,
@@ -595,21 +602,21 @@ __global__ void __launch_bounds__(CH_NT) k_l2_chunk_hist(const uint16_t* __restr
         // the wave's hot activation (its first load's last key) in a register, every other key one LDS add
         const uint32_t h = wave_hot_digit(v[0].w >> 16, a0 + 8 * tid + 7 >= start && a0 + 8 * tid + 7 < start + cs);
         uint32_t hc = 0;
-#pragma unroll
-        for (uint32_t q = 0; q <= CH_RW / 8; ++q) {
-            const uint32_t e0 = q < CH_RW / 8 ? a0 + 8 * (q * CH_NT + tid) : et;
-            const uint32_t w4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+        auto count = [&](const uint4& vq, uint32_t e0) {
+            const uint32_t w4[4] = {vq.x, vq.y, vq.z, vq.w};
 #pragma unroll
             for (uint32_t x = 0; x < 8; ++x) {
                 const uint32_t e = e0 + x;
-                const bool valid = e >= start && e < start + cs && (q < CH_RW / 8 || tid == 0);
                 const uint32_t k = (w4[x / 2] >> (16 * (x & 1))) & 0xFFFFu;
-                if (valid) {
+                if (e >= start && e < start + cs) {
                     if (k == h) ++hc;
                     else atomicAdd(&s_cnt[k], 1u);
                 }
             }
-        }
+        };
+#pragma unroll
+        for (uint32_t q = 0; q < CH_RW / 8; ++q) count(v[q], a0 + 8 * (q * CH_NT + tid));
+        if (tid == 0) count(v[CH_RW / 8], et);           // the tail past the aligned chunk: one thread
         hc = wave_sum(hc);
         if (lane == 0 && hc) atomicAdd(&s_cnt[h], hc);
         __syncthreads();
@@ -740,7 +747,6 @@ struct ChunkShared {
     uint32_t out[CH_CAP];
     uint16_t key[CH_CAP];
     uint32_t wc[CH_NW][MSD_LW];
-    uint32_t run[MSD_L];
     uint32_t delta[MSD_L];
     uint32_t red[CH_NW];
 };
@@ -805,24 +811,31 @@ __global__ void __launch_bounds__(CH_NT, 2) k_l2_chunk_scatter(const uint16_t* _
 #pragma unroll
         for (uint32_t q = 0; q < CH_RW / 2; ++q) asm volatile("" : "+v"(kp[q]));
         __syncthreads();
-        // each wave's first position per activation (exclusive prefix over the waves), the totals
-        uint32_t tlo = 0, thi = 0;
+        // each wave's first chunk position per activation (the activation's chunk start + the exclusive
+        // prefix over the waves), so a rank is a chunk position; the totals
+        uint32_t wv[CH_NW], tlo = 0, thi = 0;
 #pragma unroll
         for (int ww = 0; ww < CH_NW; ++ww) {
-            const uint32_t v = sh.wc[ww][tid];
-            sh.wc[ww][tid] = tlo | (thi << 16);
-            tlo += v & 0xFFFFu;
-            thi += v >> 16;
+            wv[ww] = sh.wc[ww][tid];
+            tlo += wv[ww] & 0xFFFFu;
+            thi += wv[ww] >> 16;
         }
         const uint32_t ex = block_excl_scan_add_n<CH_NT>(tlo + thi, sh.red);
-        sh.run[2 * tid] = ex;
-        sh.run[2 * tid + 1] = ex + tlo;
-        sh.delta[2 * tid] = gb0 - ex;                    // chunk-local position -> global position
+        {
+            uint32_t plo = ex, phi = ex + tlo;
+#pragma unroll
+            for (int ww = 0; ww < CH_NW; ++ww) {
+                sh.wc[ww][tid] = plo | (phi << 16);
+                plo += wv[ww] & 0xFFFFu;
+                phi += wv[ww] >> 16;
+            }
+        }
+        sh.delta[2 * tid] = gb0 - ex;                    // chunk position -> global position
         sh.delta[2 * tid + 1] = gb1 - ex - tlo;
         __syncthreads();
-        // the hot activation's ranks: this wave's first position among its items, then ballots
+        // the hot activation's ranks: this wave's first chunk position among its items, then ballots
         const uint32_t hk_s = hk == NONE32 ? 0u : hk;
-        uint32_t hrun = hk == NONE32 ? 0u : sh.run[hk_s] + ((sh.wc[w][hk_s >> 1] >> (16 * (hk_s & 1))) & 0xFFFFu);
+        uint32_t hrun = (sh.wc[w][hk_s >> 1] >> (16 * (hk_s & 1))) & 0xFFFFu;
         const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
         for (uint32_t g = 0; g < CH_RW; g += MSD_G) {
@@ -838,7 +851,7 @@ __global__ void __launch_bounds__(CH_NT, 2) k_l2_chunk_scatter(const uint16_t* _
                 const unsigned long long hm = __ballot(k == hk);
                 const bool cold = k != 0xFFFFu && k != hk;
                 const uint32_t rr = row_rank16<BALLOT, 10>(&sh.wc[w][k >> 1], 16 * (k & 1), k, cold);
-                const uint32_t at = k == hk ? hrun + (uint32_t)__popcll(hm & lt) : sh.run[k] + rr;
+                const uint32_t at = k == hk ? hrun + (uint32_t)__popcll(hm & lt) : rr;
                 hrun += (uint32_t)__popcll(hm);
                 if (k == 0xFFFFu) continue;
                 sh.out[at] = mm[q];
