@@ -471,6 +471,8 @@ def compact_roofline(rf, kernels, with_table=True):
     for k in ("probe_variant", "probe_index_frac_impl"):
         if rf.get(k) is not None:
             out[k] = rf[k]
+    if rf.get("random_probe_ceiling"):
+        out["random_probe_ceiling_frac"] = rf["random_probe_ceiling"].get("frac_of_ceiling")
     if rf.get("probe_index"):
         out["probe_index_frac_impl"] = rf["probe_index"].get("frac_impl")
     st = rf.get("bucketing_stage")
@@ -802,11 +804,32 @@ def route_extras(roofline: dict, e, m_recv: int, tag: str, world: int):
     roofline["probe_variant"] = PROBE_VARIANTS.get(v, str(v))
     t_l = roofline["avg_launch_ms"] * 1e-3
     slot = {0: 16, 2: 16, 3: 8}.get(v)
+    if v == 3 and world == 1:
+        pc = probe_ceiling(tag, m_recv, roofline["avg_launch_ms"])
+        if pc:
+            roofline["random_probe_ceiling"] = pc
     if slot:
         # per message: key 24 + one index slot + silo/act/status 9
         impl = m_recv * (24 + slot + 9)
         roofline["probe_index"] = {"slot_bytes": slot, "impl_bytes_per_launch": impl,
                                    "frac_impl": round(impl / t_l / 1e9 / PEAK_HBM_GBS, 4) if t_l > 0 else None}
+
+
+# The random-probe ceiling of the 8-B index (tools/ubench_fanprobe.hip, profiles/r05_ubench_fanprobe.txt):
+# probes a ms of one 64-B group (4 x 16-B loads) at random into an index of the workload's size, with a
+# 4-B key stream in and 8 B out -- no hash, ring or compare work.  cfg 2: 2^21 slots (16 MB) at load 0.5,
+# 16M probes, 0.2567 ms; cfg 4: 2^25 slots (268 MB) at load 0.3, 43M probes, 0.8226 ms.  EA requests:
+# 1.0 64-B request a probe (TCC_EA0_RDREQ_32B_sum = 0: a 32-B read still moves 64 B).
+PROBE_CEILING_PER_MS = {"cfg2": 16777216 / 0.2567, "cfg4": 43000000 / 0.8226}
+
+
+def probe_ceiling(tag: str, probes: float, launch_ms: float):
+    rate = PROBE_CEILING_PER_MS.get(tag)
+    if not rate or launch_ms <= 0:
+        return None
+    ms = probes / rate
+    return {"ms_per_launch": round(ms, 4), "frac_of_ceiling": round(ms / launch_ms, 3),
+            "source": "profiles/r05_ubench_fanprobe.txt (8-B index, random 64-B group reads)"}
 
 
 # gd_tune_get variants of the 24-B-key / N1 probes (gd_engine.hip cx_choose)
@@ -1188,6 +1211,10 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
                                         bytes_fn=cfg4_bytes)
         if roofline:
             roofline["hop_bucket_forms"] = [hop_form(e, m, n_act) for m in hop_msgs]
+            if roofline.get("kernel") == "k_fan_route" and world == 1:
+                pc = probe_ceiling("cfg4", msgs_step / roofline["launches_per_step"], roofline["avg_launch_ms"])
+                if pc:
+                    roofline["random_probe_ceiling"] = pc
 
     cpu = None
     if rank == 0 and world == 1 and with_cpu and isinstance(runner, LibraryCascade):
