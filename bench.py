@@ -55,7 +55,7 @@ def grain_keys(type_code_data: int, ks: np.ndarray) -> np.ndarray:
 
 def radix_layout(n: int, n_act: int):
     """(passes, digit bits, packed) of libgraindispatch's LSD bucketing for n messages over n_act
-    activations (gd_engine.hip bucket_lsd): <= 8-bit digits; records packed to 6 B between the passes
+    activations (eng_core.hip bucket_lsd): <= 8-bit digits; records packed to 6 B between the passes
     when the key bits above the first digit fit a u16 and the message index fits a u32 beside the
     first digit."""
     key_bits = max(1, int(n_act).bit_length())
@@ -367,7 +367,7 @@ def setup_workload(args, workload, world, rank, local, dev, tcd, msgs, grains):
 
 # Untimed steps before the W warmup steps: libgraindispatch times its probe variants (compact index in
 # group reads, directory, index in slot reads) on the first 2 x 3 eligible launches of each launch kind
-# and size, then keeps the fastest (gd_engine.hip cx_choose).  These steps let that
+# and size, then keeps the fastest (eng_core.hip cx_choose).  These steps let that
 # measurement finish before the timed region with any --warmup (the driver uses 5): every timed step
 # then runs the variant the library keeps.
 SETTLE_STEPS = 8
@@ -832,7 +832,7 @@ def probe_ceiling(tag: str, probes: float, launch_ms: float):
             "source": "profiles/r05_ubench_fanprobe.txt (8-B index, random 64-B group reads)"}
 
 
-# gd_tune_get variants of the 24-B-key / N1 probes (gd_engine.hip cx_choose)
+# gd_tune_get variants of the 24-B-key / N1 probes (eng_core.hip cx_choose)
 PROBE_VARIANTS = {0: "16-B index, 64-B group reads", 1: "directory table, 32-B slots",
                   2: "16-B index, 16-B slot reads", 3: "8-B index, 64-B group reads", -1: "still measuring"}
 

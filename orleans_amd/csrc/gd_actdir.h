@@ -46,7 +46,7 @@ __device__ __forceinline__ bool ad_find(const AdArgs& t, uint64_t n0, uint64_t n
 }
 
 // Slot of each key (TryRemove / state updates): NONE32 if absent.
-__global__ void __launch_bounds__(BLOCK) k_ad_find(const gd_key* __restrict__ keys, uint32_t n, AdArgs t,
+static __global__ void __launch_bounds__(BLOCK) k_ad_find(const gd_key* __restrict__ keys, uint32_t n, AdArgs t,
                                                    uint32_t* __restrict__ slot_of) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
@@ -66,7 +66,7 @@ __global__ void __launch_bounds__(BLOCK) k_ad_find(const gd_key* __restrict__ ke
     slot_of[i] = res;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_ad_lookup(const gd_key* __restrict__ keys, uint32_t n, AdArgs t,
+static __global__ void __launch_bounds__(BLOCK) k_ad_lookup(const gd_key* __restrict__ keys, uint32_t n, AdArgs t,
                                                      uint32_t* __restrict__ out_ctx, uint8_t* __restrict__ out_flags,
                                                      uint8_t* __restrict__ out_found) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(BLOCK) k_ad_lookup(const gd_key* __restrict__ 
 }
 
 // Flag updates, batch order: the last item of a slot wins (`last` = 1 + its index, k_up_last).
-__global__ void __launch_bounds__(BLOCK) k_ad_setflags(const uint32_t* __restrict__ slot_of,
+static __global__ void __launch_bounds__(BLOCK) k_ad_setflags(const uint32_t* __restrict__ slot_of,
                                                        const uint8_t* __restrict__ flags, uint32_t n,
                                                        const uint32_t* __restrict__ last, Slot* slots,
                                                        uint8_t* __restrict__ out_found) {
@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(BLOCK) k_ad_setflags(const uint32_t* __restric
 // caller error: ERR_CTX_RANGE in *err (the call fails with GD_EINVAL) and the message is left
 // un-enqueued (ctx NONE32, RECV_UNDECODED), so no later pass indexes past the n_ctx arrays.
 template <bool MARK_STATELESS>
-__global__ void __launch_bounds__(BLOCK) k_receive(const gd_key* __restrict__ target_grain,
+static __global__ void __launch_bounds__(BLOCK) k_receive(const gd_key* __restrict__ target_grain,
                                                    const gd_key* __restrict__ target_activation,
                                                    const uint8_t* __restrict__ direction,
                                                    const uint32_t* __restrict__ frame_flags, uint32_t n, uint32_t n_ctx,
@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(BLOCK) k_receive(const gd_key* __restrict__ ta
 // j >= limit + 1 - request_count[c] (every earlier message was enqueued and counted by
 // IncrementEnqueuedOnDispatcherCount until the first rejection; after it the count stays over the
 // limit).  Rejected messages get ctx NONE32; the caller rebuckets.
-__global__ void __launch_bounds__(BLOCK) k_overload(const uint32_t* __restrict__ rank,
+static __global__ void __launch_bounds__(BLOCK) k_overload(const uint32_t* __restrict__ rank,
                                                     const uint32_t* __restrict__ offsets, uint32_t n,
                                                     const uint8_t* __restrict__ direction,
                                                     const uint32_t* __restrict__ request_count, int32_t hard_limit,
@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(BLOCK) k_overload(const uint32_t* __restrict__
 // gd_route_frames with an ActivationDirectory: a frame whose address is already complete
 // (GD_ROUTE_ADDRESSED, Dispatcher.cs:718) gets the context of its TargetActivation when
 // FindTarget finds a Valid activation, so the bucketing puts it in that activation's FIFO.
-__global__ void __launch_bounds__(BLOCK) k_frame_addressed_act(const uint8_t* __restrict__ status,
+static __global__ void __launch_bounds__(BLOCK) k_frame_addressed_act(const uint8_t* __restrict__ status,
                                                                const gd_key* __restrict__ target_grain,
                                                                const gd_key* __restrict__ target_activation, uint32_t n,
                                                                AdArgs t, uint32_t* __restrict__ act) {

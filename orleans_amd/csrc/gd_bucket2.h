@@ -37,7 +37,7 @@ constexpr uint32_t B2_TILE = B2_NT * B2_IT;
 // Histogram of TPB consecutive tiles per workgroup, digit-major counts hist[d * tiles + t] for d < R:
 // the digit of min(key, clamp) >> shift.
 template <int NT, int IT, int TPB, int RMAX>
-__global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t clamp,
+static __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t clamp,
                                                 uint32_t R, uint32_t tiles, uint32_t* __restrict__ hist,
                                                 uint32_t shift, uint32_t xcd_rev) {
     constexpr uint32_t TILE = NT * IT;
@@ -103,7 +103,7 @@ struct B2Pack {
 // key (B2Out form) in digit order of min(key, clamp) >> shift.  gscan: the row-scanned counts
 // (k_radix_rowscan), totals: the digit totals.
 template <int NT, int IT, int RMAX, int KOUT, bool BALLOT = false>
-__global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ keys_in, uint32_t n, uint32_t clamp,
+static __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ keys_in, uint32_t n, uint32_t clamp,
                                                    uint32_t R, uint32_t tiles, const uint32_t* __restrict__ gscan,
                                                    const uint32_t* __restrict__ totals,
                                                    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,

@@ -155,7 +155,7 @@ __device__ __forceinline__ bool silo_flag(const uint8_t* m, uint32_t n, uint32_t
 // LocalLookup over a batch: the owner's partition when this handle holds it, the cache
 // otherwise.  hit[i] = 1 for a cache hit (generation update follows), cslot[i] its slot.
 template <int MODE>
-__global__ void __launch_bounds__(BLOCK) k_route_cached(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+static __global__ void __launch_bounds__(BLOCK) k_route_cached(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                         TableArgs tab, CacheArgs cache,
                                                         uint32_t* __restrict__ out_silo,
                                                         uint32_t* __restrict__ out_act,
@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_cached(const gd_key* __restrict
 // Writes the hit flags / slots the batch's generation scan reads, so plain and KeyExt hits take
 // their generations in one batch order.
 template <int MODE>
-__global__ void __launch_bounds__(BLOCK) k_route_cached_keyext(const gd_key* __restrict__ keys, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_route_cached_keyext(const gd_key* __restrict__ keys, uint32_t n,
                                                                ExtArgs ext, RingArgs ring, KxArgs kx, CacheArgs cache,
                                                                uint32_t* __restrict__ out_silo,
                                                                uint32_t* __restrict__ out_act,
@@ -307,7 +307,7 @@ __device__ __forceinline__ bool cache_find_msg(const CacheArgs& c, const gd_key*
 }
 
 // AdaptiveGrainDirectoryCache.LookUp over a batch (explicit form, no routing).
-__global__ void __launch_bounds__(BLOCK) k_cache_lookup(const gd_key* __restrict__ keys, uint32_t n, ExtArgs ext,
+static __global__ void __launch_bounds__(BLOCK) k_cache_lookup(const gd_key* __restrict__ keys, uint32_t n, ExtArgs ext,
                                                         CacheArgs cache, gd_val* __restrict__ out_vals,
                                                         int32_t* __restrict__ out_ver, uint32_t* __restrict__ hit,
                                                         uint32_t* __restrict__ cslot) {
@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(BLOCK) k_cache_lookup(const gd_key* __restrict
 
 // pos = inclusive scan of the hit flags: hit k of the batch gets generation next_gen + k
 // (TryGetValue's Interlocked.Increment in batch order); the last hit of a key wins.
-__global__ void __launch_bounds__(BLOCK) k_cache_touch(const uint32_t* __restrict__ cslot,
+static __global__ void __launch_bounds__(BLOCK) k_cache_touch(const uint32_t* __restrict__ cslot,
                                                        const uint32_t* __restrict__ pos, uint32_t n, CacheSlot* slots,
                                                        const CacheCounters* ctr) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -331,19 +331,19 @@ __global__ void __launch_bounds__(BLOCK) k_cache_touch(const uint32_t* __restric
     atomicMax(&slots[cslot[i]].gen, ctr->next_gen + pos[i]);
 }
 
-__global__ void k_cache_advance(const uint32_t* __restrict__ pos, uint32_t n, CacheCounters* ctr) {
+static __global__ void k_cache_advance(const uint32_t* __restrict__ pos, uint32_t n, CacheCounters* ctr) {
     if (threadIdx.x == 0 && blockIdx.x == 0 && n) {
         ctr->next_gen += pos[n - 1];
         ctr->hits += pos[n - 1];
     }
 }
 
-__global__ void k_cache_count_access(uint32_t n, CacheCounters* ctr) {
+static __global__ void k_cache_count_access(uint32_t n, CacheCounters* ctr) {
     if (threadIdx.x == 0 && blockIdx.x == 0) ctr->accesses += n;
 }
 
 // Slot and generation of each key (NONE32 / 0 when absent).
-__global__ void __launch_bounds__(BLOCK) k_cache_find(const gd_key* __restrict__ keys, uint32_t n, ExtArgs ext,
+static __global__ void __launch_bounds__(BLOCK) k_cache_find(const gd_key* __restrict__ keys, uint32_t n, ExtArgs ext,
                                                       CacheArgs cache, uint32_t* __restrict__ slot_of,
                                                       unsigned long long* __restrict__ gen_of) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -355,7 +355,7 @@ __global__ void __launch_bounds__(BLOCK) k_cache_find(const gd_key* __restrict__
 }
 
 // Live entries with generation <= t: count, then collect (gen, slot) in any order.
-__global__ void __launch_bounds__(BLOCK) k_cache_count_le(const CacheSlot* __restrict__ slots,
+static __global__ void __launch_bounds__(BLOCK) k_cache_count_le(const CacheSlot* __restrict__ slots,
                                                           unsigned long long cap, unsigned long long t,
                                                           unsigned long long* __restrict__ out) {
     __shared__ uint32_t s_c;
@@ -371,7 +371,7 @@ __global__ void __launch_bounds__(BLOCK) k_cache_count_le(const CacheSlot* __res
     if (threadIdx.x == 0 && s_c) atomicAdd(out, (unsigned long long)s_c);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_cache_collect_le(const CacheSlot* __restrict__ slots,
+static __global__ void __launch_bounds__(BLOCK) k_cache_collect_le(const CacheSlot* __restrict__ slots,
                                                             unsigned long long cap, unsigned long long t,
                                                             uint32_t* __restrict__ cursor,
                                                             unsigned long long* __restrict__ out_gen,
@@ -397,7 +397,7 @@ struct CacheOp {
     uint32_t pad;
 };
 
-__global__ void __launch_bounds__(BLOCK) k_cache_apply(const CacheOp* __restrict__ ops, uint32_t n, CacheSlot* slots,
+static __global__ void __launch_bounds__(BLOCK) k_cache_apply(const CacheOp* __restrict__ ops, uint32_t n, CacheSlot* slots,
                                                        CacheCounters* ctr) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
@@ -417,7 +417,7 @@ __global__ void __launch_bounds__(BLOCK) k_cache_apply(const CacheOp* __restrict
 
 // New entries (distinct keys, known absent): claim the first empty or tombstoned slot.  xm (may be
 // NULL): per entry {KeyExt uniform hash, KeyExt length + 1 (0: three-word key), heap offset}.
-__global__ void __launch_bounds__(BLOCK) k_cache_insert(const gd_key* __restrict__ keys,
+static __global__ void __launch_bounds__(BLOCK) k_cache_insert(const gd_key* __restrict__ keys,
                                                         const CacheOp* __restrict__ vals,
                                                         const uint32_t* __restrict__ xm, uint32_t n, CacheSlot* slots,
                                                         unsigned long long mask, CacheCounters* ctr) {
@@ -457,7 +457,7 @@ __global__ void __launch_bounds__(BLOCK) k_cache_insert(const gd_key* __restrict
 }
 
 // Live entries into a fresh table (tombstone compaction / growth).
-__global__ void __launch_bounds__(BLOCK) k_cache_rehash(const CacheSlot* __restrict__ old_slots,
+static __global__ void __launch_bounds__(BLOCK) k_cache_rehash(const CacheSlot* __restrict__ old_slots,
                                                         unsigned long long old_cap, CacheSlot* slots,
                                                         unsigned long long mask, CacheCounters* ctr) {
     const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
@@ -484,13 +484,13 @@ __global__ void __launch_bounds__(BLOCK) k_cache_rehash(const CacheSlot* __restr
 }
 
 // Live-slot flags for the KeyValues dump (slot order).
-__global__ void __launch_bounds__(BLOCK) k_cache_live_flag(const CacheSlot* __restrict__ slots, uint32_t cap,
+static __global__ void __launch_bounds__(BLOCK) k_cache_live_flag(const CacheSlot* __restrict__ slots, uint32_t cap,
                                                            uint32_t* __restrict__ flag) {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j < cap) flag[j] = slot_state(slots[j].meta) == SLOT_LIVE ? 1u : 0u;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_cache_dump(const CacheSlot* __restrict__ slots, uint32_t cap,
+static __global__ void __launch_bounds__(BLOCK) k_cache_dump(const CacheSlot* __restrict__ slots, uint32_t cap,
                                                       const uint32_t* __restrict__ flag,
                                                       const uint32_t* __restrict__ pos, gd_key* __restrict__ keys,
                                                       gd_val* __restrict__ vals, int32_t* __restrict__ vers,
@@ -512,7 +512,7 @@ __global__ void __launch_bounds__(BLOCK) k_cache_dump(const CacheSlot* __restric
 
 // Heap compaction: each live KeyExt entry's string size rounded to 16 B, then (after an
 // inclusive scan of the sizes) its string moved to the new heap and its offset rewritten.
-__global__ void __launch_bounds__(BLOCK) k_cx_sizes(const CacheSlot* __restrict__ slots, uint32_t cap,
+static __global__ void __launch_bounds__(BLOCK) k_cx_sizes(const CacheSlot* __restrict__ slots, uint32_t cap,
                                                     uint32_t* __restrict__ size) {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= cap) return;
@@ -520,7 +520,7 @@ __global__ void __launch_bounds__(BLOCK) k_cx_sizes(const CacheSlot* __restrict_
     size[j] = (slot_state(s.meta) == SLOT_LIVE && s.xlen1 > 1) ? ((s.xlen1 - 1u + 15u) & ~15u) : 0u;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_cx_move(CacheSlot* slots, uint32_t cap, const uint32_t* __restrict__ size,
+static __global__ void __launch_bounds__(BLOCK) k_cx_move(CacheSlot* slots, uint32_t cap, const uint32_t* __restrict__ size,
                                                    const uint32_t* __restrict__ pos, const uint8_t* __restrict__ old_heap,
                                                    uint8_t* __restrict__ new_heap) {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;

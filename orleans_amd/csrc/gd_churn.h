@@ -36,7 +36,7 @@ __device__ __forceinline__ uint32_t key_owner(uint64_t n0, uint64_t n1, uint64_t
 // flag[s] = 1 for a live slot whose owner is known and not kept here (keep[owner] == 0 or owner
 // outside keep[]).
 template <int MODE>
-__global__ void __launch_bounds__(BLOCK) k_split_mark(const Slot* __restrict__ slots, unsigned long long cap,
+static __global__ void __launch_bounds__(BLOCK) k_split_mark(const Slot* __restrict__ slots, unsigned long long cap,
                                                       RingArgs ring, const uint8_t* __restrict__ keep,
                                                       uint32_t n_keep, uint32_t* __restrict__ flag) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(BLOCK) k_split_mark(const Slot* __restrict__ s
 
 // Emit flagged slots at their scanned positions; with `move`, tombstone them (the reference's
 // RemoveGrain after RegisterMany, GrainDirectoryHandoffManager.cs:228-232).
-__global__ void __launch_bounds__(BLOCK) k_split_emit(Slot* __restrict__ slots, unsigned long long cap,
+static __global__ void __launch_bounds__(BLOCK) k_split_emit(Slot* __restrict__ slots, unsigned long long cap,
                                                       const uint32_t* __restrict__ flag,
                                                       const uint32_t* __restrict__ pos, int move,
                                                       gd_key* __restrict__ out_keys, gd_val* __restrict__ out_vals,

@@ -30,7 +30,7 @@ struct CxCounters {
     uint32_t silo_max;
 };
 
-__global__ void __launch_bounds__(BLOCK) k_cx_types(const Slot* __restrict__ slots, unsigned long long cap,
+static __global__ void __launch_bounds__(BLOCK) k_cx_types(const Slot* __restrict__ slots, unsigned long long cap,
                                                     unsigned long long* types, CxCounters* ctr) {
     const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
     if (j >= cap) return;
@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(BLOCK) k_cx_types(const Slot* __restrict__ slo
     atomicOr(&ctr->flag, 2u);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_cx_build(const Slot* __restrict__ slots, unsigned long long cap,
+static __global__ void __launch_bounds__(BLOCK) k_cx_build(const Slot* __restrict__ slots, unsigned long long cap,
                                                     const unsigned long long* __restrict__ types, uint4* cx,
                                                     unsigned long long cx_cap, CxCounters* ctr) {
     if (ctr->flag) return;                             // not eligible (uniform): nothing to build
@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(BLOCK) k_cx_build(const Slot* __restrict__ slo
 // type, activations and silos fitting a u32 together): slot = (silo + 1) << ab | act (all ab bits set
 // for a multi-activation grain) above the N1 low word, placed by a 64-bit CAS in probe order from
 // cx8_home.
-__global__ void __launch_bounds__(BLOCK) k_cx8_build(const Slot* __restrict__ slots, unsigned long long cap,
+static __global__ void __launch_bounds__(BLOCK) k_cx8_build(const Slot* __restrict__ slots, unsigned long long cap,
                                                      unsigned long long* cx8, unsigned long long cx8_cap,
                                                      uint32_t ab, CxCounters* ctr) {
     const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;

@@ -25,7 +25,7 @@ namespace gd {
 // found: 0 = no entry (AddressesAndTag default: no list, VersionTag 0), 1 = entry with a valid
 // address, 2 = entry whose activation's silo is not valid (the filtered list is empty, the tag
 // is still returned: GrainDirectoryPartition.cs:401,425-431).
-__global__ void __launch_bounds__(BLOCK) k_dir_lookup_tagged(const gd_key* __restrict__ keys, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_dir_lookup_tagged(const gd_key* __restrict__ keys, uint32_t n,
                                                              TableArgs tab, const uint32_t* __restrict__ vtag,
                                                              gd_val* __restrict__ out_vals,
                                                              int32_t* __restrict__ out_tags,
@@ -68,7 +68,7 @@ __device__ __forceinline__ bool in_set(const uint32_t* set, uint32_t silo) {
 // AdjustLocalDirectory: RemoveActivation(grain, act, Force) for every instance on a removed
 // silo; a single-activation grain loses its only instance and so the grain.  Multi-activation
 // entries (GD_ACT_MULTI) keep no per-instance silos here: they are counted, left to the host.
-__global__ void __launch_bounds__(BLOCK) k_dir_remove_silos(Slot* slots, unsigned long long cap,
+static __global__ void __launch_bounds__(BLOCK) k_dir_remove_silos(Slot* slots, unsigned long long cap,
                                                             const uint32_t* __restrict__ set, DevCounters* ctr,
                                                             unsigned long long* __restrict__ counts) {
     const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(BLOCK) k_dir_remove_silos(Slot* slots, unsigne
 // activation lives on a removed silo (RemoveActivations with t.Item1 == removedSilo).  Removal is
 // LRU.RemoveKey: no generation moves.
 template <int MODE>
-__global__ void __launch_bounds__(BLOCK) k_cache_adjust(CacheSlot* slots, unsigned long long cap, RingArgs ring,
+static __global__ void __launch_bounds__(BLOCK) k_cache_adjust(CacheSlot* slots, unsigned long long cap, RingArgs ring,
                                                         const uint8_t* __restrict__ local, uint32_t n_local,
                                                         const uint32_t* __restrict__ set, CacheCounters* ctr,
                                                         unsigned long long* __restrict__ counts) {
@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(BLOCK) k_cache_adjust(CacheSlot* slots, unsign
 
 // A merge batch is a partition (a Dictionary): one item per grain.  Items sharing a slot are
 // flagged (err bit 8).
-__global__ void __launch_bounds__(BLOCK) k_dup_mark(const uint32_t* __restrict__ slot_of, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_dup_mark(const uint32_t* __restrict__ slot_of, uint32_t n,
                                                     uint32_t* __restrict__ last, DevCounters* ctr) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n || slot_of[i] >= SLOT_RETRY) return;
@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(BLOCK) k_dup_mark(const uint32_t* __restrict__
 
 // A rejected merge batch leaves no half-made entry: its new claims become tombstones (probe chains
 // through them stay intact).
-__global__ void __launch_bounds__(BLOCK) k_reg_abort(const uint32_t* __restrict__ slot_of,
+static __global__ void __launch_bounds__(BLOCK) k_reg_abort(const uint32_t* __restrict__ slot_of,
                                                      const uint8_t* __restrict__ is_new, uint32_t n, Slot* slots,
                                                      DevCounters* ctr) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(BLOCK) k_reg_abort(const uint32_t* __restrict_
 
 // gd_activation_ids_set: ids[acts[i]] = the i-th ActivationId (batch order; the last of a repeated
 // index wins only if the host repeats it -- it should not).
-__global__ void __launch_bounds__(BLOCK) k_scatter_ids(const uint32_t* __restrict__ acts,
+static __global__ void __launch_bounds__(BLOCK) k_scatter_ids(const uint32_t* __restrict__ acts,
                                                        const gd_key* __restrict__ in, uint32_t n,
                                                        gd_key* __restrict__ ids) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -181,7 +181,7 @@ constexpr uint32_t MERGE_TAG_MULTI = 0x80000000u;   // GD_MERGE_TAG_MULTI_INSTAN
 // err bit 16.  in_tags: the incoming entries' VersionTags (NULL: a new tag); bit 31 (MERGE_TAG_MULTI)
 // marks an incoming GrainInfo whose SingleInstance is false (an AddActivation grain with one
 // instance), which partitionData.Add keeps as it is (:517-520).
-__global__ void __launch_bounds__(BLOCK) k_merge_apply(const gd_key* __restrict__ keys,
+static __global__ void __launch_bounds__(BLOCK) k_merge_apply(const gd_key* __restrict__ keys,
                                                        const gd_val* __restrict__ vals,
                                                        const int32_t* __restrict__ in_tags, uint32_t n,
                                                        const uint32_t* __restrict__ slot_of,
@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(BLOCK) k_merge_apply(const gd_key* __restrict_
 // Split entries with what travels: the ActivationId of their activation index (ids[act]; none for a
 // multi-activation entry) and their VersionTag in the public merge form (bit 31 = not SingleInstance).
 // `flag` / `pos` from k_split_mark + scan, as k_split_emit; move = tombstone the slot.
-__global__ void __launch_bounds__(BLOCK) k_split_emit_tagged(Slot* __restrict__ slots, unsigned long long cap,
+static __global__ void __launch_bounds__(BLOCK) k_split_emit_tagged(Slot* __restrict__ slots, unsigned long long cap,
                                                              const uint32_t* __restrict__ flag,
                                                              const uint32_t* __restrict__ pos, int move,
                                                              const uint32_t* __restrict__ vtag,
@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(BLOCK) k_split_emit_tagged(Slot* __restrict__ 
 }
 
 // Partition order: the split's fields by the positions k_shard_scatter left (send_idx).
-__global__ void __launch_bounds__(BLOCK) k_gather_handoff(const uint32_t* __restrict__ idx, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_gather_handoff(const uint32_t* __restrict__ idx, uint32_t n,
                                                           const gd_key* __restrict__ ids,
                                                           const uint32_t* __restrict__ silo,
                                                           const uint32_t* __restrict__ tag,
@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(BLOCK) k_gather_handoff(const uint32_t* __rest
 
 // Received entries take the receiver's activation indices act_base + j (their ActivationIds are
 // appended to its index -> ActivationId map); multi-activation entries stay GD_ACT_MULTI.
-__global__ void __launch_bounds__(BLOCK) k_handoff_vals(const gd_key* __restrict__ rids,
+static __global__ void __launch_bounds__(BLOCK) k_handoff_vals(const gd_key* __restrict__ rids,
                                                         const uint32_t* __restrict__ rsilo, uint32_t m,
                                                         uint32_t act_base, gd_key* __restrict__ ids,
                                                         gd_val* __restrict__ vals, uint32_t* __restrict__ acts) {
@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(BLOCK) k_handoff_vals(const gd_key* __restrict
 // wins, AddSingleActivation :304-326): INSERTED, SAME (the same ActivationId was there), DROPPED
 // (another activation holds the grain: the incoming one is not registered; dropped = the holder),
 // HOST (a multi-activation entry: C# unions its instances).
-__global__ void __launch_bounds__(BLOCK) k_handoff_add_status(const gd_val* __restrict__ in,
+static __global__ void __launch_bounds__(BLOCK) k_handoff_add_status(const gd_val* __restrict__ in,
                                                               const gd_val* __restrict__ got,
                                                               const uint8_t* __restrict__ ins, uint32_t m,
                                                               const gd_key* __restrict__ ids,

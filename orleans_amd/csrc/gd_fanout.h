@@ -31,7 +31,7 @@ constexpr uint32_t FAN_LDS_ITEMS = FAN_TILE;       // publishers staged per bloc
 
 // ends[i] = out-degree of frontier[i] (0 for ids outside the graph: a grain nobody follows);
 // the u64 total goes to *total (block reduce + one atomic per block).
-__global__ void __launch_bounds__(BLOCK) k_fan_degree(const uint32_t* __restrict__ row_off, uint32_t n_nodes,
+static __global__ void __launch_bounds__(BLOCK) k_fan_degree(const uint32_t* __restrict__ row_off, uint32_t n_nodes,
                                                       const uint32_t* __restrict__ frontier, uint32_t n_front,
                                                       uint32_t* __restrict__ ends,
                                                       unsigned long long* __restrict__ total) {
@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(BLOCK) k_fan_degree(const uint32_t* __restrict
 template <int IPT>
 // d_nf (optional): the frontier's length on the device (<= n_front, the grid's bound), as
 // k_frontier_compact left it -- the in-library cascade sizes a hop without reading it back first.
-__global__ void __launch_bounds__(BLOCK) k_fan_degree_tiles(const uint32_t* __restrict__ row_off, uint32_t n_nodes,
+static __global__ void __launch_bounds__(BLOCK) k_fan_degree_tiles(const uint32_t* __restrict__ row_off, uint32_t n_nodes,
                                                             const uint32_t* __restrict__ frontier, uint32_t n_front,
                                                             uint32_t* __restrict__ ends, uint32_t* __restrict__ part,
                                                             const uint32_t* __restrict__ d_nf) {
@@ -152,7 +152,7 @@ __device__ __forceinline__ void fan_item(const FanStage& s, const uint32_t* __re
 // owner instead of a 28-B header.
 // node_of (partitioned graphs, gd_fanout_multi_part_device): the frontier holds this rank's local rows
 // (activation indices); the sender written is the row's node.
-__global__ void __launch_bounds__(BLOCK) k_fan_expand(const uint32_t* __restrict__ row_off,
+static __global__ void __launch_bounds__(BLOCK) k_fan_expand(const uint32_t* __restrict__ row_off,
                                                       const uint32_t* __restrict__ dst,
                                                       const uint32_t* __restrict__ frontier, uint32_t n_front,
                                                       const uint32_t* __restrict__ ends, uint32_t total,
@@ -264,7 +264,7 @@ __device__ __forceinline__ uint32_t cx_want(const CxArgs& cx, uint64_t tcd) {
 // Route a batch of node ids (GrainId(typeCode, node), the owner side of the sharded fan-out).
 // CX: through the compact probe index.
 template <int MODE, bool CX = false, int RG = (int)CX_GROUP, bool CX8 = false>
-__global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restrict__ nodes, uint32_t n, uint64_t tcd,
+static __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restrict__ nodes, uint32_t n, uint64_t tcd,
                                                        RingArgs ring, TableArgs tab, uint32_t* __restrict__ out_silo,
                                                        uint32_t* __restrict__ out_act,
                                                        uint8_t* __restrict__ out_status, CxArgs cx = CxArgs{},
@@ -317,7 +317,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __restric
 // follower-list reads, then their first directory probes, are in flight together (one dependent
 // chain per item otherwise).
 template <int MODE, int ILP, bool CX = false, int RG = (int)CX_GROUP, bool CX8 = false>
-__global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict__ row_off,
+static __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict__ row_off,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint32_t* __restrict__ frontier, uint32_t n_front,
                                                      const uint32_t* __restrict__ ends, uint32_t total, uint64_t tcd,
@@ -467,7 +467,7 @@ __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict_
 constexpr uint32_t FR_ITEMS = 16;
 constexpr uint32_t FR_TILE = BLOCK * FR_ITEMS;
 
-__global__ void __launch_bounds__(BLOCK) k_frontier_count(const uint32_t* __restrict__ offsets, uint32_t n_act,
+static __global__ void __launch_bounds__(BLOCK) k_frontier_count(const uint32_t* __restrict__ offsets, uint32_t n_act,
                                                           uint8_t* __restrict__ visited, uint16_t* __restrict__ flags,
                                                           uint32_t* __restrict__ counts) {
     __shared__ uint32_t s_wsum[BLOCK / WAVE];
@@ -505,7 +505,7 @@ __global__ void __launch_bounds__(BLOCK) k_frontier_count(const uint32_t* __rest
     if (threadIdx.x == 0) counts[blockIdx.x] = c;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_frontier_compact(const uint16_t* __restrict__ flags,
+static __global__ void __launch_bounds__(BLOCK) k_frontier_compact(const uint16_t* __restrict__ flags,
                                                             const uint32_t* __restrict__ counts, uint32_t nb,
                                                             uint32_t* __restrict__ out, uint32_t* __restrict__ total) {
     __shared__ uint32_t s_wsum[BLOCK / WAVE];
@@ -523,7 +523,7 @@ __global__ void __launch_bounds__(BLOCK) k_frontier_compact(const uint16_t* __re
 
 // Partitioned graphs: this rank's seeds (node ids, routed on their owner) become local rows = their
 // activation indices; a seed without a live activation here counts in *bad (the host refuses the call).
-__global__ void __launch_bounds__(BLOCK) k_seed_rows(const uint32_t* __restrict__ act,
+static __global__ void __launch_bounds__(BLOCK) k_seed_rows(const uint32_t* __restrict__ act,
                                                      const uint8_t* __restrict__ status, uint32_t n, uint32_t n_act,
                                                      uint32_t* __restrict__ rows, uint32_t* __restrict__ bad) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -534,14 +534,14 @@ __global__ void __launch_bounds__(BLOCK) k_seed_rows(const uint32_t* __restrict_
 }
 
 // out[i] = table[in[i]] (a partitioned cascade's frontier rows -> their nodes).
-__global__ void __launch_bounds__(BLOCK) k_gather_u32(const uint32_t* __restrict__ in, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_gather_u32(const uint32_t* __restrict__ in, uint32_t n,
                                                       const uint32_t* __restrict__ table, uint32_t* __restrict__ out) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i < n) out[i] = table[in[i]];
 }
 
 // The seeds of a cascade have published: visited[u] = 1 for u < n_act (gd_fanout_multi_device).
-__global__ void __launch_bounds__(BLOCK) k_mark_visited(const uint32_t* __restrict__ nodes, uint32_t n, uint32_t n_act,
+static __global__ void __launch_bounds__(BLOCK) k_mark_visited(const uint32_t* __restrict__ nodes, uint32_t n, uint32_t n_act,
                                                         uint8_t* __restrict__ visited) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i < n && nodes[i] < n_act) visited[nodes[i]] = 1;

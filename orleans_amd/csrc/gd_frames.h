@@ -142,7 +142,7 @@ __device__ __forceinline__ void store_silo(uint32_t* out, uint32_t i, const uint
     for (int j = 0; j < 6; ++j) out[6ull * i + j] = s[j];
 }
 
-__global__ __launch_bounds__(BLOCK) void k_decode_frames(const uint8_t* __restrict__ buf, uint64_t buf_len,
+static __global__ __launch_bounds__(BLOCK) void k_decode_frames(const uint8_t* __restrict__ buf, uint64_t buf_len,
                                                          const uint64_t* __restrict__ frame_off, uint32_t n,
                                                          FrameFields o) {
     __shared__ uint32_t s_win[BLOCK / WAVE][WAVE][FRAME_ROW];
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(BLOCK) void k_decode_frames(const uint8_t* __restri
 
 // Dispatcher.AddressMessage skips complete addresses (Dispatcher.cs:718); frames without a decoded
 // TargetGrain go back to the C# deserializer.  Neither carries a silo / activation.
-__global__ __launch_bounds__(BLOCK) void k_frame_status(const uint32_t* __restrict__ flags, uint32_t n,
+static __global__ __launch_bounds__(BLOCK) void k_frame_status(const uint32_t* __restrict__ flags, uint32_t n,
                                                         uint32_t* __restrict__ silo, uint32_t* __restrict__ act,
                                                         uint8_t* __restrict__ status) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;

@@ -259,7 +259,7 @@ __device__ __forceinline__ void route_one(uint64_t n0, uint64_t n1, uint64_t tcd
 
 // One message per thread.  PROBE=false gives CalculateTargetSilo only.
 template <int MODE, bool PROBE>
-__global__ void __launch_bounds__(BLOCK) k_route(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+static __global__ void __launch_bounds__(BLOCK) k_route(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                  TableArgs tab, uint32_t* __restrict__ out_silo,
                                                  uint32_t* __restrict__ out_act,
                                                  uint8_t* __restrict__ out_status) {
@@ -546,7 +546,7 @@ __device__ __forceinline__ void mb_mark(unsigned long long* ts, int k, unsigned 
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(MB_ROUTE_BLOCK) k_mb_route(const gd_key* __restrict__ keys, uint32_t n,
+static __global__ void __launch_bounds__(MB_ROUTE_BLOCK) k_mb_route(const gd_key* __restrict__ keys, uint32_t n,
                                                             RingArgs ring, TableArgs tab,
                                                             uint32_t* __restrict__ out_silo,
                                                             uint32_t* __restrict__ out_act,
@@ -584,7 +584,7 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb, uint32_t x
 // src_out (optional, the exchange's receive side): message i's sender rank, from the per-sender
 // receive counts rcnt[world] (k_recv_src's job, done here beside the probe's own writes).
 template <int MODE, int M, bool NT, int N1W = 0, bool CX = false, int RG_CX = (int)CX_GROUP, bool CX8 = false>
-__global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+static __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                    TableArgs tab, uint32_t* __restrict__ out_silo,
                                                    uint32_t* __restrict__ out_act,
                                                    uint8_t* __restrict__ out_status, uint64_t tcd_u, uint32_t xcd,
@@ -636,7 +636,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ ke
 // 0.224 ms).  The region's messages are W segments, one per sender (seg: k_region_segments); the
 // G = gridDim.x / 8 workgroups of a region take its blocks of BLOCK messages grid-stride.
 template <int MODE, int N1W>
-__global__ void __launch_bounds__(BLOCK) k_route_region(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+static __global__ void __launch_bounds__(BLOCK) k_route_region(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                         TableArgs tab, uint32_t* __restrict__ out_silo,
                                                         uint32_t* __restrict__ out_act,
                                                         uint8_t* __restrict__ out_status, uint64_t tcd_u,
@@ -678,7 +678,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_region(const gd_key* __restrict
 
 // GetPrimaryTargetSilo(uint key) over raw ring keys.
 template <int MODE>
-__global__ void __launch_bounds__(BLOCK) k_ring_hashes(const uint32_t* __restrict__ hashes, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_ring_hashes(const uint32_t* __restrict__ hashes, uint32_t n,
                                                        RingArgs ring, uint32_t* __restrict__ out_silo) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     uint32_t* s_pts = s_ring;
@@ -701,7 +701,7 @@ constexpr uint32_t SLOT_RETRY = 0xFFFFFFFEu;
 
 // vals / valid (nullable): an item whose silo is not valid is skipped (slot_of = NONE32): the
 // IsValidSilo check of AddSingleActivation / AddActivation (GrainDirectoryPartition.cs:279,310).
-__global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __restrict__ keys, uint32_t n, Slot* slots,
+static __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __restrict__ keys, uint32_t n, Slot* slots,
                                                      unsigned long long mask, DevCounters* ctr,
                                                      uint32_t* __restrict__ slot_of,
                                                      uint8_t* __restrict__ is_new, uint32_t retry_only,
@@ -769,14 +769,14 @@ __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __restrict__ 
 
 // Phase 2: the lowest batch index among the items of a new entry wins (sequential
 // "first registration wins" order).
-__global__ void __launch_bounds__(BLOCK) k_reg_minwin(const uint32_t* __restrict__ slot_of,
+static __global__ void __launch_bounds__(BLOCK) k_reg_minwin(const uint32_t* __restrict__ slot_of,
                                                       const uint8_t* __restrict__ is_new, uint32_t n, Slot* slots) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n || !is_new[i]) return;
     atomicMin(&slots[slot_of[i]].act, i);   // is_new implies a real slot index
 }
 
-__global__ void __launch_bounds__(BLOCK) k_reg_resolve(const uint32_t* __restrict__ slot_of,
+static __global__ void __launch_bounds__(BLOCK) k_reg_resolve(const uint32_t* __restrict__ slot_of,
                                                        const uint8_t* __restrict__ is_new, uint32_t n,
                                                        const Slot* slots, uint32_t* __restrict__ win) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -784,7 +784,7 @@ __global__ void __launch_bounds__(BLOCK) k_reg_resolve(const uint32_t* __restric
     win[i] = is_new[i] ? slots[slot_of[i]].act : NONE32;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_reg_commit(const uint32_t* __restrict__ slot_of,
+static __global__ void __launch_bounds__(BLOCK) k_reg_commit(const uint32_t* __restrict__ slot_of,
                                                       const uint32_t* __restrict__ win,
                                                       const gd_val* __restrict__ vals, uint32_t n, Slot* slots,
                                                       DevCounters* ctr, uint32_t* __restrict__ vtag, uint32_t op) {
@@ -801,13 +801,13 @@ __global__ void __launch_bounds__(BLOCK) k_reg_commit(const uint32_t* __restrict
 
 // gd_dir_upsert: the last batch item of each slot wins (batch order), then writes its value.
 // `last` (one u32 per table slot, zero between calls) holds 1 + the winning index.
-__global__ void __launch_bounds__(BLOCK) k_up_last(const uint32_t* __restrict__ slot_of, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_up_last(const uint32_t* __restrict__ slot_of, uint32_t n,
                                                    uint32_t* __restrict__ last) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n || slot_of[i] >= SLOT_RETRY) return;
     atomicMax(&last[slot_of[i]], i + 1);
 }
-__global__ void __launch_bounds__(BLOCK) k_up_apply(const uint32_t* __restrict__ slot_of,
+static __global__ void __launch_bounds__(BLOCK) k_up_apply(const uint32_t* __restrict__ slot_of,
                                                     const uint8_t* __restrict__ is_new, const gd_val* __restrict__ vals,
                                                     uint32_t n, const uint32_t* __restrict__ last, Slot* slots,
                                                     DevCounters* ctr, uint8_t* __restrict__ out_inserted,
@@ -831,13 +831,13 @@ __global__ void __launch_bounds__(BLOCK) k_up_apply(const uint32_t* __restrict__
     }
     out_inserted[i] = ins;
 }
-__global__ void __launch_bounds__(BLOCK) k_up_clear(const uint32_t* __restrict__ slot_of, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_up_clear(const uint32_t* __restrict__ slot_of, uint32_t n,
                                                     uint32_t* __restrict__ last) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i < n && slot_of[i] < SLOT_RETRY) last[slot_of[i]] = 0;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_reg_report(const uint32_t* __restrict__ slot_of,
+static __global__ void __launch_bounds__(BLOCK) k_reg_report(const uint32_t* __restrict__ slot_of,
                                                       const uint32_t* __restrict__ win, uint32_t n,
                                                       const Slot* slots, gd_val* __restrict__ out_vals,
                                                       uint8_t* __restrict__ out_inserted) {
@@ -856,7 +856,7 @@ __global__ void __launch_bounds__(BLOCK) k_reg_report(const uint32_t* __restrict
 
 // RemoveActivation (GrainDirectoryPartition.cs:335-363, Force): find the live entry
 // whose single activation matches; the first matching item of the batch removes it.
-__global__ void __launch_bounds__(BLOCK) k_unreg_find(const gd_key* __restrict__ keys,
+static __global__ void __launch_bounds__(BLOCK) k_unreg_find(const gd_key* __restrict__ keys,
                                                       const uint32_t* __restrict__ acts, uint32_t n,
                                                       const Slot* slots, unsigned long long mask,
                                                       const DevCounters* ctr, uint32_t* __restrict__ slot_of) {
@@ -880,19 +880,19 @@ __global__ void __launch_bounds__(BLOCK) k_unreg_find(const gd_key* __restrict__
 }
 
 // The matched entry is being removed, so its n0 word can carry the election.
-__global__ void __launch_bounds__(BLOCK) k_unreg_poison(const uint32_t* __restrict__ slot_of, uint32_t n, Slot* slots) {
+static __global__ void __launch_bounds__(BLOCK) k_unreg_poison(const uint32_t* __restrict__ slot_of, uint32_t n, Slot* slots) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n || slot_of[i] == NONE32) return;
     slots[slot_of[i]].n0 = ~0ull;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_unreg_min(const uint32_t* __restrict__ slot_of, uint32_t n, Slot* slots) {
+static __global__ void __launch_bounds__(BLOCK) k_unreg_min(const uint32_t* __restrict__ slot_of, uint32_t n, Slot* slots) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n || slot_of[i] == NONE32) return;
     atomicMin(reinterpret_cast<unsigned long long*>(&slots[slot_of[i]].n0), (unsigned long long)i);
 }
 
-__global__ void __launch_bounds__(BLOCK) k_unreg_commit(const uint32_t* __restrict__ slot_of, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_unreg_commit(const uint32_t* __restrict__ slot_of, uint32_t n,
                                                         Slot* slots, DevCounters* ctr,
                                                         uint8_t* __restrict__ out_removed) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -908,7 +908,7 @@ __global__ void __launch_bounds__(BLOCK) k_unreg_commit(const uint32_t* __restri
     if (out_removed) out_removed[i] = removed;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_dir_lookup(const gd_key* __restrict__ keys, uint32_t n, TableArgs tab,
+static __global__ void __launch_bounds__(BLOCK) k_dir_lookup(const gd_key* __restrict__ keys, uint32_t n, TableArgs tab,
                                                       gd_val* __restrict__ out_vals, uint8_t* __restrict__ found) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
@@ -921,7 +921,7 @@ __global__ void __launch_bounds__(BLOCK) k_dir_lookup(const gd_key* __restrict__
 
 // Rebuild: every live entry of the old table into the new one (keys are distinct,
 // so a claimer never needs to compare keys).
-__global__ void __launch_bounds__(BLOCK) k_rehash(const Slot* __restrict__ old_slots, unsigned long long old_cap,
+static __global__ void __launch_bounds__(BLOCK) k_rehash(const Slot* __restrict__ old_slots, unsigned long long old_cap,
                                                   Slot* slots, unsigned long long mask, DevCounters* ctr,
                                                   const uint32_t* __restrict__ old_vtag, uint32_t* __restrict__ vtag) {
     const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
@@ -1041,7 +1041,7 @@ __device__ __forceinline__ void fill_grid(const FillArgs& f, uint32_t nt) {
 // digits within a wave instruction: the lanes sharing the first active lane's
 // digit (the hot key under Zipf skew) are folded into one LDS atomic.
 template <int BITS, int NT, int IT>
-__global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t clamp,
+static __global__ void __launch_bounds__(NT) k_radix_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t clamp,
                                                    uint32_t shift, uint32_t tiles, uint32_t* __restrict__ hist,
                                                    FillArgs fill) {
     constexpr uint32_t R = 1u << BITS;
@@ -1107,7 +1107,7 @@ __device__ __forceinline__ uint32_t hist_t0(uint32_t b, uint32_t nb, uint32_t tp
 // digit-major counts it writes for one digit are then TPB consecutive words, instead of one word
 // every `tiles` words per workgroup.  Same output as k_radix_hist.
 template <int BITS, int NT, int IT, int TPB>
-__global__ void __launch_bounds__(NT) k_radix_hist_multi(const uint32_t* __restrict__ keys, uint32_t n,
+static __global__ void __launch_bounds__(NT) k_radix_hist_multi(const uint32_t* __restrict__ keys, uint32_t n,
                                                          uint32_t clamp, uint32_t shift, uint32_t tiles,
                                                          uint32_t* __restrict__ hist, FillArgs fill,
                                                          uint32_t xcd_rev) {
@@ -1175,7 +1175,7 @@ __global__ void __launch_bounds__(NT) k_radix_hist_multi(const uint32_t* __restr
 // workgroup as k_radix_hist_multi (TPB = 1: k_radix_hist's layout).  Same output as those for the
 // full keys.
 template <int BITS, int NT, int IT, int TPB>
-__global__ void __launch_bounds__(NT) k_radix_hist16(const uint16_t* __restrict__ keys, uint32_t n, uint32_t shift,
+static __global__ void __launch_bounds__(NT) k_radix_hist16(const uint16_t* __restrict__ keys, uint32_t n, uint32_t shift,
                                                      uint32_t tiles, uint32_t* __restrict__ hist, uint32_t xcd_rev) {
     constexpr uint32_t R = 1u << BITS;
     constexpr uint32_t TILE = NT * IT;
@@ -1255,7 +1255,7 @@ struct Pack {
 // sorted by the whole key: the lower passes ordered it) lowers starts[key] to its output
 // position with atomicMin; the earliest tile holding the key wins (starts pre-filled with n).
 template <int BITS, bool FIRST, int NT, int IT>
-__global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict__ keys_in,
+static __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict__ keys_in,
                                                       const uint32_t* __restrict__ vals_in, uint32_t n,
                                                       uint32_t clamp, uint32_t shift, uint32_t tiles,
                                                       const uint32_t* __restrict__ gscan,
@@ -1446,7 +1446,7 @@ __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __restrict
 
 // offsets[k] = first position of key k in the sorted keys (others stay at the fill
 // value and are fixed by a reverse min-scan).
-__global__ void __launch_bounds__(BLOCK) k_bucket_starts(const uint32_t* __restrict__ skeys, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_bucket_starts(const uint32_t* __restrict__ skeys, uint32_t n,
                                                          uint32_t* __restrict__ offsets) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
@@ -1454,7 +1454,7 @@ __global__ void __launch_bounds__(BLOCK) k_bucket_starts(const uint32_t* __restr
     if (i == 0 || skeys[i - 1] != k) offsets[k] = i;
 }
 
-__global__ void k_fill_u32(uint32_t* __restrict__ p, uint32_t n, uint32_t v) {
+static __global__ void k_fill_u32(uint32_t* __restrict__ p, uint32_t n, uint32_t v) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
 }
@@ -1542,7 +1542,7 @@ __device__ __forceinline__ void scan_load(const uint32_t* in, uint32_t n, bool r
 }
 
 template <class Op, int IPT = SCAN_ITEMS>
-__global__ void __launch_bounds__(BLOCK) k_scan_reduce(const uint32_t* __restrict__ in, uint32_t n, bool rev,
+static __global__ void __launch_bounds__(BLOCK) k_scan_reduce(const uint32_t* __restrict__ in, uint32_t n, bool rev,
                                                        uint32_t* __restrict__ partials) {
     __shared__ uint32_t s_wsum[BLOCK / WAVE];
     uint32_t v[IPT];
@@ -1556,7 +1556,7 @@ __global__ void __launch_bounds__(BLOCK) k_scan_reduce(const uint32_t* __restric
 
 // Exclusive scan of `m` partials in one block (sequential over chunks).
 template <class Op>
-__global__ void __launch_bounds__(BLOCK) k_scan_partials(uint32_t* partials, uint32_t m) {
+static __global__ void __launch_bounds__(BLOCK) k_scan_partials(uint32_t* partials, uint32_t m) {
     __shared__ uint32_t s_wsum[BLOCK / WAVE];
     __shared__ uint32_t s_carry;
     if (threadIdx.x == 0) s_carry = Op::identity;
@@ -1574,7 +1574,7 @@ __global__ void __launch_bounds__(BLOCK) k_scan_partials(uint32_t* partials, uin
 }
 
 template <class Op, int IPT = SCAN_ITEMS>
-__global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_t* out, uint32_t n, bool rev,
+static __global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_t* out, uint32_t n, bool rev,
                                                      bool inclusive, const uint32_t* __restrict__ partials,
                                                      uint32_t n_partials_raw) {
     __shared__ uint32_t s_wsum[BLOCK / WAVE];
@@ -1623,7 +1623,7 @@ __global__ void __launch_bounds__(BLOCK) k_scan_down(const uint32_t* in, uint32_
 // row hist[d * tiles, (d + 1) * tiles) in place, and the row total into totals[d].  The scatter
 // adds the digit's base (the exclusive prefix of the totals) itself, so a pass takes one scan
 // launch here instead of a device-wide reduce + down-sweep.
-__global__ void __launch_bounds__(BLOCK) k_radix_rowscan(uint32_t* __restrict__ hist, uint32_t tiles,
+static __global__ void __launch_bounds__(BLOCK) k_radix_rowscan(uint32_t* __restrict__ hist, uint32_t tiles,
                                                          uint32_t* __restrict__ totals) {
     constexpr int IPT = 16;
     constexpr uint32_t CH = BLOCK * IPT;
@@ -1684,7 +1684,7 @@ constexpr uint32_t RS_THREADS = 1024;
 constexpr uint32_t RS_IPT = 16;
 constexpr uint32_t RS_RANGE = RS_THREADS * RS_IPT;      // 16,384 activations per sub-range
 constexpr uint32_t RS_MAX_SUB = 16;                      // digit ranges up to 2^18 activations
-__global__ void __launch_bounds__(RS_THREADS) k_starts_rangescan(uint32_t* __restrict__ offsets, uint32_t n_scan,
+static __global__ void __launch_bounds__(RS_THREADS) k_starts_rangescan(uint32_t* __restrict__ offsets, uint32_t n_scan,
                                                                  uint32_t shift, const uint32_t* __restrict__ totals,
                                                                  uint32_t n_digits) {
     constexpr uint32_t NW = RS_THREADS / WAVE;
@@ -2054,7 +2054,7 @@ __device__ __forceinline__ void mb_sort_runs_core(MbShared& sh, uint32_t (&kk)[I
 // the outputs: zero-copy stores to host memory are spread over as many CUs.  act_copy (optional):
 // the activations also go to the host block.
 template <int BITS, int IT>
-__global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32_t* __restrict__ act, uint32_t n,
+static __global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32_t* __restrict__ act, uint32_t n,
                                                               uint32_t passes, uint32_t n_act,
                                                               uint32_t* __restrict__ perm,
                                                               uint32_t* __restrict__ run_act,

@@ -256,7 +256,7 @@ __device__ __forceinline__ bool ext_of(const ExtArgs& e, uint32_t i, const uint8
 // The messages k_route left at GD_ROUTE_KEYEXT: owner by the KeyExt hash
 // (CalculateTargetSilo, LocalGrainDirectory.cs:477-545), then the KeyExt table.
 template <int MODE>
-__global__ void __launch_bounds__(BLOCK) k_route_keyext(const gd_key* __restrict__ keys, uint32_t n, ExtArgs ext,
+static __global__ void __launch_bounds__(BLOCK) k_route_keyext(const gd_key* __restrict__ keys, uint32_t n, ExtArgs ext,
                                                         RingArgs ring, KxArgs tab, uint32_t* __restrict__ out_silo,
                                                         uint32_t* __restrict__ out_act,
                                                         uint8_t* __restrict__ out_status) {
@@ -288,7 +288,7 @@ __global__ void __launch_bounds__(BLOCK) k_route_keyext(const gd_key* __restrict
 
 // LookUpActivations for KeyExt keys (no ring needed).  found: 1 hit, 0 miss, 2 not a KeyExt
 // lookup the device can answer (GD_KEYEXT_HOST / bad range).
-__global__ void __launch_bounds__(BLOCK) k_kx_lookup(const gd_key* __restrict__ keys, uint32_t n, ExtArgs ext,
+static __global__ void __launch_bounds__(BLOCK) k_kx_lookup(const gd_key* __restrict__ keys, uint32_t n, ExtArgs ext,
                                                      KxArgs tab, gd_val* __restrict__ out_vals,
                                                      uint8_t* __restrict__ out_found) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(BLOCK) k_kx_lookup(const gd_key* __restrict__ 
 
 // Uniform hashes of KeyExt keys on the device (the host index checks its own against these in
 // the parity tests): GD_KEYEXT_NULL -> three-word hash.
-__global__ void __launch_bounds__(BLOCK) k_kx_hash(const gd_key* __restrict__ keys, uint32_t n, ExtArgs ext,
+static __global__ void __launch_bounds__(BLOCK) k_kx_hash(const gd_key* __restrict__ keys, uint32_t n, ExtArgs ext,
                                                    uint32_t* __restrict__ out) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(BLOCK) k_kx_hash(const gd_key* __restrict__ ke
 }
 
 // Apply host-index changes: slots[idx[j]] = val[j].
-__global__ void __launch_bounds__(BLOCK) k_kx_apply(const uint64_t* __restrict__ idx, const KxSlot* __restrict__ val,
+static __global__ void __launch_bounds__(BLOCK) k_kx_apply(const uint64_t* __restrict__ idx, const KxSlot* __restrict__ val,
                                                     uint32_t m, KxSlot* __restrict__ slots) {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j < m) slots[idx[j]] = val[j];

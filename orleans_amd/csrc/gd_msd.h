@@ -265,7 +265,7 @@ __device__ __forceinline__ void msd_range(MsdShared<NT, RW>& sh, uint32_t b, uin
 // (patterns: one address, u16-pair increments, pseudo-random colliding addresses, partial EXEC),
 // refusing the handle when it fails.  One workgroup of 256 threads, 64 rounds; out[t] = thread t's
 // mismatches (vector stores, summed by the host).
-__global__ void __launch_bounds__(256) k_lane_order_check(uint32_t* __restrict__ out) {
+static __global__ void __launch_bounds__(256) k_lane_order_check(uint32_t* __restrict__ out) {
     __shared__ uint32_t s_w[4][16];
     const uint32_t lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
     uint32_t bad = 0;
@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(256) k_lane_order_check(uint32_t* __restrict__
 // Against one workgroup a range (round 3): 0.0523 -> 0.0495 ms at cfg 2, stage 0.148 -> 0.146 ms
 // (3 interleaved rounds each).
 template <bool BALLOT>
-__global__ void __launch_bounds__(MSD_NT, 1) k_msd_local(const uint16_t* __restrict__ keys16,
+static __global__ void __launch_bounds__(MSD_NT, 1) k_msd_local(const uint16_t* __restrict__ keys16,
                                                             const uint32_t* __restrict__ idx,
                                                             const uint32_t* __restrict__ totals, uint32_t R,
                                                             uint32_t n, uint32_t n_act, uint32_t* __restrict__ perm,
@@ -345,7 +345,7 @@ __global__ void __launch_bounds__(MSD_NT, 1) k_msd_local(const uint16_t* __restr
 // ranges of a few thousand messages of BASELINE cfg 4 (~4,400 a range) and cfg 3's mid ranks.  (Hot-key
 // folding measured slower here: 0.077 against 0.059 ms at cfg 3.)
 template <int NT, int RW, bool BALLOT>
-__global__ void __launch_bounds__(NT, (NT == MSD_NT ? 4 : 6)) k_msd_local_list(const uint16_t* __restrict__ keys16,
+static __global__ void __launch_bounds__(NT, (NT == MSD_NT ? 4 : 6)) k_msd_local_list(const uint16_t* __restrict__ keys16,
                                                                               const uint32_t* __restrict__ idx,
                                                                               const uint32_t* __restrict__ rs,
                                                                               const uint32_t* __restrict__ list,

@@ -65,7 +65,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // The d2 segments' starts (exclusive prefix of pass A's digit totals) and tile bases
 // (exclusive prefix of ceil(size / SEG_TILE)), every pass-B tile's segment (NONE32 past the last), and
 // the level-2 counters zeroed.  ra <= SEG_RMAX.
-__global__ void __launch_bounds__(1024) k_seg_table(const uint32_t* __restrict__ totals, uint32_t ra,
+static __global__ void __launch_bounds__(1024) k_seg_table(const uint32_t* __restrict__ totals, uint32_t ra,
                                                     uint32_t tbound, uint32_t* __restrict__ seg_start,
                                                     uint32_t* __restrict__ seg_tb, uint32_t* __restrict__ tile_seg,
                                                     uint32_t* __restrict__ ctr) {
@@ -143,7 +143,7 @@ struct SegIn {
 // alone, 16 B a load from the 16-B boundary at or below the tile's first item (items outside the tile
 // masked): 2 B a message.
 template <bool PK>
-__global__ void __launch_bounds__(SEG_NT) k_seg_hist(SegIn in, const uint32_t* __restrict__ tile_seg,
+static __global__ void __launch_bounds__(SEG_NT) k_seg_hist(SegIn in, const uint32_t* __restrict__ tile_seg,
                                                      const uint32_t* __restrict__ seg_start,
                                                      const uint32_t* __restrict__ seg_tb, uint32_t rb,
                                                      uint32_t* __restrict__ hseg) {
@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(SEG_NT) k_seg_hist(SegIn in, const uint32_t* _
 // Pass B scatter: tile j's records ranked stably by d1 and written at the flat-scanned positions
 // hseg[tb * rb + d * ts + tl] + rank: the range-local key (key & 1023) as u16 and the index.
 template <bool PK, bool BALLOT = false>
-__global__ void __launch_bounds__(SEG_NT) k_seg_scatter(SegIn in, const uint32_t* __restrict__ tile_seg,
+static __global__ void __launch_bounds__(SEG_NT) k_seg_scatter(SegIn in, const uint32_t* __restrict__ tile_seg,
                                                         const uint32_t* __restrict__ seg_start,
                                                         const uint32_t* __restrict__ seg_tb, uint32_t rb,
                                                         const uint32_t* __restrict__ hseg,
@@ -340,7 +340,7 @@ __host__ __device__ __forceinline__ uint32_t cs_items(uint32_t C) {
 // word), so the chunked ranges' first chunks increase with their entries.
 constexpr int CL_NT = 1024;                    // (256: 0.025 -> 0.031 ms at cfg 3, the list order less sequential)
 constexpr int CL_NW = CL_NT / WAVE;
-__global__ void __launch_bounds__(CL_NT) k_l2_classify(const uint32_t* __restrict__ hseg,
+static __global__ void __launch_bounds__(CL_NT) k_l2_classify(const uint32_t* __restrict__ hseg,
                                                        const uint32_t* __restrict__ seg_start,
                                                        const uint32_t* __restrict__ seg_tb, uint32_t a, uint32_t R,
                                                        uint32_t n, uint32_t t_small, uint32_t t_mid,
@@ -440,7 +440,7 @@ __global__ void __launch_bounds__(CL_NT) k_l2_classify(const uint32_t* __restric
 // starts before then -- each range is three dependent HBM round trips (list, starts, records), which
 // left the thin ranges of BASELINE cfg 3 (~96K ranges of ~60 messages) latency-bound.
 template <bool BALLOT>
-__global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16_t* __restrict__ keys16,
+static __global__ void __launch_bounds__(L2_SMALL_WAVES * WAVE) k_l2_small(const uint16_t* __restrict__ keys16,
                                                                    const uint32_t* __restrict__ idx, L2Lists l,
                                                                    uint32_t n, uint32_t n_act,
                                                                    uint32_t* __restrict__ perm,
@@ -577,7 +577,7 @@ __device__ __forceinline__ ChunkWalk chunk_walk(uint32_t m) {
 }
 
 // Level 2, hot ranges: chunk j's activation counts, hh[j * 1,024 + a].
-__global__ void __launch_bounds__(CH_NT) k_l2_chunk_hist(const uint16_t* __restrict__ keys16, L2Lists l,
+static __global__ void __launch_bounds__(CH_NT) k_l2_chunk_hist(const uint16_t* __restrict__ keys16, L2Lists l,
                                                          uint32_t* __restrict__ hh) {
     __shared__ uint32_t s_cnt[MSD_L];
     const uint32_t tid = threadIdx.x, lane = lane_id();
@@ -669,7 +669,7 @@ __device__ __forceinline__ uint32_t cs_load(const uint32_t* hh, const CsItem& x,
 }
 
 // ptot: one CS_COLS-word row a chunk-scan item (its piece's column sums), at the item's index.
-__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_ptot(L2Lists l, const uint32_t* __restrict__ hh,
+static __global__ void __launch_bounds__(MSD_NT) k_l2_chunk_ptot(L2Lists l, const uint32_t* __restrict__ hh,
                                                           uint32_t* __restrict__ ptot) {
     __shared__ uint32_t s_m[CS_ROWS * (CS_COLS + 1)];
     const uint32_t lane = lane_id(), w = threadIdx.x / WAVE;
@@ -688,7 +688,7 @@ __global__ void __launch_bounds__(MSD_NT) k_l2_chunk_ptot(L2Lists l, const uint3
     }
 }
 
-__global__ void __launch_bounds__(MSD_NT) k_l2_chunk_scan(L2Lists l, uint32_t* __restrict__ hh,
+static __global__ void __launch_bounds__(MSD_NT) k_l2_chunk_scan(L2Lists l, uint32_t* __restrict__ hh,
                                                           const uint32_t* __restrict__ ptot,
                                                           uint32_t* __restrict__ tot) {
     __shared__ uint32_t s_m[CS_ROWS * (CS_COLS + 1)];
@@ -751,7 +751,7 @@ struct ChunkShared {
     uint32_t red[CH_NW];
 };
 template <bool BALLOT>
-__global__ void __launch_bounds__(CH_NT, 2) k_l2_chunk_scatter(const uint16_t* __restrict__ keys16,
+static __global__ void __launch_bounds__(CH_NT, 2) k_l2_chunk_scatter(const uint16_t* __restrict__ keys16,
                                                                const uint32_t* __restrict__ idx, L2Lists l,
                                                                const uint32_t* __restrict__ hh,
                                                                const uint32_t* __restrict__ tot, uint32_t n,

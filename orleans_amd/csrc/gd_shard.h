@@ -72,7 +72,7 @@ __device__ __forceinline__ uint32_t key_dest(uint64_t n0, uint64_t n1, uint64_t 
 // regions (keys only; 1 or N_REGIONS): destination = owner rank * regions + the grain's table region,
 // so each rank's chunk arrives grouped by region (gd_route_multi's region-mapped probe).
 template <int MODE, bool NODES, bool EXT = true>
-__global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ recs, uint32_t n, uint64_t tcd,
+static __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ recs, uint32_t n, uint64_t tcd,
                                                       RingArgs ring, uint32_t n_shards, uint32_t bits,
                                                       uint32_t tiles, uint8_t* __restrict__ dest,
                                                       uint32_t* __restrict__ hist, ExtArgs ext,
@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_hist(const void* __restrict__ r
 // 2^32 (narrow_ok), else 8 B.  kdesc = {mode (0 full, 1 u64 N1, 2 u32 N1), flags from k_shard_hist
 // (bit 0 wide, bit 1 some N1 >= 2^32), TCD lo, TCD hi}: the descriptor every peer receives with the
 // counts.
-__global__ void k_key_desc(const gd_key* __restrict__ keys, uint32_t n, uint32_t* __restrict__ kdesc,
+static __global__ void k_key_desc(const gd_key* __restrict__ keys, uint32_t n, uint32_t* __restrict__ kdesc,
                            uint32_t narrow_ok) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const uint64_t tcd = n ? reinterpret_cast<const uint64_t*>(keys)[2] : 0ull;
@@ -180,7 +180,7 @@ constexpr uint32_t IDX16_BLOCK_TILES = 65536u / SH_TILE;
 // Sender, after the partition's scan (gscan: exclusive over (dest, tile), rank-major): for rank r
 // and block b (tiles 32b .. 32b + 31), the position in r's chunk where block b starts.  Thread 0
 // also flags the descriptor and stores this sender's block count (the counts round sends it).
-__global__ void k_block_prefix(const uint32_t* __restrict__ gscan, uint32_t tiles, uint32_t n_shards,
+static __global__ void k_block_prefix(const uint32_t* __restrict__ gscan, uint32_t tiles, uint32_t n_shards,
                                uint32_t nblk, uint32_t* __restrict__ out, uint32_t* __restrict__ kdesc,
                                uint32_t* __restrict__ nblk_out) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -197,7 +197,7 @@ __global__ void k_block_prefix(const uint32_t* __restrict__ gscan, uint32_t tile
 // back to back (2 or 4 B a message by the sender's descriptor, each chunk padded to 4 B), pcol =
 // the 2-B senders' block starts back to back (rnblk[q] each).  Writes the 4-B origin index and the
 // sender rank of every received message (k_recv_src's job).
-__global__ void __launch_bounds__(BLOCK) k_recv_idx16(const uint8_t* __restrict__ raw,
+static __global__ void __launch_bounds__(BLOCK) k_recv_idx16(const uint8_t* __restrict__ raw,
                                                       const uint32_t* __restrict__ rcount,
                                                       const uint32_t* __restrict__ rdesc,
                                                       const uint32_t* __restrict__ pcol,
@@ -261,7 +261,7 @@ __host__ __device__ __forceinline__ uint32_t header_bytes(uint32_t mode) { retur
 // Receiver of a header round where some peer sent compact headers: raw = the peers' chunks back to
 // back (8 B or 24 B per header by each peer's descriptor); rebuild the 24-B keys and the sender
 // rank of every received message (k_recv_src's job otherwise).
-__global__ void __launch_bounds__(BLOCK) k_recv_expand(const uint8_t* __restrict__ raw,
+static __global__ void __launch_bounds__(BLOCK) k_recv_expand(const uint8_t* __restrict__ raw,
                                                        const uint32_t* __restrict__ rcount,
                                                        const uint32_t* __restrict__ rdesc, uint32_t world,
                                                        uint32_t m, gd_key* __restrict__ keys,
@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(BLOCK) k_recv_expand(const uint8_t* __restrict
 // n_shards: the send to ActivationAddress.Silo after the remote lookup, LocalGrainDirectory.cs:920,
 // OutboundMessageQueue.cs:125); every other status stays on this rank.  Same counting as
 // k_shard_hist; k_shard_scatter then moves the keys with payload = position in the input.
-__global__ void __launch_bounds__(SH_NT) k_fwd_hist(const uint8_t* __restrict__ st, const uint32_t* __restrict__ silo,
+static __global__ void __launch_bounds__(SH_NT) k_fwd_hist(const uint8_t* __restrict__ st, const uint32_t* __restrict__ silo,
                                                     uint32_t n, uint32_t n_shards, uint32_t my_rank, uint32_t bits,
                                                     uint32_t tiles, uint8_t* __restrict__ dest,
                                                     uint32_t* __restrict__ hist) {
@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(SH_NT) k_fwd_hist(const uint8_t* __restrict__ 
 }
 
 // The forwarded messages' other fields in send order (pos = k_shard_scatter's payload).
-__global__ void __launch_bounds__(BLOCK) k_fwd_gather(const uint32_t* __restrict__ pos, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_fwd_gather(const uint32_t* __restrict__ pos, uint32_t n,
                                                       const uint32_t* __restrict__ idx_in,
                                                       const uint32_t* __restrict__ src_in,
                                                       const uint32_t* __restrict__ silo_in,
@@ -378,7 +378,7 @@ __global__ void __launch_bounds__(BLOCK) k_fwd_gather(const uint32_t* __restrict
 // payload_in == nullptr: the payload is the record's batch index (the origin index).  PT = uint16_t:
 // the payload is written as its low 16 bits (origin indices for the exchange, KD_IDX16).
 template <int BITS, bool NODES, bool SKIP_COMPACT = false, typename PT = uint32_t>
-__global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict__ recs,
+static __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict__ recs,
                                                          const uint32_t* __restrict__ payload_in,
                                                          const uint8_t* __restrict__ dest, uint32_t n,
                                                          uint32_t n_shards, uint32_t tiles,
@@ -526,7 +526,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_scatter(const void* __restrict_
 // case; gathering whole 24-B records measured slower than staging them: 0.18-0.24 vs 0.16 ms per
 // 16M keys at 1-8 destinations).  Same output as k_shard_scatter<BITS, false>.
 template <int BITS, typename PT = uint32_t>
-__global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict__ recs,
+static __global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict__ recs,
                                                         const uint32_t* __restrict__ payload_in,
                                                         const uint8_t* __restrict__ dest, uint32_t n,
                                                         uint32_t n_shards, uint32_t tiles,
@@ -648,7 +648,7 @@ __global__ void __launch_bounds__(SH_NT) k_shard_gather(const gd_key* __restrict
 // k_shard_hist's flags are final by now), one launch fewer on the partition stream.
 // counts[d] for the n_shards ranks; with regions, rank d's destinations are d * group .. (d + 1) * group
 // - 1 (its region chunks, contiguous in the send buffer).
-__global__ void k_shard_counts(const uint32_t* __restrict__ gscan, uint32_t tiles, uint32_t n_shards, uint32_t n,
+static __global__ void k_shard_counts(const uint32_t* __restrict__ gscan, uint32_t tiles, uint32_t n_shards, uint32_t n,
                                uint32_t* __restrict__ counts, const gd_key* __restrict__ keys,
                                uint32_t* __restrict__ kdesc, uint32_t narrow_ok, uint32_t group) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
@@ -671,7 +671,7 @@ __global__ void k_shard_counts(const uint32_t* __restrict__ gscan, uint32_t tile
 // message of region >= g.  seg[q * (N_REGIONS + 1) + g] = that position in the receive order
 // (seg[.. + N_REGIONS] = the chunk's end).  Keys: 24-B (N1W = 0) or N1s (N1W = 4 / 8, N0 = 0, tcd).
 template <int N1W>
-__global__ void k_region_segments(const void* __restrict__ keys, const uint32_t* __restrict__ rcount,
+static __global__ void k_region_segments(const void* __restrict__ keys, const uint32_t* __restrict__ rcount,
                                   uint32_t world, uint64_t tcd, uint32_t* __restrict__ seg) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= world * (N_REGIONS + 1)) return;
@@ -708,7 +708,7 @@ __global__ void k_region_segments(const void* __restrict__ keys, const uint32_t*
 
 // recv_src[i] = the rank chunk i of the receive buffer came from: off[r] <= i < off[r + 1], off =
 // exclusive scan of the per-rank receive counts (world <= 256, scanned in LDS by every block).
-__global__ void __launch_bounds__(BLOCK) k_recv_src(const uint32_t* __restrict__ rcount, uint32_t world, uint32_t m,
+static __global__ void __launch_bounds__(BLOCK) k_recv_src(const uint32_t* __restrict__ rcount, uint32_t world, uint32_t m,
                                                     uint32_t* __restrict__ src) {
     __shared__ uint32_t s_off[257];
     if (threadIdx.x == 0) {
@@ -733,7 +733,7 @@ __global__ void __launch_bounds__(BLOCK) k_recv_src(const uint32_t* __restrict__
 
 // Routes returned to the sender in shard order -> the sender's batch order (send_idx is the
 // partition's origin index): Dispatcher.AddressMessage's TargetSilo / TargetActivation per message.
-__global__ void __launch_bounds__(BLOCK) k_unpartition(const uint32_t* __restrict__ send_idx, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_unpartition(const uint32_t* __restrict__ send_idx, uint32_t n,
                                                        const uint32_t* __restrict__ silo_in,
                                                        const uint32_t* __restrict__ act_in,
                                                        const uint8_t* __restrict__ st_in, uint32_t* __restrict__ silo,
@@ -749,7 +749,7 @@ __global__ void __launch_bounds__(BLOCK) k_unpartition(const uint32_t* __restric
 
 // CalculateTargetSilo for a batch with KeyExt strings: the owner silo key_dest uses (no modulo).
 template <int MODE>
-__global__ void __launch_bounds__(BLOCK) k_owner_ext(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
+static __global__ void __launch_bounds__(BLOCK) k_owner_ext(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                      ExtArgs ext, uint32_t* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     uint32_t* s_pts = s_ring;
@@ -770,7 +770,7 @@ __device__ __forceinline__ uint32_t ext_bytes(const ExtArgs& e, uint32_t i) {
 
 // Per destination rank: bytes of KeyExt payload (LDS per block, one atomic per destination per
 // block).  group: destinations per rank in dest (N_REGIONS with a region-ordered partition).
-__global__ void __launch_bounds__(BLOCK) k_dest_bytes(const uint8_t* __restrict__ dest, uint32_t n, ExtArgs ext,
+static __global__ void __launch_bounds__(BLOCK) k_dest_bytes(const uint8_t* __restrict__ dest, uint32_t n, ExtArgs ext,
                                                       uint32_t n_shards, uint32_t* __restrict__ out, uint32_t group) {
     __shared__ uint32_t s_b[256];
     for (uint32_t d = threadIdx.x; d < 256; d += BLOCK) s_b[d] = 0;
@@ -786,7 +786,7 @@ __global__ void __launch_bounds__(BLOCK) k_dest_bytes(const uint8_t* __restrict_
 }
 
 // Lengths in send order (the partition's origin index picks them); payload sizes for the scan.
-__global__ void __launch_bounds__(BLOCK) k_send_lengths(const uint32_t* __restrict__ send_idx, uint32_t n,
+static __global__ void __launch_bounds__(BLOCK) k_send_lengths(const uint32_t* __restrict__ send_idx, uint32_t n,
                                                         ExtArgs ext, int32_t* __restrict__ send_len,
                                                         uint32_t* __restrict__ send_bytes) {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
@@ -797,7 +797,7 @@ __global__ void __launch_bounds__(BLOCK) k_send_lengths(const uint32_t* __restri
 }
 
 // Copy each message's KeyExt bytes to its place in the send blob (boff = exclusive scan).
-__global__ void __launch_bounds__(BLOCK) k_gather_ext(const uint32_t* __restrict__ send_idx, uint32_t n, ExtArgs ext,
+static __global__ void __launch_bounds__(BLOCK) k_gather_ext(const uint32_t* __restrict__ send_idx, uint32_t n, ExtArgs ext,
                                                       const uint32_t* __restrict__ boff, uint8_t* __restrict__ blob) {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j >= n) return;
@@ -812,12 +812,12 @@ __global__ void __launch_bounds__(BLOCK) k_gather_ext(const uint32_t* __restrict
 }
 
 // Receiver: payload sizes of the received lengths (for the scan), then 64-bit offsets.
-__global__ void __launch_bounds__(BLOCK) k_len_bytes(const int32_t* __restrict__ len, uint32_t m,
+static __global__ void __launch_bounds__(BLOCK) k_len_bytes(const int32_t* __restrict__ len, uint32_t m,
                                                      uint32_t* __restrict__ bytes) {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j < m) bytes[j] = len[j] > 0 ? (uint32_t)len[j] : 0u;
 }
-__global__ void __launch_bounds__(BLOCK) k_u32_to_u64(const uint32_t* __restrict__ a, uint32_t m,
+static __global__ void __launch_bounds__(BLOCK) k_u32_to_u64(const uint32_t* __restrict__ a, uint32_t m,
                                                       uint64_t* __restrict__ b) {
     const uint32_t j = blockIdx.x * BLOCK + threadIdx.x;
     if (j < m) b[j] = a[j];
