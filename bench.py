@@ -185,6 +185,8 @@ def roofline_of(kt: dict, steps: int, n: int, n_act: int, acts, tag, world: int 
     range sort, or the LSD scatter) on their implementation bytes -- `frac` -- with SURVEY 8(d)'s
     16 B/record/pass model beside them; and the whole bucketing stage against the 12-B contract.
     bytes_fn(name, form): a kernel's bytes a step when a step is not one batch (the cfg 4 cascade)."""
+    kt = dict(kt)
+    stage_ev = kt.pop("stage:bucket", None)       # one event pair around each whole bucketing (timing 2)
     form = bucket_form(kt)
     kernels = {}
     for name, (launches, ms) in kt.items():
@@ -245,10 +247,14 @@ def roofline_of(kt: dict, steps: int, n: int, n_act: int, acts, tag, world: int 
         roofline["bucketing_kernel"] = dict(form=form, bytes_model="implementation bytes (DESIGN 5); frac_pmc on "
                                             "the PMC counters' bytes where profiles/ holds them", **bk)
     stage = [k for k in BUCKET_KERNELS if k in kernels]
-    st_ms = sum(kernels[k]["ms_per_step"] for k in stage)
+    sum_ms = sum(kernels[k]["ms_per_step"] for k in stage)
+    # the stage's time: events around the whole bucketing (no events between its kernels, which add
+    # ~5 us a launch to the per-kernel sum), else the per-kernel sum
+    st_ms = stage_ev[1] / steps if stage_ev and stage_ev[0] else sum_ms
     st_b = sum(kernels[k]["alg_bytes_per_step"] or 0.0 for k in stage)
     roofline["bucketing_stage"] = {
-        "form": form, "kernels": stage, "ms_per_step": round(st_ms, 4),
+        "form": form, "kernels": stage, "ms_per_step": round(st_ms, 4), "kernel_sum_ms_per_step": round(sum_ms, 4),
+        "timing": "stage events (gd_set_kernel_timing 2)" if stage_ev and stage_ev[0] else "per-kernel events, summed",
         "impl_bytes_per_message": round(st_b / max(1, n), 2), "contract_bytes_per_message": 12,
         "frac_impl": round(st_b / (st_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4) if st_ms > 0 else None,
         "frac_contract": round(12.0 * n / (st_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4) if st_ms > 0 else None}
@@ -784,13 +790,16 @@ def profile_kernels(e, router, keys, n_act, stream, steps: int) -> dict:
     the library (gd_set_kernel_timing; events inside the timed region would perturb it)."""
     if steps <= 0:
         return {}
-    e.set_kernel_timing(True)
-    e.kernel_times_reset()
-    with torch.cuda.stream(stream):
-        for _ in range(steps):
-            router.route_bucket(keys, n_act)
-    torch.cuda.synchronize()
-    kt = e.kernel_times()
+    kt = {}
+    for mode in (1, 2):            # every launch, then the stages alone ("stage:bucket")
+        e.set_kernel_timing(mode)
+        e.kernel_times_reset()
+        with torch.cuda.stream(stream):
+            for _ in range(steps):
+                router.route_bucket(keys, n_act)
+        torch.cuda.synchronize()
+        t = e.kernel_times()
+        kt.update(t if mode == 1 else {k: v for k, v in t.items() if k.startswith("stage:")})
     e.set_kernel_timing(False)
     return kt
 
@@ -1192,12 +1201,15 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
     if profile_steps > 0:
         hop_acts = ([f["act"] for f in runner.fetch(hops)] if isinstance(runner, LibraryCascade)
                     else [None for _ in hops])
-        e.set_kernel_timing(True)
-        e.kernel_times_reset()
-        for _ in range(profile_steps):
-            step()
-        torch.cuda.synchronize()
-        kt = e.kernel_times()
+        kt = {}
+        for mode in (1, 2):        # every launch, then the stages alone ("stage:bucket")
+            e.set_kernel_timing(mode)
+            e.kernel_times_reset()
+            for _ in range(profile_steps):
+                step()
+            torch.cuda.synchronize()
+            t = e.kernel_times()
+            kt.update(t if mode == 1 else {k: v for k, v in t.items() if k.startswith("stage:")})
         e.set_kernel_timing(False)
         msgs_step = sum(hop_msgs)
 

@@ -871,7 +871,9 @@ typedef struct gd_kernel_time {
 } gd_kernel_time;
 int gd_kernel_times(gd_handle* h, gd_kernel_time* out, uint32_t max, uint32_t* out_n);
 int gd_kernel_times_reset(gd_handle* h);
-int gd_set_kernel_timing(gd_handle* h, int enable);
+int gd_set_kernel_timing(gd_handle* h, int enable);   /* 0 off, 1 every launch, 2 stages only
+                                                         ("stage:bucket": one event pair around each
+                                                         bucketing, none between its kernels) */
 
 /* ---- handle options (no reference counterpart: the reference has no device kernels) ------------
  * Round 4 replaces the library's GD_* environment switches: a host's behaviour no longer depends on

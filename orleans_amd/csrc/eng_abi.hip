@@ -38,7 +38,7 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     if (!h) return set_err(nullptr, GD_ENOMEM, "gd_create: out of host memory");
     h->cfg = *cfg;
     h->device = cfg->device;
-    h->timing = (cfg->flags & GD_CFG_KERNEL_TIMING) != 0;
+    h->timing = (cfg->flags & GD_CFG_KERNEL_TIMING) != 0 ? 1 : 0;
     h->lane_order_forced_off = (cfg->flags & GD_CFG_NO_LANE_ORDER) != 0;
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) {
@@ -573,8 +573,9 @@ int gd_kernel_times(gd_handle* h, gd_kernel_time* out, uint32_t max, uint32_t* o
 
 int gd_set_kernel_timing(gd_handle* h, int enable) {
     if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    if (enable < 0 || enable > 2) return set_err(h, GD_EINVAL, "gd_set_kernel_timing: %d (0 off, 1 launches, 2 stages)", enable);
     GD_TRY(resolve_timing(h));
-    h->timing = enable != 0;
+    h->timing = enable;
     return GD_OK;
 }
 
@@ -924,8 +925,8 @@ int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
         if (g.first == n) exec = g.second;
     if (!exec) {
         // no allocation happens inside mb_enqueue (route needs no scratch), so capture directly
-        const bool timing = h->timing;
-        h->timing = false;
+        const int timing = h->timing;
+        h->timing = 0;
         hipGraph_t graph = nullptr;
         const uint64_t routed = h->routed;       // counted per replay below, not at capture
         HIP_TRY(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));

@@ -826,6 +826,7 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
 int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                   uint32_t* rank_out) {
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    StageTime stage(h, "stage:bucket");
     uint32_t a3 = 0, ra3 = 0;
     const bool one = (n_act >> MSD_SHIFT) + 1 <= MSD_MAX_RANGES;
     const bool three = !one && msd3_split(n_act, &a3, &ra3);

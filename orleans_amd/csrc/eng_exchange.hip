@@ -119,7 +119,7 @@ int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uin
                    const uint64_t* roff, const Lane* lanes, int n_lanes) {
     const Rccl& R = *h->net;
     hipEvent_t a = nullptr, b = nullptr;
-    if (h->timing) {
+    if (h->timing == 1) {
         a = take_event(h);
         b = take_event(h);
         HIP_TRY(h, hipEventRecord(a, h->stream));
@@ -148,7 +148,7 @@ int exchange_round(gd_handle* h, const char* name, const uint32_t* sc, const uin
         }
     }
     NCCL_TRY(h, R.GroupEnd());
-    if (h->timing) {
+    if (h->timing == 1) {
         HIP_TRY(h, hipEventRecord(b, h->stream));
         h->pending.push_back(TimedLaunch{name_id(h, name), a, b});
     }

@@ -233,7 +233,7 @@ struct gd_handle {
     size_t h_pin_bytes = 0;
 
     // per-kernel timing
-    bool timing = false;
+    int timing = 0;             // gd_set_kernel_timing: 0 off, 1 every launch, 2 the stages (StageTime) only
     std::vector<std::string> tnames;
     std::vector<double> tms;
     std::vector<uint64_t> tcount;
@@ -414,19 +414,40 @@ int launch(gd_handle* h, const char* name, dim3 grid, dim3 block, size_t lds, K 
     if (grid.x == 0) return GD_OK;
     if ((writes_table(h, args) || ...)) h->tab_gen++;
     hipEvent_t a = nullptr, b = nullptr;
-    if (h->timing) {
+    if (h->timing == 1) {
         a = take_event(h);
         b = take_event(h);
         HIP_TRY(h, hipEventRecord(a, h->stream));
     }
     hipLaunchKernelGGL(kernel, grid, block, lds, h->stream, args...);
     HIP_TRY(h, hipGetLastError());
-    if (h->timing) {
+    if (h->timing == 1) {
         HIP_TRY(h, hipEventRecord(b, h->stream));
         h->pending.push_back(TimedLaunch{name_id(h, name), a, b});
     }
     return GD_OK;
 }
+
+// Stage timing (gd_set_kernel_timing 2): one event pair around a whole stage -- e.g. every launch of a
+// bucketing -- recorded under `name`, with no events between its kernels (per-launch events add ~5 us a
+// kernel and so inflate a many-kernel stage).
+struct StageTime {
+    gd_handle* h;
+    int name = -1;
+    hipEvent_t a = nullptr, b = nullptr;
+    StageTime(gd_handle* hh, const char* nm) : h(hh) {
+        if (h->timing != 2) return;
+        name = name_id(h, nm);
+        a = take_event(h);
+        b = take_event(h);
+        (void)hipEventRecord(a, h->stream);
+    }
+    ~StageTime() {
+        if (name < 0) return;
+        (void)hipEventRecord(b, h->stream);
+        h->pending.push_back(TimedLaunch{name, a, b});
+    }
+};
 
 // Brackets a launch chosen by cx_choose / tune_choose with the tune entry's events.
 struct CxMeasure {

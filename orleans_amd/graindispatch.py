@@ -1261,8 +1261,9 @@ class GrainDispatch:
         self._c(lib.gd_kernel_times(self.h, arr, 64, C.byref(n)))
         return {arr[i].name.decode(): (int(arr[i].launches), float(arr[i].total_ms)) for i in range(min(n.value, 64))}
 
-    def set_kernel_timing(self, enable: bool):
-        self._c(lib.gd_set_kernel_timing(self.h, 1 if enable else 0))
+    def set_kernel_timing(self, enable):
+        """False / True: off / every launch; 2: the stages only ("stage:bucket")."""
+        self._c(lib.gd_set_kernel_timing(self.h, 2 if enable == 2 else (1 if enable else 0)))
 
     def kernel_times_reset(self):
         self._c(lib.gd_kernel_times_reset(self.h))

@@ -181,6 +181,28 @@ def test_msd_three_pass_kernels(gd):
     e.close()
 
 
+def test_stage_timing_brackets_the_whole_bucketing(gd):
+    """gd_set_kernel_timing 2: one event pair a bucketing ("stage:bucket"), no per-launch events; the
+    stage takes no longer than the per-launch sum (which pays an event pair a kernel)."""
+    acts = _acts(1 << 21, 5_000_000, "zipf", 19)
+    e = _engine(gd, "2")
+    e.bucket(acts, 5_000_000)                                    # scratch allocated outside the timing
+    e.set_kernel_timing(2)
+    e.kernel_times_reset()
+    for _ in range(3):
+        e.bucket(acts, 5_000_000)
+    t = {k: v for k, v in e.kernel_times().items() if v[0]}
+    assert set(t) == {"stage:bucket"} and t["stage:bucket"][0] == 3, t
+    e.set_kernel_timing(True)
+    e.kernel_times_reset()
+    for _ in range(3):
+        e.bucket(acts, 5_000_000)
+    k = {n: v for n, v in e.kernel_times().items() if v[0]}
+    assert "stage:bucket" not in k and "k_seg_scatter" in k
+    assert t["stage:bucket"][1] <= 1.05 * sum(v[1] for v in k.values())
+    e.close()
+
+
 def test_msd_measured_choice_and_fused_route(gd):
     """GD_OPT_BUCKET 1 (the default): the first launches of a batch size alternate the two forms; every
     result along the way is the stable partition."""
