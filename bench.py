@@ -287,7 +287,7 @@ def setup_workload(args, workload, world, rank, local, dev, tcd, msgs, grains):
     pin_choices(e, args, workload)
     silos = SILO_SETS[args.silos]
     pts, own = e.ring_set_silos(args.mode, silos)
-    engine = DeviceEngine(e, dev)
+    engine = DeviceEngine(e, dev, pipeline=args.pipeline and world == 1)
     stream = engine.stream
     counts = torch.zeros(world, dtype=torch.int64, device=dev)
     n_act = 0
@@ -435,6 +435,9 @@ def timed_steps(router, keys, n_act, stream, steps, warmup, settle=SETTLE_STEPS,
         res = None
         for _ in range(steps):
             res = router.route_bucket(keys, n_act)
+        bstream = getattr(getattr(router, "engine", None), "bstream", None)
+        if bstream is not None:
+            stream.wait_stream(bstream)   # the last batch's bucketing ran on the bucket stream
         ev1.record(stream)
         torch.cuda.synchronize()
         # this rank's K steps end when its device is done; the closing barrier aligns the ranks and the
@@ -622,6 +625,9 @@ def main():
                     help="where the full record (every kernel table) is written; the printed line is its summary")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="a handle option for every handle (graindispatch.OPTIONS: GD_OPT_*), e.g. bucket=2")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="N=1: each batch's bucketing on a second stream (gd_set_bucket_stream), overlapping the "
+                         "next batch's route")
     ap.add_argument("--tune", default="measured", choices=["measured", "pinned"],
                     help="measured: the library times its variants on the first launches (settle steps, then "
                          "gd_tune_agree across ranks at N > 1); pinned: the variants fixed up front "
@@ -757,7 +763,8 @@ def main():
                        "silos": silos_note(args.silos),
                        "owner_share_max": w["owner_share_max"],
                        "owner_share_max_by_silo_set": w["owner_share_by_set"],
-                       "table_load": round(n_act / cap, 3), "parallelism": f"shard{world}"},
+                       "table_load": round(n_act / cap, 3), "parallelism": f"shard{world}",
+                       "batch_pipeline": bool(w["engine"].bstream is not None)},
             "routed_ok_last_step_rank0": st_ok,
             "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
             "exchange": exchange,

@@ -284,6 +284,13 @@ int gd_bucket_device(gd_handle* h, const uint32_t* d_acts, uint32_t n, uint32_t 
 int gd_route_bucket_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act,
                            uint32_t* d_silo, uint32_t* d_act, uint8_t* d_status,
                            uint32_t* d_perm, uint32_t* d_offsets);
+/* Pipelining of batches (no reference counterpart): with a bucket stream set (non-NULL, not the handle's
+ * stream), gd_route_bucket_device enqueues the route on the handle's stream and the bucketing on the
+ * bucket stream after it (an event), without making the handle's stream wait: the next batch's route
+ * overlaps this batch's bucketing.  The caller must not reuse a batch's act / perm / offsets before the
+ * bucket stream has passed them (an event on it, or gd_synchronize, which waits for both streams).
+ * NULL restores the default (everything on the handle's stream).  Synchronizes the handle. */
+int gd_set_bucket_stream(gd_handle* h, void* hip_stream);
 int gd_ring_owner_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t* d_silo);
 
 /* ---- multi-GPU helpers (directory sharded by ring owner, SURVEY 8 e) ------------ */

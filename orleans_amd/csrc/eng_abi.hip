@@ -88,6 +88,8 @@ void gd_destroy(gd_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->bstream) (void)hipStreamSynchronize(h->bstream);
+    if (h->b_ev) (void)hipEventDestroy(h->b_ev);
     for (DevBuf* b : {&h->ring_pts, &h->ring_own, &h->keys_in, &h->u32_a, &h->u32_b, &h->u32_c, &h->u32_d, &h->u8_a,
                       &h->out_a, &h->out_b, &h->out_c, &h->hist, &h->partials, &h->partials2, &h->offs})
         free_buf(*b);
@@ -480,7 +482,26 @@ int gd_route_bucket_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint3
     if (!h || !d_offsets || (n && (!d_keys || !d_silo || !d_act || !d_status || !d_perm)))
         return set_err(h, GD_EINVAL, "null argument");
     if (n) GD_TRY(route_device(h, d_keys, n, d_silo, d_act, d_status));
-    return bucket_device(h, d_act, n, n_act, d_perm, d_offsets);
+    if (!h->bstream || h->bstream == h->stream) return bucket_device(h, d_act, n, n_act, d_perm, d_offsets);
+    // the bucketing on the bucket stream once this route is done; the handle's stream goes on to the
+    // next batch's route (gd_set_bucket_stream)
+    HIP_TRY(h, hipEventRecord(h->b_ev, h->stream));
+    HIP_TRY(h, hipStreamWaitEvent(h->bstream, h->b_ev, 0));
+    const hipStream_t main = h->stream;
+    h->stream = h->bstream;
+    const int r = bucket_device(h, d_act, n, n_act, d_perm, d_offsets);
+    h->stream = main;
+    return r;
+}
+
+int gd_set_bucket_stream(gd_handle* h, void* s) {
+    if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
+    HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(resolve_timing(h));
+    GD_TRY(sync(h));
+    if (s && !h->b_ev) HIP_TRY(h, hipEventCreateWithFlags(&h->b_ev, hipEventDisableTiming));
+    h->bstream = (hipStream_t)s;
+    return GD_OK;
 }
 
 int gd_route(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* out_silo, uint32_t* out_act, uint8_t* out_status) {

@@ -71,6 +71,7 @@ hipEvent_t take_event(gd_handle* h) {
 int resolve_timing(gd_handle* h) {
     if (h->pending.empty()) return GD_OK;
     HIP_TRY(h, hipStreamSynchronize(h->stream));
+    if (h->bstream) HIP_TRY(h, hipStreamSynchronize(h->bstream));
     if (h->xstream) HIP_TRY(h, hipStreamSynchronize(h->xstream));
     if (h->pstream) HIP_TRY(h, hipStreamSynchronize(h->pstream));
     for (auto& t : h->pending) {
@@ -826,6 +827,12 @@ int msd3_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, 
 int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                   uint32_t* rank_out) {
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
+    if (h->bstream && h->bstream != h->stream) {
+        // the bucketing scratch is the bucket stream's (gd_set_bucket_stream): a bucketing enqueued on
+        // another stream waits for it
+        HIP_TRY(h, hipEventRecord(h->b_ev, h->bstream));
+        HIP_TRY(h, hipStreamWaitEvent(h->stream, h->b_ev, 0));
+    }
     StageTime stage(h, "stage:bucket");
     uint32_t a3 = 0, ra3 = 0;
     const bool one = (n_act >> MSD_SHIFT) + 1 <= MSD_MAX_RANGES;
@@ -902,6 +909,7 @@ int bucket_lsd(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, u
 
 int sync(gd_handle* h) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
+    if (h->bstream && h->bstream != h->stream) HIP_TRY(h, hipStreamSynchronize(h->bstream));
     return GD_OK;
 }
 

@@ -141,6 +141,10 @@ struct gd_handle {
     const Rccl* net = nullptr;        // the transport behind comm: RCCL, or the in-process one
     int n_ranks = 0, rank = -1;
     hipStream_t xstream = nullptr;
+    // gd_set_bucket_stream: gd_route_bucket_device's bucketing on this stream after the route (event
+    // b_ev on the handle's stream), so the next batch's route overlaps this batch's bucketing
+    hipStream_t bstream = nullptr;
+    hipEvent_t b_ev = nullptr;
     hipStream_t pstream = nullptr;    // the partition (pack) of the next batch, beside this one's rounds
     hipEvent_t x_in = nullptr, x_hdr[2] = {}, x_route[2] = {}, x_ret[2] = {}, x_done[2] = {};
     hipEvent_t p_packed = nullptr, x_sent[2] = {}, x_fwd[2] = {}, x_keys[2] = {};

@@ -31,7 +31,7 @@ RING_MODES = {"D": RING_DIRECTORY, "R": RING_CONSISTENT, "V": RING_VIRTUAL_BUCKE
 
 # C-ABI symbols the header declares (checked by tests/test_abi.py)
 EXPORTED_SYMBOLS = [
-    "gd_create", "gd_destroy", "gd_last_error", "gd_abi_version", "gd_set_stream", "gd_get_stream",
+    "gd_create", "gd_destroy", "gd_last_error", "gd_abi_version", "gd_set_stream", "gd_get_stream", "gd_set_bucket_stream",
     "gd_synchronize", "gd_stats_get", "gd_host_alloc", "gd_host_free", "gd_jenkins_hash_bytes",
     "gd_jenkins_hash_u64x3", "gd_uniform_hash",
     "gd_calculate_id_hash", "gd_silo_consistent_hash", "gd_silo_uniform_hashes", "gd_silo_compare",
@@ -208,6 +208,7 @@ def _load() -> C.CDLL:
         "gd_last_error": (C.c_char_p, [P]),
         "gd_abi_version": (C.c_int, []),
         "gd_set_stream": (C.c_int, [P, P]),
+        "gd_set_bucket_stream": (C.c_int, [P, P]),
         "gd_get_stream": (P, [P]),
         "gd_host_alloc": (C.c_int, [C.c_size_t, P]),
         "gd_host_free": (C.c_int, [P]),
@@ -490,6 +491,10 @@ class GrainDispatch:
     # -- stream ---------------------------------------------------------------
     def set_stream(self, hip_stream: Optional[int]):
         self._c(lib.gd_set_stream(self.h, C.c_void_p(hip_stream or 0)))
+
+    def set_bucket_stream(self, hip_stream: Optional[int]):
+        """gd_set_bucket_stream: route_bucket_device's bucketing on this stream, after the route."""
+        self._c(lib.gd_set_bucket_stream(self.h, C.c_void_p(hip_stream or 0)))
 
     def synchronize(self):
         self._c(lib.gd_synchronize(self.h))

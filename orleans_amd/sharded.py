@@ -42,7 +42,8 @@ class DeviceEngine:
     """libgraindispatch on this rank's GPU, driven through the *_device C-ABI
     entry points on the current torch stream."""
 
-    def __init__(self, dispatch: g.GrainDispatch, device: torch.device, stream: Optional[torch.cuda.Stream] = None):
+    def __init__(self, dispatch: g.GrainDispatch, device: torch.device, stream: Optional[torch.cuda.Stream] = None,
+                 pipeline: bool = False):
         self.gd = dispatch
         self.device = device
         # A dedicated (non-null) stream: torch's legacy default stream has handle 0,
@@ -50,6 +51,11 @@ class DeviceEngine:
         # their torch work under `with torch.cuda.stream(engine.stream)`.
         self.stream = stream or torch.cuda.Stream(device)
         self.gd.set_stream(self.stream.cuda_stream)
+        # pipeline: route_bucket's bucketing on a second stream (gd_set_bucket_stream), so batch i + 1's
+        # route overlaps batch i's bucketing; its outputs are recorded on that stream for the allocator
+        self.bstream = torch.cuda.Stream(device) if pipeline else None
+        if self.bstream is not None:
+            self.gd.set_bucket_stream(self.bstream.cuda_stream)
 
     def pack_by_shard(self, keys: torch.Tensor, n_shards: int):
         n = keys.shape[0]
@@ -96,7 +102,16 @@ class DeviceEngine:
         off = torch.empty(n_act + 2, dtype=torch.int32, device=dev)
         self.gd.route_bucket_device(keys.data_ptr(), n, n_act, silo.data_ptr(), act.data_ptr(), st.data_ptr(),
                                     perm.data_ptr(), off.data_ptr())
+        if self.bstream is not None:
+            for t in (act, perm, off):
+                t.record_stream(self.bstream)
         return st, silo, act, perm, off
+
+    def bucket_done_event(self):
+        """An event the caller's stream can wait on for the last route_bucket's buckets (pipeline mode)."""
+        ev = torch.cuda.Event()
+        ev.record(self.bstream if self.bstream is not None else self.stream)
+        return ev
 
 
 class ShardedRouter:
