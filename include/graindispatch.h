@@ -289,7 +289,9 @@ int gd_route_bucket_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint3
  * bucket stream after it (an event), without making the handle's stream wait: the next batch's route
  * overlaps this batch's bucketing.  The caller must not reuse a batch's act / perm / offsets before the
  * bucket stream has passed them (an event on it, or gd_synchronize, which waits for both streams).
- * NULL restores the default (everything on the handle's stream).  Synchronizes the handle. */
+ * NULL restores the default (everything on the handle's stream).  Synchronizes the handle.
+ * Measured on MI355X (profiles/r05_pipeline_ab.txt): route and bucketing contend for HBM and L2, and the
+ * overlap is slower than the serial order (BASELINE cfg 2 -4 %, cfg 3 -30 %); off by default. */
 int gd_set_bucket_stream(gd_handle* h, void* hip_stream);
 int gd_ring_owner_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t* d_silo);
 

@@ -90,6 +90,7 @@ void gd_destroy(gd_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->bstream) (void)hipStreamSynchronize(h->bstream);
     if (h->b_ev) (void)hipEventDestroy(h->b_ev);
+    if (h->fan_ev) (void)hipEventDestroy(h->fan_ev);
     for (DevBuf* b : {&h->ring_pts, &h->ring_own, &h->keys_in, &h->u32_a, &h->u32_b, &h->u32_c, &h->u32_d, &h->u8_a,
                       &h->out_a, &h->out_b, &h->out_c, &h->hist, &h->partials, &h->partials2, &h->offs})
         free_buf(*b);

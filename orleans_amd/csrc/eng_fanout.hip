@@ -69,56 +69,71 @@ int fan_args_ok(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint
     return GD_OK;
 }
 
-template <int MODE, bool CX>
-int fan_route_launch_cx(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier,
+// Tiles of 512 outputs below 1,024 tiles of 2,048 (a small hop -- cfg 4's first, 0.64M messages -- would
+// otherwise leave most CUs idle with 4 dependent probe rounds a thread).
+constexpr uint32_t FAN_SMALL_TILES = 1024;
+
+template <int MODE, bool CX, bool CX8, int IT>
+int fan_route_launch_it(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier,
                         uint32_t nf, uint32_t total, uint64_t tcd, uint32_t* target, uint32_t* sender, uint32_t* silo,
-                        uint32_t* act, uint8_t* status) {
-    const dim3 g(blocks_for(total, FAN_TILE)), b(BLOCK);
+                        uint32_t* act, uint8_t* status, const uint32_t* d_nf, bool dev_total) {
+    const dim3 g(blocks_for(total, BLOCK * IT)), b(BLOCK);
     const uint32_t* ends = (const uint32_t*)h->fan[0].p;
     const CxArgs cx = CX ? cx_args(h) : CxArgs{};
+    const Cx8Args cx8 = CX8 ? cx8_args(h) : Cx8Args{};
     // 2 outputs a thread in flight (1: 2.95 ms, 4: 3.03 ms against 2.87 ms a cfg 4 cascade,
     // profiles/r02_v1_fanout_cfg4_ilp_ab.jsonl)
-    return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2, CX>, row_off, dst, frontier, nf, ends,
-                  total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx, Cx8Args{});
+    return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2, CX, (int)CX_GROUP, CX8, IT>, row_off, dst,
+                  frontier, nf, ends, total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx, cx8,
+                  d_nf, (uint32_t)dev_total);
+}
+
+template <int MODE, bool CX, bool CX8>
+int fan_route_launch_cx(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier,
+                        uint32_t nf, uint32_t total, uint64_t tcd, uint32_t* target, uint32_t* sender, uint32_t* silo,
+                        uint32_t* act, uint8_t* status, const uint32_t* d_nf, bool dev_total) {
+    if (blocks_for(total, FAN_TILE) < FAN_SMALL_TILES)
+        return fan_route_launch_it<MODE, CX, CX8, 2>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo,
+                                                      act, status, d_nf, dev_total);
+    return fan_route_launch_it<MODE, CX, CX8, FAN_IT>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo,
+                                                       act, status, d_nf, dev_total);
 }
 
 template <int MODE>
 int fan_route_launch(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier, uint32_t nf,
                      uint32_t total, uint64_t tcd, uint32_t* target, uint32_t* sender, uint32_t* silo, uint32_t* act,
-                     uint8_t* status) {
+                     uint8_t* status, const uint32_t* d_nf, bool dev_total) {
     bool cx = false;
     GD_TRY(cx_ensure(h, &cx, total));
     int meas = -1;
     const int var = cx ? cx_choose(h, 2, total, &meas, h->cx8_ok ? 3 : 2) : 1;
-    cx = var == 0;
     CxMeasure m(h, meas, total);
-    if (var == 2) {                    // the 8-B index
-        const dim3 g(blocks_for(total, FAN_TILE)), b(BLOCK);
-        return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2, false, (int)CX_GROUP, true>, row_off,
-                      dst, frontier, nf, (const uint32_t*)h->fan[0].p, total, tcd, ring_args(h), table_args(h), target,
-                      sender, silo, act, status, CxArgs{}, cx8_args(h));
-    }
-    if (cx)
-        return fan_route_launch_cx<MODE, true>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo, act,
-                                               status);
-    return fan_route_launch_cx<MODE, false>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo, act,
-                                            status);
+    if (var == 2)                      // the 8-B index
+        return fan_route_launch_cx<MODE, false, true>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo,
+                                                      act, status, d_nf, dev_total);
+    if (var == 0)
+        return fan_route_launch_cx<MODE, true, false>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo,
+                                                      act, status, d_nf, dev_total);
+    return fan_route_launch_cx<MODE, false, false>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo, act,
+                                                   status, d_nf, dev_total);
 }
 
+// dev_total: `total` is the outputs' capacity and the hop's size is read on the device (k_fan_route); the
+// caller counts the messages routed once it knows them.
 int fan_route(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier, uint32_t nf,
               uint32_t total, uint64_t tcd, uint32_t* target, uint32_t* sender, uint32_t* silo, uint32_t* act,
-              uint8_t* status) {
-    h->routed += total;
+              uint8_t* status, const uint32_t* d_nf, bool dev_total) {
+    if (!dev_total) h->routed += total;
     switch (h->ring_mode) {
         case GD_RING_DIRECTORY:
             return fan_route_launch<GD_RING_DIRECTORY>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo,
-                                                       act, status);
+                                                       act, status, d_nf, dev_total);
         case GD_RING_CONSISTENT:
             return fan_route_launch<GD_RING_CONSISTENT>(h, row_off, dst, frontier, nf, total, tcd, target, sender, silo,
-                                                        act, status);
+                                                        act, status, d_nf, dev_total);
         default:
             return fan_route_launch<GD_RING_VIRTUAL_BUCKETS>(h, row_off, dst, frontier, nf, total, tcd, target, sender,
-                                                             silo, act, status);
+                                                             silo, act, status, d_nf, dev_total);
     }
 }
 
@@ -198,27 +213,21 @@ int frontier_next_dev(gd_handle* h, const uint32_t* offsets, uint32_t n_act, uin
                   (const uint32_t*)counts, nb, out, total);
 }
 
-// fan_count of a frontier whose length is on the device (*d_nf <= nf_max): the degree and scan grids
-// are sized for nf_max, and one read-back brings both the length and the total (instead of one for
-// each).  Past 16M rows it reads the length first and takes fan_count.
-int fan_count_dev(gd_handle* h, const uint32_t* row_off, uint32_t n_nodes, const uint32_t* frontier,
-                  const uint32_t* d_nf, uint32_t nf_max, uint32_t* nf, uint64_t* total) {
-    *nf = 0;
-    *total = 0;
-    if (nf_max == 0) return GD_OK;
+// Degrees + inclusive scan of a frontier (nf_max rows; with d_nf, *d_nf <= nf_max rows on the device)
+// into fan[0], then its tile sums and length copied to pinned memory behind h->fan_ev: fan_count_wait
+// reads them.  The degree and scan grids are sized for nf_max.  *nb = 0: past 16M rows (one read-back
+// cannot carry the tile sums), nothing enqueued -- fan_count_dev's slow path.
+int fan_count_post(gd_handle* h, const uint32_t* row_off, uint32_t n_nodes, const uint32_t* frontier,
+                   const uint32_t* d_nf, uint32_t nf_max, uint32_t* nb_out) {
+    *nb_out = 0;
     const uint32_t nb4 = blocks_for(nf_max, SCAN_TILE), nb16 = blocks_for(nf_max, 4 * SCAN_TILE);
-    if (!(nb4 <= 2048 || nb16 <= 4096)) {
-        GD_TRY(pinned_scratch(h, 4));
-        HIP_TRY(h, hipMemcpyAsync(h->h_pin, d_nf, 4, hipMemcpyDeviceToHost, h->stream));
-        GD_TRY(sync(h));
-        *nf = *(const uint32_t*)h->h_pin;
-        return fan_count(h, row_off, n_nodes, frontier, *nf, total);
-    }
+    if (nf_max == 0 || !(nb4 <= 2048 || nb16 <= 4096)) return GD_OK;
     const bool wide = nb4 > 2048;
     const uint32_t nb = wide ? nb16 : nb4;
     GD_TRY(ensure(h, h->fan[0], (size_t)nf_max * 4));
     GD_TRY(ensure(h, h->fan[1], (size_t)nb * 4));
     GD_TRY(pinned_scratch(h, ((size_t)nb + 1) * 4));
+    if (!h->fan_ev) HIP_TRY(h, hipEventCreateWithFlags(&h->fan_ev, hipEventDisableTiming));
     uint32_t* ends = (uint32_t*)h->fan[0].p;
     uint32_t* part = (uint32_t*)h->fan[1].p;
     if (wide) {
@@ -234,15 +243,42 @@ int fan_count_dev(gd_handle* h, const uint32_t* row_off, uint32_t n_nodes, const
     }
     uint32_t* pin = (uint32_t*)h->h_pin;
     HIP_TRY(h, hipMemcpyAsync(pin, part, (size_t)nb * 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(h, hipMemcpyAsync(pin + nb, d_nf, 4, hipMemcpyDeviceToHost, h->stream));
-    GD_TRY(sync(h));
+    if (d_nf) HIP_TRY(h, hipMemcpyAsync(pin + nb, d_nf, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipEventRecord(h->fan_ev, h->stream));
+    *nb_out = nb;
+    return GD_OK;
+}
+
+// Waits for fan_count_post's read-back only (work enqueued after it keeps running): the frontier's
+// length and the hop's u64 total.
+int fan_count_wait(gd_handle* h, uint32_t nb, const uint32_t* d_nf, uint32_t nf_max, uint32_t* nf, uint64_t* total) {
+    HIP_TRY(h, hipEventSynchronize(h->fan_ev));
+    const uint32_t* pin = (const uint32_t*)h->h_pin;
     uint64_t t = 0;
     for (uint32_t b = 0; b < nb; ++b) t += pin[b];
     if (t > 0xFFFFFFFFull)
         return set_err(h, GD_EINVAL, "fan-out of %llu messages exceeds 2^32 - 1", (unsigned long long)t);
-    *nf = pin[nb];
+    *nf = d_nf ? pin[nb] : nf_max;
     *total = t;
     return GD_OK;
+}
+
+// fan_count of a frontier whose length is on the device (*d_nf <= nf_max): one read-back brings both
+// the length and the total (instead of one for each).  Past 16M rows it reads the length first and
+// takes fan_count.
+int fan_count_dev(gd_handle* h, const uint32_t* row_off, uint32_t n_nodes, const uint32_t* frontier,
+                  const uint32_t* d_nf, uint32_t nf_max, uint32_t* nf, uint64_t* total) {
+    *nf = 0;
+    *total = 0;
+    if (nf_max == 0) return GD_OK;
+    uint32_t nb = 0;
+    GD_TRY(fan_count_post(h, row_off, n_nodes, frontier, d_nf, nf_max, &nb));
+    if (nb) return fan_count_wait(h, nb, d_nf, nf_max, nf, total);
+    GD_TRY(pinned_scratch(h, 4));
+    HIP_TRY(h, hipMemcpyAsync(h->h_pin, d_nf, 4, hipMemcpyDeviceToHost, h->stream));
+    GD_TRY(sync(h));
+    *nf = *(const uint32_t*)h->h_pin;
+    return fan_count(h, row_off, n_nodes, frontier, *nf, total);
 }
 
 // The whole single-GPU cascade in the library (gd_fanout_cascade_device): per hop the fused
@@ -254,7 +290,8 @@ int fanout_cascade(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, u
     GD_TRY(check_ring(h));
     if (n_act == 0xFFFFFFFFu) return set_err(h, GD_EINVAL, "n_act too large");
     const uint64_t tcd = grain_tcd(type_code);
-    GD_TRY(sync(h));                                   // the previous call's results may be in use
+    // no synchronisation with the previous cascade: its buffers are rewritten in stream order (ensure()
+    // synchronises before it frees one), so this cascade's first launches queue behind its last ones
     if (h->fm_hop.size() < hops) h->fm_hop.resize(hops);
     h->fm_res.assign(hops, gd_fanout_hop{});
     h->fm_n_act = n_act;
@@ -262,30 +299,47 @@ int fanout_cascade(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, u
     GD_TRY(ensure(h, S[5], (size_t)n_act + 16));
     uint8_t* visited = (uint8_t*)S[5].p;
     HIP_TRY(h, hipMemsetAsync(visited, 0, (size_t)n_act + 16, h->stream));
-    uint32_t nf = n_seeds;
     {
         std::array<DevBuf, 10>& H0 = h->fm_hop[0];
-        GD_TRY(ensure(h, H0[0], ((size_t)std::max(nf, n_act) + 4) * 4));
-        if (nf) {
-            HIP_TRY(h, hipMemcpyAsync(H0[0].p, seeds, (size_t)nf * 4, hipMemcpyDeviceToDevice, h->stream));
-            GD_TRY(launch(h, "k_mark_visited", dim3(blocks_for(nf, BLOCK)), dim3(BLOCK), 0, k_mark_visited,
-                          (const uint32_t*)H0[0].p, nf, n_act, visited));
+        GD_TRY(ensure(h, H0[0], ((size_t)std::max(n_seeds, n_act) + 4) * 4));
+        if (n_seeds) {
+            HIP_TRY(h, hipMemcpyAsync(H0[0].p, seeds, (size_t)n_seeds * 4, hipMemcpyDeviceToDevice, h->stream));
+            GD_TRY(launch(h, "k_mark_visited", dim3(blocks_for(n_seeds, BLOCK)), dim3(BLOCK), 0, k_mark_visited,
+                          (const uint32_t*)H0[0].p, n_seeds, n_act, visited));
         }
     }
-    uint64_t total = 0;
-    GD_TRY(fan_count(h, row_off, n_nodes, (const uint32_t*)h->fm_hop[0][0].p, nf, &total));
+    // Per hop: the degrees and their scan, the read-back of the hop's size behind an event, then -- when
+    // this hop's buffers (from an earlier cascade) can hold it -- k_fan_route at once, reading the size on
+    // the device, while the host waits for the read-back and then queues the bucketing behind it.  The
+    // first cascade of a shape, or a hop that outgrows its buffers, waits, sizes them and launches k_fan_route
+    // with the host's count.
+    const uint32_t* d_nf = nullptr;                    // the frontier's length on the device (hops > 0)
+    uint32_t nf_max = n_seeds, nb = 0;
+    GD_TRY(fan_count_post(h, row_off, n_nodes, (const uint32_t*)h->fm_hop[0][0].p, nullptr, nf_max, &nb));
     for (uint32_t hp = 0; hp < hops; ++hp) {
         std::array<DevBuf, 10>& H = h->fm_hop[hp];
         const uint32_t* frontier = (const uint32_t*)H[0].p;
+        uint64_t cap = ~0ull;                          // messages the hop's buffers hold
+        for (int b : {1, 2, 4, 5, 7}) cap = std::min<uint64_t>(cap, H[b].p && H[b].bytes >= 16 ? (H[b].bytes - 16) / 4 : 0);
+        cap = std::min<uint64_t>(cap, H[6].p && H[6].bytes >= 16 ? H[6].bytes - 16 : 0);
+        cap = std::min<uint64_t>(cap, 0xFFFFFFFFull);
+        const bool early = nb && cap && nf_max;
+        if (early)
+            GD_TRY(fan_route(h, row_off, dst, frontier, nf_max, (uint32_t)cap, tcd, (uint32_t*)H[1].p, (uint32_t*)H[2].p,
+                             (uint32_t*)H[4].p, (uint32_t*)H[5].p, (uint8_t*)H[6].p, d_nf, true));
+        uint32_t nf = 0;
+        uint64_t total = 0;
+        if (nb) GD_TRY(fan_count_wait(h, nb, d_nf, nf_max, &nf, &total));
+        else if (nf_max && d_nf) GD_TRY(fan_count_dev(h, row_off, n_nodes, frontier, d_nf, nf_max, &nf, &total));
+        else if (nf_max) {
+            nf = nf_max;
+            GD_TRY(fan_count(h, row_off, n_nodes, frontier, nf, &total));
+        }
         const uint32_t m = (uint32_t)total;
-        gd_fanout_hop& res = h->fm_res[hp];
-        res.n_frontier = nf;
-        res.frontier = frontier;
-        res.n_sent = total;
         const size_t m4 = (size_t)m * 4 + 16;
         const size_t want[10] = {0, m4, m4, 0, m4, m4, (size_t)m + 16, m4, ((size_t)n_act + 2) * 4, 0};
         for (int b = 1; b < 9; ++b)
-            if (want[b]) GD_TRY(ensure(h, H[b], want[b]));
+            if (want[b]) GD_TRY(ensure(h, H[b], want[b]));   // synchronises first if it reallocates
         uint32_t* target = (uint32_t*)H[1].p;
         uint32_t* sender = (uint32_t*)H[2].p;
         uint32_t* silo = (uint32_t*)H[4].p;
@@ -293,8 +347,13 @@ int fanout_cascade(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, u
         uint8_t* st = (uint8_t*)H[6].p;
         uint32_t* perm = (uint32_t*)H[7].p;
         uint32_t* offs = (uint32_t*)H[8].p;
-        if (m) GD_TRY(fan_route(h, row_off, dst, frontier, nf, m, tcd, target, sender, silo, act, st));
+        if (early && m <= cap) h->routed += m;
+        else if (m) GD_TRY(fan_route(h, row_off, dst, frontier, nf, m, tcd, target, sender, silo, act, st));
         GD_TRY(bucket_device(h, act, m, n_act, perm, offs));
+        gd_fanout_hop& res = h->fm_res[hp];
+        res.n_frontier = nf;
+        res.frontier = frontier;
+        res.n_sent = total;
         res.n_recv = m;
         res.target = target;
         res.sender = sender;
@@ -304,14 +363,14 @@ int fanout_cascade(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, u
         res.status = st;
         res.perm = perm;
         res.offsets = offs;
+        nb = 0;
         if (hp + 1 < hops) {
             std::array<DevBuf, 10>& N = h->fm_hop[hp + 1];
             GD_TRY(ensure(h, N[0], ((size_t)n_act + 4) * 4));
-            const uint32_t* d_nf = nullptr;
             GD_TRY(frontier_next_dev(h, offs, n_act, visited, (uint32_t*)N[0].p, &d_nf));
             // every new publisher received at least one of this hop's m messages: the scan's bound
-            GD_TRY(fan_count_dev(h, row_off, n_nodes, (const uint32_t*)N[0].p, d_nf, std::min(n_act, m), &nf,
-                                 &total));
+            nf_max = std::min(n_act, m);
+            GD_TRY(fan_count_post(h, row_off, n_nodes, (const uint32_t*)N[0].p, d_nf, nf_max, &nb));
         }
     }
     if (out) std::copy(h->fm_res.begin(), h->fm_res.end(), out);

@@ -145,6 +145,7 @@ struct gd_handle {
     // b_ev on the handle's stream), so the next batch's route overlaps this batch's bucketing
     hipStream_t bstream = nullptr;
     hipEvent_t b_ev = nullptr;
+    hipEvent_t fan_ev = nullptr;   // the cascade's per-hop size read-back (fan_count_post / fan_count_wait)
     hipStream_t pstream = nullptr;    // the partition (pack) of the next batch, beside this one's rounds
     hipEvent_t x_in = nullptr, x_hdr[2] = {}, x_route[2] = {}, x_ret[2] = {}, x_done[2] = {};
     hipEvent_t p_packed = nullptr, x_sent[2] = {}, x_fwd[2] = {}, x_keys[2] = {};
@@ -392,7 +393,7 @@ int fan_args_ok(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, uint
                 uint64_t* out_n);
 int fan_route(gd_handle* h, const uint32_t* row_off, const uint32_t* dst, const uint32_t* frontier, uint32_t nf,
               uint32_t total, uint64_t tcd, uint32_t* target, uint32_t* sender, uint32_t* silo, uint32_t* act,
-              uint8_t* status);
+              uint8_t* status, const uint32_t* d_nf = nullptr, bool dev_total = false);
 int cache_pull(gd_handle* h, CacheCounters* c);
 int cache_touch(gd_handle* h, uint32_t* hit, const uint32_t* cslot, uint32_t n);
 int split_emit(gd_handle* h, int move, gd_key* d_keys, gd_val* d_vals);

@@ -316,7 +316,11 @@ static __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __
 // Fused expansion + route.  out_target may be null.  ILP items of a thread at a time: their
 // follower-list reads, then their first directory probes, are in flight together (one dependent
 // chain per item otherwise).
-template <int MODE, int ILP, bool CX = false, int RG = (int)CX_GROUP, bool CX8 = false>
+// IT: rounds of BLOCK outputs a block (a tile of BLOCK * IT outputs; 2 for a small hop, whose 2048-output
+// tiles would leave most CUs idle).  d_nf / dev_total: the frontier's length on the device, and the
+// hop's total read from the inclusive scan (ends[nf - 1]) instead of the host -- `total` is then the
+// outputs' capacity and the grid is sized for it; blocks past the device total exit at once.
+template <int MODE, int ILP, bool CX = false, int RG = (int)CX_GROUP, bool CX8 = false, int IT = FAN_IT>
 static __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict__ row_off,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint32_t* __restrict__ frontier, uint32_t n_front,
@@ -326,18 +330,23 @@ static __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __re
                                                      uint32_t* __restrict__ out_sender,
                                                      uint32_t* __restrict__ out_silo, uint32_t* __restrict__ out_act,
                                                      uint8_t* __restrict__ out_status, CxArgs cx = CxArgs{},
-                                                     Cx8Args cx8 = Cx8Args{}) {
-    static_assert(FAN_IT % ILP == 0, "whole rounds");
+                                                     Cx8Args cx8 = Cx8Args{}, const uint32_t* __restrict__ d_nf = nullptr,
+                                                     uint32_t dev_total = 0) {
+    static_assert(IT % ILP == 0 && BLOCK * IT <= FAN_LDS_ITEMS, "whole rounds, staged items");
+    constexpr uint32_t TILE = BLOCK * IT;
+    if (d_nf) n_front = min(n_front, *d_nf);
+    if (dev_total) total = min(total, n_front ? ends[n_front - 1] : 0u);
+    const uint32_t p0 = blockIdx.x * TILE;
+    if (p0 >= total) return;                              // block-uniform, before any barrier
     __shared__ FanStage s;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
     stage_ring(ring, s_pts, s_own);
     const uint32_t max_probe = tab.ctr->max_probe;
-    const uint32_t p0 = blockIdx.x * FAN_TILE;
-    const uint32_t p1 = min(p0 + FAN_TILE, total);
+    const uint32_t p1 = min(p0 + TILE, total);
     fan_stage(s, row_off, frontier, n_front, ends, p0, p1);
-    for (int it0 = 0; it0 < FAN_IT; it0 += ILP) {
+    for (int it0 = 0; it0 < IT; it0 += ILP) {
         if (p0 + it0 * BLOCK >= p1) break;                 // block-uniform
         uint32_t j[ILP], sender[ILP], target[ILP], h[ILP];
         bool live[ILP];

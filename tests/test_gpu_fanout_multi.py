@@ -294,21 +294,63 @@ def test_library_cascade_equals_host_driven_cascade(gd):
     dev = torch.device("cuda", 0)
     eng = DeviceFanoutEngine(e, dev, TC)
     g = upload_graph(ro, dst, dev)
-    seeds = np.unique(np.random.default_rng(16).choice(reg, 700)).astype(np.uint32)
+    lc = LibraryCascade(eng, g, n)
+    u = lambda t: t.cpu().numpy().view(np.uint32)  # noqa: E731
+    rng = np.random.default_rng(16)
+    # the first cascade sizes the hop buffers; the repeat routes each hop before its size is read back
+    # (k_fan_route reading the size on the device); a larger seed set outgrows them, a smaller one fits
+    for rep, n_seeds in enumerate((700, 700, 2500, 90)):
+        seeds = np.unique(rng.choice(reg, n_seeds)).astype(np.uint32) if rep != 1 else seeds
+        t_seeds = torch.from_numpy(seeds.view(np.int32)).to(dev)
+        got = lc.fetch(lc.run(t_seeds, hops))
+        ref = FanoutCascade(eng, g, n).run(t_seeds, hops)
+        eng.synchronize()
+        if rep < 2:
+            assert sum(x["target"].size for x in got) > 100000
+        for h in range(hops):
+            np.testing.assert_array_equal(got[h]["frontier"], u(ref[h].frontier), err_msg=f"rep {rep} hop {h}")
+            for k in ("target", "sender", "silo", "act", "perm", "offsets"):
+                np.testing.assert_array_equal(got[h][k], u(getattr(ref[h], k)), err_msg=f"rep {rep} hop {h} {k}")
+            np.testing.assert_array_equal(got[h]["status"], ref[h].status.cpu().numpy())
+            assert (got[h]["src"] == 0).all()
+    e.close()
+
+
+def test_library_cascade_large_hops_repeat(gd):
+    """The in-library cascade at hop sizes past the small-tile bound (2,048-output tiles), run twice on
+    one handle (the repeat routes before the read-back), against the host-driven cascade."""
+    import torch
+    from orleans_amd.fanout import DeviceFanoutEngine, FanoutCascade, LibraryCascade, upload_graph
+    n, hops = 2_000_000, 3
+    silos = o.bench_silos(8)
+    ro, dst = power_law_graph(n, 10.0, seed=25, max_deg=1 << 16)
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 23, my_silo=0)
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+    keys = o.grain_keys(TC, np.arange(n))
+    e.register(keys, np.arange(n, dtype=np.uint32), e.ring_owner(keys))
+    del keys
+    dev = torch.device("cuda", 0)
+    eng = DeviceFanoutEngine(e, dev, TC)
+    g = upload_graph(ro, dst, dev)
+    seeds = np.random.default_rng(26).choice(n, size=1 << 14, replace=False).astype(np.uint32)
     t_seeds = torch.from_numpy(seeds.view(np.int32)).to(dev)
     lc = LibraryCascade(eng, g, n)
-    got = lc.fetch(lc.run(t_seeds, hops))
     ref = FanoutCascade(eng, g, n).run(t_seeds, hops)
     eng.synchronize()
-    u = lambda t: t.cpu().numpy().view(np.uint32)  # noqa: E731
-    assert sum(x["target"].size for x in got) > 100000
-    for h in range(hops):
-        np.testing.assert_array_equal(got[h]["frontier"], u(ref[h].frontier), err_msg=f"hop {h}")
-        for k in ("target", "sender", "silo", "act", "perm", "offsets"):
-            np.testing.assert_array_equal(got[h][k], u(getattr(ref[h], k)), err_msg=f"hop {h} {k}")
-        np.testing.assert_array_equal(got[h]["status"], ref[h].status.cpu().numpy())
-        assert (got[h]["src"] == 0).all()
+    assert max(int(r.target.shape[0]) for r in ref) > 4_000_000
+    for rep in range(2):
+        got = lc.fetch(lc.run(t_seeds, hops))
+        for h in range(hops):
+            assert got[h]["target"].size == int(ref[h].target.shape[0])
+            for k in ("frontier", "target", "sender", "silo", "act", "perm", "offsets"):
+                want = u32_np(getattr(ref[h], k))
+                assert np.array_equal(got[h][k], want), f"rep {rep} hop {h} {k}"
+            assert np.array_equal(got[h]["status"], ref[h].status.cpu().numpy())
     e.close()
+
+
+def u32_np(t):
+    return t.cpu().numpy().view(np.uint32)
 
 
 def test_cfg4_full_size_properties(gd):

@@ -13,4 +13,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     > "$OUT/trace.log" 2>&1 || { tail -20 "$OUT/trace.log"; exit 1; }
 cd "$ROOT" || exit 1
 KT=$(find "$OUT/t" -name '*kernel_trace.csv' | head -1)
-python3 tools/trace_gaps.py "$KT" k_route_m 2 > "$OUT/gaps.txt"
+python3 tools/trace_gaps.py "$KT" "${FIRST:-k_route_m}" 2 > "$OUT/gaps.txt"
