@@ -96,6 +96,23 @@ __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* a, uint32_t 
     return lo;
 }
 
+// The same by one wave (all 64 lanes call it): each round tests the last entry of 64 equal pieces of
+// [lo, hi) and keeps the piece holding the answer -- log64 dependent reads instead of log2 (4 instead
+// of 22 over a 5M-publisher frontier, the latency each block of k_fan_route waits before its first probe).
+__device__ __forceinline__ uint32_t wave_upper_bound_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t p) {
+    const uint32_t lane = threadIdx.x & (WAVE - 1);
+    while (hi - lo > (uint32_t)WAVE) {
+        const uint32_t step = (hi - lo + WAVE - 1) / WAVE;
+        const uint32_t i = lo + (lane + 1) * step - 1;
+        const uint32_t k = (uint32_t)__popcll(__ballot(i < hi && a[i] <= p));   // pieces wholly <= p: a prefix
+        const uint32_t nlo = lo + k * step;
+        hi = min(hi, nlo + step);
+        lo = nlo;
+    }
+    const uint32_t i = lo + lane;
+    return lo + (uint32_t)__popcll(__ballot(i < hi && a[i] <= p));
+}
+
 // Per-block staging of the publishers covering outputs [p0, p1): items [lo, lo + cnt).  When
 // cnt exceeds FAN_LDS_ITEMS (a long run of zero-follower publishers inside the range) nothing
 // is staged and fan_item searches global memory instead.
@@ -109,12 +126,14 @@ struct FanStage {
 __device__ __forceinline__ void fan_stage(FanStage& s, const uint32_t* __restrict__ row_off,
                                           const uint32_t* __restrict__ frontier, uint32_t n_front,
                                           const uint32_t* __restrict__ ends, uint32_t p0, uint32_t p1) {
-    if (threadIdx.x == 0) {
-        const uint32_t lo = upper_bound_u32(ends, 0, n_front, p0);
-        const uint32_t hi = upper_bound_u32(ends, lo, n_front, p1 - 1);
-        s.lo = lo;
-        s.cnt = hi - lo + 1;
+    // wave 0 finds the first item, wave 1 the last, in parallel
+    if (threadIdx.x < 2 * WAVE) {
+        const uint32_t r = wave_upper_bound_u32(ends, 0, n_front, threadIdx.x < WAVE ? p0 : p1 - 1);
+        if (threadIdx.x == 0) s.lo = r;
+        if (threadIdx.x == WAVE) s.cnt = r;
     }
+    __syncthreads();
+    if (threadIdx.x == 0) s.cnt = s.cnt - s.lo + 1;
     __syncthreads();
     const uint32_t lo = s.lo, cnt = s.cnt;
     if (cnt <= FAN_LDS_ITEMS) {
