@@ -177,14 +177,16 @@ def load_pmc_entry(tag: str, kernel: str):
         return json.load(f)
 
 
-def roofline_of(kt: dict, steps: int, n: int, n_act: int, acts, tag, world: int = 1, bytes_fn=None):
+def roofline_of(kt: dict, steps: int, n: int, n_act: int, acts, tag, world: int = 1, bytes_fn=None,
+                nonstage=None):
     """(kernels, roofline) from in-library HIP-event kernel times kt {name: (launches, ms)} over `steps`
     steps of one workload: per kernel its algorithmic GB/s and fraction of HBM peak; the dominant
     kernel's roofline with its PMC traffic (profiles/pmc_*.json at this workload, N = 1) and the ratio
     of that traffic to the algorithmic bytes; the bucketing kernels (the MSD scatter and the level-2
     range sort, or the LSD scatter) on their implementation bytes -- `frac` -- with SURVEY 8(d)'s
     16 B/record/pass model beside them; and the whole bucketing stage against the 12-B contract.
-    bytes_fn(name, form): a kernel's bytes a step when a step is not one batch (the cfg 4 cascade)."""
+    bytes_fn(name, form): a kernel's bytes a step when a step is not one batch (the cfg 4 cascade);
+    nonstage: {name: bytes a step} of those launched outside the bucketing (cfg 4's degree scans)."""
     kt = dict(kt)
     stage_ev = kt.pop("stage:bucket", None)       # one event pair around each whole bucketing (timing 2)
     form = bucket_form(kt)
@@ -251,7 +253,7 @@ def roofline_of(kt: dict, steps: int, n: int, n_act: int, acts, tag, world: int 
     # the stage's time: events around the whole bucketing (no events between its kernels, which add
     # ~5 us a launch to the per-kernel sum), else the per-kernel sum
     st_ms = stage_ev[1] / steps if stage_ev and stage_ev[0] else sum_ms
-    st_b = sum(kernels[k]["alg_bytes_per_step"] or 0.0 for k in stage)
+    st_b = sum((kernels[k]["alg_bytes_per_step"] or 0.0) - (nonstage or {}).get(k, 0.0) for k in stage)
     roofline["bucketing_stage"] = {
         "form": form, "kernels": stage, "ms_per_step": round(st_ms, 4), "kernel_sum_ms_per_step": round(sum_ms, 4),
         "timing": "stage events (gd_set_kernel_timing 2)" if stage_ev and stage_ev[0] else "per-kernel events, summed",
@@ -1220,14 +1222,20 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
         e.set_kernel_timing(False)
         msgs_step = sum(hop_msgs)
 
+        fan_scan = {"k_fan_degree": 16.0 * sum(hop_front), "k_scan_down": 8.0 * sum(hop_front)}
+
         def cfg4_bytes(name, _form):
             if name in ("k_fan_route", "k_route_nodes", "k_fan_expand"):
                 return fan_kernel_bytes(name, msgs_step, sum(hop_front), not args.no_target)
+            # each hop's publishers: their degrees (frontier 4 B, two row offsets 8 B, the degree 4 B),
+            # then the degrees' inclusive scan (read + write 8 B); the grids cover the frontier's bound
+            # (min(n_act, the previous hop's messages)), the bytes count the publishers
+            fan = fan_scan.get(name, 0.0)
             # the bucketing kernels: each hop's batch in the form the library keeps for its shape
-            return float(sum(bucket_bytes(hop_form(e, m, n_act), m, n_act, a).get(name, 0.0)
-                             for m, a in zip(hop_msgs, hop_acts) if m))
+            return fan + float(sum(bucket_bytes(hop_form(e, m, n_act), m, n_act, a).get(name, 0.0)
+                                   for m, a in zip(hop_msgs, hop_acts) if m))
         kernels, roofline = roofline_of(kt, profile_steps, msgs_step, n_act, None, "cfg4", world,
-                                        bytes_fn=cfg4_bytes)
+                                        bytes_fn=cfg4_bytes, nonstage=fan_scan)
         if roofline:
             roofline["hop_bucket_forms"] = [hop_form(e, m, n_act) for m in hop_msgs]
             if roofline.get("kernel") == "k_fan_route" and world == 1:
