@@ -2,7 +2,8 @@
 the tail of stdout; round 4's 21.5-KB line with every kernel table inline went unparsed), and it keeps
 the contract's fields -- metric, value, ms_per_step, steps, warmup, config, dtype, a roofline with
 bound / kernel / achieved / peak / frac / traffic, cpu_baseline with value / cores / kind / sample --
-plus the compact secondary summaries.  Checked on the committed full records of rounds 3 and 4."""
+plus the compact secondary summaries.  Checked on the committed full records of rounds 3 to 5 and on
+the printed lines of the N = 2 / 8 one-GPU rehearsals."""
 import json
 import os
 import sys
@@ -19,7 +20,8 @@ def bench():
     return b
 
 
-RECORDS = ["profiles/r04_v8_bench.json", "profiles/r03_v8_bench.json", "profiles/r04_v7_bench.json"]
+RECORDS = ["profiles/r05_v8_bench_full.json", "profiles/r04_v8_bench.json", "profiles/r03_v8_bench.json",
+           "profiles/r04_v7_bench.json"]
 
 
 @pytest.mark.parametrize("path", RECORDS)
@@ -64,3 +66,15 @@ def test_line_cap_holds_for_oversized_records(bench):
             sec["kernels"][f"k_extra_{i}"] = dict(sec["kernels"][next(iter(sec["kernels"]))])
     text = json.dumps(bench.compact_line(full, "gpurun_out/bench_full.json"))
     assert len(text) <= bench.LINE_CAP, len(text)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_rehearsal_lines_parse_under_cap(bench, world):
+    """The lines `bench.py --gpus N --rehearse-one-gpu` printed through torchrun (round 5): the last
+    stdout line is one JSON object under the cap, for N GPUs."""
+    with open(os.path.join(ROOT, f"profiles/r05_rehearsal_w{world}_line.json")) as f:
+        text = f.read().strip().splitlines()[-1]
+    assert len(text) <= bench.LINE_CAP
+    line = json.loads(text)
+    assert line["n_gpus"] == world and line["rehearsal_one_gpu"] is True
+    assert line["value"] > 0 and "roofline" in line and "config" in line
