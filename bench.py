@@ -484,6 +484,7 @@ def compact_roofline(rf, kernels, with_table=True):
             out[k] = rf[k]
     if rf.get("random_probe_ceiling"):
         out["random_probe_ceiling_frac"] = rf["random_probe_ceiling"].get("frac_of_ceiling")
+        out["random_probe_io_ceiling_frac"] = rf["random_probe_ceiling"].get("frac_of_io_ceiling")
     if rf.get("probe_index"):
         out["probe_index_frac_impl"] = rf["probe_index"].get("frac_impl")
     st = rf.get("bucketing_stage")
@@ -839,15 +840,19 @@ def route_extras(roofline: dict, e, m_recv: int, tag: str, world: int):
 # 16M probes, 0.2567 ms; cfg 4: 2^25 slots (268 MB) at load 0.3, 43M probes, 0.8226 ms.  EA requests:
 # 1.0 64-B request a probe (TCC_EA0_RDREQ_32B_sum = 0: a 32-B read still moves 64 B).
 PROBE_CEILING_PER_MS = {"cfg2": 16777216 / 0.2567, "cfg4": 43000000 / 0.8226}
+# the same probe with k_route's own streams beside it (24-B keys in, silo / act / status out: g4io)
+PROBE_IO_CEILING_PER_MS = {"cfg2": 16777216 / 0.3186, "cfg4": 43000000 / 0.9481}
 
 
 def probe_ceiling(tag: str, probes: float, launch_ms: float):
-    rate = PROBE_CEILING_PER_MS.get(tag)
+    rate, rate_io = PROBE_CEILING_PER_MS.get(tag), PROBE_IO_CEILING_PER_MS.get(tag)
     if not rate or launch_ms <= 0:
         return None
-    ms = probes / rate
+    ms, ms_io = probes / rate, probes / rate_io
     return {"ms_per_launch": round(ms, 4), "frac_of_ceiling": round(ms / launch_ms, 3),
-            "source": "profiles/r05_ubench_fanprobe.txt (8-B index, random 64-B group reads)"}
+            "with_io_ms_per_launch": round(ms_io, 4), "frac_of_io_ceiling": round(ms_io / launch_ms, 3),
+            "source": "profiles/r05_ubench_fanprobe.txt, r05_ubench_probe_io_{21,25}.txt (8-B index, random 64-B "
+                      "group reads; g4io adds the route's 24-B key reads and 9-B result writes)"}
 
 
 # gd_tune_get variants of the 24-B-key / N1 probes (eng_core.hip cx_choose)

@@ -6,6 +6,8 @@
 //   g2    the first 32 B (2 x 16-B loads), the second half only when the first holds no hit or empty
 //   g1    16 B (2 slots) a round
 //   coop  4 lanes a probe, each one 16-B piece of the group (ballots pick the first hit / empty)
+//   g4io  g4 with k_route's streams: 24-B keys {0, key, tcd} in (3 x 8-B loads), silo / act / status out
+//         (4 + 4 + 1 B) -- the probe ceiling the route kernel can reach with its own I/O
 // Each form runs `reps` times between HIP events; rocprofv3 --pmc on this binary gives its EA requests.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/ubench_fanprobe tools/ubench_fanprobe.hip
 //   tools/ubench_fanprobe [slots_log2 = 25] [n_probes = 43000000] [load = 0.3]
@@ -47,6 +49,38 @@ __global__ void k_build(uint64_t* slots, uint64_t cap, const uint32_t* keys, uin
         if (atomicCAS((unsigned long long*)(slots + s), 0ull, v) == 0ull) return;
         s = s + 1 == cap ? 0 : s + 1;
     }
+}
+
+__global__ void __launch_bounds__(256) k_probe_io(const uint4* __restrict__ slots, uint64_t cap,
+                                                   const unsigned long long* __restrict__ keys24, uint32_t n,
+                                                   uint32_t* __restrict__ silo, uint32_t* __restrict__ act,
+                                                   uint8_t* __restrict__ status) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long n0 = keys24[3 * (size_t)i], n1 = keys24[3 * (size_t)i + 1],
+                             tcd = keys24[3 * (size_t)i + 2];
+    const uint32_t key = (uint32_t)n1 ^ (uint32_t)n0 ^ (uint32_t)(tcd >> 32) ^ (uint32_t)tcd;
+    uint64_t s = home(key, cap);
+    uint32_t val = 0;
+    for (int round = 0; round < 64; ++round) {
+        uint4 q[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) q[g] = slots[(s >> 1) + g];
+        bool done = false;
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            if (done) continue;
+            const uint32_t x = (g & 1) ? q[g / 2].z : q[g / 2].x, y = (g & 1) ? q[g / 2].w : q[g / 2].y;
+            if (y == 0) done = true;
+            else if (x == key) { val = y; done = true; }
+        }
+        if (done) break;
+        s += 8;
+        if (s >= cap) s = 0;
+    }
+    __builtin_nontemporal_store(val & 7u, silo + i);
+    act[i] = val;
+    __builtin_nontemporal_store((uint8_t)(val != 0), status + i);
 }
 
 template <int FORM>
@@ -171,6 +205,17 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d_probe, hp.data(), (size_t)n * 4, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_build, dim3((m + 255) / 256), dim3(256), 0, 0, d_slots, cap, d_keys, m);
     CK(hipDeviceSynchronize());
+    // the route's 24-B keys {0, key, 0}: key ^ 0 ^ 0 = key
+    std::vector<unsigned long long> hk24((size_t)n * 3, 0ull);
+    for (uint32_t i = 0; i < n; ++i) hk24[3 * (size_t)i + 1] = hp[i];
+    unsigned long long* d_k24;
+    uint32_t *d_silo, *d_act;
+    uint8_t* d_st;
+    CK(hipMalloc(&d_k24, (size_t)n * 24));
+    CK(hipMalloc(&d_silo, (size_t)n * 4));
+    CK(hipMalloc(&d_act, (size_t)n * 4));
+    CK(hipMalloc(&d_st, (size_t)n));
+    CK(hipMemcpy(d_k24, hk24.data(), (size_t)n * 24, hipMemcpyHostToDevice));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
@@ -203,6 +248,23 @@ int main(int argc, char** argv) {
             for (uint32_t i = 0; i < n; ++i) miss += ref[i].x == 0;
             printf("g4 misses: %zu\n", miss);
         }
+    }
+    for (int rep = 0; rep < 6; ++rep) {
+        CK(hipEventRecord(a));
+        hipLaunchKernelGGL(k_probe_io, dim3((n + 255) / 256), dim3(256), 0, 0, (const uint4*)d_slots, cap, d_k24, n, d_silo,
+                           d_act, d_st);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (rep >= 2) printf("g4io slots 2^%d load %.2f probes %u: %.4f ms (%.1f G probes/s)\n", lg, load, n, ms, n / ms / 1e6);
+    }
+    {
+        std::vector<uint32_t> ga(n);
+        CK(hipMemcpy(ga.data(), d_act, (size_t)n * 4, hipMemcpyDeviceToHost));
+        size_t bad = 0;
+        for (uint32_t i = 0; i < n; ++i) bad += ga[i] != ref[i].x;
+        printf("g4io mismatches vs g4: %zu\n", bad);
     }
     return 0;
 }
