@@ -296,8 +296,8 @@ __device__ __forceinline__ void st(T* p, T v) {
 // The route kernel proper: M messages per thread (coalesced: message
 // base + j*BLOCK + tid), all M first probes issued before any is inspected so
 // that each lane keeps M random 32-B slot reads in flight.  NT streams the key
-// reads and result writes non-temporally so they do not push the table out of
-// the caches it shares with them.
+// reads (and with NT_SIDE the silo / status writes) non-temporally so they do not
+// push the table out of the caches it shares with them.
 // N1W: 0 = 24-B keys; 8 / 4 = the keys arrive as N1 alone (u64 / u32 each; N0 = 0, TypeCodeData =
 // tcd_u for all), the forms a compact exchange header round delivers (k_key_desc, gd_shard.h).
 // The per-thread part: messages base + j * STRIDE, j < M; lds_act (optional) gets act too.
@@ -525,7 +525,7 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
         const uint32_t i = base + j * STRIDE;
         if (i < n) {
             st<NT || NT_SIDE>(out_silo + i, silo[j]);      // silo / status: not read again on the device
-            st<NT>(out_act + i, act[j]);                    // act: the bucketing's input, next
+            out_act[i] = act[j];                            // act: the bucketing's input, next (temporal)
             st<NT || NT_SIDE>(out_status + i, status[j]);
             if (lds_act) lds_act[(size_t)i * lds_stride] = act[j];
         }
