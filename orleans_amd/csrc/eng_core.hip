@@ -364,6 +364,9 @@ int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, u
                   (const uint32_t*)nullptr, 0u, (uint32_t*)nullptr, CxArgs{}, Cx8Args{});
 }
 
+// The probe index up to which the routes read their key stream non-temporally (route_mode).
+constexpr uint64_t ROUTE_NT_INDEX_BYTES = 64ull << 20;
+
 // Keys given as N1 alone (u64, or u32 with n1w = 4) with one TypeCodeData (a compact exchange
 // receive); not in cache mode.
 template <int MODE>
@@ -376,6 +379,17 @@ int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uin
     int meas = -1;
     const int var = cx ? cx_choose(h, 1, n, &meas, h->cx8_ok ? 4 : 3) : 1;
     CxMeasure m(h, meas, n);
+    // the N1 stream non-temporal under route_mode's rule (world-1 exchange pipeline: 0.5791 -> 0.5773 ms,
+    // profiles/r05_route_n1_nt_ab.txt)
+    const bool nt = (uint64_t)h->cx8_tab.bytes <= ROUTE_NT_INDEX_BYTES;
+    if (var == 3 && nt && n1w == 4)
+        return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, true, 4, false, (int)CX_GROUP, true>, k, n,
+                      ring_args(h), table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{},
+                      cx8_args(h));
+    if (var == 3 && nt)
+        return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, true, 8, false, (int)CX_GROUP, true>, k, n,
+                      ring_args(h), table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{},
+                      cx8_args(h));
     if (var == 3 && n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, false, 4, false, (int)CX_GROUP, true>, k, n,
                       ring_args(h), table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{},
@@ -456,7 +470,6 @@ int route_region_device(gd_handle* h, const void* k, uint32_t n1w, uint64_t tcd,
 // the index out of L2; past that (cfg 3's 2-GB index) temporal reads measured faster (k_route 0.882
 // against 0.905 ms; profiles/r05_route_nt_ab.txt).  act is stored temporally either way: the
 // bucketing's histogram reads it next.
-constexpr uint64_t ROUTE_NT_INDEX_BYTES = 64ull << 20;
 template <int MODE>
 int route_mode(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
     const uint64_t index_bytes = h->cx8_tab.p ? (uint64_t)h->cx8_tab.bytes : (uint64_t)h->capacity * 8u;
