@@ -631,10 +631,13 @@ def main():
     ap.add_argument("--pipeline", action="store_true",
                     help="N=1: each batch's bucketing on a second stream (gd_set_bucket_stream), overlapping the "
                          "next batch's route")
-    ap.add_argument("--tune", default="measured", choices=["measured", "pinned"],
-                    help="measured: the library times its variants on the first launches (settle steps, then "
-                         "gd_tune_agree across ranks at N > 1); pinned: the variants fixed up front "
-                         "(gd_tune_set: compact-index group reads, two-level bucketing), no settle steps")
+    ap.add_argument("--tune", default="pinned", choices=["measured", "pinned"],
+                    help="pinned (default): the variants each workload's measured runs settle on, fixed up front "
+                         "(gd_tune_set: the 8-B index's group reads, two-level bucketing), no settle steps, the "
+                         "same on every rank; measured: the library times its variants on the first launches "
+                         "(settle steps, then gd_tune_agree across ranks at N > 1) -- its timings are taken beside "
+                         "the exchange's overlapped work at N > 1 and can pick a slower probe there (world-1 "
+                         "library exchange: 29.1 measured against 31.0 G/s pinned, profiles/r05_tune_exchange_ab.txt)")
     args = ap.parse_args()
     for kv in args.opt:
         k, v = kv.split("=", 1)
@@ -728,7 +731,7 @@ def main():
     kt = profile_kernels(e, router, keys, n_act, stream, args.profile_steps)
     kernels, roofline = roofline_of(kt, max(1, args.profile_steps), m_recv, n_act, acts_np, args.workload, world)
     if roofline and roofline["kernel"] == "k_route":
-        route_extras(roofline, e, m_recv, args.workload, world)
+        route_extras(roofline, e, m_recv, args.workload, world, isinstance(router, LibraryRouter))
 
     # ---- BASELINE cfg 5: 4,096-message micro-batch latency on this directory ---------
     if world == 1 and args.workload == "cfg2" and args.latency_batches > 0:
@@ -791,7 +794,7 @@ def secondary_roofline(w, res, args, tag: str, world: int):
     kt = profile_kernels(w["e"], w["router"], w["keys"], w["n_act"], w["stream"], 3)
     k, rf = roofline_of(kt, 3, m, w["n_act"], acts, tag, world)
     if rf and rf["kernel"] == "k_route":
-        route_extras(rf, w["e"], m, tag, world)
+        route_extras(rf, w["e"], m, tag, world, isinstance(w["router"], LibraryRouter))
     return k, rf
 
 
@@ -814,11 +817,11 @@ def profile_kernels(e, router, keys, n_act, stream, steps: int) -> dict:
     return kt
 
 
-def route_extras(roofline: dict, e, m_recv: int, tag: str, world: int):
+def route_extras(roofline: dict, e, m_recv: int, tag: str, world: int, exchange: bool = False):
     """k_route's side fields: the probe variant the library runs (gd_tune_get) and, when it reads a
-    compact index (gd_cx.h), the index's own bytes a message.  (Round 1's random-probe "ceiling" was
-    measured for the 32-B slot table and does not bound the 8-B index probe: no longer reported.)"""
-    kind = "probe_keys" if world == 1 else "probe_n1"
+    compact index (gd_cx.h), the index's own bytes a message.  exchange: the probe reads the library
+    exchange's N1 headers (GD_TUNE_PROBE_N1), at any world size."""
+    kind = "probe_n1" if exchange or world > 1 else "probe_keys"
     v = e.tune_get(kind, m_recv)
     roofline["probe_variant"] = PROBE_VARIANTS.get(v, str(v))
     t_l = roofline["avg_launch_ms"] * 1e-3
