@@ -464,17 +464,18 @@ int route_region_device(gd_handle* h, const void* k, uint32_t n1w, uint64_t tcd,
     }
 }
 
-// One message a thread (2 measured no faster, profiles/r03_route_cx_ab.txt).  The 24-B key stream is
-// read non-temporally when the probed index is cache-sized (<= 64 MB of 8-B slots: BASELINE cfg 2's
-// 16-MB index, k_route 0.292 -> 0.285 ms, the step 0.415 -> 0.406 ms), so the stream does not push
-// the index out of L2; past that (cfg 3's 2-GB index) temporal reads measured faster (k_route 0.882
-// against 0.905 ms; profiles/r05_route_nt_ab.txt).  act is stored temporally either way: the
-// bucketing's histogram reads it next.
+// A cache-sized probe index (<= 64 MB of 8-B slots: BASELINE cfg 2's 16 MB): one message a thread (2
+// measured no faster, profiles/r03_route_cx_ab.txt) and the 24-B key stream read non-temporally, so it
+// does not push the index out of L2 (k_route 0.292 -> 0.285 ms, the step 0.415 -> 0.406 ms).  A larger
+// one (cfg 3's 2 GB, its Zipf-hot part in L2 and the MALL): temporal reads (0.882 against 0.905 ms
+// non-temporal; profiles/r05_route_nt_ab.txt) and two messages a thread, two dependent key -> probe
+// chains in flight (0.878 -> 0.863 ms; 4: 0.963; profiles/r05_route_m_ab.txt).  act is stored
+// temporally either way: the bucketing's histogram reads it next.
 template <int MODE>
 int route_mode(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
     const uint64_t index_bytes = h->cx8_tab.p ? (uint64_t)h->cx8_tab.bytes : (uint64_t)h->capacity * 8u;
     if (index_bytes <= ROUTE_NT_INDEX_BYTES) return route_launch<MODE, 1, true>(h, keys, n, silo, act, status);
-    return route_launch<MODE, 1, false>(h, keys, n, silo, act, status);
+    return route_launch<MODE, 2, false>(h, keys, n, silo, act, status);
 }
 
 

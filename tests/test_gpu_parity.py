@@ -939,3 +939,27 @@ def test_route_bucket_host_pipelined(gd, pinned, monkeypatch):
     e.close()
     for p in bufs:
         assert gd.lib.gd_host_free(p) == 0
+
+
+@pytest.mark.parametrize("cap", [1 << 21, 1 << 24])
+def test_route_index_size_forms_vs_oracle(gd, cap):
+    """k_route's two launch forms, picked by the probe index's size (eng_core.hip route_mode): a
+    cache-sized index (one message a thread, non-temporal key stream) and a large one (two messages a
+    thread), on a ragged batch with misses, system targets and N0 != 0 keys, against the oracle."""
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    G, N = 100_000, 1_000_003
+    e = _engine(gd, silos, "D", cap=cap)
+    reg = o.grain_keys(TC, np.arange(G))
+    owner = o.ring_owner_np(spec, o.jenkins_u64x3_np(reg[:, 2], reg[:, 0], reg[:, 1])).astype(np.uint32)
+    e.register(reg, np.arange(G), owner)
+    rng = np.random.default_rng(0x5EED0301)
+    keys = o.grain_keys(TC, rng.integers(0, G + G // 4, size=N))      # a fifth unregistered: misses
+    keys[::97, 0] = rng.integers(1, 1 << 40, size=keys[::97].shape[0], dtype=np.uint64)   # N0 != 0
+    st, silo, act = e.route(keys)
+    want = o.route_batch_np(keys, spec, o.DirectoryArrays(reg, np.arange(G), owner))
+    np.testing.assert_array_equal(st, want[0])
+    np.testing.assert_array_equal(silo, want[1])
+    np.testing.assert_array_equal(act, want[2])
+    assert (st == o.ST_OK).sum() > N // 2 and (st != o.ST_OK).sum() > N // 10
+    e.close()
