@@ -197,7 +197,13 @@ int cx_ensure(gd_handle* h, bool* ok, uint64_t n) {
     const bool fits = ab < 32 && (((uint64_t)c.silo_max + 1) >> (32 - ab)) == 0;
     h->cx8_ab = ab;
     if (h->cx_ok && c.flag8 == 0 && ntypes == 1 && fits) {
-        const unsigned long long cap8 = cap;           // as many 8-B slots as the 16-B index: half its bytes
+        // as many 8-B slots as the 16-B index (half its bytes).  Both neighbours measured slower: sized for
+        // the live entries at load 0.75, cfg 3's k_route 0.87 -> 1.13 ms (longer probe chains past a
+        // group's 8 slots), cfg 4 1.93 -> 1.95 ms a cascade; twice the slots, k_route 0.86 -> 1.53 ms at
+        // cfg 3 and 0.287 -> 0.314 at cfg 2 (a 4-GB index: the hot set over more lines and pages)
+        // (profiles/r05_cx8_load_ab.txt, r05_cx8_scale_ab.txt)
+        const unsigned long long cap8 = cap;
+        h->cx8_cap = cap8;
         GD_TRY(ensure(h, h->cx8_tab, cap8 * 8));
         HIP_TRY(h, hipMemsetAsync(h->cx8_tab.p, 0, cap8 * 8, h->stream));
         GD_TRY(launch(h, "k_cx8_build", g, b, 0, k_cx8_build, (const Slot*)h->slots, (unsigned long long)h->capacity,
@@ -330,7 +336,7 @@ int cx_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar) {
 
 
 Cx8Args cx8_args(gd_handle* h) {
-    return Cx8Args{(const uint4*)h->cx8_tab.p, h->capacity * h->cx_scale, h->cx8_tcd, h->cx8_rounds, h->cx8_ab};
+    return Cx8Args{(const uint4*)h->cx8_tab.p, h->cx8_cap, h->cx8_tcd, h->cx8_rounds, h->cx8_ab};
 }
 
 CxArgs cx_args(gd_handle* h) {
@@ -381,7 +387,7 @@ int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uin
     CxMeasure m(h, meas, n);
     // the N1 stream non-temporal under route_mode's rule (world-1 exchange pipeline: 0.5791 -> 0.5773 ms,
     // profiles/r05_route_n1_nt_ab.txt)
-    const bool nt = (uint64_t)h->cx8_tab.bytes <= ROUTE_NT_INDEX_BYTES;
+    const bool nt = (uint64_t)h->cx8_cap * 8u <= ROUTE_NT_INDEX_BYTES;
     if (var == 3 && nt && n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, true, 4, false, (int)CX_GROUP, true>, k, n,
                       ring_args(h), table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{},
@@ -473,7 +479,7 @@ int route_region_device(gd_handle* h, const void* k, uint32_t n1w, uint64_t tcd,
 // temporally either way: the bucketing's histogram reads it next.
 template <int MODE>
 int route_mode(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
-    const uint64_t index_bytes = h->cx8_tab.p ? (uint64_t)h->cx8_tab.bytes : (uint64_t)h->capacity * 8u;
+    const uint64_t index_bytes = h->cx8_tab.p ? (uint64_t)h->cx8_cap * 8u : (uint64_t)h->capacity * 8u;
     if (index_bytes <= ROUTE_NT_INDEX_BYTES) return route_launch<MODE, 1, true>(h, keys, n, silo, act, status);
     return route_launch<MODE, 2, false>(h, keys, n, silo, act, status);
 }

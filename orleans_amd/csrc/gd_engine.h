@@ -217,6 +217,7 @@ struct gd_handle {
     DevBuf cxi_tab, cxi_types, cxi_ctr;
     bool cx8_ok = false;        // the 8-B index (gd_cx.h k_cx8_build) is built and current with cx
     uint32_t cx8_rounds = 0, cx8_ab = 24;
+    unsigned long long cx8_cap = 0;   // the 8-B index's slots (cx_ensure: sized for the live entries)
     uint64_t cx8_tcd = 0;
     DevBuf cx8_tab;
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
