@@ -32,11 +32,14 @@ GATHER = ("k_route", "k_fan_route")
 
 
 def launch_name(inst: str) -> str:
-    """gd::k_msd_local_list<512, 16> -> k_msd_local_mid; gd::k_b2_scatter<...> -> k_radix_scatter."""
+    """gd::k_msd_local_list<512, 16> -> k_msd_local_mid; gd::k_b2_scatter<...> -> k_radix_scatter;
+    gd::k_route<MODE, false> (the ring owner alone, gd_ring_owner_device) -> k_ring_owner, not the probe."""
     s = inst.replace("void ", "").replace("gd::", "")
     base = s.split("<")[0]
     if base == "k_msd_local_list":
         return "k_msd_local_mid" if s.split("<")[1].startswith("512") else "k_msd_local"
+    if base == "k_route" and "<" in s and s.split("<")[1].split(">")[0].replace(" ", "").endswith(",false"):
+        return "k_ring_owner"
     return RENAME.get(base, base)
 
 
