@@ -635,9 +635,8 @@ def main():
                     help="pinned (default): the variants each workload's measured runs settle on, fixed up front "
                          "(gd_tune_set: the 8-B index's group reads, two-level bucketing), no settle steps, the "
                          "same on every rank; measured: the library times its variants on the first launches "
-                         "(settle steps, then gd_tune_agree across ranks at N > 1) -- its timings are taken beside "
-                         "the exchange's overlapped work at N > 1 and can pick a slower probe there (world-1 "
-                         "library exchange: 29.1 measured against 31.0 G/s pinned, profiles/r05_tune_exchange_ab.txt)")
+                         "(settle steps, then gd_tune_agree across ranks at N > 1; the exchange pipeline runs "
+                         "unoverlapped while it times, DESIGN 10)")
     args = ap.parse_args()
     for kv in args.opt:
         k, v = kv.split("=", 1)

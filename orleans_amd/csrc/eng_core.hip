@@ -320,6 +320,7 @@ int tune_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar, int sub
         if (!t.b[v]) (void)hipEventCreate(&t.b[v]);
         *meas = key * V + v;
         ++t.round;
+        h->measured_launch = true;
     }
     return v;
 }

@@ -290,10 +290,15 @@ int route_multi(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t n_act, 
         GD_TRY(grow(h, SB[3], (size_t)n * 4 + 4));
         GD_TRY(grow(h, SB[4], (size_t)n * 4 + 4));
     }
-    if (!(flags & GD_MULTI_KEYS_READY)) {
+    // the partition waits for the handle's stream when the caller's keys are not known complete, and while
+    // the previous batch's probe or bucketing was a timed launch of the measured choices (tune_choose): a
+    // variant timed beside the next batch's partition measured slower than it is (the N1 probe's 8-B index
+    // lost to the 16-B index's group reads there), so the first launches run unoverlapped
+    if (!(flags & GD_MULTI_KEYS_READY) || h->measured_launch) {
         HIP_TRY(h, hipEventRecord(h->x_in, h->stream));
         HIP_TRY(h, hipStreamWaitEvent(h->pstream, h->x_in, 0));
     }
+    h->measured_launch = false;
     if (h->x_sent_rec[s]) HIP_TRY(h, hipStreamWaitEvent(h->pstream, h->x_sent[s], 0));
     gd_key* send_keys = (gd_key*)SB[0].p;
     uint32_t* send_idx = (uint32_t*)SB[1].p;

@@ -148,6 +148,9 @@ struct gd_handle {
     hipEvent_t fan_ev = nullptr;   // the cascade's per-hop size read-back (fan_count_post / fan_count_wait)
     hipStream_t pstream = nullptr;    // the partition (pack) of the next batch, beside this one's rounds
     hipEvent_t x_in = nullptr, x_hdr[2] = {}, x_route[2] = {}, x_ret[2] = {}, x_done[2] = {};
+    // a launch timed for tune_choose was enqueued since the last exchange call: the next call's partition
+    // waits for it (route_multi), so the timings are not taken beside the pipeline's overlapped work
+    bool measured_launch = false;
     hipEvent_t p_packed = nullptr, x_sent[2] = {}, x_fwd[2] = {}, x_keys[2] = {};
     bool x_done_rec[2] = {false, false}, x_sent_rec[2] = {false, false};
     DevBuf mx_send[2][7];             // per batch parity: send keys, send idx, counts (send/recv messages,
