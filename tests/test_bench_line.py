@@ -78,3 +78,20 @@ def test_rehearsal_lines_parse_under_cap(bench, world):
     line = json.loads(text)
     assert line["n_gpus"] == world and line["rehearsal_one_gpu"] is True
     assert line["value"] > 0 and "roofline" in line and "config" in line
+
+
+def test_pmc_kernel_families():
+    """tools/pmc_traffic.py groups template instantiations by the name bench.py's kernel tables use:
+    the MSD scatter / histogram under the radix names, the list range sorts by their size, the probe
+    forms under k_route -- and the ring-owner kernel (k_route<MODE, false>, gd_ring_owner_device) apart
+    from them (round 5: averaged in, it had taken cfg 3's k_route bytes from 3.53 down to 2.87 GB)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_traffic as pt
+    assert pt.launch_name("gd::k_b2_scatter<512, 16, 1056, 1, false>") == "k_radix_scatter"
+    assert pt.launch_name("gd::k_b2_hist<512, 16, 4, 1056>") == "k_radix_hist"
+    assert pt.launch_name("gd::k_msd_local_list<512, 16, false>") == "k_msd_local_mid"
+    assert pt.launch_name("gd::k_msd_local_list<1024, 24, false>") == "k_msd_local"
+    assert pt.launch_name("gd::k_route_m<0, 2, false, 0, false, 4, true>") == "k_route"
+    assert pt.launch_name("gd::k_route<0, false>") == "k_ring_owner"
+    assert pt.launch_name("gd::k_route<2, true>") == "k_route"
+    assert pt.launch_name("gd::k_fan_degree_tiles<16>") == "k_fan_degree"
