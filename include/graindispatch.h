@@ -918,6 +918,9 @@ int gd_set_kernel_timing(gd_handle* h, int enable);   /* 0 off, 1 every launch, 
                                    than GD_OPT_L2_SMALL) sorted by 512-thread workgroups, three a CU, the rest
                                    of the staged class by 1,024-thread ones (default 8,192, the 512-thread
                                    capacity; 0 = every staged range on the 1,024-thread sort) */
+#define GD_OPT_B2_PERSIST   14  /* one-pass two-level form's MSD scatter: k = 1..8 persistent workgroups a
+                                   CU, each loading its next tile under the current tile's write-out
+                                   (default 2); 0 one workgroup a tile */
 int gd_option_set(gd_handle* h, int option, int64_t value);
 int gd_option_get(const gd_handle* h, int option, int64_t* value);
 

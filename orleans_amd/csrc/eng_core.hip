@@ -690,8 +690,22 @@ int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uin
                       R, tiles, hist, shift, hxr));
     const uint32_t* tot = hist + (size_t)R * tiles;
     GD_TRY(launch(h, "k_radix_rowscan", dim3(R), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R * tiles));
-    GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(B2_NT), 0, k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT, BALLOT>, acts, n,
-                  n_act, R, tiles, (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk));
+    // GD_OPT_B2_PERSIST k > 0, the one-pass form (KEY16): k persistent workgroups a CU (a multiple of 8 in
+    // all), each looping over its tiles with the next tile's loads under the current write-out.  cfg 2:
+    // k_radix_scatter 0.0626 -> 0.0597 ms at k = 2, 0.087 at k = 1; pass A of the three-pass form at cfg 3
+    // (Zipf, 8-K tiles) 0.173 -> 0.19 ms, so that pass keeps one workgroup a tile
+    // (profiles/r05_b2_persist_ab.txt).  The ballot ranks keep it too (their persistent form spills).
+    bool persisted = false;
+    if constexpr (KOUT == B2_KEY16 && !BALLOT) if (h->b2_persist) {
+        const uint32_t grid = std::min<uint32_t>(tiles, std::max<uint32_t>(8, (h->b2_persist * h->n_cu) & ~7u));
+        GD_TRY(launch(h, "k_radix_scatter", dim3(grid), dim3(B2_NT), 0,
+                      k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT, BALLOT, true>, acts, n, n_act, R, tiles,
+                      (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk));
+        persisted = true;
+    }
+    if (!persisted)
+        GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(B2_NT), 0, k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT, BALLOT>,
+                      acts, n, n_act, R, tiles, (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk));
     h->last_totals = tot;
     h->last_digits = R;
     return GD_OK;

@@ -101,9 +101,13 @@ struct B2Pack {
 
 // The MSD pass's scatter: keys_in = the activations (clamped here), writes the message index and the
 // key (B2Out form) in digit order of min(key, clamp) >> shift.  gscan: the row-scanned counts
-// (k_radix_rowscan), totals: the digit totals.
-template <int NT, int IT, int RMAX, int KOUT, bool BALLOT = false>
-static __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __restrict__ keys_in, uint32_t n, uint32_t clamp,
+// (k_radix_rowscan), totals: the digit totals.  PERSIST (with a grid smaller than the tile count): the
+// workgroups are persistent -- workgroup b takes virtual tiles b, b + grid, ... (grid a multiple of 8, so
+// every tile of a workgroup stays in its XCD's range of xcd_tile), the digit totals load once, and the
+// next tile's activations load under this tile's write-out (128 VGPRs: four waves a SIMD, two
+// workgroups a CU).  Without PERSIST one workgroup a tile, as compiled before the loop existed.
+template <int NT, int IT, int RMAX, int KOUT, bool BALLOT = false, bool PERSIST = false>
+static __global__ void __launch_bounds__(NT, 4) k_b2_scatter(const uint32_t* __restrict__ keys_in, uint32_t n, uint32_t clamp,
                                                    uint32_t R, uint32_t tiles, const uint32_t* __restrict__ gscan,
                                                    const uint32_t* __restrict__ totals,
                                                    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
@@ -119,22 +123,16 @@ static __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __rest
     __shared__ uint16_t s_val[TILE];                     // position in the tile
     __shared__ uint32_t s_wsum[2 * NW];
 
-    const uint32_t tile = xcd_tile(blockIdx.x, gridDim.x, xcd);
-    const uint32_t base = tile * TILE;
-    const uint32_t cnt_tile = min(TILE, n - base);
-    for (uint32_t d = threadIdx.x; d < RMAX; d += NT) {
-#pragma unroll
-        for (int p = 0; p < NW / 2; ++p) s_cnt[p][d] = 0;
-        s_gbase[d] = d < R ? gscan[(size_t)d * tiles + tile] : 0u;
-    }
     const uint32_t lane = lane_id();
     const uint32_t w = threadIdx.x / WAVE;
     const uint32_t half = (w & 1u) * 16u;
     const unsigned long long lt = (1ull << lane) - 1ull;
     uint32_t kk[IT], rk[IT];
+    uint32_t vb = blockIdx.x;
+    uint32_t tile = xcd_tile(vb, tiles, xcd);
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
-        const uint32_t idx = base + (w * IT + r) * WAVE + lane;
+        const uint32_t idx = tile * TILE + (w * IT + r) * WAVE + lane;
         kk[r] = __builtin_nontemporal_load(keys_in + min(idx, n - 1));
     }
     uint32_t tv[DPT], my_g = 0;
@@ -143,6 +141,25 @@ static __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __rest
         const uint32_t d = threadIdx.x * DPT + q;
         tv[q] = d < R ? totals[d] : 0u;
         my_g += tv[q];
+    }
+    for (;;) {
+    const uint32_t base = tile * TILE;
+    const uint32_t cnt_tile = min(TILE, n - base);
+    // this tile's row-scanned counts: one workgroup a tile keeps the thread's own digits' (the scan below
+    // owns d = threadIdx.x * DPT + q) in registers from here to after the ranking (cfg 2 0.0626 -> 0.0607
+    // ms); the persistent form, at its register limit, stages them through LDS
+    uint32_t gb[DPT];
+    if constexpr (!PERSIST) {
+#pragma unroll
+        for (uint32_t q = 0; q < DPT; ++q) {
+            const uint32_t d = threadIdx.x * DPT + q;
+            gb[q] = d < R ? gscan[(size_t)d * tiles + tile] : 0u;
+        }
+    }
+    for (uint32_t d = threadIdx.x; d < RMAX; d += NT) {
+#pragma unroll
+        for (int p = 0; p < NW / 2; ++p) s_cnt[p][d] = 0;
+        if constexpr (PERSIST) s_gbase[d] = d < R ? gscan[(size_t)d * tiles + tile] : 0u;
     }
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
@@ -198,7 +215,7 @@ static __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __rest
                 const uint32_t t = s_lstart[d];
 #pragma unroll
                 for (int p = 0; p < NW / 2; ++p) s_cnt[p][d] += run | (run << 16);
-                s_gbase[d] = s_gbase[d] + rung - run;
+                s_gbase[d] = (PERSIST ? s_gbase[d] : gb[q]) + rung - run;
                 run += t;
                 rung += tv[q];
             }
@@ -215,6 +232,21 @@ static __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __rest
         }
     }
     __syncthreads();
+    // the next tile's activations load under this tile's write-out
+    vb += gridDim.x;
+    const bool more = PERSIST && vb < tiles;
+    const uint32_t ntile = more ? xcd_tile(vb, tiles, xcd) : tile;
+    if (more) {
+#pragma unroll
+        for (int r = 0; r < IT; ++r) {
+            // a 32-bit byte offset from the uniform base (n < 2^30 on this path): one VGPR an address, not two
+            const uint32_t off = min(ntile * TILE + (w * IT + r) * WAVE + lane, n - 1) * 4u;
+            kk[r] = __builtin_nontemporal_load(
+                reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(keys_in) + off));
+        }
+    }
+    // (a branch-free write-out -- full tiles without the tail test, g clamped below n instead of tested --
+    // measured slower: cfg 2 0.0606 -> 0.063 ms, persistent 0.0589 -> 0.067)
 #pragma unroll 4
     for (int j = 0; j < IT; ++j) {
         const uint32_t p = j * NT + threadIdx.x;
@@ -236,6 +268,10 @@ static __global__ void __launch_bounds__(NT) k_b2_scatter(const uint32_t* __rest
                 }
             }
         }
+    }
+    if (!more) break;
+    tile = ntile;
+    __syncthreads();                      // s_key / s_val / s_gbase / s_cnt are the next tile's
     }
 }
 

@@ -129,6 +129,18 @@ def test_msd_ballot_ranks_vs_oracle(gd, n, n_act, kind):
         e.close()
 
 
+@pytest.mark.parametrize("persist", [0, 1, 3])
+@pytest.mark.parametrize("n,n_act,kind", [ONE_PASS[1], ONE_PASS[2], ONE_PASS[7], ONE_PASS[8]])
+def test_msd_persistent_scatter_vs_oracle(gd, persist, n, n_act, kind):
+    """GD_OPT_B2_PERSIST: the one-pass form's MSD scatter one workgroup a tile (0) or on k persistent
+    workgroups a CU, each looping over its XCD's tiles with the next tile's loads under the current
+    write-out (tiles past the grid, ragged last tiles, the unrouted bucket, hot digits); the default (2)
+    runs in every other one-pass test; the result never changes."""
+    e2, e0 = _check(gd, _acts(n, n_act, kind, n + n_act + 5), n_act, b2_persist=persist)
+    e2.close()
+    e0.close()
+
+
 @pytest.mark.parametrize("small", [0, 300, 24576])
 def test_msd_three_pass_class_threshold(gd, small):
     """The thin-range threshold moves ranges between the wave form and the workgroup form (0: every
