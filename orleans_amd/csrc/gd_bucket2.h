@@ -99,6 +99,23 @@ struct B2Pack {
     uint32_t pbits, hb, ib;
 };
 
+// One record of the MSD scatter's output at position g: the key in its B2Out form and the message index.
+template <int KOUT>
+__device__ __forceinline__ void b2_put(uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, uint32_t g,
+                                       uint32_t k, uint32_t idx, const B2Pack& pk) {
+    if constexpr (KOUT == B2_KEY16) {
+        reinterpret_cast<uint16_t*>(keys_out)[g] = (uint16_t)(k & ((1u << B2_LOW_BITS) - 1));
+        vals_out[g] = idx;
+    } else if constexpr (KOUT == B2_PACK) {
+        const uint32_t P = k & ((1u << pk.pbits) - 1u);
+        reinterpret_cast<uint16_t*>(keys_out)[g] = (uint16_t)(P >> pk.hb);
+        vals_out[g] = pk.hb ? idx | ((P & ((1u << pk.hb) - 1u)) << pk.ib) : idx;
+    } else {
+        keys_out[g] = k;
+        vals_out[g] = idx;
+    }
+}
+
 // The MSD pass's scatter: keys_in = the activations (clamped here), writes the message index and the
 // key (B2Out form) in digit order of min(key, clamp) >> shift.  gscan: the row-scanned counts
 // (k_radix_rowscan), totals: the digit totals.  PERSIST (with a grid smaller than the tile count): the
@@ -245,28 +262,42 @@ static __global__ void __launch_bounds__(NT, 4) k_b2_scatter(const uint32_t* __r
                 reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(keys_in) + off));
         }
     }
-    // (a branch-free write-out -- full tiles without the tail test, g clamped below n instead of tested --
-    // measured slower: cfg 2 0.0606 -> 0.063 ms, persistent 0.0589 -> 0.067)
+    // The write-out.  One workgroup a tile reads its LDS in batches of WB items -- every staged key, then
+    // every digit base, then the positions, then the stores -- rather than one item's two dependent reads
+    // and a wait at a time (branches around each item made the compiler serialise them; positions past
+    // the tile read in-bounds LDS and store nothing): cfg 3 pass A 0.168 -> 0.158 ms.  The persistent form
+    // (at its register limit) keeps one item at a time: batched it spilled and took 0.060 -> 0.067 ms
+    // (profiles/r05_writeout_batch_ab.txt).  A branch-free write-out (full tiles without the tail test,
+    // g clamped below n instead of tested) was slower for both (0.0606 -> 0.063, 0.0589 -> 0.067 ms).
+    if constexpr (PERSIST) {
 #pragma unroll 4
-    for (int j = 0; j < IT; ++j) {
-        const uint32_t p = j * NT + threadIdx.x;
-        if (p < cnt_tile) {
-            const uint32_t k = s_key[p];
-            const uint32_t g = s_gbase[k >> shift] + p;
-            if (g < n) {                  // always true when the counts are right; never write out of bounds
-                const uint32_t idx = base + (uint32_t)s_val[p];
-                if constexpr (KOUT == B2_KEY16) {
-                    reinterpret_cast<uint16_t*>(keys_out)[g] = (uint16_t)(k & ((1u << B2_LOW_BITS) - 1));
-                    vals_out[g] = idx;
-                } else if constexpr (KOUT == B2_PACK) {
-                    const uint32_t P = k & ((1u << pk.pbits) - 1u);
-                    reinterpret_cast<uint16_t*>(keys_out)[g] = (uint16_t)(P >> pk.hb);
-                    vals_out[g] = pk.hb ? idx | ((P & ((1u << pk.hb) - 1u)) << pk.ib) : idx;
-                } else {
-                    keys_out[g] = k;
-                    vals_out[g] = idx;
+        for (int j = 0; j < IT; ++j) {
+            const uint32_t p = j * NT + threadIdx.x;
+            if (p < cnt_tile) {
+                const uint32_t k = s_key[p];
+                const uint32_t g = s_gbase[k >> shift] + p;
+                if (g < n) {              // always true when the counts are right; never write out of bounds
+                    const uint32_t idx = base + (uint32_t)s_val[p];
+                    b2_put<KOUT>(keys_out, vals_out, g, k, idx, pk);
                 }
             }
+        }
+    } else {
+        constexpr int WB = 8;
+#pragma unroll
+        for (int j0 = 0; j0 < IT; j0 += WB) {
+            uint32_t kq[WB], gq[WB], vq[WB];
+#pragma unroll
+            for (int u = 0; u < WB; ++u) kq[u] = s_key[(j0 + u) * NT + threadIdx.x];
+#pragma unroll
+            for (int u = 0; u < WB; ++u)
+                gq[u] = s_gbase[min(kq[u] >> shift, (uint32_t)RMAX - 1u)] + (j0 + u) * NT + threadIdx.x;
+#pragma unroll
+            for (int u = 0; u < WB; ++u) vq[u] = s_val[(j0 + u) * NT + threadIdx.x];
+#pragma unroll
+            for (int u = 0; u < WB; ++u)
+                if ((j0 + u) * NT + threadIdx.x < cnt_tile && gq[u] < n)   // g < n: as above
+                    b2_put<KOUT>(keys_out, vals_out, gq[u], kq[u], base + vq[u], pk);
         }
     }
     if (!more) break;

@@ -1418,13 +1418,24 @@ static __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __r
         }
     }
     __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < IT; ++j) {
-        const uint32_t p = j * NT + threadIdx.x;
+    // the write-out's LDS reads in batches of WB items (every staged record, then every digit base), not
+    // one item's two dependent reads and a wait at a time (as k_b2_scatter / k_seg_scatter; past the tile
+    // the records are stale LDS, masked to a digit, and nothing is stored)
+    constexpr int WB = IT < 8 ? IT : 8;
+#pragma unroll
+    for (int j0 = 0; j0 < IT; j0 += WB) {
+    uint2 kq[WB];
+    uint32_t gq[WB];
+#pragma unroll
+    for (int u = 0; u < WB; ++u) kq[u] = s_kv[(j0 + u) * NT + threadIdx.x];
+#pragma unroll
+    for (int u = 0; u < WB; ++u) gq[u] = s_gbase[(kq[u].x >> shift) & (R - 1)] + (j0 + u) * NT + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < WB; ++u) {
+        const uint32_t p = (j0 + u) * NT + threadIdx.x;
         if (p < cnt_tile) {
-            const uint2 kv = s_kv[p];
-            const uint32_t d = (kv.x >> shift) & (R - 1);
-            const uint32_t g = s_gbase[d] + p;       // s_gbase holds the digit's global base - its tile start
+            const uint2 kv = kq[u];
+            const uint32_t g = gq[u];                // s_gbase holds the digit's global base - its tile start
             if (g < n) {            // always true when the scan is right; never write out of bounds
                 if (starts) {
                     // a key's first item in the tile: the item before it holds another key (a digit
@@ -1441,6 +1452,7 @@ static __global__ void __launch_bounds__(NT) k_radix_scatter(const uint32_t* __r
                 if (rank_out) rank_out[kv.y] = g;     // the inverse permutation (last pass, on request)
             }
         }
+    }
     }
 }
 

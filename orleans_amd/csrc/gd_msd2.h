@@ -290,15 +290,25 @@ static __global__ void __launch_bounds__(SEG_NT) k_seg_scatter(SegIn in, const u
         }
     }
     __syncthreads();
-#pragma unroll 4
-    for (int j = 0; j < IT; ++j) {
-        const uint32_t p = j * SEG_NT + threadIdx.x;
-        if (p < st.cnt) {
-            const uint32_t k = s_key[p];
-            const uint32_t g = s_gbase[(k >> B2_LOW_BITS) & mask] + p;
-            keys_out[g] = (uint16_t)(k & ((1u << B2_LOW_BITS) - 1));
-            vals_out[g] = s_val[p];
-        }
+    // the write-out reads its LDS in batches of WB items (every key, every digit base, every index, then
+    // the stores), not one item's dependent reads and a wait at a time (k_b2_scatter's write-out): cfg 3
+    // 0.193 -> 0.185 ms (profiles/r05_writeout_batch_ab.txt)
+    constexpr int WB = 8;
+#pragma unroll
+    for (int j0 = 0; j0 < IT; j0 += WB) {
+        uint32_t kq[WB], gq[WB], vq[WB];
+#pragma unroll
+        for (int u = 0; u < WB; ++u) kq[u] = s_key[(j0 + u) * SEG_NT + threadIdx.x];
+#pragma unroll
+        for (int u = 0; u < WB; ++u) gq[u] = s_gbase[(kq[u] >> B2_LOW_BITS) & mask] + (j0 + u) * SEG_NT + threadIdx.x;
+#pragma unroll
+        for (int u = 0; u < WB; ++u) vq[u] = s_val[(j0 + u) * SEG_NT + threadIdx.x];
+#pragma unroll
+        for (int u = 0; u < WB; ++u)
+            if ((j0 + u) * SEG_NT + threadIdx.x < st.cnt) {
+                keys_out[gq[u]] = (uint16_t)(kq[u] & ((1u << B2_LOW_BITS) - 1));
+                vals_out[gq[u]] = vq[u];
+            }
     }
 }
 
@@ -859,6 +869,8 @@ static __global__ void __launch_bounds__(CH_NT, 2) k_l2_chunk_scatter(const uint
             }
         }
         __syncthreads();
+        // (the write-out's LDS reads batched as in k_b2_scatter / k_seg_scatter measured no faster here:
+        // 0.197 -> 0.197 ms at cfg 3, profiles/r05_writeout_batch_ab.txt)
 #pragma unroll
         for (uint32_t q = 0; q < CH_RW; ++q) {
             const uint32_t i = q * CH_NT + tid;
