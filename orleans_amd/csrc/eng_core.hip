@@ -694,9 +694,10 @@ int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uin
     // all), each looping over its tiles with the next tile's loads under the current write-out.  cfg 2:
     // k_radix_scatter 0.0626 -> 0.0597 ms at k = 2, 0.087 at k = 1; pass A of the three-pass form at cfg 3
     // (Zipf, 8-K tiles) 0.173 -> 0.19 ms, so that pass keeps one workgroup a tile
-    // (profiles/r05_b2_persist_ab.txt).  The ballot ranks keep it too (their persistent form spills).
+    // (profiles/r05_b2_persist_ab.txt).  The ballot ranks keep it too (their persistent form spills).  The
+    // persistent form addresses the activations by 32-bit byte offsets: batches up to 2^30 messages.
     bool persisted = false;
-    if constexpr (KOUT == B2_KEY16 && !BALLOT) if (h->b2_persist) {
+    if constexpr (KOUT == B2_KEY16 && !BALLOT) if (h->b2_persist && n <= (1u << 30)) {
         const uint32_t grid = std::min<uint32_t>(tiles, std::max<uint32_t>(8, (h->b2_persist * h->n_cu) & ~7u));
         GD_TRY(launch(h, "k_radix_scatter", dim3(grid), dim3(B2_NT), 0,
                       k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT, BALLOT, true>, acts, n, n_act, R, tiles,
