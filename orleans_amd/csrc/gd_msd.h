@@ -161,15 +161,17 @@ __device__ __forceinline__ void msd_range_kp(MsdShared<NT, RW>& sh, uint32_t b, 
             if (2 * tid + 1 < L) offsets[k0 + 2 * tid + 1] = base + ex + tlo;
         }
         __syncthreads();
-        // rows in order: the ranks stay stable; the message indices are loaded MSD_G rows at a time
+        // rows in order: the ranks stay stable; the message indices are loaded MSD_G rows at a time,
+        // unconditionally (clamped into the range; a row past the wave's segment has key 0xFFFF and stores
+        // nothing): a load under a lane mask put the compiler's wait for every outstanding load (vmcnt 0)
+        // at each mask's join, so a group's loads and the next group's never overlapped
+        const uint32_t* rsrc = S ? ri : idx;             // an empty range: any valid address
+        const uint32_t rlast = S ? S - 1 : 0;
 #pragma unroll
         for (int g = 0; g < RW; g += MSD_G) {
             uint32_t mm[MSD_G];
 #pragma unroll
-            for (int r = 0; r < MSD_G && g + r < RW; ++r) {
-                const uint32_t i = s0 + (g + r) * WAVE + lane;
-                mm[r] = i < s1 ? ri[i] : 0u;
-            }
+            for (int r = 0; r < MSD_G && g + r < RW; ++r) mm[r] = rsrc[min(s0 + (g + r) * WAVE + lane, rlast)];
 #pragma unroll
             for (int r = 0; r < MSD_G && g + r < RW; ++r) {
                 const uint32_t k = (kp[(g + r) / 2] >> (16 * ((g + r) & 1))) & 0xFFFFu;

@@ -849,12 +849,10 @@ static __global__ void __launch_bounds__(CH_NT, 2) k_l2_chunk_scatter(const uint
         const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
         for (uint32_t g = 0; g < CH_RW; g += MSD_G) {
+            // unconditional loads, clamped into the chunk (msd_range_kp: no vmcnt(0) at mask joins)
             uint32_t mm[MSD_G];
 #pragma unroll
-            for (uint32_t q = 0; q < (uint32_t)MSD_G; ++q) {
-                const uint32_t i = s0 + (g + q) * WAVE + lane;
-                mm[q] = i < s1 ? ri[i] : 0u;
-            }
+            for (uint32_t q = 0; q < (uint32_t)MSD_G; ++q) mm[q] = ri[min(s0 + (g + q) * WAVE + lane, cs - 1)];
 #pragma unroll
             for (uint32_t q = 0; q < (uint32_t)MSD_G; ++q) {
                 const uint32_t k = (kp[(g + q) / 2] >> (16 * ((g + q) & 1))) & 0xFFFFu;
