@@ -43,6 +43,7 @@ static __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restric
     constexpr uint32_t TILE = NT * IT;
     static_assert(TILE <= 65536 && IT % 4 == 0, "16-B loads, u16 tile positions");
     __shared__ uint32_t s_cnt[TPB][RMAX];
+    __shared__ uint32_t s_sink[WAVE];
     for (uint32_t x = threadIdx.x; x < TPB * RMAX; x += NT) (&s_cnt[0][0])[x] = 0;
     __syncthreads();
     const uint32_t t0 = hist_t0(blockIdx.x, gridDim.x, TPB, tiles, xcd_rev);
@@ -73,10 +74,7 @@ static __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restric
         for (int j = 0; j < IT; ++j) {
             const uint64_t i = base + 4 * ((j / 4) * NT + threadIdx.x) + (j % 4);
             const uint32_t d = min(k[j], clamp) >> shift;
-            if (i < n) {
-                if (d == h) ++hc;
-                else atomicAdd(&s_cnt[t][d], 1u);
-            }
+            hist_add(s_cnt[t], s_sink, d, h, i < n, hc);
         }
         hc = wave_sum(hc);
         if (lane == 0 && hc) atomicAdd(&s_cnt[t][h], hc);

@@ -1832,6 +1832,18 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // hot digit's items are then counted and ranked in registers by ballot -- no LDS atomic and none of the
 // same-address serialisation a hot counter costs (64 lanes on one LDS address take 64 cycles) -- and
 // every other item takes its own counter update.  A wave keeps one hot digit for all its rows of a tile.
+// One histogram item without a branch: a live item of the wave's hot digit h counts in the register hc,
+// any other live item adds 1 to its counter, and an item that is not live (past the tile) or hot adds 1
+// to its lane's own sink word (never read; lane-distinct, so no two lanes of one instruction meet there).
+// Replaces two nested lane-masked branches an item (their exec-mask juggling was most of the issued
+// instructions of the histogram kernels).
+__device__ __forceinline__ void hist_add(uint32_t* s_cnt, uint32_t* s_sink, uint32_t d, uint32_t h, bool live,
+                                         uint32_t& hc) {
+    const bool hot = d == h;
+    hc += live && hot ? 1u : 0u;
+    atomicAdd(live && !hot ? &s_cnt[d] : &s_sink[threadIdx.x & (WAVE - 1)], 1u);
+}
+
 __device__ __forceinline__ uint32_t wave_hot_digit(uint32_t d, bool valid) {
     uint32_t best = NONE32, bc = 7;
 #pragma unroll

@@ -138,7 +138,7 @@ __device__ __forceinline__ void msd_range_kp(MsdShared<NT, RW>& sh, uint32_t b, 
     for (uint32_t x = tid; x < NW * MSD_LW; x += NT) (&sh.wc[0][0])[x] = 0;
     if (S <= CAP) {
         const uint32_t seg = (S + NW - 1) / NW;
-        const uint32_t s0 = min(w * seg, S), s1 = min((w + 1) * seg, S);
+        const uint32_t s0 = min(w * seg, S);
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < RW; ++r) {

@@ -150,6 +150,7 @@ static __global__ void __launch_bounds__(SEG_NT) k_seg_hist(SegIn in, const uint
     constexpr uint32_t PER = PK ? 8u : 4u;               // items a 16-B load
     constexpr uint32_t NL = SEG_IT / PER;                // 16-B loads a thread covering the aligned tile
     __shared__ uint32_t s_cnt[SEG_RMAX];
+    __shared__ uint32_t s_sink[WAVE];                    // the adds of keys not counted there (hist_add)
     SegTile st;
     // XCD-contiguous tiles (xcd_tile): the digit-major counts of neighbouring tiles share cache lines,
     // which then fill in one L2 instead of going out as partial-line writes from eight
@@ -186,10 +187,7 @@ static __global__ void __launch_bounds__(SEG_NT) k_seg_hist(SegIn in, const uint
             const uint32_t e = e0 + q;
             const uint32_t k = PK ? (w4[q / 2] >> (16 * (q & 1))) & 0xFFFFu : w4[q];
             const uint32_t d = (k >> dsh) & (rb - 1);
-            if (e >= st.base && e < st.base + st.cnt) {
-                if (d == h) ++hc;
-                else atomicAdd(&s_cnt[d], 1u);
-            }
+            hist_add(s_cnt, s_sink, d, h, e - st.base < st.cnt, hc);
         }
     };
 #pragma unroll
@@ -590,6 +588,7 @@ __device__ __forceinline__ ChunkWalk chunk_walk(uint32_t m) {
 static __global__ void __launch_bounds__(CH_NT) k_l2_chunk_hist(const uint16_t* __restrict__ keys16, L2Lists l,
                                                          uint32_t* __restrict__ hh) {
     __shared__ uint32_t s_cnt[MSD_L];
+    __shared__ uint32_t s_sink[WAVE];
     const uint32_t tid = threadIdx.x, lane = lane_id();
     const ChunkWalk cw = chunk_walk(l.ctr[2]);
     for (uint32_t j = cw.j; j < cw.end; j += cw.step) {
@@ -618,10 +617,7 @@ static __global__ void __launch_bounds__(CH_NT) k_l2_chunk_hist(const uint16_t* 
             for (uint32_t x = 0; x < 8; ++x) {
                 const uint32_t e = e0 + x;
                 const uint32_t k = (w4[x / 2] >> (16 * (x & 1))) & 0xFFFFu;
-                if (e >= start && e < start + cs) {
-                    if (k == h) ++hc;
-                    else atomicAdd(&s_cnt[k], 1u);
-                }
+                hist_add(s_cnt, s_sink, k, h, e - start < cs, hc);
             }
         };
 #pragma unroll
