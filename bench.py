@@ -527,6 +527,15 @@ def compact_secondary(sec: dict) -> dict:
             out[name] = {k: v[k] for k in ("batch", "graph", "eager", "zero_copy") if k in v}
         elif name == "cfg1_ping_shape":
             out[name] = _pick(v, ("value", "ms_per_step", "workload"))
+        elif name.endswith("_churn"):
+            out[name] = _pick(v, ("value", "ms_per_step", "static_ms_per_step", "churn_vs_static",
+                                  "unregistered_per_step", "index_builds_timed", "slots_reprojected_timed",
+                                  "last_full_build_ms", "table_tombstones", "routed_ok_fraction_last_step"))
+        elif name == "cfg2_mixed":
+            out[name] = _pick(v, ("value", "ms_per_step", "k_route_ms", "k_route_vs_single_class", "index_types8",
+                                  "guid_grains", "routed_ok_fraction"))
+        elif name == "host_path":
+            out[name] = _pick(v, ("value", "ms_per_call", "pcie_GBps", "workload"))
         else:
             d = _pick(v, ("value", "unit", "ms_per_step", "steps", "workload", "n_gpus", "scaling",
                           "messages_per_step"))
@@ -714,6 +723,7 @@ def main():
             "ms_per_step": round(wall3 / steps3 * 1e3, 4), "steps": steps3,
             "workload": workload_name("cfg3", 1, w3["N"], w3["G_total"]), "msgs_per_gpu": w3["N"],
             "roofline": rf3, "kernels": k3, "cpu_baseline": c3}
+        secondary["cfg3_churn"] = churn_line(w3, args, wall3 / steps3 * 1e3, "cfg3", steps3, 3)
         w3["e"].close()
         del w3
         torch.cuda.empty_cache()
@@ -731,6 +741,15 @@ def main():
     kernels, roofline = roofline_of(kt, max(1, args.profile_steps), m_recv, n_act, acts_np, args.workload, world)
     if roofline and roofline["kernel"] == "k_route":
         route_extras(roofline, e, m_recv, args.workload, world, isinstance(router, LibraryRouter))
+
+    # ---- the directory under churn, a mixed directory, the host-buffer path (cfg 2, N = 1) -------
+    if world == 1 and args.workload == "cfg2" and not args.no_secondary:
+        secondary["cfg2_churn"] = churn_line(w, args, wall_max / args.steps * 1e3, "cfg2", args.steps,
+                                             args.warmup)
+        single = (roofline or {}).get("avg_launch_ms") if (roofline or {}).get("kernel") == "k_route" else None
+        secondary["cfg2_mixed"] = mixed_line(args, tcd, dev, max(10, args.steps // 4), max(3, args.warmup // 2),
+                                             single)
+        secondary["host_path"] = host_path_line(e, tcd, G_total, n_act)
 
     # ---- BASELINE cfg 5: 4,096-message micro-batch latency on this directory ---------
     if world == 1 and args.workload == "cfg2" and args.latency_batches > 0:
@@ -927,6 +946,150 @@ def micro_batch_latency(e, tcd: int, G: int, n_act: int, batches: int, B: int = 
     out["zero_copy"] = bool(e.get_option("mb_zerocopy"))
     mb.close()
     return out
+
+
+def churn_line(w, args, static_ms: float, tag: str, steps: int, warmup: int) -> dict:
+    """the directory under continuous registration (Catalog.cs:540-552,1270-1277 ->
+    GrainDirectoryPartition.AddSingleActivation / RemoveActivation, :304-363).  Every step removes 1 % of
+    the grains (gd_dir_unregister_device) and registers the 1 % removed the step before again
+    (gd_dir_register_device_async), then routes and buckets the workload's batch -- all enqueued on the
+    handle's stream, timed together exactly like the static steps.  The probe indexes are re-projected for
+    the touched slots (k_cx_sync), not rebuilt; index builds during the timed steps are reported."""
+    e, router, keys, stream, n_act, G = w["e"], w["router"], w["keys"], w["stream"], w["n_act"], w["G_total"]
+    dev = keys.device
+    B = max(1, G // 100)
+    nwin = max(2, min(G // B, steps + warmup + 1))
+    tcd = int(keys[0, 2].item()) & 0xFFFFFFFFFFFFFFFF
+    K, A, V = [], [], []
+    with torch.cuda.stream(stream):
+        for i in range(nwin):
+            ks = torch.arange(i * B, (i + 1) * B, device=dev, dtype=torch.int64)
+            k = grain_keys_torch(tcd, ks, dev)
+            own = torch.empty(B, dtype=torch.int32, device=dev)
+            e.ring_owner_device(k.data_ptr(), B, own.data_ptr())
+            a = ks.to(torch.int32)                       # world 1: grain k's activation is k (setup_workload)
+            K.append(k)
+            A.append(a)
+            V.append(torch.stack([a, own], 1).contiguous())
+    torch.cuda.synchronize()
+    before = e.index_stats()
+
+    def step(s_):
+        i = s_ % nwin
+        e.unregister_device(K[i].data_ptr(), A[i].data_ptr(), B)
+        if s_:
+            j = (s_ - 1) % nwin
+            e.register_device_async(K[j].data_ptr(), V[j].data_ptr(), B)
+        return router.route_bucket(keys, n_act)
+
+    with torch.cuda.stream(stream):
+        for s_ in range(warmup):
+            step(s_)
+        torch.cuda.synchronize()
+        mid = e.index_stats()
+        t0 = time.perf_counter()
+        res = None
+        for s_ in range(warmup, warmup + steps):
+            res = step(s_)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+    e.synchronize()                                    # any deferred device error of the async batches
+    after = e.index_stats()
+    st = e.stats()
+    # restore the directory: the last removed window comes back
+    last = (warmup + steps - 1) % nwin
+    e.register_device(K[last].data_ptr(), V[last].data_ptr(), B)
+    ok = int((res.status == 0).sum().item())
+    ms = wall / steps * 1e3
+    return {"value": round(w["N"] * steps / wall, 1), "unit": "messages/s", "ms_per_step": round(ms, 4),
+            "steps": steps, "static_ms_per_step": round(static_ms, 4),
+            "churn_vs_static": round(ms / static_ms, 3) if static_ms else None,
+            "unregistered_per_step": B, "registered_per_step": B,
+            "index_builds_timed": after["builds"] - mid["builds"],
+            "index_builds_total": after["builds"] - before["builds"],
+            "slots_reprojected_timed": after["synced_slots"] - mid["synced_slots"],
+            "last_full_build_ms": round(after["last_build_ms"], 3),
+            "table_live": st["table_live"], "table_tombstones": st["table_tombstones"],
+            "routed_ok_fraction_last_step": round(ok / w["N"], 4),
+            "workload": f"{tag} batch + 1% of the grains unregistered and 1% registered a step "
+                        "(gd_dir_unregister_device + gd_dir_register_device_async on the stream)"}
+
+
+def mixed_line(args, tcd_ping: int, dev, steps: int, warmup: int, single_route_ms: float) -> dict:
+    """cfg 2's shape over a mixed directory -- 2^20 grains of 8 grain classes, every
+    100th Guid-keyed (N0 != 0, UniqueKey.cs:135-143; orleans_amd.workloads.mixed_grain_keys), 16M
+    messages uniform over them.  The 8-B index holds the 8 classes, the Guid keys' messages probe the
+    directory per message.  k_route's time is compared with the single-class line's."""
+    from orleans_amd.workloads import mixed_grain_keys
+    G, N = 1 << 20, 1 << 24
+    tcds = [(3 << 56) + ((g.calculate_id_hash(f"BenchmarkGrains.Mixed.Grain{c}") & 0xFFFFFFFFFFFFFFFF)
+                         & 0x00FFFFFFFFFFFFFF) for c in range(8)]
+    e = g.GrainDispatch(device=dev.index or 0, table_capacity=2 * G, my_silo=0, kernel_timing=False)
+    e.tune_set("probe_keys", 3)
+    e.tune_set("bucket", 1)
+    pts, own = e.ring_set_silos(args.mode, SILO_SETS[args.silos])
+    reg = mixed_grain_keys(tcds, G)
+    owner = e.ring_owner(reg)
+    e.register(reg, np.arange(G, dtype=np.uint32), owner)
+    idx = np.random.default_rng(0x5EED0007).integers(0, G, size=N)
+    keys = torch.from_numpy(reg[idx].view(np.int64)).to(dev)
+    engine = DeviceEngine(e, dev)
+    router = ShardedRouter(engine)
+    stream = engine.stream
+    with torch.cuda.stream(stream):
+        for _ in range(warmup):
+            router.route_bucket(keys, G)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = None
+        for _ in range(steps):
+            res = router.route_bucket(keys, G)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+    ok = int((res.status == 0).sum().item())
+    kt = profile_kernels(e, router, keys, G, stream, 3)
+    kr = kt.get("k_route")
+    route_ms = kr[1] / kr[0] if kr and kr[0] else None
+    ist = e.index_stats()
+    e.close()
+    return {"value": round(N * steps / wall, 1), "unit": "messages/s", "ms_per_step": round(wall / steps * 1e3, 4),
+            "steps": steps, "k_route_ms": round(route_ms, 4) if route_ms else None,
+            "k_route_vs_single_class": round(route_ms / single_route_ms, 3) if route_ms and single_route_ms else None,
+            "index_types8": ist["types8"], "guid_grains": ist["n0_live"],
+            "routed_ok_fraction": round(ok / N, 4),
+            "workload": f"{N} msgs uniform over {G} grains of 8 classes, 1% Guid-keyed (N0 != 0), ring {args.mode}"}
+
+
+def host_path_line(e, tcd: int, G: int, n_act: int, steps: int = 5, warmup: int = 2) -> dict:
+    """what a C# caller sees -- gd_route_bucket on pinned host buffers (the
+    P/Invoke entry point): cfg 2's 16M keys in (24 B a message), silo / act / status /
+    perm out (13 B) and the offsets, H2D / D2H copies overlapped with the kernels in chunks."""
+    N = 1 << 24
+    hold = []
+
+    def pinned(shape, dt):
+        t = torch.empty(int(np.prod(shape)) * np.dtype(dt).itemsize, dtype=torch.uint8, pin_memory=True)
+        hold.append(t)
+        return t.numpy().view(dt).reshape(shape)
+    keys = pinned((N, 3), np.uint64)
+    silo, act, perm = (pinned((N,), np.uint32) for _ in range(3))
+    st = pinned((N,), np.uint8)
+    off = pinned((n_act + 2,), np.uint32)
+    keys[:] = grain_keys(tcd, np.random.default_rng(0x5EED0001).integers(0, G, size=N, dtype=np.int64))
+    ptr = lambda a: a.ctypes.data                       # noqa: E731
+
+    def one():
+        e._c(g.lib.gd_route_bucket(e.h, ptr(keys), N, n_act, ptr(silo), ptr(act), ptr(st), ptr(perm), ptr(off)))
+    for _ in range(warmup):
+        one()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    dt = (time.perf_counter() - t0) / steps
+    ok = int((st == 0).sum())
+    return {"value": round(N / dt, 1), "unit": "messages/s", "ms_per_call": round(dt * 1e3, 3), "steps": steps,
+            "pcie_GBps": round(N * (24 + 17) / dt / 1e9, 2), "routed_ok": ok,
+            "workload": "cfg2 keys in pinned host memory -> gd_route_bucket -> pinned host results (PCIe-inclusive)"}
 
 
 def workload_name(w: str, world: int, n: int, g_total: int) -> str:

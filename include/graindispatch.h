@@ -201,6 +201,18 @@ int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t
 /* RemoveActivation(grain, act) for a batch; out_removed may be NULL. */
 int gd_dir_unregister(gd_handle* h, const gd_key* keys, const uint32_t* acts, uint32_t n,
                       uint8_t* out_removed);
+/* The continuous-registration forms (round 6): activations register and deactivate all the time
+ * (Catalog.cs:540-552,1270-1277 -> GrainDirectoryPartition.AddSingleActivation / RemoveActivation,
+ * GrainDirectoryPartition.cs:304-363), between route batches.  Both only enqueue on the handle's
+ * stream (device arrays, outputs optional): no host round trip, so a host interleaves them with
+ * gd_route_bucket_device batches and the stream runs them back to back; the probe indexes are
+ * re-projected for the touched slots, not rebuilt.  Same semantics as gd_dir_register_device /
+ * gd_dir_unregister; a device-side failure (table full, claims not settled after the gated passes)
+ * is returned by the next synchronising call on the handle (gd_synchronize, gd_stats_get, ...). */
+int gd_dir_register_device_async(gd_handle* h, const gd_key* d_keys, const gd_val* d_vals, uint32_t n,
+                                 gd_val* d_out_vals, uint8_t* d_out_inserted);
+int gd_dir_unregister_device(gd_handle* h, const gd_key* d_keys, const uint32_t* d_acts, uint32_t n,
+                             uint8_t* d_out_removed);
 /* LookUpActivations for a batch; out_found[i] = 0 -> out_vals[i] = {GD_NO_ACTIVATION, GD_NO_SILO}. */
 int gd_dir_lookup(gd_handle* h, const gd_key* keys, uint32_t n, gd_val* out_vals, uint8_t* out_found);
 int gd_dir_clear(gd_handle* h);
@@ -955,6 +967,28 @@ int gd_tune_agree(gd_handle* h);
 #define GD_COMM_RCCL  1   /* gd_comm_init */
 #define GD_COMM_LOCAL 2   /* gd_comm_init_local (in-process device copies) */
 int gd_comm_info(gd_handle* h, int* n_ranks, int* rank, int* transport);
+
+/* ---- probe indexes (round 6) -------------------------------------------------------------------
+ * The compact probe indexes mirror the directory table slot for slot.  AddSingleActivation /
+ * AddActivation / RemoveActivation batches (gd_dir_register*, gd_dir_upsert, gd_dir_unregister) keep
+ * them current by re-projecting the slots they touched -- the reference's O(1) dictionary updates
+ * (GrainDirectoryPartition.cs:304-363) stay O(batch); other directory changes (rehash, clear, silo
+ * removal, merge, split, handoff) leave them to a full rebuild (two streaming passes) at the next large
+ * route.  Keys an index does not hold (N0 != 0, a grain class or N1 it does not cover) are probed in
+ * the directory per message.  Read-only statistics: */
+typedef struct gd_index_stats {
+    uint64_t builds;          /* full builds since gd_create                                      */
+    uint64_t synced_slots;    /* table slots re-projected by directory batches                    */
+    double   last_build_ms;   /* host wall time of the last build (both passes, one read-back)    */
+    uint32_t current;         /* 1: the indexes match the table now                               */
+    uint32_t types8;          /* grain classes (TypeCodeData) the 8-B index holds                 */
+    uint32_t act_bits8;       /* its activation and silo field widths                             */
+    uint32_t silo_bits8;
+    uint32_t n0_live;         /* at the last build: live entries with N0 != 0 (directory probe)    */
+    uint32_t out8;            /* live entries projected since the build that the 8-B index does not
+                                 hold or redirects to the directory (incl. the build's own)         */
+} gd_index_stats;
+int gd_index_stats_get(gd_handle* h, gd_index_stats* out);
 
 #ifdef __cplusplus
 }

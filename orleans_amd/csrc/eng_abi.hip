@@ -90,6 +90,7 @@ void gd_destroy(gd_handle* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->bstream) (void)hipStreamSynchronize(h->bstream);
     if (h->b_ev) (void)hipEventDestroy(h->b_ev);
+    if (h->b_fence_ev) (void)hipEventDestroy(h->b_fence_ev);
     if (h->fan_ev) (void)hipEventDestroy(h->fan_ev);
     for (DevBuf* b : {&h->ring_pts, &h->ring_own, &h->keys_in, &h->u32_a, &h->u32_b, &h->u32_c, &h->u32_d, &h->u8_a,
                       &h->out_a, &h->out_b, &h->out_c, &h->hist, &h->partials, &h->partials2, &h->offs})
@@ -115,6 +116,7 @@ void gd_destroy(gd_handle* h) {
     free_buf(h->cx_heap);
     free_buf(h->cxi_tab);
     free_buf(h->cx8_tab);
+    free_buf(h->reg_retry);
     free_buf(h->cxi_types);
     free_buf(h->cxi_ctr);
     for (auto& kt : h->cx_tune)
@@ -196,6 +198,21 @@ int gd_stats_get(gd_handle* h, gd_stats* out) {
     return GD_OK;
 }
 
+int gd_index_stats_get(gd_handle* h, gd_index_stats* out) {
+    if (!h || !out) return set_err(h, GD_EINVAL, "null argument");
+    *out = gd_index_stats{};
+    out->builds = h->cx_builds;
+    out->synced_slots = h->cx_synced;
+    out->last_build_ms = h->cx_build_ms;
+    out->current = cx_current(h) ? 1u : 0u;
+    out->types8 = h->cx8_ok ? h->cx8_layout.ntypes : 0u;
+    out->act_bits8 = h->cx8_ok ? h->cx8_layout.ab : 0u;
+    out->silo_bits8 = h->cx8_ok ? h->cx8_layout.sb : 0u;
+    out->n0_live = h->cx_ctr_host.n0_live;
+    out->out8 = h->cx_ctr_host.out8;
+    return GD_OK;
+}
+
 int gd_ring_set(gd_handle* h, int mode, const uint32_t* points, const uint32_t* owner, uint32_t n) {
     if (!h) return set_err(nullptr, GD_EINVAL, "null handle");
     if (mode < GD_RING_DIRECTORY || mode > GD_RING_VIRTUAL_BUCKETS) return set_err(h, GD_EINVAL, "bad ring mode %d", mode);
@@ -263,10 +280,13 @@ int gd_ring_lookup_hashes(gd_handle* h, const uint32_t* hashes, uint32_t n, uint
 
 namespace gdx {
 // AddSingleActivation for a batch of device-resident keys / values (first registration wins, batch
-// order); out_vals / out_ins are device arrays (either may be null).  Synchronous.
+// order); out_vals / out_ins are device arrays (either may be null).  Synchronous, or (async) only
+// enqueued: REG_PASSES gated claim passes instead of read-back-driven relaunches, no read-back at the
+// end; a device error (table full, unsettled claims) surfaces at the next synchronising call.
 int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t n, gd_val* out_vals,
-                  uint8_t* out_ins) {
-    GD_TRY(maybe_grow_table(h, n));
+                  uint8_t* out_ins, bool async) {
+    GD_TRY(bfence(h));
+    GD_TRY(async ? maybe_grow_async(h, n) : maybe_grow_table(h, n));
     const uint32_t op = ++h->dir_op;
     GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));   // slot_of
     GD_TRY(ensure(h, h->u32_b, (size_t)n * 4));   // win
@@ -277,14 +297,28 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
     uint32_t* win = (uint32_t*)h->u32_b.p;
     uint8_t* is_new = (uint8_t*)h->u8_a.p;
     const unsigned long long mask = h->capacity - 1;
-    // claim pass, then relaunches for the items that met an unpublished claim
-    for (uint32_t pass = 0;; ++pass) {
-        HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
-        GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
-                      (uint32_t)(pass > 0), dvals, table_args(h)));
-        GD_TRY(pull_counters(h));
-        if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
-        if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_register: claims did not settle");
+    TabTrack tt(h);                                // the batch re-projects its slots into the probe indexes
+    if (async) {
+        GD_TRY(ensure(h, h->reg_retry, REG_PASSES * sizeof(uint32_t)));
+        uint32_t* rc = (uint32_t*)h->reg_retry.p;
+        HIP_TRY(h, hipMemsetAsync(rc, 0, REG_PASSES * sizeof(uint32_t), h->stream));
+        for (uint32_t pass = 0; pass < REG_PASSES; ++pass)
+            GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim_gated, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
+                          dvals, table_args(h), pass ? (const uint32_t*)rc + pass - 1 : (const uint32_t*)nullptr,
+                          rc + pass));
+        GD_TRY(launch(h, "k_reg_settled", dim3(1), dim3(WAVE), 0, k_reg_settled, (const uint32_t*)rc + REG_PASSES - 1,
+                      h->ctr));
+        h->pending_in += n;
+    } else {
+        // claim pass, then relaunches for the items that met an unpublished claim
+        for (uint32_t pass = 0;; ++pass) {
+            HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
+            GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
+                          (uint32_t)(pass > 0), dvals, table_args(h)));
+            GD_TRY(pull_counters(h));
+            if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
+            if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_register: claims did not settle");
+        }
     }
     GD_TRY(launch(h, "k_reg_minwin", g, b, 0, k_reg_minwin, (const uint32_t*)slot_of, (const uint8_t*)is_new, n, h->slots));
     GD_TRY(launch(h, "k_reg_resolve", g, b, 0, k_reg_resolve, (const uint32_t*)slot_of, (const uint8_t*)is_new, n,
@@ -294,15 +328,36 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
     if (out_vals || out_ins)
         GD_TRY(launch(h, "k_reg_report", g, b, 0, k_reg_report, (const uint32_t*)slot_of, (const uint32_t*)win, n,
                       (const Slot*)h->slots, out_vals, out_ins));
+    GD_TRY(cx_sync(h, tt, slot_of, n));
+    if (async) return GD_OK;
     GD_TRY(pull_counters(h));
     if (h->ctr_host.err) {
         const uint32_t e = h->ctr_host.err;
         HIP_TRY(h, hipMemsetAsync(&h->ctr->err, 0, sizeof(uint32_t), h->stream));
         GD_TRY(sync(h));
         return set_err(h, (e & 2) ? GD_EFULL : (e & 4) ? GD_EINVAL : GD_ETIMEOUT,
-                       "gd_dir_register: device error bits 0x%x (2: table full, 4: silo index > 0xFFFE)", e);
+                       "gd_dir_register: device error bits 0x%x (2: table full, 4: silo index > 0xFFFE, "
+                       "64: an asynchronous batch's claims did not settle)", e);
     }
     return GD_OK;
+}
+
+// RemoveActivation (Force) for a batch of device-resident keys / activations; out_removed (device, may be
+// null).  Only enqueued.
+int unregister_core(gd_handle* h, const gd_key* dk, const uint32_t* dacts, uint32_t n, uint8_t* out_removed) {
+    GD_TRY(bfence(h));
+    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    uint32_t* slot_of = (uint32_t*)h->u32_a.p;
+    const unsigned long long mask = h->capacity - 1;
+    TabTrack tt(h);                               // the batch re-projects its slots into the probe indexes
+    GD_TRY(launch(h, "k_unreg_find", g, b, 0, k_unreg_find, dk, dacts, n, (const Slot*)h->slots, mask,
+                  (const DevCounters*)h->ctr, slot_of));
+    GD_TRY(launch(h, "k_unreg_poison", g, b, 0, k_unreg_poison, (const uint32_t*)slot_of, n, h->slots));
+    GD_TRY(launch(h, "k_unreg_min", g, b, 0, k_unreg_min, (const uint32_t*)slot_of, n, h->slots));
+    GD_TRY(launch(h, "k_unreg_commit", g, b, 0, k_unreg_commit, (const uint32_t*)slot_of, n, h->slots, h->ctr,
+                  out_removed));
+    return cx_sync(h, tt, slot_of, n);
 }
 }  // namespace gdx
 
@@ -320,7 +375,7 @@ int gd_dir_register(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32
     GD_TRY(ensure(h, h->out_a, (size_t)n * sizeof(gd_val)));
     GD_TRY(ensure(h, h->out_b, (size_t)n));
     GD_TRY(register_core(h, (const gd_key*)h->keys_in.p, (const gd_val*)h->out_c.p, n, (gd_val*)h->out_a.p,
-                         (uint8_t*)h->out_b.p));
+                         (uint8_t*)h->out_b.p, false));
     GD_TRY(d2h(h, out_vals, h->out_a, n));
     GD_TRY(d2h(h, out_inserted, h->out_b, n));
     return sync(h);
@@ -332,7 +387,23 @@ int gd_dir_register_device(gd_handle* h, const gd_key* d_keys, const gd_val* d_v
     if (n == 0) return GD_OK;
     HIP_TRY(h, hipSetDevice(h->device));
     GD_TRY(sync(h));                       // the caller's producers of d_keys / d_vals ran on this stream
-    return register_core(h, d_keys, d_vals, n, d_out_vals, d_out_inserted);
+    return register_core(h, d_keys, d_vals, n, d_out_vals, d_out_inserted, false);
+}
+
+int gd_dir_register_device_async(gd_handle* h, const gd_key* d_keys, const gd_val* d_vals, uint32_t n,
+                                 gd_val* d_out_vals, uint8_t* d_out_inserted) {
+    if (!h || (n && (!d_keys || !d_vals))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    return register_core(h, d_keys, d_vals, n, d_out_vals, d_out_inserted, true);
+}
+
+int gd_dir_unregister_device(gd_handle* h, const gd_key* d_keys, const uint32_t* d_acts, uint32_t n,
+                             uint8_t* d_out_removed) {
+    if (!h || (n && (!d_keys || !d_acts))) return set_err(h, GD_EINVAL, "null argument");
+    if (n == 0) return GD_OK;
+    HIP_TRY(h, hipSetDevice(h->device));
+    return unregister_core(h, d_keys, d_acts, n, d_out_removed);
 }
 
 int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t n, uint8_t* out_inserted) {
@@ -341,6 +412,7 @@ int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t
         if (vals[i].silo > 0xFFFEu) return set_err(h, GD_EINVAL, "silo index %u out of range at %u", vals[i].silo, i);
     if (n == 0) return GD_OK;
     HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(bfence(h));
     GD_TRY(maybe_grow_table(h, n));
     const uint32_t op = ++h->dir_op;
     GD_TRY(h2d(h, h->keys_in, keys, n));
@@ -359,6 +431,7 @@ int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t
     uint32_t* last = (uint32_t*)h->up_last.p;
     const gd_key* dk = (const gd_key*)h->keys_in.p;
     const unsigned long long mask = h->capacity - 1;
+    TabTrack tt(h);                               // the batch re-projects its slots into the probe indexes
     for (uint32_t pass = 0;; ++pass) {            // the registration's claim protocol (k_reg_claim)
         HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
         GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
@@ -372,6 +445,7 @@ int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t
                   (const gd_val*)h->out_c.p, n, (const uint32_t*)last, h->slots, h->ctr, (uint8_t*)h->out_b.p,
                   h->vtag, op));
     GD_TRY(launch(h, "k_up_clear", g, b, 0, k_up_clear, (const uint32_t*)slot_of, n, last));
+    GD_TRY(cx_sync(h, tt, slot_of, n));
     if (out_inserted) GD_TRY(d2h(h, out_inserted, h->out_b, n));
     GD_TRY(pull_counters(h));
     if (h->ctr_host.err) {
@@ -386,19 +460,11 @@ int gd_dir_unregister(gd_handle* h, const gd_key* keys, const uint32_t* acts, ui
     if (!h || (n && (!keys || !acts))) return set_err(h, GD_EINVAL, "null argument");
     if (n == 0) return GD_OK;
     HIP_TRY(h, hipSetDevice(h->device));
+    GD_TRY(bfence(h));
     GD_TRY(h2d(h, h->keys_in, keys, n));
     GD_TRY(h2d(h, h->u32_b, acts, n));
-    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
     GD_TRY(ensure(h, h->out_b, (size_t)n));
-    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
-    uint32_t* slot_of = (uint32_t*)h->u32_a.p;
-    const unsigned long long mask = h->capacity - 1;
-    GD_TRY(launch(h, "k_unreg_find", g, b, 0, k_unreg_find, (const gd_key*)h->keys_in.p, (const uint32_t*)h->u32_b.p, n,
-                  (const Slot*)h->slots, mask, (const DevCounters*)h->ctr, slot_of));
-    GD_TRY(launch(h, "k_unreg_poison", g, b, 0, k_unreg_poison, (const uint32_t*)slot_of, n, h->slots));
-    GD_TRY(launch(h, "k_unreg_min", g, b, 0, k_unreg_min, (const uint32_t*)slot_of, n, h->slots));
-    GD_TRY(launch(h, "k_unreg_commit", g, b, 0, k_unreg_commit, (const uint32_t*)slot_of, n, h->slots, h->ctr,
-                  (uint8_t*)h->out_b.p));
+    GD_TRY(unregister_core(h, (const gd_key*)h->keys_in.p, (const uint32_t*)h->u32_b.p, n, (uint8_t*)h->out_b.p));
     GD_TRY(d2h(h, out_removed, h->out_b, n));
     return sync(h);
 }
@@ -424,6 +490,7 @@ int gd_dir_clear(gd_handle* h) {
     h->tab_gen++;
     HIP_TRY(h, hipMemsetAsync(h->vtag, 0, h->capacity * sizeof(uint32_t), h->stream));
     HIP_TRY(h, hipMemsetAsync(h->ctr, 0, sizeof(DevCounters), h->stream));
+    h->ctr_stale = true;
     if (h->kx_cap) {                   // KeyExt entries go too
         h->kx_m.assign(h->kx_cap, KxSlot{});
         h->kx_hheap.clear();
@@ -489,9 +556,15 @@ int gd_route_bucket_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint3
     HIP_TRY(h, hipEventRecord(h->b_ev, h->stream));
     HIP_TRY(h, hipStreamWaitEvent(h->bstream, h->b_ev, 0));
     const hipStream_t main = h->stream;
+    const bool measured_before = h->measured_launch;
+    h->measured_launch = false;
     h->stream = h->bstream;
     const int r = bucket_device(h, d_act, n, n_act, d_perm, d_offsets);
     h->stream = main;
+    h->b_pending = true;
+    // a bucketing timed for tune_choose runs alone: the next batch's route waits for it
+    if (h->measured_launch) GD_TRY(bfence(h));
+    h->measured_launch = h->measured_launch || measured_before;
     return r;
 }
 
@@ -501,6 +574,8 @@ int gd_set_bucket_stream(gd_handle* h, void* s) {
     GD_TRY(resolve_timing(h));
     GD_TRY(sync(h));
     if (s && !h->b_ev) HIP_TRY(h, hipEventCreateWithFlags(&h->b_ev, hipEventDisableTiming));
+    if (s && !h->b_fence_ev) HIP_TRY(h, hipEventCreateWithFlags(&h->b_fence_ev, hipEventDisableTiming));
+    h->b_pending = false;
     h->bstream = (hipStream_t)s;
     return GD_OK;
 }

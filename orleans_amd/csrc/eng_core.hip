@@ -26,7 +26,20 @@ int set_err(gd_handle* h, int code, const char* fmt, ...) {
 }
 
 
+// A bucketing gd_route_bucket_device left running on the bucket stream (gd_set_bucket_stream) uses the
+// handle's scratch (u32_a..d, hist, partials, m3): every entry point that takes scratch on the handle's
+// own stream waits for it first (ensure() calls this).  The route itself takes no scratch,
+// so the next batch's route still overlaps this batch's bucketing.
+int bfence(gd_handle* h) {
+    if (!h->b_pending || !h->bstream || h->bstream == h->stream) return GD_OK;
+    HIP_TRY(h, hipEventRecord(h->b_fence_ev, h->bstream));
+    HIP_TRY(h, hipStreamWaitEvent(h->stream, h->b_fence_ev, 0));
+    h->b_pending = false;
+    return GD_OK;
+}
+
 int ensure(gd_handle* h, DevBuf& b, size_t bytes) {
+    GD_TRY(bfence(h));
     if (b.bytes >= bytes && b.p) return GD_OK;
     if (b.p) {
         HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -109,7 +122,11 @@ size_t ring_lds(gd_handle* h) { return (size_t)h->ring_n * 2 * sizeof(uint32_t);
 
 int pull_counters(gd_handle* h) {
     HIP_TRY(h, hipMemcpyAsync(&h->ctr_host, h->ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
+    if (h->cx_built && h->cxi_ctr.p)   // the index counters ride along (cx_ensure's rebuild rule)
+        HIP_TRY(h, hipMemcpyAsync(&h->cx_ctr_host, h->cxi_ctr.p, sizeof(CxCounters), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(h, hipStreamSynchronize(h->stream));
+    h->ctr_stale = false;
+    h->pending_in = 0;
     return GD_OK;
 }
 
@@ -146,73 +163,134 @@ unsigned long long pow2_at_least(unsigned long long x) {
     return c;
 }
 
-// ---- compact probe index (gd_cx.h) ----------------------------------------------
-// The index for the current table: rebuilt (two passes + one host sync) when the table changed since
-// the last build; false when the table is not eligible (an N0 != 0 key, too many types) or GD_CX=0.
-// n: the messages of the launch asking.  A stale index is rebuilt only for a launch of at least
-// capacity / 16 messages: a small route after a directory write takes the directory probe instead of a
-// full-table pass and a host sync; the next large launch rebuilds.
+// ---- compact probe indexes (gd_cx.h) ----------------------------------------------
+bool cx_current(const gd_handle* h) {
+    return h->cx_built && h->cx_slots_at == h->slots && h->cx_cap_at == h->capacity && h->cx_gen_at == h->tab_gen;
+}
+
+TabTrack::TabTrack(gd_handle* hh) : h(hh), was_current(cx_current(hh)) { ++h->tab_track; }
+
+static uint32_t bit_len(uint64_t x) {
+    uint32_t b = 0;
+    while (x) {
+        ++b;
+        x >>= 1;
+    }
+    return b;
+}
+
+static CxBuild cx_build_args(gd_handle* h) {
+    return CxBuild{(uint4*)h->cxi_tab.p, (unsigned long long*)h->cxi_types.p,
+                   h->cx8_ok ? (unsigned long long*)h->cx8_tab.p : nullptr, h->cx8_layout};
+}
+
+// Grid of the table-wide index passes: CXT_IT slots a thread a round, at most 16 workgroups a CU.
+static uint32_t cx_grid(gd_handle* h) {
+    return std::max<uint32_t>(1, std::min<uint64_t>(blocks_for(h->capacity, BLOCK * CXT_IT), (uint64_t)h->n_cu * 16));
+}
+
+// The full build: k_cx_types, one read-back (types, counts, widths), the 8-B layout, k_cx_project.
+// The 8-B index takes the most populous types (up to CX8_TYPES) and the activation / silo widths of the
+// live entries; fewer types when the three fields would not fit 31 bits, narrower activations last
+// (wider ones are then redirect entries: their keys probe the directory).
+static int cx_build(gd_handle* h) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const unsigned long long cap = h->capacity;
+    GD_TRY(ensure(h, h->cxi_tab, cap * 16));
+    GD_TRY(ensure(h, h->cx8_tab, cap * 8));
+    GD_TRY(ensure(h, h->cxi_types, CX_TYPES * 12));
+    GD_TRY(ensure(h, h->cxi_ctr, sizeof(CxCounters)));
+    unsigned long long* types = (unsigned long long*)h->cxi_types.p;
+    uint32_t* counts = (uint32_t*)(types + CX_TYPES);
+    CxCounters* ctr = (CxCounters*)h->cxi_ctr.p;
+    HIP_TRY(h, hipMemsetAsync(types, 0xFF, CX_TYPES * 8, h->stream));
+    HIP_TRY(h, hipMemsetAsync(counts, 0, CX_TYPES * 4, h->stream));
+    HIP_TRY(h, hipMemsetAsync(ctr, 0, sizeof(CxCounters), h->stream));
+    const dim3 g(cx_grid(h)), b(BLOCK);
+    GD_TRY(launch(h, "k_cx_types", g, b, 0, k_cx_types, (const Slot*)h->slots, cap, types, counts, ctr));
+    CxCounters c{};
+    unsigned long long ht[CX_TYPES];
+    uint32_t hc[CX_TYPES];
+    HIP_TRY(h, hipMemcpyAsync(&c, ctr, sizeof c, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(ht, types, sizeof ht, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipMemcpyAsync(hc, counts, sizeof hc, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    std::vector<std::pair<uint32_t, unsigned long long>> by_count;
+    for (uint32_t t = 0; t < CX_TYPES; ++t)
+        if (ht[t] != CX_NO_TYPE) by_count.emplace_back(hc[t], ht[t]);
+    std::stable_sort(by_count.begin(), by_count.end(),
+                     [](const auto& x, const auto& y) { return x.first > y.first; });
+    uint32_t n8 = (uint32_t)std::min<size_t>(CX8_TYPES, by_count.size());
+    uint32_t ab = std::max<uint32_t>(2, bit_len((uint64_t)c.act_max + 2));
+    const uint32_t sb = std::max<uint32_t>(1, bit_len((uint64_t)c.silo_max + 1));
+    for (;;) {
+        const uint32_t tb = n8 > 1 ? bit_len(n8 - 1) : 0;
+        if (ab + sb + tb <= 31) break;
+        if (tb > 0) {
+            n8 = 1u << (tb - 1);                       // fewer types before narrower activations
+            continue;
+        }
+        ab = sb + tb >= 29 ? 0 : 31 - sb - tb;
+        break;
+    }
+    Cx8Args p8{};
+    p8.slots = (const uint4*)h->cx8_tab.p;
+    p8.cap = cap;
+    p8.ntypes = n8;
+    for (uint32_t k = 0; k < n8; ++k) p8.tcd[k] = by_count[k].second;
+    p8.ab = ab;
+    p8.sb = sb;
+    h->cx8_layout = p8;
+    h->cx8_ok = ab >= 2;
+    uint32_t held8 = 0;
+    for (uint32_t k = 0; k < n8; ++k) held8 += by_count[k].first;
+    h->cx_held8_at = held8;
+    GD_TRY(launch(h, "k_cx_project", g, b, 0, k_cx_project, (const Slot*)h->slots, cap, cx_build_args(h), ctr));
+    HIP_TRY(h, hipMemcpyAsync(&h->cx_ctr_host, ctr, sizeof(CxCounters), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(h, hipStreamSynchronize(h->stream));
+    h->cx_ok = true;
+    h->cx_built = true;
+    h->cx_out8_at = h->cx_ctr_host.out8;              // the build's own: the baseline of the rebuild rule
+    h->cx_builds++;
+    h->cx_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return GD_OK;
+}
+
+// Re-projects the slots a directory batch touched (slot_of[n]) when the indexes were current before it.
+// Only enqueued: its counters come back with the next pull_counters, and when the batches' new entries
+// no longer fit the 8-B layout (a new grain class, wider activations or silos) beyond an eighth of the
+// entries it held, cx_ensure rebuilds with a new layout.
+int cx_sync(gd_handle* h, TabTrack& tt, const uint32_t* slot_of, uint32_t n) {
+    tt.synced = true;
+    if (!tt.was_current || n == 0) return GD_OK;   // a stale index stays stale: the next large route rebuilds
+    GD_TRY(launch(h, "k_cx_sync", dim3(blocks_for(n, BLOCK)), dim3(BLOCK), 0, k_cx_sync, slot_of, n,
+                  (const Slot*)h->slots, cx_build_args(h), (CxCounters*)h->cxi_ctr.p));
+    h->cx_synced += n;
+    return GD_OK;
+}
+
+// The index for the current table: rebuilt (two streaming passes + one host sync) when the table
+// changed since the last build by a write that did not re-project its slots (gd_dir_rehash, clear,
+// merge, silo removal, split, handoff); false when GD_OPT_PROBE = 0.  n: the messages of the launch
+// asking.  A stale index is rebuilt only for a launch of at least capacity / 16 messages: a small route
+// after such a change takes the directory probe instead of a full-table pass and a host sync (ADVICE
+// r03); the next large launch rebuilds.
 int cx_ensure(gd_handle* h, bool* ok, uint64_t n) {
     *ok = false;
-    if (!h->cx_mode || !h->slots || h->capacity < CX_GROUP) return GD_OK;
+    if (!h->cx_mode || !h->slots || h->capacity < CX8_GROUP) return GD_OK;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;   // a captured graph keeps the directory probe
     HIP_TRY(h, hipStreamIsCapturing(h->stream, &cs));
     if (cs != hipStreamCaptureStatusNone) return GD_OK;
-    if (h->cx_built && h->cx_slots_at == h->slots && h->cx_cap_at == h->capacity * h->cx_scale &&
-        h->cx_gen_at == h->tab_gen) {
-        *ok = h->cx_ok;
-        return GD_OK;
+    if (cx_current(h)) {
+        const CxCounters& c = h->cx_ctr_host;
+        if (!(h->cx8_ok && c.out8 > h->cx_out8_at && c.out8 - h->cx_out8_at > h->cx_held8_at / 8 + 4096)) {
+            *ok = h->cx_ok;
+            return GD_OK;
+        }
+        h->tab_gen++;                               // the 8-B layout no longer fits the directory: rebuild
     }
     if (h->cx_mode == 1 && n < h->capacity / 16) return GD_OK;
-    const unsigned long long cap = h->capacity * h->cx_scale;
-    GD_TRY(ensure(h, h->cxi_tab, cap * 16));
-    GD_TRY(ensure(h, h->cxi_types, CX_TYPES * 8));
-    GD_TRY(ensure(h, h->cxi_ctr, sizeof(CxCounters)));
-    HIP_TRY(h, hipMemsetAsync(h->cxi_tab.p, 0, cap * 16, h->stream));
-    HIP_TRY(h, hipMemsetAsync(h->cxi_types.p, 0xFF, CX_TYPES * 8, h->stream));
-    HIP_TRY(h, hipMemsetAsync(h->cxi_ctr.p, 0, sizeof(CxCounters), h->stream));
-    const dim3 g(blocks_for(h->capacity, BLOCK)), b(BLOCK);
-    GD_TRY(launch(h, "k_cx_types", g, b, 0, k_cx_types, (const Slot*)h->slots, (unsigned long long)h->capacity,
-                  (unsigned long long*)h->cxi_types.p, (CxCounters*)h->cxi_ctr.p));
-    GD_TRY(launch(h, "k_cx_build", g, b, 0, k_cx_build, (const Slot*)h->slots, (unsigned long long)h->capacity,
-                  (const unsigned long long*)h->cxi_types.p, (uint4*)h->cxi_tab.p, cap, (CxCounters*)h->cxi_ctr.p));
-    CxCounters c{};
-    unsigned long long types[CX_TYPES];
-    HIP_TRY(h, hipMemcpyAsync(&c, h->cxi_ctr.p, sizeof c, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(h, hipMemcpyAsync(types, h->cxi_types.p, sizeof types, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(h, hipStreamSynchronize(h->stream));
-    h->cx_built = true;
-    h->cx_ok = c.flag == 0 && c.full == 0;
-    // the 8-B index: one type, every N1 < 2^32, activation bits ab (all ones left for GD_ACT_MULTI) and
-    // silo + 1 above them in a u32
-    h->cx8_ok = false;
-    uint32_t ntypes = 0;
-    for (unsigned long long t : types)
-        if (t != CX_NO_TYPE) {
-            ++ntypes;
-            h->cx8_tcd = t;
-        }
-    uint32_t ab = 1;
-    while (ab < 32 && ((uint64_t)c.act_max + 1) >> ab) ++ab;          // act_max < 2^ab - 1
-    const bool fits = ab < 32 && (((uint64_t)c.silo_max + 1) >> (32 - ab)) == 0;
-    h->cx8_ab = ab;
-    if (h->cx_ok && c.flag8 == 0 && ntypes == 1 && fits) {
-        // as many 8-B slots as the 16-B index (half its bytes).  Both neighbours measured slower: sized for
-        // the live entries at load 0.75, cfg 3's k_route 0.87 -> 1.13 ms (longer probe chains past a
-        // group's 8 slots), cfg 4 1.93 -> 1.95 ms a cascade; twice the slots, k_route 0.86 -> 1.53 ms at
-        // cfg 3 and 0.287 -> 0.314 at cfg 2 (a 4-GB index: the hot set over more lines and pages)
-        // (profiles/r05_cx8_load_ab.txt, r05_cx8_scale_ab.txt)
-        const unsigned long long cap8 = cap;
-        h->cx8_cap = cap8;
-        GD_TRY(ensure(h, h->cx8_tab, cap8 * 8));
-        HIP_TRY(h, hipMemsetAsync(h->cx8_tab.p, 0, cap8 * 8, h->stream));
-        GD_TRY(launch(h, "k_cx8_build", g, b, 0, k_cx8_build, (const Slot*)h->slots, (unsigned long long)h->capacity,
-                      (unsigned long long*)h->cx8_tab.p, cap8, ab, (CxCounters*)h->cxi_ctr.p));
-        HIP_TRY(h, hipMemcpyAsync(&c, h->cxi_ctr.p, sizeof c, hipMemcpyDeviceToHost, h->stream));
-        HIP_TRY(h, hipStreamSynchronize(h->stream));
-        h->cx8_ok = c.full8 == 0;
-        h->cx8_rounds = c.max_rounds8;
-    }
+    GD_TRY(cx_build(h));
     for (auto& kt : h->cx_tune) {                   // a new table: measure the probes again (not the bucketing)
         if (kt.first / (64 * 32) == GD_TUNE_BUCKET) continue;
         auto& t = kt.second;
@@ -224,9 +302,8 @@ int cx_ensure(gd_handle* h, bool* ok, uint64_t n) {
         t.pick = -1;
         t.round = 0;
     }
-    h->cx_rounds = c.max_rounds;
     h->cx_slots_at = h->slots;
-    h->cx_cap_at = cap;
+    h->cx_cap_at = h->capacity;
     h->cx_gen_at = h->tab_gen;
     *ok = h->cx_ok;
     return GD_OK;
@@ -336,13 +413,10 @@ int cx_choose(gd_handle* h, int kind, uint64_t n, int* meas, int nvar) {
 }
 
 
-Cx8Args cx8_args(gd_handle* h) {
-    return Cx8Args{(const uint4*)h->cx8_tab.p, h->cx8_cap, h->cx8_tcd, h->cx8_rounds, h->cx8_ab};
-}
+Cx8Args cx8_args(gd_handle* h) { return h->cx8_layout; }
 
 CxArgs cx_args(gd_handle* h) {
-    return CxArgs{(const uint4*)h->cxi_tab.p, h->capacity * h->cx_scale, (const unsigned long long*)h->cxi_types.p,
-                  h->cx_rounds};
+    return CxArgs{(const uint4*)h->cxi_tab.p, h->capacity, (const unsigned long long*)h->cxi_types.p};
 }
 
 // ---- route -------------------------------------------------------------------
@@ -388,7 +462,7 @@ int route_n1_mode(gd_handle* h, const gd_key* k, uint32_t n1w, uint64_t tcd, uin
     CxMeasure m(h, meas, n);
     // the N1 stream non-temporal under route_mode's rule (world-1 exchange pipeline: 0.5791 -> 0.5773 ms,
     // profiles/r05_route_n1_nt_ab.txt)
-    const bool nt = (uint64_t)h->cx8_cap * 8u <= ROUTE_NT_INDEX_BYTES;
+    const bool nt = (uint64_t)h->capacity * 8u <= ROUTE_NT_INDEX_BYTES;
     if (var == 3 && nt && n1w == 4)
         return launch(h, "k_route", g, b, ring_lds(h), k_route_m<MODE, 1, true, 4, false, (int)CX_GROUP, true>, k, n,
                       ring_args(h), table_args(h), silo, act, status, tcd, xcd, rcnt, world, src, CxArgs{},
@@ -480,7 +554,7 @@ int route_region_device(gd_handle* h, const void* k, uint32_t n1w, uint64_t tcd,
 // temporally either way: the bucketing's histogram reads it next.
 template <int MODE>
 int route_mode(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
-    const uint64_t index_bytes = h->cx8_tab.p ? (uint64_t)h->cx8_cap * 8u : (uint64_t)h->capacity * 8u;
+    const uint64_t index_bytes = (uint64_t)h->capacity * 8u;
     if (index_bytes <= ROUTE_NT_INDEX_BYTES) return route_launch<MODE, 1, true>(h, keys, n, silo, act, status);
     return route_launch<MODE, 2, false>(h, keys, n, silo, act, status);
 }
@@ -980,9 +1054,22 @@ int sync_checked(gd_handle* h) {
         GD_TRY(sync(h));
         if (e == ERR_CTX_RANGE)
             return set_err(h, GD_EINVAL, "an ActivationDirectory entry's context index is not below n_ctx");
+        if (e & ERR_UNSETTLED)
+            return set_err(h, GD_ETIMEOUT, "an asynchronous registration's claims did not settle (device bits 0x%x)", e);
         return set_err(h, GD_EFULL, "device error bits 0x%x", e);
     }
     return GD_OK;
+}
+
+// maybe_grow_table without the read-back while the last copy of the counters is current (no untracked
+// table write since) and, with every asynchronous registration since counted as new entries, the table
+// stays at load <= 0.75.
+int maybe_grow_async(gd_handle* h, uint64_t incoming) {
+    if (!h->ctr_stale) {
+        const unsigned long long used = h->ctr_host.live + h->ctr_host.tomb + h->pending_in + incoming;
+        if (used * 4 <= h->capacity * 3) return GD_OK;
+    }
+    return maybe_grow_table(h, incoming);
 }
 
 int maybe_grow_table(gd_handle* h, uint64_t incoming) {

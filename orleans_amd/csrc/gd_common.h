@@ -126,8 +126,14 @@ GD_HD uint32_t fmix32(uint32_t h) {
 #endif
 constexpr uint32_t SLOT_GROUP = GD_SLOT_GROUP;
 static_assert((SLOT_GROUP & (SLOT_GROUP - 1)) == 0 && SLOT_GROUP <= 1024, "slot group: a power of two <= 1024");
+// Homes are aligned to HOME_ALIGN slots (round 6): the compact probe indexes mirror the table slot for
+// slot (gd_cx.h), and an 8-B index reads 8 slots (one 64-B atom) a round, so a home at the start of its
+// atom lets the first read cover the 8 slots a grain can first sit in -- the layout the round-4/5 index
+// had when it was placed by CAS (exact homes in the mirror: cfg 2 k_route 0.285 -> 0.397 ms, most waves
+// waiting for a second read).  The directory's own probe still reads SLOT_GROUP slots a round.
+constexpr uint32_t HOME_ALIGN = SLOT_GROUP > 8 ? SLOT_GROUP : 8;
 GD_HD unsigned long long home_slot(uint32_t h, unsigned long long mask) {
-    return (((unsigned long long)fmix32(h) * (mask + 1ull)) >> 32) & ~(unsigned long long)(SLOT_GROUP - 1);
+    return (((unsigned long long)fmix32(h) * (mask + 1ull)) >> 32) & ~(unsigned long long)(HOME_ALIGN - 1);
 }
 constexpr uint32_t N_REGIONS = 8;
 GD_HD uint32_t grain_region(uint32_t h) { return fmix32(h) >> 29; }

@@ -1,14 +1,18 @@
-// gd_cx.h -- builds the compact probe index (gd_kernels.h, CxArgs) from the directory table.
+// gd_cx.h -- builds and maintains the compact probe indexes (gd_kernels.h CxArgs, Cx8Args).
 //
-// The index is derived state: the library rebuilds it on the first route after any change of the
-// directory table (a launch that takes the table as a writable Slot*, a clear, a rehash), so every
-// directory operation keeps its semantics on the authoritative 32-B-slot table and the probe reads
-// the copy.  Two passes over the table:
-//   k_cx_types  eligibility (every live entry has N0 = 0) and the set of distinct TypeCodeData
-//               (at most CX_TYPES, open addressing, CAS-inserted);
-//   k_cx_build  each live entry into the index at cx_home(uniform hash), first free slot in probe
-//               order (CAS on the meta word), and the largest group distance any entry sits at.
-// A directory with N0 != 0 keys or more than CX_TYPES types is left to the directory probe.
+// The indexes are derived state: index slot j is a narrow projection of directory table slot j
+// (round 6), so every directory operation keeps its semantics on the authoritative 32-B-slot table
+// and the probe reads the copy.
+//   k_cx_types    one pass over the table: the set of distinct TypeCodeData of N0 = 0 entries with a
+//                 count each (per-workgroup LDS sets, one global insert per type and workgroup), the
+//                 largest activation and silo, the entries no index can hold (N0 != 0) and those the
+//                 8-B index cannot (N1 >= 2^32).  The host picks the 8-B layout from them.
+//   k_cx_project  one streaming pass: every table slot -> its 16-B and 8-B index slots (the full build).
+//   k_cx_sync     the slots one directory batch touched (register, upsert, unregister) re-projected
+//                 in place: the directory change costs a pass over the batch, not over the table
+//                 (GrainDirectoryPartition.AddSingleActivation / RemoveActivation are O(1) dictionary
+//                 operations, GrainDirectoryPartition.cs:304-363, and activations register all the
+//                 time, Catalog.cs:540-552).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -19,122 +23,240 @@
 
 namespace gd {
 
+// An 8-B slot that matches no key but keeps probe chains going: y = 1 (u = 0), x = 0.
+constexpr unsigned long long CX8_HOLE = 1ull << 32;
+
 struct CxCounters {
-    uint32_t flag;         // bit 0: an entry with N0 != 0; bit 1: more than CX_TYPES types
-    uint32_t max_rounds;   // CxArgs::max_rounds
-    uint32_t full;         // the index ran out of slots (cannot happen at cap >= live)
-    uint32_t flag8;        // the 8-B index: bit 0 an N1 >= 2^32 (one type more: the host counts them)
-    uint32_t max_rounds8;  // Cx8Args::max_rounds
-    uint32_t full8;
+    uint32_t n0_live;      // live entries with N0 != 0 (directory probe only)
+    uint32_t big_n1;       // live N0 = 0 entries with N1 >= 2^32 (not in the 8-B index)
+    uint32_t types_full;   // a type did not fit the 256-slot set (its entries: directory probe)
     uint32_t act_max;      // the largest activation (GD_ACT_MULTI aside) and silo: the host's bit split
     uint32_t silo_max;
+    uint32_t out8;         // projections (build and sync) the 8-B index does not hold or redirects
+    uint32_t pad[2];
 };
 
-static __global__ void __launch_bounds__(BLOCK) k_cx_types(const Slot* __restrict__ slots, unsigned long long cap,
-                                                    unsigned long long* types, CxCounters* ctr) {
-    const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
-    if (j >= cap) return;
-    const uint4* q = reinterpret_cast<const uint4*>(slots + j);
-    const uint4 a = q[0], b = q[1];
-    if (slot_state(b.w) != SLOT_LIVE) return;
-    if ((a.x | a.y) != 0) {
-        atomicOr(&ctr->flag, 1u);
-        return;
-    }
-    if (a.w != 0) atomicOr(&ctr->flag8, 1u);
-    if (b.z != GD_ACT_MULTI) atomicMax(&ctr->act_max, b.z);
-    atomicMax(&ctr->silo_max, slot_silo(b.w));
-    const unsigned long long tcd = (unsigned long long)b.x | ((unsigned long long)b.y << 32);
-    // one insert per distinct type in the wave: lanes holding the first lane's type stand down
-    const unsigned long long lead = __shfl(tcd, __ffsll((long long)__ballot(1)) - 1);
-    const bool is_lead = (threadIdx.x & (WAVE - 1)) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1);
-    if (tcd == lead && !is_lead) return;
+// ---- type sets ------------------------------------------------------------------
+// Global type set (CX_TYPES u64 slots, CX_NO_TYPE empty) with a count per slot: insert tcd, add c.
+__device__ __forceinline__ int cx_type_add(unsigned long long* types, uint32_t* count, uint64_t tcd, uint32_t c,
+                                           CxCounters* ctr) {
     uint32_t t = cx_type_home(tcd);
     for (uint32_t k = 0; k < CX_TYPES; ++k) {
         unsigned long long cur = __hip_atomic_load(types + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == tcd) return;
-        if (cur == CX_NO_TYPE) {
-            cur = atomicCAS(types + t, CX_NO_TYPE, tcd);
-            if (cur == CX_NO_TYPE || cur == tcd) return;
+        if (cur == CX_NO_TYPE) cur = atomicCAS(types + t, CX_NO_TYPE, (unsigned long long)tcd);
+        if (cur == CX_NO_TYPE || cur == tcd) {
+            if (count && c) atomicAdd(count + t, c);
+            return (int)t;
         }
         t = (t + 1) & (CX_TYPES - 1);
     }
-    atomicOr(&ctr->flag, 2u);
+    if (ctr) atomicOr(&ctr->types_full, 1u);
+    return -1;
 }
 
-static __global__ void __launch_bounds__(BLOCK) k_cx_build(const Slot* __restrict__ slots, unsigned long long cap,
-                                                    const unsigned long long* __restrict__ types, uint4* cx,
-                                                    unsigned long long cx_cap, CxCounters* ctr) {
-    if (ctr->flag) return;                             // not eligible (uniform): nothing to build
-    const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
-    uint32_t rounds = 0;
-    bool placed = false, live = false;
-    if (j < cap) {
-        const uint4* q = reinterpret_cast<const uint4*>(slots + j);
-        const uint4 a = q[0], b = q[1];
-        live = slot_state(b.w) == SLOT_LIVE;
-        if (live) {
-            const uint64_t n1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
-            const uint64_t tcd = (uint64_t)b.x | ((uint64_t)b.y << 32);
-            uint32_t t = cx_type_home(tcd);
-            while (types[t] != tcd) t = (t + 1) & (CX_TYPES - 1);     // present: k_cx_types put it there
-            const uint32_t meta = CX_LIVE | (t << 16) | slot_silo(b.w);
-            const unsigned long long home = cx_home(uniform_hash(0, n1, tcd), cx_cap);
-            unsigned long long s = home;
-            for (unsigned long long d = 0; d < cx_cap; ++d) {
-                if (atomicCAS(&cx[s].w, 0u, meta) == 0u) {
-                    cx[s].x = (uint32_t)n1;
-                    cx[s].y = (uint32_t)(n1 >> 32);
-                    cx[s].z = b.z;
-                    rounds = (uint32_t)((s >= home ? s - home : s + cx_cap - home) / CX_GROUP);
-                    placed = true;
-                    break;
-                }
-                s = s + 1 == cx_cap ? 0 : s + 1;
-            }
-            if (!placed) atomicOr(&ctr->full, 1u);
+// Workgroup type set in LDS (CXT_LDS slots): a run of c entries of type tcd; a full set spills to the
+// global one.
+constexpr uint32_t CXT_LDS = 64;
+__device__ __forceinline__ void cx_type_note(unsigned long long* s_t, uint32_t* s_c, uint64_t tcd, uint32_t c,
+                                             unsigned long long* types, uint32_t* count, CxCounters* ctr) {
+    uint32_t t = cx_type_home(tcd) & (CXT_LDS - 1);
+    for (uint32_t k = 0; k < CXT_LDS; ++k) {
+        unsigned long long cur = __hip_atomic_load(s_t + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == CX_NO_TYPE) cur = atomicCAS(s_t + t, CX_NO_TYPE, (unsigned long long)tcd);
+        if (cur == CX_NO_TYPE || cur == tcd) {
+            atomicAdd(s_c + t, c);
+            return;
         }
+        t = (t + 1) & (CXT_LDS - 1);
     }
-    // one atomicMax per wave on the shared counter (one per entry serialises a million of them);
-    // every lane of the wave takes part in the reduction
-    for (int off = WAVE / 2; off > 0; off >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor(rounds, off, WAVE));
-    if (lane_id() == 0 && rounds) atomicMax(&ctr->max_rounds, rounds);
+    (void)cx_type_add(types, count, tcd, c, ctr);
 }
 
-// The 8-B index (Cx8Args), built after the 16-B one when the host found it eligible (flag8 == 0, one
-// type, activations and silos fitting a u32 together): slot = (silo + 1) << ab | act (all ab bits set
-// for a multi-activation grain) above the N1 low word, placed by a 64-bit CAS in probe order from
-// cx8_home.
-static __global__ void __launch_bounds__(BLOCK) k_cx8_build(const Slot* __restrict__ slots, unsigned long long cap,
-                                                     unsigned long long* cx8, unsigned long long cx8_cap,
-                                                     uint32_t ab, CxCounters* ctr) {
-    const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
-    uint32_t rounds = 0;
-    if (j < cap) {
-        const uint4* q = reinterpret_cast<const uint4*>(slots + j);
-        const uint4 a = q[0], b = q[1];
-        if (slot_state(b.w) == SLOT_LIVE) {
-            const uint64_t n1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
-            const uint64_t tcd = (uint64_t)b.x | ((uint64_t)b.y << 32);
-            const uint32_t am = (1u << ab) - 1u;
-            const uint32_t y = ((slot_silo(b.w) + 1u) << ab) | (b.z == GD_ACT_MULTI ? am : b.z);
-            const unsigned long long v = ((unsigned long long)y << 32) | (uint32_t)n1;
-            const unsigned long long home = cx8_home(uniform_hash(0, n1, tcd), cx8_cap);
-            unsigned long long s = home;
-            bool placed = false;
-            for (unsigned long long d = 0; d < cx8_cap; ++d) {
-                if (atomicCAS(cx8 + s, 0ull, v) == 0ull) {
-                    rounds = (uint32_t)((s >= home ? s - home : s + cx8_cap - home) / CX8_GROUP);
-                    placed = true;
-                    break;
-                }
-                s = s + 1 == cx8_cap ? 0 : s + 1;
+constexpr int CXT_IT = 4;   // table slots a thread reads per round (all in flight)
+
+// Grid-stride over the table, CXT_IT coalesced slots a thread a round.  Per workgroup: the types in LDS
+// (a thread folds runs of one type before touching LDS), counters reduced, then one global update each.
+static __global__ void __launch_bounds__(BLOCK) k_cx_types(const Slot* __restrict__ slots, unsigned long long cap,
+                                                    unsigned long long* types, uint32_t* count, CxCounters* ctr) {
+    __shared__ unsigned long long s_t[CXT_LDS];
+    __shared__ uint32_t s_c[CXT_LDS];
+    __shared__ uint32_t s_red[4][BLOCK / WAVE];
+    for (uint32_t k = threadIdx.x; k < CXT_LDS; k += BLOCK) {
+        s_t[k] = CX_NO_TYPE;
+        s_c[k] = 0;
+    }
+    __syncthreads();
+    uint32_t n0c = 0, bigc = 0, amax = 0, smax = 0, run_c = 0;
+    unsigned long long run_t = CX_NO_TYPE;
+    const unsigned long long stride = (unsigned long long)gridDim.x * BLOCK * CXT_IT;
+    for (unsigned long long base = (unsigned long long)blockIdx.x * BLOCK * CXT_IT + threadIdx.x; base < cap;
+         base += stride) {
+        uint4 a[CXT_IT], b[CXT_IT];
+#pragma unroll
+        for (int r = 0; r < CXT_IT; ++r) {
+            const unsigned long long j = base + (unsigned long long)r * BLOCK;
+            b[r] = make_uint4(0, 0, 0, 0);
+            if (j < cap) {
+                const uint4* q = reinterpret_cast<const uint4*>(slots + j);
+                a[r] = q[0];
+                b[r] = q[1];
             }
-            if (!placed) atomicOr(&ctr->full8, 1u);
+        }
+#pragma unroll
+        for (int r = 0; r < CXT_IT; ++r) {
+            if (slot_state(b[r].w) != SLOT_LIVE) continue;
+            if ((a[r].x | a[r].y) != 0) {
+                ++n0c;
+                continue;
+            }
+            if (a[r].w != 0) ++bigc;
+            if (b[r].z != GD_ACT_MULTI) amax = max(amax, b[r].z);
+            smax = max(smax, slot_silo(b[r].w));
+            const unsigned long long tcd = (unsigned long long)b[r].x | ((unsigned long long)b[r].y << 32);
+            if (tcd != run_t) {
+                if (run_c) cx_type_note(s_t, s_c, run_t, run_c, types, count, ctr);
+                run_t = tcd;
+                run_c = 0;
+            }
+            ++run_c;
         }
     }
-    for (int off = WAVE / 2; off > 0; off >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor(rounds, off, WAVE));
-    if (lane_id() == 0 && rounds) atomicMax(&ctr->max_rounds8, rounds);
+    if (run_c) cx_type_note(s_t, s_c, run_t, run_c, types, count, ctr);
+    // workgroup reductions: wave shuffles, then LDS
+    for (int off = WAVE / 2; off > 0; off >>= 1) {
+        n0c += __shfl_xor(n0c, off, WAVE);
+        bigc += __shfl_xor(bigc, off, WAVE);
+        amax = max(amax, (uint32_t)__shfl_xor(amax, off, WAVE));
+        smax = max(smax, (uint32_t)__shfl_xor(smax, off, WAVE));
+    }
+    const uint32_t w = threadIdx.x / WAVE;
+    if ((threadIdx.x & (WAVE - 1)) == 0) {
+        s_red[0][w] = n0c;
+        s_red[1][w] = bigc;
+        s_red[2][w] = amax;
+        s_red[3][w] = smax;
+    }
+    __syncthreads();                                   // also: every cx_type_note of the workgroup is done
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < BLOCK / WAVE; ++k) {
+            n0c += s_red[0][k];
+            bigc += s_red[1][k];
+            amax = max(amax, s_red[2][k]);
+            smax = max(smax, s_red[3][k]);
+        }
+        if (n0c) atomicAdd(&ctr->n0_live, n0c);
+        if (bigc) atomicAdd(&ctr->big_n1, bigc);
+        if (amax) atomicMax(&ctr->act_max, amax);
+        if (smax) atomicMax(&ctr->silo_max, smax);
+    }
+    for (uint32_t k = threadIdx.x; k < CXT_LDS; k += BLOCK)
+        if (s_t[k] != CX_NO_TYPE) (void)cx_type_add(types, count, s_t[k], s_c[k], ctr);
+}
+
+// ---- projection -------------------------------------------------------------------
+struct CxBuild {
+    uint4* cx16;                   // the 16-B index (null: not kept)
+    unsigned long long* types;     // its global type set (staged in LDS by the kernels below)
+    unsigned long long* cx8;       // the 8-B index (null: not kept)
+    Cx8Args p8;                    // its layout (types, ab, sb)
+};
+
+__device__ __forceinline__ void cx_stage_types(const unsigned long long* types, unsigned long long* s_types) {
+    for (uint32_t t = threadIdx.x; t < CX_TYPES; t += blockDim.x) s_types[t] = types[t];
+    __syncthreads();
+}
+
+// Table slot j (a, b: its two halves) -> index slot j.  add_types (k_cx_sync): a type the staged set
+// lacks is looked up / inserted in the global set (a batch may register a new grain class).
+// Returns whether the 8-B index holds the entry (false for a live entry it does not hold or redirects).
+__device__ __forceinline__ bool cx_project(const uint4 a, const uint4 b, unsigned long long j, const CxBuild& B,
+                                           const unsigned long long* s_types, bool add_types) {
+    const uint32_t st = slot_state(b.w);
+    uint4 v16 = make_uint4(0, 0, 0, 0);
+    unsigned long long v8 = 0;
+    bool held8 = true;
+    if (st == SLOT_LIVE) {
+        const uint64_t n0 = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        const uint64_t n1 = (uint64_t)a.z | ((uint64_t)a.w << 32);
+        const uint64_t tcd = (uint64_t)b.x | ((uint64_t)b.y << 32);
+        const uint32_t act = b.z, silo = slot_silo(b.w);
+        if (B.cx16) {
+            int t = n0 == 0 ? cx_type_index(s_types, tcd) : -1;
+            if (t < 0 && n0 == 0 && add_types) t = cx_type_add(B.types, nullptr, tcd, 0, nullptr);
+            v16 = t >= 0 ? make_uint4(a.z, a.w, act, CX_LIVE | ((uint32_t)t << 16) | silo) : make_uint4(0, 0, 0, CX_TOMB);
+        }
+        if (B.cx8) {
+            const int t8 = cx8_type(B.p8, n0, n1, tcd);
+            if (t8 < 0) {
+                v8 = CX8_HOLE;                                     // not held: its key probes the directory
+                held8 = false;
+            } else {
+                const uint32_t ab = B.p8.ab, sb = B.p8.sb;
+                const uint32_t am = (1u << ab) - 1u, umax = ~0u >> ab;
+                uint32_t u = ((uint32_t)t8 << sb) | (silo + 1u);
+                if (((silo + 1u) >> sb) != 0 || u >= umax) u = umax;   // redirect: silo / type too wide
+                uint32_t av = act == GD_ACT_MULTI ? am : act;
+                if (act != GD_ACT_MULTI && act >= am - 1u) av = am - 1u;   // redirect: activation too wide
+                held8 = u != umax && av != am - 1u;
+                v8 = ((unsigned long long)((u << ab) | av) << 32) | a.z;
+            }
+        }
+    } else if (st != SLOT_EMPTY) {
+        v16 = make_uint4(0, 0, 0, CX_TOMB);
+        v8 = CX8_HOLE;
+    }
+    if (B.cx16) B.cx16[j] = v16;
+    if (B.cx8) B.cx8[j] = v8;
+    return held8;
+}
+
+// The full build: every table slot, grid-stride, CXT_IT slots a thread a round.
+static __global__ void __launch_bounds__(BLOCK) k_cx_project(const Slot* __restrict__ slots, unsigned long long cap,
+                                                      CxBuild B, CxCounters* ctr) {
+    __shared__ unsigned long long s_types[CX_TYPES];
+    cx_stage_types(B.types, s_types);
+    uint32_t out8 = 0;
+    const unsigned long long stride = (unsigned long long)gridDim.x * BLOCK * CXT_IT;
+    for (unsigned long long base = (unsigned long long)blockIdx.x * BLOCK * CXT_IT + threadIdx.x; base < cap;
+         base += stride) {
+        uint4 a[CXT_IT], b[CXT_IT];
+#pragma unroll
+        for (int r = 0; r < CXT_IT; ++r) {
+            const unsigned long long j = base + (unsigned long long)r * BLOCK;
+            if (j < cap) {
+                const uint4* q = reinterpret_cast<const uint4*>(slots + j);
+                a[r] = q[0];
+                b[r] = q[1];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < CXT_IT; ++r) {
+            const unsigned long long j = base + (unsigned long long)r * BLOCK;
+            if (j < cap && !cx_project(a[r], b[r], j, B, s_types, false)) ++out8;
+        }
+    }
+    for (int off = WAVE / 2; off > 0; off >>= 1) out8 += __shfl_xor(out8, off, WAVE);
+    if ((threadIdx.x & (WAVE - 1)) == 0 && out8) atomicAdd(&ctr->out8, out8);
+}
+
+// Incremental: the table slots a directory batch touched (slot_of[i]; NONE32 / SLOT_RETRY: none),
+// re-projected after the batch's last table write.  Duplicates are harmless (a projection is a function
+// of the table slot).
+static __global__ void __launch_bounds__(BLOCK) k_cx_sync(const uint32_t* __restrict__ slot_of, uint32_t n,
+                                                   const Slot* __restrict__ slots, CxBuild B, CxCounters* ctr) {
+    __shared__ unsigned long long s_types[CX_TYPES];
+    cx_stage_types(B.types, s_types);
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    bool out = false;
+    if (i < n) {
+        const uint32_t s = slot_of[i];
+        if (s < SLOT_RETRY) {
+            const uint4* q = reinterpret_cast<const uint4*>(slots + s);
+            out = !cx_project(q[0], q[1], s, B, s_types, true);
+        }
+    }
+    const unsigned long long m = __ballot(out);
+    if (lane_id() == 0 && m) atomicAdd(&ctr->out8, (uint32_t)__popcll(m));
 }
 
 }  // namespace gd

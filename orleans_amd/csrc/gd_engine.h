@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -79,6 +80,9 @@ struct gd_handle {
     unsigned long long capacity = 0;
     DevCounters* ctr = nullptr;       // device
     DevCounters ctr_host{};           // last copy
+    bool ctr_stale = true;            // an untracked table write since the last copy (maybe_grow_async pulls)
+    uint64_t pending_in = 0;          // entries asynchronous registrations may have added since the last copy
+    DevBuf reg_retry;                 // asynchronous registrations: deferred-claim counts of the gated passes
 
     // scratch
     DevBuf keys_in, u32_a, u32_b, u32_c, u32_d, u8_a, out_a, out_b, out_c, hist, partials, partials2, offs;
@@ -145,6 +149,8 @@ struct gd_handle {
     // b_ev on the handle's stream), so the next batch's route overlaps this batch's bucketing
     hipStream_t bstream = nullptr;
     hipEvent_t b_ev = nullptr;
+    hipEvent_t b_fence_ev = nullptr;  // bfence: the handle's stream waits for a bucketing on bstream
+    bool b_pending = false;           // a bucketing was enqueued on bstream since the last bfence
     hipEvent_t fan_ev = nullptr;   // the cascade's per-hop size read-back (fan_count_post / fan_count_wait)
     hipStream_t pstream = nullptr;    // the partition (pack) of the next batch, beside this one's rounds
     hipEvent_t x_in = nullptr, x_hdr[2] = {}, x_route[2] = {}, x_ret[2] = {}, x_done[2] = {};
@@ -199,7 +205,6 @@ struct gd_handle {
     uint32_t n_cu = 256;        // compute units (hipDeviceProp_t::multiProcessorCount): persistent grids
     DevBuf m3[15];              // three-pass form's scratch (msd3_bucket)
     DevBuf tune_buf;            // gd_tune_agree's send / receive records
-    uint32_t cx_scale = 1;      // index slots = cx_scale x table capacity (GD_CX_SCALE, 1 or 2)
     // per launch kind and size class: the probe variant, timed on live launches.  Variants: 0 the index
     // in 64-B group reads, 1 the directory, 2 the index in 16-B slot reads, 3 the 8-B index (24-B keys)
     static constexpr int CXV = 4;
@@ -213,17 +218,19 @@ struct gd_handle {
         uint64_t n[CXV] = {};
     };
     std::map<int, CxTune> cx_tune;   // key: (kind * 64 + size class (bit length of n)) * 32 + a second class
-    uint64_t tab_gen = 0;       // bumped by every launch that takes the table as a writable Slot*
+    uint64_t tab_gen = 0;       // bumped by every launch that takes the table as a writable Slot* (untracked)
+    uint32_t tab_track = 0;     // > 0: inside a directory batch that re-projects its slots (TabTrack, k_cx_sync)
     bool cx_built = false, cx_ok = false;
     const Slot* cx_slots_at = nullptr;
     uint64_t cx_cap_at = 0, cx_gen_at = 0;
-    uint32_t cx_rounds = 0;
-    DevBuf cxi_tab, cxi_types, cxi_ctr;
-    bool cx8_ok = false;        // the 8-B index (gd_cx.h k_cx8_build) is built and current with cx
-    uint32_t cx8_rounds = 0, cx8_ab = 24;
-    unsigned long long cx8_cap = 0;   // the 8-B index's slots (cx_ensure: sized for the live entries)
-    uint64_t cx8_tcd = 0;
+    DevBuf cxi_tab, cxi_types, cxi_ctr;   // 16-B index; its type set (+ a count per slot); CxCounters
+    bool cx8_ok = false;        // the 8-B index is built and current with cx
+    Cx8Args cx8_layout{};       // its layout (types, bits), fixed at the build
     DevBuf cx8_tab;
+    CxCounters cx_ctr_host{};   // the last read-back of the index counters
+    uint32_t cx_out8_at = 0, cx_held8_at = 0;   // at the build: live entries the 8-B index left out / held
+    uint64_t cx_builds = 0, cx_synced = 0;      // full builds; slots re-projected by k_cx_sync (gd_stats)
+    double cx_build_ms = 0.0;                   // host wall time of the last full build
     uint32_t xcd_tiles = 1;     // XCD-contiguous tile ranges in the radix scatter (GD_XCD_TILES)
     bool hist_xcd = true;       // multi-tile histograms in reverse XCD tile order (GD_HIST_XCD)
     bool compact_headers = true;    // 8-B exchange headers for uniform batches (GD_COMPACT_HEADERS=0: off)
@@ -303,6 +310,9 @@ int alloc_table(gd_handle* h, unsigned long long cap, Slot** out);
 int alloc_vtag(gd_handle* h, unsigned long long cap, uint32_t** out);
 unsigned long long pow2_at_least(unsigned long long x);
 int cx_ensure(gd_handle* h, bool* ok, uint64_t n);
+bool cx_current(const gd_handle* h);
+struct TabTrack;
+int cx_sync(gd_handle* h, TabTrack& tt, const uint32_t* slot_of, uint32_t n);
 int tune_key(int kind, uint64_t n, int sub);
 int tune_nvar(int kind);
 int tune_nvar_now(const gd_handle* h, int kind);
@@ -338,7 +348,10 @@ bool host_pinned(const void* p);
 int route_bucket_host_pipelined(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act, uint32_t* out_silo,
                                 uint32_t* out_act, uint8_t* out_status, uint32_t* out_perm, uint32_t* out_offsets);
 int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t n, gd_val* out_vals,
-                  uint8_t* out_ins);
+                  uint8_t* out_ins, bool async = false);
+int unregister_core(gd_handle* h, const gd_key* dk, const uint32_t* dacts, uint32_t n, uint8_t* out_removed);
+int maybe_grow_async(gd_handle* h, uint64_t incoming);
+int bfence(gd_handle* h);
 int split_count(gd_handle* h, const uint8_t* keep, uint32_t n_keep, uint64_t* total);
 uint64_t grain_tcd(int32_t type_code);
 int fan_count(gd_handle* h, const uint32_t* row_off, uint32_t n_nodes, const uint32_t* frontier, uint32_t nf,
@@ -418,11 +431,15 @@ bool writes_table(const gd_handle*, const T&) { return false; }
 inline bool writes_table(const gd_handle* h, Slot* p) { return p != nullptr && p == h->slots; }
 
 // Launch a kernel on the handle's stream; with GD_CFG_KERNEL_TIMING bracket it by events.  A kernel
-// handed the table as a writable Slot* invalidates the compact probe index (tab_gen).
+// handed the table as a writable Slot* invalidates the compact probe index (tab_gen), unless it runs
+// inside a TabTrack scope, whose batch re-projects the slots it touched (cx_sync).
 template <typename K, typename... Args>
 int launch(gd_handle* h, const char* name, dim3 grid, dim3 block, size_t lds, K kernel, Args... args) {
     if (grid.x == 0) return GD_OK;
-    if ((writes_table(h, args) || ...)) h->tab_gen++;
+    if (!h->tab_track && (writes_table(h, args) || ...)) {
+        h->tab_gen++;
+        h->ctr_stale = true;
+    }
     hipEvent_t a = nullptr, b = nullptr;
     if (h->timing == 1) {
         a = take_event(h);
@@ -456,6 +473,20 @@ struct StageTime {
         if (name < 0) return;
         (void)hipEventRecord(b, h->stream);
         h->pending.push_back(TimedLaunch{name, a, b});
+    }
+};
+
+// A directory batch whose table writes keep the probe indexes current: the slots it touched are
+// re-projected by cx_sync (which calls done()); a batch that ends early (an error) leaves the indexes
+// stale instead, and the next large route rebuilds them.
+struct TabTrack {
+    gd_handle* h;
+    bool was_current;
+    bool synced = false;
+    explicit TabTrack(gd_handle* hh);
+    ~TabTrack() {
+        --h->tab_track;
+        if (!synced) h->tab_gen++;
     }
 };
 

@@ -213,71 +213,47 @@ __device__ __forceinline__ uint8_t route_node(uint32_t node, uint64_t tcd, const
     return GD_ROUTE_MISS;                          // Dispatcher.cs:742 slow path
 }
 
-// The compact probe index's walk (gd_kernels.h CxArgs) from a group already read: the status of
-// GrainId(tcd, n1) given its type's `want` (0x100 | type index; 0: the type holds no entry).
-template <int RG>
-__device__ __forceinline__ uint8_t cx_walk_node(const CxArgs& cx, const TableArgs& tab, uint32_t want, uint64_t n1,
-                                                unsigned long long s, uint4 (&q)[RG], uint32_t& silo,
-                                                uint32_t& act) {
-    const uint32_t bound = (cx.max_rounds + 1) * (CX_GROUP / RG) - 1;   // reads of RG slots
+// The compact probe indexes' walks for GrainId(tcd, node) from the home's group already read
+// (gd_kernels.h cx16_walk / cx8_walk); a key the index does not hold (want 0) or a redirect entry
+// is probed in the directory (route_node).
+template <int MODE, int RG>
+__device__ __forceinline__ uint8_t cx_walk_node(const CxArgs& cx, const TableArgs& tab, uint32_t mp, uint32_t want,
+                                                uint32_t node, uint64_t tcd, unsigned long long s, uint4 (&q)[RG],
+                                                const uint32_t* s_pts, const uint32_t* s_own, const RingArgs& ring,
+                                                uint32_t& silo, uint32_t& act) {
+    if (!want) return route_node<MODE>(node, tcd, s_pts, s_own, ring, tab, lazy_max_probe(tab), silo, act);
     uint8_t st = GD_ROUTE_MISS;
-    bool done = want == 0;
-    for (uint32_t p = 0; !done;) {
-#pragma unroll
-        for (int g = 0; g < RG; ++g) {
-            if (done) continue;
-            const uint4 v = q[g];
-            if (v.w == 0) {
-                done = true;
-            } else if ((v.w >> 16) == want && ((uint64_t)v.x | ((uint64_t)v.y << 32)) == n1) {
-                const bool ok = v.z != GD_ACT_MULTI && tab_silo_valid(tab, slot_silo(v.w));
-                st = v.z == GD_ACT_MULTI ? (uint8_t)GD_ROUTE_MULTI_ACT : (ok ? (uint8_t)GD_ROUTE_OK : st);
-                act = ok ? v.z : act;
-                silo = ok ? slot_silo(v.w) : silo;
-                done = true;
-            }
-        }
-        if (done || ++p > bound) break;
-        s += RG;
-        if (s >= cx.cap) s = 0;
-#pragma unroll
-        for (int g = 0; g < RG; ++g) q[g] = cx.slots[s + g];
-    }
+    cx16_walk<RG>(cx, tab, want, node, s, q, silo, act, st);
     return st;
 }
 
-// The 8-B index's walk (Cx8Args) from a group already read (q: its 8 slots as 4 uint4): as cx_walk_node.
-__device__ __forceinline__ uint8_t cx8_walk_node(const Cx8Args& cx8, const TableArgs& tab, uint32_t key,
-                                                 unsigned long long s, uint4 (&q)[CX8_GROUP / 2], uint32_t& silo,
+template <int MODE>
+__device__ __forceinline__ uint8_t cx8_walk_node(const Cx8Args& cx8, const TableArgs& tab, uint32_t mp, int t8,
+                                                 uint32_t node, uint64_t tcd, unsigned long long s,
+                                                 uint4 (&q)[CX8_GROUP / 2], const uint32_t* s_pts,
+                                                 const uint32_t* s_own, const RingArgs& ring, uint32_t& silo,
                                                  uint32_t& act) {
-    const uint32_t am = (1u << cx8.ab) - 1u;
-    for (uint32_t p = 0;;) {
-#pragma unroll
-        for (int g = 0; g < (int)CX8_GROUP; ++g) {
-            const uint4 v = q[g / 2];
-            const uint32_t x = (g & 1) ? v.z : v.x, y = (g & 1) ? v.w : v.y;
-            if (y == 0) return GD_ROUTE_MISS;
-            if (x == key) {
-                const uint32_t a = y & am, sl = (y >> cx8.ab) - 1u;
-                if (a == am) return GD_ROUTE_MULTI_ACT;
-                if (!tab_silo_valid(tab, sl)) return GD_ROUTE_MISS;
-                act = a;
-                silo = sl;
-                return GD_ROUTE_OK;
-            }
-        }
-        if (++p > cx8.max_rounds) return GD_ROUTE_MISS;
-        s += CX8_GROUP;
-        if (s >= cx8.cap) s = 0;
-        const uint4* qp = cx8.slots + (s >> 1);
-#pragma unroll
-        for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q[g] = qp[g];
-    }
+    uint8_t st = GD_ROUTE_MISS;
+    if (t8 < 0 || cx8_walk(cx8, tab, node, (uint32_t)t8, s, q, silo, act, st))
+        return route_node<MODE>(node, tcd, s_pts, s_own, ring, tab, lazy_max_probe(tab), silo, act);
+    return st;
 }
 
 __device__ __forceinline__ uint32_t cx_want(const CxArgs& cx, uint64_t tcd) {
     const int t = cx_type_index(cx.types, tcd);
     return t < 0 ? 0u : (0x100u | (uint32_t)t);
+}
+// The first read of an index walk: the aligned group holding home slot s.
+template <int RG>
+__device__ __forceinline__ void cx_first(const CxArgs& cx, unsigned long long s, uint4 (&q)[RG]) {
+    const uint4* qp = cx.slots + (s & ~(unsigned long long)(RG - 1));
+#pragma unroll
+    for (int g = 0; g < RG; ++g) q[g] = qp[g];
+}
+__device__ __forceinline__ void cx8_first(const Cx8Args& cx8, unsigned long long s, uint4 (&q)[CX8_GROUP / 2]) {
+    const uint4* qp = cx8.slots + ((s & ~(unsigned long long)(CX8_GROUP - 1)) >> 1);
+#pragma unroll
+    for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q[g] = qp[g];
 }
 
 // Route a batch of node ids (GrainId(typeCode, node), the owner side of the sharded fan-out).
@@ -292,38 +268,31 @@ static __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
     stage_ring(ring, s_pts, s_own);
-    const uint32_t max_probe = (CX || CX8) ? 0u : tab.ctr->max_probe;
+    const uint32_t max_probe = (CX || CX8) ? 0u : tab.ctr->max_probe;   // the index walks read it lazily
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     uint32_t silo, act;
     uint8_t st;
     if constexpr (CX8) {                               // the 8-B index (gd_kernels.h Cx8Args)
-        const bool want = tcd == cx8.tcd;
         const uint32_t node = nodes[i];
+        const int t8 = cx8_type(cx8, 0, node, tcd);
         const uint32_t h = uniform_hash(0, node, tcd);
-        const unsigned long long s0 = cx8_home(h, cx8.cap);
+        const unsigned long long s0 = home_slot(h, tab.mask);
         uint4 q[CX8_GROUP / 2];
-        if (want) {
-            const uint4* qp = cx8.slots + (s0 >> 1);
-#pragma unroll
-            for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q[g] = qp[g];
-        }
+        if (t8 >= 0) cx8_first(cx8, s0, q);
         silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h)];
         act = NONE32;
-        st = want ? cx8_walk_node(cx8, tab, node, s0, q, silo, act) : (uint8_t)GD_ROUTE_MISS;
+        st = cx8_walk_node<MODE>(cx8, tab, max_probe, t8, node, tcd, s0, q, s_pts, s_own, ring, silo, act);
     } else if constexpr (CX) {
         const uint32_t want = cx_want(cx, tcd);
         const uint32_t node = nodes[i];
         const uint32_t h = uniform_hash(0, node, tcd);
-        const unsigned long long s0 = cx_home(h, cx.cap);
+        const unsigned long long s0 = home_slot(h, tab.mask);
         uint4 q[RG];
-        if (want) {
-#pragma unroll
-            for (int g = 0; g < RG; ++g) q[g] = cx.slots[s0 + g];
-        }
+        if (want) cx_first<RG>(cx, s0, q);
         silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h)];
         act = NONE32;
-        st = cx_walk_node<RG>(cx, tab, want, node, s0, q, silo, act);
+        st = cx_walk_node<MODE, RG>(cx, tab, max_probe, want, node, tcd, s0, q, s_pts, s_own, ring, silo, act);
     } else {
         st = route_node<MODE>(nodes[i], tcd, s_pts, s_own, ring, tab, max_probe, silo, act);
     }
@@ -362,7 +331,7 @@ static __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __re
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
     stage_ring(ring, s_pts, s_own);
-    const uint32_t max_probe = tab.ctr->max_probe;
+    const uint32_t max_probe = (CX || CX8) ? 0u : tab.ctr->max_probe;   // the index walks read it lazily
     const uint32_t p1 = min(p0 + TILE, total);
     fan_stage(s, row_off, frontier, n_front, ends, p0, p1);
     for (int it0 = 0; it0 < IT; it0 += ILP) {
@@ -380,26 +349,22 @@ static __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __re
 #pragma unroll
         for (int q = 0; q < ILP; ++q) target[q] = live[q] ? dst[j[q]] : 0u;
         if constexpr (CX8) {                                  // the 8-B index (gd_kernels.h Cx8Args)
-            const bool want = tcd == cx8.tcd;                 // node grains: N0 = 0, N1 = node < 2^32
+            const int t8 = cx8_type(cx8, 0, 0, tcd);          // node grains: N0 = 0, N1 = node < 2^32
             unsigned long long s8[ILP];
             uint4 q8[ILP][CX8_GROUP / 2];
 #pragma unroll
             for (int q = 0; q < ILP; ++q) {
                 h[q] = uniform_hash(0, target[q], tcd);
-                s8[q] = cx8_home(h[q], cx8.cap);
-                if (live[q] && want) {
-                    const uint4* qp = cx8.slots + (s8[q] >> 1);
-#pragma unroll
-                    for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q8[q][g] = qp[g];
-                }
+                s8[q] = home_slot(h[q], tab.mask);
+                if (live[q] && t8 >= 0) cx8_first(cx8, s8[q], q8[q]);
             }
 #pragma unroll
             for (int q = 0; q < ILP; ++q) {
                 if (!live[q]) continue;
                 const uint32_t p = p0 + (it0 + q) * BLOCK + threadIdx.x;
                 uint32_t silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[q])], act = NONE32;
-                const uint8_t st = want ? cx8_walk_node(cx8, tab, target[q], s8[q], q8[q], silo, act)
-                                        : (uint8_t)GD_ROUTE_MISS;
+                const uint8_t st = cx8_walk_node<MODE>(cx8, tab, max_probe, t8, target[q], tcd, s8[q], q8[q], s_pts,
+                                                       s_own, ring, silo, act);
                 if (out_target) out_target[p] = target[q];
                 out_sender[p] = sender[q];
                 out_silo[p] = silo;
@@ -415,18 +380,16 @@ static __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __re
 #pragma unroll
             for (int q = 0; q < ILP; ++q) {
                 h[q] = uniform_hash(0, target[q], tcd);
-                sc[q] = cx_home(h[q], cx.cap);
-                if (live[q] && want) {
-#pragma unroll
-                    for (int g = 0; g < RG; ++g) qc[q][g] = cx.slots[sc[q] + g];
-                }
+                sc[q] = home_slot(h[q], tab.mask);
+                if (live[q] && want) cx_first<RG>(cx, sc[q], qc[q]);
             }
 #pragma unroll
             for (int q = 0; q < ILP; ++q) {
                 if (!live[q]) continue;
                 const uint32_t p = p0 + (it0 + q) * BLOCK + threadIdx.x;
                 uint32_t silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[q])], act = NONE32;
-                const uint8_t st = cx_walk_node<RG>(cx, tab, want, target[q], sc[q], qc[q], silo, act);
+                const uint8_t st = cx_walk_node<MODE, RG>(cx, tab, max_probe, want, target[q], tcd, sc[q], qc[q], s_pts,
+                                                          s_own, ring, silo, act);
                 if (out_target) out_target[p] = target[q];
                 out_sender[p] = sender[q];
                 out_silo[p] = silo;

@@ -143,45 +143,50 @@ __device__ __forceinline__ bool is_membership(uint64_t n0, uint64_t n1, uint64_t
     return n0 == MEMBERSHIP_N0 && n1 == MEMBERSHIP_N1 && tcd == MEMBERSHIP_TCD;
 }
 
-// ---- compact probe index (gd_cx.h builds it) ------------------------------------------------
-// A derived, read-only copy of the directory for the probe, built when every live entry has N0 = 0
-// (long-keyed grains, GrainId.GetGrainId(typeCode, long), GrainId.cs:72-77) and at most 256 distinct
-// TypeCodeData: 16-B slots {N1, act, meta = silo | type index << 16 | CX_LIVE}, 4 to a 64-B DRAM
-// atom, so one read a round covers 4 slots of a table half the directory's size.  Homed by the
-// same uniform hash (multiply-shift over any capacity), linear probing in aligned 4-slot groups,
-// no tombstones (rebuilt, never updated).  The types: 256 u64 TypeCodeData slots (open addressing,
-// CX_NO_TYPE empty) staged in LDS by the route kernel.
+// ---- compact probe indexes (gd_cx.h builds and maintains them) -------------------------------
+// Narrow copies of the directory table for the probe, slot for slot: index slot j mirrors table slot
+// j (round 6), so a key's entry sits at the same probe distance from the same home (home_slot) as in
+// the table, the table's max_probe bounds the index walk too, the build is one streaming pass
+// (k_cx_project), and a directory change re-projects only the slots it touched (k_cx_sync) instead
+// of rebuilding.  A read covers the aligned 64-B group holding the home slot; the walk starts at the
+// home's offset in it and stops at the first empty slot (the table's own rule).
+// An index covers a subset of the keys; every other key is probed in the directory itself, per
+// message (route_m_core's fallback lanes), so a Guid key or an extra grain class no longer turns the
+// index off table-wide.
+//   16-B index: keys with N0 = 0 (GrainId.GetGrainId(typeCode, long), GrainId.cs:72-77) whose
+//   TypeCodeData is in a 256-slot type set (open addressing, CX_NO_TYPE empty; staged in LDS by the
+//   route kernel).  Slot {N1, act, meta = silo | type slot << 16 | CX_LIVE}; meta 0 = empty table
+//   slot, CX_TOMB = a tombstone, or a live entry the index does not hold (matches no key).
 constexpr uint32_t CX_GROUP = 4;
 constexpr uint32_t CX_LIVE = 1u << 24;
+constexpr uint32_t CX_TOMB = 1u << 25;
 constexpr uint32_t CX_TYPES = 256;
 constexpr unsigned long long CX_NO_TYPE = ~0ull;
 struct CxArgs {
     const uint4* slots;
-    unsigned long long cap;        // slots, a multiple of CX_GROUP
+    unsigned long long cap;        // = the table's capacity
     const unsigned long long* types;
-    uint32_t max_rounds;           // groups past the home group any entry sits
 };
 __host__ __device__ __forceinline__ uint32_t cx_type_home(uint64_t tcd) {
     return fmix32((uint32_t)tcd ^ fmix32((uint32_t)(tcd >> 32))) & (CX_TYPES - 1);
 }
-__host__ __device__ __forceinline__ unsigned long long cx_home(uint32_t h, unsigned long long cap) {
-    return (((unsigned long long)fmix32(h) * cap) >> 32) & ~(unsigned long long)(CX_GROUP - 1);
-}
-// The 8-B index (round 4): when the directory holds one TypeCodeData and every N1 < 2^32, a slot is
-// {N1 low word, (silo + 1) << ab | act} -- ab bits hold every activation with all ones left for
-// GD_ACT_MULTI, the 32 - ab above them silo + 1; 0 = empty -- half the 16-B index at the same load,
-// 8 slots a 64-B read (cx8 in gd_cx.h).
+//   8-B index: keys with N0 = 0, N1 < 2^32 and one of up to CX8_TYPES TypeCodeData (the most
+//   populous at the build, passed in the kernel arguments).  Slot {N1 low word, y}: y = u << ab | a,
+//   a = the activation (all ab bits set: GD_ACT_MULTI; all but the lowest: an activation too wide
+//   for ab bits -- probe the directory), u = type index << sb | (silo + 1) (all 32 - ab bits set: a
+//   silo or type too wide -- probe the directory).  y = 0: empty; u = 0 (y = 1): a tombstone or a
+//   live entry the index does not hold.
 constexpr uint32_t CX8_GROUP = 8;
+constexpr uint32_t CX8_TYPES = 8;
 struct Cx8Args {
     const uint4* slots;            // two 8-B slots an uint4
-    unsigned long long cap;        // slots, a multiple of CX8_GROUP
-    uint64_t tcd;                  // the one TypeCodeData
-    uint32_t max_rounds;           // groups past the home group any entry sits
+    unsigned long long cap;        // = the table's capacity
+    uint64_t tcd[CX8_TYPES];       // the types it holds, index order
+    uint32_t ntypes;
     uint32_t ab;                   // activation bits
+    uint32_t sb;                   // silo + 1 bits
+    uint32_t pad;
 };
-__host__ __device__ __forceinline__ unsigned long long cx8_home(uint32_t h, unsigned long long cap) {
-    return (((unsigned long long)fmix32(h) * cap) >> 32) & ~(unsigned long long)(CX8_GROUP - 1);
-}
 // Type index of tcd in the staged type set, or -1.
 __device__ __forceinline__ int cx_type_index(const unsigned long long* s_types, uint64_t tcd) {
     uint32_t t = cx_type_home(tcd);
@@ -192,6 +197,103 @@ __device__ __forceinline__ int cx_type_index(const unsigned long long* s_types, 
         t = (t + 1) & (CX_TYPES - 1);
     }
     return -1;
+}
+// The 8-B index's type index of a key, or -1 when the index does not hold it.
+__device__ __forceinline__ int cx8_type(const Cx8Args& c, uint64_t n0, uint64_t n1, uint64_t tcd) {
+    if (n0 != 0 || (n1 >> 32) != 0) return -1;
+    int t = -1;
+#pragma unroll
+    for (int k = (int)CX8_TYPES - 1; k >= 0; --k)
+        if ((uint32_t)k < c.ntypes && c.tcd[k] == tcd) t = k;
+    return t;
+}
+
+// Directory entry -> route result (LookUpActivations + IsValidSilo + the single-activation choice).
+__device__ __forceinline__ void entry_result(const TableArgs& tab, uint32_t a, uint32_t silo_of, uint32_t& silo,
+                                             uint32_t& act, uint8_t& status) {
+    if (a == GD_ACT_MULTI) {                       // several activations: the C# random choice
+        status = GD_ROUTE_MULTI_ACT;               // (RandomPlacementDirector.cs:33-53)
+    } else if (tab_silo_valid(tab, silo_of)) {
+        act = a;
+        silo = silo_of;                            // ActivationAddress.Silo (Message.cs:629-639)
+        status = GD_ROUTE_OK;
+    } else {
+        status = GD_ROUTE_MISS;                    // IsValidSilo filtered it (GrainDirectoryPartition.cs:431)
+    }
+}
+
+// The table's max_probe, read when a walk first leaves its home group (rare): kernels on the index do not
+// load it at their start, where the scalar load would share lgkmcnt with the LDS ring staging.
+__device__ __forceinline__ uint32_t lazy_max_probe(const TableArgs& tab) {
+    return __hip_atomic_load(&tab.ctr->max_probe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The 16-B index's walk from the home's group q (RG slots, already read): the entry of (want = 0x100 |
+// type slot, n1) or a miss (status left as is).  A key's entry lies within max_probe slots of its home.
+template <int RG>
+__device__ __forceinline__ void cx16_walk(const CxArgs& c, const TableArgs& tab, uint32_t want, uint64_t n1,
+                                          unsigned long long home, uint4 (&q)[RG], uint32_t& silo, uint32_t& act,
+                                          uint8_t& status) {
+    const uint32_t off0 = (uint32_t)(home & (RG - 1));
+    unsigned long long g = home - off0;
+    uint32_t last = 0;
+    bool done = false;
+    for (uint32_t base = 0;; base += RG) {
+#pragma unroll
+        for (int k = 0; k < RG; ++k) {
+            if (done || base + (uint32_t)k < off0) continue;
+            const uint4 v = q[k];
+            if (v.w == 0) {
+                done = true;                                            // miss
+            } else if ((v.w >> 16) == want && ((uint64_t)v.x | ((uint64_t)v.y << 32)) == n1) {
+                entry_result(tab, v.z, slot_silo(v.w), silo, act, status);
+                done = true;
+            }
+        }
+        if (done) return;
+        if (base == 0) last = off0 + lazy_max_probe(tab);
+        if (base + RG > last) return;                                   // past every entry's reach: miss
+        g += RG;
+        if (g >= c.cap) g = 0;
+#pragma unroll
+        for (int k = 0; k < RG; ++k) q[k] = c.slots[g + k];
+    }
+}
+
+// The 8-B index's walk from the home's group q (8 slots as 4 uint4, already read), for the key's low
+// N1 word and type index qt.  Returns true when a redirect entry matched: the directory must answer.
+__device__ __forceinline__ bool cx8_walk(const Cx8Args& c, const TableArgs& tab, uint32_t key, uint32_t qt,
+                                         unsigned long long home, uint4 (&q)[CX8_GROUP / 2], uint32_t& silo,
+                                         uint32_t& act, uint8_t& status) {
+    const uint32_t off0 = (uint32_t)(home & (CX8_GROUP - 1));
+    const uint32_t am = (1u << c.ab) - 1u, umax = ~0u >> c.ab, smask = (1u << c.sb) - 1u;
+    unsigned long long g = home - off0;
+    uint32_t last = 0;
+    bool done = false, redirect = false;
+    for (uint32_t base = 0;; base += CX8_GROUP) {
+#pragma unroll
+        for (int k = 0; k < (int)CX8_GROUP; ++k) {
+            if (done || base + (uint32_t)k < off0) continue;
+            const uint4 v = q[k / 2];
+            const uint32_t x = (k & 1) ? v.z : v.x, y = (k & 1) ? v.w : v.y;
+            const uint32_t u = y >> c.ab, a = y & am;
+            if (y == 0) {
+                done = true;                                            // miss
+            } else if (x == key && u != 0 && (u == umax || ((u >> c.sb) == qt))) {
+                done = true;
+                if (u == umax || a == am - 1u) redirect = true;
+                else entry_result(tab, a == am ? GD_ACT_MULTI : a, (u & smask) - 1u, silo, act, status);
+            }
+        }
+        if (done) return redirect;
+        if (base == 0) last = off0 + lazy_max_probe(tab);
+        if (base + CX8_GROUP > last) return false;                      // past every entry's reach: miss
+        g += CX8_GROUP;
+        if (g >= c.cap) g = 0;
+        const uint4* qp = c.slots + (g >> 1);
+#pragma unroll
+        for (int k = 0; k < (int)CX8_GROUP / 2; ++k) q[k] = qp[k];
+    }
 }
 
 // Linear probe of the open-addressing directory for a live entry with this key.
@@ -359,25 +461,41 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
             need[j] = true;
         }
     }
-    if constexpr (CX) {
-        // Every directory entry has N0 = 0 and one of the staged types: any other key is a miss.
-        static_assert(RG_CX == 1 || RG_CX == (int)CX_GROUP, "index reads: one slot or one group");
-        // the probe bound in reads of RG_CX slots: every entry sits within max_rounds groups of its home
-        const uint32_t bound = (cx->max_rounds + 1) * (CX_GROUP / RG_CX) - 1;
+    if constexpr (CX || CX8) {
+        static_assert(!(CX && CX8), "one index form a launch");
+        static_assert(RG_CX == 1 || RG_CX == (int)CX_GROUP, "16-B index reads: one slot or one group");
+        // Lanes whose key the index holds walk the index from the home's group; the others (fb: an N0 !=
+        // 0 key, a type or N1 the index does not hold, or a redirect entry) probe the directory itself.
+        constexpr int QW = CX ? RG_CX : (int)CX8_GROUP / 2;
         uint32_t want[M];
+        bool fb[M];
         unsigned long long s[M];
-        uint4 q[M][RG_CX];
+        uint4 q[M][QW];
 #pragma unroll
         for (int j = 0; j < M; ++j) {
             want[j] = 0;
+            fb[j] = false;
+            s[j] = home_slot(h[j], tab.mask);
             if (need[j]) {
-                const int t = n0[j] == 0 ? cx_type_index(s_types, tcd[j]) : -1;
-                want[j] = t < 0 ? 0u : (CX_LIVE | ((uint32_t)t << 16)) >> 16;
+                if constexpr (CX) {
+                    const int t = n0[j] == 0 ? cx_type_index(s_types, tcd[j]) : -1;
+                    want[j] = t < 0 ? 0u : (0x100u | (uint32_t)t);
+                } else {
+                    const int t = cx8_type(*cx8, n0[j], n1[j], tcd[j]);
+                    want[j] = t < 0 ? 0u : 1u + (uint32_t)t;
+                }
+                fb[j] = want[j] == 0;
             }
-            s[j] = cx_home(h[j], cx->cap);
             if (want[j]) {
+                if constexpr (CX) {
+                    const uint4* qp = cx->slots + (s[j] & ~(unsigned long long)(RG_CX - 1));
 #pragma unroll
-                for (int g = 0; g < RG_CX; ++g) q[j][g] = cx->slots[s[j] + g];
+                    for (int g = 0; g < QW; ++g) q[j][g] = qp[g];
+                } else {
+                    const uint4* qp = cx8->slots + ((s[j] & ~(unsigned long long)(CX8_GROUP - 1)) >> 1);
+#pragma unroll
+                    for (int g = 0; g < QW; ++g) q[j][g] = qp[g];
+                }
             }
         }
 #pragma unroll
@@ -386,85 +504,15 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
 #pragma unroll
         for (int j = 0; j < M; ++j) {
             if (!want[j]) continue;
-            bool done = false;
-            for (uint32_t p = 0;;) {
-#pragma unroll
-                for (int g = 0; g < RG_CX; ++g) {
-                    if (done) continue;
-                    const uint4 v = q[j][g];
-                    if (v.w == 0) {
-                        done = true;                                      // miss
-                    } else if ((v.w >> 16) == want[j] && ((uint64_t)v.x | ((uint64_t)v.y << 32)) == n1[j]) {
-                        if (v.z == GD_ACT_MULTI) {                        // RandomPlacementDirector.cs:33-53
-                            status[j] = GD_ROUTE_MULTI_ACT;
-                        } else if (tab_silo_valid(tab, slot_silo(v.w))) {
-                            act[j] = v.z;
-                            silo[j] = slot_silo(v.w);                     // Message.cs:629-639
-                            status[j] = GD_ROUTE_OK;
-                        }                                                 // else IsValidSilo (:431) -> MISS
-                        done = true;
-                    }
-                }
-                if (done || ++p > bound) break;
-                s[j] += RG_CX;
-                if (s[j] >= cx->cap) s[j] = 0;
-#pragma unroll
-                for (int g = 0; g < RG_CX; ++g) q[j][g] = cx->slots[s[j] + g];
-            }
-        }
-    } else if constexpr (CX8) {
-        static_assert(!CX, "one index form a launch");
-        // one type, N1 < 2^32 in every entry: any other key is a miss without a probe
-        const uint32_t bound = cx8->max_rounds;
-        bool want[M];
-        unsigned long long s[M];
-        uint4 q[M][CX8_GROUP / 2];
-#pragma unroll
-        for (int j = 0; j < M; ++j) {
-            want[j] = need[j] && n0[j] == 0 && tcd[j] == cx8->tcd && (n1[j] >> 32) == 0;
-            s[j] = cx8_home(h[j], cx8->cap);
-            if (want[j]) {
-                const uint4* qp = cx8->slots + (s[j] >> 1);
-#pragma unroll
-                for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q[j][g] = qp[g];
-            }
+            if constexpr (CX) cx16_walk<RG_CX>(*cx, tab, want[j], n1[j], s[j], q[j], silo[j], act[j], status[j]);
+            else fb[j] = cx8_walk(*cx8, tab, (uint32_t)n1[j], want[j] - 1u, s[j], q[j], silo[j], act[j], status[j]);
         }
 #pragma unroll
-        for (int j = 0; j < M; ++j)
-            if (need[j]) silo[j] = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[j])];
-#pragma unroll
         for (int j = 0; j < M; ++j) {
-            if (!want[j]) continue;
-            const uint32_t key = (uint32_t)n1[j];
-            bool done = false;
-            for (uint32_t p = 0;;) {
-#pragma unroll
-                for (int g = 0; g < (int)CX8_GROUP; ++g) {
-                    if (done) continue;
-                    const uint4 v = q[j][g / 2];
-                    const uint32_t x = (g & 1) ? v.z : v.x, y = (g & 1) ? v.w : v.y;
-                    if (y == 0) {
-                        done = true;                                      // empty: miss
-                    } else if (x == key) {
-                        const uint32_t am = (1u << cx8->ab) - 1u;
-                        const uint32_t a = y & am, sl = (y >> cx8->ab) - 1u;
-                        if (a == am) {                                    // RandomPlacementDirector.cs:33-53
-                            status[j] = GD_ROUTE_MULTI_ACT;
-                        } else if (tab_silo_valid(tab, sl)) {
-                            act[j] = a;
-                            silo[j] = sl;                                 // Message.cs:629-639
-                            status[j] = GD_ROUTE_OK;
-                        }                                                 // else IsValidSilo (:431) -> MISS
-                        done = true;
-                    }
-                }
-                if (done || ++p > bound) break;
-                s[j] += CX8_GROUP;
-                if (s[j] >= cx8->cap) s[j] = 0;
-                const uint4* qp = cx8->slots + (s[j] >> 1);
-#pragma unroll
-                for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q[j][g] = qp[g];
-            }
+            if (!fb[j]) continue;
+            uint32_t a, meta;
+            if (probe(tab.slots, tab.mask, lazy_max_probe(tab), h[j], n0[j], n1[j], tcd[j], a, meta))
+                entry_result(tab, a, slot_silo(meta), silo[j], act[j], status[j]);   // else MISS (Dispatcher.cs:742)
         }
     } else {
     // first probe of every message, all in flight together; the ring search (LDS) runs under them.
@@ -701,6 +749,11 @@ constexpr uint32_t SLOT_RETRY = 0xFFFFFFFEu;
 
 // vals / valid (nullable): an item whose silo is not valid is skipped (slot_of = NONE32): the
 // IsValidSilo check of AddSingleActivation / AddActivation (GrainDirectoryPartition.cs:279,310).
+__device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restrict__ keys, Slot* slots,
+                                               unsigned long long mask, DevCounters* ctr,
+                                               uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
+                                               const gd_val* __restrict__ vals, const TableArgs& vt, uint32_t* retry);
+
 static __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __restrict__ keys, uint32_t n, Slot* slots,
                                                      unsigned long long mask, DevCounters* ctr,
                                                      uint32_t* __restrict__ slot_of,
@@ -709,6 +762,34 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __rest
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     if (retry_only && slot_of[i] != SLOT_RETRY) return;
+    reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, &ctr->retry);
+}
+
+// The claim pass of an asynchronous batch (gd_dir_register_device_async): pass p > 0 runs only when
+// pass p - 1 deferred items (gate = its retry count; all lanes read the same word), so the host enqueues
+// REG_PASSES passes without reading a count back; k_reg_settled flags a batch still unsettled after them.
+constexpr uint32_t REG_PASSES = 6;
+static __global__ void __launch_bounds__(BLOCK) k_reg_claim_gated(const gd_key* __restrict__ keys, uint32_t n,
+                                                           Slot* slots, unsigned long long mask, DevCounters* ctr,
+                                                           uint32_t* __restrict__ slot_of,
+                                                           uint8_t* __restrict__ is_new,
+                                                           const gd_val* __restrict__ vals, TableArgs vt,
+                                                           const uint32_t* __restrict__ gate, uint32_t* retry) {
+    if (gate && *gate == 0) return;
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    if (gate && slot_of[i] != SLOT_RETRY) return;
+    reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, retry);
+}
+constexpr uint32_t ERR_UNSETTLED = 64u;     // DevCounters::err: an asynchronous batch's claims did not settle
+static __global__ void k_reg_settled(const uint32_t* __restrict__ last_retry, DevCounters* ctr) {
+    if (threadIdx.x == 0 && *last_retry) atomicOr(&ctr->err, ERR_UNSETTLED);
+}
+
+__device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restrict__ keys, Slot* slots,
+                                               unsigned long long mask, DevCounters* ctr,
+                                               uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
+                                               const gd_val* __restrict__ vals, const TableArgs& vt, uint32_t* retry) {
     if (vals && !tab_silo_valid(vt, vals[i].silo)) {
         slot_of[i] = NONE32;
         is_new[i] = 0;
@@ -719,23 +800,51 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __rest
     unsigned long long dist = 0;
     uint32_t res = NONE32;
     uint8_t fresh = 0;
+    // The key's first tombstone, reused when the chain does not hold the key (round 6: a directory under
+    // continuous RemoveActivation / AddSingleActivation churn no longer fills with tombstones until a
+    // rehash).  Every item of one key meets the same first free slot, and a claim is a CAS, so a key is
+    // never placed twice; a tombstone taken meanwhile defers the item to the next pass.
+    unsigned long long tomb_s = ~0ull, tomb_dist = 0;
+    uint32_t tomb_meta = 0;
+    // claim slot t (its meta `expected`) for the key: publish the key, then PENDING
+    auto claim = [&](unsigned long long t, uint32_t expected, unsigned long long d) -> bool {
+        uint32_t* mp = &slots[t].meta;
+        if (!__hip_atomic_compare_exchange_strong(mp, &expected, make_meta(SLOT_CLAIMED, 0), __ATOMIC_RELAXED,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return false;
+        __hip_atomic_store(&slots[t].n0, n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&slots[t].n1, n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&slots[t].tcd, tcd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&slots[t].act, NONE32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(mp, make_meta(SLOT_PENDING, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicMax(&ctr->max_probe, (uint32_t)d);
+        return true;
+    };
+    // the chain holds no copy of the key: take its first tombstone (or report a full table)
+    auto take_tomb = [&]() {
+        if (tomb_s == ~0ull) {
+            atomicOr(&ctr->err, 2u);
+        } else if (claim(tomb_s, tomb_meta, tomb_dist)) {
+            atomicAdd(&ctr->tomb, ~0ull);                    // -1
+            res = (uint32_t)tomb_s;
+            fresh = 1;
+        } else {
+            res = SLOT_RETRY;
+            atomicAdd(retry, 1u);
+        }
+    };
     for (;;) {
         uint32_t* meta_p = &slots[s].meta;
         const uint32_t meta = __hip_atomic_load(meta_p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t st = slot_state(meta);
         if (st == SLOT_EMPTY) {
-            uint32_t expected = meta;
-            if (__hip_atomic_compare_exchange_strong(meta_p, &expected, make_meta(SLOT_CLAIMED, 0),
-                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)) {
-                __hip_atomic_store(&slots[s].n0, n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&slots[s].n1, n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&slots[s].tcd, tcd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&slots[s].act, NONE32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(meta_p, make_meta(SLOT_PENDING, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                atomicMax(&ctr->max_probe, (uint32_t)dist);
+            if (tomb_s != ~0ull) {
+                take_tomb();
+                break;
+            }
+            if (claim(s, meta, dist)) {
                 res = (uint32_t)s;
                 fresh = 1;
                 break;
@@ -744,8 +853,13 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __rest
         }
         if (st == SLOT_CLAIMED) {        // claimed in this launch, key not yet visible
             res = SLOT_RETRY;
-            atomicAdd(&ctr->retry, 1u);
+            atomicAdd(retry, 1u);
             break;
+        }
+        if (st == SLOT_TOMB && tomb_s == ~0ull) {
+            tomb_s = s;
+            tomb_meta = meta;
+            tomb_dist = dist;
         }
         if (st == SLOT_LIVE || st == SLOT_PENDING) {
             const uint64_t k0 = __hip_atomic_load(&slots[s].n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -759,7 +873,7 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __rest
         }
         s = (s + 1) & mask;
         if (++dist > mask) {
-            atomicOr(&ctr->err, 2u);
+            take_tomb();
             break;
         }
     }

@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = [
     "gd_ring_owner_device", "gd_pack_by_shard_device", "gd_pack_routes_by_rank_device", "gd_kernel_times",
     "gd_kernel_times_reset",
     "gd_option_set", "gd_option_get", "gd_tune_reset", "gd_tune_set", "gd_tune_get", "gd_tune_agree",
-    "gd_comm_info",
+    "gd_comm_info", "gd_index_stats_get",
     "gd_set_kernel_timing", "gd_microbatch_create", "gd_microbatch_destroy", "gd_microbatch_keys",
     "gd_microbatch_outputs", "gd_microbatch_run", "gd_decode_frames_device", "gd_decode_frames",
     "gd_route_frames_device", "gd_route_frames", "gd_dir_split", "gd_dir_split_device",
@@ -56,7 +56,8 @@ EXPORTED_SYMBOLS = [
     "gd_comm_unique_id", "gd_comm_init", "gd_comm_init_local", "gd_comm_destroy", "gd_route_multi_device",
     "gd_route_multi",
     "gd_multi_fetch", "gd_route_multi_ext_device", "gd_route_multi_ext", "gd_ring_owner_ext",
-    "gd_dir_split_ext", "gd_dir_upsert", "gd_dir_register_device",
+    "gd_dir_split_ext", "gd_dir_upsert", "gd_dir_register_device", "gd_dir_register_device_async",
+    "gd_dir_unregister_device",
     "gd_dir_set_valid_silos", "gd_dir_lookup_tagged", "gd_dir_remove_silos", "gd_activation_ids_set", "gd_dir_merge",
     "gd_actdir_add", "gd_actdir_remove", "gd_actdir_set_flags", "gd_actdir_lookup", "gd_actdir_clear",
     "gd_actdir_count", "gd_receive", "gd_receive_device", "gd_receive_frames_device", "gd_receive_frames",
@@ -87,6 +88,12 @@ class gd_config(C.Structure):
 class gd_stats(C.Structure):
     _fields_ = [("routed", C.c_uint64), ("table_live", C.c_uint64), ("table_tombstones", C.c_uint64),
                 ("table_capacity", C.c_uint64), ("ring_points", C.c_uint64), ("ring_mode", C.c_uint64)]
+
+
+class gd_index_stats(C.Structure):
+    _fields_ = [("builds", C.c_uint64), ("synced_slots", C.c_uint64), ("last_build_ms", C.c_double),
+                ("current", C.c_uint32), ("types8", C.c_uint32), ("act_bits8", C.c_uint32),
+                ("silo_bits8", C.c_uint32), ("n0_live", C.c_uint32), ("out8", C.c_uint32)]
 
 
 class gd_cache_stats(C.Structure):
@@ -214,6 +221,7 @@ def _load() -> C.CDLL:
         "gd_host_free": (C.c_int, [P]),
         "gd_synchronize": (C.c_int, [P]),
         "gd_stats_get": (C.c_int, [P, C.POINTER(gd_stats)]),
+        "gd_index_stats_get": (C.c_int, [P, C.POINTER(gd_index_stats)]),
         "gd_jenkins_hash_bytes": (U32, [P, C.c_size_t]),
         "gd_jenkins_hash_u64x3": (U32, [U64, U64, U64]),
         "gd_uniform_hash": (U32, [C.POINTER(gd_key)]),
@@ -228,6 +236,8 @@ def _load() -> C.CDLL:
         "gd_dir_register": (C.c_int, [P, P, P, U32, P, P]),
         "gd_dir_unregister": (C.c_int, [P, P, P, U32, P]),
         "gd_dir_register_device": (C.c_int, [P, P, P, U32, P, P]),
+        "gd_dir_register_device_async": (C.c_int, [P, P, P, U32, P, P]),
+        "gd_dir_unregister_device": (C.c_int, [P, P, P, U32, P]),
         "gd_dir_set_valid_silos": (C.c_int, [P, P, U32]),
         "gd_dir_lookup_tagged": (C.c_int, [P, P, U32, P, P, P]),
         "gd_dir_remove_silos": (C.c_int, [P, P, U32, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]),
@@ -504,6 +514,12 @@ class GrainDispatch:
         self._c(lib.gd_stats_get(self.h, C.byref(s)))
         return {f: getattr(s, f) for f, _ in gd_stats._fields_}
 
+    def index_stats(self) -> dict:
+        """gd_index_stats_get: builds, slots re-projected by directory batches, the 8-B layout."""
+        s = gd_index_stats()
+        self._c(lib.gd_index_stats_get(self.h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in gd_index_stats._fields_}
+
     # -- ring -----------------------------------------------------------------
     def ring_set(self, mode, points, owner):
         m = RING_MODES[mode] if isinstance(mode, str) else mode
@@ -546,6 +562,17 @@ class GrainDispatch:
         """gd_dir_register_device: keys (n,3) u64 and values (n,2) u32 [act, silo] in HBM."""
         self._c(lib.gd_dir_register_device(self.h, C.c_void_p(d_keys), C.c_void_p(d_vals), n,
                                            C.c_void_p(d_out_vals or 0), C.c_void_p(d_out_inserted or 0)))
+
+    def register_device_async(self, d_keys: int, d_vals: int, n: int, d_out_vals: Optional[int] = None,
+                              d_out_inserted: Optional[int] = None):
+        """gd_dir_register_device_async: enqueued only (device errors at the next synchronising call)."""
+        self._c(lib.gd_dir_register_device_async(self.h, C.c_void_p(d_keys), C.c_void_p(d_vals), n,
+                                                 C.c_void_p(d_out_vals or 0), C.c_void_p(d_out_inserted or 0)))
+
+    def unregister_device(self, d_keys: int, d_acts: int, n: int, d_out_removed: Optional[int] = None):
+        """gd_dir_unregister_device: RemoveActivation over device arrays, enqueued only."""
+        self._c(lib.gd_dir_unregister_device(self.h, C.c_void_p(d_keys), C.c_void_p(d_acts), n,
+                                             C.c_void_p(d_out_removed or 0)))
 
     # -- membership change: IsValidSilo, VersionTag, silo removal, merge (SURVEY 8 f4) ----------
     def set_valid_silos(self, valid_silos, n_silos: int):

@@ -62,6 +62,31 @@ def zipf_keys_torch(tcd: int, n_grains: int, n: int, seed: int, dev, s: float = 
     return keys
 
 
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def mixed_grain_keys(tcds, n_grains: int, guid_every: int = 100) -> np.ndarray:
+    """(n_grains, 3) u64 keys of a mixed directory: grain g is of class
+    tcds[g % len(tcds)]; every guid_every-th grain is Guid-keyed (UniqueKey.NewKey(Guid), category
+    Grain: N0 and N1 from the Guid's bytes, UniqueKey.cs:135-143 -- here a splitmix64 stream, N0 != 0),
+    the others long-keyed (GrainId.GetGrainId(typeCode, g): N0 = 0, N1 = g, GrainId.cs:72-77)."""
+    g = np.arange(n_grains, dtype=np.uint64)
+    out = np.zeros((n_grains, 3), dtype=np.uint64)
+    out[:, 1] = g
+    out[:, 2] = np.asarray(tcds, dtype=np.uint64)[(g % np.uint64(len(tcds))).astype(np.int64)]
+    if guid_every:
+        sel = (g % np.uint64(guid_every)) == np.uint64(guid_every - 1)
+        out[sel, 0] = _splitmix64(g[sel] * np.uint64(2) + np.uint64(1)) | np.uint64(1)
+        out[sel, 1] = _splitmix64(g[sel] * np.uint64(2) + np.uint64(2))
+    return out
+
+
 def grain_keys_torch(tcd: int, ks, dev):
     """(n, 3) int64 keys [0, k, tcd] on `dev` for a 1-D tensor (or range) of long keys."""
     import torch

@@ -216,3 +216,111 @@ def test_cx8_matches_directory_through_changes(gd, mode, act_base):
     np.testing.assert_array_equal(act, want[2])
     a.close()
     b.close()
+
+
+def _owner(spec, k):
+    return o.ring_owner_np(spec, o.jenkins_u64x3_np(k[:, 2], k[:, 0], k[:, 1])).astype(np.uint32)
+
+
+@pytest.mark.parametrize("mode,probe", [("D", "4"), ("V", "2"), ("D", "3"), ("D", "1")])
+def test_index_kept_current_through_churn(gd, mode, probe):
+    """Round 6: AddSingleActivation / RemoveActivation / AddActivation batches re-project the slots they
+    touch (k_cx_sync), so the index stays current without a rebuild (GrainDirectoryPartition.cs:304-363
+    are O(1) dictionary updates).  Every round -- 1 % unregistered, 1 % new grains registered, a few
+    upserts -- routes equal the directory probe and the oracle, and the index was built once."""
+    rng = np.random.default_rng(61)
+    (a, b), spec = _pair(gd, mode, 1 << 15, probe)
+    G = 12000
+    reg = o.grain_keys(TC, np.arange(G))
+    acts = np.arange(G, dtype=np.uint32) * 3 + 1
+    live = {tuple(k): (int(x), int(s)) for k, x, s in zip(reg, acts, _owner(spec, reg))}
+    _both((a, b), lambda e: e.register(reg, acts, _owner(spec, reg)))
+    nxt = G
+
+    def check(n=20000):
+        keys = np.array(list(live.keys()), np.uint64).reshape(-1, 3)
+        pool = np.concatenate([keys, o.grain_keys(TC, np.arange(nxt, nxt + 500))])
+        q = pool[rng.integers(0, len(pool), size=n)]
+        q[::101, 0] = 9                                                   # N0 != 0
+        vals = np.array(list(live.values()), np.uint32).reshape(-1, 2)
+        want = o.route_batch_np(q, spec, o.DirectoryArrays(keys, vals[:, 0], vals[:, 1]))
+        st, silo, act = _same(a, b, q)
+        np.testing.assert_array_equal(st, want[0])
+        np.testing.assert_array_equal(silo, want[1])
+        np.testing.assert_array_equal(act, want[2])
+
+    check()
+    builds = a.index_stats()["builds"]
+    assert builds >= 1 or probe == "1"
+    for r in range(5):
+        keys = np.array(list(live.keys()), np.uint64).reshape(-1, 3)
+        gone = keys[rng.choice(len(keys), size=len(keys) // 100, replace=False)]
+        gacts = np.array([live[tuple(k)][0] for k in gone], np.uint32)
+        _both((a, b), lambda e: e.unregister(gone, gacts))
+        for k in gone:
+            del live[tuple(k)]
+        new = o.grain_keys(TC, np.arange(nxt, nxt + G // 100))
+        nacts = (np.arange(len(new), dtype=np.uint32) + nxt) * 3 + 1
+        _both((a, b), lambda e: e.register(new, nacts, _owner(spec, new)))
+        for k, x, s in zip(new, nacts, _owner(spec, new)):
+            live[tuple(k)] = (int(x), int(s))
+        nxt += len(new)
+        keys = np.array(list(live.keys()), np.uint64).reshape(-1, 3)
+        up = keys[rng.choice(len(keys), size=50, replace=False)]
+        uacts = rng.integers(0, 1 << 20, size=len(up)).astype(np.uint32)
+        uacts[::5] = 0xFFFFFFFE                                           # GD_ACT_MULTI
+        usil = rng.integers(0, 8, size=len(up)).astype(np.uint32)
+        _both((a, b), lambda e: e.upsert(up, uacts, usil))
+        for k, x, s in zip(up, uacts, usil):
+            live[tuple(k)] = (int(x), int(s))
+        check()
+    st = a.index_stats()
+    assert st["current"] == 1 and st["synced_slots"] > 0
+    assert st["builds"] == builds, st                                     # no rebuild through the churn
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("probe", ["4", "2", "1"])
+def test_index_mixed_directory(gd, probe):
+    """8 grain classes and 1 % Guid-keyed grains (UniqueKey.cs:135-143) keep the
+    index: the 8-B index holds the 8 classes, the Guid keys are probed in the directory per message;
+    routes equal the oracle.  Then a ninth class and activations past the 8-B layout's width arrive
+    through registration (not held / redirect entries) and routes still equal the oracle."""
+    from orleans_amd.workloads import mixed_grain_keys
+    rng = np.random.default_rng(62)
+    (a, b), spec = _pair(gd, "D", 1 << 16, probe)
+    tcds = [o.type_code_data(o.CAT_GRAIN, o.grain_type_code(f"Mixed.Grain{c}")) for c in range(8)]
+    G = 20000
+    reg = mixed_grain_keys(tcds, G)
+    acts = np.arange(G, dtype=np.uint32) + 5
+    own = _owner(spec, reg)
+    _both((a, b), lambda e: e.register(reg, acts, own))
+    extra = mixed_grain_keys(tcds, G + 300)[G:]
+    q = np.concatenate([reg, extra])[rng.integers(0, G + 300, size=40000)]
+    want = o.route_batch_np(q, spec, o.DirectoryArrays(reg, acts, own))
+    st, silo, act = _same(a, b, q)
+    np.testing.assert_array_equal(st, want[0])
+    np.testing.assert_array_equal(silo, want[1])
+    np.testing.assert_array_equal(act, want[2])
+    s = a.index_stats()
+    if probe != "1":
+        assert s["types8"] == 8 and s["n0_live"] == G // 100, s
+    # a ninth class, and activations wider than the layout's field
+    t9 = o.type_code_data(o.CAT_GRAIN, o.grain_type_code("Mixed.Grain9"))
+    k9 = mixed_grain_keys([t9], 500)
+    wide = o.grain_keys(o.grain_type_code("Mixed.Grain0"), np.arange(10 ** 7, 10 ** 7 + 200))
+    wide[:, 2] = tcds[0]
+    nk = np.concatenate([k9, wide])
+    na = np.concatenate([np.arange(500, dtype=np.uint32) + 7, np.arange(200, dtype=np.uint32) + (1 << 30)])
+    nown = _owner(spec, nk)
+    _both((a, b), lambda e: e.register(nk, na, nown))
+    allk = np.concatenate([reg, nk])
+    q = np.concatenate([allk, extra])[rng.integers(0, len(allk) + 300, size=40000)]
+    want = o.route_batch_np(q, spec, o.DirectoryArrays(allk, np.concatenate([acts, na]), np.concatenate([own, nown])))
+    st, silo, act = _same(a, b, q)
+    np.testing.assert_array_equal(st, want[0])
+    np.testing.assert_array_equal(silo, want[1])
+    np.testing.assert_array_equal(act, want[2])
+    a.close()
+    b.close()

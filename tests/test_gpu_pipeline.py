@@ -73,3 +73,56 @@ def test_pipelined_batches_match_serial(gd, G, N):
     np.testing.assert_array_equal(perm.cpu().numpy(), res[0][3].cpu().numpy())
     np.testing.assert_array_equal(off.cpu().numpy(), res[0][4].cpu().numpy())
     e.close()
+
+
+def test_pipelined_batches_with_directory_churn(gd):
+    """with the bucketing on the bucket stream, directory batches and other entry
+    points enqueued on the handle's stream between pipelined batches must not touch the scratch of a
+    bucketing still running (bfence).  Between five pipelined batches: an asynchronous RemoveActivation
+    batch, an asynchronous AddSingleActivation batch (gd_dir_unregister_device /
+    gd_dir_register_device_async) and a host ring lookup.  Every batch's routes and
+    buckets equal the oracle's for the directory as it stood when the batch was routed."""
+    import torch
+    from orleans_amd.sharded import DeviceEngine
+    dev = torch.device("cuda:0")
+    G, N, W = 1 << 16, (1 << 20) + 17, 1 << 11
+    e, owner = _setup(gd, G)
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    eng = DeviceEngine(e, dev, pipeline=True)
+    rng = np.random.default_rng(0x5EED0202)
+    reg = o.grain_keys(TC, np.arange(G))
+    live = np.ones(G, bool)
+    want, res = [], []
+    hashes = rng.integers(0, 1 << 32, size=5000, dtype=np.uint64).astype(np.uint32)
+    with torch.cuda.stream(eng.stream):
+        for b in range(5):
+            ks = rng.integers(0, G, size=N)
+            keys = torch.from_numpy(o.grain_keys(TC, ks).view(np.int64)).to(dev)
+            res.append(eng.route_bucket(keys, G))
+            d = o.DirectoryArrays(reg[live], np.arange(G)[live], owner[live])
+            w = o.route_batch_np(o.grain_keys(TC, ks), spec, d)
+            want.append((w, o.bucket_stable(w[2], G)))
+            # churn on the handle's stream while this batch's bucketing may still run
+            gone = np.arange(b * W, (b + 1) * W)
+            dk = torch.from_numpy(reg[gone].view(np.int64)).to(dev)
+            da = torch.from_numpy(gone.astype(np.int32)).to(dev)
+            e.unregister_device(dk.data_ptr(), da.data_ptr(), len(gone))
+            live[gone] = False
+            if b:
+                back = np.arange((b - 1) * W, b * W)
+                rk = torch.from_numpy(reg[back].view(np.int64)).to(dev)
+                rv = torch.from_numpy(np.stack([back, owner[back]], 1).astype(np.int32)).to(dev)
+                e.register_device_async(rk.data_ptr(), rv.data_ptr(), len(back))
+                live[back] = True
+            assert len(e.ring_lookup_hashes(hashes)) == len(hashes)
+        eng.stream.wait_stream(eng.bstream)
+    torch.cuda.synchronize()
+    e.synchronize()                                              # surfaces any deferred device error
+    for (w, (wp, wo)), (st, silo, act, perm, off) in zip(want, res):
+        np.testing.assert_array_equal(st.cpu().numpy(), w[0])
+        np.testing.assert_array_equal(silo.cpu().numpy().view(np.uint32), w[1])
+        np.testing.assert_array_equal(act.cpu().numpy().view(np.uint32), w[2])
+        np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32), wp)
+        np.testing.assert_array_equal(off.cpu().numpy().view(np.uint32), wo)
+    e.close()
