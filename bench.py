@@ -536,6 +536,8 @@ def compact_secondary(sec: dict) -> dict:
                                   "guid_grains", "routed_ok_fraction"))
         elif name == "host_path":
             out[name] = _pick(v, ("value", "ms_per_call", "pcie_GBps", "workload"))
+        elif name == "cfg2_other_silo_set":
+            out[name] = _pick(v, ("silos", "value", "ms_per_step", "owner_share_max", "exchange"))
         else:
             d = _pick(v, ("value", "unit", "ms_per_step", "steps", "workload", "n_gpus", "scaling",
                           "messages_per_step"))
@@ -559,9 +561,8 @@ def compact_line(full: dict, full_path=None) -> dict:
     cfg = dict(full.get("config") or {})
     if isinstance(cfg.get("silos"), str):
         cfg["silos"] = cfg["silos"][:90]
-    cfg.pop("owner_share_max_by_silo_set", None)
     line["config"] = cfg
-    for k in ("routed_ok_last_step_rank0", "rehearsal_one_gpu", "messages_per_step", "comm"):
+    for k in ("routed_ok_last_step_rank0", "rehearsal_one_gpu", "messages_per_step", "comm", "exchange_ms_per_rank"):
         if k in full:
             line[k] = full[k]
     if isinstance(full.get("exchange"), str):
@@ -739,6 +740,15 @@ def main():
     acts_np = res.act.cpu().numpy().view(np.uint32)
     kt = profile_kernels(e, router, keys, n_act, stream, args.profile_steps)
     kernels, roofline = roofline_of(kt, max(1, args.profile_steps), m_recv, n_act, acts_np, args.workload, world)
+    # the library exchange's RCCL rounds on every rank (HIP events around each grouped round, the
+    # profiled steps): VERDICT r05 item 5
+    ex_ms = sum(v[1] for k, v in kt.items() if k.startswith("rccl_")) / max(1, args.profile_steps)
+    ex_ms_ranks = gather_floats(ex_ms, world, dev)
+
+    # ---- N > 1: the same line on the other silo set (SURVEY 8(d)'s literal generation-1 set and the
+    # balanced one), with each set's largest owner share -------------------------------------------
+    if world > 1 and args.workload == "cfg2" and not args.no_secondary:
+        secondary["cfg2_other_silo_set"] = other_silo_set_line(args, world, rank, local, dev, tcd)
     if roofline and roofline["kernel"] == "k_route":
         route_extras(roofline, e, m_recv, args.workload, world, isinstance(router, LibraryRouter))
 
@@ -792,6 +802,7 @@ def main():
             "routed_ok_last_step_rank0": st_ok,
             "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
             "exchange": exchange,
+            "exchange_ms_per_rank": [round(x, 4) for x in ex_ms_ranks] if world > 1 else None,
             "comm": comm_info(w),
             "roofline": roofline,
             "kernels": kernels,
@@ -945,6 +956,37 @@ def micro_batch_latency(e, tcd: int, G: int, n_act: int, batches: int, B: int = 
                                                   "max": round(float(us.max()), 1)}
     out["zero_copy"] = bool(e.get_option("mb_zerocopy"))
     mb.close()
+    return out
+
+
+def gather_floats(x: float, world: int, dev) -> list:
+    """x from every rank, in rank order (all_gather; on the GPU under RCCL)."""
+    if world == 1:
+        return [x]
+    on_gpu = dist.get_backend() == "nccl"
+    t = torch.tensor([x], dtype=torch.float64, device=dev if on_gpu else "cpu")
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
+
+
+def other_silo_set_line(args, world, rank, local, dev, tcd) -> dict:
+    """The cfg 2 line on the other silo set: the balanced set gives every silo 1/8
+    of the ring; SURVEY 8(d)'s literal generation-1 set gives one silo 35.7 %, so its owner rank receives
+    that share of every batch.  Same harness, fewer steps."""
+    import copy
+    a2 = copy.copy(args)
+    a2.silos = "literal" if args.silos == "balanced" else "balanced"
+    w2 = setup_workload(a2, "cfg2", world, rank, local, dev, tcd, args.msgs, args.grains)
+    steps = max(10, args.steps // 4)
+    wall, _, _ = timed_steps(w2["router"], w2["keys"], w2["n_act"], w2["stream"], steps, max(3, args.warmup // 4),
+                             settle_steps(args), w2["agree"])
+    out = {"silos": a2.silos, "value": round(w2["N"] * steps * world / wall, 1), "unit": "messages/s",
+           "ms_per_step": round(wall / steps * 1e3, 4), "steps": steps,
+           "owner_share_max": w2["owner_share_max"], "exchange": w2["exchange"][:80]}
+    w2["e"].close()
+    del w2
+    torch.cuda.empty_cache()
     return out
 
 

@@ -117,6 +117,7 @@ void gd_destroy(gd_handle* h) {
     free_buf(h->cxi_tab);
     free_buf(h->cx8_tab);
     free_buf(h->reg_retry);
+    for (auto& d : h->dir_scr) free_buf(d);
     free_buf(h->cxi_types);
     free_buf(h->cxi_ctr);
     for (auto& kt : h->cx_tune)
@@ -285,50 +286,66 @@ namespace gdx {
 // end; a device error (table full, unsettled claims) surfaces at the next synchronising call.
 int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t n, gd_val* out_vals,
                   uint8_t* out_ins, bool async) {
-    GD_TRY(bfence(h));
     GD_TRY(async ? maybe_grow_async(h, n) : maybe_grow_table(h, n));
     const uint32_t op = ++h->dir_op;
-    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));   // slot_of
-    GD_TRY(ensure(h, h->u32_b, (size_t)n * 4));   // win
-    GD_TRY(ensure(h, h->u8_a, (size_t)n));        // is_new
-    HIP_TRY(h, hipMemsetAsync(h->u8_a.p, 0, n, h->stream));
+    // the directory batches' own scratch (dir_scr): no bucketing left running on the bucket stream
+    // shares it, so a batch need not wait for one (bfence) -- it overlaps the previous batch's bucketing
+    GD_TRY(ensure_own(h, h->dir_scr[0], (size_t)n * 4));   // slot_of
+    GD_TRY(ensure_own(h, h->dir_scr[1], (size_t)n * 4));   // k_reg_find's seen metas, then win
+    GD_TRY(ensure_own(h, h->dir_scr[2], (size_t)n));       // is_new (k_reg_find writes every item's)
+    GD_TRY(slot_words(h));                                 // the per-slot election words
     const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
-    uint32_t* slot_of = (uint32_t*)h->u32_a.p;
-    uint32_t* win = (uint32_t*)h->u32_b.p;
-    uint8_t* is_new = (uint8_t*)h->u8_a.p;
+    uint32_t* slot_of = (uint32_t*)h->dir_scr[0].p;
+    uint32_t* win = (uint32_t*)h->dir_scr[1].p;
+    uint8_t* is_new = (uint8_t*)h->dir_scr[2].p;
+    uint32_t* last = (uint32_t*)h->up_last.p;
     const unsigned long long mask = h->capacity - 1;
     TabTrack tt(h);                                // the batch re-projects its slots into the probe indexes
+    // read-only find, one CAS a new grain (k_reg_find / k_reg_take), then the full protocol for the items
+    // that lost their CAS; every item ending with a new entry elects itself in the slot's word (the lowest
+    // batch index wins: first registration wins, GrainDirectoryPartition.cs:304-326)
+    GD_TRY(launch(h, "k_reg_find", g, b, 0, k_reg_find, dk, n, (const Slot*)h->slots, mask, h->ctr, slot_of, is_new,
+                  win, dvals, table_args(h)));
+    const uint32_t* unsettled = nullptr;
+    uint32_t* retry0 = nullptr;
     if (async) {
-        GD_TRY(ensure(h, h->reg_retry, REG_PASSES * sizeof(uint32_t)));
+        if (!h->reg_retry.p) {                     // gate counters: k_reg_take / the commit keep them
+            GD_TRY(ensure_own(h, h->reg_retry, REG_PASSES * sizeof(uint32_t)));
+            HIP_TRY(h, hipMemsetAsync(h->reg_retry.p, 0, REG_PASSES * sizeof(uint32_t), h->stream));
+        }
         uint32_t* rc = (uint32_t*)h->reg_retry.p;
-        HIP_TRY(h, hipMemsetAsync(rc, 0, REG_PASSES * sizeof(uint32_t), h->stream));
-        for (uint32_t pass = 0; pass < REG_PASSES; ++pass)
+        GD_TRY(launch(h, "k_reg_take", g, b, 0, k_reg_take, dk, n, h->slots, mask, h->ctr, dvals, table_args(h),
+                      slot_of, is_new, (const uint32_t*)win, rc, rc + 1, last));
+        for (uint32_t pass = 1; pass < REG_PASSES; ++pass)
             GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim_gated, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
-                          dvals, table_args(h), pass ? (const uint32_t*)rc + pass - 1 : (const uint32_t*)nullptr,
-                          rc + pass));
-        GD_TRY(launch(h, "k_reg_settled", dim3(1), dim3(WAVE), 0, k_reg_settled, (const uint32_t*)rc + REG_PASSES - 1,
-                      h->ctr));
+                          dvals, table_args(h), (const uint32_t*)rc + pass - 1, rc + pass, last));
+        unsettled = rc + REG_PASSES - 1;
+        retry0 = rc;
         h->pending_in += n;
     } else {
-        // claim pass, then relaunches for the items that met an unpublished claim
-        for (uint32_t pass = 0;; ++pass) {
+        HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
+        GD_TRY(launch(h, "k_reg_take", g, b, 0, k_reg_take, dk, n, h->slots, mask, h->ctr, dvals, table_args(h),
+                      slot_of, is_new, (const uint32_t*)win, &h->ctr->retry, (uint32_t*)nullptr, last));
+        GD_TRY(pull_counters(h));
+        // relaunches for the items that lost their CAS or met an unpublished claim
+        for (uint32_t pass = 1; h->ctr_host.retry && !h->ctr_host.err; ++pass) {
+            if (pass > 64) return set_err(h, GD_ETIMEOUT, "gd_dir_register: claims did not settle");
             HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
-            GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
-                          (uint32_t)(pass > 0), dvals, table_args(h)));
+            GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new, 1u,
+                          dvals, table_args(h), last));
             GD_TRY(pull_counters(h));
-            if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
-            if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_register: claims did not settle");
         }
     }
-    GD_TRY(launch(h, "k_reg_minwin", g, b, 0, k_reg_minwin, (const uint32_t*)slot_of, (const uint8_t*)is_new, n, h->slots));
-    GD_TRY(launch(h, "k_reg_resolve", g, b, 0, k_reg_resolve, (const uint32_t*)slot_of, (const uint8_t*)is_new, n,
-                  (const Slot*)h->slots, win));
-    GD_TRY(launch(h, "k_reg_commit", g, b, 0, k_reg_commit, (const uint32_t*)slot_of, (const uint32_t*)win, dvals, n,
-                  h->slots, h->ctr, h->vtag, op));
+    if (cx_inline(h, tt, n))                       // the winners project their slots as they commit
+        GD_TRY(launch(h, "k_reg_commit", g, b, 0, k_reg_commit_elect_cx, (const uint32_t*)slot_of,
+                      (const uint8_t*)is_new, dvals, n, h->slots, h->ctr, h->vtag, op, last, win, unsettled, retry0,
+                      cx_build_args(h), (CxCounters*)h->cxi_ctr.p));
+    else
+        GD_TRY(launch(h, "k_reg_commit", g, b, 0, k_reg_commit_elect, (const uint32_t*)slot_of, (const uint8_t*)is_new,
+                      dvals, n, h->slots, h->ctr, h->vtag, op, last, win, unsettled, retry0));
     if (out_vals || out_ins)
         GD_TRY(launch(h, "k_reg_report", g, b, 0, k_reg_report, (const uint32_t*)slot_of, (const uint32_t*)win, n,
                       (const Slot*)h->slots, out_vals, out_ins));
-    GD_TRY(cx_sync(h, tt, slot_of, n));
     if (async) return GD_OK;
     GD_TRY(pull_counters(h));
     if (h->ctr_host.err) {
@@ -343,21 +360,31 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
 }
 
 // RemoveActivation (Force) for a batch of device-resident keys / activations; out_removed (device, may be
-// null).  Only enqueued.
+// null).  Only enqueued; its own scratch (no bfence).  The first matching item of the batch removes.
 int unregister_core(gd_handle* h, const gd_key* dk, const uint32_t* dacts, uint32_t n, uint8_t* out_removed) {
-    GD_TRY(bfence(h));
-    GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
+    GD_TRY(ensure_own(h, h->dir_scr[0], (size_t)n * 4));
+    GD_TRY(slot_words(h));
     const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
-    uint32_t* slot_of = (uint32_t*)h->u32_a.p;
+    uint32_t* slot_of = (uint32_t*)h->dir_scr[0].p;
+    uint32_t* last = (uint32_t*)h->up_last.p;
     const unsigned long long mask = h->capacity - 1;
     TabTrack tt(h);                               // the batch re-projects its slots into the probe indexes
-    GD_TRY(launch(h, "k_unreg_find", g, b, 0, k_unreg_find, dk, dacts, n, (const Slot*)h->slots, mask,
-                  (const DevCounters*)h->ctr, slot_of));
-    GD_TRY(launch(h, "k_unreg_poison", g, b, 0, k_unreg_poison, (const uint32_t*)slot_of, n, h->slots));
-    GD_TRY(launch(h, "k_unreg_min", g, b, 0, k_unreg_min, (const uint32_t*)slot_of, n, h->slots));
-    GD_TRY(launch(h, "k_unreg_commit", g, b, 0, k_unreg_commit, (const uint32_t*)slot_of, n, h->slots, h->ctr,
-                  out_removed));
-    return cx_sync(h, tt, slot_of, n);
+    GD_TRY(launch(h, "k_unreg_find", g, b, 0, k_unreg_find_elect, dk, dacts, n, (const Slot*)h->slots, mask,
+                  (const DevCounters*)h->ctr, slot_of, last));
+    if (cx_inline(h, tt, n))                      // the removers project their tombstones as they commit
+        return launch(h, "k_unreg_commit", g, b, 0, k_unreg_commit_elect_cx, (const uint32_t*)slot_of, n, h->slots,
+                      h->ctr, last, out_removed, cx_build_args(h));
+    return launch(h, "k_unreg_commit", g, b, 0, k_unreg_commit_elect, (const uint32_t*)slot_of, n, h->slots, h->ctr,
+                  last, out_removed);
+}
+
+// One u32 per table slot, zero between directory batches (gd_dir_upsert's last writer, the registration
+// and removal elections); (re)zeroed when the table grew.
+int slot_words(gd_handle* h) {
+    if (h->up_last.bytes >= h->capacity * 4) return GD_OK;
+    GD_TRY(ensure_own(h, h->up_last, h->capacity * 4));
+    HIP_TRY(h, hipMemsetAsync(h->up_last.p, 0, h->up_last.bytes, h->stream));
+    return GD_OK;
 }
 }  // namespace gdx
 
@@ -420,10 +447,7 @@ int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t
     GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));   // slot_of
     GD_TRY(ensure(h, h->u8_a, (size_t)n));        // is_new
     GD_TRY(ensure(h, h->out_b, (size_t)n));
-    if (h->up_last.bytes < h->capacity * 4) {     // one u32 per slot, kept zero between calls
-        GD_TRY(ensure(h, h->up_last, h->capacity * 4));
-        HIP_TRY(h, hipMemsetAsync(h->up_last.p, 0, h->up_last.bytes, h->stream));
-    }
+    GD_TRY(slot_words(h));                        // one u32 per slot, kept zero between calls
     HIP_TRY(h, hipMemsetAsync(h->u8_a.p, 0, n, h->stream));
     const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
     uint32_t* slot_of = (uint32_t*)h->u32_a.p;
@@ -435,7 +459,7 @@ int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t
     for (uint32_t pass = 0;; ++pass) {            // the registration's claim protocol (k_reg_claim)
         HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
         GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
-                      (uint32_t)(pass > 0), (const gd_val*)h->out_c.p, table_args(h)));
+                      (uint32_t)(pass > 0), (const gd_val*)h->out_c.p, table_args(h), (uint32_t*)nullptr));
         GD_TRY(pull_counters(h));
         if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
         if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_upsert: claims did not settle");
@@ -842,6 +866,7 @@ struct gd_microbatch {
     uint64_t runs_done = 0;
     std::vector<std::pair<uint32_t, hipGraphExec_t>> graphs;
     uint64_t graphs_gen = 0;       // handle layout the cached graphs were captured against
+    uint64_t graphs_cx = ~0ull;    // the probe index build they read (~0: the directory)
 
     uint32_t* out_u32(uint8_t* base, int k) const {
         const size_t c = capacity;
@@ -875,6 +900,12 @@ int mb_launch_sort(gd_microbatch* mb, dim3 grid, uint32_t bits, const uint32_t* 
     }
 }
 
+// The micro-batch route reads the 8-B index when it is built, current and not turned off (GD_OPT_PROBE
+// 0) or pinned to the directory (gd_tune_set(GD_TUNE_PROBE_KEYS, 1)).
+bool mb_use_index(const gd_handle* h) {
+    return h->cx_mode != 0 && h->tune_pin[GD_TUNE_PROBE_KEYS] != 1 && h->cx8_ok && cx_current(h);
+}
+
 int mb_enqueue(gd_microbatch* mb, uint32_t n) {
     gd_handle* h = mb->h;
     const bool zc = mb->zero_copy;
@@ -891,19 +922,38 @@ int mb_enqueue(gd_microbatch* mb, uint32_t n) {
         const gd_key* k = mb->h_keys_dev;
         uint32_t *so = mb->out_u32(d, 0);
         uint8_t* st = mb->out_status(d);
-        switch (h->ring_mode) {
-            case GD_RING_DIRECTORY:
-                GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_DIRECTORY>, k, n, ring_args(h),
-                              table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts));
-                break;
-            case GD_RING_CONSISTENT:
-                GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_CONSISTENT>, k, n, ring_args(h),
-                              table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts));
-                break;
-            default:
-                GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_VIRTUAL_BUCKETS>, k, n,
-                              ring_args(h), table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts));
-                break;
+        // the 8-B index when it is current (gd_microbatch_run keys its graphs by that choice)
+        if (mb_use_index(h)) {
+            const Cx8Args c8 = cx8_args(h);
+            switch (h->ring_mode) {
+                case GD_RING_DIRECTORY:
+                    GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_DIRECTORY, true>, k, n,
+                                  ring_args(h), table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts, c8));
+                    break;
+                case GD_RING_CONSISTENT:
+                    GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_CONSISTENT, true>, k, n,
+                                  ring_args(h), table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts, c8));
+                    break;
+                default:
+                    GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_VIRTUAL_BUCKETS, true>, k, n,
+                                  ring_args(h), table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts, c8));
+                    break;
+            }
+        } else {
+            switch (h->ring_mode) {
+                case GD_RING_DIRECTORY:
+                    GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_DIRECTORY>, k, n,
+                                  ring_args(h), table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts, Cx8Args{}));
+                    break;
+                case GD_RING_CONSISTENT:
+                    GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_CONSISTENT>, k, n,
+                                  ring_args(h), table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts, Cx8Args{}));
+                    break;
+                default:
+                    GD_TRY(launch(h, "k_mb_route", g, b, ring_lds(h), k_mb_route<GD_RING_VIRTUAL_BUCKETS>, k, n,
+                                  ring_args(h), table_args(h), so, act_dst, st, mb->out_u32(d, 1), mb->ts, Cx8Args{}));
+                    break;
+            }
         }
     } else if (n) {
         if (!zc)
@@ -1017,10 +1067,14 @@ int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
         GD_TRY(mb_enqueue(mb, n));
         return sync(h);
     }
-    if (mb->graphs_gen != h->layout_gen) {     // ring or table moved: drop stale graphs
+    // ring or table moved, or the probe index was rebuilt (a new layout in the captured arguments) or
+    // went stale (a directory change that did not re-project it): drop the captured graphs
+    const uint64_t cx_key = mb_use_index(h) ? h->cx_builds : ~0ull;
+    if (mb->graphs_gen != h->layout_gen || mb->graphs_cx != cx_key) {
         for (auto& g : mb->graphs) (void)hipGraphExecDestroy(g.second);
         mb->graphs.clear();
         mb->graphs_gen = h->layout_gen;
+        mb->graphs_cx = cx_key;
     }
     hipGraphExec_t exec = nullptr;
     for (auto& g : mb->graphs)

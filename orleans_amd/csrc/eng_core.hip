@@ -40,6 +40,11 @@ int bfence(gd_handle* h) {
 
 int ensure(gd_handle* h, DevBuf& b, size_t bytes) {
     GD_TRY(bfence(h));
+    return ensure_own(h, b, bytes);
+}
+
+// ensure() for a buffer no bucketing touches (the directory batches' dir_scr): no bfence.
+int ensure_own(gd_handle* h, DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return GD_OK;
     if (b.p) {
         HIP_TRY(h, hipStreamSynchronize(h->stream));
@@ -179,7 +184,7 @@ static uint32_t bit_len(uint64_t x) {
     return b;
 }
 
-static CxBuild cx_build_args(gd_handle* h) {
+CxBuild cx_build_args(gd_handle* h) {
     return CxBuild{(uint4*)h->cxi_tab.p, (unsigned long long*)h->cxi_types.p,
                    h->cx8_ok ? (unsigned long long*)h->cx8_tab.p : nullptr, h->cx8_layout};
 }
@@ -267,6 +272,15 @@ int cx_sync(gd_handle* h, TabTrack& tt, const uint32_t* slot_of, uint32_t n) {
                   (const Slot*)h->slots, cx_build_args(h), (CxCounters*)h->cxi_ctr.p));
     h->cx_synced += n;
     return GD_OK;
+}
+
+// A directory batch that projects its slots inside its commit kernel: true (and the batch counted as
+// synced) when the indexes were current before it; false leaves a stale index stale.
+bool cx_inline(gd_handle* h, TabTrack& tt, uint32_t n) {
+    tt.synced = true;
+    if (!tt.was_current || !h->cx_ok) return false;
+    h->cx_synced += n;
+    return true;
 }
 
 // The index for the current table: rebuilt (two streaming passes + one host sync) when the table
@@ -749,7 +763,8 @@ int radix_dispatch(gd_handle* h, int bits, const uint32_t* kin, const uint32_t* 
 // the three-pass form).  Leaves the digit totals in last_totals.
 template <int RMAX, int KOUT, bool BALLOT>
 int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t R, uint32_t shift, uint32_t* k1,
-             uint32_t* v1, B2Pack pk = B2Pack{0, 0, 32}) {
+             uint32_t* v1, B2Pack pk = B2Pack{0, 0, 32}, uint32_t ku = 0) {
+    const uint2 clamp = make_uint2(n_act, ku ? ku : n_act);      // keys >= n_act -> ku (b2_clamp)
     const uint32_t tiles = blocks_for(n, B2_TILE);
     const uint32_t hxr = h->hist_xcd && h->xcd_tiles ? 1u : 0u;
     GD_TRY(ensure(h, h->hist, ((size_t)R * tiles + R) * sizeof(uint32_t)));
@@ -758,9 +773,9 @@ int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uin
     // profiles/r03_msd_htpb_ab.txt: 4 is the fastest; fewer tiles leave CUs idle)
     if (tiles >= 1024)
         GD_TRY(launch(h, "k_radix_hist", dim3(blocks_for(tiles, 4)), dim3(B2_NT), 0, k_b2_hist<B2_NT, B2_IT, 4, RMAX>,
-                      acts, n, n_act, R, tiles, hist, shift, hxr));
+                      acts, n, clamp, R, tiles, hist, shift, hxr));
     else
-        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(B2_NT), 0, k_b2_hist<B2_NT, B2_IT, 1, RMAX>, acts, n, n_act,
+        GD_TRY(launch(h, "k_radix_hist", dim3(tiles), dim3(B2_NT), 0, k_b2_hist<B2_NT, B2_IT, 1, RMAX>, acts, n, clamp,
                       R, tiles, hist, shift, hxr));
     const uint32_t* tot = hist + (size_t)R * tiles;
     GD_TRY(launch(h, "k_radix_rowscan", dim3(R), dim3(BLOCK), 0, k_radix_rowscan, hist, tiles, hist + (size_t)R * tiles));
@@ -774,13 +789,13 @@ int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uin
     if constexpr (KOUT == B2_KEY16 && !BALLOT) if (h->b2_persist && n <= (1u << 30)) {
         const uint32_t grid = std::min<uint32_t>(tiles, std::max<uint32_t>(8, (h->b2_persist * h->n_cu) & ~7u));
         GD_TRY(launch(h, "k_radix_scatter", dim3(grid), dim3(B2_NT), 0,
-                      k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT, BALLOT, true>, acts, n, n_act, R, tiles,
+                      k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT, BALLOT, true>, acts, n, clamp, R, tiles,
                       (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk));
         persisted = true;
     }
     if (!persisted)
         GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(B2_NT), 0, k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT, BALLOT>,
-                      acts, n, n_act, R, tiles, (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk));
+                      acts, n, clamp, R, tiles, (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk));
     h->last_totals = tot;
     h->last_digits = R;
     return GD_OK;
@@ -792,13 +807,19 @@ int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uin
 template <bool BALLOT>
 int msd_bucket(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uint32_t* perm, uint32_t* offsets,
                uint32_t* rank_out) {
-    const uint32_t R = (n_act >> MSD_SHIFT) + 1;
+    // The MSD pass clamps the keys at ku, the first key of a range past n_act's, rather than at n_act: the
+    // unrouted messages (act >= n_act: directory misses, which a directory under churn sends in numbers)
+    // get a range of their own, copied in order (msd_range_kp, L <= 1), instead of turning n_act's range
+    // into a hot one ranked in chunks by one workgroup (1 % misses at cfg 2: k_msd_local 0.045 ->
+    // 0.47 ms, tools/churn_probe.py).
+    const uint32_t ku = msd_unrouted_key(n_act);
+    const uint32_t R = (ku >> MSD_SHIFT) + 1;
     if (R > MSD_MAX_RANGES) return set_err(h, GD_EINVAL, "two-level bucketing: n_act too large");
     GD_TRY(ensure(h, h->u32_a, (size_t)n * 4));
     GD_TRY(ensure(h, h->u32_c, (size_t)n * 4));
     uint32_t* k1 = (uint32_t*)h->u32_a.p;
     uint32_t* v1 = (uint32_t*)h->u32_c.p;
-    GD_TRY((msd_pass<B2_RMAX2, B2_KEY16, BALLOT>(h, acts, n, n_act, R, MSD_SHIFT, k1, v1)));
+    GD_TRY((msd_pass<B2_RMAX2, B2_KEY16, BALLOT>(h, acts, n, n_act, R, MSD_SHIFT, k1, v1, B2Pack{0, 0, 32}, ku)));
     return launch(h, "k_msd_local", dim3(std::min<uint32_t>(R, h->n_cu)), dim3(MSD_NT), 0, k_msd_local<BALLOT>,
                   (const uint16_t*)k1, (const uint32_t*)v1, h->last_totals, R, n, n_act, perm, offsets, rank_out);
 }
@@ -952,7 +973,7 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
     }
     StageTime stage(h, "stage:bucket");
     uint32_t a3 = 0, ra3 = 0;
-    const bool one = (n_act >> MSD_SHIFT) + 1 <= MSD_MAX_RANGES;
+    const bool one = (msd_unrouted_key(n_act) >> MSD_SHIFT) + 1 <= MSD_MAX_RANGES;
     const bool three = !one && msd3_split(n_act, &a3, &ra3);
     if (h->msd_mode && n >= (1u << 20) && (one || three)) {
         int meas = -1;

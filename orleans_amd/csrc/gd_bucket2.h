@@ -34,10 +34,14 @@ constexpr int B2_NT = 512;                               // the MSD pass's tile:
 constexpr int B2_IT = 16;
 constexpr uint32_t B2_TILE = B2_NT * B2_IT;
 
+// The clamped key: a key >= c.x (n_act: the unrouted messages) becomes c.y -- n_act itself, or (the
+// one-pass form, msd_unrouted_key) the first key of a range past n_act's, so that they form their own.
+__device__ __forceinline__ uint32_t b2_clamp(uint32_t k, uint2 c) { return k >= c.x ? c.y : k; }
+
 // Histogram of TPB consecutive tiles per workgroup, digit-major counts hist[d * tiles + t] for d < R:
-// the digit of min(key, clamp) >> shift.
+// the digit of b2_clamp(key, clamp) >> shift.
 template <int NT, int IT, int TPB, int RMAX>
-static __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t clamp,
+static __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restrict__ keys, uint32_t n, uint2 clamp,
                                                 uint32_t R, uint32_t tiles, uint32_t* __restrict__ hist,
                                                 uint32_t shift, uint32_t xcd_rev) {
     constexpr uint32_t TILE = NT * IT;
@@ -68,12 +72,12 @@ static __global__ void __launch_bounds__(NT) k_b2_hist(const uint32_t* __restric
             }
         }
         // the wave's hot digit (wave_hot_digit of its first row) counted in a register, the rest in LDS
-        const uint32_t h = wave_hot_digit(min(k[0], clamp) >> shift, base + 4 * threadIdx.x < n);
+        const uint32_t h = wave_hot_digit(b2_clamp(k[0], clamp) >> shift, base + 4 * threadIdx.x < n);
         uint32_t hc = 0;
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
             const uint64_t i = base + 4 * ((j / 4) * NT + threadIdx.x) + (j % 4);
-            const uint32_t d = min(k[j], clamp) >> shift;
+            const uint32_t d = b2_clamp(k[j], clamp) >> shift;
             hist_add(s_cnt[t], s_sink, d, h, i < n, hc);
         }
         hc = wave_sum(hc);
@@ -122,7 +126,7 @@ __device__ __forceinline__ void b2_put(uint32_t* __restrict__ keys_out, uint32_t
 // next tile's activations load under this tile's write-out (128 VGPRs: four waves a SIMD, two
 // workgroups a CU).  Without PERSIST one workgroup a tile, as compiled before the loop existed.
 template <int NT, int IT, int RMAX, int KOUT, bool BALLOT = false, bool PERSIST = false>
-static __global__ void __launch_bounds__(NT, 4) k_b2_scatter(const uint32_t* __restrict__ keys_in, uint32_t n, uint32_t clamp,
+static __global__ void __launch_bounds__(NT, 4) k_b2_scatter(const uint32_t* __restrict__ keys_in, uint32_t n, uint2 clamp,
                                                    uint32_t R, uint32_t tiles, const uint32_t* __restrict__ gscan,
                                                    const uint32_t* __restrict__ totals,
                                                    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
@@ -179,7 +183,7 @@ static __global__ void __launch_bounds__(NT, 4) k_b2_scatter(const uint32_t* __r
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
         const uint32_t pos = (w * IT + r) * WAVE + lane;
-        kk[r] = base + pos < n ? min(kk[r], clamp) : 0u;
+        kk[r] = base + pos < n ? b2_clamp(kk[r], clamp) : 0u;
     }
     __syncthreads();
     // stable rank within the wave: the wave's hot digit (wave_hot_digit of its first row) by ballot in

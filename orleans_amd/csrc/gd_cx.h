@@ -259,4 +259,83 @@ static __global__ void __launch_bounds__(BLOCK) k_cx_sync(const uint32_t* __rest
     if (lane_id() == 0 && m) atomicAdd(&ctr->out8, (uint32_t)__popcll(m));
 }
 
+// A directory batch's commits with the committed slots projected at once (the indexes current before
+// the batch): AddSingleActivation's winner (k_reg_commit) and RemoveActivation's remover
+// (k_unreg_commit) re-project their slot; no k_cx_sync launch.
+static __global__ void __launch_bounds__(BLOCK) k_reg_commit_cx(const uint32_t* __restrict__ slot_of,
+                                                         const uint32_t* __restrict__ win,
+                                                         const gd_val* __restrict__ vals, uint32_t n, Slot* slots,
+                                                         DevCounters* ctr, uint32_t* __restrict__ vtag, uint32_t op,
+                                                         CxBuild B, CxCounters* cctr) {
+    __shared__ unsigned long long s_types[CX_TYPES];
+    cx_stage_types(B.types, s_types);
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    bool out = false;
+    const bool w = i < n && win[i] == i;
+    live_delta(ctr, w, false);
+    if (w) {
+        reg_commit_item(i, slot_of, vals, slots, ctr, vtag, op);
+        const uint32_t s = slot_of[i];
+        const uint4* q = reinterpret_cast<const uint4*>(slots + s);
+        out = !cx_project(q[0], q[1], s, B, s_types, true);
+    }
+    const unsigned long long m = __ballot(out);
+    if (lane_id() == 0 && m) atomicAdd(&cctr->out8, (uint32_t)__popcll(m));
+}
+
+static __global__ void __launch_bounds__(BLOCK) k_reg_commit_elect_cx(const uint32_t* __restrict__ slot_of,
+                                                               const uint8_t* __restrict__ is_new,
+                                                               const gd_val* __restrict__ vals, uint32_t n,
+                                                               Slot* slots, DevCounters* ctr,
+                                                               uint32_t* __restrict__ vtag, uint32_t op,
+                                                               uint32_t* __restrict__ last,
+                                                               uint32_t* __restrict__ win,
+                                                               const uint32_t* __restrict__ unsettled,
+                                                               uint32_t* __restrict__ retry0, CxBuild B,
+                                                               CxCounters* cctr) {
+    __shared__ unsigned long long s_types[CX_TYPES];
+    cx_stage_types(B.types, s_types);
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i == 0 && unsettled) {
+        if (*unsettled) atomicOr(&ctr->err, ERR_UNSETTLED);
+        *retry0 = 0;
+    }
+    const bool w = reg_elected(i, n, slot_of, is_new, last, win);
+    live_delta(ctr, w, false);
+    bool out = false;
+    if (w) {
+        reg_commit_item(i, slot_of, vals, slots, ctr, vtag, op);
+        const uint32_t s = slot_of[i];
+        const uint4* q = reinterpret_cast<const uint4*>(slots + s);
+        out = !cx_project(q[0], q[1], s, B, s_types, true);
+    }
+    const unsigned long long m = __ballot(out);
+    if (lane_id() == 0 && m) atomicAdd(&cctr->out8, (uint32_t)__popcll(m));
+}
+
+static __global__ void __launch_bounds__(BLOCK) k_unreg_commit_elect_cx(const uint32_t* __restrict__ slot_of, uint32_t n,
+                                                                 Slot* slots, DevCounters* ctr,
+                                                                 uint32_t* __restrict__ last,
+                                                                 uint8_t* __restrict__ out_removed, CxBuild B) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool rm = unreg_elected_commit(i, n, slot_of, slots, last, out_removed);
+    live_delta(ctr, rm, true);
+    if (!rm) return;
+    const uint32_t s = slot_of[i];
+    if (B.cx16) B.cx16[s] = make_uint4(0, 0, 0, CX_TOMB);
+    if (B.cx8) B.cx8[s] = CX8_HOLE;
+}
+
+static __global__ void __launch_bounds__(BLOCK) k_unreg_commit_cx(const uint32_t* __restrict__ slot_of, uint32_t n,
+                                                           Slot* slots, DevCounters* ctr,
+                                                           uint8_t* __restrict__ out_removed, CxBuild B) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool rm = i < n && unreg_commit_item(i, slot_of, slots, ctr, out_removed);
+    live_delta(ctr, rm, true);
+    if (!rm) return;
+    const uint32_t s = slot_of[i];
+    if (B.cx16) B.cx16[s] = make_uint4(0, 0, 0, CX_TOMB);       // the tombstone (cx_project of a non-live slot)
+    if (B.cx8) B.cx8[s] = CX8_HOLE;
+}
+
 }  // namespace gd

@@ -83,6 +83,7 @@ struct gd_handle {
     bool ctr_stale = true;            // an untracked table write since the last copy (maybe_grow_async pulls)
     uint64_t pending_in = 0;          // entries asynchronous registrations may have added since the last copy
     DevBuf reg_retry;                 // asynchronous registrations: deferred-claim counts of the gated passes
+    DevBuf dir_scr[3];                // directory batches' scratch (slot_of, win, is_new): never the bucketing's
 
     // scratch
     DevBuf keys_in, u32_a, u32_b, u32_c, u32_d, u8_a, out_a, out_b, out_c, hist, partials, partials2, offs;
@@ -296,6 +297,7 @@ struct Lane {
 // ---- shared across the engine's translation units (definitions in eng_*.hip)
 int set_err(gd_handle* h, int code, const char* fmt, ...);
 int ensure(gd_handle* h, DevBuf& b, size_t bytes);
+int ensure_own(gd_handle* h, DevBuf& b, size_t bytes);
 void free_buf(DevBuf& b);
 int name_id(gd_handle* h, const char* name);
 hipEvent_t take_event(gd_handle* h);
@@ -313,6 +315,8 @@ int cx_ensure(gd_handle* h, bool* ok, uint64_t n);
 bool cx_current(const gd_handle* h);
 struct TabTrack;
 int cx_sync(gd_handle* h, TabTrack& tt, const uint32_t* slot_of, uint32_t n);
+bool cx_inline(gd_handle* h, TabTrack& tt, uint32_t n);
+CxBuild cx_build_args(gd_handle* h);
 int tune_key(int kind, uint64_t n, int sub);
 int tune_nvar(int kind);
 int tune_nvar_now(const gd_handle* h, int kind);
@@ -352,6 +356,7 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
 int unregister_core(gd_handle* h, const gd_key* dk, const uint32_t* dacts, uint32_t n, uint8_t* out_removed);
 int maybe_grow_async(gd_handle* h, uint64_t incoming);
 int bfence(gd_handle* h);
+int slot_words(gd_handle* h);
 int split_count(gd_handle* h, const uint8_t* keep, uint32_t n_keep, uint64_t* total);
 uint64_t grain_tcd(int32_t type_code);
 int fan_count(gd_handle* h, const uint32_t* row_off, uint32_t n_nodes, const uint32_t* frontier, uint32_t nf,

@@ -201,6 +201,7 @@ __device__ __forceinline__ int cx_type_index(const unsigned long long* s_types, 
 // The 8-B index's type index of a key, or -1 when the index does not hold it.
 __device__ __forceinline__ int cx8_type(const Cx8Args& c, uint64_t n0, uint64_t n1, uint64_t tcd) {
     if (n0 != 0 || (n1 >> 32) != 0) return -1;
+    if (c.ntypes <= 1) return c.ntypes && tcd == c.tcd[0] ? 0 : -1;   // one grain class (a uniform branch)
     int t = -1;
 #pragma unroll
     for (int k = (int)CX8_TYPES - 1; k >= 0; --k)
@@ -229,19 +230,20 @@ __device__ __forceinline__ uint32_t lazy_max_probe(const TableArgs& tab) {
 }
 
 // The 16-B index's walk from the home's group q (RG slots, already read): the entry of (want = 0x100 |
-// type slot, n1) or a miss (status left as is).  A key's entry lies within max_probe slots of its home.
+// type slot, n1) or a miss (status left as is).  A key's entry lies within max_probe slots of its home;
+// homes are HOME_ALIGN-aligned, so a walk starts at its group's first slot.
+static_assert(HOME_ALIGN % CX_GROUP == 0 && HOME_ALIGN % CX8_GROUP == 0, "index groups start at homes");
 template <int RG>
 __device__ __forceinline__ void cx16_walk(const CxArgs& c, const TableArgs& tab, uint32_t want, uint64_t n1,
                                           unsigned long long home, uint4 (&q)[RG], uint32_t& silo, uint32_t& act,
                                           uint8_t& status) {
-    const uint32_t off0 = (uint32_t)(home & (RG - 1));
-    unsigned long long g = home - off0;
+    unsigned long long g = home;
     uint32_t last = 0;
     bool done = false;
     for (uint32_t base = 0;; base += RG) {
 #pragma unroll
         for (int k = 0; k < RG; ++k) {
-            if (done || base + (uint32_t)k < off0) continue;
+            if (done) continue;
             const uint4 v = q[k];
             if (v.w == 0) {
                 done = true;                                            // miss
@@ -251,7 +253,7 @@ __device__ __forceinline__ void cx16_walk(const CxArgs& c, const TableArgs& tab,
             }
         }
         if (done) return;
-        if (base == 0) last = off0 + lazy_max_probe(tab);
+        if (base == 0) last = lazy_max_probe(tab);
         if (base + RG > last) return;                                   // past every entry's reach: miss
         g += RG;
         if (g >= c.cap) g = 0;
@@ -262,31 +264,31 @@ __device__ __forceinline__ void cx16_walk(const CxArgs& c, const TableArgs& tab,
 
 // The 8-B index's walk from the home's group q (8 slots as 4 uint4, already read), for the key's low
 // N1 word and type index qt.  Returns true when a redirect entry matched: the directory must answer.
+// Per slot only the tests (empty; key; live with this type or a redirect); the hit is decoded once.
 __device__ __forceinline__ bool cx8_walk(const Cx8Args& c, const TableArgs& tab, uint32_t key, uint32_t qt,
                                          unsigned long long home, uint4 (&q)[CX8_GROUP / 2], uint32_t& silo,
                                          uint32_t& act, uint8_t& status) {
-    const uint32_t off0 = (uint32_t)(home & (CX8_GROUP - 1));
-    const uint32_t am = (1u << c.ab) - 1u, umax = ~0u >> c.ab, smask = (1u << c.sb) - 1u;
-    unsigned long long g = home - off0;
+    const uint32_t umax = ~0u >> c.ab;
+    unsigned long long g = home;
     uint32_t last = 0;
-    bool done = false, redirect = false;
+    bool done = false;
+    uint32_t hit = 0;
     for (uint32_t base = 0;; base += CX8_GROUP) {
 #pragma unroll
         for (int k = 0; k < (int)CX8_GROUP; ++k) {
-            if (done || base + (uint32_t)k < off0) continue;
+            if (done) continue;
             const uint4 v = q[k / 2];
             const uint32_t x = (k & 1) ? v.z : v.x, y = (k & 1) ? v.w : v.y;
-            const uint32_t u = y >> c.ab, a = y & am;
+            const uint32_t u = y >> c.ab;
             if (y == 0) {
                 done = true;                                            // miss
-            } else if (x == key && u != 0 && (u == umax || ((u >> c.sb) == qt))) {
+            } else if (x == key && u != 0 && (u == umax || (u >> c.sb) == qt)) {
                 done = true;
-                if (u == umax || a == am - 1u) redirect = true;
-                else entry_result(tab, a == am ? GD_ACT_MULTI : a, (u & smask) - 1u, silo, act, status);
+                hit = y;
             }
         }
-        if (done) return redirect;
-        if (base == 0) last = off0 + lazy_max_probe(tab);
+        if (done) break;
+        if (base == 0) last = lazy_max_probe(tab);
         if (base + CX8_GROUP > last) return false;                      // past every entry's reach: miss
         g += CX8_GROUP;
         if (g >= c.cap) g = 0;
@@ -294,6 +296,11 @@ __device__ __forceinline__ bool cx8_walk(const Cx8Args& c, const TableArgs& tab,
 #pragma unroll
         for (int k = 0; k < (int)CX8_GROUP / 2; ++k) q[k] = qp[k];
     }
+    if (hit == 0) return false;
+    const uint32_t am = (1u << c.ab) - 1u, u = hit >> c.ab, a = hit & am;
+    if (u == umax || a == am - 1u) return true;                         // redirect: the directory answers
+    entry_result(tab, a == am ? GD_ACT_MULTI : a, (u & ((1u << c.sb) - 1u)) - 1u, silo, act, status);
+    return false;
 }
 
 // Linear probe of the open-addressing directory for a live entry with this key.
@@ -593,14 +600,16 @@ __device__ __forceinline__ void mb_mark(unsigned long long* ts, int k, unsigned 
     }
 }
 
-template <int MODE>
+// CX8: through the 8-B index (when it is current: gd_microbatch_run re-captures its graphs when the
+// index is rebuilt or goes stale), the directory otherwise.
+template <int MODE, bool CX8 = false>
 static __global__ void __launch_bounds__(MB_ROUTE_BLOCK) k_mb_route(const gd_key* __restrict__ keys, uint32_t n,
                                                             RingArgs ring, TableArgs tab,
                                                             uint32_t* __restrict__ out_silo,
                                                             uint32_t* __restrict__ out_act,
                                                             uint8_t* __restrict__ out_status,
                                                             uint32_t* __restrict__ act_host,
-                                                            unsigned long long* ts) {
+                                                            unsigned long long* ts, Cx8Args cx8 = Cx8Args{}) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
@@ -609,9 +618,10 @@ static __global__ void __launch_bounds__(MB_ROUTE_BLOCK) k_mb_route(const gd_key
     stage_ring(ring, s_pts, s_own);
     mb_mark(ts, 1, t);
     // act goes to HBM for the sort and, from these 64 workgroups, to the host block as well
-    route_m_core<MODE, 1, MB_ROUTE_BLOCK, false, 0>(keys, n, blockIdx.x * MB_ROUTE_BLOCK + threadIdx.x, ring,
-                                                        s_pts, s_own, tab, tab.ctr->max_probe, out_silo, out_act,
-                                                        out_status, 0, act_host, act_host ? 1u : 0u);
+    route_m_core<MODE, 1, MB_ROUTE_BLOCK, false, 0, false, false, (int)CX_GROUP, CX8>(
+        keys, n, blockIdx.x * MB_ROUTE_BLOCK + threadIdx.x, ring, s_pts, s_own, tab,
+        CX8 ? 0u : tab.ctr->max_probe, out_silo, out_act, out_status, 0, act_host, act_host ? 1u : 0u, nullptr,
+        nullptr, &cx8);
     mb_mark(ts, 2, t);
     if (ts) {
         __threadfence_system();
@@ -752,44 +762,196 @@ constexpr uint32_t SLOT_RETRY = 0xFFFFFFFEu;
 __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restrict__ keys, Slot* slots,
                                                unsigned long long mask, DevCounters* ctr,
                                                uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
-                                               const gd_val* __restrict__ vals, const TableArgs& vt, uint32_t* retry);
+                                               const gd_val* __restrict__ vals, const TableArgs& vt, uint32_t* retry,
+                                               uint32_t& pdist, bool& reused);
+// The claims' counter updates, one atomic a wave (one per item queued ~10^4 same-address atomics behind a
+// 1 % registration batch: 0.12 ms of it at cfg 2).  Every lane of the wave calls it.
+__device__ __forceinline__ void claim_counters(DevCounters* ctr, uint32_t pdist, bool reused) {
+    for (int off = WAVE / 2; off > 0; off >>= 1) pdist = max(pdist, (uint32_t)__shfl_xor(pdist, off, WAVE));
+    const unsigned long long m = __ballot(reused);
+    if ((threadIdx.x & (WAVE - 1)) == 0) {
+        if (pdist) atomicMax(&ctr->max_probe, pdist);
+        if (m) atomicAdd(&ctr->tomb, ~(unsigned long long)__popcll(m) + 1ull);   // - reused
+    }
+}
 
+// last (optional): one word per table slot, zero between batches -- an item that ends with a new entry
+// (claimed it, or found it PENDING) elects itself: atomicMax(~i), so the lowest batch index wins
+// (k_reg_commit_elect); null: the k_reg_minwin / k_reg_resolve election on the slot's act word.
 static __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __restrict__ keys, uint32_t n, Slot* slots,
                                                      unsigned long long mask, DevCounters* ctr,
                                                      uint32_t* __restrict__ slot_of,
                                                      uint8_t* __restrict__ is_new, uint32_t retry_only,
-                                                     const gd_val* __restrict__ vals, TableArgs vt) {
+                                                     const gd_val* __restrict__ vals, TableArgs vt,
+                                                     uint32_t* __restrict__ last = nullptr) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    if (retry_only && slot_of[i] != SLOT_RETRY) return;
-    reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, &ctr->retry);
+    uint32_t pd = 0;
+    bool reused = false;
+    if (i < n && (!retry_only || slot_of[i] == SLOT_RETRY)) {
+        reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, &ctr->retry, pd, reused);
+        if (last && is_new[i]) atomicMax(&last[slot_of[i]], ~i);
+    }
+    claim_counters(ctr, pd, reused);
 }
 
+constexpr uint32_t REG_PASSES = 4;          // k_reg_take + the gated claim passes of an asynchronous batch
 // The claim pass of an asynchronous batch (gd_dir_register_device_async): pass p > 0 runs only when
 // pass p - 1 deferred items (gate = its retry count; all lanes read the same word), so the host enqueues
 // REG_PASSES passes without reading a count back; k_reg_settled flags a batch still unsettled after them.
-constexpr uint32_t REG_PASSES = 6;
 static __global__ void __launch_bounds__(BLOCK) k_reg_claim_gated(const gd_key* __restrict__ keys, uint32_t n,
                                                            Slot* slots, unsigned long long mask, DevCounters* ctr,
                                                            uint32_t* __restrict__ slot_of,
                                                            uint8_t* __restrict__ is_new,
                                                            const gd_val* __restrict__ vals, TableArgs vt,
-                                                           const uint32_t* __restrict__ gate, uint32_t* retry) {
+                                                           const uint32_t* __restrict__ gate, uint32_t* retry,
+                                                           uint32_t* __restrict__ last) {
     if (gate && *gate == 0) return;
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    if (gate && slot_of[i] != SLOT_RETRY) return;
-    reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, retry);
+    // pass 0 zeroes the later passes' counters (its own, retry[0], was zeroed by the previous batch's
+    // k_reg_minwin_gated, or at allocation)
+    if (!gate && i < REG_PASSES - 1) retry[1 + i] = 0;
+    uint32_t pd = 0;
+    bool reused = false;
+    if (i < n && (!gate || slot_of[i] == SLOT_RETRY)) {
+        reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, retry, pd, reused);
+        if (is_new[i]) atomicMax(&last[slot_of[i]], ~i);    // the election (k_reg_commit_elect)
+    }
+    claim_counters(ctr, pd, reused);
 }
+// The claim as two kernels (round 6; the single claim kernel walked each chain with agent-scope atomic
+// loads, two dependent L2 round trips a slot, 0.08 ms for a 10^4-item batch at cfg 2):
+//   k_reg_find  read-only (nothing writes the table during it): each item's existing entry, or the first
+//               free slot of its chain (its first tombstone, else the empty slot ending it) and that
+//               slot's meta, with plain loads;
+//   k_reg_take  one CAS on that slot from the meta seen; an item that loses it (another item of the
+//               batch took the slot: the same key or a colliding one) is deferred to the gated claim
+//               passes (k_reg_claim_gated, the full protocol).
+constexpr uint8_t REG_CANDIDATE = 2;        // is_new: k_reg_find left a free slot to take
+static __global__ void __launch_bounds__(BLOCK) k_reg_find(const gd_key* __restrict__ keys, uint32_t n,
+                                                    const Slot* __restrict__ slots, unsigned long long mask,
+                                                    DevCounters* ctr, uint32_t* __restrict__ slot_of,
+                                                    uint8_t* __restrict__ is_new, uint32_t* __restrict__ seen,
+                                                    const gd_val* __restrict__ vals, TableArgs vt) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    if (vals && !tab_silo_valid(vt, vals[i].silo)) {
+        slot_of[i] = NONE32;
+        is_new[i] = 0;
+        return;
+    }
+    const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
+    unsigned long long s = home_slot(uniform_hash(n0, n1, tcd), mask);
+    unsigned long long free_s = ~0ull;
+    uint32_t free_meta = 0, res = NONE32;
+    uint8_t st_out = 0;
+    // four slots (one 128-B line) a step: homes are 8-slot aligned, so a chain is mostly one or two steps
+    bool done = false;
+    for (unsigned long long dist = 0; !done && dist <= mask; dist += 4) {
+        uint4 q[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4* p = reinterpret_cast<const uint4*>(slots + ((s + k) & mask));
+            q[2 * k] = p[0];
+            q[2 * k + 1] = p[1];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (done) continue;
+            const uint4 a = q[2 * k], b = q[2 * k + 1];
+            const uint32_t st = slot_state(b.w);
+            const unsigned long long sk = (s + k) & mask;
+            if (st == SLOT_EMPTY) {
+                if (free_s == ~0ull) {
+                    free_s = sk;
+                    free_meta = b.w;
+                }
+                done = true;
+            } else {
+                if (st == SLOT_TOMB && free_s == ~0ull) {
+                    free_s = sk;
+                    free_meta = b.w;
+                }
+                if (st == SLOT_LIVE && ((uint64_t)a.x | ((uint64_t)a.y << 32)) == n0 &&
+                    ((uint64_t)a.z | ((uint64_t)a.w << 32)) == n1 && ((uint64_t)b.x | ((uint64_t)b.y << 32)) == tcd) {
+                    res = (uint32_t)sk;                  // registered already
+                    done = true;
+                }
+            }
+        }
+        s = (s + 4) & mask;
+    }
+    if (res == NONE32) {
+        if (free_s == ~0ull) {
+            atomicOr(&ctr->err, 2u);                     // no free slot: the table is full
+        } else {
+            res = (uint32_t)free_s;
+            seen[i] = free_meta;
+            st_out = REG_CANDIDATE;
+        }
+    }
+    slot_of[i] = res;
+    is_new[i] = st_out;
+}
+
+static __global__ void __launch_bounds__(BLOCK) k_reg_take(const gd_key* __restrict__ keys, uint32_t n, Slot* slots,
+                                                    unsigned long long mask, DevCounters* ctr,
+                                                    const gd_val* __restrict__ vals, TableArgs vt,
+                                                    uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
+                                                    const uint32_t* __restrict__ seen, uint32_t* retry,
+                                                    uint32_t* zero, uint32_t* __restrict__ last) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (zero && i < REG_PASSES - 1) zero[i] = 0;         // the gated passes' counters (asynchronous batches)
+    uint32_t pd = 0;
+    bool reused = false;
+    if (i < n && is_new[i] == REG_CANDIDATE) {
+        const uint32_t t = slot_of[i];
+        uint32_t expected = seen[i];
+        uint32_t* mp = &slots[t].meta;
+        if (__hip_atomic_compare_exchange_strong(mp, &expected, make_meta(SLOT_CLAIMED, 0), __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
+            __hip_atomic_store(&slots[t].n0, n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&slots[t].n1, n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&slots[t].tcd, tcd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&slots[t].act, NONE32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(mp, make_meta(SLOT_PENDING, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long home = home_slot(uniform_hash(n0, n1, tcd), mask);
+            pd = (uint32_t)((t - home) & mask);
+            reused = slot_state(seen[i]) == SLOT_TOMB;
+            is_new[i] = 1;
+            atomicMax(&last[t], ~i);                     // the election (k_reg_commit_elect)
+        } else {
+            // taken meanwhile (another new grain homed nearby, or this key's twin): the full protocol from
+            // the home, here -- it defers to the gated passes only an item that meets an unpublished claim
+            reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, retry, pd, reused);
+            if (is_new[i]) atomicMax(&last[slot_of[i]], ~i);
+        }
+    }
+    claim_counters(ctr, pd, reused);
+}
+
 constexpr uint32_t ERR_UNSETTLED = 64u;     // DevCounters::err: an asynchronous batch's claims did not settle
-static __global__ void k_reg_settled(const uint32_t* __restrict__ last_retry, DevCounters* ctr) {
-    if (threadIdx.x == 0 && *last_retry) atomicOr(&ctr->err, ERR_UNSETTLED);
+// k_reg_minwin for an asynchronous batch: also flags claims still deferred after the last gated pass
+// (ERR_UNSETTLED) and zeroes pass 0's counter for the next batch.
+static __global__ void __launch_bounds__(BLOCK) k_reg_minwin_gated(const uint32_t* __restrict__ slot_of,
+                                                            const uint8_t* __restrict__ is_new, uint32_t n, Slot* slots,
+                                                            uint32_t* retry, DevCounters* ctr) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i == 0) {
+        if (retry[REG_PASSES - 1]) atomicOr(&ctr->err, ERR_UNSETTLED);
+        retry[0] = 0;
+    }
+    if (i >= n || !is_new[i]) return;
+    atomicMin(&slots[slot_of[i]].act, i);
 }
 
 __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restrict__ keys, Slot* slots,
                                                unsigned long long mask, DevCounters* ctr,
                                                uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
-                                               const gd_val* __restrict__ vals, const TableArgs& vt, uint32_t* retry) {
+                                               const gd_val* __restrict__ vals, const TableArgs& vt, uint32_t* retry,
+                                               uint32_t& pdist, bool& reused) {
     if (vals && !tab_silo_valid(vt, vals[i].silo)) {
         slot_of[i] = NONE32;
         is_new[i] = 0;
@@ -819,7 +981,7 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(mp, make_meta(SLOT_PENDING, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        atomicMax(&ctr->max_probe, (uint32_t)d);
+        pdist = (uint32_t)d;                                 // max_probe: claim_counters
         return true;
     };
     // the chain holds no copy of the key: take its first tombstone (or report a full table)
@@ -827,7 +989,7 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
         if (tomb_s == ~0ull) {
             atomicOr(&ctr->err, 2u);
         } else if (claim(tomb_s, tomb_meta, tomb_dist)) {
-            atomicAdd(&ctr->tomb, ~0ull);                    // -1
+            reused = true;                                   // tomb - 1: claim_counters
             res = (uint32_t)tomb_s;
             fresh = 1;
         } else {
@@ -898,20 +1060,72 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_resolve(const uint32_t* __
     win[i] = is_new[i] ? slots[slot_of[i]].act : NONE32;
 }
 
+__device__ __forceinline__ void reg_commit_item(uint32_t i, const uint32_t* __restrict__ slot_of,
+                                                const gd_val* __restrict__ vals, Slot* slots, DevCounters* ctr,
+                                                uint32_t* __restrict__ vtag, uint32_t op);
+// live (+1 an insert, or -1 and tomb +1 a removal) for the wave's flagged lanes, one atomic each a wave.
+// Every lane of the wave calls it.
+__device__ __forceinline__ void live_delta(DevCounters* ctr, bool flag, bool removal) {
+    const unsigned long long m = __ballot(flag);
+    if ((threadIdx.x & (WAVE - 1)) != 0 || !m) return;
+    const unsigned long long c = (unsigned long long)__popcll(m);
+    atomicAdd(&ctr->live, removal ? ~c + 1ull : c);
+    if (removal) atomicAdd(&ctr->tomb, c);
+}
 static __global__ void __launch_bounds__(BLOCK) k_reg_commit(const uint32_t* __restrict__ slot_of,
                                                       const uint32_t* __restrict__ win,
                                                       const gd_val* __restrict__ vals, uint32_t n, Slot* slots,
                                                       DevCounters* ctr, uint32_t* __restrict__ vtag, uint32_t op) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n || win[i] != i) return;
+    const bool w = i < n && win[i] == i;
+    if (w) reg_commit_item(i, slot_of, vals, slots, ctr, vtag, op);
+    live_delta(ctr, w, false);
+}
+// The commit of a batch elected by `last` (k_reg_take / the claim passes): item i commits when it holds its
+// slot's word (~i), clears the word for the next batch, and records win[i] (i or NONE32) for k_reg_report.
+// unsettled (optional): the last gated pass's deferred count -- a batch still unsettled flags ERR_UNSETTLED
+// -- and retry0, zeroed here for the next batch (k_reg_take counts into it).
+__device__ __forceinline__ bool reg_elected(uint32_t i, uint32_t n, const uint32_t* __restrict__ slot_of,
+                                            const uint8_t* __restrict__ is_new, uint32_t* __restrict__ last,
+                                            uint32_t* __restrict__ win) {
+    if (i >= n) return false;
+    bool w = false;
+    if (is_new[i]) {
+        const uint32_t s = slot_of[i];
+        w = last[s] == ~i;
+        if (w) last[s] = 0;                              // losers read ~winner or 0: never their own
+    }
+    win[i] = w ? i : NONE32;
+    return w;
+}
+__device__ __forceinline__ void reg_commit_item(uint32_t i, const uint32_t* __restrict__ slot_of,
+                                                const gd_val* __restrict__ vals, Slot* slots, DevCounters* ctr,
+                                                uint32_t* __restrict__ vtag, uint32_t op) {
     Slot& sl = slots[slot_of[i]];
     if (vals[i].silo > 0xFFFEu) atomicOr(&ctr->err, 4u);   // silo index out of range (device-side values)
     sl.act = vals[i].act;
     sl.meta = make_meta(SLOT_LIVE, vals[i].silo);
     // GrainInfo.AddSingleActivation: SingleInstance = true, VersionTag = rand.Next() (:110-124)
     if (vtag) vtag[slot_of[i]] = VTAG_SINGLE | version_tag(op, uniform_hash(sl.n0, sl.n1, sl.tcd));
-    atomicAdd(&ctr->live, 1ull);
 }
+
+static __global__ void __launch_bounds__(BLOCK) k_reg_commit_elect(const uint32_t* __restrict__ slot_of,
+                                                            const uint8_t* __restrict__ is_new,
+                                                            const gd_val* __restrict__ vals, uint32_t n, Slot* slots,
+                                                            DevCounters* ctr, uint32_t* __restrict__ vtag, uint32_t op,
+                                                            uint32_t* __restrict__ last, uint32_t* __restrict__ win,
+                                                            const uint32_t* __restrict__ unsettled,
+                                                            uint32_t* __restrict__ retry0) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i == 0 && unsettled) {
+        if (*unsettled) atomicOr(&ctr->err, ERR_UNSETTLED);
+        *retry0 = 0;                                     // k_reg_take's counter, for the next batch
+    }
+    const bool w = reg_elected(i, n, slot_of, is_new, last, win);
+    if (w) reg_commit_item(i, slot_of, vals, slots, ctr, vtag, op);
+    live_delta(ctr, w, false);
+}
+
 
 // gd_dir_upsert: the last batch item of each slot wins (batch order), then writes its value.
 // `last` (one u32 per table slot, zero between calls) holds 1 + the winning index.
@@ -993,6 +1207,55 @@ static __global__ void __launch_bounds__(BLOCK) k_unreg_find(const gd_key* __res
     slot_of[i] = res;
 }
 
+// RemoveActivation with the election in a per-slot word (round 6: 2 launches instead of 4): the find also
+// elects the first matching item of the batch (atomicMax(~i)), the commit tombstones the slot for the
+// elected item and clears the word.
+static __global__ void __launch_bounds__(BLOCK) k_unreg_find_elect(const gd_key* __restrict__ keys,
+                                                            const uint32_t* __restrict__ acts, uint32_t n,
+                                                            const Slot* slots, unsigned long long mask,
+                                                            const DevCounters* ctr, uint32_t* __restrict__ slot_of,
+                                                            uint32_t* __restrict__ last) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
+    unsigned long long s = home_slot(uniform_hash(n0, n1, tcd), mask);
+    uint32_t res = NONE32;
+    for (uint32_t p = 0; p <= ctr->max_probe; ++p) {
+        const uint4* q = reinterpret_cast<const uint4*>(slots + s);
+        const uint4 a = q[0], b = q[1];
+        const uint32_t st = slot_state(b.w);
+        if (st == SLOT_EMPTY) break;
+        if (st == SLOT_LIVE && ((uint64_t)a.x | ((uint64_t)a.y << 32)) == n0 &&
+            ((uint64_t)a.z | ((uint64_t)a.w << 32)) == n1 && ((uint64_t)b.x | ((uint64_t)b.y << 32)) == tcd) {
+            if (b.z == acts[i]) res = (uint32_t)s;
+            break;
+        }
+        s = (s + 1) & mask;
+    }
+    slot_of[i] = res;
+    if (res != NONE32) atomicMax(&last[res], ~i);
+}
+__device__ __forceinline__ bool unreg_elected_commit(uint32_t i, uint32_t n, const uint32_t* __restrict__ slot_of,
+                                                     Slot* slots, uint32_t* __restrict__ last,
+                                                     uint8_t* __restrict__ out_removed) {
+    if (i >= n) return false;
+    const uint32_t s = slot_of[i];
+    const bool rm = s != NONE32 && last[s] == ~i;
+    if (rm) {
+        slots[s].meta = make_meta(SLOT_TOMB, 0);
+        last[s] = 0;
+    }
+    if (out_removed) out_removed[i] = rm ? 1 : 0;
+    return rm;
+}
+static __global__ void __launch_bounds__(BLOCK) k_unreg_commit_elect(const uint32_t* __restrict__ slot_of, uint32_t n,
+                                                              Slot* slots, DevCounters* ctr,
+                                                              uint32_t* __restrict__ last,
+                                                              uint8_t* __restrict__ out_removed) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    live_delta(ctr, unreg_elected_commit(i, n, slot_of, slots, last, out_removed), true);
+}
+
 // The matched entry is being removed, so its n0 word can carry the election.
 static __global__ void __launch_bounds__(BLOCK) k_unreg_poison(const uint32_t* __restrict__ slot_of, uint32_t n, Slot* slots) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
@@ -1006,20 +1269,23 @@ static __global__ void __launch_bounds__(BLOCK) k_unreg_min(const uint32_t* __re
     atomicMin(reinterpret_cast<unsigned long long*>(&slots[slot_of[i]].n0), (unsigned long long)i);
 }
 
+__device__ __forceinline__ bool unreg_commit_item(uint32_t i, const uint32_t* __restrict__ slot_of, Slot* slots,
+                                                  DevCounters* ctr, uint8_t* __restrict__ out_removed) {
+    const uint32_t s = slot_of[i];
+    uint8_t removed = 0;
+    if (s != NONE32 && slots[s].n0 == (uint64_t)i) {
+        slots[s].meta = make_meta(SLOT_TOMB, 0);       // live - 1, tomb + 1: the kernel's live_delta
+        removed = 1;
+    }
+    if (out_removed) out_removed[i] = removed;
+    return removed != 0;
+}
 static __global__ void __launch_bounds__(BLOCK) k_unreg_commit(const uint32_t* __restrict__ slot_of, uint32_t n,
                                                         Slot* slots, DevCounters* ctr,
                                                         uint8_t* __restrict__ out_removed) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t s = slot_of[i];
-    uint8_t removed = 0;
-    if (s != NONE32 && slots[s].n0 == (uint64_t)i) {
-        slots[s].meta = make_meta(SLOT_TOMB, 0);
-        atomicAdd(&ctr->live, ~0ull);   // -1
-        atomicAdd(&ctr->tomb, 1ull);
-        removed = 1;
-    }
-    if (out_removed) out_removed[i] = removed;
+    const bool rm = i < n && unreg_commit_item(i, slot_of, slots, ctr, out_removed);
+    live_delta(ctr, rm, true);
 }
 
 static __global__ void __launch_bounds__(BLOCK) k_dir_lookup(const gd_key* __restrict__ keys, uint32_t n, TableArgs tab,
@@ -1039,27 +1305,32 @@ static __global__ void __launch_bounds__(BLOCK) k_rehash(const Slot* __restrict_
                                                   Slot* slots, unsigned long long mask, DevCounters* ctr,
                                                   const uint32_t* __restrict__ old_vtag, uint32_t* __restrict__ vtag) {
     const unsigned long long j = (unsigned long long)blockIdx.x * BLOCK + threadIdx.x;
-    if (j >= old_cap) return;
-    const Slot sl = old_slots[j];
-    if (slot_state(sl.meta) != SLOT_LIVE) return;
-    unsigned long long s = home_slot(uniform_hash(sl.n0, sl.n1, sl.tcd), mask);
-    for (uint32_t dist = 0; dist <= mask; ++dist) {
-        uint32_t expected = make_meta(SLOT_EMPTY, 0);
-        if (__hip_atomic_compare_exchange_strong(&slots[s].meta, &expected, make_meta(SLOT_CLAIMED, 0),
-                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            slots[s].n0 = sl.n0;
-            slots[s].n1 = sl.n1;
-            slots[s].tcd = sl.tcd;
-            slots[s].act = sl.act;
-            if (vtag) vtag[s] = old_vtag[j];
-            __hip_atomic_store(&slots[s].meta, sl.meta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            atomicMax(&ctr->max_probe, dist);
-            atomicAdd(&ctr->live, 1ull);
-            return;
+    uint32_t pd = 0;
+    bool placed = false;
+    const Slot sl = j < old_cap ? old_slots[j] : Slot{};
+    if (j < old_cap && slot_state(sl.meta) == SLOT_LIVE) {
+        unsigned long long s = home_slot(uniform_hash(sl.n0, sl.n1, sl.tcd), mask);
+        for (uint32_t dist = 0; dist <= mask; ++dist) {
+            uint32_t expected = make_meta(SLOT_EMPTY, 0);
+            if (__hip_atomic_compare_exchange_strong(&slots[s].meta, &expected, make_meta(SLOT_CLAIMED, 0),
+                                                     __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                slots[s].n0 = sl.n0;
+                slots[s].n1 = sl.n1;
+                slots[s].tcd = sl.tcd;
+                slots[s].act = sl.act;
+                if (vtag) vtag[s] = old_vtag[j];
+                __hip_atomic_store(&slots[s].meta, sl.meta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                pd = dist;
+                placed = true;
+                break;
+            }
+            s = (s + 1) & mask;
         }
-        s = (s + 1) & mask;
+        if (!placed) atomicOr(&ctr->err, 2u);
     }
-    atomicOr(&ctr->err, 2u);
+    // one max_probe / live update a wave (one an entry queued 10^6 same-address atomics at cfg 2)
+    claim_counters(ctr, pd, false);
+    live_delta(ctr, placed, false);
 }
 
 // ------------------------------------------------------------------ wave helpers

@@ -59,6 +59,11 @@ constexpr uint32_t MSD_CAP = MSD_RW * MSD_NT;      // messages a workgroup stage
 constexpr int MSD_MID_NT = 512;                    // the three-pass form's mid-size ranges: 512 threads,
 constexpr int MSD_MID_RW = 16;                     // 16 rows a wave: 8,192 messages, 52 KB of LDS (3 a CU)
 constexpr uint32_t MSD_MID_CAP = MSD_MID_NT * MSD_MID_RW;
+// One-pass form: the key the unrouted messages (act >= n_act) are clamped to -- the first key of a range
+// past the one holding n_act (n_act itself when it starts a range), so they form a range of their own.
+__host__ __device__ __forceinline__ uint32_t msd_unrouted_key(uint32_t n_act) {
+    return (uint32_t)(((uint64_t)n_act + MSD_L - 1) & ~(uint64_t)(MSD_L - 1));
+}
 
 template <int NT, int RW>
 struct MsdShared {
@@ -130,10 +135,36 @@ __device__ __forceinline__ void msd_range_kp(MsdShared<NT, RW>& sh, uint32_t b, 
     static_assert(NT >= (int)MSD_LW, "a thread for every u16-pair counter word");
     const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
     const uint32_t k0 = b << MSD_SHIFT;
-    const uint32_t L = min(MSD_L, n_act + 1 - k0);       // activations of this range
+    const uint32_t L = k0 > n_act ? 0u : min(MSD_L, n_act + 1 - k0);   // activations of this range
     const uint16_t* rk = keys16 + base;
     const uint32_t* ri = idx + base;
     if (tid == 0 && b == (n_act >> MSD_SHIFT)) offsets[n_act + 1] = n;   // the range holding n_act: the end
+    if (L <= 1) {
+        // one activation -- or, in the one-pass form, the unrouted messages, which msd_bucket keys at the
+        // first key past n_act's range (their own range, L = 0; the range before writes offsets[n_act]):
+        // the MSD pass left them in message order, which is their bucket order.  Any size, no LDS.
+        if (tid == 0 && L == 1) offsets[k0] = base;
+        after();
+        constexpr int U = 4;
+        for (uint32_t i0 = 0; i0 < S; i0 += U * NT) {
+            uint32_t v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t i = i0 + u * NT + tid;
+                v[u] = i < S ? ri[i] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t i = i0 + u * NT + tid;
+                if (i < S) {
+                    __builtin_nontemporal_store(v[u], perm + base + i);
+                    if (rank_out) rank_out[v[u]] = base + i;
+                }
+            }
+        }
+        __syncthreads();
+        return;
+    }
     for (uint32_t x = tid; x < MSD_L; x += NT) sh.run[x] = 0;
     for (uint32_t x = tid; x < NW * MSD_LW; x += NT) (&sh.wc[0][0])[x] = 0;
     if (S <= CAP) {
@@ -322,19 +353,38 @@ static __global__ void __launch_bounds__(MSD_NT, 1) k_msd_local(const uint16_t* 
         s_base[2 * tid + 1] = ex + t0;
     }
     __syncthreads();
+    // The last range holds one key (msd_bucket clamps the unrouted messages to it: L <= 1), so its bucket
+    // order is the MSD pass's order: every workgroup copies a slice of it (a 1 % miss rate puts 168K
+    // messages there at cfg 2 -- one workgroup copying them was the stage's tail).
+    {
+        const uint32_t bl = R - 1, Sl = totals[bl], basel = s_base[bl];
+        if (blockIdx.x == 0 && tid == 0 && bl == (n_act >> MSD_SHIFT)) {
+            offsets[n_act] = basel;                      // n_act starts the last range: its one activation
+            offsets[n_act + 1] = n;
+        }
+        const uint32_t per = (Sl + gridDim.x - 1) / gridDim.x;
+        const uint32_t c0 = min(Sl, blockIdx.x * per), c1 = min(Sl, c0 + per);
+        for (uint32_t i = c0 + tid; i < c1; i += MSD_NT) {
+            const uint32_t v = idx[basel + i];
+            __builtin_nontemporal_store(v, perm + basel + i);
+            if (rank_out) rank_out[v] = basel + i;
+        }
+    }
+    const uint32_t RL = R - 1;                           // the ranges sorted in LDS
     uint32_t b = blockIdx.x;
-    if (b >= R) return;                                  // uniform over the workgroup
+    if (b >= RL) return;                                 // uniform over the workgroup
     uint32_t kp[MSD_RW / 2], kn[MSD_RW / 2];
     uint32_t S = totals[b];
     msd_load_keys<MSD_NT, MSD_RW>(keys16 + s_base[b], S, kp);
-    for (; b < R; b += gridDim.x) {
+    for (; b < RL; b += gridDim.x) {
         const uint32_t nb = b + gridDim.x;
-        const uint32_t nS = nb < R ? totals[nb] : 0u;
-        const uint32_t nbase = nb < R ? s_base[nb] : 0u;
+        const uint32_t nS = nb < RL ? totals[nb] : 0u;
+        const uint32_t nbase = nb < RL ? s_base[nb] : 0u;
         auto next = [&] { msd_load_keys<MSD_NT, MSD_RW>(keys16 + nbase, nS, kn); };
         msd_range_kp<BALLOT, MSD_NT, MSD_RW>(sh, b, s_base[b], S, keys16, idx, n, n_act, perm, offsets, rank_out, kp,
                                             next);
-        if (S > MSD_CAP) next();                         // a hot range takes the chunked path: no after()
+        // a hot range of several activations takes the chunked path: no after()
+        if (S > MSD_CAP && min(MSD_L, n_act + 1 - min(b << MSD_SHIFT, n_act + 1)) > 1) next();
 #pragma unroll
         for (int j = 0; j < MSD_RW / 2; ++j) kp[j] = kn[j];
         S = nS;

@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Where a churn step's time goes: cfg 2's batch routed + bucketed (a) on the static
+directory, (b) on a directory with 1 % of its grains removed once (the misses' unrouted bucket), (c) under
+churn (1 % unregistered + 1 % registered a step, enqueued), (d) the directory batches alone.  Per-kernel
+times from the library's HIP events (gd_set_kernel_timing) over a few extra steps of each.  One JSON line."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from orleans_amd import graindispatch as g                      # noqa: E402
+from orleans_amd.workloads import grain_keys_torch              # noqa: E402
+
+SILOS = [(f"10.0.0.{i + 1}", 11111, gen) for i, gen in
+         enumerate([138558, 165678, 215136, 61804, 17808, 48728, 207265, 76820])]
+
+
+def main():
+    G, N = 1 << 20, 1 << 24
+    dev = torch.device("cuda:0")
+    tc = g.calculate_id_hash("BenchmarkGrains.Ping.PingGrain")
+    tcd = (3 << 56) + ((tc & 0xFFFFFFFFFFFFFFFF) & 0x00FFFFFFFFFFFFFF)
+    e = g.GrainDispatch(device=0, table_capacity=2 * G, my_silo=0, kernel_timing=False)
+    e.tune_set("probe_keys", 3)
+    e.tune_set("bucket", 1)
+    e.ring_set_silos("D", SILOS)
+    stream = torch.cuda.Stream(dev)
+    e.set_stream(stream.cuda_stream)
+    B = G // 100
+    perm = torch.from_numpy(np.random.default_rng(7).permutation(G).astype(np.int64)).to(dev)
+    with torch.cuda.stream(stream):
+        allk = grain_keys_torch(tcd, torch.arange(G, device=dev), dev)
+        own = torch.empty(G, dtype=torch.int32, device=dev)
+        e.ring_owner_device(allk.data_ptr(), G, own.data_ptr())
+        vals = torch.stack([torch.arange(G, device=dev, dtype=torch.int32), own], 1).contiguous()
+        e.register_device(allk.data_ptr(), vals.data_ptr(), G)
+        ks = torch.from_numpy(np.random.default_rng(0x5EED0001).integers(0, G, size=N)).to(dev)
+        keys = grain_keys_torch(tcd, ks, dev)
+        K = [allk[perm[i * B:(i + 1) * B]].contiguous() for i in range(40)]
+        A = [perm[i * B:(i + 1) * B].to(torch.int32).contiguous() for i in range(40)]
+        V = [vals[perm[i * B:(i + 1) * B]].contiguous() for i in range(40)]
+        silo = torch.empty(N, dtype=torch.int32, device=dev)
+        act = torch.empty(N, dtype=torch.int32, device=dev)
+        st = torch.empty(N, dtype=torch.uint8, device=dev)
+        pm = torch.empty(N, dtype=torch.int32, device=dev)
+        off = torch.empty(G + 2, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def rb():
+        e.route_bucket_device(keys.data_ptr(), N, G, silo.data_ptr(), act.data_ptr(), st.data_ptr(), pm.data_ptr(),
+                              off.data_ptr())
+
+    def timed(fn, steps=40, warm=5):
+        for s in range(warm):
+            fn(s)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(warm, warm + steps):
+            fn(s)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        e.set_kernel_timing(1)
+        e.kernel_times_reset()
+        for s in range(warm + steps, warm + steps + 3):
+            fn(s)
+        torch.cuda.synchronize()
+        kt = {k: round(v[1] / 3, 4) for k, v in e.kernel_times().items()}
+        e.set_kernel_timing(False)
+        return {"ms_per_step": round(ms, 4), "kernels_ms_per_step": kt}
+
+    out = {}
+    with torch.cuda.stream(stream):
+        out["static"] = timed(lambda s: rb())
+        e.unregister_device(K[39].data_ptr(), A[39].data_ptr(), B)
+        out["static_1pct_missing"] = timed(lambda s: rb())
+        e.register_device(K[39].data_ptr(), V[39].data_ptr(), B)
+
+        def churn(s):
+            i = s % 39
+            e.unregister_device(K[i].data_ptr(), A[i].data_ptr(), B)
+            if s:
+                j = (s - 1) % 39
+                e.register_device_async(K[j].data_ptr(), V[j].data_ptr(), B)
+            rb()
+        out["churn"] = timed(churn)
+        e.register_device(K[(5 + 40 + 3 - 1) % 39].data_ptr(), V[(5 + 40 + 3 - 1) % 39].data_ptr(), B)
+
+        def dir_only(s):
+            i = s % 39
+            e.unregister_device(K[i].data_ptr(), A[i].data_ptr(), B)
+            e.register_device_async(K[i].data_ptr(), V[i].data_ptr(), B)
+        out["directory_batches_only"] = timed(dir_only)
+    e.synchronize()
+    out["index"] = e.index_stats()
+    out["stats"] = e.stats()
+    print(json.dumps(out), flush=True)
+    e.close()
+
+
+if __name__ == "__main__":
+    main()
