@@ -933,6 +933,10 @@ int gd_set_kernel_timing(gd_handle* h, int enable);   /* 0 off, 1 every launch, 
 #define GD_OPT_B2_PERSIST   14  /* one-pass two-level form's MSD scatter: k = 1..8 persistent workgroups a
                                    CU, each loading its next tile under the current tile's write-out
                                    (default 2); 0 one workgroup a tile */
+#define GD_OPT_B2_ORDER     15  /* that persistent scatter's tile order within its XCD's tile range: 0 strided
+                                   (workgroup k takes tiles k, k + per, ...), 1 chunked (workgroup k takes a
+                                   run of consecutive tiles, so one digit's runs of neighbouring tiles -- one
+                                   128-B line between them -- leave one workgroup back to back) */
 int gd_option_set(gd_handle* h, int option, int64_t value);
 int gd_option_get(const gd_handle* h, int option, int64_t* value);
 

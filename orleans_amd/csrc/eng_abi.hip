@@ -772,6 +772,10 @@ int gd_option_set(gd_handle* h, int option, int64_t v) {
             if (!in(0, 8)) break;
             h->b2_persist = (uint32_t)v;
             return GD_OK;
+        case GD_OPT_B2_ORDER:
+            if (!in(0, 1)) break;
+            h->b2_order = (uint32_t)v;
+            return GD_OK;
         default: return set_err(h, GD_EINVAL, "gd_option_set: unknown option %d", option);
     }
     return set_err(h, GD_EINVAL, "gd_option_set: option %d: value %lld out of range", option, (long long)v);
@@ -795,6 +799,7 @@ int gd_option_get(const gd_handle* hc, int option, int64_t* v) {
         case GD_OPT_L2_STAGED: *v = h->l2_staged; return GD_OK;
         case GD_OPT_L2_MID: *v = h->l2_mid; return GD_OK;
         case GD_OPT_B2_PERSIST: *v = h->b2_persist; return GD_OK;
+        case GD_OPT_B2_ORDER: *v = h->b2_order; return GD_OK;
         default: return set_err(h, GD_EINVAL, "gd_option_get: unknown option %d", option);
     }
 }

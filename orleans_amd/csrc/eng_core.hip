@@ -790,12 +790,12 @@ int msd_pass(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act, uin
         const uint32_t grid = std::min<uint32_t>(tiles, std::max<uint32_t>(8, (h->b2_persist * h->n_cu) & ~7u));
         GD_TRY(launch(h, "k_radix_scatter", dim3(grid), dim3(B2_NT), 0,
                       k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT, BALLOT, true>, acts, n, clamp, R, tiles,
-                      (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk));
+                      (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk, h->b2_order));
         persisted = true;
     }
     if (!persisted)
         GD_TRY(launch(h, "k_radix_scatter", dim3(tiles), dim3(B2_NT), 0, k_b2_scatter<B2_NT, B2_IT, RMAX, KOUT, BALLOT>,
-                      acts, n, clamp, R, tiles, (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk));
+                      acts, n, clamp, R, tiles, (const uint32_t*)hist, tot, k1, v1, shift, h->xcd_tiles, pk, 0u));
     h->last_totals = tot;
     h->last_digits = R;
     return GD_OK;

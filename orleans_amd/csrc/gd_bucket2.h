@@ -125,12 +125,27 @@ __device__ __forceinline__ void b2_put(uint32_t* __restrict__ keys_out, uint32_t
 // every tile of a workgroup stays in its XCD's range of xcd_tile), the digit totals load once, and the
 // next tile's activations load under this tile's write-out (128 VGPRs: four waves a SIMD, two
 // workgroups a CU).  Without PERSIST one workgroup a tile, as compiled before the loop existed.
+// The persistent scatter's j-th tile for workgroup b (grid a multiple of 8, workgroup b on XCD b % 8):
+// strided (order 0: b + j * grid through xcd_tile), or (order 1) run j of the workgroup's consecutive tiles
+// in its XCD's tile range.  NONE32 past its last.
+__device__ __forceinline__ uint32_t b2_tile_at(uint32_t b, uint32_t j, uint32_t grid, uint32_t tiles, uint32_t xcd,
+                                               uint32_t order) {
+    if (!order || !xcd) {
+        const uint32_t vb = b + j * grid;
+        return vb < tiles ? xcd_tile(vb, tiles, xcd) : NONE32;
+    }
+    const uint32_t x = b & 7u, k = b >> 3, per = grid >> 3, q = tiles >> 3, rem = tiles & 7u;
+    const uint32_t lo = x * q + min(x, rem), len = q + (x < rem ? 1u : 0u);
+    const uint32_t J = (len + per - 1) / per, t = k * J + j;
+    return j < J && t < len ? lo + t : NONE32;
+}
+
 template <int NT, int IT, int RMAX, int KOUT, bool BALLOT = false, bool PERSIST = false>
 static __global__ void __launch_bounds__(NT, 4) k_b2_scatter(const uint32_t* __restrict__ keys_in, uint32_t n, uint2 clamp,
                                                    uint32_t R, uint32_t tiles, const uint32_t* __restrict__ gscan,
                                                    const uint32_t* __restrict__ totals,
                                                    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                   uint32_t shift, uint32_t xcd, B2Pack pk) {
+                                                   uint32_t shift, uint32_t xcd, B2Pack pk, uint32_t order = 0) {
     constexpr int NW = NT / WAVE;
     constexpr uint32_t TILE = NT * IT;
     static_assert(TILE <= 65536 && NW % 2 == 0, "u16 tile positions, wave pairs");
@@ -147,8 +162,9 @@ static __global__ void __launch_bounds__(NT, 4) k_b2_scatter(const uint32_t* __r
     const uint32_t half = (w & 1u) * 16u;
     const unsigned long long lt = (1ull << lane) - 1ull;
     uint32_t kk[IT], rk[IT];
-    uint32_t vb = blockIdx.x;
-    uint32_t tile = xcd_tile(vb, tiles, xcd);
+    uint32_t vj = 0;                                     // the workgroup's tile number (persistent form)
+    uint32_t tile = PERSIST ? b2_tile_at(blockIdx.x, 0, gridDim.x, tiles, xcd, order) : xcd_tile(blockIdx.x, tiles, xcd);
+    if (tile == NONE32) return;                          // (persistent, chunked: no tile for this workgroup)
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
         const uint32_t idx = tile * TILE + (w * IT + r) * WAVE + lane;
@@ -252,9 +268,10 @@ static __global__ void __launch_bounds__(NT, 4) k_b2_scatter(const uint32_t* __r
     }
     __syncthreads();
     // the next tile's activations load under this tile's write-out
-    vb += gridDim.x;
-    const bool more = PERSIST && vb < tiles;
-    const uint32_t ntile = more ? xcd_tile(vb, tiles, xcd) : tile;
+    ++vj;
+    const uint32_t nt_ = PERSIST ? b2_tile_at(blockIdx.x, vj, gridDim.x, tiles, xcd, order) : NONE32;
+    const bool more = PERSIST && nt_ != NONE32;
+    const uint32_t ntile = more ? nt_ : tile;
     if (more) {
 #pragma unroll
         for (int r = 0; r < IT; ++r) {

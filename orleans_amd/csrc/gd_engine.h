@@ -202,6 +202,7 @@ struct gd_handle {
     uint32_t l2_small = 1024;   // three-pass form: ranges of at most this many messages are sorted one wave a range
     uint32_t l2_mid = MSD_MID_CAP;  // three-pass form: staged ranges up to this many messages on the 512-thread sort
     uint32_t b2_persist = 2;       // one-pass MSD scatter: persistent workgroups a CU (0: one a tile; GD_OPT_B2_PERSIST)
+    uint32_t b2_order = 0;         // its tile order: 0 strided, 1 consecutive runs a workgroup (GD_OPT_B2_ORDER)
     uint32_t l2_staged = MSD_CAP;  // three-pass form: ranges up to this many messages one workgroup each, more: chunks
     uint32_t n_cu = 256;        // compute units (hipDeviceProp_t::multiProcessorCount): persistent grids
     DevBuf m3[15];              // three-pass form's scratch (msd3_bucket)

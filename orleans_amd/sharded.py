@@ -93,6 +93,9 @@ class DeviceEngine:
         return send_keys, send_pos, counts
 
     def route_bucket(self, keys: torch.Tensor, n_act: int):
+        """Route + bucket on the engine's stream.  Pipeline mode: the bucketing runs on `bstream` after the
+        route, and perm / offsets (and act's last reader) are done only once `bucket_done_event()` is --
+        a caller reading them on another stream waits on that event (or on bstream) first."""
         n = keys.shape[0]
         dev = self.device
         st = torch.empty(n, dtype=torch.uint8, device=dev)

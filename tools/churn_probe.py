@@ -44,14 +44,17 @@ def main():
         K = [allk[perm[i * B:(i + 1) * B]].contiguous() for i in range(40)]
         A = [perm[i * B:(i + 1) * B].to(torch.int32).contiguous() for i in range(40)]
         V = [vals[perm[i * B:(i + 1) * B]].contiguous() for i in range(40)]
-        silo = torch.empty(N, dtype=torch.int32, device=dev)
-        act = torch.empty(N, dtype=torch.int32, device=dev)
-        st = torch.empty(N, dtype=torch.uint8, device=dev)
-        pm = torch.empty(N, dtype=torch.int32, device=dev)
-        off = torch.empty(G + 2, dtype=torch.int32, device=dev)
+        # two output sets, alternating: with the bucket stream a batch's bucketing still reads its act
+        # while the next batch's route writes
+        outs = [[torch.empty(N, dtype=torch.int32, device=dev), torch.empty(N, dtype=torch.int32, device=dev),
+                 torch.empty(N, dtype=torch.uint8, device=dev), torch.empty(N, dtype=torch.int32, device=dev),
+                 torch.empty(G + 2, dtype=torch.int32, device=dev)] for _ in range(2)]
     torch.cuda.synchronize()
+    nb = [0]
 
     def rb():
+        silo, act, st, pm, off = outs[nb[0] & 1]
+        nb[0] += 1
         e.route_bucket_device(keys.data_ptr(), N, G, silo.data_ptr(), act.data_ptr(), st.data_ptr(), pm.data_ptr(),
                               off.data_ptr())
 
@@ -64,6 +67,7 @@ def main():
             fn(s)
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / steps * 1e3
+        torch.cuda.synchronize()
         e.set_kernel_timing(1)
         e.kernel_times_reset()
         for s in range(warm + steps, warm + steps + 3):
@@ -95,6 +99,19 @@ def main():
             e.unregister_device(K[i].data_ptr(), A[i].data_ptr(), B)
             e.register_device_async(K[i].data_ptr(), V[i].data_ptr(), B)
         out["directory_batches_only"] = timed(dir_only)
+        # the same with each batch's bucketing on a second stream (gd_set_bucket_stream): the directory
+        # batches (their own scratch, no fence on the bucket stream) overlap the previous bucketing
+        bs = torch.cuda.Stream(dev)
+        e.set_bucket_stream(bs.cuda_stream)
+
+        def rb_p():
+            rb()
+
+        out["static_pipelined"] = timed(lambda s: rb_p())
+        out["churn_pipelined"] = timed(churn)
+        stream.wait_stream(bs)
+        torch.cuda.synchronize()
+        e.set_bucket_stream(None)
     e.synchronize()
     out["index"] = e.index_stats()
     out["stats"] = e.stats()
