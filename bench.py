@@ -17,6 +17,7 @@ Prints ONE JSON line on rank 0 (see DESIGN.md for the byte model behind the
 roofline object).
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -485,6 +486,9 @@ def compact_roofline(rf, kernels, with_table=True):
     for k in ("probe_variant", "probe_index_frac_impl"):
         if rf.get(k) is not None:
             out[k] = rf[k]
+    if rf.get("route_bound"):
+        out["route_bound_ms"] = rf["route_bound"].get("ms_per_launch")
+        out["route_bound_frac"] = rf["route_bound"].get("frac_of_bound")
     if rf.get("random_probe_ceiling"):
         out["random_probe_ceiling_frac"] = rf["random_probe_ceiling"].get("frac_of_ceiling")
         out["random_probe_io_ceiling_frac"] = rf["random_probe_ceiling"].get("frac_of_io_ceiling")
@@ -753,7 +757,7 @@ def main():
     if world > 1 and args.workload == "cfg2" and not args.no_secondary:
         secondary["cfg2_other_silo_set"] = other_silo_set_line(args, world, rank, local, dev, tcd)
     if roofline and roofline["kernel"] == "k_route":
-        route_extras(roofline, e, m_recv, args.workload, world, isinstance(router, LibraryRouter))
+        route_extras(roofline, e, m_recv, args.workload, world, isinstance(router, LibraryRouter), keys, stream)
 
     # ---- the directory under churn, a mixed directory, the host-buffer path (cfg 2, N = 1) -------
     if world == 1 and args.workload == "cfg2" and not args.no_secondary:
@@ -826,7 +830,7 @@ def secondary_roofline(w, res, args, tag: str, world: int):
     kt = profile_kernels(w["e"], w["router"], w["keys"], w["n_act"], w["stream"], 3)
     k, rf = roofline_of(kt, 3, m, w["n_act"], acts, tag, world)
     if rf and rf["kernel"] == "k_route":
-        route_extras(rf, w["e"], m, tag, world, isinstance(w["router"], LibraryRouter))
+        route_extras(rf, w["e"], m, tag, world, isinstance(w["router"], LibraryRouter), w["keys"], w["stream"])
     return k, rf
 
 
@@ -849,24 +853,59 @@ def profile_kernels(e, router, keys, n_act, stream, steps: int) -> dict:
     return kt
 
 
-def route_extras(roofline: dict, e, m_recv: int, tag: str, world: int, exchange: bool = False):
+def route_extras(roofline: dict, e, m_recv: int, tag: str, world: int, exchange: bool = False, keys=None,
+                 stream=None):
     """k_route's side fields: the probe variant the library runs (gd_tune_get) and, when it reads a
     compact index (gd_cx.h), the index's own bytes a message.  exchange: the probe reads the library
-    exchange's N1 headers (GD_TUNE_PROBE_N1), at any world size."""
+    exchange's N1 headers (GD_TUNE_PROBE_N1), at any world size.  keys (24-B keys, world 1, 8-B index):
+    the route's memory bound measured live on the same index and key stream (route_bound)."""
     kind = "probe_n1" if exchange or world > 1 else "probe_keys"
     v = e.tune_get(kind, m_recv)
     roofline["probe_variant"] = PROBE_VARIANTS.get(v, str(v))
     t_l = roofline["avg_launch_ms"] * 1e-3
     slot = {0: 16, 2: 16, 3: 8}.get(v)
-    if v == 3 and world == 1:
-        pc = probe_ceiling(tag, m_recv, roofline["avg_launch_ms"])
-        if pc:
-            roofline["random_probe_ceiling"] = pc
+    if v == 3 and world == 1 and not exchange and keys is not None:
+        rb = route_bound(e, keys, stream, roofline["avg_launch_ms"])
+        if rb:
+            roofline["route_bound"] = rb
     if slot:
         # per message: key 24 + one index slot + silo/act/status 9
         impl = m_recv * (24 + slot + 9)
         roofline["probe_index"] = {"slot_bytes": slot, "impl_bytes_per_launch": impl,
                                    "frac_impl": round(impl / t_l / 1e9 / PEAK_HBM_GBS, 4) if t_l > 0 else None}
+
+
+def route_bound(e, keys, stream, launch_ms: float, reps: int = 5):
+    """gd_route_bound_device over the route's own 8-B index and key stream, `reps` launches timed by the
+    library's HIP events on its stream (as k_route is): k_route's launch shape, key reads, one 64-B
+    group read a message and its 9-B writes, with no ring search, walk or fallback (gd_kernels.h
+    k_route_bound).  frac_of_bound = bound / k_route: 1.0 would be a route with nothing but its memory
+    traffic left."""
+    n = int(keys.shape[0])
+    dev = keys.device
+    silo = torch.empty(n, dtype=torch.int32, device=dev)
+    act = torch.empty(n, dtype=torch.int32, device=dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    try:
+        with torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext():
+            e.route_bound_device(keys.data_ptr(), n, silo.data_ptr(), act.data_ptr(), st.data_ptr())   # warm
+            torch.cuda.synchronize()
+            e.set_kernel_timing(1)
+            e.kernel_times_reset()
+            for _ in range(reps):
+                e.route_bound_device(keys.data_ptr(), n, silo.data_ptr(), act.data_ptr(), st.data_ptr())
+            torch.cuda.synchronize()
+            t = e.kernel_times().get("k_route_bound")
+    except (g.GrainDispatchError, AttributeError):
+        return None
+    finally:
+        e.set_kernel_timing(False)
+    if not t or t[0] == 0 or launch_ms <= 0:
+        return None
+    ms = t[1] / t[0]
+    return {"ms_per_launch": round(ms, 4), "frac_of_bound": round(ms / launch_ms, 3),
+            "source": "gd_route_bound_device, live: same index, keys, grid and writes; one 64-B index read a "
+                      "message, no ring / walk / fallback"}
 
 
 # The random-probe ceiling of the 8-B index (tools/ubench_fanprobe.hip, profiles/r05_ubench_fanprobe.txt):

@@ -285,10 +285,11 @@ int gd_route_bucket(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act
                     uint32_t* out_perm, uint32_t* out_offsets);
 
 /* Device-pointer forms (enqueue only).  Same semantics as above.  One exception to "enqueue only": the
- * first route after a change of the directory table rebuilds the library's compact probe index (two
- * kernels over the table) and synchronises the handle's stream once to learn whether the
- * table qualifies; routes in between changes enqueue only.  GD_CX=0 in the environment at gd_create
- * turns the index off. */
+ * first large route after a directory change the probe indexes do not track (rehash, clear, silo
+ * removal, merge, split, handoff; gd_index_stats below) rebuilds them (two streaming passes over the
+ * table) and synchronises the handle's stream once to read the build's counters;
+ * registration / upsert / unregister batches keep the indexes current and routes after them enqueue
+ * only.  GD_CX=0 in the environment at gd_create turns the indexes off. */
 int gd_route_device(gd_handle* h, const gd_key* d_keys, uint32_t n,
                     uint32_t* d_silo, uint32_t* d_act, uint8_t* d_status);
 int gd_bucket_device(gd_handle* h, const uint32_t* d_acts, uint32_t n, uint32_t n_act,
@@ -936,7 +937,8 @@ int gd_set_kernel_timing(gd_handle* h, int enable);   /* 0 off, 1 every launch, 
 #define GD_OPT_B2_ORDER     15  /* that persistent scatter's tile order within its XCD's tile range: 0 strided
                                    (workgroup k takes tiles k, k + per, ...), 1 chunked (workgroup k takes a
                                    run of consecutive tiles, so one digit's runs of neighbouring tiles -- one
-                                   128-B line between them -- leave one workgroup back to back) */
+                                   128-B line between them -- leave one workgroup back to back; measured
+                                   slower, profiles/r06_b2_order_ab.txt) */
 int gd_option_set(gd_handle* h, int option, int64_t value);
 int gd_option_get(const gd_handle* h, int option, int64_t* value);
 
@@ -993,6 +995,13 @@ typedef struct gd_index_stats {
                                  hold or redirects to the directory (incl. the build's own)         */
 } gd_index_stats;
 int gd_index_stats_get(gd_handle* h, gd_index_stats* out);
+/* Diagnostic (no reference counterpart; bench.py's roofline.route_bound): gd_route_device's memory
+ * bound over the current 8-B index -- the route kernel's launch shape, key reads, one 64-B index group
+ * read per message at the key's home and its silo / act / status writes, without the ring search,
+ * the walk past the home group or the directory fallback.  The outputs are NOT route results.
+ * GD_EINVAL when the directory has no 8-B index. */
+int gd_route_bound_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t* d_silo, uint32_t* d_act,
+                          uint8_t* d_status);
 
 #ifdef __cplusplus
 }

@@ -563,6 +563,12 @@ int gd_route_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t* d_
     return n ? route_device(h, d_keys, n, d_silo, d_act, d_status) : GD_OK;
 }
 
+int gd_route_bound_device(gd_handle* h, const gd_key* d_keys, uint32_t n, uint32_t* d_silo, uint32_t* d_act,
+                          uint8_t* d_status) {
+    if (!h || (n && (!d_keys || !d_silo || !d_act || !d_status))) return set_err(h, GD_EINVAL, "null argument");
+    return n ? route_bound_device(h, d_keys, n, d_silo, d_act, d_status) : GD_OK;
+}
+
 int gd_bucket_device(gd_handle* h, const uint32_t* d_acts, uint32_t n, uint32_t n_act, uint32_t* d_perm,
                      uint32_t* d_offsets) {
     if (!h || !d_offsets || (n && (!d_acts || !d_perm))) return set_err(h, GD_EINVAL, "null argument");

@@ -434,6 +434,14 @@ CxArgs cx_args(gd_handle* h) {
 }
 
 // ---- route -------------------------------------------------------------------
+// The tune entry's second class for the bucketing form (kind 4): the messages a 1,024-activation range
+// holds, as a bit length (it decides whether ranges are staged in LDS).
+int bucket_sub(uint64_t n, uint32_t n_act) {
+    int per_range = 0;
+    while (per_range < 31 && ((uint64_t)n / ((n_act >> MSD_SHIFT) + 1) >> per_range) > 1) ++per_range;
+    return per_range;
+}
+
 template <int MODE, int M, bool NT>
 int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status) {
     bool cx = false;
@@ -571,6 +579,27 @@ int route_mode(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uin
     const uint64_t index_bytes = (uint64_t)h->capacity * 8u;
     if (index_bytes <= ROUTE_NT_INDEX_BYTES) return route_launch<MODE, 1, true>(h, keys, n, silo, act, status);
     return route_launch<MODE, 2, false>(h, keys, n, silo, act, status);
+}
+
+// gd_route_bound_device: k_route_bound over the current 8-B index, with route_mode's key-stream rule.
+int route_bound_device(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act,
+                       uint8_t* status) {
+    GD_TRY(check_ring(h));
+    bool cx = false;
+    GD_TRY(cx_ensure(h, &cx, n));
+    if (!cx || !h->cx8_ok) return set_err(h, GD_EINVAL, "route bound: the directory has no 8-B probe index");
+    const uint32_t xcd = h->route_xcd ? 1u : 0u;
+    const unsigned long long mask = h->capacity - 1ull;
+    // two messages a thread: the fastest of the forms measured (profiles/r06_route_bound_forms.json: one
+    // a thread 0.328-0.336 ms with or without the ring-staging barrier and non-temporal keys, two 0.286,
+    // four 0.288; k_route 0.288)
+    const bool nt = (uint64_t)h->capacity * 8u <= ROUTE_NT_INDEX_BYTES;
+    const dim3 g2(blocks_for(n, BLOCK * 2));
+    if (nt)
+        return launch(h, "k_route_bound", g2, dim3(BLOCK), ring_lds(h), k_route_bound<2, true>, keys, n, mask,
+                      cx8_args(h), silo, act, status, xcd);
+    return launch(h, "k_route_bound", g2, dim3(BLOCK), ring_lds(h), k_route_bound<2, false>, keys, n, mask,
+                  cx8_args(h), silo, act, status, xcd);
 }
 
 
@@ -980,8 +1009,7 @@ int bucket_device(gd_handle* h, const uint32_t* acts, uint32_t n, uint32_t n_act
         // keyed by the batch size and by the messages a range holds (which decide whether ranges are
         // staged in LDS): a handle bucketing 16M messages over 1M and over 10k activations keeps one
         // choice for each
-        int per_range = 0;
-        while (per_range < 31 && ((uint64_t)n / ((n_act >> MSD_SHIFT) + 1) >> per_range) > 1) ++per_range;
+        const int per_range = bucket_sub(n, n_act);
         const int var = h->msd_mode == 2 ? 1 : tune_choose(h, 4, n, &meas, 2, per_range);
         CxMeasure mm(h, meas, n);
         // ranks by ds_add_rtn lane order (default) or by ballots (GD_OPT_STABLE_RANK 0; gd_create's

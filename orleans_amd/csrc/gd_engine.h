@@ -337,6 +337,8 @@ int route_cached_keyext(gd_handle* h, const gd_key* keys, const ExtArgs& x, uint
                         uint8_t* st);
 int route_device(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act, uint8_t* status,
                  bool touch = true);
+int route_bound_device(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, uint32_t* act,
+                       uint8_t* status);
 KxArgs kx_args(gd_handle* h);
 int keyext_pass(gd_handle* h, const gd_key* keys, const ExtArgs& x, uint32_t n, uint32_t* silo, uint32_t* act,
                 uint8_t* st);

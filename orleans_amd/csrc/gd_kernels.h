@@ -687,6 +687,54 @@ static __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restri
     }
 }
 
+// The route's memory bound (gd_route_bound_device, a diagnostic, not a route): k_route_m<…, CX8>'s XCD
+// mapping, ring-sized LDS, key reads, home hash, one 64-B group read of the 8-B index per message and
+// silo / act / status writes -- without the ring search, the class checks, the walk past the home group,
+// the redirect decode and the directory fallback; M messages a thread (2: the fastest measured).  On the
+// route's own index and key stream it is the time k_route cannot go under without reading or writing less.
+template <int M, bool NT>
+static __global__ void __launch_bounds__(BLOCK) k_route_bound(const gd_key* __restrict__ keys, uint32_t n,
+                                                       unsigned long long mask, Cx8Args cx8,
+                                                       uint32_t* __restrict__ out_silo,
+                                                       uint32_t* __restrict__ out_act,
+                                                       uint8_t* __restrict__ out_status, uint32_t xcd) {
+    const uint32_t base = xcd_tile(blockIdx.x, gridDim.x, xcd) * (BLOCK * M) + threadIdx.x;
+    uint64_t n1[M];
+    uint4 q[M][CX8_GROUP / 2];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        const uint32_t i = base + j * BLOCK;
+        uint64_t n0 = 0, tcd = 0;
+        n1[j] = 0;
+        if (i < n) {
+            const uint64_t* kp = reinterpret_cast<const uint64_t*>(keys + i);
+            n0 = ld<NT>(kp);
+            n1[j] = ld<NT>(kp + 1);
+            tcd = ld<NT>(kp + 2);
+        }
+        const unsigned long long s = home_slot(uniform_hash(n0, n1[j], tcd), mask);
+        const uint4* qp = cx8.slots + ((s & ~(unsigned long long)(CX8_GROUP - 1)) >> 1);
+#pragma unroll
+        for (int g = 0; g < (int)CX8_GROUP / 2; ++g) q[j][g] = qp[g];
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        const uint32_t i = base + j * BLOCK;
+        uint32_t hit = 0;
+#pragma unroll
+        for (int k = 0; k < (int)CX8_GROUP; ++k) {
+            const uint4 v = q[j][k / 2];
+            const uint32_t x = (k & 1) ? v.z : v.x, y = (k & 1) ? v.w : v.y;
+            if (hit == 0 && y != 0 && x == (uint32_t)n1[j]) hit = y;
+        }
+        if (i < n) {
+            st<true>(out_silo + i, (hit >> cx8.ab) - 1u);
+            out_act[i] = hit & ((1u << cx8.ab) - 1u);
+            st<true>(out_status + i, (uint8_t)(hit == 0));
+        }
+    }
+}
+
 // The owner's probe over received chunks grouped by region (gd_route_multi with regions, SURVEY 8 e):
 // workgroup b takes region g = b % 8.  Workgroups are dispatched round-robin over the 8 XCDs (b -> XCD
 // b % 8), so all of one XCD's workgroups probe one eighth of the table (home_slot's top bits) and its

@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = [
     "gd_ring_owner_device", "gd_pack_by_shard_device", "gd_pack_routes_by_rank_device", "gd_kernel_times",
     "gd_kernel_times_reset",
     "gd_option_set", "gd_option_get", "gd_tune_reset", "gd_tune_set", "gd_tune_get", "gd_tune_agree",
-    "gd_comm_info", "gd_index_stats_get",
+    "gd_comm_info", "gd_index_stats_get", "gd_route_bound_device",
     "gd_set_kernel_timing", "gd_microbatch_create", "gd_microbatch_destroy", "gd_microbatch_keys",
     "gd_microbatch_outputs", "gd_microbatch_run", "gd_decode_frames_device", "gd_decode_frames",
     "gd_route_frames_device", "gd_route_frames", "gd_dir_split", "gd_dir_split_device",
@@ -263,6 +263,7 @@ def _load() -> C.CDLL:
         "gd_bucket": (C.c_int, [P, P, U32, U32, P, P]),
         "gd_route_bucket": (C.c_int, [P, P, U32, U32, P, P, P, P, P]),
         "gd_route_device": (C.c_int, [P, P, U32, P, P, P]),
+        "gd_route_bound_device": (C.c_int, [P, P, U32, P, P, P]),
         "gd_bucket_device": (C.c_int, [P, P, U32, U32, P, P]),
         "gd_route_bucket_device": (C.c_int, [P, P, U32, U32, P, P, P, P, P]),
         "gd_ring_owner_device": (C.c_int, [P, P, U32, P]),
@@ -1056,6 +1057,12 @@ class GrainDispatch:
     def route_device(self, d_keys: int, n: int, d_silo: int, d_act: int, d_status: int):
         self._c(lib.gd_route_device(self.h, C.c_void_p(d_keys), n, C.c_void_p(d_silo), C.c_void_p(d_act),
                                     C.c_void_p(d_status)))
+
+    def route_bound_device(self, d_keys: int, n: int, d_silo: int, d_act: int, d_status: int):
+        """gd_route_bound_device (diagnostic): the route kernel's memory bound over the 8-B index; the
+        outputs are not route results."""
+        self._c(lib.gd_route_bound_device(self.h, C.c_void_p(d_keys), n, C.c_void_p(d_silo), C.c_void_p(d_act),
+                                          C.c_void_p(d_status)))
 
     def bucket_device(self, d_acts: int, n: int, n_act: int, d_perm: int, d_offsets: int):
         self._c(lib.gd_bucket_device(self.h, C.c_void_p(d_acts), n, n_act, C.c_void_p(d_perm), C.c_void_p(d_offsets)))
