@@ -62,9 +62,9 @@ int gd_create(const gd_config* cfg, gd_handle** out) {
     int r = alloc_table(h, h->capacity, &h->slots);
     if (r == GD_OK) r = alloc_vtag(h, h->capacity, &h->vtag);
     if (r == GD_OK) {
-        e = hipMalloc(&h->ctr, sizeof(DevCounters));
+        e = hipMalloc(&h->ctr, CTR_BYTES);
         if (e != hipSuccess) r = set_err(nullptr, GD_ENOMEM, "counters: %s", hipGetErrorString(e));
-        else if ((e = hipMemsetAsync(h->ctr, 0, sizeof(DevCounters), h->stream)) != hipSuccess)
+        else if ((e = hipMemsetAsync(h->ctr, 0, CTR_BYTES, h->stream)) != hipSuccess)
             r = set_err(nullptr, GD_EHIP, "counters memset: %s", hipGetErrorString(e));
     }
     if (r == GD_OK) {
@@ -327,6 +327,7 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
         GD_TRY(launch(h, "k_reg_take", g, b, 0, k_reg_take, dk, n, h->slots, mask, h->ctr, dvals, table_args(h),
                       slot_of, is_new, (const uint32_t*)win, &h->ctr->retry, (uint32_t*)nullptr, last));
         GD_TRY(pull_counters(h));
+        if (getenv("GD_DEBUG_RETRY")) fprintf(stderr, "register n=%u take deferred %u\n", n, h->ctr_host.retry);
         // relaunches for the items that lost their CAS or met an unpublished claim
         for (uint32_t pass = 1; h->ctr_host.retry && !h->ctr_host.err; ++pass) {
             if (pass > 64) return set_err(h, GD_ETIMEOUT, "gd_dir_register: claims did not settle");
@@ -334,6 +335,7 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
             GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new, 1u,
                           dvals, table_args(h), last));
             GD_TRY(pull_counters(h));
+            if (getenv("GD_DEBUG_RETRY")) fprintf(stderr, "  pass %u deferred %u\n", pass, h->ctr_host.retry);
         }
     }
     if (cx_inline(h, tt, n))                       // the winners project their slots as they commit
@@ -513,7 +515,7 @@ int gd_dir_clear(gd_handle* h) {
     HIP_TRY(h, hipMemsetAsync(h->slots, 0, h->capacity * sizeof(Slot), h->stream));
     h->tab_gen++;
     HIP_TRY(h, hipMemsetAsync(h->vtag, 0, h->capacity * sizeof(uint32_t), h->stream));
-    HIP_TRY(h, hipMemsetAsync(h->ctr, 0, sizeof(DevCounters), h->stream));
+    HIP_TRY(h, hipMemsetAsync(h->ctr, 0, CTR_BYTES, h->stream));   // with the striped deltas
     h->ctr_stale = true;
     if (h->kx_cap) {                   // KeyExt entries go too
         h->kx_m.assign(h->kx_cap, KxSlot{});
@@ -539,8 +541,7 @@ int gd_dir_rehash(gd_handle* h, uint64_t new_capacity) {
         (void)hipFree(ns);
         return GD_ENOMEM;
     }
-    DevCounters fresh{};
-    HIP_TRY(h, hipMemcpyAsync(h->ctr, &fresh, sizeof fresh, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipMemsetAsync(h->ctr, 0, CTR_BYTES, h->stream));   // counters and their striped deltas
     const unsigned long long old_cap = h->capacity;
     const uint32_t g = (uint32_t)((old_cap + BLOCK - 1) / BLOCK);
     GD_TRY(launch(h, "k_rehash", dim3(g), dim3(BLOCK), 0, k_rehash, (const Slot*)h->slots, old_cap, ns, cap - 1, h->ctr,

@@ -125,7 +125,15 @@ bool host_silo_valid(const gd_handle* h, uint32_t silo) {
 
 size_t ring_lds(gd_handle* h) { return (size_t)h->ring_n * 2 * sizeof(uint32_t); }
 
+// The striped live / tomb deltas (gd_kernels.h CTR_STRIPES) into the counters, before a read-back.
+int fold_counters(gd_handle* h, DevCounters* c) {
+    hipLaunchKernelGGL(k_ctr_fold, dim3(1), dim3(64), 0, h->stream, c);
+    HIP_TRY(h, hipGetLastError());
+    return GD_OK;
+}
+
 int pull_counters(gd_handle* h) {
+    GD_TRY(fold_counters(h, h->ctr));
     HIP_TRY(h, hipMemcpyAsync(&h->ctr_host, h->ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
     if (h->cx_built && h->cxi_ctr.p)   // the index counters ride along (cx_ensure's rebuild rule)
         HIP_TRY(h, hipMemcpyAsync(&h->cx_ctr_host, h->cxi_ctr.p, sizeof(CxCounters), hipMemcpyDeviceToHost, h->stream));

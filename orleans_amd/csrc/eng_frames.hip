@@ -238,6 +238,7 @@ int receive_frames_device(gd_handle* h, const uint8_t* buf, uint64_t len, const 
 }
 
 int ad_pull(gd_handle* h) {
+    GD_TRY(fold_counters(h, h->ad_ctr));
     HIP_TRY(h, hipMemcpyAsync(&h->ad_host, h->ad_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
     return sync(h);
 }
@@ -247,14 +248,13 @@ int ad_rehash(gd_handle* h, unsigned long long cap) {
     Slot* ns = nullptr;
     GD_TRY(alloc_table(h, cap, &ns));
     if (!h->ad_ctr) {
-        hipError_t e = hipMalloc(&h->ad_ctr, sizeof(DevCounters));
+        hipError_t e = hipMalloc(&h->ad_ctr, CTR_BYTES);
         if (e != hipSuccess) {
             (void)hipFree(ns);
             return set_err(h, GD_ENOMEM, "activation directory counters: %s", hipGetErrorString(e));
         }
     }
-    DevCounters fresh{};
-    HIP_TRY(h, hipMemcpyAsync(h->ad_ctr, &fresh, sizeof fresh, hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(h, hipMemsetAsync(h->ad_ctr, 0, CTR_BYTES, h->stream));   // counters and their striped deltas
     if (h->ad_slots) {
         GD_TRY(launch(h, "k_rehash", dim3((uint32_t)((h->ad_cap + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, k_rehash,
                       (const Slot*)h->ad_slots, h->ad_cap, ns, cap - 1, h->ad_ctr, (const uint32_t*)nullptr,
@@ -437,7 +437,7 @@ int gd_actdir_clear(gd_handle* h) {
     HIP_TRY(h, hipSetDevice(h->device));
     if (!h->ad_slots) return GD_OK;
     HIP_TRY(h, hipMemsetAsync(h->ad_slots, 0, h->ad_cap * sizeof(Slot), h->stream));
-    HIP_TRY(h, hipMemsetAsync(h->ad_ctr, 0, sizeof(DevCounters), h->stream));
+    HIP_TRY(h, hipMemsetAsync(h->ad_ctr, 0, CTR_BYTES, h->stream));
     return sync(h);
 }
 

@@ -309,6 +309,7 @@ TableArgs table_args(gd_handle* h);
 bool host_silo_valid(const gd_handle* h, uint32_t silo);
 size_t ring_lds(gd_handle* h);
 int pull_counters(gd_handle* h);
+int fold_counters(gd_handle* h, DevCounters* c);
 int alloc_table(gd_handle* h, unsigned long long cap, Slot** out);
 int alloc_vtag(gd_handle* h, unsigned long long cap, uint32_t** out);
 unsigned long long pow2_at_least(unsigned long long x);

@@ -33,6 +33,39 @@ struct DevCounters {
     unsigned long long live;
     unsigned long long tomb;
 };
+// Striped deltas of live / tomb behind the counters (one allocation of CTR_BYTES): the directory batches'
+// kernels add a wave's (or workgroup's) count into stripe blockIdx % CTR_STRIPES, 256 B apart, instead of
+// into DevCounters itself -- device-scope atomics on one address from every XCD serialise (cfg 3's 1M-item
+// batches: 1.6 of their 2.0 ms a churn step).  k_ctr_fold adds the stripes into live / tomb (and zeroes
+// them) before every read-back (pull_counters).
+constexpr uint32_t CTR_STRIPES = 64;
+constexpr uint32_t CTR_STRIPE_U64 = 32;       // 256 B a stripe: {live delta, tomb delta, unused}
+constexpr size_t CTR_HDR = 256;
+constexpr size_t CTR_BYTES = CTR_HDR + (size_t)CTR_STRIPES * CTR_STRIPE_U64 * 8;
+static_assert(sizeof(DevCounters) <= CTR_HDR, "counters header");
+__device__ __forceinline__ unsigned long long* ctr_stripe(DevCounters* ctr) {
+    return reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ctr) + CTR_HDR) +
+           (size_t)(blockIdx.x % CTR_STRIPES) * CTR_STRIPE_U64;
+}
+static __global__ void __launch_bounds__(64) k_ctr_fold(DevCounters* ctr) {
+    unsigned long long* s = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ctr) + CTR_HDR) +
+                            (size_t)threadIdx.x * CTR_STRIPE_U64;
+    unsigned long long l = 0, t = 0;
+    if (threadIdx.x < CTR_STRIPES) {
+        l = s[0];
+        t = s[1];
+        s[0] = 0;
+        s[1] = 0;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        l += __shfl_xor(l, off, 64);
+        t += __shfl_xor(t, off, 64);
+    }
+    if (threadIdx.x == 0) {
+        ctr->live += l;
+        ctr->tomb += t;
+    }
+}
 
 // ------------------------------------------------------------------ identity
 __device__ __forceinline__ void jmix(uint32_t& a, uint32_t& b, uint32_t& c) {
@@ -818,8 +851,10 @@ __device__ __forceinline__ void claim_counters(DevCounters* ctr, uint32_t pdist,
     for (int off = WAVE / 2; off > 0; off >>= 1) pdist = max(pdist, (uint32_t)__shfl_xor(pdist, off, WAVE));
     const unsigned long long m = __ballot(reused);
     if ((threadIdx.x & (WAVE - 1)) == 0) {
-        if (pdist) atomicMax(&ctr->max_probe, pdist);
-        if (m) atomicAdd(&ctr->tomb, ~(unsigned long long)__popcll(m) + 1ull);   // - reused
+        // max_probe only grows: a wave whose distance is not past it (nearly all) skips the atomic
+        if (pdist && pdist > __hip_atomic_load(&ctr->max_probe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicMax(&ctr->max_probe, pdist);
+        if (m) atomicAdd(ctr_stripe(ctr) + 1, ~(unsigned long long)__popcll(m) + 1ull);   // tomb - reused
     }
 }
 
@@ -950,20 +985,23 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_take(const gd_key* __restr
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (zero && i < REG_PASSES - 1) zero[i] = 0;         // the gated passes' counters (asynchronous batches)
     uint32_t pd = 0;
-    bool reused = false;
+    bool reused = false, deferred = false;
     if (i < n && is_new[i] == REG_CANDIDATE) {
         const uint32_t t = slot_of[i];
         uint32_t expected = seen[i];
         uint32_t* mp = &slots[t].meta;
         if (__hip_atomic_compare_exchange_strong(mp, &expected, make_meta(SLOT_CLAIMED, 0), __ATOMIC_RELAXED,
                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            // No item of this launch reads a slot another item claimed (k_reg_find read the table before it,
+            // a CAS loser defers below), so the key needs no release here: the kernel's end publishes it to
+            // the passes and commit that read it (an agent-scope release fence writes the XCD's L2 back,
+            // per wave: 2.2 ns an item at cfg 3's 100M registrations, 72 ms a 33M batch)
             const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
-            __hip_atomic_store(&slots[t].n0, n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&slots[t].n1, n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&slots[t].tcd, tcd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&slots[t].act, NONE32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            Slot& sl = slots[t];
+            sl.n0 = n0;
+            sl.n1 = n1;
+            sl.tcd = tcd;
+            sl.act = NONE32;
             __hip_atomic_store(mp, make_meta(SLOT_PENDING, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long home = home_slot(uniform_hash(n0, n1, tcd), mask);
             pd = (uint32_t)((t - home) & mask);
@@ -971,12 +1009,15 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_take(const gd_key* __restr
             is_new[i] = 1;
             atomicMax(&last[t], ~i);                     // the election (k_reg_commit_elect)
         } else {
-            // taken meanwhile (another new grain homed nearby, or this key's twin): the full protocol from
-            // the home, here -- it defers to the gated passes only an item that meets an unpublished claim
-            reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, retry, pd, reused);
-            if (is_new[i]) atomicMax(&last[slot_of[i]], ~i);
+            // taken meanwhile (another new grain homed nearby, or this key's twin, whose key this launch
+            // has not published): the full protocol in the next claim pass
+            slot_of[i] = SLOT_RETRY;
+            is_new[i] = 0;
+            deferred = true;
         }
     }
+    const unsigned long long dm = __ballot(deferred);   // one counter atomic a wave
+    if ((threadIdx.x & (WAVE - 1)) == 0 && dm) atomicAdd(retry, (uint32_t)__popcll(dm));
     claim_counters(ctr, pd, reused);
 }
 
@@ -1117,8 +1158,9 @@ __device__ __forceinline__ void live_delta(DevCounters* ctr, bool flag, bool rem
     const unsigned long long m = __ballot(flag);
     if ((threadIdx.x & (WAVE - 1)) != 0 || !m) return;
     const unsigned long long c = (unsigned long long)__popcll(m);
-    atomicAdd(&ctr->live, removal ? ~c + 1ull : c);
-    if (removal) atomicAdd(&ctr->tomb, c);
+    unsigned long long* st = ctr_stripe(ctr);        // folded into live / tomb by k_ctr_fold
+    atomicAdd(st, removal ? ~c + 1ull : c);
+    if (removal) atomicAdd(st + 1, c);
 }
 static __global__ void __launch_bounds__(BLOCK) k_reg_commit(const uint32_t* __restrict__ slot_of,
                                                       const uint32_t* __restrict__ win,
