@@ -318,7 +318,7 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
                       slot_of, is_new, (const uint32_t*)win, rc, rc + 1, last));
         for (uint32_t pass = 1; pass < REG_PASSES; ++pass)
             GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim_gated, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
-                          dvals, table_args(h), (const uint32_t*)rc + pass - 1, rc + pass, last));
+                          dvals, table_args(h), (const uint32_t*)rc + pass - 1, rc + pass, last, pass));
         unsettled = rc + REG_PASSES - 1;
         retry0 = rc;
         h->pending_in += n;
@@ -327,15 +327,13 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
         GD_TRY(launch(h, "k_reg_take", g, b, 0, k_reg_take, dk, n, h->slots, mask, h->ctr, dvals, table_args(h),
                       slot_of, is_new, (const uint32_t*)win, &h->ctr->retry, (uint32_t*)nullptr, last));
         GD_TRY(pull_counters(h));
-        if (getenv("GD_DEBUG_RETRY")) fprintf(stderr, "register n=%u take deferred %u\n", n, h->ctr_host.retry);
         // relaunches for the items that lost their CAS or met an unpublished claim
         for (uint32_t pass = 1; h->ctr_host.retry && !h->ctr_host.err; ++pass) {
             if (pass > 64) return set_err(h, GD_ETIMEOUT, "gd_dir_register: claims did not settle");
             HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
-            GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new, 1u,
+            GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new, pass,
                           dvals, table_args(h), last));
             GD_TRY(pull_counters(h));
-            if (getenv("GD_DEBUG_RETRY")) fprintf(stderr, "  pass %u deferred %u\n", pass, h->ctr_host.retry);
         }
     }
     if (cx_inline(h, tt, n))                       // the winners project their slots as they commit
@@ -461,7 +459,7 @@ int gd_dir_upsert(gd_handle* h, const gd_key* keys, const gd_val* vals, uint32_t
     for (uint32_t pass = 0;; ++pass) {            // the registration's claim protocol (k_reg_claim)
         HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
         GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, mask, h->ctr, slot_of, is_new,
-                      (uint32_t)(pass > 0), (const gd_val*)h->out_c.p, table_args(h), (uint32_t*)nullptr));
+                      pass, (const gd_val*)h->out_c.p, table_args(h), (uint32_t*)nullptr));
         GD_TRY(pull_counters(h));
         if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
         if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_upsert: claims did not settle");

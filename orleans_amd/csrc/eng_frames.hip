@@ -350,7 +350,7 @@ int gd_actdir_add(gd_handle* h, const gd_key* act_ids, const uint32_t* ctx, cons
     for (uint32_t pass = 0;; ++pass) {            // TryAdd: the registration's claim protocol, first add wins
         HIP_TRY(h, hipMemsetAsync(&h->ad_ctr->retry, 0, sizeof(uint32_t), h->stream));
         GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->ad_slots, h->ad_cap - 1, h->ad_ctr, slot_of,
-                      is_new, (uint32_t)(pass > 0), (const gd_val*)nullptr, TableArgs{}, (uint32_t*)nullptr));
+                      is_new, pass, (const gd_val*)nullptr, TableArgs{}, (uint32_t*)nullptr));
         GD_TRY(ad_pull(h));
         if (h->ad_host.retry == 0 || h->ad_host.err) break;
         if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_actdir_add: claims did not settle");

@@ -520,7 +520,7 @@ int merge_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, const int32_
     for (uint32_t pass = 0;; ++pass) {            // the registration's claim protocol; no IsValidSilo check in Merge
         HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
         GD_TRY(launch(h, "k_reg_claim", g, b, 0, k_reg_claim, dk, n, h->slots, h->capacity - 1, h->ctr, slot_of,
-                      is_new, (uint32_t)(pass > 0), (const gd_val*)nullptr, table_args(h), (uint32_t*)nullptr));
+                      is_new, pass, (const gd_val*)nullptr, table_args(h), (uint32_t*)nullptr));
         GD_TRY(pull_counters(h));
         if (h->ctr_host.retry == 0 || h->ctr_host.err) break;
         if (pass >= 64) return set_err(h, GD_ETIMEOUT, "gd_dir_merge: claims did not settle");

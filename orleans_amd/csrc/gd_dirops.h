@@ -145,9 +145,12 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_abort(const uint32_t* __re
                                                      DevCounters* ctr) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n || !is_new[i] || slot_of[i] >= SLOT_RETRY) return;
-    uint32_t expected = make_meta(SLOT_PENDING, 0);
-    if (__hip_atomic_compare_exchange_strong(&slots[slot_of[i]].meta, &expected, make_meta(SLOT_TOMB, 0),
-                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    // PENDING carries its claim launch's tag (claim_tag) in the silo field
+    uint32_t* mp = &slots[slot_of[i]].meta;
+    uint32_t expected = __hip_atomic_load(mp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (slot_state(expected) == SLOT_PENDING &&
+        __hip_atomic_compare_exchange_strong(mp, &expected, make_meta(SLOT_TOMB, 0), __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         atomicAdd(&ctr->tomb, 1ull);
 }
 

@@ -835,8 +835,15 @@ static __global__ void __launch_bounds__(BLOCK) k_ring_hashes(const uint32_t* __
 // wait can starve the claimer of the same wave once the compiler sinks its
 // publish to the loop exit): it is marked RETRY and the host relaunches the
 // kernel for the retried items, after the kernel boundary has published every
-// claim.
+// claim.  "Not yet published" is read off the meta alone (round 6): CLAIMED, or
+// PENDING with this launch's tag in the silo field (claim_tag) -- a PENDING slot of
+// an earlier launch has its key published by that launch's end.  So a claim needs no
+// release fence (an agent-scope release writes the XCD's L2 back, per wave) and a
+// walk no acquire loads (an agent-scope acquire invalidates it): the metas are read
+// and swapped with relaxed device-coherent atomics, the keys with plain loads.
 constexpr uint32_t SLOT_RETRY = 0xFFFFFFFEu;
+// PENDING's tag of claim launch `pass` (k_reg_take's claims carry 0)
+__device__ __forceinline__ uint32_t claim_tag(uint32_t pass) { return (pass + 1u) & 0xFFFFu; }
 
 // vals / valid (nullable): an item whose silo is not valid is skipped (slot_of = NONE32): the
 // IsValidSilo check of AddSingleActivation / AddActivation (GrainDirectoryPartition.cs:279,310).
@@ -844,7 +851,7 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
                                                unsigned long long mask, DevCounters* ctr,
                                                uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
                                                const gd_val* __restrict__ vals, const TableArgs& vt, uint32_t* retry,
-                                               uint32_t& pdist, bool& reused);
+                                               uint32_t& pdist, bool& reused, uint32_t tag);
 // The claims' counter updates, one atomic a wave (one per item queued ~10^4 same-address atomics behind a
 // 1 % registration batch: 0.12 ms of it at cfg 2).  Every lane of the wave calls it.
 __device__ __forceinline__ void claim_counters(DevCounters* ctr, uint32_t pdist, bool reused) {
@@ -864,14 +871,16 @@ __device__ __forceinline__ void claim_counters(DevCounters* ctr, uint32_t pdist,
 static __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __restrict__ keys, uint32_t n, Slot* slots,
                                                      unsigned long long mask, DevCounters* ctr,
                                                      uint32_t* __restrict__ slot_of,
-                                                     uint8_t* __restrict__ is_new, uint32_t retry_only,
+                                                     uint8_t* __restrict__ is_new, uint32_t pass,
                                                      const gd_val* __restrict__ vals, TableArgs vt,
                                                      uint32_t* __restrict__ last = nullptr) {
+    // pass 0: every item; later passes: the items the previous one deferred
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t pd = 0;
     bool reused = false;
-    if (i < n && (!retry_only || slot_of[i] == SLOT_RETRY)) {
-        reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, &ctr->retry, pd, reused);
+    if (i < n && (pass == 0 || slot_of[i] == SLOT_RETRY)) {
+        reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, &ctr->retry, pd, reused,
+                       claim_tag(pass));
         if (last && is_new[i]) atomicMax(&last[slot_of[i]], ~i);
     }
     claim_counters(ctr, pd, reused);
@@ -887,7 +896,7 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim_gated(const gd_key* 
                                                            uint8_t* __restrict__ is_new,
                                                            const gd_val* __restrict__ vals, TableArgs vt,
                                                            const uint32_t* __restrict__ gate, uint32_t* retry,
-                                                           uint32_t* __restrict__ last) {
+                                                           uint32_t* __restrict__ last, uint32_t pass) {
     if (gate && *gate == 0) return;
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     // pass 0 zeroes the later passes' counters (its own, retry[0], was zeroed by the previous batch's
@@ -896,7 +905,7 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim_gated(const gd_key* 
     uint32_t pd = 0;
     bool reused = false;
     if (i < n && (!gate || slot_of[i] == SLOT_RETRY)) {
-        reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, retry, pd, reused);
+        reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, retry, pd, reused, claim_tag(pass));
         if (is_new[i]) atomicMax(&last[slot_of[i]], ~i);    // the election (k_reg_commit_elect)
     }
     claim_counters(ctr, pd, reused);
@@ -1040,7 +1049,7 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
                                                unsigned long long mask, DevCounters* ctr,
                                                uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
                                                const gd_val* __restrict__ vals, const TableArgs& vt, uint32_t* retry,
-                                               uint32_t& pdist, bool& reused) {
+                                               uint32_t& pdist, bool& reused, uint32_t tag) {
     if (vals && !tab_silo_valid(vt, vals[i].silo)) {
         slot_of[i] = NONE32;
         is_new[i] = 0;
@@ -1057,19 +1066,19 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
     // never placed twice; a tombstone taken meanwhile defers the item to the next pass.
     unsigned long long tomb_s = ~0ull, tomb_dist = 0;
     uint32_t tomb_meta = 0;
-    // claim slot t (its meta `expected`) for the key: publish the key, then PENDING
+    // claim slot t (its meta `expected`) for the key: the key, then PENDING with this launch's tag (read
+    // as unpublished by this launch's other items; published to later launches by the kernel boundary)
     auto claim = [&](unsigned long long t, uint32_t expected, unsigned long long d) -> bool {
         uint32_t* mp = &slots[t].meta;
         if (!__hip_atomic_compare_exchange_strong(mp, &expected, make_meta(SLOT_CLAIMED, 0), __ATOMIC_RELAXED,
                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
             return false;
-        __hip_atomic_store(&slots[t].n0, n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&slots[t].n1, n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&slots[t].tcd, tcd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&slots[t].act, NONE32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(mp, make_meta(SLOT_PENDING, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        Slot& sl = slots[t];
+        sl.n0 = n0;
+        sl.n1 = n1;
+        sl.tcd = tcd;
+        sl.act = NONE32;
+        __hip_atomic_store(mp, make_meta(SLOT_PENDING, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         pdist = (uint32_t)d;                                 // max_probe: claim_counters
         return true;
     };
@@ -1088,7 +1097,7 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
     };
     for (;;) {
         uint32_t* meta_p = &slots[s].meta;
-        const uint32_t meta = __hip_atomic_load(meta_p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t meta = __hip_atomic_load(meta_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t st = slot_state(meta);
         if (st == SLOT_EMPTY) {
             if (tomb_s != ~0ull) {
@@ -1102,7 +1111,8 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
             }
             continue;   // lost the CAS: re-read the same slot
         }
-        if (st == SLOT_CLAIMED) {        // claimed in this launch, key not yet visible
+        if (st == SLOT_CLAIMED || (st == SLOT_PENDING && slot_silo(meta) == tag)) {
+            // claimed in this launch: its key is not published to this launch
             res = SLOT_RETRY;
             atomicAdd(retry, 1u);
             break;
@@ -1112,10 +1122,8 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
             tomb_meta = meta;
             tomb_dist = dist;
         }
-        if (st == SLOT_LIVE || st == SLOT_PENDING) {
-            const uint64_t k0 = __hip_atomic_load(&slots[s].n0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t k1 = __hip_atomic_load(&slots[s].n1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t k2 = __hip_atomic_load(&slots[s].tcd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (st == SLOT_LIVE || st == SLOT_PENDING) {     // a key published before this launch
+            const uint64_t k0 = slots[s].n0, k1 = slots[s].n1, k2 = slots[s].tcd;
             if (k0 == n0 && k1 == n1 && k2 == tcd) {
                 res = (uint32_t)s;
                 fresh = (st == SLOT_PENDING) ? 1 : 0;
