@@ -809,7 +809,9 @@ def main():
             "routed_ok_last_step_rank0": st_ok,
             "rehearsal_one_gpu": bool(args.rehearse_one_gpu),
             "exchange": exchange,
-            "exchange_ms_per_rank": [round(x, 4) for x in ex_ms_ranks] if world > 1 else None,
+            # the library exchange's RCCL rounds per rank (HIP events); null on the torch / rehearsal exchange
+            "exchange_ms_per_rank": ([round(x, 4) for x in ex_ms_ranks]
+                                     if world > 1 and isinstance(router, LibraryRouter) else None),
             "comm": comm_info(w),
             "roofline": roofline,
             "kernels": kernels,

@@ -939,6 +939,11 @@ int gd_set_kernel_timing(gd_handle* h, int enable);   /* 0 off, 1 every launch, 
                                    run of consecutive tiles, so one digit's runs of neighbouring tiles -- one
                                    128-B line between them -- leave one workgroup back to back; measured
                                    slower, profiles/r06_b2_order_ab.txt) */
+#define GD_OPT_MB_POLL      16  /* micro-batches created after, zero-copy: a graph replay (gd_microbatch_run
+                                   with use_graph) returns when the sort's workgroups have counted
+                                   themselves done in pinned host memory (their stores fenced first)
+                                   instead of waiting for the dispatch's completion signal; eager runs
+                                   still synchronise the stream (measured faster): 1 (default) / 0 */
 int gd_option_set(gd_handle* h, int option, int64_t value);
 int gd_option_get(const gd_handle* h, int option, int64_t* value);
 

@@ -781,6 +781,10 @@ int gd_option_set(gd_handle* h, int option, int64_t v) {
             if (!in(0, 1)) break;
             h->b2_order = (uint32_t)v;
             return GD_OK;
+        case GD_OPT_MB_POLL:
+            if (!in(0, 1)) break;
+            h->mb_poll = v != 0;
+            return GD_OK;
         default: return set_err(h, GD_EINVAL, "gd_option_set: unknown option %d", option);
     }
     return set_err(h, GD_EINVAL, "gd_option_set: option %d: value %lld out of range", option, (long long)v);
@@ -805,6 +809,7 @@ int gd_option_get(const gd_handle* hc, int option, int64_t* v) {
         case GD_OPT_L2_MID: *v = h->l2_mid; return GD_OK;
         case GD_OPT_B2_PERSIST: *v = h->b2_persist; return GD_OK;
         case GD_OPT_B2_ORDER: *v = h->b2_order; return GD_OK;
+        case GD_OPT_MB_POLL: *v = h->mb_poll ? 1 : 0; return GD_OK;
         default: return set_err(h, GD_EINVAL, "gd_option_get: unknown option %d", option);
     }
 }
@@ -874,6 +879,11 @@ struct gd_microbatch {
     uint32_t max_bits = MB_MAX_BITS;    // widest radix digit (11: two passes at n_act = 2^20)
     unsigned long long* ts = nullptr;   // GD_MB_TRACE: per-phase tick sums (device), printed at destroy
     uint64_t runs_done = 0;
+    // GD_OPT_MB_POLL (zero-copy only): the sort's workgroups count themselves done into a pinned word; the
+    // run returns when the count arrives instead of waiting for the dispatch's completion signal
+    uint32_t* h_done = nullptr;         // pinned, coherent
+    uint32_t* d_done = nullptr;         // its device view (null: no poll)
+    uint32_t done_expect = 0;           // the count the last run waited for
     std::vector<std::pair<uint32_t, hipGraphExec_t>> graphs;
     uint64_t graphs_gen = 0;       // handle layout the cached graphs were captured against
     uint64_t graphs_cx = ~0ull;    // the probe index build they read (~0: the directory)
@@ -892,21 +902,21 @@ namespace gdx {
 // route (keys read from and silo / status written to pinned host memory) -> sort (perm / runs / act to host).
 template <int IT>
 int mb_launch_sort(gd_microbatch* mb, dim3 grid, uint32_t bits, const uint32_t* a, uint32_t n, uint32_t passes,
-                   uint32_t* pm, uint32_t* ra, uint32_t* rs, uint32_t* nr, uint32_t* ac) {
+                   uint32_t* pm, uint32_t* ra, uint32_t* rs, uint32_t* nr, uint32_t* ac, uint32_t* done) {
     gd_handle* h = mb->h;
     const dim3 b(MB_THREADS);
     const uint32_t na = mb->n_act;
     unsigned long long* ts = mb->ts;
     const uint32_t bal = h->radix_rank_atomic ? 0u : 1u;
     switch (bits) {
-        case 4: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<4, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
-        case 5: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<5, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
-        case 6: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<6, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
-        case 7: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<7, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
-        case 8: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<8, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
-        case 9: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<9, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
-        case 10: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<10, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
-        default: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<11, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal);
+        case 4: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<4, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal, done);
+        case 5: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<5, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal, done);
+        case 6: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<6, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal, done);
+        case 7: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<7, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal, done);
+        case 8: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<8, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal, done);
+        case 9: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<9, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal, done);
+        case 10: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<10, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal, done);
+        default: return launch(h, "k_mb_sort_runs", grid, b, 0, k_mb_sort_runs<11, IT>, a, n, passes, na, pm, ra, rs, nr, ac, ts, bal, done);
     }
 }
 
@@ -916,7 +926,13 @@ bool mb_use_index(const gd_handle* h) {
     return h->cx_mode != 0 && h->tune_pin[GD_TUNE_PROBE_KEYS] != 1 && h->cx8_ok && cx_current(h);
 }
 
-int mb_enqueue(gd_microbatch* mb, uint32_t n) {
+// k_mb_sort_runs's workgroups for n messages (each adds 1 to the done count)
+uint32_t mb_sort_grid(const gd_microbatch* mb, uint32_t n) {
+    return mb->zero_copy ? std::max<uint32_t>(1, std::min(mb->split, std::max<uint32_t>(1, n / 256))) : 1u;
+}
+
+// count_done: the sort counts itself done into mb->d_done (a captured graph's replays poll for it)
+int mb_enqueue(gd_microbatch* mb, uint32_t n, bool count_done) {
     gd_handle* h = mb->h;
     const bool zc = mb->zero_copy;
     uint8_t* d = zc ? mb->h_out_dev : mb->d_out;
@@ -975,9 +991,10 @@ int mb_enqueue(gd_microbatch* mb, uint32_t n) {
     uint32_t *pm = mb->out_u32(d, 2), *ra = mb->out_u32(d, 5), *rs = mb->out_u32(d, 4), *nr = mb->out_u32(d, 3);
     // act to the host block: k_mb_route wrote it already; the LocalLookup route did not
     uint32_t* ac = zc && h->cache_max ? mb->out_u32(d, 1) : nullptr;
-    const dim3 g1(zc ? std::max<uint32_t>(1, std::min(mb->split, std::max<uint32_t>(1, n / 256))) : 1);
-    if (n <= MB_THREADS * 4) GD_TRY(mb_launch_sort<4>(mb, g1, bits, a, n, passes, pm, ra, rs, nr, ac));
-    else GD_TRY(mb_launch_sort<8>(mb, g1, bits, a, n, passes, pm, ra, rs, nr, ac));
+    const dim3 g1(mb_sort_grid(mb, n));
+    uint32_t* done = count_done ? mb->d_done : nullptr;
+    if (n <= MB_THREADS * 4) GD_TRY(mb_launch_sort<4>(mb, g1, bits, a, n, passes, pm, ra, rs, nr, ac, done));
+    else GD_TRY(mb_launch_sort<8>(mb, g1, bits, a, n, passes, pm, ra, rs, nr, ac, done));
     if (!zc) HIP_TRY(h, hipMemcpyAsync(mb->h_out, d, mb->out_bytes, hipMemcpyDeviceToHost, h->stream));
     return GD_OK;
 }
@@ -1004,6 +1021,7 @@ void gd_microbatch_destroy(gd_microbatch* mb) {
         (void)hipFree(mb->ts);
     }
     for (auto& g : mb->graphs) (void)hipGraphExecDestroy(g.second);
+    if (mb->h_done) (void)hipHostFree(mb->h_done);
     if (mb->h_keys) (void)hipHostFree(mb->h_keys);
     if (mb->h_out) (void)hipHostFree(mb->h_out);
     if (mb->d_keys) (void)hipFree(mb->d_keys);
@@ -1038,6 +1056,11 @@ int gd_microbatch_create(gd_handle* h, uint32_t capacity, uint32_t n_act, gd_mic
     if (ok && mb->zero_copy)
         ok = hipHostGetDevicePointer((void**)&mb->h_keys_dev, mb->h_keys, 0) == hipSuccess &&
              hipHostGetDevicePointer((void**)&mb->h_out_dev, mb->h_out, 0) == hipSuccess;
+    if (ok && mb->zero_copy && h->mb_poll) {
+        ok = hipHostMalloc((void**)&mb->h_done, 64, hipHostMallocCoherent) == hipSuccess &&
+             hipHostGetDevicePointer((void**)&mb->d_done, mb->h_done, 0) == hipSuccess;
+        if (ok) *mb->h_done = 0;
+    }
     if (!ok) {
         gd_microbatch_destroy(mb);
         return set_err(h, GD_ENOMEM, "gd_microbatch_create: allocation failed");
@@ -1063,6 +1086,30 @@ int gd_microbatch_outputs(gd_microbatch* mb, uint32_t** silo, uint32_t** act, ui
     return GD_OK;
 }
 
+}  // extern "C"
+namespace gdx {
+// The end of a micro-batch graph replay: with the poll, until the sort's workgroups have counted the run done
+// (their host stores fenced before), bounded -- a run not done within 2 s (a fault, a lost dispatch)
+// falls back to the stream synchronisation, which reports it; else the stream synchronisation.
+int mb_wait(gd_microbatch* mb, uint32_t n) {
+    gd_handle* h = mb->h;
+    if (!mb->d_done) return sync(h);
+    mb->done_expect += mb_sort_grid(mb, n);
+    const uint32_t want = mb->done_expect;
+    volatile uint32_t* d = mb->h_done;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        if ((int32_t)(*d - want) >= 0) return GD_OK;
+        if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+    }
+    const int r = sync(h);
+    if (r != GD_OK) return r;
+    if ((int32_t)(*d - want) < 0) return set_err(h, GD_EHIP, "micro-batch: the sort's completion count did not arrive");
+    return GD_OK;
+}
+}  // namespace gdx
+extern "C" {
+
 int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
     if (!mb) return set_err(nullptr, GD_EINVAL, "null micro-batch");
     gd_handle* h = mb->h;
@@ -1074,7 +1121,10 @@ int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
     // gd_route* calls); a captured graph would replay freed pointers.  That mode runs eagerly.
     ++mb->runs_done;
     if (!use_graph || h->cache_max) {
-        GD_TRY(mb_enqueue(mb, n));
+        // eager launches wait on the stream, without the count: polling after them, or the count's
+        // system-scope fence and atomic at the sort's end, measured slower (p50 28.7 -> 33.7 / 40.8 us
+        // at cfg 5, profiles/r06_mb_poll.json), while a graph replay gains by the poll (35.4 -> 33.5 us)
+        GD_TRY(mb_enqueue(mb, n, false));
         return sync(h);
     }
     // ring or table moved, or the probe index was rebuilt (a new layout in the captured arguments) or
@@ -1096,7 +1146,7 @@ int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
         hipGraph_t graph = nullptr;
         const uint64_t routed = h->routed;       // counted per replay below, not at capture
         HIP_TRY(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-        const int rc = mb_enqueue(mb, n);
+        const int rc = mb_enqueue(mb, n, mb->d_done != nullptr);
         const hipError_t ec = hipStreamEndCapture(h->stream, &graph);
         h->timing = timing;
         h->routed = routed;
@@ -1112,7 +1162,7 @@ int gd_microbatch_run(gd_microbatch* mb, uint32_t n, int use_graph) {
     }
     HIP_TRY(h, hipGraphLaunch(exec, h->stream));
     h->routed += n;
-    return sync(h);
+    return mb_wait(mb, n);
 }
 
 }  // extern "C"

@@ -197,6 +197,7 @@ struct gd_handle {
     bool mb_zero_copy = true;   // micro-batches: I/O from / to pinned host memory (GD_OPT_MB_ZEROCOPY)
     uint32_t mb_split = 8;      // micro-batches: redundant sorters splitting the host stores (GD_OPT_MB_SPLIT)
     bool mb_trace = false;      // micro-batches: per-phase timestamps (GD_OPT_MB_TRACE)
+    bool mb_poll = true;        // micro-batches: completion by the sort's pinned count (GD_OPT_MB_POLL)
     int tune_pin[GD_TUNE_KINDS] = {-1, -1, -1, -1, -1};   // gd_tune_set: pinned variant per kind, -1 measured
     int msd_mode = 1;           // two-level bucketing (gd_msd.h, gd_msd2.h): 0 off, 1 measured (default), 2 always (GD_MSD)
     uint32_t l2_small = 1024;   // three-pass form: ranges of at most this many messages are sorted one wave a range
@@ -425,7 +426,7 @@ int cache_pull(gd_handle* h, CacheCounters* c);
 int cache_touch(gd_handle* h, uint32_t* hit, const uint32_t* cslot, uint32_t n);
 int split_emit(gd_handle* h, int move, gd_key* d_keys, gd_val* d_vals);
 int set_bitset(gd_handle* h, DevBuf& b, const std::vector<uint32_t>& bits);
-int mb_enqueue(gd_microbatch* mb, uint32_t n);
+int mb_enqueue(gd_microbatch* mb, uint32_t n, bool count_done);
 template <class Op>
 int scan_device(gd_handle* h, uint32_t* data, uint32_t n, bool reverse, bool inclusive, const char* tag,
                 uint32_t* out = nullptr);

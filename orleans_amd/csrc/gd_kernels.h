@@ -2559,7 +2559,9 @@ __device__ __forceinline__ void mb_sort_runs_core(MbShared& sh, uint32_t (&kk)[I
 
 // gridDim.x workgroups sort the same batch redundantly and each writes its 1/gridDim.x share of
 // the outputs: zero-copy stores to host memory are spread over as many CUs.  act_copy (optional):
-// the activations also go to the host block.
+// the activations also go to the host block.  done (optional, pinned host memory): each workgroup adds
+// 1 once its share is stored and fenced, so the host sees the batch finished without waiting for the
+// dispatch's completion signal (gd_microbatch_run's poll).
 template <int BITS, int IT>
 static __global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32_t* __restrict__ act, uint32_t n,
                                                               uint32_t passes, uint32_t n_act,
@@ -2568,7 +2570,8 @@ static __global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32
                                                               uint32_t* __restrict__ run_start,
                                                               uint32_t* __restrict__ n_runs,
                                                               uint32_t* __restrict__ act_copy,
-                                                              unsigned long long* ts, uint32_t ballot) {
+                                                              unsigned long long* ts, uint32_t ballot,
+                                                              uint32_t* done) {
     __shared__ MbShared sh;
     const uint32_t lane = lane_id(), w = threadIdx.x / WAVE;
     const uint32_t lo = (uint32_t)((uint64_t)n * blockIdx.x / gridDim.x);
@@ -2583,6 +2586,11 @@ static __global__ void __launch_bounds__(MB_THREADS) k_mb_sort_runs(const uint32
         vv[r] = idx;
     }
     mb_sort_runs_core<BITS, IT>(sh, kk, vv, n, passes, perm, run_act, run_start, n_runs, lo, hi, ts, ballot != 0);
+    if (done) {
+        __threadfence_system();                    // this thread's host stores before the count
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 }  // namespace gd

@@ -68,16 +68,27 @@ def test_line_cap_holds_for_oversized_records(bench):
     assert len(text) <= bench.LINE_CAP, len(text)
 
 
+@pytest.mark.parametrize("rnd", ["r05", "r06"])
 @pytest.mark.parametrize("world", [2, 8])
-def test_rehearsal_lines_parse_under_cap(bench, world):
-    """The lines `bench.py --gpus N --rehearse-one-gpu` printed through torchrun (round 5): the last
-    stdout line is one JSON object under the cap, for N GPUs."""
-    with open(os.path.join(ROOT, f"profiles/r05_rehearsal_w{world}_line.json")) as f:
+def test_rehearsal_lines_parse_under_cap(bench, world, rnd):
+    """The lines `bench.py --gpus N --rehearse-one-gpu` printed through torchrun (rounds 5 and 6): the
+    last stdout line is one JSON object under the cap, for N GPUs.  Round 6's also carry VERDICT r05
+    item 5's fields: the largest owner share for both silo sets, the line on the other set, the
+    communicator's rank count and the exchange's name and per-rank time (null off the library exchange)."""
+    with open(os.path.join(ROOT, f"profiles/{rnd}_rehearsal_w{world}_line.json")) as f:
         text = f.read().strip().splitlines()[-1]
     assert len(text) <= bench.LINE_CAP
     line = json.loads(text)
     assert line["n_gpus"] == world and line["rehearsal_one_gpu"] is True
     assert line["value"] > 0 and "roofline" in line and "config" in line
+    if rnd == "r06":
+        shares = line["config"]["owner_share_max_by_silo_set"]
+        assert set(shares) == {"literal", "balanced"} and all(0 < v <= 1 for v in shares.values())
+        assert abs(line["config"]["owner_share_max"] - shares["balanced"]) < 0.01
+        other = line["secondary"]["cfg2_other_silo_set"]
+        assert other["silos"] == "literal" and other["value"] > 0
+        assert "n_ranks" in line["comm"] and line["exchange"]
+        assert "exchange_ms_per_rank" in line
 
 
 def test_pmc_kernel_families():

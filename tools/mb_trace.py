@@ -43,25 +43,32 @@ def main():
     o = [torch.empty(1 << 20, dtype=torch.int32, device=dev) for _ in range(2)] + [torch.empty(1 << 20, dtype=torch.uint8, device=dev)]
     e.route_device(big.data_ptr(), 1 << 20, o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr())
     torch.cuda.synchronize()
-    mb = g.MicroBatch(e, B, G)
     rng = np.random.default_rng(0x5EED0005)
     kk = np.zeros((64, B, 3), np.uint64)
     kk[:, :, 1] = rng.integers(0, G, size=(64, B))
     kk[:, :, 2] = np.uint64(tcd)
     out = {"index": e.index_stats()}
-    for use_graph in (True, False):
-        for i in range(50):
-            mb.keys[:] = kk[i % 64]
-            mb.run(B, use_graph)
-        lat = np.empty(args.runs)
-        for i in range(args.runs):
-            mb.keys[:] = kk[i % 64]
-            t0 = time.perf_counter()
-            mb.run(B, use_graph)
-            lat[i] = (time.perf_counter() - t0) * 1e6
-        out["graph" if use_graph else "eager"] = {"p50": round(float(np.percentile(lat, 50)), 2),
-                                                  "p99": round(float(np.percentile(lat, 99)), 2)}
-    mb.close()
+    for poll in (1, 0):                        # GD_OPT_MB_POLL: completion by the sort's pinned count, or not
+        e.set_option("mb_poll", poll)
+        mb = g.MicroBatch(e, B, G)
+        ref = None
+        for use_graph in (True, False):
+            for i in range(50):
+                mb.keys[:] = kk[i % 64]
+                mb.run(B, use_graph)
+            lat = np.empty(args.runs)
+            for i in range(args.runs):
+                mb.keys[:] = kk[i % 64]
+                t0 = time.perf_counter()
+                mb.run(B, use_graph)
+                lat[i] = (time.perf_counter() - t0) * 1e6
+            # the last run's outputs, read right after the run returned
+            got = (mb.perm[:B].copy(), mb.status[:B].copy())
+            ref = ref or got
+            assert all((a == b).all() for a, b in zip(got, ref))
+            out[f"{'graph' if use_graph else 'eager'}_poll{poll}"] = {
+                "p50": round(float(np.percentile(lat, 50)), 2), "p99": round(float(np.percentile(lat, 99)), 2)}
+        mb.close()
     e.close()
     print(json.dumps(out), flush=True)
     if args.json:
