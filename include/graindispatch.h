@@ -289,7 +289,7 @@ int gd_route_bucket(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t n_act
  * removal, merge, split, handoff; gd_index_stats below) rebuilds them (two streaming passes over the
  * table) and synchronises the handle's stream once to read the build's counters;
  * registration / upsert / unregister batches keep the indexes current and routes after them enqueue
- * only.  GD_CX=0 in the environment at gd_create turns the indexes off. */
+ * only.  gd_option_set(GD_OPT_PROBE, 0) turns the indexes off. */
 int gd_route_device(gd_handle* h, const gd_key* d_keys, uint32_t n,
                     uint32_t* d_silo, uint32_t* d_act, uint8_t* d_status);
 int gd_bucket_device(gd_handle* h, const uint32_t* d_acts, uint32_t n, uint32_t n_act,
