@@ -886,7 +886,11 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __rest
     claim_counters(ctr, pd, reused);
 }
 
-constexpr uint32_t REG_PASSES = 4;          // k_reg_take + the gated claim passes of an asynchronous batch
+// k_reg_take + the gated claim passes of an asynchronous batch: a pass settles one new grain of each group
+// of new grains colliding on their first free slots (a claim hides its key from its own pass), so a
+// large batch needs several (300,000 new grains in a 2M-slot table: more than 3)
+constexpr uint32_t REG_PASSES = 12;
+constexpr uint32_t REG_PASSES_SMALL = 4;    // ... for a batch of at most 2^16 items
 // The claim pass of an asynchronous batch (gd_dir_register_device_async): pass p > 0 runs only when
 // pass p - 1 deferred items (gate = its retry count; all lanes read the same word), so the host enqueues
 // REG_PASSES passes without reading a count back; k_reg_settled flags a batch still unsettled after them.
@@ -919,13 +923,11 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim_gated(const gd_key* 
 //               batch took the slot: the same key or a colliding one) is deferred to the gated claim
 //               passes (k_reg_claim_gated, the full protocol).
 constexpr uint8_t REG_CANDIDATE = 2;        // is_new: k_reg_find left a free slot to take
-static __global__ void __launch_bounds__(BLOCK) k_reg_find(const gd_key* __restrict__ keys, uint32_t n,
-                                                    const Slot* __restrict__ slots, unsigned long long mask,
-                                                    DevCounters* ctr, uint32_t* __restrict__ slot_of,
-                                                    uint8_t* __restrict__ is_new, uint32_t* __restrict__ seen,
-                                                    const gd_val* __restrict__ vals, TableArgs vt) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
+__device__ __forceinline__ void reg_find_item(uint32_t i, const gd_key* __restrict__ keys,
+                                              const Slot* __restrict__ slots, unsigned long long mask,
+                                              DevCounters* ctr, uint32_t* __restrict__ slot_of,
+                                              uint8_t* __restrict__ is_new, uint32_t* __restrict__ seen,
+                                              const gd_val* __restrict__ vals, const TableArgs& vt) {
     if (vals && !tab_silo_valid(vt, vals[i].silo)) {
         slot_of[i] = NONE32;
         is_new[i] = 0;
@@ -984,18 +986,23 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_find(const gd_key* __restr
     slot_of[i] = res;
     is_new[i] = st_out;
 }
-
-static __global__ void __launch_bounds__(BLOCK) k_reg_take(const gd_key* __restrict__ keys, uint32_t n, Slot* slots,
-                                                    unsigned long long mask, DevCounters* ctr,
-                                                    const gd_val* __restrict__ vals, TableArgs vt,
-                                                    uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
-                                                    const uint32_t* __restrict__ seen, uint32_t* retry,
-                                                    uint32_t* zero, uint32_t* __restrict__ last) {
+static __global__ void __launch_bounds__(BLOCK) k_reg_find(const gd_key* __restrict__ keys, uint32_t n,
+                                                    const Slot* __restrict__ slots, unsigned long long mask,
+                                                    DevCounters* ctr, uint32_t* __restrict__ slot_of,
+                                                    uint8_t* __restrict__ is_new, uint32_t* __restrict__ seen,
+                                                    const gd_val* __restrict__ vals, TableArgs vt) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (zero && i < REG_PASSES - 1) zero[i] = 0;         // the gated passes' counters (asynchronous batches)
-    uint32_t pd = 0;
-    bool reused = false, deferred = false;
-    if (i < n && is_new[i] == REG_CANDIDATE) {
+    if (i < n) reg_find_item(i, keys, slots, mask, ctr, slot_of, is_new, seen, vals, vt);
+}
+
+// k_reg_take's item: one CAS on the slot k_reg_find left (pd / reused for claim_counters; deferred: the
+// item lost the CAS and goes to the next claim pass).
+__device__ __forceinline__ void reg_take_item(uint32_t i, const gd_key* __restrict__ keys, Slot* slots,
+                                              unsigned long long mask, uint32_t* __restrict__ slot_of,
+                                              uint8_t* __restrict__ is_new, const uint32_t* __restrict__ seen,
+                                              uint32_t* __restrict__ last, uint32_t& pd, bool& reused,
+                                              bool& deferred) {
+    if (is_new[i] == REG_CANDIDATE) {
         const uint32_t t = slot_of[i];
         uint32_t expected = seen[i];
         uint32_t* mp = &slots[t].meta;
@@ -1025,8 +1032,24 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_take(const gd_key* __restr
             deferred = true;
         }
     }
-    const unsigned long long dm = __ballot(deferred);   // one counter atomic a wave
+}
+// The deferred items' count, one atomic a wave (every lane of the wave calls it).
+__device__ __forceinline__ void count_deferred(uint32_t* retry, bool deferred) {
+    const unsigned long long dm = __ballot(deferred);
     if ((threadIdx.x & (WAVE - 1)) == 0 && dm) atomicAdd(retry, (uint32_t)__popcll(dm));
+}
+static __global__ void __launch_bounds__(BLOCK) k_reg_take(const gd_key* __restrict__ keys, uint32_t n, Slot* slots,
+                                                    unsigned long long mask, DevCounters* ctr,
+                                                    const gd_val* __restrict__ vals, TableArgs vt,
+                                                    uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
+                                                    const uint32_t* __restrict__ seen, uint32_t* retry,
+                                                    uint32_t* zero, uint32_t* __restrict__ last) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (zero && i < REG_PASSES - 1) zero[i] = 0;         // the gated passes' counters (asynchronous batches)
+    uint32_t pd = 0;
+    bool reused = false, deferred = false;
+    if (i < n) reg_take_item(i, keys, slots, mask, slot_of, is_new, seen, last, pd, reused, deferred);
+    count_deferred(retry, deferred);
     claim_counters(ctr, pd, reused);
 }
 
@@ -1308,13 +1331,10 @@ static __global__ void __launch_bounds__(BLOCK) k_unreg_find(const gd_key* __res
 // RemoveActivation with the election in a per-slot word (round 6: 2 launches instead of 4): the find also
 // elects the first matching item of the batch (atomicMax(~i)), the commit tombstones the slot for the
 // elected item and clears the word.
-static __global__ void __launch_bounds__(BLOCK) k_unreg_find_elect(const gd_key* __restrict__ keys,
-                                                            const uint32_t* __restrict__ acts, uint32_t n,
-                                                            const Slot* slots, unsigned long long mask,
-                                                            const DevCounters* ctr, uint32_t* __restrict__ slot_of,
-                                                            uint32_t* __restrict__ last) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
+__device__ __forceinline__ void unreg_find_elect_item(uint32_t i, const gd_key* __restrict__ keys,
+                                                      const uint32_t* __restrict__ acts, const Slot* slots,
+                                                      unsigned long long mask, const DevCounters* ctr,
+                                                      uint32_t* __restrict__ slot_of, uint32_t* __restrict__ last) {
     const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
     unsigned long long s = home_slot(uniform_hash(n0, n1, tcd), mask);
     uint32_t res = NONE32;
@@ -1332,6 +1352,14 @@ static __global__ void __launch_bounds__(BLOCK) k_unreg_find_elect(const gd_key*
     }
     slot_of[i] = res;
     if (res != NONE32) atomicMax(&last[res], ~i);
+}
+static __global__ void __launch_bounds__(BLOCK) k_unreg_find_elect(const gd_key* __restrict__ keys,
+                                                            const uint32_t* __restrict__ acts, uint32_t n,
+                                                            const Slot* slots, unsigned long long mask,
+                                                            const DevCounters* ctr, uint32_t* __restrict__ slot_of,
+                                                            uint32_t* __restrict__ last) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i < n) unreg_find_elect_item(i, keys, acts, slots, mask, ctr, slot_of, last);
 }
 __device__ __forceinline__ bool unreg_elected_commit(uint32_t i, uint32_t n, const uint32_t* __restrict__ slot_of,
                                                      Slot* slots, uint32_t* __restrict__ last,

@@ -324,3 +324,77 @@ def test_index_mixed_directory(gd, probe):
     np.testing.assert_array_equal(act, want[2])
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("n_new", [3000, 60_000, 300_000])
+def test_async_directory_batches_vs_oracle(gd, n_new):
+    """Asynchronous AddSingleActivation / RemoveActivation batches (gd_dir_register_device_async,
+    gd_dir_unregister_device) of every size against the oracle's directory: first registration wins
+    over duplicate keys inside a batch, a grain already registered is reported, not inserted, the first
+    matching item of a removal batch removes and a wrong activation removes nothing; routes equal the
+    oracle and the live count follows.  300,000 new grains in a 2M-slot table collide on their first
+    free slots often enough to need more than three claim passes (REG_PASSES)."""
+    import torch
+    dev = torch.device("cuda:0")
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    rng = np.random.default_rng(n_new)
+    G = 50_000
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 21, options={"probe": 4})
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+    reg = o.grain_keys(TC, np.arange(G))
+    acts = np.arange(G, dtype=np.uint32)
+    own = _owner(spec, reg)
+    e.register(reg, acts, own)
+    live = {tuple(k): (int(x), int(s)) for k, x, s in zip(reg, acts, own)}
+    e.route(o.grain_keys(TC, rng.integers(0, G, size=20000)))            # builds the probe index
+    for rnd in range(3):
+        # removals: 1 % of the live grains, each twice (the first removes), and some wrong activations
+        lk = np.array(list(live.keys()), np.uint64).reshape(-1, 3)
+        pick = rng.permutation(len(lk))
+        gone = lk[pick[:len(lk) // 100]]
+        still = lk[pick[len(lk) // 100:len(lk) // 100 + n_new // 50]]     # live through the round
+        gacts = np.array([live[tuple(x)][0] for x in gone], np.uint32)
+        wrong = lk[pick[-200:]]
+        wacts = np.array([live[tuple(x)][0] ^ 1 for x in wrong], np.uint32)
+        uk = np.concatenate([gone, gone, wrong])
+        ua = np.concatenate([gacts, gacts, wacts])
+        # new grains, every 7th repeated inside the batch with another value (the first wins), and grains
+        # already registered (reported, not inserted)
+        new_ids = np.arange(G + rnd * n_new, G + (rnd + 1) * n_new)
+        rep = new_ids[::7]
+        k = np.concatenate([o.grain_keys(TC, np.concatenate([new_ids, rep])), still])
+        ids = np.concatenate([new_ids, rep, still[:, 1].astype(np.int64)])
+        v = np.stack([(ids * 5 + rnd).astype(np.uint32), _owner(spec, k)], 1)
+        v[n_new:n_new + len(rep), 0] += 1                                 # the repeats' other value
+        dk = torch.from_numpy(uk.view(np.int64)).to(dev)
+        da = torch.from_numpy(ua.view(np.int32)).to(dev)
+        rm = torch.empty(len(ua), dtype=torch.uint8, device=dev)
+        e.unregister_device(dk.data_ptr(), da.data_ptr(), len(ua), rm.data_ptr())
+        rk = torch.from_numpy(k.view(np.int64)).to(dev)
+        rv = torch.from_numpy(v.view(np.int32)).to(dev)
+        ov = torch.empty((len(k), 2), dtype=torch.int32, device=dev)
+        oi = torch.empty(len(k), dtype=torch.uint8, device=dev)
+        e.register_device_async(rk.data_ptr(), rv.data_ptr(), len(k), ov.data_ptr(), oi.data_ptr())
+        e.synchronize()
+        rm, ov, oi = rm.cpu().numpy(), ov.cpu().numpy().view(np.uint32), oi.cpu().numpy()
+        assert rm[:len(gone)].all() and not rm[len(gone):].any()
+        for x in gone:
+            del live[tuple(x)]
+        assert oi[:n_new].all() and not oi[n_new:].any()                  # each new grain once, first wins
+        np.testing.assert_array_equal(ov[:n_new, 0], v[:n_new, 0])
+        np.testing.assert_array_equal(ov[n_new:n_new + len(rep), 0], v[:n_new:7, 0])
+        np.testing.assert_array_equal(ov[n_new + len(rep):, 0],
+                                      np.array([live[tuple(x)][0] for x in still], np.uint32))
+        for key, val in zip(k[:n_new], v[:n_new]):
+            live[tuple(key)] = (int(val[0]), int(val[1]))
+        keys = np.array(list(live.keys()), np.uint64).reshape(-1, 3)
+        vals = np.array(list(live.values()), np.uint32).reshape(-1, 2)
+        q = np.concatenate([keys[rng.integers(0, len(keys), size=30000)], gone[:500]])
+        want = o.route_batch_np(q, spec, o.DirectoryArrays(keys, vals[:, 0], vals[:, 1]))
+        st, silo, act = e.route(q)
+        np.testing.assert_array_equal(st, want[0])
+        np.testing.assert_array_equal(silo, want[1])
+        np.testing.assert_array_equal(act, want[2])
+        assert e.stats()["table_live"] == len(live)
+    e.close()
