@@ -301,21 +301,20 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
     uint32_t* last = (uint32_t*)h->up_last.p;
     const unsigned long long mask = h->capacity - 1;
     TabTrack tt(h);                                // the batch re-projects its slots into the probe indexes
-    // read-only find, one CAS a new grain (k_reg_find / k_reg_take), then the full protocol for the items
-    // that lost their CAS; every item ending with a new entry elects itself in the slot's word (the lowest
-    // batch index wins: first registration wins, GrainDirectoryPartition.cs:304-326)
+    // a find with plain loads and one CAS a new grain in one launch (k_reg_find_take), then the full
+    // protocol for the items that lost their CAS or met a claim of the launch; every item ending with a new
+    // entry elects itself in the slot's word (the lowest batch index wins: first registration wins,
+    // GrainDirectoryPartition.cs:304-326)
     const uint32_t* unsettled = nullptr;
     uint32_t* retry0 = nullptr;
-    GD_TRY(launch(h, "k_reg_find", g, b, 0, k_reg_find, dk, n, (const Slot*)h->slots, mask, h->ctr, slot_of, is_new,
-                  win, dvals, table_args(h)));
     if (async) {
         if (!h->reg_retry.p) {                     // gate counters: k_reg_take / the commit keep them
             GD_TRY(ensure_own(h, h->reg_retry, REG_PASSES * sizeof(uint32_t)));
             HIP_TRY(h, hipMemsetAsync(h->reg_retry.p, 0, REG_PASSES * sizeof(uint32_t), h->stream));
         }
         uint32_t* rc = (uint32_t*)h->reg_retry.p;
-        GD_TRY(launch(h, "k_reg_take", g, b, 0, k_reg_take, dk, n, h->slots, mask, h->ctr, dvals, table_args(h),
-                      slot_of, is_new, (const uint32_t*)win, rc, rc + 1, last));
+        GD_TRY(launch(h, "k_reg_find_take", g, b, 0, k_reg_find_take, dk, n, h->slots, mask, h->ctr, dvals,
+                      table_args(h), slot_of, is_new, win, rc, rc + 1, last));
         // a pass settles one new grain of each group colliding on a first free slot: a batch of 2^16 items
         // settles in 3 (cfg 2's 1 % churn batches: 222 deferred by the take, 3 by pass 1, none by pass 2),
         // and each gated launch costs ~1.4 us even when its gate is shut
@@ -328,8 +327,8 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
         h->pending_in += n;
     } else {
         HIP_TRY(h, hipMemsetAsync(&h->ctr->retry, 0, sizeof(uint32_t), h->stream));
-        GD_TRY(launch(h, "k_reg_take", g, b, 0, k_reg_take, dk, n, h->slots, mask, h->ctr, dvals, table_args(h),
-                      slot_of, is_new, (const uint32_t*)win, &h->ctr->retry, (uint32_t*)nullptr, last));
+        GD_TRY(launch(h, "k_reg_find_take", g, b, 0, k_reg_find_take, dk, n, h->slots, mask, h->ctr, dvals,
+                      table_args(h), slot_of, is_new, win, &h->ctr->retry, (uint32_t*)nullptr, last));
         GD_TRY(pull_counters(h));
         // relaunches for the items that lost their CAS or met an unpublished claim
         for (uint32_t pass = 1; h->ctr_host.retry && !h->ctr_host.err; ++pass) {

@@ -923,6 +923,10 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim_gated(const gd_key* 
 //               batch took the slot: the same key or a colliding one) is deferred to the gated claim
 //               passes (k_reg_claim_gated, the full protocol).
 constexpr uint8_t REG_CANDIDATE = 2;        // is_new: k_reg_find left a free slot to take
+// LIVE_CLAIMS (k_reg_find_take): other items of the launch claim slots while this one walks -- a slot
+// CLAIMED or PENDING may hold this key's twin, unpublished, so the item defers (SLOT_RETRY); a stale
+// EMPTY or tombstone in a cached line only makes the take's CAS fail (the CAS is the arbiter).
+template <bool LIVE_CLAIMS = false>
 __device__ __forceinline__ void reg_find_item(uint32_t i, const gd_key* __restrict__ keys,
                                               const Slot* __restrict__ slots, unsigned long long mask,
                                               DevCounters* ctr, uint32_t* __restrict__ slot_of,
@@ -959,6 +963,9 @@ __device__ __forceinline__ void reg_find_item(uint32_t i, const gd_key* __restri
                     free_s = sk;
                     free_meta = b.w;
                 }
+                done = true;
+            } else if (LIVE_CLAIMS && (st == SLOT_CLAIMED || st == SLOT_PENDING)) {
+                res = SLOT_RETRY;                        // a claim of this launch: the next pass decides
                 done = true;
             } else {
                 if (st == SLOT_TOMB && free_s == ~0ull) {
@@ -1049,6 +1056,26 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_take(const gd_key* __restr
     uint32_t pd = 0;
     bool reused = false, deferred = false;
     if (i < n) reg_take_item(i, keys, slots, mask, slot_of, is_new, seen, last, pd, reused, deferred);
+    count_deferred(retry, deferred);
+    claim_counters(ctr, pd, reused);
+}
+// k_reg_find and k_reg_take as one launch (round 6): each item walks with plain loads and takes its free
+// slot at once; an item whose walk meets a claim of this launch defers to the claim passes.
+static __global__ void __launch_bounds__(BLOCK) k_reg_find_take(const gd_key* __restrict__ keys, uint32_t n,
+                                                         Slot* slots, unsigned long long mask, DevCounters* ctr,
+                                                         const gd_val* __restrict__ vals, TableArgs vt,
+                                                         uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
+                                                         uint32_t* __restrict__ seen, uint32_t* retry, uint32_t* zero,
+                                                         uint32_t* __restrict__ last) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (zero && i < REG_PASSES - 1) zero[i] = 0;         // the gated passes' counters (asynchronous batches)
+    uint32_t pd = 0;
+    bool reused = false, deferred = false;
+    if (i < n) {
+        reg_find_item<true>(i, keys, slots, mask, ctr, slot_of, is_new, seen, vals, vt);
+        if (slot_of[i] == SLOT_RETRY) deferred = true;
+        else reg_take_item(i, keys, slots, mask, slot_of, is_new, seen, last, pd, reused, deferred);
+    }
     count_deferred(retry, deferred);
     claim_counters(ctr, pd, reused);
 }
