@@ -167,7 +167,9 @@ class ShardedRouter:
         hits travel on to the rank hosting their activation (silo % world; the send to
         ActivationAddress.Silo after a remote lookup, LocalGrainDirectory.cs:920,
         OutboundMessageQueue.cs:125) and are bucketed there; other statuses stay on the owner.
-        One grain has one owner, so each activation still sees (sender rank, sender order)."""
+        One grain has one owner, so each activation still sees (sender rank, sender order).  With the
+        engine in pipeline mode the returned perm / offsets are complete only once
+        `engine.bucket_done_event()` is: a reader on another stream waits on it first."""
         if self.world == 1:
             # no exchange: arrival order is the batch order, all from this rank
             recv_keys, recv_idx, recv_src = keys, None, None
