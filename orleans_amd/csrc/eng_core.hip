@@ -140,6 +140,9 @@ int pull_counters(gd_handle* h) {
     HIP_TRY(h, hipStreamSynchronize(h->stream));
     h->ctr_stale = false;
     h->pending_in = 0;
+    // every batch enqueued so far is done: the index is pure again if no batch left anything out
+    if (h->tab_track == 0 && h->cx_built && h->cxi_ctr.p)
+        h->cx8_pure = h->cx8_ok && h->cx8_layout.ntypes == 1 && h->cx_ctr_host.out8 == 0;
     return GD_OK;
 }
 
@@ -181,7 +184,10 @@ bool cx_current(const gd_handle* h) {
     return h->cx_built && h->cx_slots_at == h->slots && h->cx_cap_at == h->capacity && h->cx_gen_at == h->tab_gen;
 }
 
-TabTrack::TabTrack(gd_handle* hh) : h(hh), was_current(cx_current(hh)) { ++h->tab_track; }
+TabTrack::TabTrack(gd_handle* hh) : h(hh), was_current(cx_current(hh)) {
+    ++h->tab_track;
+    h->cx8_pure = false;                 // until a read-back after the batch shows the index still pure
+}
 
 static uint32_t bit_len(uint64_t x) {
     uint32_t b = 0;
@@ -264,6 +270,7 @@ static int cx_build(gd_handle* h) {
     h->cx_ok = true;
     h->cx_built = true;
     h->cx_out8_at = h->cx_ctr_host.out8;              // the build's own: the baseline of the rebuild rule
+    h->cx8_pure = h->cx8_ok && h->cx8_layout.ntypes == 1 && h->cx_ctr_host.out8 == 0;
     h->cx_builds++;
     h->cx_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return GD_OK;
@@ -457,6 +464,11 @@ int route_launch(gd_handle* h, const gd_key* keys, uint32_t n, uint32_t* silo, u
     int meas = -1;
     const int var = cx ? cx_choose(h, 0, n, &meas, h->cx8_ok ? 4 : 3) : 1;
     CxMeasure m(h, meas, n);
+    if (var == 3 && h->cx8_pure)             // nothing to fall back to the directory for (gd_engine.h cx8_pure)
+        return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h),
+                      k_route_m<MODE, M, NT, 0, false, (int)CX_GROUP, true, true>, keys, n, ring_args(h),
+                      table_args(h), silo, act, status, 0ull, h->route_xcd ? 1u : 0u, (const uint32_t*)nullptr, 0u,
+                      (uint32_t*)nullptr, CxArgs{}, cx8_args(h));
     if (var == 3)
         return launch(h, "k_route", dim3(blocks_for(n, BLOCK * M)), dim3(BLOCK), ring_lds(h),
                       k_route_m<MODE, M, NT, 0, false, (int)CX_GROUP, true>, keys, n, ring_args(h), table_args(h), silo,

@@ -228,6 +228,10 @@ struct gd_handle {
     uint64_t cx_cap_at = 0, cx_gen_at = 0;
     DevBuf cxi_tab, cxi_types, cxi_ctr;   // 16-B index; its type set (+ a count per slot); CxCounters
     bool cx8_ok = false;        // the 8-B index is built and current with cx
+    // ... and pure: one grain class, every live entry held and none redirected (CxCounters::out8 = 0), as of
+    // a counter read-back with no directory batch enqueued since -- k_route_m's PURE form, whose walks
+    // need no directory fallback
+    bool cx8_pure = false;
     Cx8Args cx8_layout{};       // its layout (types, bits), fixed at the build
     DevBuf cx8_tab;
     CxCounters cx_ctr_host{};   // the last read-back of the index counters

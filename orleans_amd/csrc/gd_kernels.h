@@ -336,6 +336,41 @@ __device__ __forceinline__ bool cx8_walk(const Cx8Args& c, const TableArgs& tab,
     return false;
 }
 
+// cx8_walk over a pure index (PURE route_m_core: one class, every live entry held, none redirected): a
+// slot matches on its key word (a hole, y = 1, never -- live slots have y >= 2), no redirect is decoded,
+// and the bound is the workgroup's staged max_probe.  With the fallback probe compiled out of the kernel
+// and no max_probe load in the walk, k_route at cfg 2 runs 0.287 against 0.292 ms.
+__device__ __forceinline__ void cx8_walk_pure(const Cx8Args& c, const TableArgs& tab, uint32_t key,
+                                              unsigned long long home, uint4 (&q)[CX8_GROUP / 2], uint32_t mp,
+                                              uint32_t& silo, uint32_t& act, uint8_t& status) {
+    unsigned long long g = home;
+    bool done = false;
+    uint32_t hit = 0;
+    for (uint32_t base = 0;; base += CX8_GROUP) {
+#pragma unroll
+        for (int k = 0; k < (int)CX8_GROUP; ++k) {
+            if (done) continue;
+            const uint4 v = q[k / 2];
+            const uint32_t x = (k & 1) ? v.z : v.x, y = (k & 1) ? v.w : v.y;
+            if (y == 0) {
+                done = true;                                            // miss
+            } else if (x == key && y > 1u) {
+                done = true;
+                hit = y;
+            }
+        }
+        if (done || base + CX8_GROUP > mp) break;                       // found, empty, or past every entry
+        g += CX8_GROUP;
+        if (g >= c.cap) g = 0;
+        const uint4* qp = c.slots + (g >> 1);
+#pragma unroll
+        for (int k = 0; k < (int)CX8_GROUP / 2; ++k) q[k] = qp[k];
+    }
+    if (hit == 0) return;
+    const uint32_t am = (1u << c.ab) - 1u, u = hit >> c.ab, a = hit & am;
+    entry_result(tab, a == am ? GD_ACT_MULTI : a, (u & ((1u << c.sb) - 1u)) - 1u, silo, act, status);
+}
+
 // Linear probe of the open-addressing directory for a live entry with this key.
 __device__ __forceinline__ bool probe(const Slot* slots, unsigned long long mask, uint32_t max_probe,
                                       uint32_t h, uint64_t n0, uint64_t n1, uint64_t tcd,
@@ -446,8 +481,10 @@ __device__ __forceinline__ void st(T* p, T v) {
 // CX: probe the compact index (cx, its type set staged in s_types) instead of the directory, RG slots
 // (16 B each) a read: CX_GROUP (one 64-B atom, the layout's group) or 1 (16 B, for hot key sets).
 // CX8: probe the 8-B index (cx8) instead, one 64-B group (8 slots) a read.
+// PURE (with CX8, k_route_m): the index is pure (gd_engine.h cx8_pure) -- a key it does not hold is in no
+// entry, so there is no directory fallback at all; mp = the table's max_probe, staged by the caller.
 template <int MODE, int M, int STRIDE, bool NT, int N1W, bool NT_SIDE = false, bool CX = false,
-          int RG_CX = (int)CX_GROUP, bool CX8 = false>
+          int RG_CX = (int)CX_GROUP, bool CX8 = false, bool PURE = false>
 __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, uint32_t n, uint32_t base,
                                              const RingArgs& ring, const uint32_t* s_pts, const uint32_t* s_own,
                                              const TableArgs& tab, uint32_t max_probe,
@@ -455,7 +492,7 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
                                              uint8_t* __restrict__ out_status, uint64_t tcd_u,
                                              uint32_t* lds_act, uint32_t lds_stride, const CxArgs* cx = nullptr,
                                              const unsigned long long* s_types = nullptr,
-                                             const Cx8Args* cx8 = nullptr) {
+                                             const Cx8Args* cx8 = nullptr, uint32_t mp = 0) {
 
     uint64_t n0[M], n1[M], tcd[M];
     uint32_t h[M], silo[M], act[M];
@@ -524,7 +561,7 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
                     const int t = cx8_type(*cx8, n0[j], n1[j], tcd[j]);
                     want[j] = t < 0 ? 0u : 1u + (uint32_t)t;
                 }
-                fb[j] = want[j] == 0;
+                fb[j] = !PURE && want[j] == 0;
             }
             if (want[j]) {
                 if constexpr (CX) {
@@ -545,14 +582,17 @@ __device__ __forceinline__ void route_m_core(const gd_key* __restrict__ keys, ui
         for (int j = 0; j < M; ++j) {
             if (!want[j]) continue;
             if constexpr (CX) cx16_walk<RG_CX>(*cx, tab, want[j], n1[j], s[j], q[j], silo[j], act[j], status[j]);
+            else if constexpr (PURE) cx8_walk_pure(*cx8, tab, (uint32_t)n1[j], s[j], q[j], mp, silo[j], act[j], status[j]);
             else fb[j] = cx8_walk(*cx8, tab, (uint32_t)n1[j], want[j] - 1u, s[j], q[j], silo[j], act[j], status[j]);
         }
+        if constexpr (!PURE) {
 #pragma unroll
-        for (int j = 0; j < M; ++j) {
-            if (!fb[j]) continue;
-            uint32_t a, meta;
-            if (probe(tab.slots, tab.mask, lazy_max_probe(tab), h[j], n0[j], n1[j], tcd[j], a, meta))
-                entry_result(tab, a, slot_silo(meta), silo[j], act[j], status[j]);   // else MISS (Dispatcher.cs:742)
+            for (int j = 0; j < M; ++j) {
+                if (!fb[j]) continue;
+                uint32_t a, meta;
+                if (probe(tab.slots, tab.mask, lazy_max_probe(tab), h[j], n0[j], n1[j], tcd[j], a, meta))
+                    entry_result(tab, a, slot_silo(meta), silo[j], act[j], status[j]);   // else MISS (Dispatcher.cs:742)
+            }
         }
     } else {
     // first probe of every message, all in flight together; the ring search (LDS) runs under them.
@@ -674,7 +714,8 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb, uint32_t x
 
 // src_out (optional, the exchange's receive side): message i's sender rank, from the per-sender
 // receive counts rcnt[world] (k_recv_src's job, done here beside the probe's own writes).
-template <int MODE, int M, bool NT, int N1W = 0, bool CX = false, int RG_CX = (int)CX_GROUP, bool CX8 = false>
+template <int MODE, int M, bool NT, int N1W = 0, bool CX = false, int RG_CX = (int)CX_GROUP, bool CX8 = false,
+          bool PURE = false>
 static __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restrict__ keys, uint32_t n, RingArgs ring,
                                                    TableArgs tab, uint32_t* __restrict__ out_silo,
                                                    uint32_t* __restrict__ out_act,
@@ -685,10 +726,12 @@ static __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restri
     extern __shared__ __attribute__((aligned(16))) uint32_t s_ring[];
     __shared__ uint32_t s_soff[257];
     __shared__ unsigned long long s_types[CX ? CX_TYPES : 1];
+    __shared__ uint32_t s_mp;
     uint32_t* s_pts = s_ring;
     uint32_t* s_own = s_ring + ring.n;
     if constexpr (CX)
         for (uint32_t t = threadIdx.x; t < CX_TYPES; t += BLOCK) s_types[t] = cx.types[t];
+    if (PURE && threadIdx.x == 0) s_mp = lazy_max_probe(tab);   // the walks' bound, one load beside the ring
     if (src_out && threadIdx.x == 0) {
         uint32_t run = 0;
         for (uint32_t q = 0; q < world; ++q) {
@@ -701,9 +744,9 @@ static __global__ void __launch_bounds__(BLOCK) k_route_m(const gd_key* __restri
     // xcd: each XCD routes a contiguous message range (xcd_tile), so the act it writes is the act the
     // same XCD's histogram and scatter workgroups read next (their XCD tile ranges match)
     const uint32_t blk = xcd_tile(blockIdx.x, gridDim.x, xcd);
-    route_m_core<MODE, M, BLOCK, NT, N1W, true, CX, RG_CX, CX8>(keys, n, blk * (BLOCK * M) + threadIdx.x, ring, s_pts,
-                                                        s_own, tab, (CX || CX8) ? 0u : tab.ctr->max_probe, out_silo,
-                                                        out_act, out_status, tcd_u, nullptr, 0, &cx, s_types, &cx8);
+    route_m_core<MODE, M, BLOCK, NT, N1W, true, CX, RG_CX, CX8, PURE>(
+        keys, n, blk * (BLOCK * M) + threadIdx.x, ring, s_pts, s_own, tab, (CX || CX8) ? 0u : tab.ctr->max_probe,
+        out_silo, out_act, out_status, tcd_u, nullptr, 0, &cx, s_types, &cx8, PURE ? s_mp : 0u);
     if (src_out) {
 #pragma unroll
         for (int j = 0; j < M; ++j) {

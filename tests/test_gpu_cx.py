@@ -398,3 +398,49 @@ def test_async_directory_batches_vs_oracle(gd, n_new):
         np.testing.assert_array_equal(act, want[2])
         assert e.stats()["table_live"] == len(live)
     e.close()
+
+
+def test_pure_index_form_follows_the_directory(gd):
+    """k_route_m's PURE form (gd_engine.h cx8_pure: one grain class, every live entry held by the 8-B
+    index, none redirected -- no directory fallback compiled in) runs only while that holds as of the last
+    counter read-back with no batch enqueued since: Guid-keyed grains registered asynchronously right
+    before a route are found (the batch itself turns the form off), and after read-backs that show the
+    index impure they keep being found; routes equal the oracle throughout."""
+    import torch
+    dev = torch.device("cuda:0")
+    silos = o.bench_silos(8)
+    spec = o.ring_spec(silos, "D")
+    rng = np.random.default_rng(17)
+    G = 40_000
+    e = gd.GrainDispatch(device=0, table_capacity=1 << 17, options={"probe": 4})
+    e.ring_set_silos("D", [(s.ip, s.port, s.gen) for s in silos])
+    reg = o.grain_keys(TC, np.arange(G))
+    own = _owner(spec, reg)
+    e.register(reg, np.arange(G, dtype=np.uint32), own)
+    live = {tuple(k): (int(i), int(s)) for i, (k, s) in enumerate(zip(reg, own))}
+
+    def check():
+        keys = np.array(list(live.keys()), np.uint64).reshape(-1, 3)
+        vals = np.array(list(live.values()), np.uint32).reshape(-1, 2)
+        q = keys[rng.integers(0, len(keys), size=20000)]
+        want = o.route_batch_np(q, spec, o.DirectoryArrays(keys, vals[:, 0], vals[:, 1]))
+        st, silo, act = e.route(q)
+        np.testing.assert_array_equal(st, want[0])
+        np.testing.assert_array_equal(silo, want[1])
+        np.testing.assert_array_equal(act, want[2])
+
+    check()                                                                # pure: one class, all held
+    e.stats()
+    guid = o.grain_keys(TC, np.arange(G, G + 200))
+    guid[:, 0] = rng.integers(1, 1 << 62, size=len(guid)).astype(np.uint64)   # N0 != 0: not in the index
+    gv = np.stack([np.arange(G, G + 200, dtype=np.uint32), _owner(spec, guid)], 1)
+    dk = torch.from_numpy(guid.view(np.int64)).to(dev)
+    dvv = torch.from_numpy(gv.view(np.int32)).to(dev)
+    e.register_device_async(dk.data_ptr(), dvv.data_ptr(), len(guid))
+    for k, v in zip(guid, gv):
+        live[tuple(k)] = (int(v[0]), int(v[1]))
+    check()                                                                # no read-back since the batch
+    e.stats()                                                              # read-back: impure now
+    check()
+    assert e.index_stats()["out8"] >= 200
+    e.close()
