@@ -11,4 +11,4 @@ for c in 2 3 4; do
   cp $d/pmc_summary.txt profiles/r05_cfg${c}_pmc_summary.txt
 done
 # setup kernels (index builds, registration) are not bench kernels
-git status --short profiles | awk '$1 == "??" {print $2}' | grep -E 'k_(cx8_build|cx_build|cx_types|cx_project|reg_|lane_order|ring_owner)' | xargs -r rm
+git status --short profiles | awk '$1 == "??" {print $2}' | grep -E 'k_(cx8_build|cx_build|cx_types|cx_project|ctr_fold|reg_|lane_order|ring_owner)' | xargs -r rm
