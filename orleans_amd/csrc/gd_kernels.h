@@ -894,7 +894,8 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
                                                unsigned long long mask, DevCounters* ctr,
                                                uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
                                                const gd_val* __restrict__ vals, const TableArgs& vt, uint32_t* retry,
-                                               uint32_t& pdist, bool& reused, uint32_t tag);
+                                               uint32_t& pdist, bool& reused, uint32_t tag,
+                                               uint32_t* __restrict__ last = nullptr);
 // The claims' counter updates, one atomic a wave (one per item queued ~10^4 same-address atomics behind a
 // 1 % registration batch: 0.12 ms of it at cfg 2).  Every lane of the wave calls it.
 __device__ __forceinline__ void claim_counters(DevCounters* ctr, uint32_t pdist, bool reused) {
@@ -923,7 +924,7 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim(const gd_key* __rest
     bool reused = false;
     if (i < n && (pass == 0 || slot_of[i] == SLOT_RETRY)) {
         reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, &ctr->retry, pd, reused,
-                       claim_tag(pass));
+                       claim_tag(pass), last);
         if (last && is_new[i]) atomicMax(&last[slot_of[i]], ~i);
     }
     claim_counters(ctr, pd, reused);
@@ -952,7 +953,8 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim_gated(const gd_key* 
     uint32_t pd = 0;
     bool reused = false;
     if (i < n && (!gate || slot_of[i] == SLOT_RETRY)) {
-        reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, retry, pd, reused, claim_tag(pass));
+        reg_claim_item(i, keys, slots, mask, ctr, slot_of, is_new, vals, vt, retry, pd, reused, claim_tag(pass),
+                       last);
         if (is_new[i]) atomicMax(&last[slot_of[i]], ~i);    // the election (k_reg_commit_elect)
     }
     claim_counters(ctr, pd, reused);
@@ -967,14 +969,17 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_claim_gated(const gd_key* 
 //               passes (k_reg_claim_gated, the full protocol).
 constexpr uint8_t REG_CANDIDATE = 2;        // is_new: k_reg_find left a free slot to take
 // LIVE_CLAIMS (k_reg_find_take): other items of the launch claim slots while this one walks -- a slot
-// CLAIMED or PENDING may hold this key's twin, unpublished, so the item defers (SLOT_RETRY); a stale
-// EMPTY or tombstone in a cached line only makes the take's CAS fail (the CAS is the arbiter).
+// CLAIMED or PENDING holds a key unpublished to this launch, whose claimer the slot's election word
+// names (last): this key's twin -- join it (is_new 1) -- or another key -- walk on; a claim not yet
+// recorded defers the item (SLOT_RETRY).  A stale EMPTY or tombstone in a cached line only makes the
+// take's CAS fail (the CAS is the arbiter).
 template <bool LIVE_CLAIMS = false>
 __device__ __forceinline__ void reg_find_item(uint32_t i, const gd_key* __restrict__ keys,
                                               const Slot* __restrict__ slots, unsigned long long mask,
                                               DevCounters* ctr, uint32_t* __restrict__ slot_of,
                                               uint8_t* __restrict__ is_new, uint32_t* __restrict__ seen,
-                                              const gd_val* __restrict__ vals, const TableArgs& vt) {
+                                              const gd_val* __restrict__ vals, const TableArgs& vt,
+                                              uint32_t* __restrict__ last = nullptr) {
     if (vals && !tab_silo_valid(vt, vals[i].silo)) {
         slot_of[i] = NONE32;
         is_new[i] = 0;
@@ -1008,8 +1013,18 @@ __device__ __forceinline__ void reg_find_item(uint32_t i, const gd_key* __restri
                 }
                 done = true;
             } else if (LIVE_CLAIMS && (st == SLOT_CLAIMED || st == SLOT_PENDING)) {
-                res = SLOT_RETRY;                        // a claim of this launch: the next pass decides
-                done = true;
+                const uint32_t w = __hip_atomic_load(&last[sk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (w == 0) {
+                    res = SLOT_RETRY;                    // a claim of this launch not yet recorded
+                    done = true;
+                } else {
+                    const gd_key& c = keys[~w];
+                    if (c.n0 == n0 && c.n1 == n1 && c.type_code_data == tcd) {
+                        res = (uint32_t)sk;              // the twin's claim: join it
+                        st_out = 1;
+                        done = true;
+                    }                                    // else another key's claim: walk on
+                }
             } else {
                 if (st == SLOT_TOMB && free_s == ~0ull) {
                     free_s = sk;
@@ -1024,7 +1039,7 @@ __device__ __forceinline__ void reg_find_item(uint32_t i, const gd_key* __restri
         }
         s = (s + 4) & mask;
     }
-    if (res == NONE32) {
+    if (res == NONE32 && !(LIVE_CLAIMS && st_out == 1)) {
         if (free_s == ~0ull) {
             atomicOr(&ctr->err, 2u);                     // no free slot: the table is full
         } else {
@@ -1062,6 +1077,7 @@ __device__ __forceinline__ void reg_take_item(uint32_t i, const gd_key* __restri
             // a CAS loser defers below), so the key needs no release here: the kernel's end publishes it to
             // the passes and commit that read it (an agent-scope release fence writes the XCD's L2 back,
             // per wave: 2.2 ns an item at cfg 3's 100M registrations, 72 ms a 33M batch)
+            atomicMax(&last[t], ~i);                     // the election (k_reg_commit_elect), and the claimer
             const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
             Slot& sl = slots[t];
             sl.n0 = n0;
@@ -1073,7 +1089,6 @@ __device__ __forceinline__ void reg_take_item(uint32_t i, const gd_key* __restri
             pd = (uint32_t)((t - home) & mask);
             reused = slot_state(seen[i]) == SLOT_TOMB;
             is_new[i] = 1;
-            atomicMax(&last[t], ~i);                     // the election (k_reg_commit_elect)
         } else {
             // taken meanwhile (another new grain homed nearby, or this key's twin, whose key this launch
             // has not published): the full protocol in the next claim pass
@@ -1115,8 +1130,9 @@ static __global__ void __launch_bounds__(BLOCK) k_reg_find_take(const gd_key* __
     uint32_t pd = 0;
     bool reused = false, deferred = false;
     if (i < n) {
-        reg_find_item<true>(i, keys, slots, mask, ctr, slot_of, is_new, seen, vals, vt);
+        reg_find_item<true>(i, keys, slots, mask, ctr, slot_of, is_new, seen, vals, vt, last);
         if (slot_of[i] == SLOT_RETRY) deferred = true;
+        else if (is_new[i] == 1) atomicMax(&last[slot_of[i]], ~i);      // joined its twin's claim
         else reg_take_item(i, keys, slots, mask, slot_of, is_new, seen, last, pd, reused, deferred);
     }
     count_deferred(retry, deferred);
@@ -1142,7 +1158,8 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
                                                unsigned long long mask, DevCounters* ctr,
                                                uint32_t* __restrict__ slot_of, uint8_t* __restrict__ is_new,
                                                const gd_val* __restrict__ vals, const TableArgs& vt, uint32_t* retry,
-                                               uint32_t& pdist, bool& reused, uint32_t tag) {
+                                               uint32_t& pdist, bool& reused, uint32_t tag,
+                                               uint32_t* __restrict__ last) {
     if (vals && !tab_silo_valid(vt, vals[i].silo)) {
         slot_of[i] = NONE32;
         is_new[i] = 0;
@@ -1166,6 +1183,7 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
         if (!__hip_atomic_compare_exchange_strong(mp, &expected, make_meta(SLOT_CLAIMED, 0), __ATOMIC_RELAXED,
                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
             return false;
+        if (last) atomicMax(&last[t], ~i);                   // the claimer, readable by this launch's walks
         Slot& sl = slots[t];
         sl.n0 = n0;
         sl.n1 = n1;
@@ -1205,17 +1223,29 @@ __device__ __forceinline__ void reg_claim_item(uint32_t i, const gd_key* __restr
             continue;   // lost the CAS: re-read the same slot
         }
         if (st == SLOT_CLAIMED || (st == SLOT_PENDING && slot_silo(meta) == tag)) {
-            // claimed in this launch: its key is not published to this launch
-            res = SLOT_RETRY;
-            atomicAdd(retry, 1u);
-            break;
+            // claimed in this launch: its key is not published to this launch, but its claimer is (the slot's
+            // election word, written right after the claim): the key's twin -- join it -- or another key's
+            // claim -- walk on.  Only a claim not yet recorded defers.
+            const uint32_t w = last ? __hip_atomic_load(&last[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            if (w == 0) {
+                res = SLOT_RETRY;
+                atomicAdd(retry, 1u);
+                break;
+            }
+            const gd_key& c = keys[~w];
+            if (c.n0 == n0 && c.n1 == n1 && c.type_code_data == tcd) {
+                res = (uint32_t)s;
+                fresh = 1;
+                break;
+            }
         }
+        const bool unpublished = st == SLOT_CLAIMED || (st == SLOT_PENDING && slot_silo(meta) == tag);
         if (st == SLOT_TOMB && tomb_s == ~0ull) {
             tomb_s = s;
             tomb_meta = meta;
             tomb_dist = dist;
         }
-        if (st == SLOT_LIVE || st == SLOT_PENDING) {     // a key published before this launch
+        if (!unpublished && (st == SLOT_LIVE || st == SLOT_PENDING)) {   // a key published before this launch
             const uint64_t k0 = slots[s].n0, k1 = slots[s].n1, k2 = slots[s].tcd;
             if (k0 == n0 && k1 == n1 && k2 == tcd) {
                 res = (uint32_t)s;
