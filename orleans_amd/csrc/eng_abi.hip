@@ -365,12 +365,19 @@ int register_core(gd_handle* h, const gd_key* dk, const gd_val* dvals, uint32_t 
 // RemoveActivation (Force) for a batch of device-resident keys / activations; out_removed (device, may be
 // null).  Only enqueued; its own scratch (no bfence).  The first matching item of the batch removes.
 int unregister_core(gd_handle* h, const gd_key* dk, const uint32_t* dacts, uint32_t n, uint8_t* out_removed) {
+    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
+    const unsigned long long mask = h->capacity - 1;
+    if (!out_removed) {
+        // nobody asks which item removed: one launch, the CAS on the meta decides (k_unreg_cas)
+        TabTrack tt(h);
+        const CxBuild none{nullptr, nullptr, nullptr, Cx8Args{}};
+        return launch(h, "k_unreg_cas", g, b, 0, k_unreg_cas, dk, dacts, n, h->slots, mask, h->ctr,
+                      cx_inline(h, tt, n) ? cx_build_args(h) : none);
+    }
     GD_TRY(ensure_own(h, h->dir_scr[0], (size_t)n * 4));
     GD_TRY(slot_words(h));
-    const dim3 g(blocks_for(n, BLOCK)), b(BLOCK);
     uint32_t* slot_of = (uint32_t*)h->dir_scr[0].p;
     uint32_t* last = (uint32_t*)h->up_last.p;
-    const unsigned long long mask = h->capacity - 1;
     TabTrack tt(h);                               // the batch re-projects its slots into the probe indexes
     GD_TRY(launch(h, "k_unreg_find", g, b, 0, k_unreg_find_elect, dk, dacts, n, (const Slot*)h->slots, mask,
                   (const DevCounters*)h->ctr, slot_of, last));

@@ -326,6 +326,47 @@ static __global__ void __launch_bounds__(BLOCK) k_unreg_commit_elect_cx(const ui
     if (B.cx8) B.cx8[s] = CX8_HOLE;
 }
 
+// RemoveActivation as one launch, for a batch whose caller does not ask which item removed (round 6,
+// gd_dir_unregister_device with no out_removed): the table's end state does not depend on which of a
+// key's matching items removes it -- every one writes the same tombstone -- so the item whose CAS turns
+// the slot's LIVE meta (as its walk read it) into TOMB removes, and projects the tombstone into the
+// indexes (B.cx16 / B.cx8; null: not current).  No election word, no slot_of, no second launch.  A walk
+// never stops at a tombstone, so an item meeting another item's fresh tombstone walks on as it would
+// have past the live entry; a duplicate's CAS fails on the changed meta.
+static __global__ void __launch_bounds__(BLOCK) k_unreg_cas(const gd_key* __restrict__ keys,
+                                                     const uint32_t* __restrict__ acts, uint32_t n, Slot* slots,
+                                                     unsigned long long mask, DevCounters* ctr, CxBuild B) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    bool rm = false;
+    unsigned long long s = 0;
+    if (i < n) {
+        const uint64_t n0 = keys[i].n0, n1 = keys[i].n1, tcd = keys[i].type_code_data;
+        const uint32_t act = acts[i], maxp = ctr->max_probe;
+        s = home_slot(uniform_hash(n0, n1, tcd), mask);
+        for (uint32_t p = 0; p <= maxp; ++p) {
+            const uint4* q = reinterpret_cast<const uint4*>(slots + s);
+            const uint4 a = q[0], b = q[1];
+            const uint32_t st = slot_state(b.w);
+            if (st == SLOT_EMPTY) break;
+            if (st == SLOT_LIVE && ((uint64_t)a.x | ((uint64_t)a.y << 32)) == n0 &&
+                ((uint64_t)a.z | ((uint64_t)a.w << 32)) == n1 && ((uint64_t)b.x | ((uint64_t)b.y << 32)) == tcd) {
+                if (b.z == act) {
+                    uint32_t expected = b.w;
+                    rm = __hip_atomic_compare_exchange_strong(&slots[s].meta, &expected, make_meta(SLOT_TOMB, 0),
+                                                              __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+                }
+                break;
+            }
+            s = (s + 1) & mask;
+        }
+    }
+    live_delta(ctr, rm, true);
+    if (!rm) return;
+    if (B.cx16) B.cx16[s] = make_uint4(0, 0, 0, CX_TOMB);
+    if (B.cx8) B.cx8[s] = CX8_HOLE;
+}
+
 static __global__ void __launch_bounds__(BLOCK) k_unreg_commit_cx(const uint32_t* __restrict__ slot_of, uint32_t n,
                                                            Slot* slots, DevCounters* ctr,
                                                            uint8_t* __restrict__ out_removed, CxBuild B) {

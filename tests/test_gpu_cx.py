@@ -326,14 +326,16 @@ def test_index_mixed_directory(gd, probe):
     b.close()
 
 
-@pytest.mark.parametrize("n_new", [3000, 60_000, 300_000])
-def test_async_directory_batches_vs_oracle(gd, n_new):
+@pytest.mark.parametrize("n_new,report", [(3000, True), (60_000, True), (300_000, True), (60_000, False)])
+def test_async_directory_batches_vs_oracle(gd, n_new, report):
     """Asynchronous AddSingleActivation / RemoveActivation batches (gd_dir_register_device_async,
     gd_dir_unregister_device) of every size against the oracle's directory: first registration wins
     over duplicate keys inside a batch, a grain already registered is reported, not inserted, the first
     matching item of a removal batch removes and a wrong activation removes nothing; routes equal the
     oracle and the live count follows.  300,000 new grains in a 2M-slot table collide on their first
-    free slots often enough to need more than three claim passes (REG_PASSES)."""
+    free slots often enough to need more than three claim passes (REG_PASSES).  report=False: the removals
+    ask for no out_removed, so they take the one-launch CAS form (k_unreg_cas); the directory's end state
+    (routes, live count) must be the same."""
     import torch
     dev = torch.device("cuda:0")
     silos = o.bench_silos(8)
@@ -370,7 +372,7 @@ def test_async_directory_batches_vs_oracle(gd, n_new):
         dk = torch.from_numpy(uk.view(np.int64)).to(dev)
         da = torch.from_numpy(ua.view(np.int32)).to(dev)
         rm = torch.empty(len(ua), dtype=torch.uint8, device=dev)
-        e.unregister_device(dk.data_ptr(), da.data_ptr(), len(ua), rm.data_ptr())
+        e.unregister_device(dk.data_ptr(), da.data_ptr(), len(ua), rm.data_ptr() if report else None)
         rk = torch.from_numpy(k.view(np.int64)).to(dev)
         rv = torch.from_numpy(v.view(np.int32)).to(dev)
         ov = torch.empty((len(k), 2), dtype=torch.int32, device=dev)
@@ -378,7 +380,8 @@ def test_async_directory_batches_vs_oracle(gd, n_new):
         e.register_device_async(rk.data_ptr(), rv.data_ptr(), len(k), ov.data_ptr(), oi.data_ptr())
         e.synchronize()
         rm, ov, oi = rm.cpu().numpy(), ov.cpu().numpy().view(np.uint32), oi.cpu().numpy()
-        assert rm[:len(gone)].all() and not rm[len(gone):].any()
+        if report:
+            assert rm[:len(gone)].all() and not rm[len(gone):].any()
         for x in gone:
             del live[tuple(x)]
         assert oi[:n_new].all() and not oi[n_new:].any()                  # each new grain once, first wins
