@@ -489,6 +489,9 @@ def compact_roofline(rf, kernels, with_table=True):
     if rf.get("route_bound"):
         out["route_bound_ms"] = rf["route_bound"].get("ms_per_launch")
         out["route_bound_frac"] = rf["route_bound"].get("frac_of_bound")
+    if rf.get("fan_bound"):
+        out["fan_bound_ms"] = rf["fan_bound"].get("ms_per_launch")
+        out["fan_bound_frac"] = rf["fan_bound"].get("frac_of_bound")
     if rf.get("random_probe_ceiling"):
         out["random_probe_ceiling_frac"] = rf["random_probe_ceiling"].get("frac_of_ceiling")
         out["random_probe_io_ceiling_frac"] = rf["random_probe_ceiling"].get("frac_of_io_ceiling")
@@ -908,6 +911,37 @@ def route_bound(e, keys, stream, launch_ms: float, reps: int = 5):
     return {"ms_per_launch": round(ms, 4), "frac_of_bound": round(ms / launch_ms, 3),
             "source": "gd_route_bound_device, live: same index, keys, grid and writes; one 64-B index read a "
                       "message, no ring / walk / fallback"}
+
+
+def fan_bound(e, step, reps: int):
+    """GD_OPT_FAN_BOUND: every hop's k_fan_route over the 8-B index preceded by k_fan_bound on the same
+    inputs (the staged publishers, follower lists, home hash, one 64-B index group read a message and the
+    same result writes into scratch; no ring search, no walk -- gd_fanout.h k_fan_route<..., BOUND>), both
+    timed by the library's HIP events over `reps` cascades.  frac_of_bound = bound / k_fan_route over the
+    same launches."""
+    try:
+        e.set_option("fan_bound", 1)
+        e.set_kernel_timing(1)
+        e.kernel_times_reset()
+        for _ in range(max(1, reps)):
+            step()
+        torch.cuda.synchronize()
+        t = e.kernel_times()
+    except (g.GrainDispatchError, AttributeError, KeyError):
+        return None
+    finally:
+        e.set_kernel_timing(False)
+        try:
+            e.set_option("fan_bound", 0)
+        except (g.GrainDispatchError, KeyError):
+            pass
+    b, r = t.get("k_fan_bound"), t.get("k_fan_route")
+    if not b or not r or b[0] != r[0] or r[1] <= 0:
+        return None
+    return {"ms_per_launch": round(b[1] / b[0], 4), "route_ms_per_launch": round(r[1] / r[0], 4),
+            "frac_of_bound": round(b[1] / r[1], 3),
+            "source": "GD_OPT_FAN_BOUND, live: the hop's own frontier, graph, index and grid; expansion reads, "
+                      "one 64-B index group read a message and the result writes, no ring search / walk"}
 
 
 # The random-probe ceiling of the 8-B index (tools/ubench_fanprobe.hip, profiles/r05_ubench_fanprobe.txt):
@@ -1529,6 +1563,9 @@ def measure_cfg4(args, world, rank, local, dev, steps, warmup, profile_steps, wi
                 pc = probe_ceiling("cfg4", msgs_step / roofline["launches_per_step"], roofline["avg_launch_ms"])
                 if pc:
                     roofline["random_probe_ceiling"] = pc
+                fb = fan_bound(e, step, profile_steps)
+                if fb:
+                    roofline["fan_bound"] = fb
 
     cpu = None
     if rank == 0 and world == 1 and with_cpu and isinstance(runner, LibraryCascade):

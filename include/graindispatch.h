@@ -208,7 +208,10 @@ int gd_dir_unregister(gd_handle* h, const gd_key* keys, const uint32_t* acts, ui
  * gd_route_bucket_device batches and the stream runs them back to back; the probe indexes are
  * re-projected for the touched slots, not rebuilt.  Same semantics as gd_dir_register_device /
  * gd_dir_unregister; a device-side failure (table full, claims not settled after the gated passes)
- * is returned by the next synchronising call on the handle (gd_synchronize, gd_stats_get, ...). */
+ * is returned by the next synchronising call on the handle (gd_synchronize, gd_stats_get, ...).
+ * gd_dir_unregister_device with d_out_removed NULL is one launch (which of a key's matching items
+ * removes it is then unobservable: the CAS on the entry's LIVE meta picks it); with a report, the
+ * first matching item of the batch is elected in a second launch. */
 int gd_dir_register_device_async(gd_handle* h, const gd_key* d_keys, const gd_val* d_vals, uint32_t n,
                                  gd_val* d_out_vals, uint8_t* d_out_inserted);
 int gd_dir_unregister_device(gd_handle* h, const gd_key* d_keys, const uint32_t* d_acts, uint32_t n,
@@ -944,6 +947,10 @@ int gd_set_kernel_timing(gd_handle* h, int enable);   /* 0 off, 1 every launch, 
                                    themselves done in pinned host memory (their stores fenced first)
                                    instead of waiting for the dispatch's completion signal; eager runs
                                    still synchronise the stream (measured faster): 1 (default) / 0 */
+#define GD_OPT_FAN_BOUND    17  /* measurement: each fan-out route over the 8-B index is preceded by a launch
+                                   of its memory traffic alone (k_fan_bound: the same expansion reads, one
+                                   64-B index group read a message and the same result writes into scratch,
+                                   no ring search, no walk), timed under its own name: 0 (default) / 1 */
 int gd_option_set(gd_handle* h, int option, int64_t value);
 int gd_option_get(const gd_handle* h, int option, int64_t* value);
 

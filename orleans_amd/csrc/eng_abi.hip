@@ -101,6 +101,7 @@ void gd_destroy(gd_handle* h) {
     for (DevBuf& b : h->fr_ext) free_buf(b);
     for (DevBuf& b : h->churn) free_buf(b);
     for (DevBuf& b : h->fan) free_buf(b);
+    free_buf(h->fan_bnd);
     for (DevBuf& b : h->cbuf) free_buf(b);
     if (h->h_pin) (void)hipHostFree(h->h_pin);
     free_buf(h->cache_local);
@@ -795,6 +796,10 @@ int gd_option_set(gd_handle* h, int option, int64_t v) {
             if (!in(0, 1)) break;
             h->mb_poll = v != 0;
             return GD_OK;
+        case GD_OPT_FAN_BOUND:
+            if (!in(0, 1)) break;
+            h->fan_bound = v != 0;
+            return GD_OK;
         default: return set_err(h, GD_EINVAL, "gd_option_set: unknown option %d", option);
     }
     return set_err(h, GD_EINVAL, "gd_option_set: option %d: value %lld out of range", option, (long long)v);
@@ -820,6 +825,7 @@ int gd_option_get(const gd_handle* hc, int option, int64_t* v) {
         case GD_OPT_B2_PERSIST: *v = h->b2_persist; return GD_OK;
         case GD_OPT_B2_ORDER: *v = h->b2_order; return GD_OK;
         case GD_OPT_MB_POLL: *v = h->mb_poll ? 1 : 0; return GD_OK;
+        case GD_OPT_FAN_BOUND: *v = h->fan_bound ? 1 : 0; return GD_OK;
         default: return set_err(h, GD_EINVAL, "gd_option_get: unknown option %d", option);
     }
 }

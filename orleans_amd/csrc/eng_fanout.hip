@@ -81,11 +81,28 @@ int fan_route_launch_it(gd_handle* h, const uint32_t* row_off, const uint32_t* d
     const uint32_t* ends = (const uint32_t*)h->fan[0].p;
     const CxArgs cx = CX ? cx_args(h) : CxArgs{};
     const Cx8Args cx8 = CX8 ? cx8_args(h) : Cx8Args{};
+    // GD_OPT_FAN_BOUND: the kernel's memory bound (k_fan_route<..., BOUND>) on this hop's own inputs, into
+    // scratch outputs of the same layout; before the real launch on even launches, after it on odd ones, so
+    // neither form always finds the other's lines in the caches
+    const bool bound = CX8 && h->fan_bound && total;
+    const bool after = bound && (h->fan_bound_n++ & 1u);
+    auto launch_bound = [&]() -> int {
+        const size_t cap = (size_t)total;
+        GD_TRY(ensure(h, h->fan_bnd, cap * 17 + 64));
+        uint32_t* o = (uint32_t*)h->fan_bnd.p;
+        return launch(h, "k_fan_bound", g, b, ring_lds(h), k_fan_route<MODE, 2, false, (int)CX_GROUP, true, IT, true>,
+                      row_off, dst, frontier, nf, ends, total, tcd, ring_args(h), table_args(h), target ? o : nullptr,
+                      o + cap, o + 2 * cap, o + 3 * cap, (uint8_t*)(o + 4 * cap), CxArgs{}, cx8, d_nf,
+                      (uint32_t)dev_total);
+    };
+    if (bound && !after) GD_TRY(launch_bound());
     // 2 outputs a thread in flight (1: 2.95 ms, 4: 3.03 ms against 2.87 ms a cfg 4 cascade,
     // profiles/r02_v1_fanout_cfg4_ilp_ab.jsonl)
-    return launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2, CX, (int)CX_GROUP, CX8, IT>, row_off, dst,
+    GD_TRY(launch(h, "k_fan_route", g, b, ring_lds(h), k_fan_route<MODE, 2, CX, (int)CX_GROUP, CX8, IT>, row_off, dst,
                   frontier, nf, ends, total, tcd, ring_args(h), table_args(h), target, sender, silo, act, status, cx, cx8,
-                  d_nf, (uint32_t)dev_total);
+                  d_nf, (uint32_t)dev_total));
+    if (after) GD_TRY(launch_bound());
+    return GD_OK;
 }
 
 template <int MODE, bool CX, bool CX8>

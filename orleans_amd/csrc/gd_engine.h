@@ -90,6 +90,7 @@ struct gd_handle {
     DevBuf fr[16];                    // header-decode scratch (host-pointer entry points)
     DevBuf fr_ext[2];                 // TargetGrain KeyExt offsets / lengths (gd_route_frames_ext*)
     DevBuf churn[5];                  // split scratch: keep mask, flags, positions, out keys/vals
+    DevBuf fan_bnd;                   // k_fan_bound's scratch outputs
     DevBuf fan[8];                    // fan-out scratch: ends, total, flags, positions, host-form buffers
 
     // non-owner directory cache (LocalLookup mode when cache_max > 0)
@@ -197,6 +198,8 @@ struct gd_handle {
     bool mb_zero_copy = true;   // micro-batches: I/O from / to pinned host memory (GD_OPT_MB_ZEROCOPY)
     uint32_t mb_split = 8;      // micro-batches: redundant sorters splitting the host stores (GD_OPT_MB_SPLIT)
     bool mb_trace = false;      // micro-batches: per-phase timestamps (GD_OPT_MB_TRACE)
+    bool fan_bound = false;     // a k_fan_bound launch beside each 8-B-index k_fan_route (GD_OPT_FAN_BOUND)
+    uint32_t fan_bound_n = 0;   // ... before it on even launches, after it on odd ones
     bool mb_poll = true;        // micro-batches: completion by the sort's pinned count (GD_OPT_MB_POLL)
     int tune_pin[GD_TUNE_KINDS] = {-1, -1, -1, -1, -1};   // gd_tune_set: pinned variant per kind, -1 measured
     int msd_mode = 1;           // two-level bucketing (gd_msd.h, gd_msd2.h): 0 off, 1 measured (default), 2 always (GD_MSD)

@@ -308,7 +308,13 @@ static __global__ void __launch_bounds__(BLOCK) k_route_nodes(const uint32_t* __
 // tiles would leave most CUs idle).  d_nf / dev_total: the frontier's length on the device, and the
 // hop's total read from the inclusive scan (ends[nf - 1]) instead of the host -- `total` is then the
 // outputs' capacity and the grid is sized for it; blocks past the device total exit at once.
-template <int MODE, int ILP, bool CX = false, int RG = (int)CX_GROUP, bool CX8 = false, int IT = FAN_IT>
+// BOUND (with CX8; k_fan_bound, round 6): the kernel's memory traffic alone -- the same expansion reads
+// (staged publishers, follower lists), home hash, one 64-B index group read a message and the same result
+// writes, with no ring search and no walk (silo / act taken from the group read so it is not dead code).
+// Launched on the hop's own inputs into scratch outputs beside the real launch (GD_OPT_FAN_BOUND), it is
+// the live memory bound bench.py divides k_fan_route's time by.
+template <int MODE, int ILP, bool CX = false, int RG = (int)CX_GROUP, bool CX8 = false, int IT = FAN_IT,
+          bool BOUND = false>
 static __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __restrict__ row_off,
                                                      const uint32_t* __restrict__ dst,
                                                      const uint32_t* __restrict__ frontier, uint32_t n_front,
@@ -362,9 +368,17 @@ static __global__ void __launch_bounds__(BLOCK) k_fan_route(const uint32_t* __re
             for (int q = 0; q < ILP; ++q) {
                 if (!live[q]) continue;
                 const uint32_t p = p0 + (it0 + q) * BLOCK + threadIdx.x;
-                uint32_t silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[q])], act = NONE32;
-                const uint8_t st = cx8_walk_node<MODE>(cx8, tab, max_probe, t8, target[q], tcd, s8[q], q8[q], s_pts,
-                                                       s_own, ring, silo, act);
+                uint32_t silo, act = NONE32;
+                uint8_t st;
+                if constexpr (BOUND) {
+                    silo = q8[q][0].x & 7u;
+                    act = q8[q][CX8_GROUP / 2 - 1].w;
+                    st = 0;
+                } else {
+                    silo = s_own[ring_position<MODE>(s_pts, ring.n, ring.top, h[q])];
+                    st = cx8_walk_node<MODE>(cx8, tab, max_probe, t8, target[q], tcd, s8[q], q8[q], s_pts, s_own, ring,
+                                             silo, act);
+                }
                 if (out_target) out_target[p] = target[q];
                 out_sender[p] = sender[q];
                 out_silo[p] = silo;

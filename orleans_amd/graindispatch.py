@@ -422,7 +422,8 @@ def _check(h, rc: int):
 # ---- handle options (include/graindispatch.h GD_OPT_*) and measured choices (GD_TUNE_*) -----------
 OPTIONS = {"probe": 1, "bucket": 2, "l2_small": 3, "stable_rank": 4, "wire_headers": 5, "region_probe": 6,
            "idx16": 7, "host_chunk": 8, "mb_zerocopy": 9, "mb_split": 10, "mb_trace": 11, "l2_staged": 12,
-           "l2_mid": 13, "b2_persist": 14, "b2_order": 15, "mb_poll": 16}
+           "l2_mid": 13, "b2_persist": 14, "b2_order": 15, "mb_poll": 16,
+           "fan_bound": 17}
 TUNE_KINDS = {"probe_keys": 0, "probe_n1": 1, "probe_fanout": 2, "probe_nodes": 3, "bucket": 4}
 # Options applied to every handle this process creates, before its own `options=` (the test and tool
 # harness sets these; a C# host calls gd_option_set on its handle instead).

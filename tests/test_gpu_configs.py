@@ -508,17 +508,18 @@ def test_options_roundtrip_and_range(gd, monkeypatch):
     defaults = {"probe": 1, "bucket": 1, "l2_small": 1024, "stable_rank": 0 if gd.FORCE_NO_LANE_ORDER else 1,
                 "wire_headers": 2,
                 "region_probe": 0, "idx16": 1, "host_chunk": 2097152, "mb_zerocopy": 1, "mb_split": 8,
-                "mb_trace": 0, "l2_staged": 24576, "l2_mid": 8192, "b2_persist": 2, "b2_order": 0, "mb_poll": 1}
+                "mb_trace": 0, "l2_staged": 24576, "l2_mid": 8192, "b2_persist": 2, "b2_order": 0, "mb_poll": 1,
+                "fan_bound": 0}
     assert set(defaults) == set(gd.OPTIONS)
     for k, v in defaults.items():
         assert e.get_option(k) == v, k
     for k, v in {"probe": 4, "bucket": 2, "l2_small": 300, "stable_rank": 0, "wire_headers": 0,
                  "region_probe": 1, "idx16": 0, "l2_staged": 9000, "l2_mid": 2000, "b2_persist": 0,
-                 "b2_order": 1, "mb_poll": 0}.items():
+                 "b2_order": 1, "mb_poll": 0, "fan_bound": 1}.items():
         e.set_option(k, v)
         assert e.get_option(k) == v, k
     for k, bad in {"probe": 5, "bucket": -1, "l2_small": 24577, "l2_mid": 8193, "l2_staged": 1 << 20,
-                   "b2_persist": 9, "b2_order": 2, "mb_poll": 2}.items():
+                   "b2_persist": 9, "b2_order": 2, "mb_poll": 2, "fan_bound": 2}.items():
         before = e.get_option(k)
         with pytest.raises(Exception):
             e.set_option(k, bad)

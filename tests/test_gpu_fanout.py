@@ -62,6 +62,30 @@ def test_fanout_hop_vs_oracle(gd, mode, probe):
     e.close()
 
 
+def test_fan_bound_launch_leaves_results(gd):
+    """GD_OPT_FAN_BOUND (bench.py's live bound of k_fan_route): each 8-B-index fan-out route is preceded by
+    k_fan_bound on the same inputs into scratch; the hop's outputs stay the oracle's, and both kernels are
+    timed once a hop."""
+    n = 6000
+    ro, dst = power_law_graph(n, 8.0, seed=13, max_deg=3000)
+    rng = np.random.default_rng(14)
+    e, spec, d = _setup(gd, n, "D", probe=4)
+    e.set_option("fan_bound", 1)
+    e.set_kernel_timing(1)
+    e.kernel_times_reset()
+    for _ in range(2):
+        frontier = rng.integers(0, n, 900).astype(np.uint32)
+        got = e.fanout_route_bucket(ro, dst, frontier, TC, n)
+        want = _want_hop(ro, dst, frontier, spec, d, n)
+        for k in want:
+            np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+    t = e.kernel_times()
+    e.set_kernel_timing(False)
+    assert t["k_fan_bound"][0] == t["k_fan_route"][0] == 2
+    e.set_option("fan_bound", 0)
+    e.close()
+
+
 def _device(gd, e):
     import torch
     from orleans_amd.fanout import DeviceFanoutEngine
